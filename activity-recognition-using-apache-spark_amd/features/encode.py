@@ -1,0 +1,202 @@
+"""Feature pipeline: StringIndexer, OneHotEncoder, VectorAssembler, Pipeline.
+
+Capability parity with ``Main/main.py:49-77``:
+
+* ``StringIndexer`` — frequency-descending vocabulary.  Spark leaves the order of
+  equal counts undefined; here ties break by ascending string value
+  (documented, deterministic).  ``handleInvalid`` = error | skip | keep.
+* ``OneHotEncoder`` (``OneHotEncoderEstimator`` in Spark 2.3) — ``dropLast=True``:
+  category ``size-1`` encodes as all zeros, so width = vocabulary size - 1
+  (934/1401/755 on WISDM -> total dim 3100, block offsets 0/934/2335/3090,
+  ``result.txt:110``).
+* ``VectorAssembler`` — concatenation into a dense ``float32`` ``vector`` column.
+  One-hot blocks additionally keep their (offset, width, index) structure in
+  the column metadata so tree learners can treat them as binary features.
+* ``Pipeline`` / ``PipelineModel`` — sequential fit/transform; the model is
+  persistable (``har.utils.persist``) so raw CSV rows can be encoded at
+  inference time exactly as in training.
+"""
+from __future__ import annotations
+
+from typing import List, Optional, Sequence
+
+import numpy as np
+
+from ..data.table import Column, Table
+from ..models.base import Estimator, Model, Transformer, new_uid
+
+
+class StringIndexerModel(Model):
+    def __init__(self, inputCol: str, outputCol: str, labels: Sequence[str], handleInvalid: str = "error",
+                 uid: Optional[str] = None):
+        super().__init__(uid or new_uid("StringIndexer"))
+        self.inputCol, self.outputCol = inputCol, outputCol
+        self.labels = list(labels)
+        self.handleInvalid = handleInvalid
+        self._index = {s: i for i, s in enumerate(self.labels)}
+
+    def transform(self, table: Table) -> Table:
+        col = table[self.inputCol]
+        keys = col.data if col.kind == "string" else [col.cell_str(i) for i in range(len(col))]
+        out = np.empty(len(keys), dtype=np.float64)
+        keep = np.ones(len(keys), dtype=bool)
+        for i, k in enumerate(keys):
+            j = None if k is None else self._index.get(str(k))
+            if j is None:
+                if self.handleInvalid == "keep":
+                    j = len(self.labels)
+                elif self.handleInvalid == "skip":
+                    keep[i] = False
+                    j = -1
+                else:
+                    raise ValueError(f"StringIndexer: unseen label {k!r} in column {self.inputCol}")
+            out[i] = j
+        meta = {"vocab": self.labels, "nullable": False}
+        t = table.with_column(Column(self.outputCol, "double", out, meta=meta))
+        return t if keep.all() else t.filter(keep)
+
+    def params(self):
+        return {"inputCol": self.inputCol, "outputCol": self.outputCol, "handleInvalid": self.handleInvalid}
+
+    def state(self):
+        return {"labels": self.labels}
+
+
+class StringIndexer(Estimator):
+    def __init__(self, inputCol: str, outputCol: str, handleInvalid: str = "error",
+                 stringOrderType: str = "frequencyDesc"):
+        super().__init__(new_uid("StringIndexer"))
+        self.inputCol, self.outputCol = inputCol, outputCol
+        self.handleInvalid = handleInvalid
+        self.stringOrderType = stringOrderType
+
+    def getOutputCol(self) -> str:
+        return self.outputCol
+
+    def fit(self, table: Table) -> StringIndexerModel:
+        col = table[self.inputCol]
+        if col.kind == "string":
+            keys = np.asarray([k for k in col.data if k is not None], dtype=object).astype(str)
+        else:
+            keys = np.asarray([col.cell_str(i) for i in range(len(col))])
+        vals, counts = np.unique(keys, return_counts=True)
+        if self.stringOrderType == "frequencyDesc":
+            order = np.lexsort((vals, -counts))
+        elif self.stringOrderType == "frequencyAsc":
+            order = np.lexsort((vals, counts))
+        elif self.stringOrderType == "alphabetDesc":
+            order = np.argsort(vals)[::-1]
+        else:  # alphabetAsc
+            order = np.argsort(vals)
+        return StringIndexerModel(self.inputCol, self.outputCol, [str(v) for v in vals[order]],
+                                  self.handleInvalid, uid=self.uid)
+
+
+class OneHotEncoderModel(Model):
+    def __init__(self, inputCols: Sequence[str], outputCols: Sequence[str], sizes: Sequence[int],
+                 dropLast: bool = True, uid: Optional[str] = None):
+        super().__init__(uid or new_uid("OneHotEncoderEstimator"))
+        self.inputCols, self.outputCols = list(inputCols), list(outputCols)
+        self.sizes = [int(s) for s in sizes]
+        self.dropLast = dropLast
+
+    def transform(self, table: Table) -> Table:
+        t = table
+        for src, dst, size in zip(self.inputCols, self.outputCols, self.sizes):
+            idx = t[src].data.astype(np.int64)
+            width = size - 1 if self.dropLast else size
+            if (idx < 0).any() or (idx >= size).any():
+                raise ValueError(f"OneHotEncoder: index out of range in {src}")
+            mat = np.zeros((len(idx), width), dtype=np.float32)
+            rows = np.nonzero(idx < width)[0]
+            mat[rows, idx[rows]] = 1.0
+            meta = {"size": width, "onehot": {"index": idx.astype(np.int32), "width": width}}
+            t = t.with_column(Column(dst, "vector", mat, meta=meta))
+        return t
+
+    def params(self):
+        return {"inputCols": self.inputCols, "outputCols": self.outputCols, "dropLast": self.dropLast}
+
+    def state(self):
+        return {"sizes": self.sizes}
+
+
+class OneHotEncoder(Estimator):
+    """Spark 2.3 ``OneHotEncoderEstimator``: sizes come from the indexer metadata."""
+
+    def __init__(self, inputCols: Sequence[str], outputCols: Sequence[str], dropLast: bool = True):
+        super().__init__(new_uid("OneHotEncoderEstimator"))
+        self.inputCols, self.outputCols, self.dropLast = list(inputCols), list(outputCols), dropLast
+
+    def fit(self, table: Table) -> OneHotEncoderModel:
+        sizes = []
+        for c in self.inputCols:
+            col = table[c]
+            vocab = (col.meta or {}).get("vocab")
+            sizes.append(len(vocab) if vocab is not None else int(col.data.max()) + 1)
+        return OneHotEncoderModel(self.inputCols, self.outputCols, sizes, self.dropLast, uid=self.uid)
+
+
+OneHotEncoderEstimator = OneHotEncoder
+
+
+class VectorAssembler(Transformer):
+    def __init__(self, inputCols: Sequence[str], outputCol: str = "features"):
+        super().__init__(new_uid("VectorAssembler"))
+        self.inputCols, self.outputCol = list(inputCols), outputCol
+
+    def transform(self, table: Table) -> Table:
+        blocks: List[np.ndarray] = []
+        structure = []
+        off = 0
+        for c in self.inputCols:
+            col = table[c]
+            if col.kind == "vector":
+                m = np.asarray(col.data, dtype=np.float32)
+                oh = (col.meta or {}).get("onehot")
+                structure.append({"name": c, "offset": off, "width": m.shape[1],
+                                  "kind": "onehot" if oh is not None else "vector",
+                                  "index": None if oh is None else oh["index"]})
+            elif col.kind in ("int", "long", "double"):
+                m = col.data.astype(np.float32)[:, None]
+                if col.missing is not None and col.missing.any():
+                    raise ValueError(f"VectorAssembler: null values in column {c}")
+                structure.append({"name": c, "offset": off, "width": 1, "kind": "numeric", "index": None})
+            else:
+                raise ValueError(f"VectorAssembler: unsupported column type {col.kind} for {c}")
+            blocks.append(m)
+            off += m.shape[1]
+        mat = np.concatenate(blocks, axis=1) if blocks else np.zeros((table.count(), 0), np.float32)
+        meta = {"size": off, "structure": structure}
+        return table.with_column(Column(self.outputCol, "vector", mat, meta=meta))
+
+    def params(self):
+        return {"inputCols": self.inputCols, "outputCol": self.outputCol}
+
+
+class PipelineModel(Model):
+    def __init__(self, stages: Sequence[Transformer], uid: Optional[str] = None):
+        super().__init__(uid or new_uid("PipelineModel"))
+        self.stages = list(stages)
+
+    def transform(self, table: Table) -> Table:
+        for s in self.stages:
+            table = s.transform(table)
+        return table
+
+
+class Pipeline(Estimator):
+    def __init__(self, stages: Sequence):
+        super().__init__(new_uid("Pipeline"))
+        self.stages = list(stages)
+
+    def fit(self, table: Table) -> PipelineModel:
+        fitted = []
+        for s in self.stages:
+            if isinstance(s, Estimator):
+                m = s.fit(table)
+            else:
+                m = s
+            table = m.transform(table)
+            fitted.append(m)
+        return PipelineModel(fitted)

@@ -1,0 +1,123 @@
+"""Estimator / Model / Transformer base classes (the Spark ML surface used by
+``Main/main.py``: ``Estimator.fit(df) -> Model``, ``Model.transform(df)`` adding
+``rawPrediction``, ``probability`` and ``prediction`` — ``result.txt:147-151``)."""
+from __future__ import annotations
+
+import copy
+import secrets
+from typing import Dict, Optional, Tuple
+
+import numpy as np
+import torch
+
+from ..data.table import Column, Table
+
+
+def new_uid(prefix: str) -> str:
+    """Spark-style uid: ``<Class>_<20 hex chars>`` (e.g. ``LogisticRegression_446cab28d15c5195e1ba``)."""
+    return f"{prefix}_{secrets.token_hex(10)}"
+
+
+def resolve_device(device=None) -> torch.device:
+    if device is None or device == "auto":
+        return torch.device("cuda" if torch.cuda.is_available() else "cpu")
+    return torch.device(device)
+
+
+class Params:
+    """Minimal Spark ``Params``: named parameters, ``copy(extra)``, ``set``."""
+
+    _param_names: Tuple[str, ...] = ()
+
+    def params(self) -> Dict:
+        return {k: getattr(self, k) for k in self._param_names if hasattr(self, k)}
+
+    def set(self, **kw):
+        for k, v in kw.items():
+            if self._param_names and k not in self._param_names:
+                raise KeyError(f"{type(self).__name__} has no param {k}")
+            setattr(self, k, v)
+        return self
+
+    def copy(self, extra: Optional[Dict] = None):
+        c = copy.copy(self)
+        if extra:
+            c.set(**extra)
+        return c
+
+
+class Transformer(Params):
+    def __init__(self, uid: Optional[str] = None):
+        self.uid = uid or new_uid(type(self).__name__)
+
+    def transform(self, table: Table) -> Table:  # pragma: no cover - abstract
+        raise NotImplementedError
+
+    def __str__(self):
+        return self.uid
+
+
+class Estimator(Params):
+    def __init__(self, uid: Optional[str] = None):
+        self.uid = uid or new_uid(type(self).__name__)
+
+    def fit(self, table: Table):  # pragma: no cover - abstract
+        raise NotImplementedError
+
+    def __str__(self):
+        return self.uid
+
+
+class Model(Transformer):
+    def state(self) -> Dict:
+        return {}
+
+
+def features_tensor(table: Table, col: str, device, dtype=torch.float32) -> torch.Tensor:
+    c = table[col]
+    arr = c.data if c.kind == "vector" else c.data[:, None]
+    return torch.as_tensor(np.ascontiguousarray(arr, dtype=np.float32)).to(device=device, dtype=dtype)
+
+
+def labels_tensor(table: Table, col: str, device) -> torch.Tensor:
+    return torch.as_tensor(table[col].data.astype(np.int64)).to(device)
+
+
+class ClassifierParams(Params):
+    featuresCol = "features"
+    labelCol = "label"
+    predictionCol = "prediction"
+    probabilityCol = "probability"
+    rawPredictionCol = "rawPrediction"
+
+
+class ClassificationModel(Model, ClassifierParams):
+    """``transform`` = one device pass producing raw scores, probabilities, argmax."""
+
+    num_classes: int = 0
+    num_features: int = 0
+    device: torch.device = torch.device("cpu")
+
+    def predict_raw(self, X: torch.Tensor) -> torch.Tensor:  # pragma: no cover - abstract
+        raise NotImplementedError
+
+    def raw_to_probability(self, raw: torch.Tensor) -> torch.Tensor:
+        s = raw.sum(dim=1, keepdim=True)
+        return torch.where(s > 0, raw / s.clamp_min(1e-300), torch.full_like(raw, 1.0 / raw.shape[1]))
+
+    def predict_all(self, X: torch.Tensor):
+        raw = self.predict_raw(X)
+        prob = self.raw_to_probability(raw)
+        pred = torch.argmax(prob, dim=1)
+        return raw, prob, pred
+
+    def predict(self, X: torch.Tensor) -> torch.Tensor:
+        return self.predict_all(X)[2]
+
+    def transform(self, table: Table) -> Table:
+        X = features_tensor(table, self.featuresCol, self.device)
+        raw, prob, pred = self.predict_all(X)
+        t = table.with_column(Column(self.rawPredictionCol, "vector", raw.double().cpu().numpy()))
+        t = t.with_column(Column(self.probabilityCol, "vector", prob.double().cpu().numpy()))
+        return t.with_column(Column(self.predictionCol, "double", pred.double().cpu().numpy(),
+                                    meta={"nullable": False}))

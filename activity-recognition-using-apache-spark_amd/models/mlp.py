@@ -1,0 +1,348 @@
+"""Multilayer perceptron classifier — bf16 MFMA training engine.
+
+New capability (the reference has no MLP; BASELINE.json config 3 "WISDM 6-class
+3-layer MLP bf16, DP all-reduce on 8xMI355X").  API modelled on Spark's
+``MultilayerPerceptronClassifier(layers=[in, h1, ..., out], maxIter, blockSize,
+stepSize, seed)``; hidden activations are ReLU and the solver is Adam.
+
+Engine layout (MI355X-first):
+
+* all parameters live in ONE flat fp32 master buffer (+ Adam m/v), with a bf16
+  compute copy refreshed by the fused Adam kernel, and ONE flat fp32 gradient
+  buffer — so data-parallel training issues exactly one RCCL all-reduce per step
+  (the whole gradient is ~0.3 MB: latency-bound on xGMI, so one bucket);
+* one training step = memset + L forward GEMMs (bias+ReLU fused) + fused
+  softmax-CE head (loss, accuracy, dlogits, bias grad) + per layer one data-grad
+  GEMM (ReLU mask + bias grad fused) and one split-K weight-grad GEMM
+  + [all-reduce] + fused Adam.  No host synchronization inside a step; the loss
+  and correct-count accumulators are read only when asked for;
+* input rows are kept resident in HBM as padded bf16 ([N, F_pad]); a step reads a
+  contiguous slice (zero-copy batches of a pre-shuffled resident dataset).
+
+The CPU path (and test oracle) is the same network in PyTorch fp32.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+from typing import List, Optional, Sequence
+
+import numpy as np
+import torch
+
+from ..data.table import Table
+from ..ops import _native, rng
+from ..ops.gemm import EPI_BIAS_RELU, EPI_F32_ATOMIC, EPI_RELU_GRAD, gemm_bf16
+from .base import ClassificationModel, ClassifierParams, Estimator, features_tensor, labels_tensor, new_uid, \
+    resolve_device
+
+HEAD_PAD = 32  # classes padded to 32 rows (two 16-wide MFMA column tiles)
+
+
+def _pad(x: int, m: int) -> int:
+    return (x + m - 1) // m * m
+
+
+@dataclass
+class Segment:
+    name: str
+    offset: int
+    shape: tuple
+
+    @property
+    def numel(self):
+        return int(np.prod(self.shape))
+
+
+class FlatLayout:
+    """Offsets of every weight/bias inside the flat buffers (16-element aligned)."""
+
+    def __init__(self, layers: Sequence[int]):
+        self.layers = list(layers)
+        self.in_pad = _pad(layers[0], 32)
+        self.hidden = list(layers[1:-1])
+        for h in self.hidden:
+            if h % 32:
+                raise ValueError("hidden layer sizes must be multiples of 32")
+        self.num_classes = layers[-1]
+        if self.num_classes > HEAD_PAD:
+            raise ValueError(f"at most {HEAD_PAD} classes")
+        dims = [self.in_pad] + self.hidden
+        self.segments: List[Segment] = []
+        off = 0
+        for i in range(len(self.hidden)):
+            for name, shape in ((f"W{i}", (dims[i + 1], dims[i])), (f"b{i}", (dims[i + 1],))):
+                self.segments.append(Segment(name, off, shape))
+                off = _pad(off + int(np.prod(shape)), 64)
+        last = dims[-1]
+        for name, shape in (("Wout", (HEAD_PAD, last)), ("bout", (HEAD_PAD,))):
+            self.segments.append(Segment(name, off, shape))
+            off = _pad(off + int(np.prod(shape)), 64)
+        self.total = off
+        self.by_name = {s.name: s for s in self.segments}
+
+    def view(self, flat: torch.Tensor, name: str) -> torch.Tensor:
+        s = self.by_name[name]
+        return flat[s.offset: s.offset + s.numel].view(s.shape)
+
+
+def init_params(layout: FlatLayout, seed: int) -> torch.Tensor:
+    """Kaiming-uniform weights from Philox (identical on every rank), zero biases."""
+    flat = torch.zeros(layout.total, dtype=torch.float32)
+    dims = [layout.in_pad] + layout.hidden
+    fan_ins = {f"W{i}": layout.layers[0] if i == 0 else dims[i] for i in range(len(layout.hidden))}
+    fan_ins["Wout"] = dims[-1]
+    for s in layout.segments:
+        if not s.name.startswith("W"):
+            continue
+        bound = math.sqrt(6.0 / fan_ins[s.name])
+        u = rng.uniform(seed, rng.STREAM_INIT, np.arange(s.offset, s.offset + s.numel, dtype=np.uint64))
+        w = torch.from_numpy(((2 * u - 1) * bound).astype(np.float32)).view(s.shape)
+        if s.name == "W0":
+            w[:, layout.layers[0]:] = 0  # padded input columns
+        if s.name == "Wout":
+            w[layout.num_classes:] = 0   # padded class rows
+        flat[s.offset: s.offset + s.numel] = w.reshape(-1)
+    return flat
+
+
+class MLPEngine:
+    """Device-resident training state + the fused native step."""
+
+    def __init__(self, layers: Sequence[int], batch_size: int, device, lr=1e-3, betas=(0.9, 0.999), eps=1e-8,
+                 weight_decay=0.0, seed=0, process_group=None, world_size: int = 1):
+        self.layout = FlatLayout(layers)
+        self.device = torch.device(device)
+        self.B = int(batch_size)
+        self.lr, self.betas, self.eps, self.wd = lr, betas, eps, weight_decay
+        self.pg = process_group
+        self.world = world_size
+        L = self.layout
+        dev = self.device
+        self.P = init_params(L, seed).to(dev)
+        self.G = torch.zeros_like(self.P)
+        self.m = torch.zeros_like(self.P)
+        self.v = torch.zeros_like(self.P)
+        self.step_count = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.native = self.device.type == "cuda"
+        if self.native:
+            self.Pb = self.P.to(torch.bfloat16)
+            dims = [L.in_pad] + L.hidden
+            self.acts = [None] + [torch.empty(self.B, h, dtype=torch.bfloat16, device=dev) for h in L.hidden]
+            hmax = max(L.hidden) if L.hidden else HEAD_PAD
+            self.dbuf = [torch.empty(self.B * hmax, dtype=torch.bfloat16, device=dev) for _ in range(2)]
+            self.dlogits = torch.zeros(self.B, HEAD_PAD, dtype=torch.bfloat16, device=dev)
+            self.loss_sum = torch.zeros(1, dtype=torch.float32, device=dev)
+            self.correct = torch.zeros(1, dtype=torch.int32, device=dev)
+            self.dims = dims
+        else:
+            self.t_step = 0
+
+    # ---------------------------------------------------------------- native
+    def _w(self, flat, name):
+        return self.layout.view(flat, name)
+
+    def forward_backward_native(self, Xb: torch.Tensor, y32: torch.Tensor, scale: float):
+        """Xb: [B, in_pad] bf16 (contiguous slice), y32: [B] int32."""
+        L, mod, s = self.layout, _native.kernels(), _native.stream_ptr()
+        B = Xb.shape[0]
+        if Xb.shape[1] != L.in_pad or Xb.dtype != torch.bfloat16 or B > self.B:
+            raise ValueError("bad batch")
+        self.G.zero_()
+        nh = len(L.hidden)
+        acts = [Xb] + [a[:B] for a in self.acts[1:]]
+        for i in range(nh):
+            gemm_bf16(acts[i], self._w(self.Pb, f"W{i}"), acts[i + 1], M=B, N=self.dims[i + 1], K=self.dims[i],
+                      layout=0, epi=EPI_BIAS_RELU, bias=self._w(self.P, f"b{i}"))
+        last = acts[nh]
+        mod.softmax_ce_head(last.data_ptr(), self._w(self.Pb, "Wout").data_ptr(), self._w(self.P, "bout").data_ptr(),
+                            y32.data_ptr(), B, self.dims[-1], L.num_classes, float(scale), self.dlogits.data_ptr(),
+                            self._w(self.G, "bout").data_ptr(), self.loss_sum.data_ptr(), self.correct.data_ptr(), 0, s)
+        dl = self.dlogits[:B]
+        # dWout = dlogits^T . last
+        gemm_bf16(dl, last, self._w(self.G, "Wout"), M=HEAD_PAD, N=self.dims[-1], K=B, layout=3, epi=EPI_F32_ATOMIC)
+        d, dW_in = dl, "Wout"
+        for i in reversed(range(nh)):
+            h = self.dims[i + 1]
+            dact = self.dbuf[i % 2][: B * h].view(B, h)
+            Wnext = self._w(self.Pb, dW_in)
+            # dact = (d . Wnext) * relu'(acts[i+1]);   db_i = colsum(dact)
+            gemm_bf16(d, Wnext, dact, M=B, N=h, K=Wnext.shape[0], layout=2, epi=EPI_RELU_GRAD,
+                      mask=acts[i + 1], colsum=self._w(self.G, f"b{i}"))
+            # dW_i = dact^T . acts[i]
+            gemm_bf16(dact, acts[i], self._w(self.G, f"W{i}"), M=h, N=self.dims[i], K=B, layout=3,
+                      epi=EPI_F32_ATOMIC)
+            d, dW_in = dact, f"W{i}"
+
+    def optimizer_step_native(self):
+        b1, b2 = self.betas
+        _native.kernels().adam_step(self.P.data_ptr(), self.G.data_ptr(), self.m.data_ptr(), self.v.data_ptr(),
+                                    self.Pb.data_ptr(), self.P.numel(), float(self.lr), b1, b2, float(self.eps),
+                                    float(self.wd), 1.0, self.step_count.data_ptr(), _native.stream_ptr())
+
+    def allreduce_grads(self):
+        if self.world > 1:
+            import torch.distributed as dist
+            dist.all_reduce(self.G, group=self.pg)
+
+    def train_step(self, Xb: torch.Tensor, yb: torch.Tensor, global_batch: int):
+        if self.native:
+            self.forward_backward_native(Xb, yb, 1.0 / global_batch)
+            self.allreduce_grads()
+            self.optimizer_step_native()
+        else:
+            self.train_step_torch(Xb, yb, global_batch)
+
+    # ---------------------------------------------------------------- torch
+    def torch_forward(self, P: torch.Tensor, X: torch.Tensor):
+        L = self.layout
+        h = X
+        if h.shape[1] < L.in_pad:
+            h = torch.nn.functional.pad(h, (0, L.in_pad - h.shape[1]))
+        for i in range(len(L.hidden)):
+            h = torch.relu(h @ L.view(P, f"W{i}").T + L.view(P, f"b{i}"))
+        z = h @ L.view(P, "Wout")[: L.num_classes].T + L.view(P, "bout")[: L.num_classes]
+        return z
+
+    def train_step_torch(self, X: torch.Tensor, y: torch.Tensor, global_batch: int):
+        """fp32 reference step (CPU path / oracle); same Adam math as the kernel."""
+        P = self.P.detach().requires_grad_(True)
+        z = self.torch_forward(P, X.float())
+        loss = torch.nn.functional.cross_entropy(z, y.long(), reduction="sum") / global_batch
+        (g,) = torch.autograd.grad(loss, P)
+        self.G.copy_(g)
+        self.allreduce_grads()
+        self.t_step += 1
+        b1, b2 = self.betas
+        with torch.no_grad():
+            self.m.mul_(b1).add_((1 - b1) * self.G)
+            self.v.mul_(b2).add_((1 - b2) * self.G * self.G)
+            upd = (self.m / (1 - b1 ** self.t_step)) / ((self.v / (1 - b2 ** self.t_step)).sqrt() + self.eps)
+            self.P.sub_(self.lr * (upd + self.wd * self.P))
+        self.last_loss = float(loss.detach()) * global_batch / X.shape[0]
+
+    # ---------------------------------------------------------------- inference
+    def logits(self, X: torch.Tensor) -> torch.Tensor:
+        L = self.layout
+        if self.native and X.is_cuda:
+            Xb = pad_input_bf16(X, L.in_pad)
+            out = torch.empty(X.shape[0], L.num_classes, dtype=torch.float32, device=X.device)
+            for r0 in range(0, X.shape[0], self.B):
+                r1 = min(X.shape[0], r0 + self.B)
+                B = r1 - r0
+                acts = [Xb[r0:r1]] + [a[:B] for a in self.acts[1:]]
+                for i in range(len(L.hidden)):
+                    gemm_bf16(acts[i], self._w(self.Pb, f"W{i}"), acts[i + 1], M=B, N=self.dims[i + 1],
+                              K=self.dims[i], layout=0, epi=EPI_BIAS_RELU, bias=self._w(self.P, f"b{i}"))
+                _native.kernels().softmax_ce_head(acts[-1].data_ptr(), self._w(self.Pb, "Wout").data_ptr(),
+                                                  self._w(self.P, "bout").data_ptr(), 0, B, self.dims[-1],
+                                                  L.num_classes, 1.0, 0, 0, 0, 0, out[r0:r1].data_ptr(),
+                                                  _native.stream_ptr())
+            return out
+        Xp = torch.zeros(X.shape[0], L.in_pad, dtype=torch.float32, device=X.device)
+        Xp[:, : X.shape[1]] = X
+        with torch.no_grad():
+            return self.torch_forward(self.P.to(X.device), Xp)
+
+
+def pad_input_bf16(X: torch.Tensor, in_pad: int) -> torch.Tensor:
+    """[N, F] fp32 -> [N, in_pad] bf16 (zero padded), on device via the HIP cast kernel."""
+    X = X.contiguous().float()
+    out = torch.empty(X.shape[0], in_pad, dtype=torch.bfloat16, device=X.device)
+    if X.is_cuda:
+        _native.kernels().cast_pad_bf16(X.data_ptr(), X.shape[0], X.shape[1], X.stride(0), out.data_ptr(), in_pad,
+                                        _native.stream_ptr())
+    else:
+        out.zero_()
+        out[:, : X.shape[1]] = X.to(torch.bfloat16)
+    return out
+
+
+class MultilayerPerceptronClassificationModel(ClassificationModel):
+    def __init__(self, engine: MLPEngine, uid=None):
+        super().__init__(uid or new_uid("MultilayerPerceptronClassifier"))
+        self.engine = engine
+        self.layers = engine.layout.layers
+        self.num_classes = engine.layout.num_classes
+        self.num_features = engine.layout.layers[0]
+        self.device = engine.device
+        self.mean = None
+        self.inv_std = None
+
+    def _prep(self, X):
+        if self.mean is not None:
+            X = (X - self.mean.to(X.device)) * self.inv_std.to(X.device)
+        return X
+
+    def predict_raw(self, X: torch.Tensor) -> torch.Tensor:
+        return self.engine.logits(self._prep(X.to(self.device)))
+
+    def raw_to_probability(self, raw):
+        return torch.softmax(raw, dim=1)
+
+    def __str__(self):
+        return f"MultilayerPerceptronClassificationModel (uid={self.uid}) with {len(self.layers)} layers"
+
+    def state(self):
+        return {"layers": self.layers, "params": self.engine.P.cpu(), "mean": self.mean, "inv_std": self.inv_std}
+
+
+class MultilayerPerceptronClassifier(Estimator, ClassifierParams):
+    """``layers=[in, h1, ..., out]``; ``maxIter`` = epochs; ``blockSize`` = per-rank batch."""
+
+    _param_names = ("layers", "maxIter", "blockSize", "stepSize", "seed", "standardize", "device", "weightDecay")
+
+    def __init__(self, layers: Optional[Sequence[int]] = None, maxIter: int = 100, blockSize: int = 1024,
+                 stepSize: float = 1e-3, seed: int = 0, standardize: bool = True, featuresCol="features",
+                 labelCol="label", device=None, weightDecay: float = 0.0):
+        super().__init__(new_uid("MultilayerPerceptronClassifier"))
+        self.layers = list(layers) if layers else None
+        self.maxIter, self.blockSize, self.stepSize, self.seed = maxIter, blockSize, stepSize, seed
+        self.standardize, self.featuresCol, self.labelCol, self.device = standardize, featuresCol, labelCol, device
+        self.weightDecay = weightDecay
+
+    def fit(self, table: Table) -> MultilayerPerceptronClassificationModel:
+        dev = resolve_device(self.device)
+        X = features_tensor(table, self.featuresCol, dev)
+        y = labels_tensor(table, self.labelCol, dev)
+        return self.fit_tensors(X, y)
+
+    def fit_tensors(self, X: torch.Tensor, y: torch.Tensor, process_group=None, rank: int = 0,
+                    world_size: int = 1) -> MultilayerPerceptronClassificationModel:
+        """DP-ready fit: every rank passes its own shard (X, y); gradients are all-reduced."""
+        dev = X.device
+        K = int(y.max()) + 1
+        layers = self.layers or [X.shape[1], 128, 128, K]
+        if layers[0] != X.shape[1]:
+            raise ValueError(f"layers[0]={layers[0]} but features have {X.shape[1]} columns")
+        mean = inv_std = None
+        if self.standardize:
+            n = torch.tensor([float(X.shape[0])], device=dev, dtype=torch.float64)
+            s1 = X.double().sum(0)
+            s2 = (X.double() ** 2).sum(0)
+            if world_size > 1:
+                import torch.distributed as dist
+                buf = torch.cat([n, s1, s2])
+                dist.all_reduce(buf, group=process_group)
+                n, s1, s2 = buf[:1], buf[1:1 + X.shape[1]], buf[1 + X.shape[1]:]
+            mean = (s1 / n).float()
+            var = (s2 / n - (s1 / n) ** 2).clamp_min(0).float()
+            inv_std = torch.where(var > 0, 1.0 / var.sqrt(), torch.zeros_like(var))
+            X = (X - mean) * inv_std
+        B = min(self.blockSize, X.shape[0])
+        eng = MLPEngine(layers, B, dev, lr=self.stepSize, seed=self.seed, process_group=process_group,
+                        world_size=world_size, weight_decay=self.weightDecay)
+        N = X.shape[0]
+        Xin = pad_input_bf16(X, eng.layout.in_pad) if eng.native else X
+        y32 = y.to(torch.int32).contiguous()
+        global_batch = B * world_size
+        steps_per_epoch = max(1, N // B)
+        g = torch.Generator(device="cpu").manual_seed(self.seed + 7919 * rank)
+        for epoch in range(self.maxIter):
+            perm = torch.randperm(N, generator=g).to(dev)
+            Xe, ye = Xin[perm].contiguous(), y32[perm].contiguous()
+            for s in range(steps_per_epoch):
+                eng.train_step(Xe[s * B:(s + 1) * B], ye[s * B:(s + 1) * B], global_batch)
+        model = MultilayerPerceptronClassificationModel(eng, uid=self.uid)
+        model.mean, model.inv_std = mean, inv_std
+        return model

@@ -1,0 +1,37 @@
+"""Device reductions for evaluation: confusion matrix and
+regression moments in one pass each (``csrc/kernels/metrics.hip``)."""
+from __future__ import annotations
+
+import torch
+
+from . import _native
+
+
+def confusion_matrix(label: torch.Tensor, pred: torch.Tensor, K: int) -> torch.Tensor:
+    """``cm[true, pred]`` counts (int64)."""
+    if label.is_cuda:
+        lab = label.to(torch.int32).contiguous()
+        prd = pred.to(device=label.device, dtype=torch.int32).contiguous()
+        if int(lab.numel()) and (int(lab.max()) >= K or int(prd.max()) >= K or int(lab.min()) < 0 or int(prd.min()) < 0):
+            raise ValueError("confusion_matrix: label/prediction out of range")
+        cm = torch.zeros(K * K, dtype=torch.int64, device=label.device)
+        _native.kernels().confusion_matrix(lab.data_ptr(), prd.data_ptr(), lab.numel(), K, cm.data_ptr(),
+                                           _native.stream_ptr())
+        return cm.view(K, K)
+    idx = label.to(torch.int64) * K + pred.to(torch.int64)
+    return torch.bincount(idx, minlength=K * K).view(K, K)
+
+
+def regression_moments(y: torch.Tensor, yhat: torch.Tensor):
+    """(n, sum (y-yh)^2, sum |y-yh|, sum y, sum y^2) — fp64 accumulation."""
+    if y.is_cuda:
+        out = torch.zeros(6, dtype=torch.float64, device=y.device)
+        yf = y.to(torch.float32).contiguous()
+        yh = yhat.to(device=y.device, dtype=torch.float32).contiguous()
+        _native.kernels().regression_moments(yf.data_ptr(), yh.data_ptr(), yf.numel(), out.data_ptr(),
+                                             _native.stream_ptr())
+        o = out.cpu().tolist()
+        return o[0], o[1], o[2], o[3], o[4]
+    d = (y - yhat).double()
+    yd = y.double()
+    return float(y.numel()), float((d * d).sum()), float(d.abs().sum()), float(yd.sum()), float((yd * yd).sum())

@@ -1,0 +1,109 @@
+"""One-process-per-GPU runtime (replaces Spark's driver/executor bootstrap,
+``SparkConf().setAppName("HAR").setMaster(master)`` / ``SparkContext`` at
+``Main/main.py:8-9``).
+
+``init()`` reads the ``torch.distributed.run`` environment (RANK, LOCAL_RANK,
+WORLD_SIZE, MASTER_ADDR/PORT), pins the process to ``cuda:LOCAL_RANK`` and
+creates the process group: backend ``nccl`` — which IS RCCL on ROCm, running
+over xGMI between the GPUs of a node — when GPUs are present, ``gloo``
+otherwise (CPU tests exercise the same code path).  Without the env it is a
+single-process world of size 1 with no process group at all.
+"""
+from __future__ import annotations
+
+import datetime
+import os
+from dataclasses import dataclass
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+
+
+@dataclass
+class DistContext:
+    rank: int
+    local_rank: int
+    world_size: int
+    device: torch.device
+    backend: Optional[str]
+    group: Optional[object] = None
+
+    @property
+    def is_distributed(self) -> bool:
+        return self.world_size > 1
+
+    @property
+    def is_main(self) -> bool:
+        return self.rank == 0
+
+
+def init(expected_world: Optional[int] = None, backend: Optional[str] = None, device: Optional[str] = None,
+         timeout_s: int = 600) -> DistContext:
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if expected_world is not None and world != expected_world and world > 1:
+        raise RuntimeError(f"launched with WORLD_SIZE={world} but --gpus {expected_world}")
+    use_cuda = torch.cuda.is_available() and (device is None or str(device).startswith("cuda"))
+    if use_cuda:
+        torch.cuda.set_device(local_rank)
+        dev = torch.device("cuda", local_rank)
+    else:
+        dev = torch.device("cpu")
+    be = None
+    if world > 1:
+        be = backend or ("nccl" if use_cuda else "gloo")
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        kw = dict(backend=be, rank=rank, world_size=world, timeout=datetime.timedelta(seconds=timeout_s))
+        if be == "nccl":
+            kw["device_id"] = dev
+        if not dist.is_initialized():
+            dist.init_process_group(**kw)
+    return DistContext(rank, local_rank, world, dev, be, None)
+
+
+def barrier(ctx: DistContext):
+    if ctx.is_distributed:
+        if ctx.backend == "nccl":
+            dist.barrier(device_ids=[ctx.local_rank])
+        else:
+            dist.barrier()
+
+
+def sync(device):
+    if isinstance(device, torch.device) and device.type == "cuda":
+        torch.cuda.synchronize(device)
+
+
+def _reduce_scalar(ctx: DistContext, x: float, op) -> float:
+    if not ctx.is_distributed:
+        return x
+    t = torch.tensor([x], dtype=torch.float64, device=ctx.device)
+    dist.all_reduce(t, op=op, group=ctx.group)
+    return float(t.item())
+
+
+def max_over_ranks(ctx: DistContext, x: float) -> float:
+    return _reduce_scalar(ctx, x, dist.ReduceOp.MAX)
+
+
+def sum_over_ranks(ctx: DistContext, x: float) -> float:
+    return _reduce_scalar(ctx, x, dist.ReduceOp.SUM)
+
+
+def mean_over_ranks(ctx: DistContext, x: float) -> float:
+    return sum_over_ranks(ctx, x) / ctx.world_size
+
+
+def shutdown(ctx: DistContext):
+    if ctx.is_distributed and dist.is_initialized():
+        barrier(ctx)
+        dist.destroy_process_group()
+
+
+def shard_range(n: int, rank: int, world: int):
+    """Contiguous [lo, hi) row range of ``rank`` (global row ids stay meaningful)."""
+    lo = (n * rank) // world
+    hi = (n * (rank + 1)) // world
+    return lo, hi

@@ -1,0 +1,139 @@
+// pybind11 module `_har_native`: host runtime (CSV parser) + kernel launchers.
+//
+// Launchers take device pointers and the HIP stream as integers (the Python
+// side passes `tensor.data_ptr()` and `torch.cuda.current_stream().cuda_stream`),
+// so this translation unit needs neither torch nor HIP device headers and the
+// kernels stay capturable into hipGraphs.
+#include <pybind11/numpy.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <hip/hip_runtime_api.h>
+
+#include <cstring>
+#include <stdexcept>
+#include <string>
+
+#include "har_kernels.h"
+#include "host/csv_parser.h"
+
+namespace py = pybind11;
+using u = uintptr_t;
+
+template <typename T>
+static T* P(u x) { return reinterpret_cast<T*>(x); }
+static hipStream_t S(u x) { return reinterpret_cast<hipStream_t>(x); }
+
+static void check(int rc, const char* what) {
+  if (rc != 0) {
+    std::string msg = std::string(what) + " failed: ";
+    if (rc > 0) msg += hipGetErrorString((hipError_t)rc);
+    else msg += "contract violation code " + std::to_string(rc);
+    throw std::runtime_error(msg);
+  }
+}
+
+static py::dict csv_parse(py::bytes data, bool header, int threads) {
+  std::string_view sv;
+  char* ptr;
+  Py_ssize_t len;
+  PyBytes_AsStringAndSize(data.ptr(), &ptr, &len);
+  har::CsvResult r;
+  {
+    py::gil_scoped_release nogil;
+    r = har::parse_csv(ptr, (size_t)len, header, threads);
+  }
+  py::dict out;
+  out["names"] = r.names;
+  out["kinds"] = r.kinds;
+  py::list dbl, ints, miss, strs;
+  for (int j = 0; j < r.ncols; ++j) {
+    py::array_t<double> d(r.nrows);
+    std::memcpy(d.mutable_data(), r.doubles[j].data(), sizeof(double) * r.nrows);
+    py::array_t<int64_t> i(r.nrows);
+    std::memcpy(i.mutable_data(), r.ints[j].data(), sizeof(int64_t) * r.nrows);
+    py::array_t<bool> m(r.nrows);
+    auto* mp = m.mutable_data();
+    for (int64_t k = 0; k < r.nrows; ++k) mp[k] = r.missing[j][k] != 0;
+    dbl.append(d);
+    ints.append(i);
+    miss.append(m);
+    py::list s;
+    if (r.kinds[j] == "string") {
+      for (int64_t k = 0; k < r.nrows; ++k) {
+        if (r.missing[j][k]) s.append(py::none());
+        else s.append(py::str(r.field(j, k)));
+      }
+    }
+    strs.append(s);
+  }
+  out["doubles"] = dbl;
+  out["ints"] = ints;
+  out["missing"] = miss;
+  out["strings"] = strs;
+  out["nrows"] = r.nrows;
+  return out;
+}
+
+static GemmParams make_gemm(u A, u B, u C, u bias, u mask, u colsum, int M, int N, int K, int lda, int ldb,
+                            int ldc, int ldmask, int k_split, float alpha) {
+  GemmParams p;
+  p.A = P<const void>(A);
+  p.B = P<const void>(B);
+  p.C = P<void>(C);
+  p.bias = P<const float>(bias);
+  p.mask = P<const void>(mask);
+  p.colsum = P<float>(colsum);
+  p.M = M; p.N = N; p.K = K;
+  p.lda = lda; p.ldb = ldb; p.ldc = ldc; p.ldmask = ldmask;
+  p.k_split = k_split;
+  p.alpha = alpha;
+  return p;
+}
+
+PYBIND11_MODULE(_har_native, m) {
+  m.doc() = "har native runtime: host CSV parser + gfx950 HIP kernel launchers";
+  m.def("csv_parse", &csv_parse, py::arg("data"), py::arg("header") = true, py::arg("threads") = 0);
+
+  m.def("gemm", [](bool bf16, int layout, int epi, u A, u B, u C, u bias, u mask, u colsum, int M, int N, int K,
+                   int lda, int ldb, int ldc, int ldmask, int k_split, float alpha, u stream) {
+    GemmParams p = make_gemm(A, B, C, bias, mask, colsum, M, N, K, lda, ldb, ldc, ldmask, k_split, alpha);
+    check(bf16 ? har_gemm_bf16(&p, layout, epi, S(stream)) : har_gemm_f32(&p, layout, epi, S(stream)), "gemm");
+  });
+
+  m.def("softmax_ce_head", [](u H, u W, u bias, u labels, int B, int D, int C, float scale, u dlogits, u dbias,
+                              u loss_sum, u correct, u logits_out, u stream) {
+    check(har_softmax_ce_head(P<const uint16_t>(H), P<const uint16_t>(W), P<const float>(bias),
+                              P<const int32_t>(labels), B, D, C, scale, P<uint16_t>(dlogits), P<float>(dbias),
+                              P<float>(loss_sum), P<int32_t>(correct), P<float>(logits_out), S(stream)),
+          "softmax_ce_head");
+  });
+
+  m.def("adam_step", [](u param, u grad, u mm, u vv, u pb, int64_t n, float lr, float b1, float b2, float eps,
+                        float wd, float gs, u step, u stream) {
+    check(har_adam_step(P<float>(param), P<const float>(grad), P<float>(mm), P<float>(vv), P<uint16_t>(pb), n, lr,
+                        b1, b2, eps, wd, gs, P<int32_t>(step), S(stream)),
+          "adam_step");
+  });
+
+  m.def("logreg_softmax_grad", [](u Z, int64_t n, int B, int K, int ld, u y, u rw, u inv_wsum, u R, u loss,
+                                  u stream) {
+    check(har_logreg_softmax_grad(P<const float>(Z), n, B, K, ld, P<const int32_t>(y), P<const float>(rw),
+                                  P<const float>(inv_wsum), P<float>(R), P<double>(loss), S(stream)),
+          "logreg_softmax_grad");
+  });
+
+  m.def("confusion_matrix", [](u label, u pred, int64_t n, int K, u cm, u stream) {
+    check(har_confusion_matrix(P<const int32_t>(label), P<const int32_t>(pred), n, K, P<int64_t>(cm), S(stream)),
+          "confusion_matrix");
+  });
+
+  m.def("regression_moments", [](u y, u yh, int64_t n, u out, u stream) {
+    check(har_regression_moments(P<const float>(y), P<const float>(yh), n, P<double>(out), S(stream)),
+          "regression_moments");
+  });
+
+  m.def("cast_pad_bf16", [](u in, int rows, int cin, int ldin, u out, int cout, u stream) {
+    check(har_cast_pad_bf16(P<const float>(in), rows, cin, ldin, P<uint16_t>(out), cout, S(stream)), "cast_pad_bf16");
+  });
+}

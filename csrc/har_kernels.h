@@ -1,0 +1,86 @@
+// C ABI of the har HIP kernels (gfx950).  Every launcher takes raw device
+// pointers plus the HIP stream to enqueue on, never allocates or synchronizes
+// (so every launch can be captured into a hipGraph), and returns 0 or a
+// hipError_t / negative contract-violation code.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct GemmParams {
+  const void* A;
+  const void* B;
+  void* C;
+  const float* bias;      // EPI_BIAS*, may be null
+  const void* mask;       // EPI_RELU_GRAD: bf16 activations of the forward pass
+  float* colsum;          // EPI_RELU_GRAD: fused bias-gradient accumulator, may be null
+  int M, N, K;
+  int lda, ldb, ldc, ldmask;
+  int k_split;            // EPI_F32_ATOMIC: K range per grid.z slice (multiple of 32)
+  float alpha;
+} GemmParams;
+
+int har_gemm_bf16(const GemmParams* p, int layout, int epi, hipStream_t s);
+int har_gemm_f32(const GemmParams* p, int layout, int epi, hipStream_t s);
+
+// Fused classifier head: logits = H . W^T + b (C <= 32 classes, W padded to 32 rows),
+// softmax, cross-entropy, dlogits = (p - onehot) * scale (bf16, 32 columns),
+// dbias += colsum(dlogits), loss_sum += sum CE, correct += #argmax==label.
+int har_softmax_ce_head(const uint16_t* H, const uint16_t* W, const float* bias, const int32_t* labels,
+                        int B, int Hdim, int C, float scale, uint16_t* dlogits, float* dbias,
+                        float* loss_sum, int32_t* correct, float* logits_out, hipStream_t s);
+
+// Fused Adam(W) over a flat fp32 parameter buffer; also writes the bf16 compute copy.
+// The step counter (*step, device int32) is incremented on the stream before the update.
+int har_adam_step(float* param, const float* grad, float* m, float* v, uint16_t* param_bf16, int64_t n,
+                  float lr, float beta1, float beta2, float eps, float weight_decay, float grad_scale,
+                  int32_t* step, hipStream_t s);
+
+// fp32 -> bf16 cast with row padding: out[r][0:cols_out] = in[r][0:cols_in], zero fill.
+int har_cast_pad_bf16(const float* in, int rows, int cols_in, int ld_in, uint16_t* out, int cols_out,
+                      hipStream_t s);
+
+// ---- randomness (Philox4x32-10 keyed by global row id) ----
+int har_philox_buckets(uint64_t seed, uint32_t stream, int64_t row0, int64_t n, const uint32_t* thr,
+                       int nthr, int32_t* out, hipStream_t s);
+int har_poisson_bootstrap(uint64_t seed, int tree0, int ntrees, int64_t row0, int64_t n, uint8_t* out,
+                          hipStream_t s);
+
+// ---- statistics / metrics ----
+// Column count/sum/sumsq/min/max (masked by optional row weights) -> stats[5][ncols] (double).
+int har_column_stats(const float* X, int64_t n, int ncols, int ld, const float* w, double* stats,
+                     hipStream_t s);
+int har_confusion_matrix(const int32_t* label, const int32_t* pred, int64_t n, int K, int64_t* cm,
+                         hipStream_t s);
+int har_regression_moments(const float* y, const float* yhat, int64_t n, double* out6, hipStream_t s);
+
+// ---- logistic regression (batched over B models, K classes padded to 8) ----
+int har_logreg_softmax_grad(const float* Z, int64_t n, int nmodels, int K, int ld, const int32_t* y,
+                            const float* rw, const float* inv_wsum, float* R, double* loss,
+                            hipStream_t s);
+
+// ---- windowed feature extraction over raw [S, A] streams ----
+int har_window_features(const float* stream, int64_t n_samples, int axes, int window, int stride,
+                        int64_t n_windows, float hz, int nbins, float* out, int ld_out, hipStream_t s);
+
+// ---- trees ----
+int har_tree_hist(const uint8_t* bins, int64_t n_rows, int n_feat, const int32_t* rows, const int32_t* node_start,
+                  const int32_t* node_count, int n_nodes, const int32_t* feats, int m_feats, const int32_t* label,
+                  const uint8_t* weight, int64_t weight_stride, const int32_t* node_tree, int n_bins, int n_classes,
+                  float* hist, hipStream_t s);
+int har_tree_split(const float* hist, int n_nodes, int m_feats, int n_bins, int n_classes, const int32_t* feats,
+                   const int32_t* nbins_feat, int min_instances, float min_info_gain, int impurity,
+                   int32_t* best_feat, int32_t* best_bin, float* best_gain, float* node_stats, hipStream_t s);
+int har_forest_predict(const float* X, int64_t n, int F, int ld, const int32_t* feat, const float* thr,
+                       const int32_t* left, const int32_t* right, const float* leaf, const int32_t* roots,
+                       int ntrees, int K, int max_depth, float* raw_out, hipStream_t s);
+
+// ---- CSV on device ----
+int har_csv_count_lines(const uint8_t* buf, int64_t n, int64_t* block_counts, int nblocks, hipStream_t s);
+
+#ifdef __cplusplus
+}
+#endif

@@ -1,0 +1,66 @@
+// Evaluation reductions: confusion matrix and regression
+// moments.  LDS-privatized counters per workgroup, one global atomic per
+// counter per workgroup; fp64 accumulation for the moments.
+#include "common.h"
+#include "../har_kernels.h"
+
+namespace {
+
+constexpr int MAXK2 = 64 * 64;
+
+__global__ __launch_bounds__(256) void confusion_kernel(const int32_t* __restrict__ label,
+                                                        const int32_t* __restrict__ pred, int64_t n, int K,
+                                                        unsigned long long* __restrict__ cm) {
+  __shared__ unsigned int h[MAXK2];
+  const int KK = K * K;
+  for (int i = threadIdx.x; i < KK; i += blockDim.x) h[i] = 0;
+  __syncthreads();
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    atomicAdd(&h[label[i] * K + pred[i]], 1u);
+  __syncthreads();
+  for (int i = threadIdx.x; i < KK; i += blockDim.x)
+    if (h[i]) atomicAdd(cm + i, (unsigned long long)h[i]);
+}
+
+__global__ __launch_bounds__(256) void moments_kernel(const float* __restrict__ y, const float* __restrict__ yh,
+                                                      int64_t n, double* __restrict__ out) {
+  double c = 0, se = 0, ae = 0, sy = 0, syy = 0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    double a = y[i], d = a - (double)yh[i];
+    c += 1; se += d * d; ae += fabs(d); sy += a; syy += a * a;
+  }
+  __shared__ double red[5][4];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  double v[5] = {c, se, ae, sy, syy};
+#pragma unroll
+  for (int k = 0; k < 5; ++k) {
+    double s = wave_sum_d(v[k]);
+    if (lane == 0) red[k][w] = s;
+  }
+  __syncthreads();
+  if (threadIdx.x < 5) {
+    double s = 0;
+    for (int j = 0; j < (int)(blockDim.x >> 6); ++j) s += red[threadIdx.x][j];
+    atomicAdd(out + threadIdx.x, s);
+  }
+}
+
+}  // namespace
+
+extern "C" int har_confusion_matrix(const int32_t* label, const int32_t* pred, int64_t n, int K, int64_t* cm,
+                                    hipStream_t s) {
+  if (K * K > MAXK2) return -2;
+  if (n == 0) return 0;
+  int blocks = (int)std::min<int64_t>(1024, (n + 255) / 256);
+  confusion_kernel<<<blocks, 256, 0, s>>>(label, pred, n, K, reinterpret_cast<unsigned long long*>(cm));
+  HAR_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int har_regression_moments(const float* y, const float* yhat, int64_t n, double* out6, hipStream_t s) {
+  if (n == 0) return 0;
+  int blocks = (int)std::min<int64_t>(1024, (n + 255) / 256);
+  moments_kernel<<<blocks, 256, 0, s>>>(y, yhat, n, out6);
+  HAR_CHECK_LAUNCH();
+  return 0;
+}

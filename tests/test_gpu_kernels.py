@@ -1,0 +1,213 @@
+"""Numerics of every HIP kernel vs. a plain PyTorch fp32/fp64 reference (GPU only)."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _bf(x):
+    return x.to(torch.bfloat16)
+
+
+LAYOUT_SHAPES = [(1000, 96, 160), (256, 256, 256), (77, 40, 64), (4096, 64, 512), (64, 32, 1024), (130, 520, 96)]
+
+
+@pytest.mark.parametrize("M,N,K", LAYOUT_SHAPES)
+@pytest.mark.parametrize("layout", [0, 2, 3])
+def test_gemm_bf16_layouts(cuda, M, N, K, layout):
+    from har.ops.gemm import EPI_F32, gemm_bf16
+
+    if layout & 1 and M % 8:
+        pytest.skip("M-major A needs M % 8 == 0 (16-byte vector rows)")
+    g = torch.Generator(device=cuda).manual_seed(M * 7 + N * 3 + K + layout)
+    A = torch.randn(M, K, device=cuda, generator=g)
+    Bm = torch.randn(K, N, device=cuda, generator=g)
+    ref = _bf(A).float() @ _bf(Bm).float()
+    a_store = _bf(A.T.contiguous()) if layout & 1 else _bf(A)          # [K][M] or [M][K]
+    b_store = _bf(Bm) if layout & 2 else _bf(Bm.T.contiguous())        # [K][N] or [N][K]
+    C = torch.full((M, N), float("nan"), device=cuda)
+    gemm_bf16(a_store, b_store, C, M=M, N=N, K=K, layout=layout, epi=EPI_F32)
+    torch.testing.assert_close(C, ref, rtol=2e-3, atol=2e-3 * K ** 0.5)
+
+
+@pytest.mark.parametrize("M,N,K", [(300, 64, 4096), (32, 256, 65536 // 8), (256, 48, 3000 // 8 * 8)])
+def test_gemm_bf16_splitk_atomic(cuda, M, N, K):
+    from har.ops.gemm import EPI_F32_ATOMIC, gemm_bf16
+
+    g = torch.Generator(device=cuda).manual_seed(5)
+    At = torch.randn(K, M, device=cuda, generator=g)   # stored [K][M]  (layout bit0)
+    Bm = torch.randn(K, N, device=cuda, generator=g)   # stored [K][N]  (layout bit1)
+    ref = _bf(At).float().T @ _bf(Bm).float()
+    C = torch.zeros(M, N, device=cuda)
+    gemm_bf16(_bf(At), _bf(Bm), C, M=M, N=N, K=K, layout=3, epi=EPI_F32_ATOMIC)
+    torch.testing.assert_close(C, ref, rtol=2e-3, atol=3e-3 * K ** 0.5)
+
+
+def test_gemm_bf16_epilogues(cuda):
+    from har.ops.gemm import EPI_BIAS, EPI_BIAS_RELU, EPI_RELU_GRAD, gemm_bf16
+
+    M, N, K = 517, 192, 96
+    g = torch.Generator(device=cuda).manual_seed(11)
+    A = _bf(torch.randn(M, K, device=cuda, generator=g))
+    W = _bf(torch.randn(N, K, device=cuda, generator=g))
+    bias = torch.randn(N, device=cuda, generator=g)
+    ref = A.float() @ W.float().T + bias
+    out = torch.empty(M, N, dtype=torch.bfloat16, device=cuda)
+    gemm_bf16(A, W, out, M=M, N=N, K=K, layout=0, epi=EPI_BIAS_RELU, bias=bias)
+    torch.testing.assert_close(out.float(), torch.relu(ref).to(torch.bfloat16).float(), rtol=1e-2, atol=2e-2)
+    gemm_bf16(A, W, out, M=M, N=N, K=K, layout=0, epi=EPI_BIAS, bias=bias)
+    torch.testing.assert_close(out.float(), ref.to(torch.bfloat16).float(), rtol=1e-2, atol=2e-2)
+    # relu-grad: dX = (dY . W) * (mask > 0), colsum -> bias grad
+    dY = _bf(torch.randn(M, N, device=cuda, generator=g))
+    mask = _bf(torch.randn(M, K, device=cuda, generator=g))
+    colsum = torch.zeros(K, device=cuda)
+    dX = torch.empty(M, K, dtype=torch.bfloat16, device=cuda)
+    gemm_bf16(dY, W, dX, M=M, N=K, K=N, layout=2, epi=EPI_RELU_GRAD, mask=mask, colsum=colsum)
+    refd = (dY.float() @ W.float()) * (mask.float() > 0)
+    torch.testing.assert_close(dX.float(), refd, rtol=1e-2, atol=5e-2)
+    torch.testing.assert_close(colsum, dX.float().sum(0), rtol=1e-4, atol=1e-3)
+
+
+@pytest.mark.parametrize("M,N,K", [(3793, 272, 3100), (100, 8, 12), (1625, 8, 3100)])
+def test_gemm_f32_exact(cuda, M, N, K):
+    from har.ops.gemm import EPI_BIAS_F32, EPI_F32_ATOMIC, gemm_f32
+
+    g = torch.Generator(device=cuda).manual_seed(3)
+    X = torch.randn(M, K, device=cuda, generator=g)
+    W = torch.randn(N, K, device=cuda, generator=g)
+    b = torch.randn(N, device=cuda, generator=g)
+    Z = torch.empty(M, N, device=cuda)
+    gemm_f32(X, W, Z, M=M, N=N, K=K, layout=0, epi=EPI_BIAS_F32, bias=b)
+    ref = (X.double() @ W.double().T + b.double()).float()
+    torch.testing.assert_close(Z, ref, rtol=1e-5, atol=1e-4)
+    # R^T X with R stored [M][N] (M-major for the transposed product)
+    G = torch.zeros(N, K, device=cuda)
+    gemm_f32(Z, X, G, M=N, N=K, K=M, layout=3, epi=EPI_F32_ATOMIC)
+    refg = (Z.double().T @ X.double()).float()
+    torch.testing.assert_close(G, refg, rtol=1e-4, atol=1e-3 * M ** 0.5)
+
+
+def test_softmax_ce_head(cuda):
+    from har.ops import _native
+
+    B, D, C = 1000, 128, 6
+    g = torch.Generator(device=cuda).manual_seed(1)
+    H = _bf(torch.randn(B, D, device=cuda, generator=g))
+    W = torch.zeros(32, D, device=cuda)
+    W[:C] = torch.randn(C, D, device=cuda, generator=g) * 0.2
+    Wb = _bf(W)
+    b = torch.zeros(32, device=cuda)
+    b[:C] = torch.randn(C, device=cuda, generator=g)
+    y = torch.randint(0, C, (B,), device=cuda, generator=g).to(torch.int32)
+    dl = torch.zeros(B, 32, dtype=torch.bfloat16, device=cuda)
+    db = torch.zeros(32, device=cuda)
+    loss = torch.zeros(1, device=cuda)
+    corr = torch.zeros(1, dtype=torch.int32, device=cuda)
+    logits = torch.empty(B, C, device=cuda)
+    scale = 1.0 / B
+    _native.kernels().softmax_ce_head(H.data_ptr(), Wb.data_ptr(), b.data_ptr(), y.data_ptr(), B, D, C, scale,
+                                      dl.data_ptr(), db.data_ptr(), loss.data_ptr(), corr.data_ptr(),
+                                      logits.data_ptr(), _native.stream_ptr())
+    z = H.float() @ Wb.float()[:C].T + b[:C]
+    torch.testing.assert_close(logits, z, rtol=1e-4, atol=1e-3)
+    ref_loss = torch.nn.functional.cross_entropy(z, y.long(), reduction="sum")
+    torch.testing.assert_close(loss[0], ref_loss, rtol=1e-4, atol=1e-2)
+    p = torch.softmax(z, 1)
+    p[torch.arange(B), y.long()] -= 1
+    torch.testing.assert_close(dl[:, :C].float(), (p * scale).to(torch.bfloat16).float(), rtol=1e-2, atol=1e-5)
+    assert dl[:, C:].float().abs().max() == 0
+    torch.testing.assert_close(db[:C], dl[:, :C].float().sum(0), rtol=1e-4, atol=1e-5)
+    assert int(corr[0]) == int((z.argmax(1) == y.long()).sum())
+
+
+def test_adam_step(cuda):
+    from har.ops import _native
+
+    n = 1037
+    g = torch.Generator(device=cuda).manual_seed(2)
+    p = torch.randn(n, device=cuda, generator=g)
+    p0 = p.clone()
+    grad = torch.randn(n, device=cuda, generator=g)
+    m = torch.zeros(n, device=cuda)
+    v = torch.zeros(n, device=cuda)
+    pb = torch.empty(n, dtype=torch.bfloat16, device=cuda)
+    step = torch.zeros(1, dtype=torch.int32, device=cuda)
+    lr, b1, b2, eps, wd = 1e-2, 0.9, 0.999, 1e-8, 0.01
+    for t in range(1, 4):
+        _native.kernels().adam_step(p.data_ptr(), grad.data_ptr(), m.data_ptr(), v.data_ptr(), pb.data_ptr(), n,
+                                    lr, b1, b2, eps, wd, 1.0, step.data_ptr(), _native.stream_ptr())
+    # reference
+    pr, mr, vr = p0.double(), torch.zeros(n, dtype=torch.float64, device=cuda), torch.zeros(n, dtype=torch.float64,
+                                                                                           device=cuda)
+    gd = grad.double()
+    for t in range(1, 4):
+        mr = b1 * mr + (1 - b1) * gd
+        vr = b2 * vr + (1 - b2) * gd * gd
+        upd = (mr / (1 - b1 ** t)) / ((vr / (1 - b2 ** t)).sqrt() + eps)
+        pr = pr - lr * (upd + wd * pr)
+    torch.testing.assert_close(p.double(), pr, rtol=1e-5, atol=1e-5)
+    assert int(step[0]) == 3
+    torch.testing.assert_close(pb.float(), p.to(torch.bfloat16).float())
+
+
+def test_mlp_step_matches_torch(cuda):
+    from har.models.mlp import MLPEngine, pad_input_bf16
+
+    B = 512
+    layers = [43, 64, 96, 6]
+    eng = MLPEngine(layers, B, cuda, lr=1e-3, seed=3)
+    ref = MLPEngine(layers, B, "cpu", lr=1e-3, seed=3)
+    g = torch.Generator(device=cuda).manual_seed(9)
+    X = torch.randn(B, 43, device=cuda, generator=g)
+    y = torch.randint(0, 6, (B,), device=cuda, generator=g)
+    Xb = pad_input_bf16(X, eng.layout.in_pad)
+    eng.forward_backward_native(Xb, y.to(torch.int32), 1.0 / B)
+    # reference gradient on the same bf16-rounded inputs, fp32 math
+    Xr = torch.zeros(B, eng.layout.in_pad)
+    Xr[:, :43] = Xb[:, :43].float().cpu()
+    P = eng.P.detach().cpu().clone().requires_grad_(True)
+    z = ref.torch_forward(P, Xr)
+    loss = torch.nn.functional.cross_entropy(z, y.cpu(), reduction="sum") / B
+    (gref,) = torch.autograd.grad(loss, P)
+    G = eng.G.cpu()
+    for seg in eng.layout.segments:
+        a = G[seg.offset: seg.offset + seg.numel]
+        r = gref[seg.offset: seg.offset + seg.numel]
+        rel = (a - r).norm() / r.norm().clamp_min(1e-12)
+        assert rel < 3e-2, f"{seg.name}: rel err {rel:.3e}"
+    torch.testing.assert_close(eng.loss_sum[0].cpu() / B, loss.detach(), rtol=2e-2, atol=2e-2)
+
+
+def test_logreg_objective_native_vs_torch(cuda):
+    from har.ops.logreg import LogregWorkspace, logreg_loss_grad_native, logreg_loss_grad_torch
+
+    N, F, B, K = 777, 124, 5, 6
+    g = torch.Generator(device=cuda).manual_seed(4)
+    X = torch.randn(N, F, device=cuda, generator=g)
+    y = torch.randint(0, K, (N,), device=cuda, generator=g)
+    W = torch.randn(B, K, F, device=cuda, generator=g) * 0.1
+    b = torch.randn(B, K, device=cuda, generator=g)
+    rw = (torch.rand(B, N, device=cuda, generator=g) > 0.2).float()
+    inv = 1.0 / rw.sum(1)
+    ws = LogregWorkspace(X, B, K)
+    l1, g1, b1 = logreg_loss_grad_native(X, y.to(torch.int32), W, b, rw, inv, ws)
+    l2, g2, b2 = logreg_loss_grad_torch(X.double(), y, W.double(), b.double(), rw.double(), inv.double())
+    torch.testing.assert_close(l1.double(), l2, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(g1.double(), g2, rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(b1.double(), b2, rtol=1e-4, atol=1e-5)
+
+
+def test_metrics_kernels(cuda):
+    from har.ops.metrics import confusion_matrix, regression_moments
+
+    g = torch.Generator(device=cuda).manual_seed(8)
+    y = torch.randint(0, 6, (10001,), device=cuda, generator=g)
+    p = torch.randint(0, 6, (10001,), device=cuda, generator=g)
+    cm = confusion_matrix(y, p, 6)
+    ref = torch.bincount((y * 6 + p).cpu(), minlength=36).view(6, 6)
+    assert torch.equal(cm.cpu(), ref)
+    n, se, ae, sy, syy = regression_moments(y.float(), p.float())
+    d = (y - p).double().cpu()
+    assert n == 10001
+    assert abs(se - float((d * d).sum())) < 1e-6 and abs(ae - float(d.abs().sum())) < 1e-6
+    assert abs(sy - float(y.double().sum())) < 1e-6

@@ -1,0 +1,47 @@
+#!/bin/bash
+# One gpurun session: GPU tests -> 1-GPU bench -> rocprofv3 kernel stats.
+# Every GPU step has its own time limit; a fault / abort / timeout ends the script
+# (exit codes 124, 134, 137, 139 or >128), plain test failures (exit 1) do not.
+#   usage: gpurun --timeout 1200 -- bash tools/gpu_session.sh [tests|bench|prof|all] [extra pytest args]
+set -u
+ROOT="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
+OUT="$ROOT/gpurun_out"
+mkdir -p "$OUT"
+cd "$ROOT"
+WHAT="${1:-all}"
+shift || true
+
+fatal() {  # $1 = exit code, $2 = step
+  local rc=$1
+  if [ "$rc" -ne 0 ] && [ "$rc" -ne 1 ] && [ "$rc" -ne 5 ]; then
+    echo "STEP $2 ended with fatal status $rc — stopping" | tee -a "$OUT/session.log"
+    exit "$rc"
+  fi
+}
+
+echo "== session $WHAT $(date)" | tee -a "$OUT/session.log"
+python tools/build_native.py > "$OUT/build.log" 2>&1 || { echo "build failed"; cat "$OUT/build.log"; exit 3; }
+
+if [ "$WHAT" = "tests" ] || [ "$WHAT" = "all" ]; then
+  timeout -k 10 900 python -m pytest tests -m gpu -q -x "$@" > "$OUT/pytest_gpu.log" 2>&1
+  rc=$?
+  tail -25 "$OUT/pytest_gpu.log"
+  fatal $rc pytest
+fi
+
+if [ "$WHAT" = "bench" ] || [ "$WHAT" = "all" ]; then
+  timeout -k 10 300 python bench.py --steps 50 --warmup 10 --out "$OUT/bench_1gpu.json" > "$OUT/bench.log" 2>&1
+  rc=$?
+  tail -3 "$OUT/bench.log"
+  fatal $rc bench
+fi
+
+if [ "$WHAT" = "prof" ] || [ "$WHAT" = "all" ]; then
+  export TMPDIR=/tmp
+  (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o bench -- \
+      python3 "$ROOT/bench.py" --steps 20 --warmup 5 --graph 0 > "$OUT/prof.log" 2>&1)
+  rc=$?
+  tail -3 "$OUT/prof.log"
+  fatal $rc rocprof
+fi
+echo "== done" | tee -a "$OUT/session.log"
