@@ -32,7 +32,7 @@ import torch
 
 from ..data.table import Table
 from ..ops import _native, rng
-from ..ops.gemm import EPI_BIAS_RELU, EPI_F32_ATOMIC, EPI_RELU_GRAD, gemm_bf16
+from ..ops.gemm import EPI_BIAS_RELU, EPI_F32_SLAB, EPI_RELU_GRAD, gemm_bf16, tile_counts
 from .base import ClassificationModel, ClassifierParams, Estimator, features_tensor, labels_tensor, new_uid, \
     resolve_device
 
@@ -41,6 +41,18 @@ HEAD_PAD = 32  # classes padded to 32 rows (two 16-wide MFMA column tiles)
 
 def _pad(x: int, m: int) -> int:
     return (x + m - 1) // m * m
+
+
+def n_splits_for(batch: int) -> int:
+    """Batch slices of the split-K weight-gradient GEMMs (>= 1024-row slices, <= 64 slabs)."""
+    return max(1, min(64, batch // 1024))
+
+
+def wgrad_tile(M: int, N: int) -> int:
+    """Weight-gradient tiles: small output tiles so (tiles x splits) fills the chip."""
+    if M <= 32:
+        return 5 if N > 32 else 2
+    return 4
 
 
 @dataclass
@@ -132,9 +144,15 @@ class MLPEngine:
             hmax = max(L.hidden) if L.hidden else HEAD_PAD
             self.dbuf = [torch.empty(self.B * hmax, dtype=torch.bfloat16, device=dev) for _ in range(2)]
             self.dlogits = torch.zeros(self.B, HEAD_PAD, dtype=torch.bfloat16, device=dev)
-            self.loss_sum = torch.zeros(1, dtype=torch.float32, device=dev)
-            self.correct = torch.zeros(1, dtype=torch.int32, device=dev)
+            nblk = _native.kernels().softmax_ce_head_blocks(self.B)
+            self.block_loss = torch.zeros(nblk, dtype=torch.float32, device=dev)
+            self.block_correct = torch.zeros(nblk, dtype=torch.int32, device=dev)
             self.dims = dims
+            # deterministic split-K: every weight-grad GEMM splits the batch into the same
+            # <= n_splits slices and writes plain partial tiles into slab z of a
+            # [n_splits, total] workspace laid out like the flat parameter buffer.
+            self.n_splits = n_splits_for(self.B)
+            self.slabs = torch.zeros(self.n_splits, L.total, dtype=torch.float32, device=dev)
         else:
             self.t_step = 0
 
@@ -142,13 +160,20 @@ class MLPEngine:
     def _w(self, flat, name):
         return self.layout.view(flat, name)
 
+    def _slab(self, name):
+        s = self.layout.by_name[name]
+        return self.slabs.view(-1)[s.offset:]
+
     def forward_backward_native(self, Xb: torch.Tensor, y32: torch.Tensor, scale: float):
-        """Xb: [B, in_pad] bf16 (contiguous slice), y32: [B] int32."""
+        """Xb: [B, in_pad] bf16 (contiguous slice), y32: [B] int32.  Leaves the split-K
+        gradient partials in ``self.slabs[:self.active_splits]``."""
         L, mod, s = self.layout, _native.kernels(), _native.stream_ptr()
         B = Xb.shape[0]
-        if Xb.shape[1] != L.in_pad or Xb.dtype != torch.bfloat16 or B > self.B:
+        if Xb.shape[1] != L.in_pad or Xb.dtype != torch.bfloat16 or B > self.B or y32.dtype != torch.int32:
             raise ValueError("bad batch")
-        self.G.zero_()
+        ks = max(32, ((B + self.n_splits - 1) // self.n_splits + 31) // 32 * 32)
+        self.active_splits = (B + ks - 1) // ks
+        total = L.total
         nh = len(L.hidden)
         acts = [Xb] + [a[:B] for a in self.acts[1:]]
         for i in range(nh):
@@ -157,28 +182,38 @@ class MLPEngine:
         last = acts[nh]
         mod.softmax_ce_head(last.data_ptr(), self._w(self.Pb, "Wout").data_ptr(), self._w(self.P, "bout").data_ptr(),
                             y32.data_ptr(), B, self.dims[-1], L.num_classes, float(scale), self.dlogits.data_ptr(),
-                            self._w(self.G, "bout").data_ptr(), self.loss_sum.data_ptr(), self.correct.data_ptr(), 0, s)
+                            self.block_loss.data_ptr(), self.block_correct.data_ptr(), 0, s)
+        self.last_batch = B
         dl = self.dlogits[:B]
-        # dWout = dlogits^T . last
-        gemm_bf16(dl, last, self._w(self.G, "Wout"), M=HEAD_PAD, N=self.dims[-1], K=B, layout=3, epi=EPI_F32_ATOMIC)
+        # dWout = dlogits^T . last  (+ dbout = row sums of dlogits^T)
+        gemm_bf16(dl, last, self._slab("Wout"), M=HEAD_PAD, N=self.dims[-1], K=B, layout=3, epi=EPI_F32_SLAB,
+                  k_split=ks, ldc=self.dims[-1], slab_stride=total, rowsum=self._slab("bout"),
+                  slab_stride_rowsum=total, tile=wgrad_tile(HEAD_PAD, self.dims[-1]))
         d, dW_in = dl, "Wout"
         for i in reversed(range(nh)):
             h = self.dims[i + 1]
             dact = self.dbuf[i % 2][: B * h].view(B, h)
             Wnext = self._w(self.Pb, dW_in)
-            # dact = (d . Wnext) * relu'(acts[i+1]);   db_i = colsum(dact)
-            gemm_bf16(d, Wnext, dact, M=B, N=h, K=Wnext.shape[0], layout=2, epi=EPI_RELU_GRAD,
-                      mask=acts[i + 1], colsum=self._w(self.G, f"b{i}"))
-            # dW_i = dact^T . acts[i]
-            gemm_bf16(dact, acts[i], self._w(self.G, f"W{i}"), M=h, N=self.dims[i], K=B, layout=3,
-                      epi=EPI_F32_ATOMIC)
+            # dact = (d . Wnext) * relu'(acts[i+1])
+            gemm_bf16(d, Wnext, dact, M=B, N=h, K=Wnext.shape[0], layout=2, epi=EPI_RELU_GRAD, mask=acts[i + 1])
+            # dW_i = dact^T . acts[i]   (+ db_i = row sums of dact^T)
+            gemm_bf16(dact, acts[i], self._slab(f"W{i}"), M=h, N=self.dims[i], K=B, layout=3, epi=EPI_F32_SLAB,
+                      k_split=ks, ldc=self.dims[i], slab_stride=total, rowsum=self._slab(f"b{i}"),
+                      slab_stride_rowsum=total, tile=wgrad_tile(h, self.dims[i]))
             d, dW_in = dact, f"W{i}"
 
-    def optimizer_step_native(self):
+    def reduce_grads_native(self):
+        """G = sum of the active gradient slabs (needed before a collective)."""
+        _native.kernels().reduce_slabs(self.slabs.data_ptr(), self.active_splits, self.layout.total,
+                                       self.G.data_ptr(), _native.stream_ptr())
+
+    def optimizer_step_native(self, from_slabs: bool):
         b1, b2 = self.betas
-        _native.kernels().adam_step(self.P.data_ptr(), self.G.data_ptr(), self.m.data_ptr(), self.v.data_ptr(),
-                                    self.Pb.data_ptr(), self.P.numel(), float(self.lr), b1, b2, float(self.eps),
-                                    float(self.wd), 1.0, self.step_count.data_ptr(), _native.stream_ptr())
+        _native.kernels().adam_step(self.P.data_ptr(), self.G.data_ptr(),
+                                    self.slabs.data_ptr() if from_slabs else 0, self.active_splits,
+                                    self.m.data_ptr(), self.v.data_ptr(), self.Pb.data_ptr(), self.P.numel(),
+                                    float(self.lr), b1, b2, float(self.eps), float(self.wd), 1.0,
+                                    self.step_count.data_ptr(), _native.stream_ptr())
 
     def allreduce_grads(self):
         if self.world > 1:
@@ -188,10 +223,18 @@ class MLPEngine:
     def train_step(self, Xb: torch.Tensor, yb: torch.Tensor, global_batch: int):
         if self.native:
             self.forward_backward_native(Xb, yb, 1.0 / global_batch)
-            self.allreduce_grads()
-            self.optimizer_step_native()
+            if self.world > 1:
+                self.reduce_grads_native()
+                self.allreduce_grads()
+                self.optimizer_step_native(from_slabs=False)
+            else:  # single GPU: the slab reduction is fused into Adam
+                self.optimizer_step_native(from_slabs=True)
         else:
             self.train_step_torch(Xb, yb, global_batch)
+
+    def last_loss_and_correct(self):
+        """(sum of CE, #correct) of the last native batch — one host sync."""
+        return float(self.block_loss.sum().item()), int(self.block_correct.sum().item())
 
     # ---------------------------------------------------------------- torch
     def torch_forward(self, P: torch.Tensor, X: torch.Tensor):
@@ -236,7 +279,7 @@ class MLPEngine:
                               K=self.dims[i], layout=0, epi=EPI_BIAS_RELU, bias=self._w(self.P, f"b{i}"))
                 _native.kernels().softmax_ce_head(acts[-1].data_ptr(), self._w(self.Pb, "Wout").data_ptr(),
                                                   self._w(self.P, "bout").data_ptr(), 0, B, self.dims[-1],
-                                                  L.num_classes, 1.0, 0, 0, 0, 0, out[r0:r1].data_ptr(),
+                                                  L.num_classes, 1.0, 0, 0, 0, out[r0:r1].data_ptr(),
                                                   _native.stream_ptr())
             return out
         Xp = torch.zeros(X.shape[0], L.in_pad, dtype=torch.float32, device=X.device)

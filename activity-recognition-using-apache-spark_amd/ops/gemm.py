@@ -4,6 +4,10 @@
 So ``layout=0`` is ``A[M,K] . B[N,K]^T`` (forward of a Linear layer),
 ``layout=2`` is ``A[M,K] . B[K,N]`` (data gradient), ``layout=3`` is
 ``A[K,M]^T . B[K,N]`` (weight gradient).
+
+Split-K products (``EPI_F32_ATOMIC`` / ``EPI_F32_SLAB``) run ``ceil(K/k_split)``
+workgroup slices; ``EPI_F32_SLAB`` writes each slice's partial tile into its
+own slab (``C + z*slab_stride``) for a deterministic reduction pass.
 """
 from __future__ import annotations
 
@@ -13,24 +17,28 @@ import torch
 
 from . import _native
 
-EPI_F32, EPI_F32_ATOMIC, EPI_BIAS_RELU, EPI_BIAS, EPI_RELU_GRAD, EPI_BIAS_F32 = range(6)
-_TARGET_BLOCKS = 1024  # >> 256 CUs, bounded atomic traffic
+EPI_F32, EPI_F32_ATOMIC, EPI_BIAS_RELU, EPI_BIAS, EPI_RELU_GRAD, EPI_BIAS_F32, EPI_F32_SLAB = range(7)
+TILES = {0: (128, 128), 1: (128, 64), 2: (128, 32), 3: (64, 128), 4: (64, 64), 5: (32, 64)}
+_TARGET_BLOCKS = 1024  # >> 256 CUs, bounded split-K traffic
 
 
-def _tile_counts(M: int, N: int):
+def auto_tile(M: int, N: int) -> int:
     if N <= 32:
-        bm, bn = 128, 32
-    elif N <= 64:
-        bm, bn = 128, 64
-    elif M <= 64:
-        bm, bn = 64, 128
-    else:
-        bm, bn = 128, 128
+        return 2
+    if N <= 64:
+        return 1
+    if M <= 64:
+        return 3
+    return 0
+
+
+def tile_counts(M: int, N: int, tile: int = -1):
+    bm, bn = TILES[auto_tile(M, N) if tile < 0 else tile]
     return (M + bm - 1) // bm, (N + bn - 1) // bn
 
 
-def auto_k_split(M: int, N: int, K: int) -> int:
-    tm, tn = _tile_counts(M, N)
+def auto_k_split(M: int, N: int, K: int, tile: int = -1) -> int:
+    tm, tn = tile_counts(M, N, tile)
     splits = max(1, min((K + 31) // 32, _TARGET_BLOCKS // max(1, tm * tn)))
     ks = (K + splits - 1) // splits
     return max(32, (ks + 31) // 32 * 32)
@@ -45,12 +53,13 @@ def _check(t: torch.Tensor, name: str):
         raise ValueError(f"{name} must be 16-byte aligned")
 
 
-def _gemm(bf16: bool, A, B, C, M, N, K, layout, epi, bias=None, mask=None, colsum=None,
-          k_split: Optional[int] = None, alpha: float = 1.0, lda=None, ldb=None, ldc=None):
+def _gemm(bf16: bool, A, B, C, M, N, K, layout, epi, bias=None, mask=None, rowsum=None,
+          k_split: Optional[int] = None, alpha: float = 1.0, lda=None, ldb=None, ldc=None, tile: int = -1,
+          slab_stride: int = 0, slab_stride_rowsum: int = 0):
     for t, n in ((A, "A"), (B, "B"), (C, "C")):
         _check(t, n)
-    if epi == EPI_F32_ATOMIC and k_split is None:
-        k_split = auto_k_split(M, N, K)
+    if epi in (EPI_F32_ATOMIC, EPI_F32_SLAB) and k_split is None:
+        k_split = auto_k_split(M, N, K, tile)
     lda = A.stride(0) if lda is None else lda
     ldb = B.stride(0) if ldb is None else ldb
     ldc = C.stride(0) if ldc is None else ldc
@@ -58,12 +67,18 @@ def _gemm(bf16: bool, A, B, C, M, N, K, layout, epi, bias=None, mask=None, colsu
     # host-side shape contract (mirrors the kernel's): rows addressed must exist
     a_rows = K if layout & 1 else M
     b_rows = K if layout & 2 else N
-    if A.shape[0] < a_rows or B.shape[0] < b_rows or C.shape[0] < M:
+    if A.shape[0] < a_rows or B.shape[0] < b_rows or (epi != EPI_F32_SLAB and C.shape[0] < M):
         raise ValueError(f"gemm operand too small: A{tuple(A.shape)} B{tuple(B.shape)} C{tuple(C.shape)} "
                          f"for M={M} N={N} K={K} layout={layout}")
+    if epi == EPI_F32_SLAB:
+        splits = (K + k_split - 1) // k_split
+        need = (splits - 1) * slab_stride + (M - 1) * ldc + N
+        if C.numel() < need:
+            raise ValueError(f"slab buffer too small ({C.numel()} < {need})")
     _native.kernels().gemm(bf16, layout, epi, A.data_ptr(), B.data_ptr(), C.data_ptr(), _native.ptr(bias),
-                           _native.ptr(mask), _native.ptr(colsum), M, N, K, lda, ldb, ldc, ldm,
-                           int(k_split or 0), float(alpha), _native.stream_ptr())
+                           _native.ptr(mask), _native.ptr(rowsum), M, N, K, lda, ldb, ldc, ldm,
+                           int(k_split or 0), int(tile), int(slab_stride), int(slab_stride_rowsum), float(alpha),
+                           _native.stream_ptr())
     return C
 
 

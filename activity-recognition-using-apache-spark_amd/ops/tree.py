@@ -1,0 +1,180 @@
+"""Tree-learning device ops.
+
+* ``find_thresholds``  — per-feature candidate thresholds (Spark ``findSplits``):
+  sorted distinct values -> midpoints when there are few, quantile cut points
+  otherwise; at most ``max_bins - 1`` per feature.
+* ``bin_features``     — fp32 -> uint8 bin ids, stored feature-major [F, N].
+* ``hist_split``       — the level step: for every active (tree, node) build the
+  weighted per-(feature, bin, class) histogram of its rows over its sampled
+  features and pick the best (feature, bin) by impurity gain.  GPU: one fused
+  HIP kernel (``har_tree_hist_split``) — an LDS-privatized histogram per
+  (node, feature-chunk) workgroup, then a wave-parallel prefix scan over bins +
+  gain + argmax, so histograms never touch HBM.  CPU: the same math with
+  ``bincount`` (the oracle).
+* ``forest_predict``   — traverse all trees for every row and accumulate the
+  (normalized) leaf statistics; GPU: ``har_forest_predict``.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+from . import _native
+
+GINI, ENTROPY = 0, 1
+LDS_BUDGET = 96 * 1024  # bytes of LDS histogram per workgroup
+
+
+def find_thresholds(X: np.ndarray, max_bins: int, sample_rows: int = 10000, seed: int = 0):
+    """List of float32 threshold arrays (``x <= thr[b]`` goes left at split b)."""
+    N, F = X.shape
+    if N > sample_rows:  # Spark samples max(maxBins^2, 10000) rows for findSplits
+        rs = np.random.default_rng(seed)
+        X = X[np.sort(rs.choice(N, size=max(sample_rows, max_bins * max_bins), replace=False))]
+    out = []
+    n_splits = max_bins - 1
+    for f in range(F):
+        v = X[:, f]
+        v = v[~np.isnan(v)]
+        u, cnt = np.unique(v, return_counts=True)
+        if len(u) <= 1:
+            out.append(np.zeros(0, dtype=np.float32))
+            continue
+        if len(u) - 1 <= n_splits:
+            thr = (u[:-1] + u[1:]) / 2.0
+        else:
+            # quantile cut points on the (weighted) distinct values
+            cum = np.cumsum(cnt)
+            total = cum[-1]
+            targets = total * np.arange(1, n_splits + 1) / (n_splits + 1)
+            idx = np.searchsorted(cum, targets, side="left")
+            idx = np.unique(np.clip(idx, 0, len(u) - 2))
+            thr = (u[idx] + u[idx + 1]) / 2.0
+        out.append(thr.astype(np.float32))
+    return out
+
+
+def bin_features(X: np.ndarray, thresholds) -> np.ndarray:
+    """uint8 bins, feature-major [F, N]: bin = #thresholds strictly below x."""
+    N, F = X.shape
+    bins = np.empty((F, N), dtype=np.uint8)
+    for f in range(F):
+        bins[f] = np.searchsorted(thresholds[f], X[:, f], side="left").astype(np.uint8)
+    return bins
+
+
+@dataclass
+class LevelResult:
+    gain: torch.Tensor      # [A] best gain (-inf if no valid split)
+    feat: torch.Tensor      # [A] best global feature id
+    bin: torch.Tensor       # [A] best bin (rows with bin <= b go left)
+    left: torch.Tensor      # [A, K] weighted class counts of the left child
+    total: torch.Tensor     # [A, K] weighted class counts of the node
+
+
+def _impurity(c: torch.Tensor, w: torch.Tensor, kind: int) -> torch.Tensor:
+    p = c / w.clamp_min(1e-30).unsqueeze(-1)
+    if kind == GINI:
+        return 1.0 - (p * p).sum(-1)
+    lp = torch.where(p > 0, torch.log2(p.clamp_min(1e-30)), torch.zeros_like(p))
+    return -(p * lp).sum(-1)
+
+
+def hist_split_torch(bins, nbins_feat, label, rows, row_w, key, n_nodes, feats, K, max_bins, min_instances,
+                     min_info_gain, impurity) -> LevelResult:
+    """CPU/oracle implementation.  ``rows``/``row_w``/``key`` list the (row, weight,
+    node) pairs; ``feats`` [A, m] sampled features per node."""
+    A, m = feats.shape
+    dev = bins.device
+    fe = feats[key]                                          # [P, m]
+    bv = bins[fe.long(), rows.long().unsqueeze(1)].long()    # [P, m]
+    y = label[rows.long()].long()
+    idx = ((key.long().unsqueeze(1) * m + torch.arange(m, device=dev)) * max_bins + bv) * K + y.unsqueeze(1)
+    w = row_w.float().unsqueeze(1).expand(-1, m)
+    hist = torch.zeros(A * m * max_bins * K, dtype=torch.float64, device=dev)
+    hist.index_add_(0, idx.reshape(-1), w.reshape(-1).double())
+    hist = hist.view(A, m, max_bins, K)
+    return split_from_hist(hist, feats, nbins_feat, min_instances, min_info_gain, impurity)
+
+
+def split_from_hist(hist, feats, nbins_feat, min_instances, min_info_gain, impurity) -> LevelResult:
+    A, m, nb, K = hist.shape
+    left = hist.cumsum(dim=2)                        # bins <= b go left
+    total = left[:, 0, -1, :]                        # [A, K]
+    right = total[:, None, None, :] - left
+    wl, wr = left.sum(-1), right.sum(-1)
+    wt = total.sum(-1)
+    imp_p = _impurity(total, wt, impurity)
+    gain = imp_p[:, None, None] - (wl / wt.clamp_min(1e-30)[:, None, None]) * _impurity(left, wl, impurity) \
+        - (wr / wt.clamp_min(1e-30)[:, None, None]) * _impurity(right, wr, impurity)
+    nbf = nbins_feat[feats.long()].long()            # [A, m]
+    valid = torch.arange(nb, device=hist.device)[None, None, :] < (nbf - 1)[:, :, None]
+    valid &= (wl >= min_instances) & (wr >= min_instances)
+    gain = torch.where(valid, gain, torch.full_like(gain, -float("inf")))
+    flat = gain.reshape(A, -1)
+    best = torch.argmax(flat, dim=1)
+    bg = flat.gather(1, best[:, None]).squeeze(1)
+    slot, b = best // nb, best % nb
+    bf = feats.long().gather(1, slot[:, None]).squeeze(1)
+    bl = left[torch.arange(A, device=hist.device), slot, b]
+    ok = torch.isfinite(bg) & (bg >= min_info_gain)
+    bg = torch.where(ok, bg, torch.full_like(bg, -float("inf")))
+    return LevelResult(gain=bg.float(), feat=bf.int(), bin=b.int(), left=bl.float(), total=total.float())
+
+
+def hist_split_native(bins, nbins_feat, label, rows, row_w, node_start, node_count, feats, K, max_bins,
+                      min_instances, min_info_gain, impurity) -> LevelResult:
+    A, m = feats.shape
+    F, N = bins.shape
+    fc = max(1, min(m, LDS_BUDGET // (max_bins * K * 4)))
+    chunks = (m + fc - 1) // fc
+    dev = bins.device
+    gain = torch.empty(A * chunks, dtype=torch.float32, device=dev)
+    feat = torch.empty(A * chunks, dtype=torch.int32, device=dev)
+    bin_ = torch.empty(A * chunks, dtype=torch.int32, device=dev)
+    left = torch.empty(A * chunks, K, dtype=torch.float32, device=dev)
+    total = torch.empty(A, K, dtype=torch.float32, device=dev)
+    if int(label.max()) >= K or int(label.min()) < 0:
+        raise ValueError("labels out of range")
+    _native.kernels().tree_hist_split(bins.data_ptr(), N, F, nbins_feat.data_ptr(), rows.data_ptr(),
+                                      row_w.data_ptr(), node_start.data_ptr(), node_count.data_ptr(), A,
+                                      feats.data_ptr(), m, fc, label.data_ptr(), K, max_bins, float(min_instances),
+                                      float(min_info_gain), impurity, gain.data_ptr(), feat.data_ptr(),
+                                      bin_.data_ptr(), left.data_ptr(), total.data_ptr(), _native.stream_ptr())
+    gain, feat, bin_, left = gain.view(A, chunks), feat.view(A, chunks), bin_.view(A, chunks), left.view(A, chunks, K)
+    best = torch.argmax(gain, dim=1)  # first max -> lowest chunk (lowest feature slot) on ties
+    ar = torch.arange(A, device=dev)
+    return LevelResult(gain=gain[ar, best], feat=feat[ar, best], bin=bin_[ar, best], left=left[ar, best],
+                       total=total)
+
+
+def forest_predict_torch(X, feature, threshold, left, right, leaf_stats, max_depth, normalize=True):
+    """X [N, F]; trees SoA [T, maxNodes]; returns summed (normalized) leaf stats [N, K]."""
+    T = feature.shape[0]
+    N = X.shape[0]
+    node = torch.zeros(T, N, dtype=torch.long, device=X.device)
+    tix = torch.arange(T, device=X.device)[:, None].expand(T, N)
+    for _ in range(max_depth + 1):
+        f = feature[tix, node].long()
+        is_leaf = f < 0
+        xv = X[torch.arange(N, device=X.device)[None, :].expand(T, N), f.clamp_min(0)]
+        go_left = xv <= threshold[tix, node]
+        nxt = torch.where(go_left, left[tix, node], right[tix, node]).long()
+        node = torch.where(is_leaf, node, nxt)
+    st = leaf_stats[tix, node]                      # [T, N, K]
+    if normalize:
+        st = st / st.sum(-1, keepdim=True).clamp_min(1e-30)
+    return st.sum(0)
+
+
+def forest_predict_native(X, feature, threshold, left, right, leaf_stats, max_depth, normalize=True):
+    T, maxn = feature.shape
+    N, F = X.shape
+    K = leaf_stats.shape[-1]
+    out = torch.zeros(N, K, dtype=torch.float32, device=X.device)
+    _native.kernels().forest_predict(X.contiguous().data_ptr(), N, F, X.stride(0), feature.data_ptr(),
+                                     threshold.data_ptr(), left.data_ptr(), right.data_ptr(), leaf_stats.data_ptr(),
+                                     T, maxn, K, max_depth, int(normalize), out.data_ptr(), _native.stream_ptr())
+    return out

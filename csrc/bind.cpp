@@ -75,18 +75,22 @@ static py::dict csv_parse(py::bytes data, bool header, int threads) {
   return out;
 }
 
-static GemmParams make_gemm(u A, u B, u C, u bias, u mask, u colsum, int M, int N, int K, int lda, int ldb,
-                            int ldc, int ldmask, int k_split, float alpha) {
+static GemmParams make_gemm(u A, u B, u C, u bias, u mask, u rowsum, int M, int N, int K, int lda, int ldb,
+                            int ldc, int ldmask, int k_split, int tile, int64_t slab_stride,
+                            int64_t slab_stride_rowsum, float alpha) {
   GemmParams p;
   p.A = P<const void>(A);
   p.B = P<const void>(B);
   p.C = P<void>(C);
   p.bias = P<const float>(bias);
   p.mask = P<const void>(mask);
-  p.colsum = P<float>(colsum);
+  p.rowsum = P<float>(rowsum);
   p.M = M; p.N = N; p.K = K;
   p.lda = lda; p.ldb = ldb; p.ldc = ldc; p.ldmask = ldmask;
   p.k_split = k_split;
+  p.tile = tile;
+  p.slab_stride = slab_stride;
+  p.slab_stride_rowsum = slab_stride_rowsum;
   p.alpha = alpha;
   return p;
 }
@@ -95,25 +99,32 @@ PYBIND11_MODULE(_har_native, m) {
   m.doc() = "har native runtime: host CSV parser + gfx950 HIP kernel launchers";
   m.def("csv_parse", &csv_parse, py::arg("data"), py::arg("header") = true, py::arg("threads") = 0);
 
-  m.def("gemm", [](bool bf16, int layout, int epi, u A, u B, u C, u bias, u mask, u colsum, int M, int N, int K,
-                   int lda, int ldb, int ldc, int ldmask, int k_split, float alpha, u stream) {
-    GemmParams p = make_gemm(A, B, C, bias, mask, colsum, M, N, K, lda, ldb, ldc, ldmask, k_split, alpha);
+  m.def("gemm", [](bool bf16, int layout, int epi, u A, u B, u C, u bias, u mask, u rowsum, int M, int N, int K,
+                   int lda, int ldb, int ldc, int ldmask, int k_split, int tile, int64_t slab_stride,
+                   int64_t slab_stride_rowsum, float alpha, u stream) {
+    GemmParams p = make_gemm(A, B, C, bias, mask, rowsum, M, N, K, lda, ldb, ldc, ldmask, k_split, tile, slab_stride,
+                             slab_stride_rowsum, alpha);
     check(bf16 ? har_gemm_bf16(&p, layout, epi, S(stream)) : har_gemm_f32(&p, layout, epi, S(stream)), "gemm");
   });
 
-  m.def("softmax_ce_head", [](u H, u W, u bias, u labels, int B, int D, int C, float scale, u dlogits, u dbias,
-                              u loss_sum, u correct, u logits_out, u stream) {
+  m.def("softmax_ce_head_blocks", &har_softmax_ce_head_blocks);
+  m.def("softmax_ce_head", [](u H, u W, u bias, u labels, int B, int D, int C, float scale, u dlogits,
+                              u block_loss, u block_correct, u logits_out, u stream) {
     check(har_softmax_ce_head(P<const uint16_t>(H), P<const uint16_t>(W), P<const float>(bias),
-                              P<const int32_t>(labels), B, D, C, scale, P<uint16_t>(dlogits), P<float>(dbias),
-                              P<float>(loss_sum), P<int32_t>(correct), P<float>(logits_out), S(stream)),
+                              P<const int32_t>(labels), B, D, C, scale, P<uint16_t>(dlogits), P<float>(block_loss),
+                              P<int32_t>(block_correct), P<float>(logits_out), S(stream)),
           "softmax_ce_head");
   });
 
-  m.def("adam_step", [](u param, u grad, u mm, u vv, u pb, int64_t n, float lr, float b1, float b2, float eps,
-                        float wd, float gs, u step, u stream) {
-    check(har_adam_step(P<float>(param), P<const float>(grad), P<float>(mm), P<float>(vv), P<uint16_t>(pb), n, lr,
-                        b1, b2, eps, wd, gs, P<int32_t>(step), S(stream)),
+  m.def("adam_step", [](u param, u grad, u slabs, int nslabs, u mm, u vv, u pb, int64_t n, float lr, float b1,
+                        float b2, float eps, float wd, float gs, u step, u stream) {
+    check(har_adam_step(P<float>(param), P<const float>(grad), P<const float>(slabs), nslabs, P<float>(mm),
+                        P<float>(vv), P<uint16_t>(pb), n, lr, b1, b2, eps, wd, gs, P<int32_t>(step), S(stream)),
           "adam_step");
+  });
+
+  m.def("reduce_slabs", [](u slabs, int nslabs, int64_t n, u dst, u stream) {
+    check(har_reduce_slabs(P<const float>(slabs), nslabs, n, P<float>(dst), S(stream)), "reduce_slabs");
   });
 
   m.def("logreg_softmax_grad", [](u Z, int64_t n, int B, int K, int ld, u y, u rw, u inv_wsum, u R, u loss,

@@ -16,10 +16,13 @@ typedef struct GemmParams {
   void* C;
   const float* bias;      // EPI_BIAS*, may be null
   const void* mask;       // EPI_RELU_GRAD: bf16 activations of the forward pass
-  float* colsum;          // EPI_RELU_GRAD: fused bias-gradient accumulator, may be null
+  float* rowsum;          // optional fused sum_k A(m,k) (bias gradient of a weight-grad product)
   int M, N, K;
   int lda, ldb, ldc, ldmask;
-  int k_split;            // EPI_F32_ATOMIC: K range per grid.z slice (multiple of 32)
+  int k_split;            // EPI_F32_ATOMIC / EPI_F32_SLAB: K range per grid.z slice (multiple of 32)
+  int tile;               // -1 = automatic tile choice, else tile id (gemm.hip)
+  int64_t slab_stride;    // EPI_F32_SLAB: elements between the C slabs of consecutive splits
+  int64_t slab_stride_rowsum;  // elements between rowsum slabs
   float alpha;
 } GemmParams;
 
@@ -27,17 +30,24 @@ int har_gemm_bf16(const GemmParams* p, int layout, int epi, hipStream_t s);
 int har_gemm_f32(const GemmParams* p, int layout, int epi, hipStream_t s);
 
 // Fused classifier head: logits = H . W^T + b (C <= 32 classes, W padded to 32 rows),
-// softmax, cross-entropy, dlogits = (p - onehot) * scale (bf16, 32 columns),
-// dbias += colsum(dlogits), loss_sum += sum CE, correct += #argmax==label.
+// softmax, cross-entropy, dlogits = (p - onehot) * scale (bf16, 32 columns).
+// Per-workgroup partial CE sums / correct counts go to block_loss[blockIdx] /
+// block_correct[blockIdx] (no same-address atomics; the host sums them lazily).
+// Returns the number of workgroups through *nblocks_out if non-null.
 int har_softmax_ce_head(const uint16_t* H, const uint16_t* W, const float* bias, const int32_t* labels,
-                        int B, int Hdim, int C, float scale, uint16_t* dlogits, float* dbias,
-                        float* loss_sum, int32_t* correct, float* logits_out, hipStream_t s);
+                        int B, int Hdim, int C, float scale, uint16_t* dlogits, float* block_loss,
+                        int32_t* block_correct, float* logits_out, hipStream_t s);
+int har_softmax_ce_head_blocks(int B);
 
 // Fused Adam(W) over a flat fp32 parameter buffer; also writes the bf16 compute copy.
+// Gradient = grad[i] (if slabs == null) or sum_s slabs[s*n + i] (fused split-K reduction).
 // The step counter (*step, device int32) is incremented on the stream before the update.
-int har_adam_step(float* param, const float* grad, float* m, float* v, uint16_t* param_bf16, int64_t n,
-                  float lr, float beta1, float beta2, float eps, float weight_decay, float grad_scale,
-                  int32_t* step, hipStream_t s);
+int har_adam_step(float* param, const float* grad, const float* slabs, int nslabs, float* m, float* v,
+                  uint16_t* param_bf16, int64_t n, float lr, float beta1, float beta2, float eps,
+                  float weight_decay, float grad_scale, int32_t* step, hipStream_t s);
+
+// dst[i] = sum_s slabs[s*n + i]  (deterministic split-K reduction)
+int har_reduce_slabs(const float* slabs, int nslabs, int64_t n, float* dst, hipStream_t s);
 
 // fp32 -> bf16 cast with row padding: out[r][0:cols_out] = in[r][0:cols_in], zero fill.
 int har_cast_pad_bf16(const float* in, int rows, int cols_in, int ld_in, uint16_t* out, int cols_out,

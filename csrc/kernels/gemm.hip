@@ -15,20 +15,28 @@
 //   bf16 : v_mfma_f32_16x16x32_bf16  (lane l: A[l&15][8(l>>4)+j], j<8)
 //   fp32 : v_mfma_f32_16x16x4_f32    (lane l: A[l&15][l>>4]) — exact fp32, used by LR
 // C/D map (both): col = lane&15, row = 4*(lane>>4) + reg.
+// Main loop: register-staged prefetch — the global loads of tile k+1 are issued
+// before the MFMAs of tile k and written to LDS after them (guide §6 G15, T14).
 //
 // Epilogues:
 //   EPI_F32        C(f32)  = alpha*acc
-//   EPI_F32_ATOMIC C(f32) += alpha*acc           (split-K partials, grid.z = splits)
+//   EPI_F32_ATOMIC C(f32) += alpha*acc                 (split-K, grid.z = splits)
 //   EPI_BIAS_RELU  C(bf16) = relu(acc + bias[n])
 //   EPI_BIAS       C(bf16) = acc + bias[n]
-//   EPI_RELU_GRAD  C(bf16) = acc * (mask(m,n) > 0);  colsum[n] += sum_m C   (fused bias grad)
+//   EPI_RELU_GRAD  C(bf16) = acc * (mask(m,n) > 0)
 //   EPI_BIAS_F32   C(f32)  = acc + bias[n]
+//   EPI_F32_SLAB   C[z](f32) = alpha*acc   plain stores into split slab z = blockIdx.z
+//                  (deterministic split-K: a later pass sums the slabs, no atomics)
+// Optional fused A-row sums (bias gradients of a weight-grad product): blocks of
+// the first N tile accumulate sum_k A(m,k) over their K range from the LDS tile
+// and store it to rowsum[z * slab_stride_rowsum + m] (atomicAdd for EPI_F32_ATOMIC).
 #include "common.h"
 #include "../har_kernels.h"
 
 namespace {
 
-enum { EPI_F32 = 0, EPI_F32_ATOMIC = 1, EPI_BIAS_RELU = 2, EPI_BIAS = 3, EPI_RELU_GRAD = 4, EPI_BIAS_F32 = 5 };
+enum { EPI_F32 = 0, EPI_F32_ATOMIC = 1, EPI_BIAS_RELU = 2, EPI_BIAS = 3, EPI_RELU_GRAD = 4, EPI_BIAS_F32 = 5,
+       EPI_F32_SLAB = 6 };
 
 constexpr int BK = 32;
 
@@ -36,7 +44,6 @@ template <typename T> struct Mfma;
 template <> struct Mfma<bf16_t> {
   static constexpr int KPER = 32;  // k per instruction
   static constexpr int VEC = 8;    // elements per lane per instruction
-  typedef bf16x8_t frag;
   __device__ static inline f32x4_t mma(const bf16_t* a, const bf16_t* b, f32x4_t c) {
     bf16x8_t fa = *reinterpret_cast<const bf16x8_t*>(a);
     bf16x8_t fb = *reinterpret_cast<const bf16x8_t*>(b);
@@ -51,40 +58,64 @@ template <> struct Mfma<float> {
   }
 };
 
+template <typename T> __device__ __forceinline__ float to_f(T v);
+template <> __device__ __forceinline__ float to_f<bf16_t>(bf16_t v) { return bf2f(v); }
+template <> __device__ __forceinline__ float to_f<float>(float v) { return v; }
+
 // LDS row pitch (elements): BK + one 16-byte pad breaks the power-of-two stride.
 template <typename T> constexpr int pitch() { return BK + 16 / (int)sizeof(T); }
 
+// A tile stager: ROWS x BK tile of a K-major ([row][k]) or row-major-in-K ([k][row])
+// operand, moved global -> registers (load) and registers -> LDS (store).
 template <typename T, int ROWS, int NT, bool KMAJOR>
-__device__ __forceinline__ void stage_tile(T* __restrict__ lds, const T* __restrict__ g, int ld,
-                                           int row0, int nrows, int k0, int K, int tid) {
-  constexpr int EPV = 16 / sizeof(T);  // elements per 16-byte vector
-  constexpr int P = pitch<T>();
-  if (KMAJOR) {
-    // [row][k] source: 16-byte vectors along k
-    constexpr int VPR = BK / EPV;
+struct Stager {
+  static constexpr int EPV = 16 / sizeof(T);
+  static constexpr int NV = (ROWS * BK / EPV + NT - 1) / NT;  // 16-byte vectors per thread
+  uint4 r[NV];
+
+  __device__ __forceinline__ void load(const T* __restrict__ g, int ld, int row0, int nrows, int k0, int K, int tid) {
 #pragma unroll
-    for (int v = tid; v < ROWS * VPR; v += NT) {
-      int r = v / VPR, kv = (v % VPR) * EPV;
-      int gr = row0 + r, gk = k0 + kv;
-      uint4 val = make_uint4(0, 0, 0, 0);
-      if (gr < nrows && gk < K) val = *reinterpret_cast<const uint4*>(g + (size_t)gr * ld + gk);
-      *reinterpret_cast<uint4*>(lds + r * P + kv) = val;
-    }
-  } else {
-    // [k][row] source: 16-byte vectors along rows, transposed on the LDS write
-    constexpr int VPK = ROWS / EPV;
-#pragma unroll
-    for (int v = tid; v < BK * VPK; v += NT) {
-      int k = v / VPK, rv = (v % VPK) * EPV;
-      int gk = k0 + k, gr = row0 + rv;
-      union { uint4 u; T e[EPV]; } val;
-      val.u = make_uint4(0, 0, 0, 0);
-      if (gk < K && gr < nrows) val.u = *reinterpret_cast<const uint4*>(g + (size_t)gk * ld + gr);
-#pragma unroll
-      for (int i = 0; i < EPV; ++i) lds[(rv + i) * P + k] = val.e[i];
+    for (int i = 0; i < NV; ++i) {
+      const int v = tid + i * NT;
+      r[i] = make_uint4(0, 0, 0, 0);
+      if (v < ROWS * BK / EPV) {
+        if (KMAJOR) {
+          constexpr int VPR = BK / EPV;
+          const int rr = v / VPR, kv = (v % VPR) * EPV;
+          const int gr = row0 + rr, gk = k0 + kv;
+          if (gr < nrows && gk < K) r[i] = *reinterpret_cast<const uint4*>(g + (size_t)gr * ld + gk);
+        } else {
+          constexpr int VPK = ROWS / EPV;
+          const int k = v / VPK, rv = (v % VPK) * EPV;
+          const int gk = k0 + k, gr = row0 + rv;
+          if (gk < K && gr < nrows) r[i] = *reinterpret_cast<const uint4*>(g + (size_t)gk * ld + gr);
+        }
+      }
     }
   }
-}
+
+  __device__ __forceinline__ void store(T* __restrict__ lds, int tid) const {
+    constexpr int P = pitch<T>();
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int v = tid + i * NT;
+      if (v < ROWS * BK / EPV) {
+        if (KMAJOR) {
+          constexpr int VPR = BK / EPV;
+          const int rr = v / VPR, kv = (v % VPR) * EPV;
+          *reinterpret_cast<uint4*>(lds + rr * P + kv) = r[i];
+        } else {
+          constexpr int VPK = ROWS / EPV;
+          const int k = v / VPK, rv = (v % VPK) * EPV;
+          union { uint4 u; T e[EPV]; } val;
+          val.u = r[i];
+#pragma unroll
+          for (int e = 0; e < EPV; ++e) lds[(rv + e) * P + k] = val.e[e];
+        }
+      }
+    }
+  }
+};
 
 template <typename T, int BM, int BN, int WM, int WN, bool A_KMAJOR, bool B_KMAJOR, int EPI>
 __global__ __launch_bounds__(WM * WN * 64) void gemm_kernel(GemmParams p) {
@@ -105,13 +136,16 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_kernel(GemmParams p) {
   // XCD-aware tile order over the (n, m) tile grid
   const int ntn = gridDim.x, ntm = gridDim.y;
   const int lin = xcd_remap(blockIdx.y * ntn + blockIdx.x, ntn * ntm);
-  const int m0 = (lin / ntn) * BM, n0 = (lin % ntn) * BN;
+  const int tn = lin % ntn;
+  const int m0 = (lin / ntn) * BM, n0 = tn * BN;
 
   int kb = 0, ke = p.K;
-  if (EPI == EPI_F32_ATOMIC) {
+  if (EPI == EPI_F32_ATOMIC || EPI == EPI_F32_SLAB) {
     kb = blockIdx.z * p.k_split;
     ke = min(p.K, kb + p.k_split);
   }
+  const bool do_rowsum = p.rowsum != nullptr && tn == 0 && tid < BM;
+  float rs = 0.f;
 
   f32x4_t acc[RM][RN];
 #pragma unroll
@@ -119,11 +153,24 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_kernel(GemmParams p) {
 #pragma unroll
     for (int j = 0; j < RN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
+  Stager<T, BM, NT, A_KMAJOR> sa;
+  Stager<T, BN, NT, B_KMAJOR> sb;
+  if (kb < ke) {
+    sa.load(A, p.lda, m0, p.M, kb, ke, tid);
+    sb.load(B, p.ldb, n0, p.N, kb, ke, tid);
+  }
   for (int k0 = kb; k0 < ke; k0 += BK) {
-    // the K bound of the tile clamps to this split's range
-    stage_tile<T, BM, NT, A_KMAJOR>(As, A, p.lda, m0, p.M, k0, ke, tid);
-    stage_tile<T, BN, NT, B_KMAJOR>(Bs, B, p.ldb, n0, p.N, k0, ke, tid);
+    sa.store(As, tid);
+    sb.store(Bs, tid);
     __syncthreads();
+    if (k0 + BK < ke) {  // prefetch the next tile into registers while the MFMAs run
+      sa.load(A, p.lda, m0, p.M, k0 + BK, ke, tid);
+      sb.load(B, p.ldb, n0, p.N, k0 + BK, ke, tid);
+    }
+    if (do_rowsum) {
+#pragma unroll
+      for (int k = 0; k < BK; ++k) rs += to_f<T>(As[tid * P + k]);
+    }
 #pragma unroll
     for (int kk = 0; kk < BK; kk += KPER) {
       const int kl = kk + q * VEC;
@@ -137,8 +184,14 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_kernel(GemmParams p) {
     __syncthreads();
   }
 
+  if (do_rowsum && m0 + tid < p.M) {
+    if (EPI == EPI_F32_ATOMIC) atomicAdd(p.rowsum + m0 + tid, p.alpha * rs);
+    else p.rowsum[(size_t)blockIdx.z * p.slab_stride_rowsum + m0 + tid] = p.alpha * rs;
+  }
+
   // ---- epilogue ----
   float* Cf = reinterpret_cast<float*>(p.C);
+  if (EPI == EPI_F32_SLAB) Cf += (size_t)blockIdx.z * p.slab_stride;
   bf16_t* Cb = reinterpret_cast<bf16_t*>(p.C);
   const bf16_t* mask = reinterpret_cast<const bf16_t*>(p.mask);
 #pragma unroll
@@ -147,34 +200,24 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_kernel(GemmParams p) {
     const bool nok = n < p.N;
     float bias = 0.f;
     if ((EPI == EPI_BIAS_RELU || EPI == EPI_BIAS || EPI == EPI_BIAS_F32) && nok && p.bias) bias = p.bias[n];
-    float csum = 0.f;
 #pragma unroll
     for (int i = 0; i < RM; ++i) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int m = m0 + wm * TM + i * 16 + q * 4 + r;
         if (!(nok && m < p.M)) continue;
-        float v = acc[i][j][r];
-        size_t off = (size_t)m * p.ldc + n;
-        if (EPI == EPI_F32) Cf[off] = p.alpha * v;
+        const float v = acc[i][j][r];
+        const size_t off = (size_t)m * p.ldc + n;
+        if (EPI == EPI_F32 || EPI == EPI_F32_SLAB) Cf[off] = p.alpha * v;
         else if (EPI == EPI_F32_ATOMIC) atomicAdd(Cf + off, p.alpha * v);
         else if (EPI == EPI_BIAS_RELU) Cb[off] = f2bf(fmaxf(v + bias, 0.f));
         else if (EPI == EPI_BIAS) Cb[off] = f2bf(v + bias);
         else if (EPI == EPI_BIAS_F32) Cf[off] = v + bias;
         else if (EPI == EPI_RELU_GRAD) {
-          bf16_t mk = mask[(size_t)m * p.ldmask + n];
-          float g = ((mk & 0x8000u) == 0 && mk != 0) ? v : 0.f;
-          bf16_t gb = f2bf(g);
-          Cb[off] = gb;
-          csum += bf2f(gb);
+          const bf16_t mk = mask[(size_t)m * p.ldmask + n];
+          Cb[off] = ((mk & 0x8000u) == 0 && mk != 0) ? f2bf(v) : (bf16_t)0;
         }
       }
-    }
-    if (EPI == EPI_RELU_GRAD && p.colsum) {
-      // lanes r16, r16+16, r16+32, r16+48 share the column
-      csum += __shfl_xor(csum, 16, 64);
-      csum += __shfl_xor(csum, 32, 64);
-      if (q == 0 && nok) atomicAdd(p.colsum + n, csum);
     }
   }
 }
@@ -182,7 +225,7 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_kernel(GemmParams p) {
 template <typename T, int BM, int BN, int WM, int WN, bool AK, bool BKm>
 int launch_epi(const GemmParams& p, int epi, hipStream_t s) {
   dim3 grid((p.N + BN - 1) / BN, (p.M + BM - 1) / BM, 1);
-  if (epi == EPI_F32_ATOMIC) grid.z = (p.K + p.k_split - 1) / p.k_split;
+  if (epi == EPI_F32_ATOMIC || epi == EPI_F32_SLAB) grid.z = (p.K + p.k_split - 1) / p.k_split;
   dim3 block(WM * WN * 64);
   switch (epi) {
     case EPI_F32: gemm_kernel<T, BM, BN, WM, WN, AK, BKm, EPI_F32><<<grid, block, 0, s>>>(p); break;
@@ -191,19 +234,33 @@ int launch_epi(const GemmParams& p, int epi, hipStream_t s) {
     case EPI_BIAS: gemm_kernel<T, BM, BN, WM, WN, AK, BKm, EPI_BIAS><<<grid, block, 0, s>>>(p); break;
     case EPI_RELU_GRAD: gemm_kernel<T, BM, BN, WM, WN, AK, BKm, EPI_RELU_GRAD><<<grid, block, 0, s>>>(p); break;
     case EPI_BIAS_F32: gemm_kernel<T, BM, BN, WM, WN, AK, BKm, EPI_BIAS_F32><<<grid, block, 0, s>>>(p); break;
+    case EPI_F32_SLAB: gemm_kernel<T, BM, BN, WM, WN, AK, BKm, EPI_F32_SLAB><<<grid, block, 0, s>>>(p); break;
     default: return -1;
   }
   HAR_CHECK_LAUNCH();
   return 0;
 }
 
+// Tile ids (host helper ops/gemm.py mirrors this table to size split-K):
+//   0: 128x128 (2x2 waves)   1: 128x64 (2x2)   2: 128x32 (4x1)   3: 64x128 (1x4)   4: 64x64 (2x2)   5: 32x64 (1x2... as 2x2 of 16x32)
 template <typename T, bool AK, bool BKm>
 int launch_tile(const GemmParams& p, int epi, hipStream_t s) {
-  // tile choice: wide tiles when both dims are large, narrow-N tiles for heads / thin outputs
-  if (p.N <= 32) return launch_epi<T, 128, 32, 4, 1, AK, BKm>(p, epi, s);
-  if (p.N <= 64) return launch_epi<T, 128, 64, 2, 2, AK, BKm>(p, epi, s);
-  if (p.M <= 64) return launch_epi<T, 64, 128, 1, 4, AK, BKm>(p, epi, s);
-  return launch_epi<T, 128, 128, 2, 2, AK, BKm>(p, epi, s);
+  int tile = p.tile;
+  if (tile < 0) {
+    if (p.N <= 32) tile = 2;
+    else if (p.N <= 64) tile = 1;
+    else if (p.M <= 64) tile = 3;
+    else tile = 0;
+  }
+  switch (tile) {
+    case 0: return launch_epi<T, 128, 128, 2, 2, AK, BKm>(p, epi, s);
+    case 1: return launch_epi<T, 128, 64, 2, 2, AK, BKm>(p, epi, s);
+    case 2: return launch_epi<T, 128, 32, 4, 1, AK, BKm>(p, epi, s);
+    case 3: return launch_epi<T, 64, 128, 1, 4, AK, BKm>(p, epi, s);
+    case 4: return launch_epi<T, 64, 64, 2, 2, AK, BKm>(p, epi, s);
+    case 5: return launch_epi<T, 32, 64, 1, 2, AK, BKm>(p, epi, s);
+    default: return -4;
+  }
 }
 
 template <typename T>
@@ -213,11 +270,11 @@ int gemm_dispatch(const GemmParams& p, int layout, int epi, hipStream_t s) {
   bool a_mmajor = layout & 1, b_nmajor = layout & 2;
   // vector-load alignment contract (checked on the host side as well)
   if ((a_mmajor ? p.M : p.K) % EPV || (b_nmajor ? p.N : p.K) % EPV || p.lda % EPV || p.ldb % EPV) return -2;
-  if (epi == EPI_F32_ATOMIC && (p.k_split <= 0 || p.k_split % BK)) return -3;
+  if ((epi == EPI_F32_ATOMIC || epi == EPI_F32_SLAB) && (p.k_split <= 0 || p.k_split % BK)) return -3;
   if (!a_mmajor && !b_nmajor) return launch_tile<T, true, true>(p, epi, s);
   if (!a_mmajor && b_nmajor) return launch_tile<T, true, false>(p, epi, s);
   if (a_mmajor && b_nmajor) return launch_tile<T, false, false>(p, epi, s);
-  return launch_tile<T, false, true>(p, epi, s);
+  return -5;  // (A M-major, B K-major) is never needed
 }
 
 }  // namespace

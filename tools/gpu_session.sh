@@ -38,7 +38,7 @@ fi
 
 if [ "$WHAT" = "prof" ] || [ "$WHAT" = "all" ]; then
   export TMPDIR=/tmp
-  (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o bench -- \
+  (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o bench -- \
       python3 "$ROOT/bench.py" --steps 20 --warmup 5 --graph 0 > "$OUT/prof.log" 2>&1)
   rc=$?
   tail -3 "$OUT/prof.log"
