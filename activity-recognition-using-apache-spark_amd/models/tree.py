@@ -1,0 +1,373 @@
+"""DecisionTreeClassifier / RandomForestClassifier — level-wise forest builder.
+
+Reference: ``DecisionTreeClassifier(maxDepth=3)`` (``Main/main.py:297``) and
+``RandomForestClassifier(numTrees=100, maxDepth=4, maxBins=32)`` (``Main/main.py:478``);
+Spark ``RandomForest.run`` semantics:
+
+* ``findSplits``: at most ``maxBins - 1`` thresholds per feature (midpoints of the
+  distinct values, or quantile cut points); a binary one-hot feature gets the
+  single split 0 | 1, which is Spark's 2-category split;
+* bagging: RandomForest with ``numTrees > 1`` draws Poisson(1) per (tree, row)
+  (``subsamplingRate = 1``), a single tree uses every row once;
+* ``featureSubsetStrategy``: ``auto`` = ``sqrt`` for a forest, ``all`` for one
+  tree; the subset is re-drawn at every node;
+* impurity gini (or entropy); a node splits only when its best gain is > 0 and
+  >= ``minInfoGain`` and both children have >= ``minInstancesPerNode`` weight;
+* prediction: a tree's ``rawPrediction`` is its leaf's class counts; a forest
+  sums each tree's *normalized* leaf distribution (soft vote,
+  ``result.txt:282-286``); probability = normalized raw.
+
+Engine: every tree of the forest grows in lock step, one level at a time.  Per
+level the rows of all active (tree, node) pairs are grouped on the device, one
+fused HIP kernel builds the LDS histograms and picks every node's best split
+(``har_tree_hist_split``), and a vectorized partition step moves rows to the
+children.  Bootstrap weights are Philox(seed, tree, global row) so forests are
+identical for any sharding.  In data-parallel mode (``parallel.forest``) the
+per-rank histograms are all-reduced before split selection.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+from typing import List, Optional
+
+import numpy as np
+import torch
+
+from ..data.table import Table
+from ..ops import _native, rng
+from ..ops import tree as T
+from .base import ClassificationModel, ClassifierParams, Estimator, features_tensor, labels_tensor, new_uid, \
+    resolve_device
+
+
+@dataclass
+class ForestArrays:
+    feature: torch.Tensor    # [T, maxn] int32, -1 = leaf
+    threshold: torch.Tensor  # [T, maxn] float32 (x <= thr goes left)
+    left: torch.Tensor       # [T, maxn] int32
+    right: torch.Tensor      # [T, maxn] int32
+    stats: torch.Tensor      # [T, maxn, K] float32 weighted class counts
+    n_nodes: np.ndarray      # [T] nodes per tree
+    max_depth: int
+    gain: Optional[torch.Tensor] = None  # [T, maxn] split gains (feature importances)
+
+    def to(self, device):
+        return ForestArrays(self.feature.to(device), self.threshold.to(device), self.left.to(device),
+                            self.right.to(device), self.stats.to(device), self.n_nodes, self.max_depth,
+                            None if self.gain is None else self.gain.to(device))
+
+
+def subset_size(strategy, n_features: int, num_trees: int) -> int:
+    s = str(strategy).lower()
+    if s == "auto":
+        s = "all" if num_trees == 1 else "sqrt"
+    if s == "all":
+        return n_features
+    if s == "sqrt":
+        return int(math.ceil(math.sqrt(n_features)))
+    if s == "log2":
+        return max(1, int(math.ceil(math.log2(n_features))))
+    if s == "onethird":
+        return max(1, int(math.ceil(n_features / 3.0)))
+    v = float(s)
+    if v >= 1.0 and v == int(v):
+        return min(n_features, int(v))
+    return max(1, int(math.ceil(v * n_features)))
+
+
+class ForestBuilder:
+    """Builds ``num_trees`` trees level-synchronously on one device (or one DP rank)."""
+
+    def __init__(self, num_classes: int, num_trees: int = 1, max_depth: int = 5, max_bins: int = 32,
+                 min_instances: int = 1, min_info_gain: float = 0.0, impurity: str = "gini",
+                 feature_subset: str = "auto", bootstrap: Optional[bool] = None, seed: int = 0,
+                 allreduce=None):
+        if max_bins > 64:
+            raise ValueError("maxBins <= 64 (one lane per bin in the split kernel)")
+        self.K, self.T, self.D = num_classes, num_trees, max_depth
+        self.max_bins, self.min_inst, self.min_gain = max_bins, float(min_instances), float(min_info_gain)
+        self.impurity = T.GINI if impurity == "gini" else T.ENTROPY
+        self.subset = feature_subset
+        self.bootstrap = (num_trees > 1) if bootstrap is None else bootstrap
+        self.seed = seed
+        self.allreduce = allreduce  # optional callable(tensor) -> None (DP histogram reduction)
+
+    def prepare(self, X: torch.Tensor, thresholds=None):
+        Xh = X.detach().float().cpu().numpy()
+        self.thresholds = thresholds if thresholds is not None else T.find_thresholds(Xh, self.max_bins, seed=self.seed)
+        F = Xh.shape[1]
+        self.nbins = torch.tensor([len(t) + 1 for t in self.thresholds], dtype=torch.int32, device=X.device)
+        thr_mat = np.full((F, self.max_bins), np.inf, dtype=np.float32)
+        for f, t in enumerate(self.thresholds):
+            thr_mat[f, : len(t)] = t
+        self.thr_mat = torch.from_numpy(thr_mat).to(X.device)
+        self.bins = torch.from_numpy(T.bin_features(Xh, self.thresholds)).to(X.device)  # [F, N]
+
+    def bootstrap_weights(self, N: int, device, row_offset: int = 0) -> torch.Tensor:
+        if not self.bootstrap:
+            return torch.ones(self.T, N, dtype=torch.float32, device=device)
+        if device.type == "cuda":
+            w = torch.empty(self.T, N, dtype=torch.uint8, device=device)
+            _native.kernels().poisson_bootstrap(self.seed, 0, self.T, row_offset, N, w.data_ptr(),
+                                                _native.stream_ptr())
+            return w.float()
+        return torch.from_numpy(rng.poisson1_weights(self.seed, range(self.T), N, row_offset)).float()
+
+    def fit(self, X: torch.Tensor, y: torch.Tensor, row_offset: int = 0, thresholds=None) -> ForestArrays:
+        dev = X.device
+        N, F = X.shape
+        self.prepare(X, thresholds)
+        Tn, K, D = self.T, self.K, self.D
+        m = subset_size(self.subset, F, Tn)
+        y32 = y.to(torch.int32).contiguous()
+        W = self.bootstrap_weights(N, dev, row_offset)        # [T, N]
+        maxn = int(min(2 ** (D + 1) - 1, 2 * max(N, 1) + 1))
+        feature = torch.full((Tn, maxn), -1, dtype=torch.int32, device=dev)
+        thresh = torch.zeros(Tn, maxn, dtype=torch.float32, device=dev)
+        left = torch.zeros(Tn, maxn, dtype=torch.int32, device=dev)
+        right = torch.zeros(Tn, maxn, dtype=torch.int32, device=dev)
+        stats = torch.zeros(Tn, maxn, K, dtype=torch.float32, device=dev)
+        gains = torch.zeros(Tn, maxn, dtype=torch.float32, device=dev)
+        # root class counts
+        root = torch.zeros(Tn, K, dtype=torch.float32, device=dev)
+        root.scatter_add_(1, y.long().view(1, -1).expand(Tn, -1), W)
+        if self.allreduce is not None:
+            self.allreduce(root)
+        stats[:, 0] = root
+        n_nodes = np.ones(Tn, dtype=np.int64)
+        node_of = torch.zeros(Tn, N, dtype=torch.int32, device=dev)   # node id per (tree,row); -1 = done
+        node_of[W == 0] = -1
+        # frontier: (tree, node, depth)
+        front_t = np.arange(Tn, dtype=np.int64)
+        front_n = np.zeros(Tn, dtype=np.int64)
+        use_native = dev.type == "cuda"
+        for depth in range(D):
+            if len(front_t) == 0:
+                break
+            st = stats[torch.as_tensor(front_t, device=dev), torch.as_tensor(front_n, device=dev)]  # [A0, K]
+            w_tot = st.sum(1)
+            imp = T._impurity(st.double(), w_tot.double(), self.impurity)
+            cand = ((imp > 1e-12) & (w_tot >= 2 * self.min_inst)).cpu().numpy()
+            ct, cn = front_t[cand], front_n[cand]
+            A = len(ct)
+            if A == 0:
+                break
+            # ---- group the rows of every candidate node ----
+            cand_idx = torch.full((Tn, maxn), -1, dtype=torch.int64, device=dev)
+            cand_idx[torch.as_tensor(ct, device=dev), torch.as_tensor(cn, device=dev)] = torch.arange(A, device=dev)
+            valid = node_of >= 0
+            key = torch.where(valid, cand_idx.gather(1, node_of.clamp_min(0).long()), torch.full_like(node_of, -1,
+                                                                                                  dtype=torch.int64))
+            sel = key >= 0
+            tt, rr = torch.nonzero(sel, as_tuple=True)
+            kk = key[tt, rr]
+            order = torch.argsort(kk, stable=True)
+            rows = rr[order].to(torch.int32).contiguous()
+            keys = kk[order]
+            row_w = W[tt[order], rr[order]].contiguous()
+            counts = torch.bincount(keys, minlength=A).to(torch.int32)
+            starts = (torch.cumsum(counts, 0) - counts).to(torch.int32)
+            feats = torch.from_numpy(rng.feature_subsets(self.seed, ct, cn, F, m)).to(dev)
+            # ---- histogram + best split ----
+            if use_native and self.allreduce is None:
+                res = T.hist_split_native(self.bins, self.nbins, y32, rows, row_w, starts, counts, feats, K,
+                                          self.max_bins, self.min_inst, self.min_gain, self.impurity)
+            else:
+                hist = T.level_histogram(self.bins, y32, rows, row_w, keys, A, feats, K, self.max_bins)
+                if self.allreduce is not None:
+                    self.allreduce(hist)
+                res = T.split_from_hist(hist, feats, self.nbins, self.min_inst, self.min_gain, self.impurity)
+            do_split = (res.gain > 0) & torch.isfinite(res.gain)
+            ds = do_split.cpu().numpy()
+            if not ds.any():
+                break
+            st_t, st_n = ct[ds], cn[ds]
+            # allocate children: per tree, consecutive ids
+            child_l = np.empty(len(st_t), dtype=np.int64)
+            for i, t in enumerate(st_t):
+                child_l[i] = n_nodes[t]
+                n_nodes[t] += 2
+            ti = torch.as_tensor(st_t, device=dev)
+            ni = torch.as_tensor(st_n, device=dev)
+            cl = torch.as_tensor(child_l, device=dev)
+            dsi = torch.as_tensor(np.nonzero(ds)[0], device=dev)
+            bf = res.feat[dsi].long()
+            bb = res.bin[dsi].long()
+            feature[ti, ni] = bf.to(torch.int32)
+            thresh[ti, ni] = self.thr_mat[bf, bb]
+            left[ti, ni] = cl.to(torch.int32)
+            right[ti, ni] = (cl + 1).to(torch.int32)
+            gains[ti, ni] = res.gain[dsi] * res.total[dsi].sum(1)
+            lstat = res.left[dsi]
+            stats[ti, cl] = lstat
+            stats[ti, cl + 1] = res.total[dsi] - lstat
+            # ---- partition: rows of the nodes split at THIS level move to a child, all others finish ----
+            lvl_feat = torch.full((Tn, maxn), -1, dtype=torch.int64, device=dev)
+            lvl_bin = torch.zeros(Tn, maxn, dtype=torch.int64, device=dev)
+            lvl_left = torch.zeros(Tn, maxn, dtype=torch.int64, device=dev)
+            lvl_feat[ti, ni] = bf
+            lvl_bin[ti, ni] = bb
+            lvl_left[ti, ni] = cl
+            idx = node_of.clamp_min(0).long()
+            f_of = lvl_feat.gather(1, idx)
+            moved = (node_of >= 0) & (f_of >= 0)
+            b_of = self.bins[f_of.clamp_min(0), torch.arange(N, device=dev).view(1, -1).expand(Tn, -1)].long()
+            go_left = b_of <= lvl_bin.gather(1, idx)
+            nxt = lvl_left.gather(1, idx) + (~go_left).long()
+            node_of = torch.where(moved, nxt, torch.full_like(nxt, -1)).to(torch.int32)
+            front_t = np.repeat(st_t, 2)
+            front_n = np.stack([child_l, child_l + 1], 1).reshape(-1)
+        return ForestArrays(feature, thresh, left, right, stats, n_nodes, D, gains)
+
+
+def predict_forest(arrs: ForestArrays, X: torch.Tensor, normalize: bool) -> torch.Tensor:
+    a = arrs if arrs.feature.device == X.device else arrs.to(X.device)
+    if X.is_cuda:
+        return T.forest_predict_native(X.float(), a.feature, a.threshold, a.left, a.right, a.stats, a.max_depth,
+                                       normalize)
+    return T.forest_predict_torch(X.float(), a.feature, a.threshold, a.left, a.right, a.stats, a.max_depth,
+                                  normalize)
+
+
+def _tree_depth(arrs: ForestArrays, t: int) -> int:
+    feat = arrs.feature[t].cpu().numpy()
+    left = arrs.left[t].cpu().numpy()
+    right = arrs.right[t].cpu().numpy()
+    best, stack = 0, [(0, 0)]
+    while stack:
+        n, d = stack.pop()
+        best = max(best, d)
+        if feat[n] >= 0:
+            stack += [(int(left[n]), d + 1), (int(right[n]), d + 1)]
+    return best
+
+
+class DecisionTreeClassificationModel(ClassificationModel):
+    def __init__(self, arrs: ForestArrays, num_features: int, num_classes: int, uid=None, device=None):
+        super().__init__(uid or new_uid("DecisionTreeClassifier"))
+        self.arrs = arrs
+        self.num_features, self.num_classes = num_features, num_classes
+        self.device = device or arrs.feature.device
+
+    @property
+    def depth(self) -> int:
+        return _tree_depth(self.arrs, 0)
+
+    @property
+    def numNodes(self) -> int:
+        return int(self.arrs.n_nodes[0])
+
+    def predict_raw(self, X):
+        return predict_forest(self.arrs, X.to(self.device), normalize=False)
+
+    @property
+    def featureImportances(self) -> torch.Tensor:
+        return _importances(self.arrs, self.num_features)
+
+    def __str__(self):
+        return (f"DecisionTreeClassificationModel (uid={self.uid}) of depth {self.depth} "
+                f"with {self.numNodes} nodes")
+
+    def state(self):
+        a = self.arrs
+        return {"feature": a.feature.cpu(), "threshold": a.threshold.cpu(), "left": a.left.cpu(),
+                "right": a.right.cpu(), "stats": a.stats.cpu(), "n_nodes": torch.as_tensor(a.n_nodes),
+                "max_depth": a.max_depth}
+
+
+class RandomForestClassificationModel(DecisionTreeClassificationModel):
+    def __init__(self, arrs: ForestArrays, num_features: int, num_classes: int, uid=None, device=None):
+        super().__init__(arrs, num_features, num_classes, uid or new_uid("RandomForestClassifier"), device)
+
+    @property
+    def getNumTrees(self) -> int:
+        return int(self.arrs.feature.shape[0])
+
+    @property
+    def totalNumNodes(self) -> int:
+        return int(self.arrs.n_nodes.sum())
+
+    def predict_raw(self, X):
+        return predict_forest(self.arrs, X.to(self.device), normalize=True)
+
+    def __str__(self):
+        return f"RandomForestClassificationModel (uid={self.uid}) with {self.getNumTrees} trees"
+
+
+def _importances(arrs: ForestArrays, F: int) -> torch.Tensor:
+    """Spark-style importances: per tree, gain-weighted split counts normalized, averaged, normalized."""
+    imp = torch.zeros(F, dtype=torch.float64)
+    feat = arrs.feature.cpu()
+    g = arrs.gain.cpu().double() if arrs.gain is not None else torch.ones_like(feat, dtype=torch.float64)
+    for t in range(feat.shape[0]):
+        m = feat[t] >= 0
+        it = torch.zeros(F, dtype=torch.float64)
+        it.index_add_(0, feat[t][m].long(), g[t][m])
+        s = it.sum()
+        if s > 0:
+            imp += it / s
+    s = imp.sum()
+    return imp / s if s > 0 else imp
+
+
+class _TreeEstimatorBase(Estimator, ClassifierParams):
+    _param_names = ("maxDepth", "maxBins", "minInstancesPerNode", "minInfoGain", "impurity", "seed",
+                    "featuresCol", "labelCol", "device")
+
+    def _prep(self, table: Table):
+        dev = resolve_device(self.device)
+        X = features_tensor(table, self.featuresCol, dev)
+        y = labels_tensor(table, self.labelCol, dev)
+        vocab = (table[self.labelCol].meta or {}).get("vocab")
+        K = int(max(int(y.max()) + 1, len(vocab) if vocab else 0))
+        return X, y, K
+
+
+class DecisionTreeClassifier(_TreeEstimatorBase):
+    def __init__(self, featuresCol="features", labelCol="label", maxDepth: int = 5, maxBins: int = 32,
+                 minInstancesPerNode: int = 1, minInfoGain: float = 0.0, impurity: str = "gini", seed: int = 0,
+                 device=None):
+        super().__init__(new_uid("DecisionTreeClassifier"))
+        self.featuresCol, self.labelCol = featuresCol, labelCol
+        self.maxDepth, self.maxBins, self.minInstancesPerNode = maxDepth, maxBins, minInstancesPerNode
+        self.minInfoGain, self.impurity, self.seed, self.device = minInfoGain, impurity, seed, device
+
+    def fit(self, table: Table) -> DecisionTreeClassificationModel:
+        X, y, K = self._prep(table)
+        return self.fit_tensors(X, y, K)
+
+    def fit_tensors(self, X, y, K) -> DecisionTreeClassificationModel:
+        b = ForestBuilder(K, 1, self.maxDepth, self.maxBins, self.minInstancesPerNode, self.minInfoGain,
+                          self.impurity, "all", bootstrap=False, seed=self.seed)
+        return DecisionTreeClassificationModel(b.fit(X, y), X.shape[1], K, uid=self.uid, device=X.device)
+
+
+class RandomForestClassifier(_TreeEstimatorBase):
+    _param_names = _TreeEstimatorBase._param_names + ("numTrees", "featureSubsetStrategy", "subsamplingRate")
+
+    def __init__(self, featuresCol="features", labelCol="label", numTrees: int = 20, maxDepth: int = 5,
+                 maxBins: int = 32, minInstancesPerNode: int = 1, minInfoGain: float = 0.0, impurity: str = "gini",
+                 featureSubsetStrategy: str = "auto", subsamplingRate: float = 1.0, seed: int = 0, device=None):
+        super().__init__(new_uid("RandomForestClassifier"))
+        self.featuresCol, self.labelCol = featuresCol, labelCol
+        self.numTrees, self.maxDepth, self.maxBins = numTrees, maxDepth, maxBins
+        self.minInstancesPerNode, self.minInfoGain, self.impurity = minInstancesPerNode, minInfoGain, impurity
+        self.featureSubsetStrategy, self.subsamplingRate = featureSubsetStrategy, subsamplingRate
+        self.seed, self.device = seed, device
+
+    def fit(self, table: Table) -> RandomForestClassificationModel:
+        X, y, K = self._prep(table)
+        return self.fit_tensors(X, y, K)
+
+    def fit_tensors(self, X, y, K, allreduce=None, row_offset: int = 0, thresholds=None):
+        if self.subsamplingRate != 1.0:
+            raise NotImplementedError("subsamplingRate != 1.0")
+        b = ForestBuilder(K, self.numTrees, self.maxDepth, self.maxBins, self.minInstancesPerNode, self.minInfoGain,
+                          self.impurity, self.featureSubsetStrategy, seed=self.seed, allreduce=allreduce)
+        arrs = b.fit(X, y, row_offset=row_offset, thresholds=thresholds)
+        return RandomForestClassificationModel(arrs, X.shape[1], K, uid=self.uid, device=X.device)
+
+
+__all__ = ["DecisionTreeClassifier", "RandomForestClassifier", "DecisionTreeClassificationModel",
+           "RandomForestClassificationModel", "ForestBuilder", "ForestArrays"]

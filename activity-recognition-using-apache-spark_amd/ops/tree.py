@@ -82,20 +82,30 @@ def _impurity(c: torch.Tensor, w: torch.Tensor, kind: int) -> torch.Tensor:
     return -(p * lp).sum(-1)
 
 
-def hist_split_torch(bins, nbins_feat, label, rows, row_w, key, n_nodes, feats, K, max_bins, min_instances,
-                     min_info_gain, impurity) -> LevelResult:
-    """CPU/oracle implementation.  ``rows``/``row_w``/``key`` list the (row, weight,
-    node) pairs; ``feats`` [A, m] sampled features per node."""
+def level_histogram(bins, label, rows, row_w, key, n_nodes, feats, K, max_bins) -> torch.Tensor:
+    """Weighted histograms [A, m, max_bins, K] of the (row, weight, node) pairs over each
+    node's sampled features ``feats`` [A, m] (torch; any device).  fp64 accumulation."""
     A, m = feats.shape
     dev = bins.device
-    fe = feats[key]                                          # [P, m]
-    bv = bins[fe.long(), rows.long().unsqueeze(1)].long()    # [P, m]
-    y = label[rows.long()].long()
-    idx = ((key.long().unsqueeze(1) * m + torch.arange(m, device=dev)) * max_bins + bv) * K + y.unsqueeze(1)
-    w = row_w.float().unsqueeze(1).expand(-1, m)
     hist = torch.zeros(A * m * max_bins * K, dtype=torch.float64, device=dev)
-    hist.index_add_(0, idx.reshape(-1), w.reshape(-1).double())
-    hist = hist.view(A, m, max_bins, K)
+    P = rows.shape[0]
+    step = max(1, (1 << 24) // max(m, 1))  # bound the [P, m] temporaries
+    for p0 in range(0, P, step):
+        r = rows[p0:p0 + step].long()
+        kk = key[p0:p0 + step].long()
+        fe = feats[kk].long()                                    # [p, m]
+        bv = bins[fe, r.unsqueeze(1)].long()                     # [p, m]
+        y = label[r].long()
+        idx = ((kk.unsqueeze(1) * m + torch.arange(m, device=dev)) * max_bins + bv) * K + y.unsqueeze(1)
+        w = row_w[p0:p0 + step].double().unsqueeze(1).expand(-1, m)
+        hist.index_add_(0, idx.reshape(-1), w.reshape(-1))
+    return hist.view(A, m, max_bins, K)
+
+
+def hist_split_torch(bins, nbins_feat, label, rows, row_w, key, n_nodes, feats, K, max_bins, min_instances,
+                     min_info_gain, impurity) -> LevelResult:
+    """CPU/oracle implementation of ``hist_split_native``."""
+    hist = level_histogram(bins, label, rows, row_w, key, n_nodes, feats, K, max_bins)
     return split_from_hist(hist, feats, nbins_feat, min_instances, min_info_gain, impurity)
 
 

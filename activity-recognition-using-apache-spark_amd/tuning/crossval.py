@@ -1,0 +1,150 @@
+"""ParamGridBuilder / CrossValidator / TrainValidationSplit.
+
+Reference: ``ParamGridBuilder().addGrid(lr.regParam, [0.1,0.3,0.5]).addGrid(
+lr.elasticNetParam, [0.0,0.1,0.2]).build()`` and ``CrossValidator(estimator,
+estimatorParamMaps, evaluator, numFolds=5)`` (``Main/main.py:202-215``; DT/RF with
+an empty grid ``:379-402, 560-583``).  SURVEY.md C18/C20/C22, N9, §3.5.
+
+Spark fits the 5 x 9 = 45 (fold, param map) models one after another
+(``parallelism=1``) — the most expensive entry point of the reference (129.9 s).
+Here, for LogisticRegression, all 45 fits are ONE batched device optimization
+(``LogisticRegression.fit_many``): each fold is a 0/1 row-weight vector over the
+resident training matrix, so the two GEMMs of every objective evaluation cover
+all 45 models at once.  Other estimators fit per (fold, map) on the device.
+
+Note on the objective: in the reference the CV evaluator is whatever object was
+last assigned to ``evaluator`` — ``RegressionEvaluator(metricName="mae")``
+(``Main/main.py:175``) — so its model selection minimizes the MAE of class
+indices.  Any evaluator can be passed here; ``main.py`` defaults to accuracy and
+offers ``--cv-metric mae`` for behavioural parity.
+"""
+from __future__ import annotations
+
+import itertools
+from typing import Dict, List, Optional, Sequence
+
+import numpy as np
+import torch
+
+from ..data.split import kfold_ids, split_ids
+from ..data.table import Column, Table
+from ..models.base import Estimator, Model, features_tensor, labels_tensor, new_uid, resolve_device
+
+
+def _pname(p) -> str:
+    return p if isinstance(p, str) else getattr(p, "name", str(p))
+
+
+class ParamGridBuilder:
+    def __init__(self):
+        self._grid: Dict[str, List] = {}
+        self._base: Dict[str, object] = {}
+
+    def addGrid(self, param, values: Sequence):
+        self._grid[_pname(param)] = list(values)
+        return self
+
+    def baseOn(self, *pairs, **kw):
+        for k, v in pairs:
+            self._base[_pname(k)] = v
+        self._base.update(kw)
+        return self
+
+    def build(self) -> List[Dict]:
+        keys = list(self._grid)
+        maps = []
+        for combo in itertools.product(*(self._grid[k] for k in keys)):
+            m = dict(self._base)
+            m.update(dict(zip(keys, combo)))
+            maps.append(m)
+        return maps or [dict(self._base)]
+
+
+def _with_predictions(model, table: Table, X: torch.Tensor, prefix: Optional[str] = None) -> Table:
+    raw, prob, pred = model.predict_all(X)
+    t = table.with_column(Column(model.rawPredictionCol, "vector", raw.double().cpu().numpy()))
+    t = t.with_column(Column(model.probabilityCol, "vector", prob.double().cpu().numpy()))
+    return t.with_column(Column(model.predictionCol, "double", pred.double().cpu().numpy()))
+
+
+class CrossValidatorModel(Model):
+    def __init__(self, bestModel, avgMetrics: List[float], bestIndex: int, subModels=None, uid=None):
+        super().__init__(uid or new_uid("CrossValidatorModel"))
+        self.bestModel, self.avgMetrics, self.bestIndex, self.subModels = bestModel, avgMetrics, bestIndex, subModels
+
+    def transform(self, table: Table) -> Table:
+        return self.bestModel.transform(table)
+
+    def __getattr__(self, item):  # delegate predict_all / num_classes ... to the best model
+        if item in ("bestModel", "__setstate__", "__getstate__"):
+            raise AttributeError(item)
+        return getattr(self.bestModel, item)
+
+    def __str__(self):
+        return self.uid
+
+
+class CrossValidator(Estimator):
+    def __init__(self, estimator=None, estimatorParamMaps: Optional[List[Dict]] = None, evaluator=None,
+                 numFolds: int = 3, seed: int = 0, parallelism: int = 1, collectSubModels: bool = False):
+        super().__init__(new_uid("CrossValidator"))
+        self.estimator, self.estimatorParamMaps, self.evaluator = estimator, estimatorParamMaps or [{}], evaluator
+        self.numFolds, self.seed, self.parallelism, self.collectSubModels = numFolds, seed, parallelism, collectSubModels
+
+    def fit(self, table: Table) -> CrossValidatorModel:
+        est, maps, ev, k = self.estimator, self.estimatorParamMaps, self.evaluator, self.numFolds
+        fold = kfold_ids(table.count(), k, self.seed)
+        metrics = np.zeros((len(maps), k), dtype=np.float64)
+        from ..models.logreg import FitSpec, LogisticRegression
+
+        if isinstance(est, LogisticRegression):
+            dev = resolve_device(est.device)
+            X = features_tensor(table, est.featuresCol, dev)
+            y = labels_tensor(table, est.labelCol, dev)
+            K = int(max(int(y.max()) + 1, len((table[est.labelCol].meta or {}).get("vocab") or [])))
+            fold_t = torch.as_tensor(fold, device=dev)
+            specs, index = [], []
+            for mi, pm in enumerate(maps):
+                sub = est.copy(pm)
+                for f in range(k):
+                    specs.append(FitSpec((fold_t != f).float(), sub.regParam, sub.elasticNetParam))
+                    index.append((mi, f))
+            # maxIter / tol / family etc. may differ per map only through regParam/elasticNetParam
+            base = est.copy(maps[0]) if maps else est
+            models = base.fit_many(X, y, specs, K)
+            for (mi, f), m in zip(index, models):
+                rows = np.nonzero(fold == f)[0]
+                vt = table.take_rows(rows)
+                metrics[mi, f] = ev.evaluate(_with_predictions(m, vt, X[torch.as_tensor(rows, device=dev)]))
+        else:
+            for f in range(k):
+                tr = table.take_rows(np.nonzero(fold != f)[0])
+                va = table.take_rows(np.nonzero(fold == f)[0])
+                for mi, pm in enumerate(maps):
+                    m = est.copy(pm).fit(tr)
+                    metrics[mi, f] = ev.evaluate(m.transform(va))
+        avg = metrics.mean(axis=1)
+        best = int(np.argmax(avg) if ev.isLargerBetter() else np.argmin(avg))
+        best_model = est.copy(maps[best]).fit(table)
+        return CrossValidatorModel(best_model, avg.tolist(), best)
+
+
+class TrainValidationSplitModel(CrossValidatorModel):
+    pass
+
+
+class TrainValidationSplit(Estimator):
+    def __init__(self, estimator=None, estimatorParamMaps=None, evaluator=None, trainRatio: float = 0.75,
+                 seed: int = 0):
+        super().__init__(new_uid("TrainValidationSplit"))
+        self.estimator, self.estimatorParamMaps, self.evaluator = estimator, estimatorParamMaps or [{}], evaluator
+        self.trainRatio, self.seed = trainRatio, seed
+
+    def fit(self, table: Table) -> TrainValidationSplitModel:
+        ids = split_ids(table.count(), [self.trainRatio, 1 - self.trainRatio], self.seed)
+        tr = table.take_rows(np.nonzero(ids == 0)[0])
+        va = table.take_rows(np.nonzero(ids == 1)[0])
+        mets = [self.evaluator.evaluate(self.estimator.copy(pm).fit(tr).transform(va)) for pm in
+                self.estimatorParamMaps]
+        best = int(np.argmax(mets) if self.evaluator.isLargerBetter() else np.argmin(mets))
+        return TrainValidationSplitModel(self.estimator.copy(self.estimatorParamMaps[best]).fit(table), mets, best)

@@ -144,6 +144,35 @@ PYBIND11_MODULE(_har_native, m) {
           "regression_moments");
   });
 
+  m.def("tree_hist_split", [](u bins, int64_t N, int F, u nbins, u rows, u row_w, u node_start, u node_count, int A,
+                              u feats, int m, int fc, u label, int K, int maxbins, float min_inst, float min_gain,
+                              int impurity, u gain, u feat, u bin, u left, u total, u stream) {
+    check(har_tree_hist_split(P<const uint8_t>(bins), N, F, P<const int32_t>(nbins), P<const int32_t>(rows),
+                              P<const float>(row_w), P<const int32_t>(node_start), P<const int32_t>(node_count), A,
+                              P<const int32_t>(feats), m, fc, P<const int32_t>(label), K, maxbins, min_inst, min_gain,
+                              impurity, P<float>(gain), P<int32_t>(feat), P<int32_t>(bin), P<float>(left),
+                              P<float>(total), S(stream)),
+          "tree_hist_split");
+  });
+
+  m.def("forest_predict", [](u X, int64_t n, int F, int ld, u feat, u thr, u left, u right, u leaf, int T, int maxn,
+                             int K, int max_depth, int normalize, u out, u stream) {
+    check(har_forest_predict(P<const float>(X), n, F, ld, P<const int32_t>(feat), P<const float>(thr),
+                             P<const int32_t>(left), P<const int32_t>(right), P<const float>(leaf), T, maxn, K,
+                             max_depth, normalize, P<float>(out), S(stream)),
+          "forest_predict");
+  });
+
+  m.def("poisson_bootstrap", [](uint64_t seed, int tree0, int ntrees, int64_t row0, int64_t n, u out, u stream) {
+    check(har_poisson_bootstrap(seed, tree0, ntrees, row0, n, P<uint8_t>(out), S(stream)), "poisson_bootstrap");
+  });
+
+  m.def("philox_buckets", [](uint64_t seed, uint32_t stream_id, int64_t row0, int64_t n, u thr, int nthr, u out,
+                             u stream) {
+    check(har_philox_buckets(seed, stream_id, row0, n, P<const uint32_t>(thr), nthr, P<int32_t>(out), S(stream)),
+          "philox_buckets");
+  });
+
   m.def("cast_pad_bf16", [](u in, int rows, int cin, int ldin, u out, int cout, u stream) {
     check(har_cast_pad_bf16(P<const float>(in), rows, cin, ldin, P<uint16_t>(out), cout, S(stream)), "cast_pad_bf16");
   });

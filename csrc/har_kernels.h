@@ -77,16 +77,19 @@ int har_window_features(const float* stream, int64_t n_samples, int axes, int wi
                         int64_t n_windows, float hz, int nbins, float* out, int ld_out, hipStream_t s);
 
 // ---- trees ----
-int har_tree_hist(const uint8_t* bins, int64_t n_rows, int n_feat, const int32_t* rows, const int32_t* node_start,
-                  const int32_t* node_count, int n_nodes, const int32_t* feats, int m_feats, const int32_t* label,
-                  const uint8_t* weight, int64_t weight_stride, const int32_t* node_tree, int n_bins, int n_classes,
-                  float* hist, hipStream_t s);
-int har_tree_split(const float* hist, int n_nodes, int m_feats, int n_bins, int n_classes, const int32_t* feats,
-                   const int32_t* nbins_feat, int min_instances, float min_info_gain, int impurity,
-                   int32_t* best_feat, int32_t* best_bin, float* best_gain, float* node_stats, hipStream_t s);
+// Fused per-level histogram + best split; grid (feature chunks, active nodes).
+// rows/row_w list each node's rows contiguously (node_start/node_count); feats [A][m].
+// Outputs per (node, chunk): gain (-inf = none), global feature, bin, left class counts [K];
+// out_total [A][K] = node class counts.
+int har_tree_hist_split(const uint8_t* bins, int64_t N, int F, const int32_t* nbins_feat, const int32_t* rows,
+                        const float* row_w, const int32_t* node_start, const int32_t* node_count, int A,
+                        const int32_t* feats, int m, int fc, const int32_t* label, int K, int maxbins,
+                        float min_inst, float min_gain, int impurity, float* out_gain, int32_t* out_feat,
+                        int32_t* out_bin, float* out_left, float* out_total, hipStream_t s);
+// Sum over trees of (normalized) leaf statistics; trees as SoA [T][maxn] arrays, feature < 0 = leaf.
 int har_forest_predict(const float* X, int64_t n, int F, int ld, const int32_t* feat, const float* thr,
-                       const int32_t* left, const int32_t* right, const float* leaf, const int32_t* roots,
-                       int ntrees, int K, int max_depth, float* raw_out, hipStream_t s);
+                       const int32_t* left, const int32_t* right, const float* leaf, int ntrees, int maxn, int K,
+                       int max_depth, int normalize, float* raw_out, hipStream_t s);
 
 // ---- CSV on device ----
 int har_csv_count_lines(const uint8_t* buf, int64_t n, int64_t* block_counts, int nblocks, hipStream_t s);

@@ -1,0 +1,222 @@
+// Decision-tree / random-forest kernels.
+//
+// tree_hist_split: one workgroup per (active node, feature chunk).  The node's
+//   rows (grouped contiguously by the caller) are streamed once per chunk; every
+//   (row, feature) pair adds its bootstrap weight to an LDS-privatized histogram
+//   [chunk features][bins][classes].  Then one wave per feature runs an inclusive
+//   prefix scan over the bins (one lane per bin, <= 64 bins), evaluates the
+//   impurity gain of every threshold in fp64, and the workgroup reduces the best
+//   (gain, feature, bin) — the histogram never leaves LDS.  Ties break to the
+//   lowest (feature slot, bin), matching the CPU oracle.
+// forest_predict: one lane per row walks every tree (SoA node arrays, L2
+//   resident) and accumulates the (normalized) leaf class statistics.
+// poisson_bootstrap: Philox4x32-10 keyed by (seed, tree, global row id) ->
+//   Poisson(1) counts, identical to har/ops/rng.py.
+#include "common.h"
+#include "philox.h"
+#include "../har_kernels.h"
+
+namespace {
+
+constexpr int KMAX = 32;
+
+__device__ __forceinline__ double impurity_of(const double* c, double w, int K, int kind) {
+  if (w <= 0) return 0.0;
+  double s = 0.0;
+  if (kind == 0) {
+    for (int k = 0; k < K; ++k) { double p = c[k] / w; s += p * p; }
+    return 1.0 - s;
+  }
+  for (int k = 0; k < K; ++k) {
+    double p = c[k] / w;
+    if (p > 0) s -= p * log2(p);
+  }
+  return s;
+}
+
+__global__ __launch_bounds__(256) void tree_hist_split_kernel(
+    const uint8_t* __restrict__ bins, int64_t N, const int32_t* __restrict__ nbins_feat,
+    const int32_t* __restrict__ rows, const float* __restrict__ row_w, const int32_t* __restrict__ node_start,
+    const int32_t* __restrict__ node_count, const int32_t* __restrict__ feats, int m, int fc,
+    const int32_t* __restrict__ label, int K, int maxbins, float min_inst, float min_gain, int impurity,
+    float* __restrict__ out_gain, int32_t* __restrict__ out_feat, int32_t* __restrict__ out_bin,
+    float* __restrict__ out_left, float* __restrict__ out_total) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int a = blockIdx.y, c = blockIdx.x, chunks = gridDim.x;
+  const int f_lo = c * fc;
+  const int f_n = min(fc, m - f_lo);
+  float* hist = smem;                                          // [fc][maxbins][K]
+  int* fid = reinterpret_cast<int*>(smem + (size_t)fc * maxbins * K);  // [fc]
+  __shared__ double red_gain[4];
+  __shared__ int red_idx[4];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int start = node_start[a], cnt = node_count[a];
+
+  for (int i = tid; i < f_n * maxbins * K; i += blockDim.x) hist[i] = 0.f;
+  for (int i = tid; i < f_n; i += blockDim.x) fid[i] = feats[(size_t)a * m + f_lo + i];
+  __syncthreads();
+
+  // ---- histogram: (feature slot, row) pairs, rows fastest -> coalesced bin reads ----
+  const int64_t pairs = (int64_t)cnt * f_n;
+  for (int64_t j = tid; j < pairs; j += blockDim.x) {
+    const int fs = (int)(j / cnt);
+    const int ri = (int)(j - (int64_t)fs * cnt);
+    const int r = rows[start + ri];
+    const float w = row_w[start + ri];
+    const int b = bins[(size_t)fid[fs] * N + r];
+    atomicAdd(&hist[(fs * maxbins + b) * K + label[r]], w);
+  }
+  __syncthreads();
+
+  // ---- split search: one wave per feature slot, one lane per bin ----
+  double best_g = -INFINITY;
+  int best_i = 0x7fffffff;
+  for (int fs = wave; fs < f_n; fs += (int)(blockDim.x >> 6)) {
+    const int nb = nbins_feat[fid[fs]];
+    double left[KMAX], tot[KMAX];
+    double wl = 0.0, wt = 0.0;
+    for (int k = 0; k < K; ++k) {
+      double v = (lane < nb && lane < maxbins) ? (double)hist[(fs * maxbins + lane) * K + k] : 0.0;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        double u = __shfl_up(v, o, 64);
+        if (lane >= o) v += u;
+      }
+      left[k] = v;
+      tot[k] = __shfl(v, max(nb - 1, 0), 64);
+      wl += v;
+      wt += tot[k];
+    }
+    const double wr = wt - wl;
+    double right[KMAX];
+    for (int k = 0; k < K; ++k) right[k] = tot[k] - left[k];
+    double g = -INFINITY;
+    if (lane < nb - 1 && wl >= min_inst && wr >= min_inst && wt > 0) {
+      g = impurity_of(tot, wt, K, impurity) - (wl / wt) * impurity_of(left, wl, K, impurity) -
+          (wr / wt) * impurity_of(right, wr, K, impurity);
+    }
+    int idx = fs * maxbins + lane;
+    // wave argmax, lowest index on ties
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      double og = __shfl_xor(g, o, 64);
+      int oi = __shfl_xor(idx, o, 64);
+      if (og > g || (og == g && oi < idx)) { g = og; idx = oi; }
+    }
+    if (g > best_g || (g == best_g && idx < best_i)) { best_g = g; best_i = idx; }
+  }
+  if (lane == 0) { red_gain[wave] = best_g; red_idx[wave] = best_i; }
+  __syncthreads();
+  if (tid == 0) {
+    double g = red_gain[0];
+    int idx = red_idx[0];
+    for (int w = 1; w < (int)(blockDim.x >> 6); ++w)
+      if (red_gain[w] > g || (red_gain[w] == g && red_idx[w] < idx)) { g = red_gain[w]; idx = red_idx[w]; }
+    const size_t o = (size_t)a * chunks + c;
+    const bool ok = isfinite(g) && g >= (double)min_gain;
+    out_gain[o] = ok ? (float)g : -INFINITY;
+    const int fs = ok ? idx / maxbins : 0, b = ok ? idx % maxbins : 0;
+    out_feat[o] = fid[fs];
+    out_bin[o] = b;
+    for (int k = 0; k < K; ++k) {
+      float s = 0.f;
+      for (int bb = 0; bb <= b; ++bb) s += hist[(fs * maxbins + bb) * K + k];
+      out_left[o * K + k] = ok ? s : 0.f;
+    }
+    if (c == 0) {
+      for (int k = 0; k < K; ++k) {
+        float s = 0.f;
+        for (int bb = 0; bb < maxbins; ++bb) s += hist[bb * K + k];
+        out_total[(size_t)a * K + k] = s;
+      }
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void forest_predict_kernel(
+    const float* __restrict__ X, int64_t n, int ld, const int32_t* __restrict__ feature,
+    const float* __restrict__ thr, const int32_t* __restrict__ left, const int32_t* __restrict__ right,
+    const float* __restrict__ leaf, int T, int maxn, int K, int max_depth, int normalize, float* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  float acc[KMAX];
+  for (int k = 0; k < K; ++k) acc[k] = 0.f;
+  const float* x = X + i * (int64_t)ld;
+  for (int t = 0; t < T; ++t) {
+    const size_t base = (size_t)t * maxn;
+    int node = 0;
+    for (int d = 0; d <= max_depth; ++d) {
+      const int f = feature[base + node];
+      if (f < 0) break;
+      node = (x[f] <= thr[base + node]) ? left[base + node] : right[base + node];
+    }
+    const float* st = leaf + (base + node) * K;
+    float s = 1.f;
+    if (normalize) {
+      s = 0.f;
+      for (int k = 0; k < K; ++k) s += st[k];
+      s = s > 0.f ? 1.f / s : 0.f;
+    }
+    for (int k = 0; k < K; ++k) acc[k] += st[k] * s;
+  }
+  for (int k = 0; k < K; ++k) out[i * K + k] = acc[k];
+}
+
+__global__ __launch_bounds__(256) void poisson_bootstrap_kernel(uint64_t seed, int tree0, int ntrees, int64_t row0,
+                                                                int64_t n, uint8_t* __restrict__ out) {
+  // uint32 CDF thresholds of Poisson(1) (same table as har/ops/rng.py)
+  const uint32_t thr[15] = {1580030168u, 3160060337u, 3950075421u, 4213413783u, 4279248373u, 4292415291u,
+                            4294609777u, 4294923276u, 4294962463u, 4294966817u, 4294967252u, 4294967292u,
+                            4294967295u, 4294967295u, 4294967295u};
+  const int64_t total = (int64_t)ntrees * n;
+  for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < total; j += (int64_t)gridDim.x * blockDim.x) {
+    const int t = (int)(j / n);
+    const int64_t r = j - (int64_t)t * n;
+    const uint32_t u = philox_u32(seed, 0x1000u + (uint32_t)(tree0 + t), (uint64_t)(row0 + r));
+    int k = 0;
+    while (k < 15 && u >= thr[k]) ++k;
+    out[j] = (uint8_t)k;
+  }
+}
+
+}  // namespace
+
+extern "C" int har_tree_hist_split(const uint8_t* bins, int64_t N, int F, const int32_t* nbins_feat,
+                                   const int32_t* rows, const float* row_w, const int32_t* node_start,
+                                   const int32_t* node_count, int A, const int32_t* feats, int m, int fc,
+                                   const int32_t* label, int K, int maxbins, float min_inst, float min_gain,
+                                   int impurity, float* out_gain, int32_t* out_feat, int32_t* out_bin,
+                                   float* out_left, float* out_total, hipStream_t s) {
+  if (K > KMAX || maxbins > 64 || fc <= 0 || m <= 0) return -2;
+  if (A == 0) return 0;
+  const int chunks = (m + fc - 1) / fc;
+  const size_t lds = (size_t)fc * maxbins * K * sizeof(float) + (size_t)fc * sizeof(int);
+  if (lds > 150 * 1024) return -3;
+  dim3 grid(chunks, A);
+  tree_hist_split_kernel<<<grid, 256, lds, s>>>(bins, N, nbins_feat, rows, row_w, node_start, node_count, feats, m,
+                                                fc, label, K, maxbins, min_inst, min_gain, impurity, out_gain,
+                                                out_feat, out_bin, out_left, out_total);
+  HAR_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int har_forest_predict(const float* X, int64_t n, int F, int ld, const int32_t* feat, const float* thr,
+                                  const int32_t* left, const int32_t* right, const float* leaf, int ntrees,
+                                  int maxn, int K, int max_depth, int normalize, float* raw_out, hipStream_t s) {
+  if (K > KMAX) return -2;
+  if (n == 0) return 0;
+  forest_predict_kernel<<<(int)((n + 255) / 256), 256, 0, s>>>(X, n, ld, feat, thr, left, right, leaf, ntrees, maxn,
+                                                               K, max_depth, normalize, raw_out);
+  HAR_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int har_poisson_bootstrap(uint64_t seed, int tree0, int ntrees, int64_t row0, int64_t n, uint8_t* out,
+                                     hipStream_t s) {
+  int64_t total = (int64_t)ntrees * n;
+  if (total == 0) return 0;
+  int blocks = (int)std::min<int64_t>(4096, (total + 255) / 256);
+  poisson_bootstrap_kernel<<<blocks, 256, 0, s>>>(seed, tree0, ntrees, row0, n, out);
+  HAR_CHECK_LAUNCH();
+  return 0;
+}

@@ -1,0 +1,191 @@
+#!/usr/bin/env python3
+"""``main.py`` — the reference entry point (``Main/main.py``), MI355X-native.
+
+Same flow and artefacts as the PySpark script: load the WISDM CSV, print the
+schema / sample / class counts / describe, run the feature pipeline, split
+70/30 (seed 2018), train and evaluate LogisticRegression, LR+CrossValidator,
+DecisionTree(+CV), RandomForest(+CV) — plus NaiveBayes and an MLP — and write
+``result.txt``, ``additional_param.csv``, ``crossFold_additional_param.csv``
+(identical headers), a ``metrics.jsonl`` record and optional plots / saved models.
+
+    python main.py                                  # the reference run (all six models)
+    python main.py --classifiers lr --device cpu     # BASELINE config 1 (plumbing)
+    python main.py --preset rf-deep                  # RF 100 trees x depth 10 on the GPU
+    python main.py --preset all-numeric --save-models models/
+
+Paths default to the reference layout relative to the working directory
+(``wisdm_main_ver_0.0/main_result``); ``--data`` points at the CSV.
+"""
+from __future__ import annotations
+
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from har.config import RunConfig, config_from_args  # noqa: E402
+from har.data.csv_io import read_csv  # noqa: E402
+from har.data.split import random_split  # noqa: E402
+from har.data.table import describe_text  # noqa: E402
+from har.evaluation.evaluators import (MulticlassClassificationEvaluator, RegressionEvaluator,  # noqa: E402
+                                       evaluate_all)
+from har.features import wisdm  # noqa: E402
+from har.models.base import features_tensor, resolve_device  # noqa: E402
+from har.models.logreg import LogisticRegression  # noqa: E402
+from har.models.mlp import MultilayerPerceptronClassifier  # noqa: E402
+from har.models.naive_bayes import NaiveBayes  # noqa: E402
+from har.models.tree import DecisionTreeClassifier, RandomForestClassifier  # noqa: E402
+from har.report import csvout  # noqa: E402
+from har.report.text import (BANNER_CLASSIFY, BANNER_PIPELINE, BANNER_TRAIN, RunLog, evaluation_block,  # noqa: E402
+                             model_header, section)
+from har.tuning.crossval import CrossValidator, ParamGridBuilder  # noqa: E402
+from har.utils import persist  # noqa: E402
+from har.utils.timing import device_sync  # noqa: E402
+
+
+def cv_evaluator(metric: str):
+    if metric in ("mae", "rmse", "mse", "r2"):
+        return RegressionEvaluator(labelCol="label", predictionCol="prediction", metricName=metric)
+    return MulticlassClassificationEvaluator(labelCol="label", predictionCol="prediction", metricName=metric)
+
+
+def build_estimator(name: str, cfg: RunConfig, dev, n_features: int, n_classes: int):
+    lr = LogisticRegression(maxIter=cfg.lr_max_iter, regParam=cfg.lr_reg, elasticNetParam=cfg.lr_elastic_net,
+                            device=dev)
+    dt = DecisionTreeClassifier(featuresCol="features", labelCol="label", maxDepth=cfg.dt_max_depth,
+                                maxBins=cfg.max_bins, device=dev)
+    rf = RandomForestClassifier(featuresCol="features", labelCol="label", numTrees=cfg.rf_num_trees,
+                                maxDepth=cfg.rf_max_depth, maxBins=cfg.max_bins, seed=cfg.seed, device=dev)
+    if name == "lr":
+        return lr
+    if name == "dt":
+        return dt
+    if name == "rf":
+        return rf
+    if name == "nb":
+        return NaiveBayes(modelType=cfg.nb_model_type, device=dev)
+    if name == "mlp":
+        return MultilayerPerceptronClassifier(layers=[n_features] + list(cfg.mlp_hidden) + [n_classes],
+                                              maxIter=cfg.mlp_epochs, blockSize=cfg.mlp_batch, stepSize=cfg.mlp_lr,
+                                              seed=cfg.seed, device=dev)
+    if name.endswith("cv"):
+        base = build_estimator(name[:-2], cfg, dev, n_features, n_classes)
+        grid = ParamGridBuilder()
+        if name == "lrcv":
+            grid = grid.addGrid("regParam", cfg.cv_reg_grid).addGrid("elasticNetParam", cfg.cv_en_grid)
+        return CrossValidator(estimator=base, estimatorParamMaps=grid.build(), evaluator=cv_evaluator(cfg.cv_metric),
+                              numFolds=cfg.cv_folds, seed=cfg.seed)
+    raise ValueError(f"unknown classifier {name}")
+
+
+def run(cfg: RunConfig) -> dict:
+    dev = resolve_device(None if cfg.device == "auto" else cfg.device)
+    os.makedirs(cfg.out_dir, exist_ok=True)
+    log = RunLog(os.path.join(cfg.out_dir, "result.txt"), echo=cfg.echo)
+    t_run = time.perf_counter()
+
+    log.print("Loading Data Set...")
+    raw = read_csv(cfg.data)
+    data, pipe_model, df = wisdm.prepare(raw, cfg.encoding)
+    section(log, "Data Schema")
+    log.print(data.print_schema(), end="")
+    section(log, "Sample Data")
+    log.print(data.show(5), end="")
+    section(log, "Activity Count")
+    log.print(data.group_count("activity").show(), end="")
+    numeric_features = [n for n, t in data.dtypes if t in ("double", "int")]
+    section(log, "Summary")
+    log.print(describe_text(data.describe(numeric_features)))
+
+    log.print(BANNER_PIPELINE)
+    cols = data.columns
+    df = df.select(["label", "features"] + cols)
+    section(log, "Model Pipeline Schema")
+    log.print(df.print_schema(), end="")
+    section(log, "Sample Feature Data")
+    import pandas as pd
+
+    head = df.head(5)
+    log.print(pd.DataFrame({c: [tuple(np.round(v[:9], 2)) if head[c].kind == "vector" else v
+                                for v in head[c].data] for c in head.columns}))
+
+    train, test = random_split(df, cfg.split, seed=cfg.seed)
+    log.print(BANNER_TRAIN)
+    log.print("Training Dataset Count : " + str(train.count()))
+    log.print("Test Dataset Count     : " + str(test.count()))
+    keep = [c for c in test.columns if c not in wisdm.MINIMIZED_VIEW]
+    log.print(train.select(keep).show(5), end="")
+    log.print(test.select(keep).show(5), end="")
+    test_data = test.select([c for c in test.columns if c not in wisdm.SKIPPED_FOR_TEST])
+    log.print(test_data.show(5), end="")
+
+    log.print(BANNER_CLASSIFY)
+    n_features = df["features"].data.shape[1]
+    vocab = df["label"].meta["vocab"]
+    n_classes = len(vocab)
+    plain_rows, cv_rows, records = [], [], {}
+    X_test = features_tensor(test_data, "features", dev)
+    y_test = torch.as_tensor(test_data["label"].data.astype(np.int64), device=dev)
+    for name in cfg.classifiers:
+        est = build_estimator(name, cfg, dev, n_features, n_classes)
+        device_sync(dev)
+        t0 = time.perf_counter()
+        model = est.fit(train)
+        device_sync(dev)
+        train_s = round(time.perf_counter() - t0, 3)
+        t0 = time.perf_counter()
+        raw_pred, prob, pred = (model.bestModel if hasattr(model, "bestModel") else model).predict_all(X_test)
+        device_sync(dev)
+        test_s = round(time.perf_counter() - t0, 3)
+        label = str(model) + (" for Logistic Regression" if name == "lrcv" else "")
+        model_header(log, label, train_s, test_s)
+        preds = model.transform(test_data)
+        show_class = 5 if name == "lr" else 0
+        pv = preds.filter(preds["prediction"].data == show_class).select(
+            ["UID", "probability", "label", "prediction"]).order_by("probability", ascending=False)
+        log.print(pv.show(n=5, truncate=30), end="")
+        r = evaluate_all(y_test, pred, raw_pred, n_classes)
+        evaluation_block(log, r)
+        row = (csvout.cv_row if name.endswith("cv") else csvout.plain_row)(str(model), r, train_s, test_s)
+        (cv_rows if name.endswith("cv") else plain_rows).append(row)
+        records[name] = {"model": str(model), "train_s": train_s, "predict_s": test_s,
+                         "train_windows_per_s": train.count() / max(train_s, 1e-9),
+                         "predict_windows_per_s": test.count() / max(test_s, 1e-9), **r.as_dict()}
+        if cfg.save_models:
+            persist.save(model, os.path.join(cfg.save_models, name), labels=vocab)
+    if cfg.save_models:
+        persist.save(pipe_model, os.path.join(cfg.save_models, "pipeline"), labels=vocab)
+
+    if plain_rows:
+        csvout.write_rows(os.path.join(cfg.out_dir, "additional_param.csv"), csvout.PLAIN_FIELDS, plain_rows,
+                          append=cfg.append_csv)
+    if cv_rows:
+        csvout.write_rows(os.path.join(cfg.out_dir, "crossFold_additional_param.csv"), csvout.CV_FIELDS, cv_rows,
+                          append=cfg.append_csv)
+    summary = {"device": str(dev), "encoding": cfg.encoding, "n_train": train.count(), "n_test": test.count(),
+               "seed": cfg.seed, "wall_s": time.perf_counter() - t_run, "models": records}
+    csvout.append_jsonl(os.path.join(cfg.out_dir, "metrics.jsonl"), summary)
+    log.close()
+    if cfg.plots:
+        from har.report.plots import write_plots
+
+        write_plots(data, numeric_features, cfg.plot_dir, seed=cfg.seed)
+    return summary
+
+
+def main(argv=None):
+    cfg = config_from_args(argv)
+    summary = run(cfg)
+    print(json.dumps({k: {kk: (round(vv, 6) if isinstance(vv, float) else vv) for kk, vv in v.items()
+                          if kk in ("accuracy", "f1", "train_s", "predict_s")} for k, v in summary["models"].items()}))
+
+
+if __name__ == "__main__":
+    main()
