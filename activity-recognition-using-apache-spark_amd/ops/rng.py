@@ -127,3 +127,28 @@ def feature_subsets(seed: int, trees, nodes, n_features: int, m: int) -> np.ndar
         chosen[:, i] = np.where(dup, j, t)
     chosen.sort(axis=1)
     return chosen.astype(np.int32)
+
+
+def device_buckets(seed: int, stream: int, row0: int, n: int, weights, device):
+    """``assign_buckets`` on the GPU (HIP kernel ``har_philox_buckets``); int32 [n]."""
+    import torch
+
+    from . import _native
+
+    thr = bucket_thresholds(weights)[:-1].astype(np.uint32)
+    thr_t = torch.from_numpy(thr.view(np.int32)).to(device)
+    out = torch.empty(n, dtype=torch.int32, device=device)
+    _native.kernels().philox_buckets(seed, stream, row0, n, thr_t.data_ptr(), len(thr), out.data_ptr(),
+                                     _native.stream_ptr())
+    return out
+
+
+def device_poisson1(seed: int, tree0: int, ntrees: int, row0: int, n: int, device):
+    """``poisson1_weights`` on the GPU (HIP kernel ``har_poisson_bootstrap``); uint8 [ntrees, n]."""
+    import torch
+
+    from . import _native
+
+    out = torch.empty(ntrees, n, dtype=torch.uint8, device=device)
+    _native.kernels().poisson_bootstrap(seed, tree0, ntrees, row0, n, out.data_ptr(), _native.stream_ptr())
+    return out

@@ -1,0 +1,134 @@
+"""GPU model paths (HIP kernels) vs the CPU oracles of the same algorithms."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _blobs(n=3000, f=20, k=6, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    mu = torch.randn(k, f, generator=g) * 1.5
+    y = torch.randint(0, k, (n,), generator=g)
+    x = mu[y] + torch.randn(n, f, generator=g)
+    return x, y
+
+
+def test_philox_buckets_device_matches_host(cuda):
+    from har.ops import rng
+
+    n = 100_003
+    host = rng.assign_buckets(2018, rng.STREAM_SPLIT, np.arange(5, 5 + n, dtype=np.uint64), [0.7, 0.3])
+    dev = rng.device_buckets(2018, rng.STREAM_SPLIT, 5, n, [0.7, 0.3], cuda).cpu().numpy()
+    assert np.array_equal(host, dev)
+
+
+def test_poisson_device_matches_host(cuda):
+    from har.ops import rng
+
+    host = rng.poisson1_weights(7, range(3, 8), 20_000, row_offset=11)
+    dev = rng.device_poisson1(7, 3, 5, 11, 20_000, cuda).cpu().numpy()
+    assert np.array_equal(host, dev)
+    assert abs(dev.mean() - 1.0) < 0.02
+
+
+def test_hist_split_native_matches_torch(cuda):
+    from har.ops import rng
+    from har.ops import tree as T
+
+    x, y = _blobs(2000, 30, 5)
+    thr = T.find_thresholds(x.numpy(), 32)
+    bins = torch.from_numpy(T.bin_features(x.numpy(), thr)).to(cuda)
+    nbins = torch.tensor([len(t) + 1 for t in thr], dtype=torch.int32, device=cuda)
+    # 3 nodes with overlapping random row subsets and weights
+    g = torch.Generator().manual_seed(1)
+    keys, rows = [], []
+    for a in range(3):
+        r = torch.randperm(2000, generator=g)[: 500 + 300 * a].sort().values
+        rows.append(r)
+        keys.append(torch.full_like(r, a))
+    rows = torch.cat(rows).to(torch.int32).to(cuda)
+    keys = torch.cat(keys).to(cuda)
+    w = torch.randint(1, 3, (rows.numel(),), generator=g).float().to(cuda)
+    counts = torch.bincount(keys, minlength=3).to(torch.int32)
+    starts = (torch.cumsum(counts, 0) - counts).to(torch.int32)
+    feats = torch.from_numpy(rng.feature_subsets(3, [0, 0, 1], [0, 1, 0], 30, 12)).to(cuda)
+    y32 = y.to(torch.int32).to(cuda)
+    nat = T.hist_split_native(bins, nbins, y32, rows, w, starts, counts, feats, 5, 32, 1.0, 0.0, T.GINI)
+    ref = T.hist_split_torch(bins, nbins, y32, rows, w, keys, 3, feats, 5, 32, 1.0, 0.0, T.GINI)
+    torch.testing.assert_close(nat.total, ref.total)
+    torch.testing.assert_close(nat.gain, ref.gain, rtol=1e-5, atol=1e-6)
+    assert torch.equal(nat.feat, ref.feat) and torch.equal(nat.bin, ref.bin)
+    torch.testing.assert_close(nat.left, ref.left)
+
+
+def test_forest_predict_native_matches_torch(cuda):
+    from har.models.tree import RandomForestClassifier
+    from har.ops import tree as T
+
+    x, y = _blobs(1500, 16, 4, seed=2)
+    m = RandomForestClassifier(numTrees=20, maxDepth=6, seed=3, device="cpu").fit_tensors(x, y, 4)
+    a = m.arrs
+    ref = T.forest_predict_torch(x, a.feature, a.threshold, a.left, a.right, a.stats, a.max_depth, True)
+    ac = a.to(cuda)
+    nat = T.forest_predict_native(x.to(cuda), ac.feature, ac.threshold, ac.left, ac.right, ac.stats, ac.max_depth,
+                                  True)
+    torch.testing.assert_close(nat.cpu(), ref, rtol=1e-5, atol=1e-5)
+
+
+def test_decision_tree_gpu_equals_cpu(cuda):
+    from har.models.tree import DecisionTreeClassifier
+
+    x, y = _blobs(2500, 12, 6, seed=4)
+    cpu = DecisionTreeClassifier(maxDepth=5, device="cpu").fit_tensors(x, y, 6)
+    gpu = DecisionTreeClassifier(maxDepth=5, device=cuda).fit_tensors(x.to(cuda), y.to(cuda), 6)
+    assert cpu.numNodes == gpu.numNodes
+    assert torch.equal(cpu.arrs.feature, gpu.arrs.feature.cpu())
+    assert torch.equal(cpu.predict(x), gpu.predict(x.to(cuda)).cpu())
+
+
+def test_random_forest_gpu_accuracy(cuda):
+    from har.models.tree import RandomForestClassifier
+
+    xa, ya = _blobs(6000, 20, 6, seed=5)
+    x, y, xt, yt = xa[:4000], ya[:4000], xa[4000:], ya[4000:]
+    gpu = RandomForestClassifier(numTrees=50, maxDepth=8, seed=1, device=cuda).fit_tensors(x.to(cuda), y.to(cuda), 6)
+    cpu = RandomForestClassifier(numTrees=50, maxDepth=8, seed=1, device="cpu").fit_tensors(x, y, 6)
+    acc_g = float((gpu.predict(xt.to(cuda)).cpu() == yt).float().mean())
+    acc_c = float((cpu.predict(xt) == yt).float().mean())
+    assert acc_g > 0.8 and abs(acc_g - acc_c) < 0.03
+
+
+def test_logreg_gpu_matches_cpu(cuda):
+    from har.models.logreg import FitSpec, LogisticRegression
+
+    x, y = _blobs(3000, 24, 6, seed=7)
+    est = LogisticRegression(maxIter=50, regParam=0.1)
+    specs = [FitSpec(None, 0.1, 0.0), FitSpec(None, 0.1, 0.5)]
+    cpu = est.fit_many(x, y, specs, 6)
+    gpu = est.fit_many(x.to(cuda), y.to(cuda), specs, 6)
+    for c, g in zip(cpu, gpu):
+        assert abs(c.summary["objective"] - g.summary["objective"]) < 1e-3
+        agree = (c.predict(x) == g.predict(x.to(cuda)).cpu()).float().mean()
+        assert agree > 0.99
+
+
+def test_naive_bayes_gpu_matches_cpu(cuda):
+    from har.models.naive_bayes import NaiveBayes
+
+    x, y = _blobs(2000, 10, 4, seed=8)
+    for mt, xx in (("gaussian", x), ("multinomial", x.abs())):
+        c = NaiveBayes(modelType=mt).fit_tensors(xx, y, 4)
+        g = NaiveBayes(modelType=mt).fit_tensors(xx.to(cuda), y.to(cuda), 4)
+        torch.testing.assert_close(g.predict_raw(xx.to(cuda)).cpu(), c.predict_raw(xx), rtol=1e-4, atol=1e-3)
+
+
+def test_main_reference_run_gpu(cuda, tmp_path, wisdm_csv):
+    import main
+
+    s = main.run(main.config_from_args(["--data", wisdm_csv, "--out-dir", str(tmp_path), "--classifiers",
+                                        "lr,lrcv,dt,rf", "--device", "cuda"]))
+    m = s["models"]
+    assert m["lr"]["accuracy"] >= 0.60 and m["lrcv"]["accuracy"] >= 0.70
+    assert m["dt"]["accuracy"] >= 0.72 and m["rf"]["accuracy"] >= 0.62
+    assert (tmp_path / "result.txt").exists() and (tmp_path / "additional_param.csv").exists()
