@@ -126,8 +126,15 @@ class LogisticRegression(Estimator, ClassifierParams):
         return model
 
     def fit_many(self, X: torch.Tensor, y: torch.Tensor, specs: Sequence[FitSpec],
-                 num_classes: Optional[int] = None) -> List[LogisticRegressionModel]:
-        """Train ``len(specs)`` models in one batched device optimization."""
+                 num_classes: Optional[int] = None, allreduce=None) -> List[LogisticRegressionModel]:
+        """Train ``len(specs)`` models in one batched device optimization.
+
+        Data parallel: every rank passes its own row shard and ``allreduce`` (an
+        in-place SUM over ranks, e.g. RCCL); the summarizer statistics and every
+        objective evaluation's (loss, gradient) bucket are summed across ranks —
+        Spark's ``treeAggregate`` as ONE flat all-reduce — and
+        the replicated optimizer then takes identical steps on every rank.
+        """
         dev = X.device
         N, F = X.shape
         K = int(num_classes or int(y.max()) + 1)
@@ -136,19 +143,24 @@ class LogisticRegression(Estimator, ClassifierParams):
         B = len(specs)
         rw = torch.stack([torch.ones(N, device=dev) if s.row_weight is None else s.row_weight.to(dev).float()
                           for s in specs])                                            # [B, N]
-        wsum = rw.sum(dim=1)
-        inv_wsum = (1.0 / wsum).float()
-        # weighted summarizer (Spark: MultivariateOnlineSummarizer + MultiClassSummarizer)
-        mean = (rw @ X) / wsum[:, None]
-        ex2 = (rw @ (X * X)) / wsum[:, None]
+        # weighted summarizer (Spark: MultivariateOnlineSummarizer + MultiClassSummarizer), fp64
+        rwd = rw.double()
+        counts = torch.zeros(B, Kp, device=dev, dtype=torch.float64)
+        counts.scatter_add_(1, y.view(1, -1).expand(B, -1).clamp_max(Kp - 1), rwd)
+        summ = torch.cat([rwd.sum(dim=1, keepdim=True), rwd @ X.double(), rwd @ (X.double() ** 2), counts], dim=1)
+        if allreduce is not None:
+            allreduce(summ)
+        wsum = summ[:, 0]
+        mean = summ[:, 1:1 + F] / wsum[:, None]
+        ex2 = summ[:, 1 + F:1 + 2 * F] / wsum[:, None]
+        counts = summ[:, 1 + 2 * F:].float()
         var = (ex2 - mean * mean) * (wsum / (wsum - 1).clamp_min(1.0))[:, None]
-        std = var.clamp_min(0).sqrt()
+        std = var.clamp_min(0).sqrt().float()
+        inv_wsum = (1.0 / wsum).float()
         if self.standardization:
-            inv_std = torch.where(std > 0, 1.0 / std.clamp_min(1e-300), torch.zeros_like(std))
+            inv_std = torch.where(std > 0, 1.0 / std.clamp_min(1e-30), torch.zeros_like(std))
         else:
             inv_std = torch.where(std > 0, torch.ones_like(std), torch.zeros_like(std))
-        counts = torch.zeros(B, Kp, device=dev)
-        counts.scatter_add_(1, y.view(1, -1).expand(B, -1).clamp_max(Kp - 1), rw)
         reg = torch.tensor([s.regParam for s in specs], device=dev, dtype=torch.float32)
         alpha = torch.tensor([s.elasticNetParam for s in specs], device=dev, dtype=torch.float32)
         l2 = reg * (1 - alpha)
@@ -191,6 +203,12 @@ class LogisticRegression(Estimator, ClassifierParams):
                 loss, gW, gb = logreg_loss_grad_native(Xc, y32, W_eff, b, rw, inv_wsum, ws)
             else:
                 loss, gW, gb = logreg_loss_grad_torch(Xc, y, W_eff, b, rw, inv_wsum)
+            if allreduce is not None:  # one flat bucket: [loss | dW | db] for all B models
+                flat = torch.cat([loss.float().view(B, 1), gW.reshape(B, -1), gb.reshape(B, -1)], dim=1)
+                allreduce(flat)
+                loss = flat[:, 0]
+                gW = flat[:, 1:1 + Kp * F].view(B, Kp, F)
+                gb = flat[:, 1 + Kp * F:].view(B, Kp)
             gbeta = gW * inv_std[:, None, :] + l2[:, None, None] * beta
             loss = loss + 0.5 * l2 * (beta * beta).sum(dim=(1, 2))
             g = torch.cat([gbeta, gb.unsqueeze(2)], dim=2) * pmask

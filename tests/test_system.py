@@ -1,0 +1,93 @@
+"""End-to-end: main.py artefacts, saved-model round trips, bench.py contract, build."""
+import csv
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_main_reference_run_cpu(tmp_path, wisdm_csv):
+    import main
+
+    cfg = main.config_from_args(["--data", wisdm_csv, "--out-dir", str(tmp_path), "--device", "cpu",
+                                 "--classifiers", "lr,dt,rf,lrcv", "--save-models", str(tmp_path / "models")])
+    s = main.run(cfg)
+    m = s["models"]
+    assert m["lr"]["accuracy"] >= 0.61 and m["dt"]["accuracy"] >= 0.72
+    assert m["rf"]["accuracy"] >= 0.62 and m["lrcv"]["accuracy"] >= 0.70
+    txt = (tmp_path / "result.txt").read_text()
+    for banner in ("Loading Data Set...", "Data Schema----", "Activity Count----", "MODELING PIPELINE",
+                   "Training Dataset Count : ", "CLASSIFICATION AND EVALUATION", "Binary Clasifier Area Under PR",
+                   "MultiClass Weighted Precision", "Mean Absolute Error on test data", "Total Correct        ="):
+        assert banner in txt
+    with open(tmp_path / "additional_param.csv") as f:
+        rows = list(csv.reader(f))
+    assert rows[0] == ['Classifier', 'Count Total', 'Correct', 'Wrong', 'Ratio Wrong', 'Ratio Correct', 'F1 Score',
+                       'Training Time', 'Testing Time', 'Accuracy']
+    assert len(rows) == 4
+    with open(tmp_path / "crossFold_additional_param.csv") as f:
+        rows = list(csv.reader(f))
+    assert rows[0][-3:] == ['Cross Validation Training Time', 'Cross Validation Testing Time', 'Cross Fold Accuracy']
+    rec = json.loads((tmp_path / "metrics.jsonl").read_text().splitlines()[-1])
+    assert rec["n_train"] + rec["n_test"] == 5418
+
+
+def test_persist_roundtrip(tmp_path, wisdm_csv):
+    from har.data.csv_io import read_csv
+    from har.data.split import random_split
+    from har.features import wisdm
+    from har.models.logreg import LogisticRegression
+    from har.models.mlp import MultilayerPerceptronClassifier
+    from har.models.naive_bayes import NaiveBayes
+    from har.models.tree import DecisionTreeClassifier, RandomForestClassifier
+    from har.utils import persist
+
+    raw = read_csv(wisdm_csv)
+    data, pm, df = wisdm.prepare(raw, "numeric43")
+    tr, te = random_split(df, [0.7, 0.3], 1)
+    X = torch.as_tensor(te["features"].data)
+    for est in (LogisticRegression(maxIter=5, device="cpu"), DecisionTreeClassifier(maxDepth=4, device="cpu"),
+                RandomForestClassifier(numTrees=5, maxDepth=3, device="cpu"), NaiveBayes(modelType="gaussian"),
+                MultilayerPerceptronClassifier(layers=[43, 32, 6], maxIter=1, device="cpu")):
+        m = est.fit(tr)
+        d = tmp_path / type(m).__name__
+        persist.save(m, str(d), labels=df["label"].meta["vocab"])
+        m2 = persist.load(str(d), device="cpu")
+        torch.testing.assert_close(m2.predict_raw(X), m.predict_raw(X))
+        md = json.loads((d / "metadata.json").read_text())
+        assert md["class"] == type(m).__name__ and md["labels"][0] == "Walking"
+    # pipeline: raw CSV rows -> identical features after reload
+    persist.save(pm, str(tmp_path / "pipe"))
+    pm2 = persist.load(str(tmp_path / "pipe"))
+    np.testing.assert_array_equal(pm2.transform(data)["features"].data, df["features"].data)
+
+
+def test_bench_contract_cpu():
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "2", "--warmup", "1",
+                        "--batch", "512"], capture_output=True, text=True, timeout=600, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-2000:]
+    rec = json.loads(r.stdout.strip().splitlines()[-1])
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+              "vs_baseline", "dtype", "data", "config"):
+        assert k in rec
+    assert rec["n_gpus"] == 1 and rec["steps"] == 2 and rec["value"] > 0
+    assert rec["config"]["parallelism"] == "dp1" and rec["scaling"] == "weak"
+
+
+def test_native_build_uptodate():
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import build_native
+
+    if not os.path.exists(build_native.HIPCC):
+        pytest.skip("no hipcc")
+    build_native.build()
+    assert not build_native.needs_build()
+    import har._har_native as nat
+
+    assert hasattr(nat, "gemm") and hasattr(nat, "tree_hist_split") and hasattr(nat, "csv_parse")
