@@ -1,24 +1,29 @@
 #!/usr/bin/env python3
-"""Flagship benchmark: WISDM-shaped 6-class 3-layer MLP, bf16 MFMA, data parallel.
+"""Benchmarks of the BASELINE.json configurations (default = the flagship).
 
-BASELINE.json config 3 ("WISDM 6-class 3-layer MLP bf16, DP all-reduce on
-8xMI355X"), metric "windows/sec (whole node) + test accuracy".  One process per
-GPU (``torch.distributed.run``), RCCL all-reduce of the flat gradient bucket
-over xGMI each step, weak scaling (fixed per-GPU batch).
+Metric (BASELINE.json): "windows/sec (whole node) + test accuracy on WISDM 6-class
+at 1/2/4/8 MI355X".  One process per GPU (``torch.distributed.run``), RCCL over
+xGMI, weak scaling (fixed per-GPU work).  Every line is ONE JSON record.
 
-A step = forward + backward + all-reduce + Adam on ``--batch`` windows per GPU
-(every window of the global batch goes through the full training step; nothing
-is skipped inside the timed region).  Data: synthetic WISDM-shaped windows
-(43 features = the WISDM transformed feature set width, 6 classes,
-class-conditional Gaussians, generated on device) — there is no network for
-the dataset; random-init weights.  After the timed region the model is scored
-on held-out synthetic windows (``test_accuracy``).
+``--config mlp``    (default; BASELINE config 3) WISDM-shaped 6-class 3-layer MLP, bf16
+                    MFMA kernels, DP all-reduce of one flat gradient bucket per step.
+                    Step = fwd + bwd + all-reduce + Adam on ``--batch`` windows per GPU.
+                    Data: synthetic WISDM-shaped windows (43 features, 6 classes,
+                    class-conditional Gaussians generated on device); random-init weights.
+``--config rf``     (config 2) RandomForest 100 trees x depth 10, 32 bins, on
+                    featurized synthetic 3-axis windows (43 WISDM features);
+                    step = one whole forest fit (histogram all-reduce per level in DP).
+``--config stream`` (config 4) raw synthetic 3-axis 20 Hz stream (1B samples per
+                    8 GPUs, i.e. 125M per GPU resident in HBM) -> HIP window featurizer
+                    -> MLP training step; step = featurize + train ``--batch`` windows.
+``--config rf9``    (config 5) 12-class 9-axis IMU RandomForest, 500 trees.
 
-``vs_baseline`` divides by the reference's published WISDM training throughput
-(LogisticRegression, 3793 windows / 9.061 s = 418.6 windows/s, run A,
-BASELINE.md §3) — the only train-windows/s number the reference publishes.
+``vs_baseline`` divides by the reference's published WISDM training throughput of
+the matching model family (run A): LogisticRegression 418.6
+windows/s for the MLP configs (the reference has no MLP; LR is its headline
+train-windows/s number), RandomForest 185.3 windows/s for the forest configs.
 
-Usage: python bench.py --gpus N --steps K --warmup W
+Usage: python bench.py --gpus N --steps K --warmup W [--config mlp|rf|stream|rf9]
 """
 from __future__ import annotations
 
@@ -30,49 +35,68 @@ import time
 
 import torch
 
-BASELINE_WINDOWS_PER_S = 418.6
 METRIC = "windows/sec (whole node) + test accuracy on WISDM 6-class at 1/2/4/8 MI355X"
+BASELINE = {"lr": 418.6, "rf": 185.3}
 N_FEATURES = 43
 N_CLASSES = 6
 WINDOW_SAMPLES = 200  # 10 s @ 20 Hz (WISDM v1.1 transformed windows)
+WISDM_PRIOR = [2081, 1625, 632, 528, 306, 246]
 
 
 def synthetic_windows(n: int, seed: int, device, class_seed: int = 2018):
     """Class-conditional Gaussian windows: x = mu[y] + noise; mu shared by all ranks."""
     g = torch.Generator(device="cpu").manual_seed(class_seed)
     mu = torch.randn(N_CLASSES, N_FEATURES, generator=g) * 0.6
-    prior = torch.tensor([2081, 1625, 632, 528, 306, 246], dtype=torch.float64)  # WISDM class mix
+    prior = torch.tensor(WISDM_PRIOR, dtype=torch.float64)
     gd = torch.Generator(device=device).manual_seed(seed)
     y = torch.multinomial(prior.to(device).float(), n, replacement=True, generator=gd)
     x = mu.to(device)[y] + torch.randn(n, N_FEATURES, device=device, generator=gd)
     return x, y
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--batch", type=int, default=65536, help="windows per GPU per step")
-    ap.add_argument("--hidden", type=int, default=256)
-    ap.add_argument("--lr", type=float, default=1e-3)
-    ap.add_argument("--graph", type=int, default=1, help="capture the step in a HIP graph")
-    ap.add_argument("--out", type=str, default="")
-    args = ap.parse_args()
+def timed(ctx, run, steps, warmup, dev):
+    from har.parallel import dist as hdist
 
-    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    for i in range(warmup):
+        run(i)
+    hdist.barrier(ctx)
+    hdist.sync(dev)
+    t0 = time.perf_counter()
+    for i in range(steps):
+        run(warmup + i)
+    hdist.sync(dev)
+    hdist.barrier(ctx)
+    return hdist.max_over_ranks(ctx, time.perf_counter() - t0)
+
+
+def capture_steps(step, nslots, enable):
+    """HIP-graph capture of one training step per batch slot (launch-bound inner loop)."""
+    if not enable:
+        return None
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        for i in range(3):
+            step(i)
+    torch.cuda.current_stream().wait_stream(s)
+    graphs = []
+    for j in range(nslots):
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            step(j)
+        graphs.append(g)
+    return graphs
+
+
+def bench_mlp(args, ctx):
     from har.models.mlp import MLPEngine, pad_input_bf16
     from har.parallel import dist as hdist
 
-    ctx = hdist.init(expected_world=args.gpus)
-    dev = ctx.device
-    rank, world = ctx.rank, ctx.world_size
+    dev, rank, world = ctx.device, ctx.rank, ctx.world_size
     B = args.batch
     layers = [N_FEATURES, args.hidden, args.hidden, N_CLASSES]
     eng = MLPEngine(layers, B, dev, lr=args.lr, seed=1234, process_group=ctx.group, world_size=world)
-
-    # resident per-rank training shard: 8 batches worth of windows
-    n_local = B * 8
+    n_local = B * 8  # resident per-rank shard: 8 batches of windows
     X, y = synthetic_windows(n_local, seed=100 + rank, device=dev)
     Xin = pad_input_bf16(X, eng.layout.in_pad) if eng.native else X
     y32 = y.to(torch.int32).contiguous()
@@ -83,59 +107,155 @@ def main():
         j = i % nb
         eng.train_step(Xin[j * B:(j + 1) * B], y32[j * B:(j + 1) * B], global_batch)
 
-    graph = None
-    if eng.native and args.graph:
-        # warm the allocator / kernels on a side stream, then capture one step per batch slot
-        s = torch.cuda.Stream()
-        s.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(s):
-            for i in range(3):
-                step(i)
-        torch.cuda.current_stream().wait_stream(s)
-        graphs = []
-        for j in range(nb):
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
-                step(j)
-            graphs.append(g)
-        graph = graphs
+    graphs = capture_steps(step, nb, eng.native and args.graph)
+    run = (lambda i: graphs[i % nb].replay()) if graphs else step
+    elapsed = timed(ctx, run, args.steps, args.warmup, dev)
+    Xt, yt = synthetic_windows(65536, seed=999, device=dev)
+    acc = float((torch.argmax(eng.logits(Xt), dim=1) == yt).float().mean())
+    return {"value": global_batch * args.steps / elapsed, "ms_per_step": elapsed * 1e3 / args.steps,
+            "vs_baseline": global_batch * args.steps / elapsed / BASELINE["lr"],
+            "data": "synthetic WISDM-shaped windows (43 features, 6 classes, class-conditional Gaussian); "
+                    "random-init weights",
+            "config": {"model": f"WISDM 6-class 3-layer MLP bf16 ({'-'.join(map(str, layers))})",
+                       "global_batch": global_batch, "seq_len": WINDOW_SAMPLES, "parallelism": f"dp{world}"},
+            "test_accuracy": hdist.mean_over_ranks(ctx, acc), "test_accuracy_data": "held-out synthetic windows",
+            "hip_graph": graphs is not None}
+
+
+def _featurized(n_windows, spec, dev, first_window):
+    from har.data.synth import generate_stream
+    from har.features.window import window_features
+
+    s, y = generate_stream(n_windows, spec, dev, first_window=first_window)
+    X = window_features(s, spec.window, spec.window, spec.hz)
+    return torch.nan_to_num(X, nan=-1.0), y
+
+
+def bench_rf(args, ctx, nine_axis=False):
+    from har.data.synth import StreamSpec
+    from har.models.tree import RandomForestClassifier
+    from har.parallel import data_parallel as dp
+    from har.parallel import dist as hdist
+
+    dev, rank, world = ctx.device, ctx.rank, ctx.world_size
+    K = 12 if nine_axis else N_CLASSES
+    spec = StreamSpec(num_classes=K, axes=9 if nine_axis else 3, hz=50.0 if nine_axis else 20.0,
+                      window=500 if nine_axis else 200, seed=2018)
+    n_local = args.rows
+    X, y = _featurized(n_local, spec, dev, first_window=rank * n_local)
+    if not nine_axis:
+        X = X[:, :N_FEATURES].contiguous()  # the WISDM-43 feature set
+    Xt, yt = _featurized(4096, spec, dev, first_window=10 ** 9)
+    if not nine_axis:
+        Xt = Xt[:, :N_FEATURES].contiguous()
+    est = RandomForestClassifier(numTrees=args.trees or (500 if nine_axis else 100), maxDepth=args.depth,
+                                 maxBins=32, seed=7, device=dev)
+    thr = dp.global_thresholds(X, 32, ctx, seed=7)
+    model = {}
 
     def run(i):
-        if graph is not None:
-            graph[i % nb].replay()
-        else:
-            step(i)
+        model["m"] = est.fit_tensors(X, y, K, allreduce=dp.allreduce_sum(ctx), row_offset=rank * n_local,
+                                     thresholds=thr)
 
-    for i in range(args.warmup):
-        run(i)
-    hdist.barrier(ctx)
-    hdist.sync(dev)
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        run(i)
-    hdist.sync(dev)
-    hdist.barrier(ctx)
-    elapsed = time.perf_counter() - t0
-    elapsed = hdist.max_over_ranks(ctx, elapsed)
-    ms = elapsed * 1e3 / args.steps
-    value = global_batch * args.steps / elapsed
+    elapsed = timed(ctx, run, args.steps, args.warmup, dev)
+    acc = float((model["m"].predict(Xt) == yt).float().mean())
+    rows = n_local * world
+    name = (f"Synthetic 12-class 9-axis IMU RandomForest {est.numTrees} trees depth {args.depth}" if nine_axis
+            else f"WISDM 6-class RandomForest {est.numTrees} trees depth {args.depth}")
+    return {"value": rows * args.steps / elapsed, "ms_per_step": elapsed * 1e3 / args.steps,
+            "vs_baseline": rows * args.steps / elapsed / BASELINE["rf"],
+            "data": f"synthetic {spec.axes}-axis {spec.hz:g} Hz streams featurized on device "
+                    f"({X.shape[1]} features, {K} classes)",
+            "config": {"model": name, "global_batch": rows, "seq_len": spec.window, "parallelism": f"dp{world}"},
+            "test_accuracy": hdist.mean_over_ranks(ctx, acc), "test_accuracy_data": "held-out synthetic windows",
+            "dtype": "fp32"}
 
-    # held-out accuracy (synthetic windows, rank-local; averaged)
-    Xt, yt = synthetic_windows(65536, seed=999, device=dev)
-    pred = torch.argmax(eng.logits(Xt), dim=1)
-    acc = float((pred == yt).float().mean())
-    acc = hdist.mean_over_ranks(ctx, acc)
 
-    rec = {"metric": METRIC, "value": value, "unit": "windows/s", "n_gpus": world, "steps": args.steps,
-           "warmup": args.warmup, "ms_per_step": ms, "higher_is_better": True, "scaling": "weak",
-           "vs_baseline": value / BASELINE_WINDOWS_PER_S, "dtype": "bf16",
-           "data": "synthetic WISDM-shaped windows (43 features, 6 classes, class-conditional Gaussian); "
-                   "random-init weights",
-           "config": {"model": f"WISDM 6-class 3-layer MLP bf16 ({'-'.join(map(str, layers))})",
-                      "global_batch": global_batch, "seq_len": WINDOW_SAMPLES, "parallelism": f"dp{world}"},
-           "test_accuracy": acc, "test_accuracy_data": "held-out synthetic windows",
-           "hip_graph": graph is not None, "device": torch.cuda.get_device_name(dev) if eng.native else "cpu"}
-    if rank == 0:
+def bench_stream(args, ctx):
+    from har.data.synth import StreamSpec, generate_stream
+    from har.features.window import n_features, window_features
+    from har.models.mlp import MLPEngine, pad_input_bf16
+    from har.parallel import dist as hdist
+
+    dev, rank, world = ctx.device, ctx.rank, ctx.world_size
+    spec = StreamSpec(seed=2018)
+    W = spec.window
+    B = args.batch
+    samples_local = args.samples // 8  # 1B samples per 8-GPU node: 125M per GPU (weak scaling)
+    nw_local = samples_local // W
+    stream = torch.empty(nw_local * W, 3, device=dev)
+    labels = torch.empty(nw_local, dtype=torch.long, device=dev)
+    chunk = 1 << 16
+    for c0 in range(0, nw_local, chunk):  # generate the resident shard in chunks
+        n = min(chunk, nw_local - c0)
+        s, yl = generate_stream(n, spec, dev, first_window=rank * nw_local + c0)
+        stream[c0 * W:(c0 + n) * W] = s
+        labels[c0:c0 + n] = yl
+    F = n_features(3)
+    eng = MLPEngine([F, args.hidden, args.hidden, N_CLASSES], B, dev, lr=args.lr, seed=1234,
+                    process_group=ctx.group, world_size=world)
+    feat = torch.empty(B, F, device=dev)
+    nb = nw_local // B
+    y32 = labels.to(torch.int32)
+    global_batch = B * world
+
+    def step(i):
+        j = i % nb
+        X = window_features(stream[j * B * W:(j + 1) * B * W], W, W, spec.hz)
+        feat.copy_(torch.nan_to_num(X, nan=-1.0))
+        Xb = pad_input_bf16(feat, eng.layout.in_pad)
+        eng.train_step(Xb, y32[j * B:(j + 1) * B], global_batch)
+
+    elapsed = timed(ctx, step, args.steps, args.warmup, dev)
+    Xt, yt = (lambda s_y: (torch.nan_to_num(window_features(s_y[0], W, W, spec.hz), nan=-1.0), s_y[1]))(
+        generate_stream(8192, spec, dev, first_window=10 ** 9))
+    acc = float((torch.argmax(eng.logits(Xt), 1) == yt).float().mean())
+    return {"value": global_batch * args.steps / elapsed, "ms_per_step": elapsed * 1e3 / args.steps,
+            "vs_baseline": global_batch * args.steps / elapsed / BASELINE["lr"],
+            "samples_per_s": global_batch * W * args.steps / elapsed,
+            "data": f"synthetic 3-axis 20 Hz stream, {samples_local * world / 1e9:.2f}B samples resident "
+                    f"({samples_local / 1e6:.0f}M per GPU), featurized on device each step",
+            "config": {"model": f"raw stream -> window features ({F}) -> MLP bf16 "
+                                f"({F}-{args.hidden}-{args.hidden}-{N_CLASSES})",
+                       "global_batch": global_batch, "seq_len": W, "parallelism": f"dp{world}"},
+            "test_accuracy": hdist.mean_over_ranks(ctx, acc), "test_accuracy_data": "held-out synthetic stream"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--config", default="mlp", choices=["mlp", "rf", "stream", "rf9"])
+    ap.add_argument("--batch", type=int, default=65536, help="windows per GPU per step (MLP configs)")
+    ap.add_argument("--hidden", type=int, default=256)
+    ap.add_argument("--lr", type=float, default=1e-3)
+    ap.add_argument("--graph", type=int, default=1, help="capture the MLP step in a HIP graph")
+    ap.add_argument("--rows", type=int, default=60000, help="windows per GPU (forest configs)")
+    ap.add_argument("--trees", type=int, default=0)
+    ap.add_argument("--depth", type=int, default=10)
+    ap.add_argument("--samples", type=int, default=1_000_000_000, help="stream samples per 8 GPUs")
+    ap.add_argument("--out", type=str, default="")
+    args = ap.parse_args()
+
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from har.parallel import dist as hdist
+
+    ctx = hdist.init(expected_world=args.gpus)
+    if args.config == "mlp":
+        r = bench_mlp(args, ctx)
+    elif args.config == "stream":
+        r = bench_stream(args, ctx)
+    else:
+        r = bench_rf(args, ctx, nine_axis=args.config == "rf9")
+    rec = {"metric": METRIC, "value": r.pop("value"), "unit": "windows/s", "n_gpus": ctx.world_size,
+           "steps": args.steps, "warmup": args.warmup, "ms_per_step": r.pop("ms_per_step"),
+           "higher_is_better": True, "scaling": "weak", "vs_baseline": r.pop("vs_baseline"),
+           "dtype": r.pop("dtype", "bf16"), "data": r.pop("data"), "config": r.pop("config")}
+    rec.update(r)
+    rec["bench_config"] = args.config
+    rec["device"] = torch.cuda.get_device_name(ctx.device) if ctx.device.type == "cuda" else "cpu"
+    if ctx.rank == 0:
         line = json.dumps(rec)
         print(line, flush=True)
         if args.out:

@@ -173,6 +173,13 @@ PYBIND11_MODULE(_har_native, m) {
           "philox_buckets");
   });
 
+  m.def("window_features", [](u stream, int64_t n_samples, int axes, int window, int stride, int64_t n_windows,
+                              float hz, int nbins, u out, int ld_out, u st) {
+    check(har_window_features(P<const float>(stream), n_samples, axes, window, stride, n_windows, hz, nbins,
+                              P<float>(out), ld_out, S(st)),
+          "window_features");
+  });
+
   m.def("cast_pad_bf16", [](u in, int rows, int cin, int ldin, u out, int cout, u stream) {
     check(har_cast_pad_bf16(P<const float>(in), rows, cin, ldin, P<uint16_t>(out), cout, S(stream)), "cast_pad_bf16");
   });

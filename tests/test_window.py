@@ -1,0 +1,66 @@
+"""Window featurization (K22): definitions on a hand-made window, synthetic
+streams, and the HIP kernel vs the PyTorch oracle."""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from har.data.synth import StreamSpec, generate_stream
+from har.features.window import WindowFeaturizer, feature_names, n_features, window_count, window_features_torch
+
+
+def test_feature_layout():
+    names = feature_names()
+    assert len(names) == n_features(3) == 55
+    assert names[:3] == ["X0", "X1", "X2"] and names[30:36] == ["XAVG", "YAVG", "ZAVG", "XPEAK", "YPEAK", "ZPEAK"]
+    assert names[42] == "RESULTANT"  # the WISDM-43 block comes first
+    assert len(feature_names(["AX", "AY", "AZ", "GX", "GY", "GZ", "MX", "MY", "MZ"])) == n_features(9) == 165
+
+
+def test_definitions_on_one_window():
+    W, hz = 40, 20.0
+    t = torch.arange(W, dtype=torch.float64)
+    x = torch.sin(2 * math.pi * t / 10)            # period 10 samples = 500 ms
+    y = torch.full((W,), 9.81, dtype=torch.float64)
+    z = torch.linspace(-1, 1, W, dtype=torch.float64)
+    f = window_features_torch(torch.stack([x, y, z], 1), W, W, hz)[0].double()
+    assert abs(f[30] - x.mean()) < 1e-6 and abs(f[31] - 9.81) < 1e-5
+    assert abs(f[33] - 500.0) < 1e-3               # XPEAK: mean time between peaks (ms)
+    assert math.isnan(float(f[34]))                 # constant axis: no peaks -> '?'
+    assert abs(f[36] - (x - x.mean()).abs().mean()) < 1e-6
+    assert abs(f[39] - x.std(unbiased=False)) < 1e-6
+    assert abs(f[42] - torch.sqrt(x * x + y * y + z * z).mean()) < 1e-5
+    assert abs(f[0:10].sum() - 1.0) < 1e-6 and abs(f[20:30].sum() - 1.0) < 1e-6
+    assert abs(f[52] - float(np.corrcoef(x, y)[0, 1] if y.std() > 0 else 0.0)) < 1e-6  # y constant -> 0
+
+
+def test_window_count_and_halo():
+    assert window_count(1000, 200, 200) == 5 and window_count(1000, 200, 100) == 9
+    fz = WindowFeaturizer(hz=50, seconds=10, overlap=0.5)
+    assert fz.window == 500 and fz.stride == 250 and fz.halo() == 250
+
+
+def test_synth_stream_shard_invariant():
+    spec = StreamSpec(seed=3)
+    s_all, y_all = generate_stream(12, spec)
+    s_b, y_b = generate_stream(6, spec, first_window=6)
+    assert torch.equal(y_all[6:], y_b)
+    assert s_all.shape == (12 * 200, 3)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("axes,window,stride", [(3, 200, 200), (3, 500, 250), (9, 500, 500), (6, 97, 31)])
+def test_window_kernel_matches_torch(cuda, axes, window, stride):
+    from har.features.window import window_features
+
+    spec = StreamSpec(axes=axes, window=window, seed=axes)
+    s, _ = generate_stream(64, spec)
+    s = s[: s.shape[0] - 13]  # ragged tail: last partial window dropped
+    ref = window_features_torch(s, window, stride, 50.0)
+    out = window_features(s.to(cuda), window, stride, 50.0).cpu()
+    assert out.shape == ref.shape
+    nb = 10 * axes
+    # bins: float32 vs float64 bin edges may move a boundary sample by one bin
+    assert (out[:, :nb] - ref[:, :nb]).abs().max() <= 1.0 / window + 1e-6
+    torch.testing.assert_close(out[:, nb:], ref[:, nb:], rtol=2e-4, atol=2e-4, equal_nan=True)

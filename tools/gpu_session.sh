@@ -1,8 +1,8 @@
 #!/bin/bash
-# One gpurun session: GPU tests -> 1-GPU bench -> rocprofv3 kernel stats.
+# One gpurun session: GPU tests -> benches -> rocprofv3 kernel stats.
 # Every GPU step has its own time limit; a fault / abort / timeout ends the script
 # (exit codes 124, 134, 137, 139 or >128), plain test failures (exit 1) do not.
-#   usage: gpurun --timeout 1200 -- bash tools/gpu_session.sh [tests|bench|prof|all] [extra pytest args]
+#   usage: gpurun --timeout 1200 -- bash tools/gpu_session.sh [tests|bench|benchall|prof|all] [pytest args]
 set -u
 ROOT="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 OUT="$ROOT/gpurun_out"
@@ -29,19 +29,30 @@ if [ "$WHAT" = "tests" ] || [ "$WHAT" = "all" ]; then
   fatal $rc pytest
 fi
 
-if [ "$WHAT" = "bench" ] || [ "$WHAT" = "all" ]; then
-  timeout -k 10 300 python bench.py --steps 50 --warmup 10 --out "$OUT/bench_1gpu.json" > "$OUT/bench.log" 2>&1
+if [ "$WHAT" = "bench" ] || [ "$WHAT" = "all" ] || [ "$WHAT" = "benchall" ]; then
+  timeout -k 10 300 python bench.py --steps 50 --warmup 10 --out "$OUT/bench_mlp.json" > "$OUT/bench.log" 2>&1
   rc=$?
-  tail -3 "$OUT/bench.log"
+  tail -2 "$OUT/bench.log"
   fatal $rc bench
+fi
+
+if [ "$WHAT" = "benchall" ]; then
+  for cfg in rf stream rf9; do
+    timeout -k 10 400 python bench.py --config $cfg --steps 3 --warmup 1 --out "$OUT/bench_$cfg.json" \
+        > "$OUT/bench_$cfg.log" 2>&1
+    rc=$?
+    tail -2 "$OUT/bench_$cfg.log"
+    fatal $rc "bench_$cfg"
+  done
 fi
 
 if [ "$WHAT" = "prof" ] || [ "$WHAT" = "all" ]; then
   export TMPDIR=/tmp
-  (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o bench -- \
-      python3 "$ROOT/bench.py" --steps 20 --warmup 5 --graph 0 > "$OUT/prof.log" 2>&1)
+  PCFG="${PROF_CONFIG:-mlp}"
+  (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_$PCFG" -o bench -- \
+      python3 "$ROOT/bench.py" --config "$PCFG" --steps "${PROF_STEPS:-20}" --warmup 2 --graph 0 > "$OUT/prof_$PCFG.log" 2>&1)
   rc=$?
-  tail -3 "$OUT/prof.log"
+  tail -2 "$OUT/prof_$PCFG.log"
   fatal $rc rocprof
 fi
 echo "== done" | tee -a "$OUT/session.log"
