@@ -48,11 +48,25 @@ def n_splits_for(batch: int) -> int:
     return max(1, min(64, batch // 1024))
 
 
+# Tile choices measured on MI355X with tools/gemm_bench.py (profiles/gemm_tile_sweep.md):
+# ids index ops.gemm.TILES = (BM, BN, BK).
+def fwd_tile(M: int, N: int, K: int) -> int:
+    if K <= 64:
+        return 12             # 64x128, BK 64
+    return 6 if N >= 256 else 12  # 128x256 reads each activation row once
+
+
+def dgrad_tile(M: int, N: int, K: int) -> int:
+    return 6 if N >= 256 else 12
+
+
 def wgrad_tile(M: int, N: int) -> int:
-    """Weight-gradient tiles: small output tiles so (tiles x splits) fills the chip."""
+    """Weight-gradient (split-K over the batch) tiles."""
     if M <= 32:
-        return 5 if N > 32 else 2
-    return 4
+        return 11 if N > 32 else 2   # 32x64, BK 128
+    if N <= 64:
+        return 8                     # 64x64, BK 128
+    return 9                         # 128x128, BK 64
 
 
 @dataclass
@@ -144,7 +158,7 @@ class MLPEngine:
             hmax = max(L.hidden) if L.hidden else HEAD_PAD
             self.dbuf = [torch.empty(self.B * hmax, dtype=torch.bfloat16, device=dev) for _ in range(2)]
             self.dlogits = torch.zeros(self.B, HEAD_PAD, dtype=torch.bfloat16, device=dev)
-            nblk = _native.kernels().softmax_ce_head_blocks(self.B)
+            nblk = _native.kernels().head_fused_blocks(self.B)
             self.block_loss = torch.zeros(nblk, dtype=torch.float32, device=dev)
             self.block_correct = torch.zeros(nblk, dtype=torch.int32, device=dev)
             self.dims = dims
@@ -153,6 +167,8 @@ class MLPEngine:
             # [n_splits, total] workspace laid out like the flat parameter buffer.
             self.n_splits = n_splits_for(self.B)
             self.slabs = torch.zeros(self.n_splits, L.total, dtype=torch.float32, device=dev)
+            self.n_groups = min(8, self.n_splits)  # two-level reduction: splits -> groups -> 1
+            self.partials = torch.zeros(self.n_groups, L.total, dtype=torch.float32, device=dev)
         else:
             self.t_step = 0
 
@@ -171,49 +187,66 @@ class MLPEngine:
         B = Xb.shape[0]
         if Xb.shape[1] != L.in_pad or Xb.dtype != torch.bfloat16 or B > self.B or y32.dtype != torch.int32:
             raise ValueError("bad batch")
-        ks = max(32, ((B + self.n_splits - 1) // self.n_splits + 31) // 32 * 32)
+        ks = max(128, ((B + self.n_splits - 1) // self.n_splits + 127) // 128 * 128)  # multiple of every BK
         self.active_splits = (B + ks - 1) // ks
         total = L.total
         nh = len(L.hidden)
         acts = [Xb] + [a[:B] for a in self.acts[1:]]
         for i in range(nh):
             gemm_bf16(acts[i], self._w(self.Pb, f"W{i}"), acts[i + 1], M=B, N=self.dims[i + 1], K=self.dims[i],
-                      layout=0, epi=EPI_BIAS_RELU, bias=self._w(self.P, f"b{i}"))
+                      layout=0, epi=EPI_BIAS_RELU, bias=self._w(self.P, f"b{i}"),
+                      tile=fwd_tile(B, self.dims[i + 1], self.dims[i]))
         last = acts[nh]
-        mod.softmax_ce_head(last.data_ptr(), self._w(self.Pb, "Wout").data_ptr(), self._w(self.P, "bout").data_ptr(),
-                            y32.data_ptr(), B, self.dims[-1], L.num_classes, float(scale), self.dlogits.data_ptr(),
-                            self.block_loss.data_ptr(), self.block_correct.data_ptr(), 0, s)
+        if nh == 0:
+            raise ValueError("the native MLP step needs at least one hidden layer")
+        # fused head: CE loss, dlogits, and dact of the last hidden layer = (dlogits . Wout) * relu'
+        dact = self.dbuf[(nh - 1) % 2][: B * self.dims[-1]].view(B, self.dims[-1])
+        mod.head_fused(last.data_ptr(), self._w(self.Pb, "Wout").data_ptr(), self._w(self.P, "bout").data_ptr(),
+                       y32.data_ptr(), B, self.dims[-1], L.num_classes, float(scale), self.dlogits.data_ptr(),
+                       dact.data_ptr(), self.block_loss.data_ptr(), self.block_correct.data_ptr(), s)
         self.last_batch = B
         dl = self.dlogits[:B]
         # dWout = dlogits^T . last  (+ dbout = row sums of dlogits^T)
         gemm_bf16(dl, last, self._slab("Wout"), M=HEAD_PAD, N=self.dims[-1], K=B, layout=3, epi=EPI_F32_SLAB,
                   k_split=ks, ldc=self.dims[-1], slab_stride=total, rowsum=self._slab("bout"),
                   slab_stride_rowsum=total, tile=wgrad_tile(HEAD_PAD, self.dims[-1]))
-        d, dW_in = dl, "Wout"
         for i in reversed(range(nh)):
             h = self.dims[i + 1]
-            dact = self.dbuf[i % 2][: B * h].view(B, h)
-            Wnext = self._w(self.Pb, dW_in)
-            # dact = (d . Wnext) * relu'(acts[i+1])
-            gemm_bf16(d, Wnext, dact, M=B, N=h, K=Wnext.shape[0], layout=2, epi=EPI_RELU_GRAD, mask=acts[i + 1])
             # dW_i = dact^T . acts[i]   (+ db_i = row sums of dact^T)
             gemm_bf16(dact, acts[i], self._slab(f"W{i}"), M=h, N=self.dims[i], K=B, layout=3, epi=EPI_F32_SLAB,
                       k_split=ks, ldc=self.dims[i], slab_stride=total, rowsum=self._slab(f"b{i}"),
                       slab_stride_rowsum=total, tile=wgrad_tile(h, self.dims[i]))
-            d, dW_in = dact, f"W{i}"
+            if i > 0:
+                # dact_{i-1} = (dact . W_i) * relu'(acts[i])
+                hp = self.dims[i]
+                prev = self.dbuf[(i - 1) % 2][: B * hp].view(B, hp)
+                gemm_bf16(dact, self._w(self.Pb, f"W{i}"), prev, M=B, N=hp, K=h, layout=2, epi=EPI_RELU_GRAD,
+                          mask=acts[i], tile=dgrad_tile(B, hp, h))
+                dact = prev
+
+    def _reduce_to_partials(self):
+        # the first reduction level also ticks the Adam step counter (one launch fewer per step)
+        _native.kernels().reduce_slabs_grouped(self.slabs.data_ptr(), self.active_splits, self.layout.total,
+                                               self.partials.data_ptr(), self.n_groups, _native.stream_ptr(),
+                                               self.step_count.data_ptr())
 
     def reduce_grads_native(self):
-        """G = sum of the active gradient slabs (needed before a collective)."""
-        _native.kernels().reduce_slabs(self.slabs.data_ptr(), self.active_splits, self.layout.total,
-                                       self.G.data_ptr(), _native.stream_ptr())
+        """G = sum of the active gradient slabs (two deterministic levels; needed before a collective)."""
+        self._reduce_to_partials()
+        _native.kernels().reduce_slabs_grouped(self.partials.data_ptr(), self.n_groups, self.layout.total,
+                                               self.G.data_ptr(), 1, _native.stream_ptr(), 0)
 
     def optimizer_step_native(self, from_slabs: bool):
+        """Adam; with ``from_slabs`` the slabs are first reduced to ``n_groups`` partials and the
+        last level of the reduction is fused into the Adam kernel."""
         b1, b2 = self.betas
+        if from_slabs:
+            self._reduce_to_partials()  # ticks the step counter
         _native.kernels().adam_step(self.P.data_ptr(), self.G.data_ptr(),
-                                    self.slabs.data_ptr() if from_slabs else 0, self.active_splits,
+                                    self.partials.data_ptr() if from_slabs else 0, self.n_groups,
                                     self.m.data_ptr(), self.v.data_ptr(), self.Pb.data_ptr(), self.P.numel(),
                                     float(self.lr), b1, b2, float(self.eps), float(self.wd), 1.0,
-                                    self.step_count.data_ptr(), _native.stream_ptr())
+                                    self.step_count.data_ptr(), _native.stream_ptr(), 0)
 
     def allreduce_grads(self):
         if self.world > 1:

@@ -18,7 +18,9 @@ import torch
 from . import _native
 
 EPI_F32, EPI_F32_ATOMIC, EPI_BIAS_RELU, EPI_BIAS, EPI_RELU_GRAD, EPI_BIAS_F32, EPI_F32_SLAB = range(7)
-TILES = {0: (128, 128), 1: (128, 64), 2: (128, 32), 3: (64, 128), 4: (64, 64), 5: (32, 64)}
+TILES = {0: (128, 128, 32), 1: (128, 64, 32), 2: (128, 32, 32), 3: (64, 128, 32), 4: (64, 64, 32), 5: (32, 64, 32),
+         6: (128, 256, 32), 7: (64, 256, 32), 8: (64, 64, 128), 9: (128, 128, 64), 10: (128, 256, 64),
+         11: (32, 64, 128), 12: (64, 128, 64), 13: (128, 64, 128)}  # (BM, BN, BK)
 _TARGET_BLOCKS = 1024  # >> 256 CUs, bounded split-K traffic
 
 
@@ -33,15 +35,16 @@ def auto_tile(M: int, N: int) -> int:
 
 
 def tile_counts(M: int, N: int, tile: int = -1):
-    bm, bn = TILES[auto_tile(M, N) if tile < 0 else tile]
+    bm, bn, _ = TILES[auto_tile(M, N) if tile < 0 else tile]
     return (M + bm - 1) // bm, (N + bn - 1) // bn
 
 
 def auto_k_split(M: int, N: int, K: int, tile: int = -1) -> int:
     tm, tn = tile_counts(M, N, tile)
     splits = max(1, min((K + 31) // 32, _TARGET_BLOCKS // max(1, tm * tn)))
+    bk = TILES[auto_tile(M, N) if tile < 0 else tile][2]
     ks = (K + splits - 1) // splits
-    return max(32, (ks + 31) // 32 * 32)
+    return max(bk, (ks + bk - 1) // bk * bk)
 
 
 def _check(t: torch.Tensor, name: str):

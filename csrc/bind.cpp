@@ -117,9 +117,9 @@ PYBIND11_MODULE(_har_native, m) {
   });
 
   m.def("adam_step", [](u param, u grad, u slabs, int nslabs, u mm, u vv, u pb, int64_t n, float lr, float b1,
-                        float b2, float eps, float wd, float gs, u step, u stream) {
+                        float b2, float eps, float wd, float gs, u step, u stream, int tick) {
     check(har_adam_step(P<float>(param), P<const float>(grad), P<const float>(slabs), nslabs, P<float>(mm),
-                        P<float>(vv), P<uint16_t>(pb), n, lr, b1, b2, eps, wd, gs, P<int32_t>(step), S(stream)),
+                        P<float>(vv), P<uint16_t>(pb), n, lr, b1, b2, eps, wd, gs, P<int32_t>(step), tick, S(stream)),
           "adam_step");
   });
 
@@ -178,6 +178,20 @@ PYBIND11_MODULE(_har_native, m) {
     check(har_window_features(P<const float>(stream), n_samples, axes, window, stride, n_windows, hz, nbins,
                               P<float>(out), ld_out, S(st)),
           "window_features");
+  });
+
+  m.def("head_fused_blocks", &har_head_fused_blocks);
+  m.def("head_fused", [](u H, u W, u bias, u labels, int B, int D, int C, float scale, u dlogits, u dH, u block_loss,
+                         u block_correct, u stream) {
+    check(har_head_fused(P<const uint16_t>(H), P<const uint16_t>(W), P<const float>(bias), P<const int32_t>(labels),
+                         B, D, C, scale, P<uint16_t>(dlogits), P<uint16_t>(dH), P<float>(block_loss),
+                         P<int32_t>(block_correct), S(stream)),
+          "head_fused");
+  });
+
+  m.def("reduce_slabs_grouped", [](u slabs, int S_, int64_t n, u dst, int G, u stream, u tick) {
+    check(har_reduce_slabs_grouped(P<const float>(slabs), S_, n, P<float>(dst), G, P<int32_t>(tick), S(stream)),
+          "reduce_slabs_grouped");
   });
 
   m.def("cast_pad_bf16", [](u in, int rows, int cin, int ldin, u out, int cout, u stream) {

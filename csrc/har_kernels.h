@@ -41,10 +41,22 @@ int har_softmax_ce_head_blocks(int B);
 
 // Fused Adam(W) over a flat fp32 parameter buffer; also writes the bf16 compute copy.
 // Gradient = grad[i] (if slabs == null) or sum_s slabs[s*n + i] (fused split-K reduction).
-// The step counter (*step, device int32) is incremented on the stream before the update.
+// The step counter (*step, device int32) is incremented on the stream before the update
+// (by this call when tick != 0, else by an earlier kernel such as har_reduce_slabs_grouped).
 int har_adam_step(float* param, const float* grad, const float* slabs, int nslabs, float* m, float* v,
                   uint16_t* param_bf16, int64_t n, float lr, float beta1, float beta2, float eps,
-                  float weight_decay, float grad_scale, int32_t* step, hipStream_t s);
+                  float weight_decay, float grad_scale, int32_t* step, int tick, hipStream_t s);
+
+// Fused head + last hidden layer's data gradient: logits/softmax/CE/dlogits as above plus
+// dH = (dlogits . Wout) * (H > 0) written as bf16 [B][D].  Per-workgroup partials (64 rows each).
+int har_head_fused(const uint16_t* H, const uint16_t* W, const float* bias, const int32_t* labels, int B, int D,
+                   int C, float scale, uint16_t* dlogits, uint16_t* dH, float* block_loss, int32_t* block_correct,
+                   hipStream_t s);
+int har_head_fused_blocks(int B);
+
+// dst[g*n + i] = sum of slabs[s*n + i] over the g-th group of ceil(S/G) slabs (deterministic).
+// A non-null tick is incremented once by the first workgroup (the optimizer step counter).
+int har_reduce_slabs_grouped(const float* slabs, int S, int64_t n, float* dst, int G, int32_t* tick, hipStream_t s);
 
 // dst[i] = sum_s slabs[s*n + i]  (deterministic split-K reduction)
 int har_reduce_slabs(const float* slabs, int nslabs, int64_t n, float* dst, hipStream_t s);

@@ -179,9 +179,9 @@ extern "C" int har_softmax_ce_head(const uint16_t* H, const uint16_t* W, const f
 
 extern "C" int har_adam_step(float* param, const float* grad, const float* slabs, int nslabs, float* m, float* v,
                              uint16_t* pb, int64_t n, float lr, float b1, float b2, float eps, float wd, float gs,
-                             int32_t* step, hipStream_t s) {
+                             int32_t* step, int tick, hipStream_t s) {
   if (n % 4) return -2;
-  adam_tick_kernel<<<1, 1, 0, s>>>(step);
+  if (tick) adam_tick_kernel<<<1, 1, 0, s>>>(step);
   adam_kernel<<<grid_for(n / 4), 256, 0, s>>>(param, grad, slabs, nslabs, m, v, pb, n, lr, b1, b2, eps, wd, gs,
                                               step);
   HAR_CHECK_LAUNCH();

@@ -83,7 +83,7 @@ def test_gemm_bf16_slab_rowsum(cuda, tile):
     gemm_bf16(At, Bm, slabs.view(-1), M=M, N=N, K=K, layout=3, epi=EPI_F32_SLAB, k_split=ks, ldc=N,
               slab_stride=stride, rowsum=slabs.view(-1)[M * N:], slab_stride_rowsum=stride, tile=tile)
     out = torch.empty(stride, device=cuda)
-    _native.kernels().reduce_slabs(slabs.data_ptr(), splits, stride, out.data_ptr(), _native.stream_ptr())
+    _native.kernels().reduce_slabs_grouped(slabs.data_ptr(), splits, stride, out.data_ptr(), 1, _native.stream_ptr(), 0)
     ref = At.float().T @ Bm.float()
     torch.testing.assert_close(out[: M * N].view(M, N), ref, rtol=2e-3, atol=3e-3 * K ** 0.5)
     torch.testing.assert_close(out[M * N:], At.float().sum(0), rtol=1e-3, atol=1e-2)
@@ -155,7 +155,7 @@ def test_adam_step(cuda):
     lr, b1, b2, eps, wd = 1e-2, 0.9, 0.999, 1e-8, 0.01
     for t in range(1, 4):
         _native.kernels().adam_step(p.data_ptr(), grad.data_ptr(), 0, 0, m.data_ptr(), v.data_ptr(), pb.data_ptr(),
-                                    n, lr, b1, b2, eps, wd, 1.0, step.data_ptr(), _native.stream_ptr())
+                                    n, lr, b1, b2, eps, wd, 1.0, step.data_ptr(), _native.stream_ptr(), 1)
     # reference
     pr, mr, vr = p0.double(), torch.zeros(n, dtype=torch.float64, device=cuda), torch.zeros(n, dtype=torch.float64,
                                                                                            device=cuda)
