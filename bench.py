@@ -107,7 +107,8 @@ def bench_mlp(args, ctx):
         j = i % nb
         eng.train_step(Xin[j * B:(j + 1) * B], y32[j * B:(j + 1) * B], global_batch)
 
-    graphs = capture_steps(step, nb, eng.native and args.graph)
+    use_graph = args.graph == 1 or (args.graph < 0 and world == 1)
+    graphs = capture_steps(step, nb, eng.native and use_graph)
     run = (lambda i: graphs[i % nb].replay()) if graphs else step
     elapsed = timed(ctx, run, args.steps, args.warmup, dev)
     Xt, yt = synthetic_windows(65536, seed=999, device=dev)
@@ -230,7 +231,9 @@ def main():
     ap.add_argument("--batch", type=int, default=65536, help="windows per GPU per step (MLP configs)")
     ap.add_argument("--hidden", type=int, default=256)
     ap.add_argument("--lr", type=float, default=1e-3)
-    ap.add_argument("--graph", type=int, default=1, help="capture the MLP step in a HIP graph")
+    ap.add_argument("--graph", type=int, default=-1,
+                    help="capture the MLP step in a HIP graph (default: on for 1 GPU; multi-GPU steps with the "
+                         "RCCL all-reduce run eager unless --graph 1)")
     ap.add_argument("--rows", type=int, default=60000, help="windows per GPU (forest configs)")
     ap.add_argument("--trees", type=int, default=0)
     ap.add_argument("--depth", type=int, default=10)
