@@ -97,11 +97,17 @@ def parse_csv_bytes(buf: bytes, header: bool = True, use_native: Optional[bool] 
 
 
 def read_csv(path: str, header: bool = True, infer_schema: bool = True,
-             use_native: Optional[bool] = None) -> Table:
-    """Load a CSV file into a columnar :class:`Table`."""
-    with open(path, "rb") as f:
-        buf = f.read()
-    t = parse_csv_bytes(buf, header=header, use_native=use_native)
+             use_native: Optional[bool] = None, device=None) -> Table:
+    """Load a CSV file into a columnar :class:`Table`.  ``device="cuda"`` parses on the
+    GPU (``har.data.csv_device``: HIP line index + field parse + dictionary encoding)."""
+    if device is not None and str(device).startswith("cuda"):
+        from .csv_device import read_csv_device
+
+        t = read_csv_device(path, device=device, header=header).to_table()
+    else:
+        with open(path, "rb") as f:
+            buf = f.read()
+        t = parse_csv_bytes(buf, header=header, use_native=use_native)
     if not infer_schema:  # Spark without inferSchema: every column is a string
         t = Table([Column(c.name, "string", np.asarray([c.cell_str(i) for i in range(len(c))], dtype=object))
                    for c in (t[n] for n in t.columns)])

@@ -94,15 +94,19 @@ class ForestBuilder:
         self.allreduce = allreduce  # optional callable(tensor) -> None (DP histogram reduction)
 
     def prepare(self, X: torch.Tensor, thresholds=None):
-        Xh = X.detach().float().cpu().numpy()
-        self.thresholds = thresholds if thresholds is not None else T.find_thresholds(Xh, self.max_bins, seed=self.seed)
-        F = Xh.shape[1]
+        from ..ops.stats import bin_features
+
+        if thresholds is None:
+            Xh = X.detach().float().cpu().numpy()
+            thresholds = T.find_thresholds(Xh, self.max_bins, seed=self.seed)
+        self.thresholds = thresholds
+        F = X.shape[1]
         self.nbins = torch.tensor([len(t) + 1 for t in self.thresholds], dtype=torch.int32, device=X.device)
         thr_mat = np.full((F, self.max_bins), np.inf, dtype=np.float32)
         for f, t in enumerate(self.thresholds):
             thr_mat[f, : len(t)] = t
         self.thr_mat = torch.from_numpy(thr_mat).to(X.device)
-        self.bins = torch.from_numpy(T.bin_features(Xh, self.thresholds)).to(X.device)  # [F, N]
+        self.bins = bin_features(X, self.thresholds).to(X.device)  # [F, N] uint8 (HIP kernel on the GPU)
 
     def bootstrap_weights(self, N: int, device, row_offset: int = 0) -> torch.Tensor:
         if not self.bootstrap:

@@ -194,6 +194,33 @@ PYBIND11_MODULE(_har_native, m) {
           "reduce_slabs_grouped");
   });
 
+  m.def("column_stats_workspace", &har_column_stats_workspace);
+  m.def("column_stats", [](u X, int64_t n, int ncols, int ld, u w, u stats, u ws, u stream) {
+    check(har_column_stats(P<const float>(X), n, ncols, ld, P<const float>(w), P<double>(stats), P<double>(ws),
+                           S(stream)),
+          "column_stats");
+  });
+  m.def("bin_features", [](u X, int64_t n, int F, int ld, u thr, int maxb, u nthr, u bins, u stream) {
+    check(har_bin_features(P<const float>(X), n, F, ld, P<const float>(thr), maxb, P<const int32_t>(nthr),
+                           P<uint8_t>(bins), S(stream)),
+          "bin_features");
+  });
+
+  m.def("csv_count_newlines", [](u buf, int64_t n, u counts, u stream) {
+    check(har_csv_count_newlines(P<const uint8_t>(buf), n, P<int32_t>(counts), S(stream)), "csv_count_newlines");
+  });
+  m.def("csv_newline_pos", [](u buf, int64_t n, u block_off, u pos, u stream) {
+    check(har_csv_newline_pos(P<const uint8_t>(buf), n, P<const int64_t>(block_off), P<int64_t>(pos), S(stream)),
+          "csv_newline_pos");
+  });
+  m.def("csv_parse_rows", [](u buf, u starts, u ends, int64_t nrows, int ncols, u vals, u hashes, u flags, u fstart,
+                             u flen, u stream) {
+    check(har_csv_parse_rows(P<const uint8_t>(buf), P<const int64_t>(starts), P<const int64_t>(ends), nrows, ncols,
+                             P<double>(vals), P<uint64_t>(hashes), P<uint8_t>(flags), P<int64_t>(fstart),
+                             P<int32_t>(flen), S(stream)),
+          "csv_parse_rows");
+  });
+
   m.def("cast_pad_bf16", [](u in, int rows, int cin, int ldin, u out, int cout, u stream) {
     check(har_cast_pad_bf16(P<const float>(in), rows, cin, ldin, P<uint16_t>(out), cout, S(stream)), "cast_pad_bf16");
   });

@@ -72,9 +72,14 @@ int har_poisson_bootstrap(uint64_t seed, int tree0, int ntrees, int64_t row0, in
                           hipStream_t s);
 
 // ---- statistics / metrics ----
-// Column count/sum/sumsq/min/max (masked by optional row weights) -> stats[5][ncols] (double).
+// Column count/sum/sumsq/min/max (optional row weights, NaN skipped) -> stats[5][ncols] (double);
+// workspace: har_column_stats_workspace(n, ncols) doubles.
 int har_column_stats(const float* X, int64_t n, int ncols, int ld, const float* w, double* stats,
-                     hipStream_t s);
+                     double* workspace, hipStream_t s);
+int64_t har_column_stats_workspace(int64_t n, int ncols);
+// bins[f][i] = #{b < nthr[f] : thr[f][b] < X[i][f]}  (uint8, feature-major)
+int har_bin_features(const float* X, int64_t n, int F, int ld, const float* thr, int maxb, const int32_t* nthr,
+                     uint8_t* bins, hipStream_t s);
 int har_confusion_matrix(const int32_t* label, const int32_t* pred, int64_t n, int K, int64_t* cm,
                          hipStream_t s);
 int har_regression_moments(const float* y, const float* yhat, int64_t n, double* out6, hipStream_t s);
@@ -103,8 +108,14 @@ int har_forest_predict(const float* X, int64_t n, int F, int ld, const int32_t* 
                        const int32_t* left, const int32_t* right, const float* leaf, int ntrees, int maxn, int K,
                        int max_depth, int normalize, float* raw_out, hipStream_t s);
 
-// ---- CSV on device ----
-int har_csv_count_lines(const uint8_t* buf, int64_t n, int64_t* block_counts, int nblocks, hipStream_t s);
+// ---- CSV on device (4 KiB chunks per workgroup) ----
+int har_csv_count_newlines(const uint8_t* buf, int64_t n, int32_t* counts, hipStream_t s);
+int har_csv_newline_pos(const uint8_t* buf, int64_t n, const int64_t* block_off, int64_t* pos, hipStream_t s);
+// Per (col, row) outputs ([ncols][nrows]): fp64 value (NaN if not numeric), FNV-1a hash,
+// flags (bit0 present, bit1 int literal, bit2 float literal, bit3 quoted), byte span.
+int har_csv_parse_rows(const uint8_t* buf, const int64_t* starts, const int64_t* ends, int64_t nrows, int ncols,
+                       double* vals, uint64_t* hashes, uint8_t* flags, int64_t* fstart, int32_t* flen,
+                       hipStream_t s);
 
 #ifdef __cplusplus
 }

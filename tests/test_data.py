@@ -123,3 +123,23 @@ def test_random_split_wisdm_sizes(wisdm_csv):
     tr, te = random_split(t, [0.7, 0.3], 2018)
     assert tr.count() + te.count() == 5418
     assert abs(tr.count() - 3793) < 120  # Spark's own draw gave 3793 / 1625
+
+
+@pytest.mark.gpu
+def test_device_csv_matches_host(cuda, wisdm_csv, tmp_path):
+    from har.data.csv_device import read_csv_device
+
+    for path in (wisdm_csv, None):
+        if path is None:
+            path = str(tmp_path / "s.csv")
+            with open(path, "wb") as f:
+                f.write(SAMPLE + b"4,5e2,zz,\"\",7\n\n")
+        host = read_csv(path, use_native=True)  # native host parser: quoted "" is a present empty string
+        dev = read_csv_device(path, cuda).to_table()
+        assert dev.columns == host.columns and dev.count() == host.count()
+        for c in host.columns:
+            assert dev[c].kind == host[c].kind, c
+            if host[c].kind == "double":
+                np.testing.assert_array_equal(dev[c].data, host[c].data)
+            else:
+                assert list(dev[c].data) == list(host[c].data), c

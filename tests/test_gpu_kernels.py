@@ -252,3 +252,19 @@ def test_metrics_kernels(cuda):
     assert n == 10001
     assert abs(se - float((d * d).sum())) < 1e-6 and abs(ae - float(d.abs().sum())) < 1e-6
     assert abs(sy - float(y.double().sum())) < 1e-6
+
+
+def test_column_stats_and_binning(cuda):
+    from har.ops import stats
+    from har.ops import tree as T
+
+    g = torch.Generator(device=cuda).manual_seed(12)
+    X = torch.randn(3001, 37, device=cuda, generator=g)
+    X[5, 3] = float("nan")
+    w = (torch.rand(3001, device=cuda, generator=g) > 0.3).float()
+    st = stats.column_stats(X, w)
+    ref = stats.column_stats(X.cpu(), w.cpu())
+    torch.testing.assert_close(st.cpu(), ref, rtol=1e-9, atol=1e-7)
+    thr = T.find_thresholds(X.cpu().numpy(), 32)
+    b = stats.bin_features(X, thr).cpu()
+    assert torch.equal(b, torch.from_numpy(T.bin_features(X.cpu().numpy(), thr)))
