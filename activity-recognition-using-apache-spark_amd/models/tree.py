@@ -174,9 +174,10 @@ class ForestBuilder:
             starts = (torch.cumsum(counts, 0) - counts).to(torch.int32)
             feats = torch.from_numpy(rng.feature_subsets(self.seed, ct, cn, F, m)).to(dev)
             # ---- histogram + best split ----
-            if use_native and self.allreduce is None:
+            if use_native:
                 res = T.hist_split_native(self.bins, self.nbins, y32, rows, row_w, starts, counts, feats, K,
-                                          self.max_bins, self.min_inst, self.min_gain, self.impurity)
+                                          self.max_bins, self.min_inst, self.min_gain, self.impurity,
+                                          allreduce=self.allreduce)
             else:
                 hist = T.level_histogram(self.bins, y32, rows, row_w, keys, A, feats, K, self.max_bins)
                 if self.allreduce is not None:

@@ -135,7 +135,10 @@ def split_from_hist(hist, feats, nbins_feat, min_instances, min_info_gain, impur
 
 
 def hist_split_native(bins, nbins_feat, label, rows, row_w, node_start, node_count, feats, K, max_bins,
-                      min_instances, min_info_gain, impurity) -> LevelResult:
+                      min_instances, min_info_gain, impurity, allreduce=None) -> LevelResult:
+    """Fused LDS histogram + split on one device; with ``allreduce`` (data parallel) the
+    kernel runs twice: histogram-only into a [A, m, bins, K] buffer, one RCCL all-reduce
+    of it, then split search from the summed histograms."""
     A, m = feats.shape
     F, N = bins.shape
     fc = max(1, min(m, LDS_BUDGET // (max_bins * K * 4)))
@@ -146,13 +149,20 @@ def hist_split_native(bins, nbins_feat, label, rows, row_w, node_start, node_cou
     bin_ = torch.empty(A * chunks, dtype=torch.int32, device=dev)
     left = torch.empty(A * chunks, K, dtype=torch.float32, device=dev)
     total = torch.empty(A, K, dtype=torch.float32, device=dev)
-    if int(label.max()) >= K or int(label.min()) < 0:
+    if label.numel() and (int(label.max()) >= K or int(label.min()) < 0):
         raise ValueError("labels out of range")
-    _native.kernels().tree_hist_split(bins.data_ptr(), N, F, nbins_feat.data_ptr(), rows.data_ptr(),
-                                      row_w.data_ptr(), node_start.data_ptr(), node_count.data_ptr(), A,
-                                      feats.data_ptr(), m, fc, label.data_ptr(), K, max_bins, float(min_instances),
-                                      float(min_info_gain), impurity, gain.data_ptr(), feat.data_ptr(),
-                                      bin_.data_ptr(), left.data_ptr(), total.data_ptr(), _native.stream_ptr())
+    mod = _native.kernels()
+    args = [bins.data_ptr(), N, F, nbins_feat.data_ptr(), rows.data_ptr(), row_w.data_ptr(), node_start.data_ptr(),
+            node_count.data_ptr(), A, feats.data_ptr(), m, fc, label.data_ptr(), K, max_bins, float(min_instances),
+            float(min_info_gain), impurity, gain.data_ptr(), feat.data_ptr(), bin_.data_ptr(), left.data_ptr(),
+            total.data_ptr()]
+    if allreduce is None:
+        mod.tree_hist_split(*args, 0, 0, _native.stream_ptr())
+    else:
+        ghist = torch.empty(A, m, max_bins, K, dtype=torch.float32, device=dev)
+        mod.tree_hist_split(*args, 1, ghist.data_ptr(), _native.stream_ptr())
+        allreduce(ghist)
+        mod.tree_hist_split(*args, 2, ghist.data_ptr(), _native.stream_ptr())
     gain, feat, bin_, left = gain.view(A, chunks), feat.view(A, chunks), bin_.view(A, chunks), left.view(A, chunks, K)
     best = torch.argmax(gain, dim=1)  # first max -> lowest chunk (lowest feature slot) on ties
     ar = torch.arange(A, device=dev)

@@ -181,6 +181,12 @@ CsvResult parse_csv(const char* data, size_t size, bool header, int num_threads)
           for (int j = 0; j < ncol; ++j) {
             if (j >= nf || f[j].len == 0) {
               res.missing[j][r] = 1;
+              if (j < nf && f[j].quoted) {  // "" : a present, empty string (makes the column a string)
+                quoted[(size_t)j * nrows + r] = 1;
+                res.spans[(size_t)j * nrows + r] = {f[j].off, 0};
+                any_nonempty[t][j] = 1;
+                votes[t][j] |= 3;
+              }
               continue;
             }
             const char* p = data + f[j].off;

@@ -40,7 +40,9 @@ __global__ __launch_bounds__(256) void tree_hist_split_kernel(
     const int32_t* __restrict__ node_count, const int32_t* __restrict__ feats, int m, int fc,
     const int32_t* __restrict__ label, int K, int maxbins, float min_inst, float min_gain, int impurity,
     float* __restrict__ out_gain, int32_t* __restrict__ out_feat, int32_t* __restrict__ out_bin,
-    float* __restrict__ out_left, float* __restrict__ out_total) {
+    float* __restrict__ out_left, float* __restrict__ out_total, int mode, float* __restrict__ ghist) {
+  // mode 0: fused histogram + split; 1: histogram only -> ghist [A][m][maxbins][K] (data parallel:
+  // summed across ranks by RCCL); 2: split search from a (reduced) ghist
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int a = blockIdx.y, c = blockIdx.x, chunks = gridDim.x;
   const int f_lo = c * fc;
@@ -52,12 +54,13 @@ __global__ __launch_bounds__(256) void tree_hist_split_kernel(
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int start = node_start[a], cnt = node_count[a];
 
-  for (int i = tid; i < f_n * maxbins * K; i += blockDim.x) hist[i] = 0.f;
+  float* gh = ghist ? ghist + ((size_t)a * m + f_lo) * maxbins * K : nullptr;
+  for (int i = tid; i < f_n * maxbins * K; i += blockDim.x) hist[i] = (mode == 2) ? gh[i] : 0.f;
   for (int i = tid; i < f_n; i += blockDim.x) fid[i] = feats[(size_t)a * m + f_lo + i];
   __syncthreads();
 
   // ---- histogram: (feature slot, row) pairs, rows fastest -> coalesced bin reads ----
-  const int64_t pairs = (int64_t)cnt * f_n;
+  const int64_t pairs = mode == 2 ? 0 : (int64_t)cnt * f_n;
   for (int64_t j = tid; j < pairs; j += blockDim.x) {
     const int fs = (int)(j / cnt);
     const int ri = (int)(j - (int64_t)fs * cnt);
@@ -67,6 +70,10 @@ __global__ __launch_bounds__(256) void tree_hist_split_kernel(
     atomicAdd(&hist[(fs * maxbins + b) * K + label[r]], w);
   }
   __syncthreads();
+  if (mode == 1) {
+    for (int i = tid; i < f_n * maxbins * K; i += blockDim.x) gh[i] = hist[i];
+    return;
+  }
 
   // ---- split search: one wave per feature slot, one lane per bin ----
   double best_g = -INFINITY;
@@ -186,8 +193,9 @@ extern "C" int har_tree_hist_split(const uint8_t* bins, int64_t N, int F, const 
                                    const int32_t* node_count, int A, const int32_t* feats, int m, int fc,
                                    const int32_t* label, int K, int maxbins, float min_inst, float min_gain,
                                    int impurity, float* out_gain, int32_t* out_feat, int32_t* out_bin,
-                                   float* out_left, float* out_total, hipStream_t s) {
+                                   float* out_left, float* out_total, int mode, float* ghist, hipStream_t s) {
   if (K > KMAX || maxbins > 64 || fc <= 0 || m <= 0) return -2;
+  if (mode != 0 && !ghist) return -4;
   if (A == 0) return 0;
   const int chunks = (m + fc - 1) / fc;
   const size_t lds = (size_t)fc * maxbins * K * sizeof(float) + (size_t)fc * sizeof(int);
@@ -195,7 +203,7 @@ extern "C" int har_tree_hist_split(const uint8_t* bins, int64_t N, int F, const 
   dim3 grid(chunks, A);
   tree_hist_split_kernel<<<grid, 256, lds, s>>>(bins, N, nbins_feat, rows, row_w, node_start, node_count, feats, m,
                                                 fc, label, K, maxbins, min_inst, min_gain, impurity, out_gain,
-                                                out_feat, out_bin, out_left, out_total);
+                                                out_feat, out_bin, out_left, out_total, mode, ghist);
   HAR_CHECK_LAUNCH();
   return 0;
 }

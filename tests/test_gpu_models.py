@@ -60,6 +60,12 @@ def test_hist_split_native_matches_torch(cuda):
     torch.testing.assert_close(nat.gain, ref.gain, rtol=1e-5, atol=1e-6)
     assert torch.equal(nat.feat, ref.feat) and torch.equal(nat.bin, ref.bin)
     torch.testing.assert_close(nat.left, ref.left)
+    # data-parallel form: histogram-only pass, (identity) all-reduce, split pass == fused kernel
+    two = T.hist_split_native(bins, nbins, y32, rows, w, starts, counts, feats, 5, 32, 1.0, 0.0, T.GINI,
+                              allreduce=lambda t: None)
+    assert torch.equal(two.feat, nat.feat) and torch.equal(two.bin, nat.bin)
+    torch.testing.assert_close(two.gain, nat.gain)
+    torch.testing.assert_close(two.total, nat.total)
 
 
 def test_forest_predict_native_matches_torch(cuda):
