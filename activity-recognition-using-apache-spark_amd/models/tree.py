@@ -188,11 +188,11 @@ class ForestBuilder:
             if not ds.any():
                 break
             st_t, st_n = ct[ds], cn[ds]
-            # allocate children: per tree, consecutive ids
-            child_l = np.empty(len(st_t), dtype=np.int64)
-            for i, t in enumerate(st_t):
-                child_l[i] = n_nodes[t]
-                n_nodes[t] += 2
+            # allocate children: per tree, consecutive ids (the frontier stays grouped by tree,
+            # so a node's rank inside its tree is its offset from the tree's first entry)
+            rank_in_tree = np.arange(len(st_t)) - np.searchsorted(st_t, st_t, side="left")
+            child_l = n_nodes[st_t] + 2 * rank_in_tree
+            n_nodes += 2 * np.bincount(st_t, minlength=Tn)
             ti = torch.as_tensor(st_t, device=dev)
             ni = torch.as_tensor(st_n, device=dev)
             cl = torch.as_tensor(child_l, device=dev)

@@ -156,13 +156,22 @@ def hist_split_native(bins, nbins_feat, label, rows, row_w, node_start, node_cou
             node_count.data_ptr(), A, feats.data_ptr(), m, fc, label.data_ptr(), K, max_bins, float(min_instances),
             float(min_info_gain), impurity, gain.data_ptr(), feat.data_ptr(), bin_.data_ptr(), left.data_ptr(),
             total.data_ptr()]
-    if allreduce is None:
-        mod.tree_hist_split(*args, 0, 0, _native.stream_ptr())
+    # few large nodes (the top levels): split every node's rows over several workgroups so the
+    # launch still fills 256 CUs; their LDS histograms merge into a global one
+    blocks = A * chunks
+    max_rows = int(node_count.max()) if A else 0
+    row_chunks = 1
+    if blocks < 1024 and max_rows > 4096:
+        row_chunks = int(min((1024 + blocks - 1) // blocks, (max_rows + 2047) // 2048))
+    st = _native.stream_ptr()
+    if allreduce is None and row_chunks == 1:
+        mod.tree_hist_split(*args, 0, 0, 1, st)
     else:
-        ghist = torch.empty(A, m, max_bins, K, dtype=torch.float32, device=dev)
-        mod.tree_hist_split(*args, 1, ghist.data_ptr(), _native.stream_ptr())
-        allreduce(ghist)
-        mod.tree_hist_split(*args, 2, ghist.data_ptr(), _native.stream_ptr())
+        ghist = (torch.zeros if row_chunks > 1 else torch.empty)(A, m, max_bins, K, dtype=torch.float32, device=dev)
+        mod.tree_hist_split(*args, 1, ghist.data_ptr(), row_chunks, st)
+        if allreduce is not None:
+            allreduce(ghist)
+        mod.tree_hist_split(*args, 2, ghist.data_ptr(), 1, st)
     gain, feat, bin_, left = gain.view(A, chunks), feat.view(A, chunks), bin_.view(A, chunks), left.view(A, chunks, K)
     best = torch.argmax(gain, dim=1)  # first max -> lowest chunk (lowest feature slot) on ties
     ar = torch.arange(A, device=dev)

@@ -98,13 +98,14 @@ int har_window_features(const float* stream, int64_t n_samples, int axes, int wi
 // rows/row_w list each node's rows contiguously (node_start/node_count); feats [A][m].
 // Outputs per (node, chunk): gain (-inf = none), global feature, bin, left class counts [K];
 // out_total [A][K] = node class counts.  mode 0 fused; 1 histogram only -> ghist [A][m][maxbins][K];
-// 2 split search from ghist (after a cross-rank reduction).
+// 2 split search from ghist (after a cross-rank reduction).  row_chunks > 1 (mode 1 only): each node's
+// rows are split over that many workgroups that atomically merge into a ZEROED ghist.
 int har_tree_hist_split(const uint8_t* bins, int64_t N, int F, const int32_t* nbins_feat, const int32_t* rows,
                         const float* row_w, const int32_t* node_start, const int32_t* node_count, int A,
                         const int32_t* feats, int m, int fc, const int32_t* label, int K, int maxbins,
                         float min_inst, float min_gain, int impurity, float* out_gain, int32_t* out_feat,
                         int32_t* out_bin, float* out_left, float* out_total, int mode, float* ghist,
-                        hipStream_t s);
+                        int row_chunks, hipStream_t s);
 // Sum over trees of (normalized) leaf statistics; trees as SoA [T][maxn] arrays, feature < 0 = leaf.
 int har_forest_predict(const float* X, int64_t n, int F, int ld, const int32_t* feat, const float* thr,
                        const int32_t* left, const int32_t* right, const float* leaf, int ntrees, int maxn, int K,

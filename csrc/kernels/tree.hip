@@ -52,7 +52,11 @@ __global__ __launch_bounds__(256) void tree_hist_split_kernel(
   __shared__ double red_gain[4];
   __shared__ int red_idx[4];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int start = node_start[a], cnt = node_count[a];
+  // grid.z > 1 (histogram-only mode): the node's rows are split over gridDim.z workgroups
+  const int cnt_all = node_count[a];
+  const int per_z = (cnt_all + gridDim.z - 1) / gridDim.z;
+  const int zb = min(cnt_all, (int)blockIdx.z * per_z);
+  const int start = node_start[a] + zb, cnt = min(cnt_all, zb + per_z) - zb;
 
   float* gh = ghist ? ghist + ((size_t)a * m + f_lo) * maxbins * K : nullptr;
   for (int i = tid; i < f_n * maxbins * K; i += blockDim.x) hist[i] = (mode == 2) ? gh[i] : 0.f;
@@ -71,7 +75,12 @@ __global__ __launch_bounds__(256) void tree_hist_split_kernel(
   }
   __syncthreads();
   if (mode == 1) {
-    for (int i = tid; i < f_n * maxbins * K; i += blockDim.x) gh[i] = hist[i];
+    if (gridDim.z == 1) {
+      for (int i = tid; i < f_n * maxbins * K; i += blockDim.x) gh[i] = hist[i];
+    } else {  // row-split node: merge into the zeroed global histogram (integer-valued sums: exact)
+      for (int i = tid; i < f_n * maxbins * K; i += blockDim.x)
+        if (hist[i] != 0.f) atomicAdd(gh + i, hist[i]);
+    }
     return;
   }
 
@@ -193,14 +202,16 @@ extern "C" int har_tree_hist_split(const uint8_t* bins, int64_t N, int F, const 
                                    const int32_t* node_count, int A, const int32_t* feats, int m, int fc,
                                    const int32_t* label, int K, int maxbins, float min_inst, float min_gain,
                                    int impurity, float* out_gain, int32_t* out_feat, int32_t* out_bin,
-                                   float* out_left, float* out_total, int mode, float* ghist, hipStream_t s) {
+                                   float* out_left, float* out_total, int mode, float* ghist, int row_chunks,
+                                   hipStream_t s) {
   if (K > KMAX || maxbins > 64 || fc <= 0 || m <= 0) return -2;
   if (mode != 0 && !ghist) return -4;
   if (A == 0) return 0;
   const int chunks = (m + fc - 1) / fc;
   const size_t lds = (size_t)fc * maxbins * K * sizeof(float) + (size_t)fc * sizeof(int);
   if (lds > 150 * 1024) return -3;
-  dim3 grid(chunks, A);
+  if (row_chunks > 1 && mode != 1) return -5;
+  dim3 grid(chunks, A, row_chunks > 1 ? row_chunks : 1);
   tree_hist_split_kernel<<<grid, 256, lds, s>>>(bins, N, nbins_feat, rows, row_w, node_start, node_count, feats, m,
                                                 fc, label, K, maxbins, min_inst, min_gain, impurity, out_gain,
                                                 out_feat, out_bin, out_left, out_total, mode, ghist);
