@@ -265,6 +265,21 @@ class MLPEngine:
         else:
             self.train_step_torch(Xb, yb, global_batch)
 
+    def state_tensors(self):
+        """Everything needed to resume training bit-for-bit."""
+        step = self.step_count.clone() if self.native else torch.tensor([self.t_step], dtype=torch.int32)
+        return {"P": self.P, "m": self.m, "v": self.v, "step": step}
+
+    def load_state(self, st):
+        self.P.copy_(st["P"].to(self.P.device))
+        self.m.copy_(st["m"].to(self.m.device))
+        self.v.copy_(st["v"].to(self.v.device))
+        if self.native:
+            self.step_count.copy_(st["step"].to(self.step_count.device))
+            self.Pb.copy_(self.P.to(torch.bfloat16))
+        else:
+            self.t_step = int(st["step"][0])
+
     def last_loss_and_correct(self):
         """(sum of CE, #correct) of the last native batch — one host sync."""
         return float(self.block_loss.sum().item()), int(self.block_correct.sum().item())
@@ -366,16 +381,19 @@ class MultilayerPerceptronClassificationModel(ClassificationModel):
 class MultilayerPerceptronClassifier(Estimator, ClassifierParams):
     """``layers=[in, h1, ..., out]``; ``maxIter`` = epochs; ``blockSize`` = per-rank batch."""
 
-    _param_names = ("layers", "maxIter", "blockSize", "stepSize", "seed", "standardize", "device", "weightDecay")
+    _param_names = ("layers", "maxIter", "blockSize", "stepSize", "seed", "standardize", "device", "weightDecay",
+                    "checkpointDir", "checkpointInterval")
 
     def __init__(self, layers: Optional[Sequence[int]] = None, maxIter: int = 100, blockSize: int = 1024,
                  stepSize: float = 1e-3, seed: int = 0, standardize: bool = True, featuresCol="features",
-                 labelCol="label", device=None, weightDecay: float = 0.0):
+                 labelCol="label", device=None, weightDecay: float = 0.0, checkpointDir: Optional[str] = None,
+                 checkpointInterval: int = 0):
         super().__init__(new_uid("MultilayerPerceptronClassifier"))
         self.layers = list(layers) if layers else None
         self.maxIter, self.blockSize, self.stepSize, self.seed = maxIter, blockSize, stepSize, seed
         self.standardize, self.featuresCol, self.labelCol, self.device = standardize, featuresCol, labelCol, device
         self.weightDecay = weightDecay
+        self.checkpointDir, self.checkpointInterval = checkpointDir, checkpointInterval
 
     def fit(self, table: Table) -> MultilayerPerceptronClassificationModel:
         dev = resolve_device(self.device)
@@ -430,12 +448,31 @@ class MultilayerPerceptronClassifier(Estimator, ClassifierParams):
             st = torch.tensor([steps_per_epoch], device=dev)
             dist.all_reduce(st, op=dist.ReduceOp.MIN, group=process_group)
             steps_per_epoch = int(st.item())
-        g = torch.Generator(device="cpu").manual_seed(self.seed + 7919 * rank)
-        for epoch in range(self.maxIter):
+        ckpt = None
+        start_epoch, start_step = 0, 0
+        if self.checkpointDir:
+            from ..utils.checkpoint import Checkpointer
+
+            ckpt = Checkpointer(self.checkpointDir, rank=rank)
+            last = ckpt.latest()
+            if last is not None:  # resume: parameters, Adam moments, step counter, data position
+                state, meta = last
+                eng.load_state(state)
+                start_epoch, start_step = int(meta["epoch"]), int(meta["step_in_epoch"])
+        from ..utils.checkpoint import maybe_inject_fault
+
+        for epoch in range(start_epoch, self.maxIter):
+            # data order is a pure function of (seed, rank, epoch): resumable without RNG state
+            g = torch.Generator(device="cpu").manual_seed(self.seed + 7919 * rank + 104729 * epoch)
             perm = torch.randperm(N, generator=g).to(dev)
             Xe, ye = Xin[perm].contiguous(), y32[perm].contiguous()
-            for s in range(steps_per_epoch):
+            for s in range(start_step if epoch == start_epoch else 0, steps_per_epoch):
+                gstep = epoch * steps_per_epoch + s
+                maybe_inject_fault(gstep, rank)
                 eng.train_step(Xe[s * B:(s + 1) * B], ye[s * B:(s + 1) * B], global_batch)
+                if ckpt is not None and self.checkpointInterval and (gstep + 1) % self.checkpointInterval == 0:
+                    nxt_e, nxt_s = (epoch, s + 1) if s + 1 < steps_per_epoch else (epoch + 1, 0)
+                    ckpt.save(gstep + 1, eng.state_tensors(), {"epoch": nxt_e, "step_in_epoch": nxt_s})
         model = MultilayerPerceptronClassificationModel(eng, uid=self.uid)
         model.mean, model.inv_std = mean, inv_std
         return model

@@ -82,7 +82,7 @@ class ForestBuilder:
     def __init__(self, num_classes: int, num_trees: int = 1, max_depth: int = 5, max_bins: int = 32,
                  min_instances: int = 1, min_info_gain: float = 0.0, impurity: str = "gini",
                  feature_subset: str = "auto", bootstrap: Optional[bool] = None, seed: int = 0,
-                 allreduce=None):
+                 allreduce=None, tree_offset: int = 0):
         if max_bins > 64:
             raise ValueError("maxBins <= 64 (one lane per bin in the split kernel)")
         self.K, self.T, self.D = num_classes, num_trees, max_depth
@@ -92,6 +92,7 @@ class ForestBuilder:
         self.bootstrap = (num_trees > 1) if bootstrap is None else bootstrap
         self.seed = seed
         self.allreduce = allreduce  # optional callable(tensor) -> None (DP histogram reduction)
+        self.tree_offset = tree_offset  # global id of tree 0 (bootstrap / feature-subset streams)
 
     def prepare(self, X: torch.Tensor, thresholds=None):
         from ..ops.stats import bin_features
@@ -113,10 +114,11 @@ class ForestBuilder:
             return torch.ones(self.T, N, dtype=torch.float32, device=device)
         if device.type == "cuda":
             w = torch.empty(self.T, N, dtype=torch.uint8, device=device)
-            _native.kernels().poisson_bootstrap(self.seed, 0, self.T, row_offset, N, w.data_ptr(),
+            _native.kernels().poisson_bootstrap(self.seed, self.tree_offset, self.T, row_offset, N, w.data_ptr(),
                                                 _native.stream_ptr())
             return w.float()
-        return torch.from_numpy(rng.poisson1_weights(self.seed, range(self.T), N, row_offset)).float()
+        return torch.from_numpy(rng.poisson1_weights(self.seed, range(self.tree_offset, self.tree_offset + self.T),
+                                                     N, row_offset)).float()
 
     def fit(self, X: torch.Tensor, y: torch.Tensor, row_offset: int = 0, thresholds=None) -> ForestArrays:
         dev = X.device
@@ -172,7 +174,7 @@ class ForestBuilder:
             row_w = W[tt[order], rr[order]].contiguous()
             counts = torch.bincount(keys, minlength=A).to(torch.int32)
             starts = (torch.cumsum(counts, 0) - counts).to(torch.int32)
-            feats = torch.from_numpy(rng.feature_subsets(self.seed, ct, cn, F, m)).to(dev)
+            feats = torch.from_numpy(rng.feature_subsets(self.seed, ct + self.tree_offset, cn, F, m)).to(dev)
             # ---- histogram + best split ----
             if use_native:
                 res = T.hist_split_native(self.bins, self.nbins, y32, rows, row_w, starts, counts, feats, K,
@@ -365,13 +367,78 @@ class RandomForestClassifier(_TreeEstimatorBase):
         X, y, K = self._prep(table)
         return self.fit_tensors(X, y, K)
 
-    def fit_tensors(self, X, y, K, allreduce=None, row_offset: int = 0, thresholds=None):
+    def fit_tensors(self, X, y, K, allreduce=None, row_offset: int = 0, thresholds=None,
+                    tree_wave: int = 0, checkpoint_dir: Optional[str] = None, rank: int = 0):
+        """Grow the forest (all trees in lock step, or in waves of ``tree_wave`` trees —
+        each wave checkpointed under ``checkpoint_dir`` and skipped on resume).  Trees
+        are keyed by their global id, so a waved forest equals the one-shot forest."""
         if self.subsamplingRate != 1.0:
             raise NotImplementedError("subsamplingRate != 1.0")
-        b = ForestBuilder(K, self.numTrees, self.maxDepth, self.maxBins, self.minInstancesPerNode, self.minInfoGain,
-                          self.impurity, self.featureSubsetStrategy, seed=self.seed, allreduce=allreduce)
-        arrs = b.fit(X, y, row_offset=row_offset, thresholds=thresholds)
-        return RandomForestClassificationModel(arrs, X.shape[1], K, uid=self.uid, device=X.device)
+        strategy = self.featureSubsetStrategy
+        if str(strategy).lower() == "auto":
+            strategy = "all" if self.numTrees == 1 else "sqrt"
+        if thresholds is None:
+            thresholds = T.find_thresholds(X.detach().float().cpu().numpy(), self.maxBins, seed=self.seed)
+        wave = tree_wave if tree_wave and tree_wave < self.numTrees else self.numTrees
+        ckpt = None
+        parts: List[ForestArrays] = []
+        if checkpoint_dir:
+            from ..utils.checkpoint import Checkpointer
+
+            ckpt = Checkpointer(checkpoint_dir, rank=rank)
+            last = ckpt.latest()
+            if last is not None:
+                parts.append(_arrays_from_state(last[0]))
+        from ..utils.checkpoint import maybe_inject_fault
+
+        done = sum(p.feature.shape[0] for p in parts)
+        while done < self.numTrees:
+            maybe_inject_fault(done, rank)
+            nt = min(wave, self.numTrees - done)
+            b = ForestBuilder(K, nt, self.maxDepth, self.maxBins, self.minInstancesPerNode, self.minInfoGain,
+                              self.impurity, strategy, bootstrap=self.numTrees > 1, seed=self.seed,
+                              allreduce=allreduce, tree_offset=done)
+            parts.append(b.fit(X, y, row_offset=row_offset, thresholds=thresholds))
+            done += nt
+            if ckpt is not None and done < self.numTrees:
+                merged = _concat_arrays(parts)
+                parts = [merged]
+                ckpt.save(done, _arrays_state(merged), {"trees": done})
+        arrs = _concat_arrays(parts) if len(parts) > 1 else parts[0]
+        return RandomForestClassificationModel(arrs.to(X.device), X.shape[1], K, uid=self.uid, device=X.device)
+
+
+def _concat_arrays(parts: List[ForestArrays]) -> ForestArrays:
+    maxn = max(p.feature.shape[1] for p in parts)
+
+    def pad(t, fill):
+        if t.shape[1] == maxn:
+            return t
+        shape = (t.shape[0], maxn - t.shape[1]) + tuple(t.shape[2:])
+        return torch.cat([t, torch.full(shape, fill, dtype=t.dtype, device=t.device)], dim=1)
+
+    dev = parts[0].feature.device
+    return ForestArrays(torch.cat([pad(p.feature.to(dev), -1) for p in parts]),
+                        torch.cat([pad(p.threshold.to(dev), 0) for p in parts]),
+                        torch.cat([pad(p.left.to(dev), 0) for p in parts]),
+                        torch.cat([pad(p.right.to(dev), 0) for p in parts]),
+                        torch.cat([pad(p.stats.to(dev), 0) for p in parts]),
+                        np.concatenate([p.n_nodes for p in parts]), max(p.max_depth for p in parts),
+                        torch.cat([pad(p.gain.to(dev), 0) for p in parts]) if all(p.gain is not None for p in parts)
+                        else None)
+
+
+def _arrays_state(a: ForestArrays):
+    st = {"feature": a.feature, "threshold": a.threshold, "left": a.left, "right": a.right, "stats": a.stats,
+          "n_nodes": torch.as_tensor(a.n_nodes), "max_depth": torch.tensor([a.max_depth])}
+    if a.gain is not None:
+        st["gain"] = a.gain
+    return st
+
+
+def _arrays_from_state(st) -> ForestArrays:
+    return ForestArrays(st["feature"], st["threshold"], st["left"], st["right"], st["stats"], st["n_nodes"].numpy(),
+                        int(st["max_depth"][0]), st.get("gain"))
 
 
 __all__ = ["DecisionTreeClassifier", "RandomForestClassifier", "DecisionTreeClassificationModel",

@@ -1,0 +1,128 @@
+"""Checkpoint / resume / fault injection (SURVEY.md §5 failure handling).
+
+A training process is hard-killed mid-run by ``HAR_FAULT_INJECT`` (exit code 17,
+like a crashed rank); re-running the same command resumes from the newest
+checkpoint and must produce exactly the model an uninterrupted run produces.
+"""
+import os
+import subprocess
+import sys
+
+import pytest
+import torch
+
+from har.models.tree import RandomForestClassifier
+from har.utils.checkpoint import FAULT_EXIT_CODE, Checkpointer
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+_SCRIPT = r"""
+import sys, torch
+torch.set_num_threads(2)
+from har.models.mlp import MultilayerPerceptronClassifier
+from har.models.tree import RandomForestClassifier
+kind, ckpt, out, dev = sys.argv[1:5]
+g = torch.Generator().manual_seed(0)
+mu = torch.randn(4, 12, generator=g) * 2
+y = torch.randint(0, 4, (1024,), generator=g)
+X = (mu[y] + torch.randn(1024, 12, generator=g)).to(dev)
+y = y.to(dev)
+ck = None if ckpt == "-" else ckpt
+if kind == "mlp":
+    m = MultilayerPerceptronClassifier(layers=[12, 32, 32, 4], maxIter=3, blockSize=128, stepSize=3e-3, seed=5,
+                                       device=dev, checkpointDir=ck, checkpointInterval=4).fit_tensors(X, y)
+    torch.save({"P": m.engine.P.detach().cpu()}, out)
+else:
+    rf = RandomForestClassifier(numTrees=12, maxDepth=4, seed=3, device=dev)
+    m = rf.fit_tensors(X, y, 4, tree_wave=4, checkpoint_dir=ck)
+    torch.save({"raw": m.predict_all(X)[0].detach().float().cpu()}, out)
+"""
+
+
+def _run(kind, ckpt, out, dev="cpu", fault=None):
+    env = dict(os.environ, PYTHONPATH=REPO + os.pathsep + os.environ.get("PYTHONPATH", ""))
+    env.pop("HAR_FAULT_INJECT", None)
+    if fault is not None:
+        env["HAR_FAULT_INJECT"] = str(fault)
+    return subprocess.run([sys.executable, "-c", _SCRIPT, kind, ckpt, out, dev], env=env, capture_output=True,
+                          text=True, timeout=300)
+
+
+@pytest.mark.parametrize("kind,fault", [("mlp", 10), ("rf", 8)])
+def test_fault_then_resume_matches_uninterrupted(tmp_path, kind, fault):
+    ref = _run(kind, "-", str(tmp_path / "ref.pt"))
+    assert ref.returncode == 0, ref.stderr
+    ck = str(tmp_path / "ckpt")
+    crashed = _run(kind, ck, str(tmp_path / "crash.pt"), fault=fault)
+    assert crashed.returncode == FAULT_EXIT_CODE, crashed.stderr
+    assert not os.path.exists(tmp_path / "crash.pt")
+    assert Checkpointer(ck).latest() is not None  # something to resume from
+    resumed = _run(kind, ck, str(tmp_path / "res.pt"))
+    assert resumed.returncode == 0, resumed.stderr
+    a = torch.load(tmp_path / "ref.pt", weights_only=True)
+    b = torch.load(tmp_path / "res.pt", weights_only=True)
+    for k in a:
+        assert torch.equal(a[k], b[k]), k
+
+
+def test_checkpointer_keeps_latest(tmp_path):
+    c = Checkpointer(str(tmp_path), keep=2)
+    for s in (1, 2, 3):
+        c.save(s, {"x": torch.tensor([float(s)])}, {"tag": s})
+    st, meta = c.latest()
+    assert meta["step"] == 3 and float(st["x"][0]) == 3.0
+    assert len([p for p in os.listdir(tmp_path) if p.endswith(".pt")]) == 2
+    # non-zero ranks never write (replicated state has one writer)
+    Checkpointer(str(tmp_path / "r1"), rank=1).save(9, {"x": torch.zeros(1)})
+    assert Checkpointer(str(tmp_path / "r1")).latest() is None
+
+
+def test_rf_waves_equal_one_shot():
+    g = torch.Generator().manual_seed(1)
+    mu = torch.randn(3, 10, generator=g) * 2
+    y = torch.randint(0, 3, (900,), generator=g)
+    X = mu[y] + torch.randn(900, 10, generator=g)
+    one = RandomForestClassifier(numTrees=10, maxDepth=5, seed=7, device="cpu").fit_tensors(X, y, 3)
+    wav = RandomForestClassifier(numTrees=10, maxDepth=5, seed=7, device="cpu").fit_tensors(X, y, 3, tree_wave=3)
+    assert torch.equal(one.predict_all(X)[0], wav.predict_all(X)[0])
+    assert torch.equal(one.arrs.feature, wav.arrs.feature)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind,fault", [("mlp", 10), ("rf", 8)])
+def test_fault_then_resume_gpu(tmp_path, kind, fault):
+    """Same as the CPU test through the HIP kernels: the native MLP step (device-side Adam
+    step counter restored) and the waved GPU forest resume bit-for-bit."""
+    ref = _run(kind, "-", str(tmp_path / "ref.pt"), dev="cuda")
+    assert ref.returncode == 0, ref.stderr
+    ck = str(tmp_path / "ckpt")
+    assert _run(kind, ck, str(tmp_path / "c.pt"), dev="cuda", fault=fault).returncode == FAULT_EXIT_CODE
+    res = _run(kind, ck, str(tmp_path / "res.pt"), dev="cuda")
+    assert res.returncode == 0, res.stderr
+    a = torch.load(tmp_path / "ref.pt", weights_only=True)
+    b = torch.load(tmp_path / "res.pt", weights_only=True)
+    for k in a:
+        assert torch.equal(a[k], b[k]), k
+
+
+@pytest.mark.gpu
+def test_gpu_training_is_deterministic(cuda):
+    """Split-K slabs + fixed-order reductions (no float atomics on the training path):
+    two identical runs give bitwise-identical parameters / forests."""
+    from har.models.mlp import MultilayerPerceptronClassifier
+
+    g = torch.Generator().manual_seed(3)
+    mu = torch.randn(6, 43, generator=g) * 2
+    y = torch.randint(0, 6, (8192,), generator=g)
+    X = (mu[y] + torch.randn(8192, 43, generator=g)).cuda()
+    y = y.cuda()
+    ps = []
+    for _ in range(2):
+        m = MultilayerPerceptronClassifier(layers=[43, 128, 128, 6], maxIter=2, blockSize=1024, seed=1,
+                                           device="cuda").fit_tensors(X, y)
+        ps.append(m.engine.P.detach().clone())
+    assert torch.equal(ps[0], ps[1])
+    fs = [RandomForestClassifier(numTrees=16, maxDepth=8, seed=2, device="cuda").fit_tensors(X, y, 6)
+          for _ in range(2)]
+    assert torch.equal(fs[0].arrs.feature, fs[1].arrs.feature)
+    assert torch.equal(fs[0].arrs.threshold, fs[1].arrs.threshold)
