@@ -25,6 +25,11 @@ def _data(n=1200, f=12, k=4, seed=0):
     return mu[y] + torch.randn(n, f, generator=g), y
 
 
+def _stream(n=3001, seed=4):
+    g = torch.Generator().manual_seed(seed)
+    return torch.randn(n, 3, generator=g).cumsum(0) * 0.1
+
+
 def _worker(rank, world, port, out_dir, what):
     os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
                       MASTER_PORT=str(port))
@@ -46,6 +51,15 @@ def _worker(rank, world, port, out_dir, what):
 
         m = dp.fit_forest_dp(RandomForestClassifier(numTrees=8, maxDepth=4, seed=5), Xs, ys, 4, off, ctx)
         res = m.predict_raw(X)
+    elif what == "stream":
+        from har.features.window import WindowFeaturizer
+        from har.parallel.stream import sharded_window_features
+
+        S = _stream()
+        cut = 1337  # unequal shards, cut not on a window/stride boundary
+        local = S[:cut] if rank == 0 else S[cut:]
+        feats, first = sharded_window_features(ctx, local, WindowFeaturizer(hz=20.0, seconds=10.0, overlap=0.5))
+        res = torch.cat([torch.tensor([[float(first)] * feats.shape[1]]), feats])
     else:
         from har.models.mlp import MLPEngine
 
@@ -98,3 +112,14 @@ def test_dp_mlp_equals_single():
     for s in range(3):
         eng.train_step(X[s * 128:(s + 1) * 128], y[s * 128:(s + 1) * 128], 128)
     torch.testing.assert_close(outs[0], eng.P, rtol=1e-4, atol=1e-5)
+
+
+def test_sharded_stream_halo_equals_single():
+    from har.features.window import WindowFeaturizer
+
+    outs = _run("stream")
+    full = WindowFeaturizer(hz=20.0, seconds=10.0, overlap=0.5).transform(_stream())
+    firsts = [int(o[0, 0]) for o in outs]
+    got = torch.cat([o[1:] for o in outs])
+    assert firsts[0] == 0 and firsts[1] == outs[0].shape[0] - 1  # contiguous window ids
+    torch.testing.assert_close(got, full, equal_nan=True)
