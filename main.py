@@ -47,7 +47,7 @@ from har.report.text import (BANNER_CLASSIFY, BANNER_PIPELINE, BANNER_TRAIN, Run
                              model_header, section)
 from har.tuning.crossval import CrossValidator, ParamGridBuilder  # noqa: E402
 from har.utils import persist  # noqa: E402
-from har.utils.timing import device_sync  # noqa: E402
+from har.utils.timing import PhaseTimer, device_sync  # noqa: E402
 
 
 def cv_evaluator(metric: str):
@@ -106,10 +106,13 @@ def run(cfg: RunConfig) -> dict:
     os.makedirs(cfg.out_dir, exist_ok=True)
     log = RunLog(os.path.join(cfg.out_dir, "result.txt"), echo=cfg.echo)
     t_run = time.perf_counter()
+    timer = PhaseTimer(dev)
 
     log.print("Loading Data Set...")
-    raw = read_csv(cfg.data)
-    data, pipe_model, df = wisdm.prepare(raw, cfg.encoding)
+    with timer.phase("load_csv"):
+        raw = read_csv(cfg.data)
+    with timer.phase("feature_pipeline"):
+        data, pipe_model, df = wisdm.prepare(raw, cfg.encoding)
     section(log, "Data Schema")
     log.print(data.print_schema(), end="")
     section(log, "Sample Data")
@@ -132,7 +135,8 @@ def run(cfg: RunConfig) -> dict:
     log.print(pd.DataFrame({c: [tuple(np.round(v[:9], 2)) if head[c].kind == "vector" else v
                                 for v in head[c].data] for c in head.columns}))
 
-    train, test = random_split(df, cfg.split, seed=cfg.seed)
+    with timer.phase("random_split"):
+        train, test = random_split(df, cfg.split, seed=cfg.seed)
     log.print(BANNER_TRAIN)
     log.print("Training Dataset Count : " + str(train.count()))
     log.print("Test Dataset Count     : " + str(test.count()))
@@ -143,7 +147,8 @@ def run(cfg: RunConfig) -> dict:
     log.print(test_data.show(5), end="")
 
     if dev.type == "cuda":
-        warm_up_device(dev, train, cfg)
+        with timer.phase("device_warmup"):
+            warm_up_device(dev, train, cfg)
     log.print(BANNER_CLASSIFY)
     n_features = df["features"].data.shape[1]
     vocab = df["label"].meta["vocab"]
@@ -153,15 +158,12 @@ def run(cfg: RunConfig) -> dict:
     y_test = torch.as_tensor(test_data["label"].data.astype(np.int64), device=dev)
     for name in cfg.classifiers:
         est = build_estimator(name, cfg, dev, n_features, n_classes)
-        device_sync(dev)
-        t0 = time.perf_counter()
-        model = est.fit(train)
-        device_sync(dev)
-        train_s = round(time.perf_counter() - t0, 3)
-        t0 = time.perf_counter()
-        raw_pred, prob, pred = (model.bestModel if hasattr(model, "bestModel") else model).predict_all(X_test)
-        device_sync(dev)
-        test_s = round(time.perf_counter() - t0, 3)
+        with timer.phase(f"fit:{name}"):
+            model = est.fit(train)
+        train_s = round(timer.get(f"fit:{name}"), 3)
+        with timer.phase(f"predict:{name}"):
+            raw_pred, prob, pred = (model.bestModel if hasattr(model, "bestModel") else model).predict_all(X_test)
+        test_s = round(timer.get(f"predict:{name}"), 3)
         label = str(model) + (" for Logistic Regression" if name == "lrcv" else "")
         model_header(log, label, train_s, test_s)
         preds = model.transform(test_data)
@@ -169,7 +171,8 @@ def run(cfg: RunConfig) -> dict:
         pv = preds.filter(preds["prediction"].data == show_class).select(
             ["UID", "probability", "label", "prediction"]).order_by("probability", ascending=False)
         log.print(pv.show(n=5, truncate=30), end="")
-        r = evaluate_all(y_test, pred, raw_pred, n_classes)
+        with timer.phase(f"evaluate:{name}"):
+            r = evaluate_all(y_test, pred, raw_pred, n_classes)
         evaluation_block(log, r)
         row = (csvout.cv_row if name.endswith("cv") else csvout.plain_row)(str(model), r, train_s, test_s)
         (cv_rows if name.endswith("cv") else plain_rows).append(row)
@@ -188,7 +191,8 @@ def run(cfg: RunConfig) -> dict:
         csvout.write_rows(os.path.join(cfg.out_dir, "crossFold_additional_param.csv"), csvout.CV_FIELDS, cv_rows,
                           append=cfg.append_csv)
     summary = {"device": str(dev), "encoding": cfg.encoding, "n_train": train.count(), "n_test": test.count(),
-               "seed": cfg.seed, "wall_s": time.perf_counter() - t_run, "models": records}
+               "seed": cfg.seed, "wall_s": time.perf_counter() - t_run, "models": records,
+               "phases_s": {k: round(v, 6) for k, v in timer.as_dict().items()}}
     csvout.append_jsonl(os.path.join(cfg.out_dir, "metrics.jsonl"), summary)
     log.close()
     if cfg.plots:

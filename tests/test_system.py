@@ -36,6 +36,9 @@ def test_main_reference_run_cpu(tmp_path, wisdm_csv):
     assert rows[0][-3:] == ['Cross Validation Training Time', 'Cross Validation Testing Time', 'Cross Fold Accuracy']
     rec = json.loads((tmp_path / "metrics.jsonl").read_text().splitlines()[-1])
     assert rec["n_train"] + rec["n_test"] == 5418
+    ph = rec["phases_s"]
+    assert {"load_csv", "feature_pipeline", "random_split", "fit:lr", "predict:lr"} <= set(ph)
+    assert abs(ph["fit:lr"] - rec["models"]["lr"]["train_s"]) < 2e-3
 
 
 def test_persist_roundtrip(tmp_path, wisdm_csv):
