@@ -94,3 +94,25 @@ def test_native_build_uptodate():
     import har._har_native as nat
 
     assert hasattr(nat, "gemm") and hasattr(nat, "tree_hist_split") and hasattr(nat, "csv_parse")
+
+
+def test_yaml_configs_load():
+    """Every configs/*.yaml is a valid RunConfig overlay (bench-only files hold a ``bench:`` block)."""
+    import glob
+
+    import yaml
+
+    from har.config import config_from_args
+
+    files = sorted(glob.glob(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "configs",
+                                          "*.yaml")))
+    assert len(files) >= 5
+    for f in files:
+        with open(f) as fh:
+            d = yaml.safe_load(fh)
+        if "bench" in d:
+            assert d["bench"]["config"] in ("mlp", "rf", "stream", "rf9")
+            continue
+        cfg = config_from_args(["--preset-file", f])
+        for k, v in d.items():
+            assert getattr(cfg, k) == v
