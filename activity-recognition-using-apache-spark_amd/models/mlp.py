@@ -180,9 +180,10 @@ class MLPEngine:
         s = self.layout.by_name[name]
         return self.slabs.view(-1)[s.offset:]
 
-    def forward_backward_native(self, Xb: torch.Tensor, y32: torch.Tensor, scale: float):
+    def forward_backward_native(self, Xb: torch.Tensor, y32: torch.Tensor, scale: float, on_grad=None):
         """Xb: [B, in_pad] bf16 (contiguous slice), y32: [B] int32.  Leaves the split-K
-        gradient partials in ``self.slabs[:self.active_splits]``."""
+        gradient partials in ``self.slabs[:self.active_splits]``; ``on_grad(name)`` is called
+        as soon as layer ``name``'s weight/bias gradient slabs are enqueued (DP bucketing)."""
         L, mod, s = self.layout, _native.kernels(), _native.stream_ptr()
         B = Xb.shape[0]
         if Xb.shape[1] != L.in_pad or Xb.dtype != torch.bfloat16 or B > self.B or y32.dtype != torch.int32:
@@ -210,12 +211,16 @@ class MLPEngine:
         gemm_bf16(dl, last, self._slab("Wout"), M=HEAD_PAD, N=self.dims[-1], K=B, layout=3, epi=EPI_F32_SLAB,
                   k_split=ks, ldc=self.dims[-1], slab_stride=total, rowsum=self._slab("bout"),
                   slab_stride_rowsum=total, tile=wgrad_tile(HEAD_PAD, self.dims[-1]))
+        if on_grad is not None:
+            on_grad("Wout")
         for i in reversed(range(nh)):
             h = self.dims[i + 1]
             # dW_i = dact^T . acts[i]   (+ db_i = row sums of dact^T)
             gemm_bf16(dact, acts[i], self._slab(f"W{i}"), M=h, N=self.dims[i], K=B, layout=3, epi=EPI_F32_SLAB,
                       k_split=ks, ldc=self.dims[i], slab_stride=total, rowsum=self._slab(f"b{i}"),
                       slab_stride_rowsum=total, tile=wgrad_tile(h, self.dims[i]))
+            if on_grad is not None:
+                on_grad(f"W{i}")
             if i > 0:
                 # dact_{i-1} = (dact . W_i) * relu'(acts[i])
                 hp = self.dims[i]
@@ -236,6 +241,48 @@ class MLPEngine:
         _native.kernels().reduce_slabs_grouped(self.partials.data_ptr(), self.n_groups, self.layout.total,
                                                self.G.data_ptr(), 1, _native.stream_ptr(), 0)
 
+    def _layer_range(self, name):
+        """[lo, hi) of layer ``name``'s weight + bias in the flat buffers."""
+        L = self.layout
+        k = L.segments.index(L.by_name[name])
+        return L.segments[k].offset, (L.segments[k + 2].offset if k + 2 < len(L.segments) else L.total)
+
+    def _reduce_range(self, lo: int, hi: int, tick: bool):
+        """Two-level slab reduction of G[lo:hi] only (same summation order as the whole-buffer one)."""
+        mod, st, total = _native.kernels(), _native.stream_ptr(), self.layout.total
+        mod.reduce_slabs_grouped(self.slabs.data_ptr() + 4 * lo, self.active_splits, hi - lo,
+                                 self.partials.data_ptr() + 4 * lo, self.n_groups, st,
+                                 self.step_count.data_ptr() if tick else 0, lds=total, ldd=total)
+        mod.reduce_slabs_grouped(self.partials.data_ptr() + 4 * lo, self.n_groups, hi - lo, self.G.data_ptr() + 4 * lo,
+                                 1, st, 0, lds=total, ldd=hi - lo)
+
+    def train_step_overlapped(self, Xb: torch.Tensor, yb: torch.Tensor, global_batch: int,
+                              bucket_bytes: int = 64 << 10):
+        """DP step with the gradient all-reduce bucketed and overlapped with backward: as soon
+        as the layers finished so far hold >= ``bucket_bytes`` of gradient, their slabs are
+        reduced and an async RCCL all-reduce of that contiguous slice of G starts on the
+        communicator's stream while the remaining dgrad/wgrad GEMMs run; Adam waits for all
+        buckets.  Layers finish in reverse order, so every bucket is one contiguous range."""
+        import torch.distributed as dist
+
+        works, pend = [], []
+
+        def flush():
+            lo, hi = pend[-1][0], pend[0][1]
+            self._reduce_range(lo, hi, tick=not works)
+            works.append(dist.all_reduce(self.G[lo:hi], group=self.pg, async_op=True))
+            pend.clear()
+
+        def on_grad(name):
+            pend.append(self._layer_range(name))
+            if (pend[0][1] - pend[-1][0]) * 4 >= bucket_bytes or name == "W0":
+                flush()
+
+        self.forward_backward_native(Xb, yb, 1.0 / global_batch, on_grad=on_grad)
+        for w in works:
+            w.wait()  # stream-ordered: the compute stream waits on the RCCL stream, the host does not
+        self.optimizer_step_native(from_slabs=False)
+
     def optimizer_step_native(self, from_slabs: bool):
         """Adam; with ``from_slabs`` the slabs are first reduced to ``n_groups`` partials and the
         last level of the reduction is fused into the Adam kernel."""
@@ -253,14 +300,22 @@ class MLPEngine:
             import torch.distributed as dist
             dist.all_reduce(self.G, group=self.pg)
 
+    def grad_phase(self, Xb: torch.Tensor, yb: torch.Tensor, global_batch: int):
+        """DP step, part 1 (graph-capturable): fwd + bwd + deterministic slab reduction into G."""
+        self.forward_backward_native(Xb, yb, 1.0 / global_batch)
+        self.reduce_grads_native()
+
+    def apply_phase(self):
+        """DP step, part 3 (graph-capturable): Adam from the all-reduced G (part 2 is the RCCL
+        all-reduce, issued eagerly between the two graph replays)."""
+        self.optimizer_step_native(from_slabs=False)
+
     def train_step(self, Xb: torch.Tensor, yb: torch.Tensor, global_batch: int):
         if self.native:
-            self.forward_backward_native(Xb, yb, 1.0 / global_batch)
             if self.world > 1:
-                self.reduce_grads_native()
-                self.allreduce_grads()
-                self.optimizer_step_native(from_slabs=False)
+                self.train_step_overlapped(Xb, yb, global_batch)
             else:  # single GPU: the slab reduction is fused into Adam
+                self.forward_backward_native(Xb, yb, 1.0 / global_batch)
                 self.optimizer_step_native(from_slabs=True)
         else:
             self.train_step_torch(Xb, yb, global_batch)

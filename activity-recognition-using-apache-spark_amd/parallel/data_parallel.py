@@ -12,7 +12,8 @@ combines are RCCL collectives over xGMI:
   summed with one ``all_reduce`` and every rank selects the same splits
   (``reduce_scatter`` by node owner + ``all_gather`` of the winners is the
   bandwidth-optimal variant for very large forests);
-* MLP: one flat fp32 gradient bucket per step (``MLPEngine.allreduce_grads``).
+* MLP: fp32 gradient buckets (>= 64 KB, contiguous layer ranges of the flat buffer) all-reduced
+  asynchronously while backward continues (``MLPEngine.train_step_overlapped``).
 
 ``gloo`` runs the identical code on CPU for the multi-process tests.
 """

@@ -107,9 +107,31 @@ def bench_mlp(args, ctx):
         j = i % nb
         eng.train_step(Xin[j * B:(j + 1) * B], y32[j * B:(j + 1) * B], global_batch)
 
-    use_graph = args.graph == 1 or (args.graph < 0 and world == 1)
-    graphs = capture_steps(step, nb, eng.native and use_graph)
-    run = (lambda i: graphs[i % nb].replay()) if graphs else step
+    # default eager: the step is GPU-bound (eager 0.168 ms vs one-graph replay 0.173 ms per step on
+    # MI355X, profiles/bench_mlp_graph_modes.md) and in DP the eager step overlaps the bucketed
+    # RCCL all-reduce with backward, which a captured graph cannot
+    mode = args.graph if args.graph >= 0 else 0
+    graphs = None
+    if eng.native and mode == 1:  # whole step (collective included) in one graph per slot
+        graphs = capture_steps(step, nb, True)
+        run = lambda i: graphs[i % nb].replay()  # noqa: E731
+    elif eng.native and mode == 2:
+        # segmented: graph(fwd+bwd+slab reduce) -> eager RCCL all-reduce of the flat fp32
+        # gradient bucket -> graph(Adam); no collective inside a captured graph
+        def grad(i):
+            j = i % nb
+            eng.grad_phase(Xin[j * B:(j + 1) * B], y32[j * B:(j + 1) * B], global_batch)
+
+        gA = capture_steps(grad, nb, True)
+        gB = capture_steps(lambda i: eng.apply_phase(), 1, True)[0]
+        graphs = gA + [gB]
+
+        def run(i):
+            gA[i % nb].replay()
+            eng.allreduce_grads()
+            gB.replay()
+    else:
+        run = step
     elapsed = timed(ctx, run, args.steps, args.warmup, dev)
     Xt, yt = synthetic_windows(65536, seed=999, device=dev)
     acc = float((torch.argmax(eng.logits(Xt), dim=1) == yt).float().mean())
@@ -120,7 +142,7 @@ def bench_mlp(args, ctx):
             "config": {"model": f"WISDM 6-class 3-layer MLP bf16 ({'-'.join(map(str, layers))})",
                        "global_batch": global_batch, "seq_len": WINDOW_SAMPLES, "parallelism": f"dp{world}"},
             "test_accuracy": hdist.mean_over_ranks(ctx, acc), "test_accuracy_data": "held-out synthetic windows",
-            "hip_graph": graphs is not None}
+            "hip_graph": {0: "off", 1: "whole-step", 2: "segmented"}[mode if graphs else 0]}
 
 
 def _featurized(n_windows, spec, dev, first_window):
@@ -232,8 +254,8 @@ def main():
     ap.add_argument("--hidden", type=int, default=256)
     ap.add_argument("--lr", type=float, default=1e-3)
     ap.add_argument("--graph", type=int, default=-1,
-                    help="capture the MLP step in a HIP graph (default: on for 1 GPU; multi-GPU steps with the "
-                         "RCCL all-reduce run eager unless --graph 1)")
+                    help="HIP graphs for the MLP step: 0 eager (default; DP overlaps the bucketed all-reduce with "
+                         "backward), 1 whole step in one graph, 2 graphs around an eager RCCL all-reduce")
     ap.add_argument("--rows", type=int, default=60000, help="windows per GPU (forest configs)")
     ap.add_argument("--trees", type=int, default=0)
     ap.add_argument("--depth", type=int, default=10)

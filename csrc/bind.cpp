@@ -190,10 +190,15 @@ PYBIND11_MODULE(_har_native, m) {
           "head_fused");
   });
 
-  m.def("reduce_slabs_grouped", [](u slabs, int S_, int64_t n, u dst, int G, u stream, u tick) {
-    check(har_reduce_slabs_grouped(P<const float>(slabs), S_, n, P<float>(dst), G, P<int32_t>(tick), S(stream)),
-          "reduce_slabs_grouped");
-  });
+  m.def(
+      "reduce_slabs_grouped",
+      [](u slabs, int S_, int64_t n, u dst, int G, u stream, u tick, int64_t lds, int64_t ldd) {
+        check(har_reduce_slabs_grouped(P<const float>(slabs), S_, n, lds < 0 ? n : lds, P<float>(dst), G,
+                                       ldd < 0 ? n : ldd, P<int32_t>(tick), S(stream)),
+              "reduce_slabs_grouped");
+      },
+      py::arg("slabs"), py::arg("S"), py::arg("n"), py::arg("dst"), py::arg("G"), py::arg("stream"),
+      py::arg("tick"), py::arg("lds") = -1, py::arg("ldd") = -1);
 
   m.def("column_stats_workspace", &har_column_stats_workspace);
   m.def("column_stats", [](u X, int64_t n, int ncols, int ld, u w, u stats, u ws, u stream) {

@@ -56,7 +56,8 @@ int har_head_fused_blocks(int B);
 
 // dst[g*n + i] = sum of slabs[s*n + i] over the g-th group of ceil(S/G) slabs (deterministic).
 // A non-null tick is incremented once by the first workgroup (the optimizer step counter).
-int har_reduce_slabs_grouped(const float* slabs, int S, int64_t n, float* dst, int G, int32_t* tick, hipStream_t s);
+int har_reduce_slabs_grouped(const float* slabs, int S, int64_t n, int64_t lds, float* dst, int G, int64_t ldd,
+                             int32_t* tick, hipStream_t s);
 
 // dst[i] = sum_s slabs[s*n + i]  (deterministic split-K reduction)
 int har_reduce_slabs(const float* slabs, int nslabs, int64_t n, float* dst, hipStream_t s);

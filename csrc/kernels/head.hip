@@ -150,8 +150,8 @@ __global__ __launch_bounds__(256) void head_fused_kernel(
 
 // dst[g][i] = sum over slabs s in group g of slabs[s][i]  (G groups of ceil(S/G) slabs)
 __global__ __launch_bounds__(256) void reduce_slabs_grouped_kernel(const float* __restrict__ slabs, int S, int64_t n,
-                                                                   float* __restrict__ dst, int G,
-                                                                   int32_t* __restrict__ tick) {
+                                                                   int64_t lds, float* __restrict__ dst, int G,
+                                                                   int64_t ldd, int32_t* __restrict__ tick) {
   const int g = blockIdx.y;
   // optional optimizer-step tick (saves a one-thread launch; the Adam kernel runs after this one)
   if (tick && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) *tick += 1;
@@ -162,20 +162,20 @@ __global__ __launch_bounds__(256) void reduce_slabs_grouped_kernel(const float* 
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
     int s = s0;
     for (; s + 4 <= s1; s += 4) {  // 4 independent loads in flight
-      const float4 x0 = reinterpret_cast<const float4*>(slabs + (size_t)s * n)[i];
-      const float4 x1 = reinterpret_cast<const float4*>(slabs + (size_t)(s + 1) * n)[i];
-      const float4 x2 = reinterpret_cast<const float4*>(slabs + (size_t)(s + 2) * n)[i];
-      const float4 x3 = reinterpret_cast<const float4*>(slabs + (size_t)(s + 3) * n)[i];
+      const float4 x0 = reinterpret_cast<const float4*>(slabs + (size_t)s * lds)[i];
+      const float4 x1 = reinterpret_cast<const float4*>(slabs + (size_t)(s + 1) * lds)[i];
+      const float4 x2 = reinterpret_cast<const float4*>(slabs + (size_t)(s + 2) * lds)[i];
+      const float4 x3 = reinterpret_cast<const float4*>(slabs + (size_t)(s + 3) * lds)[i];
       acc.x += (x0.x + x1.x) + (x2.x + x3.x);
       acc.y += (x0.y + x1.y) + (x2.y + x3.y);
       acc.z += (x0.z + x1.z) + (x2.z + x3.z);
       acc.w += (x0.w + x1.w) + (x2.w + x3.w);
     }
     for (; s < s1; ++s) {
-      const float4 x = reinterpret_cast<const float4*>(slabs + (size_t)s * n)[i];
+      const float4 x = reinterpret_cast<const float4*>(slabs + (size_t)s * lds)[i];
       acc.x += x.x; acc.y += x.y; acc.z += x.z; acc.w += x.w;
     }
-    reinterpret_cast<float4*>(dst + (size_t)g * n)[i] = acc;
+    reinterpret_cast<float4*>(dst + (size_t)g * ldd)[i] = acc;
   }
 }
 
@@ -205,12 +205,13 @@ extern "C" int har_head_fused(const uint16_t* H, const uint16_t* W, const float*
   return 0;
 }
 
-extern "C" int har_reduce_slabs_grouped(const float* slabs, int S, int64_t n, float* dst, int G, int32_t* tick,
-                                        hipStream_t s) {
-  if (n % 4 || G <= 0 || S <= 0) return -2;
+extern "C" int har_reduce_slabs_grouped(const float* slabs, int S, int64_t n, int64_t lds, float* dst, int G,
+                                        int64_t ldd, int32_t* tick, hipStream_t s) {
+  if (n % 4 || lds % 4 || ldd % 4 || lds < n || (G > 1 && ldd < n) || G <= 0 || S <= 0) return -2;
+  if ((reinterpret_cast<uintptr_t>(slabs) | reinterpret_cast<uintptr_t>(dst)) & 15) return -3;
   const int64_t n4 = n / 4;
   const int bx = (int)std::max<int64_t>(1, std::min<int64_t>(1024, (n4 + 255) / 256));
-  reduce_slabs_grouped_kernel<<<dim3(bx, G), 256, 0, s>>>(slabs, S, n, dst, G, tick);
+  reduce_slabs_grouped_kernel<<<dim3(bx, G), 256, 0, s>>>(slabs, S, n, lds, dst, G, ldd, tick);
   HAR_CHECK_LAUNCH();
   return 0;
 }

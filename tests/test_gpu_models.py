@@ -138,3 +138,38 @@ def test_main_reference_run_gpu(cuda, tmp_path, wisdm_csv):
     assert m["lr"]["accuracy"] >= 0.60 and m["lrcv"]["accuracy"] >= 0.70
     assert m["dt"]["accuracy"] >= 0.72 and m["rf"]["accuracy"] >= 0.62
     assert (tmp_path / "result.txt").exists() and (tmp_path / "additional_param.csv").exists()
+
+
+def test_mlp_overlapped_dp_step_equals_fused(cuda):
+    """The bucketed, backward-overlapped DP step (ranged slab reductions + async RCCL all-reduce
+    per bucket; a 1-rank RCCL group here) gives bitwise the parameters of the whole-buffer
+    reduce -> all-reduce -> Adam step."""
+    import socket
+
+    import torch.distributed as dist
+
+    from har.models.mlp import MLPEngine, pad_input_bf16
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1, device_id=cuda)
+    try:
+        B = 4096
+        layers = [43, 256, 256, 6]
+        a = MLPEngine(layers, B, cuda, lr=1e-3, seed=4)
+        b = MLPEngine(layers, B, cuda, lr=1e-3, seed=4)
+        g = torch.Generator(device=cuda).manual_seed(2)
+        for _ in range(3):
+            X = pad_input_bf16(torch.randn(B, 43, device=cuda, generator=g), a.layout.in_pad)
+            y = torch.randint(0, 6, (B,), device=cuda, generator=g).to(torch.int32)
+            a.forward_backward_native(X, y, 1.0 / B)  # whole-buffer reduction, then Adam
+            a.reduce_grads_native()
+            a.optimizer_step_native(from_slabs=False)
+            b.train_step_overlapped(X, y, B, bucket_bytes=1)  # one bucket per layer
+        torch.cuda.synchronize()
+        assert torch.equal(a.P, b.P) and torch.equal(a.m, b.m) and torch.equal(a.step_count, b.step_count)
+        assert int(b.step_count[0]) == 3
+    finally:
+        dist.destroy_process_group()
