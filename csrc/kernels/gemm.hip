@@ -35,8 +35,9 @@
 //   EPI_F32_SLAB   C[z](f32) = alpha*acc   plain stores into split slab z = blockIdx.z
 //                  (deterministic split-K: a later pass sums the slabs, no atomics)
 // Optional fused A-row sums (bias gradients of a weight-grad product): blocks of
-// the first N tile accumulate sum_k A(m,k) over their K range from the LDS tile
-// and store it to rowsum[z * slab_stride_rowsum + m] (atomicAdd for EPI_F32_ATOMIC).
+// the first N tile sum the k-slots of the A fragments they feed to the MFMAs and
+// store sum_k A(m,k) over their K range to rowsum[z * slab_stride_rowsum + m]
+// (atomicAdd for EPI_F32_ATOMIC).
 #include "common.h"
 #include "../har_kernels.h"
 
@@ -153,6 +154,17 @@ template <int ROWS, int BK> struct Frag<float, ROWS, false, BK> {
   }
 };
 
+// Sum of the k-values a lane holds in an A fragment (fused bias-gradient row sums).
+__device__ __forceinline__ float frag_sum(bf16x8_t a) {
+  typedef __attribute__((ext_vector_type(4))) uint32_t u32x4_t;
+  const u32x4_t w = __builtin_bit_cast(u32x4_t, a);
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) s += __uint_as_float(w[j] << 16) + __uint_as_float(w[j] & 0xffff0000u);
+  return s;
+}
+__device__ __forceinline__ float frag_sum(float a) { return a; }
+
 __device__ __forceinline__ f32x4_t mma(bf16x8_t a, bf16x8_t b, f32x4_t c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
@@ -199,8 +211,13 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_kernel(GemmParams p) {
     kb = blockIdx.z * p.k_split;
     ke = min(p.K, kb + p.k_split);
   }
-  const bool do_rowsum = p.rowsum != nullptr && tn == 0 && tid < BM;
-  float rs = 0.f;
+  // bias-gradient row sums come from the A fragments already in registers: waves of the
+  // first N-column (wn == 0) of the first N tile add up their k-slots (free VALU work next
+  // to the MFMAs), one cross-lane reduction at the end
+  const bool rs_wave = p.rowsum != nullptr && tn == 0 && wn == 0;
+  float rs[RM];
+#pragma unroll
+  for (int i = 0; i < RM; ++i) rs[i] = 0.f;
 
   f32x4_t acc[RM][RN];
 #pragma unroll
@@ -222,16 +239,12 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_kernel(GemmParams p) {
       sa.load(A, p.lda, m0, p.M, k0 + BK, ke, tid);
       sb.load(B, p.ldb, n0, p.N, k0 + BK, ke, tid);
     }
-    if (do_rowsum) {
-#pragma unroll
-      for (int k = 0; k < BK; ++k)
-        rs += to_f<T>(A_KMAJOR ? As[tid * ImgA::PITCH + k] : As[k * ImgA::PITCH + tid]);
-    }
 #pragma unroll
     for (int kk = 0; kk < BK; kk += KPER) {
 #pragma unroll
       for (int i = 0; i < RM; ++i) {
         const auto a = Frag<T, BM, A_KMAJOR, BK>::get(As, wm * TM + i * 16, kk, lane);
+        if (rs_wave) rs[i] += frag_sum(a);
 #pragma unroll
         for (int j = 0; j < RN; ++j)
           acc[i][j] = mma(a, Frag<T, BN, B_KMAJOR, BK>::get(Bs, wn * TN + j * 16, kk, lane), acc[i][j]);
@@ -240,9 +253,18 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_kernel(GemmParams p) {
     __syncthreads();
   }
 
-  if (do_rowsum && m0 + tid < p.M) {
-    if (EPI == EPI_F32_ATOMIC) atomicAdd(p.rowsum + m0 + tid, p.alpha * rs);
-    else p.rowsum[(size_t)blockIdx.z * p.slab_stride_rowsum + m0 + tid] = p.alpha * rs;
+  if (rs_wave) {
+#pragma unroll
+    for (int i = 0; i < RM; ++i) {  // lanes r16, r16+16, r16+32, r16+48 hold the same row
+      float v = rs[i];
+      v += __shfl_xor(v, 16);
+      v += __shfl_xor(v, 32);
+      const int m = m0 + wm * TM + i * 16 + r16;
+      if (q == 0 && m < p.M) {
+        if (EPI == EPI_F32_ATOMIC) atomicAdd(p.rowsum + m, p.alpha * v);
+        else p.rowsum[(size_t)blockIdx.z * p.slab_stride_rowsum + m] = p.alpha * v;
+      }
+    }
   }
 
   // ---- epilogue ----

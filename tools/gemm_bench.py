@@ -42,6 +42,8 @@ def main():
         "wgrad_W1": (lambda t: gemm_bf16(h2, h1, slab, M=H, N=H, K=B, layout=3, epi=EPI_F32_SLAB, k_split=ks, ldc=H,
                                          slab_stride=H * H + H, rowsum=rowsum, slab_stride_rowsum=H * H + H, tile=t),
                      [0, 3, 4, 8, 9, 12, 13]),
+        "wgrad_W1_norowsum": (lambda t: gemm_bf16(h2, h1, slab, M=H, N=H, K=B, layout=3, epi=EPI_F32_SLAB,
+                                                  k_split=ks, ldc=H, slab_stride=H * H + H, tile=t), [0, 9]),
         "wgrad_W0": (lambda t: gemm_bf16(h2, X, slab, M=H, N=64, K=B, layout=3, epi=EPI_F32_SLAB, k_split=ks, ldc=64,
                                          slab_stride=H * H + H, rowsum=rowsum, slab_stride_rowsum=H * H + H, tile=t),
                      [1, 4, 8, 13]),
