@@ -24,6 +24,7 @@ The CPU path (and test oracle) is the same network in PyTorch fp32.
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass
 from typing import List, Optional, Sequence
 
@@ -169,6 +170,16 @@ class MLPEngine:
             self.slabs = torch.zeros(self.n_splits, L.total, dtype=torch.float32, device=dev)
             self.n_groups = min(8, self.n_splits)  # two-level reduction: splits -> groups -> 1
             self.partials = torch.zeros(self.n_groups, L.total, dtype=torch.float32, device=dev)
+            # one-kernel forward + head + dWout (mlp_fused.hip) for the 2-hidden-layer shapes it covers
+            self.fused_ok = (len(L.hidden) == 2 and L.hidden[0] == L.hidden[1] and L.hidden[0] in (128, 256)
+                             and L.in_pad in (32, 64) and L.num_classes <= 16
+                             and os.environ.get("HAR_MLP_FUSED", "1") != "0")
+            if self.fused_ok:
+                nwg = _native.kernels().mlp_fwd_head_grid(self.B)
+                self.fslab = torch.zeros(nwg, 16 * L.hidden[-1] + 16, dtype=torch.float32, device=dev)
+                self.fblock_loss = torch.zeros(nwg, dtype=torch.float32, device=dev)
+                self.fblock_correct = torch.zeros(nwg, dtype=torch.int32, device=dev)
+            self.last_fused = False
         else:
             self.t_step = 0
 
@@ -193,6 +204,9 @@ class MLPEngine:
         total = L.total
         nh = len(L.hidden)
         acts = [Xb] + [a[:B] for a in self.acts[1:]]
+        if self.fused_ok and B % 16 == 0:
+            return self._forward_backward_fused(Xb, y32, scale, on_grad, ks, acts)
+        self.last_fused = False
         for i in range(nh):
             gemm_bf16(acts[i], self._w(self.Pb, f"W{i}"), acts[i + 1], M=B, N=self.dims[i + 1], K=self.dims[i],
                       layout=0, epi=EPI_BIAS_RELU, bias=self._w(self.P, f"b{i}"),
@@ -229,11 +243,61 @@ class MLPEngine:
                           mask=acts[i], tile=dgrad_tile(B, hp, h))
                 dact = prev
 
+    def _forward_backward_fused(self, Xb, y32, scale, on_grad, ks, acts):
+        """2-hidden-layer step: ONE kernel for fwd L1 + fwd L2 + head + dWout/dbout (h2 and the
+        logit gradients stay on chip), then dW1, dgrad and dW0 as split-K MFMA GEMMs."""
+        L, mod, s = self.layout, _native.kernels(), _native.stream_ptr()
+        B, H, K0 = Xb.shape[0], self.dims[-1], L.in_pad
+        total = L.total
+        h1 = acts[1]
+        dact = self.dbuf[1][: B * H].view(B, H)
+        self.fused_nwg = mod.mlp_fwd_head_grid(B)
+        mod.mlp_fwd_head(Xb.data_ptr(), K0, self._w(self.Pb, "W0").data_ptr(), self._w(self.P, "b0").data_ptr(),
+                         self._w(self.Pb, "W1").data_ptr(), self._w(self.P, "b1").data_ptr(), H,
+                         self._w(self.Pb, "Wout").data_ptr(), self._w(self.P, "bout").data_ptr(), y32.data_ptr(),
+                         B, L.num_classes, float(scale), h1.data_ptr(), dact.data_ptr(), self.fslab.data_ptr(),
+                         self.fblock_loss.data_ptr(), self.fblock_correct.data_ptr(), s)
+        self.last_fused = True
+        self.last_batch = B
+        if on_grad is not None:
+            on_grad("Wout")
+        gemm_bf16(dact, h1, self._slab("W1"), M=H, N=H, K=B, layout=3, epi=EPI_F32_SLAB, k_split=ks, ldc=H,
+                  slab_stride=total, rowsum=self._slab("b1"), slab_stride_rowsum=total, tile=wgrad_tile(H, H))
+        if on_grad is not None:
+            on_grad("W1")
+        prev = self.dbuf[0][: B * H].view(B, H)
+        gemm_bf16(dact, self._w(self.Pb, "W1"), prev, M=B, N=H, K=H, layout=2, epi=EPI_RELU_GRAD, mask=h1,
+                  tile=dgrad_tile(B, H, H))
+        gemm_bf16(prev, Xb, self._slab("W0"), M=H, N=K0, K=B, layout=3, epi=EPI_F32_SLAB, k_split=ks, ldc=K0,
+                  slab_stride=total, rowsum=self._slab("b0"), slab_stride_rowsum=total, tile=wgrad_tile(H, K0))
+        if on_grad is not None:
+            on_grad("W0")
+
+    def _first_level(self, lo: int, hi: int, tick: bool):
+        """Split-K slabs (and, after a fused step, the fused kernel's dWout/dbout workgroup
+        slabs) -> n_groups partials over [lo, hi); optionally ticks the Adam step counter."""
+        mod, st, total = _native.kernels(), _native.stream_ptr(), self.layout.total
+        tk = self.step_count.data_ptr() if tick else 0
+        woff = self.layout.by_name["Wout"].offset
+        if not self.last_fused or hi <= woff:
+            mod.reduce_slabs_grouped(self.slabs.data_ptr() + 4 * lo, self.active_splits, hi - lo,
+                                     self.partials.data_ptr() + 4 * lo, self.n_groups, st, tk, lds=total, ldd=total)
+            return
+        if lo < woff:
+            mod.reduce_slabs_grouped(self.slabs.data_ptr() + 4 * lo, self.active_splits, woff - lo,
+                                     self.partials.data_ptr() + 4 * lo, self.n_groups, st, tk, lds=total, ldd=total)
+            tk = 0
+        H = self.dims[-1]
+        w = self.fslab.shape[1]
+        mod.reduce_slabs_grouped(self.fslab.data_ptr(), self.fused_nwg, 16 * H, self.partials.data_ptr() + 4 * woff,
+                                 self.n_groups, st, tk, lds=w, ldd=total)
+        mod.reduce_slabs_grouped(self.fslab.data_ptr() + 4 * 16 * H, self.fused_nwg, 16,
+                                 self.partials.data_ptr() + 4 * self.layout.by_name["bout"].offset, self.n_groups, st,
+                                 0, lds=w, ldd=total)
+
     def _reduce_to_partials(self):
         # the first reduction level also ticks the Adam step counter (one launch fewer per step)
-        _native.kernels().reduce_slabs_grouped(self.slabs.data_ptr(), self.active_splits, self.layout.total,
-                                               self.partials.data_ptr(), self.n_groups, _native.stream_ptr(),
-                                               self.step_count.data_ptr())
+        self._first_level(0, self.layout.total, True)
 
     def reduce_grads_native(self):
         """G = sum of the active gradient slabs (two deterministic levels; needed before a collective)."""
@@ -250,9 +314,7 @@ class MLPEngine:
     def _reduce_range(self, lo: int, hi: int, tick: bool):
         """Two-level slab reduction of G[lo:hi] only (same summation order as the whole-buffer one)."""
         mod, st, total = _native.kernels(), _native.stream_ptr(), self.layout.total
-        mod.reduce_slabs_grouped(self.slabs.data_ptr() + 4 * lo, self.active_splits, hi - lo,
-                                 self.partials.data_ptr() + 4 * lo, self.n_groups, st,
-                                 self.step_count.data_ptr() if tick else 0, lds=total, ldd=total)
+        self._first_level(lo, hi, tick)
         mod.reduce_slabs_grouped(self.partials.data_ptr() + 4 * lo, self.n_groups, hi - lo, self.G.data_ptr() + 4 * lo,
                                  1, st, 0, lds=total, ldd=hi - lo)
 
@@ -337,6 +399,9 @@ class MLPEngine:
 
     def last_loss_and_correct(self):
         """(sum of CE, #correct) of the last native batch — one host sync."""
+        if self.last_fused:
+            n = self.fused_nwg
+            return float(self.fblock_loss[:n].sum().item()), int(self.fblock_correct[:n].sum().item())
         return float(self.block_loss.sum().item()), int(self.block_correct.sum().item())
 
     # ---------------------------------------------------------------- torch

@@ -120,7 +120,10 @@ class ForestBuilder:
         return torch.from_numpy(rng.poisson1_weights(self.seed, range(self.tree_offset, self.tree_offset + self.T),
                                                      N, row_offset)).float()
 
-    def fit(self, X: torch.Tensor, y: torch.Tensor, row_offset: int = 0, thresholds=None) -> ForestArrays:
+    def fit(self, X: torch.Tensor, y: torch.Tensor, row_offset: int = 0, thresholds=None,
+            row_weight: Optional[torch.Tensor] = None) -> ForestArrays:
+        """``row_weight`` [T, N] multiplies the bootstrap weights (0 = row not seen by that
+        tree): the cross-validation folds of several forests grow in one lock-step build."""
         dev = X.device
         N, F = X.shape
         self.prepare(X, thresholds)
@@ -128,6 +131,8 @@ class ForestBuilder:
         m = subset_size(self.subset, F, Tn)
         y32 = y.to(torch.int32).contiguous()
         W = self.bootstrap_weights(N, dev, row_offset)        # [T, N]
+        if row_weight is not None:
+            W = W * row_weight.to(device=dev, dtype=W.dtype)
         maxn = int(min(2 ** (D + 1) - 1, 2 * max(N, 1) + 1))
         feature = torch.full((Tn, maxn), -1, dtype=torch.int32, device=dev)
         thresh = torch.zeros(Tn, maxn, dtype=torch.float32, device=dev)
@@ -344,10 +349,19 @@ class DecisionTreeClassifier(_TreeEstimatorBase):
         X, y, K = self._prep(table)
         return self.fit_tensors(X, y, K)
 
-    def fit_tensors(self, X, y, K) -> DecisionTreeClassificationModel:
+    def fit_tensors(self, X, y, K, thresholds=None) -> DecisionTreeClassificationModel:
         b = ForestBuilder(K, 1, self.maxDepth, self.maxBins, self.minInstancesPerNode, self.minInfoGain,
                           self.impurity, "all", bootstrap=False, seed=self.seed)
-        return DecisionTreeClassificationModel(b.fit(X, y), X.shape[1], K, uid=self.uid, device=X.device)
+        return DecisionTreeClassificationModel(b.fit(X, y, thresholds=thresholds), X.shape[1], K, uid=self.uid,
+                                               device=X.device)
+
+    def fit_folds(self, X, y, K, masks: torch.Tensor) -> List["DecisionTreeClassificationModel"]:
+        """One tree per fold (``masks`` [k, N]: 1 = training row of fold f), all grown together."""
+        b = ForestBuilder(K, masks.shape[0], self.maxDepth, self.maxBins, self.minInstancesPerNode, self.minInfoGain,
+                          self.impurity, "all", bootstrap=False, seed=self.seed)
+        arrs = b.fit(X, y, row_weight=masks)
+        return [DecisionTreeClassificationModel(_slice_arrays(arrs, f, f + 1), X.shape[1], K, uid=self.uid,
+                                                device=X.device) for f in range(masks.shape[0])]
 
 
 class RandomForestClassifier(_TreeEstimatorBase):
@@ -406,6 +420,26 @@ class RandomForestClassifier(_TreeEstimatorBase):
                 ckpt.save(done, _arrays_state(merged), {"trees": done})
         arrs = _concat_arrays(parts) if len(parts) > 1 else parts[0]
         return RandomForestClassificationModel(arrs.to(X.device), X.shape[1], K, uid=self.uid, device=X.device)
+
+    def fit_folds(self, X, y, K, masks: torch.Tensor) -> List["RandomForestClassificationModel"]:
+        """k forests of numTrees trees (fold f: trees f*T .. f*T+T-1, its own bootstrap / feature
+        streams) grown as ONE level-synchronous build of k*T trees over the shared binned matrix."""
+        if self.subsamplingRate != 1.0:
+            raise NotImplementedError("subsamplingRate != 1.0")
+        T_, k = self.numTrees, masks.shape[0]
+        strategy = self.featureSubsetStrategy
+        if str(strategy).lower() == "auto":
+            strategy = "all" if T_ == 1 else "sqrt"
+        b = ForestBuilder(K, k * T_, self.maxDepth, self.maxBins, self.minInstancesPerNode, self.minInfoGain,
+                          self.impurity, strategy, bootstrap=T_ > 1, seed=self.seed)
+        arrs = b.fit(X, y, row_weight=masks.repeat_interleave(T_, dim=0))
+        return [RandomForestClassificationModel(_slice_arrays(arrs, f * T_, (f + 1) * T_), X.shape[1], K, uid=self.uid,
+                                                device=X.device) for f in range(k)]
+
+
+def _slice_arrays(a: ForestArrays, lo: int, hi: int) -> ForestArrays:
+    return ForestArrays(a.feature[lo:hi], a.threshold[lo:hi], a.left[lo:hi], a.right[lo:hi], a.stats[lo:hi],
+                        a.n_nodes[lo:hi], a.max_depth, None if a.gain is None else a.gain[lo:hi])
 
 
 def _concat_arrays(parts: List[ForestArrays]) -> ForestArrays:

@@ -10,7 +10,10 @@ Spark fits the 5 x 9 = 45 (fold, param map) models one after another
 Here, for LogisticRegression, all 45 fits are ONE batched device optimization
 (``LogisticRegression.fit_many``): each fold is a 0/1 row-weight vector over the
 resident training matrix, so the two GEMMs of every objective evaluation cover
-all 45 models at once.  Other estimators fit per (fold, map) on the device.
+all 45 models at once.  DecisionTree / RandomForest grow the trees of all k folds
+as one level-synchronous forest (fold masks multiply the bootstrap weights; split
+candidates come from the whole CV input, labels never); other estimators fit per
+(fold, map) on the device.
 
 Note on the objective: in the reference the CV evaluator is whatever object was
 last assigned to ``evaluator`` — ``RegressionEvaluator(metricName="mae")``
@@ -116,6 +119,16 @@ class CrossValidator(Estimator):
                 rows = np.nonzero(fold == f)[0]
                 vt = table.take_rows(rows)
                 metrics[mi, f] = ev.evaluate(_with_predictions(m, vt, X[torch.as_tensor(rows, device=dev)]))
+        elif hasattr(est, "fit_folds"):  # trees: every fold's tree(s) in one lock-step build
+            dev = resolve_device(est.device)
+            X, y, K = est._prep(table)
+            fold_t = torch.as_tensor(fold, device=dev)
+            masks = torch.stack([(fold_t != f).float() for f in range(k)])
+            for mi, pm in enumerate(maps):
+                for f, m in enumerate(est.copy(pm).fit_folds(X, y, K, masks)):
+                    rows = np.nonzero(fold == f)[0]
+                    vt = table.take_rows(rows)
+                    metrics[mi, f] = ev.evaluate(_with_predictions(m, vt, X[torch.as_tensor(rows, device=dev)]))
         else:
             for f in range(k):
                 tr = table.take_rows(np.nonzero(fold != f)[0])

@@ -182,6 +182,15 @@ PYBIND11_MODULE(_har_native, m) {
   });
 
   m.def("head_fused_blocks", &har_head_fused_blocks);
+  m.def("mlp_fwd_head_grid", &har_mlp_fwd_head_grid);
+  m.def("mlp_fwd_head", [](u X, int K0, u W0, u b0, u W1, u b1, int H, u Wo, u bo, u labels, int B, int C,
+                           float scale, u h1, u dact, u slab, u block_loss, u block_correct, u stream) {
+    check(har_mlp_fwd_head(P<const uint16_t>(X), K0, P<const uint16_t>(W0), P<const float>(b0),
+                           P<const uint16_t>(W1), P<const float>(b1), H, P<const uint16_t>(Wo), P<const float>(bo),
+                           P<const int32_t>(labels), B, C, scale, P<uint16_t>(h1), P<uint16_t>(dact), P<float>(slab),
+                           P<float>(block_loss), P<int32_t>(block_correct), S(stream)),
+          "mlp_fwd_head");
+  });
   m.def("head_fused", [](u H, u W, u bias, u labels, int B, int D, int C, float scale, u dlogits, u dH, u block_loss,
                          u block_correct, u stream) {
     check(har_head_fused(P<const uint16_t>(H), P<const uint16_t>(W), P<const float>(bias), P<const int32_t>(labels),

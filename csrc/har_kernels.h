@@ -54,6 +54,17 @@ int har_head_fused(const uint16_t* H, const uint16_t* W, const float* bias, cons
                    hipStream_t s);
 int har_head_fused_blocks(int B);
 
+// Fused 2-hidden-layer MLP forward + head + head weight gradient (mlp_fused.hip):
+// X [B][K0] bf16 (K0 = 32/64), W0 [H][K0], W1 [H][H], Wo [>=16][H] bf16 (H = 128/256),
+// fp32 biases, C <= 16 classes, B % 16 == 0.  Writes h1 and dact2 = (dz . Wo) * (h2 > 0)
+// ([B][H] bf16), per-workgroup slabs [grid][16*H + 16] (dWout rows 0..15, dbout 0..15)
+// and per-workgroup loss / #correct.  Grid size: har_mlp_fwd_head_grid(B).
+int har_mlp_fwd_head(const uint16_t* X, int K0, const uint16_t* W0, const float* b0, const uint16_t* W1,
+                     const float* b1, int H, const uint16_t* Wo, const float* bo, const int32_t* labels, int B,
+                     int C, float scale, uint16_t* h1, uint16_t* dact, float* slab, float* block_loss,
+                     int32_t* block_correct, hipStream_t s);
+int har_mlp_fwd_head_grid(int B);
+
 // dst[g*n + i] = sum of slabs[s*n + i] over the g-th group of ceil(S/G) slabs (deterministic).
 // A non-null tick is incremented once by the first workgroup (the optimizer step counter).
 int har_reduce_slabs_grouped(const float* slabs, int S, int64_t n, int64_t lds, float* dst, int G, int64_t ldd,

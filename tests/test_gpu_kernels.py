@@ -268,3 +268,43 @@ def test_column_stats_and_binning(cuda):
     thr = T.find_thresholds(X.cpu().numpy(), 32)
     b = stats.bin_features(X, thr).cpu()
     assert torch.equal(b, torch.from_numpy(T.bin_features(X.cpu().numpy(), thr)))
+
+
+@pytest.mark.parametrize("H,F", [(256, 43), (128, 20)])
+def test_mlp_fused_fwd_head_matches_unfused(cuda, H, F):
+    """mlp_fused.hip (fwd L1 + fwd L2 + head + dWout/dbout in one kernel) against the unfused
+    kernel chain: same h1 / dact2 / reduced gradients / loss up to bf16 summation-order noise."""
+    from har.models.mlp import MLPEngine, pad_input_bf16
+
+    B = 4096
+    layers = [F, H, H, 6]
+    a = MLPEngine(layers, B, cuda, lr=1e-3, seed=5)
+    b = MLPEngine(layers, B, cuda, lr=1e-3, seed=5)
+    b.fused_ok = False
+    assert a.fused_ok
+    g = torch.Generator(device=cuda).manual_seed(11)
+    X = pad_input_bf16(torch.randn(B, F, device=cuda, generator=g), a.layout.in_pad)
+    y = torch.randint(0, 6, (B,), device=cuda, generator=g).to(torch.int32)
+    for e in (a, b):
+        e.forward_backward_native(X, y, 1.0 / B)
+        e.reduce_grads_native()
+    torch.cuda.synchronize()
+    assert a.last_fused and not b.last_fused
+    torch.testing.assert_close(a.acts[1].float(), b.acts[1].float(), rtol=2e-2, atol=2e-2)
+    da, db = a.dbuf[1][: B * H].float(), b.dbuf[1][: B * H].float()
+    assert (da - db).norm() / db.norm() < 2e-2
+    L = a.layout
+    for s in L.segments:
+        ga, gb = L.view(a.G, s.name), L.view(b.G, s.name)
+        rel = float((ga - gb).norm() / gb.norm().clamp_min(1e-12))
+        assert rel < 2e-2, f"{s.name}: {rel:.3e}"
+    la, ca = a.last_loss_and_correct()
+    lb, cb = b.last_loss_and_correct()
+    assert abs(la - lb) / lb < 1e-3 and abs(ca - cb) <= 2
+    # full steps: parameters track the unfused engine; a batch that is not a multiple of 16 falls back
+    for _ in range(3):
+        a.train_step(X, y, B)
+        b.train_step(X, y, B)
+    torch.testing.assert_close(a.P, b.P, rtol=0, atol=5e-4)
+    a.forward_backward_native(X[:4090], y[:4090], 1.0 / 4090)
+    assert not a.last_fused

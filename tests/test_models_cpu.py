@@ -173,3 +173,34 @@ def test_mlp_flat_layout():
     assert float(L.view(eng.P, "W0")[:, 43:].abs().max()) == 0.0
     assert float(L.view(eng.P, "Wout")[6:].abs().max()) == 0.0
     assert all(s.offset % 64 == 0 for s in L.segments)
+
+
+def test_tree_cv_folds_batched_equal_per_fold():
+    """The fold-batched build (fold masks x bootstrap weights, one lock-step forest) gives, for
+    a decision tree, exactly the tree fitted on that fold's rows with the same split candidates."""
+    from har.data.split import kfold_ids
+
+    X, y = _blobs(900, 8, 3, seed=4)
+    fold = torch.as_tensor(kfold_ids(900, 3, 7))
+    masks = torch.stack([(fold != f).float() for f in range(3)])
+    thr = T.find_thresholds(X.numpy(), 32)
+    dt = DecisionTreeClassifier(maxDepth=4, device="cpu")
+    batched = dt.fit_folds(X, y, 3, masks)
+    for f in range(3):
+        keep = fold != f
+        single = dt.fit_tensors(X[keep], y[keep], 3, thresholds=thr)
+        assert torch.equal(batched[f].arrs.feature, single.arrs.feature)
+        torch.testing.assert_close(batched[f].predict_raw(X), single.predict_raw(X))
+    rfs = RandomForestClassifier(numTrees=6, maxDepth=4, seed=1, device="cpu").fit_folds(X, y, 3, masks)
+    assert len(rfs) == 3 and all(m.arrs.feature.shape[0] == 6 for m in rfs)
+    assert all(float((m.predict(X) == y).float().mean()) > 0.8 for m in rfs)
+
+
+def test_crossvalidator_trees(wisdm_split):
+    train, test = wisdm_split
+    ev = MulticlassClassificationEvaluator(metricName="accuracy")
+    cv = CrossValidator(estimator=DecisionTreeClassifier(maxDepth=3, device="cpu"),
+                        estimatorParamMaps=ParamGridBuilder().addGrid("maxDepth", [2, 3]).build(), evaluator=ev,
+                        numFolds=5, seed=3).fit(train)
+    assert len(cv.avgMetrics) == 2 and cv.bestIndex == 1 and cv.avgMetrics[1] > 0.6
+    assert _acc(cv, test) > 0.6
