@@ -35,7 +35,7 @@ typedef __attribute__((address_space(3))) s16x4_t lds_s16x4_t;
 typedef __attribute__((ext_vector_type(4))) uint32_t u32x4_t;
 
 constexpr int NCLS = 16;
-constexpr int SCR = 5 * 256;  // per-wave scratch: 4 h2 tiles + 1 dz tile, 16x16 bf16 each
+constexpr int SCR = 3 * 256;  // per-wave scratch: 2 h2 tiles + 1 dz tile, 16x16 bf16 each
 
 // [rows][H + 8] bf16 images (one 16-byte pad per row): the 8-byte A-fragment reads of
 // stages 2/3 (row 16t + lane&15, column 32kc + 4g [+16]) hit bank pair 2(2 row + chunk)
@@ -73,13 +73,27 @@ __global__ __launch_bounds__(256) void mlp_fwd_head_kernel(
   bf16_t* W1s = lds;              // [H][P]
   bf16_t* Wos = W1s + H * P;      // [16][P]
   bf16_t* WoT = Wos + NCLS * P;   // [H][16]
-  bf16_t* scr = WoT + H * NCLS;   // [4][SCR]
+  float* bs = reinterpret_cast<float*>(WoT + H * NCLS);  // b0 [H], b1 [H]
+  bf16_t* scr = reinterpret_cast<bf16_t*>(bs + 2 * H);   // [4][SCR]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int c16 = lane & 15, g = lane >> 4;
 
-  for (int v = tid; v < H * H / 8; v += 256) {
-    const int r = v / (H / 8), c = (v % (H / 8)) * 8;
-    *reinterpret_cast<uint4*>(W1s + r * P + c) = *reinterpret_cast<const uint4*>(W1 + (size_t)r * H + c);
+  // ---- prologue: weights into LDS, 8 16-byte loads in flight per thread ----
+  {
+    constexpr int NV = H * H / 8, PER = 8 * 256;
+    for (int v0 = 0; v0 < NV; v0 += PER) {
+      uint4 buf[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int v = v0 + i * 256 + tid;
+        buf[i] = v < NV ? *reinterpret_cast<const uint4*>(W1 + (size_t)v * 8) : make_uint4(0, 0, 0, 0);
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int v = v0 + i * 256 + tid;
+        if (v < NV) *reinterpret_cast<uint4*>(W1s + (v / (H / 8)) * P + (v % (H / 8)) * 8) = buf[i];
+      }
+    }
   }
   for (int v = tid; v < NCLS * H / 8; v += 256) {
     const int r = v / (H / 8), c = (v % (H / 8)) * 8;
@@ -89,10 +103,22 @@ __global__ __launch_bounds__(256) void mlp_fwd_head_kernel(
     const int cls = e / H, u = e % H;
     WoT[u * NCLS + cls] = Wo[(size_t)cls * H + u];
   }
+  for (int e = tid; e < H; e += 256) {
+    bs[e] = b0[e];
+    bs[H + e] = b1[e];
+  }
+  // W0 A-fragments stay in registers for the whole kernel (no global loads in the loop:
+  // vmcnt is in-order on CDNA, so a load behind the previous tile's stores would wait for them)
+  bf16x8_t w0f[NT][K0C];
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int kc = 0; kc < K0C; ++kc)
+      w0f[t][kc] = *reinterpret_cast<const bf16x8_t*>(W0 + (size_t)(16 * t + c16) * K0 + kc * 32 + g * 8);
   __syncthreads();
 
   bf16_t* sw = scr + wave * SCR;
-  bf16_t* dzs = sw + 4 * 256;
+  bf16_t* dzs = sw + 2 * 256;
   const int tr_off = (4 * g + (c16 >> 2)) * 16 + (c16 & 3) * 4;  // ds_read_b64_tr_b16 lane address in a tile
   f32x4_t acc5[NT];
 #pragma unroll
@@ -105,41 +131,65 @@ __global__ __launch_bounds__(256) void mlp_fwd_head_kernel(
   for (int r = 0; r < 4; ++r) bo_r[r] = (4 * g + r < C) ? bo[4 * g + r] : 0.f;
 
   const int ntiles = B / 16;
-  for (int T = blockIdx.x * 4 + wave; T < ntiles; T += gridDim.x * 4) {
-    const int row = T * 16 + c16;
-    const int y = labels[row];
-    // ---- stage 1: h1^T = W0 . X^T ----
-    bf16x8_t xb[K0C];
+  const int stride = gridDim.x * 4;
+  int T = blockIdx.x * 4 + wave;
+  bf16x8_t xb[K0C];
+  int y = 0;
+  if (T < ntiles) {
 #pragma unroll
     for (int kc = 0; kc < K0C; ++kc)
-      xb[kc] = *reinterpret_cast<const bf16x8_t*>(X + (size_t)row * K0 + kc * 32 + g * 8);
+      xb[kc] = *reinterpret_cast<const bf16x8_t*>(X + (size_t)(T * 16 + c16) * K0 + kc * 32 + g * 8);
+    y = labels[T * 16 + c16];
+  }
+  for (; T < ntiles; T += stride) {
+    const int row = T * 16 + c16;
+    // ---- stage 1: h1^T = W0 . X^T ----
     uint32_t h1p[NT][2];
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
       f32x4_t a = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int kc = 0; kc < K0C; ++kc)
-        a = mma32(*reinterpret_cast<const bf16x8_t*>(W0 + (size_t)(16 * t + c16) * K0 + kc * 32 + g * 8), xb[kc], a);
-      const float4 bb = *reinterpret_cast<const float4*>(b0 + 16 * t + 4 * g);
+      for (int kc = 0; kc < K0C; ++kc) a = mma32(w0f[t][kc], xb[kc], a);
+      const float4 bb = *reinterpret_cast<const float4*>(bs + 16 * t + 4 * g);
       h1p[t][0] = pack2(fmaxf(a[0] + bb.x, 0.f), fmaxf(a[1] + bb.y, 0.f));
       h1p[t][1] = pack2(fmaxf(a[2] + bb.z, 0.f), fmaxf(a[3] + bb.w, 0.f));
       *reinterpret_cast<uint2*>(h1out + (size_t)row * H + 16 * t + 4 * g) = make_uint2(h1p[t][0], h1p[t][1]);
-      __builtin_amdgcn_sched_barrier(0);  // keep the per-tile loads from being hoisted (VGPR pressure)
     }
-    // ---- stage 2: h2^T = W1 . h1^T ----
+    // prefetch the next tile's X rows and labels (issued before this tile's dact2 stores)
+    const int Tn = T + stride;
+    const int yc = y;
+    if (Tn < ntiles) {
+#pragma unroll
+      for (int kc = 0; kc < K0C; ++kc)
+        xb[kc] = *reinterpret_cast<const bf16x8_t*>(X + (size_t)(Tn * 16 + c16) * K0 + kc * 32 + g * 8);
+      y = labels[Tn * 16 + c16];
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    // ---- stage 2: h2^T = W1 . h1^T  (A fragments software-pipelined one tile ahead) ----
     uint32_t h2p[NT][2];
+    uint2 fr[2][KC][2];
+#pragma unroll
+    for (int kc = 0; kc < KC; ++kc) {
+      fr[0][kc][0] = *reinterpret_cast<const uint2*>(W1s + c16 * P + 32 * kc + 4 * g);
+      fr[0][kc][1] = *reinterpret_cast<const uint2*>(W1s + c16 * P + 32 * kc + 16 + 4 * g);
+    }
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
-      const int wr = 16 * t + c16;
+      const int cb = t & 1, nb = cb ^ 1;
+      if (t + 1 < NT) {
+        const int wr = 16 * (t + 1) + c16;
+#pragma unroll
+        for (int kc = 0; kc < KC; ++kc) {
+          fr[nb][kc][0] = *reinterpret_cast<const uint2*>(W1s + wr * P + 32 * kc + 4 * g);
+          fr[nb][kc][1] = *reinterpret_cast<const uint2*>(W1s + wr * P + 32 * kc + 16 + 4 * g);
+        }
+      }
       f32x4_t a = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int kc = 0; kc < KC; ++kc) {
-        const uint2 lo = *reinterpret_cast<const uint2*>(W1s + wr * P + 32 * kc + 4 * g);
-        const uint2 hi = *reinterpret_cast<const uint2*>(W1s + wr * P + 32 * kc + 16 + 4 * g);
-        a = mma32(cat8(lo.x, lo.y, hi.x, hi.y),
+      for (int kc = 0; kc < KC; ++kc)
+        a = mma32(cat8(fr[cb][kc][0].x, fr[cb][kc][0].y, fr[cb][kc][1].x, fr[cb][kc][1].y),
                   cat8(h1p[2 * kc][0], h1p[2 * kc][1], h1p[2 * kc + 1][0], h1p[2 * kc + 1][1]), a);
-      }
-      const float4 bb = *reinterpret_cast<const float4*>(b1 + 16 * t + 4 * g);
+      const float4 bb = *reinterpret_cast<const float4*>(bs + H + 16 * t + 4 * g);
       h2p[t][0] = pack2(fmaxf(a[0] + bb.x, 0.f), fmaxf(a[1] + bb.y, 0.f));
       h2p[t][1] = pack2(fmaxf(a[2] + bb.z, 0.f), fmaxf(a[3] + bb.w, 0.f));
       __builtin_amdgcn_sched_barrier(0);
@@ -181,16 +231,17 @@ __global__ __launch_bounds__(256) void mlp_fwd_head_kernel(
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int cls = 4 * g + r;
-      dl[r] = cls < C ? (e[r] * inv - (cls == y ? 1.f : 0.f)) * scale : 0.f;
-      if (cls == y) lsum += lse - zz[r];
+      dl[r] = cls < C ? (e[r] * inv - (cls == yc ? 1.f : 0.f)) * scale : 0.f;
+      if (cls == yc) lsum += lse - zz[r];
     }
-    if (g == 0 && amx == y) ncorr += 1;
+    if (g == 0 && amx == yc) ncorr += 1;
     const uint32_t dz01 = pack2(dl[0], dl[1]), dz23 = pack2(dl[2], dl[3]);
     dbo[0] += __uint_as_float(dz01 << 16);
     dbo[1] += __uint_as_float(dz01 & 0xffff0000u);
     dbo[2] += __uint_as_float(dz23 << 16);
     dbo[3] += __uint_as_float(dz23 & 0xffff0000u);
     const s16x4_t dzv = __builtin_bit_cast(s16x4_t, make_uint2(dz01, dz23));
+    __builtin_amdgcn_sched_barrier(0);
     // ---- stage 4: dact2^T = Wout^T . dz^T, masked by relu'(h2) ----
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
@@ -200,26 +251,27 @@ __global__ __launch_bounds__(256) void mlp_fwd_head_kernel(
       const float d0 = bf_pos(m0) ? d[0] : 0.f, d1 = bf_pos(m0 >> 16) ? d[1] : 0.f;
       const float d2 = bf_pos(m1) ? d[2] : 0.f, d3 = bf_pos(m1 >> 16) ? d[3] : 0.f;
       *reinterpret_cast<uint2*>(dact + (size_t)row * H + 16 * t + 4 * g) = make_uint2(pack2(d0, d1), pack2(d2, d3));
-      __builtin_amdgcn_sched_barrier(0);
     }
+    __builtin_amdgcn_sched_barrier(0);
     // ---- stage 5: dWout^T += h2^T . dz over the tile's 16 rows ----
     *reinterpret_cast<uint2*>(dzs + c16 * 16 + 4 * g) = make_uint2(dz01, dz23);
 #pragma unroll
-    for (int t0 = 0; t0 < NT; t0 += 4) {
+    for (int t0 = 0; t0 < NT; t0 += 2) {
 #pragma unroll
-      for (int tt = 0; tt < 4; ++tt)
+      for (int tt = 0; tt < 2; ++tt)
         *reinterpret_cast<uint2*>(sw + tt * 256 + c16 * 16 + 4 * g) = make_uint2(h2p[t0 + tt][0], h2p[t0 + tt][1]);
       __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's tiles are in LDS
       __builtin_amdgcn_wave_barrier();
       const s16x4_t bz = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(dzs + tr_off));
 #pragma unroll
-      for (int tt = 0; tt < 4; ++tt) {
+      for (int tt = 0; tt < 2; ++tt) {
         const s16x4_t ah = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(sw + tt * 256 + tr_off));
         acc5[t0 + tt] = mma16(ah, bz, acc5[t0 + tt]);
       }
       __builtin_amdgcn_s_waitcnt(0xc07f);  // reads done before the tiles are overwritten
       __builtin_amdgcn_wave_barrier();
     }
+    __builtin_amdgcn_sched_barrier(0);
   }
 
   // ---- per-workgroup reduction (fixed order) into this workgroup's slab ----
@@ -256,7 +308,7 @@ template <int H, int K0>
 int launch(const bf16_t* X, const bf16_t* W0, const float* b0, const bf16_t* W1, const float* b1,
            const bf16_t* Wo, const float* bo, const int32_t* labels, int B, int C, float scale, bf16_t* h1,
            bf16_t* dact, float* slab, float* block_loss, int32_t* block_correct, int nwg, hipStream_t s) {
-  const size_t lds = ((size_t)(H + NCLS) * Pitch<H>::v + NCLS * H + 4 * SCR) * sizeof(bf16_t);
+  const size_t lds = ((size_t)(H + NCLS) * Pitch<H>::v + NCLS * H + 4 * SCR) * sizeof(bf16_t) + 2 * H * sizeof(float);
   mlp_fwd_head_kernel<H, K0><<<nwg, 256, lds, s>>>(X, W0, b0, W1, b1, Wo, bo, labels, B, C, scale, h1, dact, slab,
                                                    block_loss, block_correct);
   HAR_CHECK_LAUNCH();
