@@ -60,6 +60,17 @@ __device__ __forceinline__ bf16x8_t cat8(uint32_t a, uint32_t b, uint32_t c, uin
 
 __device__ __forceinline__ bool bf_pos(uint32_t h) { return (h & 0x8000u) == 0 && (h & 0xffffu) != 0; }
 
+// An empty asm that consumes N loaded vectors: the compiler must issue all N loads before it
+// (one vmcnt wait for the batch) instead of sinking each load next to its LDS store.
+template <int N> __device__ __forceinline__ void hold_all(u32x4_t (&b)[N]);
+template <> __device__ __forceinline__ void hold_all<8>(u32x4_t (&b)[8]) {
+  asm volatile("" ::"v"(b[0]), "v"(b[1]), "v"(b[2]), "v"(b[3]), "v"(b[4]), "v"(b[5]), "v"(b[6]), "v"(b[7]));
+}
+template <> __device__ __forceinline__ void hold_all<16>(u32x4_t (&b)[16]) {
+  asm volatile("" ::"v"(b[0]), "v"(b[1]), "v"(b[2]), "v"(b[3]), "v"(b[4]), "v"(b[5]), "v"(b[6]), "v"(b[7]),
+               "v"(b[8]), "v"(b[9]), "v"(b[10]), "v"(b[11]), "v"(b[12]), "v"(b[13]), "v"(b[14]), "v"(b[15]));
+}
+
 template <int H, int K0>
 __global__ __launch_bounds__(256) void mlp_fwd_head_kernel(
     const bf16_t* __restrict__ X, const bf16_t* __restrict__ W0, const float* __restrict__ b0,
@@ -78,35 +89,7 @@ __global__ __launch_bounds__(256) void mlp_fwd_head_kernel(
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int c16 = lane & 15, g = lane >> 4;
 
-  // ---- prologue: weights into LDS, 8 16-byte loads in flight per thread ----
-  {
-    constexpr int NV = H * H / 8, PER = 8 * 256;
-    for (int v0 = 0; v0 < NV; v0 += PER) {
-      uint4 buf[8];
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const int v = v0 + i * 256 + tid;
-        buf[i] = v < NV ? *reinterpret_cast<const uint4*>(W1 + (size_t)v * 8) : make_uint4(0, 0, 0, 0);
-      }
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const int v = v0 + i * 256 + tid;
-        if (v < NV) *reinterpret_cast<uint4*>(W1s + (v / (H / 8)) * P + (v % (H / 8)) * 8) = buf[i];
-      }
-    }
-  }
-  for (int v = tid; v < NCLS * H / 8; v += 256) {
-    const int r = v / (H / 8), c = (v % (H / 8)) * 8;
-    *reinterpret_cast<uint4*>(Wos + r * P + c) = *reinterpret_cast<const uint4*>(Wo + (size_t)r * H + c);
-  }
-  for (int e = tid; e < NCLS * H; e += 256) {
-    const int cls = e / H, u = e % H;
-    WoT[u * NCLS + cls] = Wo[(size_t)cls * H + u];
-  }
-  for (int e = tid; e < H; e += 256) {
-    bs[e] = b0[e];
-    bs[H + e] = b1[e];
-  }
+  // ---- prologue: every global load of the weights is issued before the first wait ----
   // W0 A-fragments stay in registers for the whole kernel (no global loads in the loop:
   // vmcnt is in-order on CDNA, so a load behind the previous tile's stores would wait for them)
   bf16x8_t w0f[NT][K0C];
@@ -115,6 +98,44 @@ __global__ __launch_bounds__(256) void mlp_fwd_head_kernel(
 #pragma unroll
     for (int kc = 0; kc < K0C; ++kc)
       w0f[t][kc] = *reinterpret_cast<const bf16x8_t*>(W0 + (size_t)(16 * t + c16) * K0 + kc * 32 + g * 8);
+  {
+    constexpr int NV = H * H / 8, NB = NV / 256 < 16 ? NV / 256 : 16;  // W1 16-byte vectors in flight
+    static_assert(NV % (NB * 256) == 0, "W1 staging: whole batches");
+    constexpr int NO = NCLS * H / 8;        // Wout rows 0..15
+    uint4 wo[(NO + 255) / 256];
+#pragma unroll
+    for (int i = 0; i < (NO + 255) / 256; ++i) {
+      const int v = i * 256 + tid;
+      wo[i] = v < NO ? *reinterpret_cast<const uint4*>(Wo + (size_t)v * 8) : make_uint4(0, 0, 0, 0);
+    }
+    const float bv0 = tid < H ? b0[tid] : 0.f, bv1 = tid < H ? b1[tid] : 0.f;
+#pragma unroll 1
+    for (int v0 = 0; v0 < NV; v0 += NB * 256) {
+      u32x4_t buf[NB];
+#pragma unroll
+      for (int i = 0; i < NB; ++i) buf[i] = *reinterpret_cast<const u32x4_t*>(W1 + (size_t)(v0 + i * 256 + tid) * 8);
+      hold_all<NB>(buf);  // every load issued before the first wait (else: load / wait / store x NB)
+#pragma unroll
+      for (int i = 0; i < NB; ++i) {
+        const int v = v0 + i * 256 + tid;
+        *reinterpret_cast<u32x4_t*>(W1s + (v / (H / 8)) * P + (v % (H / 8)) * 8) = buf[i];
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < (NO + 255) / 256; ++i) {
+      const int v = i * 256 + tid;
+      if (v < NO) *reinterpret_cast<uint4*>(Wos + (v / (H / 8)) * P + (v % (H / 8)) * 8) = wo[i];
+    }
+    if (tid < H) {
+      bs[tid] = bv0;
+      bs[H + tid] = bv1;
+    }
+  }
+  __syncthreads();
+  for (int e = tid; e < NCLS * H; e += 256) {  // Wout^T image from the LDS copy
+    const int cls = e / H, u = e % H;
+    WoT[u * NCLS + cls] = Wos[cls * P + u];
+  }
   __syncthreads();
 
   bf16_t* sw = scr + wave * SCR;
@@ -141,6 +162,10 @@ __global__ __launch_bounds__(256) void mlp_fwd_head_kernel(
       xb[kc] = *reinterpret_cast<const bf16x8_t*>(X + (size_t)(T * 16 + c16) * K0 + kc * 32 + g * 8);
     y = labels[T * 16 + c16];
   }
+  // drain the first prefetch here: otherwise the loop-header wait the compiler derives from
+  // this path (vmcnt(0)) also applies on the back edge, where it would wait for every
+  // dact2 store of the previous tile
+  __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0)
   for (; T < ntiles; T += stride) {
     const int row = T * 16 + c16;
     // ---- stage 1: h1^T = W0 . X^T ----

@@ -22,7 +22,8 @@ def main():
     X = pad_input_bf16(torch.randn(Bmax, 43, device=dev, generator=g), eng.layout.in_pad)
     y = torch.randint(0, 6, (Bmax,), device=dev, generator=g).to(torch.int32)
     mod, L = _native.kernels(), eng.layout
-    for B in (1024, 4096, 16384, 32768, 65536, 131072, 262144):
+    sizes = [int(b) for b in os.environ.get("PROBE_B", "1024,4096,16384,32768,65536,131072,262144").split(",")]
+    for B in sizes:
         def run():
             mod.mlp_fwd_head(X.data_ptr(), L.in_pad, eng._w(eng.Pb, "W0").data_ptr(), eng._w(eng.P, "b0").data_ptr(),
                              eng._w(eng.Pb, "W1").data_ptr(), eng._w(eng.P, "b1").data_ptr(), H,
