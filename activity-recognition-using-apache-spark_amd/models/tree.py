@@ -82,7 +82,7 @@ class ForestBuilder:
     def __init__(self, num_classes: int, num_trees: int = 1, max_depth: int = 5, max_bins: int = 32,
                  min_instances: int = 1, min_info_gain: float = 0.0, impurity: str = "gini",
                  feature_subset: str = "auto", bootstrap: Optional[bool] = None, seed: int = 0,
-                 allreduce=None, tree_offset: int = 0):
+                 allreduce=None, tree_offset: int = 0, owner=None):
         if max_bins > 64:
             raise ValueError("maxBins <= 64 (one lane per bin in the split kernel)")
         self.K, self.T, self.D = num_classes, num_trees, max_depth
@@ -93,6 +93,11 @@ class ForestBuilder:
         self.seed = seed
         self.allreduce = allreduce  # optional callable(tensor) -> None (DP histogram reduction)
         self.tree_offset = tree_offset  # global id of tree 0 (bootstrap / feature-subset streams)
+        # optional owner-computes communicator (reduce_scatter / all_gather / allreduce); when
+        # given, level histograms are reduce-scattered by node owner instead of all-reduced
+        self.owner = owner
+        if owner is not None and allreduce is None:
+            self.allreduce = owner.allreduce
 
     def prepare(self, X: torch.Tensor, thresholds=None):
         from ..ops.stats import bin_features
@@ -184,12 +189,17 @@ class ForestBuilder:
             if use_native:
                 res = T.hist_split_native(self.bins, self.nbins, y32, rows, row_w, starts, counts, feats, K,
                                           self.max_bins, self.min_inst, self.min_gain, self.impurity,
-                                          allreduce=self.allreduce)
+                                          allreduce=None if self.owner is not None else self.allreduce,
+                                          owner=self.owner)
             else:
                 hist = T.level_histogram(self.bins, y32, rows, row_w, keys, A, feats, K, self.max_bins)
-                if self.allreduce is not None:
-                    self.allreduce(hist)
-                res = T.split_from_hist(hist, feats, self.nbins, self.min_inst, self.min_gain, self.impurity)
+                if self.owner is not None:
+                    res = T.split_owner(hist, feats, K, self.owner, lambda h, a0, a1: T.split_from_hist(
+                        h, feats[a0:a1], self.nbins, self.min_inst, self.min_gain, self.impurity))
+                else:
+                    if self.allreduce is not None:
+                        self.allreduce(hist)
+                    res = T.split_from_hist(hist, feats, self.nbins, self.min_inst, self.min_gain, self.impurity)
             do_split = (res.gain > 0) & torch.isfinite(res.gain)
             ds = do_split.cpu().numpy()
             if not ds.any():
@@ -382,7 +392,7 @@ class RandomForestClassifier(_TreeEstimatorBase):
         return self.fit_tensors(X, y, K)
 
     def fit_tensors(self, X, y, K, allreduce=None, row_offset: int = 0, thresholds=None,
-                    tree_wave: int = 0, checkpoint_dir: Optional[str] = None, rank: int = 0):
+                    tree_wave: int = 0, checkpoint_dir: Optional[str] = None, rank: int = 0, owner=None):
         """Grow the forest (all trees in lock step, or in waves of ``tree_wave`` trees —
         each wave checkpointed under ``checkpoint_dir`` and skipped on resume).  Trees
         are keyed by their global id, so a waved forest equals the one-shot forest."""
@@ -411,7 +421,7 @@ class RandomForestClassifier(_TreeEstimatorBase):
             nt = min(wave, self.numTrees - done)
             b = ForestBuilder(K, nt, self.maxDepth, self.maxBins, self.minInstancesPerNode, self.minInfoGain,
                               self.impurity, strategy, bootstrap=self.numTrees > 1, seed=self.seed,
-                              allreduce=allreduce, tree_offset=done)
+                              allreduce=allreduce, tree_offset=done, owner=owner)
             parts.append(b.fit(X, y, row_offset=row_offset, thresholds=thresholds))
             done += nt
             if ckpt is not None and done < self.numTrees:

@@ -134,11 +134,42 @@ def split_from_hist(hist, feats, nbins_feat, min_instances, min_info_gain, impur
     return LevelResult(gain=bg.float(), feat=bf.int(), bin=b.int(), left=bl.float(), total=total.float())
 
 
+def pack_level(res: LevelResult) -> torch.Tensor:
+    """[A, 3 + 2K] fp32 rows (gain, feature, bin, left, total) — feature/bin ids are exact
+    in fp32 (< 2^24); one tensor so the winners travel in ONE all-gather."""
+    return torch.cat([res.gain[:, None].float(), res.feat[:, None].float(), res.bin[:, None].float(),
+                      res.left.float(), res.total.float()], 1)
+
+
+def unpack_level(t: torch.Tensor, K: int) -> LevelResult:
+    return LevelResult(gain=t[:, 0].contiguous(), feat=t[:, 1].to(torch.int32), bin=t[:, 2].to(torch.int32),
+                       left=t[:, 3:3 + K].contiguous(), total=t[:, 3 + K:3 + 2 * K].contiguous())
+
+
+def split_owner(hist: torch.Tensor, feats: torch.Tensor, K: int, owner, split_fn) -> LevelResult:
+    """Owner-computes split search (data parallel): ``owner.reduce_scatter``
+    sums the per-node histograms across ranks and leaves each rank the node slice
+    ``[a0, a1)`` it owns; the rank searches splits for those nodes only
+    (``split_fn(local_hist, a0, a1)``) and ``owner.all_gather`` gives every rank all the
+    winners.  Traffic per rank: (P-1)/P x histogram + a few bytes per node, vs.
+    2 (P-1)/P x histogram for the all-reduce variant, and the split search is not
+    repeated on every rank.  Spark's equivalent is ``reduceByKey(node)`` followed by
+    ``collectAsMap`` (``Main/main.py:300,481``)."""
+    A = hist.shape[0]
+    local, a0, a1 = owner.reduce_scatter(hist)
+    if a1 > a0:
+        packed = pack_level(split_fn(local[: a1 - a0], a0, a1))
+    else:
+        packed = torch.zeros(0, 3 + 2 * K, dtype=torch.float32, device=hist.device)
+    return unpack_level(owner.all_gather(packed, A), K)
+
+
 def hist_split_native(bins, nbins_feat, label, rows, row_w, node_start, node_count, feats, K, max_bins,
-                      min_instances, min_info_gain, impurity, allreduce=None) -> LevelResult:
-    """Fused LDS histogram + split on one device; with ``allreduce`` (data parallel) the
-    kernel runs twice: histogram-only into a [A, m, bins, K] buffer, one RCCL all-reduce
-    of it, then split search from the summed histograms."""
+                      min_instances, min_info_gain, impurity, allreduce=None, owner=None) -> LevelResult:
+    """Fused LDS histogram + split on one device; in data parallel the kernel runs twice:
+    histogram-only into a [A, m, bins, K] buffer, then either one RCCL all-reduce of it and
+    split search for every node (``allreduce``), or a reduce-scatter by node owner, split
+    search for the owned nodes and an all-gather of the winners (``owner``)."""
     A, m = feats.shape
     F, N = bins.shape
     fc = max(1, min(m, LDS_BUDGET // (max_bins * K * 4)))
@@ -164,6 +195,26 @@ def hist_split_native(bins, nbins_feat, label, rows, row_w, node_start, node_cou
     if blocks < 1024 and max_rows > 4096:
         row_chunks = int(min((1024 + blocks - 1) // blocks, (max_rows + 2047) // 2048))
     st = _native.stream_ptr()
+    if owner is not None:
+        ghist = (torch.zeros if row_chunks > 1 else torch.empty)(A, m, max_bins, K, dtype=torch.float32, device=dev)
+        mod.tree_hist_split(*args, 1, ghist.data_ptr(), row_chunks, st)
+
+        def split_slice(local, a0, a1):
+            n = a1 - a0
+            g = torch.empty(n * chunks, dtype=torch.float32, device=dev)
+            f = torch.empty(n * chunks, dtype=torch.int32, device=dev)
+            b = torch.empty(n * chunks, dtype=torch.int32, device=dev)
+            lf = torch.empty(n * chunks, K, dtype=torch.float32, device=dev)
+            tot = torch.empty(n, K, dtype=torch.float32, device=dev)
+            loc = local.contiguous()
+            sl = [bins.data_ptr(), N, F, nbins_feat.data_ptr(), rows.data_ptr(), row_w.data_ptr(),
+                  node_start.data_ptr() + 4 * a0, node_count.data_ptr() + 4 * a0, n, feats.data_ptr() + 4 * a0 * m,
+                  m, fc, label.data_ptr(), K, max_bins, float(min_instances), float(min_info_gain), impurity,
+                  g.data_ptr(), f.data_ptr(), b.data_ptr(), lf.data_ptr(), tot.data_ptr()]
+            mod.tree_hist_split(*sl, 2, loc.data_ptr(), 1, st)
+            return _best_chunk(g, f, b, lf, tot, n, chunks, K)
+
+        return split_owner(ghist, feats, K, owner, split_slice)
     if allreduce is None and row_chunks == 1:
         mod.tree_hist_split(*args, 0, 0, 1, st)
     else:
@@ -172,9 +223,13 @@ def hist_split_native(bins, nbins_feat, label, rows, row_w, node_start, node_cou
         if allreduce is not None:
             allreduce(ghist)
         mod.tree_hist_split(*args, 2, ghist.data_ptr(), 1, st)
+    return _best_chunk(gain, feat, bin_, left, total, A, chunks, K)
+
+
+def _best_chunk(gain, feat, bin_, left, total, A, chunks, K) -> LevelResult:
     gain, feat, bin_, left = gain.view(A, chunks), feat.view(A, chunks), bin_.view(A, chunks), left.view(A, chunks, K)
     best = torch.argmax(gain, dim=1)  # first max -> lowest chunk (lowest feature slot) on ties
-    ar = torch.arange(A, device=dev)
+    ar = torch.arange(A, device=gain.device)
     return LevelResult(gain=gain[ar, best], feat=feat[ar, best], bin=bin_[ar, best], left=left[ar, best],
                        total=total)
 

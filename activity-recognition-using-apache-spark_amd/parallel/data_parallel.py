@@ -9,9 +9,12 @@ combines are RCCL collectives over xGMI:
 * LogisticRegression: one flat ``all_reduce`` of [loss | dW | db] per objective
   evaluation (~75 KB per model: latency-bound, so one bucket, never per tensor);
 * RandomForest: per level, the (tree, node, feature, bin, class) histograms are
-  summed with one ``all_reduce`` and every rank selects the same splits
-  (``reduce_scatter`` by node owner + ``all_gather`` of the winners is the
-  bandwidth-optimal variant for very large forests);
+  either summed with one ``all_reduce`` (every rank then searches every split), or
+  — the default, ``NodeOwner`` — ``reduce_scatter``-ed by node owner: each rank sums
+  and searches only its slice of the nodes and one ``all_gather`` of the packed
+  winners (3 + 2K floats per node) gives everybody the level's splits.  Half the
+  histogram bytes on the wire and no redundant split search (Spark:
+  ``reduceByKey(node)`` + ``collectAsMap``, SURVEY.md M9);
 * MLP: fp32 gradient buckets (>= 64 KB, contiguous layer ranges of the flat buffer) all-reduced
   asynchronously while backward continues (``MLPEngine.train_step_overlapped``).
 
@@ -72,8 +75,54 @@ def global_thresholds(X_shard: torch.Tensor, max_bins: int, ctx: DistContext, sa
     return out[0]
 
 
-def fit_forest_dp(estimator, X_shard, y_shard, num_classes: int, row_offset: int, ctx: DistContext):
+class NodeOwner:
+    """Owner-computes reduction of per-node tensors ``[A, ...]``: node ``a`` belongs to
+    rank ``a // ceil(A / P)`` (contiguous slices, so a slice is one contiguous buffer)."""
+
+    def __init__(self, ctx: DistContext):
+        self.ctx = ctx
+        self.allreduce = allreduce_sum(ctx) or (lambda t: None)
+
+    def _dev(self, t):
+        # RCCL needs device tensors; host tensors are staged through HBM
+        return t if (t.is_cuda or self.ctx.backend != "nccl") else t.to(self.ctx.device)
+
+    def reduce_scatter(self, hist: torch.Tensor):
+        P, r = self.ctx.world_size, self.ctx.rank
+        A = hist.shape[0]
+        S = max(1, -(-A // P))
+        a0, a1 = min(A, r * S), min(A, (r + 1) * S)
+        if P == 1:
+            return hist, 0, A
+        flat = hist.reshape(A, -1)
+        src = torch.zeros(P * S, flat.shape[1], dtype=flat.dtype, device=flat.device)
+        src[:A] = flat
+        src = self._dev(src)
+        out = torch.empty(S, flat.shape[1], dtype=flat.dtype, device=src.device)
+        dist.reduce_scatter_tensor(out, src, group=self.ctx.group)
+        out = out.to(hist.device)
+        return out.view(S, *hist.shape[1:]), a0, a1
+
+    def all_gather(self, local: torch.Tensor, A: int) -> torch.Tensor:
+        P = self.ctx.world_size
+        if P == 1:
+            return local
+        S = max(1, -(-A // P))
+        buf = torch.zeros(S, *local.shape[1:], dtype=local.dtype, device=local.device)
+        buf[: local.shape[0]] = local
+        buf = self._dev(buf)
+        out = torch.empty(P * S, *local.shape[1:], dtype=local.dtype, device=buf.device)
+        dist.all_gather_into_tensor(out, buf, group=self.ctx.group)
+        return out[:A].to(local.device)
+
+
+def fit_forest_dp(estimator, X_shard, y_shard, num_classes: int, row_offset: int, ctx: DistContext,
+                  reduction: str = "owner"):
+    """``reduction``: ``owner`` (reduce-scatter + all-gather of winners) or ``allreduce``."""
     thr = global_thresholds(X_shard, estimator.maxBins, ctx, seed=estimator.seed)
+    if reduction == "owner" and ctx.is_distributed:
+        return estimator.fit_tensors(X_shard, y_shard, num_classes, row_offset=row_offset, thresholds=thr,
+                                     owner=NodeOwner(ctx))
     return estimator.fit_tensors(X_shard, y_shard, num_classes, allreduce=allreduce_sum(ctx), row_offset=row_offset,
                                  thresholds=thr)
 

@@ -12,7 +12,9 @@ xGMI, weak scaling (fixed per-GPU work).  Every line is ONE JSON record.
                     class-conditional Gaussians generated on device); random-init weights.
 ``--config rf``     (config 2) RandomForest 100 trees x depth 10, 32 bins, on
                     featurized synthetic 3-axis windows (43 WISDM features);
-                    step = one whole forest fit (histogram all-reduce per level in DP).
+                    step = one whole forest fit (per level in DP: histograms reduce-scattered
+                    by node owner, winners all-gathered; ``--rf-reduce allreduce`` for the
+                    all-reduce variant).
 ``--config stream`` (config 4) raw synthetic 3-axis 20 Hz stream (1B samples per
                     8 GPUs, i.e. 125M per GPU resident in HBM) -> HIP window featurizer
                     -> MLP training step; step = featurize + train ``--batch`` windows.
@@ -176,9 +178,11 @@ def bench_rf(args, ctx, nine_axis=False):
     thr = dp.global_thresholds(X, 32, ctx, seed=7)
     model = {}
 
+    owner = dp.NodeOwner(ctx) if (args.rf_reduce == "owner" and ctx.is_distributed) else None
+
     def run(i):
-        model["m"] = est.fit_tensors(X, y, K, allreduce=dp.allreduce_sum(ctx), row_offset=rank * n_local,
-                                     thresholds=thr)
+        model["m"] = est.fit_tensors(X, y, K, allreduce=None if owner else dp.allreduce_sum(ctx),
+                                     row_offset=rank * n_local, thresholds=thr, owner=owner)
 
     elapsed = timed(ctx, run, args.steps, args.warmup, dev)
     acc = float((model["m"].predict(Xt) == yt).float().mean())
@@ -191,7 +195,7 @@ def bench_rf(args, ctx, nine_axis=False):
                     f"({X.shape[1]} features, {K} classes)",
             "config": {"model": name, "global_batch": rows, "seq_len": spec.window, "parallelism": f"dp{world}"},
             "test_accuracy": hdist.mean_over_ranks(ctx, acc), "test_accuracy_data": "held-out synthetic windows",
-            "dtype": "fp32"}
+            "dtype": "fp32", "histogram_reduction": args.rf_reduce if world > 1 else "none"}
 
 
 def bench_stream(args, ctx):
@@ -259,6 +263,8 @@ def main():
     ap.add_argument("--rows", type=int, default=60000, help="windows per GPU (forest configs)")
     ap.add_argument("--trees", type=int, default=0)
     ap.add_argument("--depth", type=int, default=10)
+    ap.add_argument("--rf-reduce", default="owner", choices=["owner", "allreduce"],
+                    help="DP forest histograms: reduce-scatter by node owner + all-gather of splits, or all-reduce")
     ap.add_argument("--samples", type=int, default=1_000_000_000, help="stream samples per 8 GPUs")
     ap.add_argument("--out", type=str, default="")
     args = ap.parse_args()

@@ -46,10 +46,11 @@ def _worker(rank, world, port, out_dir, what):
         ms = dp.fit_logreg_dp(LogisticRegression(maxIter=15), Xs, ys,
                               [FitSpec(None, 0.1, 0.0), FitSpec(None, 0.05, 0.3)], 4, ctx)
         res = torch.stack([m.coefficientMatrix for m in ms])
-    elif what == "rf":
+    elif what in ("rf", "rf_allreduce"):
         from har.models.tree import RandomForestClassifier
 
-        m = dp.fit_forest_dp(RandomForestClassifier(numTrees=8, maxDepth=4, seed=5), Xs, ys, 4, off, ctx)
+        m = dp.fit_forest_dp(RandomForestClassifier(numTrees=8, maxDepth=4, seed=5), Xs, ys, 4, off, ctx,
+                             reduction="owner" if what == "rf" else "allreduce")
         res = m.predict_raw(X)
     elif what == "stream":
         from har.features.window import WindowFeaturizer
@@ -89,12 +90,16 @@ def test_dp_logreg_equals_single():
     torch.testing.assert_close(outs[0], torch.stack([m.coefficientMatrix for m in ms]), rtol=1e-3, atol=1e-4)
 
 
-def test_dp_forest_equals_single():
+@pytest.mark.parametrize("what,world", [("rf", 2), ("rf", 3), ("rf_allreduce", 2)])
+def test_dp_forest_equals_single(what, world):
+    """Owner-computes (reduce-scatter by node + all-gather of winners; world 3 leaves
+    uneven node slices) and all-reduce histogram reductions both equal one process."""
     from har.models.tree import RandomForestClassifier
     from har.ops import tree as T
 
-    outs = _run("rf")
-    torch.testing.assert_close(outs[0], outs[1])
+    outs = _run(what, world)
+    for o in outs[1:]:
+        torch.testing.assert_close(outs[0], o)
     X, y = _data()
     # single process with the thresholds the DP run used (rank 0 sample of both shards == all rows here)
     thr = T.find_thresholds(X.numpy(), 32)
