@@ -14,7 +14,12 @@ import dataclasses
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional
 
-DEFAULT_WISDM = "/root/reference/Main/wisdm_main_ver_0.0/data/wisdm_data.csv"
+import os as _os
+
+_REF_WISDM = "/root/reference/Main/wisdm_main_ver_0.0/data/wisdm_data.csv"
+_VENDORED_WISDM = _os.path.join(_os.path.dirname(_os.path.dirname(_os.path.abspath(__file__))), "tests", "data",
+                                "wisdm_data.csv")
+DEFAULT_WISDM = _REF_WISDM if _os.path.exists(_REF_WISDM) else _VENDORED_WISDM
 
 
 @dataclass
@@ -27,6 +32,7 @@ class RunConfig:
     split: List[float] = field(default_factory=lambda: [0.7, 0.3])
     seed: int = 2018
     device: str = "auto"
+    csv_device: bool = False               # parse + dictionary-encode the CSV with the HIP kernels
     # LogisticRegression (main.py:115)
     lr_max_iter: int = 20
     lr_reg: float = 0.3

@@ -73,6 +73,63 @@ class Model(Transformer):
         return {}
 
 
+# ---------------------------------------------------------------------------
+# Data-parallel scope.  Inside ``with data_parallel(ctx):`` every ``Estimator.fit(table)``
+# (and CrossValidator's batched fits) trains on this rank's contiguous row shard and
+# combines its partial statistics with collectives over ``ctx`` (RCCL on GPUs, gloo on
+# CPU) — the analogue of Spark running the same ``fit`` over partitioned RDDs with
+# ``treeAggregate`` / ``reduceByKey``.  Every rank holds the whole
+# (small) input table; global row ids stay meaningful, so split / fold / bootstrap draws
+# are the same as in one process.
+_DP_CTX = None
+
+
+class data_parallel:
+    def __init__(self, ctx):
+        self.ctx = ctx if (ctx is not None and ctx.is_distributed) else None
+
+    def __enter__(self):
+        global _DP_CTX
+        self._prev, _DP_CTX = _DP_CTX, self.ctx
+        return self.ctx
+
+    def __exit__(self, *exc):
+        global _DP_CTX
+        _DP_CTX = self._prev
+        return False
+
+
+def dp_context():
+    """The active distributed context (None outside ``data_parallel`` or for world size 1)."""
+    return _DP_CTX
+
+
+def dp_rows(n: int) -> Tuple[int, int]:
+    """This rank's contiguous [lo, hi) share of ``n`` rows (all rows outside DP)."""
+    ctx = _DP_CTX
+    if ctx is None:
+        return 0, n
+    return (n * ctx.rank) // ctx.world_size, (n * (ctx.rank + 1)) // ctx.world_size
+
+
+def dp_allreduce():
+    """In-place SUM over ranks (None outside DP)."""
+    if _DP_CTX is None:
+        return None
+    from ..parallel.data_parallel import allreduce_sum
+
+    return allreduce_sum(_DP_CTX)
+
+
+def dp_owner():
+    """Owner-computes node communicator for tree levels (None outside DP)."""
+    if _DP_CTX is None:
+        return None
+    from ..parallel.data_parallel import NodeOwner
+
+    return NodeOwner(_DP_CTX)
+
+
 def features_tensor(table: Table, col: str, device, dtype=torch.float32) -> torch.Tensor:
     c = table[col]
     arr = c.data if c.kind == "vector" else c.data[:, None]

@@ -33,8 +33,8 @@ from ..data.table import Table
 from ..ops import _native
 from ..ops.logreg import LogregWorkspace, logreg_loss_grad_native, logreg_loss_grad_torch
 from ..optim import lbfgs
-from .base import ClassificationModel, ClassifierParams, Estimator, features_tensor, labels_tensor, new_uid, \
-    resolve_device
+from .base import ClassificationModel, ClassifierParams, Estimator, dp_allreduce, dp_context, dp_owner, dp_rows, \
+    features_tensor, labels_tensor, new_uid, resolve_device
 
 
 @dataclass
@@ -121,7 +121,10 @@ class LogisticRegression(Estimator, ClassifierParams):
         if self.weightCol:
             w = torch.as_tensor(table[self.weightCol].data.astype(np.float32), device=dev)
         num_classes = int(max(int(y.max()) + 1, len((table[self.labelCol].meta or {}).get("vocab") or [])))
-        model = self.fit_many(X, y, [FitSpec(w, self.regParam, self.elasticNetParam)], num_classes)[0]
+        lo, hi = dp_rows(X.shape[0])  # data parallel: this rank's row shard + one all-reduce per evaluation
+        model = self.fit_many(X[lo:hi], y[lo:hi], [FitSpec(None if w is None else w[lo:hi], self.regParam,
+                                                           self.elasticNetParam)], num_classes,
+                              allreduce=dp_allreduce())[0]
         model.uid = self.uid
         return model
 

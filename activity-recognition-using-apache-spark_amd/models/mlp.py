@@ -34,8 +34,8 @@ import torch
 from ..data.table import Table
 from ..ops import _native, rng
 from ..ops.gemm import EPI_BIAS_RELU, EPI_F32_SLAB, EPI_RELU_GRAD, gemm_bf16, tile_counts
-from .base import ClassificationModel, ClassifierParams, Estimator, features_tensor, labels_tensor, new_uid, \
-    resolve_device
+from .base import ClassificationModel, ClassifierParams, Estimator, dp_allreduce, dp_context, dp_owner, dp_rows, \
+    features_tensor, labels_tensor, new_uid, resolve_device
 
 HEAD_PAD = 32  # classes padded to 32 rows (two 16-wide MFMA column tiles)
 
@@ -519,7 +519,14 @@ class MultilayerPerceptronClassifier(Estimator, ClassifierParams):
         dev = resolve_device(self.device)
         X = features_tensor(table, self.featuresCol, dev)
         y = labels_tensor(table, self.labelCol, dev)
-        return self.fit_tensors(X, y)
+        vocab = (table[self.labelCol].meta or {}).get("vocab")
+        K = int(max(int(y.max()) + 1, len(vocab) if vocab else 0))
+        ctx = dp_context()
+        if ctx is None:
+            return self.fit_tensors(X, y, num_classes=K)
+        lo, hi = dp_rows(X.shape[0])  # data parallel: row shard, gradients all-reduced every step
+        return self.fit_tensors(X[lo:hi], y[lo:hi], process_group=ctx.group, rank=ctx.rank,
+                                world_size=ctx.world_size, num_classes=K)
 
     def fit_tensors(self, X: torch.Tensor, y: torch.Tensor, process_group=None, rank: int = 0,
                     world_size: int = 1, num_classes: Optional[int] = None) -> MultilayerPerceptronClassificationModel:

@@ -16,8 +16,8 @@ import torch
 
 from ..data.table import Table
 from ..ops.gemm import EPI_BIAS_F32, EPI_F32_ATOMIC, gemm_f32
-from .base import ClassificationModel, ClassifierParams, Estimator, features_tensor, labels_tensor, new_uid, \
-    resolve_device
+from .base import ClassificationModel, ClassifierParams, Estimator, dp_allreduce, dp_context, dp_owner, dp_rows, \
+    features_tensor, labels_tensor, new_uid, resolve_device
 
 
 def _pad4(x: int) -> int:
@@ -117,16 +117,24 @@ class NaiveBayes(Estimator, ClassifierParams):
         w = None
         if self.weightCol:
             w = torch.as_tensor(table[self.weightCol].data, dtype=torch.float32, device=dev)
-        m = self.fit_tensors(X, y, K, w)
+        lo, hi = dp_rows(X.shape[0])  # data parallel: per-class moments of the shard, one all-reduce
+        m = self.fit_tensors(X[lo:hi], y[lo:hi], K, None if w is None else w[lo:hi], allreduce=dp_allreduce())
         m.uid = self.uid
         return m
 
-    def fit_tensors(self, X, y, K, w=None) -> NaiveBayesModel:
+    def fit_tensors(self, X, y, K, w=None, allreduce=None) -> NaiveBayesModel:
+        """``allreduce`` (in-place SUM over ranks): X/y/w are this rank's shard and the
+        class counts / first / second moments are summed in ONE flat bucket."""
         lam = float(self.smoothing)
         if self.modelType in ("multinomial", "bernoulli") and bool((X < 0).any()):
             raise ValueError(f"{self.modelType} NaiveBayes requires nonnegative feature values")
         n, s1, s2 = class_moments(X.float(), y, K, w)
         n, s1, s2 = n.double(), s1.double(), s2.double()
+        if allreduce is not None:
+            F = X.shape[1]
+            buf = torch.cat([n.reshape(-1), s1.reshape(-1), s2.reshape(-1)])
+            allreduce(buf)
+            n, s1, s2 = buf[:K], buf[K:K + K * F].view(K, F), buf[K + K * F:].view(K, F)
         N = float(n.sum())
         pi = torch.log((n + lam) / (N + lam * K))
         sigma = None

@@ -37,8 +37,8 @@ import torch
 from ..data.table import Table
 from ..ops import _native, rng
 from ..ops import tree as T
-from .base import ClassificationModel, ClassifierParams, Estimator, features_tensor, labels_tensor, new_uid, \
-    resolve_device
+from .base import ClassificationModel, ClassifierParams, Estimator, dp_allreduce, dp_context, dp_owner, dp_rows, \
+    features_tensor, labels_tensor, new_uid, resolve_device
 
 
 @dataclass
@@ -138,7 +138,12 @@ class ForestBuilder:
         W = self.bootstrap_weights(N, dev, row_offset)        # [T, N]
         if row_weight is not None:
             W = W * row_weight.to(device=dev, dtype=W.dtype)
-        maxn = int(min(2 ** (D + 1) - 1, 2 * max(N, 1) + 1))
+        n_all = N
+        if self.allreduce is not None:  # data parallel: the node capacity must agree across ranks
+            nt = torch.tensor([float(N)], dtype=torch.float64, device=dev)
+            self.allreduce(nt)
+            n_all = int(nt.item())
+        maxn = int(min(2 ** (D + 1) - 1, 2 * max(n_all, 1) + 1))
         feature = torch.full((Tn, maxn), -1, dtype=torch.int32, device=dev)
         thresh = torch.zeros(Tn, maxn, dtype=torch.float32, device=dev)
         left = torch.zeros(Tn, maxn, dtype=torch.int32, device=dev)
@@ -357,19 +362,25 @@ class DecisionTreeClassifier(_TreeEstimatorBase):
 
     def fit(self, table: Table) -> DecisionTreeClassificationModel:
         X, y, K = self._prep(table)
-        return self.fit_tensors(X, y, K)
+        if dp_context() is None:
+            return self.fit_tensors(X, y, K)
+        thr = T.find_thresholds(X.detach().float().cpu().numpy(), self.maxBins, seed=self.seed)
+        lo, hi = dp_rows(X.shape[0])
+        return self.fit_tensors(X[lo:hi], y[lo:hi], K, thresholds=thr, owner=dp_owner(), row_offset=lo)
 
-    def fit_tensors(self, X, y, K, thresholds=None) -> DecisionTreeClassificationModel:
+    def fit_tensors(self, X, y, K, thresholds=None, allreduce=None, owner=None,
+                    row_offset: int = 0) -> DecisionTreeClassificationModel:
         b = ForestBuilder(K, 1, self.maxDepth, self.maxBins, self.minInstancesPerNode, self.minInfoGain,
-                          self.impurity, "all", bootstrap=False, seed=self.seed)
-        return DecisionTreeClassificationModel(b.fit(X, y, thresholds=thresholds), X.shape[1], K, uid=self.uid,
-                                               device=X.device)
+                          self.impurity, "all", bootstrap=False, seed=self.seed, allreduce=allreduce, owner=owner)
+        return DecisionTreeClassificationModel(b.fit(X, y, row_offset=row_offset, thresholds=thresholds), X.shape[1],
+                                               K, uid=self.uid, device=X.device)
 
     def fit_folds(self, X, y, K, masks: torch.Tensor) -> List["DecisionTreeClassificationModel"]:
-        """One tree per fold (``masks`` [k, N]: 1 = training row of fold f), all grown together."""
+        """One tree per fold (``masks`` [k, N]: 1 = training row of fold f), all grown together
+        (data parallel inside ``data_parallel``: row shards, owner-computes splits)."""
         b = ForestBuilder(K, masks.shape[0], self.maxDepth, self.maxBins, self.minInstancesPerNode, self.minInfoGain,
-                          self.impurity, "all", bootstrap=False, seed=self.seed)
-        arrs = b.fit(X, y, row_weight=masks)
+                          self.impurity, "all", bootstrap=False, seed=self.seed, owner=dp_owner())
+        arrs = _fit_sharded(b, X, y, masks, self.maxBins, self.seed)
         return [DecisionTreeClassificationModel(_slice_arrays(arrs, f, f + 1), X.shape[1], K, uid=self.uid,
                                                 device=X.device) for f in range(masks.shape[0])]
 
@@ -389,7 +400,11 @@ class RandomForestClassifier(_TreeEstimatorBase):
 
     def fit(self, table: Table) -> RandomForestClassificationModel:
         X, y, K = self._prep(table)
-        return self.fit_tensors(X, y, K)
+        if dp_context() is None:
+            return self.fit_tensors(X, y, K)
+        thr = T.find_thresholds(X.detach().float().cpu().numpy(), self.maxBins, seed=self.seed)
+        lo, hi = dp_rows(X.shape[0])
+        return self.fit_tensors(X[lo:hi], y[lo:hi], K, row_offset=lo, thresholds=thr, owner=dp_owner())
 
     def fit_tensors(self, X, y, K, allreduce=None, row_offset: int = 0, thresholds=None,
                     tree_wave: int = 0, checkpoint_dir: Optional[str] = None, rank: int = 0, owner=None):
@@ -441,10 +456,20 @@ class RandomForestClassifier(_TreeEstimatorBase):
         if str(strategy).lower() == "auto":
             strategy = "all" if T_ == 1 else "sqrt"
         b = ForestBuilder(K, k * T_, self.maxDepth, self.maxBins, self.minInstancesPerNode, self.minInfoGain,
-                          self.impurity, strategy, bootstrap=T_ > 1, seed=self.seed)
-        arrs = b.fit(X, y, row_weight=masks.repeat_interleave(T_, dim=0))
+                          self.impurity, strategy, bootstrap=T_ > 1, seed=self.seed, owner=dp_owner())
+        arrs = _fit_sharded(b, X, y, masks.repeat_interleave(T_, dim=0), self.maxBins, self.seed)
         return [RandomForestClassificationModel(_slice_arrays(arrs, f * T_, (f + 1) * T_), X.shape[1], K, uid=self.uid,
                                                 device=X.device) for f in range(k)]
+
+
+def _fit_sharded(b: "ForestBuilder", X, y, row_weight, max_bins: int, seed: int) -> ForestArrays:
+    """``b.fit`` over the whole matrix, or — inside ``data_parallel`` — over this rank's
+    row shard (thresholds from the whole matrix, so every rank bins identically)."""
+    if dp_context() is None:
+        return b.fit(X, y, row_weight=row_weight)
+    thr = T.find_thresholds(X.detach().float().cpu().numpy(), max_bins, seed=seed)
+    lo, hi = dp_rows(X.shape[0])
+    return b.fit(X[lo:hi], y[lo:hi], row_offset=lo, thresholds=thr, row_weight=row_weight[:, lo:hi])
 
 
 def _slice_arrays(a: ForestArrays, lo: int, hi: int) -> ForestArrays:

@@ -31,7 +31,8 @@ import torch
 
 from ..data.split import kfold_ids, split_ids
 from ..data.table import Column, Table
-from ..models.base import Estimator, Model, features_tensor, labels_tensor, new_uid, resolve_device
+from ..models.base import Estimator, Model, dp_allreduce, dp_context, dp_rows, features_tensor, labels_tensor, \
+    new_uid, resolve_device
 
 
 def _pname(p) -> str:
@@ -114,7 +115,10 @@ class CrossValidator(Estimator):
                     index.append((mi, f))
             # maxIter / tol / family etc. may differ per map only through regParam/elasticNetParam
             base = est.copy(maps[0]) if maps else est
-            models = base.fit_many(X, y, specs, K)
+            lo, hi = dp_rows(X.shape[0])  # data parallel: all 45 fits on this rank's row shard
+            if dp_context() is not None:
+                specs = [FitSpec(s.row_weight[lo:hi], s.regParam, s.elasticNetParam) for s in specs]
+            models = base.fit_many(X[lo:hi], y[lo:hi], specs, K, allreduce=dp_allreduce())
             for (mi, f), m in zip(index, models):
                 rows = np.nonzero(fold == f)[0]
                 vt = table.take_rows(rows)

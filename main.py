@@ -12,6 +12,14 @@ DecisionTree(+CV), RandomForest(+CV) — plus NaiveBayes and an MLP — and writ
     python main.py --classifiers lr --device cpu     # BASELINE config 1 (plumbing)
     python main.py --preset rf-deep                  # RF 100 trees x depth 10 on the GPU
     python main.py --preset all-numeric --save-models models/
+    python main.py --csv-device                      # CSV parsed + dictionary-encoded by the HIP kernels
+    torchrun --nproc-per-node 8 --master-addr 127.0.0.1 main.py   # data parallel over 8 GPUs (RCCL)
+
+Under ``torch.distributed.run`` every rank loads the (small) table and every model is
+fit data-parallel on the rank's row shard (``har.models.base.data_parallel``): one
+all-reduce per L-BFGS evaluation for LR / LR-CV, owner-computed tree levels
+(reduce-scatter + all-gather) for DT / RF (+CV), gradient all-reduce for the MLP,
+one moment all-reduce for NaiveBayes.  Rank 0 writes the artefacts.
 
 Paths default to the reference layout relative to the working directory
 (``wisdm_main_ver_0.0/main_result``); ``--data`` points at the CSV.
@@ -37,7 +45,8 @@ from har.data.table import describe_text  # noqa: E402
 from har.evaluation.evaluators import (MulticlassClassificationEvaluator, RegressionEvaluator,  # noqa: E402
                                        evaluate_all)
 from har.features import wisdm  # noqa: E402
-from har.models.base import features_tensor, resolve_device  # noqa: E402
+from har.models.base import data_parallel, features_tensor, resolve_device  # noqa: E402
+from har.parallel import dist as hdist  # noqa: E402
 from har.models.logreg import LogisticRegression  # noqa: E402
 from har.models.mlp import MultilayerPerceptronClassifier  # noqa: E402
 from har.models.naive_bayes import NaiveBayes  # noqa: E402
@@ -101,16 +110,17 @@ def warm_up_device(dev, train, cfg: RunConfig):
     device_sync(dev)
 
 
-def run(cfg: RunConfig) -> dict:
-    dev = resolve_device(None if cfg.device == "auto" else cfg.device)
+def run(cfg: RunConfig, ctx=None) -> dict:
+    dev = ctx.device if ctx is not None else resolve_device(None if cfg.device == "auto" else cfg.device)
+    main_rank = ctx is None or ctx.is_main
     os.makedirs(cfg.out_dir, exist_ok=True)
-    log = RunLog(os.path.join(cfg.out_dir, "result.txt"), echo=cfg.echo)
+    log = RunLog(os.path.join(cfg.out_dir, "result.txt") if main_rank else os.devnull, echo=cfg.echo and main_rank)
     t_run = time.perf_counter()
     timer = PhaseTimer(dev)
 
     log.print("Loading Data Set...")
     with timer.phase("load_csv"):
-        raw = read_csv(cfg.data)
+        raw = read_csv(cfg.data, device=dev if (cfg.csv_device and dev.type == "cuda") else None)
     with timer.phase("feature_pipeline"):
         data, pipe_model, df = wisdm.prepare(raw, cfg.encoding)
     section(log, "Data Schema")
@@ -158,7 +168,7 @@ def run(cfg: RunConfig) -> dict:
     y_test = torch.as_tensor(test_data["label"].data.astype(np.int64), device=dev)
     for name in cfg.classifiers:
         est = build_estimator(name, cfg, dev, n_features, n_classes)
-        with timer.phase(f"fit:{name}"):
+        with timer.phase(f"fit:{name}"), data_parallel(ctx):
             model = est.fit(train)
         train_s = round(timer.get(f"fit:{name}"), 3)
         with timer.phase(f"predict:{name}"):
@@ -179,10 +189,14 @@ def run(cfg: RunConfig) -> dict:
         records[name] = {"model": str(model), "train_s": train_s, "predict_s": test_s,
                          "train_windows_per_s": train.count() / max(train_s, 1e-9),
                          "predict_windows_per_s": test.count() / max(test_s, 1e-9), **r.as_dict()}
-        if cfg.save_models:
+        if cfg.save_models and main_rank:
             persist.save(model, os.path.join(cfg.save_models, name), labels=vocab)
-    if cfg.save_models:
+    if cfg.save_models and main_rank:
         persist.save(pipe_model, os.path.join(cfg.save_models, "pipeline"), labels=vocab)
+    world = ctx.world_size if ctx is not None else 1
+    if not main_rank:
+        log.close()
+        return {"device": str(dev), "world_size": world, "models": records}
 
     if plain_rows:
         csvout.write_rows(os.path.join(cfg.out_dir, "additional_param.csv"), csvout.PLAIN_FIELDS, plain_rows,
@@ -190,7 +204,7 @@ def run(cfg: RunConfig) -> dict:
     if cv_rows:
         csvout.write_rows(os.path.join(cfg.out_dir, "crossFold_additional_param.csv"), csvout.CV_FIELDS, cv_rows,
                           append=cfg.append_csv)
-    summary = {"device": str(dev), "encoding": cfg.encoding, "n_train": train.count(), "n_test": test.count(),
+    summary = {"device": str(dev), "world_size": world, "encoding": cfg.encoding, "n_train": train.count(), "n_test": test.count(),
                "seed": cfg.seed, "wall_s": time.perf_counter() - t_run, "models": records,
                "phases_s": {k: round(v, 6) for k, v in timer.as_dict().items()}}
     csvout.append_jsonl(os.path.join(cfg.out_dir, "metrics.jsonl"), summary)
@@ -204,7 +218,14 @@ def run(cfg: RunConfig) -> dict:
 
 def main(argv=None):
     cfg = config_from_args(argv)
-    summary = run(cfg)
+    ctx = None
+    if int(os.environ.get("WORLD_SIZE", "1")) > 1:  # launched by torch.distributed.run: one rank per GPU
+        ctx = hdist.init(device=None if cfg.device == "auto" else cfg.device)
+    summary = run(cfg, ctx)
+    if ctx is not None:
+        hdist.shutdown(ctx)
+        if not ctx.is_main:
+            return
     print(json.dumps({k: {kk: (round(vv, 6) if isinstance(vv, float) else vv) for kk, vv in v.items()
                           if kk in ("accuracy", "f1", "train_s", "predict_s")} for k, v in summary["models"].items()}))
 

@@ -10,6 +10,9 @@ if ROOT not in sys.path:
 WISDM_CANDIDATES = [
     os.environ.get("HAR_WISDM_CSV", ""),
     os.path.join(ROOT, "data", "wisdm_data.csv"),
+    # WISDM v1.1 transformed table (the reference's dataset, Main/wisdm_main_ver_0.0/data/wisdm_data.csv),
+    # vendored so the GPU box — where /root/reference does not exist — runs the WISDM tests too
+    os.path.join(ROOT, "tests", "data", "wisdm_data.csv"),
     "/root/reference/Main/wisdm_main_ver_0.0/data/wisdm_data.csv",
 ]
 
