@@ -67,6 +67,29 @@ def test_hist_split_native_matches_torch(cuda):
     torch.testing.assert_close(two.gain, nat.gain)
     torch.testing.assert_close(two.total, nat.total)
 
+    # owner-computes form: this "rank" owns node slice [a0, a1); the split kernel runs on that
+    # slice only (pointer-offset node / feature arrays) and the gathered rows must equal the
+    # fused kernel's; the other rows stay zero (another rank's share)
+    class SliceOwner:
+        def __init__(self, a0, a1):
+            self.a0, self.a1 = a0, a1
+
+        def reduce_scatter(self, hist):
+            return hist[self.a0:self.a1].clone(), self.a0, self.a1
+
+        def all_gather(self, local, A):
+            out = torch.zeros(A, *local.shape[1:], dtype=local.dtype, device=local.device)
+            out[self.a0:self.a1] = local
+            return out
+
+    for a0, a1 in ((1, 3), (0, 1), (2, 3)):
+        own = T.hist_split_native(bins, nbins, y32, rows, w, starts, counts, feats, 5, 32, 1.0, 0.0, T.GINI,
+                                  owner=SliceOwner(a0, a1))
+        assert torch.equal(own.feat[a0:a1], nat.feat[a0:a1]) and torch.equal(own.bin[a0:a1], nat.bin[a0:a1])
+        torch.testing.assert_close(own.gain[a0:a1], nat.gain[a0:a1])
+        torch.testing.assert_close(own.left[a0:a1], nat.left[a0:a1])
+        torch.testing.assert_close(own.total[a0:a1], nat.total[a0:a1])
+
 
 def test_forest_predict_native_matches_torch(cuda):
     from har.models.tree import RandomForestClassifier
@@ -138,6 +161,35 @@ def test_main_reference_run_gpu(cuda, tmp_path, wisdm_csv):
     assert m["lr"]["accuracy"] >= 0.60 and m["lrcv"]["accuracy"] >= 0.70
     assert m["dt"]["accuracy"] >= 0.72 and m["rf"]["accuracy"] >= 0.62
     assert (tmp_path / "result.txt").exists() and (tmp_path / "additional_param.csv").exists()
+
+
+def test_main_csv_device_matches_host_parse(cuda, tmp_path, wisdm_csv):
+    """``main.py --csv-device``: the CSV is parsed and dictionary-encoded by the HIP kernels;
+    the run must reproduce the host-parsed run's metrics exactly."""
+    import main
+
+    base = ["--data", wisdm_csv, "--classifiers", "lr,dt", "--device", "cuda"]
+    a = main.run(main.config_from_args(base + ["--out-dir", str(tmp_path / "host")]))
+    b = main.run(main.config_from_args(base + ["--out-dir", str(tmp_path / "dev"), "--csv-device"]))
+    for name in ("lr", "dt"):
+        assert a["models"][name]["accuracy"] == b["models"][name]["accuracy"]
+        assert a["models"][name]["f1"] == b["models"][name]["f1"]
+
+
+def test_dictionary_encode_device(cuda, wisdm_csv):
+    from har.data.csv_device import read_csv_device
+    from har.features.encode import StringIndexer
+    from har.data.csv_io import read_csv
+
+    d = read_csv_device(wisdm_csv, cuda)
+    codes, vocab, counts = d.dictionary_encode("ACTIVITY")
+    assert vocab == ["Walking", "Jogging", "Upstairs", "Downstairs", "Sitting", "Standing"]
+    assert counts.tolist() == [2081, 1625, 632, 528, 306, 246]
+    host = read_csv(wisdm_csv)
+    sm = StringIndexer(inputCol="XPEAK", outputCol="i").fit(host)
+    c2, v2, _ = d.dictionary_encode("XPEAK")
+    assert v2 == list(sm.labels) and len(v2) == 935  # "?" included; frequency-desc, ties by value
+    assert int(codes.min()) == 0 and codes.device.type == "cuda"
 
 
 def test_mlp_overlapped_dp_step_equals_fused(cuda):
