@@ -456,10 +456,28 @@ class MLPEngine:
         self.last_loss = float(loss.detach()) * global_batch / X.shape[0]
 
     # ---------------------------------------------------------------- inference
+    def infer_fused(self, Xb: torch.Tensor):
+        """Serving path: ONE fused kernel (mlp_fused.hip, INFER variant) per call — logits
+        [B, C] fp32 and the argmax class [B] int32 from padded bf16 inputs."""
+        L = self.layout
+        B = Xb.shape[0]
+        if not (self.fused_ok and B % 16 == 0 and Xb.dtype == torch.bfloat16 and Xb.shape[1] == L.in_pad):
+            raise ValueError("infer_fused: unsupported shape")
+        out = torch.empty(B, L.num_classes, dtype=torch.float32, device=Xb.device)
+        pred = torch.empty(B, dtype=torch.int32, device=Xb.device)
+        _native.kernels().mlp_fwd_infer(Xb.data_ptr(), L.in_pad, self._w(self.Pb, "W0").data_ptr(),
+                                        self._w(self.P, "b0").data_ptr(), self._w(self.Pb, "W1").data_ptr(),
+                                        self._w(self.P, "b1").data_ptr(), self.dims[-1],
+                                        self._w(self.Pb, "Wout").data_ptr(), self._w(self.P, "bout").data_ptr(), B,
+                                        L.num_classes, out.data_ptr(), pred.data_ptr(), _native.stream_ptr())
+        return out, pred
+
     def logits(self, X: torch.Tensor) -> torch.Tensor:
         L = self.layout
         if self.native and X.is_cuda:
             Xb = pad_input_bf16(X, L.in_pad)
+            if self.fused_ok and X.shape[0] % 16 == 0:
+                return self.infer_fused(Xb)[0]
             out = torch.empty(X.shape[0], L.num_classes, dtype=torch.float32, device=X.device)
             for r0 in range(0, X.shape[0], self.B):
                 r1 = min(X.shape[0], r0 + self.B)

@@ -19,6 +19,8 @@ xGMI, weak scaling (fixed per-GPU work).  Every line is ONE JSON record.
                     8 GPUs, i.e. 125M per GPU resident in HBM) -> HIP window featurizer
                     -> MLP training step; step = featurize + train ``--batch`` windows.
 ``--config rf9``    (config 5) 12-class 9-axis IMU RandomForest, 500 trees.
+``--config infer``  serving: windows/s classified by the trained config-3 MLP (fused
+                    forward + head kernel, logits + argmax); no reference number exists.
 
 ``vs_baseline`` divides by the reference's published WISDM training throughput of
 the matching model family (run A): LogisticRegression 418.6
@@ -147,6 +149,51 @@ def bench_mlp(args, ctx):
             "hip_graph": {0: "off", 1: "whole-step", 2: "segmented"}[mode if graphs else 0]}
 
 
+def bench_infer(args, ctx):
+    """Serving throughput: the MLP of config 3 (trained ``--train-steps`` steps first, untimed)
+    classifies ``--batch`` fp32 feature windows per GPU per step — cast/pad to bf16 + ONE fused
+    forward+head kernel (logits and argmax).  The reference has no measurable inference path
+    (its "Prediction made in" timer is lazy-plan time, Main/main.py:121-123)."""
+    from har.models.mlp import MLPEngine, pad_input_bf16
+    from har.parallel import dist as hdist
+
+    dev, rank, world = ctx.device, ctx.rank, ctx.world_size
+    B = args.batch
+    layers = [N_FEATURES, args.hidden, args.hidden, N_CLASSES]
+    tb = 8192
+    eng = MLPEngine(layers, tb, dev, lr=args.lr, seed=1234, process_group=ctx.group, world_size=world)
+    Xtr, ytr = synthetic_windows(tb * 8, seed=100 + rank, device=dev)
+    Xtr_b = pad_input_bf16(Xtr, eng.layout.in_pad) if eng.native else Xtr
+    ytr32 = ytr.to(torch.int32)
+    for i in range(args.train_steps):
+        j = i % 8
+        eng.train_step(Xtr_b[j * tb:(j + 1) * tb], ytr32[j * tb:(j + 1) * tb], tb * world)
+    nb = 4
+    X, y = synthetic_windows(B * nb, seed=500 + rank, device=dev)
+    correct = torch.zeros((), dtype=torch.int64, device=dev)
+
+    def step(i):
+        j = i % nb
+        xb = X[j * B:(j + 1) * B]
+        if eng.native:
+            _, pred = eng.infer_fused(pad_input_bf16(xb, eng.layout.in_pad))
+        else:
+            pred = torch.argmax(eng.logits(xb), 1)
+        if i < nb:
+            correct.add_((pred.long() == y[j * B:(j + 1) * B]).sum())
+
+    elapsed = timed(ctx, step, args.steps, args.warmup, dev)
+    acc = float(correct) / (B * min(nb, args.steps + args.warmup))
+    return {"value": B * world * args.steps / elapsed, "ms_per_step": elapsed * 1e3 / args.steps,
+            "vs_baseline": None,
+            "data": "synthetic WISDM-shaped windows (43 features, 6 classes); MLP trained "
+                    f"{args.train_steps} steps on synthetic windows first (untimed)",
+            "config": {"model": f"WISDM 6-class 3-layer MLP bf16 inference ({'-'.join(map(str, layers))})",
+                       "global_batch": B * world, "seq_len": WINDOW_SAMPLES, "parallelism": f"dp{world}"},
+            "test_accuracy": hdist.mean_over_ranks(ctx, acc), "test_accuracy_data": "held-out synthetic windows",
+            "mode": "inference"}
+
+
 def _featurized(n_windows, spec, dev, first_window):
     from har.data.synth import generate_stream
     from har.features.window import window_features
@@ -253,7 +300,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--config", default="mlp", choices=["mlp", "rf", "stream", "rf9"])
+    ap.add_argument("--config", default="mlp", choices=["mlp", "rf", "stream", "rf9", "infer"])
+    ap.add_argument("--train-steps", type=int, default=200, help="untimed MLP training steps before --config infer")
     ap.add_argument("--batch", type=int, default=65536, help="windows per GPU per step (MLP configs)")
     ap.add_argument("--hidden", type=int, default=256)
     ap.add_argument("--lr", type=float, default=1e-3)
@@ -277,6 +325,8 @@ def main():
         r = bench_mlp(args, ctx)
     elif args.config == "stream":
         r = bench_stream(args, ctx)
+    elif args.config == "infer":
+        r = bench_infer(args, ctx)
     else:
         r = bench_rf(args, ctx, nine_axis=args.config == "rf9")
     rec = {"metric": METRIC, "value": r.pop("value"), "unit": "windows/s", "n_gpus": ctx.world_size,

@@ -64,6 +64,10 @@ int har_mlp_fwd_head(const uint16_t* X, int K0, const uint16_t* W0, const float*
                      int C, float scale, uint16_t* h1, uint16_t* dact, float* slab, float* block_loss,
                      int32_t* block_correct, hipStream_t s);
 int har_mlp_fwd_head_grid(int B);
+// Serving variant of the same kernel: logits [B][C] fp32 + argmax class [B] int32, nothing else.
+int har_mlp_fwd_infer(const uint16_t* X, int K0, const uint16_t* W0, const float* b0, const uint16_t* W1,
+                      const float* b1, int H, const uint16_t* Wo, const float* bo, int B, int C, float* logits,
+                      int32_t* pred, hipStream_t s);
 
 // dst[g*n + i] = sum of slabs[s*n + i] over the g-th group of ceil(S/G) slabs (deterministic).
 // A non-null tick is incremented once by the first workgroup (the optimizer step counter).

@@ -71,13 +71,16 @@ template <> __device__ __forceinline__ void hold_all<16>(u32x4_t (&b)[16]) {
                "v"(b[8]), "v"(b[9]), "v"(b[10]), "v"(b[11]), "v"(b[12]), "v"(b[13]), "v"(b[14]), "v"(b[15]));
 }
 
-template <int H, int K0>
+// INFER = true: the serving variant — stages 1-3 only; writes the logits [B][C] (fp32) and the
+// argmax class per row, no label / loss / gradient work and no h1 store.
+template <int H, int K0, bool INFER>
 __global__ __launch_bounds__(256) void mlp_fwd_head_kernel(
     const bf16_t* __restrict__ X, const bf16_t* __restrict__ W0, const float* __restrict__ b0,
     const bf16_t* __restrict__ W1, const float* __restrict__ b1, const bf16_t* __restrict__ Wo,
     const float* __restrict__ bo, const int32_t* __restrict__ labels, int B, int C, float scale,
     bf16_t* __restrict__ h1out, bf16_t* __restrict__ dact, float* __restrict__ slab,
-    float* __restrict__ block_loss, int32_t* __restrict__ block_correct) {
+    float* __restrict__ block_loss, int32_t* __restrict__ block_correct, float* __restrict__ logits_out,
+    int32_t* __restrict__ pred_out) {
   constexpr int NT = H / 16, KC = H / 32, K0C = K0 / 32;
   extern __shared__ __attribute__((aligned(16))) bf16_t lds[];
   constexpr int P = Pitch<H>::v;
@@ -160,7 +163,7 @@ __global__ __launch_bounds__(256) void mlp_fwd_head_kernel(
 #pragma unroll
     for (int kc = 0; kc < K0C; ++kc)
       xb[kc] = *reinterpret_cast<const bf16x8_t*>(X + (size_t)(T * 16 + c16) * K0 + kc * 32 + g * 8);
-    y = labels[T * 16 + c16];
+    if (!INFER) y = labels[T * 16 + c16];
   }
   // drain the first prefetch here: otherwise the loop-header wait the compiler derives from
   // this path (vmcnt(0)) also applies on the back edge, where it would wait for every
@@ -178,7 +181,8 @@ __global__ __launch_bounds__(256) void mlp_fwd_head_kernel(
       const float4 bb = *reinterpret_cast<const float4*>(bs + 16 * t + 4 * g);
       h1p[t][0] = pack2(fmaxf(a[0] + bb.x, 0.f), fmaxf(a[1] + bb.y, 0.f));
       h1p[t][1] = pack2(fmaxf(a[2] + bb.z, 0.f), fmaxf(a[3] + bb.w, 0.f));
-      *reinterpret_cast<uint2*>(h1out + (size_t)row * H + 16 * t + 4 * g) = make_uint2(h1p[t][0], h1p[t][1]);
+      if (!INFER)
+        *reinterpret_cast<uint2*>(h1out + (size_t)row * H + 16 * t + 4 * g) = make_uint2(h1p[t][0], h1p[t][1]);
     }
     // prefetch the next tile's X rows and labels (issued before this tile's dact2 stores)
     const int Tn = T + stride;
@@ -187,7 +191,7 @@ __global__ __launch_bounds__(256) void mlp_fwd_head_kernel(
 #pragma unroll
       for (int kc = 0; kc < K0C; ++kc)
         xb[kc] = *reinterpret_cast<const bf16x8_t*>(X + (size_t)(Tn * 16 + c16) * K0 + kc * 32 + g * 8);
-      y = labels[Tn * 16 + c16];
+      if (!INFER) y = labels[Tn * 16 + c16];
     }
     __builtin_amdgcn_sched_barrier(0);
     // ---- stage 2: h2^T = W1 . h1^T  (A fragments software-pipelined one tile ahead) ----
@@ -242,6 +246,13 @@ __global__ __launch_bounds__(256) void mlp_fwd_head_kernel(
       const float om = __shfl_xor(mx, o, 64);
       const int oa = __shfl_xor(amx, o, 64);
       if (om > mx || (om == mx && oa < amx)) { mx = om; amx = oa; }
+    }
+    if constexpr (INFER) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (4 * g + r < C) logits_out[(size_t)row * C + 4 * g + r] = zz[r];
+      if (g == 0) pred_out[row] = amx;
+      continue;
     }
     float e[4], se = 0.f;
 #pragma unroll
@@ -299,6 +310,7 @@ __global__ __launch_bounds__(256) void mlp_fwd_head_kernel(
     __builtin_amdgcn_sched_barrier(0);
   }
 
+  if constexpr (INFER) return;
   // ---- per-workgroup reduction (fixed order) into this workgroup's slab ----
   __syncthreads();  // W1 image no longer needed: reuse it
   float* red = reinterpret_cast<float*>(lds);  // [4][16 classes][H]
@@ -329,13 +341,14 @@ __global__ __launch_bounds__(256) void mlp_fwd_head_kernel(
   }
 }
 
-template <int H, int K0>
+template <int H, int K0, bool INFER = false>
 int launch(const bf16_t* X, const bf16_t* W0, const float* b0, const bf16_t* W1, const float* b1,
            const bf16_t* Wo, const float* bo, const int32_t* labels, int B, int C, float scale, bf16_t* h1,
-           bf16_t* dact, float* slab, float* block_loss, int32_t* block_correct, int nwg, hipStream_t s) {
+           bf16_t* dact, float* slab, float* block_loss, int32_t* block_correct, int nwg, hipStream_t s,
+           float* logits = nullptr, int32_t* pred = nullptr) {
   const size_t lds = ((size_t)(H + NCLS) * Pitch<H>::v + NCLS * H + 4 * SCR) * sizeof(bf16_t) + 2 * H * sizeof(float);
-  mlp_fwd_head_kernel<H, K0><<<nwg, 256, lds, s>>>(X, W0, b0, W1, b1, Wo, bo, labels, B, C, scale, h1, dact, slab,
-                                                   block_loss, block_correct);
+  mlp_fwd_head_kernel<H, K0, INFER><<<nwg, 256, lds, s>>>(X, W0, b0, W1, b1, Wo, bo, labels, B, C, scale, h1, dact,
+                                                          slab, block_loss, block_correct, logits, pred);
   HAR_CHECK_LAUNCH();
   return 0;
 }
@@ -360,5 +373,19 @@ extern "C" int har_mlp_fwd_head(const uint16_t* X, int K0, const uint16_t* W0, c
   if (H == 256 && K0 == 32) return launch<256, 32>(X, W0, b0, W1, b1, Wo, bo, labels, B, C, scale, h1, dact, slab, block_loss, block_correct, nwg, s);
   if (H == 128 && K0 == 64) return launch<128, 64>(X, W0, b0, W1, b1, Wo, bo, labels, B, C, scale, h1, dact, slab, block_loss, block_correct, nwg, s);
   if (H == 128 && K0 == 32) return launch<128, 32>(X, W0, b0, W1, b1, Wo, bo, labels, B, C, scale, h1, dact, slab, block_loss, block_correct, nwg, s);
+  return -4;
+}
+
+extern "C" int har_mlp_fwd_infer(const uint16_t* X, int K0, const uint16_t* W0, const float* b0, const uint16_t* W1,
+                                 const float* b1, int H, const uint16_t* Wo, const float* bo, int B, int C,
+                                 float* logits, int32_t* pred, hipStream_t s) {
+  if (B <= 0 || B % 16 || C < 1 || C > NCLS) return -2;
+  if (((uintptr_t)X | (uintptr_t)W0 | (uintptr_t)W1 | (uintptr_t)Wo | (uintptr_t)b0 | (uintptr_t)b1) & 15) return -3;
+  const int nwg = har_mlp_fwd_head_grid(B);
+  const bf16_t* x = X;
+  if (H == 256 && K0 == 64) return launch<256, 64, true>(x, W0, b0, W1, b1, Wo, bo, nullptr, B, C, 1.f, nullptr, nullptr, nullptr, nullptr, nullptr, nwg, s, logits, pred);
+  if (H == 256 && K0 == 32) return launch<256, 32, true>(x, W0, b0, W1, b1, Wo, bo, nullptr, B, C, 1.f, nullptr, nullptr, nullptr, nullptr, nullptr, nwg, s, logits, pred);
+  if (H == 128 && K0 == 64) return launch<128, 64, true>(x, W0, b0, W1, b1, Wo, bo, nullptr, B, C, 1.f, nullptr, nullptr, nullptr, nullptr, nullptr, nwg, s, logits, pred);
+  if (H == 128 && K0 == 32) return launch<128, 32, true>(x, W0, b0, W1, b1, Wo, bo, nullptr, B, C, 1.f, nullptr, nullptr, nullptr, nullptr, nullptr, nwg, s, logits, pred);
   return -4;
 }

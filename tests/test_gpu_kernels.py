@@ -308,3 +308,25 @@ def test_mlp_fused_fwd_head_matches_unfused(cuda, H, F):
     torch.testing.assert_close(a.P, b.P, rtol=0, atol=5e-4)
     a.forward_backward_native(X[:4090], y[:4090], 1.0 / 4090)
     assert not a.last_fused
+
+
+@pytest.mark.parametrize("H,F", [(256, 43), (128, 20)])
+def test_mlp_fused_infer_matches_fp32(cuda, H, F):
+    """Serving variant of the fused kernel (logits + argmax only) vs the fp32 PyTorch forward
+    of the same parameters (bf16 operands: relative logit error ~1e-2)."""
+    from har.models.mlp import MLPEngine, pad_input_bf16
+
+    B = 4096
+    eng = MLPEngine([F, H, H, 6], B, cuda, lr=1e-3, seed=9)
+    g = torch.Generator(device=cuda).manual_seed(3)
+    X = torch.randn(B, F, device=cuda, generator=g)
+    logits, pred = eng.infer_fused(pad_input_bf16(X, eng.layout.in_pad))
+    Xp = torch.zeros(B, eng.layout.in_pad, device=cuda)
+    Xp[:, :F] = X
+    ref = eng.torch_forward(eng.P, Xp).float()
+    assert logits.shape == (B, 6) and pred.dtype == torch.int32
+    assert float((logits - ref).norm() / ref.norm()) < 2e-2
+    assert torch.equal(pred.long(), torch.argmax(logits, 1))  # in-kernel argmax of its own logits
+    agree = float((pred.long() == torch.argmax(ref, 1)).float().mean())
+    assert agree > 0.97
+    torch.testing.assert_close(eng.logits(X), logits)  # logits() takes the fused path

@@ -116,3 +116,34 @@ def test_yaml_configs_load():
         cfg = config_from_args(["--preset-file", f])
         for k, v in d.items():
             assert getattr(cfg, k) == v
+
+
+def test_predict_cli_from_saved_models(tmp_path, wisdm_csv):
+    """predict.py re-encodes raw CSV rows with the saved PipelineModel and reproduces the
+    saved model's predictions; unlabeled input (no ACTIVITY column) is served too."""
+    import main
+    import predict
+
+    mdir = tmp_path / "models"
+    main.run(main.config_from_args(["--data", wisdm_csv, "--out-dir", str(tmp_path / "out"), "--device", "cpu",
+                                    "--preset", "all-numeric", "--classifiers", "dt,nb",
+                                    "--save-models", str(mdir)]))
+    rec = predict.main(["--models", str(mdir), "--model", "dt", "--data", wisdm_csv, "--device", "cpu",
+                        "--out", str(tmp_path / "p.csv")])
+    assert rec["rows"] == 5418 and rec["accuracy"] > 0.6 and rec["predict_windows_per_s"] > 0
+    with open(tmp_path / "p.csv") as f:
+        rows = list(csv.reader(f))
+    assert rows[0] == ["row", "UID", "prediction", "label_name", "probability"] and len(rows) == 5419
+    assert rows[1][3] in ("Walking", "Jogging", "Upstairs", "Downstairs", "Sitting", "Standing")
+    # unlabeled serving input: drop ACTIVITY -> no metrics, same predictions
+    lines = open(wisdm_csv).read().splitlines()
+    hdr = lines[0].split(",")
+    j = hdr.index("ACTIVITY")
+    unl = tmp_path / "unlabeled.csv"
+    unl.write_text("\n".join(",".join(c for k, c in enumerate(l.split(",")) if k != j) for l in lines[:201]) + "\n")
+    rec2 = predict.main(["--models", str(mdir), "--model", "dt", "--data", str(unl), "--device", "cpu",
+                         "--out", str(tmp_path / "q.csv")])
+    assert rec2["rows"] == 200 and "accuracy" not in rec2
+    with open(tmp_path / "q.csv") as f:
+        q = list(csv.reader(f))
+    assert [r[2] for r in q[1:]] == [r[2] for r in rows[1:201]]
