@@ -112,7 +112,7 @@ class ForestBuilder:
         for f, t in enumerate(self.thresholds):
             thr_mat[f, : len(t)] = t
         self.thr_mat = torch.from_numpy(thr_mat).to(X.device)
-        self.bins = bin_features(X, self.thresholds).to(X.device)  # [F, N] uint8 (HIP kernel on the GPU)
+        self.bins = bin_features(X, self.thresholds).to(X.device).contiguous()  # [F, N] uint8 (HIP on the GPU)
 
     def bootstrap_weights(self, N: int, device, row_offset: int = 0) -> torch.Tensor:
         if not self.bootstrap:
@@ -151,8 +151,8 @@ class ForestBuilder:
         stats = torch.zeros(Tn, maxn, K, dtype=torch.float32, device=dev)
         gains = torch.zeros(Tn, maxn, dtype=torch.float32, device=dev)
         # root class counts
-        root = torch.zeros(Tn, K, dtype=torch.float32, device=dev)
-        root.scatter_add_(1, y.long().view(1, -1).expand(Tn, -1), W)
+        # [T, N] x one-hot [N, K]: one GEMM (exact: integer weights) instead of T*N contended atomics
+        root = W @ torch.nn.functional.one_hot(y.long(), K).to(W.dtype)
         if self.allreduce is not None:
             self.allreduce(root)
         stats[:, 0] = root
@@ -175,21 +175,49 @@ class ForestBuilder:
             if A == 0:
                 break
             # ---- group the rows of every candidate node ----
-            cand_idx = torch.full((Tn, maxn), -1, dtype=torch.int64, device=dev)
-            cand_idx[torch.as_tensor(ct, device=dev), torch.as_tensor(cn, device=dev)] = torch.arange(A, device=dev)
-            valid = node_of >= 0
-            key = torch.where(valid, cand_idx.gather(1, node_of.clamp_min(0).long()), torch.full_like(node_of, -1,
-                                                                                                  dtype=torch.int64))
-            sel = key >= 0
-            tt, rr = torch.nonzero(sel, as_tuple=True)
-            kk = key[tt, rr]
-            order = torch.argsort(kk, stable=True)
-            rows = rr[order].to(torch.int32).contiguous()
-            keys = kk[order]
-            row_w = W[tt[order], rr[order]].contiguous()
-            counts = torch.bincount(keys, minlength=A).to(torch.int32)
-            starts = (torch.cumsum(counts, 0) - counts).to(torch.int32)
-            feats = torch.from_numpy(rng.feature_subsets(self.seed, ct + self.tree_offset, cn, F, m)).to(dev)
+            if use_native:
+                # device: int32 keys from one HIP pass, a 32-bit radix sort, counts by binary search
+                # over the sorted keys (no atomics), feature subsets drawn on the device
+                mod = _native.kernels()
+                st_ptr = _native.stream_ptr()
+                cand_idx = torch.full((Tn, maxn), -1, dtype=torch.int32, device=dev)
+                cand_idx[torch.as_tensor(ct, device=dev), torch.as_tensor(cn, device=dev)] = \
+                    torch.arange(A, dtype=torch.int32, device=dev)
+                key = torch.empty(Tn * N, dtype=torch.int32, device=dev)
+                mod.tree_level_keys(node_of.data_ptr(), cand_idx.data_ptr(), Tn, N, maxn, key.data_ptr(), st_ptr)
+                flat = torch.nonzero(key >= 0).squeeze(1)
+                keys, order = torch.sort(key[flat], stable=True)
+                fo = flat[order]
+                rows = (fo % N).to(torch.int32).contiguous()
+                row_w = W.reshape(-1)[fo].contiguous()
+                bounds = torch.searchsorted(keys, torch.arange(A + 1, dtype=torch.int32, device=dev))
+                counts = (bounds[1:] - bounds[:-1]).to(torch.int32)
+                starts = bounds[:-1].to(torch.int32).contiguous()
+                if m >= F:
+                    feats = torch.arange(F, dtype=torch.int32, device=dev).repeat(A, 1)
+                else:
+                    feats = torch.empty(A, m, dtype=torch.int32, device=dev)
+                    tr = torch.as_tensor(ct + self.tree_offset, dtype=torch.int32, device=dev)
+                    nd = torch.as_tensor(cn, dtype=torch.int32, device=dev)
+                    mod.tree_feature_subsets(self.seed, tr.data_ptr(), nd.data_ptr(), A, F, m, feats.data_ptr(),
+                                             st_ptr)
+            else:
+                cand_idx = torch.full((Tn, maxn), -1, dtype=torch.int64, device=dev)
+                cand_idx[torch.as_tensor(ct, device=dev), torch.as_tensor(cn, device=dev)] = torch.arange(A,
+                                                                                                         device=dev)
+                valid = node_of >= 0
+                key = torch.where(valid, cand_idx.gather(1, node_of.clamp_min(0).long()),
+                                  torch.full_like(node_of, -1, dtype=torch.int64))
+                sel = key >= 0
+                tt, rr = torch.nonzero(sel, as_tuple=True)
+                kk = key[tt, rr]
+                order = torch.argsort(kk, stable=True)
+                rows = rr[order].to(torch.int32).contiguous()
+                keys = kk[order]
+                row_w = W[tt[order], rr[order]].contiguous()
+                counts = torch.bincount(keys, minlength=A).to(torch.int32)
+                starts = (torch.cumsum(counts, 0) - counts).to(torch.int32)
+                feats = torch.from_numpy(rng.feature_subsets(self.seed, ct + self.tree_offset, cn, F, m)).to(dev)
             # ---- histogram + best split ----
             if use_native:
                 res = T.hist_split_native(self.bins, self.nbins, y32, rows, row_w, starts, counts, feats, K,
@@ -230,6 +258,19 @@ class ForestBuilder:
             stats[ti, cl] = lstat
             stats[ti, cl + 1] = res.total[dsi] - lstat
             # ---- partition: rows of the nodes split at THIS level move to a child, all others finish ----
+            if use_native:
+                lf = torch.full((Tn, maxn), -1, dtype=torch.int32, device=dev)
+                lb = torch.zeros(Tn, maxn, dtype=torch.int32, device=dev)
+                ll = torch.zeros(Tn, maxn, dtype=torch.int32, device=dev)
+                lf[ti, ni] = bf.to(torch.int32)
+                lb[ti, ni] = bb.to(torch.int32)
+                ll[ti, ni] = cl.to(torch.int32)
+                node_of = node_of.contiguous()
+                _native.kernels().tree_partition(node_of.data_ptr(), lf.data_ptr(), lb.data_ptr(), ll.data_ptr(),
+                                                 self.bins.data_ptr(), Tn, N, maxn, _native.stream_ptr())
+                front_t = np.repeat(st_t, 2)
+                front_n = np.stack([child_l, child_l + 1], 1).reshape(-1)
+                continue
             lvl_feat = torch.full((Tn, maxn), -1, dtype=torch.int64, device=dev)
             lvl_bin = torch.zeros(Tn, maxn, dtype=torch.int64, device=dev)
             lvl_left = torch.zeros(Tn, maxn, dtype=torch.int64, device=dev)

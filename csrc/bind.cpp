@@ -228,6 +228,22 @@ PYBIND11_MODULE(_har_native, m) {
           "bin_features");
   });
 
+  m.def("tree_feature_subsets", [](uint64_t seed, u trees, u nodes, int64_t npairs, int F, int m_, u out, u stream) {
+    check(har_tree_feature_subsets(seed, P<const int32_t>(trees), P<const int32_t>(nodes), npairs, F, m_,
+                                   P<int32_t>(out), S(stream)),
+          "tree_feature_subsets");
+  });
+  m.def("tree_level_keys", [](u node_of, u cand_idx, int T, int64_t N, int maxn, u key, u stream) {
+    check(har_tree_level_keys(P<const int32_t>(node_of), P<const int32_t>(cand_idx), T, N, maxn, P<int32_t>(key),
+                              S(stream)),
+          "tree_level_keys");
+  });
+  m.def("tree_partition", [](u node_of, u lvl_feat, u lvl_bin, u lvl_left, u bins, int T, int64_t N, int maxn,
+                             u stream) {
+    check(har_tree_partition(P<int32_t>(node_of), P<const int32_t>(lvl_feat), P<const int32_t>(lvl_bin),
+                             P<const int32_t>(lvl_left), P<const uint8_t>(bins), T, N, maxn, S(stream)),
+          "tree_partition");
+  });
   m.def("csv_count_newlines", [](u buf, int64_t n, u counts, u stream) {
     check(har_csv_count_newlines(P<const uint8_t>(buf), n, P<int32_t>(counts), S(stream)), "csv_count_newlines");
   });

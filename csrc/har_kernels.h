@@ -123,6 +123,14 @@ int har_tree_hist_split(const uint8_t* bins, int64_t N, int F, const int32_t* nb
                         int32_t* out_bin, float* out_left, float* out_total, int mode, float* ghist,
                         int row_chunks, hipStream_t s);
 // Sum over trees of (normalized) leaf statistics; trees as SoA [T][maxn] arrays, feature < 0 = leaf.
+// Level bookkeeping of the forest builder (tree_level.hip): Floyd feature subsets per (tree, node)
+// (bit-identical to har/ops/rng.py), per-(tree,row) candidate keys, and the row -> child partition.
+int har_tree_feature_subsets(uint64_t seed, const int32_t* trees, const int32_t* nodes, int64_t P, int F, int m,
+                             int32_t* out, hipStream_t s);
+int har_tree_level_keys(const int32_t* node_of, const int32_t* cand_idx, int T, int64_t N, int maxn, int32_t* key,
+                        hipStream_t s);
+int har_tree_partition(int32_t* node_of, const int32_t* lvl_feat, const int32_t* lvl_bin, const int32_t* lvl_left,
+                       const uint8_t* bins, int T, int64_t N, int maxn, hipStream_t s);
 int har_forest_predict(const float* X, int64_t n, int F, int ld, const int32_t* feat, const float* thr,
                        const int32_t* left, const int32_t* right, const float* leaf, int ntrees, int maxn, int K,
                        int max_depth, int normalize, float* raw_out, hipStream_t s);

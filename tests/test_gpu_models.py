@@ -225,3 +225,41 @@ def test_mlp_overlapped_dp_step_equals_fused(cuda):
         assert int(b.step_count[0]) == 3
     finally:
         dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("F,m", [(165, 13), (3100, 56), (43, 7), (20, 20)])
+def test_feature_subsets_device_matches_host(cuda, F, m):
+    """tree_level.hip Floyd sampler == har.ops.rng.feature_subsets (the CPU oracle), bit for bit."""
+    from har.ops import _native
+    from har.ops import rng
+
+    g = np.random.default_rng(F)
+    trees = g.integers(0, 600, 5000)
+    nodes = g.integers(0, 2047, 5000)
+    host = rng.feature_subsets(7, trees, nodes, F, m)
+    out = torch.empty(5000, m, dtype=torch.int32, device=cuda)
+    tr = torch.as_tensor(trees, dtype=torch.int32, device=cuda)
+    nd = torch.as_tensor(nodes, dtype=torch.int32, device=cuda)
+    _native.kernels().tree_feature_subsets(7, tr.data_ptr(), nd.data_ptr(), 5000, F, m, out.data_ptr(),
+                                           _native.stream_ptr())
+    assert np.array_equal(out.cpu().numpy(), host)
+
+
+def test_random_forest_gpu_equals_cpu_builder(cuda):
+    """The device level loop (HIP keys / partition / feature subsets) grows the forest of the
+    CPU builder (PyTorch oracle) on integer-weighted bootstraps: identical top levels; deeper,
+    a near-tie between two candidate splits may resolve differently (fp64 gains summed in a
+    different order), so the forests' predictions are compared there."""
+    from har.models.tree import RandomForestClassifier
+    from har.ops import tree as T
+
+    x, y = _blobs(3000, 24, 5, seed=3)
+    thr = T.find_thresholds(x.numpy(), 32)
+    c = RandomForestClassifier(numTrees=12, maxDepth=6, seed=4).fit_tensors(x, y, 5, thresholds=thr)
+    g = RandomForestClassifier(numTrees=12, maxDepth=6, seed=4).fit_tensors(x.to(cuda), y.to(cuda), 5,
+                                                                            thresholds=thr)
+    assert torch.equal(g.arrs.feature[:, :7].cpu(), c.arrs.feature[:, :7])  # depth 0-2 of every tree
+    torch.testing.assert_close(g.arrs.stats[:, :7].cpu(), c.arrs.stats[:, :7])
+    same_node = float((g.arrs.feature.cpu() == c.arrs.feature).float().mean())
+    agree = float((g.predict(x.to(cuda)).cpu() == c.predict(x)).float().mean())
+    assert same_node > 0.97 and agree > 0.99, (same_node, agree)
