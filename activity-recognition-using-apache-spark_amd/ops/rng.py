@@ -108,7 +108,7 @@ def feature_subsets(seed: int, trees, nodes, n_features: int, m: int) -> np.ndar
     """Floyd's sampling of ``m`` distinct features out of ``n_features`` for each
     (tree, node) pair (vectorized over pairs).  Draw i of pair (t, n) uses
     counter ``t<<32 | n<<8 | i`` (so m <= 256, node < 2^24).  Returns int32
-    [P, m], each row sorted ascending.  ``csrc/kernels/tree.hip`` implements the
+    [P, m], each row sorted ascending.  ``csrc/kernels/tree_level.hip`` implements the
     identical procedure per node on device."""
     trees = np.asarray(trees, dtype=np.uint64).reshape(-1)
     nodes = np.asarray(nodes, dtype=np.uint64).reshape(-1)

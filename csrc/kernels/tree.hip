@@ -20,20 +20,6 @@ namespace {
 
 constexpr int KMAX = 32;
 
-__device__ __forceinline__ double impurity_of(const double* c, double w, int K, int kind) {
-  if (w <= 0) return 0.0;
-  double s = 0.0;
-  if (kind == 0) {
-    for (int k = 0; k < K; ++k) { double p = c[k] / w; s += p * p; }
-    return 1.0 - s;
-  }
-  for (int k = 0; k < K; ++k) {
-    double p = c[k] / w;
-    if (p > 0) s -= p * log2(p);
-  }
-  return s;
-}
-
 __global__ __launch_bounds__(256) void tree_hist_split_kernel(
     const uint8_t* __restrict__ bins, int64_t N, const int32_t* __restrict__ nbins_feat,
     const int32_t* __restrict__ rows, const float* __restrict__ row_w, const int32_t* __restrict__ node_start,
@@ -63,15 +49,29 @@ __global__ __launch_bounds__(256) void tree_hist_split_kernel(
   for (int i = tid; i < f_n; i += blockDim.x) fid[i] = feats[(size_t)a * m + f_lo + i];
   __syncthreads();
 
-  // ---- histogram: (feature slot, row) pairs, rows fastest -> coalesced bin reads ----
-  const int64_t pairs = mode == 2 ? 0 : (int64_t)cnt * f_n;
-  for (int64_t j = tid; j < pairs; j += blockDim.x) {
-    const int fs = (int)(j / cnt);
-    const int ri = (int)(j - (int64_t)fs * cnt);
-    const int r = rows[start + ri];
-    const float w = row_w[start + ri];
-    const int b = bins[(size_t)fid[fs] * N + r];
-    atomicAdd(&hist[(fs * maxbins + b) * K + label[r]], w);
+  // ---- histogram ----
+  if (mode != 2 && cnt >= (int)blockDim.x) {
+    // large node: one row per lane, its (row id, weight, label) loaded once for all f_n features
+    for (int ri = tid; ri < cnt; ri += blockDim.x) {
+      const int r = rows[start + ri];
+      const float w = row_w[start + ri];
+      float* hl = hist + label[r];
+      for (int fs = 0; fs < f_n; ++fs) {
+        const int b = bins[(size_t)fid[fs] * N + r];
+        atomicAdd(hl + (fs * maxbins + b) * K, w);
+      }
+    }
+  } else if (mode != 2) {
+    // small node: (feature slot, row) pairs, rows fastest, so every lane has work
+    const int64_t pairs = (int64_t)cnt * f_n;
+    for (int64_t j = tid; j < pairs; j += blockDim.x) {
+      const int fs = (int)(j / cnt);
+      const int ri = (int)(j - (int64_t)fs * cnt);
+      const int r = rows[start + ri];
+      const float w = row_w[start + ri];
+      const int b = bins[(size_t)fid[fs] * N + r];
+      atomicAdd(&hist[(fs * maxbins + b) * K + label[r]], w);
+    }
   }
   __syncthreads();
   if (mode == 1) {
@@ -85,12 +85,14 @@ __global__ __launch_bounds__(256) void tree_hist_split_kernel(
   }
 
   // ---- split search: one wave per feature slot, one lane per bin ----
+  // Per lane (= threshold bin) the class loop keeps only running sums — no per-class arrays
+  // (which lived in scratch): gini needs sum c^2 of left / right / parent, entropy needs
+  // sum c log2 c (imp = log2 w - sum c log2 c / w), plus the weights.
   double best_g = -INFINITY;
   int best_i = 0x7fffffff;
   for (int fs = wave; fs < f_n; fs += (int)(blockDim.x >> 6)) {
     const int nb = nbins_feat[fid[fs]];
-    double left[KMAX], tot[KMAX];
-    double wl = 0.0, wt = 0.0;
+    double wl = 0.0, wt = 0.0, ql = 0.0, qr = 0.0, qt = 0.0;
     for (int k = 0; k < K; ++k) {
       double v = (lane < nb && lane < maxbins) ? (double)hist[(fs * maxbins + lane) * K + k] : 0.0;
 #pragma unroll
@@ -98,18 +100,28 @@ __global__ __launch_bounds__(256) void tree_hist_split_kernel(
         double u = __shfl_up(v, o, 64);
         if (lane >= o) v += u;
       }
-      left[k] = v;
-      tot[k] = __shfl(v, max(nb - 1, 0), 64);
+      const double t = __shfl(v, max(nb - 1, 0), 64);
+      const double r = t - v;
       wl += v;
-      wt += tot[k];
+      wt += t;
+      if (impurity == 0) {
+        ql += v * v; qr += r * r; qt += t * t;
+      } else {
+        ql += v > 0 ? v * log2(v) : 0.0;
+        qr += r > 0 ? r * log2(r) : 0.0;
+        qt += t > 0 ? t * log2(t) : 0.0;
+      }
     }
     const double wr = wt - wl;
-    double right[KMAX];
-    for (int k = 0; k < K; ++k) right[k] = tot[k] - left[k];
     double g = -INFINITY;
     if (lane < nb - 1 && wl >= min_inst && wr >= min_inst && wt > 0) {
-      g = impurity_of(tot, wt, K, impurity) - (wl / wt) * impurity_of(left, wl, K, impurity) -
-          (wr / wt) * impurity_of(right, wr, K, impurity);
+      double ip, il, ir;
+      if (impurity == 0) {
+        ip = 1.0 - qt / (wt * wt); il = 1.0 - ql / (wl * wl); ir = 1.0 - qr / (wr * wr);
+      } else {
+        ip = log2(wt) - qt / wt; il = log2(wl) - ql / wl; ir = log2(wr) - qr / wr;
+      }
+      g = ip - (wl / wt) * il - (wr / wt) * ir;
     }
     int idx = fs * maxbins + lane;
     // wave argmax, lowest index on ties
