@@ -114,6 +114,9 @@ class ForestBuilder:
         self.thr_mat = torch.from_numpy(thr_mat).to(X.device)
         self.bins = bin_features(X, self.thresholds).to(X.device).contiguous()  # [F, N] uint8 (HIP on the GPU)
 
+    def _levels_native(self, *a):
+        _levels_native_impl(self, *a)
+
     def bootstrap_weights(self, N: int, device, row_offset: int = 0) -> torch.Tensor:
         if not self.bootstrap:
             return torch.ones(self.T, N, dtype=torch.float32, device=device)
@@ -163,6 +166,11 @@ class ForestBuilder:
         front_t = np.arange(Tn, dtype=np.int64)
         front_n = np.zeros(Tn, dtype=np.int64)
         use_native = dev.type == "cuda"
+        if use_native:
+            if y32.numel() and (int(y32.max()) >= K or int(y32.min()) < 0):
+                raise ValueError("labels out of range")
+            self._levels_native(y32, W, N, F, m, maxn, stats, feature, thresh, left, right, gains, n_nodes, node_of)
+            return ForestArrays(feature, thresh, left, right, stats, n_nodes, D, gains)
         for depth in range(D):
             if len(front_t) == 0:
                 break
@@ -287,6 +295,131 @@ class ForestBuilder:
             front_t = np.repeat(st_t, 2)
             front_n = np.stack([child_l, child_l + 1], 1).reshape(-1)
         return ForestArrays(feature, thresh, left, right, stats, n_nodes, D, gains)
+
+
+class _Pinned:
+    """Reusable page-locked staging buffer for the per-level host -> device uploads: an
+    upload from pageable memory synchronizes the stream, so every level would stall
+    several times; one non-blocking copy from here does not.  Each upload site owns one
+    buffer, and the level loop synchronizes once per level (its single device -> host
+    transfer) between two uses of the same buffer, so a copy never reads a rewritten one."""
+
+    def __init__(self, n: int):
+        self.buf = torch.empty(max(1, n), dtype=torch.int64).pin_memory()
+
+    def upload(self, arrays, device):
+        n = sum(len(a) for a in arrays)
+        if n > self.buf.numel():
+            self.buf = torch.empty(2 * n, dtype=torch.int64).pin_memory()
+        o, out = 0, []
+        host = self.buf.numpy()
+        for a in arrays:
+            host[o:o + len(a)] = a
+            o += len(a)
+        dev = self.buf[:n].to(device, non_blocking=True)
+        o = 0
+        for a in arrays:
+            out.append(dev[o:o + len(a)])
+            o += len(a)
+        return out
+
+
+def _levels_native_impl(b: "ForestBuilder", y32, W, N: int, F: int, m: int, maxn: int, stats, feature, thresh,
+                        left, right, gains, n_nodes, node_of):
+    """Device level loop with ONE device -> host transfer per level.
+
+    Per level: candidate keys (HIP), a 32-bit radix sort of all (tree, row) keys (finished
+    rows sort first, key -1, so no compaction / nonzero sync), node row ranges by binary
+    search, device feature subsets, the fused histogram + split kernel, then — for every
+    candidate — split decision and both children's candidacy computed on the device and
+    fetched together; the host only allocates child ids (numpy) and uploads them through a
+    pinned buffer without blocking."""
+    dev = W.device
+    Tn, K, D = b.T, b.K, b.D
+    mod = _native.kernels()
+    st_ptr = _native.stream_ptr()
+    pin_a, pin_b = _Pinned(8 * Tn), _Pinned(8 * Tn)  # one per upload site (see _Pinned)
+    Wf = W.reshape(-1).contiguous()
+    ar_n = None
+    bins_rm = b.bins.t().contiguous()  # [N, F] for the histogram gathers (partition keeps [F, N])
+
+    def candidacy(c: torch.Tensor):
+        w = c.sum(-1)
+        imp = T._impurity(c.double(), w.double(), b.impurity)
+        return (imp > 1e-12) & (w >= 2 * b.min_inst), w
+
+    c0, w0 = candidacy(stats[:, 0])
+    host0 = torch.stack([c0.float(), w0.float()]).cpu().numpy()
+    front_t = np.arange(Tn, dtype=np.int64)
+    front_n = np.zeros(Tn, dtype=np.int64)
+    cand = host0[0] > 0
+    wtot = host0[1]
+    for depth in range(D):
+        ct, cn, cw = front_t[cand], front_n[cand], wtot[cand]
+        A = len(ct)
+        if A == 0:
+            break
+        ct_d, cn_d, tr_d = pin_a.upload([ct, cn, ct + b.tree_offset], dev)
+        cand_idx = torch.full((Tn, maxn), -1, dtype=torch.int32, device=dev)
+        cand_idx[ct_d, cn_d] = torch.arange(A, dtype=torch.int32, device=dev)
+        key = torch.empty(Tn * N, dtype=torch.int32, device=dev)
+        mod.tree_level_keys(node_of.data_ptr(), cand_idx.data_ptr(), Tn, N, maxn, key.data_ptr(), st_ptr)
+        keys, order = torch.sort(key, stable=True)
+        rows = (order % N).to(torch.int32)
+        row_w = Wf[order]
+        if ar_n is None or ar_n.numel() < A + 1:
+            ar_n = torch.arange(max(A + 1, 2 * Tn), dtype=torch.int32, device=dev)
+        bounds = torch.searchsorted(keys, ar_n[:A + 1])
+        counts = (bounds[1:] - bounds[:-1]).to(torch.int32)
+        starts = bounds[:-1].to(torch.int32)
+        if m >= F:
+            feats = torch.arange(F, dtype=torch.int32, device=dev).repeat(A, 1)
+        else:
+            feats = torch.empty(A, m, dtype=torch.int32, device=dev)
+            tr32 = tr_d.to(torch.int32)
+            cn32 = cn_d.to(torch.int32)
+            mod.tree_feature_subsets(b.seed, tr32.data_ptr(), cn32.data_ptr(), A, F, m, feats.data_ptr(), st_ptr)
+        res = T.hist_split_native(b.bins, b.nbins, y32, rows, row_w, starts, counts, feats, K, b.max_bins,
+                                  b.min_inst, b.min_gain, b.impurity,
+                                  allreduce=None if b.owner is not None else b.allreduce, owner=b.owner,
+                                  max_rows=int(cw.max()) if A else 0, check_labels=False, bins_rm=bins_rm)
+        do_split = (res.gain > 0) & torch.isfinite(res.gain)
+        lstat = res.left
+        rstat = res.total - lstat
+        cl_ok, wl = candidacy(lstat)
+        cr_ok, wr = candidacy(rstat)
+        h = torch.stack([do_split.float(), cl_ok.float(), cr_ok.float(), wl.float(), wr.float()]).cpu().numpy()
+        ds = h[0] > 0
+        if not ds.any():
+            break
+        st_t, st_n = ct[ds], cn[ds]
+        # children: per tree, consecutive ids (the frontier stays grouped by tree)
+        rank_in_tree = np.arange(len(st_t)) - np.searchsorted(st_t, st_t, side="left")
+        child_l = n_nodes[st_t] + 2 * rank_in_tree
+        n_nodes += 2 * np.bincount(st_t, minlength=Tn)
+        dsi_h = np.nonzero(ds)[0]
+        ti, ni, cl, dsi = pin_b.upload([st_t, st_n, child_l, dsi_h], dev)
+        bf = res.feat[dsi].long()
+        bb = res.bin[dsi].long()
+        feature[ti, ni] = bf.to(torch.int32)
+        thresh[ti, ni] = b.thr_mat[bf, bb]
+        left[ti, ni] = cl.to(torch.int32)
+        right[ti, ni] = (cl + 1).to(torch.int32)
+        gains[ti, ni] = res.gain[dsi] * res.total[dsi].sum(1)
+        stats[ti, cl] = lstat[dsi]
+        stats[ti, cl + 1] = rstat[dsi]
+        lf = torch.full((Tn, maxn), -1, dtype=torch.int32, device=dev)
+        lb = torch.zeros(Tn, maxn, dtype=torch.int32, device=dev)
+        ll = torch.zeros(Tn, maxn, dtype=torch.int32, device=dev)
+        lf[ti, ni] = bf.to(torch.int32)
+        lb[ti, ni] = bb.to(torch.int32)
+        ll[ti, ni] = cl.to(torch.int32)
+        mod.tree_partition(node_of.data_ptr(), lf.data_ptr(), lb.data_ptr(), ll.data_ptr(), b.bins.data_ptr(), Tn, N,
+                           maxn, st_ptr)
+        front_t = np.repeat(st_t, 2)
+        front_n = np.stack([child_l, child_l + 1], 1).reshape(-1)
+        cand = np.stack([h[1][ds] > 0, h[2][ds] > 0], 1).reshape(-1)
+        wtot = np.stack([h[3][ds], h[4][ds]], 1).reshape(-1)
 
 
 def predict_forest(arrs: ForestArrays, X: torch.Tensor, normalize: bool) -> torch.Tensor:

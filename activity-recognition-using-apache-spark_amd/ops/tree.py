@@ -165,7 +165,8 @@ def split_owner(hist: torch.Tensor, feats: torch.Tensor, K: int, owner, split_fn
 
 
 def hist_split_native(bins, nbins_feat, label, rows, row_w, node_start, node_count, feats, K, max_bins,
-                      min_instances, min_info_gain, impurity, allreduce=None, owner=None) -> LevelResult:
+                      min_instances, min_info_gain, impurity, allreduce=None, owner=None, max_rows=None,
+                      check_labels: bool = True, bins_rm=None) -> LevelResult:
     """Fused LDS histogram + split on one device; in data parallel the kernel runs twice:
     histogram-only into a [A, m, bins, K] buffer, then either one RCCL all-reduce of it and
     split search for every node (``allreduce``), or a reduce-scatter by node owner, split
@@ -180,17 +181,21 @@ def hist_split_native(bins, nbins_feat, label, rows, row_w, node_start, node_cou
     bin_ = torch.empty(A * chunks, dtype=torch.int32, device=dev)
     left = torch.empty(A * chunks, K, dtype=torch.float32, device=dev)
     total = torch.empty(A, K, dtype=torch.float32, device=dev)
-    if label.numel() and (int(label.max()) >= K or int(label.min()) < 0):
+    # (host syncs) the forest builder checks the labels once per fit and passes a row-count hint
+    if check_labels and label.numel() and (int(label.max()) >= K or int(label.min()) < 0):
         raise ValueError("labels out of range")
     mod = _native.kernels()
-    args = [bins.data_ptr(), N, F, nbins_feat.data_ptr(), rows.data_ptr(), row_w.data_ptr(), node_start.data_ptr(),
+    # bins_rm: optional row-major [N, F] copy of the bins (one row's features in one or two lines)
+    bptr, row_major = (bins_rm.data_ptr(), 1) if bins_rm is not None else (bins.data_ptr(), 0)
+    args = [bptr, N, F, row_major, nbins_feat.data_ptr(), rows.data_ptr(), row_w.data_ptr(), node_start.data_ptr(),
             node_count.data_ptr(), A, feats.data_ptr(), m, fc, label.data_ptr(), K, max_bins, float(min_instances),
             float(min_info_gain), impurity, gain.data_ptr(), feat.data_ptr(), bin_.data_ptr(), left.data_ptr(),
             total.data_ptr()]
     # few large nodes (the top levels): split every node's rows over several workgroups so the
     # launch still fills 256 CUs; their LDS histograms merge into a global one
     blocks = A * chunks
-    max_rows = int(node_count.max()) if A else 0
+    if max_rows is None:
+        max_rows = int(node_count.max()) if A else 0
     row_chunks = 1
     if blocks < 1024 and max_rows > 4096:
         row_chunks = int(min((1024 + blocks - 1) // blocks, (max_rows + 2047) // 2048))
@@ -207,7 +212,7 @@ def hist_split_native(bins, nbins_feat, label, rows, row_w, node_start, node_cou
             lf = torch.empty(n * chunks, K, dtype=torch.float32, device=dev)
             tot = torch.empty(n, K, dtype=torch.float32, device=dev)
             loc = local.contiguous()
-            sl = [bins.data_ptr(), N, F, nbins_feat.data_ptr(), rows.data_ptr(), row_w.data_ptr(),
+            sl = [bptr, N, F, row_major, nbins_feat.data_ptr(), rows.data_ptr(), row_w.data_ptr(),
                   node_start.data_ptr() + 4 * a0, node_count.data_ptr() + 4 * a0, n, feats.data_ptr() + 4 * a0 * m,
                   m, fc, label.data_ptr(), K, max_bins, float(min_instances), float(min_info_gain), impurity,
                   g.data_ptr(), f.data_ptr(), b.data_ptr(), lf.data_ptr(), tot.data_ptr()]

@@ -144,11 +144,11 @@ PYBIND11_MODULE(_har_native, m) {
           "regression_moments");
   });
 
-  m.def("tree_hist_split", [](u bins, int64_t N, int F, u nbins, u rows, u row_w, u node_start, u node_count, int A,
+  m.def("tree_hist_split", [](u bins, int64_t N, int F, int row_major, u nbins, u rows, u row_w, u node_start, u node_count, int A,
                               u feats, int m, int fc, u label, int K, int maxbins, float min_inst, float min_gain,
                               int impurity, u gain, u feat, u bin, u left, u total, int mode, u ghist, int row_chunks,
                               u stream) {
-    check(har_tree_hist_split(P<const uint8_t>(bins), N, F, P<const int32_t>(nbins), P<const int32_t>(rows),
+    check(har_tree_hist_split(P<const uint8_t>(bins), N, F, row_major, P<const int32_t>(nbins), P<const int32_t>(rows),
                               P<const float>(row_w), P<const int32_t>(node_start), P<const int32_t>(node_count), A,
                               P<const int32_t>(feats), m, fc, P<const int32_t>(label), K, maxbins, min_inst, min_gain,
                               impurity, P<float>(gain), P<int32_t>(feat), P<int32_t>(bin), P<float>(left),

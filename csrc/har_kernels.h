@@ -116,7 +116,7 @@ int har_window_features(const float* stream, int64_t n_samples, int axes, int wi
 // out_total [A][K] = node class counts.  mode 0 fused; 1 histogram only -> ghist [A][m][maxbins][K];
 // 2 split search from ghist (after a cross-rank reduction).  row_chunks > 1 (mode 1 only): each node's
 // rows are split over that many workgroups that atomically merge into a ZEROED ghist.
-int har_tree_hist_split(const uint8_t* bins, int64_t N, int F, const int32_t* nbins_feat, const int32_t* rows,
+int har_tree_hist_split(const uint8_t* bins, int64_t N, int F, int row_major, const int32_t* nbins_feat, const int32_t* rows,
                         const float* row_w, const int32_t* node_start, const int32_t* node_count, int A,
                         const int32_t* feats, int m, int fc, const int32_t* label, int K, int maxbins,
                         float min_inst, float min_gain, int impurity, float* out_gain, int32_t* out_feat,

@@ -21,7 +21,7 @@ namespace {
 constexpr int KMAX = 32;
 
 __global__ __launch_bounds__(256) void tree_hist_split_kernel(
-    const uint8_t* __restrict__ bins, int64_t N, const int32_t* __restrict__ nbins_feat,
+    const uint8_t* __restrict__ bins, int64_t fstride, int64_t rstride, const int32_t* __restrict__ nbins_feat,
     const int32_t* __restrict__ rows, const float* __restrict__ row_w, const int32_t* __restrict__ node_start,
     const int32_t* __restrict__ node_count, const int32_t* __restrict__ feats, int m, int fc,
     const int32_t* __restrict__ label, int K, int maxbins, float min_inst, float min_gain, int impurity,
@@ -57,7 +57,7 @@ __global__ __launch_bounds__(256) void tree_hist_split_kernel(
       const float w = row_w[start + ri];
       float* hl = hist + label[r];
       for (int fs = 0; fs < f_n; ++fs) {
-        const int b = bins[(size_t)fid[fs] * N + r];
+        const int b = bins[fid[fs] * fstride + r * rstride];
         atomicAdd(hl + (fs * maxbins + b) * K, w);
       }
     }
@@ -69,7 +69,7 @@ __global__ __launch_bounds__(256) void tree_hist_split_kernel(
       const int ri = (int)(j - (int64_t)fs * cnt);
       const int r = rows[start + ri];
       const float w = row_w[start + ri];
-      const int b = bins[(size_t)fid[fs] * N + r];
+      const int b = bins[fid[fs] * fstride + r * rstride];
       atomicAdd(&hist[(fs * maxbins + b) * K + label[r]], w);
     }
   }
@@ -209,7 +209,9 @@ __global__ __launch_bounds__(256) void poisson_bootstrap_kernel(uint64_t seed, i
 
 }  // namespace
 
-extern "C" int har_tree_hist_split(const uint8_t* bins, int64_t N, int F, const int32_t* nbins_feat,
+// bins: feature-major [F][N] (row_major = 0) or row-major [N][F] (row_major = 1: the bytes of one
+// row's sampled features share one or two cache lines — the deep levels gather far less).
+extern "C" int har_tree_hist_split(const uint8_t* bins, int64_t N, int F, int row_major, const int32_t* nbins_feat,
                                    const int32_t* rows, const float* row_w, const int32_t* node_start,
                                    const int32_t* node_count, int A, const int32_t* feats, int m, int fc,
                                    const int32_t* label, int K, int maxbins, float min_inst, float min_gain,
@@ -224,7 +226,8 @@ extern "C" int har_tree_hist_split(const uint8_t* bins, int64_t N, int F, const 
   if (lds > 150 * 1024) return -3;
   if (row_chunks > 1 && mode != 1) return -5;
   dim3 grid(chunks, A, row_chunks > 1 ? row_chunks : 1);
-  tree_hist_split_kernel<<<grid, 256, lds, s>>>(bins, N, nbins_feat, rows, row_w, node_start, node_count, feats, m,
+  const int64_t fstride = row_major ? 1 : N, rstride = row_major ? F : 1;
+  tree_hist_split_kernel<<<grid, 256, lds, s>>>(bins, fstride, rstride, nbins_feat, rows, row_w, node_start, node_count, feats, m,
                                                 fc, label, K, maxbins, min_inst, min_gain, impurity, out_gain,
                                                 out_feat, out_bin, out_left, out_total, mode, ghist);
   HAR_CHECK_LAUNCH();
