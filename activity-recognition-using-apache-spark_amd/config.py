@@ -55,6 +55,7 @@ class RunConfig:
     mlp_lr: float = 2e-3
     # artefacts
     plots: bool = False
+    report: bool = False                   # Results table + charts + index.html (report/summary.py)
     save_models: Optional[str] = None
     append_csv: bool = False
     echo: bool = False

@@ -13,6 +13,7 @@ DecisionTree(+CV), RandomForest(+CV) — plus NaiveBayes and an MLP — and writ
     python main.py --preset rf-deep                  # RF 100 trees x depth 10 on the GPU
     python main.py --preset all-numeric --save-models models/
     python main.py --csv-device                      # CSV parsed + dictionary-encoded by the HIP kernels
+    python main.py --report                          # + Results table, charts and index.html (report/)
     torchrun --nproc-per-node 8 --master-addr 127.0.0.1 main.py   # data parallel over 8 GPUs (RCCL)
 
 Under ``torch.distributed.run`` every rank loads the (small) table and every model is
@@ -209,6 +210,11 @@ def run(cfg: RunConfig, ctx=None) -> dict:
                "phases_s": {k: round(v, 6) for k, v in timer.as_dict().items()}}
     csvout.append_jsonl(os.path.join(cfg.out_dir, "metrics.jsonl"), summary)
     log.close()
+    if cfg.report:
+        from har.report.summary import write_report
+
+        with open(os.path.join(cfg.out_dir, "result.txt")) as fh:
+            write_report(summary, os.path.join(cfg.out_dir, "report"), fh.read())
     if cfg.plots:
         from har.report.plots import write_plots
 

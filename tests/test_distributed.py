@@ -80,17 +80,19 @@ def _run(what, world=2):
     return [torch.load(os.path.join(d, f"{what}_{r}.pt"), weights_only=True) for r in range(world)]
 
 
-def test_dp_logreg_equals_single():
+@pytest.mark.parametrize("world", [2, 4])
+def test_dp_logreg_equals_single(world):
     from har.models.logreg import FitSpec, LogisticRegression
 
-    outs = _run("lr")
-    torch.testing.assert_close(outs[0], outs[1])
+    outs = _run("lr", world)
+    for o in outs[1:]:
+        torch.testing.assert_close(outs[0], o)
     X, y = _data()
     ms = LogisticRegression(maxIter=15).fit_many(X, y, [FitSpec(None, 0.1, 0.0), FitSpec(None, 0.05, 0.3)], 4)
     torch.testing.assert_close(outs[0], torch.stack([m.coefficientMatrix for m in ms]), rtol=1e-3, atol=1e-4)
 
 
-@pytest.mark.parametrize("what,world", [("rf", 2), ("rf", 3), ("rf_allreduce", 2)])
+@pytest.mark.parametrize("what,world", [("rf", 2), ("rf", 3), ("rf", 4), ("rf_allreduce", 2)])
 def test_dp_forest_equals_single(what, world):
     """Owner-computes (reduce-scatter by node + all-gather of winners; world 3 leaves
     uneven node slices) and all-reduce histogram reductions both equal one process."""

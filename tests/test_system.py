@@ -16,7 +16,8 @@ def test_main_reference_run_cpu(tmp_path, wisdm_csv):
     import main
 
     cfg = main.config_from_args(["--data", wisdm_csv, "--out-dir", str(tmp_path), "--device", "cpu",
-                                 "--classifiers", "lr,dt,rf,lrcv", "--save-models", str(tmp_path / "models")])
+                                 "--classifiers", "lr,dt,rf,lrcv", "--save-models", str(tmp_path / "models"),
+                                 "--report"])
     s = main.run(cfg)
     m = s["models"]
     assert m["lr"]["accuracy"] >= 0.61 and m["dt"]["accuracy"] >= 0.72
@@ -39,6 +40,17 @@ def test_main_reference_run_cpu(tmp_path, wisdm_csv):
     ph = rec["phases_s"]
     assert {"load_csv", "feature_pipeline", "random_split", "fit:lr", "predict:lr"} <= set(ph)
     assert abs(ph["fit:lr"] - rec["models"]["lr"]["train_s"]) < 2e-3
+    # curated results (the reference's Results.xls / Graph.pdf / docs page, generated)
+    rep = tmp_path / "report"
+    with open(rep / "Results.csv") as f:
+        res = list(csv.DictReader(f))
+    assert [r["Classifier"] for r in res] == ["Logistic Regression", "Decision Tree", "Random Forest",
+                                              "Logistic Regression (5-fold CV)"]
+    assert int(res[0]["Correct"]) + int(res[0]["Wrong"]) == rec["n_test"]
+    for png in ("prediction.png", "prediction_ratio.png", "accuracy.png", "lr_vs_lrcv.png", "training_time.png"):
+        assert (rep / png).read_bytes()[:4] == b"\x89PNG"
+    page = (rep / "index.html").read_text()
+    assert "Results" in page and "data:image/png;base64," in page and "CLASSIFICATION AND EVALUATION" in page
 
 
 def test_persist_roundtrip(tmp_path, wisdm_csv):
