@@ -45,8 +45,10 @@ def _pad(x: int, m: int) -> int:
 
 
 def n_splits_for(batch: int) -> int:
-    """Batch slices of the split-K weight-gradient GEMMs (>= 1024-row slices, <= 64 slabs)."""
-    return max(1, min(64, batch // 1024))
+    """Batch slices of the split-K weight-gradient GEMMs (>= 1024-row slices, <= 64 slabs;
+    ``HAR_MLP_SPLITS`` overrides the slab cap for tuning)."""
+    cap = int(os.environ.get("HAR_MLP_SPLITS", "64"))
+    return max(1, min(cap, batch // max(1, 65536 // cap)))
 
 
 # Tile choices measured on MI355X with tools/gemm_bench.py (profiles/gemm_tile_sweep.md):
