@@ -300,25 +300,27 @@ class MLPEngine:
 
     def _first_level(self, lo: int, hi: int, tick: bool):
         """Split-K slabs (and, after a fused step, the fused kernel's dWout/dbout workgroup
-        slabs) -> n_groups partials over [lo, hi); optionally ticks the Adam step counter."""
+        slabs) -> n_groups partials over [lo, hi) in ONE launch (one grid.z segment per
+        source); optionally ticks the Adam step counter."""
         mod, st, total = _native.kernels(), _native.stream_ptr(), self.layout.total
         tk = self.step_count.data_ptr() if tick else 0
         woff = self.layout.by_name["Wout"].offset
+        pbase = self.partials.data_ptr()
+        segs = []  # (slabs ptr, S, n, lds, dst ptr, ldd)
         if not self.last_fused or hi <= woff:
-            mod.reduce_slabs_grouped(self.slabs.data_ptr() + 4 * lo, self.active_splits, hi - lo,
-                                     self.partials.data_ptr() + 4 * lo, self.n_groups, st, tk, lds=total, ldd=total)
-            return
-        if lo < woff:
-            mod.reduce_slabs_grouped(self.slabs.data_ptr() + 4 * lo, self.active_splits, woff - lo,
-                                     self.partials.data_ptr() + 4 * lo, self.n_groups, st, tk, lds=total, ldd=total)
-            tk = 0
-        H = self.dims[-1]
-        w = self.fslab.shape[1]
-        mod.reduce_slabs_grouped(self.fslab.data_ptr(), self.fused_nwg, 16 * H, self.partials.data_ptr() + 4 * woff,
-                                 self.n_groups, st, tk, lds=w, ldd=total)
-        mod.reduce_slabs_grouped(self.fslab.data_ptr() + 4 * 16 * H, self.fused_nwg, 16,
-                                 self.partials.data_ptr() + 4 * self.layout.by_name["bout"].offset, self.n_groups, st,
-                                 0, lds=w, ldd=total)
+            segs.append((self.slabs.data_ptr() + 4 * lo, self.active_splits, hi - lo, total, pbase + 4 * lo, total))
+        else:
+            if lo < woff:
+                segs.append((self.slabs.data_ptr() + 4 * lo, self.active_splits, woff - lo, total, pbase + 4 * lo,
+                             total))
+            H = self.dims[-1]
+            w = self.fslab.shape[1]
+            segs.append((self.fslab.data_ptr(), self.fused_nwg, 16 * H, w, pbase + 4 * woff, total))
+            segs.append((self.fslab.data_ptr() + 4 * 16 * H, self.fused_nwg, 16, w,
+                         pbase + 4 * self.layout.by_name["bout"].offset, total))
+        cols = list(zip(*segs))
+        mod.reduce_slabs_multi(list(cols[0]), list(cols[1]), list(cols[2]), list(cols[3]), list(cols[4]),
+                               list(cols[5]), self.n_groups, tk, st)
 
     def _reduce_to_partials(self):
         # the first reduction level also ticks the Adam step counter (one launch fewer per step)

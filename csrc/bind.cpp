@@ -181,6 +181,20 @@ PYBIND11_MODULE(_har_native, m) {
           "window_features");
   });
 
+  m.def("reduce_slabs_multi", [](std::vector<u> slabs, std::vector<int> nsl, std::vector<int64_t> n,
+                                 std::vector<int64_t> lds, std::vector<u> dst, std::vector<int64_t> ldd, int G,
+                                 u tick, u stream) {
+    const int k = (int)slabs.size();
+    if ((int)nsl.size() != k || (int)n.size() != k || (int)lds.size() != k || (int)dst.size() != k ||
+        (int)ldd.size() != k)
+      throw std::runtime_error("reduce_slabs_multi: segment lists differ in length");
+    std::vector<const float*> sp(k);
+    std::vector<float*> dp(k);
+    for (int i = 0; i < k; ++i) { sp[i] = P<const float>(slabs[i]); dp[i] = P<float>(dst[i]); }
+    check(har_reduce_slabs_multi(k, sp.data(), nsl.data(), n.data(), lds.data(), dp.data(), ldd.data(), G,
+                                 P<int32_t>(tick), S(stream)),
+          "reduce_slabs_multi");
+  });
   m.def("head_fused_blocks", &har_head_fused_blocks);
   m.def("mlp_fwd_head_grid", &har_mlp_fwd_head_grid);
   m.def("mlp_fwd_head", [](u X, int K0, u W0, u b0, u W1, u b1, int H, u Wo, u bo, u labels, int B, int C,

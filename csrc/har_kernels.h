@@ -71,6 +71,9 @@ int har_mlp_fwd_infer(const uint16_t* X, int K0, const uint16_t* W0, const float
 
 // dst[g*n + i] = sum of slabs[s*n + i] over the g-th group of ceil(S/G) slabs (deterministic).
 // A non-null tick is incremented once by the first workgroup (the optimizer step counter).
+// Up to 4 independent grouped slab reductions in one launch (per-segment slabs / S / n / lds / dst / ldd).
+int har_reduce_slabs_multi(int nseg, const float* const* slabs, const int* S, const int64_t* n, const int64_t* lds,
+                           float* const* dst, const int64_t* ldd, int G, int32_t* tick, hipStream_t s);
 int har_reduce_slabs_grouped(const float* slabs, int S, int64_t n, int64_t lds, float* dst, int G, int64_t ldd,
                              int32_t* tick, hipStream_t s);
 

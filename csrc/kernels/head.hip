@@ -179,7 +179,66 @@ __global__ __launch_bounds__(256) void reduce_slabs_grouped_kernel(const float* 
   }
 }
 
+// Several independent grouped reductions in ONE launch (blockIdx.z = segment): the per-step
+// first reduction level of the MLP gradient (split-K slabs of W0..b1 + the fused kernel's
+// per-workgroup dWout / dbout slabs) costs one launch instead of three.
+struct ReduceSegs {
+  const float* slabs[4];
+  float* dst[4];
+  int64_t n[4], lds[4], ldd[4];
+  int S[4];
+};
+
+__global__ __launch_bounds__(256) void reduce_slabs_multi_kernel(ReduceSegs sg, int G, int32_t* __restrict__ tick) {
+  const int z = blockIdx.z, g = blockIdx.y;
+  if (tick && blockIdx.x == 0 && g == 0 && z == 0 && threadIdx.x == 0) *tick += 1;
+  const float* __restrict__ slabs = sg.slabs[z];
+  const int S = sg.S[z];
+  const int64_t lds = sg.lds[z];
+  const int per = (S + G - 1) / G;
+  const int s0 = g * per, s1 = min(S, s0 + per);
+  const int64_t n4 = sg.n[z] / 4;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    int s = s0;
+    for (; s + 4 <= s1; s += 4) {
+      const float4 x0 = reinterpret_cast<const float4*>(slabs + (size_t)s * lds)[i];
+      const float4 x1 = reinterpret_cast<const float4*>(slabs + (size_t)(s + 1) * lds)[i];
+      const float4 x2 = reinterpret_cast<const float4*>(slabs + (size_t)(s + 2) * lds)[i];
+      const float4 x3 = reinterpret_cast<const float4*>(slabs + (size_t)(s + 3) * lds)[i];
+      acc.x += (x0.x + x1.x) + (x2.x + x3.x);
+      acc.y += (x0.y + x1.y) + (x2.y + x3.y);
+      acc.z += (x0.z + x1.z) + (x2.z + x3.z);
+      acc.w += (x0.w + x1.w) + (x2.w + x3.w);
+    }
+    for (; s < s1; ++s) {
+      const float4 x = reinterpret_cast<const float4*>(slabs + (size_t)s * lds)[i];
+      acc.x += x.x; acc.y += x.y; acc.z += x.z; acc.w += x.w;
+    }
+    reinterpret_cast<float4*>(sg.dst[z] + (size_t)g * sg.ldd[z])[i] = acc;
+  }
+}
+
 }  // namespace
+
+extern "C" int har_reduce_slabs_multi(int nseg, const float* const* slabs, const int* S, const int64_t* n,
+                                      const int64_t* lds, float* const* dst, const int64_t* ldd, int G, int32_t* tick,
+                                      hipStream_t s) {
+  if (nseg <= 0 || nseg > 4 || G <= 0) return -2;
+  ReduceSegs sg{};
+  int64_t n4max = 1;
+  for (int z = 0; z < nseg; ++z) {
+    if (n[z] % 4 || lds[z] % 4 || ldd[z] % 4 || lds[z] < n[z] || (G > 1 && ldd[z] < n[z]) || S[z] <= 0) return -2;
+    if ((reinterpret_cast<uintptr_t>(slabs[z]) | reinterpret_cast<uintptr_t>(dst[z])) & 15) return -3;
+    sg.slabs[z] = slabs[z]; sg.dst[z] = dst[z]; sg.n[z] = n[z]; sg.lds[z] = lds[z]; sg.ldd[z] = ldd[z];
+    sg.S[z] = S[z];
+    n4max = std::max<int64_t>(n4max, n[z] / 4);
+  }
+  const int bx = (int)std::max<int64_t>(1, std::min<int64_t>(1024, (n4max + 255) / 256));
+  reduce_slabs_multi_kernel<<<dim3(bx, G, nseg), 256, 0, s>>>(sg, G, tick);
+  HAR_CHECK_LAUNCH();
+  return 0;
+}
 
 extern "C" int har_head_fused_blocks(int B) { return (B + ROWS - 1) / ROWS; }
 
