@@ -476,9 +476,27 @@ class MLPEngine:
                                         L.num_classes, out.data_ptr(), pred.data_ptr(), _native.stream_ptr())
         return out, pred
 
+    def infer_fused_f32(self, X: torch.Tensor):
+        """Serving from raw fp32 features [B, F] (row stride >= F): ONE kernel, the bf16 cast
+        and zero padding happen in its loads.  Returns (logits [B, C] fp32, argmax [B] int32)."""
+        L = self.layout
+        B, F = X.shape
+        if not (self.fused_ok and B % 16 == 0 and X.dtype == torch.float32 and X.stride(1) == 1 and F <= L.in_pad):
+            raise ValueError("infer_fused_f32: unsupported shape")
+        out = torch.empty(B, L.num_classes, dtype=torch.float32, device=X.device)
+        pred = torch.empty(B, dtype=torch.int32, device=X.device)
+        _native.kernels().mlp_fwd_infer_f32(X.data_ptr(), X.stride(0), F, L.in_pad, self._w(self.Pb, "W0").data_ptr(),
+                                            self._w(self.P, "b0").data_ptr(), self._w(self.Pb, "W1").data_ptr(),
+                                            self._w(self.P, "b1").data_ptr(), self.dims[-1],
+                                            self._w(self.Pb, "Wout").data_ptr(), self._w(self.P, "bout").data_ptr(),
+                                            B, L.num_classes, out.data_ptr(), pred.data_ptr(), _native.stream_ptr())
+        return out, pred
+
     def logits(self, X: torch.Tensor) -> torch.Tensor:
         L = self.layout
         if self.native and X.is_cuda:
+            if self.fused_ok and X.shape[0] % 16 == 0 and X.dtype == torch.float32 and X.stride(1) == 1:
+                return self.infer_fused_f32(X)[0]
             Xb = pad_input_bf16(X, L.in_pad)
             if self.fused_ok and X.shape[0] % 16 == 0:
                 return self.infer_fused(Xb)[0]

@@ -205,6 +205,13 @@ PYBIND11_MODULE(_har_native, m) {
                            P<float>(block_loss), P<int32_t>(block_correct), S(stream)),
           "mlp_fwd_head");
   });
+  m.def("mlp_fwd_infer_f32", [](u X, int ldx, int F, int K0, u W0, u b0, u W1, u b1, int H, u Wo, u bo, int B,
+                                int C, u logits, u pred, u stream) {
+    check(har_mlp_fwd_infer_f32(P<const float>(X), ldx, F, K0, P<const uint16_t>(W0), P<const float>(b0),
+                                P<const uint16_t>(W1), P<const float>(b1), H, P<const uint16_t>(Wo), P<const float>(bo),
+                                B, C, P<float>(logits), P<int32_t>(pred), S(stream)),
+          "mlp_fwd_infer_f32");
+  });
   m.def("mlp_fwd_infer", [](u X, int K0, u W0, u b0, u W1, u b1, int H, u Wo, u bo, int B, int C, u logits, u pred,
                             u stream) {
     check(har_mlp_fwd_infer(P<const uint16_t>(X), K0, P<const uint16_t>(W0), P<const float>(b0),

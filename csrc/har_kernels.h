@@ -65,6 +65,9 @@ int har_mlp_fwd_head(const uint16_t* X, int K0, const uint16_t* W0, const float*
                      int32_t* block_correct, hipStream_t s);
 int har_mlp_fwd_head_grid(int B);
 // Serving variant of the same kernel: logits [B][C] fp32 + argmax class [B] int32, nothing else.
+int har_mlp_fwd_infer_f32(const float* X, int ldx, int F, int K0, const uint16_t* W0, const float* b0,
+                          const uint16_t* W1, const float* b1, int H, const uint16_t* Wo, const float* bo, int B, int C,
+                          float* logits, int32_t* pred, hipStream_t s);
 int har_mlp_fwd_infer(const uint16_t* X, int K0, const uint16_t* W0, const float* b0, const uint16_t* W1,
                       const float* b1, int H, const uint16_t* Wo, const float* bo, int B, int C, float* logits,
                       int32_t* pred, hipStream_t s);

@@ -71,16 +71,33 @@ template <> __device__ __forceinline__ void hold_all<16>(u32x4_t (&b)[16]) {
                "v"(b[8]), "v"(b[9]), "v"(b[10]), "v"(b[11]), "v"(b[12]), "v"(b[13]), "v"(b[14]), "v"(b[15]));
 }
 
+// X fragment of one lane: 8 consecutive k of row `row`.  XF = 0: padded bf16 [B][K0];
+// XF = 1 (serving): raw fp32 features [B][ldx] with F valid columns, converted in registers —
+// no separate cast/pad pass over the input.
+template <int K0, int XF>
+__device__ __forceinline__ bf16x8_t load_x(const bf16_t* __restrict__ X, int row, int kc, int g, int F, int ldx) {
+  if constexpr (XF == 0) {
+    return *reinterpret_cast<const bf16x8_t*>(X + (size_t)row * K0 + kc * 32 + g * 8);
+  } else {
+    const float* xf = reinterpret_cast<const float*>(X) + (size_t)row * ldx;
+    const int k0 = kc * 32 + g * 8;
+    bf16x8_t r;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) r[j] = (__bf16)(k0 + j < F ? xf[k0 + j] : 0.f);
+    return r;
+  }
+}
+
 // INFER = true: the serving variant — stages 1-3 only; writes the logits [B][C] (fp32) and the
 // argmax class per row, no label / loss / gradient work and no h1 store.
-template <int H, int K0, bool INFER>
+template <int H, int K0, bool INFER, int XF = 0>
 __global__ __launch_bounds__(256) void mlp_fwd_head_kernel(
     const bf16_t* __restrict__ X, const bf16_t* __restrict__ W0, const float* __restrict__ b0,
     const bf16_t* __restrict__ W1, const float* __restrict__ b1, const bf16_t* __restrict__ Wo,
     const float* __restrict__ bo, const int32_t* __restrict__ labels, int B, int C, float scale,
     bf16_t* __restrict__ h1out, bf16_t* __restrict__ dact, float* __restrict__ slab,
     float* __restrict__ block_loss, int32_t* __restrict__ block_correct, float* __restrict__ logits_out,
-    int32_t* __restrict__ pred_out) {
+    int32_t* __restrict__ pred_out, int F, int ldx) {
   constexpr int NT = H / 16, KC = H / 32, K0C = K0 / 32;
   extern __shared__ __attribute__((aligned(16))) bf16_t lds[];
   constexpr int P = Pitch<H>::v;
@@ -162,7 +179,7 @@ __global__ __launch_bounds__(256) void mlp_fwd_head_kernel(
   if (T < ntiles) {
 #pragma unroll
     for (int kc = 0; kc < K0C; ++kc)
-      xb[kc] = *reinterpret_cast<const bf16x8_t*>(X + (size_t)(T * 16 + c16) * K0 + kc * 32 + g * 8);
+      xb[kc] = load_x<K0, XF>(X, T * 16 + c16, kc, g, F, ldx);
     if (!INFER) y = labels[T * 16 + c16];
   }
   // drain the first prefetch here: otherwise the loop-header wait the compiler derives from
@@ -190,7 +207,7 @@ __global__ __launch_bounds__(256) void mlp_fwd_head_kernel(
     if (Tn < ntiles) {
 #pragma unroll
       for (int kc = 0; kc < K0C; ++kc)
-        xb[kc] = *reinterpret_cast<const bf16x8_t*>(X + (size_t)(Tn * 16 + c16) * K0 + kc * 32 + g * 8);
+        xb[kc] = load_x<K0, XF>(X, Tn * 16 + c16, kc, g, F, ldx);
       if (!INFER) y = labels[Tn * 16 + c16];
     }
     __builtin_amdgcn_sched_barrier(0);
@@ -341,14 +358,15 @@ __global__ __launch_bounds__(256) void mlp_fwd_head_kernel(
   }
 }
 
-template <int H, int K0, bool INFER = false>
+template <int H, int K0, bool INFER = false, int XF = 0>
 int launch(const bf16_t* X, const bf16_t* W0, const float* b0, const bf16_t* W1, const float* b1,
            const bf16_t* Wo, const float* bo, const int32_t* labels, int B, int C, float scale, bf16_t* h1,
            bf16_t* dact, float* slab, float* block_loss, int32_t* block_correct, int nwg, hipStream_t s,
-           float* logits = nullptr, int32_t* pred = nullptr) {
+           float* logits = nullptr, int32_t* pred = nullptr, int F = K0, int ldx = K0) {
   const size_t lds = ((size_t)(H + NCLS) * Pitch<H>::v + NCLS * H + 4 * SCR) * sizeof(bf16_t) + 2 * H * sizeof(float);
-  mlp_fwd_head_kernel<H, K0, INFER><<<nwg, 256, lds, s>>>(X, W0, b0, W1, b1, Wo, bo, labels, B, C, scale, h1, dact,
-                                                          slab, block_loss, block_correct, logits, pred);
+  mlp_fwd_head_kernel<H, K0, INFER, XF><<<nwg, 256, lds, s>>>(X, W0, b0, W1, b1, Wo, bo, labels, B, C, scale, h1,
+                                                              dact, slab, block_loss, block_correct, logits, pred, F,
+                                                              ldx);
   HAR_CHECK_LAUNCH();
   return 0;
 }
@@ -387,5 +405,23 @@ extern "C" int har_mlp_fwd_infer(const uint16_t* X, int K0, const uint16_t* W0, 
   if (H == 256 && K0 == 32) return launch<256, 32, true>(x, W0, b0, W1, b1, Wo, bo, nullptr, B, C, 1.f, nullptr, nullptr, nullptr, nullptr, nullptr, nwg, s, logits, pred);
   if (H == 128 && K0 == 64) return launch<128, 64, true>(x, W0, b0, W1, b1, Wo, bo, nullptr, B, C, 1.f, nullptr, nullptr, nullptr, nullptr, nullptr, nwg, s, logits, pred);
   if (H == 128 && K0 == 32) return launch<128, 32, true>(x, W0, b0, W1, b1, Wo, bo, nullptr, B, C, 1.f, nullptr, nullptr, nullptr, nullptr, nullptr, nwg, s, logits, pred);
+  return -4;
+}
+
+// Serving from raw fp32 features X [B][ldx] (F <= K0 valid columns): the bf16 cast / zero pad
+// happens in the kernel's X loads.
+extern "C" int har_mlp_fwd_infer_f32(const float* X, int ldx, int F, int K0, const uint16_t* W0, const float* b0,
+                                     const uint16_t* W1, const float* b1, int H, const uint16_t* Wo, const float* bo,
+                                     int B, int C, float* logits, int32_t* pred, hipStream_t s) {
+  if (B <= 0 || B % 16 || C < 1 || C > NCLS || F < 1 || F > K0 || ldx < F) return -2;
+  if (((uintptr_t)W0 | (uintptr_t)W1 | (uintptr_t)Wo | (uintptr_t)b0 | (uintptr_t)b1) & 15) return -3;
+  const int nwg = har_mlp_fwd_head_grid(B);
+  const bf16_t* x = reinterpret_cast<const bf16_t*>(X);
+#define HAR_INFER_F32(HH, KK)                                                                                     \
+  if (H == HH && K0 == KK)                                                                                        \
+    return launch<HH, KK, true, 1>(x, W0, b0, W1, b1, Wo, bo, nullptr, B, C, 1.f, nullptr, nullptr, nullptr,       \
+                                   nullptr, nullptr, nwg, s, logits, pred, F, ldx);
+  HAR_INFER_F32(256, 64) HAR_INFER_F32(256, 32) HAR_INFER_F32(128, 64) HAR_INFER_F32(128, 32)
+#undef HAR_INFER_F32
   return -4;
 }

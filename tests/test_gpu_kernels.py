@@ -329,4 +329,7 @@ def test_mlp_fused_infer_matches_fp32(cuda, H, F):
     assert torch.equal(pred.long(), torch.argmax(logits, 1))  # in-kernel argmax of its own logits
     agree = float((pred.long() == torch.argmax(ref, 1)).float().mean())
     assert agree > 0.97
-    torch.testing.assert_close(eng.logits(X), logits)  # logits() takes the fused path
+    lf, pf = eng.infer_fused_f32(X)  # fp32 features straight into the kernel: same bf16 rounding
+    torch.testing.assert_close(lf, logits)
+    assert torch.equal(pf, pred)
+    torch.testing.assert_close(eng.logits(X), logits)  # logits() takes the fused fp32 path
