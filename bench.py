@@ -272,23 +272,38 @@ def bench_stream(args, ctx):
     nb = nw_local // B
     y32 = labels.to(torch.int32)
     global_batch = B * world
+    # feature standardization (Spark StandardScaler analogue): moments of a 16k-window sample of
+    # every rank's shard, summed across ranks (untimed setup; HIP column-stats kernel on the GPU)
+    from har.ops.stats import column_stats
+
+    ns = min(nw_local, 16384)
+    st = column_stats(torch.nan_to_num(window_features(stream[:ns * W], W, W, spec.hz), nan=-1.0))[:3].contiguous()
+    if world > 1:
+        import torch.distributed as tdist
+        tdist.all_reduce(st, group=ctx.group)
+    mean = (st[1] / st[0]).float()
+    var = (st[2] / st[0]).float() - mean * mean
+    inv_std = torch.where(var > 1e-12, var.clamp_min(1e-12).rsqrt(), torch.ones_like(var))
+
+    def featurize(s):
+        X = torch.nan_to_num(window_features(s, W, W, spec.hz), nan=-1.0)
+        return (X - mean) * inv_std
 
     def step(i):
         j = i % nb
-        X = window_features(stream[j * B * W:(j + 1) * B * W], W, W, spec.hz)
-        feat.copy_(torch.nan_to_num(X, nan=-1.0))
+        feat.copy_(featurize(stream[j * B * W:(j + 1) * B * W]))
         Xb = pad_input_bf16(feat, eng.layout.in_pad)
         eng.train_step(Xb, y32[j * B:(j + 1) * B], global_batch)
 
     elapsed = timed(ctx, step, args.steps, args.warmup, dev)
-    Xt, yt = (lambda s_y: (torch.nan_to_num(window_features(s_y[0], W, W, spec.hz), nan=-1.0), s_y[1]))(
-        generate_stream(8192, spec, dev, first_window=10 ** 9))
+    st_, yt = generate_stream(8192, spec, dev, first_window=10 ** 9)
+    Xt = featurize(st_)
     acc = float((torch.argmax(eng.logits(Xt), 1) == yt).float().mean())
     return {"value": global_batch * args.steps / elapsed, "ms_per_step": elapsed * 1e3 / args.steps,
             "vs_baseline": global_batch * args.steps / elapsed / BASELINE["lr"],
             "samples_per_s": global_batch * W * args.steps / elapsed,
             "data": f"synthetic 3-axis 20 Hz stream, {samples_local * world / 1e9:.2f}B samples resident "
-                    f"({samples_local / 1e6:.0f}M per GPU), featurized on device each step",
+                    f"({samples_local / 1e6:.0f}M per GPU), featurized + standardized on device each step",
             "config": {"model": f"raw stream -> window features ({F}) -> MLP bf16 "
                                 f"({F}-{args.hidden}-{args.hidden}-{N_CLASSES})",
                        "global_batch": global_batch, "seq_len": W, "parallelism": f"dp{world}"},
