@@ -581,7 +581,8 @@ class RandomForestClassifier(_TreeEstimatorBase):
         return self.fit_tensors(X[lo:hi], y[lo:hi], K, row_offset=lo, thresholds=thr, owner=dp_owner())
 
     def fit_tensors(self, X, y, K, allreduce=None, row_offset: int = 0, thresholds=None,
-                    tree_wave: int = 0, checkpoint_dir: Optional[str] = None, rank: int = 0, owner=None):
+                    tree_wave: int = 0, checkpoint_dir: Optional[str] = None, rank: int = 0, owner=None,
+                    tree_offset: int = 0, num_trees: Optional[int] = None):
         """Grow the forest (all trees in lock step, or in waves of ``tree_wave`` trees —
         each wave checkpointed under ``checkpoint_dir`` and skipped on resume).  Trees
         are keyed by their global id, so a waved forest equals the one-shot forest."""
@@ -592,7 +593,10 @@ class RandomForestClassifier(_TreeEstimatorBase):
             strategy = "all" if self.numTrees == 1 else "sqrt"
         if thresholds is None:
             thresholds = T.find_thresholds(X.detach().float().cpu().numpy(), self.maxBins, seed=self.seed)
-        wave = tree_wave if tree_wave and tree_wave < self.numTrees else self.numTrees
+        # tree-parallel mode grows trees [tree_offset, tree_offset + num_trees) of the forest: global tree
+        # ids key the bootstrap and feature-subset streams, so the slices concatenate into the forest
+        total = self.numTrees if num_trees is None else int(num_trees)
+        wave = tree_wave if tree_wave and tree_wave < total else total
         ckpt = None
         parts: List[ForestArrays] = []
         if checkpoint_dir:
@@ -605,15 +609,15 @@ class RandomForestClassifier(_TreeEstimatorBase):
         from ..utils.checkpoint import maybe_inject_fault
 
         done = sum(p.feature.shape[0] for p in parts)
-        while done < self.numTrees:
+        while done < total:
             maybe_inject_fault(done, rank)
-            nt = min(wave, self.numTrees - done)
+            nt = min(wave, total - done)
             b = ForestBuilder(K, nt, self.maxDepth, self.maxBins, self.minInstancesPerNode, self.minInfoGain,
                               self.impurity, strategy, bootstrap=self.numTrees > 1, seed=self.seed,
-                              allreduce=allreduce, tree_offset=done, owner=owner)
+                              allreduce=allreduce, tree_offset=tree_offset + done, owner=owner)
             parts.append(b.fit(X, y, row_offset=row_offset, thresholds=thresholds))
             done += nt
-            if ckpt is not None and done < self.numTrees:
+            if ckpt is not None and done < total:
                 merged = _concat_arrays(parts)
                 parts = [merged]
                 ckpt.save(done, _arrays_state(merged), {"trees": done})

@@ -15,6 +15,8 @@ combines are RCCL collectives over xGMI:
   winners (3 + 2K floats per node) gives everybody the level's splits.  Half the
   histogram bytes on the wire and no redundant split search (Spark:
   ``reduceByKey(node)`` + ``collectAsMap``, SURVEY.md M9);
+* RandomForest, tree-parallel (``fit_forest_tree_parallel``): every rank grows a slice of the
+  trees over all rows; one all-gather of the node arrays at the end;
 * MLP: fp32 gradient buckets (>= 64 KB, contiguous layer ranges of the flat buffer) all-reduced
   asynchronously while backward continues (``MLPEngine.train_step_overlapped``).
 
@@ -125,6 +127,45 @@ def fit_forest_dp(estimator, X_shard, y_shard, num_classes: int, row_offset: int
                                      owner=NodeOwner(ctx))
     return estimator.fit_tensors(X_shard, y_shard, num_classes, allreduce=allreduce_sum(ctx), row_offset=row_offset,
                                  thresholds=thr)
+
+
+def fit_forest_tree_parallel(estimator, X, y, num_classes: int, ctx: DistContext, thresholds=None):
+    """Tree parallelism: every rank holds ALL rows and grows its contiguous
+    slice of the forest's trees — keyed by global tree id, so bootstraps and feature subsets
+    are those of the single-process forest — with zero communication until ONE all-gather of
+    the node arrays at the end.  The result equals the single-process forest.  Pays when the
+    data fits every GPU (288 GB each) and trees are many; row-sharded DP (``fit_forest_dp``)
+    pays when rows are many."""
+    from ..models.tree import ForestArrays, RandomForestClassificationModel
+
+    T_, P, r = estimator.numTrees, ctx.world_size, ctx.rank
+    lo, hi = (T_ * r) // P, (T_ * (r + 1)) // P
+    if thresholds is None:
+        thresholds = T.find_thresholds(X.detach().float().cpu().numpy(), estimator.maxBins, seed=estimator.seed)
+    part = estimator.fit_tensors(X, y, num_classes, thresholds=thresholds, tree_offset=lo, num_trees=hi - lo)
+    if not ctx.is_distributed:
+        return part
+    a = part.arrs
+    S = -(-T_ // P)  # trees per rank, padded
+
+    def gather(t: torch.Tensor) -> torch.Tensor:
+        buf = torch.zeros((S,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+        buf[: t.shape[0]] = t
+        src = buf if (buf.is_cuda or ctx.backend != "nccl") else buf.to(ctx.device)
+        out = torch.empty((P * S,) + tuple(t.shape[1:]), dtype=t.dtype, device=src.device)
+        dist.all_gather_into_tensor(out, src, group=ctx.group)
+        keep = torch.cat([torch.arange(q * S, q * S + (T_ * (q + 1)) // P - (T_ * q) // P) for q in range(P)])
+        return out[keep.to(out.device)].to(t.device)
+
+    nn = torch.as_tensor(a.n_nodes, dtype=torch.int64, device=a.feature.device)
+    md = torch.tensor([a.max_depth], device=a.feature.device)
+    mds = torch.empty(P, dtype=md.dtype, device=md.device)
+    dist.all_gather_into_tensor(mds, md if (md.is_cuda or ctx.backend != "nccl") else md.to(ctx.device),
+                                group=ctx.group)
+    full = ForestArrays(gather(a.feature), gather(a.threshold), gather(a.left), gather(a.right), gather(a.stats),
+                        gather(nn.view(-1, 1)).view(-1).cpu().numpy(), int(mds.max()),
+                        gather(a.gain) if a.gain is not None else None)
+    return RandomForestClassificationModel(full, X.shape[1], num_classes, uid=estimator.uid, device=X.device)
 
 
 def fit_mlp_dp(estimator, X_shard, y_shard, ctx: DistContext, num_classes: Optional[int] = None):

@@ -52,6 +52,14 @@ def _worker(rank, world, port, out_dir, what):
         m = dp.fit_forest_dp(RandomForestClassifier(numTrees=8, maxDepth=4, seed=5), Xs, ys, 4, off, ctx,
                              reduction="owner" if what == "rf" else "allreduce")
         res = m.predict_raw(X)
+    elif what == "rf_tree":
+        from har.models.tree import RandomForestClassifier
+        from har.ops import tree as T
+
+        thr = T.find_thresholds(X.numpy(), 32)
+        m = dp.fit_forest_tree_parallel(RandomForestClassifier(numTrees=7, maxDepth=4, seed=5), X, y, 4, ctx,
+                                        thresholds=thr)
+        res = m.predict_raw(X)
     elif what == "stream":
         from har.features.window import WindowFeaturizer
         from har.parallel.stream import sharded_window_features
@@ -160,3 +168,19 @@ def test_main_data_parallel_matches_single(tmp_path, wisdm_csv):
         assert abs(a["accuracy"] - b["accuracy"]) <= tol, (name, a["accuracy"], b["accuracy"])
     rows = (tmp_path / "dp" / "additional_param.csv").read_text().splitlines()
     assert len(rows) == 5  # header + 4 models, written once (rank 0)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_tree_parallel_forest_equals_single(world):
+    """Tree parallelism: ranks grow disjoint tree-id slices (7 trees over 2 or 3 ranks: uneven)
+    over all rows; the all-gathered forest is the single-process forest."""
+    from har.models.tree import RandomForestClassifier
+    from har.ops import tree as T
+
+    outs = _run("rf_tree", world)
+    for o in outs[1:]:
+        torch.testing.assert_close(outs[0], o)
+    X, y = _data()
+    thr = T.find_thresholds(X.numpy(), 32)
+    single = RandomForestClassifier(numTrees=7, maxDepth=4, seed=5).fit_tensors(X, y, 4, thresholds=thr)
+    torch.testing.assert_close(outs[0], single.predict_raw(X))
