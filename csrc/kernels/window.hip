@@ -1,11 +1,14 @@
 // Windowed feature extraction over raw IMU streams.
 //
 // Input: stream [S][A] fp32 (sample-major, axes interleaved), windows of W
-// samples every `stride` samples.  One wave64 per window: the window's W*A
-// contiguous floats are staged into LDS with coalesced loads, then every lane
-// owns samples lane, lane+64, ... and the statistics are wave-reduced in two
-// passes (pass 1: sum / min / max / sum of squares; pass 2: deviations, 10-bin
-// distribution, cross-axis covariance, resultant, peaks).
+// samples every `stride` samples.  A group of LPW lanes per window — 16 (four
+// windows per wave) when the block's window images fit 64 KB of LDS, else the
+// whole wave: the windows' W*A floats are staged into LDS (one contiguous 16-byte
+// load stream per wave for non-overlapping windows), every lane owns samples
+// sub, sub+LPW, ... and the statistics are group-reduced with xor shuffles in
+// two passes (pass 1: sum / min / max / sum of squares; pass 2: deviations,
+// 10-bin distribution — two 16-bit counters per register — cross-axis
+// covariance, resultant, peaks).
 //
 // Output row (F = 17*A + 4*(A/3) floats), WISDM-43 first for A = 3:
 //   [bins: A x 10][avg: A][peak ms: A][absdev: A][std: A][resultant: A/3]
@@ -24,21 +27,76 @@ constexpr int MAXA = 9;
 constexpr int NB = 10;
 constexpr int WAVES = 4;
 
+// Reductions over the LPW lanes of one window group (xor offsets < LPW stay inside the group).
+template <int LPW> __device__ __forceinline__ float gsum(float v) {
+#pragma unroll
+  for (int o = LPW / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+template <int LPW> __device__ __forceinline__ int gsumi(int v) {
+#pragma unroll
+  for (int o = LPW / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+template <int LPW> __device__ __forceinline__ float gmin(float v) {
+#pragma unroll
+  for (int o = LPW / 2; o > 0; o >>= 1) v = fminf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+template <int LPW> __device__ __forceinline__ float gmax(float v) {
+#pragma unroll
+  for (int o = LPW / 2; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+template <int LPW> __device__ __forceinline__ int gmini(int v) {
+#pragma unroll
+  for (int o = LPW / 2; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o, 64));
+  return v;
+}
+template <int LPW> __device__ __forceinline__ int gmaxi(int v) {
+#pragma unroll
+  for (int o = LPW / 2; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
 // A is a template parameter so every per-axis register array is statically indexed
 // (runtime-indexed register arrays spill to scratch — guide §5.4 rule 20).
-template <int A>
+// LPW lanes per window: 16 (four windows per wave — every shuffle-reduction instruction
+// serves four windows, and a 200-sample window keeps 12-13 samples per lane busy) or 64
+// (one window per wave, for windows whose LDS image is large).
+template <int A, int LPW>
 __global__ __launch_bounds__(WAVES * 64) void window_features_kernel(const float* __restrict__ stream,
                                                                      int64_t n_samples, int W, int stride,
                                                                      int64_t n_windows, float ms_per_sample,
                                                                      float* __restrict__ out, int ld_out) {
-  extern __shared__ float lds[];  // [WAVES][W*A]
+  constexpr int G = 64 / LPW;  // windows per wave
+  extern __shared__ __attribute__((aligned(16))) float lds[];  // [WAVES * G][W*A]
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int64_t win = (int64_t)blockIdx.x * WAVES + wave;
-  if (win >= n_windows) return;  // wave-uniform; no block barrier below
-  float* buf = lds + (size_t)wave * W * A;
-  const float* src = stream + win * (int64_t)stride * A;
+  const int sub = lane % LPW, grp = lane / LPW;
+  const int64_t win0 = ((int64_t)blockIdx.x * WAVES + wave) * G;
+  if (win0 >= n_windows) return;  // wave-uniform; no block barrier below
+  const int64_t win = win0 + grp;
+  const bool valid = win < n_windows;
   const int n = W * A;
-  for (int i = lane; i < n; i += 64) buf[i] = src[i];
+  float* wbuf = lds + (size_t)wave * G * n;
+  float* buf = wbuf + (size_t)grp * n;
+  // ---- stage the wave's windows in LDS ----
+  const int nw = (int)min<int64_t>(G, n_windows - win0);
+  if (stride == W && G > 1) {
+    // non-overlapping windows: the wave's windows are one contiguous run; 16-byte loads when aligned
+    const float* src = stream + win0 * (int64_t)W * A;
+    const int tot = nw * n;
+    if (((reinterpret_cast<uintptr_t>(src) & 15) == 0) && (tot % 4 == 0) && (n % 4 == 0)) {
+      const float4* s4 = reinterpret_cast<const float4*>(src);
+      float4* d4 = reinterpret_cast<float4*>(wbuf);
+      for (int i = lane; i < tot / 4; i += 64) d4[i] = s4[i];
+    } else {
+      for (int i = lane; i < tot; i += 64) wbuf[i] = src[i];
+    }
+  } else if (valid) {
+    const float* src = stream + win * (int64_t)stride * A;
+    for (int i = sub; i < n; i += LPW) buf[i] = src[i];
+  }
   __builtin_amdgcn_s_waitcnt(0);
   __builtin_amdgcn_wave_barrier();
 
@@ -48,21 +106,19 @@ __global__ __launch_bounds__(WAVES * 64) void window_features_kernel(const float
 #pragma unroll
   for (int a = 0; a < A; ++a) {
     float s = 0.f, q = 0.f, lo = INFINITY, hi = -INFINITY;
-    for (int t = lane; t < W; t += 64) {
-      float v = buf[t * A + a];
-      s += v; q += v * v; lo = fminf(lo, v); hi = fmaxf(hi, v);
-    }
-    s = wave_sum(s);
-    q = wave_sum(q);
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      lo = fminf(lo, __shfl_xor(lo, o, 64));
-      hi = fmaxf(hi, __shfl_xor(hi, o, 64));
-    }
+    if (valid)
+      for (int t = sub; t < W; t += LPW) {
+        float v = buf[t * A + a];
+        s += v; q += v * v; lo = fminf(lo, v); hi = fmaxf(hi, v);
+      }
+    s = gsum<LPW>(s);
+    q = gsum<LPW>(q);
+    lo = gmin<LPW>(lo);
+    hi = gmax<LPW>(hi);
     mean[a] = s * invW; en[a] = q * invW; mn[a] = lo; mx[a] = hi;
   }
   constexpr int T3 = A / 3;
-  float* o = out + win * (int64_t)ld_out;
+  float* o = out + (valid ? win : 0) * (int64_t)ld_out;
   const int off_avg = A * NB, off_peak = off_avg + A, off_abs = off_peak + A, off_std = off_abs + A;
   const int off_res = off_std + A, off_min = off_res + T3, off_max = off_min + A, off_en = off_max + A;
   const int off_corr = off_en + A;
@@ -73,48 +129,45 @@ __global__ __launch_bounds__(WAVES * 64) void window_features_kernel(const float
     const float m = mean[a], lo = mn[a], range = mx[a] - mn[a];
     const float thr = m + 0.5f * (mx[a] - m);
     float ad = 0.f, v2 = 0.f;
-    int cnt[NB];
+    int cnt[NB / 2];  // two 16-bit bin counters per register (W < 65536): 5 reductions, not 10
 #pragma unroll
-    for (int b = 0; b < NB; ++b) cnt[b] = 0;
+    for (int b = 0; b < NB / 2; ++b) cnt[b] = 0;
     int first = 0x7fffffff, last = -1, npk = 0;
-    for (int t = lane; t < W; t += 64) {
-      const float v = buf[t * A + a];
-      const float d = v - m;
-      ad += fabsf(d);
-      v2 += d * d;
-      int b = range > 0.f ? (int)((v - lo) / range * NB) : 0;
-      b = b < 0 ? 0 : (b >= NB ? NB - 1 : b);
+    if (valid)
+      for (int t = sub; t < W; t += LPW) {
+        const float v = buf[t * A + a];
+        const float d = v - m;
+        ad += fabsf(d);
+        v2 += d * d;
+        int b = range > 0.f ? (int)((v - lo) / range * NB) : 0;
+        b = b < 0 ? 0 : (b >= NB ? NB - 1 : b);
+        const int inc = (b & 1) ? 0x10000 : 1;
 #pragma unroll
-      for (int k = 0; k < NB; ++k) cnt[k] += (k == b);
-      if (t > 0 && t < W - 1) {
-        const float pv = buf[(t - 1) * A + a], nv = buf[(t + 1) * A + a];
-        if (v > pv && v >= nv && v > thr) {
-          first = min(first, t); last = max(last, t); ++npk;
+        for (int k = 0; k < NB / 2; ++k) cnt[k] += ((b >> 1) == k) ? inc : 0;
+        if (t > 0 && t < W - 1) {
+          const float pv = buf[(t - 1) * A + a], nv = buf[(t + 1) * A + a];
+          if (v > pv && v >= nv && v > thr) {
+            first = min(first, t); last = max(last, t); ++npk;
+          }
         }
       }
-    }
-    ad = wave_sum(ad);
-    v2 = wave_sum(v2);
+    ad = gsum<LPW>(ad);
+    v2 = gsum<LPW>(v2);
 #pragma unroll
-    for (int k = 0; k < NB; ++k) {
-      int c = cnt[k];
-#pragma unroll
-      for (int s = 32; s > 0; s >>= 1) c += __shfl_xor(c, s, 64);
-      cnt[k] = c;
-    }
-#pragma unroll
-    for (int s = 32; s > 0; s >>= 1) {
-      first = min(first, __shfl_xor(first, s, 64));
-      last = max(last, __shfl_xor(last, s, 64));
-      npk += __shfl_xor(npk, s, 64);
-    }
+    for (int k = 0; k < NB / 2; ++k) cnt[k] = gsumi<LPW>(cnt[k]);
+    first = gmini<LPW>(first);
+    last = gmaxi<LPW>(last);
+    npk = gsumi<LPW>(npk);
     var[a] = v2 * invW;
-    // every lane holds the reduced counts; lane k writes bin k (static register indices only)
+    // every lane of the group holds the reduced counts; lane k of the group writes bin k
     float mine = 0.f;
 #pragma unroll
-    for (int k = 0; k < NB; ++k) mine = (lane == k) ? (float)cnt[k] : mine;
-    if (lane < NB) o[a * NB + lane] = mine * invW;
-    if (lane == 0) {
+    for (int k = 0; k < NB; ++k) {
+      const int c = (k & 1) ? (cnt[k >> 1] >> 16) : (cnt[k >> 1] & 0xffff);
+      mine = (sub == k) ? (float)c : mine;
+    }
+    if (valid && sub < NB) o[a * NB + sub] = mine * invW;
+    if (valid && sub == 0) {
       o[off_avg + a] = m;
       o[off_peak + a] = npk >= 2 ? (float)(last - first) / (float)(npk - 1) * ms_per_sample : NAN;
       o[off_abs + a] = ad * invW;
@@ -129,14 +182,15 @@ __global__ __launch_bounds__(WAVES * 64) void window_features_kernel(const float
   for (int g = 0; g < T3; ++g) {
     const int ax = 3 * g;
     float res = 0.f, cxy = 0.f, cxz = 0.f, cyz = 0.f;
-    for (int t = lane; t < W; t += 64) {
-      const float x = buf[t * A + ax], y = buf[t * A + ax + 1], z = buf[t * A + ax + 2];
-      res += sqrtf(x * x + y * y + z * z);
-      const float dx = x - mean[ax], dy = y - mean[ax + 1], dz = z - mean[ax + 2];
-      cxy += dx * dy; cxz += dx * dz; cyz += dy * dz;
-    }
-    res = wave_sum(res); cxy = wave_sum(cxy); cxz = wave_sum(cxz); cyz = wave_sum(cyz);
-    if (lane == 0) {
+    if (valid)
+      for (int t = sub; t < W; t += LPW) {
+        const float x = buf[t * A + ax], y = buf[t * A + ax + 1], z = buf[t * A + ax + 2];
+        res += sqrtf(x * x + y * y + z * z);
+        const float dx = x - mean[ax], dy = y - mean[ax + 1], dz = z - mean[ax + 2];
+        cxy += dx * dy; cxz += dx * dz; cyz += dy * dz;
+      }
+    res = gsum<LPW>(res); cxy = gsum<LPW>(cxy); cxz = gsum<LPW>(cxz); cyz = gsum<LPW>(cyz);
+    if (valid && sub == 0) {
       o[off_res + g] = res * invW;
       const float sx = sqrtf(var[ax]), sy = sqrtf(var[ax + 1]), sz = sqrtf(var[ax + 2]);
       o[off_corr + 3 * g + 0] = (sx > 0.f && sy > 0.f) ? cxy * invW / (sx * sy) : 0.f;
@@ -146,26 +200,37 @@ __global__ __launch_bounds__(WAVES * 64) void window_features_kernel(const float
   }
 }
 
+template <int A>
+int launch_axes(const float* stream, int64_t n_samples, int window, int stride, int64_t n_windows, float ms,
+                float* out, int ld_out, hipStream_t s) {
+  // four windows per wave while the block's 16 window images fit 64 KB of LDS, else one
+  const size_t img = (size_t)window * A * sizeof(float);
+  if ((size_t)WAVES * 4 * img <= 64 * 1024) {
+    const int64_t blocks = (n_windows + WAVES * 4 - 1) / (WAVES * 4);
+    window_features_kernel<A, 16><<<(unsigned)blocks, WAVES * 64, WAVES * 4 * img, s>>>(
+        stream, n_samples, window, stride, n_windows, ms, out, ld_out);
+  } else {
+    if ((size_t)WAVES * img > 160 * 1024) return -5;
+    const int64_t blocks = (n_windows + WAVES - 1) / WAVES;
+    window_features_kernel<A, 64><<<(unsigned)blocks, WAVES * 64, WAVES * img, s>>>(
+        stream, n_samples, window, stride, n_windows, ms, out, ld_out);
+  }
+  HAR_CHECK_LAUNCH();
+  return 0;
+}
+
 }  // namespace
 
 extern "C" int har_window_features(const float* stream, int64_t n_samples, int axes, int window, int stride,
                                    int64_t n_windows, float hz, int nbins, float* out, int ld_out, hipStream_t s) {
-  if (axes > MAXA || axes % 3 || nbins != NB || window < 3 || stride <= 0) return -2;
+  if (axes > MAXA || axes % 3 || nbins != NB || window < 3 || window >= 65536 || stride <= 0) return -2;
   if ((n_windows - 1) * (int64_t)stride + window > n_samples) return -3;  // every window must be in bounds
   if (ld_out < 17 * axes + 4 * (axes / 3)) return -4;
-  const size_t lds = (size_t)WAVES * window * axes * sizeof(float);
-  if (lds > 160 * 1024) return -5;
   if (n_windows == 0) return 0;
-  const int64_t blocks = (n_windows + WAVES - 1) / WAVES;
   const float ms = 1000.f / hz;
   switch (axes) {
-    case 3: window_features_kernel<3><<<(unsigned)blocks, WAVES * 64, lds, s>>>(stream, n_samples, window, stride,
-                                                                                 n_windows, ms, out, ld_out); break;
-    case 6: window_features_kernel<6><<<(unsigned)blocks, WAVES * 64, lds, s>>>(stream, n_samples, window, stride,
-                                                                                 n_windows, ms, out, ld_out); break;
-    default: window_features_kernel<9><<<(unsigned)blocks, WAVES * 64, lds, s>>>(stream, n_samples, window, stride,
-                                                                                  n_windows, ms, out, ld_out);
+    case 3: return launch_axes<3>(stream, n_samples, window, stride, n_windows, ms, out, ld_out, s);
+    case 6: return launch_axes<6>(stream, n_samples, window, stride, n_windows, ms, out, ld_out, s);
+    default: return launch_axes<9>(stream, n_samples, window, stride, n_windows, ms, out, ld_out, s);
   }
-  HAR_CHECK_LAUNCH();
-  return 0;
 }
