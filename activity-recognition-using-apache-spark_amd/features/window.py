@@ -102,6 +102,33 @@ def window_features(stream: torch.Tensor, window: int, stride: int, hz: float) -
     return out
 
 
+def window_features_mlp(stream: torch.Tensor, window: int, stride: int, hz: float, mean: torch.Tensor,
+                        inv_std: torch.Tensor, in_pad: int, nan_value: float = -1.0,
+                        out: torch.Tensor = None) -> torch.Tensor:
+    """Training input in ONE pass: [S, A] raw samples -> bf16 [n_windows, in_pad] rows of
+    ``((isnan(f) ? nan_value : f) - mean) * inv_std`` with zero padding — the window kernel's
+    MLP output mode (no fp32 feature matrix, no separate NaN-fill / scale / cast / pad kernels)."""
+    S, A = stream.shape
+    nw = window_count(S, window, stride)
+    F = n_features(A)
+    if not stream.is_cuda:
+        X = torch.nan_to_num(window_features_torch(stream, window, stride, hz).float(), nan=nan_value)
+        Xs = (X - mean.float().cpu()) * inv_std.float().cpu()
+        res = torch.zeros(nw, in_pad, dtype=torch.bfloat16)
+        res[:, :F] = Xs.to(torch.bfloat16)
+        return res
+    if out is None:
+        out = torch.empty(nw, in_pad, dtype=torch.bfloat16, device=stream.device)
+    if nw:
+        s = stream.contiguous().float()
+        m = mean.float().contiguous()
+        r = inv_std.float().contiguous()
+        _native.kernels().window_features_mlp(s.data_ptr(), S, A, window, stride, nw, float(hz), m.data_ptr(),
+                                              r.data_ptr(), float(nan_value), out.data_ptr(), in_pad,
+                                              _native.stream_ptr())
+    return out
+
+
 class WindowFeaturizer:
     """``transform(stream [S, A]) -> features [W, F]`` with the WISDM window defaults
     (10 s at ``hz``; non-overlapping unless ``overlap`` > 0)."""

@@ -247,7 +247,7 @@ def bench_rf(args, ctx, nine_axis=False):
 
 def bench_stream(args, ctx):
     from har.data.synth import StreamSpec, generate_stream
-    from har.features.window import n_features, window_features
+    from har.features.window import n_features, window_features, window_features_mlp
     from har.models.mlp import MLPEngine, pad_input_bf16
     from har.parallel import dist as hdist
 
@@ -289,11 +289,17 @@ def bench_stream(args, ctx):
         X = torch.nan_to_num(window_features(s, W, W, spec.hz), nan=-1.0)
         return (X - mean) * inv_std
 
+    xin = torch.empty(B, eng.layout.in_pad, dtype=torch.bfloat16, device=dev) if eng.native else None
+
     def step(i):
         j = i % nb
-        feat.copy_(featurize(stream[j * B * W:(j + 1) * B * W]))
-        Xb = pad_input_bf16(feat, eng.layout.in_pad)
-        eng.train_step(Xb, y32[j * B:(j + 1) * B], global_batch)
+        s = stream[j * B * W:(j + 1) * B * W]
+        if eng.native:  # one kernel: featurize + NaN fill + standardize + bf16 + pad
+            window_features_mlp(s, W, W, spec.hz, mean, inv_std, eng.layout.in_pad, -1.0, out=xin)
+            eng.train_step(xin, y32[j * B:(j + 1) * B], global_batch)
+        else:
+            feat.copy_(featurize(s))
+            eng.train_step(pad_input_bf16(feat, eng.layout.in_pad), y32[j * B:(j + 1) * B], global_batch)
 
     elapsed = timed(ctx, step, args.steps, args.warmup, dev)
     st_, yt = generate_stream(8192, spec, dev, first_window=10 ** 9)

@@ -174,6 +174,13 @@ PYBIND11_MODULE(_har_native, m) {
           "philox_buckets");
   });
 
+  m.def("window_features_mlp", [](u stream, int64_t n_samples, int axes, int window, int stride, int64_t n_windows,
+                                  float hz, u mean, u inv_std, float nan_value, u out, int ld_out, u stream_) {
+    check(har_window_features_mlp(P<const float>(stream), n_samples, axes, window, stride, n_windows, hz,
+                                  P<const float>(mean), P<const float>(inv_std), nan_value, P<uint16_t>(out), ld_out,
+                                  S(stream_)),
+          "window_features_mlp");
+  });
   m.def("window_features", [](u stream, int64_t n_samples, int axes, int window, int stride, int64_t n_windows,
                               float hz, int nbins, u out, int ld_out, u st) {
     check(har_window_features(P<const float>(stream), n_samples, axes, window, stride, n_windows, hz, nbins,

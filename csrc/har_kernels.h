@@ -112,6 +112,10 @@ int har_logreg_softmax_grad(const float* Z, int64_t n, int nmodels, int K, int l
                             hipStream_t s);
 
 // ---- windowed feature extraction over raw [S, A] streams ----
+// Training-input variant: bf16 ((isnan(v) ? nan_value : v) - mean) * inv_std rows, zero-padded to ld_out.
+int har_window_features_mlp(const float* stream, int64_t n_samples, int axes, int window, int stride,
+                            int64_t n_windows, float hz, const float* mean, const float* inv_std, float nan_value,
+                            uint16_t* out, int ld_out, hipStream_t s);
 int har_window_features(const float* stream, int64_t n_samples, int axes, int window, int stride,
                         int64_t n_windows, float hz, int nbins, float* out, int ld_out, hipStream_t s);
 

@@ -64,11 +64,22 @@ template <int LPW> __device__ __forceinline__ int gmaxi(int v) {
 // LPW lanes per window: 16 (four windows per wave — every shuffle-reduction instruction
 // serves four windows, and a 200-sample window keeps 12-13 samples per lane busy) or 64
 // (one window per wave, for windows whose LDS image is large).
-template <int A, int LPW>
+// MLP = true: the training-input variant — every feature is written as bf16
+// ((isnan(v) ? nan_value : v) - mean[f]) * inv_std[f] into a zero-padded [n_windows][ld_out] row,
+// so featurize -> NaN fill -> standardize -> cast -> pad is ONE pass.
+struct MlpOut {
+  const float* mean;
+  const float* inv_std;
+  float nan_value;
+  uint16_t* out;
+};
+
+template <int A, int LPW, bool MLP>
 __global__ __launch_bounds__(WAVES * 64) void window_features_kernel(const float* __restrict__ stream,
                                                                      int64_t n_samples, int W, int stride,
                                                                      int64_t n_windows, float ms_per_sample,
-                                                                     float* __restrict__ out, int ld_out) {
+                                                                     float* __restrict__ out, int ld_out,
+                                                                     MlpOut mo) {
   constexpr int G = 64 / LPW;  // windows per wave
   extern __shared__ __attribute__((aligned(16))) float lds[];  // [WAVES * G][W*A]
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -118,7 +129,21 @@ __global__ __launch_bounds__(WAVES * 64) void window_features_kernel(const float
     mean[a] = s * invW; en[a] = q * invW; mn[a] = lo; mx[a] = hi;
   }
   constexpr int T3 = A / 3;
-  float* o = out + (valid ? win : 0) * (int64_t)ld_out;
+  float* o = MLP ? nullptr : out + (valid ? win : 0) * (int64_t)ld_out;
+  uint16_t* ob = MLP ? mo.out + (valid ? win : 0) * (int64_t)ld_out : nullptr;
+  auto emit = [&](int f, float v) {
+    if constexpr (MLP) {
+      const float x = v != v ? mo.nan_value : v;
+      ob[f] = f2bf((x - mo.mean[f]) * mo.inv_std[f]);
+    } else {
+      o[f] = v;
+    }
+  };
+  if constexpr (MLP) {  // zero the pad columns of the row
+    constexpr int F = 17 * A + 4 * (A / 3);
+    for (int f = F + sub; f < ld_out; f += LPW)
+      if (valid) ob[f] = 0;
+  }
   const int off_avg = A * NB, off_peak = off_avg + A, off_abs = off_peak + A, off_std = off_abs + A;
   const int off_res = off_std + A, off_min = off_res + T3, off_max = off_min + A, off_en = off_max + A;
   const int off_corr = off_en + A;
@@ -166,15 +191,15 @@ __global__ __launch_bounds__(WAVES * 64) void window_features_kernel(const float
       const int c = (k & 1) ? (cnt[k >> 1] >> 16) : (cnt[k >> 1] & 0xffff);
       mine = (sub == k) ? (float)c : mine;
     }
-    if (valid && sub < NB) o[a * NB + sub] = mine * invW;
+    if (valid && sub < NB) emit(a * NB + sub, mine * invW);
     if (valid && sub == 0) {
-      o[off_avg + a] = m;
-      o[off_peak + a] = npk >= 2 ? (float)(last - first) / (float)(npk - 1) * ms_per_sample : NAN;
-      o[off_abs + a] = ad * invW;
-      o[off_std + a] = sqrtf(var[a]);
-      o[off_min + a] = mn[a];
-      o[off_max + a] = mx[a];
-      o[off_en + a] = en[a];
+      emit(off_avg + a, m);
+      emit(off_peak + a, npk >= 2 ? (float)(last - first) / (float)(npk - 1) * ms_per_sample : NAN);
+      emit(off_abs + a, ad * invW);
+      emit(off_std + a, sqrtf(var[a]));
+      emit(off_min + a, mn[a]);
+      emit(off_max + a, mx[a]);
+      emit(off_en + a, en[a]);
     }
   }
   // ---- per triad: resultant + correlations ----
@@ -191,29 +216,29 @@ __global__ __launch_bounds__(WAVES * 64) void window_features_kernel(const float
       }
     res = gsum<LPW>(res); cxy = gsum<LPW>(cxy); cxz = gsum<LPW>(cxz); cyz = gsum<LPW>(cyz);
     if (valid && sub == 0) {
-      o[off_res + g] = res * invW;
+      emit(off_res + g, res * invW);
       const float sx = sqrtf(var[ax]), sy = sqrtf(var[ax + 1]), sz = sqrtf(var[ax + 2]);
-      o[off_corr + 3 * g + 0] = (sx > 0.f && sy > 0.f) ? cxy * invW / (sx * sy) : 0.f;
-      o[off_corr + 3 * g + 1] = (sx > 0.f && sz > 0.f) ? cxz * invW / (sx * sz) : 0.f;
-      o[off_corr + 3 * g + 2] = (sy > 0.f && sz > 0.f) ? cyz * invW / (sy * sz) : 0.f;
+      emit(off_corr + 3 * g + 0, (sx > 0.f && sy > 0.f) ? cxy * invW / (sx * sy) : 0.f);
+      emit(off_corr + 3 * g + 1, (sx > 0.f && sz > 0.f) ? cxz * invW / (sx * sz) : 0.f);
+      emit(off_corr + 3 * g + 2, (sy > 0.f && sz > 0.f) ? cyz * invW / (sy * sz) : 0.f);
     }
   }
 }
 
-template <int A>
+template <int A, bool MLP>
 int launch_axes(const float* stream, int64_t n_samples, int window, int stride, int64_t n_windows, float ms,
-                float* out, int ld_out, hipStream_t s) {
+                float* out, int ld_out, MlpOut mo, hipStream_t s) {
   // four windows per wave while the block's 16 window images fit 64 KB of LDS, else one
   const size_t img = (size_t)window * A * sizeof(float);
   if ((size_t)WAVES * 4 * img <= 64 * 1024) {
     const int64_t blocks = (n_windows + WAVES * 4 - 1) / (WAVES * 4);
-    window_features_kernel<A, 16><<<(unsigned)blocks, WAVES * 64, WAVES * 4 * img, s>>>(
-        stream, n_samples, window, stride, n_windows, ms, out, ld_out);
+    window_features_kernel<A, 16, MLP><<<(unsigned)blocks, WAVES * 64, WAVES * 4 * img, s>>>(
+        stream, n_samples, window, stride, n_windows, ms, out, ld_out, mo);
   } else {
     if ((size_t)WAVES * img > 160 * 1024) return -5;
     const int64_t blocks = (n_windows + WAVES - 1) / WAVES;
-    window_features_kernel<A, 64><<<(unsigned)blocks, WAVES * 64, WAVES * img, s>>>(
-        stream, n_samples, window, stride, n_windows, ms, out, ld_out);
+    window_features_kernel<A, 64, MLP><<<(unsigned)blocks, WAVES * 64, WAVES * img, s>>>(
+        stream, n_samples, window, stride, n_windows, ms, out, ld_out, mo);
   }
   HAR_CHECK_LAUNCH();
   return 0;
@@ -228,9 +253,26 @@ extern "C" int har_window_features(const float* stream, int64_t n_samples, int a
   if (ld_out < 17 * axes + 4 * (axes / 3)) return -4;
   if (n_windows == 0) return 0;
   const float ms = 1000.f / hz;
+  const MlpOut none{nullptr, nullptr, 0.f, nullptr};
   switch (axes) {
-    case 3: return launch_axes<3>(stream, n_samples, window, stride, n_windows, ms, out, ld_out, s);
-    case 6: return launch_axes<6>(stream, n_samples, window, stride, n_windows, ms, out, ld_out, s);
-    default: return launch_axes<9>(stream, n_samples, window, stride, n_windows, ms, out, ld_out, s);
+    case 3: return launch_axes<3, false>(stream, n_samples, window, stride, n_windows, ms, out, ld_out, none, s);
+    case 6: return launch_axes<6, false>(stream, n_samples, window, stride, n_windows, ms, out, ld_out, none, s);
+    default: return launch_axes<9, false>(stream, n_samples, window, stride, n_windows, ms, out, ld_out, none, s);
+  }
+}
+
+extern "C" int har_window_features_mlp(const float* stream, int64_t n_samples, int axes, int window, int stride,
+                                       int64_t n_windows, float hz, const float* mean, const float* inv_std,
+                                       float nan_value, uint16_t* out, int ld_out, hipStream_t s) {
+  if (axes > MAXA || axes % 3 || window < 3 || window >= 65536 || stride <= 0) return -2;
+  if ((n_windows - 1) * (int64_t)stride + window > n_samples) return -3;
+  if (ld_out < 17 * axes + 4 * (axes / 3) || !mean || !inv_std || !out) return -4;
+  if (n_windows == 0) return 0;
+  const float ms = 1000.f / hz;
+  const MlpOut mo{mean, inv_std, nan_value, out};
+  switch (axes) {
+    case 3: return launch_axes<3, true>(stream, n_samples, window, stride, n_windows, ms, nullptr, ld_out, mo, s);
+    case 6: return launch_axes<6, true>(stream, n_samples, window, stride, n_windows, ms, nullptr, ld_out, mo, s);
+    default: return launch_axes<9, true>(stream, n_samples, window, stride, n_windows, ms, nullptr, ld_out, mo, s);
   }
 }

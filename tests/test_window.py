@@ -64,3 +64,23 @@ def test_window_kernel_matches_torch(cuda, axes, window, stride):
     # bins: float32 vs float64 bin edges may move a boundary sample by one bin
     assert (out[:, :nb] - ref[:, :nb]).abs().max() <= 1.0 / window + 1e-6
     torch.testing.assert_close(out[:, nb:], ref[:, nb:], rtol=2e-4, atol=2e-4, equal_nan=True)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("axes,window,stride", [(3, 200, 200), (9, 500, 500), (3, 128, 64)])
+def test_window_kernel_mlp_output(cuda, axes, window, stride):
+    """MLP-input mode of the window kernel: bf16 standardized, NaN-filled, zero-padded rows equal
+    the fp32 features pushed through the same transform (bf16 rounding of the result only)."""
+    from har.features.window import window_features, window_features_mlp
+
+    spec = StreamSpec(axes=axes, window=window, seed=axes + 7)
+    s, _ = generate_stream(48, spec, cuda)
+    F = n_features(axes)
+    mean = torch.randn(F, device=cuda)
+    inv_std = torch.rand(F, device=cuda) + 0.5
+    pad = (F + 31) // 32 * 32
+    ref = (torch.nan_to_num(window_features(s, window, stride, 50.0), nan=-1.0) - mean) * inv_std
+    out = window_features_mlp(s, window, stride, 50.0, mean, inv_std, pad)
+    assert out.shape == (ref.shape[0], pad) and out.dtype == torch.bfloat16
+    assert torch.count_nonzero(out[:, F:]) == 0
+    torch.testing.assert_close(out[:, :F].float(), ref.to(torch.bfloat16).float(), rtol=0, atol=0)
