@@ -113,20 +113,24 @@ __global__ __launch_bounds__(WAVES * 64) void window_features_kernel(const float
 
   const float invW = 1.f / (float)W;
   float mean[A], mn[A], mx[A], en[A];
-  // ---- pass 1 ----
+  // ---- pass 1: one sweep over the samples for all axes ----
+  {
+    float s[A], q[A], lo[A], hi[A];
 #pragma unroll
-  for (int a = 0; a < A; ++a) {
-    float s = 0.f, q = 0.f, lo = INFINITY, hi = -INFINITY;
+    for (int a = 0; a < A; ++a) { s[a] = 0.f; q[a] = 0.f; lo[a] = INFINITY; hi[a] = -INFINITY; }
     if (valid)
       for (int t = sub; t < W; t += LPW) {
-        float v = buf[t * A + a];
-        s += v; q += v * v; lo = fminf(lo, v); hi = fmaxf(hi, v);
+#pragma unroll
+        for (int a = 0; a < A; ++a) {
+          const float v = buf[t * A + a];
+          s[a] += v; q[a] += v * v; lo[a] = fminf(lo[a], v); hi[a] = fmaxf(hi[a], v);
+        }
       }
-    s = gsum<LPW>(s);
-    q = gsum<LPW>(q);
-    lo = gmin<LPW>(lo);
-    hi = gmax<LPW>(hi);
-    mean[a] = s * invW; en[a] = q * invW; mn[a] = lo; mx[a] = hi;
+#pragma unroll
+    for (int a = 0; a < A; ++a) {
+      mean[a] = gsum<LPW>(s[a]) * invW; en[a] = gsum<LPW>(q[a]) * invW;
+      mn[a] = gmin<LPW>(lo[a]); mx[a] = gmax<LPW>(hi[a]);
+    }
   }
   constexpr int T3 = A / 3;
   float* o = MLP ? nullptr : out + (valid ? win : 0) * (int64_t)ld_out;
@@ -152,6 +156,7 @@ __global__ __launch_bounds__(WAVES * 64) void window_features_kernel(const float
 #pragma unroll
   for (int a = 0; a < A; ++a) {
     const float m = mean[a], lo = mn[a], range = mx[a] - mn[a];
+    const float bscale = range > 0.f ? (float)NB / range : 0.f;  // one reciprocal per axis, not per sample
     const float thr = m + 0.5f * (mx[a] - m);
     float ad = 0.f, v2 = 0.f;
     int cnt[NB / 2];  // two 16-bit bin counters per register (W < 65536): 5 reductions, not 10
@@ -164,7 +169,7 @@ __global__ __launch_bounds__(WAVES * 64) void window_features_kernel(const float
         const float d = v - m;
         ad += fabsf(d);
         v2 += d * d;
-        int b = range > 0.f ? (int)((v - lo) / range * NB) : 0;
+        int b = (int)((v - lo) * bscale);
         b = b < 0 ? 0 : (b >= NB ? NB - 1 : b);
         const int inc = (b & 1) ? 0x10000 : 1;
 #pragma unroll
