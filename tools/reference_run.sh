@@ -7,10 +7,10 @@ cd "$ROOT"
 OUT="$ROOT/gpurun_out/reference_run"
 mkdir -p "$OUT"
 python tools/build_native.py > /dev/null || exit 3
-DATA="${HAR_WISDM_CSV:-$ROOT/data/wisdm_data.csv}"
+DATA="${HAR_WISDM_CSV:-$ROOT/tests/data/wisdm_data.csv}"
 for preset in reference rf-deep mlp all-numeric; do
   timeout -k 10 600 python main.py --preset $preset --data "$DATA" --device cuda \
-      --out-dir "$OUT/$preset" ${EXTRA:-} > "$OUT/$preset.log" 2>&1
+      --out-dir "$OUT/$preset" --report ${EXTRA:-} > "$OUT/$preset.log" 2>&1
   rc=$?
   tail -1 "$OUT/$preset.log" | cut -c1-600
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "preset $preset fatal $rc"; exit $rc; fi
