@@ -63,10 +63,14 @@ __global__ __launch_bounds__(256) void tree_hist_split_kernel(
     }
   } else if (mode != 2) {
     // small node: (feature slot, row) pairs, rows fastest, so every lane has work
-    const int64_t pairs = (int64_t)cnt * f_n;
-    for (int64_t j = tid; j < pairs; j += blockDim.x) {
-      const int fs = (int)(j / cnt);
-      const int ri = (int)(j - (int64_t)fs * cnt);
+    // j -> (fs, ri) by a float reciprocal + one correction step instead of an integer division
+    // (~40 VALU ops per pair; j < 2^24 is exact in fp32, so the estimate is off by at most one)
+    const int pairs = cnt * f_n;
+    const float inv_cnt = 1.f / (float)cnt;
+    for (int j = tid; j < pairs; j += blockDim.x) {
+      int fs = (int)((float)j * inv_cnt);
+      int ri = j - fs * cnt;
+      if (ri < 0) { --fs; ri += cnt; } else if (ri >= cnt) { ++fs; ri -= cnt; }
       const int r = rows[start + ri];
       const float w = row_w[start + ri];
       const int b = bins[fid[fs] * fstride + r * rstride];
@@ -161,33 +165,87 @@ __global__ __launch_bounds__(256) void tree_hist_split_kernel(
   }
 }
 
+// Leaf statistics of tree t for input row x (normalized to a distribution when asked), added
+// into acc[0..K).  KC >= K is a compile-time bound so acc stays in registers.
+template <int KC>
+__device__ __forceinline__ void add_tree(const float* __restrict__ x, size_t base, const int32_t* __restrict__ feature,
+                                         const float* __restrict__ thr, const int32_t* __restrict__ left,
+                                         const int32_t* __restrict__ right, const float* __restrict__ leaf, int K,
+                                         int max_depth, int normalize, float (&acc)[KC]) {
+  int node = 0;
+  for (int d = 0; d <= max_depth; ++d) {
+    const int f = feature[base + node];
+    if (f < 0) break;
+    node = (x[f] <= thr[base + node]) ? left[base + node] : right[base + node];
+  }
+  const float* st = leaf + (base + node) * K;
+  float v[KC];
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < KC; ++k) {
+    v[k] = k < K ? st[k] : 0.f;
+    s += v[k];
+  }
+  const float sc = normalize ? (s > 0.f ? 1.f / s : 0.f) : 1.f;
+#pragma unroll
+  for (int k = 0; k < KC; ++k) acc[k] += v[k] * sc;
+}
+
+// Many rows: one lane per row walks every tree.
+template <int KC>
 __global__ __launch_bounds__(256) void forest_predict_kernel(
     const float* __restrict__ X, int64_t n, int ld, const int32_t* __restrict__ feature,
     const float* __restrict__ thr, const int32_t* __restrict__ left, const int32_t* __restrict__ right,
     const float* __restrict__ leaf, int T, int maxn, int K, int max_depth, int normalize, float* __restrict__ out) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  float acc[KMAX];
-  for (int k = 0; k < K; ++k) acc[k] = 0.f;
+  float acc[KC];
+#pragma unroll
+  for (int k = 0; k < KC; ++k) acc[k] = 0.f;
   const float* x = X + i * (int64_t)ld;
-  for (int t = 0; t < T; ++t) {
-    const size_t base = (size_t)t * maxn;
-    int node = 0;
-    for (int d = 0; d <= max_depth; ++d) {
-      const int f = feature[base + node];
-      if (f < 0) break;
-      node = (x[f] <= thr[base + node]) ? left[base + node] : right[base + node];
-    }
-    const float* st = leaf + (base + node) * K;
-    float s = 1.f;
-    if (normalize) {
-      s = 0.f;
-      for (int k = 0; k < K; ++k) s += st[k];
-      s = s > 0.f ? 1.f / s : 0.f;
-    }
-    for (int k = 0; k < K; ++k) acc[k] += st[k] * s;
+  for (int t = 0; t < T; ++t)
+    add_tree<KC>(x, (size_t)t * maxn, feature, thr, left, right, leaf, K, max_depth, normalize, acc);
+#pragma unroll
+  for (int k = 0; k < KC; ++k)
+    if (k < K) out[i * K + k] = acc[k];
+}
+
+// Few rows (serving batches, evaluation sets): one wave per row, lanes split the trees, one
+// wave reduction per class — 64x the parallelism of the lane-per-row form.
+template <int KC>
+__global__ __launch_bounds__(256) void forest_predict_wave_kernel(
+    const float* __restrict__ X, int64_t n, int ld, const int32_t* __restrict__ feature,
+    const float* __restrict__ thr, const int32_t* __restrict__ left, const int32_t* __restrict__ right,
+    const float* __restrict__ leaf, int T, int maxn, int K, int max_depth, int normalize, float* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const int64_t i = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (i >= n) return;  // wave-uniform
+  float acc[KC];
+#pragma unroll
+  for (int k = 0; k < KC; ++k) acc[k] = 0.f;
+  const float* x = X + i * (int64_t)ld;
+  for (int t = lane; t < T; t += 64)
+    add_tree<KC>(x, (size_t)t * maxn, feature, thr, left, right, leaf, K, max_depth, normalize, acc);
+#pragma unroll
+  for (int k = 0; k < KC; ++k) {
+    float v = acc[k];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    if (lane == k && k < K) out[i * K + k] = v;
   }
-  for (int k = 0; k < K; ++k) out[i * K + k] = acc[k];
+}
+
+template <int KC>
+void launch_predict(const float* X, int64_t n, int ld, const int32_t* feat, const float* thr, const int32_t* left,
+                    const int32_t* right, const float* leaf, int ntrees, int maxn, int K, int max_depth,
+                    int normalize, float* raw_out, hipStream_t s) {
+  if (ntrees >= 16) {  // 1M rows x 100 trees on MI355X: 11.5 ms here vs 16.8 ms lane-per-row
+    forest_predict_wave_kernel<KC><<<(int)((n + 3) / 4), 256, 0, s>>>(X, n, ld, feat, thr, left, right, leaf, ntrees,
+                                                                       maxn, K, max_depth, normalize, raw_out);
+  } else {
+    forest_predict_kernel<KC><<<(int)((n + 255) / 256), 256, 0, s>>>(X, n, ld, feat, thr, left, right, leaf, ntrees,
+                                                                     maxn, K, max_depth, normalize, raw_out);
+  }
 }
 
 __global__ __launch_bounds__(256) void poisson_bootstrap_kernel(uint64_t seed, int tree0, int ntrees, int64_t row0,
@@ -239,8 +297,10 @@ extern "C" int har_forest_predict(const float* X, int64_t n, int F, int ld, cons
                                   int maxn, int K, int max_depth, int normalize, float* raw_out, hipStream_t s) {
   if (K > KMAX) return -2;
   if (n == 0) return 0;
-  forest_predict_kernel<<<(int)((n + 255) / 256), 256, 0, s>>>(X, n, ld, feat, thr, left, right, leaf, ntrees, maxn,
-                                                               K, max_depth, normalize, raw_out);
+  if (K <= 8) launch_predict<8>(X, n, ld, feat, thr, left, right, leaf, ntrees, maxn, K, max_depth, normalize, raw_out, s);
+  else if (K <= 16) launch_predict<16>(X, n, ld, feat, thr, left, right, leaf, ntrees, maxn, K, max_depth, normalize,
+                                       raw_out, s);
+  else launch_predict<32>(X, n, ld, feat, thr, left, right, leaf, ntrees, maxn, K, max_depth, normalize, raw_out, s);
   HAR_CHECK_LAUNCH();
   return 0;
 }
