@@ -98,13 +98,17 @@ __global__ __launch_bounds__(256) void tree_hist_split_kernel(
     const int nb = nbins_feat[fid[fs]];
     double wl = 0.0, wt = 0.0, ql = 0.0, qr = 0.0, qt = 0.0;
     for (int k = 0; k < K; ++k) {
-      double v = (lane < nb && lane < maxbins) ? (double)hist[(fs * maxbins + lane) * K + k] : 0.0;
+      // the bin scan runs in fp32 (one ds_bpermute per step instead of two): the sums are exact
+      // for integer-valued weights below 2^24 (bootstrap counts, fold masks) and are what the
+      // CPU oracle's float32 cumsum computes anyway; the gains below are fp64
+      float vf = (lane < nb && lane < maxbins) ? hist[(fs * maxbins + lane) * K + k] : 0.f;
 #pragma unroll
       for (int o = 1; o < 64; o <<= 1) {
-        double u = __shfl_up(v, o, 64);
-        if (lane >= o) v += u;
+        const float u = __shfl_up(vf, o, 64);
+        if (lane >= o) vf += u;
       }
-      const double t = __shfl(v, max(nb - 1, 0), 64);
+      const double v = (double)vf;
+      const double t = (double)__shfl(vf, max(nb - 1, 0), 64);
       const double r = t - v;
       wl += v;
       wt += t;
