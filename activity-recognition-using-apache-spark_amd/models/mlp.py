@@ -60,16 +60,16 @@ def fwd_tile(M: int, N: int, K: int) -> int:
 
 
 def dgrad_tile(M: int, N: int, K: int) -> int:
-    return 6 if N >= 256 else 12
+    return 18 if N >= 256 else 12    # 128x128 / 8 waves (24.0 us vs 24.8 for 128x256 at B = 65536)
 
 
 def wgrad_tile(M: int, N: int) -> int:
-    """Weight-gradient (split-K over the batch) tiles."""
+    """Weight-gradient (split-K over the batch) tiles (profiles/gemm_tile_sweep_v2.md)."""
     if M <= 32:
         return 11 if N > 32 else 2   # 32x64, BK 128
     if N <= 64:
-        return 8                     # 64x64, BK 128
-    return 9                         # 128x128, BK 64
+        return 20                    # 64x64, BK 128, 8 waves: 13.1 us vs 14.4 (4 waves)
+    return 18                        # 128x128, BK 64, 8 waves: 23.4 us vs 30.0 (4 waves)
 
 
 @dataclass

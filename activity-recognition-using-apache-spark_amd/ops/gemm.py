@@ -20,7 +20,8 @@ from . import _native
 EPI_F32, EPI_F32_ATOMIC, EPI_BIAS_RELU, EPI_BIAS, EPI_RELU_GRAD, EPI_BIAS_F32, EPI_F32_SLAB = range(7)
 TILES = {0: (128, 128, 32), 1: (128, 64, 32), 2: (128, 32, 32), 3: (64, 128, 32), 4: (64, 64, 32), 5: (32, 64, 32),
          6: (128, 256, 32), 7: (64, 256, 32), 8: (64, 64, 128), 9: (128, 128, 64), 10: (128, 256, 64),
-         11: (32, 64, 128), 12: (64, 128, 64), 13: (128, 64, 128)}  # (BM, BN, BK)
+         11: (32, 64, 128), 12: (64, 128, 64), 13: (128, 64, 128), 18: (128, 128, 64), 20: (64, 64, 128)}
+# (BM, BN, BK); 18 and 20 run 8 waves (4 x 2), the rest <= 2 x 4
 _TARGET_BLOCKS = 1024  # >> 256 CUs, bounded split-K traffic
 
 

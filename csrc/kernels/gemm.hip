@@ -364,6 +364,9 @@ int launch_epi(const GemmParams& p, int epi, hipStream_t s) {
 //   0: 128x128 (2x2 waves)  1: 128x64 (2x2)  2: 128x32 (4x1)  3: 64x128 (1x4)  4: 64x64 (2x2)  5: 32x64 (1x2)
 //   6: 128x256 (2x4, 512 threads)  7: 64x256 (1x4)            (all BK = 32)
 //   8: 64x64 BK128  9: 128x128 BK64  10: 128x256 BK64  11: 32x64 BK128  12: 64x128 BK64  13: 128x64 BK128
+//   18: 128x128 BK64 with 8 waves (4 x 2)   20: 64x64 BK128 with 8 waves (4 x 2) — the split-K
+//   weight-gradient tiles (profiles/gemm_tile_sweep_v2.md: 8 waves of 32-row slices beat 4 waves,
+//   2 x 4 and 4 x 4 arrangements)
 template <typename T, bool AK, bool BKm>
 int launch_tile(const GemmParams& p, int epi, hipStream_t s) {
   int tile = p.tile;
@@ -388,6 +391,8 @@ int launch_tile(const GemmParams& p, int epi, hipStream_t s) {
     case 11: return launch_epi<T, 32, 64, 128, 1, 2, AK, BKm>(p, epi, s);
     case 12: return launch_epi<T, 64, 128, 64, 1, 4, AK, BKm>(p, epi, s);
     case 13: return launch_epi<T, 128, 64, 128, 2, 2, AK, BKm>(p, epi, s);
+    case 18: return launch_epi<T, 128, 128, 64, 4, 2, AK, BKm>(p, epi, s);
+    case 20: return launch_epi<T, 64, 64, 128, 4, 2, AK, BKm>(p, epi, s);
     default: return -4;
   }
 }

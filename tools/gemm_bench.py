@@ -34,19 +34,19 @@ def main():
     rowsum = torch.empty(S * (H * H + H), device=dev)
     cases = {
         "fwd_L1": (lambda t: gemm_bf16(X, W0, out, M=B, N=H, K=64, layout=0, epi=EPI_BIAS_RELU, bias=bias, tile=t),
-                   [0, 3, 6, 7, 9, 10, 12]),
+                   [12, 3]),
         "fwd_L2": (lambda t: gemm_bf16(h1, W1, out, M=B, N=H, K=H, layout=0, epi=EPI_BIAS_RELU, bias=bias, tile=t),
                    [0, 3, 6, 7, 9, 10, 12]),
         "dgrad_L1": (lambda t: gemm_bf16(h2, W1, out, M=B, N=H, K=H, layout=2, epi=EPI_RELU_GRAD, mask=h1, tile=t),
-                     [0, 3, 6, 7, 9, 10, 12]),
+                     [6, 18]),
         "wgrad_W1": (lambda t: gemm_bf16(h2, h1, slab, M=H, N=H, K=B, layout=3, epi=EPI_F32_SLAB, k_split=ks, ldc=H,
                                          slab_stride=H * H + H, rowsum=rowsum, slab_stride_rowsum=H * H + H, tile=t),
-                     [0, 3, 4, 8, 9, 12, 13]),
+                     [9, 18]),
         "wgrad_W1_norowsum": (lambda t: gemm_bf16(h2, h1, slab, M=H, N=H, K=B, layout=3, epi=EPI_F32_SLAB,
                                                   k_split=ks, ldc=H, slab_stride=H * H + H, tile=t), [0, 9]),
         "wgrad_W0": (lambda t: gemm_bf16(h2, X, slab, M=H, N=64, K=B, layout=3, epi=EPI_F32_SLAB, k_split=ks, ldc=64,
                                          slab_stride=H * H + H, rowsum=rowsum, slab_stride_rowsum=H * H + H, tile=t),
-                     [1, 4, 8, 13]),
+                     [8, 20]),
         "wgrad_Wout": (lambda t: gemm_bf16(dl, h2, slab, M=32, N=H, K=B, layout=3, epi=EPI_F32_SLAB, k_split=ks,
                                            ldc=H, slab_stride=H * H + H, rowsum=rowsum, slab_stride_rowsum=H * H + H,
                                            tile=t),
