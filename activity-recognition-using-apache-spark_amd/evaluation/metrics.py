@@ -15,7 +15,7 @@
 
 On the GPU the confusion matrix and the regression moments are single HIP
 reductions (``csrc/kernels/metrics.hip``); the ROC/PR curve is a device sort +
-segmented scan.
+one HIP pass over the sorted scores (``csrc/kernels/roc.hip``).
 """
 from __future__ import annotations
 
@@ -65,6 +65,9 @@ def multiclass_metrics(label, pred, num_classes: int) -> Dict[str, float]:
 
 def binary_metrics(score, label) -> Dict[str, float]:
     """areaUnderROC / areaUnderPR for scores vs. (label > 0.5)."""
+    if isinstance(score, torch.Tensor) and score.is_cuda:
+        auroc, aupr = mops.roc_pr_auc(score, _t(label))
+        return {"areaUnderROC": auroc, "areaUnderPR": aupr}
     s = _t(score, torch.float64).reshape(-1)
     y = (_t(label, torch.float64).reshape(-1) > 0.5).to(torch.float64)
     order = torch.argsort(s, descending=True, stable=True)

@@ -22,6 +22,27 @@ def confusion_matrix(label: torch.Tensor, pred: torch.Tensor, K: int) -> torch.T
     return torch.bincount(idx, minlength=K * K).view(K, K)
 
 
+def roc_pr_auc(score: torch.Tensor, label: torch.Tensor):
+    """(areaUnderROC, areaUnderPR) of ``score`` vs ``label > 0.5`` on the device (K19): a
+    descending sort (rocPRIM radix sort behind ``torch.sort``), then ONE HIP pass over the sorted
+    scores that forms the tie-grouped curve points and sums the trapezoids
+    (``csrc/kernels/roc.hip``).  Scores are compared in fp32 (the models' raw predictions)."""
+    s = score.reshape(-1).to(torch.float32)
+    y = label.reshape(-1).to(device=s.device, dtype=torch.float32)
+    vals, order = torch.sort(s, descending=True)
+    ys = y[order].contiguous()
+    vals = vals.contiguous()
+    out = torch.zeros(4, dtype=torch.float64, device=s.device)
+    _native.kernels().roc_pr_sums(vals.data_ptr(), ys.data_ptr(), vals.numel(), out.data_ptr(),
+                                  _native.stream_ptr())
+    roc, pr, P, N = out.cpu().tolist()
+    # the curve closes at (1, 1); without negatives its last point is (0, 1) and the closing
+    # segment is the whole area (without positives tpr is 0 everywhere)
+    auroc = (roc / (2.0 * P * N) if P > 0 and N > 0 else 0.0) + (0.0 if N > 0 else (1.0 + (P > 0)) / 2.0)
+    aupr = pr / (2.0 * P) if P > 0 else 0.0
+    return auroc, aupr
+
+
 def regression_moments(y: torch.Tensor, yhat: torch.Tensor):
     """(n, sum (y-yh)^2, sum |y-yh|, sum y, sum y^2) — fp64 accumulation."""
     if y.is_cuda:

@@ -144,6 +144,10 @@ PYBIND11_MODULE(_har_native, m) {
           "regression_moments");
   });
 
+  m.def("roc_pr_sums", [](u s, u y, int64_t n, u out, u stream) {
+    check(har_roc_pr_sums(P<const float>(s), P<const float>(y), n, P<double>(out), S(stream)), "roc_pr_sums");
+  });
+
   m.def("tree_hist_split", [](u bins, int64_t N, int F, int row_major, u nbins, u rows, u row_w, u node_start, u node_count, int A,
                               u feats, int m, int fc, u label, int K, int maxbins, float min_inst, float min_gain,
                               int impurity, u gain, u feat, u bin, u left, u total, int mode, u ghist, int row_chunks,

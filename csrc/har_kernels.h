@@ -105,6 +105,9 @@ int har_bin_features(const float* X, int64_t n, int F, int ld, const float* thr,
 int har_confusion_matrix(const int32_t* label, const int32_t* pred, int64_t n, int K, int64_t* cm,
                          hipStream_t s);
 int har_regression_moments(const float* y, const float* yhat, int64_t n, double* out6, hipStream_t s);
+// scores sorted descending, labels permuted alike (positive iff > 0.5):
+// out4 = {sum dFP (TP + TP_prev), sum dTP (prec + prec_prev), P, N} over tie-group end points
+int har_roc_pr_sums(const float* sorted_scores, const float* labels, int64_t n, double* out4, hipStream_t s);
 
 // ---- logistic regression (batched over B models, K classes padded to 8) ----
 int har_logreg_softmax_grad(const float* Z, int64_t n, int nmodels, int K, int ld, const int32_t* y,

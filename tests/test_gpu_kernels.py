@@ -254,6 +254,31 @@ def test_metrics_kernels(cuda):
     assert abs(sy - float(y.double().sum())) < 1e-6
 
 
+def test_roc_pr_kernel(cuda):
+    """roc.hip (K19) vs the fp64 PyTorch curve: tie groups, ties straddling threads and chunks,
+    a single row, and no-positive / no-negative label sets."""
+    from har.evaluation import metrics as M
+    from har.ops.metrics import roc_pr_auc
+
+    g = torch.Generator().manual_seed(4)
+    for n, levels in ((1625, 0), (10001, 37), (4096 * 3 + 5, 7), (5, 2), (1, 0)):
+        s = torch.randn(n, generator=g)
+        if levels:
+            s = torch.round(s * levels) / levels
+        y = torch.randint(0, 6, (n,), generator=g).float()
+        ref = M.binary_metrics(s, y)  # CPU oracle
+        auroc, aupr = roc_pr_auc(s.to(cuda), y.to(cuda))
+        assert abs(auroc - ref["areaUnderROC"]) < 1e-9, (n, auroc, ref)
+        assert abs(aupr - ref["areaUnderPR"]) < 1e-9, (n, aupr, ref)
+    for yv in (0.0, 3.0):
+        s = torch.randn(300, generator=g)
+        y = torch.full((300,), yv)
+        ref = M.binary_metrics(s, y)
+        got = M.binary_metrics(s.to(cuda), y.to(cuda))  # evaluator entry point takes the kernel
+        assert abs(got["areaUnderROC"] - ref["areaUnderROC"]) < 1e-12
+        assert abs(got["areaUnderPR"] - ref["areaUnderPR"]) < 1e-12
+
+
 def test_column_stats_and_binning(cuda):
     from har.ops import stats
     from har.ops import tree as T
