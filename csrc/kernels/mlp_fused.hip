@@ -25,6 +25,8 @@
 // Outputs: h1 (bf16, for dW1 / dgrad), dact2 = (dz . Wout) * (h2 > 0) (bf16, for
 // dW1 / dgrad), per-workgroup dWout rows 0..15 + dbout slabs (fp32, deterministic
 // reduction later), per-workgroup loss / #correct.
+#include <cstdlib>
+
 #include "common.h"
 #include "../har_kernels.h"
 
@@ -371,11 +373,361 @@ int launch(const bf16_t* X, const bf16_t* W0, const float* b0, const bf16_t* W1,
   return 0;
 }
 
+// ---------------------------------------------------------------------------------------------
+// v2 (H = 256, batch a multiple of 32; the default for those shapes, HAR_MLP_FUSED_V1=1 keeps
+// v1): 8 waves per workgroup; wave w owns hidden units [32w, 32w + 32) of BOTH hidden layers,
+// so its slices of W0, W1 (64 VGPRs per lane) and Wout stay in registers and the LDS holds only
+// per-tile data — the 32-row h1 tile (written by all 8 waves, read by all), the partial logits
+// and the stage-5 transpose images (~69 KB).  At <= 256 registers per lane two waves share each
+// SIMD (v1: one; its resident W1 image filled the LDS), so one wave's LDS / VALU / store
+// latency runs under the other's MFMAs.
+//
+//   stage 1  h1^T[u][r] = W0[u] . x_r        A = W0 (registers), B = X rows (16-byte loads)
+//            -> h1 (global) and the LDS h1 tile                                  | barrier
+//   stage 2  h2^T[u] = W1[u] . h1^T          A = W1 (registers), B = 16-byte LDS reads
+//   stage 3  partial z^T = Wout[:, u] . h2^T over the wave's 32 units -> LDS    | barrier
+//            z = sum of the 8 partials in a fixed order (identical bits in every wave), then
+//            softmax / CE / argmax per wave; wave 0 counts loss, #correct and dbout
+//   stage 4  dact2^T[u] = Wout^T[u] . dz^T, masked by relu'(h2)      16x16x16, K = classes
+//   stage 5  dWout^T[u] += h2^T . dz over the tile's 32 rows          16x16x32, K = rows: both
+//            operands transposed through a per-wave [32][16] LDS image + ds_read_b64_tr_b16
+constexpr int V2_W = 8, V2_U = 32, V2_RT = 32, V2_H = 256;
+constexpr int V2_HP = V2_H + 8;        // h1 tile pitch (bf16 elements)
+constexpr int V2_SP = 16 + 8;          // transpose image pitch
+constexpr int V2_IMG = V2_RT * V2_SP;  // elements per transpose image
+constexpr size_t V2_LDS = (size_t)2 * V2_RT * V2_HP * 2 + (size_t)V2_W * 2 * 64 * 16 + 2 * 64 * 8 +
+                          (size_t)V2_W * 3 * V2_IMG * 2;
+
+// The value lane ^ 16 / lane ^ 32 holds, by the gfx950 row / half swaps (VALU, no LDS round trip
+// like ds_bpermute).  `self` is the swap's result for the lane's own id: it fixes which of the
+// two outputs carries the partner, independent of the operand order convention.
+struct LaneSwap {
+  bool hi16, hi32;
+  __device__ __forceinline__ explicit LaneSwap(int lane) {
+    const auto a = __builtin_amdgcn_permlane16_swap((uint32_t)lane, (uint32_t)lane, false, false);
+    const auto b = __builtin_amdgcn_permlane32_swap((uint32_t)lane, (uint32_t)lane, false, false);
+    hi16 = a[0] == (uint32_t)(lane ^ 16);
+    hi32 = b[0] == (uint32_t)(lane ^ 32);
+  }
+  __device__ __forceinline__ uint32_t x16(uint32_t v) const {
+    const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+    return hi16 ? r[0] : r[1];
+  }
+  __device__ __forceinline__ uint32_t x32(uint32_t v) const {
+    const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+    return hi32 ? r[0] : r[1];
+  }
+  __device__ __forceinline__ float x16(float v) const { return __uint_as_float(x16(__float_as_uint(v))); }
+  __device__ __forceinline__ float x32(float v) const { return __uint_as_float(x32(__float_as_uint(v))); }
+};
+
+// Copy a [32][V2_HP] LDS tile to rows r0.. of a [B][256] global matrix: two 16-byte vectors per
+// thread, every row one contiguous 512-byte run (row-per-lane dwordx2 stores are issue-bound)
+__device__ __forceinline__ void v2_store_tile(const bf16_t* tile, bf16_t* __restrict__ dst, int r0, int tid) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int v = tid + 512 * i, row = v >> 5, col = (v & 31) * 8;
+    *reinterpret_cast<uint4*>(dst + (size_t)(r0 + row) * V2_H + col) =
+        *reinterpret_cast<const uint4*>(tile + row * V2_HP + col);
+  }
+}
+
+// MFMA operand fragment (8 consecutive k of column lane & 15) of a [k][cols] bf16 LDS image:
+// two transposing 4 x 16 reads per lane
+__device__ __forceinline__ bf16x8_t frag_tr(const bf16_t* img, int pitch, int col0, int lane) {
+  const int li = lane & 15, g = lane >> 4;
+  const bf16_t* p0 = img + (8 * g + (li >> 2)) * pitch + col0 + 4 * (li & 3);
+  const s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)p0);
+  const s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(p0 + 4 * pitch));
+  typedef __attribute__((ext_vector_type(8))) short s16x8_t;
+  const s16x8_t v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8_t, v);
+}
+
+template <int K0, bool INFER, int XF = 0>
+__global__ __launch_bounds__(512) void mlp_fwd_head_v2_kernel(
+    const bf16_t* __restrict__ X, const bf16_t* __restrict__ W0, const float* __restrict__ b0,
+    const bf16_t* __restrict__ W1, const float* __restrict__ b1, const bf16_t* __restrict__ Wo,
+    const float* __restrict__ bo, const int32_t* __restrict__ labels, int B, int C, float scale,
+    bf16_t* __restrict__ h1out, bf16_t* __restrict__ dact, float* __restrict__ slab,
+    float* __restrict__ block_loss, int32_t* __restrict__ block_correct, float* __restrict__ logits_out,
+    int32_t* __restrict__ pred_out, int F, int ldx) {
+  constexpr int H = V2_H, K0C = K0 / 32, KC = H / 32;
+  extern __shared__ __attribute__((aligned(16))) bf16_t lds[];
+  bf16_t* h1s = lds;                                          // [32][V2_HP] h1 tile
+  bf16_t* dts = h1s + V2_RT * V2_HP;                          // [32][V2_HP] dact2 tile (copied out a tile later)
+  float* zs = reinterpret_cast<float*>(dts + V2_RT * V2_HP);  // [8 waves][2 halves][64 lanes][4]
+  uint32_t* dzs = reinterpret_cast<uint32_t*>(zs + V2_W * 2 * 64 * 4);  // [2 halves][64 lanes][2]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int c16 = lane & 15, g = lane >> 4;
+  const int u0 = wave * V2_U;
+  bf16_t* img = reinterpret_cast<bf16_t*>(dzs + 2 * 64 * 2) + wave * 3 * V2_IMG;  // h2 t=0, t=1, dz
+  const LaneSwap swp(lane);
+
+  // ---- this wave's weight slices, in registers for the whole kernel ----
+  bf16x8_t w0f[2][K0C], w1f[2][KC];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+#pragma unroll
+    for (int kc = 0; kc < K0C; ++kc)
+      w0f[t][kc] = *reinterpret_cast<const bf16x8_t*>(W0 + (size_t)(u0 + 16 * t + c16) * K0 + kc * 32 + g * 8);
+#pragma unroll
+    for (int kc = 0; kc < KC; ++kc)
+      w1f[t][kc] = *reinterpret_cast<const bf16x8_t*>(W1 + (size_t)(u0 + 16 * t + c16) * H + kc * 32 + g * 8);
+  }
+  // stage-3 A fragment: Wout[class c16][u0 + 4g + j] (j < 4), [u0 + 16 + 4g + j - 4] (j >= 4) —
+  // the k permutation of the h2 register pairs (see "Operand trick" at the top)
+  const uint2 wlo = *reinterpret_cast<const uint2*>(Wo + (size_t)c16 * H + u0 + 4 * g);
+  const uint2 whi = *reinterpret_cast<const uint2*>(Wo + (size_t)c16 * H + u0 + 16 + 4 * g);
+  const bf16x8_t wo3 = cat8(wlo.x, wlo.y, whi.x, whi.y);
+  // stage-4 A fragments: Wout[class 4g + j][u0 + 16t + c16], j < 4
+  s16x4_t wo4[2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) wo4[t][j] = (short)Wo[(size_t)(4 * g + j) * H + u0 + 16 * t + c16];
+  float4 b0r[2], b1r[2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    b0r[t] = *reinterpret_cast<const float4*>(b0 + u0 + 16 * t + 4 * g);
+    b1r[t] = *reinterpret_cast<const float4*>(b1 + u0 + 16 * t + 4 * g);
+  }
+  float bo_r[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) bo_r[r] = (4 * g + r < C) ? bo[4 * g + r] : 0.f;
+
+  f32x4_t acc5[2] = {f32x4_t{0.f, 0.f, 0.f, 0.f}, f32x4_t{0.f, 0.f, 0.f, 0.f}};
+  float dbo[4] = {0.f, 0.f, 0.f, 0.f};
+  float lsum = 0.f;
+  int ncorr = 0;
+  const int ntiles = B / V2_RT;
+  int T = blockIdx.x;
+  bf16x8_t xb[2][K0C];
+  int y[2] = {0, 0};
+  int prev_r0 = -1;
+  if (T < ntiles) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+#pragma unroll
+      for (int kc = 0; kc < K0C; ++kc) xb[h][kc] = load_x<K0, XF>(X, T * V2_RT + 16 * h + c16, kc, g, F, ldx);
+      if (!INFER) y[h] = labels[T * V2_RT + 16 * h + c16];
+    }
+  }
+  for (; T < ntiles; T += gridDim.x) {
+    const int r0 = T * V2_RT;
+    // ---- stage 1: h1^T = W0 . X^T for this wave's units ----
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        f32x4_t a = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kc = 0; kc < K0C; ++kc) a = mma32(w0f[t][kc], xb[h][kc], a);
+        const uint2 v = make_uint2(pack2(fmaxf(a[0] + b0r[t].x, 0.f), fmaxf(a[1] + b0r[t].y, 0.f)),
+                                   pack2(fmaxf(a[2] + b0r[t].z, 0.f), fmaxf(a[3] + b0r[t].w, 0.f)));
+        *reinterpret_cast<uint2*>(h1s + (16 * h + c16) * V2_HP + u0 + 16 * t + 4 * g) = v;
+      }
+    // prefetch the next tile's X rows and labels (into the registers stage 1 just consumed)
+    const int Tn = T + gridDim.x;
+    const int yc0 = y[0], yc1 = y[1];
+    if (Tn < ntiles) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+#pragma unroll
+        for (int kc = 0; kc < K0C; ++kc) xb[h][kc] = load_x<K0, XF>(X, Tn * V2_RT + 16 * h + c16, kc, g, F, ldx);
+        if (!INFER) y[h] = labels[Tn * V2_RT + 16 * h + c16];
+      }
+    }
+    __syncthreads();  // the h1 tile (and the previous tile's dact2 tile) is complete
+    if (!INFER) {  // coalesced row stores of h1 (this tile) and dact2 (the previous tile)
+      v2_store_tile(h1s, h1out, r0, tid);
+      if (prev_r0 >= 0) v2_store_tile(dts, dact, prev_r0, tid);
+      prev_r0 = r0;
+    }
+    // ---- stage 2: h2^T = W1 . h1^T (4 independent accumulators) ----
+    f32x4_t acc[2][2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int t = 0; t < 2; ++t) acc[h][t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kc = 0; kc < KC; ++kc) {
+      bf16x8_t hb[2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+        hb[h] = *reinterpret_cast<const bf16x8_t*>(h1s + (16 * h + c16) * V2_HP + kc * 32 + 8 * g);
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int t = 0; t < 2; ++t) acc[h][t] = mma32(w1f[t][kc], hb[h], acc[h][t]);
+    }
+    uint32_t h2p[2][2][2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        h2p[h][t][0] = pack2(fmaxf(acc[h][t][0] + b1r[t].x, 0.f), fmaxf(acc[h][t][1] + b1r[t].y, 0.f));
+        h2p[h][t][1] = pack2(fmaxf(acc[h][t][2] + b1r[t].z, 0.f), fmaxf(acc[h][t][3] + b1r[t].w, 0.f));
+      }
+    // ---- stage 3: partial logits over this wave's 32 units ----
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const f32x4_t zp = mma32(wo3, cat8(h2p[h][0][0], h2p[h][0][1], h2p[h][1][0], h2p[h][1][1]),
+                               f32x4_t{0.f, 0.f, 0.f, 0.f});
+      *reinterpret_cast<f32x4_t*>(zs + ((wave * 2 + h) * 64 + lane) * 4) = zp;
+    }
+    __syncthreads();  // every wave's partial logits are in
+    // ---- logits, softmax, CE of half h in wave h < 2 (the other waves only need dz) ----
+    if (wave < 2) {
+      const int h = wave;
+      f32x4_t z = *reinterpret_cast<const f32x4_t*>(zs + (h * 64 + lane) * 4);
+#pragma unroll
+      for (int w = 1; w < V2_W; ++w) z += *reinterpret_cast<const f32x4_t*>(zs + ((w * 2 + h) * 64 + lane) * 4);
+      const int row = r0 + 16 * h + c16;
+      const int yc = h ? yc1 : yc0;
+      float zz[4];
+      float mx = -INFINITY;
+      int amx = 1 << 30;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int cls = 4 * g + r;
+        zz[r] = cls < C ? z[r] + bo_r[r] : -INFINITY;
+        if (zz[r] > mx) { mx = zz[r]; amx = cls; }
+      }
+      {
+        float om = swp.x16(mx);
+        int oa = (int)swp.x16((uint32_t)amx);
+        if (om > mx || (om == mx && oa < amx)) { mx = om; amx = oa; }
+        om = swp.x32(mx);
+        oa = (int)swp.x32((uint32_t)amx);
+        if (om > mx || (om == mx && oa < amx)) { mx = om; amx = oa; }
+      }
+      if constexpr (INFER) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (4 * g + r < C) logits_out[(size_t)row * C + 4 * g + r] = zz[r];
+        if (g == 0) pred_out[row] = amx;
+      } else {
+        float e[4], se = 0.f;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          e[r] = (4 * g + r < C) ? __expf(zz[r] - mx) : 0.f;
+          se += e[r];
+        }
+        se += swp.x16(se);
+        se += swp.x32(se);
+        const float inv = 1.f / se, lse = mx + __logf(se);
+        float dl[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int cls = 4 * g + r;
+          dl[r] = cls < C ? (e[r] * inv - (cls == yc ? 1.f : 0.f)) * scale : 0.f;
+          if (cls == yc) lsum += lse - zz[r];
+        }
+        if (g == 0 && amx == yc) ncorr += 1;
+        const uint32_t dz01 = pack2(dl[0], dl[1]), dz23 = pack2(dl[2], dl[3]);
+        dbo[0] += __uint_as_float(dz01 << 16);
+        dbo[1] += __uint_as_float(dz01 & 0xffff0000u);
+        dbo[2] += __uint_as_float(dz23 << 16);
+        dbo[3] += __uint_as_float(dz23 & 0xffff0000u);
+        *reinterpret_cast<uint2*>(dzs + (h * 64 + lane) * 2) = make_uint2(dz01, dz23);
+      }
+    }
+    if constexpr (INFER) continue;
+    __syncthreads();  // dz of both halves is in
+    uint32_t dz[2][2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const uint2 v = *reinterpret_cast<const uint2*>(dzs + (h * 64 + lane) * 2);
+      dz[h][0] = v.x;
+      dz[h][1] = v.y;
+    }
+    // ---- stage 4: dact2^T = Wout^T . dz^T, masked by relu'(h2) ----
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const s16x4_t dzv = __builtin_bit_cast(s16x4_t, make_uint2(dz[h][0], dz[h][1]));
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const f32x4_t d = mma16(wo4[t], dzv, f32x4_t{0.f, 0.f, 0.f, 0.f});
+        const uint32_t m0 = h2p[h][t][0], m1 = h2p[h][t][1];
+        const float d0 = bf_pos(m0) ? d[0] : 0.f, d1 = bf_pos(m0 >> 16) ? d[1] : 0.f;
+        const float d2 = bf_pos(m1) ? d[2] : 0.f, d3 = bf_pos(m1 >> 16) ? d[3] : 0.f;
+        *reinterpret_cast<uint2*>(dts + (16 * h + c16) * V2_HP + u0 + 16 * t + 4 * g) =
+            make_uint2(pack2(d0, d1), pack2(d2, d3));
+      }
+    }
+    // ---- stage 5: dWout^T += h2^T . dz over the tile's 32 rows (per-wave transposes) ----
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+        *reinterpret_cast<uint2*>(img + t * V2_IMG + (16 * h + c16) * V2_SP + 4 * g) =
+            make_uint2(h2p[h][t][0], h2p[h][t][1]);
+      *reinterpret_cast<uint2*>(img + 2 * V2_IMG + (16 * h + c16) * V2_SP + 4 * g) = make_uint2(dz[h][0], dz[h][1]);
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's images are in LDS
+    __builtin_amdgcn_wave_barrier();
+    const bf16x8_t bz = frag_tr(img + 2 * V2_IMG, V2_SP, 0, lane);
+#pragma unroll
+    for (int t = 0; t < 2; ++t) acc5[t] = mma32(frag_tr(img + t * V2_IMG, V2_SP, 0, lane), bz, acc5[t]);
+  }
+
+  if constexpr (INFER) return;
+  __syncthreads();  // the last tile's dact2 tile is complete
+  if (prev_r0 >= 0) v2_store_tile(dts, dact, prev_r0, tid);
+  // ---- this wave's units of the workgroup slab: dWout rows 0..15 x units, dbout, loss ----
+  float* out = slab + (size_t)blockIdx.x * (NCLS * H + NCLS);
+#pragma unroll
+  for (int t = 0; t < 2; ++t) *reinterpret_cast<f32x4_t*>(out + (size_t)c16 * H + u0 + 16 * t + 4 * g) = acc5[t];
+  float* red = zs;  // waves 0 / 1 (halves 0 / 1): dbout [2][16], loss [2], #correct [2]
+  if (wave < 2) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) dbo[r] += __shfl_xor(dbo[r], o, 64);
+    if (c16 == 0) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) red[wave * NCLS + 4 * g + r] = dbo[r];
+    }
+    lsum = wave_sum(lsum);
+    const float nc = wave_sum((float)ncorr);
+    if (lane == 0) {
+      red[2 * NCLS + wave] = lsum;
+      red[2 * NCLS + 2 + wave] = nc;
+    }
+  }
+  __syncthreads();
+  if (tid < NCLS) out[NCLS * H + tid] = red[tid] + red[NCLS + tid];
+  if (tid == 0) {
+    block_loss[blockIdx.x] = red[2 * NCLS] + red[2 * NCLS + 1];
+    block_correct[blockIdx.x] = (int)(red[2 * NCLS + 2] + red[2 * NCLS + 3]);
+  }
+}
+
+template <int K0, bool INFER = false, int XF = 0>
+int launch_v2(const bf16_t* X, const bf16_t* W0, const float* b0, const bf16_t* W1, const float* b1,
+              const bf16_t* Wo, const float* bo, const int32_t* labels, int B, int C, float scale, bf16_t* h1,
+              bf16_t* dact, float* slab, float* block_loss, int32_t* block_correct, int nwg, hipStream_t s,
+              float* logits = nullptr, int32_t* pred = nullptr, int F = K0, int ldx = K0) {
+  mlp_fwd_head_v2_kernel<K0, INFER, XF><<<nwg, 512, V2_LDS, s>>>(X, W0, b0, W1, b1, Wo, bo, labels, B, C, scale,
+                                                                 h1, dact, slab, block_loss, block_correct, logits,
+                                                                 pred, F, ldx);
+  HAR_CHECK_LAUNCH();
+  return 0;
+}
+
+bool use_v2(int H, int B) {
+  if (H != V2_H || B % V2_RT) return false;
+  const char* e = getenv("HAR_MLP_FUSED_V1");
+  return !(e && e[0] == '1');
+}
+
 }  // namespace
 
 extern "C" int har_mlp_fwd_head_grid(int B) {
-  const int tiles = B / 16;
-  return std::max(1, std::min(256, (tiles + 3) / 4));
+  // persistent: at most one workgroup per CU; a workgroup-tile is 32 rows (v2: two 16-row halves,
+  // v1: two waves' 16-row tiles)
+  return std::max(1, std::min(256, (B / 16 + 1) / 2));
 }
 
 extern "C" int har_mlp_fwd_head(const uint16_t* X, int K0, const uint16_t* W0, const float* b0, const uint16_t* W1,
@@ -387,6 +739,10 @@ extern "C" int har_mlp_fwd_head(const uint16_t* X, int K0, const uint16_t* W0, c
        (uintptr_t)b0 | (uintptr_t)b1 | (uintptr_t)slab) & 15)
     return -3;
   const int nwg = har_mlp_fwd_head_grid(B);
+  if (use_v2(H, B)) {
+    if (K0 == 64) return launch_v2<64>(X, W0, b0, W1, b1, Wo, bo, labels, B, C, scale, h1, dact, slab, block_loss, block_correct, nwg, s);
+    if (K0 == 32) return launch_v2<32>(X, W0, b0, W1, b1, Wo, bo, labels, B, C, scale, h1, dact, slab, block_loss, block_correct, nwg, s);
+  }
   if (H == 256 && K0 == 64) return launch<256, 64>(X, W0, b0, W1, b1, Wo, bo, labels, B, C, scale, h1, dact, slab, block_loss, block_correct, nwg, s);
   if (H == 256 && K0 == 32) return launch<256, 32>(X, W0, b0, W1, b1, Wo, bo, labels, B, C, scale, h1, dact, slab, block_loss, block_correct, nwg, s);
   if (H == 128 && K0 == 64) return launch<128, 64>(X, W0, b0, W1, b1, Wo, bo, labels, B, C, scale, h1, dact, slab, block_loss, block_correct, nwg, s);
@@ -401,6 +757,10 @@ extern "C" int har_mlp_fwd_infer(const uint16_t* X, int K0, const uint16_t* W0, 
   if (((uintptr_t)X | (uintptr_t)W0 | (uintptr_t)W1 | (uintptr_t)Wo | (uintptr_t)b0 | (uintptr_t)b1) & 15) return -3;
   const int nwg = har_mlp_fwd_head_grid(B);
   const bf16_t* x = X;
+  if (use_v2(H, B)) {
+    if (K0 == 64) return launch_v2<64, true>(x, W0, b0, W1, b1, Wo, bo, nullptr, B, C, 1.f, nullptr, nullptr, nullptr, nullptr, nullptr, nwg, s, logits, pred);
+    if (K0 == 32) return launch_v2<32, true>(x, W0, b0, W1, b1, Wo, bo, nullptr, B, C, 1.f, nullptr, nullptr, nullptr, nullptr, nullptr, nwg, s, logits, pred);
+  }
   if (H == 256 && K0 == 64) return launch<256, 64, true>(x, W0, b0, W1, b1, Wo, bo, nullptr, B, C, 1.f, nullptr, nullptr, nullptr, nullptr, nullptr, nwg, s, logits, pred);
   if (H == 256 && K0 == 32) return launch<256, 32, true>(x, W0, b0, W1, b1, Wo, bo, nullptr, B, C, 1.f, nullptr, nullptr, nullptr, nullptr, nullptr, nwg, s, logits, pred);
   if (H == 128 && K0 == 64) return launch<128, 64, true>(x, W0, b0, W1, b1, Wo, bo, nullptr, B, C, 1.f, nullptr, nullptr, nullptr, nullptr, nullptr, nwg, s, logits, pred);
@@ -417,6 +777,10 @@ extern "C" int har_mlp_fwd_infer_f32(const float* X, int ldx, int F, int K0, con
   if (((uintptr_t)W0 | (uintptr_t)W1 | (uintptr_t)Wo | (uintptr_t)b0 | (uintptr_t)b1) & 15) return -3;
   const int nwg = har_mlp_fwd_head_grid(B);
   const bf16_t* x = reinterpret_cast<const bf16_t*>(X);
+  if (use_v2(H, B)) {
+    if (K0 == 64) return launch_v2<64, true, 1>(x, W0, b0, W1, b1, Wo, bo, nullptr, B, C, 1.f, nullptr, nullptr, nullptr, nullptr, nullptr, nwg, s, logits, pred, F, ldx);
+    if (K0 == 32) return launch_v2<32, true, 1>(x, W0, b0, W1, b1, Wo, bo, nullptr, B, C, 1.f, nullptr, nullptr, nullptr, nullptr, nullptr, nwg, s, logits, pred, F, ldx);
+  }
 #define HAR_INFER_F32(HH, KK)                                                                                     \
   if (H == HH && K0 == KK)                                                                                        \
     return launch<HH, KK, true, 1>(x, W0, b0, W1, b1, Wo, bo, nullptr, B, C, 1.f, nullptr, nullptr, nullptr,       \

@@ -295,7 +295,7 @@ def test_column_stats_and_binning(cuda):
     assert torch.equal(b, torch.from_numpy(T.bin_features(X.cpu().numpy(), thr)))
 
 
-@pytest.mark.parametrize("H,F", [(256, 43), (128, 20)])
+@pytest.mark.parametrize("H,F", [(256, 43), (256, 20), (128, 20)])
 def test_mlp_fused_fwd_head_matches_unfused(cuda, H, F):
     """mlp_fused.hip (fwd L1 + fwd L2 + head + dWout/dbout in one kernel) against the unfused
     kernel chain: same h1 / dact2 / reduced gradients / loss up to bf16 summation-order noise."""
@@ -358,3 +358,32 @@ def test_mlp_fused_infer_matches_fp32(cuda, H, F):
     torch.testing.assert_close(lf, logits)
     assert torch.equal(pf, pred)
     torch.testing.assert_close(eng.logits(X), logits)  # logits() takes the fused fp32 path
+
+
+def test_mlp_fused_v2_matches_v1(cuda, monkeypatch):
+    """The 8-wave fused forward (W1 distributed over the waves' registers, H = 256) against the
+    4-wave LDS-resident-W1 kernel on the same batch: same h1, dact2, gradient slabs and loss up
+    to bf16 / summation-order noise (HAR_MLP_FUSED_V1 selects the kernel per launch)."""
+    from har.models.mlp import MLPEngine, pad_input_bf16
+
+    B, H, F = 8192, 256, 43
+    g = torch.Generator(device=cuda).manual_seed(12)
+    X = pad_input_bf16(torch.randn(B, F, device=cuda, generator=g), 64)
+    y = torch.randint(0, 6, (B,), device=cuda, generator=g).to(torch.int32)
+    outs = []
+    for v1 in ("1", "0"):
+        monkeypatch.setenv("HAR_MLP_FUSED_V1", v1)
+        e = MLPEngine([F, H, H, 6], B, cuda, lr=1e-3, seed=5)
+        e.forward_backward_native(X, y, 1.0 / B)
+        e.reduce_grads_native()
+        torch.cuda.synchronize()
+        assert e.last_fused
+        outs.append((e.acts[1].float().clone(), e.dbuf[1][: B * H].float().clone(), e.G.clone(),
+                     e.last_loss_and_correct(), e))
+    (h_a, d_a, g_a, (l_a, c_a), ea), (h_b, d_b, g_b, (l_b, c_b), eb) = outs
+    assert torch.equal(h_a, h_b)  # stage 1 is the same bf16 product in both kernels
+    assert (d_a - d_b).norm() / d_b.norm() < 1e-2
+    for s in ea.layout.segments:
+        ga, gb = ea.layout.view(g_a, s.name), ea.layout.view(g_b, s.name)
+        assert float((ga - gb).norm() / gb.norm().clamp_min(1e-12)) < 1e-2, s.name
+    assert abs(l_a - l_b) / l_b < 1e-4 and abs(c_a - c_b) <= 2
