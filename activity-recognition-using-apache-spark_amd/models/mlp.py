@@ -182,6 +182,14 @@ class MLPEngine:
                 self.fblock_loss = torch.zeros(nwg, dtype=torch.float32, device=dev)
                 self.fblock_correct = torch.zeros(nwg, dtype=torch.int32, device=dev)
             self.last_fused = False
+            # fused layer-1 backward (mlp_fused.hip mlp_bwd_l1): dgrad -> relu' -> dW0 / db0 in one
+            # kernel, dact1 never reaches HBM (H = 256, batch % 32; HAR_MLP_BWD_FUSED=0 keeps the GEMMs)
+            self.bwd_ok = (self.fused_ok and L.hidden[0] == 256
+                           and os.environ.get("HAR_MLP_BWD_FUSED", "1") != "0")
+            if self.bwd_ok:
+                nbw = _native.kernels().mlp_bwd_l1_grid(self.B)
+                self.bslab = torch.zeros(nbw, 256 * L.in_pad + 256, dtype=torch.float32, device=dev)
+            self.last_bwd = False
             # optional: the two backward branches after the fused forward — dW1 (split-K over the
             # batch) and dgrad -> dW0 — are independent, so HAR_MLP_STREAMS=1 runs dW1 on a second
             # HIP stream (fork/join with events; graph-capturable).  Measured on MI355X at batch
@@ -216,6 +224,7 @@ class MLPEngine:
         if self.fused_ok and B % 16 == 0:
             return self._forward_backward_fused(Xb, y32, scale, on_grad, ks, acts)
         self.last_fused = False
+        self.last_bwd = False
         for i in range(nh):
             gemm_bf16(acts[i], self._w(self.Pb, f"W{i}"), acts[i + 1], M=B, N=self.dims[i + 1], K=self.dims[i],
                       layout=0, epi=EPI_BIAS_RELU, bias=self._w(self.P, f"b{i}"),
@@ -289,38 +298,54 @@ class MLPEngine:
             dw1()
             if on_grad is not None:
                 on_grad("W1")
-        gemm_bf16(dact, self._w(self.Pb, "W1"), prev, M=B, N=H, K=H, layout=2, epi=EPI_RELU_GRAD, mask=h1,
-                  tile=dgrad_tile(B, H, H))
-        gemm_bf16(prev, Xb, self._slab("W0"), M=H, N=K0, K=B, layout=3, epi=EPI_F32_SLAB, k_split=ks, ldc=K0,
-                  slab_stride=total, rowsum=self._slab("b0"), slab_stride_rowsum=total, tile=wgrad_tile(H, K0))
+        if self.bwd_ok and B % 32 == 0:  # dact1 stays on chip: dgrad + relu' + dW0 / db0 in one kernel
+            self.bwd_nwg = mod.mlp_bwd_l1_grid(B)
+            mod.mlp_bwd_l1(dact.data_ptr(), h1.data_ptr(), Xb.data_ptr(), K0, self._w(self.Pb, "W1").data_ptr(), H,
+                           B, self.bslab.data_ptr(), s)
+            self.last_bwd = True
+        else:
+            self.last_bwd = False
+            gemm_bf16(dact, self._w(self.Pb, "W1"), prev, M=B, N=H, K=H, layout=2, epi=EPI_RELU_GRAD, mask=h1,
+                      tile=dgrad_tile(B, H, H))
+            gemm_bf16(prev, Xb, self._slab("W0"), M=H, N=K0, K=B, layout=3, epi=EPI_F32_SLAB, k_split=ks, ldc=K0,
+                      slab_stride=total, rowsum=self._slab("b0"), slab_stride_rowsum=total, tile=wgrad_tile(H, K0))
         if on_grad is not None:
             on_grad("W0")
         if self.side is not None:  # join: the W1 slabs (and the next step's h1 / dact2 reuse) are ordered
             main.wait_event(self.ev_join)
 
     def _first_level(self, lo: int, hi: int, tick: bool):
-        """Split-K slabs (and, after a fused step, the fused kernel's dWout/dbout workgroup
-        slabs) -> n_groups partials over [lo, hi) in ONE launch (one grid.z segment per
-        source); optionally ticks the Adam step counter."""
-        mod, st, total = _native.kernels(), _native.stream_ptr(), self.layout.total
-        tk = self.step_count.data_ptr() if tick else 0
-        woff = self.layout.by_name["Wout"].offset
+        """First reduction level of G[lo:hi] into ``n_groups`` partials in ONE launch (one grid.z
+        segment per source region): the split-K GEMM slabs, and after a fused step the fused
+        kernels' per-workgroup slabs (dWout / dbout of the forward kernel, dW0 / db0 of the
+        layer-1 backward kernel); optionally ticks the Adam step counter."""
+        mod, st, L = _native.kernels(), _native.stream_ptr(), self.layout
+        total = L.total
+        regions = []  # (start, end, source pointer at start, #slabs, slab stride) in flat order
+        start = 0
+        if self.last_bwd:
+            w0, b0 = L.by_name["W0"], L.by_name["b0"]
+            bs, ldb = self.bslab.data_ptr(), self.bslab.shape[1]
+            regions.append((w0.offset, w0.offset + w0.numel, bs, self.bwd_nwg, ldb))
+            regions.append((b0.offset, b0.offset + b0.numel, bs + 4 * w0.numel, self.bwd_nwg, ldb))
+            start = L.by_name["W1"].offset
+        end = L.by_name["Wout"].offset if self.last_fused else total
+        regions.append((start, end, self.slabs.data_ptr() + 4 * start, self.active_splits, total))
+        if self.last_fused:
+            H = self.dims[-1]
+            fs, w = self.fslab.data_ptr(), self.fslab.shape[1]
+            wo, bo = L.by_name["Wout"].offset, L.by_name["bout"].offset
+            regions.append((wo, wo + 16 * H, fs, self.fused_nwg, w))
+            regions.append((bo, bo + 16, fs + 4 * 16 * H, self.fused_nwg, w))
         pbase = self.partials.data_ptr()
         segs = []  # (slabs ptr, S, n, lds, dst ptr, ldd)
-        if not self.last_fused or hi <= woff:
-            segs.append((self.slabs.data_ptr() + 4 * lo, self.active_splits, hi - lo, total, pbase + 4 * lo, total))
-        else:
-            if lo < woff:
-                segs.append((self.slabs.data_ptr() + 4 * lo, self.active_splits, woff - lo, total, pbase + 4 * lo,
-                             total))
-            H = self.dims[-1]
-            w = self.fslab.shape[1]
-            segs.append((self.fslab.data_ptr(), self.fused_nwg, 16 * H, w, pbase + 4 * woff, total))
-            segs.append((self.fslab.data_ptr() + 4 * 16 * H, self.fused_nwg, 16, w,
-                         pbase + 4 * self.layout.by_name["bout"].offset, total))
+        for a, b, ptr, S, lds in regions:
+            a2, b2 = max(a, lo), min(b, hi)
+            if a2 < b2:
+                segs.append((ptr + 4 * (a2 - a), S, b2 - a2, lds, pbase + 4 * a2, total))
         cols = list(zip(*segs))
         mod.reduce_slabs_multi(list(cols[0]), list(cols[1]), list(cols[2]), list(cols[3]), list(cols[4]),
-                               list(cols[5]), self.n_groups, tk, st)
+                               list(cols[5]), self.n_groups, self.step_count.data_ptr() if tick else 0, st)
 
     def _reduce_to_partials(self):
         # the first reduction level also ticks the Adam step counter (one launch fewer per step)

@@ -208,6 +208,12 @@ PYBIND11_MODULE(_har_native, m) {
   });
   m.def("head_fused_blocks", &har_head_fused_blocks);
   m.def("mlp_fwd_head_grid", &har_mlp_fwd_head_grid);
+  m.def("mlp_bwd_l1_grid", &har_mlp_bwd_l1_grid);
+  m.def("mlp_bwd_l1", [](u dact2, u h1, u X, int K0, u W1, int H, int B, u slab, u stream) {
+    check(har_mlp_bwd_l1(P<const uint16_t>(dact2), P<const uint16_t>(h1), P<const uint16_t>(X), K0,
+                         P<const uint16_t>(W1), H, B, P<float>(slab), S(stream)),
+          "mlp_bwd_l1");
+  });
   m.def("mlp_fwd_head", [](u X, int K0, u W0, u b0, u W1, u b1, int H, u Wo, u bo, u labels, int B, int C,
                            float scale, u h1, u dact, u slab, u block_loss, u block_correct, u stream) {
     check(har_mlp_fwd_head(P<const uint16_t>(X), K0, P<const uint16_t>(W0), P<const float>(b0),

@@ -64,6 +64,11 @@ int har_mlp_fwd_head(const uint16_t* X, int K0, const uint16_t* W0, const float*
                      int C, float scale, uint16_t* h1, uint16_t* dact, float* slab, float* block_loss,
                      int32_t* block_correct, hipStream_t s);
 int har_mlp_fwd_head_grid(int B);
+// Fused layer-1 backward (H = 256, B % 32 == 0): dact1 = (dact2 . W1) * relu'(h1) reduced in-kernel
+// into per-workgroup slabs [H*K0 | H] of dW0 / db0; grid har_mlp_bwd_l1_grid(B).
+int har_mlp_bwd_l1(const uint16_t* dact2, const uint16_t* h1, const uint16_t* X, int K0, const uint16_t* W1, int H,
+                   int B, float* slab, hipStream_t s);
+int har_mlp_bwd_l1_grid(int B);
 // Serving variant of the same kernel: logits [B][C] fp32 + argmax class [B] int32, nothing else.
 int har_mlp_fwd_infer_f32(const float* X, int ldx, int F, int K0, const uint16_t* W0, const float* b0,
                           const uint16_t* W1, const float* b1, int H, const uint16_t* Wo, const float* bo, int B, int C,

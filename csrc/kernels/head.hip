@@ -183,10 +183,10 @@ __global__ __launch_bounds__(256) void reduce_slabs_grouped_kernel(const float* 
 // first reduction level of the MLP gradient (split-K slabs of W0..b1 + the fused kernel's
 // per-workgroup dWout / dbout slabs) costs one launch instead of three.
 struct ReduceSegs {
-  const float* slabs[4];
-  float* dst[4];
-  int64_t n[4], lds[4], ldd[4];
-  int S[4];
+  const float* slabs[6];
+  float* dst[6];
+  int64_t n[6], lds[6], ldd[6];
+  int S[6];
 };
 
 __global__ __launch_bounds__(256) void reduce_slabs_multi_kernel(ReduceSegs sg, int G, int32_t* __restrict__ tick) {
@@ -224,7 +224,7 @@ __global__ __launch_bounds__(256) void reduce_slabs_multi_kernel(ReduceSegs sg, 
 extern "C" int har_reduce_slabs_multi(int nseg, const float* const* slabs, const int* S, const int64_t* n,
                                       const int64_t* lds, float* const* dst, const int64_t* ldd, int G, int32_t* tick,
                                       hipStream_t s) {
-  if (nseg <= 0 || nseg > 4 || G <= 0) return -2;
+  if (nseg <= 0 || nseg > 6 || G <= 0) return -2;
   ReduceSegs sg{};
   int64_t n4max = 1;
   for (int z = 0; z < nseg; ++z) {

@@ -716,6 +716,143 @@ int launch_v2(const bf16_t* X, const bf16_t* W0, const float* b0, const bf16_t* 
   return 0;
 }
 
+// ---------------------------------------------------------------------------------------------
+// Layer-1 backward in one kernel (H = 256, batch a multiple of 32):
+//   dact1 = (dact2 . W1) * relu'(h1),   dW0 = dact1^T . X,   db0 = sum_rows dact1
+// dact1 never reaches HBM (the unfused chain writes it and reads it back: 2 x 32 MB at batch
+// 65536).  Same split as v2: 8 waves, wave w owns h1 units [32w, 32w + 32); the W1 columns it
+// contracts with (W1[:, u]) stay in registers (64 VGPRs/lane).  Per 32-row tile the dact2 rows
+// and X rows are staged once in LDS (register-staged prefetch of the next tile under this
+// tile's MFMAs); dact1 is masked in registers, transposed through a per-wave [32][16] image and
+// fed to the dW0 MFMAs (K = rows).  Each workgroup leaves one deterministic [H*K0 | H] slab.
+constexpr int B1_DP = V2_H + 8;  // dact2 tile pitch
+
+template <int K0>
+__global__ __launch_bounds__(512) void mlp_bwd_l1_kernel(const bf16_t* __restrict__ dact2,
+                                                        const bf16_t* __restrict__ h1,
+                                                        const bf16_t* __restrict__ X,
+                                                        const bf16_t* __restrict__ W1, int B,
+                                                        float* __restrict__ slab) {
+  constexpr int H = V2_H, KC = H / 32, NF = K0 / 16, XP = K0 + 8;
+  constexpr int DV = V2_RT * H / 8 / 512;  // 16-byte vectors of a dact2 tile per thread (2)
+  constexpr int XV = V2_RT * K0 / 8;       // 16-byte vectors of an X tile (256 / 128)
+  extern __shared__ __attribute__((aligned(16))) bf16_t lds[];
+  bf16_t* dsm = lds;                        // [32][B1_DP]
+  bf16_t* xsm = dsm + V2_RT * B1_DP;        // [32][XP]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int c16 = lane & 15, g = lane >> 4;
+  const int u0 = wave * V2_U;
+  bf16_t* img = xsm + V2_RT * XP + wave * 2 * V2_IMG;  // dact1 units t = 0, 1
+
+  // A fragments of dact1^T = W1^T . dact2^T: A[i][k = j] = W1[j][i], i = u0 + 16t + c16
+  bf16x8_t w1t[2][KC];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int kc = 0; kc < KC; ++kc) {
+      typedef __attribute__((ext_vector_type(8))) short s16x8_t;
+      s16x8_t v;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = (short)W1[(size_t)(kc * 32 + 8 * g + j) * H + u0 + 16 * t + c16];
+      w1t[t][kc] = __builtin_bit_cast(bf16x8_t, v);
+    }
+  f32x4_t acc0[2][NF];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int f = 0; f < NF; ++f) acc0[t][f] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  float rs[2][4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+
+  const int ntiles = B / V2_RT;
+  // dact2 / X tiles are contiguous [32][H] / [32][K0] row blocks: register-staged 16-byte loads
+  uint4 pd0 = make_uint4(0, 0, 0, 0), pd1 = pd0, px = pd0;
+  static_assert(DV == 2, "two dact2 vectors per thread");
+  int T = blockIdx.x;
+#define HAR_BWD_L1_LOAD(tt)                                                                            \
+  {                                                                                                    \
+    const bf16_t* d_ = dact2 + (size_t)(tt) * V2_RT * H;                                               \
+    pd0 = *reinterpret_cast<const uint4*>(d_ + (size_t)tid * 8);                                       \
+    pd1 = *reinterpret_cast<const uint4*>(d_ + (size_t)(tid + 512) * 8);                               \
+    if (tid < XV) px = *reinterpret_cast<const uint4*>(X + (size_t)(tt) * V2_RT * K0 + (size_t)tid * 8); \
+  }
+  if (T < ntiles) HAR_BWD_L1_LOAD(T)
+  for (; T < ntiles; T += gridDim.x) {
+    const int r0 = T * V2_RT;
+    __syncthreads();  // the previous tile's LDS reads are done
+    *reinterpret_cast<uint4*>(dsm + (tid / (H / 8)) * B1_DP + (tid % (H / 8)) * 8) = pd0;
+    *reinterpret_cast<uint4*>(dsm + ((tid + 512) / (H / 8)) * B1_DP + ((tid + 512) % (H / 8)) * 8) = pd1;
+    if (tid < XV) *reinterpret_cast<uint4*>(xsm + (tid / (K0 / 8)) * XP + (tid % (K0 / 8)) * 8) = px;
+    // relu'(h1) words of this lane's (row, unit) pairs
+    uint2 mk[2][2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+        mk[h][t] = *reinterpret_cast<const uint2*>(h1 + (size_t)(r0 + 16 * h + c16) * H + u0 + 16 * t + 4 * g);
+    __syncthreads();  // the tiles are in LDS
+    if (T + gridDim.x < ntiles) HAR_BWD_L1_LOAD(T + gridDim.x)
+    // ---- dact1^T = W1^T . dact2^T for this wave's units ----
+    f32x4_t a[2][2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int t = 0; t < 2; ++t) a[h][t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kc = 0; kc < KC; ++kc) {
+      bf16x8_t b[2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+        b[h] = *reinterpret_cast<const bf16x8_t*>(dsm + (16 * h + c16) * B1_DP + kc * 32 + 8 * g);
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int t = 0; t < 2; ++t) a[h][t] = mma32(w1t[t][kc], b[h], a[h][t]);
+    }
+    // ---- relu' mask, bf16, db0 row sums, transposed image for dW0 ----
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const uint32_t m0 = mk[h][t].x, m1 = mk[h][t].y;
+        const float d0 = bf_pos(m0) ? a[h][t][0] : 0.f, d1 = bf_pos(m0 >> 16) ? a[h][t][1] : 0.f;
+        const float d2 = bf_pos(m1) ? a[h][t][2] : 0.f, d3 = bf_pos(m1 >> 16) ? a[h][t][3] : 0.f;
+        const uint32_t p0 = pack2(d0, d1), p1 = pack2(d2, d3);
+        rs[t][0] += __uint_as_float(p0 << 16);
+        rs[t][1] += __uint_as_float(p0 & 0xffff0000u);
+        rs[t][2] += __uint_as_float(p1 << 16);
+        rs[t][3] += __uint_as_float(p1 & 0xffff0000u);
+        *reinterpret_cast<uint2*>(img + t * V2_IMG + (16 * h + c16) * V2_SP + 4 * g) = make_uint2(p0, p1);
+      }
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's images are in LDS
+    __builtin_amdgcn_wave_barrier();
+    // ---- dW0 += dact1^T . X over the tile's 32 rows ----
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const bf16x8_t A = frag_tr(img + t * V2_IMG, V2_SP, 0, lane);
+#pragma unroll
+      for (int f = 0; f < NF; ++f) acc0[t][f] = mma32(A, frag_tr(xsm, XP, 16 * f, lane), acc0[t][f]);
+    }
+  }
+#undef HAR_BWD_L1_LOAD
+  // ---- this wave's rows of the workgroup slab: dW0 [H][K0], db0 [H] ----
+  float* out = slab + (size_t)blockIdx.x * (H * K0 + H);
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int f = 0; f < NF; ++f)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) out[(size_t)(u0 + 16 * t + 4 * g + r) * K0 + 16 * f + c16] = acc0[t][f][r];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float v = rs[t][r];
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) v += __shfl_xor(v, o, 64);
+      if (c16 == 0) out[H * K0 + u0 + 16 * t + 4 * g + r] = v;
+    }
+}
+
 bool use_v2(int H, int B) {
   if (H != V2_H || B % V2_RT) return false;
   const char* e = getenv("HAR_MLP_FUSED_V1");
@@ -788,4 +925,19 @@ extern "C" int har_mlp_fwd_infer_f32(const float* X, int ldx, int F, int K0, con
   HAR_INFER_F32(256, 64) HAR_INFER_F32(256, 32) HAR_INFER_F32(128, 64) HAR_INFER_F32(128, 32)
 #undef HAR_INFER_F32
   return -4;
+}
+
+extern "C" int har_mlp_bwd_l1_grid(int B) { return std::max(1, std::min(256, B / V2_RT)); }
+
+// dact1 = (dact2 . W1) * relu'(h1) -> per-workgroup slabs [H*K0 | H] of dW0 / db0 (H = 256).
+extern "C" int har_mlp_bwd_l1(const uint16_t* dact2, const uint16_t* h1, const uint16_t* X, int K0,
+                              const uint16_t* W1, int H, int B, float* slab, hipStream_t s) {
+  if (H != V2_H || B <= 0 || B % V2_RT || (K0 != 32 && K0 != 64)) return -2;
+  if (((uintptr_t)dact2 | (uintptr_t)h1 | (uintptr_t)X | (uintptr_t)W1 | (uintptr_t)slab) & 15) return -3;
+  const int nwg = har_mlp_bwd_l1_grid(B);
+  const size_t lds = ((size_t)V2_RT * B1_DP + (size_t)V2_RT * (K0 + 8) + (size_t)V2_W * 2 * V2_IMG) * sizeof(bf16_t);
+  if (K0 == 64) mlp_bwd_l1_kernel<64><<<nwg, 512, lds, s>>>(dact2, h1, X, W1, B, slab);
+  else mlp_bwd_l1_kernel<32><<<nwg, 512, lds, s>>>(dact2, h1, X, W1, B, slab);
+  HAR_CHECK_LAUNCH();
+  return 0;
 }

@@ -387,3 +387,30 @@ def test_mlp_fused_v2_matches_v1(cuda, monkeypatch):
         ga, gb = ea.layout.view(g_a, s.name), ea.layout.view(g_b, s.name)
         assert float((ga - gb).norm() / gb.norm().clamp_min(1e-12)) < 1e-2, s.name
     assert abs(l_a - l_b) / l_b < 1e-4 and abs(c_a - c_b) <= 2
+
+
+@pytest.mark.parametrize("F", [43, 20])
+def test_mlp_bwd_l1_matches_gemms(cuda, monkeypatch, F):
+    """Fused layer-1 backward (dgrad + relu' + dW0 / db0 in one kernel, dact1 on chip) against
+    the dgrad GEMM + split-K weight-gradient GEMM pair on the same fused-forward outputs."""
+    from har.models.mlp import MLPEngine, pad_input_bf16
+
+    B, H = 8192, 256
+    g = torch.Generator(device=cuda).manual_seed(13)
+    X = torch.randn(B, F, device=cuda, generator=g)
+    y = torch.randint(0, 6, (B,), device=cuda, generator=g).to(torch.int32)
+    Gs = []
+    for flag in ("0", "1"):
+        monkeypatch.setenv("HAR_MLP_BWD_FUSED", flag)
+        e = MLPEngine([F, H, H, 6], B, cuda, lr=1e-3, seed=7)
+        Xb = pad_input_bf16(X, e.layout.in_pad)
+        e.forward_backward_native(Xb, y, 1.0 / B)
+        e.reduce_grads_native()
+        torch.cuda.synchronize()
+        assert e.last_bwd == (flag == "1")
+        Gs.append((e.G.clone(), e.layout))
+    (ga, L), (gb, _) = Gs
+    for s in L.segments:
+        a, b = L.view(ga, s.name), L.view(gb, s.name)
+        rel = float((a - b).norm() / b.norm().clamp_min(1e-12))
+        assert rel < 1e-2, f"{s.name}: {rel:.3e}"
