@@ -774,7 +774,13 @@ __global__ __launch_bounds__(512) void mlp_bwd_l1_kernel(const bf16_t* __restric
     pd0 = *reinterpret_cast<const uint4*>(d_ + (size_t)tid * 8);                                       \
     pd1 = *reinterpret_cast<const uint4*>(d_ + (size_t)(tid + 512) * 8);                               \
     if (tid < XV) px = *reinterpret_cast<const uint4*>(X + (size_t)(tt) * V2_RT * K0 + (size_t)tid * 8); \
+    for (int h_ = 0; h_ < 2; ++h_)                                                                     \
+      for (int t_ = 0; t_ < 2; ++t_)                                                                   \
+        mk[h_][t_] = *reinterpret_cast<const uint2*>(h1 + (size_t)((tt) * V2_RT + 16 * h_ + c16) * H + \
+                                                     u0 + 16 * t_ + 4 * g);                            \
   }
+  // relu'(h1) words of this lane's (row, unit) pairs, prefetched a tile ahead with the tiles
+  uint2 mk[2][2] = {{make_uint2(0, 0), make_uint2(0, 0)}, {make_uint2(0, 0), make_uint2(0, 0)}};
   if (T < ntiles) HAR_BWD_L1_LOAD(T)
   for (; T < ntiles; T += gridDim.x) {
     const int r0 = T * V2_RT;
@@ -782,13 +788,7 @@ __global__ __launch_bounds__(512) void mlp_bwd_l1_kernel(const bf16_t* __restric
     *reinterpret_cast<uint4*>(dsm + (tid / (H / 8)) * B1_DP + (tid % (H / 8)) * 8) = pd0;
     *reinterpret_cast<uint4*>(dsm + ((tid + 512) / (H / 8)) * B1_DP + ((tid + 512) % (H / 8)) * 8) = pd1;
     if (tid < XV) *reinterpret_cast<uint4*>(xsm + (tid / (K0 / 8)) * XP + (tid % (K0 / 8)) * 8) = px;
-    // relu'(h1) words of this lane's (row, unit) pairs
-    uint2 mk[2][2];
-#pragma unroll
-    for (int h = 0; h < 2; ++h)
-#pragma unroll
-      for (int t = 0; t < 2; ++t)
-        mk[h][t] = *reinterpret_cast<const uint2*>(h1 + (size_t)(r0 + 16 * h + c16) * H + u0 + 16 * t + 4 * g);
+    const uint2 mc[2][2] = {{mk[0][0], mk[0][1]}, {mk[1][0], mk[1][1]}};
     __syncthreads();  // the tiles are in LDS
     if (T + gridDim.x < ntiles) HAR_BWD_L1_LOAD(T + gridDim.x)
     // ---- dact1^T = W1^T . dact2^T for this wave's units ----
@@ -813,7 +813,7 @@ __global__ __launch_bounds__(512) void mlp_bwd_l1_kernel(const bf16_t* __restric
     for (int h = 0; h < 2; ++h)
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
-        const uint32_t m0 = mk[h][t].x, m1 = mk[h][t].y;
+        const uint32_t m0 = mc[h][t].x, m1 = mc[h][t].y;
         const float d0 = bf_pos(m0) ? a[h][t][0] : 0.f, d1 = bf_pos(m0 >> 16) ? a[h][t][1] : 0.f;
         const float d2 = bf_pos(m1) ? a[h][t][2] : 0.f, d3 = bf_pos(m1 >> 16) ? a[h][t][3] : 0.f;
         const uint32_t p0 = pack2(d0, d1), p1 = pack2(d2, d3);
