@@ -432,6 +432,19 @@ __device__ __forceinline__ void v2_store_tile(const bf16_t* tile, bf16_t* __rest
   }
 }
 
+typedef __attribute__((ext_vector_type(2))) short s16x2_t;
+typedef __attribute__((ext_vector_type(2))) unsigned short u16x2_t;
+// relu of two packed bf16 (sign bit set = negative, -0 -> +0): one v_pk_max_i16
+__device__ __forceinline__ uint32_t relu2(uint32_t p) {
+  return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(s16x2_t, p), s16x2_t{0, 0}));
+}
+// d where the packed activation m (relu2 output: never negative) is nonzero, else 0, per half:
+// v_pk_min_u16 -> {0, 1}, v_pk_mul_lo_u16
+__device__ __forceinline__ uint32_t mask2(uint32_t d, uint32_t m) {
+  const u16x2_t nz = __builtin_elementwise_min(__builtin_bit_cast(u16x2_t, m), u16x2_t{1, 1});
+  return __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2_t, d) * nz);
+}
+
 // MFMA operand fragment (8 consecutive k of column lane & 15) of a [k][cols] bf16 LDS image:
 // two transposing 4 x 16 reads per lane
 __device__ __forceinline__ bf16x8_t frag_tr(const bf16_t* img, int pitch, int col0, int lane) {
@@ -520,11 +533,10 @@ __global__ __launch_bounds__(512) void mlp_fwd_head_v2_kernel(
     for (int h = 0; h < 2; ++h)
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
-        f32x4_t a = {0.f, 0.f, 0.f, 0.f};
+        f32x4_t a = {b0r[t].x, b0r[t].y, b0r[t].z, b0r[t].w};  // bias as the initial accumulator
 #pragma unroll
         for (int kc = 0; kc < K0C; ++kc) a = mma32(w0f[t][kc], xb[h][kc], a);
-        const uint2 v = make_uint2(pack2(fmaxf(a[0] + b0r[t].x, 0.f), fmaxf(a[1] + b0r[t].y, 0.f)),
-                                   pack2(fmaxf(a[2] + b0r[t].z, 0.f), fmaxf(a[3] + b0r[t].w, 0.f)));
+        const uint2 v = make_uint2(relu2(pack2(a[0], a[1])), relu2(pack2(a[2], a[3])));
         *reinterpret_cast<uint2*>(h1s + (16 * h + c16) * V2_HP + u0 + 16 * t + 4 * g) = v;
       }
     // prefetch the next tile's X rows and labels (into the registers stage 1 just consumed)
@@ -549,7 +561,7 @@ __global__ __launch_bounds__(512) void mlp_fwd_head_v2_kernel(
 #pragma unroll
     for (int h = 0; h < 2; ++h)
 #pragma unroll
-      for (int t = 0; t < 2; ++t) acc[h][t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+      for (int t = 0; t < 2; ++t) acc[h][t] = f32x4_t{b1r[t].x, b1r[t].y, b1r[t].z, b1r[t].w};
 #pragma unroll
     for (int kc = 0; kc < KC; ++kc) {
       bf16x8_t hb[2];
@@ -566,8 +578,8 @@ __global__ __launch_bounds__(512) void mlp_fwd_head_v2_kernel(
     for (int h = 0; h < 2; ++h)
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
-        h2p[h][t][0] = pack2(fmaxf(acc[h][t][0] + b1r[t].x, 0.f), fmaxf(acc[h][t][1] + b1r[t].y, 0.f));
-        h2p[h][t][1] = pack2(fmaxf(acc[h][t][2] + b1r[t].z, 0.f), fmaxf(acc[h][t][3] + b1r[t].w, 0.f));
+        h2p[h][t][0] = relu2(pack2(acc[h][t][0], acc[h][t][1]));
+        h2p[h][t][1] = relu2(pack2(acc[h][t][2], acc[h][t][3]));
       }
     // ---- stage 3: partial logits over this wave's 32 units ----
 #pragma unroll
@@ -649,11 +661,8 @@ __global__ __launch_bounds__(512) void mlp_fwd_head_v2_kernel(
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
         const f32x4_t d = mma16(wo4[t], dzv, f32x4_t{0.f, 0.f, 0.f, 0.f});
-        const uint32_t m0 = h2p[h][t][0], m1 = h2p[h][t][1];
-        const float d0 = bf_pos(m0) ? d[0] : 0.f, d1 = bf_pos(m0 >> 16) ? d[1] : 0.f;
-        const float d2 = bf_pos(m1) ? d[2] : 0.f, d3 = bf_pos(m1 >> 16) ? d[3] : 0.f;
         *reinterpret_cast<uint2*>(dts + (16 * h + c16) * V2_HP + u0 + 16 * t + 4 * g) =
-            make_uint2(pack2(d0, d1), pack2(d2, d3));
+            make_uint2(mask2(pack2(d[0], d[1]), h2p[h][t][0]), mask2(pack2(d[2], d[3]), h2p[h][t][1]));
       }
     }
     // ---- stage 5: dWout^T += h2^T . dz over the tile's 32 rows (per-wave transposes) ----
