@@ -374,8 +374,8 @@ int launch(const bf16_t* X, const bf16_t* W0, const float* b0, const bf16_t* W1,
 }
 
 // ---------------------------------------------------------------------------------------------
-// v2 (H = 256, batch a multiple of 32; the default for those shapes, HAR_MLP_FUSED_V1=1 keeps
-// v1): 8 waves per workgroup; wave w owns hidden units [32w, 32w + 32) of BOTH hidden layers,
+// v2 (training step; H = 256, batch a multiple of 32; the default for those shapes,
+// HAR_MLP_FUSED_V1=1 keeps v1): 8 waves per workgroup; wave w owns hidden units [32w, 32w + 32) of BOTH hidden layers,
 // so its slices of W0, W1 (64 VGPRs per lane) and Wout stay in registers and the LDS holds only
 // per-tile data — the 32-row h1 tile (written by all 8 waves, read by all), the partial logits
 // and the stage-5 transpose images (~69 KB).  At <= 256 registers per lane two waves share each
@@ -862,6 +862,9 @@ __global__ __launch_bounds__(512) void mlp_bwd_l1_kernel(const bf16_t* __restric
     }
 }
 
+// Training only: serving (stages 1-3) keeps v1 — without the backward stages, v2's two barriers
+// and partial-logit exchange per tile cost more than its occupancy gains (batch 1M: 0.67 vs
+// 0.43 ms on MI355X).
 bool use_v2(int H, int B) {
   if (H != V2_H || B % V2_RT) return false;
   const char* e = getenv("HAR_MLP_FUSED_V1");
@@ -903,10 +906,6 @@ extern "C" int har_mlp_fwd_infer(const uint16_t* X, int K0, const uint16_t* W0, 
   if (((uintptr_t)X | (uintptr_t)W0 | (uintptr_t)W1 | (uintptr_t)Wo | (uintptr_t)b0 | (uintptr_t)b1) & 15) return -3;
   const int nwg = har_mlp_fwd_head_grid(B);
   const bf16_t* x = X;
-  if (use_v2(H, B)) {
-    if (K0 == 64) return launch_v2<64, true>(x, W0, b0, W1, b1, Wo, bo, nullptr, B, C, 1.f, nullptr, nullptr, nullptr, nullptr, nullptr, nwg, s, logits, pred);
-    if (K0 == 32) return launch_v2<32, true>(x, W0, b0, W1, b1, Wo, bo, nullptr, B, C, 1.f, nullptr, nullptr, nullptr, nullptr, nullptr, nwg, s, logits, pred);
-  }
   if (H == 256 && K0 == 64) return launch<256, 64, true>(x, W0, b0, W1, b1, Wo, bo, nullptr, B, C, 1.f, nullptr, nullptr, nullptr, nullptr, nullptr, nwg, s, logits, pred);
   if (H == 256 && K0 == 32) return launch<256, 32, true>(x, W0, b0, W1, b1, Wo, bo, nullptr, B, C, 1.f, nullptr, nullptr, nullptr, nullptr, nullptr, nwg, s, logits, pred);
   if (H == 128 && K0 == 64) return launch<128, 64, true>(x, W0, b0, W1, b1, Wo, bo, nullptr, B, C, 1.f, nullptr, nullptr, nullptr, nullptr, nullptr, nwg, s, logits, pred);
@@ -923,10 +922,6 @@ extern "C" int har_mlp_fwd_infer_f32(const float* X, int ldx, int F, int K0, con
   if (((uintptr_t)W0 | (uintptr_t)W1 | (uintptr_t)Wo | (uintptr_t)b0 | (uintptr_t)b1) & 15) return -3;
   const int nwg = har_mlp_fwd_head_grid(B);
   const bf16_t* x = reinterpret_cast<const bf16_t*>(X);
-  if (use_v2(H, B)) {
-    if (K0 == 64) return launch_v2<64, true, 1>(x, W0, b0, W1, b1, Wo, bo, nullptr, B, C, 1.f, nullptr, nullptr, nullptr, nullptr, nullptr, nwg, s, logits, pred, F, ldx);
-    if (K0 == 32) return launch_v2<32, true, 1>(x, W0, b0, W1, b1, Wo, bo, nullptr, B, C, 1.f, nullptr, nullptr, nullptr, nullptr, nullptr, nwg, s, logits, pred, F, ldx);
-  }
 #define HAR_INFER_F32(HH, KK)                                                                                     \
   if (H == HH && K0 == KK)                                                                                        \
     return launch<HH, KK, true, 1>(x, W0, b0, W1, b1, Wo, bo, nullptr, B, C, 1.f, nullptr, nullptr, nullptr,       \
