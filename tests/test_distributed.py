@@ -184,3 +184,26 @@ def test_tree_parallel_forest_equals_single(world):
     thr = T.find_thresholds(X.numpy(), 32)
     single = RandomForestClassifier(numTrees=7, maxDepth=4, seed=5).fit_tensors(X, y, 4, thresholds=thr)
     torch.testing.assert_close(outs[0], single.predict_raw(X))
+
+
+@pytest.mark.parametrize("config,extra", [("mlp", ["--batch", "512"]), ("rf", ["--rows", "3000", "--trees", "3"])])
+def test_bench_contract_torchrun(config, extra):
+    """The driver's N>1 launch (``torch.distributed.run ... bench.py --gpus N``) on 2 gloo ranks:
+    exactly one JSON line (rank 0), whole-job aggregate value, dp2 config."""
+    import json
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(root, "bench.py"),
+           "--gpus", "2", "--steps", "2", "--warmup", "1", "--config", config] + extra
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=root,
+                       env=dict(os.environ, OMP_NUM_THREADS="1"))
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == 2 and rec["config"]["parallelism"] == "dp2" and rec["value"] > 0
+    if config == "mlp":  # value = whole-job windows per second = global batch / step time
+        assert abs(rec["value"] - rec["config"]["global_batch"] / (rec["ms_per_step"] * 1e-3)) <= 1e-6 * rec["value"]
