@@ -28,6 +28,7 @@ per-rank histograms are all-reduced before split selection.
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass
 from typing import List, Optional
 
@@ -297,6 +298,9 @@ class ForestBuilder:
         return ForestArrays(feature, thresh, left, right, stats, n_nodes, D, gains)
 
 
+GROUP_MAX_NT = 4096  # tree_level.hip: per-tree candidates a level grouping keeps in LDS
+
+
 class _Pinned:
     """Reusable page-locked staging buffer for the per-level host -> device uploads: an
     upload from pageable memory synchronizes the stream, so every level would stall
@@ -341,6 +345,10 @@ def _levels_native_impl(b: "ForestBuilder", y32, W, N: int, F: int, m: int, maxn
     pin_a, pin_b = _Pinned(8 * Tn), _Pinned(8 * Tn)  # one per upload site (see _Pinned)
     Wf = W.reshape(-1).contiguous()
     ar_n = None
+    # HAR_TREE_LEVEL_SORT=1 keeps the radix-sort grouping (A/B and oracle for the counting sort)
+    use_group = os.environ.get("HAR_TREE_LEVEL_SORT", "0") != "1"
+    nch = mod.tree_level_group_chunks(N)
+    rows_buf = roww_buf = cnt_ws = None
     bins_rm = b.bins.t().contiguous()  # [N, F] for the histogram gathers (partition keeps [F, N])
 
     def candidacy(c: torch.Tensor):
@@ -359,19 +367,39 @@ def _levels_native_impl(b: "ForestBuilder", y32, W, N: int, F: int, m: int, maxn
         A = len(ct)
         if A == 0:
             break
-        ct_d, cn_d, tr_d = pin_a.upload([ct, cn, ct + b.tree_offset], dev)
+        per_tree = np.bincount(ct, minlength=Tn)
+        grouped = use_group and int(per_tree.max()) <= GROUP_MAX_NT and bool(np.all(ct[1:] >= ct[:-1]))
+        tree_lo = np.concatenate([[0], np.cumsum(per_tree)]) if grouped else np.zeros(0, dtype=np.int64)
+        ct_d, cn_d, tr_d, lo_d = pin_a.upload([ct, cn, ct + b.tree_offset, tree_lo], dev)
         cand_idx = torch.full((Tn, maxn), -1, dtype=torch.int32, device=dev)
         cand_idx[ct_d, cn_d] = torch.arange(A, dtype=torch.int32, device=dev)
-        key = torch.empty(Tn * N, dtype=torch.int32, device=dev)
-        mod.tree_level_keys(node_of.data_ptr(), cand_idx.data_ptr(), Tn, N, maxn, key.data_ptr(), st_ptr)
-        keys, order = torch.sort(key, stable=True)
-        rows = (order % N).to(torch.int32)
-        row_w = Wf[order]
-        if ar_n is None or ar_n.numel() < A + 1:
-            ar_n = torch.arange(max(A + 1, 2 * Tn), dtype=torch.int32, device=dev)
-        bounds = torch.searchsorted(keys, ar_n[:A + 1])
-        counts = (bounds[1:] - bounds[:-1]).to(torch.int32)
-        starts = bounds[:-1].to(torch.int32)
+        if grouped:
+            # stable counting-sort grouping by candidate (tree_level.hip): same order as the sort
+            # below, but only the active rows are written and no key array reaches HBM
+            if rows_buf is None:
+                rows_buf = torch.empty(Tn * N, dtype=torch.int32, device=dev)
+                roww_buf = torch.empty(Tn * N, dtype=torch.float32, device=dev)
+            if cnt_ws is None or cnt_ws.numel() < nch * A:
+                cnt_ws = torch.empty(nch * max(A, 2 * Tn), dtype=torch.int32, device=dev)
+            counts = torch.empty(A, dtype=torch.int32, device=dev)
+            starts = torch.empty(A, dtype=torch.int32, device=dev)
+            lo32 = lo_d.to(torch.int32)
+            mod.tree_level_group(node_of.data_ptr(), cand_idx.data_ptr(), lo32.data_ptr(),
+                                 Wf.data_ptr(), Tn, N, maxn, A, int(per_tree.max()), cnt_ws.data_ptr(),
+                                 counts.data_ptr(), starts.data_ptr(), rows_buf.data_ptr(), roww_buf.data_ptr(),
+                                 st_ptr)
+            rows, row_w = rows_buf, roww_buf
+        else:
+            key = torch.empty(Tn * N, dtype=torch.int32, device=dev)
+            mod.tree_level_keys(node_of.data_ptr(), cand_idx.data_ptr(), Tn, N, maxn, key.data_ptr(), st_ptr)
+            keys, order = torch.sort(key, stable=True)
+            rows = (order % N).to(torch.int32)
+            row_w = Wf[order]
+            if ar_n is None or ar_n.numel() < A + 1:
+                ar_n = torch.arange(max(A + 1, 2 * Tn), dtype=torch.int32, device=dev)
+            bounds = torch.searchsorted(keys, ar_n[:A + 1])
+            counts = (bounds[1:] - bounds[:-1]).to(torch.int32)
+            starts = bounds[:-1].to(torch.int32)
         if m >= F:
             feats = torch.arange(F, dtype=torch.int32, device=dev).repeat(A, 1)
         else:

@@ -276,6 +276,14 @@ PYBIND11_MODULE(_har_native, m) {
                               S(stream)),
           "tree_level_keys");
   });
+  m.def("tree_level_group", [](u node_of, u cand_idx, u tree_lo, u W, int T, int64_t N, int maxn, int A, int nt_max,
+                               u cnt_ws, u counts, u starts, u rows, u row_w, u stream) {
+    check(har_tree_level_group(P<const int32_t>(node_of), P<const int32_t>(cand_idx), P<const int32_t>(tree_lo),
+                               P<const float>(W), T, N, maxn, A, nt_max, P<int32_t>(cnt_ws), P<int32_t>(counts),
+                               P<int32_t>(starts), P<int32_t>(rows), P<float>(row_w), S(stream)),
+          "tree_level_group");
+  });
+  m.def("tree_level_group_chunks", [](int64_t N) { return har_tree_level_group_chunks(N); });
   m.def("tree_partition", [](u node_of, u lvl_feat, u lvl_bin, u lvl_left, u bins, int T, int64_t N, int maxn,
                              u stream) {
     check(har_tree_partition(P<int32_t>(node_of), P<const int32_t>(lvl_feat), P<const int32_t>(lvl_bin),

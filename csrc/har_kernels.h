@@ -147,6 +147,12 @@ int har_tree_feature_subsets(uint64_t seed, const int32_t* trees, const int32_t*
                              int32_t* out, hipStream_t s);
 int har_tree_level_keys(const int32_t* node_of, const int32_t* cand_idx, int T, int64_t N, int maxn, int32_t* key,
                         hipStream_t s);
+// Stable grouping of the level's (tree, row) pairs by candidate node (no sort); cnt_ws holds
+// har_tree_level_group_chunks(N) x A ints.  -4: a tree has more than 4096 candidates.
+int har_tree_level_group(const int32_t* node_of, const int32_t* cand_idx, const int32_t* tree_lo, const float* W,
+                         int T, int64_t N, int maxn, int A, int nt_max, int32_t* cnt_ws, int32_t* counts,
+                         int32_t* starts, int32_t* rows, float* row_w, hipStream_t s);
+int har_tree_level_group_chunks(int64_t N);
 int har_tree_partition(int32_t* node_of, const int32_t* lvl_feat, const int32_t* lvl_bin, const int32_t* lvl_left,
                        const uint8_t* bins, int T, int64_t N, int maxn, hipStream_t s);
 int har_forest_predict(const float* X, int64_t n, int F, int ld, const int32_t* feat, const float* thr,

@@ -8,6 +8,12 @@
 //                          stream 0x7F000000), sorted ascending (featureSubsetStrategy).
 //   tree_level_keys      : key[t][r] = candidate index of the node row r of tree t sits in
 //                          (-1: out of bag, finished, or node not split this level).
+//   tree_level_group     : the level's (tree, row) -> candidate grouping WITHOUT a sort:
+//                          per-chunk counts, a column prefix over chunks, one scan over
+//                          candidates, then a stable wave-ordered scatter of row ids and
+//                          bootstrap weights — the same order as a stable sort of the
+//                          keys, but only the active rows are written and no key array
+//                          ever reaches HBM.
 //   tree_partition       : after the level's splits, move every row of a split node to
 //                          its child (bin <= threshold bin -> left) and retire the rows
 //                          of nodes that became leaves — one pass over [T][N] int32.
@@ -76,6 +82,137 @@ __global__ __launch_bounds__(256) void tree_partition_kernel(int32_t* __restrict
   }
 }
 
+
+// ---- level grouping (replaces sort + gather + binary search of the level keys) ----------
+// Chunks of GROUP_CH rows of one tree, one wave each (4 per workgroup); the candidates of a
+// tree are the contiguous range [tree_lo[t], tree_lo[t+1]) (the frontier is tree-ordered), so a
+// wave keeps per-candidate counters for its tree in a private LDS slice of nt_max ints.
+constexpr int GROUP_CH = 1024;
+constexpr int GROUP_WAVES = 4;
+constexpr int GROUP_MAX_NT = 4096;  // 4 waves x 4096 x 4 B = 64 KB of LDS
+
+__device__ __forceinline__ int group_key(const int32_t* __restrict__ no, const int32_t* __restrict__ ci, int64_t r,
+                                         int64_t r1, int lo) {
+  if (r >= r1) return -1;
+  const int n = no[r];
+  if (n < 0) return -1;
+  const int a = ci[n];
+  return a >= 0 ? a - lo : -1;
+}
+
+__global__ __launch_bounds__(256) void tree_group_count_kernel(const int32_t* __restrict__ node_of,
+                                                               const int32_t* __restrict__ cand_idx,
+                                                               const int32_t* __restrict__ tree_lo, int64_t N,
+                                                               int maxn, int nch, int A, int nt_max,
+                                                               int32_t* __restrict__ cnt) {
+  extern __shared__ int32_t glds[];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int t = blockIdx.y, c = blockIdx.x * GROUP_WAVES + wave;
+  const int lo = tree_lo[t], nt = tree_lo[t + 1] - lo;
+  const bool live = c < nch;
+  int32_t* h = glds + wave * nt_max;
+  for (int i = lane; i < nt; i += 64) h[i] = 0;
+  __syncthreads();
+  const int32_t* no = node_of + (int64_t)t * N;
+  const int32_t* ci = cand_idx + (int64_t)t * maxn;
+  const int64_t r0 = (int64_t)c * GROUP_CH, r1 = live ? (r0 + GROUP_CH < N ? r0 + GROUP_CH : N) : r0;
+  for (int64_t r = r0 + lane; r < r1; r += 64) {
+    const int k = group_key(no, ci, r, r1, lo);
+    if (k >= 0) atomicAdd(&h[k], 1);
+  }
+  __syncthreads();
+  if (live)
+    for (int i = lane; i < nt; i += 64) cnt[(int64_t)c * A + lo + i] = h[i];
+}
+
+// cnt[c][a] -> exclusive prefix over chunks c; total[a] = sum.  Coalesced over a.
+__global__ __launch_bounds__(256) void tree_group_colscan_kernel(int32_t* __restrict__ cnt, int nch, int A,
+                                                                 int32_t* __restrict__ total) {
+  const int a = blockIdx.x * 256 + threadIdx.x;
+  if (a >= A) return;
+  int run = 0;
+  for (int c = 0; c < nch; ++c) {
+    const int v = cnt[(int64_t)c * A + a];
+    cnt[(int64_t)c * A + a] = run;
+    run += v;
+  }
+  total[a] = run;
+}
+
+// One workgroup: exclusive scan of total[0..A) -> starts (A is the level's candidate count).
+__global__ __launch_bounds__(1024) void tree_group_scan_kernel(const int32_t* __restrict__ total, int A,
+                                                               int32_t* __restrict__ starts) {
+  __shared__ int32_t wsum[16];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int per = (A + 1023) / 1024;
+  const int b = tid * per, e = b + per < A ? b + per : A;
+  int s = 0;
+  for (int i = b; i < e; ++i) s += total[i];
+  int x = s;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) wsum[w] = x;
+  __syncthreads();
+  int run = x - s;
+  for (int i = 0; i < w; ++i) run += wsum[i];
+  for (int i = b; i < e; ++i) {
+    starts[i] = run;
+    run += total[i];
+  }
+}
+
+// Stable scatter: a wave walks its chunk 64 rows at a time; lanes with the same candidate
+// find each other with one ballot per key bit, the lowest such lane advances the LDS cursor,
+// and each lane's slot is the cursor plus the number of same-key lanes below it — exactly
+// the position a stable sort of (key, tree * N + row) would give.
+__global__ __launch_bounds__(256) void tree_group_scatter_kernel(const int32_t* __restrict__ node_of,
+                                                                 const int32_t* __restrict__ cand_idx,
+                                                                 const int32_t* __restrict__ tree_lo,
+                                                                 const float* __restrict__ W, int64_t N, int maxn,
+                                                                 int nch, int A, int nt_max,
+                                                                 const int32_t* __restrict__ cnt,
+                                                                 const int32_t* __restrict__ starts,
+                                                                 int32_t* __restrict__ rows,
+                                                                 float* __restrict__ row_w) {
+  extern __shared__ int32_t glds[];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int t = blockIdx.y, c = blockIdx.x * GROUP_WAVES + wave;
+  const int lo = tree_lo[t], nt = tree_lo[t + 1] - lo;
+  const bool live = c < nch;
+  int32_t* h = glds + wave * nt_max;
+  if (live)
+    for (int i = lane; i < nt; i += 64) h[i] = cnt[(int64_t)c * A + lo + i] + starts[lo + i];
+  __syncthreads();
+  const int nbits = nt > 1 ? 32 - __clz(nt - 1) : 0;
+  const int32_t* no = node_of + (int64_t)t * N;
+  const int32_t* ci = cand_idx + (int64_t)t * maxn;
+  const float* wt = W + (int64_t)t * N;
+  const uint64_t below = (1ull << lane) - 1ull;
+  const int64_t r0 = (int64_t)c * GROUP_CH, r1 = live ? (r0 + GROUP_CH < N ? r0 + GROUP_CH : N) : r0;
+  for (int64_t rb = r0; rb < r1; rb += 64) {  // wave-uniform trip count: every ballot has all lanes
+    const int64_t r = rb + lane;
+    const int k = group_key(no, ci, r, r1, lo);
+    uint64_t peers = __ballot(k >= 0);
+    for (int bit = 0; bit < nbits; ++bit) {
+      const int on = (k >> bit) & 1;
+      const uint64_t m = __ballot(on);
+      peers &= on ? m : ~m;
+    }
+    const int base = k >= 0 ? h[k] : 0;
+    __builtin_amdgcn_wave_barrier();
+    if (k >= 0) {
+      if ((peers & below) == 0) h[k] = base + (int)__popcll(peers);
+      const int pos = base + (int)__popcll(peers & below);
+      rows[pos] = (int32_t)r;
+      row_w[pos] = wt[r];
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
 int grid_for(int64_t total) { return (int)std::max<int64_t>(1, std::min<int64_t>(8192, (total + 255) / 256)); }
 
 }  // namespace
@@ -106,3 +243,26 @@ extern "C" int har_tree_partition(int32_t* node_of, const int32_t* lvl_feat, con
   HAR_CHECK_LAUNCH();
   return 0;
 }
+
+extern "C" int har_tree_level_group(const int32_t* node_of, const int32_t* cand_idx, const int32_t* tree_lo,
+                                    const float* W, int T, int64_t N, int maxn, int A, int nt_max, int32_t* cnt_ws,
+                                    int32_t* counts, int32_t* starts, int32_t* rows, float* row_w, hipStream_t s) {
+  if (nt_max > GROUP_MAX_NT || nt_max < 1) return -4;
+  if (A == 0 || T == 0 || N == 0) return 0;
+  const int nch = (int)((N + GROUP_CH - 1) / GROUP_CH);
+  const dim3 grid((nch + GROUP_WAVES - 1) / GROUP_WAVES, T);
+  const size_t lds = (size_t)GROUP_WAVES * nt_max * sizeof(int32_t);
+  tree_group_count_kernel<<<grid, 64 * GROUP_WAVES, lds, s>>>(node_of, cand_idx, tree_lo, N, maxn, nch, A, nt_max,
+                                                              cnt_ws);
+  HAR_CHECK_LAUNCH();
+  tree_group_colscan_kernel<<<(A + 255) / 256, 256, 0, s>>>(cnt_ws, nch, A, counts);
+  HAR_CHECK_LAUNCH();
+  tree_group_scan_kernel<<<1, 1024, 0, s>>>(counts, A, starts);
+  HAR_CHECK_LAUNCH();
+  tree_group_scatter_kernel<<<grid, 64 * GROUP_WAVES, lds, s>>>(node_of, cand_idx, tree_lo, W, N, maxn, nch, A,
+                                                                nt_max, cnt_ws, starts, rows, row_w);
+  HAR_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int har_tree_level_group_chunks(int64_t N) { return (int)((N + GROUP_CH - 1) / GROUP_CH); }

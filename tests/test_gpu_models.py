@@ -263,3 +263,21 @@ def test_random_forest_gpu_equals_cpu_builder(cuda):
     same_node = float((g.arrs.feature.cpu() == c.arrs.feature).float().mean())
     agree = float((g.predict(x.to(cuda)).cpu() == c.predict(x)).float().mean())
     assert same_node > 0.97 and agree > 0.99, (same_node, agree)
+
+
+def test_level_grouping_equals_sort_path(cuda, monkeypatch):
+    """tree_level_group (counting sort: per-chunk counts, prefix, wave-stable scatter) feeds the
+    histogram kernel the rows in exactly the order of the stable radix sort of the level keys, so
+    the two device builders grow bit-identical forests (N not a multiple of the 1024-row chunk,
+    deep trees so late levels have thousands of candidates)."""
+    from har.models.tree import RandomForestClassifier
+
+    x, y = _blobs(5300, 16, 6, seed=7)
+    xc, yc = x.to(cuda), y.to(cuda)
+    fits = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("HAR_TREE_LEVEL_SORT", mode)
+        fits[mode] = RandomForestClassifier(numTrees=40, maxDepth=12, seed=11).fit_tensors(xc, yc, 6)
+    a, b = fits["1"].arrs, fits["0"].arrs
+    for name in ("feature", "threshold", "left", "right", "stats"):
+        assert torch.equal(getattr(a, name), getattr(b, name)), name
