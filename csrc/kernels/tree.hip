@@ -19,6 +19,9 @@
 namespace {
 
 constexpr int KMAX = 32;
+#ifndef HIST_UNROLL
+#define HIST_UNROLL 4
+#endif
 
 __global__ __launch_bounds__(256) void tree_hist_split_kernel(
     const uint8_t* __restrict__ bins, int64_t fstride, int64_t rstride, const int32_t* __restrict__ nbins_feat,
@@ -50,7 +53,45 @@ __global__ __launch_bounds__(256) void tree_hist_split_kernel(
   __syncthreads();
 
   // ---- histogram ----
-  if (mode != 2 && cnt >= (int)blockDim.x) {
+  const int rpi = f_n <= 64 ? (int)blockDim.x / f_n : 0;
+  if (mode != 2 && rpi > 0) {
+    // (row, feature slot) pairs with the feature slot fastest: the lanes of one instruction
+    // add into f_n different feature histograms (a row-at-a-time mapping sends most lanes of a
+    // nearly pure node to the same (bin, class) word — same-address LDS atomics serialize), and
+    // the lanes sharing a row read its id / weight / label as one broadcast and its row-major
+    // bins from one line.  Slot and row phase come from tid once; no division in the loop.
+    const int fs = tid % f_n, rs = tid / f_n;
+    if (rs < rpi) {
+      const int64_t fo = (int64_t)fid[fs] * fstride;
+      float* hb = hist + fs * maxbins * K;
+      // HU rows in flight per lane: the row id -> (bins, label) loads are a dependent chain of
+      // two L2 / MALL round trips, so issue HU chains before the first atomic needs its data
+      constexpr int HU = HIST_UNROLL;
+      int ri = rs;
+      for (; ri + (HU - 1) * rpi < cnt; ri += HU * rpi) {
+        int r[HU], b[HU], l[HU];
+        float w[HU];
+#pragma unroll
+        for (int u = 0; u < HU; ++u) {
+          r[u] = rows[start + ri + u * rpi];
+          w[u] = row_w[start + ri + u * rpi];
+        }
+#pragma unroll
+        for (int u = 0; u < HU; ++u) {
+          b[u] = bins[fo + (int64_t)r[u] * rstride];
+          l[u] = label[r[u]];
+        }
+#pragma unroll
+        for (int u = 0; u < HU; ++u) atomicAdd(hb + b[u] * K + l[u], w[u]);
+      }
+      for (; ri < cnt; ri += rpi) {
+        const int r = rows[start + ri];
+        const float w = row_w[start + ri];
+        const int b = bins[fo + (int64_t)r * rstride];
+        atomicAdd(hb + b * K + label[r], w);
+      }
+    }
+  } else if (mode != 2 && cnt >= (int)blockDim.x) {
     // large node: one row per lane, its (row id, weight, label) loaded once for all f_n features
     for (int ri = tid; ri < cnt; ri += blockDim.x) {
       const int r = rows[start + ri];
