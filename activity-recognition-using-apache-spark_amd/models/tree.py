@@ -349,6 +349,7 @@ def _levels_native_impl(b: "ForestBuilder", y32, W, N: int, F: int, m: int, maxn
     use_group = os.environ.get("HAR_TREE_LEVEL_SORT", "0") != "1"
     nch = mod.tree_level_group_chunks(N)
     rows_buf = roww_buf = cnt_ws = None
+    split_bin = torch.zeros(Tn, maxn, dtype=torch.int32, device=dev) if use_group else None
     bins_rm = b.bins.t().contiguous()  # [N, F] for the histogram gathers (partition keeps [F, N])
 
     def candidacy(c: torch.Tensor):
@@ -427,6 +428,23 @@ def _levels_native_impl(b: "ForestBuilder", y32, W, N: int, F: int, m: int, maxn
         n_nodes += 2 * np.bincount(st_t, minlength=Tn)
         dsi_h = np.nonzero(ds)[0]
         ti, ni, cl, dsi = pin_b.upload([st_t, st_n, child_l, dsi_h], dev)
+        if use_group:
+            res = T.LevelResult(gain=res.gain.contiguous(), feat=res.feat.contiguous(), bin=res.bin.contiguous(),
+                                left=res.left.contiguous(), total=res.total.contiguous())
+            # one launch commits every split and both children's stats; the partition reads the
+            # committed arrays (tree_level.hip)
+            mod.tree_commit_level(len(dsi_h), ti.data_ptr(), ni.data_ptr(), cl.data_ptr(), dsi.data_ptr(),
+                                  res.feat.data_ptr(), res.bin.data_ptr(), res.gain.data_ptr(), res.left.data_ptr(),
+                                  res.total.data_ptr(), K, b.thr_mat.data_ptr(), b.thr_mat.shape[1], maxn,
+                                  feature.data_ptr(), split_bin.data_ptr(), thresh.data_ptr(), left.data_ptr(),
+                                  right.data_ptr(), gains.data_ptr(), stats.data_ptr(), st_ptr)
+            mod.tree_partition_split(node_of.data_ptr(), feature.data_ptr(), split_bin.data_ptr(), left.data_ptr(),
+                                     b.bins.data_ptr(), Tn, N, maxn, st_ptr)
+            front_t = np.repeat(st_t, 2)
+            front_n = np.stack([child_l, child_l + 1], 1).reshape(-1)
+            cand = np.stack([h[1][ds] > 0, h[2][ds] > 0], 1).reshape(-1)
+            wtot = np.stack([h[3][ds], h[4][ds]], 1).reshape(-1)
+            continue
         bf = res.feat[dsi].long()
         bb = res.bin[dsi].long()
         feature[ti, ni] = bf.to(torch.int32)

@@ -284,6 +284,23 @@ PYBIND11_MODULE(_har_native, m) {
           "tree_level_group");
   });
   m.def("tree_level_group_chunks", [](int64_t N) { return har_tree_level_group_chunks(N); });
+  m.def("tree_commit_level", [](int nsplit, u ti, u ni, u cl, u dsi, u rfeat, u rbin, u rgain, u rleft, u rtotal, int K,
+                                u thr_mat, int ldthr, int maxn, u feature, u split_bin, u thresh, u left, u right,
+                                u gains, u stats, u stream) {
+    check(har_tree_commit_level(nsplit, P<const int64_t>(ti), P<const int64_t>(ni), P<const int64_t>(cl),
+                                P<const int64_t>(dsi), P<const int32_t>(rfeat), P<const int32_t>(rbin),
+                                P<const float>(rgain), P<const float>(rleft), P<const float>(rtotal), K,
+                                P<const float>(thr_mat), ldthr, maxn, P<int32_t>(feature), P<int32_t>(split_bin),
+                                P<float>(thresh), P<int32_t>(left), P<int32_t>(right), P<float>(gains),
+                                P<float>(stats), S(stream)),
+          "tree_commit_level");
+  });
+  m.def("tree_partition_split", [](u node_of, u feature, u split_bin, u left, u bins, int T, int64_t N, int maxn,
+                                   u stream) {
+    check(har_tree_partition_split(P<int32_t>(node_of), P<const int32_t>(feature), P<const int32_t>(split_bin),
+                                   P<const int32_t>(left), P<const uint8_t>(bins), T, N, maxn, S(stream)),
+          "tree_partition_split");
+  });
   m.def("tree_partition", [](u node_of, u lvl_feat, u lvl_bin, u lvl_left, u bins, int T, int64_t N, int maxn,
                              u stream) {
     check(har_tree_partition(P<int32_t>(node_of), P<const int32_t>(lvl_feat), P<const int32_t>(lvl_bin),

@@ -153,6 +153,15 @@ int har_tree_level_group(const int32_t* node_of, const int32_t* cand_idx, const 
                          int T, int64_t N, int maxn, int A, int nt_max, int32_t* cnt_ws, int32_t* counts,
                          int32_t* starts, int32_t* rows, float* row_w, hipStream_t s);
 int har_tree_level_group_chunks(int64_t N);
+// Commit the level's splits (feature / bin / threshold / children / gain / child stats) in one launch,
+// then move rows with the committed arrays (no per-level temporaries).
+int har_tree_commit_level(int S, const int64_t* ti, const int64_t* ni, const int64_t* cl, const int64_t* dsi,
+                          const int32_t* rfeat, const int32_t* rbin, const float* rgain, const float* rleft,
+                          const float* rtotal, int K, const float* thr_mat, int ldthr, int maxn, int32_t* feature,
+                          int32_t* split_bin, float* thresh, int32_t* left, int32_t* right, float* gains,
+                          float* stats, hipStream_t s);
+int har_tree_partition_split(int32_t* node_of, const int32_t* feature, const int32_t* split_bin, const int32_t* left,
+                             const uint8_t* bins, int T, int64_t N, int maxn, hipStream_t s);
 int har_tree_partition(int32_t* node_of, const int32_t* lvl_feat, const int32_t* lvl_bin, const int32_t* lvl_left,
                        const uint8_t* bins, int T, int64_t N, int maxn, hipStream_t s);
 int har_forest_predict(const float* X, int64_t n, int F, int ld, const int32_t* feat, const float* thr,

@@ -213,6 +213,62 @@ __global__ __launch_bounds__(256) void tree_group_scatter_kernel(const int32_t* 
   }
 }
 
+// One thread per node split this level: write the node's split (feature, bin, threshold,
+// children, gain) and both children's class statistics — the level's ~15 index_put / gather
+// launches as one.  Indices come from the host (int64, one pinned upload).
+__global__ __launch_bounds__(256) void tree_commit_level_kernel(
+    int S, const int64_t* __restrict__ ti, const int64_t* __restrict__ ni, const int64_t* __restrict__ cl,
+    const int64_t* __restrict__ dsi, const int32_t* __restrict__ rfeat, const int32_t* __restrict__ rbin,
+    const float* __restrict__ rgain, const float* __restrict__ rleft, const float* __restrict__ rtotal, int K,
+    const float* __restrict__ thr_mat, int ldthr, int maxn, int32_t* __restrict__ feature,
+    int32_t* __restrict__ split_bin, float* __restrict__ thresh, int32_t* __restrict__ left,
+    int32_t* __restrict__ right, float* __restrict__ gains, float* __restrict__ stats) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= S) return;
+  const int64_t j = dsi[i];
+  const int64_t o = ti[i] * maxn + ni[i];
+  const int c = (int)cl[i];
+  const int f = rfeat[j], b = rbin[j];
+  feature[o] = f;
+  split_bin[o] = b;
+  thresh[o] = thr_mat[(int64_t)f * ldthr + b];
+  left[o] = c;
+  right[o] = c + 1;
+  const float* L = rleft + j * K;
+  const float* Tt = rtotal + j * K;
+  float* sl = stats + (ti[i] * maxn + c) * K;
+  float tw = 0.f;
+  for (int k = 0; k < K; ++k) {
+    const float l = L[k], t = Tt[k];
+    sl[k] = l;
+    sl[K + k] = t - l;
+    tw += t;
+  }
+  gains[o] = rgain[j] * tw;
+}
+
+// Row -> child move reading the committed split arrays directly (feature < 0: the node is a
+// leaf or was not split this level, the row is done).
+__global__ __launch_bounds__(256) void tree_partition_split_kernel(int32_t* __restrict__ node_of,
+                                                                   const int32_t* __restrict__ feature,
+                                                                   const int32_t* __restrict__ split_bin,
+                                                                   const int32_t* __restrict__ left,
+                                                                   const uint8_t* __restrict__ bins, int T,
+                                                                   int64_t N, int maxn) {
+  const int64_t total = (int64_t)T * N;
+  for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < total; j += (int64_t)gridDim.x * blockDim.x) {
+    const int n = node_of[j];
+    if (n < 0) continue;
+    const int t = (int)(j / N);
+    const int64_t r = j - (int64_t)t * N;
+    const int64_t o = (int64_t)t * maxn + n;
+    const int f = feature[o];
+    if (f < 0) { node_of[j] = -1; continue; }
+    const int b = bins[(int64_t)f * N + r];
+    node_of[j] = left[o] + (b <= split_bin[o] ? 0 : 1);
+  }
+}
+
 int grid_for(int64_t total) { return (int)std::max<int64_t>(1, std::min<int64_t>(8192, (total + 255) / 256)); }
 
 }  // namespace
@@ -266,3 +322,26 @@ extern "C" int har_tree_level_group(const int32_t* node_of, const int32_t* cand_
 }
 
 extern "C" int har_tree_level_group_chunks(int64_t N) { return (int)((N + GROUP_CH - 1) / GROUP_CH); }
+
+extern "C" int har_tree_commit_level(int S, const int64_t* ti, const int64_t* ni, const int64_t* cl, const int64_t* dsi,
+                                     const int32_t* rfeat, const int32_t* rbin, const float* rgain, const float* rleft,
+                                     const float* rtotal, int K, const float* thr_mat, int ldthr, int maxn,
+                                     int32_t* feature, int32_t* split_bin, float* thresh, int32_t* left,
+                                     int32_t* right, float* gains, float* stats, hipStream_t s) {
+  if (S <= 0) return 0;
+  tree_commit_level_kernel<<<(S + 255) / 256, 256, 0, s>>>(S, ti, ni, cl, dsi, rfeat, rbin, rgain, rleft, rtotal, K,
+                                                           thr_mat, ldthr, maxn, feature, split_bin, thresh, left,
+                                                           right, gains, stats);
+  HAR_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int har_tree_partition_split(int32_t* node_of, const int32_t* feature, const int32_t* split_bin,
+                                        const int32_t* left, const uint8_t* bins, int T, int64_t N, int maxn,
+                                        hipStream_t s) {
+  if ((int64_t)T * N == 0) return 0;
+  tree_partition_split_kernel<<<grid_for((int64_t)T * N), 256, 0, s>>>(node_of, feature, split_bin, left, bins, T, N,
+                                                                       maxn);
+  HAR_CHECK_LAUNCH();
+  return 0;
+}
