@@ -412,12 +412,21 @@ def _levels_native_impl(b: "ForestBuilder", y32, W, N: int, F: int, m: int, maxn
                                   b.min_inst, b.min_gain, b.impurity,
                                   allreduce=None if b.owner is not None else b.allreduce, owner=b.owner,
                                   max_rows=int(cw.max()) if A else 0, check_labels=False, bins_rm=bins_rm)
-        do_split = (res.gain > 0) & torch.isfinite(res.gain)
-        lstat = res.left
-        rstat = res.total - lstat
-        cl_ok, wl = candidacy(lstat)
-        cr_ok, wr = candidacy(rstat)
-        h = torch.stack([do_split.float(), cl_ok.float(), cr_ok.float(), wl.float(), wr.float()]).cpu().numpy()
+        if use_group:
+            res = T.LevelResult(gain=res.gain.contiguous(), feat=res.feat.contiguous(), bin=res.bin.contiguous(),
+                                left=res.left.contiguous(), total=res.total.contiguous())
+            dec = torch.empty(5, A, dtype=torch.float32, device=dev)
+            mod.tree_level_decide(A, res.gain.data_ptr(), res.left.data_ptr(), res.total.data_ptr(), K, b.impurity,
+                                  float(2 * b.min_inst), dec.data_ptr(), st_ptr)
+            h = dec.cpu().numpy()
+            lstat = rstat = None
+        else:
+            do_split = (res.gain > 0) & torch.isfinite(res.gain)
+            lstat = res.left
+            rstat = res.total - lstat
+            cl_ok, wl = candidacy(lstat)
+            cr_ok, wr = candidacy(rstat)
+            h = torch.stack([do_split.float(), cl_ok.float(), cr_ok.float(), wl.float(), wr.float()]).cpu().numpy()
         ds = h[0] > 0
         if not ds.any():
             break
@@ -429,8 +438,6 @@ def _levels_native_impl(b: "ForestBuilder", y32, W, N: int, F: int, m: int, maxn
         dsi_h = np.nonzero(ds)[0]
         ti, ni, cl, dsi = pin_b.upload([st_t, st_n, child_l, dsi_h], dev)
         if use_group:
-            res = T.LevelResult(gain=res.gain.contiguous(), feat=res.feat.contiguous(), bin=res.bin.contiguous(),
-                                left=res.left.contiguous(), total=res.total.contiguous())
             # one launch commits every split and both children's stats; the partition reads the
             # committed arrays (tree_level.hip)
             mod.tree_commit_level(len(dsi_h), ti.data_ptr(), ni.data_ptr(), cl.data_ptr(), dsi.data_ptr(),

@@ -301,6 +301,11 @@ PYBIND11_MODULE(_har_native, m) {
                                    P<const int32_t>(left), P<const uint8_t>(bins), T, N, maxn, S(stream)),
           "tree_partition_split");
   });
+  m.def("tree_level_decide", [](int A, u gain, u left, u total, int K, int impurity, float min2, u out, u stream) {
+    check(har_tree_level_decide(A, P<const float>(gain), P<const float>(left), P<const float>(total), K, impurity, min2,
+                                P<float>(out), S(stream)),
+          "tree_level_decide");
+  });
   m.def("tree_partition", [](u node_of, u lvl_feat, u lvl_bin, u lvl_left, u bins, int T, int64_t N, int maxn,
                              u stream) {
     check(har_tree_partition(P<int32_t>(node_of), P<const int32_t>(lvl_feat), P<const int32_t>(lvl_bin),

@@ -162,6 +162,8 @@ int har_tree_commit_level(int S, const int64_t* ti, const int64_t* ni, const int
                           float* stats, hipStream_t s);
 int har_tree_partition_split(int32_t* node_of, const int32_t* feature, const int32_t* split_bin, const int32_t* left,
                              const uint8_t* bins, int T, int64_t N, int maxn, hipStream_t s);
+int har_tree_level_decide(int A, const float* gain, const float* left, const float* total, int K, int impurity,
+                          float min2, float* out, hipStream_t s);
 int har_tree_partition(int32_t* node_of, const int32_t* lvl_feat, const int32_t* lvl_bin, const int32_t* lvl_left,
                        const uint8_t* bins, int T, int64_t N, int maxn, hipStream_t s);
 int har_forest_predict(const float* X, int64_t n, int F, int ld, const int32_t* feat, const float* thr,

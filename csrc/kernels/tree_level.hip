@@ -269,6 +269,46 @@ __global__ __launch_bounds__(256) void tree_partition_split_kernel(int32_t* __re
   }
 }
 
+// Per candidate after the split search: split or not, and whether each child is itself a
+// candidate of the next level (impurity > 1e-12 in fp64 and weight >= 2 * min_instances) —
+// out rows: [do_split, left ok, right ok, left weight, right weight], one D2H copy per level.
+__global__ __launch_bounds__(256) void tree_level_decide_kernel(int A, const float* __restrict__ gain,
+                                                                const float* __restrict__ left,
+                                                                const float* __restrict__ total, int K,
+                                                                int impurity, float min2, float* __restrict__ out) {
+  const int a = blockIdx.x * blockDim.x + threadIdx.x;
+  if (a >= A) return;
+  const float g = gain[a];
+  const float* L = left + (int64_t)a * K;
+  const float* Tt = total + (int64_t)a * K;
+  float wl = 0.f, wr = 0.f;
+  for (int k = 0; k < K; ++k) {
+    wl += L[k];
+    wr += Tt[k] - L[k];
+  }
+  const double dl = fmax((double)wl, 1e-30), dr = fmax((double)wr, 1e-30);
+  double il = 0.0, ir = 0.0;
+  for (int k = 0; k < K; ++k) {
+    const double pl = (double)L[k] / dl, pr = (double)(Tt[k] - L[k]) / dr;
+    if (impurity == 0) {
+      il += pl * pl;
+      ir += pr * pr;
+    } else {
+      il -= pl > 0 ? pl * log2(fmax(pl, 1e-30)) : 0.0;
+      ir -= pr > 0 ? pr * log2(fmax(pr, 1e-30)) : 0.0;
+    }
+  }
+  if (impurity == 0) {
+    il = 1.0 - il;
+    ir = 1.0 - ir;
+  }
+  out[a] = (g > 0.f && isfinite(g)) ? 1.f : 0.f;
+  out[A + a] = (il > 1e-12 && wl >= min2) ? 1.f : 0.f;
+  out[2 * A + a] = (ir > 1e-12 && wr >= min2) ? 1.f : 0.f;
+  out[3 * A + a] = wl;
+  out[4 * A + a] = wr;
+}
+
 int grid_for(int64_t total) { return (int)std::max<int64_t>(1, std::min<int64_t>(8192, (total + 255) / 256)); }
 
 }  // namespace
@@ -342,6 +382,14 @@ extern "C" int har_tree_partition_split(int32_t* node_of, const int32_t* feature
   if ((int64_t)T * N == 0) return 0;
   tree_partition_split_kernel<<<grid_for((int64_t)T * N), 256, 0, s>>>(node_of, feature, split_bin, left, bins, T, N,
                                                                        maxn);
+  HAR_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int har_tree_level_decide(int A, const float* gain, const float* left, const float* total, int K,
+                                     int impurity, float min2, float* out, hipStream_t s) {
+  if (A <= 0) return 0;
+  tree_level_decide_kernel<<<(A + 255) / 256, 256, 0, s>>>(A, gain, left, total, K, impurity, min2, out);
   HAR_CHECK_LAUNCH();
   return 0;
 }
