@@ -116,7 +116,11 @@ class ForestBuilder:
         self.bins = bin_features(X, self.thresholds).to(X.device).contiguous()  # [F, N] uint8 (HIP on the GPU)
 
     def _levels_native(self, *a):
-        _levels_native_impl(self, *a)
+        # HAR_TREE_LEVEL_SORT=1 keeps the host-frontier radix-sort loop (A/B and equality oracle)
+        if os.environ.get("HAR_TREE_LEVEL_SORT", "0") != "1":
+            _levels_device_frontier(self, *a)
+        else:
+            _levels_native_impl(self, *a)
 
     def bootstrap_weights(self, N: int, device, row_offset: int = 0) -> torch.Tensor:
         if not self.bootstrap:
@@ -473,6 +477,112 @@ def _levels_native_impl(b: "ForestBuilder", y32, W, N: int, F: int, m: int, maxn
         front_n = np.stack([child_l, child_l + 1], 1).reshape(-1)
         cand = np.stack([h[1][ds] > 0, h[2][ds] > 0], 1).reshape(-1)
         wtot = np.stack([h[3][ds], h[4][ds]], 1).reshape(-1)
+
+
+def _levels_device_frontier(b: "ForestBuilder", y32, W, N: int, F: int, m: int, maxn: int, stats, feature, thresh,
+                            left, right, gains, n_nodes, node_of):
+    """Device level loop with the frontier resident on the GPU and ONE 16-byte device -> host
+    read per level (splits, next candidates, max candidates per tree, max candidate weight).
+
+    Per level (tree_level.hip unless noted): stable counting-sort grouping of the (tree, row)
+    pairs by candidate node; Floyd feature subsets; the fused histogram + split kernel
+    (tree.hip); the split / child-candidacy decision; the frontier update (split slots by a
+    scan, child ids per tree, next candidates by a second scan, their cand_idx entries and tree
+    starts); the commit of every split and both children's stats; the row partition.  The
+    host does no per-level numpy work and uploads nothing; it grows the forest the
+    host-frontier loop (``_levels_native_impl``) grows, node for node."""
+    dev = W.device
+    Tn, K, D = b.T, b.K, b.D
+    mod = _native.kernels()
+    st = _native.stream_ptr()
+    i32 = dict(dtype=torch.int32, device=dev)
+    Wf = W.reshape(-1).contiguous()
+    bins_rm = b.bins.t().contiguous()  # [N, F] for the histogram gathers (partition keeps [F, N])
+    nch = mod.tree_level_group_chunks(N)
+
+    w0 = stats[:, 0].sum(-1)
+    imp0 = T._impurity(stats[:, 0].double(), w0.double(), b.impurity)
+    c0 = ((imp0 > 1e-12) & (w0 >= 2 * b.min_inst)).cpu().numpy()
+    ct0 = np.nonzero(c0)[0]
+    A = len(ct0)
+    if A == 0:
+        return
+    max_w = float(w0.cpu().numpy()[c0].max())
+    ct = torch.from_numpy(ct0.astype(np.int32)).to(dev)
+    cn = torch.zeros(A, **i32)
+    tlo = torch.from_numpy(np.concatenate([[0], np.cumsum(c0.astype(np.int64))]).astype(np.int32)).to(dev)
+    nt_max = 1
+    cand_idx = torch.full((Tn, maxn), -1, **i32)  # stale entries name nodes no row sits in any more
+    cand_idx[ct.long(), 0] = torch.arange(A, **i32)
+    nn = torch.from_numpy(n_nodes.astype(np.int32)).to(dev)
+    nn_next = torch.empty_like(nn)
+    split_bin = torch.zeros(Tn, maxn, **i32)
+    rows_buf = torch.empty(Tn * N, **i32)
+    roww_buf = torch.empty(Tn * N, dtype=torch.float32, device=dev)
+    tlo_next = torch.empty(Tn + 1, **i32)
+    scal = torch.zeros(4, **i32)
+    scal_h = torch.empty(4, dtype=torch.int32).pin_memory()
+    cnt_ws = None
+    for depth in range(D):
+        if cnt_ws is None or cnt_ws.numel() < nch * A:
+            cnt_ws = torch.empty(nch * max(A, 2 * Tn), **i32)
+        counts, starts = torch.empty(A, **i32), torch.empty(A, **i32)
+        if nt_max <= GROUP_MAX_NT:
+            mod.tree_level_group(node_of.data_ptr(), cand_idx.data_ptr(), tlo.data_ptr(), Wf.data_ptr(), Tn, N,
+                                 maxn, A, nt_max, cnt_ws.data_ptr(), counts.data_ptr(), starts.data_ptr(),
+                                 rows_buf.data_ptr(), roww_buf.data_ptr(), st)
+            rows, row_w = rows_buf, roww_buf
+        else:  # a tree with > GROUP_MAX_NT candidates: the same order from a stable radix sort
+            key = torch.empty(Tn * N, **i32)
+            mod.tree_level_keys(node_of.data_ptr(), cand_idx.data_ptr(), Tn, N, maxn, key.data_ptr(), st)
+            keys, order = torch.sort(key, stable=True)
+            rows, row_w = (order % N).to(torch.int32), Wf[order]
+            bounds = torch.searchsorted(keys, torch.arange(A + 1, **i32))
+            counts = (bounds[1:] - bounds[:-1]).to(torch.int32)
+            starts = bounds[:-1].to(torch.int32)
+        if m >= F:
+            feats = torch.arange(F, **i32).repeat(A, 1)
+        else:
+            feats = torch.empty(A, m, **i32)
+            tr = ct + b.tree_offset if b.tree_offset else ct
+            mod.tree_feature_subsets(b.seed, tr.data_ptr(), cn.data_ptr(), A, F, m, feats.data_ptr(), st)
+        res = T.hist_split_native(b.bins, b.nbins, y32, rows, row_w, starts, counts, feats, K, b.max_bins,
+                                  b.min_inst, b.min_gain, b.impurity,
+                                  allreduce=None if b.owner is not None else b.allreduce, owner=b.owner,
+                                  max_rows=int(max_w), check_labels=False, bins_rm=bins_rm)
+        res = T.LevelResult(gain=res.gain.contiguous(), feat=res.feat.contiguous(), bin=res.bin.contiguous(),
+                            left=res.left.contiguous(), total=res.total.contiguous())
+        dec = torch.empty(5, A, dtype=torch.float32, device=dev)
+        mod.tree_level_decide(A, res.gain.data_ptr(), res.left.data_ptr(), res.total.data_ptr(), K, b.impurity,
+                              float(2 * b.min_inst), dec.data_ptr(), st)
+        pos = torch.empty(A + 1, **i32)
+        ti, ni, cl, dsi = (torch.empty(A, dtype=torch.int64, device=dev) for _ in range(4))
+        front = torch.empty(2 * A, dtype=torch.float32, device=dev)
+        q = torch.empty(2 * A + 1, **i32)
+        ct_next, cn_next = torch.empty(2 * A, **i32), torch.empty(2 * A, **i32)
+        mod.tree_frontier(A, Tn, maxn, ct.data_ptr(), cn.data_ptr(), tlo.data_ptr(), dec.data_ptr(), nn.data_ptr(),
+                          nn_next.data_ptr(), pos.data_ptr(), ti.data_ptr(), ni.data_ptr(), cl.data_ptr(),
+                          dsi.data_ptr(), front.data_ptr(), q.data_ptr(), ct_next.data_ptr(), cn_next.data_ptr(),
+                          tlo_next.data_ptr(), cand_idx.data_ptr(), scal.data_ptr(), st)
+        scal_h.copy_(scal)  # the level's one sync
+        S, A_next, nt_next, wbits = (int(v) for v in scal_h.tolist())
+        if S == 0:
+            break
+        mod.tree_commit_level(S, ti.data_ptr(), ni.data_ptr(), cl.data_ptr(), dsi.data_ptr(), res.feat.data_ptr(),
+                              res.bin.data_ptr(), res.gain.data_ptr(), res.left.data_ptr(), res.total.data_ptr(), K,
+                              b.thr_mat.data_ptr(), b.thr_mat.shape[1], maxn, feature.data_ptr(),
+                              split_bin.data_ptr(), thresh.data_ptr(), left.data_ptr(), right.data_ptr(),
+                              gains.data_ptr(), stats.data_ptr(), st)
+        mod.tree_partition_split(node_of.data_ptr(), feature.data_ptr(), split_bin.data_ptr(), left.data_ptr(),
+                                 b.bins.data_ptr(), Tn, N, maxn, st)
+        nn, nn_next = nn_next, nn
+        ct, cn, A = ct_next[:A_next], cn_next[:A_next], A_next
+        tlo, tlo_next = tlo_next, tlo
+        nt_max = max(nt_next, 1)
+        max_w = float(np.array([wbits], dtype=np.int32).view(np.float32)[0])
+        if A == 0:
+            break
+    n_nodes[:] = nn.cpu().numpy()
 
 
 def predict_forest(arrs: ForestArrays, X: torch.Tensor, normalize: bool) -> torch.Tensor:

@@ -306,6 +306,16 @@ PYBIND11_MODULE(_har_native, m) {
                                 P<float>(out), S(stream)),
           "tree_level_decide");
   });
+  m.def("tree_frontier", [](int A, int Tn, int maxn, u ct, u cn, u tlo, u dec, u n_nodes, u n_nodes_next, u pos_ws,
+                            u ti, u ni, u cl, u dsi, u front, u q_ws, u ct_next, u cn_next, u tlo_next, u cand_idx,
+                            u scal, u stream) {
+    check(har_tree_frontier(A, Tn, maxn, P<const int32_t>(ct), P<const int32_t>(cn), P<const int32_t>(tlo),
+                            P<const float>(dec), P<const int32_t>(n_nodes), P<int32_t>(n_nodes_next),
+                            P<int32_t>(pos_ws), P<int64_t>(ti), P<int64_t>(ni), P<int64_t>(cl), P<int64_t>(dsi),
+                            P<float>(front), P<int32_t>(q_ws), P<int32_t>(ct_next), P<int32_t>(cn_next),
+                            P<int32_t>(tlo_next), P<int32_t>(cand_idx), P<int32_t>(scal), S(stream)),
+          "tree_frontier");
+  });
   m.def("tree_partition", [](u node_of, u lvl_feat, u lvl_bin, u lvl_left, u bins, int T, int64_t N, int maxn,
                              u stream) {
     check(har_tree_partition(P<int32_t>(node_of), P<const int32_t>(lvl_feat), P<const int32_t>(lvl_bin),

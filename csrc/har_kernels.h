@@ -164,6 +164,13 @@ int har_tree_partition_split(int32_t* node_of, const int32_t* feature, const int
                              const uint8_t* bins, int T, int64_t N, int maxn, hipStream_t s);
 int har_tree_level_decide(int A, const float* gain, const float* left, const float* total, int K, int impurity,
                           float min2, float* out, hipStream_t s);
+// Device-resident frontier update from the level decisions (see tree_level.hip): commit records
+// ti/ni/cl/dsi [<= A], next candidates ct/cn [<= 2A], tree starts [Tn + 1], cand_idx entries, and
+// scal = [splits, next candidates, max per tree, max weight float bits] (the level's one D2H).
+int har_tree_frontier(int A, int Tn, int maxn, const int32_t* ct, const int32_t* cn, const int32_t* tlo,
+                      const float* dec, const int32_t* n_nodes, int32_t* n_nodes_next, int32_t* pos_ws, int64_t* ti,
+                      int64_t* ni, int64_t* cl, int64_t* dsi, float* front, int32_t* q_ws, int32_t* ct_next,
+                      int32_t* cn_next, int32_t* tlo_next, int32_t* cand_idx, int32_t* scal, hipStream_t s);
 int har_tree_partition(int32_t* node_of, const int32_t* lvl_feat, const int32_t* lvl_bin, const int32_t* lvl_left,
                        const uint8_t* bins, int T, int64_t N, int maxn, hipStream_t s);
 int har_forest_predict(const float* X, int64_t n, int F, int ld, const int32_t* feat, const float* thr,

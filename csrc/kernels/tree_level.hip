@@ -309,6 +309,99 @@ __global__ __launch_bounds__(256) void tree_level_decide_kernel(int A, const flo
   out[4 * A + a] = wr;
 }
 
+// ---- device-resident frontier: the level's split bookkeeping without host numpy ------------
+// Exclusive scan of (flags > 0) over n entries (n = n_mul * *n_dev when n_dev is given) in
+// one workgroup; out[n] = total.
+__global__ __launch_bounds__(1024) void frontier_scan_kernel(const float* __restrict__ flags, int n_static,
+                                                             const int32_t* __restrict__ n_dev, int n_mul,
+                                                             int32_t* __restrict__ out) {
+  __shared__ int32_t wsum[16];
+  const int n = n_dev ? n_mul * (*n_dev) : n_static;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int per = (n + 1023) / 1024;
+  const int b = tid * per, e = b + per < n ? b + per : n;
+  int s = 0;
+  for (int i = b; i < e; ++i) s += flags[i] > 0.f;
+  int x = s;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) wsum[w] = x;
+  __syncthreads();
+  int run = x - s;
+  for (int i = 0; i < w; ++i) run += wsum[i];
+  for (int i = b; i < e; ++i) {
+    out[i] = run;
+    run += flags[i] > 0.f;
+  }
+  if (tid == 1023) out[n] = run;
+}
+
+// Per candidate a that splits (slot p = pos[a]): its commit record (tree, node, left child id,
+// candidate index) and its two children's "candidate next level" flags at front[2p], [2p+1];
+// per tree t: the node counter advances by 2 x its splits (into n_nodes_next).
+__global__ __launch_bounds__(256) void frontier_children_kernel(int A, int Tn, const int32_t* __restrict__ ct,
+                                                                const int32_t* __restrict__ cn,
+                                                                const int32_t* __restrict__ tlo,
+                                                                const float* __restrict__ dec,
+                                                                const int32_t* __restrict__ pos,
+                                                                const int32_t* __restrict__ n_nodes,
+                                                                int32_t* __restrict__ n_nodes_next,
+                                                                int64_t* __restrict__ ti, int64_t* __restrict__ ni,
+                                                                int64_t* __restrict__ cl, int64_t* __restrict__ dsi,
+                                                                float* __restrict__ front) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < Tn) n_nodes_next[i] = n_nodes[i] + 2 * (pos[tlo[i + 1]] - pos[tlo[i]]);
+  if (i >= A || !(dec[i] > 0.f)) return;
+  const int p = pos[i], t = ct[i];
+  const int c = n_nodes[t] + 2 * (p - pos[tlo[t]]);
+  ti[p] = t;
+  ni[p] = cn[i];
+  cl[p] = c;
+  dsi[p] = i;
+  front[2 * p] = dec[A + i];
+  front[2 * p + 1] = dec[2 * A + i];
+}
+
+// Front entry e (child e & 1 of split e >> 1) that is a candidate becomes next-level candidate
+// q[e]: its (tree, node), weight and cand_idx entry; tree starts of the next level; scalars
+// [splits, next candidates, max candidates per tree, max candidate weight (float bits)].
+__global__ __launch_bounds__(256) void frontier_next_kernel(int A, int Tn, int maxn, const int32_t* __restrict__ tlo,
+                                                            const float* __restrict__ dec,
+                                                            const int32_t* __restrict__ pos,
+                                                            const int64_t* __restrict__ ti,
+                                                            const int64_t* __restrict__ cl,
+                                                            const int64_t* __restrict__ dsi,
+                                                            const float* __restrict__ front,
+                                                            const int32_t* __restrict__ q,
+                                                            int32_t* __restrict__ ct_next,
+                                                            int32_t* __restrict__ cn_next,
+                                                            int32_t* __restrict__ tlo_next,
+                                                            int32_t* __restrict__ cand_idx,
+                                                            int32_t* __restrict__ scal) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  const int S = pos[A];
+  if (e <= Tn) {
+    const int lo = q[2 * pos[tlo[e]]];
+    tlo_next[e] = lo;
+    if (e < Tn) atomicMax(&scal[2], q[2 * pos[tlo[e + 1]]] - lo);
+  }
+  if (e == 0) {
+    scal[0] = S;
+    scal[1] = q[2 * S];
+  }
+  if (e >= 2 * S || !(front[e] > 0.f)) return;
+  const int p = e >> 1, i = q[e];
+  const int t = (int)ti[p], n = (int)cl[p] + (e & 1);
+  ct_next[i] = t;
+  cn_next[i] = n;
+  cand_idx[(int64_t)t * maxn + n] = i;
+  const float wgt = dec[(3 + (e & 1)) * A + dsi[p]];
+  atomicMax(&scal[3], __float_as_int(wgt));  // weights >= 0: float order == int order
+}
+
 int grid_for(int64_t total) { return (int)std::max<int64_t>(1, std::min<int64_t>(8192, (total + 255) / 256)); }
 
 }  // namespace
@@ -390,6 +483,29 @@ extern "C" int har_tree_level_decide(int A, const float* gain, const float* left
                                      int impurity, float min2, float* out, hipStream_t s) {
   if (A <= 0) return 0;
   tree_level_decide_kernel<<<(A + 255) / 256, 256, 0, s>>>(A, gain, left, total, K, impurity, min2, out);
+  HAR_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int har_tree_frontier(int A, int Tn, int maxn, const int32_t* ct, const int32_t* cn, const int32_t* tlo,
+                                 const float* dec, const int32_t* n_nodes, int32_t* n_nodes_next, int32_t* pos_ws,
+                                 int64_t* ti, int64_t* ni, int64_t* cl, int64_t* dsi, float* front, int32_t* q_ws,
+                                 int32_t* ct_next, int32_t* cn_next, int32_t* tlo_next, int32_t* cand_idx,
+                                 int32_t* scal, hipStream_t s) {
+  if (A <= 0) return -2;
+  hipError_t err = hipMemsetAsync(scal, 0, 4 * sizeof(int32_t), s);
+  if (err != hipSuccess) return (int)err;
+  frontier_scan_kernel<<<1, 1024, 0, s>>>(dec, A, nullptr, 1, pos_ws);
+  HAR_CHECK_LAUNCH();
+  const int g1 = (std::max(A, Tn + 1) + 255) / 256;
+  frontier_children_kernel<<<g1, 256, 0, s>>>(A, Tn, ct, cn, tlo, dec, pos_ws, n_nodes, n_nodes_next, ti, ni, cl, dsi,
+                                              front);
+  HAR_CHECK_LAUNCH();
+  frontier_scan_kernel<<<1, 1024, 0, s>>>(front, 0, pos_ws + A, 2, q_ws);
+  HAR_CHECK_LAUNCH();
+  const int g2 = (std::max(2 * A, Tn + 1) + 255) / 256;
+  frontier_next_kernel<<<g2, 256, 0, s>>>(A, Tn, maxn, tlo, dec, pos_ws, ti, cl, dsi, front, q_ws, ct_next, cn_next,
+                                          tlo_next, cand_idx, scal);
   HAR_CHECK_LAUNCH();
   return 0;
 }
