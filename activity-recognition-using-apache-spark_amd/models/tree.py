@@ -104,8 +104,8 @@ class ForestBuilder:
         from ..ops.stats import bin_features
 
         if thresholds is None:
-            Xh = X.detach().float().cpu().numpy()
-            thresholds = T.find_thresholds(Xh, self.max_bins, seed=self.seed)
+            # GPU: device findSplits (one sort, one small copy back; the same thresholds)
+            thresholds = T.thresholds_for(X, self.max_bins, seed=self.seed)
         self.thresholds = thresholds
         F = X.shape[1]
         self.nbins = torch.tensor([len(t) + 1 for t in self.thresholds], dtype=torch.int32, device=X.device)
@@ -701,7 +701,7 @@ class DecisionTreeClassifier(_TreeEstimatorBase):
         X, y, K = self._prep(table)
         if dp_context() is None:
             return self.fit_tensors(X, y, K)
-        thr = T.find_thresholds(X.detach().float().cpu().numpy(), self.maxBins, seed=self.seed)
+        thr = T.thresholds_for(X, self.maxBins, seed=self.seed)
         lo, hi = dp_rows(X.shape[0])
         return self.fit_tensors(X[lo:hi], y[lo:hi], K, thresholds=thr, owner=dp_owner(), row_offset=lo)
 
@@ -739,7 +739,7 @@ class RandomForestClassifier(_TreeEstimatorBase):
         X, y, K = self._prep(table)
         if dp_context() is None:
             return self.fit_tensors(X, y, K)
-        thr = T.find_thresholds(X.detach().float().cpu().numpy(), self.maxBins, seed=self.seed)
+        thr = T.thresholds_for(X, self.maxBins, seed=self.seed)
         lo, hi = dp_rows(X.shape[0])
         return self.fit_tensors(X[lo:hi], y[lo:hi], K, row_offset=lo, thresholds=thr, owner=dp_owner())
 
@@ -755,7 +755,7 @@ class RandomForestClassifier(_TreeEstimatorBase):
         if str(strategy).lower() == "auto":
             strategy = "all" if self.numTrees == 1 else "sqrt"
         if thresholds is None:
-            thresholds = T.find_thresholds(X.detach().float().cpu().numpy(), self.maxBins, seed=self.seed)
+            thresholds = T.thresholds_for(X, self.maxBins, seed=self.seed)
         # tree-parallel mode grows trees [tree_offset, tree_offset + num_trees) of the forest: global tree
         # ids key the bootstrap and feature-subset streams, so the slices concatenate into the forest
         total = self.numTrees if num_trees is None else int(num_trees)
@@ -808,7 +808,7 @@ def _fit_sharded(b: "ForestBuilder", X, y, row_weight, max_bins: int, seed: int)
     row shard (thresholds from the whole matrix, so every rank bins identically)."""
     if dp_context() is None:
         return b.fit(X, y, row_weight=row_weight)
-    thr = T.find_thresholds(X.detach().float().cpu().numpy(), max_bins, seed=seed)
+    thr = T.thresholds_for(X, max_bins, seed=seed)
     lo, hi = dp_rows(X.shape[0])
     return b.fit(X[lo:hi], y[lo:hi], row_offset=lo, thresholds=thr, row_weight=row_weight[:, lo:hi])
 

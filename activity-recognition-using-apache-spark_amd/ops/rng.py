@@ -28,6 +28,7 @@ STREAM_SPLIT = 0
 STREAM_KFOLD = 1
 STREAM_SAMPLE = 2
 STREAM_INIT = 3
+STREAM_FINDSPLITS = 4  # findSplits row sample (Bernoulli, keyed by global row id)
 STREAM_BOOTSTRAP_BASE = 0x1000  # + tree id
 STREAM_FEATURE_SUBSET = 0x7F000000  # per (tree,node) in counter
 

@@ -21,18 +21,45 @@ from dataclasses import dataclass
 import numpy as np
 import torch
 
-from . import _native
+from . import _native, rng
 
 GINI, ENTROPY = 0, 1
 LDS_BUDGET = 96 * 1024  # bytes of LDS histogram per workgroup
 
 
-def find_thresholds(X: np.ndarray, max_bins: int, sample_rows: int = 10000, seed: int = 0):
-    """List of float32 threshold arrays (``x <= thr[b]`` goes left at split b)."""
+def threshold_sample_weights(n_total: int, max_bins: int, sample_rows: int = 10000):
+    """Bernoulli weights [keep, drop] of the findSplits row sample (None = every row).  Like
+    Spark's ``findSplits`` (``input.sample(false, fraction)``, fraction = max(maxBins^2,
+    10000) / N) the sample is a Bernoulli draw per row — here Philox keyed by (seed, global
+    row id), so the sample is the same for any sharding of the rows."""
+    if n_total <= sample_rows:
+        return None
+    frac = min(1.0, max(sample_rows, max_bins * max_bins) / float(n_total))
+    return [frac, 1.0 - frac]
+
+
+def threshold_sample_mask(N: int, max_bins: int, sample_rows: int = 10000, seed: int = 0, row_offset: int = 0,
+                          n_total: int = None, device=None):
+    """Rows [row_offset, row_offset + N) of an ``n_total``-row table kept by the findSplits
+    sample: bool numpy [N] (device=None) or a device bool tensor (HIP Philox kernel)."""
+    w = threshold_sample_weights(N if n_total is None else n_total, max_bins, sample_rows)
+    if w is None:
+        return None
+    if device is not None and torch.device(device).type == "cuda":
+        return rng.device_buckets(seed, rng.STREAM_FINDSPLITS, row_offset, N, w, device) == 0
+    rows = np.arange(row_offset, row_offset + N, dtype=np.uint64)
+    m = rng.assign_buckets(seed, rng.STREAM_FINDSPLITS, rows, w) == 0
+    return m if device is None else torch.from_numpy(m).to(device)
+
+
+def find_thresholds(X: np.ndarray, max_bins: int, sample_rows: int = 10000, seed: int = 0, row_offset: int = 0,
+                    n_total: int = None):
+    """List of float32 threshold arrays (``x <= thr[b]`` goes left at split b).  NumPy
+    oracle of ``find_thresholds_device``."""
     N, F = X.shape
-    if N > sample_rows:  # Spark samples max(maxBins^2, 10000) rows for findSplits
-        rs = np.random.default_rng(seed)
-        X = X[np.sort(rs.choice(N, size=max(sample_rows, max_bins * max_bins), replace=False))]
+    keep = threshold_sample_mask(N, max_bins, sample_rows, seed, row_offset, n_total)
+    if keep is not None:
+        X = X[keep]
     out = []
     n_splits = max_bins - 1
     for f in range(F):
@@ -54,6 +81,63 @@ def find_thresholds(X: np.ndarray, max_bins: int, sample_rows: int = 10000, seed
             thr = (u[idx] + u[idx + 1]) / 2.0
         out.append(thr.astype(np.float32))
     return out
+
+
+def find_thresholds_device(X: torch.Tensor, max_bins: int, sample_rows: int = 10000, seed: int = 0,
+                           row_offset: int = 0, n_total: int = None):
+    """``find_thresholds`` on the tensor's device, threshold for threshold identical to the
+    NumPy version (same Philox row sample, same fp32 midpoints, same fp64 quantile targets).
+
+    The sampled rows are compacted (one size sync); one sort of their columns [F, n] puts
+    NaN last, distinct values are the run starts, and the quantile target t of
+    the host version (first distinct value whose cumulative count reaches t) is the distinct
+    value at sorted position ceil(t) - 1.  Every feature's thresholds come back in ONE
+    [F, max_bins - 1] device -> host copy."""
+    N, F = X.shape
+    Xs = X.float()
+    keep_rows = threshold_sample_mask(N, max_bins, sample_rows, seed, row_offset, n_total, device=X.device)
+    if keep_rows is not None:  # compact the ~10k sampled rows (one size sync) before the sort
+        Xs = Xs[keep_rows]
+    n = Xs.shape[0]
+    ns = max_bins - 1
+    if n == 0 or ns <= 0:
+        return [np.zeros(0, dtype=np.float32) for _ in range(F)]
+    s = torch.sort(Xs.t().contiguous(), dim=1).values  # [F, n], NaN sorted last
+    nvalid = (~torch.isnan(s)).sum(1)  # [F]
+    pos = torch.arange(n, device=X.device)
+    valid = pos.view(1, n) < nvalid.view(F, 1)
+    newd = torch.ones_like(valid)
+    newd[:, 1:] = s[:, 1:] != s[:, :-1]
+    newd &= valid
+    drank = torch.cumsum(newd.to(torch.int64), 1) - 1  # distinct index of every sorted position
+    ndist = newd.sum(1)  # [F]
+    U = torch.zeros(F, n + 1, dtype=s.dtype, device=X.device)  # distinct values, compacted
+    U.scatter_(1, torch.where(newd, drank, torch.full_like(drank, n)), s)
+    k = torch.arange(ns, device=X.device)
+    # few distinct values: every midpoint (j = 0 .. ndist - 2)
+    few = (ndist - 1) <= ns
+    # quantile cut points: t = total * (k + 1) / (ns + 1) (fp64, as in NumPy), j = distinct index
+    # of sorted position ceil(t) - 1, clipped to [0, ndist - 2]
+    t = nvalid.double().view(F, 1) * (k + 1).double().view(1, ns) / (ns + 1)
+    q = (torch.ceil(t).to(torch.int64) - 1).clamp(0, n - 1)
+    jq = torch.gather(drank, 1, q)
+    jq = torch.minimum(jq, (ndist - 2).clamp_min(0).view(F, 1)).clamp_min(0)
+    J = torch.where(few.view(F, 1), k.view(1, ns).expand(F, ns), jq)
+    keep = torch.where(few.view(F, 1), k.view(1, ns) < (ndist - 1).view(F, 1),
+                       torch.ones(F, ns, dtype=torch.bool, device=X.device))
+    keep[:, 1:] &= few.view(F, 1) | (J[:, 1:] != J[:, :-1])  # np.unique of the (sorted) cut indices
+    keep &= (ndist > 1).view(F, 1)
+    thr = (torch.gather(U, 1, J) + torch.gather(U, 1, J + 1)) / 2.0
+    packed = torch.cat([thr, keep.to(thr.dtype)], 1).cpu().numpy()  # the one device -> host copy
+    thr_h, keep_h = packed[:, :ns], packed[:, ns:] > 0.5
+    return [thr_h[f][keep_h[f]].astype(np.float32) for f in range(F)]
+
+
+def thresholds_for(X: torch.Tensor, max_bins: int, sample_rows: int = 10000, seed: int = 0):
+    """findSplits where the data lives: the device version for GPU tensors, NumPy otherwise."""
+    if X.is_cuda:
+        return find_thresholds_device(X.detach(), max_bins, sample_rows, seed)
+    return find_thresholds(X.detach().float().cpu().numpy(), max_bins, sample_rows, seed)
 
 
 def bin_features(X: np.ndarray, thresholds) -> np.ndarray:
@@ -232,6 +316,8 @@ def hist_split_native(bins, nbins_feat, label, rows, row_w, node_start, node_cou
 
 
 def _best_chunk(gain, feat, bin_, left, total, A, chunks, K) -> LevelResult:
+    if chunks == 1:  # every sampled feature in one workgroup: the kernel's winner is the node's
+        return LevelResult(gain=gain, feat=feat, bin=bin_, left=left.view(A, K), total=total)
     gain, feat, bin_, left = gain.view(A, chunks), feat.view(A, chunks), bin_.view(A, chunks), left.view(A, chunks, K)
     best = torch.argmax(gain, dim=1)  # first max -> lowest chunk (lowest feature slot) on ties
     ar = torch.arange(A, device=gain.device)

@@ -60,21 +60,36 @@ def fit_logreg_dp(estimator, X_shard, y_shard, specs, num_classes, ctx: DistCont
 
 def global_thresholds(X_shard: torch.Tensor, max_bins: int, ctx: DistContext, sample_rows: int = 10000,
                       seed: int = 0):
-    """findSplits over a sample gathered from every rank (Spark samples the whole
-    RDD); rank 0 computes, everybody receives the same thresholds."""
-    Xh = X_shard.detach().float().cpu().numpy()
+    """findSplits over the whole (sharded) table, as Spark samples the whole RDD.
+
+    The sample is a Philox Bernoulli draw keyed by global row id (``T.threshold_sample_mask``),
+    so it is the single-process sample for any world size.  Each rank keeps its sampled rows,
+    one all-gather (sizes first: shards may differ) puts the union — in global row order — on
+    every rank, and every rank runs the device findSplits on it: the same thresholds as a
+    single process, on every rank, without a broadcast."""
+    X = X_shard.detach().float()
     if not ctx.is_distributed:
-        return T.find_thresholds(Xh, max_bins, sample_rows, seed)
-    per = max(1, sample_rows // ctx.world_size)
-    rs = np.random.default_rng(seed + ctx.rank)
-    take = Xh[np.sort(rs.choice(Xh.shape[0], size=min(per, Xh.shape[0]), replace=False))]
-    parts = [None] * ctx.world_size
-    dist.all_gather_object(parts, take, group=ctx.group)
-    out = [None]
-    if ctx.rank == 0:
-        out[0] = T.find_thresholds(np.concatenate(parts, 0), max_bins, sample_rows, seed)
-    dist.broadcast_object_list(out, src=0, group=ctx.group)
-    return out[0]
+        return T.thresholds_for(X, max_bins, sample_rows, seed)
+    P = ctx.world_size
+
+    def gather_sizes(v: int):
+        t = torch.tensor([v], dtype=torch.int64, device=X.device)
+        out = [torch.empty_like(t) for _ in range(P)]
+        dist.all_gather(out, t, group=ctx.group)
+        return [int(o.item()) for o in out]
+
+    shard_rows = gather_sizes(X.shape[0])
+    n_total, row0 = sum(shard_rows), sum(shard_rows[:ctx.rank])
+    keep = T.threshold_sample_mask(X.shape[0], max_bins, sample_rows, seed, row0, n_total, device=X.device)
+    take = X if keep is None else X[keep]
+    counts = gather_sizes(take.shape[0])
+    buf = torch.zeros(max(counts), X.shape[1], dtype=X.dtype, device=X.device)
+    buf[:take.shape[0]] = take
+    parts = [torch.empty_like(buf) for _ in range(P)]
+    dist.all_gather(parts, buf, group=ctx.group)
+    sample = torch.cat([p[:c] for p, c in zip(parts, counts)], 0)
+    # already sampled: no second draw (n_total <= sample_rows disables it)
+    return T.thresholds_for(sample, max_bins, sample_rows=max(sample_rows, sample.shape[0]), seed=seed)
 
 
 class NodeOwner:
@@ -141,7 +156,7 @@ def fit_forest_tree_parallel(estimator, X, y, num_classes: int, ctx: DistContext
     T_, P, r = estimator.numTrees, ctx.world_size, ctx.rank
     lo, hi = (T_ * r) // P, (T_ * (r + 1)) // P
     if thresholds is None:
-        thresholds = T.find_thresholds(X.detach().float().cpu().numpy(), estimator.maxBins, seed=estimator.seed)
+        thresholds = T.thresholds_for(X, estimator.maxBins, seed=estimator.seed)
     part = estimator.fit_tensors(X, y, num_classes, thresholds=thresholds, tree_offset=lo, num_trees=hi - lo)
     if not ctx.is_distributed:
         return part

@@ -222,12 +222,13 @@ def bench_rf(args, ctx, nine_axis=False):
         Xt = Xt[:, :N_FEATURES].contiguous()
     est = RandomForestClassifier(numTrees=args.trees or (500 if nine_axis else 100), maxDepth=args.depth,
                                  maxBins=32, seed=7, device=dev)
-    thr = dp.global_thresholds(X, 32, ctx, seed=7)
     model = {}
 
     owner = dp.NodeOwner(ctx) if (args.rf_reduce == "owner" and ctx.is_distributed) else None
 
     def run(i):
+        # the whole fit is timed, findSplits included (sample all-gather + device sort + binning)
+        thr = dp.global_thresholds(X, 32, ctx, seed=7)
         model["m"] = est.fit_tensors(X, y, K, allreduce=None if owner else dp.allreduce_sum(ctx),
                                      row_offset=rank * n_local, thresholds=thr, owner=owner)
 

@@ -414,3 +414,21 @@ def test_mlp_bwd_l1_matches_gemms(cuda, monkeypatch, F):
         a, b = L.view(ga, s.name), L.view(gb, s.name)
         rel = float((a - b).norm() / b.norm().clamp_min(1e-12))
         assert rel < 1e-2, f"{s.name}: {rel:.3e}"
+
+
+def test_find_thresholds_device_matches_numpy():
+    """Device findSplits (HIP Philox sample mask + one sort) == the NumPy oracle on the host."""
+    import numpy as np
+
+    from har.ops import tree as T
+
+    g = torch.Generator().manual_seed(3)
+    X = torch.randn(60000, 13, generator=g)
+    X[:, 1] = torch.round(X[:, 1] * 3)        # few distinct values
+    X[torch.rand(60000, generator=g) < 0.2, 2] = float("nan")
+    X[:, 3] = 2.0                             # constant column
+    for row0, n_total in ((0, None), (120000, 480000)):
+        a = T.find_thresholds(X.numpy(), 32, seed=5, row_offset=row0, n_total=n_total)
+        b = T.find_thresholds_device(X.cuda(), 32, seed=5, row_offset=row0, n_total=n_total)
+        for f in range(X.shape[1]):
+            assert np.array_equal(a[f], b[f]), f

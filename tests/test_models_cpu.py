@@ -204,3 +204,37 @@ def test_crossvalidator_trees(wisdm_split):
                         numFolds=5, seed=3).fit(train)
     assert len(cv.avgMetrics) == 2 and cv.bestIndex == 1 and cv.avgMetrics[1] > 0.6
     assert _acc(cv, test) > 0.6
+
+
+def test_find_thresholds_device_equals_numpy():
+    """Device findSplits (one sort of the sampled columns) == the NumPy oracle, threshold for
+    threshold: ties, NaNs, constant columns, few / many distinct values, sampled and not."""
+    rng = np.random.default_rng(0)
+    for trial in range(24):
+        N, F = int(rng.integers(1, 25000)), int(rng.integers(1, 10))
+        X = rng.normal(size=(N, F)).astype(np.float32)
+        for f in range(F):
+            if trial % 4 == 1:
+                X[:, f] = np.round(X[:, f] * rng.integers(1, 20))
+            if trial % 4 == 2:
+                X[rng.random(N) < 0.3, f] = np.nan
+            if trial % 4 == 3 and f == 0:
+                X[:, f] = 1.0
+        mb = int(rng.choice([2, 4, 16, 32, 64]))
+        a = T.find_thresholds(X, mb, 10000, seed=trial)
+        b = T.find_thresholds_device(torch.from_numpy(X), mb, 10000, seed=trial)
+        for f in range(F):
+            assert b[f].dtype == np.float32 and np.array_equal(a[f], b[f]), (trial, f)
+
+
+def test_threshold_sample_is_shard_invariant():
+    """The findSplits row sample is keyed by global row id: the shards' samples concatenate
+    into the single-process sample, and its size is close to max(maxBins^2, 10000)."""
+    N = 60000
+    full = T.threshold_sample_mask(N, 32, 10000, seed=7)
+    bounds = [0, 7001, 30000, 45555, N]
+    parts = [T.threshold_sample_mask(b - a, 32, 10000, seed=7, row_offset=a, n_total=N)
+             for a, b in zip(bounds[:-1], bounds[1:])]
+    assert np.array_equal(full, np.concatenate(parts))
+    assert 9500 < full.sum() < 10500
+    assert T.threshold_sample_mask(9000, 32, 10000) is None
