@@ -159,3 +159,20 @@ def test_predict_cli_from_saved_models(tmp_path, wisdm_csv):
     with open(tmp_path / "q.csv") as f:
         q = list(csv.reader(f))
     assert [r[2] for r in q[1:]] == [r[2] for r in rows[1:201]]
+
+
+def test_plots_hexbin_grid_and_scatter_matrix(tmp_path, wisdm_csv):
+    """C29 (main.py:686-710): a seeded 10% sample, one hexbin PNG per ordered column pair
+    ("Fig <x>_<y>.png") and Scatter_Matrix.png."""
+    from har.data.csv_io import read_csv
+    from har.report.plots import sample_numeric, write_plots
+
+    t = read_csv(wisdm_csv)
+    cols = ["YAVG", "ZAVG", "RESULTANT"]
+    df = sample_numeric(t, cols, 0.1, seed=3)
+    assert 400 < len(df) < 700 and list(df.columns) == cols
+    written = write_plots(t, cols, str(tmp_path / "plot"), seed=3)
+    names = sorted(os.path.basename(p) for p in written)
+    assert "Scatter_Matrix.png" in names and "Fig YAVG_ZAVG.png" in names
+    assert len([n for n in names if n.startswith("Fig ")]) == len(cols) ** 2
+    assert all(os.path.getsize(p) > 1000 for p in written)
