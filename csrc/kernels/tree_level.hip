@@ -311,32 +311,66 @@ __global__ __launch_bounds__(256) void tree_level_decide_kernel(int A, const flo
 
 // ---- device-resident frontier: the level's split bookkeeping without host numpy ------------
 // Exclusive scan of (flags > 0) over n entries (n = n_mul * *n_dev when n_dev is given) in
-// one workgroup; out[n] = total.
+// one workgroup; out[n] = total.  Tiles of 1024 x 8 entries: each thread reads its 8
+// consecutive flags as two 16-byte loads (scalar loads only in the ragged last tile, so no
+// load passes n), a wave shuffle scan + 16 wave sums give the exclusive prefix, and the
+// tile total carries into the next tile.
 __global__ __launch_bounds__(1024) void frontier_scan_kernel(const float* __restrict__ flags, int n_static,
                                                              const int32_t* __restrict__ n_dev, int n_mul,
                                                              int32_t* __restrict__ out) {
+  constexpr int PT = 8, TILE = 1024 * PT;
   __shared__ int32_t wsum[16];
   const int n = n_dev ? n_mul * (*n_dev) : n_static;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int per = (n + 1023) / 1024;
-  const int b = tid * per, e = b + per < n ? b + per : n;
-  int s = 0;
-  for (int i = b; i < e; ++i) s += flags[i] > 0.f;
-  int x = s;
+  int carry = 0;
+  for (int base = 0; base < n; base += TILE) {
+    const int i0 = base + tid * PT;
+    int v[PT];
+    if (i0 + PT <= n) {
+      const float4 f0 = *reinterpret_cast<const float4*>(flags + i0);
+      const float4 f1 = *reinterpret_cast<const float4*>(flags + i0 + 4);
+      v[0] = f0.x > 0.f; v[1] = f0.y > 0.f; v[2] = f0.z > 0.f; v[3] = f0.w > 0.f;
+      v[4] = f1.x > 0.f; v[5] = f1.y > 0.f; v[6] = f1.z > 0.f; v[7] = f1.w > 0.f;
+    } else {
 #pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const int y = __shfl_up(x, o, 64);
-    if (lane >= o) x += y;
+      for (int j = 0; j < PT; ++j) v[j] = (i0 + j < n) ? (flags[i0 + j] > 0.f) : 0;
+    }
+    int s = 0;
+#pragma unroll
+    for (int j = 0; j < PT; ++j) s += v[j];
+    int x = s;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int y = __shfl_up(x, o, 64);
+      if (lane >= o) x += y;
+    }
+    if (lane == 63) wsum[w] = x;
+    __syncthreads();
+    int run = carry + x - s, tot = 0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const int ws = wsum[k];
+      run += k < w ? ws : 0;
+      tot += ws;
+    }
+    __syncthreads();  // wsum is rewritten by the next tile
+    int r[PT];
+#pragma unroll
+    for (int j = 0; j < PT; ++j) {
+      r[j] = run;
+      run += v[j];
+    }
+    if (i0 + PT <= n) {
+      *reinterpret_cast<int4*>(out + i0) = make_int4(r[0], r[1], r[2], r[3]);
+      *reinterpret_cast<int4*>(out + i0 + 4) = make_int4(r[4], r[5], r[6], r[7]);
+    } else {
+#pragma unroll
+      for (int j = 0; j < PT; ++j)
+        if (i0 + j < n) out[i0 + j] = r[j];
+    }
+    carry += tot;
   }
-  if (lane == 63) wsum[w] = x;
-  __syncthreads();
-  int run = x - s;
-  for (int i = 0; i < w; ++i) run += wsum[i];
-  for (int i = b; i < e; ++i) {
-    out[i] = run;
-    run += flags[i] > 0.f;
-  }
-  if (tid == 1023) out[n] = run;
+  if (tid == 0) out[n] = carry;
 }
 
 // Per candidate a that splits (slot p = pos[a]): its commit record (tree, node, left child id,
@@ -493,6 +527,8 @@ extern "C" int har_tree_frontier(int A, int Tn, int maxn, const int32_t* ct, con
                                  int32_t* ct_next, int32_t* cn_next, int32_t* tlo_next, int32_t* cand_idx,
                                  int32_t* scal, hipStream_t s) {
   if (A <= 0) return -2;
+  // frontier_scan_kernel reads / writes 16-byte vectors from these bases
+  if (((uintptr_t)dec | (uintptr_t)front | (uintptr_t)pos_ws | (uintptr_t)q_ws) & 15) return -3;
   hipError_t err = hipMemsetAsync(scal, 0, 4 * sizeof(int32_t), s);
   if (err != hipSuccess) return (int)err;
   frontier_scan_kernel<<<1, 1024, 0, s>>>(dec, A, nullptr, 1, pos_ws);
