@@ -44,7 +44,7 @@ from .table import Column, Table
 CHUNK = 4096  # bytes per workgroup of csv_count_newlines / csv_newline_pos
 INT32_MAX = 2 ** 31 - 1
 INT32_MIN = -(2 ** 31)
-F_NONEMPTY, F_INT, F_FLOAT, F_QUOTED = 1, 2, 4, 8
+F_NONEMPTY, F_INT, F_FLOAT, F_QUOTED, F_INEXACT = 1, 2, 4, 8, 16
 
 
 def _unquote(raw: bytes, quoted: bool) -> str:
@@ -218,11 +218,23 @@ def parse_csv_device(raw: bytes, device="cuda", header: bool = True) -> DeviceCs
         mod.csv_parse_rows(buf.data_ptr(), starts.data_ptr(), ends.data_ptr(), nrows, ncols, vals.data_ptr(),
                            hashes.data_ptr(), flags.data_ptr(), fstart.data_ptr(), flen.data_ptr(),
                            _native.stream_ptr(dev))
-    kinds = _infer_kinds(vals, flags)
+    kinds, n_inexact = _infer_kinds(vals, flags)
+    if n_inexact:
+        _fix_inexact(raw, vals, flags, fstart, flen)
     return DeviceCsv(raw, buf, names, kinds, vals, hashes, flags, fstart, flen)
 
 
-def _infer_kinds(vals: torch.Tensor, flags: torch.Tensor) -> List[str]:
+def _fix_inexact(raw: bytes, vals: torch.Tensor, flags: torch.Tensor, fstart: torch.Tensor, flen: torch.Tensor):
+    """Fields the kernel's fast path cannot round exactly (mantissa > 2^53 or |exp| > 22, bit
+    F_INEXACT) are re-parsed on the host with ``float`` (strtod) — rare, so few bytes move."""
+    idx = torch.nonzero(((flags & F_INEXACT) != 0).reshape(-1)).squeeze(1)
+    st = fstart.reshape(-1)[idx].cpu().numpy()
+    ln = flen.reshape(-1)[idx].cpu().numpy()
+    fixed = torch.tensor([float(raw[a:a + b].decode("ascii")) for a, b in zip(st, ln)], dtype=torch.float64)
+    vals.view(-1)[idx] = fixed.to(vals.device)
+
+
+def _infer_kinds(vals: torch.Tensor, flags: torch.Tensor):
     """Per-column type votes as device reductions (one host transfer of [ncols, 4])."""
     ne = (flags & F_NONEMPTY) != 0
     isint = (flags & F_INT) != 0
@@ -234,16 +246,17 @@ def _infer_kinds(vals: torch.Tensor, flags: torch.Tensor) -> List[str]:
     fits32 = (vals <= INT32_MAX) & (vals >= INT32_MIN)
     overflow32 = (isint & ~fits32).any(1)
     non_int = non_int | (isint & big).any(1)
-    votes = torch.stack([any_ne, non_float, non_int, overflow32], 1).cpu().numpy()
+    inexact = ((flags & F_INEXACT) != 0).sum(1)
+    votes = torch.stack([any_ne, non_float, non_int, overflow32, inexact.bool()], 1).cpu().numpy()
     kinds = []
-    for a, nf, ni, ov in votes:
+    for a, nf, ni, ov, _ in votes:
         if not a or nf:
             kinds.append("string")
         elif not ni:
             kinds.append("long" if ov else "int")
         else:
             kinds.append("double")
-    return kinds
+    return kinds, int(votes[:, 4].sum())
 
 
 def read_numeric_device(path: str, columns: List[str], device="cuda") -> Dict[str, torch.Tensor]:

@@ -669,7 +669,10 @@ class MultilayerPerceptronClassifier(Estimator, ClassifierParams):
             from ..utils.checkpoint import Checkpointer
 
             ckpt = Checkpointer(self.checkpointDir, rank=rank)
-            last = ckpt.latest()
+            fp = {"layers": list(layers), "seed": self.seed, "batch": B, "world_size": world_size,
+                  "stepSize": self.stepSize, "weightDecay": self.weightDecay, "rows": int(N),
+                  "steps_per_epoch": steps_per_epoch, "standardize": bool(self.standardize)}
+            last = ckpt.latest(fingerprint=fp)
             if last is not None:  # resume: parameters, Adam moments, step counter, data position
                 state, meta = last
                 eng.load_state(state)
@@ -687,7 +690,8 @@ class MultilayerPerceptronClassifier(Estimator, ClassifierParams):
                 eng.train_step(Xe[s * B:(s + 1) * B], ye[s * B:(s + 1) * B], global_batch)
                 if ckpt is not None and self.checkpointInterval and (gstep + 1) % self.checkpointInterval == 0:
                     nxt_e, nxt_s = (epoch, s + 1) if s + 1 < steps_per_epoch else (epoch + 1, 0)
-                    ckpt.save(gstep + 1, eng.state_tensors(), {"epoch": nxt_e, "step_in_epoch": nxt_s})
+                    ckpt.save(gstep + 1, eng.state_tensors(), {"epoch": nxt_e, "step_in_epoch": nxt_s},
+                              fingerprint=fp)
         model = MultilayerPerceptronClassificationModel(eng, uid=self.uid)
         model.mean, model.inv_std = mean, inv_std
         return model

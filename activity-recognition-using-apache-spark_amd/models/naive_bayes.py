@@ -3,7 +3,9 @@ north star; not in the reference script).  API and math follow Spark ML's
 ``NaiveBayes(smoothing=1.0, modelType="multinomial")``.
 
 Fitting is one pass of class-conditional moments: counts, sum x and sum x^2
-per class are two products ``onehot(y)^T . [X, X^2]`` — on the GPU
+per class are two products ``onehot(y)^T . [X, X^2]``; the
+Gaussian model adds a second pass over the centred rows ``x - mu_y`` so its
+variances are two-pass accurate — on the GPU
 an exact-fp32 MFMA split-K GEMM (``har_gemm_f32``).  Scoring is a GEMM as well:
 ``raw = [X, X^2] . Theta^T + b``.
 """
@@ -145,7 +147,14 @@ class NaiveBayes(Estimator, ClassifierParams):
         else:
             pi = torch.log(n / N)
             mu = s1 / n.clamp_min(1)[:, None]
-            var = (s2 / n.clamp_min(1)[:, None] - mu * mu).clamp_min(0)
+            # second pass over the rows: centred moments sum_i w_i (x_i - mu_{y_i})^2, so the
+            # variance does not cancel the way E[x^2] - mu^2 does for large-mean features
+            D = X.float() - mu.float()[y.long()]
+            _, _, c2 = class_moments(D, y, K, w)
+            c2 = c2.double()
+            if allreduce is not None:
+                allreduce(c2)
+            var = (c2 / n.clamp_min(1)[:, None]).clamp_min(0)
             eps = 1e-9 * float(var.max()) if var.numel() else 1e-9
             # global variance floor (sklearn/Spark style epsilon) keeps constant features finite
             var = var + max(eps, 1e-12)

@@ -760,15 +760,26 @@ class RandomForestClassifier(_TreeEstimatorBase):
         # ids key the bootstrap and feature-subset streams, so the slices concatenate into the forest
         total = self.numTrees if num_trees is None else int(num_trees)
         wave = tree_wave if tree_wave and tree_wave < total else total
+        # (tree, row) slots of one lock-step build are int32-indexed on the device
+        # (tree_level.hip row lists / scans): cap a wave at 2^31 - 1 slots
+        max_wave = max(1, (2 ** 31 - 1) // max(1, X.shape[0]))
+        if wave > max_wave:
+            wave = max_wave
         ckpt = None
         parts: List[ForestArrays] = []
+        fp = {"numTrees": total, "tree_offset": tree_offset, "seed": self.seed, "maxDepth": self.maxDepth,
+              "maxBins": self.maxBins, "minInstancesPerNode": self.minInstancesPerNode,
+              "minInfoGain": self.minInfoGain, "impurity": self.impurity, "strategy": str(strategy),
+              "subsamplingRate": self.subsamplingRate, "rows": int(X.shape[0]), "features": int(X.shape[1]),
+              "classes": int(K), "row_offset": int(row_offset)}
         if checkpoint_dir:
             from ..utils.checkpoint import Checkpointer
 
             ckpt = Checkpointer(checkpoint_dir, rank=rank)
-            last = ckpt.latest()
+            last = ckpt.latest(fingerprint=fp)
             if last is not None:
-                parts.append(_arrays_from_state(last[0]))
+                prev = _arrays_from_state(last[0])
+                parts.append(_slice_arrays(prev, 0, min(total, prev.feature.shape[0])))
         from ..utils.checkpoint import maybe_inject_fault
 
         done = sum(p.feature.shape[0] for p in parts)
@@ -783,7 +794,7 @@ class RandomForestClassifier(_TreeEstimatorBase):
             if ckpt is not None and done < total:
                 merged = _concat_arrays(parts)
                 parts = [merged]
-                ckpt.save(done, _arrays_state(merged), {"trees": done})
+                ckpt.save(done, _arrays_state(merged), {"trees": done}, fingerprint=fp)
         arrs = _concat_arrays(parts) if len(parts) > 1 else parts[0]
         return RandomForestClassificationModel(arrs.to(X.device), X.shape[1], K, uid=self.uid, device=X.device)
 

@@ -26,16 +26,24 @@ def _import():
         if _MOD is not None or _ERR is not None:
             return _MOD
         try:
-            if os.environ.get("HAR_AUTOBUILD", "1") == "1":
-                import sys
-                root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-                tools = os.path.join(root, "tools")
+            import sys
+            root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+            tools = os.path.join(root, "tools")
+            bn = None
+            if os.path.isdir(os.path.join(root, "csrc")):
                 if tools not in sys.path:
                     sys.path.insert(0, tools)
-                import build_native  # type: ignore
-                if build_native.needs_build():
-                    build_native.build()
-            _MOD = importlib.import_module("har._har_native")
+                import build_native as bn  # type: ignore
+                if os.environ.get("HAR_AUTOBUILD", "1") == "1" and bn.needs_build():
+                    bn.build()
+            mod = importlib.import_module("har._har_native")
+            if bn is not None:  # the loaded binary must come from exactly these sources
+                want = bn.source_hash()
+                got = mod.source_hash() if hasattr(mod, "source_hash") else "none"
+                if got != want:
+                    raise RuntimeError(f"_har_native.so was built from other sources (hash {got}, tree {want}); "
+                                       "rebuild with python tools/build_native.py")
+            _MOD = mod
         except Exception as e:  # pragma: no cover
             _ERR = e
         return _MOD

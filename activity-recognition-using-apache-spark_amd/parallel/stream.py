@@ -15,7 +15,7 @@ the north-star raw-ingest path (BASELINE config 4).
 """
 from __future__ import annotations
 
-from typing import Optional, Tuple
+from typing import List, Optional, Tuple
 
 import torch
 import torch.distributed as dist
@@ -24,24 +24,36 @@ from ..features.window import WindowFeaturizer, window_count
 from .dist import DistContext
 
 
-def shard_offsets(ctx: DistContext, local_len: int, device) -> Tuple[int, int]:
-    """(global offset of this rank's shard, total samples) from an all-gather of shard lengths."""
+def shard_lengths(ctx: DistContext, local_len: int, device) -> List[int]:
+    """Every rank's shard length (one all-gather of one integer; one host read)."""
     if not ctx.is_distributed:
-        return 0, local_len
+        return [local_len]
     t = torch.tensor([local_len], dtype=torch.long, device=device)
-    allv = [torch.zeros_like(t) for _ in range(ctx.world_size)]
-    dist.all_gather(allv, t, group=ctx.group)
-    lens = [int(v.item()) for v in allv]
+    allv = torch.zeros(ctx.world_size, dtype=torch.long, device=device)
+    dist.all_gather_into_tensor(allv, t, group=ctx.group)
+    return [int(v) for v in allv.cpu().tolist()]
+
+
+def shard_offsets(ctx: DistContext, local_len: int, device, lens: Optional[List[int]] = None) -> Tuple[int, int]:
+    """(global offset of this rank's shard, total samples) from an all-gather of shard lengths."""
+    lens = lens if lens is not None else shard_lengths(ctx, local_len, device)
     return sum(lens[: ctx.rank]), sum(lens)
 
 
-def exchange_halo(ctx: DistContext, local: torch.Tensor, halo: int) -> torch.Tensor:
-    """Return the first ``halo`` samples of rank r+1's shard (empty on the last rank)."""
+def exchange_halo(ctx: DistContext, local: torch.Tensor, halo: int, lens: Optional[List[int]] = None) -> torch.Tensor:
+    """Return the first ``halo`` samples of rank r+1's shard (empty on the last rank).
+
+    Every rank validates EVERY shard length (from ``lens`` or one all-gather) before
+    any point-to-point op is posted, so a too-short shard makes all ranks raise
+    together instead of leaving its neighbours blocked in ``batch_isend_irecv``."""
     A = local.shape[1]
     if not ctx.is_distributed or halo == 0:
         return local.new_zeros(0, A)
-    if local.shape[0] < halo and ctx.rank > 0:
-        raise ValueError(f"shard of {local.shape[0]} samples is shorter than the halo ({halo})")
+    lens = lens if lens is not None else shard_lengths(ctx, local.shape[0], local.device)
+    short = [r for r in range(1, ctx.world_size) if lens[r] < halo]
+    if short:
+        raise ValueError(f"shard(s) of rank(s) {short} ({[lens[r] for r in short]} samples) are shorter than "
+                         f"the halo ({halo} samples)")
     ops = []
     recv = None
     if ctx.rank > 0:
@@ -61,9 +73,10 @@ def sharded_window_features(ctx: DistContext, local: torch.Tensor, featurizer: W
     Returns ``(features [n_owned, F], first_window)`` where ``first_window`` is the
     global index of the first owned window (labels / ids line up with it)."""
     W, st = featurizer.window, featurizer.stride
+    lens = shard_lengths(ctx, local.shape[0], local.device)
     if offset is None or total is None:
-        offset, total = shard_offsets(ctx, local.shape[0], local.device)
-    ext = torch.cat([local, exchange_halo(ctx, local, W - 1)], 0)
+        offset, total = shard_offsets(ctx, local.shape[0], local.device, lens)
+    ext = torch.cat([local, exchange_halo(ctx, local, W - 1, lens)], 0)
     p0 = -(-offset // st) * st                       # first window start inside the shard
     end = offset + local.shape[0]
     n_starts = max(0, -(-(end - p0) // st))

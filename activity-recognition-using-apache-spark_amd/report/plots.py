@@ -32,7 +32,6 @@ def write_plots(table: Table, cols: Sequence[str], out_dir: str, fraction: float
 
     matplotlib.use("Agg")
     import matplotlib.pyplot as plt
-    from pandas.plotting import scatter_matrix
 
     os.makedirs(out_dir, exist_ok=True)
     df = sample_numeric(table, cols, fraction, seed)
@@ -47,17 +46,32 @@ def write_plots(table: Table, cols: Sequence[str], out_dir: str, fraction: float
                 plt.close("all")
                 written.append(p)
     if scatter:
-        axs = scatter_matrix(df, diagonal="hist", alpha=0.2, figsize=(16, 16))
-        for i in range(n):
-            v = axs[i, 0]
-            v.yaxis.label.set_rotation(0)
-            v.yaxis.label.set_ha("right")
-            v.set_yticks(())
-            h = axs[n - 1, i]
-            h.xaxis.label.set_rotation(90)
-            h.set_xticks(())
-        p = os.path.join(out_dir, "Scatter_Matrix.png")
-        plt.savefig(p)
-        plt.close("all")
-        written.append(p)
+        written.append(_pair_grid(df, os.path.join(out_dir, "Scatter_Matrix.png"), plt))
     return written
+
+
+def _pair_grid(df, path: str, plt) -> str:
+    """n x n pair grid drawn directly with matplotlib: histograms on the diagonal,
+    translucent scatters elsewhere; only the outer row / column carry axis names
+    (horizontal on the left edge, vertical along the bottom) and no tick labels."""
+    names = list(df.columns)
+    n = len(names)
+    fig, grid = plt.subplots(n, n, figsize=(16, 16), squeeze=False)
+    vals = [df[c].to_numpy() for c in names]
+    for r in range(n):
+        for c in range(n):
+            ax = grid[r][c]
+            if r == c:
+                ax.hist(vals[c], bins=20, color="tab:blue")
+            else:
+                ax.scatter(vals[c], vals[r], s=2, alpha=0.2, color="tab:blue")
+            ax.set_xticks([])
+            ax.set_yticks([])
+            if c == 0:
+                ax.set_ylabel(names[r], rotation="horizontal", horizontalalignment="right")
+            if r == n - 1:
+                ax.set_xlabel(names[c], rotation="vertical")
+    fig.subplots_adjust(wspace=0, hspace=0)
+    fig.savefig(path)
+    plt.close(fig)
+    return path

@@ -95,8 +95,15 @@ static GemmParams make_gemm(u A, u B, u C, u bias, u mask, u rowsum, int M, int 
   return p;
 }
 
+#ifndef HAR_SOURCE_HASH
+#define HAR_SOURCE_HASH "unknown"
+#endif
+
 PYBIND11_MODULE(_har_native, m) {
   m.doc() = "har native runtime: host CSV parser + gfx950 HIP kernel launchers";
+  // content hash of every source / header / flag the library was built from (tools/build_native.py);
+  // ops/_native.py refuses a library whose hash differs from the tree it is imported from
+  m.def("source_hash", []() { return std::string(HAR_SOURCE_HASH); });
   m.def("csv_parse", &csv_parse, py::arg("data"), py::arg("header") = true, py::arg("threads") = 0);
 
   m.def("gemm", [](bool bf16, int layout, int epi, u A, u B, u C, u bias, u mask, u rowsum, int M, int N, int K,

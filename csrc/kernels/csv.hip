@@ -60,7 +60,8 @@ __device__ __forceinline__ double pow10i(int e) {
   return (e >= 0 && e <= 22) ? t[e] : pow(10.0, (double)e);
 }
 
-// flags: bit0 non-empty, bit1 int literal, bit2 float literal (ints included), bit3 quoted
+// flags: bit0 non-empty, bit1 int literal, bit2 float literal (ints included), bit3 quoted,
+// bit4 value not exactly representable by the fast path (host strtod fix-up)
 __device__ void parse_field(const uint8_t* p, int len, bool quoted, double* val, uint8_t* flags) {
   uint8_t f = len > 0 ? 1 : 0;
   if (quoted) f |= 8;
@@ -70,8 +71,11 @@ __device__ void parse_field(const uint8_t* p, int len, bool quoted, double* val,
   bool neg = false;
   if (p[0] == '+' || p[0] == '-') { neg = p[0] == '-'; i = 1; }
   if (len - i == 3 && p[i] == 'N' && p[i + 1] == 'a' && p[i + 2] == 'N') { *flags = f | 4; return; }
-  if (len - i == 8 && p[i] == 'I' && p[i + 1] == 'n' && p[i + 2] == 'f') {
-    *val = neg ? -INFINITY : INFINITY; *flags = f | 4; return;
+  if (len - i == 8) {  // exactly "Infinity" (the host parser's rule; "Infected" stays a string)
+    const char inf[8] = {'I', 'n', 'f', 'i', 'n', 'i', 't', 'y'};
+    bool is_inf = true;
+    for (int k = 0; k < 8; ++k) is_inf &= p[i + k] == (uint8_t)inf[k];
+    if (is_inf) { *val = neg ? -INFINITY : INFINITY; *flags = f | 4; return; }
   }
   uint64_t mant = 0;
   int digits = 0, sig = 0, exp10 = 0;
@@ -104,7 +108,10 @@ __device__ void parse_field(const uint8_t* p, int len, bool quoted, double* val,
   double v = (double)mant;
   v = exp10 >= 0 ? v * pow10i(exp10) : v / pow10i(-exp10);
   *val = neg ? -v : v;
-  *flags = f | 4 | (is_int ? 2 : 0);
+  // one correctly rounded multiply / divide of two exact doubles == strtod; otherwise (mantissa
+  // beyond 2^53 or |exp| > 22) bit 4 asks the host to re-parse this field with strtod
+  const bool exact = mant <= (1ull << 53) && exp10 <= 22 && exp10 >= -22;
+  *flags = f | 4 | (is_int ? 2 : 0) | (exact ? 0 : 16);
 }
 
 __global__ __launch_bounds__(256) void csv_parse_rows(const uint8_t* __restrict__ buf, const int64_t* __restrict__ starts,

@@ -43,72 +43,16 @@ from har.config import RunConfig, config_from_args  # noqa: E402
 from har.data.csv_io import read_csv  # noqa: E402
 from har.data.split import random_split  # noqa: E402
 from har.data.table import describe_text  # noqa: E402
-from har.evaluation.evaluators import (MulticlassClassificationEvaluator, RegressionEvaluator,  # noqa: E402
-                                       evaluate_all)
+from har.evaluation.evaluators import evaluate_all  # noqa: E402
 from har.features import wisdm  # noqa: E402
 from har.models.base import data_parallel, features_tensor, resolve_device  # noqa: E402
 from har.parallel import dist as hdist  # noqa: E402
-from har.models.logreg import LogisticRegression  # noqa: E402
-from har.models.mlp import MultilayerPerceptronClassifier  # noqa: E402
-from har.models.naive_bayes import NaiveBayes  # noqa: E402
-from har.models.tree import DecisionTreeClassifier, RandomForestClassifier  # noqa: E402
 from har.report import csvout  # noqa: E402
 from har.report.text import (BANNER_CLASSIFY, BANNER_PIPELINE, BANNER_TRAIN, RunLog, evaluation_block,  # noqa: E402
                              model_header, section)
-from har.tuning.crossval import CrossValidator, ParamGridBuilder  # noqa: E402
+from har.suite import build_estimator, warm_up_device  # noqa: E402
 from har.utils import persist  # noqa: E402
 from har.utils.timing import PhaseTimer, device_sync  # noqa: E402
-
-
-def cv_evaluator(metric: str):
-    if metric in ("mae", "rmse", "mse", "r2"):
-        return RegressionEvaluator(labelCol="label", predictionCol="prediction", metricName=metric)
-    return MulticlassClassificationEvaluator(labelCol="label", predictionCol="prediction", metricName=metric)
-
-
-def build_estimator(name: str, cfg: RunConfig, dev, n_features: int, n_classes: int):
-    lr = LogisticRegression(maxIter=cfg.lr_max_iter, regParam=cfg.lr_reg, elasticNetParam=cfg.lr_elastic_net,
-                            device=dev)
-    dt = DecisionTreeClassifier(featuresCol="features", labelCol="label", maxDepth=cfg.dt_max_depth,
-                                maxBins=cfg.max_bins, device=dev)
-    rf = RandomForestClassifier(featuresCol="features", labelCol="label", numTrees=cfg.rf_num_trees,
-                                maxDepth=cfg.rf_max_depth, maxBins=cfg.max_bins, seed=cfg.seed, device=dev)
-    if name == "lr":
-        return lr
-    if name == "dt":
-        return dt
-    if name == "rf":
-        return rf
-    if name == "nb":
-        return NaiveBayes(modelType=cfg.nb_model_type, device=dev)
-    if name == "mlp":
-        return MultilayerPerceptronClassifier(layers=[n_features] + list(cfg.mlp_hidden) + [n_classes],
-                                              maxIter=cfg.mlp_epochs, blockSize=cfg.mlp_batch, stepSize=cfg.mlp_lr,
-                                              seed=cfg.seed, device=dev)
-    if name.endswith("cv"):
-        base = build_estimator(name[:-2], cfg, dev, n_features, n_classes)
-        grid = ParamGridBuilder()
-        if name == "lrcv":
-            grid = grid.addGrid("regParam", cfg.cv_reg_grid).addGrid("elasticNetParam", cfg.cv_en_grid)
-        return CrossValidator(estimator=base, estimatorParamMaps=grid.build(), evaluator=cv_evaluator(cfg.cv_metric),
-                              numFolds=cfg.cv_folds, seed=cfg.seed)
-    raise ValueError(f"unknown classifier {name}")
-
-
-def warm_up_device(dev, train, cfg: RunConfig):
-    """Load the HIP code objects and warm the allocator outside the timed regions — the
-    analogue of the reference's SparkContext start-up, which its timers also exclude
-    (``Main/main.py:8-9`` vs the ``time()`` brackets at ``:116-124``)."""
-    small = train.head(min(256, train.count()))
-    n_classes = len(train["label"].meta["vocab"])
-    for name in cfg.classifiers:
-        base = name[:-2] if name.endswith("cv") else name
-        est = build_estimator(base, cfg, dev, small["features"].data.shape[1], n_classes)
-        for attr, v in (("maxIter", 2), ("numTrees", 2)):
-            if hasattr(est, attr):
-                setattr(est, attr, v)
-        est.fit(small).predict_all(features_tensor(small, "features", dev))
-    device_sync(dev)
 
 
 def run(cfg: RunConfig, ctx=None) -> dict:
@@ -160,6 +104,8 @@ def run(cfg: RunConfig, ctx=None) -> dict:
     if dev.type == "cuda":
         with timer.phase("device_warmup"):
             warm_up_device(dev, train, cfg)
+        # not part of any "trained in" time below (the reference's timers exclude SparkContext start-up too)
+        log.print("Device warm-up (HIP code objects, allocator) %.6f seconds" % timer.get("device_warmup"))
     log.print(BANNER_CLASSIFY)
     n_features = df["features"].data.shape[1]
     vocab = df["label"].meta["vocab"]
@@ -171,10 +117,10 @@ def run(cfg: RunConfig, ctx=None) -> dict:
         est = build_estimator(name, cfg, dev, n_features, n_classes)
         with timer.phase(f"fit:{name}"), data_parallel(ctx):
             model = est.fit(train)
-        train_s = round(timer.get(f"fit:{name}"), 3)
+        train_s = round(timer.get(f"fit:{name}"), 6)  # us resolution: sub-ms fits do not print as 0
         with timer.phase(f"predict:{name}"):
             raw_pred, prob, pred = (model.bestModel if hasattr(model, "bestModel") else model).predict_all(X_test)
-        test_s = round(timer.get(f"predict:{name}"), 3)
+        test_s = round(timer.get(f"predict:{name}"), 6)
         label = str(model) + (" for Logistic Regression" if name == "lrcv" else "")
         model_header(log, label, train_s, test_s)
         preds = model.transform(test_data)

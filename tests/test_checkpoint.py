@@ -77,6 +77,24 @@ def test_checkpointer_keeps_latest(tmp_path):
     assert Checkpointer(str(tmp_path / "r1")).latest() is None
 
 
+def test_stale_checkpoint_of_another_fit_is_ignored(tmp_path):
+    """A checkpoint written by a forest with other parameters (here: more trees, another seed)
+    must not be resumed: the fit starts over and returns exactly the requested forest."""
+    g = torch.Generator().manual_seed(2)
+    y = torch.randint(0, 3, (600,), generator=g)
+    X = torch.randn(3, 8, generator=g)[y] * 2 + torch.randn(600, 8, generator=g)
+    ck = str(tmp_path / "ck")
+    RandomForestClassifier(numTrees=9, maxDepth=3, seed=1, device="cpu").fit_tensors(X, y, 3, tree_wave=3,
+                                                                                     checkpoint_dir=ck)
+    assert Checkpointer(ck).latest() is not None
+    with pytest.warns(UserWarning, match="different fit"):
+        m = RandomForestClassifier(numTrees=6, maxDepth=3, seed=2, device="cpu").fit_tensors(
+            X, y, 3, tree_wave=3, checkpoint_dir=ck)
+    fresh = RandomForestClassifier(numTrees=6, maxDepth=3, seed=2, device="cpu").fit_tensors(X, y, 3)
+    assert m.getNumTrees == 6
+    assert torch.equal(m.predict_all(X)[0], fresh.predict_all(X)[0])
+
+
 def test_rf_waves_equal_one_shot():
     g = torch.Generator().manual_seed(1)
     mu = torch.randn(3, 10, generator=g) * 2

@@ -143,3 +143,25 @@ def test_device_csv_matches_host(cuda, wisdm_csv, tmp_path):
                 np.testing.assert_array_equal(dev[c].data, host[c].data)
             else:
                 assert list(dev[c].data) == list(host[c].data), c
+
+
+@pytest.mark.gpu
+def test_device_csv_edge_tokens_match_host(cuda, tmp_path):
+    """'Infected' is a string (only the exact 'Infinity' is a number), and values outside the
+    kernel's exact fast path (17+ significant digits, |exp| > 22) equal strtod bit for bit."""
+    from har.data.csv_device import read_csv_device
+
+    path = str(tmp_path / "edge.csv")
+    with open(path, "wb") as f:
+        f.write(b"a,b,c\n"
+                b"1.2345678901234567891,Infected,3e-30\n"
+                b"9007199254740993,Infinity,1.7976931348623157e308\n"
+                b"-0.1000000000000000055511151231257827,-Infinity,4.9e-324\n")
+    host = read_csv(path, use_native=True)
+    dev = read_csv_device(path, cuda).to_table()
+    for c in host.columns:
+        assert dev[c].kind == host[c].kind, c
+        if host[c].kind == "double":
+            np.testing.assert_array_equal(dev[c].data, host[c].data)
+        else:
+            assert list(dev[c].data) == list(host[c].data), c

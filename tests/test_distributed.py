@@ -69,6 +69,17 @@ def _worker(rank, world, port, out_dir, what):
         local = S[:cut] if rank == 0 else S[cut:]
         feats, first = sharded_window_features(ctx, local, WindowFeaturizer(hz=20.0, seconds=10.0, overlap=0.5))
         res = torch.cat([torch.tensor([[float(first)] * feats.shape[1]]), feats])
+    elif what == "stream_short":
+        from har.features.window import WindowFeaturizer
+        from har.parallel.stream import sharded_window_features
+
+        S = _stream()
+        local = S[:2900] if rank == 0 else S[2900:]  # rank 1: 101 samples < halo of 199
+        try:
+            sharded_window_features(ctx, local, WindowFeaturizer(hz=20.0, seconds=10.0, overlap=0.5))
+            res = torch.tensor([0.0])
+        except ValueError:
+            res = torch.tensor([1.0])  # every rank must raise (none may block in the p2p exchange)
     else:
         from har.models.mlp import MLPEngine
 
@@ -138,6 +149,11 @@ def test_sharded_stream_halo_equals_single():
     got = torch.cat([o[1:] for o in outs])
     assert firsts[0] == 0 and firsts[1] == outs[0].shape[0] - 1  # contiguous window ids
     torch.testing.assert_close(got, full, equal_nan=True)
+
+
+def test_sharded_stream_short_shard_raises_on_every_rank():
+    outs = _run("stream_short")
+    assert [float(o[0]) for o in outs] == [1.0, 1.0]
 
 
 def _main_worker(rank, world, port, out_dir, argv):

@@ -159,6 +159,14 @@ def test_naive_bayes_vs_sklearn():
         NaiveBayes(modelType="multinomial").fit_tensors(x, y, 3)  # negative features
 
 
+def test_naive_bayes_gaussian_large_mean_variance():
+    """Two-pass variance: a feature offset by 1e4 (fp32 E[x^2]-mu^2 would lose ~all digits)."""
+    x, y = _blobs(600, 4, 3, seed=3)
+    g0 = NaiveBayes(modelType="gaussian").fit_tensors(x, y, 3)
+    g1 = NaiveBayes(modelType="gaussian").fit_tensors(x + 1.0e4, y, 3)
+    np.testing.assert_allclose(g1.sigma.numpy(), g0.sigma.numpy(), rtol=2e-3)
+
+
 def test_mlp_cpu_trains():
     x, y = _blobs(2048, 43, 6, seed=2)
     m = MultilayerPerceptronClassifier(layers=[43, 64, 64, 6], maxIter=15, blockSize=256, stepSize=3e-3,

@@ -8,11 +8,19 @@ linked with ``csrc/bind.cpp`` (pybind11) into
 ``har._har_native``.  The ``.so`` is git-ignored but travels to the GPU box with
 the gpurun snapshot.  No torch headers are involved, so a full rebuild takes
 well under a minute.
+
+Staleness is content based, not mtime based: every object records the SHA-256
+of its source, all headers and its flags (``<obj>.sha``), and the whole library
+embeds the hash of all of them (``source_hash()`` in the module), which
+``ops/_native.py`` compares with the tree at import time — a library built
+from other sources is rebuilt (or refused when auto-build is off), even if
+its file times look newer.
 """
 from __future__ import annotations
 
 import argparse
 import concurrent.futures as cf
+import hashlib
 import os
 import subprocess
 import sys
@@ -59,33 +67,67 @@ def _obj_for(src):
     return os.path.join(OBJ, rel + ".o")
 
 
-def _stale(target, deps):
-    if not os.path.exists(target):
-        return True
-    t = os.path.getmtime(target)
-    return any(os.path.getmtime(d) > t for d in deps)
+def _digest(paths, extra=()) -> str:
+    h = hashlib.sha256()
+    for p in paths:
+        h.update(os.path.relpath(p, ROOT).encode())
+        with open(p, "rb") as f:
+            h.update(f.read())
+    for e in extra:
+        h.update(str(e).encode())
+    return h.hexdigest()
+
+
+def _flag_key(flags) -> str:
+    """Compile flags without machine-specific absolute paths (the tree is checked out at a
+    different path on the GPU box, and the hash must still match there)."""
+    return " ".join("<path>" if f.startswith("/") else f for f in flags)
+
+
+def source_hash() -> str:
+    """Hash of every input of the library (sources, headers, compile flags, arch)."""
+    srcs = _sources()
+    return _digest(sorted(srcs + _headers()), [ARCH] + [_flag_key(_flags(s)) for s in srcs])[:32]
+
+
+def _read(p):
+    try:
+        with open(p) as f:
+            return f.read().strip()
+    except OSError:
+        return None
+
+
+def _stale(target, digest):
+    return not os.path.exists(target) or _read(target + ".sha") != digest
 
 
 def needs_build() -> bool:
-    srcs = _sources()
-    return _stale(OUT, srcs + _headers())
+    return _stale(OUT, source_hash())
 
 
 def build(verbose: bool = False, jobs: int = 8) -> str:
     os.makedirs(OBJ, exist_ok=True)
-    headers = _headers()
+    headers = sorted(_headers())
     srcs = _sources()
+    lib_hash = source_hash()
 
     def compile_one(src):
         obj = _obj_for(src)
-        if not _stale(obj, [src] + headers):
+        flags = _flags(src)
+        if src.endswith("bind.cpp"):
+            flags = flags + [f'-DHAR_SOURCE_HASH="{lib_hash}"']
+        digest = _digest([src] + headers, [ARCH, _flag_key(flags)])
+        if not _stale(obj, digest):
             return obj, None
-        cmd = [HIPCC] + _flags(src) + ["-c", src, "-o", obj]
+        cmd = [HIPCC] + flags + ["-c", src, "-o", obj]
         if verbose:
             print(" ".join(cmd), flush=True)
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             return obj, f"{src}:\n{r.stdout}\n{r.stderr}"
+        with open(obj + ".sha", "w") as f:
+            f.write(digest)
         return obj, None
 
     with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
@@ -94,7 +136,7 @@ def build(verbose: bool = False, jobs: int = 8) -> str:
     if errs:
         raise RuntimeError("native build failed:\n" + "\n".join(errs))
     objs = [o for o, _ in results]
-    if _stale(OUT, objs):
+    if _stale(OUT, lib_hash):
         cmd = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", OUT] + objs + \
               ["-L/opt/rocm/lib", "-lamdhip64", "-lpthread", "-Wl,-rpath,/opt/rocm/lib"]
         if verbose:
@@ -102,6 +144,8 @@ def build(verbose: bool = False, jobs: int = 8) -> str:
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n{r.stdout}\n{r.stderr}")
+        with open(OUT + ".sha", "w") as f:
+            f.write(lib_hash)
     return OUT
 
 
