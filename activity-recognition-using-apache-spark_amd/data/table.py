@@ -14,7 +14,7 @@ columns; the column-level ``missing`` mask is kept alongside.
 from __future__ import annotations
 
 from collections import OrderedDict
-from dataclasses import dataclass
+from dataclasses import dataclass, field
 from typing import Dict, Iterable, List, Optional, Sequence
 
 import numpy as np
@@ -44,10 +44,16 @@ class Column:
     data: np.ndarray
     missing: Optional[np.ndarray] = None  # bool mask, numeric columns only
     meta: Optional[dict] = None  # e.g. vocabulary of an indexed column, vector size
+    # device copies of this column's data (models.base.features_tensor, features.hybrid): one
+    # host->device transfer per column and device, shared by every fit / predict on the column;
+    # a row subset (take_rows / filter / split) is a new Column with an empty cache
+    cache: Optional[dict] = field(default=None, repr=False, compare=False)
 
     def __post_init__(self):
         if self.kind not in KINDS:
             raise ValueError(f"unknown column kind {self.kind}")
+        if self.cache is None:
+            self.cache = {}
 
     def __len__(self):
         return int(self.data.shape[0])

@@ -105,3 +105,50 @@ def regression_metrics(label, pred) -> Dict[str, float]:
     r2 = 1.0 - se / ss_tot if ss_tot > 0 else float("nan")
     return {"rmse": float(np.sqrt(mse)), "mse": float(mse), "r2": float(r2), "mae": float(ae / n),
             "var": float(var_y)}
+
+
+def batched_metrics(metric: str, label: torch.Tensor, pred: torch.Tensor, mask: torch.Tensor, num_classes: int,
+                    raw: torch.Tensor = None) -> np.ndarray:
+    """One metric for B models at once: ``pred`` / ``mask`` are ``[B, N]`` (mask = the rows each
+    model is scored on, e.g. its CrossValidator validation fold); returns ``[B]`` with the same
+    definitions as the single-model functions above.  Multiclass metrics come from a batched
+    confusion matrix (one einsum), regression metrics from masked moments; one host read.
+    Binary metrics (``raw [B, N, K]``) fall back to one sort per model."""
+    B, N = pred.shape
+    y = label.to(pred.device).long().view(1, N)
+    w = mask.to(torch.float64)
+    if metric in ("areaUnderROC", "areaUnderPR"):
+        out = []
+        for b in range(B):
+            rows = torch.nonzero(mask[b]).squeeze(1)
+            sc = raw[b][rows][:, 1] if raw.shape[-1] > 1 else raw[b][rows].reshape(-1)
+            out.append(binary_metrics(sc, label.to(rows.device)[rows])[metric])
+        return np.asarray(out, dtype=np.float64)
+    if metric in ("rmse", "mse", "r2", "mae", "var"):
+        yd = y.double().expand(B, N)
+        e = pred.double() - yd
+        n = w.sum(1).clamp_min(1e-300)
+        se = (w * e * e).sum(1)
+        res = {"mse": se / n, "rmse": (se / n).sqrt(), "mae": (w * e.abs()).sum(1) / n}
+        my = (w * yd).sum(1) / n
+        var_y = (w * yd * yd).sum(1) / n - my * my
+        res["var"] = var_y
+        ss_tot = var_y * n
+        res["r2"] = torch.where(ss_tot > 0, 1.0 - se / ss_tot.clamp_min(1e-300), torch.full_like(se, float("nan")))
+        return res[metric].cpu().numpy()
+    K = num_classes
+    Y1 = torch.nn.functional.one_hot(y.view(N), K).double()                  # [N, K]
+    P1 = torch.nn.functional.one_hot(pred.long().clamp(0, K - 1), K).double()  # [B, N, K]
+    cm = torch.einsum("bn,nk,bnj->bkj", w, Y1, P1)                            # [B, true, pred]
+    n = cm.sum((1, 2))
+    tp = torch.diagonal(cm, dim1=1, dim2=2)
+    lc, pc = cm.sum(2), cm.sum(1)
+    prec = torch.where(pc > 0, tp / pc.clamp_min(1), torch.zeros_like(tp))
+    rec = torch.where(lc > 0, tp / lc.clamp_min(1), torch.zeros_like(tp))
+    f1 = torch.where(prec + rec > 0, 2 * prec * rec / (prec + rec).clamp_min(1e-300), torch.zeros_like(tp))
+    wt = torch.where(lc > 0, lc / n.clamp_min(1e-300)[:, None], torch.zeros_like(lc))
+    res = {"accuracy": tp.sum(1) / n.clamp_min(1e-300), "weightedPrecision": (prec * wt).sum(1),
+           "weightedRecall": (rec * wt).sum(1), "f1": (f1 * wt).sum(1)}
+    res["weightedFMeasure"] = res["f1"]
+    res["weightedTruePositiveRate"] = res["weightedRecall"]
+    return res[metric].cpu().numpy()

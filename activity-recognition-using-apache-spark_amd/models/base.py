@@ -131,9 +131,18 @@ def dp_owner():
 
 
 def features_tensor(table: Table, col: str, device, dtype=torch.float32) -> torch.Tensor:
+    """Device matrix of a feature column, transferred once per (column, device, dtype) and cached
+    on the column (HBM-resident for every later fit / predict — SURVEY.md N12)."""
     c = table[col]
+    key = ("dense", str(device), str(dtype))
+    hit = c.cache.get(key) if c.cache is not None else None
+    if hit is not None:
+        return hit
     arr = c.data if c.kind == "vector" else c.data[:, None]
-    return torch.as_tensor(np.ascontiguousarray(arr, dtype=np.float32)).to(device=device, dtype=dtype)
+    t = torch.as_tensor(np.ascontiguousarray(arr, dtype=np.float32)).to(device=device, dtype=dtype)
+    if c.cache is not None:
+        c.cache[key] = t
+    return t
 
 
 def labels_tensor(table: Table, col: str, device) -> torch.Tensor:
@@ -171,9 +180,12 @@ class ClassificationModel(Model, ClassifierParams):
     def predict(self, X: torch.Tensor) -> torch.Tensor:
         return self.predict_all(X)[2]
 
+    def features_input(self, table: Table):
+        """What ``predict_all`` consumes for ``table`` (the cached dense device matrix by default)."""
+        return features_tensor(table, self.featuresCol, self.device)
+
     def transform(self, table: Table) -> Table:
-        X = features_tensor(table, self.featuresCol, self.device)
-        raw, prob, pred = self.predict_all(X)
+        raw, prob, pred = self.predict_all(self.features_input(table))
         t = table.with_column(Column(self.rawPredictionCol, "vector", raw.double().cpu().numpy()))
         t = t.with_column(Column(self.probabilityCol, "vector", prob.double().cpu().numpy()))
         return t.with_column(Column(self.predictionCol, "double", pred.double().cpu().numpy(),

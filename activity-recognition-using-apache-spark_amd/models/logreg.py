@@ -31,7 +31,10 @@ import torch
 
 from ..data.table import Table
 from ..ops import _native
-from ..ops.logreg import LogregWorkspace, logreg_loss_grad_native, logreg_loss_grad_torch
+from ..features.hybrid import HybridMatrix, hybrid_features
+from ..features.hybrid import from_dense as hybrid_from_dense
+from ..ops.logreg import (DeviceLogregSolver, LogregDesign, LogregWorkspace, logreg_loss_grad_native,
+                          logreg_margins_native)
 from ..optim import lbfgs
 from .base import ClassificationModel, ClassifierParams, Estimator, dp_allreduce, dp_context, dp_owner, dp_rows, \
     features_tensor, labels_tensor, new_uid, resolve_device
@@ -56,6 +59,7 @@ class LogisticRegressionModel(ClassificationModel):
         self.num_features = coefficientMatrix.shape[1]
         self.device = resolve_device(device) if device is not None else coefficientMatrix.device
         self.summary = summary or {}
+        self.featuresCol = "features"
 
     @property
     def coefficients(self):
@@ -65,21 +69,51 @@ class LogisticRegressionModel(ClassificationModel):
     def intercept(self):
         return float(self.interceptVector[0]) if self.binomial else self.interceptVector
 
-    def predict_raw(self, X: torch.Tensor) -> torch.Tensor:
-        W = self.coefficientMatrix.to(X.device)
-        b = self.interceptVector.to(X.device)
-        if X.is_cuda and X.shape[1] % 4 == 0:
-            from ..ops.gemm import EPI_BIAS_F32, gemm_f32
-            rows = max(8, (W.shape[0] + 7) // 8 * 8)
-            Wp = torch.zeros(rows, W.shape[1], device=X.device)
-            Wp[: W.shape[0]] = W
-            bp = torch.zeros(rows, device=X.device)
-            bp[: b.shape[0]] = b
-            Z = torch.empty(X.shape[0], rows, device=X.device)
-            gemm_f32(X.contiguous(), Wp, Z, M=X.shape[0], N=rows, K=X.shape[1], layout=0, epi=EPI_BIAS_F32, bias=bp)
-            m = Z[:, : W.shape[0]]
+    def weight_table(self, KP: int) -> torch.Tensor:
+        """[1, F+1, KP] effective weights of the evaluation kernel (row F = intercepts)."""
+        W, b = self.coefficientMatrix, self.interceptVector
+        out = torch.zeros(1, self.num_features + 1, KP, device=W.device)
+        out[0, :self.num_features, :W.shape[0]] = W.T
+        out[0, self.num_features, :W.shape[0]] = b
+        return out
+
+    def features_input(self, table):
+        return hybrid_features(table, self.featuresCol, self.device)
+
+    def predict_raw(self, X) -> torch.Tensor:
+        """Margins (binomial: ``[-m, m]``).  ``X``: dense ``[N, F]`` or a HybridMatrix.  On the GPU
+        the logreg_qn.hip evaluation kernel (prediction mode) runs for any hybrid input and for
+        dense inputs up to its LDS tile width; wider dense inputs use the exact-fp32 MFMA GEMM."""
+        k = self.coefficientMatrix.shape[0]
+        if isinstance(X, HybridMatrix) or X.is_cuda:
+            hm = X if isinstance(X, HybridMatrix) else None
+            dense_w = X.shape[1] if hm is None else int(hm.dense.shape[1])
+            if hm is None and dense_w <= _native.kernels().logreg_max_dense():
+                hm = hybrid_from_dense(X.float(), [])
+            if hm is not None and hm.device.type == "cuda" and int(hm.dense.shape[1]) <= \
+                    _native.kernels().logreg_max_dense():
+                KP = 8 if k <= 8 else 16
+                m = logreg_margins_native(hm, self.weight_table(KP).to(hm.device), k, 1)[0, :, :k]
+            elif hm is not None and hm.device.type != "cuda":
+                Xd = hm.to_dense()
+                m = Xd @ self.coefficientMatrix.to(Xd.device).T + self.interceptVector.to(Xd.device)
+            else:
+                from ..ops.gemm import EPI_BIAS_F32, gemm_f32
+                Xd = X if hm is None else hm.to_dense()
+                W = self.coefficientMatrix.to(Xd.device)
+                F4 = (Xd.shape[1] + 3) // 4 * 4
+                if F4 != Xd.shape[1]:
+                    Xd = torch.nn.functional.pad(Xd, (0, F4 - Xd.shape[1]))
+                rows = max(8, (k + 7) // 8 * 8)
+                Wp = torch.zeros(rows, F4, device=Xd.device)
+                Wp[:k, :W.shape[1]] = W
+                bp = torch.zeros(rows, device=Xd.device)
+                bp[:k] = self.interceptVector.to(Xd.device)
+                Z = torch.empty(Xd.shape[0], rows, device=Xd.device)
+                gemm_f32(Xd.contiguous(), Wp, Z, M=Xd.shape[0], N=rows, K=F4, layout=0, epi=EPI_BIAS_F32, bias=bp)
+                m = Z[:, :k]
         else:
-            m = X @ W.T + b
+            m = X @ self.coefficientMatrix.to(X.device).T + self.interceptVector.to(X.device)
         if self.binomial:
             return torch.cat([-m, m], dim=1)
         return m
@@ -100,57 +134,46 @@ class LogisticRegressionModel(ClassificationModel):
 
 class LogisticRegression(Estimator, ClassifierParams):
     _param_names = ("maxIter", "regParam", "elasticNetParam", "tol", "fitIntercept", "standardization", "family",
-                    "featuresCol", "labelCol", "weightCol", "device")
+                    "featuresCol", "labelCol", "weightCol", "device", "lineSearchTrials")
 
     def __init__(self, featuresCol="features", labelCol="label", maxIter: int = 100, regParam: float = 0.0,
                  elasticNetParam: float = 0.0, tol: float = 1e-6, fitIntercept: bool = True,
                  standardization: bool = True, family: str = "auto", weightCol: Optional[str] = None,
-                 device=None):
+                 device=None, lineSearchTrials: int = 4):
         super().__init__(new_uid("LogisticRegression"))
         self.featuresCol, self.labelCol = featuresCol, labelCol
         self.maxIter, self.regParam, self.elasticNetParam = maxIter, regParam, elasticNetParam
         self.tol, self.fitIntercept, self.standardization = tol, fitIntercept, standardization
         self.family, self.weightCol, self.device = family, weightCol, device
+        self.lineSearchTrials = lineSearchTrials  # step lengths 2^-t evaluated together per line search
 
     # ------------------------------------------------------------------
     def fit(self, table: Table) -> LogisticRegressionModel:
         dev = resolve_device(self.device)
-        X = features_tensor(table, self.featuresCol, dev)
+        hm = hybrid_features(table, self.featuresCol, dev)
         y = labels_tensor(table, self.labelCol, dev)
         w = None
         if self.weightCol:
             w = torch.as_tensor(table[self.weightCol].data.astype(np.float32), device=dev)
         num_classes = int(max(int(y.max()) + 1, len((table[self.labelCol].meta or {}).get("vocab") or [])))
-        lo, hi = dp_rows(X.shape[0])  # data parallel: this rank's row shard + one all-reduce per evaluation
-        model = self.fit_many(X[lo:hi], y[lo:hi], [FitSpec(None if w is None else w[lo:hi], self.regParam,
-                                                           self.elasticNetParam)], num_classes,
+        lo, hi = dp_rows(hm.n_rows)  # data parallel: this rank's row shard + one all-reduce per evaluation
+        model = self.fit_many(hm.rows(lo, hi), y[lo:hi], [FitSpec(None if w is None else w[lo:hi], self.regParam,
+                                                                  self.elasticNetParam)], num_classes,
                               allreduce=dp_allreduce())[0]
         model.uid = self.uid
         return model
 
-    def fit_many(self, X: torch.Tensor, y: torch.Tensor, specs: Sequence[FitSpec],
-                 num_classes: Optional[int] = None, allreduce=None) -> List[LogisticRegressionModel]:
-        """Train ``len(specs)`` models in one batched device optimization.
-
-        Data parallel: every rank passes its own row shard and ``allreduce`` (an
-        in-place SUM over ranks, e.g. RCCL); the summarizer statistics and every
-        objective evaluation's (loss, gradient) bucket are summed across ranks —
-        Spark's ``treeAggregate`` as ONE flat all-reduce — and
-        the replicated optimizer then takes identical steps on every rank.
-        """
-        dev = X.device
-        N, F = X.shape
-        K = int(num_classes or int(y.max()) + 1)
+    def _setup(self, hm: HybridMatrix, y: torch.Tensor, specs: Sequence[FitSpec], K: int, allreduce):
+        """Summarizer (+ its one all-reduce) -> standardization, masks, regularization vectors, x0."""
+        dev = hm.device
+        N, F = hm.n_rows, hm.n_features
         binomial = self.family == "binomial" or (self.family == "auto" and K <= 2)
         Kp = 2 if binomial else K
         B = len(specs)
         rw = torch.stack([torch.ones(N, device=dev) if s.row_weight is None else s.row_weight.to(dev).float()
                           for s in specs])                                            # [B, N]
-        # weighted summarizer (Spark: MultivariateOnlineSummarizer + MultiClassSummarizer), fp64
-        rwd = rw.double()
-        counts = torch.zeros(B, Kp, device=dev, dtype=torch.float64)
-        counts.scatter_add_(1, y.view(1, -1).expand(B, -1).clamp_max(Kp - 1), rwd)
-        summ = torch.cat([rwd.sum(dim=1, keepdim=True), rwd @ X.double(), rwd @ (X.double() ** 2), counts], dim=1)
+        design = LogregDesign(hm, y, rw, Kp)
+        summ = design.summary()
         if allreduce is not None:
             allreduce(summ)
         wsum = summ[:, 0]
@@ -166,8 +189,6 @@ class LogisticRegression(Estimator, ClassifierParams):
             inv_std = torch.where(std > 0, torch.ones_like(std), torch.zeros_like(std))
         reg = torch.tensor([s.regParam for s in specs], device=dev, dtype=torch.float32)
         alpha = torch.tensor([s.elasticNetParam for s in specs], device=dev, dtype=torch.float32)
-        l2 = reg * (1 - alpha)
-        l1_coef = reg * alpha
         D = Kp * (F + 1)
         # parameters x[b] = [K, F+1] in standardized space (last column = intercept)
         x0 = torch.zeros(B, Kp, F + 1, device=dev)
@@ -183,43 +204,59 @@ class LogisticRegression(Estimator, ClassifierParams):
             coef_mask[:, F] = 0
         if binomial:  # pivot: class-0 row is fixed at zero
             coef_mask[0] = 0
-        coef_mask = coef_mask.expand(B, Kp, F + 1)
         feat_mask = torch.cat([(inv_std > 0).float(), torch.ones(B, 1, device=dev)], dim=1)  # zero-std -> frozen
-        pmask = coef_mask * feat_mask[:, None, :]
-        l1 = None
-        if bool((l1_coef > 0).any()):
-            l1 = torch.zeros(B, Kp, F + 1, device=dev)
-            l1[:, :, :F] = l1_coef[:, None, None]
-            l1 = (l1 * pmask).reshape(B, D)
+        pmask = coef_mask[None] * feat_mask[:, None, :]                                      # [B, Kp, F+1]
+        notb = torch.ones(F + 1, device=dev)
+        notb[F] = 0  # the intercept is never regularized
+        l2v = ((reg * (1 - alpha))[:, None, None] * pmask * notb).reshape(B, D).contiguous()
+        l1c = reg * alpha
+        l1v = ((l1c[:, None, None] * pmask * notb).reshape(B, D).contiguous()
+               if bool((l1c > 0).any()) else None)
+        return design, binomial, Kp, inv_std, inv_wsum, pmask, l2v, l1v, x0 * pmask
 
-        y32 = y.to(torch.int32).contiguous()
-        use_native = X.is_cuda and F % 4 == 0
-        ws = LogregWorkspace(X, B, Kp) if use_native else None
-        Xc = X.contiguous()
+    def fit_many(self, X, y: torch.Tensor, specs: Sequence[FitSpec], num_classes: Optional[int] = None,
+                 allreduce=None) -> List[LogisticRegressionModel]:
+        """Train ``len(specs)`` models in one batched device optimization.
 
-        def objective(xflat):
-            xv = xflat.view(B, Kp, F + 1) * pmask
-            beta = xv[:, :, :F]
-            W_eff = beta * inv_std[:, None, :]
-            b = xv[:, :, F]
-            if use_native:
-                loss, gW, gb = logreg_loss_grad_native(Xc, y32, W_eff, b, rw, inv_wsum, ws)
-            else:
-                loss, gW, gb = logreg_loss_grad_torch(Xc, y, W_eff, b, rw, inv_wsum)
-            if allreduce is not None:  # one flat bucket: [loss | dW | db] for all B models
-                flat = torch.cat([loss.float().view(B, 1), gW.reshape(B, -1), gb.reshape(B, -1)], dim=1)
-                allreduce(flat)
-                loss = flat[:, 0]
-                gW = flat[:, 1:1 + Kp * F].view(B, Kp, F)
-                gb = flat[:, 1 + Kp * F:].view(B, Kp)
-            gbeta = gW * inv_std[:, None, :] + l2[:, None, None] * beta
-            loss = loss + 0.5 * l2 * (beta * beta).sum(dim=(1, 2))
-            g = torch.cat([gbeta, gb.unsqueeze(2)], dim=2) * pmask
-            return loss, g.reshape(B, D)
+        ``X`` is a dense ``[N, F]`` tensor or a :class:`HybridMatrix` (one-hot indices + dense
+        columns).  Data parallel: every rank passes its own row shard and ``allreduce`` (an
+        in-place SUM over ranks, e.g. RCCL); the summarizer statistics and every batched
+        objective evaluation's (loss, gradient) are summed across ranks — Spark's
+        ``treeAggregate`` — and the replicated optimizer takes identical
+        steps on every rank.
+        """
+        hm = X if isinstance(X, HybridMatrix) else hybrid_from_dense(X.float(), [])
+        dev = hm.device
+        F = hm.n_features
+        K = int(num_classes or int(y.max()) + 1)
+        design, binomial, Kp, inv_std, inv_wsum, pmask, l2v, l1v, x0 = self._setup(hm, y, specs, K, allreduce)
+        B, D = len(specs), Kp * (F + 1)
+        T = max(1, int(self.lineSearchTrials))
+        poll = 10 if self.maxIter > 20 else 0
+        if dev.type == "cuda" and design.Fd <= _native.kernels().logreg_max_dense() and Kp <= 16:
+            solver = DeviceLogregSolver(design, B, T, 10, inv_std, pmask, inv_wsum, l2v, l1v, self.maxIter, self.tol,
+                                        allreduce=allreduce)
+            xs, fobj, iters = solver.solve(x0, poll=poll)
+            n_evals, history = solver.n_evals, solver.hist
+        elif dev.type == "cuda":
+            xs, fobj, iters, n_evals, history = self._fit_wide_dense(hm, y, design, inv_std, inv_wsum, pmask, l2v,
+                                                                     l1v, x0, allreduce)
+        else:
+            def evaluate(xt):
+                loss, G = design.eval_torch(xt.view(-1, Kp, F + 1), T if xt.shape[0] != B else 1, inv_std, pmask,
+                                            inv_wsum)
+                if allreduce is not None:
+                    allreduce(G)
+                    allreduce(loss)
+                return loss, G
 
-        res = lbfgs.minimize(objective, x0.reshape(B, D), max_iter=self.maxIter, m=10, tol=self.tol, l1=l1)
-        xs = res.x.view(B, Kp, F + 1) * pmask
+            res = lbfgs.minimize_trials(evaluate, x0.reshape(B, D), l2v, l1v, max_iter=self.maxIter, m=10,
+                                        tol=self.tol, trials=T, poll=poll)
+            xs, fobj, iters, n_evals, history = res.x, res.f, res.iterations, res.n_evals, res.history
+        xs = xs.view(B, Kp, F + 1) * pmask
         models = []
+        fobj_h = fobj.double().cpu()
+        iters_h = iters.cpu()
         for bi in range(B):
             coef = xs[bi, :, :F] * inv_std[bi][None, :]
             icpt = xs[bi, :, F].clone()
@@ -227,11 +264,40 @@ class LogisticRegression(Estimator, ClassifierParams):
                 coef, icpt = coef[1:2], icpt[1:2]
             elif self.fitIntercept:
                 icpt = icpt - icpt.mean()
-            summary = {"objective": float(res.f[bi]), "iterations": int(res.iterations[bi]),
-                       "n_evals": res.n_evals, "objectiveHistory": res.history}
+            summary = {"objective": float(fobj_h[bi]), "iterations": int(iters_h[bi]), "n_evals": n_evals,
+                       "objectiveHistory": history}
             models.append(LogisticRegressionModel(coef.detach(), icpt.detach(), binomial, device=dev,
                                                   summary=summary))
         return models
+
+    def _fit_wide_dense(self, hm, y, design, inv_std, inv_wsum, pmask, l2v, l1v, x0, allreduce):
+        """GPU objective for dense blocks wider than the fused kernel's LDS tile: exact-fp32 MFMA
+        GEMMs (ops.logreg.logreg_loss_grad_native, F padded to a multiple of 4) driven by the
+        serial-backtracking L-BFGS."""
+        X = hm.to_dense()
+        B, Kp, Fp1 = x0.shape
+        F = Fp1 - 1
+        F4 = (F + 3) // 4 * 4
+        if F4 != F:
+            X = torch.nn.functional.pad(X, (0, F4 - F))
+        ws = LogregWorkspace(X, B, Kp)
+        y32 = y.to(torch.int32).contiguous()
+        rw = design.rw
+
+        def objective(xflat):
+            xv = xflat.view(B, Kp, F + 1) * pmask
+            W_eff = torch.nn.functional.pad(xv[:, :, :F] * inv_std[:, None, :], (0, F4 - F))
+            loss, gW, gb = logreg_loss_grad_native(X, y32, W_eff, xv[:, :, F], rw, inv_wsum, ws)
+            G = torch.cat([gW[:, :, :F] * inv_std[:, None, :], gb.unsqueeze(2)], dim=2) * pmask
+            G = G.reshape(B, -1)
+            if allreduce is not None:
+                allreduce(G)
+                allreduce(loss)
+            xr = xflat
+            return loss + 0.5 * (l2v * xr * xr).sum(1), G + l2v * xr
+
+        res = lbfgs.minimize(objective, x0.reshape(B, -1), max_iter=self.maxIter, m=10, tol=self.tol, l1=l1v)
+        return res.x, res.f, res.iterations, res.n_evals, res.history
 
 
 __all__ = ["LogisticRegression", "LogisticRegressionModel", "FitSpec"]

@@ -82,3 +82,189 @@ def logreg_loss_grad_native(X, y32, W, b, rw, inv_wsum, ws: LogregWorkspace):
     gW = ws.G[: B * K].view(B, K, F)
     gb = ws.R[:, : B * K].sum(dim=0).view(B, K)
     return ws.loss.to(torch.float32), gW, gb
+
+
+# ------------------------------------------------------------------------------------------
+# Hybrid-layout objective + device L-BFGS (csrc/kernels/logreg_qn.hip)
+# ------------------------------------------------------------------------------------------
+def _kp(K: int) -> int:
+    return 8 if K <= 8 else 16
+
+
+class LogregDesign:
+    """Device data of one fit: the hybrid feature layout, labels, per-spec row weights, the
+    one-hot CSC row lists and the column map of the gradient kernel."""
+
+    def __init__(self, hm, y: torch.Tensor, rw: torch.Tensor, K: int):
+        self.hm = hm
+        self.N, self.F = hm.n_rows, hm.n_features
+        self.Fd, self.C = int(hm.dense.shape[1]), int(hm.cat.shape[1])
+        self.K = K
+        self.KP = _kp(K)
+        self.y32 = y.to(torch.int32).contiguous()
+        self.rw = rw.float().contiguous()                       # [S, N]
+        self.csc_off, self.csc_rows = hm.csc()
+        if self.csc_rows.numel() == 0:
+            self.csc_rows = torch.zeros(1, dtype=torch.int32, device=hm.device)
+        self.col_map = hm.col_map()
+        self.dense = hm.dense if self.Fd else torch.zeros(max(1, self.N), 1, device=hm.device)
+        self.dense_cols = hm.dense_cols if self.Fd else torch.zeros(1, dtype=torch.int32, device=hm.device)
+        self.cat = hm.cat if self.C else torch.zeros(max(1, self.N), 1, dtype=torch.int32, device=hm.device)
+
+    def summary(self):
+        """Weighted summarizer per spec (Spark MultivariateOnlineSummarizer + MultiClassSummarizer):
+        [S, 1 + 2F + K] float64 = (sum w, sum w x, sum w x^2, class counts).  One-hot columns are
+        segment sums of the weights over their CSC row lists (fp64 scan), dense columns one fp64
+        product — every sum in a fixed order."""
+        S_, N, F, K = self.rw.shape[0], self.N, self.F, self.K
+        dev = self.rw.device
+        rwd = self.rw.double()
+        out = torch.zeros(S_, 1 + 2 * F + K, dtype=torch.float64, device=dev)
+        out[:, 0] = rwd.sum(1)
+        if self.C:
+            off = self.csc_off.long()
+            n = int(off[-1])
+            cs = torch.zeros(S_, n + 1, dtype=torch.float64, device=dev)
+            if n:
+                cs[:, 1:] = torch.cumsum(rwd[:, self.csc_rows[:n].long()], dim=1)
+            seg = cs[:, off[1:F + 1]] - cs[:, off[:F]]            # [S, F]
+            out[:, 1:1 + F] += seg
+            out[:, 1 + F:1 + 2 * F] += seg
+        if self.Fd:
+            Xd = self.hm.dense.double()
+            cols = self.hm.dense_cols.long()
+            out[:, 1 + cols] = rwd @ Xd
+            out[:, 1 + F + cols] = rwd @ (Xd * Xd)
+        out[:, 1 + 2 * F:] = rwd @ torch.nn.functional.one_hot(self.y32.long(), K).double()
+        return out
+
+    # ---- torch reference objective (CPU oracle and non-GPU path) ----
+    def eval_torch(self, xt: torch.Tensor, T: int, inv_std: torch.Tensor, pmask: torch.Tensor,
+                   inv_wsum: torch.Tensor):
+        """xt [S*T, K, F+1] -> (data loss [S*T] float64, data grad [S*T, K*(F+1)] masked, scaled)."""
+        BT = xt.shape[0]
+        F, K = self.F, self.K
+        spec = torch.arange(BT, device=xt.device) // T
+        Weff = xt[:, :, :F] * inv_std[spec][:, None, :] * pmask[spec][:, :, :F]
+        b = xt[:, :, F] * pmask[spec][:, :, F]
+        if getattr(self, "_X", None) is None:
+            self._X = self.hm.to_dense()
+        X = self._X.to(xt.dtype)
+        rw = self.rw[spec].to(xt.dtype)
+        loss, gW, gb = logreg_loss_grad_torch(X, self.y32.long(), Weff, b, rw, inv_wsum[spec])
+        G = torch.cat([gW * inv_std[spec][:, None, :], gb.unsqueeze(2)], dim=2) * pmask[spec]
+        return loss.double(), G.reshape(BT, -1)
+
+
+class DeviceLogregSolver:
+    """Runs ``optim.lbfgs.minimize_trials``' algorithm for the LR objective entirely with the
+    logreg_qn.hip kernels: 4 launches per iteration (direction + trials, evaluate, gradient,
+    pick + history), no host synchronization unless ``poll`` asks for a convergence check."""
+
+    def __init__(self, design: LogregDesign, B: int, T: int, m: int, inv_std, pmask, inv_wsum, l2v, l1v,
+                 max_iter: int, tol: float, c1: float = 1e-4, allreduce=None):
+        self.d = design
+        dev = design.rw.device
+        K, F = design.K, design.F
+        self.B, self.T, self.m = B, T, m
+        self.D = K * (F + 1)
+        D = self.D
+        BT = B * T
+        f32 = dict(dtype=torch.float32, device=dev)
+        f64 = dict(dtype=torch.float64, device=dev)
+        i32 = dict(dtype=torch.int32, device=dev)
+        self.inv_std = inv_std.float().contiguous()
+        self.pmask = pmask.float().reshape(B, D).contiguous()
+        self.inv_wsum = inv_wsum.float().contiguous()
+        self.l2v = l2v.float().contiguous()
+        self.l1v = None if l1v is None else l1v.float().contiguous()
+        self.max_iter, self.tol, self.c1 = max_iter, tol, c1
+        self.allreduce = allreduce
+        self.x = torch.zeros(B, D, **f32)
+        self.g = torch.zeros(B, D, **f32)
+        self.fobj = torch.zeros(B, **f64)
+        self.S = torch.zeros(m, B, D, **f32)
+        self.Y = torch.zeros(m, B, D, **f32)
+        self.rho = torch.zeros(m, B, **f64)
+        self.work = torch.zeros(B, D, **f32)
+        self.xtrial = torch.zeros(BT, D, **f32)
+        self.weff = torch.zeros(BT, F + 1, design.KP, **f32)   # padded classes stay 0
+        self.reg = torch.zeros(BT, **f64)
+        self.decr = torch.zeros(BT, **f64)
+        self.G = torch.zeros(BT, D, **f32)        # data gradient of every trial (the DP all-reduce bucket)
+        self.loss = torch.zeros(BT, **f64)        # data loss of every trial (fp64, its own small all-reduce)
+        self.step_scale = torch.ones(B, **f32)
+        self.active = torch.ones(B, **i32)
+        self.fails = torch.zeros(B, **i32)
+        self.iters = torch.zeros(B, **i32)
+        self.hist = torch.zeros(max_iter + 1, B, **f64)
+        self.ntiles = _native.kernels().logreg_eval_tiles(design.N)
+        self.slab = torch.zeros(BT, max(1, self.ntiles), design.Fd * design.KP + design.KP + 1, **f32)
+        self.R = torch.zeros(BT, max(1, design.N), design.KP, **f32) if design.C else None
+        self.n_evals = 0
+
+    def _args(self, init: int, head: int, filled: int, it: int):
+        p = lambda t: 0 if t is None else t.data_ptr()  # noqa: E731
+        return {"B": self.B, "T": self.T, "K": self.d.K, "F": self.d.F, "m": self.m, "head": head,
+                "filled": filled, "init": init, "it": it, "D": self.D, "x": p(self.x), "g": p(self.g),
+                "fobj": p(self.fobj), "l1": p(self.l1v), "l2": p(self.l2v), "pmask": p(self.pmask),
+                "inv_std": p(self.inv_std), "S": p(self.S), "Y": p(self.Y), "rho": p(self.rho),
+                "work": p(self.work), "xtrial": p(self.xtrial), "weff": p(self.weff), "reg": p(self.reg),
+                "decr": p(self.decr), "G": p(self.G), "loss": p(self.loss), "step_scale": p(self.step_scale),
+                "active": p(self.active), "fails": p(self.fails), "iters": p(self.iters), "hist": p(self.hist),
+                "c1": float(self.c1), "tol": float(self.tol)}
+
+    def _evaluate(self, tstride: int):
+        d, mod, s = self.d, _native.kernels(), _native.stream_ptr()
+        n_models = (self.B * self.T) // tstride
+        mod.logreg_eval(d.dense.data_ptr(), d.dense.stride(0), d.Fd, d.dense_cols.data_ptr(), d.cat.data_ptr(), d.C,
+                        d.y32.data_ptr(), d.rw.data_ptr(), self.inv_wsum.data_ptr(), self.weff.data_ptr(), d.N, d.F,
+                        d.K, self.T, tstride, 0, 0 if self.R is None else self.R.data_ptr(), self.slab.data_ptr(),
+                        d.KP, n_models, s)
+        mod.logreg_grad(self.slab.data_ptr(), 0 if self.R is None else self.R.data_ptr(), d.col_map.data_ptr(),
+                        d.csc_off.data_ptr(), d.csc_rows.data_ptr(), self.inv_std.data_ptr(), self.pmask.data_ptr(),
+                        d.N, d.F, d.Fd, d.K, self.T, tstride, self.ntiles, self.G.data_ptr(), self.loss.data_ptr(),
+                        d.KP, n_models, s)
+        if self.allreduce is not None:  # data parallel: the flat fp32 gradient bucket + the fp64 losses
+            self.allreduce(self.G)
+            self.allreduce(self.loss)
+        self.n_evals += 1
+
+    def solve(self, x0: torch.Tensor, poll: int = 0):
+        mod, s, KP = _native.kernels(), _native.stream_ptr(), self.d.KP
+        self.x.copy_(x0.reshape(self.B, self.D))
+        mod.lbfgs_phase(0, self._args(1, 0, 0, 0), KP, s)
+        self._evaluate(self.T)
+        mod.lbfgs_phase(1, self._args(1, 0, 0, 0), KP, s)
+        head = filled = 0
+        for it in range(self.max_iter):
+            mod.lbfgs_phase(0, self._args(0, head, filled, it + 1), KP, s)
+            self._evaluate(1)
+            mod.lbfgs_phase(1, self._args(0, head, filled, it + 1), KP, s)
+            head = (head + 1) % self.m
+            filled = min(filled + 1, self.m)
+            if poll and (it + 1) % poll == 0 and not bool(self.active.any()):
+                break
+        return self.x, self.fobj, self.iters
+
+    def margins(self, W_models: torch.Tensor, hm, n_models: int) -> torch.Tensor:
+        """Raw margins of ``n_models`` weight tables ``[n, F+1, KP]`` over ``hm`` rows: [n, N, KP]."""
+        return logreg_margins_native(hm, W_models, self.d.K, n_models)
+
+
+def logreg_margins_native(hm, W_models: torch.Tensor, K: int, n_models: int) -> torch.Tensor:
+    """Margins of ``n_models`` LR weight tables ``W_models [n, F+1, KP]`` (row F = intercept) over a
+    hybrid matrix, with the evaluation kernel in prediction mode: [n, N, KP] float32."""
+    mod, s = _native.kernels(), _native.stream_ptr()
+    KP = W_models.shape[2]
+    N, F = hm.n_rows, hm.n_features
+    dev = hm.device
+    Fd, C = int(hm.dense.shape[1]), int(hm.cat.shape[1])
+    dense = hm.dense if Fd else torch.zeros(max(1, N), 1, device=dev)
+    dcols = hm.dense_cols if Fd else torch.zeros(1, dtype=torch.int32, device=dev)
+    cat = hm.cat if C else torch.zeros(max(1, N), 1, dtype=torch.int32, device=dev)
+    out = torch.empty(n_models, max(1, N), KP, device=dev)
+    ones = torch.ones(1, device=dev)
+    mod.logreg_eval(dense.data_ptr(), dense.stride(0), Fd, dcols.data_ptr(), cat.data_ptr(), C, 0, 0, ones.data_ptr(),
+                    W_models.contiguous().data_ptr(), N, F, K, 1, 1, 1, out.data_ptr(), 0, KP, n_models, s)
+    return out[:, :N]

@@ -148,3 +148,134 @@ def minimize(fun: Objective, x0: torch.Tensor, max_iter: int = 100, m: int = 10,
         if not bool(active.any()):
             break
     return LbfgsResult(x=x, f=F, iterations=iters, n_evals=n_evals, history=history)
+
+
+# ------------------------------------------------------------------------------------------
+# Parallel-trial line search: the algorithm the device kernels run (csrc/kernels/logreg_qn.hip)
+# ------------------------------------------------------------------------------------------
+@dataclass
+class TrialResult:
+    x: torch.Tensor           # [B, D]
+    f: torch.Tensor           # [B] objective (data loss + regularization), float64
+    iterations: torch.Tensor  # [B]
+    n_evals: int              # batched evaluations (each covers B x T trial points)
+    history: list             # per-iteration mean objective
+
+
+def _reg_value(x, l2v, l1v):
+    r = 0.5 * (l2v.double() * x.double() * x.double()).sum(dim=1)
+    if l1v is not None:
+        r = r + (l1v.double() * x.double().abs()).sum(dim=1)
+    return r
+
+
+def minimize_trials(evaluate, x0: torch.Tensor, l2v: torch.Tensor, l1v: Optional[torch.Tensor] = None,
+                    max_iter: int = 100, m: int = 10, tol: float = 1e-6, trials: int = 4, c1: float = 1e-4,
+                    poll: int = 0) -> TrialResult:
+    """Minimize ``B`` problems ``data(x_b) + 0.5 sum l2v x^2 + sum l1v |x|`` in lock step with
+    L-BFGS (OWL-QN where ``l1v`` is non-zero), evaluating ``trials`` step lengths
+    ``a 2^-t`` of every line search in ONE batched call instead of backtracking serially.
+
+    ``evaluate(xt [B*T, D]) -> (loss [B*T] float64, grad [B*T, D])`` returns the DATA part.
+    Per iteration a model takes the largest trial step satisfying the Armijo condition; if
+    none does it stays put, its next steps shrink 16x, and a second consecutive failure
+    freezes it.  A model also freezes on ``|dF| / max(|F|, |F'|, 1) < tol`` or
+    ``|pg| <= tol * max(1, |x|)``.  This is the reference math of the device kernels
+    (``har.ops.logreg.DeviceLogregSolver``), float32 vectors with float64 reductions.
+    """
+    B, D = x0.shape
+    dev = x0.device
+    T = int(trials)
+    x = x0.clone().float()
+    if l1v is not None and not bool((l1v > 0).any()):
+        l1v = None
+    loss, G = evaluate(x)
+    g = G.float() + l2v * x
+    Fo = loss.double() + _reg_value(x, l2v, l1v)
+    S = torch.zeros(m, B, D, device=dev)
+    Y = torch.zeros(m, B, D, device=dev)
+    rho = torch.zeros(m, B, dtype=torch.float64, device=dev)
+    active = torch.ones(B, dtype=torch.bool, device=dev)
+    fails = torch.zeros(B, dtype=torch.int64, device=dev)
+    iters = torch.zeros(B, dtype=torch.int64, device=dev)
+    scale = torch.ones(B, device=dev)
+    head, filled, n_evals = 0, 0, 1
+    history = [float(Fo.mean())]
+    pg_fn = lambda xx, gg: _pseudo_grad(xx, gg, l1v)  # noqa: E731
+    for it in range(max_iter):
+        pg = pg_fn(x, g)
+        q = pg.clone()
+        alphas = []
+        for i in range(filled):
+            j = (head - 1 - i) % m
+            a = rho[j] * (S[j].double() * q.double()).sum(1)
+            alphas.append(a)
+            q = torch.where((rho[j] != 0)[:, None], (q.double() - a[:, None] * Y[j].double()).float(), q)
+        if filled:
+            j = (head - 1) % m
+            yy = (Y[j].double() ** 2).sum(1)
+            sy = (S[j].double() * Y[j].double()).sum(1)
+            gamma = torch.where((rho[j] > 0) & (yy > 0), sy / yy.clamp_min(1e-300), torch.ones_like(yy))
+        else:
+            gamma = 1.0 / (pg.double() ** 2).sum(1).sqrt().clamp_min(1e-12)
+        q = (gamma[:, None] * q.double()).float()
+        for i in reversed(range(filled)):
+            j = (head - 1 - i) % m
+            bcoef = rho[j] * (Y[j].double() * q.double()).sum(1)
+            coef = alphas[i] - bcoef
+            q = torch.where((rho[j] != 0)[:, None], (q.double() + coef[:, None] * S[j].double()).float(), q)
+        d = -q
+        if l1v is not None:
+            d = torch.where(d * pg < 0, d, torch.zeros_like(d))
+        dd = (pg.double() * d.double()).sum(1)
+        bad = dd >= 0
+        d = torch.where(bad[:, None], -pg, d)
+        dd = torch.where(bad, -(pg.double() ** 2).sum(1), dd)
+        # T trial points per model
+        steps = scale[:, None] * torch.pow(2.0, -torch.arange(T, device=dev, dtype=torch.float32))[None, :]
+        xt = x[:, None, :] + steps[:, :, None] * d[:, None, :]                        # [B, T, D]
+        decr = steps.double() * dd[:, None]
+        if l1v is not None:
+            xi = torch.where(x != 0, torch.sign(x), torch.sign(-pg))
+            xt = torch.where(torch.sign(xt) == xi[:, None, :], xt, torch.zeros_like(xt))
+            decr = (pg[:, None, :].double() * (xt.double() - x[:, None, :].double())).sum(2)
+        xt = torch.where(active[:, None, None], xt, x[:, None, :])
+        xt_flat = xt.reshape(B * T, D)
+        reg = _reg_value(xt_flat, l2v.repeat_interleave(T, 0),
+                         None if l1v is None else l1v.repeat_interleave(T, 0)).view(B, T)
+        loss_t, G_t = evaluate(xt_flat)
+        n_evals += 1
+        Ft = loss_t.double().view(B, T) + reg
+        ok = torch.isfinite(Ft) & (Ft <= Fo[:, None] + c1 * decr)
+        first = torch.where(ok.any(1), ok.float().argmax(1), torch.full((B,), -1, device=dev, dtype=torch.int64))
+        take = active & (first >= 0)
+        pick = first.clamp_min(0)
+        ar = torch.arange(B, device=dev)
+        x_new = xt[ar, pick]
+        g_new = G_t.view(B, T, D)[ar, pick].float() + l2v * x_new
+        F_new = Ft[ar, pick]
+        s_vec = x_new - x
+        y_vec = g_new - g
+        sy = (s_vec.double() * y_vec.double()).sum(1)
+        good = sy > 1e-10 * (s_vec.double().norm(dim=1) * y_vec.double().norm(dim=1)).clamp_min(1e-300)
+        S[head] = torch.where(take[:, None], s_vec, S[head])
+        Y[head] = torch.where(take[:, None], y_vec, Y[head])
+        rho[head] = torch.where(take & good, 1.0 / sy.clamp_min(1e-300), torch.zeros_like(sy))
+        rel = (Fo - F_new).abs() / torch.maximum(torch.maximum(Fo.abs(), F_new.abs()), torch.ones_like(Fo))
+        pgn = (pg_fn(x_new, g_new).double() ** 2).sum(1).sqrt()
+        xn = (x_new.double() ** 2).sum(1).sqrt()
+        conv = (rel < tol) | (pgn <= tol * xn.clamp_min(1.0))
+        x = torch.where(take[:, None], x_new, x)
+        g = torch.where(take[:, None], g_new, g)
+        Fo = torch.where(take, F_new, Fo)
+        iters = iters + take.long()
+        failed = active & ~take
+        fails = torch.where(take, torch.zeros_like(fails), fails + failed.long())
+        scale = torch.where(take, torch.ones_like(scale), torch.where(failed, scale / 16, scale))
+        active = active & ~(take & conv) & ~(fails >= 2)
+        head = (head + 1) % m
+        filled = min(filled + 1, m)
+        history.append(float(Fo.mean()))
+        if poll and (it + 1) % poll == 0 and not bool(active.any()):
+            break
+    return TrialResult(x=x, f=Fo, iterations=iters, n_evals=n_evals, history=history)

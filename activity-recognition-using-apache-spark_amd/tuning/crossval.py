@@ -64,11 +64,20 @@ class ParamGridBuilder:
         return maps or [dict(self._base)]
 
 
-def _with_predictions(model, table: Table, X: torch.Tensor, prefix: Optional[str] = None) -> Table:
-    raw, prob, pred = model.predict_all(X)
-    t = table.with_column(Column(model.rawPredictionCol, "vector", raw.double().cpu().numpy()))
-    t = t.with_column(Column(model.probabilityCol, "vector", prob.double().cpu().numpy()))
-    return t.with_column(Column(model.predictionCol, "double", pred.double().cpu().numpy()))
+def _lr_margins(models, hm) -> torch.Tensor:
+    """Raw predictions ``[n, N, K]`` of n logistic-regression models (binomial: ``[-m, m]``): one
+    launch of the evaluation kernel in prediction mode on the GPU."""
+    k = models[0].coefficientMatrix.shape[0]
+    if hm.device.type == "cuda":
+        from ..ops import _native
+        from ..ops.logreg import logreg_margins_native
+
+        if int(hm.dense.shape[1]) <= _native.kernels().logreg_max_dense():
+            KP = 8 if k <= 8 else 16
+            W = torch.cat([m.weight_table(KP).to(hm.device) for m in models])
+            m = logreg_margins_native(hm, W, k, len(models))[:, :, :k]
+            return torch.cat([-m, m], dim=2) if models[0].binomial else m
+    return torch.stack([mm.predict_raw(hm) for mm in models])
 
 
 class CrossValidatorModel(Model):
@@ -102,8 +111,10 @@ class CrossValidator(Estimator):
         from ..models.logreg import FitSpec, LogisticRegression
 
         if isinstance(est, LogisticRegression):
+            from ..features.hybrid import hybrid_features
+
             dev = resolve_device(est.device)
-            X = features_tensor(table, est.featuresCol, dev)
+            hm = hybrid_features(table, est.featuresCol, dev)
             y = labels_tensor(table, est.labelCol, dev)
             K = int(max(int(y.max()) + 1, len((table[est.labelCol].meta or {}).get("vocab") or [])))
             fold_t = torch.as_tensor(fold, device=dev)
@@ -115,24 +126,29 @@ class CrossValidator(Estimator):
                     index.append((mi, f))
             # maxIter / tol / family etc. may differ per map only through regParam/elasticNetParam
             base = est.copy(maps[0]) if maps else est
-            lo, hi = dp_rows(X.shape[0])  # data parallel: all 45 fits on this rank's row shard
+            lo, hi = dp_rows(hm.n_rows)  # data parallel: all 45 fits on this rank's row shard
             if dp_context() is not None:
                 specs = [FitSpec(s.row_weight[lo:hi], s.regParam, s.elasticNetParam) for s in specs]
-            models = base.fit_many(X[lo:hi], y[lo:hi], specs, K, allreduce=dp_allreduce())
-            for (mi, f), m in zip(index, models):
-                rows = np.nonzero(fold == f)[0]
-                vt = table.take_rows(rows)
-                metrics[mi, f] = ev.evaluate(_with_predictions(m, vt, X[torch.as_tensor(rows, device=dev)]))
+            models = base.fit_many(hm.rows(lo, hi), y[lo:hi], specs, K, allreduce=dp_allreduce())
+            # every (map, fold) model scored on its validation fold in ONE batched pass
+            raw = _lr_margins(models, hm)                                          # [n, N, K]
+            pred = torch.argmax(raw, dim=2)
+            mask = torch.stack([fold_t == f for _, f in index])
+            vals = ev.evaluate_batched(y, pred, mask, K, raw)
+            for (mi, f), v in zip(index, vals):
+                metrics[mi, f] = v
         elif hasattr(est, "fit_folds"):  # trees: every fold's tree(s) in one lock-step build
             dev = resolve_device(est.device)
             X, y, K = est._prep(table)
             fold_t = torch.as_tensor(fold, device=dev)
             masks = torch.stack([(fold_t != f).float() for f in range(k)])
             for mi, pm in enumerate(maps):
-                for f, m in enumerate(est.copy(pm).fit_folds(X, y, K, masks)):
-                    rows = np.nonzero(fold == f)[0]
-                    vt = table.take_rows(rows)
-                    metrics[mi, f] = ev.evaluate(_with_predictions(m, vt, X[torch.as_tensor(rows, device=dev)]))
+                fms = est.copy(pm).fit_folds(X, y, K, masks)
+                raws = [m.predict_raw(X) for m in fms]
+                raw = torch.stack([m.raw_to_probability(r) for m, r in zip(fms, raws)])
+                pred = torch.argmax(raw, dim=2)
+                vals = ev.evaluate_batched(y, pred, masks == 0, K, torch.stack(raws))
+                metrics[mi, :] = vals
         else:
             for f in range(k):
                 tr = table.take_rows(np.nonzero(fold != f)[0])

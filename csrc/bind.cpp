@@ -141,6 +141,98 @@ PYBIND11_MODULE(_har_native, m) {
           "logreg_softmax_grad");
   });
 
+  // ---- device logistic regression + batched L-BFGS / OWL-QN (logreg_qn.hip) ----
+  m.def("logreg_eval_tiles", &har_logreg_eval_tiles);
+  m.def("logreg_max_dense", []() { return HAR_LOGREG_MAX_DENSE; });
+  m.def("logreg_eval", [](u dense, int64_t ldd, int Fd, u dense_cols, u cat, int C, u y, u rw, u inv_wsum, u W,
+                          int64_t N, int F, int K, int T, int tstride, int mode, u R, u slab, int KP, int n_models,
+                          u stream) {
+    LogregEvalArgs a;
+    a.dense = P<const float>(dense);
+    a.ldd = ldd;
+    a.Fd = Fd;
+    a.dense_cols = P<const int32_t>(dense_cols);
+    a.cat = P<const int32_t>(cat);
+    a.C = C;
+    a.y = P<const int32_t>(y);
+    a.rw = P<const float>(rw);
+    a.inv_wsum = P<const float>(inv_wsum);
+    a.W = P<const float>(W);
+    a.N = N;
+    a.F = F;
+    a.K = K;
+    a.T = T;
+    a.tstride = tstride;
+    a.mode = mode;
+    a.R = P<float>(R);
+    a.slab = P<float>(slab);
+    check(har_logreg_eval(&a, KP, n_models, S(stream)), "logreg_eval");
+  });
+  m.def("logreg_grad", [](u slab, u R, u col_map, u csc_off, u csc_rows, u inv_std, u pmask, int64_t N, int F,
+                          int Fd, int K, int T, int tstride, int ntiles, u G, u loss, int KP, int n_models,
+                          u stream) {
+    LogregGradArgs a;
+    a.slab = P<const float>(slab);
+    a.R = P<const float>(R);
+    a.col_map = P<const int32_t>(col_map);
+    a.csc_off = P<const int32_t>(csc_off);
+    a.csc_rows = P<const int32_t>(csc_rows);
+    a.inv_std = P<const float>(inv_std);
+    a.pmask = P<const float>(pmask);
+    a.N = N;
+    a.F = F;
+    a.Fd = Fd;
+    a.K = K;
+    a.T = T;
+    a.tstride = tstride;
+    a.ntiles = ntiles;
+    a.G = P<float>(G);
+    a.loss = P<double>(loss);
+    check(har_logreg_grad(&a, KP, n_models, S(stream)), "logreg_grad");
+  });
+  // one L-BFGS phase (0 = direction + trial points, 1 = line-search pick + history update); the
+  // QnArgs fields come from a dict of ints / floats / device pointers (har.optim.lbfgs_device)
+  m.def("lbfgs_phase", [](int phase, py::dict d, int KP, u stream) {
+    auto I = [&](const char* k) { return d[k].cast<int64_t>(); };
+    auto U = [&](const char* k) { return d[k].cast<u>(); };
+    QnArgs a;
+    a.B = (int)I("B");
+    a.T = (int)I("T");
+    a.K = (int)I("K");
+    a.F = (int)I("F");
+    a.m = (int)I("m");
+    a.head = (int)I("head");
+    a.filled = (int)I("filled");
+    a.init = (int)I("init");
+    a.it = (int)I("it");
+    a.D = I("D");
+    a.x = P<float>(U("x"));
+    a.g = P<float>(U("g"));
+    a.fobj = P<double>(U("fobj"));
+    a.l1 = P<const float>(U("l1"));
+    a.l2 = P<const float>(U("l2"));
+    a.pmask = P<const float>(U("pmask"));
+    a.inv_std = P<const float>(U("inv_std"));
+    a.S = P<float>(U("S"));
+    a.Y = P<float>(U("Y"));
+    a.rho = P<double>(U("rho"));
+    a.work = P<float>(U("work"));
+    a.xtrial = P<float>(U("xtrial"));
+    a.weff = P<float>(U("weff"));
+    a.reg = P<double>(U("reg"));
+    a.decr = P<double>(U("decr"));
+    a.G = P<const float>(U("G"));
+    a.loss = P<const double>(U("loss"));
+    a.step_scale = P<float>(U("step_scale"));
+    a.active = P<int32_t>(U("active"));
+    a.fails = P<int32_t>(U("fails"));
+    a.iters = P<int32_t>(U("iters"));
+    a.hist = P<double>(U("hist"));
+    a.c1 = d["c1"].cast<double>();
+    a.tol = d["tol"].cast<double>();
+    check(phase == 0 ? har_lbfgs_direction(&a, KP, S(stream)) : har_lbfgs_update(&a, S(stream)), "lbfgs_phase");
+  });
+
   m.def("confusion_matrix", [](u label, u pred, int64_t n, int K, u cm, u stream) {
     check(har_confusion_matrix(P<const int32_t>(label), P<const int32_t>(pred), n, K, P<int64_t>(cm), S(stream)),
           "confusion_matrix");

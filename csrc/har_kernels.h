@@ -115,6 +115,74 @@ int har_regression_moments(const float* y, const float* yhat, int64_t n, double*
 int har_roc_pr_sums(const float* sorted_scores, const float* labels, int64_t n, double* out4, hipStream_t s);
 
 // ---- logistic regression (batched over B models, K classes padded to 8) ----
+// ---- device logistic regression + batched L-BFGS / OWL-QN (logreg_qn.hip) ----
+#define HAR_LOGREG_MAX_DENSE 48
+typedef struct LogregEvalArgs {
+  const float* dense;       // [N][ldd] dense feature columns (Fd used)
+  int64_t ldd;
+  int Fd;
+  const int32_t* dense_cols;  // [Fd] global column id of each dense column
+  const int32_t* cat;       // [N][C] global column id of each row's one-hot entry, -1 = none
+  int C;
+  const int32_t* y;         // [N] labels (mode 0)
+  const float* rw;          // [S][N] row weights per spec (null = 1)
+  const float* inv_wsum;    // [S]
+  const float* W;           // [n_trial_models][F+1][KP] effective weights (row F = intercept)
+  int64_t N;
+  int F, K, T, tstride;     // model bt = blockIdx.y * tstride, spec = bt / T
+  int mode;                 // 0 = loss/gradient, 1 = margins into R
+  float* R;                 // [n_trial_models][N][KP] residuals (mode 0, needed when C > 0) / margins
+  float* slab;              // [n_trial_models][tiles][Fd*KP + KP + 1]
+} LogregEvalArgs;
+
+typedef struct LogregGradArgs {
+  const float* slab;
+  const float* R;
+  const int32_t* col_map;   // [F+1]: >= 0 dense index, -1 intercept, <= -2 one-hot (CSC rows)
+  const int32_t* csc_off;   // [F+2] row-list offsets per column
+  const int32_t* csc_rows;  // row ids, ascending per column
+  const float* inv_std;     // [S][F]
+  const float* pmask;       // [S][K][F+1]
+  int64_t N;
+  int F, Fd, K, T, tstride, ntiles;
+  float* G;                 // [n_trial_models][K][F+1]
+  double* loss;             // [n_trial_models]
+} LogregGradArgs;
+
+typedef struct QnArgs {
+  int B, T, K, F, m, head, filled, init, it;
+  int64_t D;                // K * (F + 1)
+  float* x;                 // [B][D] standardized parameters
+  float* g;                 // [B][D] smooth gradient at x
+  double* fobj;             // [B] objective at x (smooth + regularization)
+  const float* l1;          // [B][D] per-element L1 weights (null = pure L-BFGS)
+  const float* l2;          // [B][D] per-element L2 weights
+  const float* pmask;       // [B][D]
+  const float* inv_std;     // [B][F]
+  float* S;                 // [m][B][D]
+  float* Y;                 // [m][B][D]
+  double* rho;              // [m][B] (0 = empty / rejected slot)
+  float* work;              // [B][D]
+  float* xtrial;            // [B*T][D]
+  float* weff;              // [B*T][F+1][KP]
+  double* reg;              // [B*T]
+  double* decr;             // [B*T]
+  const float* G;           // [B*T][D] data gradient of each trial (masked, scaled)
+  const double* loss;       // [B*T] data loss of each trial
+  float* step_scale;        // [B]
+  int32_t* active;          // [B]
+  int32_t* fails;           // [B]
+  int32_t* iters;           // [B]
+  double* hist;             // [max_iter][B] objective per iteration (nullable)
+  double c1, tol;
+} QnArgs;
+
+int har_logreg_eval(const LogregEvalArgs* a, int KP, int n_models, hipStream_t s);
+int har_logreg_eval_tiles(int64_t n);
+int har_logreg_grad(const LogregGradArgs* a, int KP, int n_models, hipStream_t s);
+int har_lbfgs_direction(const QnArgs* a, int KP, hipStream_t s);
+int har_lbfgs_update(const QnArgs* a, hipStream_t s);
+
 int har_logreg_softmax_grad(const float* Z, int64_t n, int nmodels, int K, int ld, const int32_t* y,
                             const float* rw, const float* inv_wsum, float* R, double* loss,
                             hipStream_t s);

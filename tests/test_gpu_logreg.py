@@ -1,0 +1,134 @@
+"""Device logistic regression (csrc/kernels/logreg_qn.hip) against its fp32/fp64 PyTorch oracles.
+
+* the fused evaluation + gradient kernels on a HYBRID layout (one-hot index blocks + dense
+  columns, per-spec row weights, several trial models) vs ``LogregDesign.eval_torch`` in fp64;
+* the prediction-mode margins vs a dense fp64 product;
+* the device L-BFGS / OWL-QN solver vs ``optim.lbfgs.minimize_trials`` (same algorithm in torch);
+* bitwise determinism of a device fit (no atomics anywhere on the path);
+* the WISDM reference-encoding fits (LR, LR CrossValidator) through the public estimators.
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _hybrid_problem(dev, N=1500, seed=0, blocks=((0, 40), (40, 25)), Fd=9, K=6):
+    from har.features.hybrid import from_dense
+
+    g = torch.Generator().manual_seed(seed)
+    F = sum(w for _, w in blocks) + Fd
+    X = torch.zeros(N, F)
+    y = torch.randint(0, K, (N,), generator=g)
+    for off, w in blocks:
+        idx = torch.randint(0, w + 1, (N,), generator=g)  # w == dropped last category
+        idx = torch.where(torch.rand(N, generator=g) < 0.5, (y * 7) % (w + 1), idx)
+        ok = idx < w
+        X[torch.nonzero(ok).squeeze(1), off + idx[ok]] = 1.0
+    X[:, F - Fd:] = torch.randn(N, Fd, generator=g) + y[:, None].float() * 0.3
+    hm = from_dense(X.to(dev), list(blocks))
+    assert hm is not None and hm.cat.shape[1] == len(blocks) and hm.dense.shape[1] == Fd
+    return X, y, hm
+
+
+def test_hybrid_eval_kernel_matches_fp64(cuda):
+    from har.ops.logreg import DeviceLogregSolver, LogregDesign
+
+    X, y, hm = _hybrid_problem(cuda)
+    N, F = X.shape
+    K, S, T = 6, 3, 2
+    g = torch.Generator().manual_seed(1)
+    rw = (torch.rand(S, N, generator=g) > 0.25).float().to(cuda)
+    design = LogregDesign(hm, y.to(cuda), rw, K)
+    inv_std = (torch.rand(S, F, generator=g) + 0.5).to(cuda)
+    pmask = torch.ones(S, K, F + 1, device=cuda)
+    pmask[:, :, 3] = 0  # a frozen column
+    inv_wsum = 1.0 / rw.sum(1)
+    D = K * (F + 1)
+    solver = DeviceLogregSolver(design, S, T, 4, inv_std, pmask, inv_wsum, torch.zeros(S, D, device=cuda), None, 1,
+                                1e-6)
+    xt = torch.randn(S * T, K, F + 1, generator=g).to(cuda) * 0.3
+    spec = torch.arange(S * T, device=cuda) // T
+    W = xt[:, :, :F] * inv_std[spec][:, None, :] * pmask[spec][:, :, :F]
+    solver.weff.zero_()
+    solver.weff[:, :F, :K] = W.transpose(1, 2)
+    solver.weff[:, F, :K] = xt[:, :, F] * pmask[spec][:, :, F]
+    solver._evaluate(1)
+    ref_loss, ref_G = LogregDesign(hm, y.to(cuda), rw.double(), K).eval_torch(
+        xt.double(), T, inv_std.double(), pmask.double(), inv_wsum.double())
+    torch.testing.assert_close(solver.loss, ref_loss, rtol=2e-5, atol=1e-6)
+    torch.testing.assert_close(solver.G.double(), ref_G, rtol=2e-4, atol=2e-6)
+    assert float(solver.G.view(S * T, K, F + 1)[:, :, 3].abs().max()) == 0.0
+
+
+def test_margins_kernel_matches_dense(cuda):
+    from har.ops.logreg import logreg_margins_native
+
+    X, y, hm = _hybrid_problem(cuda, N=700, seed=3)
+    F = X.shape[1]
+    g = torch.Generator().manual_seed(2)
+    W = torch.randn(3, F + 1, 8, generator=g)
+    W[:, :, 6:] = 0
+    out = logreg_margins_native(hm, W.to(cuda), 6, 3)
+    ref = torch.einsum("nf,bfk->bnk", X.double(), W[:, :F].double()) + W[:, F].double()[:, None, :]
+    torch.testing.assert_close(out.double().cpu(), ref, rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("alpha", [0.0, 0.4])
+def test_device_solver_matches_torch_algorithm(cuda, alpha):
+    """The kernels run the algorithm of minimize_trials: same objective after the fit, and the
+    same predictions (fp32 differences only)."""
+    from har.models.logreg import FitSpec, LogisticRegression
+
+    X, y, hm = _hybrid_problem(cuda, N=2000, seed=5)
+    est = LogisticRegression(maxIter=30, regParam=0.05)
+    specs = [FitSpec(None, 0.05, alpha), FitSpec((torch.arange(2000) % 5 != 0).float(), 0.02, alpha)]
+    cpu = est.fit_many(X, y, specs, 6)
+    gpu = est.fit_many(hm, y.to(cuda), [FitSpec(None if s.row_weight is None else s.row_weight.to(cuda),
+                                                 s.regParam, s.elasticNetParam) for s in specs], 6)
+    for c, gm in zip(cpu, gpu):
+        assert abs(c.summary["objective"] - gm.summary["objective"]) <= 2e-4 * max(1.0, abs(c.summary["objective"]))
+        agree = (c.predict(X) == gm.predict(hm).cpu()).float().mean()
+        assert agree > 0.99
+        if alpha > 0:  # OWL-QN leaves exact zeros
+            assert int((gm.coefficientMatrix == 0).sum()) > 0
+
+
+def test_device_fit_is_bitwise_deterministic(cuda):
+    from har.models.logreg import FitSpec, LogisticRegression
+
+    _, y, hm = _hybrid_problem(cuda, N=3000, seed=6)
+    est = LogisticRegression(maxIter=20, regParam=0.1)
+    specs = [FitSpec(None, 0.1, 0.0), FitSpec(None, 0.3, 0.1)]
+    a = est.fit_many(hm, y.to(cuda), specs, 6)
+    b = est.fit_many(hm, y.to(cuda), specs, 6)
+    for m1, m2 in zip(a, b):
+        assert torch.equal(m1.coefficientMatrix, m2.coefficientMatrix)
+        assert torch.equal(m1.interceptVector, m2.interceptVector)
+
+
+def test_wisdm_reference_lr_and_cv_on_device(cuda, wisdm_csv):
+    from har.data.csv_io import read_csv
+    from har.data.split import random_split
+    from har.evaluation.evaluators import RegressionEvaluator
+    from har.features import wisdm
+    from har.models.base import features_tensor
+    from har.models.logreg import LogisticRegression
+    from har.tuning.crossval import CrossValidator, ParamGridBuilder
+
+    _, _, df = wisdm.prepare(read_csv(wisdm_csv), "reference")
+    tr, te = random_split(df, [0.7, 0.3], 2018)
+    yt = torch.as_tensor(te["label"].data.astype(np.int64), device=cuda)
+    lr = LogisticRegression(maxIter=20, regParam=0.3, device=cuda)
+    m = lr.fit(tr)
+    acc = float((m.predict(m.features_input(te)) == yt).float().mean())
+    assert acc >= 0.61
+    # the hybrid-layout prediction equals the dense (3100-wide MFMA GEMM) prediction
+    dense = m.predict_raw(features_tensor(te, "features", cuda))
+    torch.testing.assert_close(m.predict_raw(m.features_input(te)), dense, rtol=1e-4, atol=1e-4)
+    grid = ParamGridBuilder().addGrid("regParam", [0.1, 0.3, 0.5]).addGrid("elasticNetParam", [0.0, 0.1, 0.2]).build()
+    cv = CrossValidator(estimator=LogisticRegression(maxIter=20, device=cuda), estimatorParamMaps=grid,
+                        evaluator=RegressionEvaluator(metricName="mae"), numFolds=5, seed=2018).fit(tr)
+    acc_cv = float((cv.bestModel.predict(cv.bestModel.features_input(te)) == yt).float().mean())
+    assert acc_cv >= 0.70 and len(cv.avgMetrics) == 9

@@ -2,7 +2,7 @@
 # One gpurun session: GPU tests -> benches -> rocprofv3 kernel stats.
 # Every GPU step has its own time limit; a fault / abort / timeout ends the script
 # (exit codes 124, 134, 137, 139 or >128), plain test failures (exit 1) do not.
-#   usage: gpurun --timeout 1200 -- bash tools/gpu_session.sh [tests|bench|benchall|prof|all] [pytest args]
+#   usage: gpurun --timeout 1200 -- bash tools/gpu_session.sh [tests|bench|ref|benchall|prof|all] [pytest args]
 set -u
 ROOT="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 OUT="$ROOT/gpurun_out"
@@ -34,6 +34,14 @@ if [ "$WHAT" = "bench" ] || [ "$WHAT" = "all" ] || [ "$WHAT" = "benchall" ]; the
   rc=$?
   tail -2 "$OUT/bench.log"
   fatal $rc bench
+fi
+
+if [ "$WHAT" = "ref" ] || [ "$WHAT" = "bench" ] || [ "$WHAT" = "all" ] || [ "$WHAT" = "benchall" ]; then
+  timeout -k 10 300 python bench.py --config reference --steps 5 --warmup 2 --out "$OUT/bench_reference.json" \
+      > "$OUT/bench_reference.log" 2>&1
+  rc=$?
+  tail -c 600 "$OUT/bench_reference.log"
+  fatal $rc bench_reference
 fi
 
 if [ "$WHAT" = "benchall" ]; then
