@@ -33,6 +33,12 @@ class RunConfig:
     seed: int = 2018
     device: str = "auto"
     csv_device: bool = False               # parse + dictionary-encode the CSV with the HIP kernels
+    # raw accelerometer rows (user,activity,timestamp,x,y,z) instead of the pre-windowed table:
+    # windowed + featurized on the device into the WISDM columns (features/raw.py)
+    raw: Optional[str] = None
+    hz: float = 20.0                       # WISDM v1.1 sampling rate (BASELINE.json configs use 50)
+    window_sec: float = 10.0               # WISDM window length
+    overlap: float = 0.0                   # fraction of a window shared with the next one
     # LogisticRegression (main.py:115)
     lr_max_iter: int = 20
     lr_reg: float = 0.3

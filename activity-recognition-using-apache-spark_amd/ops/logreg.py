@@ -111,6 +111,36 @@ class LogregDesign:
         self.dense_cols = hm.dense_cols if self.Fd else torch.zeros(1, dtype=torch.int32, device=hm.device)
         self.cat = hm.cat if self.C else torch.zeros(max(1, self.N), 1, dtype=torch.int32, device=hm.device)
 
+    def grad_partition(self, cols_per_block: int = 128):
+        """Work partition of the gradient kernel (one host read of the CSC offsets per fit):
+        every one-hot column's row list is cut into slices of <= SL rows, SL chosen so no
+        ``cols_per_block``-column window holds more than 256 slices; returns device int32
+        (slice_lo [n_slices+1], col_slice [F+2], blk_col [nb+1], blk_slice [nb+1]) and nb."""
+        if getattr(self, "_part", None) is not None:
+            return self._part
+        import numpy as np
+
+        F = self.F
+        off = self.csc_off.cpu().numpy().astype(np.int64)
+        L = off[1:F + 2] - off[:F + 1]                                   # rows per column (F+1)
+        starts = np.arange(0, F + 1, cols_per_block)
+        win = np.add.reduceat(L, starts) if L.size else np.zeros(1, np.int64)
+        SL = max(16, int(-(-int(win.max()) // cols_per_block)) if win.size else 16)
+        ns = -(-L // SL)
+        col_slice = np.zeros(F + 2, np.int64)
+        col_slice[1:] = np.cumsum(ns)
+        total = int(col_slice[-1])
+        col_of = np.repeat(np.arange(F + 1), ns)
+        within = np.arange(total) - col_slice[col_of]
+        slice_lo = np.concatenate([off[col_of] + within * SL, [off[F + 1]]])
+        blk_col = np.concatenate([starts, [F + 1]])
+        blk_slice = col_slice[blk_col]
+        assert int(np.max(np.diff(blk_slice), initial=0)) <= 256 and int(np.max(np.diff(blk_col))) <= 256
+        dev = self.rw.device
+        t = lambda a: torch.as_tensor(a.astype(np.int32)).to(dev)  # noqa: E731
+        self._part = (t(slice_lo), t(col_slice), t(blk_col), t(blk_slice), len(starts))
+        return self._part
+
     def summary(self):
         """Weighted summarizer per spec (Spark MultivariateOnlineSummarizer + MultiClassSummarizer):
         [S, 1 + 2F + K] float64 = (sum w, sum w x, sum w x^2, class counts).  One-hot columns are
@@ -186,7 +216,8 @@ class DeviceLogregSolver:
         self.S = torch.zeros(m, B, D, **f32)
         self.Y = torch.zeros(m, B, D, **f32)
         self.rho = torch.zeros(m, B, **f64)
-        self.work = torch.zeros(B, D, **f32)
+        self.SY = torch.zeros(B, m, m, **f64)   # history Gram matrices (compact two-loop recursion)
+        self.YY = torch.zeros(B, m, m, **f64)
         self.xtrial = torch.zeros(BT, D, **f32)
         self.weff = torch.zeros(BT, F + 1, design.KP, **f32)   # padded classes stay 0
         self.reg = torch.zeros(BT, **f64)
@@ -197,22 +228,31 @@ class DeviceLogregSolver:
         self.active = torch.ones(B, **i32)
         self.fails = torch.zeros(B, **i32)
         self.iters = torch.zeros(B, **i32)
+        self.steep = torch.zeros(B, **i32)
+        self.pick = torch.zeros(B, **i32)
+        self.nch = _native.kernels().qn_chunks(D)
+        self.P1 = torch.zeros(B, self.nch, 2 * 10 + 1, **f64)   # chunk partials (QN_MAX_M = 10)
+        self.P2 = torch.zeros(B, self.nch, 3 * 4 + 2, **f64)    # (QN_MAX_TRIALS = 4)
+        self.P3 = torch.zeros(B, self.nch, 5 + 3 * 10, **f64)
         self.hist = torch.zeros(max_iter + 1, B, **f64)
         self.ntiles = _native.kernels().logreg_eval_tiles(design.N)
         self.slab = torch.zeros(BT, max(1, self.ntiles), design.Fd * design.KP + design.KP + 1, **f32)
         self.R = torch.zeros(BT, max(1, design.N), design.KP, **f32) if design.C else None
         self.n_evals = 0
 
-    def _args(self, init: int, head: int, filled: int, it: int):
+    def _args(self, init: int = 0, head: int = 0, filled: int = 0, fin: int = 0, fin_init: int = 0,
+              fin_head: int = 0, fin_it: int = 0):
         p = lambda t: 0 if t is None else t.data_ptr()  # noqa: E731
         return {"B": self.B, "T": self.T, "K": self.d.K, "F": self.d.F, "m": self.m, "head": head,
-                "filled": filled, "init": init, "it": it, "D": self.D, "x": p(self.x), "g": p(self.g),
+                "filled": filled, "init": init, "nch": self.nch, "fin": fin, "fin_init": fin_init,
+                "fin_head": fin_head, "fin_it": fin_it, "D": self.D, "x": p(self.x), "g": p(self.g),
                 "fobj": p(self.fobj), "l1": p(self.l1v), "l2": p(self.l2v), "pmask": p(self.pmask),
                 "inv_std": p(self.inv_std), "S": p(self.S), "Y": p(self.Y), "rho": p(self.rho),
-                "work": p(self.work), "xtrial": p(self.xtrial), "weff": p(self.weff), "reg": p(self.reg),
-                "decr": p(self.decr), "G": p(self.G), "loss": p(self.loss), "step_scale": p(self.step_scale),
-                "active": p(self.active), "fails": p(self.fails), "iters": p(self.iters), "hist": p(self.hist),
-                "c1": float(self.c1), "tol": float(self.tol)}
+                "SY": p(self.SY), "YY": p(self.YY), "P1": p(self.P1), "P2": p(self.P2), "P3": p(self.P3),
+                "xtrial": p(self.xtrial), "weff": p(self.weff), "reg": p(self.reg), "decr": p(self.decr),
+                "G": p(self.G), "loss": p(self.loss), "step_scale": p(self.step_scale), "active": p(self.active),
+                "fails": p(self.fails), "iters": p(self.iters), "steep": p(self.steep), "pick": p(self.pick),
+                "hist": p(self.hist), "c1": float(self.c1), "tol": float(self.tol)}
 
     def _evaluate(self, tstride: int):
         d, mod, s = self.d, _native.kernels(), _native.stream_ptr()
@@ -221,30 +261,43 @@ class DeviceLogregSolver:
                         d.y32.data_ptr(), d.rw.data_ptr(), self.inv_wsum.data_ptr(), self.weff.data_ptr(), d.N, d.F,
                         d.K, self.T, tstride, 0, 0 if self.R is None else self.R.data_ptr(), self.slab.data_ptr(),
                         d.KP, n_models, s)
+        slice_lo, col_slice, blk_col, blk_slice, nb = d.grad_partition()
         mod.logreg_grad(self.slab.data_ptr(), 0 if self.R is None else self.R.data_ptr(), d.col_map.data_ptr(),
-                        d.csc_off.data_ptr(), d.csc_rows.data_ptr(), self.inv_std.data_ptr(), self.pmask.data_ptr(),
-                        d.N, d.F, d.Fd, d.K, self.T, tstride, self.ntiles, self.G.data_ptr(), self.loss.data_ptr(),
-                        d.KP, n_models, s)
+                        d.csc_rows.data_ptr(), slice_lo.data_ptr(), col_slice.data_ptr(), blk_col.data_ptr(),
+                        blk_slice.data_ptr(), nb, self.inv_std.data_ptr(), self.pmask.data_ptr(), d.N, d.F, d.Fd,
+                        d.K, self.T, tstride, self.ntiles, self.G.data_ptr(), self.loss.data_ptr(), d.KP, n_models, s)
         if self.allreduce is not None:  # data parallel: the flat fp32 gradient bucket + the fp64 losses
             self.allreduce(self.G)
             self.allreduce(self.loss)
         self.n_evals += 1
 
     def solve(self, x0: torch.Tensor, poll: int = 0):
+        """Per iteration: phase 0 (finalize the previous update + history dots), phase 1 (direction
+        + T trial points), evaluate + gradient of the B*T trials, phase 2 (pick + history).  The
+        host polls ``active`` (one sync) every ``poll`` iterations only."""
         mod, s, KP = _native.kernels(), _native.stream_ptr(), self.d.KP
         self.x.copy_(x0.reshape(self.B, self.D))
-        mod.lbfgs_phase(0, self._args(1, 0, 0, 0), KP, s)
+        mod.lbfgs_phase(1, self._args(init=1), KP, s)
         self._evaluate(self.T)
-        mod.lbfgs_phase(1, self._args(1, 0, 0, 0), KP, s)
+        mod.lbfgs_phase(2, self._args(init=1), KP, s)
         head = filled = 0
+        prev = -1  # history slot written by the previous phase 2 (-1: the init update)
+        finalized = False
         for it in range(self.max_iter):
-            mod.lbfgs_phase(0, self._args(0, head, filled, it + 1), KP, s)
+            mod.lbfgs_phase(0, self._args(head=head, filled=filled, fin=1, fin_init=int(prev < 0),
+                                          fin_head=max(prev, 0), fin_it=it), KP, s)
+            if poll and it and it % poll == 0 and not bool(self.active.any()):
+                finalized = True
+                break
+            mod.lbfgs_phase(1, self._args(head=head, filled=filled), KP, s)
             self._evaluate(1)
-            mod.lbfgs_phase(1, self._args(0, head, filled, it + 1), KP, s)
+            mod.lbfgs_phase(2, self._args(head=head, filled=filled), KP, s)
+            prev = head
             head = (head + 1) % self.m
             filled = min(filled + 1, self.m)
-            if poll and (it + 1) % poll == 0 and not bool(self.active.any()):
-                break
+        if not finalized:
+            mod.lbfgs_phase(3, self._args(fin=1, fin_init=int(prev < 0), fin_head=max(prev, 0),
+                                          fin_it=self.max_iter), KP, s)
         return self.x, self.fobj, self.iters
 
     def margins(self, W_models: torch.Tensor, hm, n_models: int) -> torch.Tensor:

@@ -179,7 +179,8 @@ def minimize_trials(evaluate, x0: torch.Tensor, l2v: torch.Tensor, l1v: Optional
     ``evaluate(xt [B*T, D]) -> (loss [B*T] float64, grad [B*T, D])`` returns the DATA part.
     Per iteration a model takes the largest trial step satisfying the Armijo condition; if
     none does it stays put, its next steps shrink 16x, and a second consecutive failure
-    freezes it.  A model also freezes on ``|dF| / max(|F|, |F'|, 1) < tol`` or
+    freezes it.  A two-loop direction that is not a descent direction is rejected and the
+    model takes steepest descent on its pseudo-gradient in the next iteration.  A model also freezes on ``|dF| / max(|F|, |F'|, 1) < tol`` or
     ``|pg| <= tol * max(1, |x|)``.  This is the reference math of the device kernels
     (``har.ops.logreg.DeviceLogregSolver``), float32 vectors with float64 reductions.
     """
@@ -199,6 +200,7 @@ def minimize_trials(evaluate, x0: torch.Tensor, l2v: torch.Tensor, l1v: Optional
     fails = torch.zeros(B, dtype=torch.int64, device=dev)
     iters = torch.zeros(B, dtype=torch.int64, device=dev)
     scale = torch.ones(B, device=dev)
+    steep = torch.zeros(B, dtype=torch.bool, device=dev)
     head, filled, n_evals = 0, 0, 1
     history = [float(Fo.mean())]
     pg_fn = lambda xx, gg: _pseudo_grad(xx, gg, l1v)  # noqa: E731
@@ -227,10 +229,9 @@ def minimize_trials(evaluate, x0: torch.Tensor, l2v: torch.Tensor, l1v: Optional
         d = -q
         if l1v is not None:
             d = torch.where(d * pg < 0, d, torch.zeros_like(d))
+        # a model whose last direction was not a descent direction takes steepest descent now
+        d = torch.where(steep[:, None], -pg, d)
         dd = (pg.double() * d.double()).sum(1)
-        bad = dd >= 0
-        d = torch.where(bad[:, None], -pg, d)
-        dd = torch.where(bad, -(pg.double() ** 2).sum(1), dd)
         # T trial points per model
         steps = scale[:, None] * torch.pow(2.0, -torch.arange(T, device=dev, dtype=torch.float32))[None, :]
         xt = x[:, None, :] + steps[:, :, None] * d[:, None, :]                        # [B, T, D]
@@ -248,6 +249,8 @@ def minimize_trials(evaluate, x0: torch.Tensor, l2v: torch.Tensor, l1v: Optional
         Ft = loss_t.double().view(B, T) + reg
         ok = torch.isfinite(Ft) & (Ft <= Fo[:, None] + c1 * decr)
         first = torch.where(ok.any(1), ok.float().argmax(1), torch.full((B,), -1, device=dev, dtype=torch.int64))
+        nondescent = active & (dd >= 0) & ~steep   # rejected; steepest descent next iteration
+        first = torch.where(dd >= 0, torch.full_like(first, -1), first)
         take = active & (first >= 0)
         pick = first.clamp_min(0)
         ar = torch.arange(B, device=dev)
@@ -269,9 +272,10 @@ def minimize_trials(evaluate, x0: torch.Tensor, l2v: torch.Tensor, l1v: Optional
         g = torch.where(take[:, None], g_new, g)
         Fo = torch.where(take, F_new, Fo)
         iters = iters + take.long()
-        failed = active & ~take
+        failed = active & ~take & ~nondescent
         fails = torch.where(take, torch.zeros_like(fails), fails + failed.long())
         scale = torch.where(take, torch.ones_like(scale), torch.where(failed, scale / 16, scale))
+        steep = torch.where(take, torch.zeros_like(steep), steep | nondescent)
         active = active & ~(take & conv) & ~(fails >= 2)
         head = (head + 1) % m
         filled = min(filled + 1, m)

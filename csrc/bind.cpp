@@ -168,15 +168,19 @@ PYBIND11_MODULE(_har_native, m) {
     a.slab = P<float>(slab);
     check(har_logreg_eval(&a, KP, n_models, S(stream)), "logreg_eval");
   });
-  m.def("logreg_grad", [](u slab, u R, u col_map, u csc_off, u csc_rows, u inv_std, u pmask, int64_t N, int F,
-                          int Fd, int K, int T, int tstride, int ntiles, u G, u loss, int KP, int n_models,
-                          u stream) {
+  m.def("logreg_grad", [](u slab, u R, u col_map, u csc_rows, u slice_lo, u col_slice, u blk_col, u blk_slice,
+                          int n_blocks, u inv_std, u pmask, int64_t N, int F, int Fd, int K, int T, int tstride,
+                          int ntiles, u G, u loss, int KP, int n_models, u stream) {
     LogregGradArgs a;
     a.slab = P<const float>(slab);
     a.R = P<const float>(R);
     a.col_map = P<const int32_t>(col_map);
-    a.csc_off = P<const int32_t>(csc_off);
     a.csc_rows = P<const int32_t>(csc_rows);
+    a.slice_lo = P<const int32_t>(slice_lo);
+    a.col_slice = P<const int32_t>(col_slice);
+    a.blk_col = P<const int32_t>(blk_col);
+    a.blk_slice = P<const int32_t>(blk_slice);
+    a.n_blocks = n_blocks;
     a.inv_std = P<const float>(inv_std);
     a.pmask = P<const float>(pmask);
     a.N = N;
@@ -190,8 +194,9 @@ PYBIND11_MODULE(_har_native, m) {
     a.loss = P<double>(loss);
     check(har_logreg_grad(&a, KP, n_models, S(stream)), "logreg_grad");
   });
-  // one L-BFGS phase (0 = direction + trial points, 1 = line-search pick + history update); the
-  // QnArgs fields come from a dict of ints / floats / device pointers (har.optim.lbfgs_device)
+  // one L-BFGS phase (logreg_qn.hip: 0 finalize + dots, 1 direction + trials, 2 pick + history,
+  // 3 finalize only); the QnArgs fields come from a dict of ints / floats / device pointers
+  m.def("qn_chunks", &har_qn_chunks);
   m.def("lbfgs_phase", [](int phase, py::dict d, int KP, u stream) {
     auto I = [&](const char* k) { return d[k].cast<int64_t>(); };
     auto U = [&](const char* k) { return d[k].cast<u>(); };
@@ -204,7 +209,12 @@ PYBIND11_MODULE(_har_native, m) {
     a.head = (int)I("head");
     a.filled = (int)I("filled");
     a.init = (int)I("init");
-    a.it = (int)I("it");
+    a.nch = (int)I("nch");
+    a.fin = (int)I("fin");
+    a.fin_only = 0;
+    a.fin_init = (int)I("fin_init");
+    a.fin_head = (int)I("fin_head");
+    a.fin_it = (int)I("fin_it");
     a.D = I("D");
     a.x = P<float>(U("x"));
     a.g = P<float>(U("g"));
@@ -216,7 +226,11 @@ PYBIND11_MODULE(_har_native, m) {
     a.S = P<float>(U("S"));
     a.Y = P<float>(U("Y"));
     a.rho = P<double>(U("rho"));
-    a.work = P<float>(U("work"));
+    a.SY = P<double>(U("SY"));
+    a.YY = P<double>(U("YY"));
+    a.P1 = P<double>(U("P1"));
+    a.P2 = P<double>(U("P2"));
+    a.P3 = P<double>(U("P3"));
     a.xtrial = P<float>(U("xtrial"));
     a.weff = P<float>(U("weff"));
     a.reg = P<double>(U("reg"));
@@ -227,10 +241,12 @@ PYBIND11_MODULE(_har_native, m) {
     a.active = P<int32_t>(U("active"));
     a.fails = P<int32_t>(U("fails"));
     a.iters = P<int32_t>(U("iters"));
+    a.steep = P<int32_t>(U("steep"));
+    a.pick = P<int32_t>(U("pick"));
     a.hist = P<double>(U("hist"));
     a.c1 = d["c1"].cast<double>();
     a.tol = d["tol"].cast<double>();
-    check(phase == 0 ? har_lbfgs_direction(&a, KP, S(stream)) : har_lbfgs_update(&a, S(stream)), "lbfgs_phase");
+    check(har_lbfgs_phase(&a, KP, phase, S(stream)), "lbfgs_phase");
   });
 
   m.def("confusion_matrix", [](u label, u pred, int64_t n, int K, u cm, u stream) {

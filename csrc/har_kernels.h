@@ -139,8 +139,12 @@ typedef struct LogregGradArgs {
   const float* slab;
   const float* R;
   const int32_t* col_map;   // [F+1]: >= 0 dense index, -1 intercept, <= -2 one-hot (CSC rows)
-  const int32_t* csc_off;   // [F+2] row-list offsets per column
-  const int32_t* csc_rows;  // row ids, ascending per column
+  const int32_t* csc_rows;  // row ids of the one-hot columns, column-major, ascending per column
+  const int32_t* slice_lo;  // [n_slices + 1] CSC range of every row slice (<= SL rows, one column each)
+  const int32_t* col_slice; // [F+2] first slice of each column
+  const int32_t* blk_col;   // [n_blocks + 1] column range of every workgroup (<= 256 columns)
+  const int32_t* blk_slice; // [n_blocks + 1] slice range of every workgroup (<= 256 slices)
+  int n_blocks;
   const float* inv_std;     // [S][F]
   const float* pmask;       // [S][K][F+1]
   int64_t N;
@@ -150,7 +154,8 @@ typedef struct LogregGradArgs {
 } LogregGradArgs;
 
 typedef struct QnArgs {
-  int B, T, K, F, m, head, filled, init, it;
+  int B, T, K, F, m, head, filled, init, nch;
+  int fin, fin_only, fin_init, fin_head, fin_it;  // phase 0 / 3: finalize the previous phase 2
   int64_t D;                // K * (F + 1)
   float* x;                 // [B][D] standardized parameters
   float* g;                 // [B][D] smooth gradient at x
@@ -162,7 +167,11 @@ typedef struct QnArgs {
   float* S;                 // [m][B][D]
   float* Y;                 // [m][B][D]
   double* rho;              // [m][B] (0 = empty / rejected slot)
-  float* work;              // [B][D]
+  double* SY;               // [B][m][m] history Gram matrix s_i . y_j
+  double* YY;               // [B][m][m] history Gram matrix y_i . y_j
+  double* P1;               // [B][nch][2m+1] chunk partials (phase 0)
+  double* P2;               // [B][nch][3T+2] chunk partials (phase 1)
+  double* P3;               // [B][nch][5+3m] chunk partials (phase 2)
   float* xtrial;            // [B*T][D]
   float* weff;              // [B*T][F+1][KP]
   double* reg;              // [B*T]
@@ -173,15 +182,17 @@ typedef struct QnArgs {
   int32_t* active;          // [B]
   int32_t* fails;           // [B]
   int32_t* iters;           // [B]
-  double* hist;             // [max_iter][B] objective per iteration (nullable)
+  int32_t* steep;           // [B] steepest descent this iteration (the last direction was not descent)
+  int32_t* pick;            // [B] trial taken by the last phase 2 (-1 none, -2 non-descent)
+  double* hist;             // [max_iter + 1][B] objective per iteration (nullable)
   double c1, tol;
 } QnArgs;
 
 int har_logreg_eval(const LogregEvalArgs* a, int KP, int n_models, hipStream_t s);
 int har_logreg_eval_tiles(int64_t n);
 int har_logreg_grad(const LogregGradArgs* a, int KP, int n_models, hipStream_t s);
-int har_lbfgs_direction(const QnArgs* a, int KP, hipStream_t s);
-int har_lbfgs_update(const QnArgs* a, hipStream_t s);
+int har_qn_chunks(int64_t D);
+int har_lbfgs_phase(const QnArgs* a, int KP, int phase, hipStream_t s);
 
 int har_logreg_softmax_grad(const float* Z, int64_t n, int nmodels, int K, int ld, const int32_t* y,
                             const float* rw, const float* inv_wsum, float* R, double* loss,

@@ -34,7 +34,6 @@
 namespace {
 
 constexpr int EVAL_ROWS = 256;
-constexpr int QN_THREADS = 1024;
 
 // ---------------------------------------------------------------------------------------------
 // logreg_eval: one workgroup = EVAL_ROWS rows x one (trial) model
@@ -153,13 +152,19 @@ __global__ __launch_bounds__(EVAL_ROWS) void logreg_eval_kernel(LogregEvalArgs a
 }
 
 // ---------------------------------------------------------------------------------------------
-// logreg_grad: one lane per (column, trial model); G[bt][k][col], loss[bt]
+// logreg_grad: G[bt][k][col], loss[bt].  Workgroup w owns the column range
+// [blk_col[w], blk_col[w+1]) and the row SLICES of its one-hot columns [blk_slice[w],
+// blk_slice[w+1]) (<= 256 of each; a column's CSC row list is cut into slices of <= SL rows on
+// the host, so a frequent category — '?' in XPEAK, hundreds of rows — is spread over many lanes
+// instead of serializing one).  Phase 1: one lane per slice sums its rows' residuals into LDS;
+// phase 2: one lane per column sums its slices (or the tile slabs of a dense column / the
+// intercept) in order.  Fixed summation order everywhere: bitwise reproducible.
 // ---------------------------------------------------------------------------------------------
 template <int KP>
 __global__ __launch_bounds__(256) void logreg_grad_kernel(LogregGradArgs a) {
+  __shared__ float part[256 * KP];
   const int bt = blockIdx.y * a.tstride;
   const int s = bt / a.T;
-  const int col = blockIdx.x * 256 + threadIdx.x;
   const int Fp1 = a.F + 1;
   const int SW = a.Fd * KP + KP + 1;
   const float* slab = a.slab + (int64_t)bt * a.ntiles * SW;
@@ -168,21 +173,16 @@ __global__ __launch_bounds__(256) void logreg_grad_kernel(LogregGradArgs a) {
     for (int t = 0; t < a.ntiles; ++t) l += (double)slab[(int64_t)t * SW + SW - 1];
     a.loss[bt] = l;
   }
-  if (col >= Fp1) return;
-  const int cm = a.col_map[col];
-  float g[KP];
+  const int s0 = a.blk_slice[blockIdx.x], s1 = a.blk_slice[blockIdx.x + 1];
+  const int c0 = a.blk_col[blockIdx.x], c1 = a.blk_col[blockIdx.x + 1];
+  const float* R = a.R + (int64_t)bt * a.N * KP;
+  if (threadIdx.x < s1 - s0) {
+    const int sl = s0 + threadIdx.x;
+    const int lo = a.slice_lo[sl], hi = a.slice_lo[sl + 1];
+    float g[KP];
 #pragma unroll
-  for (int k = 0; k < KP; ++k) g[k] = 0.f;
-  if (cm >= 0 || cm == -1) {  // dense column j = cm, or the intercept (slab entries after the dense block)
-    const int off = cm >= 0 ? cm * KP : a.Fd * KP;
-    for (int t = 0; t < a.ntiles; ++t) {
-      const float* p = slab + (int64_t)t * SW + off;
-#pragma unroll
-      for (int k = 0; k < KP; ++k) g[k] += p[k];
-    }
-  } else {  // one-hot column: its rows (CSC list, ascending row order)
-    const int lo = a.csc_off[col], hi = a.csc_off[col + 1];
-    const float* R = a.R + (int64_t)bt * a.N * KP;
+    for (int k = 0; k < KP; ++k) g[k] = 0.f;
+#pragma unroll 4
     for (int i = lo; i < hi; ++i) {
       const f32x4_t* rp = reinterpret_cast<const f32x4_t*>(R + (int64_t)a.csc_rows[i] * KP);
 #pragma unroll
@@ -194,6 +194,28 @@ __global__ __launch_bounds__(256) void logreg_grad_kernel(LogregGradArgs a) {
         g[4 * q + 3] += r4[3];
       }
     }
+#pragma unroll
+    for (int k = 0; k < KP; ++k) part[threadIdx.x * KP + k] = g[k];
+  }
+  __syncthreads();
+  const int col = c0 + threadIdx.x;
+  if (col >= c1) return;
+  const int cm = a.col_map[col];
+  float g[KP];
+#pragma unroll
+  for (int k = 0; k < KP; ++k) g[k] = 0.f;
+  if (cm >= 0 || cm == -1) {  // dense column j = cm, or the intercept (slab entries after the dense block)
+    const int off = cm >= 0 ? cm * KP : a.Fd * KP;
+    for (int t = 0; t < a.ntiles; ++t) {
+      const float* p = slab + (int64_t)t * SW + off;
+#pragma unroll
+      for (int k = 0; k < KP; ++k) g[k] += p[k];
+    }
+  } else {  // one-hot column: its slices, in row order
+    for (int sl = a.col_slice[col]; sl < a.col_slice[col + 1]; ++sl) {
+#pragma unroll
+      for (int k = 0; k < KP; ++k) g[k] += part[(sl - s0) * KP + k];
+    }
   }
   const float sc = col < a.F ? a.inv_std[(int64_t)s * a.F + col] : 1.f;
   const int64_t D = (int64_t)a.K * Fp1;
@@ -203,8 +225,38 @@ __global__ __launch_bounds__(256) void logreg_grad_kernel(LogregGradArgs a) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// block reductions for the QN kernels (1024 threads = 16 waves)
+// Batched L-BFGS / OWL-QN, chunked over the whole chip.
+//
+// Every model's parameter vector (D = K (F+1) = 18,606 for WISDM) is cut into QN_CHUNK-element
+// chunks and each phase runs one 256-thread workgroup per (chunk, model), so a single fit
+// streams its history (m = 10 pairs of D floats) with tens of CUs instead of one.  Cross-chunk
+// sums go through per-chunk fp64 partial slabs reduced in chunk order by the consumer (fixed
+// order: bitwise reproducible).  The two-loop recursion runs in coefficient space on the history
+// Gram matrices SY[i][j] = s_i.y_j and YY[i][j] = y_i.y_j (maintained as pairs enter), so a
+// direction costs two streaming sweeps instead of 4m dependent ones.
+//
+//   phase 0  (chunks x B)  lane 0 of chunk 0 finalizes the previous update of its model (Gram
+//                          rows of the new pair, rho, objective, convergence / failure flags);
+//                          every chunk: pg and the partial dots s_j.pg, y_j.pg, pg.pg -> P1
+//   phase 1  (chunks x B)  reduce P1 -> recursion coefficients (lane 0) -> per element
+//                          d = -(gamma pg + sum cY_j y_j + cS_j s_j) (orthant-restricted), the T
+//                          trial points x + a0 2^-t d and their W_eff; partial reg / decrease /
+//                          pg.d -> P2
+//   (logreg_eval + logreg_grad evaluate the B*T trial models)
+//   phase 2  (chunks x B)  reduce P2 -> pick the largest Armijo-satisfying trial (or reject a
+//                          non-descent direction: steepest descent next iteration) -> per element
+//                          s, y into the history slot, x, g; partial dots of the new pair with
+//                          every slot -> P3
+//   phase 3  (B)           finalize only (after the last iteration)
 // ---------------------------------------------------------------------------------------------
+constexpr int QN_BLOCK = 256;
+constexpr int QN_CHUNK = 2048;
+constexpr int QN_MAX_TRIALS = 4;
+constexpr int QN_MAX_M = 10;
+constexpr int NP1 = 2 * QN_MAX_M + 1;        // s_j.pg, y_j.pg, pg.pg
+constexpr int NP2 = 3 * QN_MAX_TRIALS + 2;   // per trial: 0.5 l2 x^2, l1 |x|, pg.(xt - x); then pg.d, pg.pg
+constexpr int NP3 = 5 + 3 * QN_MAX_M;        // s.y, s.s, y.y, x.x, pg.pg, then s.y_j, s_j.y, y.y_j
+
 template <int NV>
 __device__ __forceinline__ void block_sum(double (&v)[NV], double* sh) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -219,10 +271,29 @@ __device__ __forceinline__ void block_sum(double (&v)[NV], double* sh) {
 #pragma unroll
   for (int q = 0; q < NV; ++q) {
     double t = 0.0;
-    for (int i = 0; i < QN_THREADS / 64; ++i) t += sh[i * NV + q];  // fixed order
+#pragma unroll
+    for (int i = 0; i < QN_BLOCK / 64; ++i) t += sh[i * NV + q];  // fixed order
     v[q] = t;
   }
   __syncthreads();
+}
+
+template <int NV>
+__device__ __forceinline__ void reduce_chunks(const double* P, int nch, double (&v)[NV]) {
+#pragma unroll
+  for (int q = 0; q < NV; ++q) v[q] = 0.0;
+  for (int c = 0; c < nch; ++c) {
+#pragma unroll
+    for (int q = 0; q < NV; ++q) v[q] += P[c * NV + q];
+  }
+}
+
+template <int NV>
+__device__ __forceinline__ void store_partial(double (&v)[NV], double* P) {
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int q = 0; q < NV; ++q) P[q] = v[q];
+  }
 }
 
 __device__ __forceinline__ float pseudo_grad(float x, float g, float l1) {
@@ -235,218 +306,306 @@ __device__ __forceinline__ float pseudo_grad(float x, float g, float l1) {
 
 __device__ __forceinline__ float sgnf(float v) { return v > 0.f ? 1.f : (v < 0.f ? -1.f : 0.f); }
 
-// ---------------------------------------------------------------------------------------------
-// lbfgs_direction: one workgroup per model b
-// ---------------------------------------------------------------------------------------------
-template <int KP>
-__global__ __launch_bounds__(QN_THREADS) void lbfgs_direction_kernel(QnArgs a) {
-  __shared__ double sh[16 * 4];
-  __shared__ double alph[32];
-  const int b = blockIdx.x;
-  const int64_t D = a.D;
-  const int Fp1 = a.F + 1;
-  const float* x = a.x + b * D;
-  const float* g = a.g + b * D;
-  const float* l1v = a.l1 ? a.l1 + b * D : nullptr;
-  float* q = a.work + b * D;  // q, then r, then the direction
-  const int tid = threadIdx.x;
-  const bool active = a.active[b] != 0;
-
-  double dd = 0.0, gamma = 1.0;
-  if (a.init) {
-    for (int64_t e = tid; e < D; e += QN_THREADS) q[e] = 0.f;
+// the previous phase 2 of model b, completed by one lane (pick[b]: >= 0 accepted trial, -1 no
+// trial accepted / inactive, -2 non-descent direction)
+__device__ void qn_finalize(const QnArgs& a, int b) {
+  const int mm = a.m;
+  const int p = a.pick[b];
+  if (a.fin_init) {
+    a.fobj[b] = a.loss[b * a.T] + a.reg[b * a.T];
+    if (a.hist) a.hist[b] = a.fobj[b];
+    return;
+  }
+  const int h = a.fin_head;
+  if (p >= 0) {
+    double v[NP3];
+    reduce_chunks<NP3>(a.P3 + (int64_t)b * a.nch * NP3, a.nch, v);
+    double* SY = a.SY + (int64_t)b * mm * mm;
+    double* YY = a.YY + (int64_t)b * mm * mm;
+    SY[h * mm + h] = v[0];
+    YY[h * mm + h] = v[2];
+    for (int j = 0; j < mm; ++j) {
+      if (j == h) continue;
+      SY[h * mm + j] = v[5 + 3 * j];
+      SY[j * mm + h] = v[6 + 3 * j];
+      YY[h * mm + j] = YY[j * mm + h] = v[7 + 3 * j];
+    }
+    const bool good = v[0] > 1e-10 * fmax(sqrt(v[1]) * sqrt(v[2]), 1e-300);
+    a.rho[h * a.B + b] = good ? 1.0 / v[0] : 0.0;
+    const int bt = b * a.T + p;
+    const double Fn = a.loss[bt] + a.reg[bt];
+    const double F0 = a.fobj[b];
+    const double rel = fabs(F0 - Fn) / fmax(fmax(fabs(F0), fabs(Fn)), 1.0);
+    a.fobj[b] = Fn;
+    a.iters[b] += 1;
+    a.fails[b] = 0;
+    a.steep[b] = 0;
+    a.step_scale[b] = 1.0f;
+    if (rel < a.tol || sqrt(v[4]) <= a.tol * fmax(sqrt(v[3]), 1.0)) a.active[b] = 0;
+  } else if (p == -2) {  // the recursion produced no descent direction: steepest descent next
+    a.rho[h * a.B + b] = 0.0;
+    a.steep[b] = 1;
   } else {
-    // pseudo-gradient -> q
-    double pn[1] = {0.0};
-    for (int64_t e = tid; e < D; e += QN_THREADS) {
-      const float pg = pseudo_grad(x[e], g[e], l1v ? l1v[e] : 0.f);
-      q[e] = pg;
-      pn[0] += (double)pg * pg;
-    }
-    block_sum<1>(pn, sh);
-    // first loop: newest -> oldest
-    for (int i = 0; i < a.filled; ++i) {
-      const int j = (a.head - 1 - i + a.m) % a.m;
-      const float* S = a.S + ((int64_t)j * a.B + b) * D;
-      const float* Y = a.Y + ((int64_t)j * a.B + b) * D;
-      const double rho = a.rho[j * a.B + b];
-      double v[1] = {0.0};
-      if (rho != 0.0)
-        for (int64_t e = tid; e < D; e += QN_THREADS) v[0] += (double)S[e] * q[e];
-      block_sum<1>(v, sh);
-      const double al = rho * v[0];
-      if (tid == 0) alph[i] = al;
-      if (rho != 0.0)
-        for (int64_t e = tid; e < D; e += QN_THREADS) q[e] = (float)((double)q[e] - al * Y[e]);
-    }
-    if (a.filled > 0) {
-      const int j = (a.head - 1 + a.m) % a.m;
-      const float* S = a.S + ((int64_t)j * a.B + b) * D;
-      const float* Y = a.Y + ((int64_t)j * a.B + b) * D;
-      const double rho = a.rho[j * a.B + b];
-      double v[2] = {0.0, 0.0};
-      for (int64_t e = tid; e < D; e += QN_THREADS) {
-        v[0] += (double)Y[e] * Y[e];
-        v[1] += (double)S[e] * Y[e];
-      }
-      block_sum<2>(v, sh);
-      gamma = (rho > 0.0 && v[0] > 0.0) ? v[1] / v[0] : 1.0;
-    } else {
-      gamma = 1.0 / fmax(sqrt(pn[0]), 1e-12);
-    }
-    for (int64_t e = tid; e < D; e += QN_THREADS) q[e] = (float)(gamma * q[e]);
-    __syncthreads();
-    // second loop: oldest -> newest
-    for (int i = a.filled - 1; i >= 0; --i) {
-      const int j = (a.head - 1 - i + a.m) % a.m;
-      const float* S = a.S + ((int64_t)j * a.B + b) * D;
-      const float* Y = a.Y + ((int64_t)j * a.B + b) * D;
-      const double rho = a.rho[j * a.B + b];
-      double v[1] = {0.0};
-      if (rho != 0.0)
-        for (int64_t e = tid; e < D; e += QN_THREADS) v[0] += (double)Y[e] * q[e];
-      block_sum<1>(v, sh);
-      const double coef = alph[i] - rho * v[0];
-      if (rho != 0.0)
-        for (int64_t e = tid; e < D; e += QN_THREADS) q[e] = (float)((double)q[e] + coef * S[e]);
-    }
-    __syncthreads();
-    // direction d = -r, orthant-restricted for OWL-QN; descent check
-    double v[2] = {0.0, 0.0};
-    for (int64_t e = tid; e < D; e += QN_THREADS) {
-      const float pg = pseudo_grad(x[e], g[e], l1v ? l1v[e] : 0.f);
-      float d = -q[e];
-      if (l1v && d * pg >= 0.f) d = 0.f;
-      q[e] = d;
-      v[0] += (double)pg * d;
-      v[1] += (double)pg * pg;
-    }
-    block_sum<2>(v, sh);
-    dd = v[0];
-    if (dd >= 0.0) {  // not a descent direction: steepest descent on the pseudo-gradient
-      for (int64_t e = tid; e < D; e += QN_THREADS) q[e] = -pseudo_grad(x[e], g[e], l1v ? l1v[e] : 0.f);
-      dd = -v[1];
-    }
-    __syncthreads();
-  }
-  // trial points, their effective weights, regularization and Armijo decrease terms
-  const int T = a.init ? 1 : a.T;
-  for (int t = 0; t < T; ++t) {
-    const float step = a.init ? 0.f : a.step_scale[b] * ldexpf(1.f, -t);
-    const int bt = b * a.T + t;
-    float* xt = a.xtrial + (int64_t)bt * D;
-    float* W = a.weff + (int64_t)bt * Fp1 * KP;
-    double v[3] = {0.0, 0.0, 0.0};  // 0.5 l2 |beta|^2, l1 |x|_1, pg . (xt - x)
-    for (int64_t e = tid; e < D; e += QN_THREADS) {
-      const float xe = x[e];
-      float xn = xe + step * q[e];
-      const float l1e = l1v ? l1v[e] : 0.f;
-      if (l1v && !a.init) {  // stay in the orthant of x (or of -pg where x == 0)
-        const float pg = pseudo_grad(xe, g[e], l1e);
-        const float xi = xe != 0.f ? sgnf(xe) : sgnf(-pg);
-        if (sgnf(xn) != xi) xn = 0.f;
-        v[2] += (double)pg * (xn - xe);
-      }
-      if (!active) xn = xe;
-      xt[e] = xn;
-      const float l2e = a.l2[b * D + e];
-      v[0] += 0.5 * (double)l2e * xn * xn;
-      v[1] += (double)l1e * fabsf(xn);
-      const int k = (int)(e / Fp1), col = (int)(e % Fp1);
-      const float pm = a.pmask[b * D + e];
-      const float sc = col < a.F ? a.inv_std[(int64_t)b * a.F + col] : 1.f;
-      W[(int64_t)col * KP + k] = xn * sc * pm;
-    }
-    block_sum<3>(v, sh);
-    if (tid == 0) {
-      a.reg[bt] = v[0] + v[1];
-      a.decr[bt] = l1v ? v[2] : (double)step * dd;
+    a.rho[h * a.B + b] = 0.0;
+    if (a.active[b]) {
+      a.step_scale[b] *= 1.0f / 16.0f;
+      if (++a.fails[b] >= 2) a.active[b] = 0;
     }
   }
+  if (a.hist) a.hist[(int64_t)a.fin_it * a.B + b] = a.fobj[b];
 }
 
-// ---------------------------------------------------------------------------------------------
-// lbfgs_update: one workgroup per model b
-// ---------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(QN_THREADS) void lbfgs_update_kernel(QnArgs a) {
-  __shared__ double sh[16 * 5];
-  __shared__ int pick;
-  const int b = blockIdx.x;
-  const int64_t D = a.D;
-  const int tid = threadIdx.x;
-  float* x = a.x + b * D;
-  float* g = a.g + b * D;
-  const float* l1v = a.l1 ? a.l1 + b * D : nullptr;
+// phase 0
+__global__ __launch_bounds__(QN_BLOCK) void qn_dots_kernel(QnArgs a) {
+  __shared__ double sh[4 * NP1];
+  const int c = blockIdx.x, b = blockIdx.y;
+  if (a.fin && c == 0 && threadIdx.x == 0) qn_finalize(a, b);
+  if (a.fin_only) return;
+  const int D = (int)a.D;
+  const int mm = a.m;
+  const int64_t sstride = (int64_t)a.B * D;
+  const float* __restrict__ x = a.x + (int64_t)b * D;
+  const float* __restrict__ g = a.g + (int64_t)b * D;
+  const float* __restrict__ l1v = a.l1 ? a.l1 + (int64_t)b * D : nullptr;
+  const float* __restrict__ Sb = a.S + (int64_t)b * D;
+  const float* __restrict__ Yb = a.Y + (int64_t)b * D;
+  const int e1 = min(D, (c + 1) * QN_CHUNK);
+  float acc[NP1];
+#pragma unroll
+  for (int j = 0; j < NP1; ++j) acc[j] = 0.f;
+#pragma unroll 2
+  for (int e = c * QN_CHUNK + threadIdx.x; e < e1; e += QN_BLOCK) {
+    const float pg = pseudo_grad(x[e], g[e], l1v ? l1v[e] : 0.f);
+    acc[2 * QN_MAX_M] = fmaf(pg, pg, acc[2 * QN_MAX_M]);
+#pragma unroll
+    for (int j = 0; j < QN_MAX_M; ++j) {
+      if (j < mm) {
+        acc[j] = fmaf(Sb[j * sstride + e], pg, acc[j]);
+        acc[QN_MAX_M + j] = fmaf(Yb[j * sstride + e], pg, acc[QN_MAX_M + j]);
+      }
+    }
+  }
+  double v[NP1];
+#pragma unroll
+  for (int j = 0; j < NP1; ++j) v[j] = (double)acc[j];
+  block_sum<NP1>(v, sh);
+  store_partial<NP1>(v, a.P1 + ((int64_t)b * a.nch + c) * NP1);
+}
+
+// phase 1
+template <int KP>
+__global__ __launch_bounds__(QN_BLOCK) void qn_direction_kernel(QnArgs a) {
+  __shared__ double sh[4 * NP2];
+  __shared__ float cS[QN_MAX_M], cY[QN_MAX_M];
+  __shared__ float gam;
+  const int c = blockIdx.x, b = blockIdx.y;
+  const int D = (int)a.D;
+  const int mm = a.m;
+  const int Fp1 = a.F + 1;
+  const bool steep = a.steep[b] != 0;
+  if (threadIdx.x == 0) {
+    float gamma = 0.f;
+    for (int j = 0; j < QN_MAX_M; ++j) cS[j] = cY[j] = 0.f;
+    if (!a.init && !steep) {  // the two-loop recursion on coefficients
+      double v[NP1];
+      reduce_chunks<NP1>(a.P1 + (int64_t)b * a.nch * NP1, a.nch, v);
+      const double* SY = a.SY + (int64_t)b * mm * mm;
+      const double* YY = a.YY + (int64_t)b * mm * mm;
+      double u[QN_MAX_M], w[QN_MAX_M], al[QN_MAX_M];
+      for (int j = 0; j < QN_MAX_M; ++j) u[j] = w[j] = al[j] = 0.0;
+      for (int i = 0; i < a.filled; ++i) {  // newest -> oldest: q = pg + sum u_k y_k
+        const int j = (a.head - 1 - i + mm) % mm;
+        const double rho = a.rho[j * a.B + b];
+        if (rho == 0.0) continue;
+        double sq = v[j];
+        for (int k = 0; k < mm; ++k) sq += u[k] * SY[j * mm + k];
+        al[j] = rho * sq;
+        u[j] -= al[j];
+      }
+      double gm;
+      if (a.filled == 0) {
+        gm = 1.0 / fmax(sqrt(v[2 * QN_MAX_M]), 1e-12);
+      } else {
+        const int n = (a.head - 1 + mm) % mm;
+        const double yy = YY[n * mm + n];
+        gm = (a.rho[n * a.B + b] > 0.0 && yy > 0.0) ? SY[n * mm + n] / yy : 1.0;
+      }
+      for (int i = a.filled - 1; i >= 0; --i) {  // oldest -> newest: r = gamma q + sum w_k s_k
+        const int j = (a.head - 1 - i + mm) % mm;
+        const double rho = a.rho[j * a.B + b];
+        if (rho == 0.0) continue;
+        double yr = v[QN_MAX_M + j];
+        for (int k = 0; k < mm; ++k) yr += u[k] * YY[j * mm + k];
+        yr *= gm;
+        for (int k = 0; k < mm; ++k) yr += w[k] * SY[k * mm + j];
+        w[j] += al[j] - rho * yr;
+      }
+      for (int j = 0; j < mm; ++j) {
+        cY[j] = (float)(gm * u[j]);
+        cS[j] = (float)w[j];
+      }
+      gamma = (float)gm;
+    }
+    gam = gamma;
+  }
+  __syncthreads();
+  const int64_t sstride = (int64_t)a.B * D;
+  const float* __restrict__ x = a.x + (int64_t)b * D;
+  const float* __restrict__ g = a.g + (int64_t)b * D;
+  const float* __restrict__ l1v = a.l1 ? a.l1 + (int64_t)b * D : nullptr;
+  const float* __restrict__ Sb = a.S + (int64_t)b * D;
+  const float* __restrict__ Yb = a.Y + (int64_t)b * D;
   const bool active = a.active[b] != 0;
-  if (tid == 0) {
+  const int T = a.init ? 1 : a.T;
+  const float s0 = a.init ? 0.f : a.step_scale[b];
+  const float gamma = gam;
+  const int e1 = min(D, (c + 1) * QN_CHUNK);
+  float r[NP2];
+#pragma unroll
+  for (int t = 0; t < NP2; ++t) r[t] = 0.f;
+#pragma unroll 2
+  for (int e = c * QN_CHUNK + threadIdx.x; e < e1; e += QN_BLOCK) {
+    const float xe = x[e];
+    const float l1e = l1v ? l1v[e] : 0.f;
+    const float pg = a.init ? 0.f : pseudo_grad(xe, g[e], l1e);
+    float d = 0.f;
+    if (!a.init) {
+      if (steep) {
+        d = -pg;
+      } else {
+        float acc = gamma * pg;
+#pragma unroll
+        for (int j = 0; j < QN_MAX_M; ++j) {
+          if (j < mm) {
+            acc = fmaf(cY[j], Yb[j * sstride + e], acc);
+            acc = fmaf(cS[j], Sb[j * sstride + e], acc);
+          }
+        }
+        d = -acc;
+        if (l1v && d * pg >= 0.f) d = 0.f;  // OWL-QN: keep the direction in pg's orthant
+      }
+    }
+    r[3 * QN_MAX_TRIALS] = fmaf(pg, d, r[3 * QN_MAX_TRIALS]);
+    r[3 * QN_MAX_TRIALS + 1] = fmaf(pg, pg, r[3 * QN_MAX_TRIALS + 1]);
+    const float xi = xe != 0.f ? sgnf(xe) : sgnf(-pg);
+    const float hl2 = 0.5f * a.l2[(int64_t)b * D + e];
+    const int k = e / Fp1, col = e - k * Fp1;
+    const float wsc = a.pmask[(int64_t)b * D + e] * (col < a.F ? a.inv_std[(int64_t)b * a.F + col] : 1.f);
+#pragma unroll
+    for (int t = 0; t < QN_MAX_TRIALS; ++t) {
+      if (t < T) {
+        float xn = xe + s0 * ldexpf(1.f, -t) * d;
+        if (l1v && !a.init) {  // stay in the orthant of x (or of -pg where x == 0)
+          if (sgnf(xn) != xi) xn = 0.f;
+          r[3 * t + 2] = fmaf(pg, xn - xe, r[3 * t + 2]);
+        }
+        if (!active) xn = xe;
+        const int bt = b * a.T + t;
+        a.xtrial[(int64_t)bt * D + e] = xn;
+        r[3 * t] = fmaf(hl2, xn * xn, r[3 * t]);
+        r[3 * t + 1] = fmaf(l1e, fabsf(xn), r[3 * t + 1]);
+        a.weff[((int64_t)bt * Fp1 + col) * KP + k] = xn * wsc;
+      }
+    }
+  }
+  double v[NP2];
+#pragma unroll
+  for (int t = 0; t < NP2; ++t) v[t] = (double)r[t];
+  block_sum<NP2>(v, sh);
+  store_partial<NP2>(v, a.P2 + ((int64_t)b * a.nch + c) * NP2);
+}
+
+// phase 2
+__global__ __launch_bounds__(QN_BLOCK) void qn_update_kernel(QnArgs a) {
+  __shared__ double sh[4 * NP3];
+  __shared__ int pick;
+  const int c = blockIdx.x, b = blockIdx.y;
+  const int D = (int)a.D;
+  const int mm = a.m;
+  const bool active = a.active[b] != 0;
+  if (threadIdx.x == 0) {
+    double v[NP2];
+    reduce_chunks<NP2>(a.P2 + (int64_t)b * a.nch * NP2, a.nch, v);
+    const bool steep = a.steep[b] != 0;
+    const double dd = steep ? -v[3 * QN_MAX_TRIALS + 1] : v[3 * QN_MAX_TRIALS];
+    const int T = a.init ? 1 : a.T;
+    const float s0 = a.init ? 0.f : a.step_scale[b];
     int p = -1;
     if (a.init) {
       p = 0;
     } else if (active) {
-      const double F0 = a.fobj[b];
-      for (int t = 0; t < a.T && p < 0; ++t) {
-        const int bt = b * a.T + t;
-        const double Ft = a.loss[bt] + a.reg[bt];
-        if (isfinite(Ft) && Ft <= F0 + a.c1 * a.decr[bt]) p = t;
+      if (dd >= 0.0) {
+        p = steep ? -1 : -2;
+      } else {
+        const double F0 = a.fobj[b];
+        for (int t = 0; t < T && p < 0; ++t) {
+          const int bt = b * a.T + t;
+          const double decr = a.l1 ? v[3 * t + 2] : (double)(s0 * ldexpf(1.f, -t)) * dd;
+          const double Ft = a.loss[bt] + v[3 * t] + v[3 * t + 1];
+          if (isfinite(Ft) && Ft <= F0 + a.c1 * decr) p = t;
+        }
+      }
+    }
+    if (c == 0) {
+      a.pick[b] = p;
+      for (int t = 0; t < T; ++t) {
+        a.reg[b * a.T + t] = v[3 * t] + v[3 * t + 1];
+        a.decr[b * a.T + t] = a.l1 ? v[3 * t + 2] : (double)(s0 * ldexpf(1.f, -t)) * dd;
       }
     }
     pick = p;
   }
   __syncthreads();
   const int p = pick;
-  float* S = a.S + ((int64_t)a.head * a.B + b) * D;
-  float* Y = a.Y + ((int64_t)a.head * a.B + b) * D;
-  if (p < 0) {  // inactive, or no trial accepted: keep x; disable the slot; shrink the next steps
+  if (p < 0) return;
+  const int64_t sstride = (int64_t)a.B * D;
+  float* __restrict__ x = a.x + (int64_t)b * D;
+  float* __restrict__ g = a.g + (int64_t)b * D;
+  const float* __restrict__ l1v = a.l1 ? a.l1 + (int64_t)b * D : nullptr;
+  float* __restrict__ Sh = a.S + (int64_t)a.head * sstride + (int64_t)b * D;
+  float* __restrict__ Yh = a.Y + (int64_t)a.head * sstride + (int64_t)b * D;
+  const float* __restrict__ Sb = a.S + (int64_t)b * D;
+  const float* __restrict__ Yb = a.Y + (int64_t)b * D;
+  const int bt = b * a.T + p;
+  const float* __restrict__ xt = a.xtrial + (int64_t)bt * D;
+  const float* __restrict__ Gt = a.G + (int64_t)bt * D;
+  const float* __restrict__ l2 = a.l2 + (int64_t)b * D;
+  const int e1 = min(D, (c + 1) * QN_CHUNK);
+  float ps[NP3];
+#pragma unroll
+  for (int q = 0; q < NP3; ++q) ps[q] = 0.f;
+#pragma unroll 2
+  for (int e = c * QN_CHUNK + threadIdx.x; e < e1; e += QN_BLOCK) {
+    const float xn = xt[e];
+    const float gn = Gt[e] + l2[e] * xn;  // data gradient (masked, scaled) + L2 term
     if (!a.init) {
-      if (tid == 0) {
-        a.rho[a.head * a.B + b] = 0.0;
-        if (active) {
-          a.step_scale[b] *= 1.0f / 16.0f;
-          if (++a.fails[b] >= 2) a.active[b] = 0;
+      const float se = xn - x[e], ye = gn - g[e];
+      Sh[e] = se;
+      Yh[e] = ye;
+      ps[0] = fmaf(se, ye, ps[0]);
+      ps[1] = fmaf(se, se, ps[1]);
+      ps[2] = fmaf(ye, ye, ps[2]);
+#pragma unroll
+      for (int j = 0; j < QN_MAX_M; ++j) {
+        if (j < mm && j != a.head) {
+          const float sj = Sb[j * sstride + e], yj = Yb[j * sstride + e];
+          ps[5 + 3 * j] = fmaf(se, yj, ps[5 + 3 * j]);
+          ps[6 + 3 * j] = fmaf(sj, ye, ps[6 + 3 * j]);
+          ps[7 + 3 * j] = fmaf(ye, yj, ps[7 + 3 * j]);
         }
       }
     }
-    return;
-  }
-  const int bt = b * a.T + p;
-  const float* xt = a.xtrial + (int64_t)bt * D;
-  const float* Gt = a.G + (int64_t)bt * D;
-  double v[5] = {0.0, 0.0, 0.0, 0.0, 0.0};  // s.y, |s|^2, |y|^2, |x_new|^2, |pg_new|^2
-  for (int64_t e = tid; e < D; e += QN_THREADS) {
-    const float xn = xt[e];
-    const float gn = Gt[e] + a.l2[b * D + e] * xn;  // data gradient (masked, scaled) + L2 term
-    if (!a.init) {
-      const float se = xn - x[e], ye = gn - g[e];
-      S[e] = se;
-      Y[e] = ye;
-      v[0] += (double)se * ye;
-      v[1] += (double)se * se;
-      v[2] += (double)ye * ye;
-    }
     const float pg = pseudo_grad(xn, gn, l1v ? l1v[e] : 0.f);
-    v[3] += (double)xn * xn;
-    v[4] += (double)pg * pg;
+    ps[3] = fmaf(xn, xn, ps[3]);
+    ps[4] = fmaf(pg, pg, ps[4]);
     x[e] = xn;
     g[e] = gn;
   }
-  block_sum<5>(v, sh);
-  if (tid == 0) {
-    const double Fn = a.loss[bt] + a.reg[bt];
-    if (a.init) {
-      a.fobj[b] = Fn;
-    } else {
-      const bool good = v[0] > 1e-10 * fmax(sqrt(v[1]) * sqrt(v[2]), 1e-300);
-      a.rho[a.head * a.B + b] = good ? 1.0 / v[0] : 0.0;
-      const double F0 = a.fobj[b];
-      const double rel = fabs(F0 - Fn) / fmax(fmax(fabs(F0), fabs(Fn)), 1.0);
-      a.fobj[b] = Fn;
-      a.iters[b] += 1;
-      a.fails[b] = 0;
-      a.step_scale[b] = 1.0f;
-      if (rel < a.tol || sqrt(v[4]) <= a.tol * fmax(sqrt(v[3]), 1.0)) a.active[b] = 0;
-    }
-    if (a.hist) a.hist[(int64_t)a.it * a.B + b] = a.fobj[b];
-  }
+  double v[NP3];
+#pragma unroll
+  for (int q = 0; q < NP3; ++q) v[q] = (double)ps[q];
+  block_sum<NP3>(v, sh);
+  store_partial<NP3>(v, a.P3 + ((int64_t)b * a.nch + c) * NP3);
 }
 
 }  // namespace
@@ -472,9 +631,11 @@ extern "C" int har_logreg_eval_tiles(int64_t n) { return (int)((n + EVAL_ROWS - 
 
 extern "C" int har_logreg_grad(const LogregGradArgs* args, int KP, int n_models, hipStream_t s) {
   const LogregGradArgs& a = *args;
-  if (a.K < 1 || a.K > KP || (KP != 8 && KP != 16) || a.T < 1 || a.tstride < 1) return -2;
+  if (a.K < 1 || a.K > KP || (KP != 8 && KP != 16) || a.T < 1 || a.tstride < 1 || a.n_blocks < 1 ||
+      a.blk_col == nullptr || a.blk_slice == nullptr || a.col_slice == nullptr || a.slice_lo == nullptr)
+    return -2;
   if (n_models == 0) return 0;
-  dim3 grid((a.F + 1 + 255) / 256, n_models);
+  dim3 grid(a.n_blocks, n_models);
   if (KP == 8)
     logreg_grad_kernel<8><<<grid, 256, 0, s>>>(a);
   else
@@ -483,23 +644,30 @@ extern "C" int har_logreg_grad(const LogregGradArgs* args, int KP, int n_models,
   return 0;
 }
 
-extern "C" int har_lbfgs_direction(const QnArgs* args, int KP, hipStream_t s) {
-  const QnArgs& a = *args;
-  if ((KP != 8 && KP != 16) || a.K > KP || a.m > 32 || a.T < 1 || a.D != (int64_t)a.K * (a.F + 1)) return -2;
-  if (a.B == 0) return 0;
-  if (KP == 8)
-    lbfgs_direction_kernel<8><<<a.B, QN_THREADS, 0, s>>>(a);
-  else
-    lbfgs_direction_kernel<16><<<a.B, QN_THREADS, 0, s>>>(a);
-  HAR_CHECK_LAUNCH();
-  return 0;
-}
+extern "C" int har_qn_chunks(int64_t D) { return (int)((D + QN_CHUNK - 1) / QN_CHUNK); }
 
-extern "C" int har_lbfgs_update(const QnArgs* args, hipStream_t s) {
+extern "C" int har_lbfgs_phase(const QnArgs* args, int KP, int phase, hipStream_t s) {
   const QnArgs& a = *args;
-  if (a.m > 32 || a.T < 1) return -2;
+  if ((KP != 8 && KP != 16) || a.K > KP || a.m < 1 || a.m > QN_MAX_M || a.T < 1 || a.T > QN_MAX_TRIALS ||
+      a.D != (int64_t)a.K * (a.F + 1) || a.D >= (1LL << 31) || a.nch != har_qn_chunks(a.D) || phase < 0 ||
+      phase > 3)
+    return -2;
   if (a.B == 0) return 0;
-  lbfgs_update_kernel<<<a.B, QN_THREADS, 0, s>>>(a);
+  if (phase == 3) {
+    QnArgs f = a;
+    f.fin = 1;
+    f.fin_only = 1;
+    qn_dots_kernel<<<dim3(1, a.B), QN_BLOCK, 0, s>>>(f);
+  } else if (phase == 0) {
+    qn_dots_kernel<<<dim3(a.nch, a.B), QN_BLOCK, 0, s>>>(a);
+  } else if (phase == 1) {
+    if (KP == 8)
+      qn_direction_kernel<8><<<dim3(a.nch, a.B), QN_BLOCK, 0, s>>>(a);
+    else
+      qn_direction_kernel<16><<<dim3(a.nch, a.B), QN_BLOCK, 0, s>>>(a);
+  } else {
+    qn_update_kernel<<<dim3(a.nch, a.B), QN_BLOCK, 0, s>>>(a);
+  }
   HAR_CHECK_LAUNCH();
   return 0;
 }

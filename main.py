@@ -14,6 +14,7 @@ DecisionTree(+CV), RandomForest(+CV) — plus NaiveBayes and an MLP — and writ
     python main.py --preset all-numeric --save-models models/
     python main.py --csv-device                      # CSV parsed + dictionary-encoded by the HIP kernels
     python main.py --report                          # + Results table, charts and index.html (report/)
+    python main.py --raw raw.csv --hz 20 --window-sec 10 --overlap 0.5   # raw user,activity,timestamp,x,y,z rows
     torchrun --nproc-per-node 8 --master-addr 127.0.0.1 main.py   # data parallel over 8 GPUs (RCCL)
 
 Under ``torch.distributed.run`` every rank loads the (small) table and every model is
@@ -65,7 +66,15 @@ def run(cfg: RunConfig, ctx=None) -> dict:
 
     log.print("Loading Data Set...")
     with timer.phase("load_csv"):
-        raw = read_csv(cfg.data, device=dev if (cfg.csv_device and dev.type == "cuda") else None)
+        if cfg.raw:  # raw sensor rows -> device windowing + featurization -> the WISDM table
+            from har.features.raw import raw_to_table
+
+            raw = raw_to_table(cfg.raw, hz=cfg.hz, window_sec=cfg.window_sec, overlap=cfg.overlap, device=dev,
+                               ctx=ctx)
+            log.print(f"Raw stream {cfg.raw}: {raw.count()} windows of {int(round(cfg.hz * cfg.window_sec))} "
+                      f"samples ({cfg.window_sec:g} s at {cfg.hz:g} Hz, overlap {cfg.overlap:g})")
+        else:
+            raw = read_csv(cfg.data, device=dev if (cfg.csv_device and dev.type == "cuda") else None)
     with timer.phase("feature_pipeline"):
         data, pipe_model, df = wisdm.prepare(raw, cfg.encoding)
     section(log, "Data Schema")
