@@ -32,7 +32,9 @@ class RunConfig:
     split: List[float] = field(default_factory=lambda: [0.7, 0.3])
     seed: int = 2018
     device: str = "auto"
-    csv_device: bool = False               # parse + dictionary-encode the CSV with the HIP kernels
+    # on a GPU: parse + dictionary-encode the CSV with the HIP kernels and keep the table in HBM
+    # (the feature pipeline then runs on the device); --no-csv-device keeps the host parser
+    csv_device: bool = True
     # raw accelerometer rows (user,activity,timestamp,x,y,z) instead of the pre-windowed table:
     # windowed + featurized on the device into the WISDM columns (features/raw.py)
     raw: Optional[str] = None

@@ -123,6 +123,48 @@ class DeviceCsv:
         codes[present] = rank_t[inv]
         return codes, [vocab[i] for i in order], torch.from_numpy(counts[np.asarray(order, dtype=np.int64)])
 
+    def to_device_table(self) -> Table:
+        """Table of :class:`DeviceColumn` s: numeric planes stay in HBM (fp64 / int64 + missing
+        mask), string columns become device dictionary codes + host vocabulary (frequency
+        order is decided later by StringIndexer) with their fp64 parse kept for CastToDouble."""
+        from .table import DeviceColumn
+
+        cols = []
+        for j, (name, kind) in enumerate(zip(self.names, self.kinds)):
+            f = self.flags[j]
+            if kind in ("int", "long"):
+                miss = (f & F_FLOAT) == 0
+                v = torch.where(miss, torch.zeros_like(self.vals[j]), self.vals[j]).to(torch.int64)
+                cols.append(DeviceColumn(name, kind, v, miss))
+            elif kind == "double":
+                cols.append(DeviceColumn(name, "double", self.vals[j], (f & F_FLOAT) == 0))
+            else:
+                codes, vocab = self.dictionary_codes(name)
+                num = torch.where((f & F_FLOAT) != 0, self.vals[j], torch.full_like(self.vals[j], float("nan")))
+                cols.append(DeviceColumn(name, "string", codes, None, None, vocab, num))
+        return Table(cols)
+
+    def dictionary_codes(self, name: str) -> Tuple[torch.Tensor, List[str]]:
+        """Device dictionary codes (first-occurrence order, -1 = missing) and the vocabulary:
+        ``torch.unique`` over the 64-bit hashes, one representative span per value decoded."""
+        j = self.col_index(name)
+        miss = self.missing(j)
+        h = self.hashes[j]
+        present = ~miss
+        hp = h[present]
+        uniq, inv = torch.unique(hp, return_inverse=True)
+        rows = torch.nonzero(present).squeeze(1)
+        first = torch.full((uniq.numel(),), rows.numel(), dtype=torch.int64, device=h.device)
+        first.scatter_reduce_(0, inv, torch.arange(rows.numel(), device=h.device), reduce="amin")
+        rep = rows[first]
+        st = self.fstart[j][rep].cpu().numpy()
+        ln = self.flen[j][rep].cpu().numpy()
+        qt = ((self.flags[j][rep] & F_QUOTED) != 0).cpu().numpy()
+        vocab = [_unquote(self.raw[a:a + b], q) for a, b, q in zip(st, ln, qt)]
+        codes = torch.full((self.nrows,), -1, dtype=torch.int64, device=h.device)
+        codes[present] = inv
+        return codes, vocab
+
     def to_table(self) -> Table:
         cols = []
         flags = self.flags.cpu().numpy()

@@ -97,13 +97,16 @@ def parse_csv_bytes(buf: bytes, header: bool = True, use_native: Optional[bool] 
 
 
 def read_csv(path: str, header: bool = True, infer_schema: bool = True,
-             use_native: Optional[bool] = None, device=None) -> Table:
+             use_native: Optional[bool] = None, device=None, resident: bool = True) -> Table:
     """Load a CSV file into a columnar :class:`Table`.  ``device="cuda"`` parses on the
-    GPU (``har.data.csv_device``: HIP line index + field parse + dictionary encoding)."""
+    GPU (``har.data.csv_device``: HIP line index + field parse + dictionary encoding) and,
+    with ``resident``, keeps every column in HBM (:class:`DeviceColumn`: the feature pipeline
+    then runs on the device); ``resident=False`` returns the equivalent host table."""
     if device is not None and str(device).startswith("cuda"):
         from .csv_device import read_csv_device
 
-        t = read_csv_device(path, device=device, header=header).to_table()
+        d = read_csv_device(path, device=device, header=header)
+        t = d.to_device_table() if (resident and infer_schema) else d.to_table()
     else:
         with open(path, "rb") as f:
             buf = f.read()

@@ -86,6 +86,73 @@ class Column:
         return "[" + ",".join(java_double_str(float(a)) for a in vec) + "]"
 
 
+class DeviceColumn(Column):
+    """A column resident in device memory (the columnar HIP ETL).
+
+    * numeric (``int``/``long``/``double``): ``tensor`` [N] (fp64 / int64), ``missing_t`` bool [N]
+      or None;
+    * ``string``: ``tensor`` = dictionary codes int64 [N] (-1 = null) into ``vocab`` (host list of
+      the distinct strings), plus ``numeric_t`` (fp64 value of every field that parses as a
+      number, NaN otherwise — what ``CastToDouble`` needs);
+    * ``vector``: ``hybrid`` (:class:`har.features.hybrid.HybridMatrix`: one-hot indices + dense
+      columns), never densified on the device unless a model asks for it.
+
+    ``data`` / ``missing`` materialize the host (NumPy) form lazily — only for printing
+    (``show``, ``describe`` output, saved CSVs).  Row subsets (``take_rows``: splits, folds,
+    filters) index the device tensors."""
+
+    def __init__(self, name: str, kind: str, tensor=None, missing_t=None, meta: Optional[dict] = None,
+                 vocab: Optional[List[str]] = None, numeric_t=None, hybrid=None):
+        if kind not in KINDS:
+            raise ValueError(f"unknown column kind {kind}")
+        self.name, self.kind, self.meta = name, kind, meta
+        self.tensor, self.missing_t, self.vocab, self.numeric_t, self.hybrid = tensor, missing_t, vocab, numeric_t, hybrid
+        self.cache = {}
+        self._host = None
+        self._host_missing = False
+
+    @property
+    def device(self):
+        return self.hybrid.device if self.kind == "vector" else self.tensor.device
+
+    def __len__(self):
+        return self.hybrid.n_rows if self.kind == "vector" else int(self.tensor.shape[0])
+
+    @property
+    def data(self):
+        if self._host is None:
+            if self.kind == "vector":
+                self._host = self.hybrid.to_dense().cpu().numpy()
+            elif self.kind == "string":
+                codes = self.tensor.cpu().numpy()
+                table = np.asarray(list(self.vocab) + [None], dtype=object)
+                self._host = table[np.where(codes < 0, len(self.vocab), codes)]
+            else:
+                v = self.tensor.cpu().numpy()
+                self._host = v.astype(np.int64) if self.kind in ("int", "long") else v.astype(np.float64)
+        return self._host
+
+    @property
+    def missing(self):
+        if self._host_missing is False:
+            m = None
+            if self.missing_t is not None:
+                mh = self.missing_t.cpu().numpy()
+                m = mh if mh.any() else None
+            self._host_missing = m
+        return self._host_missing
+
+    def take_rows(self, idx) -> "DeviceColumn":
+        import torch
+
+        it = idx if isinstance(idx, torch.Tensor) else torch.as_tensor(np.asarray(idx, dtype=np.int64))
+        it = it.to(self.device)
+        if self.kind == "vector":
+            return DeviceColumn(self.name, "vector", meta=self.meta, hybrid=self.hybrid.take(it))
+        return DeviceColumn(self.name, self.kind, self.tensor[it], None if self.missing_t is None else self.missing_t[it],
+                            self.meta, self.vocab, None if self.numeric_t is None else self.numeric_t[it])
+
+
 class Table:
     """Ordered set of equally long columns."""
 
@@ -178,6 +245,16 @@ class Table:
     def group_count(self, name: str) -> "Table":
         """``groupBy(name).count().orderBy(col("count").desc())`` (main.py:35-38)."""
         c = self[name]
+        if isinstance(c, DeviceColumn) and c.kind == "string":  # value_counts kernel over the codes
+            from .device_ops import value_counts
+
+            counts_all = value_counts(c.tensor, len(c.vocab))
+            present = np.nonzero(counts_all > 0)[0]
+            vals = np.asarray([c.vocab[i] for i in present], dtype=object)
+            counts = counts_all[present]
+            order = np.lexsort((vals.astype(str), -counts))
+            return Table([Column(name.lower() if name != c.name else c.name, "string", vals[order]),
+                          Column("count", "long", counts[order].astype(np.int64))])
         vals, counts = np.unique(c.data.astype(str) if c.kind == "string" else c.data, return_counts=True)
         order = np.lexsort((vals, -counts))
         return Table([Column(name.lower() if name != c.name else c.name, c.kind if c.kind != "string" else "string",
@@ -196,8 +273,17 @@ class Table:
         return s
 
     def show(self, n: int = 20, truncate=20, out=None) -> str:
-        cols = list(self._cols.values())
         k = min(n, self._n)
+        if any(isinstance(c, DeviceColumn) for c in self._cols.values()):  # fetch only the shown rows
+            head = self.head(k)
+            host = Table([Column(c.name, c.kind, c.data, c.missing, c.meta) for c in head._cols.values()])
+            shown = host.show(k, truncate)
+            if self._n > k:
+                shown += f"only showing top {k} row{'s' if k != 1 else ''}\n"
+            if out is not None:
+                print(shown, file=out)
+            return shown
+        cols = list(self._cols.values())
         trunc = 20 if truncate is True else (0 if truncate is False else int(truncate))
         cells = []
         for c in cols:
@@ -225,6 +311,19 @@ class Table:
         """count/mean/stddev(sample)/min/max per numeric column, as strings (Spark ``describe``)."""
         names = names or [c.name for c in self._cols.values() if c.kind in ("int", "long", "double")]
         out: Dict[str, List[str]] = {"summary": ["count", "mean", "stddev", "min", "max"]}
+        dev_cols = [self[n] for n in names if isinstance(self[n], DeviceColumn)]
+        if dev_cols and len(dev_cols) == len(names):
+            from .device_ops import describe_device
+
+            cnt, mean, std, mn, mx = describe_device(dev_cols)
+            for j, c in enumerate(dev_cols):
+                if c.kind in ("int", "long"):
+                    lo, hi = str(int(mn[j])), str(int(mx[j]))
+                else:
+                    lo, hi = java_double_str(float(mn[j])), java_double_str(float(mx[j]))
+                out[c.name] = [str(int(cnt[j])), java_double_str(float(mean[j])),
+                               java_double_str(float(std[j])) if cnt[j] > 1 else "NaN", lo, hi]
+            return out
         for name in names:
             c = self[name]
             x = c.data.astype(np.float64)

@@ -15,14 +15,22 @@ Capability parity with ``Main/main.py:49-77``:
 * ``Pipeline`` / ``PipelineModel`` — sequential fit/transform; the model is
   persistable (``har.utils.persist``) so raw CSV rows can be encoded at
   inference time exactly as in training.
+
+Device path: on a device-resident table (``DeviceColumn`` s from
+the HIP CSV parser) every stage runs on the GPU — the indexer's ``countByValue`` is the
+``value_counts`` kernel over dictionary codes, indexing is one gather through a
+vocabulary -> label lookup table, one-hot blocks are never materialized (a one-hot
+column is a ``HybridMatrix`` holding one index per row) and the assembler concatenates
+them with the numeric columns into the hybrid layout the models consume directly.
 """
 from __future__ import annotations
 
 from typing import List, Optional, Sequence
 
 import numpy as np
+import torch
 
-from ..data.table import Column, Table
+from ..data.table import Column, DeviceColumn, Table
 from ..models.base import Estimator, Model, Transformer, new_uid
 
 
@@ -37,6 +45,8 @@ class StringIndexerModel(Model):
 
     def transform(self, table: Table) -> Table:
         col = table[self.inputCol]
+        if isinstance(col, DeviceColumn) and col.kind == "string":
+            return self._transform_device(table, col)
         keys = col.data if col.kind == "string" else [col.cell_str(i) for i in range(len(col))]
         out = np.empty(len(keys), dtype=np.float64)
         keep = np.ones(len(keys), dtype=bool)
@@ -54,6 +64,26 @@ class StringIndexerModel(Model):
         meta = {"vocab": self.labels, "nullable": False}
         t = table.with_column(Column(self.outputCol, "double", out, meta=meta))
         return t if keep.all() else t.filter(keep)
+
+    def _transform_device(self, table: Table, col: DeviceColumn) -> Table:
+        """codes -> label index through a [V] lookup table (one gather on the device)."""
+        dev = col.tensor.device
+        lut = torch.as_tensor(np.asarray([self._index.get(str(v), -1) for v in col.vocab] + [-1], dtype=np.int64),
+                              device=dev)
+        codes = col.tensor
+        idx = lut[torch.where(codes >= 0, codes, torch.full_like(codes, len(col.vocab)))]
+        bad = idx < 0
+        keep = None
+        if bool(bad.any()):
+            if self.handleInvalid == "keep":
+                idx = torch.where(bad, torch.full_like(idx, len(self.labels)), idx)
+            elif self.handleInvalid == "skip":
+                keep = torch.nonzero(~bad).squeeze(1)
+            else:
+                raise ValueError(f"StringIndexer: unseen or null label in column {self.inputCol}")
+        meta = {"vocab": self.labels, "nullable": False}
+        t = table.with_column(DeviceColumn(self.outputCol, "double", idx.double(), None, meta))
+        return t if keep is None else t.take_rows(keep)
 
     def params(self):
         return {"inputCol": self.inputCol, "outputCol": self.outputCol, "handleInvalid": self.handleInvalid}
@@ -75,11 +105,22 @@ class StringIndexer(Estimator):
 
     def fit(self, table: Table) -> StringIndexerModel:
         col = table[self.inputCol]
-        if col.kind == "string":
+        if isinstance(col, DeviceColumn) and col.kind == "string":  # countByValue on the device
+            from ..data.device_ops import value_counts
+
+            allc = value_counts(col.tensor, len(col.vocab))
+            present = np.nonzero(allc > 0)[0]
+            vals = np.asarray([str(col.vocab[i]) for i in present])
+            counts = allc[present]
+            if len(vals):
+                vals, first = np.unique(vals, return_index=True)  # (distinct strings: a no-op re-sort)
+                counts = counts[first]
+        elif col.kind == "string":
             keys = np.asarray([k for k in col.data if k is not None], dtype=object).astype(str)
+            vals, counts = np.unique(keys, return_counts=True)
         else:
             keys = np.asarray([col.cell_str(i) for i in range(len(col))])
-        vals, counts = np.unique(keys, return_counts=True)
+            vals, counts = np.unique(keys, return_counts=True)
         if self.stringOrderType == "frequencyDesc":
             order = np.lexsort((vals, -counts))
         elif self.stringOrderType == "frequencyAsc":
@@ -103,6 +144,20 @@ class OneHotEncoderModel(Model):
     def transform(self, table: Table) -> Table:
         t = table
         for src, dst, size in zip(self.inputCols, self.outputCols, self.sizes):
+            if isinstance(t[src], DeviceColumn):  # one index per row, never a dense block
+                from .hybrid import HybridMatrix
+
+                idx = t[src].tensor.to(torch.int64)
+                width = size - 1 if self.dropLast else size
+                if bool(((idx < 0) | (idx >= size)).any()):
+                    raise ValueError(f"OneHotEncoder: index out of range in {src}")
+                dev = idx.device
+                cat = torch.where(idx < width, idx, torch.full_like(idx, -1)).to(torch.int32)[:, None].contiguous()
+                hm = HybridMatrix(torch.zeros(idx.numel(), 0, device=dev), torch.zeros(0, dtype=torch.int32, device=dev),
+                                  cat, [(0, width)], width)
+                t = t.with_column(DeviceColumn(dst, "vector", meta={"size": width, "onehot": {"width": width}},
+                                               hybrid=hm))
+                continue
             idx = t[src].data.astype(np.int64)
             width = size - 1 if self.dropLast else size
             if (idx < 0).any() or (idx >= size).any():
@@ -145,7 +200,46 @@ class VectorAssembler(Transformer):
         super().__init__(new_uid("VectorAssembler"))
         self.inputCols, self.outputCol = list(inputCols), outputCol
 
+    def _transform_device(self, table: Table) -> Table:
+        from .hybrid import HybridMatrix
+
+        dense, dcols, cats, blocks, structure = [], [], [], [], []
+        off = 0
+        dev = table[self.inputCols[0]].device
+        n = len(table[self.inputCols[0]])
+        for c in self.inputCols:
+            col = table[c]
+            if col.kind == "vector":
+                hm = col.hybrid
+                if hm.dense.shape[1]:
+                    dense.append(hm.dense)
+                    dcols.append(hm.dense_cols.to(torch.int64) + off)
+                if hm.cat.shape[1]:
+                    cats.append(torch.where(hm.cat >= 0, hm.cat + off, hm.cat))
+                blocks += [(o + off, w) for o, w in hm.blocks]
+                structure.append({"name": c, "offset": off, "width": hm.n_features,
+                                  "kind": "onehot" if (col.meta or {}).get("onehot") is not None else "vector",
+                                  "index": None})
+                off += hm.n_features
+            elif col.kind in ("int", "long", "double"):
+                if col.missing_t is not None and bool(col.missing_t.any()):
+                    raise ValueError(f"VectorAssembler: null values in column {c}")
+                dense.append(col.tensor.to(torch.float32)[:, None])
+                dcols.append(torch.tensor([off], dtype=torch.int64, device=dev))
+                structure.append({"name": c, "offset": off, "width": 1, "kind": "numeric", "index": None})
+                off += 1
+            else:
+                raise ValueError(f"VectorAssembler: unsupported column type {col.kind} for {c}")
+        hm = HybridMatrix(torch.cat(dense, 1).contiguous() if dense else torch.zeros(n, 0, device=dev),
+                          torch.cat(dcols).to(torch.int32) if dcols else torch.zeros(0, dtype=torch.int32, device=dev),
+                          torch.cat(cats, 1).to(torch.int32).contiguous() if cats else
+                          torch.zeros(n, 0, dtype=torch.int32, device=dev), blocks, off)
+        meta = {"size": off, "structure": structure}
+        return table.with_column(DeviceColumn(self.outputCol, "vector", meta=meta, hybrid=hm))
+
     def transform(self, table: Table) -> Table:
+        if self.inputCols and all(isinstance(table[c], DeviceColumn) for c in self.inputCols):
+            return self._transform_device(table)
         blocks: List[np.ndarray] = []
         structure = []
         off = 0

@@ -112,6 +112,7 @@ def from_dense(X: torch.Tensor, blocks: Sequence[Tuple[int, int]]) -> Optional[H
 def hybrid_features(table, col: str, device) -> HybridMatrix:
     """Cached device HybridMatrix of a ``vector`` column (one-hot blocks from its assembler
     metadata; a plain dense matrix when the column has none)."""
+    from ..data.table import DeviceColumn
     from ..models.base import features_tensor
 
     c = table[col]
@@ -119,6 +120,8 @@ def hybrid_features(table, col: str, device) -> HybridMatrix:
     hit = c.cache.get(key) if c.cache is not None else None
     if hit is not None:
         return hit
+    if isinstance(c, DeviceColumn) and c.kind == "vector" and str(c.hybrid.device) == str(torch.device(device)):
+        return c.hybrid  # assembled on the device (features.encode.VectorAssembler)
     X = features_tensor(table, col, device)
     hm = from_dense(X, onehot_blocks((c.meta or {}).get("structure")))
     if hm is None:

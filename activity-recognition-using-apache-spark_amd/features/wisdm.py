@@ -15,7 +15,7 @@ from typing import List
 
 import numpy as np
 
-from ..data.table import Column, Table
+from ..data.table import Column, DeviceColumn, Table
 from ..models.base import Transformer, new_uid
 from .encode import OneHotEncoder, Pipeline, StringIndexer, VectorAssembler
 
@@ -45,6 +45,14 @@ class CastToDouble(Transformer):
         t = table
         for c in self.inputCols:
             col = t[c]
+            if isinstance(col, DeviceColumn):  # the device CSV's fp64 parse of every field
+                import torch
+
+                v = col.numeric_t if col.kind == "string" else col.tensor.double()
+                bad = torch.isnan(v) if col.kind == "string" else (
+                    col.missing_t if col.missing_t is not None else torch.zeros_like(v, dtype=torch.bool))
+                t = t.with_column(DeviceColumn(c, "double", torch.where(bad, torch.full_like(v, self.missing_value), v)))
+                continue
             if col.kind == "string":
                 vals = np.empty(len(col), dtype=np.float64)
                 for i, s in enumerate(col.data):

@@ -10,7 +10,7 @@ from typing import Dict, Optional, Tuple
 import numpy as np
 import torch
 
-from ..data.table import Column, Table
+from ..data.table import Column, DeviceColumn, Table
 
 
 def new_uid(prefix: str) -> str:
@@ -138,15 +138,22 @@ def features_tensor(table: Table, col: str, device, dtype=torch.float32) -> torc
     hit = c.cache.get(key) if c.cache is not None else None
     if hit is not None:
         return hit
-    arr = c.data if c.kind == "vector" else c.data[:, None]
-    t = torch.as_tensor(np.ascontiguousarray(arr, dtype=np.float32)).to(device=device, dtype=dtype)
+    if isinstance(c, DeviceColumn):  # already in HBM: densify the hybrid layout on the device
+        t = (c.hybrid.to_dense() if c.kind == "vector" else c.tensor[:, None]).to(device=device, dtype=dtype)
+        t = t.contiguous()
+    else:
+        arr = c.data if c.kind == "vector" else c.data[:, None]
+        t = torch.as_tensor(np.ascontiguousarray(arr, dtype=np.float32)).to(device=device, dtype=dtype)
     if c.cache is not None:
         c.cache[key] = t
     return t
 
 
 def labels_tensor(table: Table, col: str, device) -> torch.Tensor:
-    return torch.as_tensor(table[col].data.astype(np.int64)).to(device)
+    c = table[col]
+    if isinstance(c, DeviceColumn):
+        return c.tensor.to(device=device, dtype=torch.int64)
+    return torch.as_tensor(c.data.astype(np.int64)).to(device)
 
 
 class ClassifierParams(Params):

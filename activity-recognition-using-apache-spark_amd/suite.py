@@ -24,7 +24,7 @@ import numpy as np
 import torch
 
 from .config import RunConfig
-from .models.base import data_parallel, features_tensor
+from .models.base import data_parallel, features_tensor, labels_tensor
 from .utils.timing import device_sync
 
 # Reference run A (Main/wisdm_main_ver_0.0/main_result/result.txt): train seconds and accuracy
@@ -82,6 +82,13 @@ def build_estimator(name: str, cfg: RunConfig, dev, n_features: int, n_classes: 
     raise ValueError(f"unknown classifier {name}")
 
 
+def n_feature_columns(table, col: str = "features") -> int:
+    """Width of an assembled feature vector from its metadata (no host copy of a device column)."""
+    c = table[col]
+    size = (c.meta or {}).get("size")
+    return int(size) if size is not None else int(c.data.shape[1])
+
+
 def warm_up_device(dev, train, cfg: RunConfig, classifiers: Optional[Sequence[str]] = None):
     """Load the HIP code objects and warm the allocator outside the timed regions — the
     analogue of the reference's SparkContext start-up, which its timers also exclude
@@ -90,7 +97,7 @@ def warm_up_device(dev, train, cfg: RunConfig, classifiers: Optional[Sequence[st
     n_classes = len(train["label"].meta["vocab"])
     for name in classifiers or cfg.classifiers:
         base = name[:-2] if name.endswith("cv") else name
-        est = build_estimator(base, cfg, dev, small["features"].data.shape[1], n_classes)
+        est = build_estimator(base, cfg, dev, n_feature_columns(small), n_classes)
         for attr, v in (("maxIter", 2), ("numTrees", 2)):
             if hasattr(est, attr):
                 setattr(est, attr, v)
@@ -98,14 +105,16 @@ def warm_up_device(dev, train, cfg: RunConfig, classifiers: Optional[Sequence[st
     device_sync(dev)
 
 
-def load_wisdm(path: str, encoding: str = "reference", seed: int = 2018, split=(0.7, 0.3)):
-    """CSV -> feature pipeline -> 70/30 split; returns (train, test, seconds)."""
+def load_wisdm(path: str, encoding: str = "reference", seed: int = 2018, split=(0.7, 0.3), device=None):
+    """CSV -> feature pipeline -> 70/30 split; returns (train, test, seconds).  On a GPU device the
+    table is parsed, encoded and split in HBM (DeviceColumn) by the HIP ETL kernels."""
     from .data.csv_io import read_csv
     from .data.split import random_split
     from .features import wisdm
 
     t0 = time.perf_counter()
-    raw = read_csv(path)
+    cuda = device is not None and torch.device(device).type == "cuda"
+    raw = read_csv(path, device=device if cuda else None)
     _, _, df = wisdm.prepare(raw, encoding)
     train, test = random_split(df, list(split), seed=seed)
     return train, test, time.perf_counter() - t0
@@ -123,13 +132,14 @@ def run_reference_suite(dev, path: str, models: Sequence[str] = ("lr", "lrcv", "
     """
     cfg = RunConfig(cv_metric=cv_metric)
     t_load = time.perf_counter()
-    train, test, _ = load_wisdm(path, "reference", cfg.seed)
+    train, test, _ = load_wisdm(path, "reference", cfg.seed, device=dev)
+    device_sync(dev)
     load_s = time.perf_counter() - t_load
     n_train = train.count()
-    n_features = train["features"].data.shape[1]
+    n_features = n_feature_columns(train)
     n_classes = len(train["label"].meta["vocab"])
     X_test = features_tensor(test, "features", dev)
-    y_test = torch.as_tensor(test["label"].data.astype(np.int64), device=dev)
+    y_test = labels_tensor(test, "label", dev)
     t_w = time.perf_counter()
     if dev.type == "cuda":
         warm_up_device(dev, train, cfg, [m[:-2] if m.endswith("cv") else m for m in models])
@@ -187,7 +197,7 @@ def wisdm_mlp_accuracy(dev, path: str, layers_hidden=(256, 256), epochs: int = 6
     (numeric-43 encoding, 70/30 split, seed 2018) and report its test accuracy."""
     from .models.mlp import MultilayerPerceptronClassifier
 
-    train, test, _ = load_wisdm(path, "numeric43", seed)
+    train, test, _ = load_wisdm(path, "numeric43", seed, device=dev)
     K = len(train["label"].meta["vocab"])
     F = train["features"].data.shape[1]
     est = MultilayerPerceptronClassifier(layers=[F] + list(layers_hidden) + [K], maxIter=epochs, blockSize=batch,
@@ -198,7 +208,7 @@ def wisdm_mlp_accuracy(dev, path: str, layers_hidden=(256, 256), epochs: int = 6
     device_sync(dev)
     fit_s = time.perf_counter() - t0
     X_test = features_tensor(test, "features", dev)
-    y_test = torch.as_tensor(test["label"].data.astype(np.int64), device=dev)
+    y_test = labels_tensor(test, "label", dev)
     acc = float((model.predict(X_test) == y_test).float().mean())
     return {"accuracy": acc, "fit_s": fit_s, "n_train": train.count(), "n_test": test.count(),
             "layers": [F] + list(layers_hidden) + [K], "epochs": epochs, "batch": batch,

@@ -249,6 +249,9 @@ PYBIND11_MODULE(_har_native, m) {
     check(har_lbfgs_phase(&a, KP, phase, S(stream)), "lbfgs_phase");
   });
 
+  m.def("value_counts", [](u codes, int64_t n, int V, u out, u stream) {
+    check(har_value_counts(P<const int64_t>(codes), n, V, P<int64_t>(out), S(stream)), "value_counts");
+  });
   m.def("confusion_matrix", [](u label, u pred, int64_t n, int K, u cm, u stream) {
     check(har_confusion_matrix(P<const int32_t>(label), P<const int32_t>(pred), n, K, P<int64_t>(cm), S(stream)),
           "confusion_matrix");
@@ -370,6 +373,11 @@ PYBIND11_MODULE(_har_native, m) {
       py::arg("tick"), py::arg("lds") = -1, py::arg("ldd") = -1);
 
   m.def("column_stats_workspace", &har_column_stats_workspace);
+  m.def("column_stats_f64", [](u X, int64_t n, int ncols, u center, u stats, u ws, u stream) {
+    check(har_column_stats_f64(P<const double>(X), n, ncols, P<const double>(center), P<double>(stats),
+                               P<double>(ws), S(stream)),
+          "column_stats_f64");
+  });
   m.def("column_stats", [](u X, int64_t n, int ncols, int ld, u w, u stats, u ws, u stream) {
     check(har_column_stats(P<const float>(X), n, ncols, ld, P<const float>(w), P<double>(stats), P<double>(ws),
                            S(stream)),

@@ -103,10 +103,14 @@ int har_poisson_bootstrap(uint64_t seed, int tree0, int ntrees, int64_t row0, in
 // workspace: har_column_stats_workspace(n, ncols) doubles.
 int har_column_stats(const float* X, int64_t n, int ncols, int ld, const float* w, double* stats,
                      double* workspace, hipStream_t s);
+int har_column_stats_f64(const double* X, int64_t n, int ncols, const double* center, double* stats,
+                         double* workspace, hipStream_t s);
 int64_t har_column_stats_workspace(int64_t n, int ncols);
 // bins[f][i] = #{b < nthr[f] : thr[f][b] < X[i][f]}  (uint8, feature-major)
 int har_bin_features(const float* X, int64_t n, int F, int ld, const float* thr, int maxb, const int32_t* nthr,
                      uint8_t* bins, hipStream_t s);
+// counts of codes in [0, V) (V <= 32768; -1 / out-of-range ignored) into out[V] (zeroed here)
+int har_value_counts(const int64_t* codes, int64_t n, int V, int64_t* out, hipStream_t s);
 int har_confusion_matrix(const int32_t* label, const int32_t* pred, int64_t n, int K, int64_t* cm,
                          hipStream_t s);
 int har_regression_moments(const float* y, const float* yhat, int64_t n, double* out6, hipStream_t s);

@@ -1,5 +1,6 @@
 // Evaluation reductions: confusion matrix and regression
-// moments.  LDS-privatized counters per workgroup, one global atomic per
+// moments; value_counts (K3/K5): counts of dictionary codes — StringIndexer's countByValue
+// and groupBy().count() (Main/main.py:35-38, 55-61) on the device.  LDS-privatized counters per workgroup, one global atomic per
 // counter per workgroup; fp64 accumulation for the moments.
 #include "common.h"
 #include "../har_kernels.h"
@@ -20,6 +21,22 @@ __global__ __launch_bounds__(256) void confusion_kernel(const int32_t* __restric
   __syncthreads();
   for (int i = threadIdx.x; i < KK; i += blockDim.x)
     if (h[i]) atomicAdd(cm + i, (unsigned long long)h[i]);
+}
+
+// codes in [0, V) (others ignored: -1 = null); LDS-privatized 32-bit counters, one 64-bit global
+// atomic per non-zero counter per workgroup (integer adds: order-independent, exact)
+__global__ __launch_bounds__(256) void value_counts_kernel(const int64_t* __restrict__ codes, int64_t n, int V,
+                                                           unsigned long long* __restrict__ out) {
+  extern __shared__ unsigned int hv[];
+  for (int i = threadIdx.x; i < V; i += blockDim.x) hv[i] = 0;
+  __syncthreads();
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t c = codes[i];
+    if (c >= 0 && c < V) atomicAdd(&hv[c], 1u);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < V; i += blockDim.x)
+    if (hv[i]) atomicAdd(out + i, (unsigned long long)hv[i]);
 }
 
 __global__ __launch_bounds__(256) void moments_kernel(const float* __restrict__ y, const float* __restrict__ yh,
@@ -61,6 +78,17 @@ extern "C" int har_regression_moments(const float* y, const float* yhat, int64_t
   if (n == 0) return 0;
   int blocks = (int)std::min<int64_t>(1024, (n + 255) / 256);
   moments_kernel<<<blocks, 256, 0, s>>>(y, yhat, n, out6);
+  HAR_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int har_value_counts(const int64_t* codes, int64_t n, int V, int64_t* out, hipStream_t s) {
+  if (V <= 0 || V > 32768) return -2;  // LDS counters: <= 128 KB
+  hipMemsetAsync(out, 0, sizeof(int64_t) * (size_t)V, s);
+  if (n == 0) return 0;
+  const int blocks = (int)std::min<int64_t>(256, (n + 255) / 256);
+  value_counts_kernel<<<blocks, 256, sizeof(unsigned int) * (size_t)V, s>>>(codes, n, V,
+                                                                        reinterpret_cast<unsigned long long*>(out));
   HAR_CHECK_LAUNCH();
   return 0;
 }

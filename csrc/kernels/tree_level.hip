@@ -26,29 +26,37 @@ namespace {
 constexpr uint32_t STREAM_FEATURE_SUBSET = 0x7F000000u;
 constexpr int MAX_SUBSET = 128;
 
+// One wave per (tree, node): lane L draws Floyd step i = L (and L + 64) — the Philox values
+// do not depend on earlier steps — then the m sequential membership tests are wave ballots over
+// the lanes' chosen values (no per-thread scratch arrays), and the ascending order is each
+// value's rank among the m distinct choices.
 __global__ __launch_bounds__(256) void tree_feature_subsets_kernel(uint64_t seed, const int32_t* __restrict__ trees,
                                                                    const int32_t* __restrict__ nodes, int64_t P,
                                                                    int F, int m, int32_t* __restrict__ out) {
-  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= P) return;
+  const int lane = threadIdx.x & 63;
+  const int64_t p = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (p >= P) return;  // wave-uniform
   const uint64_t base = ((uint64_t)(uint32_t)trees[p] << 32) | ((uint64_t)(uint32_t)nodes[p] << 8);
-  int chosen[MAX_SUBSET];
+  int t0 = 0, t1 = 0;  // the draw of step lane / lane + 64 (t in [0, j], j = F - m + i)
+  if (lane < m) t0 = (int)(philox_u32(seed, STREAM_FEATURE_SUBSET, base + (uint64_t)lane) % (uint32_t)(F - m + lane + 1));
+  if (lane + 64 < m)
+    t1 = (int)(philox_u32(seed, STREAM_FEATURE_SUBSET, base + (uint64_t)(lane + 64)) % (uint32_t)(F - m + lane + 65));
+  int c0 = -1, c1 = -1;  // chosen[lane], chosen[lane + 64]
   for (int i = 0; i < m; ++i) {
-    const int j = F - m + i;
-    const uint32_t d = philox_u32(seed, STREAM_FEATURE_SUBSET, base + (uint64_t)i);
-    const int t = (int)(d % (uint32_t)(j + 1));
-    bool dup = false;
-    for (int q = 0; q < i; ++q) dup |= chosen[q] == t;
-    chosen[i] = dup ? j : t;
+    const int t = i < 64 ? __shfl(t0, i, 64) : __shfl(t1, i - 64, 64);
+    const bool dup = __any((c0 == t) || (c1 == t));
+    const int v = dup ? F - m + i : t;
+    if (i < 64) { if (lane == i) c0 = v; } else if (lane == i - 64) c1 = v;
   }
-  for (int i = 1; i < m; ++i) {  // insertion sort (m <= 128, mostly ~sqrt(F))
-    const int v = chosen[i];
-    int q = i - 1;
-    while (q >= 0 && chosen[q] > v) { chosen[q + 1] = chosen[q]; --q; }
-    chosen[q + 1] = v;
+  int r0 = 0, r1 = 0;  // ranks among the distinct choices
+  for (int q = 0; q < m; ++q) {
+    const int v = q < 64 ? __shfl(c0, q, 64) : __shfl(c1, q - 64, 64);
+    r0 += v < c0;
+    r1 += v < c1;
   }
   int32_t* o = out + p * m;
-  for (int i = 0; i < m; ++i) o[i] = chosen[i];
+  if (lane < m) o[r0] = c0;
+  if (lane + 64 < m) o[r1] = c1;
 }
 
 __global__ __launch_bounds__(256) void tree_level_keys_kernel(const int32_t* __restrict__ node_of,
@@ -444,7 +452,7 @@ extern "C" int har_tree_feature_subsets(uint64_t seed, const int32_t* trees, con
                                         int m, int32_t* out, hipStream_t s) {
   if (m <= 0 || m > MAX_SUBSET || m > F) return -2;
   if (P == 0) return 0;
-  tree_feature_subsets_kernel<<<(unsigned)((P + 255) / 256), 256, 0, s>>>(seed, trees, nodes, P, F, m, out);
+  tree_feature_subsets_kernel<<<(unsigned)((P + 3) / 4), 256, 0, s>>>(seed, trees, nodes, P, F, m, out);
   HAR_CHECK_LAUNCH();
   return 0;
 }

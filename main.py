@@ -51,7 +51,7 @@ from har.parallel import dist as hdist  # noqa: E402
 from har.report import csvout  # noqa: E402
 from har.report.text import (BANNER_CLASSIFY, BANNER_PIPELINE, BANNER_TRAIN, RunLog, evaluation_block,  # noqa: E402
                              model_header, section)
-from har.suite import build_estimator, warm_up_device  # noqa: E402
+from har.suite import build_estimator, n_feature_columns, warm_up_device  # noqa: E402
 from har.utils import persist  # noqa: E402
 from har.utils.timing import PhaseTimer, device_sync  # noqa: E402
 
@@ -116,7 +116,7 @@ def run(cfg: RunConfig, ctx=None) -> dict:
         # not part of any "trained in" time below (the reference's timers exclude SparkContext start-up too)
         log.print("Device warm-up (HIP code objects, allocator) %.6f seconds" % timer.get("device_warmup"))
     log.print(BANNER_CLASSIFY)
-    n_features = df["features"].data.shape[1]
+    n_features = n_feature_columns(df)
     vocab = df["label"].meta["vocab"]
     n_classes = len(vocab)
     plain_rows, cv_rows, records = [], [], {}
