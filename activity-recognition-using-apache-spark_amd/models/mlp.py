@@ -11,11 +11,15 @@ Engine layout (MI355X-first):
   compute copy refreshed by the fused Adam kernel, and ONE flat fp32 gradient
   buffer — so data-parallel training issues exactly one RCCL all-reduce per step
   (the whole gradient is ~0.3 MB: latency-bound on xGMI, so one bucket);
-* one training step = memset + L forward GEMMs (bias+ReLU fused) + fused
-  softmax-CE head (loss, accuracy, dlogits, bias grad) + per layer one data-grad
-  GEMM (ReLU mask + bias grad fused) and one split-K weight-grad GEMM
-  + [all-reduce] + fused Adam.  No host synchronization inside a step; the loss
-  and correct-count accumulators are read only when asked for;
+* one training step of the 2-hidden-layer (H = 256) network = THREE kernels
+  (mlp_fused.hip, mlp.hip): fused forward (layer 1, layer 2, softmax-CE head, dlogits,
+  dact2, dWout / dbout / db1 partials; h2 and the logits never leave the CU) ->
+  fused backward (dW1, dgrad, relu', dW0 / db0 in one pass over dact2 / h1 / X; dact1
+  never leaves the CU) -> one deterministic gradient reduction with Adam fused in
+  (N > 1: the reduction stores G, ONE RCCL all-reduce, then Adam from G).  Other
+  shapes run the same math as split-K MFMA GEMMs (gemm.hip) + the fused head.
+  No host synchronization inside a step; the loss and correct-count accumulators are
+  read only when asked for;
 * input rows are kept resident in HBM as padded bf16 ([N, F_pad]); a step reads a
   contiguous slice (zero-copy batches of a pre-shuffled resident dataset).
 
@@ -169,26 +173,26 @@ class MLPEngine:
             # <= n_splits slices and writes plain partial tiles into slab z of a
             # [n_splits, total] workspace laid out like the flat parameter buffer.
             self.n_splits = n_splits_for(self.B)
-            self.slabs = torch.zeros(self.n_splits, L.total, dtype=torch.float32, device=dev)
-            self.n_groups = min(8, self.n_splits)  # two-level reduction: splits -> groups -> 1
-            self.partials = torch.zeros(self.n_groups, L.total, dtype=torch.float32, device=dev)
+            # the fused backward (mlp_bwd_fused) writes one partial per row slice into the same slabs
+            n_slab = max(self.n_splits, _native.kernels().mlp_bwd_fused_slices(self.B))
+            self.slabs = torch.zeros(n_slab, L.total, dtype=torch.float32, device=dev)
+            self.done = torch.zeros(1, dtype=torch.int32, device=dev)  # grad_reduce_adam's workgroup counter
             # one-kernel forward + head + dWout (mlp_fused.hip) for the 2-hidden-layer shapes it covers
             self.fused_ok = (len(L.hidden) == 2 and L.hidden[0] == L.hidden[1] and L.hidden[0] in (128, 256)
                              and L.in_pad in (32, 64) and L.num_classes <= 16
                              and os.environ.get("HAR_MLP_FUSED", "1") != "0")
             if self.fused_ok:
                 nwg = _native.kernels().mlp_fwd_head_grid(self.B)
-                self.fslab = torch.zeros(nwg, 16 * L.hidden[-1] + 16, dtype=torch.float32, device=dev)
+                H = L.hidden[-1]  # per workgroup: dWout rows 0..15 [16][H], dbout [16], db1 [H] (8-wave variant)
+                self.fslab = torch.zeros(nwg, 16 * H + 16 + H, dtype=torch.float32, device=dev)
                 self.fblock_loss = torch.zeros(nwg, dtype=torch.float32, device=dev)
                 self.fblock_correct = torch.zeros(nwg, dtype=torch.int32, device=dev)
             self.last_fused = False
-            # fused layer-1 backward (mlp_fused.hip mlp_bwd_l1): dgrad -> relu' -> dW0 / db0 in one
-            # kernel, dact1 never reaches HBM (H = 256, batch % 32; HAR_MLP_BWD_FUSED=0 keeps the GEMMs)
+            # fused backward (mlp_fused.hip mlp_bwd_fused): dW1, dgrad -> relu' -> dW0 / db0 in ONE pass
+            # over dact2 / h1 / X, dact1 never reaches HBM (H = 256, batch % 32, after the 8-wave
+            # forward, which supplies db1; HAR_MLP_BWD_FUSED=0 keeps the split-K GEMMs)
             self.bwd_ok = (self.fused_ok and L.hidden[0] == 256
                            and os.environ.get("HAR_MLP_BWD_FUSED", "1") != "0")
-            if self.bwd_ok:
-                nbw = _native.kernels().mlp_bwd_l1_grid(self.B)
-                self.bslab = torch.zeros(nbw, 256 * L.in_pad + 256, dtype=torch.float32, device=dev)
             self.last_bwd = False
             # optional: the two backward branches after the fused forward — dW1 (split-K over the
             # batch) and dgrad -> dW0 — are independent, so HAR_MLP_STREAMS=1 runs dW1 on a second
@@ -209,9 +213,9 @@ class MLPEngine:
         return self.slabs.view(-1)[s.offset:]
 
     def forward_backward_native(self, Xb: torch.Tensor, y32: torch.Tensor, scale: float, on_grad=None):
-        """Xb: [B, in_pad] bf16 (contiguous slice), y32: [B] int32.  Leaves the split-K
-        gradient partials in ``self.slabs[:self.active_splits]``; ``on_grad(name)`` is called
-        as soon as layer ``name``'s weight/bias gradient slabs are enqueued (DP bucketing)."""
+        """Xb: [B, in_pad] bf16 (contiguous slice), y32: [B] int32.  Leaves the gradient partials
+        in the slabs (``_grad_regions``); ``on_grad(name)`` is called as soon as layer ``name``'s
+        weight/bias gradient slabs are enqueued (a hook for tracing / tests)."""
         L, mod, s = self.layout, _native.kernels(), _native.stream_ptr()
         B = Xb.shape[0]
         if Xb.shape[1] != L.in_pad or Xb.dtype != torch.bfloat16 or B > self.B or y32.dtype != torch.int32:
@@ -262,8 +266,9 @@ class MLPEngine:
                 dact = prev
 
     def _forward_backward_fused(self, Xb, y32, scale, on_grad, ks, acts):
-        """2-hidden-layer step: ONE kernel for fwd L1 + fwd L2 + head + dWout/dbout (h2 and the
-        logit gradients stay on chip), then dW1, dgrad and dW0 as split-K MFMA GEMMs."""
+        """2-hidden-layer step: ONE kernel for fwd L1 + fwd L2 + head + dWout/dbout (+ db1) (h2 and
+        the logit gradients stay on chip), then ONE kernel for dW1 + dgrad + dW0 / db0 (H = 256),
+        or dW1, dgrad and dW0 as split-K MFMA GEMMs."""
         L, mod, s = self.layout, _native.kernels(), _native.stream_ptr()
         B, H, K0 = Xb.shape[0], self.dims[-1], L.in_pad
         total = L.total
@@ -277,8 +282,21 @@ class MLPEngine:
                          self.fblock_loss.data_ptr(), self.fblock_correct.data_ptr(), s)
         self.last_fused = True
         self.last_batch = B
+        self.last_bwd = self.bwd_ok and B % 64 == 0 and mod.mlp_fwd_head_variant(H, B) == 2
         if on_grad is not None:
             on_grad("Wout")
+
+        if self.last_bwd:
+            # dW1 + dgrad + relu' + dW0 / db0: one kernel, one partial per row slice in self.slabs
+            self.bwd_S = mod.mlp_bwd_fused_slices(B)
+            sb = self.slabs.data_ptr()
+            mod.mlp_bwd_fused(dact.data_ptr(), h1.data_ptr(), Xb.data_ptr(), K0, self._w(self.Pb, "W1").data_ptr(), H,
+                              B, sb + 4 * L.by_name["W1"].offset, sb + 4 * L.by_name["W0"].offset,
+                              sb + 4 * L.by_name["b0"].offset, total, s)
+            if on_grad is not None:
+                on_grad("W1")
+                on_grad("W0")
+            return
 
         def dw1():
             gemm_bf16(dact, h1, self._slab("W1"), M=H, N=H, K=B, layout=3, epi=EPI_F32_SLAB, k_split=ks, ldc=H,
@@ -286,128 +304,78 @@ class MLPEngine:
 
         prev = self.dbuf[0][: B * H].view(B, H)
         main = torch.cuda.current_stream(self.device)
-        if self.side is not None:  # fork: dW1 (+ its DP bucket) on the side stream, dgrad -> dW0 here
+        if self.side is not None:  # fork: dW1 on the side stream, dgrad -> dW0 here
             self.ev_fork.record(main)
             self.side.wait_event(self.ev_fork)
             with torch.cuda.stream(self.side):
                 dw1()
                 if on_grad is not None:
-                    on_grad("W1")  # DP: the W1 bucket's slab reduction + async all-reduce start here
+                    on_grad("W1")
                 self.ev_join.record(self.side)
         else:
             dw1()
             if on_grad is not None:
                 on_grad("W1")
-        if self.bwd_ok and B % 32 == 0:  # dact1 stays on chip: dgrad + relu' + dW0 / db0 in one kernel
-            self.bwd_nwg = mod.mlp_bwd_l1_grid(B)
-            mod.mlp_bwd_l1(dact.data_ptr(), h1.data_ptr(), Xb.data_ptr(), K0, self._w(self.Pb, "W1").data_ptr(), H,
-                           B, self.bslab.data_ptr(), s)
-            self.last_bwd = True
-        else:
-            self.last_bwd = False
-            gemm_bf16(dact, self._w(self.Pb, "W1"), prev, M=B, N=H, K=H, layout=2, epi=EPI_RELU_GRAD, mask=h1,
-                      tile=dgrad_tile(B, H, H))
-            gemm_bf16(prev, Xb, self._slab("W0"), M=H, N=K0, K=B, layout=3, epi=EPI_F32_SLAB, k_split=ks, ldc=K0,
-                      slab_stride=total, rowsum=self._slab("b0"), slab_stride_rowsum=total, tile=wgrad_tile(H, K0))
+        gemm_bf16(dact, self._w(self.Pb, "W1"), prev, M=B, N=H, K=H, layout=2, epi=EPI_RELU_GRAD, mask=h1,
+                  tile=dgrad_tile(B, H, H))
+        gemm_bf16(prev, Xb, self._slab("W0"), M=H, N=K0, K=B, layout=3, epi=EPI_F32_SLAB, k_split=ks, ldc=K0,
+                  slab_stride=total, rowsum=self._slab("b0"), slab_stride_rowsum=total, tile=wgrad_tile(H, K0))
         if on_grad is not None:
             on_grad("W0")
         if self.side is not None:  # join: the W1 slabs (and the next step's h1 / dact2 reuse) are ordered
             main.wait_event(self.ev_join)
 
-    def _first_level(self, lo: int, hi: int, tick: bool):
-        """First reduction level of G[lo:hi] into ``n_groups`` partials in ONE launch (one grid.z
-        segment per source region): the split-K GEMM slabs, and after a fused step the fused
-        kernels' per-workgroup slabs (dWout / dbout of the forward kernel, dW0 / db0 of the
-        layer-1 backward kernel); optionally ticks the Adam step counter."""
-        mod, st, L = _native.kernels(), _native.stream_ptr(), self.layout
-        total = L.total
-        regions = []  # (start, end, source pointer at start, #slabs, slab stride) in flat order
-        start = 0
+    def _grad_regions(self):
+        """Sources of the flat gradient after the last native batch, in flat order: (start, end,
+        pointer of slab 0 at start, #slabs, slab stride) — the split-K GEMM slabs or the fused
+        backward's per-slice partials, and after a fused step the forward kernel's per-workgroup
+        slabs (dWout / dbout, and db1 when the fused backward ran)."""
+        L, total = self.layout, self.layout.total
+        regions = []
+        fs = self.fslab.data_ptr() if self.last_fused else 0
         if self.last_bwd:
-            w0, b0 = L.by_name["W0"], L.by_name["b0"]
-            bs, ldb = self.bslab.data_ptr(), self.bslab.shape[1]
-            regions.append((w0.offset, w0.offset + w0.numel, bs, self.bwd_nwg, ldb))
-            regions.append((b0.offset, b0.offset + b0.numel, bs + 4 * w0.numel, self.bwd_nwg, ldb))
-            start = L.by_name["W1"].offset
-        end = L.by_name["Wout"].offset if self.last_fused else total
-        regions.append((start, end, self.slabs.data_ptr() + 4 * start, self.active_splits, total))
-        if self.last_fused:
             H = self.dims[-1]
-            fs, w = self.fslab.data_ptr(), self.fslab.shape[1]
+            w0, b1 = L.by_name["W0"].offset, L.by_name["b1"].offset
+            regions.append((w0, b1, self.slabs.data_ptr() + 4 * w0, self.bwd_S, total))  # W0, b0, W1
+            regions.append((b1, b1 + H, fs + 4 * (16 * H + 16), self.fused_nwg, self.fslab.shape[1]))
+        else:
+            end = L.by_name["Wout"].offset if self.last_fused else total
+            regions.append((0, end, self.slabs.data_ptr(), self.active_splits, total))
+        if self.last_fused:
+            H, w = self.dims[-1], self.fslab.shape[1]
             wo, bo = L.by_name["Wout"].offset, L.by_name["bout"].offset
             regions.append((wo, wo + 16 * H, fs, self.fused_nwg, w))
             regions.append((bo, bo + 16, fs + 4 * 16 * H, self.fused_nwg, w))
-        pbase = self.partials.data_ptr()
-        segs = []  # (slabs ptr, S, n, lds, dst ptr, ldd)
-        for a, b, ptr, S, lds in regions:
-            a2, b2 = max(a, lo), min(b, hi)
-            if a2 < b2:
-                segs.append((ptr + 4 * (a2 - a), S, b2 - a2, lds, pbase + 4 * a2, total))
-        cols = list(zip(*segs))
-        mod.reduce_slabs_multi(list(cols[0]), list(cols[1]), list(cols[2]), list(cols[3]), list(cols[4]),
-                               list(cols[5]), self.n_groups, self.step_count.data_ptr() if tick else 0, st)
+        return regions
 
-    def _reduce_to_partials(self):
-        # the first reduction level also ticks the Adam step counter (one launch fewer per step)
-        self._first_level(0, self.layout.total, True)
+    GR_REDUCE, GR_STORE, GR_ADAM = 1, 2, 4
+
+    def _grad_kernel(self, mode: int):
+        """mlp.hip grad_reduce_adam: one deterministic single-level reduction of every gradient
+        slab (fixed order) and/or the Adam update; the same kernel for every world size."""
+        b1, b2 = self.betas
+        regs = self._grad_regions() if mode & self.GR_REDUCE else []
+        cols = list(zip(*regs)) if regs else [[]] * 5
+        _native.kernels().grad_reduce_adam(
+            list(cols[2]), list(cols[0]), [e - a for a, e in zip(cols[0], cols[1])], list(cols[4]), list(cols[3]),
+            self.layout.total, self.G.data_ptr(), self.P.data_ptr(), self.m.data_ptr(), self.v.data_ptr(),
+            self.Pb.data_ptr(), float(self.lr), b1, b2, float(self.eps), float(self.wd), self.step_count.data_ptr(),
+            self.done.data_ptr(), mode, _native.stream_ptr())
 
     def reduce_grads_native(self):
-        """G = sum of the active gradient slabs (two deterministic levels; needed before a collective)."""
-        self._reduce_to_partials()
-        _native.kernels().reduce_slabs_grouped(self.partials.data_ptr(), self.n_groups, self.layout.total,
-                                               self.G.data_ptr(), 1, _native.stream_ptr(), 0)
+        """G = the sum of the last batch's gradient slabs (needed before a collective)."""
+        self._grad_kernel(self.GR_REDUCE | self.GR_STORE)
 
-    def _layer_range(self, name):
-        """[lo, hi) of layer ``name``'s weight + bias in the flat buffers."""
-        L = self.layout
-        k = L.segments.index(L.by_name[name])
-        return L.segments[k].offset, (L.segments[k + 2].offset if k + 2 < len(L.segments) else L.total)
+    def optimizer_step_native(self):
+        """Adam from G (after the all-reduce); ticks the device step counter."""
+        self._grad_kernel(self.GR_ADAM)
 
-    def _reduce_range(self, lo: int, hi: int, tick: bool):
-        """Two-level slab reduction of G[lo:hi] only (same summation order as the whole-buffer one)."""
-        mod, st, total = _native.kernels(), _native.stream_ptr(), self.layout.total
-        self._first_level(lo, hi, tick)
-        mod.reduce_slabs_grouped(self.partials.data_ptr() + 4 * lo, self.n_groups, hi - lo, self.G.data_ptr() + 4 * lo,
-                                 1, st, 0, lds=total, ldd=hi - lo)
-
-    def train_step_overlapped(self, Xb: torch.Tensor, yb: torch.Tensor, global_batch: int,
-                              bucket_bytes: int = 64 << 10):
-        """DP step with the gradient all-reduce bucketed and overlapped with backward: as soon
-        as the layers finished so far hold >= ``bucket_bytes`` of gradient, their slabs are
-        reduced and an async RCCL all-reduce of that contiguous slice of G starts on the
-        communicator's stream while the remaining dgrad/wgrad GEMMs run; Adam waits for all
-        buckets.  Layers finish in reverse order, so every bucket is one contiguous range."""
-        import torch.distributed as dist
-
-        works, pend = [], []
-
-        def flush():
-            lo, hi = pend[-1][0], pend[0][1]
-            self._reduce_range(lo, hi, tick=not works)
-            works.append(dist.all_reduce(self.G[lo:hi], group=self.pg, async_op=True))
-            pend.clear()
-
-        def on_grad(name):
-            pend.append(self._layer_range(name))
-            if (pend[0][1] - pend[-1][0]) * 4 >= bucket_bytes or name == "W0":
-                flush()
-
-        self.forward_backward_native(Xb, yb, 1.0 / global_batch, on_grad=on_grad)
-        for w in works:
-            w.wait()  # stream-ordered: the compute stream waits on the RCCL stream, the host does not
-        self.optimizer_step_native(from_slabs=False)
-
-    def optimizer_step_native(self, from_slabs: bool):
-        """Adam; with ``from_slabs`` the slabs are first reduced to ``n_groups`` partials and the
-        last level of the reduction is fused into the Adam kernel."""
-        b1, b2 = self.betas
-        if from_slabs:
-            self._reduce_to_partials()  # ticks the step counter
-        _native.kernels().adam_step(self.P.data_ptr(), self.G.data_ptr(),
-                                    self.partials.data_ptr() if from_slabs else 0, self.n_groups,
-                                    self.m.data_ptr(), self.v.data_ptr(), self.Pb.data_ptr(), self.P.numel(),
-                                    float(self.lr), b1, b2, float(self.eps), float(self.wd), 1.0,
-                                    self.step_count.data_ptr(), _native.stream_ptr(), 0)
+    def collective_stats(self):
+        """Collectives of one DP training step: ONE flat all-reduce of the whole fp32 gradient
+        (~0.34 MB for 43-256-256-6: latency-bound on xGMI, so no bucketing)."""
+        if self.world <= 1:
+            return {"all_reduce": 0, "bytes": 0}
+        return {"all_reduce": 1, "bytes": int(self.G.numel() * 4), "world": self.world}
 
     def allreduce_grads(self):
         if self.world > 1:
@@ -422,15 +390,20 @@ class MLPEngine:
     def apply_phase(self):
         """DP step, part 3 (graph-capturable): Adam from the all-reduced G (part 2 is the RCCL
         all-reduce, issued eagerly between the two graph replays)."""
-        self.optimizer_step_native(from_slabs=False)
+        self.optimizer_step_native()
 
     def train_step(self, Xb: torch.Tensor, yb: torch.Tensor, global_batch: int):
+        """One step.  Native: fwd kernel + bwd kernel + ONE reduction kernel; at N = 1 the Adam
+        update is fused into that kernel, at N > 1 it stores G, one RCCL all-reduce of G follows and
+        Adam runs from G — the same kernels and the same summation order at every N."""
         if self.native:
+            self.forward_backward_native(Xb, yb, 1.0 / global_batch)
             if self.world > 1:
-                self.train_step_overlapped(Xb, yb, global_batch)
-            else:  # single GPU: the slab reduction is fused into Adam
-                self.forward_backward_native(Xb, yb, 1.0 / global_batch)
-                self.optimizer_step_native(from_slabs=True)
+                self.reduce_grads_native()
+                self.allreduce_grads()
+                self.optimizer_step_native()
+            else:
+                self._grad_kernel(self.GR_REDUCE | self.GR_ADAM)
         else:
             self.train_step_torch(Xb, yb, global_batch)
 

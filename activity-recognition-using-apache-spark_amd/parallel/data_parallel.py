@@ -17,8 +17,10 @@ combines are RCCL collectives over xGMI:
   ``reduceByKey(node)`` + ``collectAsMap``, SURVEY.md M9);
 * RandomForest, tree-parallel (``fit_forest_tree_parallel``): every rank grows a slice of the
   trees over all rows; one all-gather of the node arrays at the end;
-* MLP: fp32 gradient buckets (>= 64 KB, contiguous layer ranges of the flat buffer) all-reduced
-  asynchronously while backward continues (``MLPEngine.train_step_overlapped``).
+* MLP: ONE all-reduce of the flat fp32 gradient per step (~0.34 MB: a latency-bound message on
+  xGMI, where splitting it into buckets only adds per-collective latency), between the
+  deterministic slab reduction and Adam — the N = 1 step runs the same kernels with Adam fused
+  into the reduction (``MLPEngine.train_step``).
 
 ``gloo`` runs the identical code on CPU for the multi-process tests.
 """

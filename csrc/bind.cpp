@@ -310,6 +310,20 @@ PYBIND11_MODULE(_har_native, m) {
           "window_features");
   });
 
+  m.def("grad_reduce_adam", [](std::vector<u> src, std::vector<int64_t> start, std::vector<int64_t> len,
+                               std::vector<int64_t> lds, std::vector<int> nsl, int64_t n, u G, u param, u mm, u vv,
+                               u pb, float lr, float b1, float b2, float eps, float wd, u step, u done, int mode,
+                               u stream) {
+    const int k = (int)src.size();
+    if ((int)start.size() != k || (int)len.size() != k || (int)lds.size() != k || (int)nsl.size() != k)
+      throw std::runtime_error("grad_reduce_adam: region lists differ in length");
+    std::vector<const float*> sp(k);
+    for (int i = 0; i < k; ++i) sp[i] = P<const float>(src[i]);
+    check(har_grad_reduce_adam(k, sp.data(), start.data(), len.data(), lds.data(), nsl.data(), n, P<float>(G),
+                               P<float>(param), P<float>(mm), P<float>(vv), P<uint16_t>(pb), lr, b1, b2, eps, wd,
+                               P<int32_t>(step), P<uint32_t>(done), mode, S(stream)),
+          "grad_reduce_adam");
+  });
   m.def("reduce_slabs_multi", [](std::vector<u> slabs, std::vector<int> nsl, std::vector<int64_t> n,
                                  std::vector<int64_t> lds, std::vector<u> dst, std::vector<int64_t> ldd, int G,
                                  u tick, u stream) {
@@ -326,11 +340,14 @@ PYBIND11_MODULE(_har_native, m) {
   });
   m.def("head_fused_blocks", &har_head_fused_blocks);
   m.def("mlp_fwd_head_grid", &har_mlp_fwd_head_grid);
-  m.def("mlp_bwd_l1_grid", &har_mlp_bwd_l1_grid);
-  m.def("mlp_bwd_l1", [](u dact2, u h1, u X, int K0, u W1, int H, int B, u slab, u stream) {
-    check(har_mlp_bwd_l1(P<const uint16_t>(dact2), P<const uint16_t>(h1), P<const uint16_t>(X), K0,
-                         P<const uint16_t>(W1), H, B, P<float>(slab), S(stream)),
-          "mlp_bwd_l1");
+  m.def("mlp_bwd_fused_slices", &har_mlp_bwd_fused_slices);
+  m.def("mlp_fwd_head_variant", &har_mlp_fwd_head_variant);
+  m.def("mlp_bwd_fused", [](u dact2, u h1, u X, int K0, u W1, int H, int B, u gw1, u gw0, u gb0, int64_t stride,
+                            u stream) {
+    check(har_mlp_bwd_fused(P<const uint16_t>(dact2), P<const uint16_t>(h1), P<const uint16_t>(X), K0,
+                            P<const uint16_t>(W1), H, B, P<float>(gw1), P<float>(gw0), P<float>(gb0), stride,
+                            S(stream)),
+          "mlp_bwd_fused");
   });
   m.def("mlp_fwd_head", [](u X, int K0, u W0, u b0, u W1, u b1, int H, u Wo, u bo, u labels, int B, int C,
                            float scale, u h1, u dact, u slab, u block_loss, u block_correct, u stream) {

@@ -43,6 +43,13 @@ int har_softmax_ce_head_blocks(int B);
 // Gradient = grad[i] (if slabs == null) or sum_s slabs[s*n + i] (fused split-K reduction).
 // The step counter (*step, device int32) is incremented on the stream before the update
 // (by this call when tick != 0, else by an earlier kernel such as har_reduce_slabs_grouped).
+// Flat-gradient reduction (+ Adam) of the MLP step (mlp.hip): mode bits 1 = reduce the regions' slabs,
+// 2 = store G, 4 = Adam with t = *step + 1 (the last workgroup writes *step = t; `done` is a zeroed
+// device counter).  Regions: sorted, disjoint, 4-aligned [start, start + len), S slabs at src + s * lds.
+int har_grad_reduce_adam(int nreg, const float* const* src, const int64_t* start, const int64_t* len,
+                         const int64_t* lds, const int* S, int64_t n, float* G, float* param, float* m, float* v,
+                         uint16_t* pb, float lr, float b1, float b2, float eps, float wd, int32_t* step,
+                         uint32_t* done, int mode, hipStream_t s);
 int har_adam_step(float* param, const float* grad, const float* slabs, int nslabs, float* m, float* v,
                   uint16_t* param_bf16, int64_t n, float lr, float beta1, float beta2, float eps,
                   float weight_decay, float grad_scale, int32_t* step, int tick, hipStream_t s);
@@ -64,11 +71,13 @@ int har_mlp_fwd_head(const uint16_t* X, int K0, const uint16_t* W0, const float*
                      int C, float scale, uint16_t* h1, uint16_t* dact, float* slab, float* block_loss,
                      int32_t* block_correct, hipStream_t s);
 int har_mlp_fwd_head_grid(int B);
-// Fused layer-1 backward (H = 256, B % 32 == 0): dact1 = (dact2 . W1) * relu'(h1) reduced in-kernel
-// into per-workgroup slabs [H*K0 | H] of dW0 / db0; grid har_mlp_bwd_l1_grid(B).
-int har_mlp_bwd_l1(const uint16_t* dact2, const uint16_t* h1, const uint16_t* X, int K0, const uint16_t* W1, int H,
-                   int B, float* slab, hipStream_t s);
-int har_mlp_bwd_l1_grid(int B);
+// Fused backward after the fused forward (H = 256, B % 32 == 0): dW1 = dact2^T h1, dact1 = (dact2 W1) *
+// relu'(h1), dW0 = dact1^T X, db0 in one pass; per-slice partials at gw1 / gw0 / gb0 + s * slab_stride for
+// s < har_mlp_bwd_fused_slices(B).  har_mlp_fwd_head_variant: 2 = the 8-wave forward (writes db1 too).
+int har_mlp_bwd_fused(const uint16_t* dact2, const uint16_t* h1, const uint16_t* X, int K0, const uint16_t* W1,
+                      int H, int B, float* gw1, float* gw0, float* gb0, int64_t slab_stride, hipStream_t s);
+int har_mlp_bwd_fused_slices(int B);
+int har_mlp_fwd_head_variant(int H, int B);
 // Serving variant of the same kernel: logits [B][C] fp32 + argmax class [B] int32, nothing else.
 int har_mlp_fwd_infer_f32(const float* X, int ldx, int F, int K0, const uint16_t* W0, const float* b0,
                           const uint16_t* W1, const float* b1, int H, const uint16_t* Wo, const float* bo, int B, int C,

@@ -94,6 +94,13 @@ __global__ __launch_bounds__(256) void softmax_ce_head_kernel(
   }
 }
 
+struct GradRegions {
+  const float* src[8];
+  int64_t start[8], len[8], lds[8];
+  int S[8];
+  int nreg;
+};
+
 // Step counter lives on the device so a captured hipGraph replays correct bias corrections.
 __global__ void adam_tick_kernel(int32_t* step) { *step += 1; }
 
@@ -159,6 +166,118 @@ __global__ void cast_pad_kernel(const float* __restrict__ in, int rows, int cin,
   }
 }
 
+// ---- gradient reduction + Adam (one kernel, shared by every world size) ----
+// Sources of the flat gradient: up to 8 disjoint, 4-aligned regions [start, start + len), each
+// the sum of S slabs (slab s at src + s * lds).  Modes (bit set):
+//   GR_REDUCE  g = sum of the region's slabs (fixed order)    else g = G[i] (already reduced)
+//   GR_STORE   G[i] = g                                         (DP: before the all-reduce)
+//   GR_ADAM    Adam update of param / m / v / bf16 copy with t = *step + 1; the last workgroup to
+//              finish (one device counter) writes *step = t, after every workgroup has read it
+// A workgroup = 16 waves x 64 float4 columns: wave q sums slabs q, q + 16, q + 32, ... (eight loads
+// in flight per step: the 256 per-workgroup slabs of the forward kernel take two steps), the 16
+// partials are added in a fixed tree order -> bitwise reproducible, and N = 1 (GR_REDUCE |
+// GR_ADAM) and N > 1 (GR_REDUCE | GR_STORE, all-reduce, GR_ADAM) apply the same summation and the
+// same Adam arithmetic.
+constexpr int GR_REDUCE = 1, GR_STORE = 2, GR_ADAM = 4;
+constexpr int GR_W = 16;  // waves per workgroup
+
+__global__ __launch_bounds__(1024) void grad_reduce_adam_kernel(GradRegions rg, int64_t n, float* __restrict__ G,
+                                                                float* __restrict__ param, float* __restrict__ m,
+                                                                float* __restrict__ v, bf16_t* __restrict__ pb,
+                                                                float lr, float b1, float b2, float eps, float wd,
+                                                                int32_t* __restrict__ step,
+                                                                uint32_t* __restrict__ done, int mode) {
+  __shared__ float4 part[GR_W][64];
+  const int q = threadIdx.x >> 6, k = threadIdx.x & 63;
+  const int64_t i4 = (int64_t)blockIdx.x * 64 + k, e = i4 * 4;
+  if (mode & GR_REDUCE) {
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (e < n) {
+      for (int r = 0; r < rg.nreg; ++r) {
+        if (e < rg.start[r] || e >= rg.start[r] + rg.len[r]) continue;
+        const float* p = rg.src[r] + (e - rg.start[r]);
+        const int S = rg.S[r];
+        const int64_t ld = rg.lds[r];
+        int s = q;
+        for (; s + 7 * GR_W < S; s += 8 * GR_W) {
+          float4 x[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) x[j] = *reinterpret_cast<const float4*>(p + (size_t)(s + j * GR_W) * ld);
+          acc.x += ((x[0].x + x[1].x) + (x[2].x + x[3].x)) + ((x[4].x + x[5].x) + (x[6].x + x[7].x));
+          acc.y += ((x[0].y + x[1].y) + (x[2].y + x[3].y)) + ((x[4].y + x[5].y) + (x[6].y + x[7].y));
+          acc.z += ((x[0].z + x[1].z) + (x[2].z + x[3].z)) + ((x[4].z + x[5].z) + (x[6].z + x[7].z));
+          acc.w += ((x[0].w + x[1].w) + (x[2].w + x[3].w)) + ((x[4].w + x[5].w) + (x[6].w + x[7].w));
+        }
+        for (; s + 3 * GR_W < S; s += 4 * GR_W) {
+          float4 x[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) x[j] = *reinterpret_cast<const float4*>(p + (size_t)(s + j * GR_W) * ld);
+          acc.x += (x[0].x + x[1].x) + (x[2].x + x[3].x);
+          acc.y += (x[0].y + x[1].y) + (x[2].y + x[3].y);
+          acc.z += (x[0].z + x[1].z) + (x[2].z + x[3].z);
+          acc.w += (x[0].w + x[1].w) + (x[2].w + x[3].w);
+        }
+        for (; s < S; s += GR_W) {
+          const float4 x = *reinterpret_cast<const float4*>(p + (size_t)s * ld);
+          acc.x += x.x; acc.y += x.y; acc.z += x.z; acc.w += x.w;
+        }
+      }
+    }
+    part[q][k] = acc;
+    __syncthreads();
+    if (q < 4) {  // 16 -> 4 partials (fixed pairs)
+      const float4 a = part[q][k], b = part[q + 4][k], c = part[q + 8][k], d = part[q + 12][k];
+      part[q][k] = make_float4((a.x + b.x) + (c.x + d.x), (a.y + b.y) + (c.y + d.y), (a.z + b.z) + (c.z + d.z),
+                               (a.w + b.w) + (c.w + d.w));
+    }
+    __syncthreads();
+  }
+  const int32_t t_int = (mode & GR_ADAM) ? *step + 1 : 0;
+  if (q == 0 && e < n) {
+    float4 g;
+    if (mode & GR_REDUCE) {
+      const float4 a = part[0][k], b = part[1][k], c = part[2][k], d = part[3][k];
+      g = make_float4((a.x + b.x) + (c.x + d.x), (a.y + b.y) + (c.y + d.y), (a.z + b.z) + (c.z + d.z),
+                      (a.w + b.w) + (c.w + d.w));
+    } else {
+      g = reinterpret_cast<const float4*>(G)[i4];
+    }
+    if (mode & GR_STORE) reinterpret_cast<float4*>(G)[i4] = g;
+    if (mode & GR_ADAM) {
+      const float t = (float)t_int;
+      const float bc1 = 1.f - powf(b1, t), bc2 = 1.f - powf(b2, t);
+      float4 pp = reinterpret_cast<float4*>(param)[i4];
+      float4 mm = reinterpret_cast<float4*>(m)[i4];
+      float4 vv = reinterpret_cast<float4*>(v)[i4];
+      float* pa = &pp.x; float* ma = &mm.x; float* va = &vv.x; const float* ga = &g.x;
+      ushort4 ob;
+      unsigned short* oa = &ob.x;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        ma[j] = b1 * ma[j] + (1.f - b1) * ga[j];
+        va[j] = b2 * va[j] + (1.f - b2) * ga[j] * ga[j];
+        const float upd = (ma[j] / bc1) / (sqrtf(va[j] / bc2) + eps);
+        pa[j] = pa[j] - lr * (upd + wd * pa[j]);
+        oa[j] = f2bf(pa[j]);
+      }
+      reinterpret_cast<float4*>(param)[i4] = pp;
+      reinterpret_cast<float4*>(m)[i4] = mm;
+      reinterpret_cast<float4*>(v)[i4] = vv;
+      reinterpret_cast<ushort4*>(pb)[i4] = ob;
+    }
+  }
+  if (mode & GR_ADAM) {
+    __syncthreads();  // every thread of this workgroup has read *step
+    if (threadIdx.x == 0) {
+      __threadfence();
+      if (atomicAdd(done, 1u) == gridDim.x - 1) {  // the last workgroup: all others have read *step
+        *step = t_int;
+        *done = 0;
+      }
+    }
+  }
+}
+
 int grid_for(int64_t n4) { return (int)std::max<int64_t>(1, std::min<int64_t>(2048, (n4 + 255) / 256)); }
 
 }  // namespace
@@ -201,6 +320,27 @@ extern "C" int har_cast_pad_bf16(const float* in, int rows, int cin, int ldin, u
   int blocks = (int)std::min<int64_t>(4096, (total + 255) / 256);
   if (blocks == 0) return 0;
   cast_pad_kernel<<<blocks, 256, 0, s>>>(in, rows, cin, ldin, out, cout);
+  HAR_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int har_grad_reduce_adam(int nreg, const float* const* src, const int64_t* start, const int64_t* len,
+                                    const int64_t* lds, const int* S, int64_t n, float* G, float* param, float* m,
+                                    float* v, uint16_t* pb, float lr, float b1, float b2, float eps, float wd,
+                                    int32_t* step, uint32_t* done, int mode, hipStream_t s) {
+  if (n % 4 || nreg < 0 || nreg > 8 || ((mode & GR_REDUCE) && nreg == 0)) return -2;
+  GradRegions rg{};
+  rg.nreg = nreg;
+  for (int r = 0; r < nreg; ++r) {
+    if (start[r] % 4 || len[r] % 4 || lds[r] % 4 || S[r] <= 0 || start[r] < 0 || start[r] + len[r] > n) return -2;
+    if (reinterpret_cast<uintptr_t>(src[r]) & 15) return -3;
+    if (r > 0 && start[r] < start[r - 1] + len[r - 1]) return -2;  // sorted, disjoint
+    rg.src[r] = src[r]; rg.start[r] = start[r]; rg.len[r] = len[r]; rg.lds[r] = lds[r]; rg.S[r] = S[r];
+  }
+  const int64_t blocks = (n / 4 + 63) / 64;
+  if (blocks == 0) return 0;
+  grad_reduce_adam_kernel<<<(int)blocks, 64 * GR_W, 0, s>>>(rg, n, G, param, m, v, pb, lr, b1, b2, eps, wd, step,
+                                                            done, mode);
   HAR_CHECK_LAUNCH();
   return 0;
 }

@@ -37,6 +37,8 @@ typedef __attribute__((address_space(3))) s16x4_t lds_s16x4_t;
 typedef __attribute__((ext_vector_type(4))) uint32_t u32x4_t;
 
 constexpr int NCLS = 16;
+// per-workgroup gradient slab of the forward kernel: dWout rows 0..15 [16][H], dbout [16], db1 [H]
+__host__ __device__ constexpr int fwd_slab_width(int H) { return NCLS * H + NCLS + H; }
 constexpr int SCR = 3 * 256;  // per-wave scratch: 2 h2 tiles + 1 dz tile, 16x16 bf16 each
 
 // [rows][H + 8] bf16 images (one 16-byte pad per row): the 8-byte A-fragment reads of
@@ -350,7 +352,7 @@ __global__ __launch_bounds__(256) void mlp_fwd_head_kernel(
   const float nc = wave_sum((float)ncorr);
   if (lane == 0) { redl[wave] = lsum; redl[4 + wave] = nc; }
   __syncthreads();
-  float* out = slab + (size_t)blockIdx.x * (NCLS * H + NCLS);
+  float* out = slab + (size_t)blockIdx.x * fwd_slab_width(H);  // v1 leaves db1 to the unfused backward
   for (int i = tid; i < NCLS * H; i += 256)
     out[i] = ((red[i] + red[NCLS * H + i]) + (red[2 * NCLS * H + i] + red[3 * NCLS * H + i]));
   if (tid < NCLS) out[NCLS * H + tid] = (redb[tid] + redb[NCLS + tid]) + (redb[2 * NCLS + tid] + redb[3 * NCLS + tid]);
@@ -510,6 +512,7 @@ __global__ __launch_bounds__(512) void mlp_fwd_head_v2_kernel(
   for (int r = 0; r < 4; ++r) bo_r[r] = (4 * g + r < C) ? bo[4 * g + r] : 0.f;
 
   f32x4_t acc5[2] = {f32x4_t{0.f, 0.f, 0.f, 0.f}, f32x4_t{0.f, 0.f, 0.f, 0.f}};
+  float db1[2][4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};  // column sums of this lane's dact2 values
   float dbo[4] = {0.f, 0.f, 0.f, 0.f};
   float lsum = 0.f;
   int ncorr = 0;
@@ -661,8 +664,12 @@ __global__ __launch_bounds__(512) void mlp_fwd_head_v2_kernel(
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
         const f32x4_t d = mma16(wo4[t], dzv, f32x4_t{0.f, 0.f, 0.f, 0.f});
-        *reinterpret_cast<uint2*>(dts + (16 * h + c16) * V2_HP + u0 + 16 * t + 4 * g) =
-            make_uint2(mask2(pack2(d[0], d[1]), h2p[h][t][0]), mask2(pack2(d[2], d[3]), h2p[h][t][1]));
+        const uint32_t q0 = mask2(pack2(d[0], d[1]), h2p[h][t][0]), q1 = mask2(pack2(d[2], d[3]), h2p[h][t][1]);
+        *reinterpret_cast<uint2*>(dts + (16 * h + c16) * V2_HP + u0 + 16 * t + 4 * g) = make_uint2(q0, q1);
+        db1[t][0] += __uint_as_float(q0 << 16);
+        db1[t][1] += __uint_as_float(q0 & 0xffff0000u);
+        db1[t][2] += __uint_as_float(q1 << 16);
+        db1[t][3] += __uint_as_float(q1 & 0xffff0000u);
       }
     }
     // ---- stage 5: dWout^T += h2^T . dz over the tile's 32 rows (per-wave transposes) ----
@@ -685,9 +692,19 @@ __global__ __launch_bounds__(512) void mlp_fwd_head_v2_kernel(
   __syncthreads();  // the last tile's dact2 tile is complete
   if (prev_r0 >= 0) v2_store_tile(dts, dact, prev_r0, tid);
   // ---- this wave's units of the workgroup slab: dWout rows 0..15 x units, dbout, loss ----
-  float* out = slab + (size_t)blockIdx.x * (NCLS * H + NCLS);
+  float* out = slab + (size_t)blockIdx.x * fwd_slab_width(H);
 #pragma unroll
   for (int t = 0; t < 2; ++t) *reinterpret_cast<f32x4_t*>(out + (size_t)c16 * H + u0 + 16 * t + 4 * g) = acc5[t];
+  // db1 of this wave's units: sum over the 16 row lanes of each lane group
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float v = db1[t][r];
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) v += __shfl_xor(v, o, 64);
+      if (c16 == 0) out[NCLS * H + NCLS + u0 + 16 * t + 4 * g + r] = v;
+    }
   float* red = zs;  // waves 0 / 1 (halves 0 / 1): dbout [2][16], loss [2], #correct [2]
   if (wave < 2) {
 #pragma unroll
@@ -726,140 +743,228 @@ int launch_v2(const bf16_t* X, const bf16_t* W0, const float* b0, const bf16_t* 
 }
 
 // ---------------------------------------------------------------------------------------------
-// Layer-1 backward in one kernel (H = 256, batch a multiple of 32):
-//   dact1 = (dact2 . W1) * relu'(h1),   dW0 = dact1^T . X,   db0 = sum_rows dact1
-// dact1 never reaches HBM (the unfused chain writes it and reads it back: 2 x 32 MB at batch
-// 65536).  Same split as v2: 8 waves, wave w owns h1 units [32w, 32w + 32); the W1 columns it
-// contracts with (W1[:, u]) stay in registers (64 VGPRs/lane).  Per 32-row tile the dact2 rows
-// and X rows are staged once in LDS (register-staged prefetch of the next tile under this
-// tile's MFMAs); dact1 is masked in registers, transposed through a per-wave [32][16] image and
-// fed to the dW0 MFMAs (K = rows).  Each workgroup leaves one deterministic [H*K0 | H] slab.
-constexpr int B1_DP = V2_H + 8;  // dact2 tile pitch
+// Layer-2 weight gradient + layer-1 backward in ONE pass (H = 256, batch a multiple of 64):
+//   dW1 = dact2^T . h1,   dact1 = (dact2 . W1) * relu'(h1),   dW0 = dact1^T . X,   db0 = sum_rows dact1
+// (db1 = the column sums of dact2 come from the forward kernel, which produces dact2).  The
+// split-K dW1 GEMM and a separate layer-1 kernel each read dact2 and h1 (2 x 64 MB at batch
+// 65536); here they are read once, and dact1 never reaches HBM.
+//
+// Grid: S row slices x 4 h1-unit quadrants (64 units each).  After the XCD remap the four
+// quadrant workgroups of a slice are adjacent (same XCD), so the dact2 / X tiles they all read
+// come from that XCD's L2 after the first.  Workgroup (s, q) owns dW1[:, 64q..64q+64),
+// dW0[64q..64q+64, :] and db0[64q..64q+64) of slab s — one deterministic partial per slice, laid
+// out like the flat parameter buffer (reduced later in a fixed order).
+//
+// Software pipeline, ONE barrier per 64-row tile i (8 waves):
+//   stage tile i+1 (registers -> LDS buffer (i+1)&1) | refill the registers with tile i+2 |
+//   (a) dact1^T[u][r] = W1[:, u]^T . dact2^T   A = W1 columns (registers, two unit blocks per
+//       wave), B = dact2 rows (LDS b128); relu'(h1) mask; dact1 -> LDS buffer i&1
+//       wave: rows 16 (w & 3).., unit blocks 2 (w >> 2) + {0, 1}
+//   (b) dW1[j][u] += dact2^T . h1 (two K = 32 row steps; both operands transposed out of LDS)
+//       wave: unit blocks 2 (w & 1) + {0, 1} x j blocks 4 (w >> 1) + {0..3}
+//   (c) dW0[u][k] += dact1^T . X for tile i-1 (its dact1 is complete after the last barrier)
+//       wave: unit block w & 3, k blocks of half w >> 2  |  barrier
+// X tiles rotate through three buffers (tile i-1 is read by (c) while tile i+1 is staged).
+// Row order of the transposed operands (frag_rows): lane group g supplies rows 4g..4g+3 and
+// 16+4g..16+4g+3 of a 32-row step — one permutation of K, used by both operands of a product.
+// With row pitches of an odd multiple of 8 dwords the 32 lanes of an LDS bank group then read 8
+// consecutive rows: conflict-free, and the row-per-lane b128 reads of (a) are conflict-free too.
+constexpr int BF_Q = 4, BF_QU = V2_H / BF_Q;  // 64 h1 units per workgroup
+constexpr int BF_RT = 64;                     // rows per pipeline tile
+constexpr int BF_DP = V2_H + 16;              // dact2 tile pitch: 136 dwords (8 mod 64)
+constexpr int BF_UP = BF_QU + 16;             // h1 / dact1 quadrant tile pitch: 40 dwords
+
+__device__ __forceinline__ bf16x8_t frag_rows(const bf16_t* img, int pitch, int col0, int lane) {
+  const int li = lane & 15, g = lane >> 4;
+  const bf16_t* p0 = img + (4 * g + (li >> 2)) * pitch + col0 + 4 * (li & 3);
+  const s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)p0);
+  const s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(p0 + 16 * pitch));
+  typedef __attribute__((ext_vector_type(8))) short s16x8_t;
+  const s16x8_t v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8_t, v);
+}
+
+template <int K0> struct BwdLds {
+  static constexpr int XP = K0 + 16;
+  static constexpr int DSM = BF_RT * BF_DP, HS = BF_RT * BF_UP, XS = BF_RT * XP;  // elements per buffer
+  static constexpr size_t bytes = (size_t)(2 * DSM + 2 * HS + 2 * HS + 3 * XS) * sizeof(bf16_t) +
+                                  4 * BF_QU * sizeof(float);
+};
 
 template <int K0>
-__global__ __launch_bounds__(512) void mlp_bwd_l1_kernel(const bf16_t* __restrict__ dact2,
-                                                        const bf16_t* __restrict__ h1,
-                                                        const bf16_t* __restrict__ X,
-                                                        const bf16_t* __restrict__ W1, int B,
-                                                        float* __restrict__ slab) {
-  constexpr int H = V2_H, KC = H / 32, NF = K0 / 16, XP = K0 + 8;
-  constexpr int DV = V2_RT * H / 8 / 512;  // 16-byte vectors of a dact2 tile per thread (2)
-  constexpr int XV = V2_RT * K0 / 8;       // 16-byte vectors of an X tile (256 / 128)
+__global__ __launch_bounds__(512) void mlp_bwd_fused_kernel(const bf16_t* __restrict__ dact2,
+                                                           const bf16_t* __restrict__ h1,
+                                                           const bf16_t* __restrict__ X,
+                                                           const bf16_t* __restrict__ W1, int B, int S,
+                                                           float* __restrict__ gw1, float* __restrict__ gw0,
+                                                           float* __restrict__ gb0, int64_t slab_stride) {
+  using L = BwdLds<K0>;
+  constexpr int H = V2_H, KC = H / 32, XP = L::XP, NFW = K0 / 32;
+  constexpr int XV = BF_RT * K0 / 8;  // 16-byte vectors of an X tile (512 / 256)
   extern __shared__ __attribute__((aligned(16))) bf16_t lds[];
-  bf16_t* dsm = lds;                        // [32][B1_DP]
-  bf16_t* xsm = dsm + V2_RT * B1_DP;        // [32][XP]
+  bf16_t* const dsm0 = lds;                 // [2][64][BF_DP] dact2 tiles
+  bf16_t* const hs0 = dsm0 + 2 * L::DSM;    // [2][64][BF_UP] h1 quadrant tiles
+  bf16_t* const d1s0 = hs0 + 2 * L::HS;     // [2][64][BF_UP] dact1 quadrant tiles
+  bf16_t* const xs0 = d1s0 + 2 * L::HS;     // [3][64][XP] X tiles
+  float* const red = reinterpret_cast<float*>(xs0 + 3 * L::XS);  // [4][64] db0 of the row blocks
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int c16 = lane & 15, g = lane >> 4;
-  const int u0 = wave * V2_U;
-  bf16_t* img = xsm + V2_RT * XP + wave * 2 * V2_IMG;  // dact1 units t = 0, 1
+  const int b = xcd_remap(blockIdx.x, gridDim.x);
+  const int slice = b / BF_Q, qu0 = (b % BF_Q) * BF_QU;
+  const int rb = wave & 3, up = 2 * (wave >> 2);            // (a)
+  const int ubp = 2 * (wave & 1), jb0 = 4 * (wave >> 1);    // (b)
+  const int ub = wave & 3, fb = (wave >> 2) * NFW;          // (c)
+  const int ntiles = B / BF_RT, per = (ntiles + S - 1) / S;
+  const int t0 = slice * per, n = max(0, min(ntiles, t0 + per) - t0);
 
-  // A fragments of dact1^T = W1^T . dact2^T: A[i][k = j] = W1[j][i], i = u0 + 16t + c16
+  // (a) A fragments: A[u][k = j] = W1[kc * 32 + 8g + i][qu0 + 16 (up + e) + c16]
   bf16x8_t w1t[2][KC];
 #pragma unroll
-  for (int t = 0; t < 2; ++t)
+  for (int e = 0; e < 2; ++e)
 #pragma unroll
     for (int kc = 0; kc < KC; ++kc) {
       typedef __attribute__((ext_vector_type(8))) short s16x8_t;
       s16x8_t v;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = (short)W1[(size_t)(kc * 32 + 8 * g + j) * H + u0 + 16 * t + c16];
-      w1t[t][kc] = __builtin_bit_cast(bf16x8_t, v);
+      for (int i = 0; i < 8; ++i) v[i] = (short)W1[(size_t)(kc * 32 + 8 * g + i) * H + qu0 + 16 * (up + e) + c16];
+      w1t[e][kc] = __builtin_bit_cast(bf16x8_t, v);
     }
-  f32x4_t acc0[2][NF];
+  f32x4_t acc1[4][2], acc0[NFW];
 #pragma unroll
-  for (int t = 0; t < 2; ++t)
+  for (int i = 0; i < 4; ++i) acc1[i][0] = acc1[i][1] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int f = 0; f < NF; ++f) acc0[t][f] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  for (int f = 0; f < NFW; ++f) acc0[f] = f32x4_t{0.f, 0.f, 0.f, 0.f};
   float rs[2][4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
 
-  const int ntiles = B / V2_RT;
-  // dact2 / X tiles are contiguous [32][H] / [32][K0] row blocks: register-staged 16-byte loads
-  uint4 pd0 = make_uint4(0, 0, 0, 0), pd1 = pd0, px = pd0;
-  static_assert(DV == 2, "two dact2 vectors per thread");
-  int T = blockIdx.x;
-#define HAR_BWD_L1_LOAD(tt)                                                                            \
-  {                                                                                                    \
-    const bf16_t* d_ = dact2 + (size_t)(tt) * V2_RT * H;                                               \
-    pd0 = *reinterpret_cast<const uint4*>(d_ + (size_t)tid * 8);                                       \
-    pd1 = *reinterpret_cast<const uint4*>(d_ + (size_t)(tid + 512) * 8);                               \
-    if (tid < XV) px = *reinterpret_cast<const uint4*>(X + (size_t)(tt) * V2_RT * K0 + (size_t)tid * 8); \
-    for (int h_ = 0; h_ < 2; ++h_)                                                                     \
-      for (int t_ = 0; t_ < 2; ++t_)                                                                   \
-        mk[h_][t_] = *reinterpret_cast<const uint2*>(h1 + (size_t)((tt) * V2_RT + 16 * h_ + c16) * H + \
-                                                     u0 + 16 * t_ + 4 * g);                            \
+  // Register staging of a tile: four dact2 vectors, one h1-quadrant vector and one X vector per
+  // thread (for K0 = 32 threads 256.. reload threads 0..255's X vector and store the same bytes
+  // to the same place).  Per-thread pointers are fixed once; every load is unconditional (a tile
+  // index past the slice is clamped to a valid tile whose bytes are staged but never used), so
+  // the compiler's vmcnt accounting is exact on every path.
+  const bf16_t* ldd = dact2 + (size_t)tid * 8;
+  const bf16_t* ldh = h1 + (size_t)(tid >> 3) * H + qu0 + (tid & 7) * 8;
+  const bf16_t* ldx = X + (size_t)(tid & (XV - 1)) * 8;
+  const int sdd = (tid >> 5) * BF_DP + (tid & 31) * 8;  // + 16 rows * BF_DP per dact2 vector
+  const int sdh = (tid >> 3) * BF_UP + (tid & 7) * 8;
+  const int sdx = ((tid & (XV - 1)) / (K0 / 8)) * XP + ((tid & (XV - 1)) % (K0 / 8)) * 8;
+  const int tlast = ntiles - 1;
+  uint4 r0, r1, r2, r3, r4, r5;
+#define HAR_BWD_LOAD(t)                                                      \
+  {                                                                          \
+    const int64_t tt_ = min(t, tlast);                                       \
+    const bf16_t* d_ = ldd + tt_ * BF_RT * H;                                \
+    r0 = *reinterpret_cast<const uint4*>(d_);                                \
+    r1 = *reinterpret_cast<const uint4*>(d_ + 16 * H);                       \
+    r2 = *reinterpret_cast<const uint4*>(d_ + 32 * H);                       \
+    r3 = *reinterpret_cast<const uint4*>(d_ + 48 * H);                       \
+    r4 = *reinterpret_cast<const uint4*>(ldh + tt_ * BF_RT * H);             \
+    r5 = *reinterpret_cast<const uint4*>(ldx + tt_ * BF_RT * K0);            \
   }
-  // relu'(h1) words of this lane's (row, unit) pairs, prefetched a tile ahead with the tiles
-  uint2 mk[2][2] = {{make_uint2(0, 0), make_uint2(0, 0)}, {make_uint2(0, 0), make_uint2(0, 0)}};
-  if (T < ntiles) HAR_BWD_L1_LOAD(T)
-  for (; T < ntiles; T += gridDim.x) {
-    const int r0 = T * V2_RT;
-    __syncthreads();  // the previous tile's LDS reads are done
-    *reinterpret_cast<uint4*>(dsm + (tid / (H / 8)) * B1_DP + (tid % (H / 8)) * 8) = pd0;
-    *reinterpret_cast<uint4*>(dsm + ((tid + 512) / (H / 8)) * B1_DP + ((tid + 512) % (H / 8)) * 8) = pd1;
-    if (tid < XV) *reinterpret_cast<uint4*>(xsm + (tid / (K0 / 8)) * XP + (tid % (K0 / 8)) * 8) = px;
-    const uint2 mc[2][2] = {{mk[0][0], mk[0][1]}, {mk[1][0], mk[1][1]}};
-    __syncthreads();  // the tiles are in LDS
-    if (T + gridDim.x < ntiles) HAR_BWD_L1_LOAD(T + gridDim.x)
-    // ---- dact1^T = W1^T . dact2^T for this wave's units ----
-    f32x4_t a[2][2];
-#pragma unroll
-    for (int h = 0; h < 2; ++h)
-#pragma unroll
-      for (int t = 0; t < 2; ++t) a[h][t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#define HAR_BWD_STAGE(i)                                                     \
+  {                                                                          \
+    bf16_t* d_ = dsm0 + ((i) & 1) * L::DSM + sdd;                            \
+    *reinterpret_cast<uint4*>(d_) = r0;                                      \
+    *reinterpret_cast<uint4*>(d_ + 16 * BF_DP) = r1;                         \
+    *reinterpret_cast<uint4*>(d_ + 32 * BF_DP) = r2;                         \
+    *reinterpret_cast<uint4*>(d_ + 48 * BF_DP) = r3;                         \
+    *reinterpret_cast<uint4*>(hs0 + ((i) & 1) * L::HS + sdh) = r4;           \
+    *reinterpret_cast<uint4*>(xs0 + ((i) % 3) * L::XS + sdx) = r5;           \
+  }
+
+  // (a) + (b) of local tile i (LDS buffers i & 1)
+  auto tile_ab = [&](int i) __attribute__((always_inline)) {
+    const bf16_t* dsm = dsm0 + (i & 1) * L::DSM;
+    const bf16_t* hs = hs0 + (i & 1) * L::HS;
+    bf16_t* d1s = d1s0 + (i & 1) * L::HS;
+    f32x4_t a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int kc = 0; kc < KC; ++kc) {
-      bf16x8_t b[2];
-#pragma unroll
-      for (int h = 0; h < 2; ++h)
-        b[h] = *reinterpret_cast<const bf16x8_t*>(dsm + (16 * h + c16) * B1_DP + kc * 32 + 8 * g);
-#pragma unroll
-      for (int h = 0; h < 2; ++h)
-#pragma unroll
-        for (int t = 0; t < 2; ++t) a[h][t] = mma32(w1t[t][kc], b[h], a[h][t]);
+      const bf16x8_t bv = *reinterpret_cast<const bf16x8_t*>(dsm + (16 * rb + c16) * BF_DP + kc * 32 + 8 * g);
+      a0 = mma32(w1t[0][kc], bv, a0);
+      a1 = mma32(w1t[1][kc], bv, a1);
     }
-    // ---- relu' mask, bf16, db0 row sums, transposed image for dW0 ----
 #pragma unroll
-    for (int h = 0; h < 2; ++h)
+    for (int e = 0; e < 2; ++e) {
+      const f32x4_t& a = e ? a1 : a0;
+      const int col = 16 * (up + e) + 4 * g;
+      const uint2 m = *reinterpret_cast<const uint2*>(hs + (16 * rb + c16) * BF_UP + col);
+      const float d0 = bf_pos(m.x) ? a[0] : 0.f, d1 = bf_pos(m.x >> 16) ? a[1] : 0.f;
+      const float d2 = bf_pos(m.y) ? a[2] : 0.f, d3 = bf_pos(m.y >> 16) ? a[3] : 0.f;
+      const uint32_t p0 = pack2(d0, d1), p1 = pack2(d2, d3);
+      rs[e][0] += __uint_as_float(p0 << 16);
+      rs[e][1] += __uint_as_float(p0 & 0xffff0000u);
+      rs[e][2] += __uint_as_float(p1 << 16);
+      rs[e][3] += __uint_as_float(p1 & 0xffff0000u);
+      *reinterpret_cast<uint2*>(d1s + (16 * rb + c16) * BF_UP + col) = make_uint2(p0, p1);
+    }
 #pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        const uint32_t m0 = mc[h][t].x, m1 = mc[h][t].y;
-        const float d0 = bf_pos(m0) ? a[h][t][0] : 0.f, d1 = bf_pos(m0 >> 16) ? a[h][t][1] : 0.f;
-        const float d2 = bf_pos(m1) ? a[h][t][2] : 0.f, d3 = bf_pos(m1 >> 16) ? a[h][t][3] : 0.f;
-        const uint32_t p0 = pack2(d0, d1), p1 = pack2(d2, d3);
-        rs[t][0] += __uint_as_float(p0 << 16);
-        rs[t][1] += __uint_as_float(p0 & 0xffff0000u);
-        rs[t][2] += __uint_as_float(p1 << 16);
-        rs[t][3] += __uint_as_float(p1 & 0xffff0000u);
-        *reinterpret_cast<uint2*>(img + t * V2_IMG + (16 * h + c16) * V2_SP + 4 * g) = make_uint2(p0, p1);
+    for (int ks = 0; ks < 2; ++ks) {
+      const bf16x8_t hb0 = frag_rows(hs + 32 * ks * BF_UP, BF_UP, 16 * ubp, lane);
+      const bf16x8_t hb1 = frag_rows(hs + 32 * ks * BF_UP, BF_UP, 16 * (ubp + 1), lane);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const bf16x8_t da = frag_rows(dsm + 32 * ks * BF_DP, BF_DP, 16 * (jb0 + j), lane);
+        acc1[j][0] = mma32(da, hb0, acc1[j][0]);
+        acc1[j][1] = mma32(da, hb1, acc1[j][1]);
       }
-    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's images are in LDS
-    __builtin_amdgcn_wave_barrier();
-    // ---- dW0 += dact1^T . X over the tile's 32 rows ----
-#pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      const bf16x8_t A = frag_tr(img + t * V2_IMG, V2_SP, 0, lane);
-#pragma unroll
-      for (int f = 0; f < NF; ++f) acc0[t][f] = mma32(A, frag_tr(xsm, XP, 16 * f, lane), acc0[t][f]);
     }
+  };
+  // (c) of local tile i (its dact1 buffer i & 1, X buffer i % 3)
+  auto tile_c = [&](int i) __attribute__((always_inline)) {
+    const bf16_t* d1s = d1s0 + (i & 1) * L::HS;
+    const bf16_t* xs = xs0 + (i % 3) * L::XS;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const bf16x8_t A = frag_rows(d1s + 32 * ks * BF_UP, BF_UP, 16 * ub, lane);
+#pragma unroll
+      for (int f = 0; f < NFW; ++f)
+        acc0[f] = mma32(A, frag_rows(xs + 32 * ks * XP, XP, 16 * (fb + f), lane), acc0[f]);
+    }
+  };
+
+  HAR_BWD_LOAD(t0)
+  HAR_BWD_STAGE(0)
+  HAR_BWD_LOAD(t0 + 1)
+  __builtin_amdgcn_sched_barrier(0);
+  __syncthreads();  // tile 0 is in LDS
+  for (int i = 0; i < n; ++i) {
+    HAR_BWD_STAGE(i + 1)          // waits for the refill issued one iteration ago
+    HAR_BWD_LOAD(t0 + i + 2)
+    __builtin_amdgcn_sched_barrier(0);  // the refill is issued before the compute
+    tile_ab(i);
+    if (i > 0) tile_c(i - 1);     // wave-uniform
+    __syncthreads();              // tile i+1 staged; tile i's dact1 complete; buffers of i-1 free
   }
-#undef HAR_BWD_L1_LOAD
-  // ---- this wave's rows of the workgroup slab: dW0 [H][K0], db0 [H] ----
-  float* out = slab + (size_t)blockIdx.x * (H * K0 + H);
+  if (n > 0) tile_c(n - 1);
+#undef HAR_BWD_LOAD
+#undef HAR_BWD_STAGE
+
+  // ---- this workgroup's parts of slab `slice` ----
+  float* w1o = gw1 + (size_t)slice * slab_stride;
 #pragma unroll
-  for (int t = 0; t < 2; ++t)
+  for (int j = 0; j < 4; ++j)
 #pragma unroll
-    for (int f = 0; f < NF; ++f)
+    for (int uu = 0; uu < 2; ++uu)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) out[(size_t)(u0 + 16 * t + 4 * g + r) * K0 + 16 * f + c16] = acc0[t][f][r];
+      for (int r = 0; r < 4; ++r)
+        w1o[(size_t)(16 * (jb0 + j) + 4 * g + r) * H + qu0 + 16 * (ubp + uu) + c16] = acc1[j][uu][r];
+  float* w0o = gw0 + (size_t)slice * slab_stride;
 #pragma unroll
-  for (int t = 0; t < 2; ++t)
+  for (int f = 0; f < NFW; ++f)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) w0o[(size_t)(qu0 + 16 * ub + 4 * g + r) * K0 + 16 * (fb + f) + c16] = acc0[f][r];
+#pragma unroll
+  for (int e = 0; e < 2; ++e)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      float v = rs[t][r];
+      float v = rs[e][r];
 #pragma unroll
       for (int o = 1; o < 16; o <<= 1) v += __shfl_xor(v, o, 64);
-      if (c16 == 0) out[H * K0 + u0 + 16 * t + 4 * g + r] = v;
+      if (c16 == 0) red[rb * BF_QU + 16 * (up + e) + 4 * g + r] = v;
     }
+  __syncthreads();
+  if (tid < BF_QU)
+    gb0[(size_t)slice * slab_stride + qu0 + tid] = (red[tid] + red[BF_QU + tid]) + (red[2 * BF_QU + tid] + red[3 * BF_QU + tid]);
 }
 
 // Training only: serving (stages 1-3) keeps v1 — without the backward stages, v2's two barriers
@@ -931,17 +1036,25 @@ extern "C" int har_mlp_fwd_infer_f32(const float* X, int ldx, int F, int K0, con
   return -4;
 }
 
-extern "C" int har_mlp_bwd_l1_grid(int B) { return std::max(1, std::min(256, B / V2_RT)); }
+extern "C" int har_mlp_fwd_head_variant(int H, int B) { return use_v2(H, B) ? 2 : 1; }
 
-// dact1 = (dact2 . W1) * relu'(h1) -> per-workgroup slabs [H*K0 | H] of dW0 / db0 (H = 256).
-extern "C" int har_mlp_bwd_l1(const uint16_t* dact2, const uint16_t* h1, const uint16_t* X, int K0,
-                              const uint16_t* W1, int H, int B, float* slab, hipStream_t s) {
-  if (H != V2_H || B <= 0 || B % V2_RT || (K0 != 32 && K0 != 64)) return -2;
-  if (((uintptr_t)dact2 | (uintptr_t)h1 | (uintptr_t)X | (uintptr_t)W1 | (uintptr_t)slab) & 15) return -3;
-  const int nwg = har_mlp_bwd_l1_grid(B);
-  const size_t lds = ((size_t)V2_RT * B1_DP + (size_t)V2_RT * (K0 + 8) + (size_t)V2_W * 2 * V2_IMG) * sizeof(bf16_t);
-  if (K0 == 64) mlp_bwd_l1_kernel<64><<<nwg, 512, lds, s>>>(dact2, h1, X, W1, B, slab);
-  else mlp_bwd_l1_kernel<32><<<nwg, 512, lds, s>>>(dact2, h1, X, W1, B, slab);
+// Row slices of the fused backward: >= 4 tiles (256 rows) per slice, <= 64 slices (one slab each).
+extern "C" int har_mlp_bwd_fused_slices(int B) { return std::max(1, std::min(64, B / BF_RT / 4)); }
+
+// dW1 / dW0 / db0 of the 2-hidden-layer step (H = 256, B % 64 == 0): per-slice partials written at
+// gw1 / gw0 / gb0 + s * slab_stride (s < har_mlp_bwd_fused_slices(B)).
+extern "C" int har_mlp_bwd_fused(const uint16_t* dact2, const uint16_t* h1, const uint16_t* X, int K0,
+                                 const uint16_t* W1, int H, int B, float* gw1, float* gw0, float* gb0,
+                                 int64_t slab_stride, hipStream_t s) {
+  if (H != V2_H || B <= 0 || B % BF_RT || (K0 != 32 && K0 != 64) || slab_stride < (int64_t)H * H) return -2;
+  if (((uintptr_t)dact2 | (uintptr_t)h1 | (uintptr_t)X | (uintptr_t)W1) & 15) return -3;
+  const int S = har_mlp_bwd_fused_slices(B);
+  if (K0 == 64)
+    mlp_bwd_fused_kernel<64><<<S * BF_Q, 512, BwdLds<64>::bytes, s>>>(dact2, h1, X, W1, B, S, gw1, gw0, gb0,
+                                                                      slab_stride);
+  else
+    mlp_bwd_fused_kernel<32><<<S * BF_Q, 512, BwdLds<32>::bytes, s>>>(dact2, h1, X, W1, B, S, gw1, gw0, gb0,
+                                                                      slab_stride);
   HAR_CHECK_LAUNCH();
   return 0;
 }

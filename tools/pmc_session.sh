@@ -15,7 +15,7 @@ while read -r grp; do
   [ -z "$grp" ] && continue
   i=$((i + 1))
   timeout -s KILL 120 rocprofv3 --pmc $grp --output-format csv -d "$OUT/pmc$i" -o pmc -- \
-      python3 "$ROOT/bench.py" --steps ${PMC_STEPS:-5} --warmup 2 > "$OUT/pmc$i.log" 2>&1
+      python3 "$ROOT/bench.py" --steps ${PMC_STEPS:-5} --warmup 2 ${BENCH_ARGS:-} > "$OUT/pmc$i.log" 2>&1
   rc=$?
   echo "pass $i ($grp): rc=$rc"
   [ $rc -ne 0 ] && exit $rc
