@@ -176,7 +176,6 @@ class MLPEngine:
             # the fused backward (mlp_bwd_fused) writes one partial per row slice into the same slabs
             n_slab = max(self.n_splits, _native.kernels().mlp_bwd_fused_slices(self.B))
             self.slabs = torch.zeros(n_slab, L.total, dtype=torch.float32, device=dev)
-            self.done = torch.zeros(1, dtype=torch.int32, device=dev)  # grad_reduce_adam's workgroup counter
             # one-kernel forward + head + dWout (mlp_fused.hip) for the 2-hidden-layer shapes it covers
             self.fused_ok = (len(L.hidden) == 2 and L.hidden[0] == L.hidden[1] and L.hidden[0] in (128, 256)
                              and L.in_pad in (32, 64) and L.num_classes <= 16
@@ -292,7 +291,7 @@ class MLPEngine:
             sb = self.slabs.data_ptr()
             mod.mlp_bwd_fused(dact.data_ptr(), h1.data_ptr(), Xb.data_ptr(), K0, self._w(self.Pb, "W1").data_ptr(), H,
                               B, sb + 4 * L.by_name["W1"].offset, sb + 4 * L.by_name["W0"].offset,
-                              sb + 4 * L.by_name["b0"].offset, total, s)
+                              sb + 4 * L.by_name["b0"].offset, total, self.step_count.data_ptr(), s)
             if on_grad is not None:
                 on_grad("W1")
                 on_grad("W0")
@@ -350,9 +349,10 @@ class MLPEngine:
 
     GR_REDUCE, GR_STORE, GR_ADAM = 1, 2, 4
 
-    def _grad_kernel(self, mode: int):
+    def _grad_kernel(self, mode: int, tick: bool = False):
         """mlp.hip grad_reduce_adam: one deterministic single-level reduction of every gradient
-        slab (fixed order) and/or the Adam update; the same kernel for every world size."""
+        slab (fixed order) and/or the Adam update; the same kernel for every world size.  The
+        step counter ticks once per step: in the fused backward kernel, else here (``tick``)."""
         b1, b2 = self.betas
         regs = self._grad_regions() if mode & self.GR_REDUCE else []
         cols = list(zip(*regs)) if regs else [[]] * 5
@@ -360,14 +360,14 @@ class MLPEngine:
             list(cols[2]), list(cols[0]), [e - a for a, e in zip(cols[0], cols[1])], list(cols[4]), list(cols[3]),
             self.layout.total, self.G.data_ptr(), self.P.data_ptr(), self.m.data_ptr(), self.v.data_ptr(),
             self.Pb.data_ptr(), float(self.lr), b1, b2, float(self.eps), float(self.wd), self.step_count.data_ptr(),
-            self.done.data_ptr(), mode, _native.stream_ptr())
+            int(tick), mode, _native.stream_ptr())
 
     def reduce_grads_native(self):
         """G = the sum of the last batch's gradient slabs (needed before a collective)."""
-        self._grad_kernel(self.GR_REDUCE | self.GR_STORE)
+        self._grad_kernel(self.GR_REDUCE | self.GR_STORE, tick=not self.last_bwd)
 
     def optimizer_step_native(self):
-        """Adam from G (after the all-reduce); ticks the device step counter."""
+        """Adam from G (after the all-reduce; the step counter ticked with the gradient)."""
         self._grad_kernel(self.GR_ADAM)
 
     def collective_stats(self):
@@ -403,7 +403,7 @@ class MLPEngine:
                 self.allreduce_grads()
                 self.optimizer_step_native()
             else:
-                self._grad_kernel(self.GR_REDUCE | self.GR_ADAM)
+                self._grad_kernel(self.GR_REDUCE | self.GR_ADAM, tick=not self.last_bwd)
         else:
             self.train_step_torch(Xb, yb, global_batch)
 

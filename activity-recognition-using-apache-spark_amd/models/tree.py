@@ -28,7 +28,6 @@ per-rank histograms are all-reduced before split selection.
 from __future__ import annotations
 
 import math
-import os
 from dataclasses import dataclass
 from typing import List, Optional
 
@@ -115,13 +114,6 @@ class ForestBuilder:
         self.thr_mat = torch.from_numpy(thr_mat).to(X.device)
         self.bins = bin_features(X, self.thresholds).to(X.device).contiguous()  # [F, N] uint8 (HIP on the GPU)
 
-    def _levels_native(self, *a):
-        # HAR_TREE_LEVEL_SORT=1 keeps the host-frontier radix-sort loop (A/B and equality oracle)
-        if os.environ.get("HAR_TREE_LEVEL_SORT", "0") != "1":
-            _levels_device_frontier(self, *a)
-        else:
-            _levels_native_impl(self, *a)
-
     def bootstrap_weights(self, N: int, device, row_offset: int = 0) -> torch.Tensor:
         if not self.bootstrap:
             return torch.ones(self.T, N, dtype=torch.float32, device=device)
@@ -143,9 +135,6 @@ class ForestBuilder:
         Tn, K, D = self.T, self.K, self.D
         m = subset_size(self.subset, F, Tn)
         y32 = y.to(torch.int32).contiguous()
-        W = self.bootstrap_weights(N, dev, row_offset)        # [T, N]
-        if row_weight is not None:
-            W = W * row_weight.to(device=dev, dtype=W.dtype)
         n_all = N
         if self.allreduce is not None:  # data parallel: the node capacity must agree across ranks
             nt = torch.tensor([float(N)], dtype=torch.float64, device=dev)
@@ -158,24 +147,38 @@ class ForestBuilder:
         right = torch.zeros(Tn, maxn, dtype=torch.int32, device=dev)
         stats = torch.zeros(Tn, maxn, K, dtype=torch.float32, device=dev)
         gains = torch.zeros(Tn, maxn, dtype=torch.float32, device=dev)
-        # root class counts
-        # [T, N] x one-hot [N, K]: one GEMM (exact: integer weights) instead of T*N contended atomics
+        n_nodes = np.ones(Tn, dtype=np.int64)
+        if dev.type == "cuda":
+            # ONE kernel (tree.hip tree_init): bootstrap weights x row weights, node ids, root class
+            # counts into stats[:, 0], label range check (read with the level loop's first sync)
+            W = torch.empty(Tn, N, dtype=torch.float32, device=dev)
+            node_of = torch.empty(Tn, N, dtype=torch.int32, device=dev)
+            bad = torch.zeros(1, dtype=torch.int32, device=dev)
+            rw = None if row_weight is None else row_weight.to(device=dev, dtype=torch.float32).contiguous()
+            _native.kernels().tree_init(self.seed, self.tree_offset, Tn, row_offset, N, int(self.bootstrap),
+                                        0 if rw is None else rw.data_ptr(), y32.data_ptr(), K, W.data_ptr(),
+                                        node_of.data_ptr(), stats.data_ptr(), maxn * K, bad.data_ptr(),
+                                        _native.stream_ptr())
+            if self.allreduce is not None:
+                root = stats[:, 0].contiguous()
+                self.allreduce(root)
+                stats[:, 0] = root
+            _levels_device_frontier(self, y32, W, N, F, m, maxn, stats, feature, thresh, left, right, gains,
+                                    n_nodes, node_of, bad)
+            return ForestArrays(feature, thresh, left, right, stats, n_nodes, D, gains)
+        # ---- CPU builder (PyTorch; the oracle of the device loop) ----
+        W = self.bootstrap_weights(N, dev, row_offset)        # [T, N]
+        if row_weight is not None:
+            W = W * row_weight.to(device=dev, dtype=W.dtype)
+        # [T, N] x one-hot [N, K]: exact (integer weights)
         root = W @ torch.nn.functional.one_hot(y.long(), K).to(W.dtype)
         if self.allreduce is not None:
             self.allreduce(root)
         stats[:, 0] = root
-        n_nodes = np.ones(Tn, dtype=np.int64)
         node_of = torch.zeros(Tn, N, dtype=torch.int32, device=dev)   # node id per (tree,row); -1 = done
         node_of[W == 0] = -1
-        # frontier: (tree, node, depth)
-        front_t = np.arange(Tn, dtype=np.int64)
+        front_t = np.arange(Tn, dtype=np.int64)   # frontier: (tree, node)
         front_n = np.zeros(Tn, dtype=np.int64)
-        use_native = dev.type == "cuda"
-        if use_native:
-            if y32.numel() and (int(y32.max()) >= K or int(y32.min()) < 0):
-                raise ValueError("labels out of range")
-            self._levels_native(y32, W, N, F, m, maxn, stats, feature, thresh, left, right, gains, n_nodes, node_of)
-            return ForestArrays(feature, thresh, left, right, stats, n_nodes, D, gains)
         for depth in range(D):
             if len(front_t) == 0:
                 break
@@ -188,64 +191,28 @@ class ForestBuilder:
             if A == 0:
                 break
             # ---- group the rows of every candidate node ----
-            if use_native:
-                # device: int32 keys from one HIP pass, a 32-bit radix sort, counts by binary search
-                # over the sorted keys (no atomics), feature subsets drawn on the device
-                mod = _native.kernels()
-                st_ptr = _native.stream_ptr()
-                cand_idx = torch.full((Tn, maxn), -1, dtype=torch.int32, device=dev)
-                cand_idx[torch.as_tensor(ct, device=dev), torch.as_tensor(cn, device=dev)] = \
-                    torch.arange(A, dtype=torch.int32, device=dev)
-                key = torch.empty(Tn * N, dtype=torch.int32, device=dev)
-                mod.tree_level_keys(node_of.data_ptr(), cand_idx.data_ptr(), Tn, N, maxn, key.data_ptr(), st_ptr)
-                flat = torch.nonzero(key >= 0).squeeze(1)
-                keys, order = torch.sort(key[flat], stable=True)
-                fo = flat[order]
-                rows = (fo % N).to(torch.int32).contiguous()
-                row_w = W.reshape(-1)[fo].contiguous()
-                bounds = torch.searchsorted(keys, torch.arange(A + 1, dtype=torch.int32, device=dev))
-                counts = (bounds[1:] - bounds[:-1]).to(torch.int32)
-                starts = bounds[:-1].to(torch.int32).contiguous()
-                if m >= F:
-                    feats = torch.arange(F, dtype=torch.int32, device=dev).repeat(A, 1)
-                else:
-                    feats = torch.empty(A, m, dtype=torch.int32, device=dev)
-                    tr = torch.as_tensor(ct + self.tree_offset, dtype=torch.int32, device=dev)
-                    nd = torch.as_tensor(cn, dtype=torch.int32, device=dev)
-                    mod.tree_feature_subsets(self.seed, tr.data_ptr(), nd.data_ptr(), A, F, m, feats.data_ptr(),
-                                             st_ptr)
-            else:
-                cand_idx = torch.full((Tn, maxn), -1, dtype=torch.int64, device=dev)
-                cand_idx[torch.as_tensor(ct, device=dev), torch.as_tensor(cn, device=dev)] = torch.arange(A,
-                                                                                                         device=dev)
-                valid = node_of >= 0
-                key = torch.where(valid, cand_idx.gather(1, node_of.clamp_min(0).long()),
-                                  torch.full_like(node_of, -1, dtype=torch.int64))
-                sel = key >= 0
-                tt, rr = torch.nonzero(sel, as_tuple=True)
-                kk = key[tt, rr]
-                order = torch.argsort(kk, stable=True)
-                rows = rr[order].to(torch.int32).contiguous()
-                keys = kk[order]
-                row_w = W[tt[order], rr[order]].contiguous()
-                counts = torch.bincount(keys, minlength=A).to(torch.int32)
-                starts = (torch.cumsum(counts, 0) - counts).to(torch.int32)
-                feats = torch.from_numpy(rng.feature_subsets(self.seed, ct + self.tree_offset, cn, F, m)).to(dev)
+            cand_idx = torch.full((Tn, maxn), -1, dtype=torch.int64, device=dev)
+            cand_idx[torch.as_tensor(ct, device=dev), torch.as_tensor(cn, device=dev)] = torch.arange(A, device=dev)
+            valid = node_of >= 0
+            key = torch.where(valid, cand_idx.gather(1, node_of.clamp_min(0).long()),
+                              torch.full_like(node_of, -1, dtype=torch.int64))
+            sel = key >= 0
+            tt, rr = torch.nonzero(sel, as_tuple=True)
+            kk = key[tt, rr]
+            order = torch.argsort(kk, stable=True)
+            rows = rr[order].to(torch.int32).contiguous()
+            keys = kk[order]
+            row_w = W[tt[order], rr[order]].contiguous()
+            feats = torch.from_numpy(rng.feature_subsets(self.seed, ct + self.tree_offset, cn, F, m)).to(dev)
             # ---- histogram + best split ----
-            if use_native:
-                res = T.hist_split_native(self.bins, self.nbins, y32, rows, row_w, starts, counts, feats, K,
-                                          self.max_bins, self.min_inst, self.min_gain, self.impurity,
-                                          allreduce=None if self.owner is not None else self.allreduce,
-                                          owner=self.owner)
+            hist = T.level_histogram(self.bins, y32, rows, row_w, keys, A, feats, K, self.max_bins)
+            if self.owner is not None:
+                res = T.split_owner(hist, feats, K, self.owner, lambda h, a0, a1: T.split_from_hist(
+                    h, feats[a0:a1], self.nbins, self.min_inst, self.min_gain, self.impurity))
             else:
-                hist = T.level_histogram(self.bins, y32, rows, row_w, keys, A, feats, K, self.max_bins)
-                if self.owner is not None:
-                    res = T.split_owner(hist, feats, K, self.owner, lambda h, a0, a1: T.split_from_hist(
-                        h, feats[a0:a1], self.nbins, self.min_inst, self.min_gain, self.impurity))
-                else:
-                    if self.allreduce is not None:
-                        self.allreduce(hist)
-                    res = T.split_from_hist(hist, feats, self.nbins, self.min_inst, self.min_gain, self.impurity)
+                if self.allreduce is not None:
+                    self.allreduce(hist)
+                res = T.split_from_hist(hist, feats, self.nbins, self.min_inst, self.min_gain, self.impurity)
             do_split = (res.gain > 0) & torch.isfinite(res.gain)
             ds = do_split.cpu().numpy()
             if not ds.any():
@@ -271,19 +238,6 @@ class ForestBuilder:
             stats[ti, cl] = lstat
             stats[ti, cl + 1] = res.total[dsi] - lstat
             # ---- partition: rows of the nodes split at THIS level move to a child, all others finish ----
-            if use_native:
-                lf = torch.full((Tn, maxn), -1, dtype=torch.int32, device=dev)
-                lb = torch.zeros(Tn, maxn, dtype=torch.int32, device=dev)
-                ll = torch.zeros(Tn, maxn, dtype=torch.int32, device=dev)
-                lf[ti, ni] = bf.to(torch.int32)
-                lb[ti, ni] = bb.to(torch.int32)
-                ll[ti, ni] = cl.to(torch.int32)
-                node_of = node_of.contiguous()
-                _native.kernels().tree_partition(node_of.data_ptr(), lf.data_ptr(), lb.data_ptr(), ll.data_ptr(),
-                                                 self.bins.data_ptr(), Tn, N, maxn, _native.stream_ptr())
-                front_t = np.repeat(st_t, 2)
-                front_n = np.stack([child_l, child_l + 1], 1).reshape(-1)
-                continue
             lvl_feat = torch.full((Tn, maxn), -1, dtype=torch.int64, device=dev)
             lvl_bin = torch.zeros(Tn, maxn, dtype=torch.int64, device=dev)
             lvl_left = torch.zeros(Tn, maxn, dtype=torch.int64, device=dev)
@@ -305,182 +259,13 @@ class ForestBuilder:
 GROUP_MAX_NT = 4096  # tree_level.hip: per-tree candidates a level grouping keeps in LDS
 
 
-class _Pinned:
-    """Reusable page-locked staging buffer for the per-level host -> device uploads: an
-    upload from pageable memory synchronizes the stream, so every level would stall
-    several times; one non-blocking copy from here does not.  Each upload site owns one
-    buffer, and the level loop synchronizes once per level (its single device -> host
-    transfer) between two uses of the same buffer, so a copy never reads a rewritten one."""
-
-    def __init__(self, n: int):
-        self.buf = torch.empty(max(1, n), dtype=torch.int64).pin_memory()
-
-    def upload(self, arrays, device):
-        n = sum(len(a) for a in arrays)
-        if n > self.buf.numel():
-            self.buf = torch.empty(2 * n, dtype=torch.int64).pin_memory()
-        o, out = 0, []
-        host = self.buf.numpy()
-        for a in arrays:
-            host[o:o + len(a)] = a
-            o += len(a)
-        dev = self.buf[:n].to(device, non_blocking=True)
-        o = 0
-        for a in arrays:
-            out.append(dev[o:o + len(a)])
-            o += len(a)
-        return out
-
-
-def _levels_native_impl(b: "ForestBuilder", y32, W, N: int, F: int, m: int, maxn: int, stats, feature, thresh,
-                        left, right, gains, n_nodes, node_of):
-    """Device level loop with ONE device -> host transfer per level.
-
-    Per level: candidate keys (HIP), a 32-bit radix sort of all (tree, row) keys (finished
-    rows sort first, key -1, so no compaction / nonzero sync), node row ranges by binary
-    search, device feature subsets, the fused histogram + split kernel, then — for every
-    candidate — split decision and both children's candidacy computed on the device and
-    fetched together; the host only allocates child ids (numpy) and uploads them through a
-    pinned buffer without blocking."""
-    dev = W.device
-    Tn, K, D = b.T, b.K, b.D
-    mod = _native.kernels()
-    st_ptr = _native.stream_ptr()
-    pin_a, pin_b = _Pinned(8 * Tn), _Pinned(8 * Tn)  # one per upload site (see _Pinned)
-    Wf = W.reshape(-1).contiguous()
-    ar_n = None
-    # HAR_TREE_LEVEL_SORT=1 keeps the radix-sort grouping (A/B and oracle for the counting sort)
-    use_group = os.environ.get("HAR_TREE_LEVEL_SORT", "0") != "1"
-    nch = mod.tree_level_group_chunks(N)
-    rows_buf = roww_buf = cnt_ws = None
-    split_bin = torch.zeros(Tn, maxn, dtype=torch.int32, device=dev) if use_group else None
-    bins_rm = b.bins.t().contiguous()  # [N, F] for the histogram gathers (partition keeps [F, N])
-
-    def candidacy(c: torch.Tensor):
-        w = c.sum(-1)
-        imp = T._impurity(c.double(), w.double(), b.impurity)
-        return (imp > 1e-12) & (w >= 2 * b.min_inst), w
-
-    c0, w0 = candidacy(stats[:, 0])
-    host0 = torch.stack([c0.float(), w0.float()]).cpu().numpy()
-    front_t = np.arange(Tn, dtype=np.int64)
-    front_n = np.zeros(Tn, dtype=np.int64)
-    cand = host0[0] > 0
-    wtot = host0[1]
-    for depth in range(D):
-        ct, cn, cw = front_t[cand], front_n[cand], wtot[cand]
-        A = len(ct)
-        if A == 0:
-            break
-        per_tree = np.bincount(ct, minlength=Tn)
-        grouped = use_group and int(per_tree.max()) <= GROUP_MAX_NT and bool(np.all(ct[1:] >= ct[:-1]))
-        tree_lo = np.concatenate([[0], np.cumsum(per_tree)]) if grouped else np.zeros(0, dtype=np.int64)
-        ct_d, cn_d, tr_d, lo_d = pin_a.upload([ct, cn, ct + b.tree_offset, tree_lo], dev)
-        cand_idx = torch.full((Tn, maxn), -1, dtype=torch.int32, device=dev)
-        cand_idx[ct_d, cn_d] = torch.arange(A, dtype=torch.int32, device=dev)
-        if grouped:
-            # stable counting-sort grouping by candidate (tree_level.hip): same order as the sort
-            # below, but only the active rows are written and no key array reaches HBM
-            if rows_buf is None:
-                rows_buf = torch.empty(Tn * N, dtype=torch.int32, device=dev)
-                roww_buf = torch.empty(Tn * N, dtype=torch.float32, device=dev)
-            if cnt_ws is None or cnt_ws.numel() < nch * A:
-                cnt_ws = torch.empty(nch * max(A, 2 * Tn), dtype=torch.int32, device=dev)
-            counts = torch.empty(A, dtype=torch.int32, device=dev)
-            starts = torch.empty(A, dtype=torch.int32, device=dev)
-            lo32 = lo_d.to(torch.int32)
-            mod.tree_level_group(node_of.data_ptr(), cand_idx.data_ptr(), lo32.data_ptr(),
-                                 Wf.data_ptr(), Tn, N, maxn, A, int(per_tree.max()), cnt_ws.data_ptr(),
-                                 counts.data_ptr(), starts.data_ptr(), rows_buf.data_ptr(), roww_buf.data_ptr(),
-                                 st_ptr)
-            rows, row_w = rows_buf, roww_buf
-        else:
-            key = torch.empty(Tn * N, dtype=torch.int32, device=dev)
-            mod.tree_level_keys(node_of.data_ptr(), cand_idx.data_ptr(), Tn, N, maxn, key.data_ptr(), st_ptr)
-            keys, order = torch.sort(key, stable=True)
-            rows = (order % N).to(torch.int32)
-            row_w = Wf[order]
-            if ar_n is None or ar_n.numel() < A + 1:
-                ar_n = torch.arange(max(A + 1, 2 * Tn), dtype=torch.int32, device=dev)
-            bounds = torch.searchsorted(keys, ar_n[:A + 1])
-            counts = (bounds[1:] - bounds[:-1]).to(torch.int32)
-            starts = bounds[:-1].to(torch.int32)
-        if m >= F:
-            feats = torch.arange(F, dtype=torch.int32, device=dev).repeat(A, 1)
-        else:
-            feats = torch.empty(A, m, dtype=torch.int32, device=dev)
-            tr32 = tr_d.to(torch.int32)
-            cn32 = cn_d.to(torch.int32)
-            mod.tree_feature_subsets(b.seed, tr32.data_ptr(), cn32.data_ptr(), A, F, m, feats.data_ptr(), st_ptr)
-        res = T.hist_split_native(b.bins, b.nbins, y32, rows, row_w, starts, counts, feats, K, b.max_bins,
-                                  b.min_inst, b.min_gain, b.impurity,
-                                  allreduce=None if b.owner is not None else b.allreduce, owner=b.owner,
-                                  max_rows=int(cw.max()) if A else 0, check_labels=False, bins_rm=bins_rm)
-        if use_group:
-            res = T.LevelResult(gain=res.gain.contiguous(), feat=res.feat.contiguous(), bin=res.bin.contiguous(),
-                                left=res.left.contiguous(), total=res.total.contiguous())
-            dec = torch.empty(5, A, dtype=torch.float32, device=dev)
-            mod.tree_level_decide(A, res.gain.data_ptr(), res.left.data_ptr(), res.total.data_ptr(), K, b.impurity,
-                                  float(2 * b.min_inst), dec.data_ptr(), st_ptr)
-            h = dec.cpu().numpy()
-            lstat = rstat = None
-        else:
-            do_split = (res.gain > 0) & torch.isfinite(res.gain)
-            lstat = res.left
-            rstat = res.total - lstat
-            cl_ok, wl = candidacy(lstat)
-            cr_ok, wr = candidacy(rstat)
-            h = torch.stack([do_split.float(), cl_ok.float(), cr_ok.float(), wl.float(), wr.float()]).cpu().numpy()
-        ds = h[0] > 0
-        if not ds.any():
-            break
-        st_t, st_n = ct[ds], cn[ds]
-        # children: per tree, consecutive ids (the frontier stays grouped by tree)
-        rank_in_tree = np.arange(len(st_t)) - np.searchsorted(st_t, st_t, side="left")
-        child_l = n_nodes[st_t] + 2 * rank_in_tree
-        n_nodes += 2 * np.bincount(st_t, minlength=Tn)
-        dsi_h = np.nonzero(ds)[0]
-        ti, ni, cl, dsi = pin_b.upload([st_t, st_n, child_l, dsi_h], dev)
-        if use_group:
-            # one launch commits every split and both children's stats; the partition reads the
-            # committed arrays (tree_level.hip)
-            mod.tree_commit_level(len(dsi_h), ti.data_ptr(), ni.data_ptr(), cl.data_ptr(), dsi.data_ptr(),
-                                  res.feat.data_ptr(), res.bin.data_ptr(), res.gain.data_ptr(), res.left.data_ptr(),
-                                  res.total.data_ptr(), K, b.thr_mat.data_ptr(), b.thr_mat.shape[1], maxn,
-                                  feature.data_ptr(), split_bin.data_ptr(), thresh.data_ptr(), left.data_ptr(),
-                                  right.data_ptr(), gains.data_ptr(), stats.data_ptr(), st_ptr)
-            mod.tree_partition_split(node_of.data_ptr(), feature.data_ptr(), split_bin.data_ptr(), left.data_ptr(),
-                                     b.bins.data_ptr(), Tn, N, maxn, st_ptr)
-            front_t = np.repeat(st_t, 2)
-            front_n = np.stack([child_l, child_l + 1], 1).reshape(-1)
-            cand = np.stack([h[1][ds] > 0, h[2][ds] > 0], 1).reshape(-1)
-            wtot = np.stack([h[3][ds], h[4][ds]], 1).reshape(-1)
-            continue
-        bf = res.feat[dsi].long()
-        bb = res.bin[dsi].long()
-        feature[ti, ni] = bf.to(torch.int32)
-        thresh[ti, ni] = b.thr_mat[bf, bb]
-        left[ti, ni] = cl.to(torch.int32)
-        right[ti, ni] = (cl + 1).to(torch.int32)
-        gains[ti, ni] = res.gain[dsi] * res.total[dsi].sum(1)
-        stats[ti, cl] = lstat[dsi]
-        stats[ti, cl + 1] = rstat[dsi]
-        lf = torch.full((Tn, maxn), -1, dtype=torch.int32, device=dev)
-        lb = torch.zeros(Tn, maxn, dtype=torch.int32, device=dev)
-        ll = torch.zeros(Tn, maxn, dtype=torch.int32, device=dev)
-        lf[ti, ni] = bf.to(torch.int32)
-        lb[ti, ni] = bb.to(torch.int32)
-        ll[ti, ni] = cl.to(torch.int32)
-        mod.tree_partition(node_of.data_ptr(), lf.data_ptr(), lb.data_ptr(), ll.data_ptr(), b.bins.data_ptr(), Tn, N,
-                           maxn, st_ptr)
-        front_t = np.repeat(st_t, 2)
-        front_n = np.stack([child_l, child_l + 1], 1).reshape(-1)
-        cand = np.stack([h[1][ds] > 0, h[2][ds] > 0], 1).reshape(-1)
-        wtot = np.stack([h[3][ds], h[4][ds]], 1).reshape(-1)
+# Test hook: when True the level loop groups rows with the stable radix sort of the level keys
+# instead of the counting-sort kernel (the two must grow bit-identical forests).
+FORCE_SORT_GROUPING = False
 
 
 def _levels_device_frontier(b: "ForestBuilder", y32, W, N: int, F: int, m: int, maxn: int, stats, feature, thresh,
-                            left, right, gains, n_nodes, node_of):
+                            left, right, gains, n_nodes, node_of, bad):
     """Device level loop with the frontier resident on the GPU and ONE 16-byte device -> host
     read per level (splits, next candidates, max candidates per tree, max candidate weight).
 
@@ -500,14 +285,24 @@ def _levels_device_frontier(b: "ForestBuilder", y32, W, N: int, F: int, m: int, 
     bins_rm = b.bins.t().contiguous()  # [N, F] for the histogram gathers (partition keeps [F, N])
     nch = mod.tree_level_group_chunks(N)
 
-    w0 = stats[:, 0].sum(-1)
-    imp0 = T._impurity(stats[:, 0].double(), w0.double(), b.impurity)
-    c0 = ((imp0 > 1e-12) & (w0 >= 2 * b.min_inst)).cpu().numpy()
+    # the root class counts and the label check in ONE device -> host read; root candidacy on the
+    # host in fp64 (the device decision kernel's rule: impurity > 1e-12, weight >= 2 minInstances)
+    head = torch.cat([stats[:, 0].reshape(-1), bad.to(torch.float32)]).cpu().numpy()
+    if head[-1] != 0:
+        raise ValueError("labels out of range")
+    root = head[:-1].reshape(Tn, K).astype(np.float64)
+    w0 = root.sum(1)
+    p0 = root / np.maximum(w0, 1e-30)[:, None]
+    if b.impurity == T.GINI:
+        imp0 = 1.0 - (p0 * p0).sum(1)
+    else:
+        imp0 = -(p0 * np.where(p0 > 0, np.log2(np.maximum(p0, 1e-30)), 0.0)).sum(1)
+    c0 = (imp0 > 1e-12) & (w0 >= 2 * b.min_inst)
     ct0 = np.nonzero(c0)[0]
     A = len(ct0)
     if A == 0:
         return
-    max_w = float(w0.cpu().numpy()[c0].max())
+    max_w = float(w0[c0].max())
     ct = torch.from_numpy(ct0.astype(np.int32)).to(dev)
     cn = torch.zeros(A, **i32)
     tlo = torch.from_numpy(np.concatenate([[0], np.cumsum(c0.astype(np.int64))]).astype(np.int32)).to(dev)
@@ -527,7 +322,7 @@ def _levels_device_frontier(b: "ForestBuilder", y32, W, N: int, F: int, m: int, 
         if cnt_ws is None or cnt_ws.numel() < nch * A:
             cnt_ws = torch.empty(nch * max(A, 2 * Tn), **i32)
         counts, starts = torch.empty(A, **i32), torch.empty(A, **i32)
-        if nt_max <= GROUP_MAX_NT:
+        if nt_max <= GROUP_MAX_NT and not FORCE_SORT_GROUPING:
             mod.tree_level_group(node_of.data_ptr(), cand_idx.data_ptr(), tlo.data_ptr(), Wf.data_ptr(), Tn, N,
                                  maxn, A, nt_max, cnt_ws.data_ptr(), counts.data_ptr(), starts.data_ptr(),
                                  rows_buf.data_ptr(), roww_buf.data_ptr(), st)

@@ -286,6 +286,16 @@ PYBIND11_MODULE(_har_native, m) {
           "forest_predict");
   });
 
+  m.def("tree_init", [](uint64_t seed, int tree0, int ntrees, int64_t row0, int64_t n, int bootstrap, u rw, u y, int K,
+                        u W, u node_of, u stats, int64_t stride, u bad, u stream) {
+    check(har_tree_init(seed, tree0, ntrees, row0, n, bootstrap, P<const float>(rw), P<const int32_t>(y), K,
+                        P<float>(W), P<int32_t>(node_of), P<float>(stats), stride, P<int32_t>(bad), S(stream)),
+          "tree_init");
+  });
+  m.def("find_splits_post_sort", [](u sorted, int F, int n, int ns, u out, u stream) {
+    check(har_find_splits_post_sort(P<const float>(sorted), F, n, ns, P<float>(out), S(stream)),
+          "find_splits_post_sort");
+  });
   m.def("poisson_bootstrap", [](uint64_t seed, int tree0, int ntrees, int64_t row0, int64_t n, u out, u stream) {
     check(har_poisson_bootstrap(seed, tree0, ntrees, row0, n, P<uint8_t>(out), S(stream)), "poisson_bootstrap");
   });
@@ -312,7 +322,7 @@ PYBIND11_MODULE(_har_native, m) {
 
   m.def("grad_reduce_adam", [](std::vector<u> src, std::vector<int64_t> start, std::vector<int64_t> len,
                                std::vector<int64_t> lds, std::vector<int> nsl, int64_t n, u G, u param, u mm, u vv,
-                               u pb, float lr, float b1, float b2, float eps, float wd, u step, u done, int mode,
+                               u pb, float lr, float b1, float b2, float eps, float wd, u step, int tick, int mode,
                                u stream) {
     const int k = (int)src.size();
     if ((int)start.size() != k || (int)len.size() != k || (int)lds.size() != k || (int)nsl.size() != k)
@@ -321,7 +331,7 @@ PYBIND11_MODULE(_har_native, m) {
     for (int i = 0; i < k; ++i) sp[i] = P<const float>(src[i]);
     check(har_grad_reduce_adam(k, sp.data(), start.data(), len.data(), lds.data(), nsl.data(), n, P<float>(G),
                                P<float>(param), P<float>(mm), P<float>(vv), P<uint16_t>(pb), lr, b1, b2, eps, wd,
-                               P<int32_t>(step), P<uint32_t>(done), mode, S(stream)),
+                               P<int32_t>(step), tick, mode, S(stream)),
           "grad_reduce_adam");
   });
   m.def("reduce_slabs_multi", [](std::vector<u> slabs, std::vector<int> nsl, std::vector<int64_t> n,
@@ -343,10 +353,10 @@ PYBIND11_MODULE(_har_native, m) {
   m.def("mlp_bwd_fused_slices", &har_mlp_bwd_fused_slices);
   m.def("mlp_fwd_head_variant", &har_mlp_fwd_head_variant);
   m.def("mlp_bwd_fused", [](u dact2, u h1, u X, int K0, u W1, int H, int B, u gw1, u gw0, u gb0, int64_t stride,
-                            u stream) {
+                            u tick, u stream) {
     check(har_mlp_bwd_fused(P<const uint16_t>(dact2), P<const uint16_t>(h1), P<const uint16_t>(X), K0,
                             P<const uint16_t>(W1), H, B, P<float>(gw1), P<float>(gw0), P<float>(gb0), stride,
-                            S(stream)),
+                            P<int32_t>(tick), S(stream)),
           "mlp_bwd_fused");
   });
   m.def("mlp_fwd_head", [](u X, int K0, u W0, u b0, u W1, u b1, int H, u Wo, u bo, u labels, int B, int C,

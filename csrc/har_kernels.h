@@ -44,12 +44,12 @@ int har_softmax_ce_head_blocks(int B);
 // The step counter (*step, device int32) is incremented on the stream before the update
 // (by this call when tick != 0, else by an earlier kernel such as har_reduce_slabs_grouped).
 // Flat-gradient reduction (+ Adam) of the MLP step (mlp.hip): mode bits 1 = reduce the regions' slabs,
-// 2 = store G, 4 = Adam with t = *step + 1 (the last workgroup writes *step = t; `done` is a zeroed
-// device counter).  Regions: sorted, disjoint, 4-aligned [start, start + len), S slabs at src + s * lds.
+// 2 = store G, 4 = Adam with t = *step (tick != 0: *step += 1 first, in its own launch).  Regions:
+// sorted, disjoint, 4-aligned [start, start + len), S slabs at src + s * lds.
 int har_grad_reduce_adam(int nreg, const float* const* src, const int64_t* start, const int64_t* len,
                          const int64_t* lds, const int* S, int64_t n, float* G, float* param, float* m, float* v,
-                         uint16_t* pb, float lr, float b1, float b2, float eps, float wd, int32_t* step,
-                         uint32_t* done, int mode, hipStream_t s);
+                         uint16_t* pb, float lr, float b1, float b2, float eps, float wd, int32_t* step, int tick,
+                         int mode, hipStream_t s);
 int har_adam_step(float* param, const float* grad, const float* slabs, int nslabs, float* m, float* v,
                   uint16_t* param_bf16, int64_t n, float lr, float beta1, float beta2, float eps,
                   float weight_decay, float grad_scale, int32_t* step, int tick, hipStream_t s);
@@ -75,7 +75,8 @@ int har_mlp_fwd_head_grid(int B);
 // relu'(h1), dW0 = dact1^T X, db0 in one pass; per-slice partials at gw1 / gw0 / gb0 + s * slab_stride for
 // s < har_mlp_bwd_fused_slices(B).  har_mlp_fwd_head_variant: 2 = the 8-wave forward (writes db1 too).
 int har_mlp_bwd_fused(const uint16_t* dact2, const uint16_t* h1, const uint16_t* X, int K0, const uint16_t* W1,
-                      int H, int B, float* gw1, float* gw0, float* gb0, int64_t slab_stride, hipStream_t s);
+                      int H, int B, float* gw1, float* gw0, float* gb0, int64_t slab_stride, int32_t* tick,
+                      hipStream_t s);
 int har_mlp_bwd_fused_slices(int B);
 int har_mlp_fwd_head_variant(int H, int B);
 // Serving variant of the same kernel: logits [B][C] fp32 + argmax class [B] int32, nothing else.
@@ -104,6 +105,15 @@ int har_cast_pad_bf16(const float* in, int rows, int cols_in, int ld_in, uint16_
 // ---- randomness (Philox4x32-10 keyed by global row id) ----
 int har_philox_buckets(uint64_t seed, uint32_t stream, int64_t row0, int64_t n, const uint32_t* thr,
                        int nthr, int32_t* out, hipStream_t s);
+// Per-fit init (tree.hip): W [T][N] = Poisson(1) bootstrap (or 1) x optional rw [T][N]; node_of [T][N]
+// = 0 / -1 (zero weight); root class counts added into stats + t * stats_tree_stride; *bad = 1 on a
+// label outside [0, K).
+int har_tree_init(uint64_t seed, int tree0, int ntrees, int64_t row0, int64_t n, int bootstrap, const float* rw,
+                  const int32_t* y, int K, float* W, int32_t* node_of, float* stats, int64_t stats_tree_stride,
+                  int32_t* bad, hipStream_t s);
+// findSplits cut points from the per-feature sorted sample [F][n] (NaN last), n <= 16384, ns <= 63:
+// out [F][ns + 1] = thresholds then their count.
+int har_find_splits_post_sort(const float* sorted, int F, int n, int ns, float* out, hipStream_t s);
 int har_poisson_bootstrap(uint64_t seed, int tree0, int ntrees, int64_t row0, int64_t n, uint8_t* out,
                           hipStream_t s);
 

@@ -171,8 +171,8 @@ __global__ void cast_pad_kernel(const float* __restrict__ in, int rows, int cin,
 // the sum of S slabs (slab s at src + s * lds).  Modes (bit set):
 //   GR_REDUCE  g = sum of the region's slabs (fixed order)    else g = G[i] (already reduced)
 //   GR_STORE   G[i] = g                                         (DP: before the all-reduce)
-//   GR_ADAM    Adam update of param / m / v / bf16 copy with t = *step + 1; the last workgroup to
-//              finish (one device counter) writes *step = t, after every workgroup has read it
+//   GR_ADAM    Adam update of param / m / v / bf16 copy with t = *step (ticked earlier in the step
+//              by the fused backward kernel or adam_tick_kernel: no kernel both ticks and reads it)
 // A workgroup = 16 waves x 64 float4 columns: wave q sums slabs q, q + 16, q + 32, ... (eight loads
 // in flight per step: the 256 per-workgroup slabs of the forward kernel take two steps), the 16
 // partials are added in a fixed tree order -> bitwise reproducible, and N = 1 (GR_REDUCE |
@@ -185,8 +185,7 @@ __global__ __launch_bounds__(1024) void grad_reduce_adam_kernel(GradRegions rg, 
                                                                 float* __restrict__ param, float* __restrict__ m,
                                                                 float* __restrict__ v, bf16_t* __restrict__ pb,
                                                                 float lr, float b1, float b2, float eps, float wd,
-                                                                int32_t* __restrict__ step,
-                                                                uint32_t* __restrict__ done, int mode) {
+                                                                const int32_t* __restrict__ step, int mode) {
   __shared__ float4 part[GR_W][64];
   const int q = threadIdx.x >> 6, k = threadIdx.x & 63;
   const int64_t i4 = (int64_t)blockIdx.x * 64 + k, e = i4 * 4;
@@ -232,7 +231,7 @@ __global__ __launch_bounds__(1024) void grad_reduce_adam_kernel(GradRegions rg, 
     }
     __syncthreads();
   }
-  const int32_t t_int = (mode & GR_ADAM) ? *step + 1 : 0;
+  const int32_t t_int = (mode & GR_ADAM) ? *step : 0;
   if (q == 0 && e < n) {
     float4 g;
     if (mode & GR_REDUCE) {
@@ -264,16 +263,6 @@ __global__ __launch_bounds__(1024) void grad_reduce_adam_kernel(GradRegions rg, 
       reinterpret_cast<float4*>(m)[i4] = mm;
       reinterpret_cast<float4*>(v)[i4] = vv;
       reinterpret_cast<ushort4*>(pb)[i4] = ob;
-    }
-  }
-  if (mode & GR_ADAM) {
-    __syncthreads();  // every thread of this workgroup has read *step
-    if (threadIdx.x == 0) {
-      __threadfence();
-      if (atomicAdd(done, 1u) == gridDim.x - 1) {  // the last workgroup: all others have read *step
-        *step = t_int;
-        *done = 0;
-      }
     }
   }
 }
@@ -327,7 +316,7 @@ extern "C" int har_cast_pad_bf16(const float* in, int rows, int cin, int ldin, u
 extern "C" int har_grad_reduce_adam(int nreg, const float* const* src, const int64_t* start, const int64_t* len,
                                     const int64_t* lds, const int* S, int64_t n, float* G, float* param, float* m,
                                     float* v, uint16_t* pb, float lr, float b1, float b2, float eps, float wd,
-                                    int32_t* step, uint32_t* done, int mode, hipStream_t s) {
+                                    int32_t* step, int tick, int mode, hipStream_t s) {
   if (n % 4 || nreg < 0 || nreg > 8 || ((mode & GR_REDUCE) && nreg == 0)) return -2;
   GradRegions rg{};
   rg.nreg = nreg;
@@ -339,8 +328,9 @@ extern "C" int har_grad_reduce_adam(int nreg, const float* const* src, const int
   }
   const int64_t blocks = (n / 4 + 63) / 64;
   if (blocks == 0) return 0;
+  if (tick) adam_tick_kernel<<<1, 1, 0, s>>>(step);
   grad_reduce_adam_kernel<<<(int)blocks, 64 * GR_W, 0, s>>>(rg, n, G, param, m, v, pb, lr, b1, b2, eps, wd, step,
-                                                            done, mode);
+                                                            mode);
   HAR_CHECK_LAUNCH();
   return 0;
 }

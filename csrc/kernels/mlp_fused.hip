@@ -543,15 +543,16 @@ __global__ __launch_bounds__(512) void mlp_fwd_head_v2_kernel(
         *reinterpret_cast<uint2*>(h1s + (16 * h + c16) * V2_HP + u0 + 16 * t + 4 * g) = v;
       }
     // prefetch the next tile's X rows and labels (into the registers stage 1 just consumed)
-    const int Tn = T + gridDim.x;
+    // unconditional (index clamped to a valid tile): a conditional load merges two paths with
+    // different outstanding-load counts and the compiler then drains vmcnt(0) — including the
+    // previous tile's h1 / dact2 stores — every tile
+    const int Tn = min(T + (int)gridDim.x, ntiles - 1);
     const int yc0 = y[0], yc1 = y[1];
-    if (Tn < ntiles) {
 #pragma unroll
-      for (int h = 0; h < 2; ++h) {
+    for (int h = 0; h < 2; ++h) {
 #pragma unroll
-        for (int kc = 0; kc < K0C; ++kc) xb[h][kc] = load_x<K0, XF>(X, Tn * V2_RT + 16 * h + c16, kc, g, F, ldx);
-        if (!INFER) y[h] = labels[Tn * V2_RT + 16 * h + c16];
-      }
+      for (int kc = 0; kc < K0C; ++kc) xb[h][kc] = load_x<K0, XF>(X, Tn * V2_RT + 16 * h + c16, kc, g, F, ldx);
+      if (!INFER) y[h] = labels[Tn * V2_RT + 16 * h + c16];
     }
     __syncthreads();  // the h1 tile (and the previous tile's dact2 tile) is complete
     if (!INFER) {  // coalesced row stores of h1 (this tile) and dact2 (the previous tile)
@@ -797,8 +798,11 @@ __global__ __launch_bounds__(512) void mlp_bwd_fused_kernel(const bf16_t* __rest
                                                            const bf16_t* __restrict__ X,
                                                            const bf16_t* __restrict__ W1, int B, int S,
                                                            float* __restrict__ gw1, float* __restrict__ gw0,
-                                                           float* __restrict__ gb0, int64_t slab_stride) {
+                                                           float* __restrict__ gb0, int64_t slab_stride,
+                                                           int32_t* __restrict__ tick) {
   using L = BwdLds<K0>;
+  // the training step counter ticks here (one thread, before the reduction kernel reads it for Adam)
+  if (tick && blockIdx.x == 0 && threadIdx.x == 0) *tick += 1;
   constexpr int H = V2_H, KC = H / 32, XP = L::XP, NFW = K0 / 32;
   constexpr int XV = BF_RT * K0 / 8;  // 16-byte vectors of an X tile (512 / 256)
   extern __shared__ __attribute__((aligned(16))) bf16_t lds[];
@@ -1045,16 +1049,16 @@ extern "C" int har_mlp_bwd_fused_slices(int B) { return std::max(1, std::min(64,
 // gw1 / gw0 / gb0 + s * slab_stride (s < har_mlp_bwd_fused_slices(B)).
 extern "C" int har_mlp_bwd_fused(const uint16_t* dact2, const uint16_t* h1, const uint16_t* X, int K0,
                                  const uint16_t* W1, int H, int B, float* gw1, float* gw0, float* gb0,
-                                 int64_t slab_stride, hipStream_t s) {
+                                 int64_t slab_stride, int32_t* tick, hipStream_t s) {
   if (H != V2_H || B <= 0 || B % BF_RT || (K0 != 32 && K0 != 64) || slab_stride < (int64_t)H * H) return -2;
   if (((uintptr_t)dact2 | (uintptr_t)h1 | (uintptr_t)X | (uintptr_t)W1) & 15) return -3;
   const int S = har_mlp_bwd_fused_slices(B);
   if (K0 == 64)
     mlp_bwd_fused_kernel<64><<<S * BF_Q, 512, BwdLds<64>::bytes, s>>>(dact2, h1, X, W1, B, S, gw1, gw0, gb0,
-                                                                      slab_stride);
+                                                                      slab_stride, tick);
   else
     mlp_bwd_fused_kernel<32><<<S * BF_Q, 512, BwdLds<32>::bytes, s>>>(dact2, h1, X, W1, B, S, gw1, gw0, gb0,
-                                                                      slab_stride);
+                                                                      slab_stride, tick);
   HAR_CHECK_LAUNCH();
   return 0;
 }

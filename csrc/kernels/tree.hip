@@ -310,6 +310,117 @@ __global__ __launch_bounds__(256) void poisson_bootstrap_kernel(uint64_t seed, i
   }
 }
 
+// One pass per fit over the (tree, row) slots: bootstrap weight (Poisson(1) from Philox keyed by
+// (seed, global tree, global row), or 1) times an optional row weight -> W [T][N] fp32; node
+// ids [T][N] (0, or -1 where the weight is 0); root class counts written straight into
+// stats[t][0][K] (stats zeroed by the caller).  Labels outside [0, K) set *bad.  The counts are
+// sums of integer-valued weights (< 2^24), so the LDS partials and the one global atomic per
+// (workgroup, class) are exact in any order: the result is deterministic.
+constexpr int INIT_ROWS = 2048;
+__global__ __launch_bounds__(256) void tree_init_kernel(uint64_t seed, int tree0, int64_t row0, int64_t n,
+                                                        int bootstrap, const float* __restrict__ rw,
+                                                        const int32_t* __restrict__ y, int K,
+                                                        float* __restrict__ W, int32_t* __restrict__ node_of,
+                                                        float* __restrict__ stats, int64_t stats_tree_stride,
+                                                        int32_t* __restrict__ bad) {
+  const uint32_t thr[15] = {1580030168u, 3160060337u, 3950075421u, 4213413783u, 4279248373u, 4292415291u,
+                            4294609777u, 4294923276u, 4294962463u, 4294966817u, 4294967252u, 4294967292u,
+                            4294967295u, 4294967295u, 4294967295u};
+  __shared__ float cnt[KMAX];
+  const int t = blockIdx.y;
+  if (threadIdx.x < KMAX) cnt[threadIdx.x] = 0.f;
+  __syncthreads();
+  const int64_t r0 = (int64_t)blockIdx.x * INIT_ROWS, r1 = min(n, r0 + INIT_ROWS);
+  int badl = 0;
+  for (int64_t r = r0 + threadIdx.x; r < r1; r += 256) {
+    float w = 1.f;
+    if (bootstrap) {
+      const uint32_t u = philox_u32(seed, 0x1000u + (uint32_t)(tree0 + t), (uint64_t)(row0 + r));
+      int k = 0;
+      while (k < 15 && u >= thr[k]) ++k;
+      w = (float)k;
+    }
+    if (rw) w *= rw[(int64_t)t * n + r];
+    W[(int64_t)t * n + r] = w;
+    node_of[(int64_t)t * n + r] = w == 0.f ? -1 : 0;
+    const int c = y[r];
+    if (c < 0 || c >= K) badl = 1;
+    else if (w != 0.f) atomicAdd(&cnt[c], w);
+  }
+  if (badl) *bad = 1;
+  __syncthreads();
+  if (threadIdx.x < K && cnt[threadIdx.x] != 0.f) atomicAdd(stats + t * stats_tree_stride + threadIdx.x, cnt[threadIdx.x]);
+}
+
+// findSplits after the sort (ops/tree.py find_thresholds_device): one workgroup per feature of
+// the [F][n] sorted sample (NaN last).  A block-wide scan over the distinct-value starts gives
+// every sorted position its distinct rank (LDS) and compacts the distinct values; then the
+// ns = maxBins - 1 candidate cut points — every midpoint when there are few distinct values,
+// else the fp64 quantile targets t = nvalid (k + 1) / (ns + 1) mapped to the distinct rank of
+// sorted position ceil(t) - 1 — are deduplicated and written in order.  out [F][ns + 1]: the
+// thresholds, then their count (as float): the ONE device -> host copy of findSplits.
+constexpr int FS_MAXN = 16384;
+__global__ __launch_bounds__(256) void find_splits_post_sort_kernel(const float* __restrict__ sorted, int n, int ns,
+                                                                    float* __restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) int fs_smem[];
+  int* drank = fs_smem;                                     // [n]
+  float* U = reinterpret_cast<float*>(fs_smem + n);         // [n] distinct values
+  __shared__ int wsum[4], s_nvalid, s_base;
+  __shared__ int Jk[64];
+  const int f = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const float* s = sorted + (size_t)f * n;
+  if (tid == 0) { s_nvalid = n; s_base = 0; }
+  __syncthreads();
+  for (int i = tid; i < n; i += 256)
+    if (isnan(s[i]) && (i == 0 || !isnan(s[i - 1]))) s_nvalid = i;  // the single NaN start
+  __syncthreads();
+  const int nvalid = s_nvalid;
+  for (int c0 = 0; c0 < n; c0 += 256) {
+    const int i = c0 + tid;
+    const bool nd = i < nvalid && (i == 0 || s[i] != s[i - 1]);
+    const uint64_t mask = __ballot(nd);
+    const int before = __popcll(mask & ((1ull << lane) - 1));
+    if (lane == 0) wsum[wave] = __popcll(mask);
+    __syncthreads();
+    int off = s_base;
+    for (int w = 0; w < wave; ++w) off += wsum[w];
+    const int rank = off + before + (nd ? 1 : 0) - 1;  // distinct index of this sorted position
+    if (i < n) {
+      drank[i] = rank;
+      if (nd) U[rank] = s[i];
+    }
+    __syncthreads();
+    if (tid == 0) s_base += wsum[0] + wsum[1] + wsum[2] + wsum[3];
+    __syncthreads();
+  }
+  const int ndist = s_base;
+  const bool few = ndist - 1 <= ns;
+  if (tid < ns) {
+    int j;
+    if (few) {
+      j = tid;
+    } else {
+      const double tq = (double)nvalid * (double)(tid + 1) / (double)(ns + 1);
+      int64_t q = (int64_t)ceil(tq) - 1;
+      q = q < 0 ? 0 : (q > n - 1 ? n - 1 : q);
+      j = drank[q];
+      j = min(j, max(ndist - 2, 0));
+      j = max(j, 0);
+    }
+    Jk[tid] = j;
+  }
+  __syncthreads();
+  if (wave == 0) {
+    bool keep = lane < ns && ndist > 1;
+    if (keep) keep = few ? lane < ndist - 1 : (lane == 0 || Jk[lane] != Jk[lane - 1]);
+    const uint64_t mask = __ballot(keep);
+    const int pos = __popcll(mask & ((1ull << lane) - 1));
+    float* o = out + (size_t)f * (ns + 1);
+    if (keep) o[pos] = (U[Jk[lane]] + U[Jk[lane] + 1]) / 2.0f;
+    if (lane == 0) o[ns] = (float)__popcll(mask);
+  }
+}
+
 }  // namespace
 
 // bins: feature-major [F][N] (row_major = 0) or row-major [N][F] (row_major = 1: the bytes of one
@@ -356,6 +467,26 @@ extern "C" int har_poisson_bootstrap(uint64_t seed, int tree0, int ntrees, int64
   if (total == 0) return 0;
   int blocks = (int)std::min<int64_t>(4096, (total + 255) / 256);
   poisson_bootstrap_kernel<<<blocks, 256, 0, s>>>(seed, tree0, ntrees, row0, n, out);
+  HAR_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int har_tree_init(uint64_t seed, int tree0, int ntrees, int64_t row0, int64_t n, int bootstrap,
+                             const float* rw, const int32_t* y, int K, float* W, int32_t* node_of, float* stats,
+                             int64_t stats_tree_stride, int32_t* bad, hipStream_t s) {
+  if (K <= 0 || K > KMAX) return -2;
+  if (n == 0 || ntrees == 0) return 0;
+  dim3 grid((unsigned)((n + INIT_ROWS - 1) / INIT_ROWS), (unsigned)ntrees);
+  tree_init_kernel<<<grid, 256, 0, s>>>(seed, tree0, row0, n, bootstrap, rw, y, K, W, node_of, stats,
+                                        stats_tree_stride, bad);
+  HAR_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int har_find_splits_post_sort(const float* sorted, int F, int n, int ns, float* out, hipStream_t s) {
+  if (n <= 0 || n > FS_MAXN || ns <= 0 || ns > 63) return -2;
+  if (F == 0) return 0;
+  find_splits_post_sort_kernel<<<F, 256, (size_t)2 * n * sizeof(int), s>>>(sorted, n, ns, out);
   HAR_CHECK_LAUNCH();
   return 0;
 }

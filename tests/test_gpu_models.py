@@ -272,15 +272,16 @@ def test_level_grouping_equals_sort_path(cuda, monkeypatch):
     histogram kernel the rows in exactly the order of the stable radix sort of the level keys, so
     the two device builders grow bit-identical forests (N not a multiple of the 1024-row chunk,
     deep trees so late levels have thousands of candidates)."""
+    from har.models import tree as tree_mod
     from har.models.tree import RandomForestClassifier
 
     x, y = _blobs(5300, 16, 6, seed=7)
     xc, yc = x.to(cuda), y.to(cuda)
     fits = {}
-    for mode in ("1", "0"):
-        monkeypatch.setenv("HAR_TREE_LEVEL_SORT", mode)
-        fits[mode] = RandomForestClassifier(numTrees=40, maxDepth=12, seed=11).fit_tensors(xc, yc, 6)
-    a, b = fits["1"].arrs, fits["0"].arrs
+    for force_sort in (True, False):
+        monkeypatch.setattr(tree_mod, "FORCE_SORT_GROUPING", force_sort)
+        fits[force_sort] = RandomForestClassifier(numTrees=40, maxDepth=12, seed=11).fit_tensors(xc, yc, 6)
+    a, b = fits[True].arrs, fits[False].arrs
     for name in ("feature", "threshold", "left", "right", "stats"):
         assert torch.equal(getattr(a, name), getattr(b, name)), name
     # the commit kernel sums the node weight sequentially, torch.sum may pair it differently
