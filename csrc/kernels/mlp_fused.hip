@@ -423,14 +423,22 @@ struct LaneSwap {
   __device__ __forceinline__ float x32(float v) const { return __uint_as_float(x32(__float_as_uint(v))); }
 };
 
+// Non-temporal 16-byte store (streaming: no L2 allocation; the consumer is the next kernel)
+__device__ __forceinline__ void nt_store4(uint4* p, uint4 v) {
+  __builtin_nontemporal_store(v.x, reinterpret_cast<uint32_t*>(p));
+  __builtin_nontemporal_store(v.y, reinterpret_cast<uint32_t*>(p) + 1);
+  __builtin_nontemporal_store(v.z, reinterpret_cast<uint32_t*>(p) + 2);
+  __builtin_nontemporal_store(v.w, reinterpret_cast<uint32_t*>(p) + 3);
+}
+
 // Copy a [32][V2_HP] LDS tile to rows r0.. of a [B][256] global matrix: two 16-byte vectors per
 // thread, every row one contiguous 512-byte run (row-per-lane dwordx2 stores are issue-bound)
 __device__ __forceinline__ void v2_store_tile(const bf16_t* tile, bf16_t* __restrict__ dst, int r0, int tid) {
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int v = tid + 512 * i, row = v >> 5, col = (v & 31) * 8;
-    *reinterpret_cast<uint4*>(dst + (size_t)(r0 + row) * V2_H + col) =
-        *reinterpret_cast<const uint4*>(tile + row * V2_HP + col);
+    const uint4 v4 = *reinterpret_cast<const uint4*>(tile + row * V2_HP + col);
+    nt_store4(reinterpret_cast<uint4*>(dst + (size_t)(r0 + row) * V2_H + col), v4);
   }
 }
 
@@ -519,14 +527,12 @@ __global__ __launch_bounds__(512) void mlp_fwd_head_v2_kernel(
   const int ntiles = B / V2_RT;
   int T = blockIdx.x;
   bf16x8_t xb[2][K0C];
-  int y[2] = {0, 0};
   int prev_r0 = -1;
   if (T < ntiles) {
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
 #pragma unroll
       for (int kc = 0; kc < K0C; ++kc) xb[h][kc] = load_x<K0, XF>(X, T * V2_RT + 16 * h + c16, kc, g, F, ldx);
-      if (!INFER) y[h] = labels[T * V2_RT + 16 * h + c16];
     }
   }
   for (; T < ntiles; T += gridDim.x) {
@@ -542,24 +548,40 @@ __global__ __launch_bounds__(512) void mlp_fwd_head_v2_kernel(
         const uint2 v = make_uint2(relu2(pack2(a[0], a[1])), relu2(pack2(a[2], a[3])));
         *reinterpret_cast<uint2*>(h1s + (16 * h + c16) * V2_HP + u0 + 16 * t + 4 * g) = v;
       }
-    // prefetch the next tile's X rows and labels (into the registers stage 1 just consumed)
-    // unconditional (index clamped to a valid tile): a conditional load merges two paths with
-    // different outstanding-load counts and the compiler then drains vmcnt(0) — including the
-    // previous tile's h1 / dact2 stores — every tile
-    const int Tn = min(T + (int)gridDim.x, ntiles - 1);
-    const int yc0 = y[0], yc1 = y[1];
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-#pragma unroll
-      for (int kc = 0; kc < K0C; ++kc) xb[h][kc] = load_x<K0, XF>(X, Tn * V2_RT + 16 * h + c16, kc, g, F, ldx);
-      if (!INFER) y[h] = labels[Tn * V2_RT + 16 * h + c16];
+    // this tile's labels, loaded after stage 1 (whose X reads the compiler waits for) and first
+    // used by the softmax two barriers later (a label prefetched one tile ahead is loop-carried in
+    // a renamed register: the copy at the back edge made every tile wait for its own X prefetch).
+    // The loads are inline asm so the compiler cannot sink them next to their use (it did, and
+    // then drained vmcnt(0) there, X prefetch included); the explicit counted wait before the
+    // softmax (label_wait) retires them while the 2 * K0C X loads and the 4 tile stores issued
+    // after them stay in flight.
+    int yc0 = 0, yc1 = 0;
+    if (!INFER) {
+      const int32_t* lp = labels + r0 + c16;
+      asm volatile("global_load_dword %0, %2, off\n\tglobal_load_dword %1, %2, off offset:64"
+                   : "=&v"(yc0), "=&v"(yc1)
+                   : "v"(lp)
+                   : "memory");
     }
     __syncthreads();  // the h1 tile (and the previous tile's dact2 tile) is complete
     if (!INFER) {  // coalesced row stores of h1 (this tile) and dact2 (the previous tile)
       v2_store_tile(h1s, h1out, r0, tid);
-      if (prev_r0 >= 0) v2_store_tile(dts, dact, prev_r0, tid);
+      // unconditional (same store count every tile, so the waits stay counted): the first tile
+      // writes its not-yet-computed dact2 rows, which the same threads overwrite a tile later
+      v2_store_tile(dts, dact, prev_r0 >= 0 ? prev_r0 : r0, tid);
       prev_r0 = r0;
     }
+    // prefetch the next tile's X rows, after this tile's stores: the loop-top wait for them is then
+    // the same on the first and on every later tile (the youngest ops either way), and it comes a
+    // whole tile later.  Unconditional (index clamped to a valid tile): a conditional load merges
+    // paths with different outstanding-load counts and the compiler then drains vmcnt(0) mid-tile
+    const int Tn = min(T + (int)gridDim.x, ntiles - 1);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+#pragma unroll
+      for (int kc = 0; kc < K0C; ++kc) xb[h][kc] = load_x<K0, XF>(X, Tn * V2_RT + 16 * h + c16, kc, g, F, ldx);
+    }
+
     // ---- stage 2: h2^T = W1 . h1^T (4 independent accumulators) ----
     f32x4_t acc[2][2];
 #pragma unroll
@@ -593,6 +615,10 @@ __global__ __launch_bounds__(512) void mlp_fwd_head_v2_kernel(
       *reinterpret_cast<f32x4_t*>(zs + ((wave * 2 + h) * 64 + lane) * 4) = zp;
     }
     __syncthreads();  // every wave's partial logits are in
+    if (!INFER) {  // the labels (issued first this tile) are in: vmcnt(2 * K0C X loads + 4 stores)
+      if constexpr (K0C == 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    }
     // ---- logits, softmax, CE of half h in wave h < 2 (the other waves only need dz) ----
     if (wave < 2) {
       const int h = wave;
@@ -695,7 +721,8 @@ __global__ __launch_bounds__(512) void mlp_fwd_head_v2_kernel(
   // ---- this wave's units of the workgroup slab: dWout rows 0..15 x units, dbout, loss ----
   float* out = slab + (size_t)blockIdx.x * fwd_slab_width(H);
 #pragma unroll
-  for (int t = 0; t < 2; ++t) *reinterpret_cast<f32x4_t*>(out + (size_t)c16 * H + u0 + 16 * t + 4 * g) = acc5[t];
+  for (int t = 0; t < 2; ++t)
+    nt_store4(reinterpret_cast<uint4*>(out + (size_t)c16 * H + u0 + 16 * t + 4 * g), __builtin_bit_cast(uint4, acc5[t]));
   // db1 of this wave's units: sum over the 16 row lanes of each lane group
 #pragma unroll
   for (int t = 0; t < 2; ++t)
