@@ -578,6 +578,15 @@ class RandomForestClassifier(_TreeEstimatorBase):
         from ..utils.checkpoint import maybe_inject_fault
 
         done = sum(p.feature.shape[0] for p in parts)
+        if total <= 0:  # a tree-parallel rank with an empty slice (more ranks than trees)
+            D = self.maxDepth
+            maxn = int(min(2 ** (D + 1) - 1, 2 * max(int(X.shape[0]), 1) + 1))
+            dev = X.device
+            parts.append(ForestArrays(torch.full((0, maxn), -1, dtype=torch.int32, device=dev),
+                                      torch.zeros(0, maxn, device=dev), torch.zeros(0, maxn, dtype=torch.int32, device=dev),
+                                      torch.zeros(0, maxn, dtype=torch.int32, device=dev),
+                                      torch.zeros(0, maxn, K, device=dev), np.zeros(0, dtype=np.int64), D,
+                                      torch.zeros(0, maxn, device=dev)))
         while done < total:
             maybe_inject_fault(done, rank)
             nt = min(wave, total - done)

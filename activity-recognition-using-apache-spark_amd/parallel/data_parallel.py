@@ -75,10 +75,11 @@ def global_thresholds(X_shard: torch.Tensor, max_bins: int, ctx: DistContext, sa
     P = ctx.world_size
 
     def gather_sizes(v: int):
+        # one all-gather of a [1] tensor per rank, ONE host read of all P sizes
         t = torch.tensor([v], dtype=torch.int64, device=X.device)
-        out = [torch.empty_like(t) for _ in range(P)]
-        dist.all_gather(out, t, group=ctx.group)
-        return [int(o.item()) for o in out]
+        out = torch.empty(P, dtype=torch.int64, device=X.device)
+        dist.all_gather_into_tensor(out, t, group=ctx.group)
+        return out.tolist()
 
     shard_rows = gather_sizes(X.shape[0])
     n_total, row0 = sum(shard_rows), sum(shard_rows[:ctx.rank])
@@ -87,24 +88,39 @@ def global_thresholds(X_shard: torch.Tensor, max_bins: int, ctx: DistContext, sa
     counts = gather_sizes(take.shape[0])
     buf = torch.zeros(max(counts), X.shape[1], dtype=X.dtype, device=X.device)
     buf[:take.shape[0]] = take
-    parts = [torch.empty_like(buf) for _ in range(P)]
-    dist.all_gather(parts, buf, group=ctx.group)
-    sample = torch.cat([p[:c] for p, c in zip(parts, counts)], 0)
+    parts = torch.empty(P * buf.shape[0], X.shape[1], dtype=X.dtype, device=X.device)
+    dist.all_gather_into_tensor(parts, buf, group=ctx.group)
+    parts = parts.view(P, buf.shape[0], X.shape[1])
+    sample = torch.cat([parts[q, :c] for q, c in enumerate(counts)], 0)
     # already sampled: no second draw (n_total <= sample_rows disables it)
     return T.thresholds_for(sample, max_bins, sample_rows=max(sample_rows, sample.shape[0]), seed=seed)
 
 
 class NodeOwner:
     """Owner-computes reduction of per-node tensors ``[A, ...]``: node ``a`` belongs to
-    rank ``a // ceil(A / P)`` (contiguous slices, so a slice is one contiguous buffer)."""
+    rank ``a // ceil(A / P)`` (contiguous slices, so a slice is one contiguous buffer).
+
+    The send / receive buffers are grow-only workspaces kept for the lifetime of the object
+    (one fit): a level reuses them as views instead of allocating and padding fresh tensors.
+    ``stats`` counts the collectives issued and their bytes (bench records)."""
 
     def __init__(self, ctx: DistContext):
         self.ctx = ctx
         self.allreduce = allreduce_sum(ctx) or (lambda t: None)
+        self._ws = {}
+        self.stats = {"reduce_scatter": 0, "all_gather": 0, "bytes": 0}
 
-    def _dev(self, t):
+    def _buf(self, name: str, numel: int, dtype, device) -> torch.Tensor:
+        key = (name, dtype, str(device))
+        t = self._ws.get(key)
+        if t is None or t.numel() < numel:
+            t = torch.empty(max(numel, 2 * (0 if t is None else t.numel())), dtype=dtype, device=device)
+            self._ws[key] = t
+        return t[:numel]
+
+    def _dev(self):
         # RCCL needs device tensors; host tensors are staged through HBM
-        return t if (t.is_cuda or self.ctx.backend != "nccl") else t.to(self.ctx.device)
+        return self.ctx.device if self.ctx.backend == "nccl" else None
 
     def reduce_scatter(self, hist: torch.Tensor):
         P, r = self.ctx.world_size, self.ctx.rank
@@ -114,25 +130,33 @@ class NodeOwner:
         if P == 1:
             return hist, 0, A
         flat = hist.reshape(A, -1)
-        src = torch.zeros(P * S, flat.shape[1], dtype=flat.dtype, device=flat.device)
-        src[:A] = flat
-        src = self._dev(src)
-        out = torch.empty(S, flat.shape[1], dtype=flat.dtype, device=src.device)
+        w = flat.shape[1]
+        dev = self._dev() or flat.device
+        src = self._buf("rs_src", P * S * w, flat.dtype, dev).view(P * S, w)
+        src[:A].copy_(flat)
+        src[A:].zero_()  # only the pad rows of the last owner's slice
+        out = self._buf("rs_out", S * w, flat.dtype, dev).view(S, w)
         dist.reduce_scatter_tensor(out, src, group=self.ctx.group)
-        out = out.to(hist.device)
-        return out.view(S, *hist.shape[1:]), a0, a1
+        self.stats["reduce_scatter"] += 1
+        self.stats["bytes"] += src.numel() * src.element_size()
+        return out.to(hist.device).view(S, *hist.shape[1:]), a0, a1
 
     def all_gather(self, local: torch.Tensor, A: int) -> torch.Tensor:
         P = self.ctx.world_size
         if P == 1:
             return local
         S = max(1, -(-A // P))
-        buf = torch.zeros(S, *local.shape[1:], dtype=local.dtype, device=local.device)
-        buf[: local.shape[0]] = local
-        buf = self._dev(buf)
-        out = torch.empty(P * S, *local.shape[1:], dtype=local.dtype, device=buf.device)
+        inner = tuple(local.shape[1:])
+        w = int(np.prod(inner)) if inner else 1
+        dev = self._dev() or local.device
+        buf = self._buf("ag_src", S * w, local.dtype, dev).view(S, w)
+        buf[: local.shape[0]].copy_(local.reshape(local.shape[0], w))
+        buf[local.shape[0]:].zero_()
+        out = self._buf("ag_out", P * S * w, local.dtype, dev).view(P * S, w)
         dist.all_gather_into_tensor(out, buf, group=self.ctx.group)
-        return out[:A].to(local.device)
+        self.stats["all_gather"] += 1
+        self.stats["bytes"] += out.numel() * out.element_size()
+        return out[:A].view((A,) + inner).to(local.device).clone()
 
 
 def fit_forest_dp(estimator, X_shard, y_shard, num_classes: int, row_offset: int, ctx: DistContext,

@@ -297,7 +297,9 @@ def bench_rf(args, ctx, nine_axis=False):
                     f"({X.shape[1]} features, {K} classes)",
             "config": {"model": name, "global_batch": rows, "seq_len": spec.window, "parallelism": f"dp{world}"},
             "test_accuracy": hdist.mean_over_ranks(ctx, acc), "test_accuracy_data": "held-out synthetic windows",
-            "dtype": "fp32", "histogram_reduction": args.rf_reduce if world > 1 else "none"}
+            "dtype": "fp32", "histogram_reduction": args.rf_reduce if world > 1 else "none",
+            "collectives_per_step": ({k: v / (args.steps + args.warmup) for k, v in owner.stats.items()}
+                                     if owner is not None else None)}
 
 
 def bench_stream(args, ctx):

@@ -65,8 +65,9 @@ def _worker(rank, world, port, out_dir, what):
         from har.parallel.stream import sharded_window_features
 
         S = _stream()
-        cut = 1337  # unequal shards, cut not on a window/stride boundary
-        local = S[:cut] if rank == 0 else S[cut:]
+        # unequal shards, cuts not on a window / stride boundary, every shard longer than the halo
+        cuts = [0] + [int(3001 * (q + 0.37 * (q % 2)) / world) for q in range(1, world)] + [3001]
+        local = S[cuts[rank]:cuts[rank + 1]]
         feats, first = sharded_window_features(ctx, local, WindowFeaturizer(hz=20.0, seconds=10.0, overlap=0.5))
         res = torch.cat([torch.tensor([[float(first)] * feats.shape[1]]), feats])
     elif what == "stream_short":
@@ -83,10 +84,11 @@ def _worker(rank, world, port, out_dir, what):
     else:
         from har.models.mlp import MLPEngine
 
-        eng = MLPEngine([12, 32, 4], 64, "cpu", lr=1e-2, seed=1, process_group=ctx.group, world_size=ctx.world_size)
-        lo = rank * 64
-        for s in range(3):  # global batch 128 = 2 ranks x 64 rows
-            b = slice(s * 128 + lo, s * 128 + lo + 64)
+        per = 128 // world
+        eng = MLPEngine([12, 32, 4], per, "cpu", lr=1e-2, seed=1, process_group=ctx.group, world_size=ctx.world_size)
+        lo = rank * per
+        for s in range(3):  # global batch 128 = world ranks x 128 / world rows
+            b = slice(s * 128 + lo, s * 128 + lo + per)
             eng.train_step(X[b], y[b], 128)
         res = eng.P.clone()
     torch.save(res, os.path.join(out_dir, f"{what}_{rank}.pt"))
@@ -99,7 +101,7 @@ def _run(what, world=2):
     return [torch.load(os.path.join(d, f"{what}_{r}.pt"), weights_only=True) for r in range(world)]
 
 
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_dp_logreg_equals_single(world):
     from har.models.logreg import FitSpec, LogisticRegression
 
@@ -111,7 +113,8 @@ def test_dp_logreg_equals_single(world):
     torch.testing.assert_close(outs[0], torch.stack([m.coefficientMatrix for m in ms]), rtol=1e-3, atol=1e-4)
 
 
-@pytest.mark.parametrize("what,world", [("rf", 2), ("rf", 3), ("rf", 4), ("rf_allreduce", 2)])
+@pytest.mark.parametrize("what,world", [("rf", 2), ("rf", 3), ("rf", 4), ("rf", 8), ("rf_allreduce", 2),
+                                        ("rf_allreduce", 8)])
 def test_dp_forest_equals_single(what, world):
     """Owner-computes (reduce-scatter by node + all-gather of winners; world 3 leaves
     uneven node slices) and all-reduce histogram reductions both equal one process."""
@@ -128,11 +131,13 @@ def test_dp_forest_equals_single(what, world):
     torch.testing.assert_close(outs[0], single.predict_raw(X))
 
 
-def test_dp_mlp_equals_single():
+@pytest.mark.parametrize("world", [2, 8])
+def test_dp_mlp_equals_single(world):
     from har.models.mlp import MLPEngine
 
-    outs = _run("mlp")
-    torch.testing.assert_close(outs[0], outs[1])
+    outs = _run("mlp", world)
+    for o in outs[1:]:
+        torch.testing.assert_close(outs[0], o)
     X, y = _data()
     eng = MLPEngine([12, 32, 4], 128, "cpu", lr=1e-2, seed=1)
     for s in range(3):
@@ -140,14 +145,17 @@ def test_dp_mlp_equals_single():
     torch.testing.assert_close(outs[0], eng.P, rtol=1e-4, atol=1e-5)
 
 
-def test_sharded_stream_halo_equals_single():
+@pytest.mark.parametrize("world", [2, 8])
+def test_sharded_stream_halo_equals_single(world):
     from har.features.window import WindowFeaturizer
 
-    outs = _run("stream")
+    outs = _run("stream", world)
     full = WindowFeaturizer(hz=20.0, seconds=10.0, overlap=0.5).transform(_stream())
     firsts = [int(o[0, 0]) for o in outs]
     got = torch.cat([o[1:] for o in outs])
-    assert firsts[0] == 0 and firsts[1] == outs[0].shape[0] - 1  # contiguous window ids
+    assert firsts[0] == 0
+    for q in range(1, world):  # contiguous window ids across the shards
+        assert firsts[q] == firsts[q - 1] + outs[q - 1].shape[0] - 1
     torch.testing.assert_close(got, full, equal_nan=True)
 
 
@@ -165,8 +173,9 @@ def _main_worker(rank, world, port, out_dir, argv):
     main.main(argv + ["--out-dir", out_dir])
 
 
-def test_main_data_parallel_matches_single(tmp_path, wisdm_csv):
-    """``torchrun main.py`` (2 gloo ranks): every model fit data-parallel on row shards —
+@pytest.mark.parametrize("world", [2, 8])
+def test_main_data_parallel_matches_single(tmp_path, wisdm_csv, world):
+    """``torchrun main.py`` (2 or 8 gloo ranks): every model fit data-parallel on row shards —
     LR (all-reduced objective), DT / RF (owner-computed levels), NaiveBayes (all-reduced
     moments) — gives the single-process metrics; rank 0 alone writes the artefacts."""
     import json
@@ -174,10 +183,10 @@ def test_main_data_parallel_matches_single(tmp_path, wisdm_csv):
     import main
 
     argv = ["--data", wisdm_csv, "--device", "cpu", "--classifiers", "lr,dt,rf,nb"]
-    mp.spawn(_main_worker, args=(2, _free_port(), str(tmp_path / "dp"), argv), nprocs=2, join=True)
+    mp.spawn(_main_worker, args=(world, _free_port(), str(tmp_path / "dp"), argv), nprocs=world, join=True)
     dp = json.loads((tmp_path / "dp" / "metrics.jsonl").read_text().splitlines()[-1])
     single = main.run(main.config_from_args(argv + ["--out-dir", str(tmp_path / "one")]))
-    assert dp["world_size"] == 2 and single["world_size"] == 1
+    assert dp["world_size"] == world and single["world_size"] == 1
     for name in ("lr", "dt", "rf", "nb"):
         a, b = dp["models"][name], single["models"][name]
         tol = 0.0 if name in ("dt", "rf") else 2e-3  # LR / NB: fp32 sums in another order
@@ -186,7 +195,7 @@ def test_main_data_parallel_matches_single(tmp_path, wisdm_csv):
     assert len(rows) == 5  # header + 4 models, written once (rank 0)
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 8])
 def test_tree_parallel_forest_equals_single(world):
     """Tree parallelism: ranks grow disjoint tree-id slices (7 trees over 2 or 3 ranks: uneven)
     over all rows; the all-gathered forest is the single-process forest."""
