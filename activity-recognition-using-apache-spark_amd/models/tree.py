@@ -262,6 +262,9 @@ GROUP_MAX_NT = 4096  # tree_level.hip: per-tree candidates a level grouping keep
 # Test hook: when True the level loop groups rows with the stable radix sort of the level keys
 # instead of the counting-sort kernel (the two must grow bit-identical forests).
 FORCE_SORT_GROUPING = False
+# Test hook: when True a single-device level runs one workgroup per node (hist_split_native)
+# instead of the row-balanced plan (hist_split_planned); both grow the same forest.
+FORCE_NODE_BLOCKS = False
 
 
 def _levels_device_frontier(b: "ForestBuilder", y32, W, N: int, F: int, m: int, maxn: int, stats, feature, thresh,
@@ -341,10 +344,15 @@ def _levels_device_frontier(b: "ForestBuilder", y32, W, N: int, F: int, m: int, 
             feats = torch.empty(A, m, **i32)
             tr = ct + b.tree_offset if b.tree_offset else ct
             mod.tree_feature_subsets(b.seed, tr.data_ptr(), cn.data_ptr(), A, F, m, feats.data_ptr(), st)
-        res = T.hist_split_native(b.bins, b.nbins, y32, rows, row_w, starts, counts, feats, K, b.max_bins,
-                                  b.min_inst, b.min_gain, b.impurity,
-                                  allreduce=None if b.owner is not None else b.allreduce, owner=b.owner,
-                                  max_rows=int(max_w), check_labels=False, bins_rm=bins_rm)
+        if b.owner is None and b.allreduce is None and not FORCE_NODE_BLOCKS:
+            # one device: work items by rows (big nodes chunked), no host sync (ops/tree.py)
+            res = T.hist_split_planned(b.bins, b.nbins, y32, rows, row_w, starts, counts, feats, K, b.max_bins,
+                                       b.min_inst, b.min_gain, b.impurity, rows_bound=Tn * N, bins_rm=bins_rm)
+        else:
+            res = T.hist_split_native(b.bins, b.nbins, y32, rows, row_w, starts, counts, feats, K, b.max_bins,
+                                      b.min_inst, b.min_gain, b.impurity,
+                                      allreduce=None if b.owner is not None else b.allreduce, owner=b.owner,
+                                      max_rows=int(max_w), check_labels=False, bins_rm=bins_rm)
         res = T.LevelResult(gain=res.gain.contiguous(), feat=res.feat.contiguous(), bin=res.bin.contiguous(),
                             left=res.left.contiguous(), total=res.total.contiguous())
         dec = torch.empty(5, A, dtype=torch.float32, device=dev)

@@ -321,6 +321,48 @@ def hist_split_native(bins, nbins_feat, label, rows, row_w, node_start, node_cou
     return _best_chunk(gain, feat, bin_, left, total, A, chunks, K)
 
 
+PLAN_ROWS = 2048  # rows per work item of a load-balanced level (larger nodes are chunked)
+
+
+def hist_split_planned(bins, nbins_feat, label, rows, row_w, node_start, node_count, feats, K, max_bins,
+                       min_instances, min_info_gain, impurity, rows_bound: int, bins_rm=None,
+                       prows: int = PLAN_ROWS) -> LevelResult:
+    """Load-balanced fused histogram + split for one level on one device (no host sync).
+
+    Work is split by ROWS, not by node: a node of <= ``prows`` rows is one work item (fused LDS
+    histogram + split, as ``hist_split_native``); a bigger node becomes ceil(rows / prows) chunk
+    items whose LDS histograms are added into the node's merged slot (integer-valued weights:
+    exact in any order), followed by one split-search pass over the merged big nodes.  Without it a
+    level's time is its largest node's: the deep levels of a forest keep a few nodes of tens of
+    thousands of rows beside thousands of small ones.  ``rows_bound`` bounds the level's total
+    rows (grid sizes are upper bounds; surplus workgroups exit on the device-side counts)."""
+    A, m = feats.shape
+    F, N = bins.shape
+    fc = max(1, min(m, LDS_BUDGET // (max_bins * K * 4)))
+    chunks = (m + fc - 1) // fc
+    dev = bins.device
+    gain = torch.empty(A * chunks, dtype=torch.float32, device=dev)
+    feat = torch.empty(A * chunks, dtype=torch.int32, device=dev)
+    bin_ = torch.empty(A * chunks, dtype=torch.int32, device=dev)
+    left = torch.empty(A * chunks, K, dtype=torch.float32, device=dev)
+    total = torch.empty(A, K, dtype=torch.float32, device=dev)
+    items_ub = A + rows_bound // prows
+    max_big = max(1, min(A, rows_bound // (prows + 1)))
+    plan = torch.empty(4 + (A + 1) + 3 * A + items_ub, dtype=torch.int32, device=dev)
+    slot = m * max_bins * K
+    ghist = torch.empty(max_big * slot, dtype=torch.float32, device=dev)
+    mod, st = _native.kernels(), _native.stream_ptr()
+    mod.tree_plan(node_count.data_ptr(), A, prows, plan.data_ptr(), slot, ghist.data_ptr(), max_big, st)
+    bptr, row_major = (bins_rm.data_ptr(), 1) if bins_rm is not None else (bins.data_ptr(), 0)
+    args = [bptr, N, F, row_major, nbins_feat.data_ptr(), rows.data_ptr(), row_w.data_ptr(), node_start.data_ptr(),
+            node_count.data_ptr(), A, feats.data_ptr(), m, fc, label.data_ptr(), K, max_bins, float(min_instances),
+            float(min_info_gain), impurity, gain.data_ptr(), feat.data_ptr(), bin_.data_ptr(), left.data_ptr(),
+            total.data_ptr()]
+    mod.tree_hist_split_planned(*args, 3, ghist.data_ptr(), plan.data_ptr(), prows, items_ub, st)
+    mod.tree_hist_split_planned(*args, 4, ghist.data_ptr(), plan.data_ptr(), prows, max_big, st)
+    return _best_chunk(gain, feat, bin_, left, total, A, chunks, K)
+
+
 def _best_chunk(gain, feat, bin_, left, total, A, chunks, K) -> LevelResult:
     if chunks == 1:  # every sampled feature in one workgroup: the kernel's winner is the node's
         return LevelResult(gain=gain, feat=feat, bin=bin_, left=left.view(A, K), total=total)

@@ -278,6 +278,25 @@ PYBIND11_MODULE(_har_native, m) {
           "tree_hist_split");
   });
 
+  m.def("tree_plan", [](u counts, int A, int prows, u plan, int64_t slot_elems, u ghist, int max_big, u stream) {
+    check(har_tree_plan(P<const int32_t>(counts), A, prows, P<int32_t>(plan), slot_elems, P<float>(ghist), max_big,
+                        S(stream)),
+          "tree_plan");
+  });
+  m.def("tree_hist_split_planned", [](u bins, int64_t N, int F, int row_major, u nbins, u rows, u row_w, u node_start,
+                                      u node_count, int A, u feats, int m, int fc, u label, int K, int maxbins,
+                                      float min_inst, float min_gain, int impurity, u gain, u feat, u bin, u left,
+                                      u total, int mode, u ghist, u plan, int prows, int bound, u stream) {
+    check(har_tree_hist_split_planned(P<const uint8_t>(bins), N, F, row_major, P<const int32_t>(nbins),
+                                      P<const int32_t>(rows), P<const float>(row_w), P<const int32_t>(node_start),
+                                      P<const int32_t>(node_count), A, P<const int32_t>(feats), m, fc,
+                                      P<const int32_t>(label), K, maxbins, min_inst, min_gain, impurity,
+                                      P<float>(gain), P<int32_t>(feat), P<int32_t>(bin), P<float>(left),
+                                      P<float>(total), mode, P<float>(ghist), 1, P<const int32_t>(plan), prows, bound,
+                                      S(stream)),
+          "tree_hist_split_planned");
+  });
+
   m.def("forest_predict", [](u X, int64_t n, int F, int ld, u feat, u thr, u left, u right, u leaf, int T, int maxn,
                              int K, int max_depth, int normalize, u out, u stream) {
     check(har_forest_predict(P<const float>(X), n, F, ld, P<const int32_t>(feat), P<const float>(thr),

@@ -242,6 +242,20 @@ int har_tree_hist_split(const uint8_t* bins, int64_t N, int F, int row_major, co
                         float min_inst, float min_gain, int impurity, float* out_gain, int32_t* out_feat,
                         int32_t* out_bin, float* out_left, float* out_total, int mode, float* ghist,
                         int row_chunks, hipStream_t s);
+// Load-balanced level (tree.hip): har_tree_plan builds the work plan from the node row counts
+// (nodes of > prows rows become ceil(count / prows) chunk items with a merged-histogram slot, zeroed
+// here for at most max_big slots of slot_elems floats); then har_tree_hist_split_planned mode 3
+// (grid.y = an upper bound of the items: fused small nodes + chunk histograms) and mode 4 (grid.y
+// = max_big: split search of the merged big nodes).
+int har_tree_plan(const int32_t* counts, int A, int prows, int32_t* plan, int64_t slot_elems, float* ghist,
+                  int max_big, hipStream_t s);
+int har_tree_hist_split_planned(const uint8_t* bins, int64_t N, int F, int row_major, const int32_t* nbins_feat,
+                                const int32_t* rows, const float* row_w, const int32_t* node_start,
+                                const int32_t* node_count, int A, const int32_t* feats, int m, int fc,
+                                const int32_t* label, int K, int maxbins, float min_inst, float min_gain, int impurity,
+                                float* out_gain, int32_t* out_feat, int32_t* out_bin, float* out_left,
+                                float* out_total, int mode, float* ghist, int row_chunks, const int32_t* plan,
+                                int prows, int bound, hipStream_t s);
 // Sum over trees of (normalized) leaf statistics; trees as SoA [T][maxn] arrays, feature < 0 = leaf.
 // Level bookkeeping of the forest builder (tree_level.hip): Floyd feature subsets per (tree, node)
 // (bit-identical to har/ops/rng.py), per-(tree,row) candidate keys, and the row -> child partition.

@@ -23,17 +23,93 @@ constexpr int KMAX = 32;
 #define HIST_UNROLL 4
 #endif
 
+// Split search of TWO feature slots per wave (maxBins <= 32): lanes 0..31 hold the bins of slot
+// 2p, lanes 32..63 those of slot 2p + 1.  KC class prefix sums at a time advance together through
+// ONE 5-step scan over the 32-lane halves (independent shuffles pipeline), instead of a dependent
+// 6-step 64-lane scan per class and slot.  The per-lane gain arithmetic (fp64, classes summed in
+// order) and the lowest-index tie rule are those of the one-slot-per-wave search, so the winner
+// is bit for bit the same.
+template <int KC>
+__device__ __forceinline__ void split_search_pairs(const float* hist, const int* fid, const int32_t* nbins_feat,
+                                                   int f_n, int maxbins, int K, float min_inst, int impurity,
+                                                   int wave, int nwaves, int lane, double& best_g, int& best_i) {
+  const int half = lane >> 5, bl = lane & 31;
+  for (int fp = wave; 2 * fp < f_n; fp += nwaves) {
+    const int fs = 2 * fp + half;
+    const bool fv = fs < f_n;
+    const int nb = fv ? nbins_feat[fid[fs]] : 0;
+    const int src = (lane & 32) + max(nb - 1, 0);
+    double wl = 0.0, wt = 0.0, ql = 0.0, qr = 0.0, qt = 0.0;
+    // classes in groups of KC (registers), accumulated in class order
+    for (int k0 = 0; k0 < K; k0 += KC) {
+      float c[KC];
+#pragma unroll
+      for (int k = 0; k < KC; ++k)
+        c[k] = (k0 + k < K && bl < nb && bl < maxbins) ? hist[(fs * maxbins + bl) * K + k0 + k] : 0.f;
+#pragma unroll
+      for (int o = 1; o < 32; o <<= 1) {
+#pragma unroll
+        for (int k = 0; k < KC; ++k) {
+          const float u = __shfl_up(c[k], o, 32);
+          if (bl >= o) c[k] += u;
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < KC; ++k) {
+        const float tf = __shfl(c[k], src, 64);
+        if (k0 + k < K) {
+          const double v = (double)c[k], t = (double)tf, r = t - v;
+          wl += v;
+          wt += t;
+          if (impurity == 0) {
+            ql += v * v; qr += r * r; qt += t * t;
+          } else {
+            ql += v > 0 ? v * log2(v) : 0.0;
+            qr += r > 0 ? r * log2(r) : 0.0;
+            qt += t > 0 ? t * log2(t) : 0.0;
+          }
+        }
+      }
+    }
+    const double wr = wt - wl;
+    double g = -INFINITY;
+    if (fv && bl < nb - 1 && wl >= min_inst && wr >= min_inst && wt > 0) {
+      double ip, il, ir;
+      if (impurity == 0) {
+        ip = 1.0 - qt / (wt * wt); il = 1.0 - ql / (wl * wl); ir = 1.0 - qr / (wr * wr);
+      } else {
+        ip = log2(wt) - qt / wt; il = log2(wl) - ql / wl; ir = log2(wr) - qr / wr;
+      }
+      g = ip - (wl / wt) * il - (wr / wt) * ir;
+    }
+    int idx = fs * maxbins + bl;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const double og = __shfl_xor(g, o, 64);
+      const int oi = __shfl_xor(idx, o, 64);
+      if (og > g || (og == g && oi < idx)) { g = og; idx = oi; }
+    }
+    if (g > best_g || (g == best_g && idx < best_i)) { best_g = g; best_i = idx; }
+  }
+}
+
 __global__ __launch_bounds__(256) void tree_hist_split_kernel(
     const uint8_t* __restrict__ bins, int64_t fstride, int64_t rstride, const int32_t* __restrict__ nbins_feat,
     const int32_t* __restrict__ rows, const float* __restrict__ row_w, const int32_t* __restrict__ node_start,
     const int32_t* __restrict__ node_count, const int32_t* __restrict__ feats, int m, int fc,
     const int32_t* __restrict__ label, int K, int maxbins, float min_inst, float min_gain, int impurity,
     float* __restrict__ out_gain, int32_t* __restrict__ out_feat, int32_t* __restrict__ out_bin,
-    float* __restrict__ out_left, float* __restrict__ out_total, int mode, float* __restrict__ ghist) {
+    float* __restrict__ out_left, float* __restrict__ out_total, int mode, float* __restrict__ ghist,
+    const int32_t* __restrict__ plan, int prows) {
   // mode 0: fused histogram + split; 1: histogram only -> ghist [A][m][maxbins][K] (data parallel:
-  // summed across ranks by RCCL); 2: split search from a (reduced) ghist
+  // summed across ranks by RCCL); 2: split search from a (reduced) ghist.
+  // Planned (load-balanced) level, plan = tree_plan_kernel's output (see there):
+  // mode 3: work item blockIdx.y: a node of <= prows rows -> fused histogram + split (as mode 0);
+  //         one prows-row chunk of a larger node -> its histogram added into that node's ghist slot
+  // mode 4: blockIdx.y = big-node slot: split search from its merged ghist (as mode 2)
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  const int a = blockIdx.y, c = blockIdx.x, chunks = gridDim.x;
+  const int c = blockIdx.x, chunks = gridDim.x;
+  int a = blockIdx.y, gslot = blockIdx.y;
   const int f_lo = c * fc;
   const int f_n = min(fc, m - f_lo);
   float* hist = smem;                                          // [fc][maxbins][K]
@@ -41,13 +117,41 @@ __global__ __launch_bounds__(256) void tree_hist_split_kernel(
   __shared__ double red_gain[4];
   __shared__ int red_idx[4];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  // grid.z > 1 (histogram-only mode): the node's rows are split over gridDim.z workgroups
-  const int cnt_all = node_count[a];
-  const int per_z = (cnt_all + gridDim.z - 1) / gridDim.z;
-  const int zb = min(cnt_all, (int)blockIdx.z * per_z);
-  const int start = node_start[a] + zb, cnt = min(cnt_all, zb + per_z) - zb;
+  int start, cnt;
+  if (mode == 3 || mode == 4) {
+    const int A = plan[2];
+    const int32_t* item_start = plan + 4;            // [A + 1]
+    const int32_t* big_rank = item_start + A + 1;    // [A]  (-1: not big)
+    const int32_t* big_list = big_rank + A;          // [A]
+    const int32_t* item_node = big_list + A;         // [items]
+    if (mode == 3) {
+      if ((int)blockIdx.y >= plan[0]) return;        // beyond this level's work items
+      a = item_node[blockIdx.y];
+      gslot = big_rank[a];
+      const int z = blockIdx.y - item_start[a];
+      const int cnt_all = node_count[a];
+      start = node_start[a] + z * prows;
+      cnt = gslot < 0 ? cnt_all : min(prows, cnt_all - z * prows);
+      if (gslot >= 0) mode = 1;                      // a chunk of a big node: histogram only
+      else mode = 0;
+    } else {
+      if ((int)blockIdx.y >= plan[1]) return;        // beyond this level's big nodes
+      a = big_list[blockIdx.y];
+      mode = 2;
+      start = 0;
+      cnt = 0;
+    }
+  } else {
+    // grid.z > 1 (histogram-only mode): the node's rows are split over gridDim.z workgroups
+    const int cnt_all = node_count[a];
+    const int per_z = (cnt_all + gridDim.z - 1) / gridDim.z;
+    const int zb = min(cnt_all, (int)blockIdx.z * per_z);
+    start = node_start[a] + zb;
+    cnt = min(cnt_all, zb + per_z) - zb;
+  }
+  const bool merge = (gridDim.z > 1) || (plan != nullptr);  // mode 1 adds into a zeroed ghist
 
-  float* gh = ghist ? ghist + ((size_t)a * m + f_lo) * maxbins * K : nullptr;
+  float* gh = ghist ? ghist + ((size_t)gslot * m + f_lo) * maxbins * K : nullptr;
   for (int i = tid; i < f_n * maxbins * K; i += blockDim.x) hist[i] = (mode == 2) ? gh[i] : 0.f;
   for (int i = tid; i < f_n; i += blockDim.x) fid[i] = feats[(size_t)a * m + f_lo + i];
   __syncthreads();
@@ -120,7 +224,7 @@ __global__ __launch_bounds__(256) void tree_hist_split_kernel(
   }
   __syncthreads();
   if (mode == 1) {
-    if (gridDim.z == 1) {
+    if (!merge) {
       for (int i = tid; i < f_n * maxbins * K; i += blockDim.x) gh[i] = hist[i];
     } else {  // row-split node: merge into the zeroed global histogram (integer-valued sums: exact)
       for (int i = tid; i < f_n * maxbins * K; i += blockDim.x)
@@ -135,7 +239,12 @@ __global__ __launch_bounds__(256) void tree_hist_split_kernel(
   // sum c log2 c (imp = log2 w - sum c log2 c / w), plus the weights.
   double best_g = -INFINITY;
   int best_i = 0x7fffffff;
-  for (int fs = wave; fs < f_n; fs += (int)(blockDim.x >> 6)) {
+  const int nwaves = (int)(blockDim.x >> 6);
+  const bool pairs = maxbins <= 32;
+  if (pairs)
+    split_search_pairs<8>(hist, fid, nbins_feat, f_n, maxbins, K, min_inst, impurity, wave, nwaves, lane, best_g,
+                          best_i);
+  for (int fs = wave; !pairs && fs < f_n; fs += nwaves) {
     const int nb = nbins_feat[fid[fs]];
     double wl = 0.0, wt = 0.0, ql = 0.0, qr = 0.0, qt = 0.0;
     for (int k = 0; k < K; ++k) {
@@ -184,27 +293,34 @@ __global__ __launch_bounds__(256) void tree_hist_split_kernel(
   }
   if (lane == 0) { red_gain[wave] = best_g; red_idx[wave] = best_i; }
   __syncthreads();
-  if (tid == 0) {
+  if (wave == 0) {
+    // every lane reads the four wave winners (LDS broadcast); lanes = bins for the class sums:
+    // the left child's counts (bins <= b of the winning feature) and the node totals are wave
+    // reductions instead of one thread's 2 x K x maxbins serial LDS reads (integer-valued
+    // weights: the sums are exact in any order)
     double g = red_gain[0];
     int idx = red_idx[0];
     for (int w = 1; w < (int)(blockDim.x >> 6); ++w)
       if (red_gain[w] > g || (red_gain[w] == g && red_idx[w] < idx)) { g = red_gain[w]; idx = red_idx[w]; }
     const size_t o = (size_t)a * chunks + c;
     const bool ok = isfinite(g) && g >= (double)min_gain;
-    out_gain[o] = ok ? (float)g : -INFINITY;
     const int fs = ok ? idx / maxbins : 0, b = ok ? idx % maxbins : 0;
-    out_feat[o] = fid[fs];
-    out_bin[o] = b;
-    for (int k = 0; k < K; ++k) {
-      float s = 0.f;
-      for (int bb = 0; bb <= b; ++bb) s += hist[(fs * maxbins + bb) * K + k];
-      out_left[o * K + k] = ok ? s : 0.f;
+    if (lane == 0) {
+      out_gain[o] = ok ? (float)g : -INFINITY;
+      out_feat[o] = fid[fs];
+      out_bin[o] = b;
     }
-    if (c == 0) {
-      for (int k = 0; k < K; ++k) {
-        float s = 0.f;
-        for (int bb = 0; bb < maxbins; ++bb) s += hist[bb * K + k];
-        out_total[(size_t)a * K + k] = s;
+    for (int k = 0; k < K; ++k) {
+      float vl = (ok && lane <= b) ? hist[(fs * maxbins + lane) * K + k] : 0.f;
+      float vt = (c == 0 && lane < maxbins) ? hist[lane * K + k] : 0.f;
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) {
+        vl += __shfl_xor(vl, off, 64);
+        vt += __shfl_xor(vt, off, 64);
+      }
+      if (lane == 0) {
+        out_left[o * K + k] = vl;
+        if (c == 0) out_total[(size_t)a * K + k] = vt;
       }
     }
   }
@@ -421,6 +537,70 @@ __global__ __launch_bounds__(256) void find_splits_post_sort_kernel(const float*
   }
 }
 
+// Load-balanced level plan (one workgroup): node a is one work item when it has <= prows rows,
+// else ceil(count / prows) chunk items and a slot in the merged-histogram buffer.  plan layout
+// (int32): [0] items, [1] big nodes, [2] A, [3] unused, item_start [A + 1], big_rank [A] (-1 = not
+// big), big_list [A], item_node [items].  Block-wide scans over A in 1024-node steps.
+__global__ __launch_bounds__(1024) void tree_plan_kernel(const int32_t* __restrict__ counts, int A, int prows,
+                                                         int32_t* __restrict__ plan) {
+  __shared__ int wsum_i[16], wsum_b[16];
+  __shared__ int base_i, base_b;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  int32_t* item_start = plan + 4;
+  int32_t* big_rank = item_start + A + 1;
+  int32_t* big_list = big_rank + A;
+  int32_t* item_node = big_list + A;
+  if (tid == 0) { base_i = 0; base_b = 0; }
+  __syncthreads();
+  int cnt_next = tid < A ? counts[tid] : 0;  // counts are prefetched one step ahead
+  for (int a0 = 0; a0 < A; a0 += 1024) {
+    const int a = a0 + tid;
+    const int cnt = cnt_next;
+    cnt_next = a + 1024 < A ? counts[a + 1024] : 0;
+    const bool big = a < A && cnt > prows;
+    const int zc = a < A ? (big ? (cnt + prows - 1) / prows : 1) : 0;
+    // inclusive wave scans (shuffles), then across the 16 waves through LDS
+    int si = zc, sb = big ? 1 : 0;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int ui = __shfl_up(si, o, 64), ub = __shfl_up(sb, o, 64);
+      if (lane >= o) { si += ui; sb += ub; }
+    }
+    if (lane == 63) { wsum_i[wave] = si; wsum_b[wave] = sb; }
+    __syncthreads();
+    int oi = base_i, ob = base_b;
+    for (int w = 0; w < wave; ++w) { oi += wsum_i[w]; ob += wsum_b[w]; }
+    const int first = oi + si - zc, rank = ob + sb - (big ? 1 : 0);
+    if (a < A) {
+      item_start[a] = first;
+      big_rank[a] = big ? rank : -1;
+      if (big) big_list[rank] = a;
+      for (int z = 0; z < zc; ++z) item_node[first + z] = a;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      for (int w = 0; w < 16; ++w) { base_i += wsum_i[w]; base_b += wsum_b[w]; }
+    }
+    __syncthreads();
+  }
+  if (tid == 0) {
+    item_start[A] = base_i;
+    plan[0] = base_i;
+    plan[1] = base_b;
+    plan[2] = A;
+    plan[3] = 0;
+  }
+}
+
+// Zero the merged-histogram slots of this level's big nodes only (grid = an upper bound; the
+// real count is read from the plan).
+__global__ __launch_bounds__(256) void tree_plan_zero_kernel(const int32_t* __restrict__ plan, int64_t slot_elems,
+                                                             float* __restrict__ ghist) {
+  const int64_t n = (int64_t)plan[1] * slot_elems;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    ghist[i] = 0.f;
+}
+
 }  // namespace
 
 // bins: feature-major [F][N] (row_major = 0) or row-major [N][F] (row_major = 1: the bytes of one
@@ -432,18 +612,35 @@ extern "C" int har_tree_hist_split(const uint8_t* bins, int64_t N, int F, int ro
                                    int impurity, float* out_gain, int32_t* out_feat, int32_t* out_bin,
                                    float* out_left, float* out_total, int mode, float* ghist, int row_chunks,
                                    hipStream_t s) {
+  return har_tree_hist_split_planned(bins, N, F, row_major, nbins_feat, rows, row_w, node_start, node_count, A, feats,
+                                     m, fc, label, K, maxbins, min_inst, min_gain, impurity, out_gain, out_feat,
+                                     out_bin, out_left, out_total, mode, ghist, row_chunks, nullptr, 0, 0, s);
+}
+
+// mode 3 / 4 (plan != nullptr): grid.y = `bound` (items for mode 3, big-node slots for mode 4)
+extern "C" int har_tree_hist_split_planned(const uint8_t* bins, int64_t N, int F, int row_major,
+                                           const int32_t* nbins_feat, const int32_t* rows, const float* row_w,
+                                           const int32_t* node_start, const int32_t* node_count, int A,
+                                           const int32_t* feats, int m, int fc, const int32_t* label, int K,
+                                           int maxbins, float min_inst, float min_gain, int impurity,
+                                           float* out_gain, int32_t* out_feat, int32_t* out_bin, float* out_left,
+                                           float* out_total, int mode, float* ghist, int row_chunks,
+                                           const int32_t* plan, int prows, int bound, hipStream_t s) {
   if (K > KMAX || maxbins > 64 || fc <= 0 || m <= 0) return -2;
   if (mode != 0 && !ghist) return -4;
+  if ((mode == 3 || mode == 4) && (!plan || prows <= 0)) return -6;
   if (A == 0) return 0;
   const int chunks = (m + fc - 1) / fc;
   const size_t lds = (size_t)fc * maxbins * K * sizeof(float) + (size_t)fc * sizeof(int);
   if (lds > 150 * 1024) return -3;
   if (row_chunks > 1 && mode != 1) return -5;
-  dim3 grid(chunks, A, row_chunks > 1 ? row_chunks : 1);
+  if ((mode == 3 || mode == 4) && bound <= 0) return 0;
+  dim3 grid(chunks, (mode == 3 || mode == 4) ? bound : A, row_chunks > 1 ? row_chunks : 1);
   const int64_t fstride = row_major ? 1 : N, rstride = row_major ? F : 1;
   tree_hist_split_kernel<<<grid, 256, lds, s>>>(bins, fstride, rstride, nbins_feat, rows, row_w, node_start, node_count, feats, m,
                                                 fc, label, K, maxbins, min_inst, min_gain, impurity, out_gain,
-                                                out_feat, out_bin, out_left, out_total, mode, ghist);
+                                                out_feat, out_bin, out_left, out_total, mode, ghist,
+                                                (mode == 3 || mode == 4) ? plan : nullptr, prows);
   HAR_CHECK_LAUNCH();
   return 0;
 }
@@ -488,5 +685,19 @@ extern "C" int har_find_splits_post_sort(const float* sorted, int F, int n, int 
   if (F == 0) return 0;
   find_splits_post_sort_kernel<<<F, 256, (size_t)2 * n * sizeof(int), s>>>(sorted, n, ns, out);
   HAR_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int har_tree_plan(const int32_t* counts, int A, int prows, int32_t* plan, int64_t slot_elems,
+                             float* ghist, int max_big, hipStream_t s) {
+  if (A <= 0 || prows <= 0) return -2;
+  tree_plan_kernel<<<1, 1024, 0, s>>>(counts, A, prows, plan);
+  HAR_CHECK_LAUNCH();
+  if (ghist && max_big > 0) {
+    const int64_t n = (int64_t)max_big * slot_elems;
+    const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(4096, (n + 255) / 256));
+    tree_plan_zero_kernel<<<blocks, 256, 0, s>>>(plan, slot_elems, ghist);
+    HAR_CHECK_LAUNCH();
+  }
   return 0;
 }

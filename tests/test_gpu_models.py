@@ -286,3 +286,21 @@ def test_level_grouping_equals_sort_path(cuda, monkeypatch):
         assert torch.equal(getattr(a, name), getattr(b, name)), name
     # the commit kernel sums the node weight sequentially, torch.sum may pair it differently
     torch.testing.assert_close(a.gain, b.gain)
+
+
+def test_planned_levels_equal_node_blocks(cuda, monkeypatch):
+    """Row-balanced levels (big nodes split into 2048-row chunk items whose LDS histograms merge
+    into a slot, then a split pass over the merged nodes) grow bit-identically the forest of one
+    workgroup per node: integer-valued weights make the merged histograms exact."""
+    from har.models import tree as tree_mod
+    from har.models.tree import RandomForestClassifier
+
+    x, y = _blobs(9000, 20, 6, seed=9)
+    xc, yc = x.to(cuda), y.to(cuda)
+    fits = {}
+    for node_blocks in (True, False):
+        monkeypatch.setattr(tree_mod, "FORCE_NODE_BLOCKS", node_blocks)
+        fits[node_blocks] = RandomForestClassifier(numTrees=30, maxDepth=9, seed=3).fit_tensors(xc, yc, 6)
+    a, b = fits[True].arrs, fits[False].arrs
+    for name in ("feature", "threshold", "left", "right", "stats", "gain"):
+        assert torch.equal(getattr(a, name), getattr(b, name)), name
