@@ -178,10 +178,33 @@ class ClassificationModel(Model, ClassifierParams):
         s = raw.sum(dim=1, keepdim=True)
         return torch.where(s > 0, raw / s.clamp_min(1e-300), torch.full_like(raw, 1.0 / raw.shape[1]))
 
+    # Spark ProbabilisticClassificationModel.thresholds: the class with the largest p / t wins; a
+    # zero threshold makes its class win wherever its probability is positive.  None = argmax(p).
+    thresholds = None
+
+    def setThresholds(self, value):
+        if value is not None:
+            t = [float(v) for v in value]
+            if any(v < 0 for v in t) or sum(1 for v in t if v == 0) > 1:
+                raise ValueError("thresholds must be >= 0 with at most one zero")
+            value = t
+        self.thresholds = value
+        return self
+
+    def _predict_from_probability(self, prob: torch.Tensor) -> torch.Tensor:
+        if self.thresholds is None:
+            return torch.argmax(prob, dim=1)
+        t = torch.as_tensor(self.thresholds, dtype=prob.dtype, device=prob.device)
+        if t.numel() != prob.shape[1]:
+            raise ValueError(f"{t.numel()} thresholds for {prob.shape[1]} classes")
+        scaled = torch.where(t > 0, prob / t.clamp_min(1e-300),
+                             torch.where(prob > 0, torch.full_like(prob, float("inf")), torch.zeros_like(prob)))
+        return torch.argmax(scaled, dim=1)
+
     def predict_all(self, X: torch.Tensor):
         raw = self.predict_raw(X)
         prob = self.raw_to_probability(raw)
-        pred = torch.argmax(prob, dim=1)
+        pred = self._predict_from_probability(prob)
         return raw, prob, pred
 
     def predict(self, X: torch.Tensor) -> torch.Tensor:

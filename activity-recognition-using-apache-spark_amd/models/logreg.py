@@ -134,13 +134,21 @@ class LogisticRegressionModel(ClassificationModel):
 
 class LogisticRegression(Estimator, ClassifierParams):
     _param_names = ("maxIter", "regParam", "elasticNetParam", "tol", "fitIntercept", "standardization", "family",
-                    "featuresCol", "labelCol", "weightCol", "device", "lineSearchTrials")
+                    "featuresCol", "labelCol", "weightCol", "device", "lineSearchTrials", "threshold", "thresholds",
+                    "checkpointDir")
 
     def __init__(self, featuresCol="features", labelCol="label", maxIter: int = 100, regParam: float = 0.0,
                  elasticNetParam: float = 0.0, tol: float = 1e-6, fitIntercept: bool = True,
                  standardization: bool = True, family: str = "auto", weightCol: Optional[str] = None,
-                 device=None, lineSearchTrials: int = 4):
+                 device=None, lineSearchTrials: int = 4, threshold: float = 0.5,
+                 thresholds: Optional[Sequence[float]] = None, checkpointDir: Optional[str] = None):
         super().__init__(new_uid("LogisticRegression"))
+        # Spark: binary ``threshold`` t == thresholds [1 - t, t]; ``thresholds`` (any K) wins if set
+        self.threshold, self.thresholds = threshold, thresholds
+        # fit-level checkpoint: a finished batch of fits is saved (coefficients, intercepts,
+        # summaries) under a fingerprint of its parameters and data; a rerun with the same
+        # fingerprint (a restarted job) resumes by loading it instead of solving again
+        self.checkpointDir = checkpointDir
         self.featuresCol, self.labelCol = featuresCol, labelCol
         self.maxIter, self.regParam, self.elasticNetParam = maxIter, regParam, elasticNetParam
         self.tol, self.fitIntercept, self.standardization = tol, fitIntercept, standardization
@@ -161,6 +169,13 @@ class LogisticRegression(Estimator, ClassifierParams):
                                                                   self.elasticNetParam)], num_classes,
                               allreduce=dp_allreduce())[0]
         model.uid = self.uid
+        return model
+
+    def _apply_thresholds(self, model: "LogisticRegressionModel"):
+        if self.thresholds is not None:
+            model.setThresholds(self.thresholds)
+        elif model.binomial and self.threshold != 0.5:
+            model.setThresholds([1.0 - float(self.threshold), float(self.threshold)])
         return model
 
     def _setup(self, hm: HybridMatrix, y: torch.Tensor, specs: Sequence[FitSpec], K: int, allreduce):
@@ -229,6 +244,19 @@ class LogisticRegression(Estimator, ClassifierParams):
         dev = hm.device
         F = hm.n_features
         K = int(num_classes or int(y.max()) + 1)
+        ckpt = fp = None
+        if self.checkpointDir:
+            from ..utils.checkpoint import Checkpointer
+
+            ckpt = Checkpointer(self.checkpointDir)
+            fp = {"rows": int(hm.n_rows), "features": int(F), "classes": K, "maxIter": self.maxIter,
+                  "tol": self.tol, "fitIntercept": self.fitIntercept, "standardization": self.standardization,
+                  "family": self.family, "lineSearchTrials": self.lineSearchTrials,
+                  "specs": [[s.regParam, s.elasticNetParam, s.row_weight is None] for s in specs],
+                  "labels_sum": int(y.long().sum()), "world": 0 if allreduce is None else 1}
+            last = ckpt.latest(fingerprint=fp)
+            if last is not None:
+                return self._models_from_state(last[0], last[1], len(specs), dev)
         design, binomial, Kp, inv_std, inv_wsum, pmask, l2v, l1v, x0 = self._setup(hm, y, specs, K, allreduce)
         B, D = len(specs), Kp * (F + 1)
         T = max(1, int(self.lineSearchTrials))
@@ -266,9 +294,24 @@ class LogisticRegression(Estimator, ClassifierParams):
                 icpt = icpt - icpt.mean()
             summary = {"objective": float(fobj_h[bi]), "iterations": int(iters_h[bi]), "n_evals": n_evals,
                        "objectiveHistory": history}
-            models.append(LogisticRegressionModel(coef.detach(), icpt.detach(), binomial, device=dev,
-                                                  summary=summary))
+            models.append(self._apply_thresholds(LogisticRegressionModel(coef.detach(), icpt.detach(), binomial,
+                                                                         device=dev, summary=summary)))
+        if ckpt is not None:
+            st = {}
+            for bi, mo in enumerate(models):
+                st[f"coef{bi}"], st[f"icpt{bi}"] = mo.coefficientMatrix, mo.interceptVector
+            ckpt.save(1, st, {"binomial": binomial, "summaries": [
+                {k: v for k, v in mo.summary.items() if k != "objectiveHistory"} for mo in models]}, fingerprint=fp)
         return models
+
+    def _models_from_state(self, st, meta, B: int, dev) -> List[LogisticRegressionModel]:
+        out = []
+        for bi in range(B):
+            summary = dict(meta["summaries"][bi], resumed=True)
+            out.append(self._apply_thresholds(LogisticRegressionModel(
+                st[f"coef{bi}"].to(dev), st[f"icpt{bi}"].to(dev), bool(meta["binomial"]), device=dev,
+                summary=summary)))
+        return out
 
     def _fit_wide_dense(self, hm, y, design, inv_std, inv_wsum, pmask, l2v, l1v, x0, allreduce):
         """GPU objective for dense blocks wider than the fused kernel's LDS tile: exact-fp32 MFMA

@@ -7,8 +7,8 @@ Spark ``RandomForest.run`` semantics:
 * ``findSplits``: at most ``maxBins - 1`` thresholds per feature (midpoints of the
   distinct values, or quantile cut points); a binary one-hot feature gets the
   single split 0 | 1, which is Spark's 2-category split;
-* bagging: RandomForest with ``numTrees > 1`` draws Poisson(1) per (tree, row)
-  (``subsamplingRate = 1``), a single tree uses every row once;
+* bagging: RandomForest with ``numTrees > 1`` draws Poisson(subsamplingRate) per (tree, row)
+  (with replacement), a single tree Bernoulli(subsamplingRate) (without; every row once at 1);
 * ``featureSubsetStrategy``: ``auto`` = ``sqrt`` for a forest, ``all`` for one
   tree; the subset is re-drawn at every node;
 * impurity gini (or entropy); a node splits only when its best gain is > 0 and
@@ -82,7 +82,7 @@ class ForestBuilder:
     def __init__(self, num_classes: int, num_trees: int = 1, max_depth: int = 5, max_bins: int = 32,
                  min_instances: int = 1, min_info_gain: float = 0.0, impurity: str = "gini",
                  feature_subset: str = "auto", bootstrap: Optional[bool] = None, seed: int = 0,
-                 allreduce=None, tree_offset: int = 0, owner=None):
+                 allreduce=None, tree_offset: int = 0, owner=None, subsample: float = 1.0):
         if max_bins > 64:
             raise ValueError("maxBins <= 64 (one lane per bin in the split kernel)")
         self.K, self.T, self.D = num_classes, num_trees, max_depth
@@ -90,6 +90,17 @@ class ForestBuilder:
         self.impurity = T.GINI if impurity == "gini" else T.ENTROPY
         self.subset = feature_subset
         self.bootstrap = (num_trees > 1) if bootstrap is None else bootstrap
+        if not 0.0 < subsample <= 1.0:
+            raise ValueError("subsamplingRate must be in (0, 1]")
+        self.subsample = float(subsample)
+        # Spark BaggedPoint: with replacement (a forest) Poisson(rate) counts, without replacement
+        # (one tree) Bernoulli(rate) at rate < 1, else every row once
+        if self.bootstrap:
+            self.cdf = rng.poisson_thresholds(self.subsample)
+        elif self.subsample < 1.0:
+            self.cdf = rng.bernoulli_thresholds(self.subsample)
+        else:
+            self.cdf = None
         self.seed = seed
         self.allreduce = allreduce  # optional callable(tensor) -> None (DP histogram reduction)
         self.tree_offset = tree_offset  # global id of tree 0 (bootstrap / feature-subset streams)
@@ -115,15 +126,11 @@ class ForestBuilder:
         self.bins = bin_features(X, self.thresholds).to(X.device).contiguous()  # [F, N] uint8 (HIP on the GPU)
 
     def bootstrap_weights(self, N: int, device, row_offset: int = 0) -> torch.Tensor:
-        if not self.bootstrap:
+        """Host oracle of the device tree_init draws (same Philox keys, same CDF table)."""
+        if self.cdf is None:
             return torch.ones(self.T, N, dtype=torch.float32, device=device)
-        if device.type == "cuda":
-            w = torch.empty(self.T, N, dtype=torch.uint8, device=device)
-            _native.kernels().poisson_bootstrap(self.seed, self.tree_offset, self.T, row_offset, N, w.data_ptr(),
-                                                _native.stream_ptr())
-            return w.float()
-        return torch.from_numpy(rng.poisson1_weights(self.seed, range(self.tree_offset, self.tree_offset + self.T),
-                                                     N, row_offset)).float()
+        return torch.from_numpy(rng.bootstrap_weights(self.seed, range(self.tree_offset, self.tree_offset + self.T),
+                                                      N, row_offset, self.cdf)).float().to(device)
 
     def fit(self, X: torch.Tensor, y: torch.Tensor, row_offset: int = 0, thresholds=None,
             row_weight: Optional[torch.Tensor] = None) -> ForestArrays:
@@ -155,7 +162,8 @@ class ForestBuilder:
             node_of = torch.empty(Tn, N, dtype=torch.int32, device=dev)
             bad = torch.zeros(1, dtype=torch.int32, device=dev)
             rw = None if row_weight is None else row_weight.to(device=dev, dtype=torch.float32).contiguous()
-            _native.kernels().tree_init(self.seed, self.tree_offset, Tn, row_offset, N, int(self.bootstrap),
+            cdf = [] if self.cdf is None else [int(v) for v in self.cdf]
+            _native.kernels().tree_init(self.seed, self.tree_offset, Tn, row_offset, N, cdf,
                                         0 if rw is None else rw.data_ptr(), y32.data_ptr(), K, W.data_ptr(),
                                         node_of.data_ptr(), stats.data_ptr(), maxn * K, bad.data_ptr(),
                                         _native.stream_ptr())
@@ -552,8 +560,6 @@ class RandomForestClassifier(_TreeEstimatorBase):
         """Grow the forest (all trees in lock step, or in waves of ``tree_wave`` trees —
         each wave checkpointed under ``checkpoint_dir`` and skipped on resume).  Trees
         are keyed by their global id, so a waved forest equals the one-shot forest."""
-        if self.subsamplingRate != 1.0:
-            raise NotImplementedError("subsamplingRate != 1.0")
         strategy = self.featureSubsetStrategy
         if str(strategy).lower() == "auto":
             strategy = "all" if self.numTrees == 1 else "sqrt"
@@ -600,7 +606,8 @@ class RandomForestClassifier(_TreeEstimatorBase):
             nt = min(wave, total - done)
             b = ForestBuilder(K, nt, self.maxDepth, self.maxBins, self.minInstancesPerNode, self.minInfoGain,
                               self.impurity, strategy, bootstrap=self.numTrees > 1, seed=self.seed,
-                              allreduce=allreduce, tree_offset=tree_offset + done, owner=owner)
+                              allreduce=allreduce, tree_offset=tree_offset + done, owner=owner,
+                              subsample=self.subsamplingRate)
             parts.append(b.fit(X, y, row_offset=row_offset, thresholds=thresholds))
             done += nt
             if ckpt is not None and done < total:
@@ -613,14 +620,13 @@ class RandomForestClassifier(_TreeEstimatorBase):
     def fit_folds(self, X, y, K, masks: torch.Tensor) -> List["RandomForestClassificationModel"]:
         """k forests of numTrees trees (fold f: trees f*T .. f*T+T-1, its own bootstrap / feature
         streams) grown as ONE level-synchronous build of k*T trees over the shared binned matrix."""
-        if self.subsamplingRate != 1.0:
-            raise NotImplementedError("subsamplingRate != 1.0")
         T_, k = self.numTrees, masks.shape[0]
         strategy = self.featureSubsetStrategy
         if str(strategy).lower() == "auto":
             strategy = "all" if T_ == 1 else "sqrt"
         b = ForestBuilder(K, k * T_, self.maxDepth, self.maxBins, self.minInstancesPerNode, self.minInfoGain,
-                          self.impurity, strategy, bootstrap=T_ > 1, seed=self.seed, owner=dp_owner())
+                          self.impurity, strategy, bootstrap=T_ > 1, seed=self.seed, owner=dp_owner(),
+                          subsample=self.subsamplingRate)
         arrs = _fit_sharded(b, X, y, masks.repeat_interleave(T_, dim=0), self.maxBins, self.seed)
         return [RandomForestClassificationModel(_slice_arrays(arrs, f * T_, (f + 1) * T_), X.shape[1], K, uid=self.uid,
                                                 device=X.device) for f in range(k)]

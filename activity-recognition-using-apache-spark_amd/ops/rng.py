@@ -82,17 +82,41 @@ def assign_buckets(seed: int, stream: int, row_ids, weights) -> np.ndarray:
     return np.searchsorted(thr, u, side="right").astype(np.int64)
 
 
-def _poisson1_thresholds(kmax: int = 15) -> np.ndarray:
-    """uint32 CDF thresholds of Poisson(1): draw = #{k : u >= thr[k]}."""
-    cdf, p, out = 0.0, math.exp(-1.0), []
+def poisson_thresholds(rate: float = 1.0, kmax: int = 15) -> np.ndarray:
+    """uint32 CDF thresholds of Poisson(rate): draw = #{k : u >= thr[k]} (rate 1: Spark's
+    bootstrap with replacement at subsamplingRate 1)."""
+    cdf, p, out = 0.0, math.exp(-float(rate)), []
     for k in range(kmax):
         cdf += p
-        p /= (k + 1)
+        p = p * float(rate) / (k + 1)
         out.append(min(int(math.floor(cdf * 4294967296.0)), 4294967295))
     return np.asarray(out, dtype=np.uint64)
 
 
+def bernoulli_thresholds(rate: float) -> np.ndarray:
+    """Sampling without replacement at ``rate`` (Spark: one tree, subsamplingRate < 1): one
+    threshold, draw = 1 when u >= (1 - rate) * 2^32."""
+    return np.asarray([min(int(math.floor((1.0 - float(rate)) * 4294967296.0)), 4294967295)], dtype=np.uint64)
+
+
+def _poisson1_thresholds(kmax: int = 15) -> np.ndarray:
+    return poisson_thresholds(1.0, kmax)
+
+
 POISSON1_THR = _poisson1_thresholds()
+
+
+def bootstrap_weights(seed: int, tree_ids, n_rows: int, row_offset: int = 0, thresholds=None) -> np.ndarray:
+    """Per-(tree, global row) bootstrap counts from a CDF threshold table (``poisson_thresholds``
+    / ``bernoulli_thresholds``), shape [len(tree_ids), n_rows], uint8; None table = all ones."""
+    if thresholds is None:
+        return np.ones((len(tree_ids), n_rows), dtype=np.uint8)
+    rows = np.arange(row_offset, row_offset + n_rows, dtype=np.uint64)
+    out = np.empty((len(tree_ids), n_rows), dtype=np.uint8)
+    for i, t in enumerate(tree_ids):
+        u = uniform_u32(seed, STREAM_BOOTSTRAP_BASE + int(t), rows).astype(np.uint64)
+        out[i] = np.searchsorted(thresholds, u, side="right")
+    return out
 
 
 def poisson1_weights(seed: int, tree_ids, n_rows: int, row_offset: int = 0) -> np.ndarray:

@@ -305,10 +305,11 @@ PYBIND11_MODULE(_har_native, m) {
           "forest_predict");
   });
 
-  m.def("tree_init", [](uint64_t seed, int tree0, int ntrees, int64_t row0, int64_t n, int bootstrap, u rw, u y, int K,
-                        u W, u node_of, u stats, int64_t stride, u bad, u stream) {
-    check(har_tree_init(seed, tree0, ntrees, row0, n, bootstrap, P<const float>(rw), P<const int32_t>(y), K,
-                        P<float>(W), P<int32_t>(node_of), P<float>(stats), stride, P<int32_t>(bad), S(stream)),
+  m.def("tree_init", [](uint64_t seed, int tree0, int ntrees, int64_t row0, int64_t n, std::vector<uint32_t> cdf,
+                        u rw, u y, int K, u W, u node_of, u stats, int64_t stride, u bad, u stream) {
+    check(har_tree_init(seed, tree0, ntrees, row0, n, cdf.data(), (int)cdf.size(), P<const float>(rw),
+                        P<const int32_t>(y), K, P<float>(W), P<int32_t>(node_of), P<float>(stats), stride,
+                        P<int32_t>(bad), S(stream)),
           "tree_init");
   });
   m.def("find_splits_post_sort", [](u sorted, int F, int n, int ns, u out, u stream) {

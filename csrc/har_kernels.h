@@ -105,12 +105,13 @@ int har_cast_pad_bf16(const float* in, int rows, int cols_in, int ld_in, uint16_
 // ---- randomness (Philox4x32-10 keyed by global row id) ----
 int har_philox_buckets(uint64_t seed, uint32_t stream, int64_t row0, int64_t n, const uint32_t* thr,
                        int nthr, int32_t* out, hipStream_t s);
-// Per-fit init (tree.hip): W [T][N] = Poisson(1) bootstrap (or 1) x optional rw [T][N]; node_of [T][N]
+// Per-fit init (tree.hip): W [T][N] = bootstrap draw from the CDF table (or 1) x optional rw [T][N]; node_of [T][N]
 // = 0 / -1 (zero weight); root class counts added into stats + t * stats_tree_stride; *bad = 1 on a
 // label outside [0, K).
-int har_tree_init(uint64_t seed, int tree0, int ntrees, int64_t row0, int64_t n, int bootstrap, const float* rw,
-                  const int32_t* y, int K, float* W, int32_t* node_of, float* stats, int64_t stats_tree_stride,
-                  int32_t* bad, hipStream_t s);
+// cdf: HOST array of ncdf (<= 16) uint32 bootstrap CDF thresholds (ncdf = 0: every weight 1).
+int har_tree_init(uint64_t seed, int tree0, int ntrees, int64_t row0, int64_t n, const uint32_t* cdf, int ncdf,
+                  const float* rw, const int32_t* y, int K, float* W, int32_t* node_of, float* stats,
+                  int64_t stats_tree_stride, int32_t* bad, hipStream_t s);
 // findSplits cut points from the per-feature sorted sample [F][n] (NaN last), n <= 16384, ns <= 63:
 // out [F][ns + 1] = thresholds then their count.
 int har_find_splits_post_sort(const float* sorted, int F, int n, int ns, float* out, hipStream_t s);

@@ -433,15 +433,17 @@ __global__ __launch_bounds__(256) void poisson_bootstrap_kernel(uint64_t seed, i
 // sums of integer-valued weights (< 2^24), so the LDS partials and the one global atomic per
 // (workgroup, class) are exact in any order: the result is deterministic.
 constexpr int INIT_ROWS = 2048;
+struct CdfTable {
+  uint32_t thr[16];
+  int n;  // 0: every weight 1 (no sampling)
+};
+
 __global__ __launch_bounds__(256) void tree_init_kernel(uint64_t seed, int tree0, int64_t row0, int64_t n,
-                                                        int bootstrap, const float* __restrict__ rw,
+                                                        CdfTable cdf, const float* __restrict__ rw,
                                                         const int32_t* __restrict__ y, int K,
                                                         float* __restrict__ W, int32_t* __restrict__ node_of,
                                                         float* __restrict__ stats, int64_t stats_tree_stride,
                                                         int32_t* __restrict__ bad) {
-  const uint32_t thr[15] = {1580030168u, 3160060337u, 3950075421u, 4213413783u, 4279248373u, 4292415291u,
-                            4294609777u, 4294923276u, 4294962463u, 4294966817u, 4294967252u, 4294967292u,
-                            4294967295u, 4294967295u, 4294967295u};
   __shared__ float cnt[KMAX];
   const int t = blockIdx.y;
   if (threadIdx.x < KMAX) cnt[threadIdx.x] = 0.f;
@@ -450,10 +452,10 @@ __global__ __launch_bounds__(256) void tree_init_kernel(uint64_t seed, int tree0
   int badl = 0;
   for (int64_t r = r0 + threadIdx.x; r < r1; r += 256) {
     float w = 1.f;
-    if (bootstrap) {
+    if (cdf.n > 0) {  // bootstrap draw: #{k : u >= thr[k]} (Poisson(rate) or Bernoulli(rate) table)
       const uint32_t u = philox_u32(seed, 0x1000u + (uint32_t)(tree0 + t), (uint64_t)(row0 + r));
       int k = 0;
-      while (k < 15 && u >= thr[k]) ++k;
+      while (k < cdf.n && u >= cdf.thr[k]) ++k;
       w = (float)k;
     }
     if (rw) w *= rw[(int64_t)t * n + r];
@@ -668,14 +670,17 @@ extern "C" int har_poisson_bootstrap(uint64_t seed, int tree0, int ntrees, int64
   return 0;
 }
 
-extern "C" int har_tree_init(uint64_t seed, int tree0, int ntrees, int64_t row0, int64_t n, int bootstrap,
-                             const float* rw, const int32_t* y, int K, float* W, int32_t* node_of, float* stats,
-                             int64_t stats_tree_stride, int32_t* bad, hipStream_t s) {
-  if (K <= 0 || K > KMAX) return -2;
+extern "C" int har_tree_init(uint64_t seed, int tree0, int ntrees, int64_t row0, int64_t n, const uint32_t* cdf,
+                             int ncdf, const float* rw, const int32_t* y, int K, float* W, int32_t* node_of,
+                             float* stats, int64_t stats_tree_stride, int32_t* bad, hipStream_t s) {
+  if (K <= 0 || K > KMAX || ncdf < 0 || ncdf > 16) return -2;
   if (n == 0 || ntrees == 0) return 0;
+  CdfTable tab{};
+  tab.n = ncdf;
+  for (int i = 0; i < ncdf; ++i) tab.thr[i] = cdf[i];  // host array (kernel argument)
   dim3 grid((unsigned)((n + INIT_ROWS - 1) / INIT_ROWS), (unsigned)ntrees);
-  tree_init_kernel<<<grid, 256, 0, s>>>(seed, tree0, row0, n, bootstrap, rw, y, K, W, node_of, stats,
-                                        stats_tree_stride, bad);
+  tree_init_kernel<<<grid, 256, 0, s>>>(seed, tree0, row0, n, tab, rw, y, K, W, node_of, stats, stats_tree_stride,
+                                        bad);
   HAR_CHECK_LAUNCH();
   return 0;
 }

@@ -304,3 +304,19 @@ def test_planned_levels_equal_node_blocks(cuda, monkeypatch):
     a, b = fits[True].arrs, fits[False].arrs
     for name in ("feature", "threshold", "left", "right", "stats", "gain"):
         assert torch.equal(getattr(a, name), getattr(b, name)), name
+
+
+@pytest.mark.parametrize("trees,rate", [(12, 0.6), (1, 0.4)])
+def test_subsampled_forest_gpu_equals_cpu(cuda, trees, rate):
+    """subsamplingRate on the device (tree_init: Poisson(rate) / Bernoulli(rate) from the CDF table)
+    draws the host oracle's weights: identical root counts and top levels."""
+    from har.models.tree import RandomForestClassifier
+    from har.ops import tree as T
+
+    x, y = _blobs(3000, 16, 5, seed=8)
+    thr = T.find_thresholds(x.numpy(), 32)
+    kw = dict(numTrees=trees, maxDepth=5, seed=6, subsamplingRate=rate)
+    c = RandomForestClassifier(**kw).fit_tensors(x, y, 5, thresholds=thr)
+    g = RandomForestClassifier(**kw).fit_tensors(x.to(cuda), y.to(cuda), 5, thresholds=thr)
+    torch.testing.assert_close(g.arrs.stats[:, 0].cpu(), c.arrs.stats[:, 0], rtol=0, atol=0)
+    assert torch.equal(g.arrs.feature[:, :3].cpu(), c.arrs.feature[:, :3])

@@ -246,3 +246,75 @@ def test_threshold_sample_is_shard_invariant():
     assert np.array_equal(full, np.concatenate(parts))
     assert 9500 < full.sum() < 10500
     assert T.threshold_sample_mask(9000, 32, 10000) is None
+
+
+def test_random_forest_subsampling_rate():
+    """subsamplingRate (Spark BaggedPoint): a forest draws Poisson(rate) counts per (tree, row),
+    one tree Bernoulli(rate); the draws come from one CDF table shared with the device kernel."""
+    import numpy as np
+
+    from har.models.tree import ForestBuilder, RandomForestClassifier
+    from har.ops import rng
+
+    b = ForestBuilder(3, num_trees=40, subsample=0.5, seed=3)
+    w = b.bootstrap_weights(20000, torch.device("cpu")).numpy()
+    assert abs(w.mean() - 0.5) < 0.01 and abs(w.var() - 0.5) < 0.02  # Poisson(0.5): mean = var = 0.5
+    one = ForestBuilder(3, num_trees=1, subsample=0.3, seed=3).bootstrap_weights(20000, torch.device("cpu")).numpy()
+    assert set(np.unique(one)) <= {0, 1} and abs(one.mean() - 0.3) < 0.01
+    assert np.array_equal(ForestBuilder(3, num_trees=5, seed=3).cdf, rng.POISSON1_THR)  # rate 1 unchanged
+    g = torch.Generator().manual_seed(1)
+    X = torch.randn(600, 6, generator=g)
+    y = (X[:, 0] > 0).long() + (X[:, 1] > 0.5).long()
+    m = RandomForestClassifier(numTrees=10, maxDepth=4, subsamplingRate=0.6, seed=2).fit_tensors(X, y, 3)
+    assert float((m.predict(X) == y).float().mean()) > 0.8
+    with pytest.raises(ValueError):
+        ForestBuilder(3, num_trees=2, subsample=1.5)
+
+
+def test_classification_thresholds():
+    """Spark thresholds: argmax of p / t; a zero threshold wins wherever its probability is > 0;
+    binary LogisticRegression(threshold=t) == thresholds [1 - t, t]."""
+    from har.models.logreg import LogisticRegression
+
+    g = torch.Generator().manual_seed(0)
+    X = torch.randn(800, 4, generator=g)
+    y = (X[:, 0] + 0.3 * torch.randn(800, generator=g) > 0).long()
+    base = LogisticRegression(maxIter=30, device="cpu").fit_many(X, y, [FitSpec(None, 0.0, 0.0)], 2)[0]
+    raw, prob, pred = base.predict_all(X)
+    assert torch.equal(pred, torch.argmax(prob, 1))
+    strict = LogisticRegression(maxIter=30, device="cpu", threshold=0.9)
+    m = strict._apply_thresholds(base)
+    _, prob2, pred2 = m.predict_all(X)
+    assert torch.equal(pred2, (prob2[:, 1] > 0.9).long())
+    assert int(pred2.sum()) < int(pred.sum())
+    m.setThresholds([0.0, 1.0])  # class 0 wins wherever p0 > 0
+    _, p3, pred3 = m.predict_all(X)
+    assert int(pred3[p3[:, 0] > 0].sum()) == 0 and bool((pred3[p3[:, 0] == 0] == 1).all())
+    with pytest.raises(ValueError):
+        m.setThresholds([0.0, 0.0])
+
+
+def test_logreg_checkpoint_resume(tmp_path, monkeypatch):
+    """A finished LR fit batch is checkpointed under its fingerprint; a rerun (restarted job)
+    loads it without solving and returns the same models; other parameters refit."""
+    from har.models import logreg as lr_mod
+    from har.models.logreg import FitSpec, LogisticRegression
+
+    g = torch.Generator().manual_seed(4)
+    X = torch.randn(500, 5, generator=g)
+    y = torch.randint(0, 3, (500,), generator=g)
+    specs = [FitSpec(None, 0.1, 0.0), FitSpec(None, 0.05, 0.5)]
+    ck = str(tmp_path / "lr")
+    a = LogisticRegression(maxIter=20, device="cpu", checkpointDir=ck).fit_many(X, y, specs, 3)
+
+    def boom(*args, **kw):
+        raise AssertionError("resumed fit must not solve again")
+
+    monkeypatch.setattr(lr_mod.LogisticRegression, "_setup", boom)
+    b = LogisticRegression(maxIter=20, device="cpu", checkpointDir=ck).fit_many(X, y, specs, 3)
+    for ma, mb in zip(a, b):
+        assert torch.equal(ma.coefficientMatrix, mb.coefficientMatrix)
+        assert torch.equal(ma.interceptVector, mb.interceptVector)
+        assert mb.summary["resumed"] and mb.summary["iterations"] == ma.summary["iterations"]
+    with pytest.raises(AssertionError):  # a different fit (maxIter) is not resumed from the stale checkpoint
+        LogisticRegression(maxIter=21, device="cpu", checkpointDir=ck).fit_many(X, y, specs, 3)
