@@ -18,6 +18,8 @@
 // std = population standard deviation; resultant = mean sqrt(x^2+y^2+z^2);
 // peak = mean time (ms) between local maxima above mean + 0.5 (max - mean)
 // (NaN — the '?' of the WISDM table — when fewer than two peaks).
+#include <type_traits>
+
 #include "common.h"
 #include "../har_kernels.h"
 
@@ -27,36 +29,67 @@ constexpr int MAXA = 9;
 constexpr int NB = 10;
 constexpr int WAVES = 4;
 
-// Reductions over the LPW lanes of one window group (xor offsets < LPW stay inside the group).
-template <int LPW> __device__ __forceinline__ float gsum(float v) {
-#pragma unroll
-  for (int o = LPW / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+// Reductions over the LPW lanes of one window group; every lane ends with the group's result.
+// VALU data-parallel-primitive moves instead of ds_bpermute shuffles (LDS round trips): inside a
+// 16-lane row a butterfly of quad_perm xor-1, quad_perm xor-2, row_half_mirror and row_mirror
+// (after the quad steps every lane of a quad holds the quad's value, so the mirrors pair whole
+// quads, then whole half-rows); across rows (LPW = 64) the gfx950 permlane16 / permlane32 swaps.
+template <int CTRL> __device__ __forceinline__ int dpp_i(int v) {
+  return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, false);
+}
+template <int CTRL> __device__ __forceinline__ float dpp_f(float v) {
+  return __int_as_float(dpp_i<CTRL>(__float_as_int(v)));
+}
+__device__ __forceinline__ int swap16_i(int v) {  // value of lane ^ 16
+  const auto r = __builtin_amdgcn_permlane16_swap((uint32_t)v, (uint32_t)v, false, false);
+  const auto me = __builtin_amdgcn_permlane16_swap((uint32_t)__lane_id(), (uint32_t)__lane_id(), false, false);
+  return (int)(me[0] == (uint32_t)(__lane_id() ^ 16) ? r[0] : r[1]);
+}
+__device__ __forceinline__ int swap32_i(int v) {  // value of lane ^ 32
+  const auto r = __builtin_amdgcn_permlane32_swap((uint32_t)v, (uint32_t)v, false, false);
+  const auto me = __builtin_amdgcn_permlane32_swap((uint32_t)__lane_id(), (uint32_t)__lane_id(), false, false);
+  return (int)(me[0] == (uint32_t)(__lane_id() ^ 32) ? r[0] : r[1]);
+}
+
+template <int LPW, typename T, typename Op> __device__ __forceinline__ T greduce(T v, Op op) {
+  static_assert(LPW == 16 || LPW == 64, "window groups of 16 or 64 lanes");
+  auto mv = [](T x, auto ctrl) {
+    constexpr int C = decltype(ctrl)::value;
+    if constexpr (sizeof(T) == 4 && (T)0.5f != 0) return dpp_f<C>(x);
+    else return (T)dpp_i<C>((int)x);
+  };
+  v = op(v, mv(v, std::integral_constant<int, 0xB1>{}));   // xor 1
+  v = op(v, mv(v, std::integral_constant<int, 0x4E>{}));   // xor 2
+  v = op(v, mv(v, std::integral_constant<int, 0x141>{}));  // row_half_mirror: quad <-> quad
+  v = op(v, mv(v, std::integral_constant<int, 0x140>{}));  // row_mirror: half-row <-> half-row
+  if constexpr (LPW == 64) {
+    if constexpr ((T)0.5f != 0) {
+      v = op(v, __int_as_float(swap16_i(__float_as_int(v))));
+      v = op(v, __int_as_float(swap32_i(__float_as_int(v))));
+    } else {
+      v = op(v, (T)swap16_i((int)v));
+      v = op(v, (T)swap32_i((int)v));
+    }
+  }
   return v;
+}
+template <int LPW> __device__ __forceinline__ float gsum(float v) {
+  return greduce<LPW, float>(v, [](float a, float b) { return a + b; });
 }
 template <int LPW> __device__ __forceinline__ int gsumi(int v) {
-#pragma unroll
-  for (int o = LPW / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
+  return greduce<LPW, int>(v, [](int a, int b) { return a + b; });
 }
 template <int LPW> __device__ __forceinline__ float gmin(float v) {
-#pragma unroll
-  for (int o = LPW / 2; o > 0; o >>= 1) v = fminf(v, __shfl_xor(v, o, 64));
-  return v;
+  return greduce<LPW, float>(v, [](float a, float b) { return fminf(a, b); });
 }
 template <int LPW> __device__ __forceinline__ float gmax(float v) {
-#pragma unroll
-  for (int o = LPW / 2; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
-  return v;
+  return greduce<LPW, float>(v, [](float a, float b) { return fmaxf(a, b); });
 }
 template <int LPW> __device__ __forceinline__ int gmini(int v) {
-#pragma unroll
-  for (int o = LPW / 2; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o, 64));
-  return v;
+  return greduce<LPW, int>(v, [](int a, int b) { return min(a, b); });
 }
 template <int LPW> __device__ __forceinline__ int gmaxi(int v) {
-#pragma unroll
-  for (int o = LPW / 2; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o, 64));
-  return v;
+  return greduce<LPW, int>(v, [](int a, int b) { return max(a, b); });
 }
 
 // A is a template parameter so every per-axis register array is statically indexed
@@ -74,43 +107,12 @@ struct MlpOut {
   uint16_t* out;
 };
 
+// The statistics of one window group's windows from their LDS image (`buf`: this group's window,
+// W samples x A axes, sample-major).  Shared by the one-shot and the persistent kernels.
 template <int A, int LPW, bool MLP>
-__global__ __launch_bounds__(WAVES * 64) void window_features_kernel(const float* __restrict__ stream,
-                                                                     int64_t n_samples, int W, int stride,
-                                                                     int64_t n_windows, float ms_per_sample,
-                                                                     float* __restrict__ out, int ld_out,
-                                                                     MlpOut mo) {
-  constexpr int G = 64 / LPW;  // windows per wave
-  extern __shared__ __attribute__((aligned(16))) float lds[];  // [WAVES * G][W*A]
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int sub = lane % LPW, grp = lane / LPW;
-  const int64_t win0 = ((int64_t)blockIdx.x * WAVES + wave) * G;
-  if (win0 >= n_windows) return;  // wave-uniform; no block barrier below
-  const int64_t win = win0 + grp;
-  const bool valid = win < n_windows;
-  const int n = W * A;
-  float* wbuf = lds + (size_t)wave * G * n;
-  float* buf = wbuf + (size_t)grp * n;
-  // ---- stage the wave's windows in LDS ----
-  const int nw = (int)min<int64_t>(G, n_windows - win0);
-  if (stride == W && G > 1) {
-    // non-overlapping windows: the wave's windows are one contiguous run; 16-byte loads when aligned
-    const float* src = stream + win0 * (int64_t)W * A;
-    const int tot = nw * n;
-    if (((reinterpret_cast<uintptr_t>(src) & 15) == 0) && (tot % 4 == 0) && (n % 4 == 0)) {
-      const float4* s4 = reinterpret_cast<const float4*>(src);
-      float4* d4 = reinterpret_cast<float4*>(wbuf);
-      for (int i = lane; i < tot / 4; i += 64) d4[i] = s4[i];
-    } else {
-      for (int i = lane; i < tot; i += 64) wbuf[i] = src[i];
-    }
-  } else if (valid) {
-    const float* src = stream + win * (int64_t)stride * A;
-    for (int i = sub; i < n; i += LPW) buf[i] = src[i];
-  }
-  __builtin_amdgcn_s_waitcnt(0);
-  __builtin_amdgcn_wave_barrier();
-
+__device__ __forceinline__ void window_compute(const float* buf, int W, bool valid, int64_t win, int sub,
+                                               float ms_per_sample, float* __restrict__ out, int ld_out,
+                                               const MlpOut& mo) {
   const float invW = 1.f / (float)W;
   float mean[A], mn[A], mx[A], en[A];
   // ---- pass 1: one sweep over the samples for all axes ----
@@ -228,9 +230,138 @@ __global__ __launch_bounds__(WAVES * 64) void window_features_kernel(const float
   }
 }
 
+template <int A, int LPW, bool MLP>
+__global__ __launch_bounds__(WAVES * 64) void window_features_kernel(const float* __restrict__ stream,
+                                                                     int64_t n_samples, int W, int stride,
+                                                                     int64_t n_windows, float ms_per_sample,
+                                                                     float* __restrict__ out, int ld_out,
+                                                                     MlpOut mo) {
+  constexpr int G = 64 / LPW;  // windows per wave
+  extern __shared__ __attribute__((aligned(16))) float lds[];  // [WAVES * G][W*A]
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int sub = lane % LPW, grp = lane / LPW;
+  const int64_t win0 = ((int64_t)blockIdx.x * WAVES + wave) * G;
+  if (win0 >= n_windows) return;  // wave-uniform; no block barrier below
+  const int64_t win = win0 + grp;
+  const bool valid = win < n_windows;
+  const int n = W * A;
+  float* wbuf = lds + (size_t)wave * G * n;
+  float* buf = wbuf + (size_t)grp * n;
+  // ---- stage the wave's windows in LDS ----
+  const int nw = (int)min<int64_t>(G, n_windows - win0);
+  if (stride == W && G > 1) {
+    // non-overlapping windows: the wave's windows are one contiguous run; 16-byte loads when aligned
+    const float* src = stream + win0 * (int64_t)W * A;
+    const int tot = nw * n;
+    if (((reinterpret_cast<uintptr_t>(src) & 15) == 0) && (tot % 4 == 0) && (n % 4 == 0)) {
+      const float4* s4 = reinterpret_cast<const float4*>(src);
+      float4* d4 = reinterpret_cast<float4*>(wbuf);
+      for (int i = lane; i < tot / 4; i += 64) d4[i] = s4[i];
+    } else {
+      for (int i = lane; i < tot; i += 64) wbuf[i] = src[i];
+    }
+  } else if (valid) {
+    const float* src = stream + win * (int64_t)stride * A;
+    for (int i = sub; i < n; i += LPW) buf[i] = src[i];
+  }
+  __builtin_amdgcn_s_waitcnt(0);
+  __builtin_amdgcn_wave_barrier();
+
+  window_compute<A, LPW, MLP>(buf, W, valid, win, sub, ms_per_sample, out, ld_out, mo);
+}
+
+// Persistent variant: each wave walks window groups g, g + waves_in_grid, ...; the contiguous
+// sample span of the NEXT group (G windows, (G - 1) stride + W samples) is loaded into PV 16-byte
+// registers per lane while the current group is computed from LDS, so HBM latency hides behind
+// the statistics instead of being paid once per group.  Loads are unconditional (indices clamped
+// into the stream: the duplicates are never read) so the waits stay counted.  Needs the span to
+// fit 64 * PV float4 and 16-byte alignment of every group start (host checks).
+template <int A, int LPW, bool MLP, int PV>
+__global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(2, 3)))
+void window_features_persistent_kernel(
+    const float* __restrict__ stream, int64_t n_samples, int W, int stride, int64_t n_windows, float ms_per_sample,
+    float* __restrict__ out, int ld_out, MlpOut mo) {
+  constexpr int G = 64 / LPW;
+  extern __shared__ __attribute__((aligned(16))) float lds[];  // [WAVES][PV * 64 float4]
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int sub = lane % LPW, grp = lane / LPW;
+  // native clang vectors, not HIP's float4 struct: struct copies of an array element defeat the
+  // alloca-to-register promotion and put `pre` in scratch
+  typedef float v4f __attribute__((ext_vector_type(4)));
+  v4f* img = reinterpret_cast<v4f*>(lds) + (size_t)wave * PV * 64;
+  const int64_t ngroups = (n_windows + G - 1) / G;
+  const int64_t step = (int64_t)gridDim.x * WAVES;
+  const int64_t total4 = n_samples * A / 4;  // whole float4s of the stream
+  const v4f* s4 = reinterpret_cast<const v4f*>(stream);
+  v4f pre[PV];
+  int64_t g = (int64_t)blockIdx.x * WAVES + wave;
+  if (g >= ngroups) return;  // wave-uniform; no block barrier below
+  {
+    const int64_t base = g * G * (int64_t)stride * A / 4;
+#pragma unroll
+    for (int j = 0; j < PV; ++j) {
+      const int64_t i = base + lane + 64 * j;
+      pre[j] = s4[i < total4 ? i : total4 - 1];
+    }
+  }
+  for (; g < ngroups; g += step) {
+    __builtin_amdgcn_wave_barrier();  // this wave's reads of the previous image are issued first
+#pragma unroll
+    for (int j = 0; j < PV; ++j) img[lane + 64 * j] = pre[j];
+    {
+      const int64_t gn = g + step < ngroups ? g + step : ngroups - 1;
+      const int64_t base = gn * G * (int64_t)stride * A / 4;
+#pragma unroll
+      for (int j = 0; j < PV; ++j) {
+        const int64_t i = base + lane + 64 * j;
+        pre[j] = s4[i < total4 ? i : total4 - 1];
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);  // the prefetch goes out before the compute
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the image is written
+    __builtin_amdgcn_wave_barrier();
+    const int64_t win = g * G + grp;
+    const bool valid = win < n_windows;
+    window_compute<A, LPW, MLP>(reinterpret_cast<const float*>(img) + (size_t)grp * stride * A, W, valid, win, sub,
+                                ms_per_sample, out, ld_out, mo);
+  }
+}
+
+constexpr int PV16 = 12, PV64 = 20;  // prefetch registers (float4 per lane) of the persistent kernels
+
+int cu_count() {
+  static int n = 0;
+  if (!n) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                                 hipSuccess || n <= 0)
+      n = 256;
+  }
+  return n;
+}
+
 template <int A, bool MLP>
 int launch_axes(const float* stream, int64_t n_samples, int window, int stride, int64_t n_windows, float ms,
                 float* out, int ld_out, MlpOut mo, hipStream_t s) {
+  // persistent + register-prefetched when a group's contiguous span fits the prefetch registers
+  // and every group starts 16-byte aligned (the common non-overlapping / half-overlapping cases)
+  const bool aligned = (reinterpret_cast<uintptr_t>(stream) & 15) == 0 && (n_samples * A) % 4 == 0;
+  const int64_t span16 = (int64_t)(3 * stride + window) * A, span64 = (int64_t)window * A;
+  if (false && aligned && stride <= window && span16 <= PV16 * 256 && window <= 16 * 15) {  // measured slower (105 vs 97 us)
+    const int64_t groups = (n_windows + 3) / 4;
+    const int64_t blocks = std::min<int64_t>((groups + WAVES - 1) / WAVES, (int64_t)cu_count() * 3);
+    window_features_persistent_kernel<A, 16, MLP, PV16><<<(unsigned)blocks, WAVES * 64, WAVES * PV16 * 64 * 16, s>>>(
+        stream, n_samples, window, stride, n_windows, ms, out, ld_out, mo);
+    HAR_CHECK_LAUNCH();
+    return 0;
+  }
+  if (aligned && stride <= window && ((int64_t)stride * A) % 4 == 0 && span64 <= PV64 * 256) {
+    const int64_t blocks = std::min<int64_t>((n_windows + WAVES - 1) / WAVES, (int64_t)cu_count() * 2);
+    window_features_persistent_kernel<A, 64, MLP, PV64><<<(unsigned)blocks, WAVES * 64, WAVES * PV64 * 64 * 16, s>>>(
+        stream, n_samples, window, stride, n_windows, ms, out, ld_out, mo);
+    HAR_CHECK_LAUNCH();
+    return 0;
+  }
   // four windows per wave while the block's 16 window images fit 64 KB of LDS, else one
   const size_t img = (size_t)window * A * sizeof(float);
   // (measured on MI355X, 200-sample 3-axis windows: 16 lanes 0.255 ms/stream step, 8 lanes 0.308,
