@@ -15,7 +15,7 @@
 //     and accumulate per lane with no per-sample masking except in the first and the last
 //     iterations (t = 0, t >= W - 1);
 //   * the distribution counts are packed 6 bits per bin in one 64-bit register per axis
-//     (one v_lshl_add_u64 per sample) and the local maxima as one bit per iteration,
+//     (one v_lshl_add_u64 per sample) and the local maxima as a shift register of flags,
 //     both flushed every 32 iterations; npk / first / last come from popcount / ctz / clz;
 //   * the 16-lane reductions are DPP butterflies (quad_perm, row_half_mirror, row_mirror):
 //     VALU moves, no LDS round trips.
@@ -27,6 +27,9 @@
 // spanning [min, max] of the window; absdev = mean |x - mean|; std = population standard
 // deviation; resultant = mean sqrt(x^2+y^2+z^2); peak = mean time (ms) between local maxima
 // above mean + 0.5 (max - mean) (NaN — the '?' of the WISDM table — when fewer than two peaks).
+#include <algorithm>
+#include <type_traits>
+
 #include "common.h"
 #include "../har_kernels.h"
 
@@ -39,13 +42,15 @@ constexpr int SLACK = 16;  // floats after it: the t = W neighbour read of the l
 
 typedef float v4f __attribute__((ext_vector_type(4)));
 
-// Reductions over one 16-lane row; every lane ends with the row's result.  quad_perm xor-1,
-// quad_perm xor-2, then row_half_mirror and row_mirror (after the quad steps every lane of a
-// quad holds the quad's value, so the mirrors pair whole quads, then whole half-rows).
+// Reductions over one group of LPW = 8 or 16 lanes; every lane ends with the group's result.
+// quad_perm xor-1, quad_perm xor-2, then row_half_mirror (and row_mirror for 16 lanes): after
+// the quad steps every lane of a quad holds the quad's value, so the mirrors pair whole quads,
+// then whole half-rows.
 template <int CTRL> __device__ __forceinline__ int dpp_i(int v) {
   return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, false);
 }
-template <typename T, typename Op> __device__ __forceinline__ T rreduce(T v, Op op) {
+template <int LPW, typename T, typename Op> __device__ __forceinline__ T rreduce(T v, Op op) {
+  static_assert(LPW == 8 || LPW == 16, "window groups of 8 or 16 lanes");
   auto mv = [](T x, auto ctrl) {
     constexpr int C = decltype(ctrl)::value;
     if constexpr (sizeof(T) == 4 && (T)0.5f != 0) return __int_as_float(dpp_i<C>(__float_as_int(x)));
@@ -54,17 +59,27 @@ template <typename T, typename Op> __device__ __forceinline__ T rreduce(T v, Op 
   v = op(v, mv(v, std::integral_constant<int, 0xB1>{}));   // xor 1
   v = op(v, mv(v, std::integral_constant<int, 0x4E>{}));   // xor 2
   v = op(v, mv(v, std::integral_constant<int, 0x141>{}));  // row_half_mirror: quad <-> quad
-  v = op(v, mv(v, std::integral_constant<int, 0x140>{}));  // row_mirror: half-row <-> half-row
+  if constexpr (LPW == 16) v = op(v, mv(v, std::integral_constant<int, 0x140>{}));  // row_mirror: half-row <-> half-row
   return v;
 }
-__device__ __forceinline__ float rsum(float v) { return rreduce<float>(v, [](float a, float b) { return a + b; }); }
-__device__ __forceinline__ uint32_t rsumu(uint32_t v) {
-  return rreduce<uint32_t>(v, [](uint32_t a, uint32_t b) { return a + b; });
+template <int LPW> __device__ __forceinline__ float rsum(float v) {
+  return rreduce<LPW, float>(v, [](float a, float b) { return a + b; });
 }
-__device__ __forceinline__ float rmin(float v) { return rreduce<float>(v, [](float a, float b) { return fminf(a, b); }); }
-__device__ __forceinline__ float rmax(float v) { return rreduce<float>(v, [](float a, float b) { return fmaxf(a, b); }); }
-__device__ __forceinline__ int rmini(int v) { return rreduce<int>(v, [](int a, int b) { return min(a, b); }); }
-__device__ __forceinline__ int rmaxi(int v) { return rreduce<int>(v, [](int a, int b) { return max(a, b); }); }
+template <int LPW> __device__ __forceinline__ uint32_t rsumu(uint32_t v) {
+  return rreduce<LPW, uint32_t>(v, [](uint32_t a, uint32_t b) { return a + b; });
+}
+template <int LPW> __device__ __forceinline__ float rmin(float v) {
+  return rreduce<LPW, float>(v, [](float a, float b) { return fminf(a, b); });
+}
+template <int LPW> __device__ __forceinline__ float rmax(float v) {
+  return rreduce<LPW, float>(v, [](float a, float b) { return fmaxf(a, b); });
+}
+template <int LPW> __device__ __forceinline__ int rmini(int v) {
+  return rreduce<LPW, int>(v, [](int a, int b) { return min(a, b); });
+}
+template <int LPW> __device__ __forceinline__ int rmaxi(int v) {
+  return rreduce<LPW, int>(v, [](int a, int b) { return max(a, b); });
+}
 
 // MLP = true: the training-input variant — every feature is written as bf16
 // ((isnan(v) ? nan_value : v) - mean[f]) * inv_std[f] into a zero-padded [n_windows][ld_out] row,
@@ -84,7 +99,7 @@ struct Pass2K {
 struct Pass2Acc {
   float ad[3], v2[3], res, cxy, cxz, cyz;
   uint64_t h[3];    // 10 bins x 6 bits (at most 32 samples per lane between flushes)
-  uint32_t pk[3];   // bit j: the sample of iteration kbase + j is a peak
+  uint32_t pk[3];   // shift register of peak flags: bit j <-> iteration kbase + n - 1 - j of an n-iteration chunk
   uint32_t hw[3][5];  // flushed counts, two 16-bit bins per word
   int npk[3], first[3], last[3];
 };
@@ -92,8 +107,7 @@ struct Pass2Acc {
 // One iteration of pass 2 at sample t.  EDGE iterations (the first, and those reaching t >= W - 1)
 // mask samples past the window and exclude t = 0 / t = W - 1 from the peaks.
 template <int A, bool EDGE>
-__device__ __forceinline__ void pass2_step(const float* img, int t, int W, const Pass2K& K, Pass2Acc& a,
-                                           uint32_t bit) {
+__device__ __forceinline__ void pass2_step(const float* img, int t, int W, const Pass2K& K, Pass2Acc& a) {
   bool ok = true, pkok = true;
   int tt = t;
   if constexpr (EDGE) {
@@ -117,17 +131,17 @@ __device__ __forceinline__ void pass2_step(const float* img, int t, int W, const
     const uint64_t inc = (EDGE && !ok) ? 0ull : 1ull;
     a.h[c] += inc << (6 * b);
     const bool peak = x > pv && x >= nv && x > K.thr[c] && pkok;
-    a.pk[c] |= peak ? bit : 0u;
+    a.pk[c] = (a.pk[c] << 1) + (peak ? 1u : 0u);  // one v_addc (pk + pk + carry)
   }
-  const float r = __builtin_sqrtf(fmaf(v[0], v[0], fmaf(v[1], v[1], v[2] * v[2])));
+  const float r = __builtin_amdgcn_sqrtf(fmaf(v[0], v[0], fmaf(v[1], v[1], v[2] * v[2])));  // v_sqrt_f32, no denormal scaling
   a.res += (EDGE && !ok) ? 0.f : r;
   a.cxy = fmaf(d[0], d[1], a.cxy);
   a.cxz = fmaf(d[0], d[2], a.cxz);
   a.cyz = fmaf(d[1], d[2], a.cyz);
 }
 
-// fold the packed counts and peak bits of the 32-iteration chunk starting at kbase
-__device__ __forceinline__ void pass2_flush(Pass2Acc& a, int sub, int kbase) {
+// fold the packed counts and peak bits of the n-iteration chunk starting at kbase
+template <int LPW> __device__ __forceinline__ void pass2_flush(Pass2Acc& a, int sub, int kbase, int n) {
 #pragma unroll
   for (int c = 0; c < 3; ++c) {
     const uint64_t h = a.h[c];
@@ -137,79 +151,30 @@ __device__ __forceinline__ void pass2_flush(Pass2Acc& a, int sub, int kbase) {
     a.h[c] = 0;
     const uint32_t pk = a.pk[c];
     a.npk[c] += __builtin_popcount(pk);
-    const int f = sub + 16 * (kbase + __builtin_ctz(pk | 0x80000000u));
-    const int l = sub + 16 * (kbase + 31 - __builtin_clz(pk | 1u));
+    const int f = sub + LPW * (kbase + n - 1 - (31 - __builtin_clz(pk | 1u)));  // oldest flag: highest bit
+    const int l = sub + LPW * (kbase + n - 1 - __builtin_ctz(pk | 0x80000000u));  // newest: lowest bit
     a.first[c] = pk ? min(a.first[c], f) : a.first[c];
     a.last[c] = pk ? max(a.last[c], l) : a.last[c];
     a.pk[c] = 0;
   }
 }
 
-// One block = `waves` waves = 4 * waves groups = 4 * waves / (A / 3) whole windows (host picks
-// `waves` so that divides).  One-shot: stage, compute, write.
-template <int A, bool MLP>
-__global__ __launch_bounds__(256) void window_features_kernel(const float* __restrict__ stream, int64_t n_samples,
-                                                              int W, int stride, int64_t n_windows,
-                                                              float ms_per_sample, float* __restrict__ out,
-                                                              int ld_out, MlpOut mo) {
-  constexpr int T3 = A / 3;
-  extern __shared__ __attribute__((aligned(16))) float lds[];
-  const int nt = (int)blockDim.x, tid = (int)threadIdx.x;
-  const int wpb = (nt >> 6) * 4 / T3;
-  const int64_t w0 = (int64_t)blockIdx.x * wpb;
-  const int nwin = (int)min<int64_t>(wpb, n_windows - w0);
-  const bool contiguous = stride <= W;
-  const int istride = (contiguous ? stride : W) * A;  // floats between window images in LDS
-  float* img0;
-  // ---- stage the block's windows in LDS ----
-  if (contiguous) {
-    const int64_t s0 = w0 * stride * A;
-    const int64_t len = ((int64_t)(nwin - 1) * stride + W) * A;
-    const int lead = (int)(s0 & 3);
-    float* dst = lds + PAD;  // 16-byte aligned; holds the span from the float4 containing s0
-    img0 = dst + lead;
-    if ((reinterpret_cast<uintptr_t>(stream) & 15) == 0) {
-      const int64_t t4 = n_samples * A >> 2;  // whole float4s of the stream
-      const int64_t a4 = (s0 - lead) >> 2;
-      const int n4 = (int)((lead + len + 3) >> 2);
-      const v4f* s4 = reinterpret_cast<const v4f*>(stream);
-      v4f* d4 = reinterpret_cast<v4f*>(dst);
-      for (int i0 = tid; i0 < n4; i0 += 8 * nt) {
-        v4f r[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {  // unconditional (clamped) loads: eight in flight
-          const int64_t gi = a4 + i0 + j * nt;
-          r[j] = s4[gi < t4 ? gi : t4 - 1];
-        }
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const int i = i0 + j * nt;
-          if (i < n4 && a4 + i < t4) d4[i] = r[j];
-        }
-      }
-      // floats past the stream's last whole float4 (n_samples * A % 4 != 0)
-      for (int64_t e = max(t4 * 4, s0) + tid; e < s0 + len; e += nt) img0[e - s0] = stream[e];
-    } else {
-      for (int64_t e = tid; e < len; e += nt) img0[e] = stream[s0 + e];
-    }
-  } else {  // windows with gaps between them: one image each
-    img0 = lds + PAD;
-    const int n = W * A;
-    for (int i = 0; i < nwin; ++i) {
-      const float* src = stream + (w0 + i) * stride * A;
-      for (int e = tid; e < n; e += nt) img0[i * n + e] = src[e];
-    }
-  }
-  __syncthreads();
-
-  const int lane = tid & 63, sub = lane & 15;
-  const int gl = (tid >> 6) * 4 + (lane >> 4);  // this row's group
-  const int wi = gl / T3, g = gl % T3;
+// The statistics of every (window, triad) group of one staged batch: `img0` holds windows
+// w0 .. w0 + nwin - 1, `pitch` floats apart.
+template <int A, int LPW, bool MLP>
+__device__ __forceinline__ void window_groups(const float* img0, int64_t w0, int nwin, int W, int pitch,
+                                              float ms_per_sample, float* __restrict__ out, int ld_out,
+                                              const MlpOut& mo) {
+  constexpr int T3 = A / 3, GPW = 64 / LPW;
+  const int tid = (int)threadIdx.x;
+  const int lane = tid & 63, sub = lane % LPW;
+  const int wave = tid >> 6, g = wave % T3;
+  const int wi = GPW * (wave / T3) + lane / LPW;
   const bool valid = wi < nwin;
   const int64_t win = w0 + (valid ? wi : 0);
-  const float* img = img0 + (valid ? wi : 0) * istride + 3 * g;  // the group's triad: A floats per sample
-  const int C = (W + 15) >> 4;       // iterations (samples per lane, the last partial)
-  const int kfull = (W - 1) >> 4;    // k < kfull: every t = sub + 16k lies in [0, W - 2]
+  const float* img = img0 + (valid ? wi : 0) * pitch + 3 * g;  // the group's triad: A floats per sample
+  const int C = (W + LPW - 1) / LPW;  // iterations (samples per lane, the last partial)
+  const int kfull = (W - 1) / LPW;    // k < kfull: every t = sub + LPW k lies in [0, W - 2]
   const float invW = 1.f / (float)W;
 
   // ---- pass 1: sum, sum of squares, min, max ----
@@ -221,7 +186,7 @@ __global__ __launch_bounds__(256) void window_features_kernel(const float* __res
     const float* p = img + sub * A;
     int k = 0;
 #pragma unroll 2
-    for (; k < kfull; ++k, p += 16 * A) {
+    for (; k < kfull; ++k, p += LPW * A) {
 #pragma unroll
       for (int c = 0; c < 3; ++c) {
         const float v = p[c];
@@ -229,7 +194,7 @@ __global__ __launch_bounds__(256) void window_features_kernel(const float* __res
       }
     }
     for (; k < C; ++k) {
-      const int t = sub + 16 * k;
+      const int t = sub + LPW * k;
       const bool ok = t < W;
       const float* pp = img + (ok ? t : W - 1) * A;  // a duplicate of a window sample: min / max unchanged
 #pragma unroll
@@ -240,8 +205,8 @@ __global__ __launch_bounds__(256) void window_features_kernel(const float* __res
     }
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
-      mean[c] = rsum(s[c]) * invW; en[c] = rsum(q[c]) * invW;
-      mn[c] = rmin(lo[c]); mx[c] = rmax(hi[c]);
+      mean[c] = rsum<LPW>(s[c]) * invW; en[c] = rsum<LPW>(q[c]) * invW;
+      mn[c] = rmin<LPW>(lo[c]); mx[c] = rmax<LPW>(hi[c]);
     }
   }
 
@@ -260,18 +225,18 @@ __global__ __launch_bounds__(256) void window_features_kernel(const float* __res
     for (int j = 0; j < 5; ++j) a.hw[c][j] = 0;
   }
   a.res = 0.f; a.cxy = 0.f; a.cxz = 0.f; a.cyz = 0.f;
-  pass2_step<A, true>(img, sub, W, K, a, 1u);  // k = 0 holds t = 0
+  pass2_step<A, true>(img, sub, W, K, a);  // k = 0 holds t = 0
   int k = 1;
 #pragma unroll 2
   for (; k < kfull; ++k) {
-    pass2_step<A, false>(img, sub + 16 * k, W, K, a, 1u << (k & 31));
-    if ((k & 31) == 31) pass2_flush(a, sub, k - 31);
+    pass2_step<A, false>(img, sub + LPW * k, W, K, a);
+    if ((k & 31) == 31) pass2_flush<LPW>(a, sub, k - 31, 32);
   }
   for (; k < C; ++k) {
-    pass2_step<A, true>(img, sub + 16 * k, W, K, a, 1u << (k & 31));
-    if ((k & 31) == 31) pass2_flush(a, sub, k - 31);
+    pass2_step<A, true>(img, sub + LPW * k, W, K, a);
+    if ((k & 31) == 31) pass2_flush<LPW>(a, sub, k - 31, 32);
   }
-  if (C & 31) pass2_flush(a, sub, (C - 1) & ~31);
+  if (C & 31) pass2_flush<LPW>(a, sub, C & ~31, C & 31);
 
   // ---- reduce + write ----
   float* o = MLP ? nullptr : out + win * (int64_t)ld_out;
@@ -288,7 +253,7 @@ __global__ __launch_bounds__(256) void window_features_kernel(const float* __res
   constexpr int F = 17 * A + 4 * T3;
   if constexpr (MLP) {  // zero the pad columns of the row (triad 0's group)
     if (g == 0)
-      for (int f = F + sub; f < ld_out; f += 16)
+      for (int f = F + sub; f < ld_out; f += LPW)
         if (valid) ob[f] = 0;
   }
   const int off_avg = A * NB, off_peak = off_avg + A, off_abs = off_peak + A, off_std = off_abs + A;
@@ -298,22 +263,30 @@ __global__ __launch_bounds__(256) void window_features_kernel(const float* __res
 #pragma unroll
   for (int c = 0; c < 3; ++c) {
     const int ax = 3 * g + c;
-    const float ad = rsum(a.ad[c]) * invW;
-    const float var = rsum(a.v2[c]) * invW;
-    sd[c] = sqrtf(var);
-    const int npk = (int)rsumu((uint32_t)a.npk[c]);
-    const int first = rmini(a.first[c]), last = rmaxi(a.last[c]);
-    // bins: lane `sub` < 10 writes bin `sub` (its word picked by a select chain, not an indexed array)
-    uint32_t word = 0;
+    const float ad = rsum<LPW>(a.ad[c]) * invW;
+    const float var = rsum<LPW>(a.v2[c]) * invW;
+    sd[c] = __builtin_amdgcn_sqrtf(var);
+    const int npk = (int)rsumu<LPW>((uint32_t)a.npk[c]);
+    const int first = rmini<LPW>(a.first[c]), last = rmaxi<LPW>(a.last[c]);
+    // bins: lane `sub` writes bin `sub` (and lanes 0, 1 of 8-lane groups bins 8, 9); the word is
+    // picked by a select chain, not an indexed register array
+    uint32_t hw[5];
 #pragma unroll
-    for (int j = 0; j < 5; ++j) {
-      const uint32_t wj = rsumu(a.hw[c][j]);
-      word = (sub >> 1) == j ? wj : word;
+    for (int j = 0; j < 5; ++j) hw[j] = rsumu<LPW>(a.hw[c][j]);
+    {
+      uint32_t word = hw[0];
+#pragma unroll
+      for (int j = 1; j < 5; ++j) word = (sub >> 1) == j ? hw[j] : word;
+      const uint32_t cnt = (sub & 1) ? word >> 16 : word & 0xffffu;
+      emit(sub < NB, ax * NB + sub, (float)cnt * invW);
     }
-    const uint32_t cnt = (sub & 1) ? word >> 16 : word & 0xffffu;
-    emit(sub < NB, ax * NB + sub, (float)cnt * invW);
+    if constexpr (LPW < NB) {
+      const uint32_t cnt = (sub & 1) ? hw[4] >> 16 : hw[4] & 0xffffu;
+      emit(sub < NB - LPW, ax * NB + LPW + sub, (float)cnt * invW);
+    }
     // scalars: lanes 0..6
-    const float peak = npk >= 2 ? (float)(last - first) / (float)(npk - 1) * ms_per_sample : NAN;
+    const float peak =
+        npk >= 2 ? (float)(last - first) * __builtin_amdgcn_rcpf((float)(npk - 1)) * ms_per_sample : NAN;
     float v = mean[c];
     int f = off_avg + ax;
     v = sub == 1 ? peak : v;       f = sub == 1 ? off_peak + ax : f;
@@ -326,11 +299,11 @@ __global__ __launch_bounds__(256) void window_features_kernel(const float* __res
   }
   // triad: resultant (lane 0) and the three correlations (lanes 1..3)
   {
-    const float res = rsum(a.res) * invW;
-    const float cxy = rsum(a.cxy) * invW, cxz = rsum(a.cxz) * invW, cyz = rsum(a.cyz) * invW;
-    const float rxy = (sd[0] > 0.f && sd[1] > 0.f) ? cxy / (sd[0] * sd[1]) : 0.f;
-    const float rxz = (sd[0] > 0.f && sd[2] > 0.f) ? cxz / (sd[0] * sd[2]) : 0.f;
-    const float ryz = (sd[1] > 0.f && sd[2] > 0.f) ? cyz / (sd[1] * sd[2]) : 0.f;
+    const float res = rsum<LPW>(a.res) * invW;
+    const float cxy = rsum<LPW>(a.cxy) * invW, cxz = rsum<LPW>(a.cxz) * invW, cyz = rsum<LPW>(a.cyz) * invW;
+    const float rxy = (sd[0] > 0.f && sd[1] > 0.f) ? cxy * __builtin_amdgcn_rcpf(sd[0] * sd[1]) : 0.f;
+    const float rxz = (sd[0] > 0.f && sd[2] > 0.f) ? cxz * __builtin_amdgcn_rcpf(sd[0] * sd[2]) : 0.f;
+    const float ryz = (sd[1] > 0.f && sd[2] > 0.f) ? cyz * __builtin_amdgcn_rcpf(sd[1] * sd[2]) : 0.f;
     float v = res;
     int f = off_res + g;
     v = sub == 1 ? rxy : v;  f = sub == 1 ? off_corr + 3 * g : f;
@@ -340,32 +313,240 @@ __global__ __launch_bounds__(256) void window_features_kernel(const float* __res
   }
 }
 
+// One block = `waves` waves = 4 * waves groups = 4 * waves / (A / 3) whole windows (host picks
+// `waves` as a multiple of A / 3).  Wave v takes triad v % (A / 3) of the four windows
+// 4 (v / (A / 3)) .. + 3, one per row.  Every window gets its own LDS image, `pitch` floats apart:
+// with pitch = 16 A (mod 64) dwords the four rows of a wave (same triad, consecutive images)
+// read disjoint bank sets — lane banks A * sub + r * pitch are distinct over the 64 lanes for odd A
+// (the host picks the pitch).  One-shot: stage, compute, write.
+template <int A, int LPW, bool MLP>
+__global__ __launch_bounds__(256) void window_features_kernel(const float* __restrict__ stream, int64_t n_samples,
+                                                              int W, int stride, int64_t n_windows,
+                                                              float ms_per_sample, float* __restrict__ out,
+                                                              int ld_out, MlpOut mo, int pitch) {
+  constexpr int T3 = A / 3, GPW = 64 / LPW;  // groups per wave
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int nt = (int)blockDim.x, tid = (int)threadIdx.x;
+  const int wpb = (nt >> 6) * GPW / T3;
+  const int64_t w0 = (int64_t)blockIdx.x * wpb;
+  const int nwin = (int)min<int64_t>(wpb, n_windows - w0);
+  float* img0 = lds + PAD;
+  // ---- stage the block's windows in LDS ----
+  const int n = W * A;
+  if ((reinterpret_cast<uintptr_t>(stream) & 15) == 0 && ((int64_t)stride * A) % 4 == 0 &&
+      (int64_t)stride * A * nwin < 0x7fffffff) {
+    // every window starts on a float4: 16-byte loads, eight in flight per thread
+    const int64_t t4 = n_samples * A >> 2;  // whole float4s of the stream
+    const int n4 = (n + 3) >> 2;            // float4s per window (the last may run past it: pitch >= that)
+    const int tot = nwin * n4;
+    const v4f* s4 = reinterpret_cast<const v4f*>(stream);
+    const int64_t g40 = w0 * stride * A >> 2;
+    const int gs4 = stride * A >> 2;
+    const int p4 = pitch >> 2;
+    v4f* d4 = reinterpret_cast<v4f*>(img0);
+    // flat float4 index f -> (window i, float4 j): i = umulhi(f, magic) is exact for f * n4 < 2^32
+    const uint32_t magic = 0xffffffffu / (uint32_t)n4 + 1u;
+    const int64_t lim = t4 - g40;  // relative float4 indices at or past this are outside the stream
+    const int rlim = (int)min<int64_t>(lim, 0x7fffffff);
+    const v4f* sb = s4 + g40;
+    for (int f0 = tid; f0 < tot; f0 += 8 * nt) {
+      v4f r[8];
+      int rel[8], di[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int f = f0 + u * nt;
+        const int i = (int)__umulhi((uint32_t)f, magic), j = f - i * n4;
+        rel[u] = i * gs4 + j;
+        di[u] = i * p4 + j;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) r[u] = sb[rel[u] < rlim ? rel[u] : rlim - 1];  // unconditional (clamped) loads
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (f0 + u * nt < tot && rel[u] < rlim) d4[di[u]] = r[u];
+    }
+    // floats past the stream's last whole float4 (n_samples * A % 4 != 0): the last window only
+    const int64_t last0 = (w0 + nwin - 1) * stride * A;
+    for (int64_t e = max(t4 * 4, last0) + tid; e < last0 + n; e += nt) img0[(nwin - 1) * pitch + (e - last0)] = stream[e];
+  } else {
+    for (int i = 0; i < nwin; ++i) {
+      const float* src = stream + (w0 + i) * stride * A;
+      for (int e = tid; e < n; e += nt) img0[i * pitch + e] = src[e];
+    }
+  }
+  __syncthreads();
+
+  window_groups<A, LPW, MLP>(img0, w0, nwin, W, pitch, ms_per_sample, out, ld_out, mo);
+}
+
+// Persistent variant (16-byte aligned window starts): each block walks batches b, b + grid, ...
+// of `wpb` windows.  The NEXT batch is loaded into NR float4 registers per thread while the
+// current one is computed from LDS, so the HBM latency of a batch hides behind the statistics of
+// the previous one instead of being paid by every block up front (one-shot blocks: stage, then
+// compute, with only four or two blocks per CU).  Loads are unconditional (clamped into the
+// stream) so their waits stay counted; the host picks NR >= float4s per batch / threads.
+template <int A, int LPW, bool MLP, int NR>
+__global__ __launch_bounds__(256) void window_features_persistent_kernel(
+    const float* __restrict__ stream, int64_t n_samples, int W, int stride, int64_t n_windows, float ms_per_sample,
+    float* __restrict__ out, int ld_out, MlpOut mo, int pitch) {
+  constexpr int T3 = A / 3, GPW = 64 / LPW;
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int nt = (int)blockDim.x, tid = (int)threadIdx.x;
+  const int wpb = (nt >> 6) * GPW / T3;
+  const int64_t nbatch = (n_windows + wpb - 1) / wpb;
+  float* img0 = lds + PAD;
+  v4f* d4 = reinterpret_cast<v4f*>(img0);
+  const int n = W * A, n4 = (n + 3) >> 2, p4 = pitch >> 2, gs4 = stride * A >> 2;
+  // non-overlapping windows with unpadded images: float4 f of a batch is float4 f of its image
+  // span in the stream AND in LDS — no (window, offset) split per float4
+  const bool flat = stride == W && pitch == n;
+  const int64_t t4 = n_samples * A >> 2;  // whole float4s of the stream
+  const v4f* s4 = reinterpret_cast<const v4f*>(stream);
+  const uint32_t magic = 0xffffffffu / (uint32_t)n4 + 1u;  // f / n4 = umulhi(f, magic) for f * n4 < 2^32
+  const int totmax = wpb * n4;
+  int64_t b = blockIdx.x;
+  if (b >= nbatch) return;  // block-uniform; no barrier reached
+  // (stream, LDS) float4 offsets of this thread's u-th float4 of a batch; slots past the batch
+  // re-load slot 0 (cache hits).  Recomputed per use behind an opaque copy of tid: held, they
+  // would cost two VGPRs per float4.
+  int tid_ = tid;
+  auto offs = [&](int u, int& rel, int& di) {
+    const int f0 = tid_ + u * nt, f = f0 < totmax ? f0 : tid_;
+    if (flat) {
+      rel = f; di = f;
+    } else {
+      const int i = (int)__umulhi((uint32_t)f, magic), j = f - i * n4;
+      rel = i * gs4 + j; di = i * p4 + j;
+    }
+  };
+  auto base = [&](int64_t batch, int& rlim) {
+    const int64_t g40 = batch * wpb * (int64_t)stride * A >> 2;
+    rlim = (int)min<int64_t>(t4 - g40, 0x7fffffff);
+    return s4 + g40;
+  };
+  v4f r[NR];
+  {
+    asm volatile("" : "+v"(tid_));
+    int rlim;
+    const v4f* sb = base(b, rlim);
+#pragma unroll
+    for (int u = 0; u < NR; ++u) {
+      int rel, di;
+      offs(u, rel, di);
+      r[u] = sb[rel < rlim ? rel : rlim - 1];  // unconditional (clamped) loads: counted waits
+    }
+  }
+  for (; b < nbatch; b += gridDim.x) {
+    const int64_t w0 = b * wpb;
+    const int nwin = (int)min<int64_t>(wpb, n_windows - w0);
+    const int tot = nwin * n4;
+    const bool more = b + gridDim.x < nbatch;
+    {
+      asm volatile("" : "+v"(tid_));
+      int rlim, rlim_n;
+      base(b, rlim);
+      const v4f* sbn = base(more ? b + gridDim.x : b, rlim_n);
+      // store this batch's float4 u, then reuse its registers for the next batch's float4 u (the
+      // last batch re-loads itself: cache hits)
+#pragma unroll
+      for (int u = 0; u < NR; ++u) {
+        int rel, di;
+        offs(u, rel, di);
+        if (tid + u * nt < tot && rel < rlim) d4[di] = r[u];
+        r[u] = sbn[rel < rlim_n ? rel : rlim_n - 1];  // unconditional: a conditional load would drain vmcnt
+      }
+      // floats past the stream's last whole float4 (n_samples * A % 4 != 0): the last window only
+      const int64_t last0 = (w0 + nwin - 1) * stride * A;
+      for (int64_t e = max(t4 * 4, last0) + tid; e < last0 + n; e += nt)
+        img0[(nwin - 1) * pitch + (e - last0)] = stream[e];
+    }
+    __syncthreads();
+    window_groups<A, LPW, MLP>(img0, w0, nwin, W, pitch, ms_per_sample, out, ld_out, mo);
+    __syncthreads();  // every wave is done with the images before they are overwritten
+  }
+}
+
+int cu_count() {
+  static int n = 0;
+  if (!n) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                                 hipSuccess || n <= 0)
+      n = 256;
+  }
+  return n;
+}
+
 template <int A, bool MLP>
 int launch_axes(const float* stream, int64_t n_samples, int window, int stride, int64_t n_windows, float ms,
                 float* out, int ld_out, MlpOut mo, hipStream_t s) {
   constexpr int T3 = A / 3;
-  const bool contiguous = stride <= window;
-  auto lds_bytes = [&](int wpb) -> int64_t {
-    const int64_t span = contiguous ? ((int64_t)(wpb - 1) * stride + window) * A : (int64_t)wpb * window * A;
-    return (PAD + 4 + span + SLACK) * (int64_t)sizeof(float);
+  // image pitch: 16 A (mod 64) dwords for odd A (conflict-free rows, see the kernel); 32 (mod 64)
+  // for A = 6 (even A only ever reaches even banks: rows one image apart stay disjoint)
+  const int n = window * A;
+  // do the 64 lanes of a wave (rows one image apart, lanes A floats apart) hit 64 distinct banks?
+  auto conflict_free = [&](int lpw, int pitch) {
+    uint64_t seen = 0;
+    for (int l = 0; l < 64; ++l) {
+      const uint64_t bit = 1ull << (((l / lpw) * pitch + (l % lpw) * A) & 63);
+      if (seen & bit) return false;
+      seen |= bit;
+    }
+    return true;
   };
-  // waves per block: 4 * waves groups must be whole windows (T3 = 3: three waves = four windows);
-  // otherwise the most waves whose span stays within 64 KB (three or more blocks per CU)
-  int waves = 0;
-  if constexpr (T3 == 3) {
-    if (lds_bytes(4) <= 160 * 1024) waves = 3;
-  } else {
-    for (int w = 4; w >= 1 && !waves; w >>= 1)
-      if (lds_bytes(4 * w / T3) <= 64 * 1024 || (w == 1 && lds_bytes(4 / T3) <= 160 * 1024)) waves = w;
+  auto pitch_for = [&](int lpw) {
+    // contiguous images (flat staging, see the persistent kernel) unless that costs bank conflicts
+    if (stride == window && n % 4 == 0 && (conflict_free(lpw, n) || A % 2 == 0)) return n;
+    const int want = (A % 2) ? (lpw * A) % 64 : 32;
+    return n + (((want - n) % 64) + 64) % 64;
+  };
+  auto lds_bytes = [&](int wpb, int pitch) -> int64_t {
+    return (PAD + (int64_t)wpb * pitch + SLACK) * (int64_t)sizeof(float);
+  };
+  const bool vec = (reinterpret_cast<uintptr_t>(stream) & 15) == 0 && ((int64_t)stride * A) % 4 == 0;
+  // one block's launch: persistent + register-prefetched when the window starts are 16-byte
+  // aligned and a batch fits 24 float4 registers per thread (two waves per SIMD), else one-shot
+  auto launch = [&](auto lpw_c, int waves, int pitch) -> int {
+    constexpr int LPW = decltype(lpw_c)::value;
+    const int wpb = waves * (64 / LPW) / T3, nt = 64 * waves;
+    const int64_t bytes = lds_bytes(wpb, pitch);
+    const int64_t nbatch = (n_windows + wpb - 1) / wpb;
+    const int per = (int)((wpb * (int64_t)((n + 3) / 4) + nt - 1) / nt);  // float4s per thread per batch
+    if (vec && per <= 24 && (int64_t)stride * A * wpb < 0x7fffffff) {
+      const int64_t resident = std::max<int64_t>(1, std::min<int64_t>(8, (160 * 1024) / bytes));
+      const unsigned grid = (unsigned)std::min<int64_t>(nbatch, resident * cu_count());
+#define HAR_WIN_P(NR)                                                                              \
+  window_features_persistent_kernel<A, LPW, MLP, NR><<<grid, nt, (size_t)bytes, s>>>(              \
+      stream, n_samples, window, stride, n_windows, ms, out, ld_out, mo, pitch)
+      if (per <= 8) HAR_WIN_P(8);
+      else if (per <= 16) HAR_WIN_P(16);
+      else HAR_WIN_P(24);
+#undef HAR_WIN_P
+    } else {
+      window_features_kernel<A, LPW, MLP><<<(unsigned)nbatch, nt, (size_t)bytes, s>>>(
+          stream, n_samples, window, stride, n_windows, ms, out, ld_out, mo, pitch);
+    }
+    HAR_CHECK_LAUNCH();
+    return 0;
+  };
+  // 8-lane groups (half the reduction and write-out work per window) when two waves' sixteen
+  // 3-axis windows fit 64 KB — the short-window WISDM case; else 16-lane groups
+  if constexpr (A == 3) {
+    if (lds_bytes(16, pitch_for(8)) <= 64 * 1024) return launch(std::integral_constant<int, 8>{}, 2, pitch_for(8));
   }
+  const int pitch = pitch_for(16);
+  // waves per block: a multiple of T3 (whole windows); the most whose images fit 64 KB (three or
+  // more blocks per CU), else the fewest if they fit the 160 KB LDS
+  int waves = 0;
+  for (int w = 4; w >= 1; --w) {
+    if (w % T3) continue;
+    if (lds_bytes(4 * w / T3, pitch) <= 64 * 1024) { waves = w; break; }
+  }
+  if (!waves && lds_bytes(4, pitch) <= 160 * 1024) waves = T3;
   if (!waves) return -5;  // one block's windows do not fit the LDS
-  const int wpb = 4 * waves / T3;
-  const int64_t blocks = (n_windows + wpb - 1) / wpb;
-  window_features_kernel<A, MLP><<<(unsigned)blocks, 64 * waves, (size_t)lds_bytes(wpb), s>>>(
-      stream, n_samples, window, stride, n_windows, ms, out, ld_out, mo);
-  HAR_CHECK_LAUNCH();
-  return 0;
+  return launch(std::integral_constant<int, 16>{}, waves, pitch);
 }
+
 
 }  // namespace
 
