@@ -125,9 +125,9 @@ def bench_mlp(args, ctx):
         j = i % nb
         eng.train_step(Xin[j * B:(j + 1) * B], y32[j * B:(j + 1) * B], global_batch)
 
-    # default eager: the step is GPU-bound (eager 0.168 ms vs one-graph replay 0.173 ms per step on
-    # MI355X, profiles/bench_mlp_graph_modes.md) and in DP the eager step overlaps the bucketed
-    # RCCL all-reduce with backward, which a captured graph cannot
+    # default eager: the three-kernel step is GPU-bound (round 2 on MI355X, 200 steps: eager
+    # 0.0821 / 0.0825 ms, whole-step graph 0.0860 / 0.0872 ms, segmented graphs 0.0930 ms), and in
+    # DP the one flat all-reduce sits between the reduction and Adam kernels
     mode = args.graph if args.graph >= 0 else 0
     graphs = None
     if eng.native and mode == 1:  # whole step (collective included) in one graph per slot
