@@ -265,6 +265,17 @@ class ForestBuilder:
 
 
 GROUP_MAX_NT = 4096  # tree_level.hip: per-tree candidates a level grouping keeps in LDS
+# Bounds of a level enqueued without reading its counts back (the kernels read the real counts from
+# the device; arrays and grids are sized by these bounds): node-count bound, and the bound times
+# the grouping's row chunks (its count workspace).
+ASYNC_MAX_NODES = 1 << 22
+ASYNC_MAX_COUNT_WS = 1 << 27
+# Sibling subtraction (trees that search every feature at every node: DecisionTree, featureSubset
+# "all"): per-level histogram store cap in bytes; a level whose store would exceed it histograms
+# every node directly.  With per-node random feature subsets (RandomForest sqrt / log2 / onethird)
+# a child's features are not its parent's, so there is no parent histogram to subtract from.
+SUBTRACT_MAX_BYTES = 4 << 30
+SIBLING_SUBTRACTION = True
 
 
 # Test hook: when True the level loop groups rows with the stable radix sort of the level keys
@@ -273,20 +284,30 @@ FORCE_SORT_GROUPING = False
 # Test hook: when True a single-device level runs one workgroup per node (hist_split_native)
 # instead of the row-balanced plan (hist_split_planned); both grow the same forest.
 FORCE_NODE_BLOCKS = False
+# Test hook: when True every level reads its counts back (one 16-byte D2H per level) instead of
+# running on device-side counts; both grow the same forest.
+FORCE_LEVEL_SYNC = False
 
 
 def _levels_device_frontier(b: "ForestBuilder", y32, W, N: int, F: int, m: int, maxn: int, stats, feature, thresh,
                             left, right, gains, n_nodes, node_of, bad):
-    """Device level loop with the frontier resident on the GPU and ONE 16-byte device -> host
-    read per level (splits, next candidates, max candidates per tree, max candidate weight).
+    """Device level loop with the frontier resident on the GPU.
 
     Per level (tree_level.hip unless noted): stable counting-sort grouping of the (tree, row)
     pairs by candidate node; Floyd feature subsets; the fused histogram + split kernel
     (tree.hip); the split / child-candidacy decision; the frontier update (split slots by a
     scan, child ids per tree, next candidates by a second scan, their cand_idx entries and tree
-    starts); the commit of every split and both children's stats; the row partition.  The
-    host does no per-level numpy work and uploads nothing; it grows the forest the
-    host-frontier loop (``_levels_native_impl``) grows, node for node."""
+    starts); the commit of every split and both children's stats; the row partition.
+
+    Counts on the device: the frontier kernel writes each level's [splits, next candidates, max
+    candidates per tree, max candidate weight] into its own row of ``scal_all``; the next level's
+    kernels read the candidate count from there (``a_dev``) while the host sizes grids and arrays
+    by a bound (next candidates <= 2 x this level's, per tree <= 2 x the per-tree maximum).  On one
+    device the whole fit is therefore enqueued with no device -> host read until the final node
+    counts.  A level whose bound would exceed ``ASYNC_MAX_NODES`` / ``ASYNC_MAX_COUNT_WS`` or the
+    grouping's LDS (``GROUP_MAX_NT`` per tree), and every level of a data-parallel fit (the
+    collectives are sized on the host), first reads the previous level's 16 bytes back — the
+    kernels then get the exact counts.  Both modes grow the same forest node for node."""
     dev = W.device
     Tn, K, D = b.T, b.K, b.D
     mod = _native.kernels()
@@ -295,6 +316,11 @@ def _levels_device_frontier(b: "ForestBuilder", y32, W, N: int, F: int, m: int, 
     Wf = W.reshape(-1).contiguous()
     bins_rm = b.bins.t().contiguous()  # [N, F] for the histogram gathers (partition keeps [F, N])
     nch = mod.tree_level_group_chunks(N)
+    planned = b.owner is None and b.allreduce is None and not FORCE_NODE_BLOCKS
+    async_ok = planned and not FORCE_SORT_GROUPING and not FORCE_LEVEL_SYNC
+    slot_bytes = 4 * F * b.max_bins * K
+    subtract = planned and m >= F and SIBLING_SUBTRACTION
+    hprev = parent_of = derive_from = None  # the previous level's store and this level's derive info
 
     # the root class counts and the label check in ONE device -> host read; root candidacy on the
     # host in fp64 (the device decision kernel's rule: impurity > 1e-12, weight >= 2 minInstances)
@@ -318,6 +344,7 @@ def _levels_device_frontier(b: "ForestBuilder", y32, W, N: int, F: int, m: int, 
     cn = torch.zeros(A, **i32)
     tlo = torch.from_numpy(np.concatenate([[0], np.cumsum(c0.astype(np.int64))]).astype(np.int32)).to(dev)
     nt_max = 1
+    exact = True  # A / nt_max are this level's exact counts (else bounds; the counts live in scal_all)
     cand_idx = torch.full((Tn, maxn), -1, **i32)  # stale entries name nodes no row sits in any more
     cand_idx[ct.long(), 0] = torch.arange(A, **i32)
     nn = torch.from_numpy(n_nodes.astype(np.int32)).to(dev)
@@ -326,19 +353,21 @@ def _levels_device_frontier(b: "ForestBuilder", y32, W, N: int, F: int, m: int, 
     rows_buf = torch.empty(Tn * N, **i32)
     roww_buf = torch.empty(Tn * N, dtype=torch.float32, device=dev)
     tlo_next = torch.empty(Tn + 1, **i32)
-    scal = torch.zeros(4, **i32)
+    scal_all = torch.zeros(4 * (D + 1), **i32)
     scal_h = torch.empty(4, dtype=torch.int32).pin_memory()
     cnt_ws = None
     for depth in range(D):
+        a_dev = 0 if exact else scal_all.data_ptr() + 4 * (4 * depth + 1)
+        scal = scal_all[4 * (depth + 1):4 * (depth + 2)]
         if cnt_ws is None or cnt_ws.numel() < nch * A:
             cnt_ws = torch.empty(nch * max(A, 2 * Tn), **i32)
         counts, starts = torch.empty(A, **i32), torch.empty(A, **i32)
         if nt_max <= GROUP_MAX_NT and not FORCE_SORT_GROUPING:
             mod.tree_level_group(node_of.data_ptr(), cand_idx.data_ptr(), tlo.data_ptr(), Wf.data_ptr(), Tn, N,
                                  maxn, A, nt_max, cnt_ws.data_ptr(), counts.data_ptr(), starts.data_ptr(),
-                                 rows_buf.data_ptr(), roww_buf.data_ptr(), st)
+                                 rows_buf.data_ptr(), roww_buf.data_ptr(), a_dev, st)
             rows, row_w = rows_buf, roww_buf
-        else:  # a tree with > GROUP_MAX_NT candidates: the same order from a stable radix sort
+        else:  # a tree with > GROUP_MAX_NT candidates (exact level): a stable radix sort of the keys
             key = torch.empty(Tn * N, **i32)
             mod.tree_level_keys(node_of.data_ptr(), cand_idx.data_ptr(), Tn, N, maxn, key.data_ptr(), st)
             keys, order = torch.sort(key, stable=True)
@@ -351,11 +380,16 @@ def _levels_device_frontier(b: "ForestBuilder", y32, W, N: int, F: int, m: int, 
         else:
             feats = torch.empty(A, m, **i32)
             tr = ct + b.tree_offset if b.tree_offset else ct
-            mod.tree_feature_subsets(b.seed, tr.data_ptr(), cn.data_ptr(), A, F, m, feats.data_ptr(), st)
-        if b.owner is None and b.allreduce is None and not FORCE_NODE_BLOCKS:
+            mod.tree_feature_subsets(b.seed, tr.data_ptr(), cn.data_ptr(), A, F, m, feats.data_ptr(), a_dev, st)
+        store = None
+        if subtract and A * slot_bytes <= SUBTRACT_MAX_BYTES:
+            store = torch.empty(A * slot_bytes // 4, dtype=torch.float32, device=dev)
+        if planned:
             # one device: work items by rows (big nodes chunked), no host sync (ops/tree.py)
             res = T.hist_split_planned(b.bins, b.nbins, y32, rows, row_w, starts, counts, feats, K, b.max_bins,
-                                       b.min_inst, b.min_gain, b.impurity, rows_bound=Tn * N, bins_rm=bins_rm)
+                                       b.min_inst, b.min_gain, b.impurity, rows_bound=Tn * N, bins_rm=bins_rm,
+                                       a_dev=a_dev, store=store, hprev=hprev, derive_from=derive_from,
+                                       parent_of=parent_of)
         else:
             res = T.hist_split_native(b.bins, b.nbins, y32, rows, row_w, starts, counts, feats, K, b.max_bins,
                                       b.min_inst, b.min_gain, b.impurity,
@@ -365,32 +399,46 @@ def _levels_device_frontier(b: "ForestBuilder", y32, W, N: int, F: int, m: int, 
                             left=res.left.contiguous(), total=res.total.contiguous())
         dec = torch.empty(5, A, dtype=torch.float32, device=dev)
         mod.tree_level_decide(A, res.gain.data_ptr(), res.left.data_ptr(), res.total.data_ptr(), K, b.impurity,
-                              float(2 * b.min_inst), dec.data_ptr(), st)
+                              float(2 * b.min_inst), dec.data_ptr(), a_dev, st)
         pos = torch.empty(A + 1, **i32)
         ti, ni, cl, dsi = (torch.empty(A, dtype=torch.int64, device=dev) for _ in range(4))
         front = torch.empty(2 * A, dtype=torch.float32, device=dev)
         q = torch.empty(2 * A + 1, **i32)
         ct_next, cn_next = torch.empty(2 * A, **i32), torch.empty(2 * A, **i32)
+        A_b = min(2 * A, Tn * N)
+        # the next level derives siblings when this level kept its histograms and the next one can
+        derive = store is not None and A_b * slot_bytes <= SUBTRACT_MAX_BYTES
+        par_n = torch.empty(2 * A, **i32) if derive else None
+        der_n = torch.empty(2 * A, **i32) if derive else None
         mod.tree_frontier(A, Tn, maxn, ct.data_ptr(), cn.data_ptr(), tlo.data_ptr(), dec.data_ptr(), nn.data_ptr(),
                           nn_next.data_ptr(), pos.data_ptr(), ti.data_ptr(), ni.data_ptr(), cl.data_ptr(),
                           dsi.data_ptr(), front.data_ptr(), q.data_ptr(), ct_next.data_ptr(), cn_next.data_ptr(),
-                          tlo_next.data_ptr(), cand_idx.data_ptr(), scal.data_ptr(), st)
-        scal_h.copy_(scal)  # the level's one sync
-        S, A_next, nt_next, wbits = (int(v) for v in scal_h.tolist())
-        if S == 0:
-            break
+                          tlo_next.data_ptr(), cand_idx.data_ptr(), scal.data_ptr(), a_dev,
+                          par_n.data_ptr() if derive else 0, der_n.data_ptr() if derive else 0, st)
+        stay_async = (async_ok and depth + 1 < D and A_b <= ASYNC_MAX_NODES and nch * A_b <= ASYNC_MAX_COUNT_WS
+                      and 2 * nt_max <= GROUP_MAX_NT)
+        if stay_async:  # the next level runs on the device counts in scal
+            S, s_dev, A_next, nt_next = A, scal.data_ptr(), A_b, 2 * nt_max
+        else:
+            scal_h.copy_(scal)  # this level's one sync
+            S, A_next, nt_next, wbits = (int(v) for v in scal_h.tolist())
+            s_dev = 0
+            max_w = float(np.array([wbits], dtype=np.int32).view(np.float32)[0])
+            if S == 0:
+                break
         mod.tree_commit_level(S, ti.data_ptr(), ni.data_ptr(), cl.data_ptr(), dsi.data_ptr(), res.feat.data_ptr(),
                               res.bin.data_ptr(), res.gain.data_ptr(), res.left.data_ptr(), res.total.data_ptr(), K,
                               b.thr_mat.data_ptr(), b.thr_mat.shape[1], maxn, feature.data_ptr(),
                               split_bin.data_ptr(), thresh.data_ptr(), left.data_ptr(), right.data_ptr(),
-                              gains.data_ptr(), stats.data_ptr(), st)
+                              gains.data_ptr(), stats.data_ptr(), s_dev, st)
         mod.tree_partition_split(node_of.data_ptr(), feature.data_ptr(), split_bin.data_ptr(), left.data_ptr(),
                                  b.bins.data_ptr(), Tn, N, maxn, st)
         nn, nn_next = nn_next, nn
         ct, cn, A = ct_next[:A_next], cn_next[:A_next], A_next
         tlo, tlo_next = tlo_next, tlo
         nt_max = max(nt_next, 1)
-        max_w = float(np.array([wbits], dtype=np.int32).view(np.float32)[0])
+        exact = not stay_async
+        hprev, parent_of, derive_from = (store, par_n, der_n) if derive else (None, None, None)
         if A == 0:
             break
     n_nodes[:] = nn.cpu().numpy()

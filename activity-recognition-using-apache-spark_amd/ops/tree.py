@@ -326,7 +326,8 @@ PLAN_ROWS = 2048  # rows per work item of a load-balanced level (larger nodes ar
 
 def hist_split_planned(bins, nbins_feat, label, rows, row_w, node_start, node_count, feats, K, max_bins,
                        min_instances, min_info_gain, impurity, rows_bound: int, bins_rm=None,
-                       prows: int = PLAN_ROWS) -> LevelResult:
+                       prows: int = PLAN_ROWS, a_dev: int = 0, store=None, hprev=None, derive_from=None,
+                       parent_of=None) -> LevelResult:
     """Load-balanced fused histogram + split for one level on one device (no host sync).
 
     Work is split by ROWS, not by node: a node of <= ``prows`` rows is one work item (fused LDS
@@ -335,7 +336,15 @@ def hist_split_planned(bins, nbins_feat, label, rows, row_w, node_start, node_co
     exact in any order), followed by one split-search pass over the merged big nodes.  Without it a
     level's time is its largest node's: the deep levels of a forest keep a few nodes of tens of
     thousands of rows beside thousands of small ones.  ``rows_bound`` bounds the level's total
-    rows (grid sizes are upper bounds; surplus workgroups exit on the device-side counts)."""
+    rows (grid sizes are upper bounds; surplus workgroups exit on the device-side counts).
+    ``a_dev`` (a device pointer, 0 = none) holds the level's real node count; ``feats.shape[0]``
+    is then only a bound, so the level needs no host-known node count at all.
+
+    Sibling subtraction: with ``store`` (a [A, m, max_bins, K] fp32 buffer) every node's histogram
+    is kept there for the next level; with ``derive_from`` / ``parent_of`` (the previous level's
+    frontier output) and ``hprev`` (the previous level's store) the nodes marked
+    ``derive_from[a] >= 0`` — the heavier of two candidate siblings, whose rows the grouping skipped —
+    take parent - sibling instead of a pass over their rows (exact: integer-valued weights)."""
     A, m = feats.shape
     F, N = bins.shape
     fc = max(1, min(m, LDS_BUDGET // (max_bins * K * 4)))
@@ -350,16 +359,24 @@ def hist_split_planned(bins, nbins_feat, label, rows, row_w, node_start, node_co
     max_big = max(1, min(A, rows_bound // (prows + 1)))
     plan = torch.empty(4 + (A + 1) + 3 * A + items_ub, dtype=torch.int32, device=dev)
     slot = m * max_bins * K
-    ghist = torch.empty(max_big * slot, dtype=torch.float32, device=dev)
+    by_node = store is not None
+    ghist = store if by_node else torch.empty(max_big * slot, dtype=torch.float32, device=dev)
     mod, st = _native.kernels(), _native.stream_ptr()
-    mod.tree_plan(node_count.data_ptr(), A, prows, plan.data_ptr(), slot, ghist.data_ptr(), max_big, st)
+    mod.tree_plan(node_count.data_ptr(), A, prows, plan.data_ptr(), slot, ghist.data_ptr(), max_big, int(by_node),
+                  a_dev, st)
     bptr, row_major = (bins_rm.data_ptr(), 1) if bins_rm is not None else (bins.data_ptr(), 0)
     args = [bptr, N, F, row_major, nbins_feat.data_ptr(), rows.data_ptr(), row_w.data_ptr(), node_start.data_ptr(),
             node_count.data_ptr(), A, feats.data_ptr(), m, fc, label.data_ptr(), K, max_bins, float(min_instances),
             float(min_info_gain), impurity, gain.data_ptr(), feat.data_ptr(), bin_.data_ptr(), left.data_ptr(),
             total.data_ptr()]
-    mod.tree_hist_split_planned(*args, 3, ghist.data_ptr(), plan.data_ptr(), prows, items_ub, st)
-    mod.tree_hist_split_planned(*args, 4, ghist.data_ptr(), plan.data_ptr(), prows, max_big, st)
+    dptr = derive_from.data_ptr() if derive_from is not None else 0
+    mod.tree_hist_split_planned(*args, 3, ghist.data_ptr(), plan.data_ptr(), prows, items_ub, int(by_node), 0, dptr,
+                                0, st)
+    mod.tree_hist_split_planned(*args, 4, ghist.data_ptr(), plan.data_ptr(), prows, max_big, int(by_node), 0, 0, 0,
+                                st)
+    if derive_from is not None:
+        mod.tree_hist_split_planned(*args, 5, ghist.data_ptr(), plan.data_ptr(), prows, A, 1, hprev.data_ptr(), dptr,
+                                    parent_of.data_ptr(), st)
     return _best_chunk(gain, feat, bin_, left, total, A, chunks, K)
 
 

@@ -39,7 +39,12 @@ class DistContext:
 
 
 def init(expected_world: Optional[int] = None, backend: Optional[str] = None, device: Optional[str] = None,
-         timeout_s: int = 600) -> DistContext:
+         timeout_s: Optional[int] = None) -> DistContext:
+    """``timeout_s`` (default ``HAR_DIST_TIMEOUT_S`` or 600) bounds every collective: a rank that
+    stalls or dies makes its peers raise instead of blocking forever, and ``torchrun
+    --max-restarts`` then restarts the group from the newest checkpoint."""
+    if timeout_s is None:
+        timeout_s = int(os.environ.get("HAR_DIST_TIMEOUT_S", "600"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -58,6 +63,14 @@ def init(expected_world: Optional[int] = None, backend: Optional[str] = None, de
         kw = dict(backend=be, rank=rank, world_size=world, timeout=datetime.timedelta(seconds=timeout_s))
         if be == "nccl":
             kw["device_id"] = dev
+        restart = os.environ.get("TORCHELASTIC_RESTART_COUNT")
+        if restart is not None and not dist.is_initialized():
+            # under torchrun --max-restarts the rendezvous store can outlive a failed attempt: key
+            # this attempt's process group under its own prefix, or a restarted rank may read a dead
+            # peer's (stale) transport address from the previous attempt and fail to connect
+            store, _, _ = next(dist.rendezvous("env://", rank=rank, world_size=world,
+                                               timeout=datetime.timedelta(seconds=timeout_s)))
+            kw["store"] = dist.PrefixStore(f"har/attempt{restart}", store)
         if not dist.is_initialized():
             dist.init_process_group(**kw)
     return DistContext(rank, local_rank, world, dev, be, None)

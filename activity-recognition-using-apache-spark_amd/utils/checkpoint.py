@@ -14,7 +14,9 @@ no checkpointing; Spark only re-computes lost partitions from lineage).
   different configuration.
 * Fault injection for tests: ``HAR_FAULT_INJECT="<step>"`` or ``"<rank>:<step>"``
   makes ``maybe_inject_fault`` hard-exit the process (exit code 17) when training
-  reaches that step — exactly like a crashed rank.
+  reaches that step — exactly like a crashed rank.  Under ``torchrun --max-restarts`` the fault
+  fires on the first attempt only (``TORCHELASTIC_RESTART_COUNT`` = 0): the restarted group resumes
+  from the newest checkpoint and runs to the end (``tests/test_checkpoint.py``).
 """
 from __future__ import annotations
 
@@ -84,7 +86,7 @@ def _canon(d: dict) -> dict:
 
 def maybe_inject_fault(step: int, rank: int = 0):
     spec = os.environ.get("HAR_FAULT_INJECT", "")
-    if not spec:
+    if not spec or int(os.environ.get("TORCHELASTIC_RESTART_COUNT", "0")) > 0:
         return
     if ":" in spec:
         r, s = spec.split(":", 1)

@@ -19,6 +19,8 @@ xGMI, weak scaling (fixed per-GPU work).  Every line is ONE JSON record.
                     8 GPUs, i.e. 125M per GPU resident in HBM) -> HIP window featurizer
                     -> MLP training step; step = featurize + train ``--batch`` windows.
 ``--config rf9``    (config 5) 12-class 9-axis IMU RandomForest, 500 trees.
+``--config dt``     DecisionTree (every feature at every node) on config 2's windows; sibling
+                   histogram subtraction on (``--no-subtract``: every node histogrammed directly).
 ``--config infer``  serving: windows/s classified by the trained config-3 MLP (fused
                     forward + head kernel, logits + argmax); no reference number exists.
 
@@ -256,9 +258,10 @@ def _featurized(n_windows, spec, dev, first_window):
     return torch.nan_to_num(X, nan=-1.0), y
 
 
-def bench_rf(args, ctx, nine_axis=False):
+def bench_rf(args, ctx, nine_axis=False, single_tree=False):
     from har.data.synth import StreamSpec
-    from har.models.tree import RandomForestClassifier
+    from har.models import tree as tree_mod
+    from har.models.tree import DecisionTreeClassifier, RandomForestClassifier
     from har.parallel import data_parallel as dp
     from har.parallel import dist as hdist
 
@@ -273,8 +276,12 @@ def bench_rf(args, ctx, nine_axis=False):
     Xt, yt = _featurized(4096, spec, dev, first_window=10 ** 9)
     if not nine_axis:
         Xt = Xt[:, :N_FEATURES].contiguous()
-    est = RandomForestClassifier(numTrees=args.trees or (500 if nine_axis else 100), maxDepth=args.depth,
-                                 maxBins=32, seed=7, device=dev)
+    if single_tree:  # every feature at every node: sibling subtraction applies (--no-subtract: off)
+        tree_mod.SIBLING_SUBTRACTION = not args.no_subtract
+        est = DecisionTreeClassifier(maxDepth=args.depth, maxBins=32, device=dev)
+    else:
+        est = RandomForestClassifier(numTrees=args.trees or (500 if nine_axis else 100), maxDepth=args.depth,
+                                     maxBins=32, seed=7, device=dev)
     model = {}
 
     owner = dp.NodeOwner(ctx) if (args.rf_reduce == "owner" and ctx.is_distributed) else None
@@ -288,8 +295,13 @@ def bench_rf(args, ctx, nine_axis=False):
     elapsed = timed(ctx, run, args.steps, args.warmup, dev)
     acc = float((model["m"].predict(Xt) == yt).float().mean())
     rows = n_local * world
-    name = (f"Synthetic 12-class 9-axis IMU RandomForest {est.numTrees} trees depth {args.depth}" if nine_axis
-            else f"WISDM 6-class RandomForest {est.numTrees} trees depth {args.depth}")
+    if single_tree:
+        name = (f"WISDM 6-class DecisionTree depth {args.depth} (all features, sibling subtraction "
+                f"{'off' if args.no_subtract else 'on'})")
+    elif nine_axis:
+        name = f"Synthetic 12-class 9-axis IMU RandomForest {est.numTrees} trees depth {args.depth}"
+    else:
+        name = f"WISDM 6-class RandomForest {est.numTrees} trees depth {args.depth}"
     return {"value": rows * args.steps / elapsed, "ms_per_step": elapsed * 1e3 / args.steps,
             "vs_baseline": None, "vs_baseline_note": "reference RF is 100 trees x depth 4 on 3793 WISDM rows; "
                                                     "see --config reference",
@@ -378,7 +390,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--config", default="mlp", choices=["mlp", "rf", "stream", "rf9", "infer", "reference"])
+    ap.add_argument("--config", default="mlp", choices=["mlp", "rf", "stream", "rf9", "infer", "reference", "dt"])
     ap.add_argument("--wisdm", default=DEFAULT_WISDM, help="WISDM transformed CSV (accuracy / reference suite)")
     ap.add_argument("--no-wisdm", action="store_true", help="skip the WISDM accuracy / reference-suite extras")
     ap.add_argument("--train-steps", type=int, default=200, help="untimed MLP training steps before --config infer")
@@ -391,6 +403,7 @@ def main():
     ap.add_argument("--rows", type=int, default=60000, help="windows per GPU (forest configs)")
     ap.add_argument("--trees", type=int, default=0)
     ap.add_argument("--depth", type=int, default=10)
+    ap.add_argument("--no-subtract", action="store_true", help="--config dt: histogram every node directly")
     ap.add_argument("--rf-reduce", default="owner", choices=["owner", "allreduce"],
                     help="DP forest histograms: reduce-scatter by node owner + all-gather of splits, or all-reduce")
     ap.add_argument("--samples", type=int, default=1_000_000_000, help="stream samples per 8 GPUs")
@@ -410,7 +423,7 @@ def main():
     elif args.config == "reference":
         r = bench_reference(args, ctx)
     else:
-        r = bench_rf(args, ctx, nine_axis=args.config == "rf9")
+        r = bench_rf(args, ctx, nine_axis=args.config == "rf9", single_tree=args.config == "dt")
     rec = {"metric": METRIC, "value": r.pop("value"), "unit": "windows/s", "n_gpus": ctx.world_size,
            "steps": args.steps, "warmup": args.warmup, "ms_per_step": r.pop("ms_per_step"),
            "higher_is_better": True, "scaling": "weak", "vs_baseline": r.pop("vs_baseline"),

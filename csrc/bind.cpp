@@ -278,22 +278,25 @@ PYBIND11_MODULE(_har_native, m) {
           "tree_hist_split");
   });
 
-  m.def("tree_plan", [](u counts, int A, int prows, u plan, int64_t slot_elems, u ghist, int max_big, u stream) {
+  m.def("tree_plan", [](u counts, int A, int prows, u plan, int64_t slot_elems, u ghist, int max_big, int by_node,
+                        u a_dev, u stream) {
     check(har_tree_plan(P<const int32_t>(counts), A, prows, P<int32_t>(plan), slot_elems, P<float>(ghist), max_big,
-                        S(stream)),
+                        by_node, P<const int32_t>(a_dev), S(stream)),
           "tree_plan");
   });
   m.def("tree_hist_split_planned", [](u bins, int64_t N, int F, int row_major, u nbins, u rows, u row_w, u node_start,
                                       u node_count, int A, u feats, int m, int fc, u label, int K, int maxbins,
                                       float min_inst, float min_gain, int impurity, u gain, u feat, u bin, u left,
-                                      u total, int mode, u ghist, u plan, int prows, int bound, u stream) {
+                                      u total, int mode, u ghist, u plan, int prows, int bound, int by_node,
+                                      u hprev, u derive_from, u parent_of, u stream) {
     check(har_tree_hist_split_planned(P<const uint8_t>(bins), N, F, row_major, P<const int32_t>(nbins),
                                       P<const int32_t>(rows), P<const float>(row_w), P<const int32_t>(node_start),
                                       P<const int32_t>(node_count), A, P<const int32_t>(feats), m, fc,
                                       P<const int32_t>(label), K, maxbins, min_inst, min_gain, impurity,
                                       P<float>(gain), P<int32_t>(feat), P<int32_t>(bin), P<float>(left),
                                       P<float>(total), mode, P<float>(ghist), 1, P<const int32_t>(plan), prows, bound,
-                                      S(stream)),
+                                      by_node, P<const float>(hprev), P<const int32_t>(derive_from),
+                                      P<const int32_t>(parent_of), S(stream)),
           "tree_hist_split_planned");
   });
 
@@ -436,9 +439,10 @@ PYBIND11_MODULE(_har_native, m) {
           "bin_features");
   });
 
-  m.def("tree_feature_subsets", [](uint64_t seed, u trees, u nodes, int64_t npairs, int F, int m_, u out, u stream) {
+  m.def("tree_feature_subsets", [](uint64_t seed, u trees, u nodes, int64_t npairs, int F, int m_, u out, u p_dev,
+                                   u stream) {
     check(har_tree_feature_subsets(seed, P<const int32_t>(trees), P<const int32_t>(nodes), npairs, F, m_,
-                                   P<int32_t>(out), S(stream)),
+                                   P<int32_t>(out), P<const int32_t>(p_dev), S(stream)),
           "tree_feature_subsets");
   });
   m.def("tree_level_keys", [](u node_of, u cand_idx, int T, int64_t N, int maxn, u key, u stream) {
@@ -447,22 +451,23 @@ PYBIND11_MODULE(_har_native, m) {
           "tree_level_keys");
   });
   m.def("tree_level_group", [](u node_of, u cand_idx, u tree_lo, u W, int T, int64_t N, int maxn, int A, int nt_max,
-                               u cnt_ws, u counts, u starts, u rows, u row_w, u stream) {
+                               u cnt_ws, u counts, u starts, u rows, u row_w, u a_dev, u stream) {
     check(har_tree_level_group(P<const int32_t>(node_of), P<const int32_t>(cand_idx), P<const int32_t>(tree_lo),
                                P<const float>(W), T, N, maxn, A, nt_max, P<int32_t>(cnt_ws), P<int32_t>(counts),
-                               P<int32_t>(starts), P<int32_t>(rows), P<float>(row_w), S(stream)),
+                               P<int32_t>(starts), P<int32_t>(rows), P<float>(row_w), P<const int32_t>(a_dev),
+                               S(stream)),
           "tree_level_group");
   });
   m.def("tree_level_group_chunks", [](int64_t N) { return har_tree_level_group_chunks(N); });
   m.def("tree_commit_level", [](int nsplit, u ti, u ni, u cl, u dsi, u rfeat, u rbin, u rgain, u rleft, u rtotal, int K,
                                 u thr_mat, int ldthr, int maxn, u feature, u split_bin, u thresh, u left, u right,
-                                u gains, u stats, u stream) {
+                                u gains, u stats, u s_dev, u stream) {
     check(har_tree_commit_level(nsplit, P<const int64_t>(ti), P<const int64_t>(ni), P<const int64_t>(cl),
                                 P<const int64_t>(dsi), P<const int32_t>(rfeat), P<const int32_t>(rbin),
                                 P<const float>(rgain), P<const float>(rleft), P<const float>(rtotal), K,
                                 P<const float>(thr_mat), ldthr, maxn, P<int32_t>(feature), P<int32_t>(split_bin),
                                 P<float>(thresh), P<int32_t>(left), P<int32_t>(right), P<float>(gains),
-                                P<float>(stats), S(stream)),
+                                P<float>(stats), P<const int32_t>(s_dev), S(stream)),
           "tree_commit_level");
   });
   m.def("tree_partition_split", [](u node_of, u feature, u split_bin, u left, u bins, int T, int64_t N, int maxn,
@@ -471,19 +476,21 @@ PYBIND11_MODULE(_har_native, m) {
                                    P<const int32_t>(left), P<const uint8_t>(bins), T, N, maxn, S(stream)),
           "tree_partition_split");
   });
-  m.def("tree_level_decide", [](int A, u gain, u left, u total, int K, int impurity, float min2, u out, u stream) {
+  m.def("tree_level_decide", [](int A, u gain, u left, u total, int K, int impurity, float min2, u out, u a_dev,
+                                u stream) {
     check(har_tree_level_decide(A, P<const float>(gain), P<const float>(left), P<const float>(total), K, impurity, min2,
-                                P<float>(out), S(stream)),
+                                P<float>(out), P<const int32_t>(a_dev), S(stream)),
           "tree_level_decide");
   });
   m.def("tree_frontier", [](int A, int Tn, int maxn, u ct, u cn, u tlo, u dec, u n_nodes, u n_nodes_next, u pos_ws,
                             u ti, u ni, u cl, u dsi, u front, u q_ws, u ct_next, u cn_next, u tlo_next, u cand_idx,
-                            u scal, u stream) {
+                            u scal, u a_dev, u parent_of, u derive_from, u stream) {
     check(har_tree_frontier(A, Tn, maxn, P<const int32_t>(ct), P<const int32_t>(cn), P<const int32_t>(tlo),
                             P<const float>(dec), P<const int32_t>(n_nodes), P<int32_t>(n_nodes_next),
                             P<int32_t>(pos_ws), P<int64_t>(ti), P<int64_t>(ni), P<int64_t>(cl), P<int64_t>(dsi),
                             P<float>(front), P<int32_t>(q_ws), P<int32_t>(ct_next), P<int32_t>(cn_next),
-                            P<int32_t>(tlo_next), P<int32_t>(cand_idx), P<int32_t>(scal), S(stream)),
+                            P<int32_t>(tlo_next), P<int32_t>(cand_idx), P<int32_t>(scal), P<const int32_t>(a_dev),
+                            P<int32_t>(parent_of), P<int32_t>(derive_from), S(stream)),
           "tree_frontier");
   });
   m.def("tree_partition", [](u node_of, u lvl_feat, u lvl_bin, u lvl_left, u bins, int T, int64_t N, int maxn,

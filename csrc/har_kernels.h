@@ -243,32 +243,38 @@ int har_tree_hist_split(const uint8_t* bins, int64_t N, int F, int row_major, co
                         float min_inst, float min_gain, int impurity, float* out_gain, int32_t* out_feat,
                         int32_t* out_bin, float* out_left, float* out_total, int mode, float* ghist,
                         int row_chunks, hipStream_t s);
+// Device-count convention of the level kernels below: a non-null a_dev / p_dev / s_dev points at the
+// level's real count on the device and the host's A / P / S is then only an upper bound (grid size
+// and array stride), so a whole fit can be enqueued without reading counts back per level.
 // Load-balanced level (tree.hip): har_tree_plan builds the work plan from the node row counts
 // (nodes of > prows rows become ceil(count / prows) chunk items with a merged-histogram slot, zeroed
 // here for at most max_big slots of slot_elems floats); then har_tree_hist_split_planned mode 3
 // (grid.y = an upper bound of the items: fused small nodes + chunk histograms) and mode 4 (grid.y
-// = max_big: split search of the merged big nodes).
+// = max_big: split search of the merged big nodes).  by_node = 1 keeps every node's histogram in
+// ghist = a per-node store [A][m][bins][K]; mode 5 then derives the nodes marked derive_from[a] >= 0
+// (sibling subtraction, parents in hprev, frontier-provided parent_of / derive_from).
 int har_tree_plan(const int32_t* counts, int A, int prows, int32_t* plan, int64_t slot_elems, float* ghist,
-                  int max_big, hipStream_t s);
+                  int max_big, int by_node, const int32_t* a_dev, hipStream_t s);
 int har_tree_hist_split_planned(const uint8_t* bins, int64_t N, int F, int row_major, const int32_t* nbins_feat,
                                 const int32_t* rows, const float* row_w, const int32_t* node_start,
                                 const int32_t* node_count, int A, const int32_t* feats, int m, int fc,
                                 const int32_t* label, int K, int maxbins, float min_inst, float min_gain, int impurity,
                                 float* out_gain, int32_t* out_feat, int32_t* out_bin, float* out_left,
                                 float* out_total, int mode, float* ghist, int row_chunks, const int32_t* plan,
-                                int prows, int bound, hipStream_t s);
+                                int prows, int bound, int by_node, const float* hprev, const int32_t* derive_from,
+                                const int32_t* parent_of, hipStream_t s);
 // Sum over trees of (normalized) leaf statistics; trees as SoA [T][maxn] arrays, feature < 0 = leaf.
 // Level bookkeeping of the forest builder (tree_level.hip): Floyd feature subsets per (tree, node)
 // (bit-identical to har/ops/rng.py), per-(tree,row) candidate keys, and the row -> child partition.
 int har_tree_feature_subsets(uint64_t seed, const int32_t* trees, const int32_t* nodes, int64_t P, int F, int m,
-                             int32_t* out, hipStream_t s);
+                             int32_t* out, const int32_t* p_dev, hipStream_t s);
 int har_tree_level_keys(const int32_t* node_of, const int32_t* cand_idx, int T, int64_t N, int maxn, int32_t* key,
                         hipStream_t s);
 // Stable grouping of the level's (tree, row) pairs by candidate node (no sort); cnt_ws holds
 // har_tree_level_group_chunks(N) x A ints.  -4: a tree has more than 4096 candidates.
 int har_tree_level_group(const int32_t* node_of, const int32_t* cand_idx, const int32_t* tree_lo, const float* W,
                          int T, int64_t N, int maxn, int A, int nt_max, int32_t* cnt_ws, int32_t* counts,
-                         int32_t* starts, int32_t* rows, float* row_w, hipStream_t s);
+                         int32_t* starts, int32_t* rows, float* row_w, const int32_t* a_dev, hipStream_t s);
 int har_tree_level_group_chunks(int64_t N);
 // Commit the level's splits (feature / bin / threshold / children / gain / child stats) in one launch,
 // then move rows with the committed arrays (no per-level temporaries).
@@ -276,18 +282,19 @@ int har_tree_commit_level(int S, const int64_t* ti, const int64_t* ni, const int
                           const int32_t* rfeat, const int32_t* rbin, const float* rgain, const float* rleft,
                           const float* rtotal, int K, const float* thr_mat, int ldthr, int maxn, int32_t* feature,
                           int32_t* split_bin, float* thresh, int32_t* left, int32_t* right, float* gains,
-                          float* stats, hipStream_t s);
+                          float* stats, const int32_t* s_dev, hipStream_t s);
 int har_tree_partition_split(int32_t* node_of, const int32_t* feature, const int32_t* split_bin, const int32_t* left,
                              const uint8_t* bins, int T, int64_t N, int maxn, hipStream_t s);
 int har_tree_level_decide(int A, const float* gain, const float* left, const float* total, int K, int impurity,
-                          float min2, float* out, hipStream_t s);
+                          float min2, float* out, const int32_t* a_dev, hipStream_t s);
 // Device-resident frontier update from the level decisions (see tree_level.hip): commit records
 // ti/ni/cl/dsi [<= A], next candidates ct/cn [<= 2A], tree starts [Tn + 1], cand_idx entries, and
 // scal = [splits, next candidates, max per tree, max weight float bits] (the level's one D2H).
 int har_tree_frontier(int A, int Tn, int maxn, const int32_t* ct, const int32_t* cn, const int32_t* tlo,
                       const float* dec, const int32_t* n_nodes, int32_t* n_nodes_next, int32_t* pos_ws, int64_t* ti,
                       int64_t* ni, int64_t* cl, int64_t* dsi, float* front, int32_t* q_ws, int32_t* ct_next,
-                      int32_t* cn_next, int32_t* tlo_next, int32_t* cand_idx, int32_t* scal, hipStream_t s);
+                      int32_t* cn_next, int32_t* tlo_next, int32_t* cand_idx, int32_t* scal, const int32_t* a_dev,
+                      int32_t* parent_of, int32_t* derive_from, hipStream_t s);
 int har_tree_partition(int32_t* node_of, const int32_t* lvl_feat, const int32_t* lvl_bin, const int32_t* lvl_left,
                        const uint8_t* bins, int T, int64_t N, int maxn, hipStream_t s);
 int har_forest_predict(const float* X, int64_t n, int F, int ld, const int32_t* feat, const float* thr,

@@ -100,13 +100,20 @@ __global__ __launch_bounds__(256) void tree_hist_split_kernel(
     const int32_t* __restrict__ label, int K, int maxbins, float min_inst, float min_gain, int impurity,
     float* __restrict__ out_gain, int32_t* __restrict__ out_feat, int32_t* __restrict__ out_bin,
     float* __restrict__ out_left, float* __restrict__ out_total, int mode, float* __restrict__ ghist,
-    const int32_t* __restrict__ plan, int prows) {
+    const int32_t* __restrict__ plan, int prows, int by_node, const float* __restrict__ hprev,
+    const int32_t* __restrict__ derive_from, const int32_t* __restrict__ parent_of) {
   // mode 0: fused histogram + split; 1: histogram only -> ghist [A][m][maxbins][K] (data parallel:
   // summed across ranks by RCCL); 2: split search from a (reduced) ghist.
   // Planned (load-balanced) level, plan = tree_plan_kernel's output (see there):
   // mode 3: work item blockIdx.y: a node of <= prows rows -> fused histogram + split (as mode 0);
   //         one prows-row chunk of a larger node -> its histogram added into that node's ghist slot
   // mode 4: blockIdx.y = big-node slot: split search from its merged ghist (as mode 2)
+  // Sibling subtraction (by_node = 1: ghist is the level's per-node histogram store [A][m][bins][K],
+  // every node's histogram is kept there for the next level):
+  //   mode 3 skips the nodes marked derive_from[a] >= 0 (their rows were not grouped), writes each
+  //   fused node's LDS histogram to its store slot, and merges big-node chunks into slot a;
+  //   mode 5: blockIdx.y = node a with derive_from[a] = sibling s: hist = hprev[parent_of[a]] -
+  //   store[s] (integer-valued weights: exact), kept in store[a], then the split search (mode 2).
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int c = blockIdx.x, chunks = gridDim.x;
   int a = blockIdx.y, gslot = blockIdx.y;
@@ -127,6 +134,7 @@ __global__ __launch_bounds__(256) void tree_hist_split_kernel(
     if (mode == 3) {
       if ((int)blockIdx.y >= plan[0]) return;        // beyond this level's work items
       a = item_node[blockIdx.y];
+      if (derive_from && derive_from[a] >= 0) return;  // histogram = parent - sibling (mode 5)
       gslot = big_rank[a];
       const int z = blockIdx.y - item_start[a];
       const int cnt_all = node_count[a];
@@ -134,13 +142,19 @@ __global__ __launch_bounds__(256) void tree_hist_split_kernel(
       cnt = gslot < 0 ? cnt_all : min(prows, cnt_all - z * prows);
       if (gslot >= 0) mode = 1;                      // a chunk of a big node: histogram only
       else mode = 0;
+      if (by_node) gslot = a;
     } else {
       if ((int)blockIdx.y >= plan[1]) return;        // beyond this level's big nodes
       a = big_list[blockIdx.y];
+      gslot = by_node ? a : blockIdx.y;
       mode = 2;
       start = 0;
       cnt = 0;
     }
+  } else if (mode == 5) {
+    if (a >= plan[2] || derive_from[a] < 0) return;
+    start = 0;
+    cnt = 0;
   } else {
     // grid.z > 1 (histogram-only mode): the node's rows are split over gridDim.z workgroups
     const int cnt_all = node_count[a];
@@ -152,7 +166,19 @@ __global__ __launch_bounds__(256) void tree_hist_split_kernel(
   const bool merge = (gridDim.z > 1) || (plan != nullptr);  // mode 1 adds into a zeroed ghist
 
   float* gh = ghist ? ghist + ((size_t)gslot * m + f_lo) * maxbins * K : nullptr;
-  for (int i = tid; i < f_n * maxbins * K; i += blockDim.x) hist[i] = (mode == 2) ? gh[i] : 0.f;
+  if (mode == 5) {
+    const size_t slot = (size_t)m * maxbins * K, off = (size_t)f_lo * maxbins * K;
+    const float* hp = hprev + (size_t)parent_of[a] * slot + off;
+    const float* hs = ghist + (size_t)derive_from[a] * slot + off;
+    for (int i = tid; i < f_n * maxbins * K; i += blockDim.x) {
+      const float v = hp[i] - hs[i];
+      hist[i] = v;
+      gh[i] = v;
+    }
+    mode = 2;
+  } else {
+    for (int i = tid; i < f_n * maxbins * K; i += blockDim.x) hist[i] = (mode == 2) ? gh[i] : 0.f;
+  }
   for (int i = tid; i < f_n; i += blockDim.x) fid[i] = feats[(size_t)a * m + f_lo + i];
   __syncthreads();
 
@@ -223,6 +249,8 @@ __global__ __launch_bounds__(256) void tree_hist_split_kernel(
     }
   }
   __syncthreads();
+  if (mode == 0 && by_node)  // keep the fused node's histogram for its children's subtraction
+    for (int i = tid; i < f_n * maxbins * K; i += blockDim.x) gh[i] = hist[i];
   if (mode == 1) {
     if (!merge) {
       for (int i = tid; i < f_n * maxbins * K; i += blockDim.x) gh[i] = hist[i];
@@ -544,9 +572,10 @@ __global__ __launch_bounds__(256) void find_splits_post_sort_kernel(const float*
 // (int32): [0] items, [1] big nodes, [2] A, [3] unused, item_start [A + 1], big_rank [A] (-1 = not
 // big), big_list [A], item_node [items].  Block-wide scans over A in 1024-node steps.
 __global__ __launch_bounds__(1024) void tree_plan_kernel(const int32_t* __restrict__ counts, int A, int prows,
-                                                         int32_t* __restrict__ plan) {
+                                                         int32_t* __restrict__ plan, const int32_t* __restrict__ a_dev) {
   __shared__ int wsum_i[16], wsum_b[16];
   __shared__ int base_i, base_b;
+  if (a_dev) A = *a_dev;  // the level's candidate count (the host's A is then only a bound)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   int32_t* item_start = plan + 4;
   int32_t* big_rank = item_start + A + 1;
@@ -597,10 +626,14 @@ __global__ __launch_bounds__(1024) void tree_plan_kernel(const int32_t* __restri
 // Zero the merged-histogram slots of this level's big nodes only (grid = an upper bound; the
 // real count is read from the plan).
 __global__ __launch_bounds__(256) void tree_plan_zero_kernel(const int32_t* __restrict__ plan, int64_t slot_elems,
-                                                             float* __restrict__ ghist) {
+                                                             float* __restrict__ ghist, int by_node) {
   const int64_t n = (int64_t)plan[1] * slot_elems;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
-    ghist[i] = 0.f;
+  const int32_t* big_list = plan + 4 + (plan[2] + 1) + plan[2];
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    // by_node: the big nodes' own slots of the per-node store (else slots 0..big nodes - 1)
+    const int64_t j = i / slot_elems;
+    ghist[by_node ? (int64_t)big_list[j] * slot_elems + (i - j * slot_elems) : i] = 0.f;
+  }
 }
 
 }  // namespace
@@ -616,7 +649,8 @@ extern "C" int har_tree_hist_split(const uint8_t* bins, int64_t N, int F, int ro
                                    hipStream_t s) {
   return har_tree_hist_split_planned(bins, N, F, row_major, nbins_feat, rows, row_w, node_start, node_count, A, feats,
                                      m, fc, label, K, maxbins, min_inst, min_gain, impurity, out_gain, out_feat,
-                                     out_bin, out_left, out_total, mode, ghist, row_chunks, nullptr, 0, 0, s);
+                                     out_bin, out_left, out_total, mode, ghist, row_chunks, nullptr, 0, 0, 0,
+                                     nullptr, nullptr, nullptr, s);
 }
 
 // mode 3 / 4 (plan != nullptr): grid.y = `bound` (items for mode 3, big-node slots for mode 4)
@@ -627,22 +661,28 @@ extern "C" int har_tree_hist_split_planned(const uint8_t* bins, int64_t N, int F
                                            int maxbins, float min_inst, float min_gain, int impurity,
                                            float* out_gain, int32_t* out_feat, int32_t* out_bin, float* out_left,
                                            float* out_total, int mode, float* ghist, int row_chunks,
-                                           const int32_t* plan, int prows, int bound, hipStream_t s) {
+                                           const int32_t* plan, int prows, int bound, int by_node,
+                                           const float* hprev, const int32_t* derive_from,
+                                           const int32_t* parent_of, hipStream_t s) {
   if (K > KMAX || maxbins > 64 || fc <= 0 || m <= 0) return -2;
   if (mode != 0 && !ghist) return -4;
-  if ((mode == 3 || mode == 4) && (!plan || prows <= 0)) return -6;
+  const bool planned = mode == 3 || mode == 4 || mode == 5;
+  if (planned && (!plan || prows <= 0)) return -6;
+  if (mode == 5 && (!by_node || !hprev || !derive_from || !parent_of)) return -7;
+  if (by_node && !planned) return -7;
   if (A == 0) return 0;
   const int chunks = (m + fc - 1) / fc;
   const size_t lds = (size_t)fc * maxbins * K * sizeof(float) + (size_t)fc * sizeof(int);
   if (lds > 150 * 1024) return -3;
   if (row_chunks > 1 && mode != 1) return -5;
-  if ((mode == 3 || mode == 4) && bound <= 0) return 0;
-  dim3 grid(chunks, (mode == 3 || mode == 4) ? bound : A, row_chunks > 1 ? row_chunks : 1);
+  if (planned && bound <= 0) return 0;
+  dim3 grid(chunks, planned ? bound : A, row_chunks > 1 ? row_chunks : 1);
   const int64_t fstride = row_major ? 1 : N, rstride = row_major ? F : 1;
   tree_hist_split_kernel<<<grid, 256, lds, s>>>(bins, fstride, rstride, nbins_feat, rows, row_w, node_start, node_count, feats, m,
                                                 fc, label, K, maxbins, min_inst, min_gain, impurity, out_gain,
                                                 out_feat, out_bin, out_left, out_total, mode, ghist,
-                                                (mode == 3 || mode == 4) ? plan : nullptr, prows);
+                                                planned ? plan : nullptr, prows, by_node, hprev, derive_from,
+                                                parent_of);
   HAR_CHECK_LAUNCH();
   return 0;
 }
@@ -694,14 +734,14 @@ extern "C" int har_find_splits_post_sort(const float* sorted, int F, int n, int 
 }
 
 extern "C" int har_tree_plan(const int32_t* counts, int A, int prows, int32_t* plan, int64_t slot_elems,
-                             float* ghist, int max_big, hipStream_t s) {
+                             float* ghist, int max_big, int by_node, const int32_t* a_dev, hipStream_t s) {
   if (A <= 0 || prows <= 0) return -2;
-  tree_plan_kernel<<<1, 1024, 0, s>>>(counts, A, prows, plan);
+  tree_plan_kernel<<<1, 1024, 0, s>>>(counts, A, prows, plan, a_dev);
   HAR_CHECK_LAUNCH();
   if (ghist && max_big > 0) {
     const int64_t n = (int64_t)max_big * slot_elems;
     const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(4096, (n + 255) / 256));
-    tree_plan_zero_kernel<<<blocks, 256, 0, s>>>(plan, slot_elems, ghist);
+    tree_plan_zero_kernel<<<blocks, 256, 0, s>>>(plan, slot_elems, ghist, by_node);
     HAR_CHECK_LAUNCH();
   }
   return 0;

@@ -32,10 +32,11 @@ constexpr int MAX_SUBSET = 128;
 // value's rank among the m distinct choices.
 __global__ __launch_bounds__(256) void tree_feature_subsets_kernel(uint64_t seed, const int32_t* __restrict__ trees,
                                                                    const int32_t* __restrict__ nodes, int64_t P,
-                                                                   int F, int m, int32_t* __restrict__ out) {
+                                                                   int F, int m, int32_t* __restrict__ out,
+                                                                   const int32_t* __restrict__ p_dev) {
   const int lane = threadIdx.x & 63;
   const int64_t p = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-  if (p >= P) return;  // wave-uniform
+  if (p >= (p_dev ? (int64_t)*p_dev : P)) return;  // wave-uniform (P = grid bound when p_dev is given)
   const uint64_t base = ((uint64_t)(uint32_t)trees[p] << 32) | ((uint64_t)(uint32_t)nodes[p] << 8);
   int t0 = 0, t1 = 0;  // the draw of step lane / lane + 64 (t in [0, j], j = F - m + i)
   if (lane < m) t0 = (int)(philox_u32(seed, STREAM_FEATURE_SUBSET, base + (uint64_t)lane) % (uint32_t)(F - m + lane + 1));
@@ -117,6 +118,7 @@ __global__ __launch_bounds__(256) void tree_group_count_kernel(const int32_t* __
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int t = blockIdx.y, c = blockIdx.x * GROUP_WAVES + wave;
   const int lo = tree_lo[t], nt = tree_lo[t + 1] - lo;
+  if (nt == 0) return;  // block-uniform: no candidate of tree t at this level, nothing to count
   const bool live = c < nch;
   int32_t* h = glds + wave * nt_max;
   for (int i = lane; i < nt; i += 64) h[i] = 0;
@@ -134,10 +136,12 @@ __global__ __launch_bounds__(256) void tree_group_count_kernel(const int32_t* __
 }
 
 // cnt[c][a] -> exclusive prefix over chunks c; total[a] = sum.  Coalesced over a.
+// A is the row stride of cnt; a_dev (if given) the level's candidate count (<= A).
 __global__ __launch_bounds__(256) void tree_group_colscan_kernel(int32_t* __restrict__ cnt, int nch, int A,
-                                                                 int32_t* __restrict__ total) {
+                                                                 int32_t* __restrict__ total,
+                                                                 const int32_t* __restrict__ a_dev) {
   const int a = blockIdx.x * 256 + threadIdx.x;
-  if (a >= A) return;
+  if (a >= (a_dev ? *a_dev : A)) return;
   int run = 0;
   for (int c = 0; c < nch; ++c) {
     const int v = cnt[(int64_t)c * A + a];
@@ -149,8 +153,10 @@ __global__ __launch_bounds__(256) void tree_group_colscan_kernel(int32_t* __rest
 
 // One workgroup: exclusive scan of total[0..A) -> starts (A is the level's candidate count).
 __global__ __launch_bounds__(1024) void tree_group_scan_kernel(const int32_t* __restrict__ total, int A,
-                                                               int32_t* __restrict__ starts) {
+                                                               int32_t* __restrict__ starts,
+                                                               const int32_t* __restrict__ a_dev) {
   __shared__ int32_t wsum[16];
+  if (a_dev) A = *a_dev;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int per = (A + 1023) / 1024;
   const int b = tid * per, e = b + per < A ? b + per : A;
@@ -189,6 +195,7 @@ __global__ __launch_bounds__(256) void tree_group_scatter_kernel(const int32_t* 
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int t = blockIdx.y, c = blockIdx.x * GROUP_WAVES + wave;
   const int lo = tree_lo[t], nt = tree_lo[t + 1] - lo;
+  if (nt == 0) return;  // block-uniform
   const bool live = c < nch;
   int32_t* h = glds + wave * nt_max;
   if (live)
@@ -230,9 +237,10 @@ __global__ __launch_bounds__(256) void tree_commit_level_kernel(
     const float* __restrict__ rgain, const float* __restrict__ rleft, const float* __restrict__ rtotal, int K,
     const float* __restrict__ thr_mat, int ldthr, int maxn, int32_t* __restrict__ feature,
     int32_t* __restrict__ split_bin, float* __restrict__ thresh, int32_t* __restrict__ left,
-    int32_t* __restrict__ right, float* __restrict__ gains, float* __restrict__ stats) {
+    int32_t* __restrict__ right, float* __restrict__ gains, float* __restrict__ stats,
+    const int32_t* __restrict__ s_dev) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= S) return;
+  if (i >= (s_dev ? *s_dev : S)) return;
   const int64_t j = dsi[i];
   const int64_t o = ti[i] * maxn + ni[i];
   const int c = (int)cl[i];
@@ -283,9 +291,11 @@ __global__ __launch_bounds__(256) void tree_partition_split_kernel(int32_t* __re
 __global__ __launch_bounds__(256) void tree_level_decide_kernel(int A, const float* __restrict__ gain,
                                                                 const float* __restrict__ left,
                                                                 const float* __restrict__ total, int K,
-                                                                int impurity, float min2, float* __restrict__ out) {
+                                                                int impurity, float min2, float* __restrict__ out,
+                                                                const int32_t* __restrict__ a_dev) {
+  // A: row stride of out; a_dev (if given): the level's candidate count
   const int a = blockIdx.x * blockDim.x + threadIdx.x;
-  if (a >= A) return;
+  if (a >= (a_dev ? *a_dev : A)) return;
   const float g = gain[a];
   const float* L = left + (int64_t)a * K;
   const float* Tt = total + (int64_t)a * K;
@@ -393,10 +403,15 @@ __global__ __launch_bounds__(256) void frontier_children_kernel(int A, int Tn, c
                                                                 int32_t* __restrict__ n_nodes_next,
                                                                 int64_t* __restrict__ ti, int64_t* __restrict__ ni,
                                                                 int64_t* __restrict__ cl, int64_t* __restrict__ dsi,
-                                                                float* __restrict__ front) {
+                                                                float* __restrict__ front,
+                                                                const int32_t* __restrict__ a_dev,
+                                                                int32_t* __restrict__ scal) {
+  // A: row stride of dec; An: the level's candidate count; scal[0] = splits (the next scan's n)
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const int An = a_dev ? *a_dev : A;
+  if (i == 0) scal[0] = pos[An];
   if (i < Tn) n_nodes_next[i] = n_nodes[i] + 2 * (pos[tlo[i + 1]] - pos[tlo[i]]);
-  if (i >= A || !(dec[i] > 0.f)) return;
+  if (i >= An || !(dec[i] > 0.f)) return;
   const int p = pos[i], t = ct[i];
   const int c = n_nodes[t] + 2 * (p - pos[tlo[t]]);
   ti[p] = t;
@@ -422,9 +437,12 @@ __global__ __launch_bounds__(256) void frontier_next_kernel(int A, int Tn, int m
                                                             int32_t* __restrict__ cn_next,
                                                             int32_t* __restrict__ tlo_next,
                                                             int32_t* __restrict__ cand_idx,
-                                                            int32_t* __restrict__ scal) {
+                                                            int32_t* __restrict__ scal,
+                                                            const int32_t* __restrict__ a_dev,
+                                                            int32_t* __restrict__ parent_of,
+                                                            int32_t* __restrict__ derive_from) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
-  const int S = pos[A];
+  const int S = pos[a_dev ? *a_dev : A];
   if (e <= Tn) {
     const int lo = q[2 * pos[tlo[e]]];
     tlo_next[e] = lo;
@@ -437,10 +455,19 @@ __global__ __launch_bounds__(256) void frontier_next_kernel(int A, int Tn, int m
   if (e >= 2 * S || !(front[e] > 0.f)) return;
   const int p = e >> 1, i = q[e];
   const int t = (int)ti[p], n = (int)cl[p] + (e & 1);
+  const float wgt = dec[(3 + (e & 1)) * A + dsi[p]];
+  // sibling subtraction (parent_of given): of two candidate siblings the heavier (the right one
+  // on a tie) takes its histogram as parent - sibling, and its rows are not grouped (cand_idx -1)
+  bool derived = false;
+  if (parent_of) {
+    const float wsib = dec[(3 + ((e & 1) ^ 1)) * A + dsi[p]];
+    derived = front[e ^ 1] > 0.f && (wgt > wsib || (wgt == wsib && (e & 1)));
+    parent_of[i] = (int)dsi[p];
+    derive_from[i] = derived ? q[e ^ 1] : -1;
+  }
   ct_next[i] = t;
   cn_next[i] = n;
-  cand_idx[(int64_t)t * maxn + n] = i;
-  const float wgt = dec[(3 + (e & 1)) * A + dsi[p]];
+  cand_idx[(int64_t)t * maxn + n] = derived ? -1 : i;
   atomicMax(&scal[3], __float_as_int(wgt));  // weights >= 0: float order == int order
 }
 
@@ -449,10 +476,10 @@ int grid_for(int64_t total) { return (int)std::max<int64_t>(1, std::min<int64_t>
 }  // namespace
 
 extern "C" int har_tree_feature_subsets(uint64_t seed, const int32_t* trees, const int32_t* nodes, int64_t P, int F,
-                                        int m, int32_t* out, hipStream_t s) {
+                                        int m, int32_t* out, const int32_t* p_dev, hipStream_t s) {
   if (m <= 0 || m > MAX_SUBSET || m > F) return -2;
   if (P == 0) return 0;
-  tree_feature_subsets_kernel<<<(unsigned)((P + 3) / 4), 256, 0, s>>>(seed, trees, nodes, P, F, m, out);
+  tree_feature_subsets_kernel<<<(unsigned)((P + 3) / 4), 256, 0, s>>>(seed, trees, nodes, P, F, m, out, p_dev);
   HAR_CHECK_LAUNCH();
   return 0;
 }
@@ -477,7 +504,8 @@ extern "C" int har_tree_partition(int32_t* node_of, const int32_t* lvl_feat, con
 
 extern "C" int har_tree_level_group(const int32_t* node_of, const int32_t* cand_idx, const int32_t* tree_lo,
                                     const float* W, int T, int64_t N, int maxn, int A, int nt_max, int32_t* cnt_ws,
-                                    int32_t* counts, int32_t* starts, int32_t* rows, float* row_w, hipStream_t s) {
+                                    int32_t* counts, int32_t* starts, int32_t* rows, float* row_w,
+                                    const int32_t* a_dev, hipStream_t s) {
   if (nt_max > GROUP_MAX_NT || nt_max < 1) return -4;
   if (A == 0 || T == 0 || N == 0) return 0;
   const int nch = (int)((N + GROUP_CH - 1) / GROUP_CH);
@@ -486,9 +514,9 @@ extern "C" int har_tree_level_group(const int32_t* node_of, const int32_t* cand_
   tree_group_count_kernel<<<grid, 64 * GROUP_WAVES, lds, s>>>(node_of, cand_idx, tree_lo, N, maxn, nch, A, nt_max,
                                                               cnt_ws);
   HAR_CHECK_LAUNCH();
-  tree_group_colscan_kernel<<<(A + 255) / 256, 256, 0, s>>>(cnt_ws, nch, A, counts);
+  tree_group_colscan_kernel<<<(A + 255) / 256, 256, 0, s>>>(cnt_ws, nch, A, counts, a_dev);
   HAR_CHECK_LAUNCH();
-  tree_group_scan_kernel<<<1, 1024, 0, s>>>(counts, A, starts);
+  tree_group_scan_kernel<<<1, 1024, 0, s>>>(counts, A, starts, a_dev);
   HAR_CHECK_LAUNCH();
   tree_group_scatter_kernel<<<grid, 64 * GROUP_WAVES, lds, s>>>(node_of, cand_idx, tree_lo, W, N, maxn, nch, A,
                                                                 nt_max, cnt_ws, starts, rows, row_w);
@@ -502,11 +530,12 @@ extern "C" int har_tree_commit_level(int S, const int64_t* ti, const int64_t* ni
                                      const int32_t* rfeat, const int32_t* rbin, const float* rgain, const float* rleft,
                                      const float* rtotal, int K, const float* thr_mat, int ldthr, int maxn,
                                      int32_t* feature, int32_t* split_bin, float* thresh, int32_t* left,
-                                     int32_t* right, float* gains, float* stats, hipStream_t s) {
+                                     int32_t* right, float* gains, float* stats, const int32_t* s_dev,
+                                     hipStream_t s) {
   if (S <= 0) return 0;
   tree_commit_level_kernel<<<(S + 255) / 256, 256, 0, s>>>(S, ti, ni, cl, dsi, rfeat, rbin, rgain, rleft, rtotal, K,
                                                            thr_mat, ldthr, maxn, feature, split_bin, thresh, left,
-                                                           right, gains, stats);
+                                                           right, gains, stats, s_dev);
   HAR_CHECK_LAUNCH();
   return 0;
 }
@@ -522,9 +551,9 @@ extern "C" int har_tree_partition_split(int32_t* node_of, const int32_t* feature
 }
 
 extern "C" int har_tree_level_decide(int A, const float* gain, const float* left, const float* total, int K,
-                                     int impurity, float min2, float* out, hipStream_t s) {
+                                     int impurity, float min2, float* out, const int32_t* a_dev, hipStream_t s) {
   if (A <= 0) return 0;
-  tree_level_decide_kernel<<<(A + 255) / 256, 256, 0, s>>>(A, gain, left, total, K, impurity, min2, out);
+  tree_level_decide_kernel<<<(A + 255) / 256, 256, 0, s>>>(A, gain, left, total, K, impurity, min2, out, a_dev);
   HAR_CHECK_LAUNCH();
   return 0;
 }
@@ -533,23 +562,24 @@ extern "C" int har_tree_frontier(int A, int Tn, int maxn, const int32_t* ct, con
                                  const float* dec, const int32_t* n_nodes, int32_t* n_nodes_next, int32_t* pos_ws,
                                  int64_t* ti, int64_t* ni, int64_t* cl, int64_t* dsi, float* front, int32_t* q_ws,
                                  int32_t* ct_next, int32_t* cn_next, int32_t* tlo_next, int32_t* cand_idx,
-                                 int32_t* scal, hipStream_t s) {
+                                 int32_t* scal, const int32_t* a_dev, int32_t* parent_of, int32_t* derive_from,
+                                 hipStream_t s) {
   if (A <= 0) return -2;
   // frontier_scan_kernel reads / writes 16-byte vectors from these bases
   if (((uintptr_t)dec | (uintptr_t)front | (uintptr_t)pos_ws | (uintptr_t)q_ws) & 15) return -3;
   hipError_t err = hipMemsetAsync(scal, 0, 4 * sizeof(int32_t), s);
   if (err != hipSuccess) return (int)err;
-  frontier_scan_kernel<<<1, 1024, 0, s>>>(dec, A, nullptr, 1, pos_ws);
+  frontier_scan_kernel<<<1, 1024, 0, s>>>(dec, A, a_dev, 1, pos_ws);
   HAR_CHECK_LAUNCH();
   const int g1 = (std::max(A, Tn + 1) + 255) / 256;
   frontier_children_kernel<<<g1, 256, 0, s>>>(A, Tn, ct, cn, tlo, dec, pos_ws, n_nodes, n_nodes_next, ti, ni, cl, dsi,
-                                              front);
+                                              front, a_dev, scal);
   HAR_CHECK_LAUNCH();
-  frontier_scan_kernel<<<1, 1024, 0, s>>>(front, 0, pos_ws + A, 2, q_ws);
+  frontier_scan_kernel<<<1, 1024, 0, s>>>(front, 0, scal, 2, q_ws);  // n = 2 x splits (scal[0])
   HAR_CHECK_LAUNCH();
   const int g2 = (std::max(2 * A, Tn + 1) + 255) / 256;
   frontier_next_kernel<<<g2, 256, 0, s>>>(A, Tn, maxn, tlo, dec, pos_ws, ti, cl, dsi, front, q_ws, ct_next, cn_next,
-                                          tlo_next, cand_idx, scal);
+                                          tlo_next, cand_idx, scal, a_dev, parent_of, derive_from);
   HAR_CHECK_LAUNCH();
   return 0;
 }

@@ -144,3 +144,106 @@ def test_gpu_training_is_deterministic(cuda):
           for _ in range(2)]
     assert torch.equal(fs[0].arrs.feature, fs[1].arrs.feature)
     assert torch.equal(fs[0].arrs.threshold, fs[1].arrs.threshold)
+
+
+_ELASTIC = r"""
+import os, sys, torch
+torch.set_num_threads(1)
+from har.parallel import dist as hd
+from har.models.mlp import MultilayerPerceptronClassifier
+ckpt, out = sys.argv[1:3]
+ctx = hd.init(device="cpu")
+g = torch.Generator().manual_seed(0)
+mu = torch.randn(4, 12, generator=g) * 2
+y = torch.randint(0, 4, (1024,), generator=g)
+X = mu[y] + torch.randn(1024, 12, generator=g)
+per = 1024 // ctx.world_size
+lo = ctx.rank * per
+m = MultilayerPerceptronClassifier(layers=[12, 32, 32, 4], maxIter=3, blockSize=64, stepSize=3e-3, seed=5,
+                                   device="cpu", checkpointDir=None if ckpt == "-" else ckpt,
+                                   checkpointInterval=4).fit_tensors(X[lo:lo + per], y[lo:lo + per],
+                                                                     process_group=ctx.group, rank=ctx.rank,
+                                                                     world_size=ctx.world_size, num_classes=4)
+if ctx.rank == 0:
+    torch.save({"P": m.engine.P.detach().cpu(),
+                "attempt": torch.tensor(int(os.environ.get("TORCHELASTIC_RESTART_COUNT", "0")))}, out)
+hd.shutdown(ctx)
+"""
+
+
+def _torchrun(tmp_path, ckpt, out, fault=None, restarts=0):
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    script = tmp_path / "elastic.py"
+    script.write_text(_ELASTIC)
+    env = dict(os.environ, PYTHONPATH=REPO + os.pathsep + os.environ.get("PYTHONPATH", ""), HAR_DIST_TIMEOUT_S="60")
+    env.pop("HAR_FAULT_INJECT", None)
+    if fault is not None:
+        env["HAR_FAULT_INJECT"] = fault
+    # dynamic (c10d) rendezvous: each restart forms a new round on the agent's store
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           f"--max-restarts={restarts}", "--rdzv-backend=c10d", f"--rdzv-endpoint=127.0.0.1:{port}",
+           "--rdzv-id=har-elastic-test", "--monitor-interval=0.5", str(script), ckpt, out]
+    return subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
+
+
+def test_torchrun_rank_failure_restarts_and_resumes(tmp_path):
+    """A DP rank crashes mid-fit (rank 1 at step 10 of 48, exit 17); torchrun's elastic agent
+    tears the group down and restarts it (--max-restarts 1); both ranks resume from the newest
+    checkpoint (step 8) and the final model equals an uninterrupted 2-rank fit bit for bit."""
+    ref = _torchrun(tmp_path, "-", str(tmp_path / "ref.pt"))
+    assert ref.returncode == 0, ref.stderr[-3000:]
+    ck = str(tmp_path / "ckpt")
+    res = _torchrun(tmp_path, ck, str(tmp_path / "res.pt"), fault="1:10", restarts=1)
+    assert res.returncode == 0, res.stderr[-3000:]
+    a = torch.load(tmp_path / "ref.pt", weights_only=True)
+    b = torch.load(tmp_path / "res.pt", weights_only=True)
+    assert int(b["attempt"]) == 1  # the run that finished is the restarted one
+    assert torch.equal(a["P"], b["P"])
+    # without a restart budget the same failure ends the job with an error instead of hanging
+    fail = _torchrun(tmp_path, str(tmp_path / "ckpt2"), str(tmp_path / "fail.pt"), fault="1:10", restarts=0)
+    assert fail.returncode != 0 and not os.path.exists(tmp_path / "fail.pt")
+
+
+def _stall_worker(rank, port, out_dir):
+    import time
+
+    import torch.distributed as dist
+
+    os.environ.update(RANK=str(rank), WORLD_SIZE="2", LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port))
+    from har.parallel import dist as hd
+
+    ctx = hd.init(device="cpu", timeout_s=4)
+    if rank == 1:
+        time.sleep(10)  # a stalled rank: never reaches the collective in time
+    t0 = time.time()
+    err = ""
+    try:
+        dist.all_reduce(torch.ones(4))
+    except Exception as e:  # gloo raises on the timeout (peer stalled / gone)
+        err = type(e).__name__ + ": " + str(e)[:200]
+    with open(os.path.join(out_dir, f"stall_{rank}.txt"), "w") as f:
+        f.write(f"{time.time() - t0:.2f}\n{err}")
+    os._exit(0)  # the group is broken: skip destroy_process_group
+
+
+def test_stalled_rank_makes_peers_time_out(tmp_path):
+    """Failure detection: a rank that stalls before a collective makes its peer's collective raise
+    after the group timeout (HAR_DIST_TIMEOUT_S / init(timeout_s=...)) instead of hanging."""
+    import socket
+
+    import torch.multiprocessing as mp
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    mp.spawn(_stall_worker, args=(port, str(tmp_path)), nprocs=2, join=True)
+    elapsed, err = (tmp_path / "stall_0.txt").read_text().split("\n", 1)
+    assert err, "rank 0's all_reduce returned although rank 1 never joined"
+    assert float(elapsed) < 9.0, elapsed  # raised by the 4 s timeout, not by rank 1 arriving at 10 s

@@ -242,7 +242,7 @@ def test_feature_subsets_device_matches_host(cuda, F, m):
     out = torch.empty(5000, m, dtype=torch.int32, device=cuda)
     tr = torch.as_tensor(trees, dtype=torch.int32, device=cuda)
     nd = torch.as_tensor(nodes, dtype=torch.int32, device=cuda)
-    _native.kernels().tree_feature_subsets(7, tr.data_ptr(), nd.data_ptr(), 5000, F, m, out.data_ptr(),
+    _native.kernels().tree_feature_subsets(7, tr.data_ptr(), nd.data_ptr(), 5000, F, m, out.data_ptr(), 0,
                                            _native.stream_ptr())
     assert np.array_equal(out.cpu().numpy(), host)
 
@@ -302,6 +302,57 @@ def test_planned_levels_equal_node_blocks(cuda, monkeypatch):
         monkeypatch.setattr(tree_mod, "FORCE_NODE_BLOCKS", node_blocks)
         fits[node_blocks] = RandomForestClassifier(numTrees=30, maxDepth=9, seed=3).fit_tensors(xc, yc, 6)
     a, b = fits[True].arrs, fits[False].arrs
+    for name in ("feature", "threshold", "left", "right", "stats", "gain"):
+        assert torch.equal(getattr(a, name), getattr(b, name)), name
+
+
+@pytest.mark.parametrize("kind,depth", [("rf", 14), ("rf", 6), ("dt", 8)])
+def test_device_count_levels_equal_synced_levels(cuda, monkeypatch, kind, depth):
+    """Levels enqueued on device-side counts (grids / arrays sized by bounds, no D2H until the
+    fit ends) grow the forest of levels that read their counts back every level, node for node.
+    Depth 14 crosses the grouping's per-tree bound, so that fit switches to a synced level
+    mid-way and back; the DT case samples every feature (m = F) with entropy."""
+    from har.models import tree as tree_mod
+    from har.models.tree import DecisionTreeClassifier, RandomForestClassifier
+
+    x, y = _blobs(7000, 18, 6, seed=21)
+    xc, yc = x.to(cuda), y.to(cuda)
+    fits = {}
+    for sync in (True, False):
+        monkeypatch.setattr(tree_mod, "FORCE_LEVEL_SYNC", sync)
+        if kind == "rf":
+            est = RandomForestClassifier(numTrees=24, maxDepth=depth, seed=5)
+        else:
+            est = DecisionTreeClassifier(maxDepth=depth, impurity="entropy")
+        fits[sync] = est.fit_tensors(xc, yc, 6)
+    a, b = fits[True].arrs, fits[False].arrs
+    assert np.array_equal(np.asarray(a.n_nodes), np.asarray(b.n_nodes))
+    for name in ("feature", "threshold", "left", "right", "stats", "gain"):
+        assert torch.equal(getattr(a, name), getattr(b, name)), name
+
+
+@pytest.mark.parametrize("kind,F", [("dt", 24), ("dt", 200), ("rf_all", 30)])
+def test_sibling_subtraction_equals_direct_histograms(cuda, monkeypatch, kind, F):
+    """Trees that search every feature keep each level's node histograms and take the heavier
+    sibling's as parent - lighter sibling (its rows skip the grouping and histogram passes); with
+    integer-valued weights the subtraction is exact, so the forest equals the one built from
+    direct histograms, bit for bit.  F = 200 splits the features over two LDS chunks; 9000 rows
+    make the top nodes 2048-row chunked (merged) work items."""
+    from har.models import tree as tree_mod
+    from har.models.tree import DecisionTreeClassifier, RandomForestClassifier
+
+    x, y = _blobs(9000, F, 6, seed=31)
+    xc, yc = x.to(cuda), y.to(cuda)
+    fits = {}
+    for sub in (False, True):
+        monkeypatch.setattr(tree_mod, "SIBLING_SUBTRACTION", sub)
+        if kind == "dt":
+            est = DecisionTreeClassifier(maxDepth=9)
+        else:
+            est = RandomForestClassifier(numTrees=6, maxDepth=8, featureSubsetStrategy="all", seed=2)
+        fits[sub] = est.fit_tensors(xc, yc, 6)
+    a, b = fits[False].arrs, fits[True].arrs
+    assert np.array_equal(np.asarray(a.n_nodes), np.asarray(b.n_nodes))
     for name in ("feature", "threshold", "left", "right", "stats", "gain"):
         assert torch.equal(getattr(a, name), getattr(b, name)), name
 
