@@ -570,54 +570,58 @@ __global__ __launch_bounds__(256) void find_splits_post_sort_kernel(const float*
 // Load-balanced level plan (one workgroup): node a is one work item when it has <= prows rows,
 // else ceil(count / prows) chunk items and a slot in the merged-histogram buffer.  plan layout
 // (int32): [0] items, [1] big nodes, [2] A, [3] unused, item_start [A + 1], big_rank [A] (-1 = not
-// big), big_list [A], item_node [items].  Block-wide scans over A in 1024-node steps.
+// big), big_list [A], item_node [items].  Thread t owns the contiguous nodes [t * per, (t+1) * per):
+// one pass sums its items / big nodes, ONE block scan gives its offsets, a second pass writes —
+// two barriers per level instead of three per 1024 nodes.
 __global__ __launch_bounds__(1024) void tree_plan_kernel(const int32_t* __restrict__ counts, int A, int prows,
                                                          int32_t* __restrict__ plan, const int32_t* __restrict__ a_dev) {
   __shared__ int wsum_i[16], wsum_b[16];
-  __shared__ int base_i, base_b;
   if (a_dev) A = *a_dev;  // the level's candidate count (the host's A is then only a bound)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   int32_t* item_start = plan + 4;
   int32_t* big_rank = item_start + A + 1;
   int32_t* big_list = big_rank + A;
   int32_t* item_node = big_list + A;
-  if (tid == 0) { base_i = 0; base_b = 0; }
-  __syncthreads();
-  int cnt_next = tid < A ? counts[tid] : 0;  // counts are prefetched one step ahead
-  for (int a0 = 0; a0 < A; a0 += 1024) {
-    const int a = a0 + tid;
-    const int cnt = cnt_next;
-    cnt_next = a + 1024 < A ? counts[a + 1024] : 0;
-    const bool big = a < A && cnt > prows;
-    const int zc = a < A ? (big ? (cnt + prows - 1) / prows : 1) : 0;
-    // inclusive wave scans (shuffles), then across the 16 waves through LDS
-    int si = zc, sb = big ? 1 : 0;
+  const int per = (A + 1023) >> 10;
+  const int b = min(A, tid * per), e = min(A, b + per);
+  int ti = 0, tb = 0;
+  for (int a = b; a < e; ++a) {
+    const int cnt = counts[a];
+    const bool big = cnt > prows;
+    ti += big ? (cnt + prows - 1) / prows : 1;
+    tb += big;
+  }
+  // exclusive block scan of (items, big nodes): wave shuffles, then the 16 wave totals
+  int si = ti, sb = tb;
 #pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const int ui = __shfl_up(si, o, 64), ub = __shfl_up(sb, o, 64);
-      if (lane >= o) { si += ui; sb += ub; }
-    }
-    if (lane == 63) { wsum_i[wave] = si; wsum_b[wave] = sb; }
-    __syncthreads();
-    int oi = base_i, ob = base_b;
-    for (int w = 0; w < wave; ++w) { oi += wsum_i[w]; ob += wsum_b[w]; }
-    const int first = oi + si - zc, rank = ob + sb - (big ? 1 : 0);
-    if (a < A) {
-      item_start[a] = first;
-      big_rank[a] = big ? rank : -1;
-      if (big) big_list[rank] = a;
-      for (int z = 0; z < zc; ++z) item_node[first + z] = a;
-    }
-    __syncthreads();
-    if (tid == 0) {
-      for (int w = 0; w < 16; ++w) { base_i += wsum_i[w]; base_b += wsum_b[w]; }
-    }
-    __syncthreads();
+  for (int o = 1; o < 64; o <<= 1) {
+    const int ui = __shfl_up(si, o, 64), ub = __shfl_up(sb, o, 64);
+    if (lane >= o) { si += ui; sb += ub; }
+  }
+  if (lane == 63) { wsum_i[wave] = si; wsum_b[wave] = sb; }
+  __syncthreads();
+  int oi = si - ti, ob = sb - tb, all_i = 0, all_b = 0;
+#pragma unroll
+  for (int w = 0; w < 16; ++w) {
+    oi += w < wave ? wsum_i[w] : 0;
+    ob += w < wave ? wsum_b[w] : 0;
+    all_i += wsum_i[w];
+    all_b += wsum_b[w];
+  }
+  for (int a = b; a < e; ++a) {
+    const int cnt = counts[a];
+    const bool big = cnt > prows;
+    const int zc = big ? (cnt + prows - 1) / prows : 1;
+    item_start[a] = oi;
+    big_rank[a] = big ? ob : -1;
+    if (big) big_list[ob++] = a;
+    for (int z = 0; z < zc; ++z) item_node[oi + z] = a;
+    oi += zc;
   }
   if (tid == 0) {
-    item_start[A] = base_i;
-    plan[0] = base_i;
-    plan[1] = base_b;
+    item_start[A] = all_i;
+    plan[0] = all_i;
+    plan[1] = all_b;
     plan[2] = A;
     plan[3] = 0;
   }
