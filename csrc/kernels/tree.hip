@@ -93,6 +93,17 @@ __device__ __forceinline__ void split_search_pairs(const float* hist, const int*
   }
 }
 
+// Histogram add.  INTW: the weights are non-negative integers (bootstrap / subsample counts x 0/1
+// fold masks — every weight the forest builder produces), so the LDS histogram accumulates them as
+// uint32 (ds_add_u32) and is converted to fp32 once before the split search: the same sums (exact
+// below 2^24) without the float LDS atomic.
+template <bool INTW>
+__device__ __forceinline__ void hist_add(float* p, float w) {
+  if constexpr (INTW) atomicAdd(reinterpret_cast<unsigned int*>(p), (unsigned int)w);
+  else atomicAdd(p, w);
+}
+
+template <bool INTW>
 __global__ __launch_bounds__(256) void tree_hist_split_kernel(
     const uint8_t* __restrict__ bins, int64_t fstride, int64_t rstride, const int32_t* __restrict__ nbins_feat,
     const int32_t* __restrict__ rows, const float* __restrict__ row_w, const int32_t* __restrict__ node_start,
@@ -212,13 +223,13 @@ __global__ __launch_bounds__(256) void tree_hist_split_kernel(
           l[u] = label[r[u]];
         }
 #pragma unroll
-        for (int u = 0; u < HU; ++u) atomicAdd(hb + b[u] * K + l[u], w[u]);
+        for (int u = 0; u < HU; ++u) hist_add<INTW>(hb + b[u] * K + l[u], w[u]);
       }
       for (; ri < cnt; ri += rpi) {
         const int r = rows[start + ri];
         const float w = row_w[start + ri];
         const int b = bins[fo + (int64_t)r * rstride];
-        atomicAdd(hb + b * K + label[r], w);
+        hist_add<INTW>(hb + b * K + label[r], w);
       }
     }
   } else if (mode != 2 && cnt >= (int)blockDim.x) {
@@ -229,7 +240,7 @@ __global__ __launch_bounds__(256) void tree_hist_split_kernel(
       float* hl = hist + label[r];
       for (int fs = 0; fs < f_n; ++fs) {
         const int b = bins[fid[fs] * fstride + r * rstride];
-        atomicAdd(hl + (fs * maxbins + b) * K, w);
+        hist_add<INTW>(hl + (fs * maxbins + b) * K, w);
       }
     }
   } else if (mode != 2) {
@@ -245,10 +256,15 @@ __global__ __launch_bounds__(256) void tree_hist_split_kernel(
       const int r = rows[start + ri];
       const float w = row_w[start + ri];
       const int b = bins[fid[fs] * fstride + r * rstride];
-      atomicAdd(&hist[(fs * maxbins + b) * K + label[r]], w);
+      hist_add<INTW>(&hist[(fs * maxbins + b) * K + label[r]], w);
     }
   }
   __syncthreads();
+  if (INTW && mode != 2) {  // uint32 counts -> fp32 (exact below 2^24)
+    const unsigned int* hu = reinterpret_cast<const unsigned int*>(hist);
+    for (int i = tid; i < f_n * maxbins * K; i += blockDim.x) hist[i] = (float)hu[i];
+    __syncthreads();
+  }
   if (mode == 0 && by_node)  // keep the fused node's histogram for its children's subtraction
     for (int i = tid; i < f_n * maxbins * K; i += blockDim.x) gh[i] = hist[i];
   if (mode == 1) {
@@ -682,11 +698,16 @@ extern "C" int har_tree_hist_split_planned(const uint8_t* bins, int64_t N, int F
   if (planned && bound <= 0) return 0;
   dim3 grid(chunks, planned ? bound : A, row_chunks > 1 ? row_chunks : 1);
   const int64_t fstride = row_major ? 1 : N, rstride = row_major ? F : 1;
-  tree_hist_split_kernel<<<grid, 256, lds, s>>>(bins, fstride, rstride, nbins_feat, rows, row_w, node_start, node_count, feats, m,
-                                                fc, label, K, maxbins, min_inst, min_gain, impurity, out_gain,
-                                                out_feat, out_bin, out_left, out_total, mode, ghist,
-                                                planned ? plan : nullptr, prows, by_node, hprev, derive_from,
-                                                parent_of);
+  // integer-weight accumulation unless HAR_HIST_FLOAT_ATOMICS=1 (A/B switch; same results)
+  static const bool float_atomics = [] {
+    const char* e = getenv("HAR_HIST_FLOAT_ATOMICS");
+    return e && e[0] == '1';
+  }();
+  auto kern = float_atomics ? tree_hist_split_kernel<false> : tree_hist_split_kernel<true>;
+  kern<<<grid, 256, lds, s>>>(bins, fstride, rstride, nbins_feat, rows, row_w, node_start, node_count, feats, m, fc,
+                              label, K, maxbins, min_inst, min_gain, impurity, out_gain, out_feat, out_bin, out_left,
+                              out_total, mode, ghist, planned ? plan : nullptr, prows, by_node, hprev, derive_from,
+                              parent_of);
   HAR_CHECK_LAUNCH();
   return 0;
 }
