@@ -28,6 +28,8 @@ per-rank histograms are all-reduced before split selection.
 from __future__ import annotations
 
 import math
+import os
+import time
 from dataclasses import dataclass
 from typing import List, Optional
 
@@ -156,24 +158,8 @@ class ForestBuilder:
         gains = torch.zeros(Tn, maxn, dtype=torch.float32, device=dev)
         n_nodes = np.ones(Tn, dtype=np.int64)
         if dev.type == "cuda":
-            # ONE kernel (tree.hip tree_init): bootstrap weights x row weights, node ids, root class
-            # counts into stats[:, 0], label range check (read with the level loop's first sync)
-            W = torch.empty(Tn, N, dtype=torch.float32, device=dev)
-            node_of = torch.empty(Tn, N, dtype=torch.int32, device=dev)
-            bad = torch.zeros(1, dtype=torch.int32, device=dev)
             rw = None if row_weight is None else row_weight.to(device=dev, dtype=torch.float32).contiguous()
-            cdf = [] if self.cdf is None else [int(v) for v in self.cdf]
-            _native.kernels().tree_init(self.seed, self.tree_offset, Tn, row_offset, N, cdf,
-                                        0 if rw is None else rw.data_ptr(), y32.data_ptr(), K, W.data_ptr(),
-                                        node_of.data_ptr(), stats.data_ptr(), maxn * K, bad.data_ptr(),
-                                        _native.stream_ptr())
-            if self.allreduce is not None:
-                root = stats[:, 0].contiguous()
-                self.allreduce(root)
-                stats[:, 0] = root
-            _levels_device_frontier(self, y32, W, N, F, m, maxn, stats, feature, thresh, left, right, gains,
-                                    n_nodes, node_of, bad)
-            return ForestArrays(feature, thresh, left, right, stats, n_nodes, D, gains)
+            return _fit_device(self, y32, rw, row_offset, N, F, m, maxn)
         # ---- CPU builder (PyTorch; the oracle of the device loop) ----
         W = self.bootstrap_weights(N, dev, row_offset)        # [T, N]
         if row_weight is not None:
@@ -276,6 +262,10 @@ ASYNC_MAX_COUNT_WS = 1 << 27
 # a child's features are not its parent's, so there is no parent histogram to subtract from.
 SUBTRACT_MAX_BYTES = 4 << 30
 SIBLING_SUBTRACTION = True
+# ... and only for fits of at least this many (tree, row) pairs: below it a level is launch-bound and
+# the store writes + derive pass cost more than the halved histogram work saves (bench --config dt:
+# 60k rows 2.71 ms with, 2.57 ms without)
+SUBTRACT_MIN_PAIRS = 1 << 20
 
 
 # Test hook: when True the level loop groups rows with the stable radix sort of the level keys
@@ -287,11 +277,17 @@ FORCE_NODE_BLOCKS = False
 # Test hook: when True every level reads its counts back (one 16-byte D2H per level) instead of
 # running on device-side counts; both grow the same forest.
 FORCE_LEVEL_SYNC = False
+# host timestamps of the last device level loop: (start, every level enqueued, node counts read back)
+LAST_LEVEL_TIMES = (0.0, 0.0, 0.0)
 
 
 def _levels_device_frontier(b: "ForestBuilder", y32, W, N: int, F: int, m: int, maxn: int, stats, feature, thresh,
-                            left, right, gains, n_nodes, node_of, bad):
-    """Device level loop with the frontier resident on the GPU.
+                            left, right, gains, node_of):
+    """Device level loop with the frontier resident on the GPU; returns the per-tree node counts
+    (a device tensor: the caller reads them back once).
+
+    The root frontier (candidate roots: impurity > 1e-12 in fp64 and weight >= 2 minInstances, the
+    decision kernel's rule) is built on the device from the root class counts (tree_root_frontier).
 
     Per level (tree_level.hip unless noted): stable counting-sort grouping of the (tree, row)
     pairs by candidate node; Floyd feature subsets; the fused histogram + split kernel
@@ -319,43 +315,36 @@ def _levels_device_frontier(b: "ForestBuilder", y32, W, N: int, F: int, m: int, 
     planned = b.owner is None and b.allreduce is None and not FORCE_NODE_BLOCKS
     async_ok = planned and not FORCE_SORT_GROUPING and not FORCE_LEVEL_SYNC
     slot_bytes = 4 * F * b.max_bins * K
-    subtract = planned and m >= F and SIBLING_SUBTRACTION
+    subtract = planned and m >= F and SIBLING_SUBTRACTION and Tn * N >= SUBTRACT_MIN_PAIRS
     hprev = parent_of = derive_from = None  # the previous level's store and this level's derive info
 
-    # the root class counts and the label check in ONE device -> host read; root candidacy on the
-    # host in fp64 (the device decision kernel's rule: impurity > 1e-12, weight >= 2 minInstances)
-    head = torch.cat([stats[:, 0].reshape(-1), bad.to(torch.float32)]).cpu().numpy()
-    if head[-1] != 0:
-        raise ValueError("labels out of range")
-    root = head[:-1].reshape(Tn, K).astype(np.float64)
-    w0 = root.sum(1)
-    p0 = root / np.maximum(w0, 1e-30)[:, None]
-    if b.impurity == T.GINI:
-        imp0 = 1.0 - (p0 * p0).sum(1)
-    else:
-        imp0 = -(p0 * np.where(p0 > 0, np.log2(np.maximum(p0, 1e-30)), 0.0)).sum(1)
-    c0 = (imp0 > 1e-12) & (w0 >= 2 * b.min_inst)
-    ct0 = np.nonzero(c0)[0]
-    A = len(ct0)
-    if A == 0:
-        return
-    max_w = float(w0[c0].max())
-    ct = torch.from_numpy(ct0.astype(np.int32)).to(dev)
-    cn = torch.zeros(A, **i32)
-    tlo = torch.from_numpy(np.concatenate([[0], np.cumsum(c0.astype(np.int64))]).astype(np.int32)).to(dev)
-    nt_max = 1
-    exact = True  # A / nt_max are this level's exact counts (else bounds; the counts live in scal_all)
+    # root frontier on the device: scal_all row 0 = [0, root candidates, 1, max root weight bits]
+    A, nt_max = Tn, 1  # bounds (exact = False: the kernels read the root candidate count from row 0)
+    exact = False
+    ct, cn, tlo = torch.empty(A, **i32), torch.empty(A, **i32), torch.empty(Tn + 1, **i32)
     cand_idx = torch.full((Tn, maxn), -1, **i32)  # stale entries name nodes no row sits in any more
-    cand_idx[ct.long(), 0] = torch.arange(A, **i32)
-    nn = torch.from_numpy(n_nodes.astype(np.int32)).to(dev)
+    scal_all = torch.zeros(4 * (D + 1), **i32)
+    mod.tree_root_frontier(stats.data_ptr(), Tn, K, maxn * K, b.impurity, float(2 * b.min_inst), maxn,
+                           ct.data_ptr(), cn.data_ptr(), tlo.data_ptr(), cand_idx.data_ptr(), scal_all.data_ptr(), st)
+    nn = torch.ones(Tn, **i32)
     nn_next = torch.empty_like(nn)
     split_bin = torch.zeros(Tn, maxn, **i32)
     rows_buf = torch.empty(Tn * N, **i32)
     roww_buf = torch.empty(Tn * N, dtype=torch.float32, device=dev)
     tlo_next = torch.empty(Tn + 1, **i32)
-    scal_all = torch.zeros(4 * (D + 1), **i32)
-    scal_h = torch.empty(4, dtype=torch.int32).pin_memory()
+    scal_h = None
+    max_w = 0.0
+    if not async_ok:  # exact counts from the start (data parallel / test hooks): read row 0 back
+        scal_h = torch.empty(4, dtype=torch.int32).pin_memory()
+        scal_h.copy_(scal_all[:4])
+        A, wbits = int(scal_h[1]), int(scal_h[3])
+        max_w = float(np.array([wbits], dtype=np.int32).view(np.float32)[0])
+        exact = True
+        if A == 0:
+            return nn
+        ct, cn = ct[:A], cn[:A]
     cnt_ws = None
+    t_start = time.perf_counter()
     for depth in range(D):
         a_dev = 0 if exact else scal_all.data_ptr() + 4 * (4 * depth + 1)
         scal = scal_all[4 * (depth + 1):4 * (depth + 2)]
@@ -415,11 +404,14 @@ def _levels_device_frontier(b: "ForestBuilder", y32, W, N: int, F: int, m: int, 
                           dsi.data_ptr(), front.data_ptr(), q.data_ptr(), ct_next.data_ptr(), cn_next.data_ptr(),
                           tlo_next.data_ptr(), cand_idx.data_ptr(), scal.data_ptr(), a_dev,
                           par_n.data_ptr() if derive else 0, der_n.data_ptr() if derive else 0, st)
-        stay_async = (async_ok and depth + 1 < D and A_b <= ASYNC_MAX_NODES and nch * A_b <= ASYNC_MAX_COUNT_WS
-                      and 2 * nt_max <= GROUP_MAX_NT)
+        # the last level commits on the device count too (nothing after it needs the host)
+        bounds_ok = A_b <= ASYNC_MAX_NODES and nch * A_b <= ASYNC_MAX_COUNT_WS and 2 * nt_max <= GROUP_MAX_NT
+        stay_async = async_ok and (depth + 1 == D or bounds_ok)
         if stay_async:  # the next level runs on the device counts in scal
             S, s_dev, A_next, nt_next = A, scal.data_ptr(), A_b, 2 * nt_max
         else:
+            if scal_h is None:
+                scal_h = torch.empty(4, dtype=torch.int32).pin_memory()
             scal_h.copy_(scal)  # this level's one sync
             S, A_next, nt_next, wbits = (int(v) for v in scal_h.tolist())
             s_dev = 0
@@ -441,7 +433,135 @@ def _levels_device_frontier(b: "ForestBuilder", y32, W, N: int, F: int, m: int, 
         hprev, parent_of, derive_from = (store, par_n, der_n) if derive else (None, None, None)
         if A == 0:
             break
-    n_nodes[:] = nn.cpu().numpy()
+    global LAST_LEVEL_TIMES
+    LAST_LEVEL_TIMES = (t_start, time.perf_counter(), 0.0)
+    return nn
+
+
+def levels_all_async(b: "ForestBuilder", N: int, F: int, m: int) -> bool:
+    """True when every level of this fit runs on device-side counts (no host read inside the
+    loop): the condition for capturing the fit in a HIP graph.  The loop's decisions depend only
+    on the bounds, so this replays them."""
+    if b.owner is not None or b.allreduce is not None or FORCE_NODE_BLOCKS or FORCE_SORT_GROUPING \
+            or FORCE_LEVEL_SYNC:
+        return False
+    nch = _native.kernels().tree_level_group_chunks(N)
+    A, nt = b.T, 1
+    for depth in range(b.D - 1):
+        A_b = min(2 * A, b.T * N)
+        if A_b > ASYNC_MAX_NODES or nch * A_b > ASYNC_MAX_COUNT_WS or 2 * nt > GROUP_MAX_NT:
+            return False
+        A, nt = A_b, 2 * nt
+    return True
+
+
+# HIP graphs of whole device fits (tree_init + root frontier + every level), keyed by everything
+# the launches bake in; a signature is captured the second time it is fitted (a one-off fit stays
+# eager: capture costs about one eager fit) and replayed from then on, after its inputs are
+# copied into the graph's static buffers.  HAR_TREE_GRAPH=0 disables it.
+FIT_GRAPHS = os.environ.get("HAR_TREE_GRAPH", "1") != "0"
+FIT_GRAPH_MAX = 8
+_fit_graph_seen: dict = {}
+_fit_graphs: dict = {}
+
+
+class _FitGraph:
+    def __init__(self, b: "ForestBuilder", y32, rw, N: int, F: int, maxn: int):
+        dev = y32.device
+        Tn, K = b.T, b.K
+        self.bins = torch.empty_like(b.bins)
+        self.nbins = torch.empty_like(b.nbins)
+        self.thr_mat = torch.empty_like(b.thr_mat)
+        self.y32 = torch.empty_like(y32)
+        self.rw = None if rw is None else torch.empty_like(rw)
+        self.bufs = _alloc_fit_buffers(Tn, N, K, maxn, dev)
+        self.graph = None
+        self.maxn = maxn
+
+    def load(self, b: "ForestBuilder", y32, rw):
+        self.bins.copy_(b.bins)
+        self.nbins.copy_(b.nbins)
+        self.thr_mat.copy_(b.thr_mat)
+        self.y32.copy_(y32)
+        if rw is not None:
+            self.rw.copy_(rw)
+
+
+def _alloc_fit_buffers(Tn: int, N: int, K: int, maxn: int, dev) -> dict:
+    return dict(W=torch.empty(Tn, N, dtype=torch.float32, device=dev),
+                node_of=torch.empty(Tn, N, dtype=torch.int32, device=dev),
+                bad=torch.empty(1, dtype=torch.int32, device=dev),
+                feature=torch.empty(Tn, maxn, dtype=torch.int32, device=dev),
+                thresh=torch.empty(Tn, maxn, dtype=torch.float32, device=dev),
+                left=torch.empty(Tn, maxn, dtype=torch.int32, device=dev),
+                right=torch.empty(Tn, maxn, dtype=torch.int32, device=dev),
+                stats=torch.empty(Tn, maxn, K, dtype=torch.float32, device=dev),
+                gains=torch.empty(Tn, maxn, dtype=torch.float32, device=dev))
+
+
+def _enqueue_fit(b: "ForestBuilder", bufs: dict, y32, rw, row_offset: int, N: int, F: int, m: int, maxn: int):
+    """Every launch of one device fit into ``bufs`` (no host read on one device): initial node
+    arrays, tree_init (bootstrap weights x row weights, node ids, root class counts, label check), the
+    DP all-reduce of the root counts, the level loop.  Returns the node-count tensor."""
+    Tn, K = b.T, b.K
+    bufs["feature"].fill_(-1)
+    for k in ("thresh", "left", "right", "stats", "gains"):
+        bufs[k].zero_()
+    bufs["bad"].zero_()
+    cdf = [] if b.cdf is None else [int(v) for v in b.cdf]
+    _native.kernels().tree_init(b.seed, b.tree_offset, Tn, row_offset, N, cdf, 0 if rw is None else rw.data_ptr(),
+                                y32.data_ptr(), K, bufs["W"].data_ptr(), bufs["node_of"].data_ptr(),
+                                bufs["stats"].data_ptr(), maxn * K, bufs["bad"].data_ptr(), _native.stream_ptr())
+    if b.allreduce is not None:
+        root = bufs["stats"][:, 0].contiguous()
+        b.allreduce(root)
+        bufs["stats"][:, 0] = root
+    return _levels_device_frontier(b, y32, bufs["W"], N, F, m, maxn, bufs["stats"], bufs["feature"], bufs["thresh"],
+                                   bufs["left"], bufs["right"], bufs["gains"], bufs["node_of"])
+
+
+def _finish_fit(b: "ForestBuilder", bufs: dict, nn, clone: bool) -> ForestArrays:
+    h = torch.cat([nn, bufs["bad"]]).cpu().numpy()  # the fit's one device -> host read
+    if h[-1] != 0:
+        raise ValueError("labels out of range")
+    o = {k: (v.clone() if clone else v) for k, v in bufs.items()}
+    return ForestArrays(o["feature"], o["thresh"], o["left"], o["right"], o["stats"], h[:-1].astype(np.int64), b.D,
+                        o["gains"])
+
+
+def _fit_device(b: "ForestBuilder", y32, rw, row_offset: int, N: int, F: int, m: int, maxn: int) -> ForestArrays:
+    dev = y32.device
+    key = None
+    if FIT_GRAPHS and levels_all_async(b, N, F, m):
+        key = (dev.index, b.T, b.K, b.D, N, F, m, maxn, b.max_bins, b.impurity, b.min_inst, b.min_gain, b.seed,
+               b.tree_offset, None if b.cdf is None else tuple(int(v) for v in b.cdf), rw is not None, row_offset,
+               SIBLING_SUBTRACTION, SUBTRACT_MIN_PAIRS, SUBTRACT_MAX_BYTES, ASYNC_MAX_NODES, ASYNC_MAX_COUNT_WS,
+               b.bins.shape, tuple(b.thr_mat.shape))
+    ent = _fit_graphs.get(key) if key is not None else None
+    if ent is None and key is not None and _fit_graph_seen.get(key, 0) >= 1 and len(_fit_graphs) < FIT_GRAPH_MAX:
+        # second fit of this signature: capture it (the first, eager fit warmed every kernel up)
+        ent = _FitGraph(b, y32, rw, N, F, maxn)
+        ent.load(b, y32, rw)
+        own = (b.bins, b.nbins, b.thr_mat)
+        b.bins, b.nbins, b.thr_mat = ent.bins, ent.nbins, ent.thr_mat
+        try:
+            torch.cuda.synchronize(dev)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                ent.nn = _enqueue_fit(b, ent.bufs, ent.y32, ent.rw, row_offset, N, F, m, maxn)
+            ent.graph = g
+        finally:
+            b.bins, b.nbins, b.thr_mat = own
+        _fit_graphs[key] = ent
+    if ent is not None:
+        ent.load(b, y32, rw)
+        ent.graph.replay()
+        return _finish_fit(b, ent.bufs, ent.nn, clone=True)
+    if key is not None:
+        _fit_graph_seen[key] = _fit_graph_seen.get(key, 0) + 1
+    bufs = _alloc_fit_buffers(b.T, N, b.K, maxn, dev)
+    nn = _enqueue_fit(b, bufs, y32, rw, row_offset, N, F, m, maxn)
+    return _finish_fit(b, bufs, nn, clone=False)
 
 
 def predict_forest(arrs: ForestArrays, X: torch.Tensor, normalize: bool) -> torch.Tensor:

@@ -278,6 +278,7 @@ def bench_rf(args, ctx, nine_axis=False, single_tree=False):
         Xt = Xt[:, :N_FEATURES].contiguous()
     if single_tree:  # every feature at every node: sibling subtraction applies (--no-subtract: off)
         tree_mod.SIBLING_SUBTRACTION = not args.no_subtract
+        tree_mod.SUBTRACT_MIN_PAIRS = 0  # measure the subtraction at every size
         est = DecisionTreeClassifier(maxDepth=args.depth, maxBins=32, device=dev)
     else:
         est = RandomForestClassifier(numTrees=args.trees or (500 if nine_axis else 100), maxDepth=args.depth,

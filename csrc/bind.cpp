@@ -493,6 +493,12 @@ PYBIND11_MODULE(_har_native, m) {
                             P<int32_t>(parent_of), P<int32_t>(derive_from), S(stream)),
           "tree_frontier");
   });
+  m.def("tree_root_frontier", [](u stats, int Tn, int K, int64_t tree_stride, int impurity, float min2, int maxn, u ct,
+                                 u cn, u tlo, u cand_idx, u scal, u stream) {
+    check(har_tree_root_frontier(P<const float>(stats), Tn, K, tree_stride, impurity, min2, maxn, P<int32_t>(ct),
+                                 P<int32_t>(cn), P<int32_t>(tlo), P<int32_t>(cand_idx), P<int32_t>(scal), S(stream)),
+          "tree_root_frontier");
+  });
   m.def("tree_partition", [](u node_of, u lvl_feat, u lvl_bin, u lvl_left, u bins, int T, int64_t N, int maxn,
                              u stream) {
     check(har_tree_partition(P<int32_t>(node_of), P<const int32_t>(lvl_feat), P<const int32_t>(lvl_bin),

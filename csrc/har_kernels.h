@@ -295,6 +295,11 @@ int har_tree_frontier(int A, int Tn, int maxn, const int32_t* ct, const int32_t*
                       int64_t* ni, int64_t* cl, int64_t* dsi, float* front, int32_t* q_ws, int32_t* ct_next,
                       int32_t* cn_next, int32_t* tlo_next, int32_t* cand_idx, int32_t* scal, const int32_t* a_dev,
                       int32_t* parent_of, int32_t* derive_from, hipStream_t s);
+// Root frontier (candidate roots, tree starts, cand_idx, scal = [0, A, 1, max weight bits]) from the
+// root class counts stats[t * tree_stride .. + K), on the device.
+int har_tree_root_frontier(const float* stats, int Tn, int K, int64_t tree_stride, int impurity, float min2,
+                           int maxn, int32_t* ct, int32_t* cn, int32_t* tlo, int32_t* cand_idx, int32_t* scal,
+                           hipStream_t s);
 int har_tree_partition(int32_t* node_of, const int32_t* lvl_feat, const int32_t* lvl_bin, const int32_t* lvl_left,
                        const uint8_t* bins, int T, int64_t N, int maxn, hipStream_t s);
 int har_forest_predict(const float* X, int64_t n, int F, int ld, const int32_t* feat, const float* thr,

@@ -484,6 +484,79 @@ __global__ __launch_bounds__(256) void frontier_next_kernel(int A, int Tn, int m
   atomicMax(&scal[3], __float_as_int(wgt));  // weights >= 0: float order == int order
 }
 
+// Root frontier on the device (one workgroup): tree t's root is a candidate when its impurity is
+// > 1e-12 (fp64) and its weight >= 2 minInstances — the rule of tree_level_decide_kernel.
+// Candidates are compacted in tree order: ct (tree ids), cn = 0, tlo[t] = first candidate of tree t,
+// cand_idx[t][0]; scal = [0, candidates, 1 (max per tree), max candidate weight (float bits)].
+// Thread i owns the contiguous trees [i * per, (i + 1) * per); one block scan.
+__global__ __launch_bounds__(1024) void tree_root_frontier_kernel(const float* __restrict__ stats, int Tn, int K,
+                                                                  int64_t tree_stride, int impurity, float min2,
+                                                                  int maxn, int32_t* __restrict__ ct,
+                                                                  int32_t* __restrict__ cn, int32_t* __restrict__ tlo,
+                                                                  int32_t* __restrict__ cand_idx,
+                                                                  int32_t* __restrict__ scal) {
+  __shared__ int wsum[16];
+  __shared__ int wmax[16];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int per = (Tn + 1023) >> 10;
+  const int b = min(Tn, tid * per), e = min(Tn, b + per);
+  auto cand = [&](int t, float& w_out) {
+    const float* st = stats + (int64_t)t * tree_stride;
+    float w = 0.f;
+    for (int k = 0; k < K; ++k) w += st[k];
+    const double dw = fmax((double)w, 1e-30);
+    double q = 0.0;
+    for (int k = 0; k < K; ++k) {
+      const double p = (double)st[k] / dw;
+      if (impurity == 0) q += p * p;
+      else q -= p > 0 ? p * log2(fmax(p, 1e-30)) : 0.0;
+    }
+    const double imp = impurity == 0 ? 1.0 - q : q;
+    w_out = w;
+    return imp > 1e-12 && w >= min2;
+  };
+  int cnt = 0, mx = 0;
+  for (int t = b; t < e; ++t) {
+    float w;
+    if (cand(t, w)) { ++cnt; mx = max(mx, __float_as_int(w)); }  // weights >= 0: int order = float order
+  }
+  int x = cnt, m = mx;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+    m = max(m, __shfl_xor(m, o, 64));
+  }
+  if (lane == 63) wsum[wave] = x;
+  if (lane == 0) wmax[wave] = m;
+  __syncthreads();
+  int run = x - cnt, tot = 0, gmax = 0;
+#pragma unroll
+  for (int w = 0; w < 16; ++w) {
+    run += w < wave ? wsum[w] : 0;
+    tot += wsum[w];
+    gmax = max(gmax, wmax[w]);
+  }
+  for (int t = b; t < e; ++t) {
+    float w;
+    const bool c = cand(t, w);
+    tlo[t] = run;
+    if (c) {
+      ct[run] = t;
+      cn[run] = 0;
+      cand_idx[(int64_t)t * maxn] = run;
+      ++run;
+    }
+  }
+  if (tid == 0) {
+    tlo[Tn] = tot;
+    scal[0] = 0;
+    scal[1] = tot;
+    scal[2] = 1;
+    scal[3] = gmax;
+  }
+}
+
 int grid_for(int64_t total) { return (int)std::max<int64_t>(1, std::min<int64_t>(8192, (total + 255) / 256)); }
 
 }  // namespace
@@ -593,6 +666,16 @@ extern "C" int har_tree_frontier(int A, int Tn, int maxn, const int32_t* ct, con
   const int g2 = (std::max(2 * A, Tn + 1) + 255) / 256;
   frontier_next_kernel<<<g2, 256, 0, s>>>(A, Tn, maxn, tlo, dec, pos_ws, ti, cl, dsi, front, q_ws, ct_next, cn_next,
                                           tlo_next, cand_idx, scal, a_dev, parent_of, derive_from);
+  HAR_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int har_tree_root_frontier(const float* stats, int Tn, int K, int64_t tree_stride, int impurity, float min2,
+                                      int maxn, int32_t* ct, int32_t* cn, int32_t* tlo, int32_t* cand_idx,
+                                      int32_t* scal, hipStream_t s) {
+  if (Tn <= 0 || K <= 0) return -2;
+  tree_root_frontier_kernel<<<1, 1024, 0, s>>>(stats, Tn, K, tree_stride, impurity, min2, maxn, ct, cn, tlo, cand_idx,
+                                               scal);
   HAR_CHECK_LAUNCH();
   return 0;
 }

@@ -331,6 +331,38 @@ def test_device_count_levels_equal_synced_levels(cuda, monkeypatch, kind, depth)
         assert torch.equal(getattr(a, name), getattr(b, name)), name
 
 
+@pytest.mark.parametrize("kind", ["rf", "dt_sub"])
+def test_fit_graph_replays_equal_eager_fits(cuda, monkeypatch, kind):
+    """A fit signature seen twice is captured as ONE HIP graph (tree_init, device root frontier,
+    every level) and replayed with new inputs copied into its static buffers: each replay grows
+    exactly the forest an eager fit of the same data grows (two data sets, alternating)."""
+    from har.models import tree as tree_mod
+    from har.models.tree import DecisionTreeClassifier, RandomForestClassifier
+
+    monkeypatch.setattr(tree_mod, "_fit_graphs", {})
+    monkeypatch.setattr(tree_mod, "_fit_graph_seen", {})
+    monkeypatch.setattr(tree_mod, "SUBTRACT_MIN_PAIRS", 0)
+    data = [_blobs(6000, 20, 6, seed=s) for s in (41, 42)]
+    data = [(x.to(cuda), y.to(cuda)) for x, y in data]
+
+    def fit(x, y):
+        if kind == "rf":
+            return RandomForestClassifier(numTrees=16, maxDepth=8, seed=9).fit_tensors(x, y, 6).arrs
+        return DecisionTreeClassifier(maxDepth=9).fit_tensors(x, y, 6).arrs
+
+    monkeypatch.setattr(tree_mod, "FIT_GRAPHS", False)
+    eager = [fit(*d) for d in data]
+    monkeypatch.setattr(tree_mod, "FIT_GRAPHS", True)
+    order = [0, 1, 0, 1]  # eager (first sighting), capture + replay, replay, replay
+    got = [fit(*data[i]) for i in order]
+    assert len(tree_mod._fit_graphs) == 1
+    for i, a in zip(order, got):
+        b = eager[i]
+        assert np.array_equal(np.asarray(a.n_nodes), np.asarray(b.n_nodes))
+        for name in ("feature", "threshold", "left", "right", "stats", "gain"):
+            assert torch.equal(getattr(a, name), getattr(b, name)), (i, name)
+
+
 @pytest.mark.parametrize("kind,F", [("dt", 24), ("dt", 200), ("rf_all", 30)])
 def test_sibling_subtraction_equals_direct_histograms(cuda, monkeypatch, kind, F):
     """Trees that search every feature keep each level's node histograms and take the heavier
@@ -344,6 +376,7 @@ def test_sibling_subtraction_equals_direct_histograms(cuda, monkeypatch, kind, F
     x, y = _blobs(9000, F, 6, seed=31)
     xc, yc = x.to(cuda), y.to(cuda)
     fits = {}
+    monkeypatch.setattr(tree_mod, "SUBTRACT_MIN_PAIRS", 0)
     for sub in (False, True):
         monkeypatch.setattr(tree_mod, "SIBLING_SUBTRACTION", sub)
         if kind == "dt":
