@@ -42,6 +42,10 @@ from .base import ClassificationModel, ClassifierParams, Estimator, dp_allreduce
     features_tensor, labels_tensor, new_uid, resolve_device
 
 HEAD_PAD = 32  # classes padded to 32 rows (two 16-wide MFMA column tiles)
+# The fused backward recomputes h1 = relu(W0 x + b0) from the X tiles it reads anyway (bit-identical
+# to the forward's h1) instead of the forward writing and the backward reading B x 256 bf16 through
+# HBM; HAR_MLP_RECOMPUTE_H1=0 restores the stored h1 (A/B switch).
+RECOMPUTE_H1 = os.environ.get("HAR_MLP_RECOMPUTE_H1", "1") != "0"
 
 
 def _pad(x: int, m: int) -> int:
@@ -274,14 +278,16 @@ class MLPEngine:
         h1 = acts[1]
         dact = self.dbuf[1][: B * H].view(B, H)
         self.fused_nwg = mod.mlp_fwd_head_grid(B)
+        self.last_bwd = self.bwd_ok and B % 64 == 0 and mod.mlp_fwd_head_variant(H, B) == 2
+        # with the fused backward, h1 never reaches HBM: that kernel recomputes it from X (same bits)
+        rh1 = self.last_bwd and RECOMPUTE_H1
         mod.mlp_fwd_head(Xb.data_ptr(), K0, self._w(self.Pb, "W0").data_ptr(), self._w(self.P, "b0").data_ptr(),
                          self._w(self.Pb, "W1").data_ptr(), self._w(self.P, "b1").data_ptr(), H,
                          self._w(self.Pb, "Wout").data_ptr(), self._w(self.P, "bout").data_ptr(), y32.data_ptr(),
-                         B, L.num_classes, float(scale), h1.data_ptr(), dact.data_ptr(), self.fslab.data_ptr(),
-                         self.fblock_loss.data_ptr(), self.fblock_correct.data_ptr(), s)
+                         B, L.num_classes, float(scale), 0 if rh1 else h1.data_ptr(), dact.data_ptr(),
+                         self.fslab.data_ptr(), self.fblock_loss.data_ptr(), self.fblock_correct.data_ptr(), s)
         self.last_fused = True
         self.last_batch = B
-        self.last_bwd = self.bwd_ok and B % 64 == 0 and mod.mlp_fwd_head_variant(H, B) == 2
         if on_grad is not None:
             on_grad("Wout")
 
@@ -289,9 +295,11 @@ class MLPEngine:
             # dW1 + dgrad + relu' + dW0 / db0: one kernel, one partial per row slice in self.slabs
             self.bwd_S = mod.mlp_bwd_fused_slices(B)
             sb = self.slabs.data_ptr()
-            mod.mlp_bwd_fused(dact.data_ptr(), h1.data_ptr(), Xb.data_ptr(), K0, self._w(self.Pb, "W1").data_ptr(), H,
-                              B, sb + 4 * L.by_name["W1"].offset, sb + 4 * L.by_name["W0"].offset,
-                              sb + 4 * L.by_name["b0"].offset, total, self.step_count.data_ptr(), s)
+            mod.mlp_bwd_fused(dact.data_ptr(), 0 if rh1 else h1.data_ptr(), Xb.data_ptr(), K0,
+                              self._w(self.Pb, "W1").data_ptr(), H, B, sb + 4 * L.by_name["W1"].offset,
+                              sb + 4 * L.by_name["W0"].offset, sb + 4 * L.by_name["b0"].offset, total,
+                              self.step_count.data_ptr(), self._w(self.Pb, "W0").data_ptr(),
+                              self._w(self.P, "b0").data_ptr(), s)
             if on_grad is not None:
                 on_grad("W1")
                 on_grad("W0")

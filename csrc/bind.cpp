@@ -376,10 +376,10 @@ PYBIND11_MODULE(_har_native, m) {
   m.def("mlp_bwd_fused_slices", &har_mlp_bwd_fused_slices);
   m.def("mlp_fwd_head_variant", &har_mlp_fwd_head_variant);
   m.def("mlp_bwd_fused", [](u dact2, u h1, u X, int K0, u W1, int H, int B, u gw1, u gw0, u gb0, int64_t stride,
-                            u tick, u stream) {
+                            u tick, u W0, u b0, u stream) {
     check(har_mlp_bwd_fused(P<const uint16_t>(dact2), P<const uint16_t>(h1), P<const uint16_t>(X), K0,
                             P<const uint16_t>(W1), H, B, P<float>(gw1), P<float>(gw0), P<float>(gb0), stride,
-                            P<int32_t>(tick), S(stream)),
+                            P<int32_t>(tick), P<const uint16_t>(W0), P<const float>(b0), S(stream)),
           "mlp_bwd_fused");
   });
   m.def("mlp_fwd_head", [](u X, int K0, u W0, u b0, u W1, u b1, int H, u Wo, u bo, u labels, int B, int C,

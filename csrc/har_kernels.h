@@ -74,9 +74,10 @@ int har_mlp_fwd_head_grid(int B);
 // Fused backward after the fused forward (H = 256, B % 32 == 0): dW1 = dact2^T h1, dact1 = (dact2 W1) *
 // relu'(h1), dW0 = dact1^T X, db0 in one pass; per-slice partials at gw1 / gw0 / gb0 + s * slab_stride for
 // s < har_mlp_bwd_fused_slices(B).  har_mlp_fwd_head_variant: 2 = the 8-wave forward (writes db1 too).
+// h1 = nullptr: h1 is recomputed from X with W0 / b0 (pass h1 = nullptr to har_mlp_fwd_head too).
 int har_mlp_bwd_fused(const uint16_t* dact2, const uint16_t* h1, const uint16_t* X, int K0, const uint16_t* W1,
                       int H, int B, float* gw1, float* gw0, float* gb0, int64_t slab_stride, int32_t* tick,
-                      hipStream_t s);
+                      const uint16_t* W0, const float* b0, hipStream_t s);
 int har_mlp_bwd_fused_slices(int B);
 int har_mlp_fwd_head_variant(int H, int B);
 // Serving variant of the same kernel: logits [B][C] fp32 + argmax class [B] int32, nothing else.

@@ -467,7 +467,9 @@ __device__ __forceinline__ bf16x8_t frag_tr(const bf16_t* img, int pitch, int co
   return __builtin_bit_cast(bf16x8_t, v);
 }
 
-template <int K0, bool INFER, int XF = 0>
+// SH1 = false: h1 is not written (the fused backward recomputes it from X: 2 x B x 256 bf16 of HBM
+// traffic saved per step for ~2 GFLOP of MFMA work)
+template <int K0, bool INFER, int XF = 0, bool SH1 = true>
 __global__ __launch_bounds__(512) void mlp_fwd_head_v2_kernel(
     const bf16_t* __restrict__ X, const bf16_t* __restrict__ W0, const float* __restrict__ b0,
     const bf16_t* __restrict__ W1, const float* __restrict__ b1, const bf16_t* __restrict__ Wo,
@@ -565,7 +567,7 @@ __global__ __launch_bounds__(512) void mlp_fwd_head_v2_kernel(
     }
     __syncthreads();  // the h1 tile (and the previous tile's dact2 tile) is complete
     if (!INFER) {  // coalesced row stores of h1 (this tile) and dact2 (the previous tile)
-      v2_store_tile(h1s, h1out, r0, tid);
+      if constexpr (SH1) v2_store_tile(h1s, h1out, r0, tid);
       // unconditional (same store count every tile, so the waits stay counted): the first tile
       // writes its not-yet-computed dact2 rows, which the same threads overwrite a tile later
       v2_store_tile(dts, dact, prev_r0 >= 0 ? prev_r0 : r0, tid);
@@ -616,8 +618,13 @@ __global__ __launch_bounds__(512) void mlp_fwd_head_v2_kernel(
     }
     __syncthreads();  // every wave's partial logits are in
     if (!INFER) {  // the labels (issued first this tile) are in: vmcnt(2 * K0C X loads + 4 stores)
-      if constexpr (K0C == 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      if constexpr (SH1) {
+        if constexpr (K0C == 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      } else {  // two tile stores fewer behind the labels
+        if constexpr (K0C == 2) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      }
     }
     // ---- logits, softmax, CE of half h in wave h < 2 (the other waves only need dz) ----
     if (wave < 2) {
@@ -763,9 +770,9 @@ int launch_v2(const bf16_t* X, const bf16_t* W0, const float* b0, const bf16_t* 
               const bf16_t* Wo, const float* bo, const int32_t* labels, int B, int C, float scale, bf16_t* h1,
               bf16_t* dact, float* slab, float* block_loss, int32_t* block_correct, int nwg, hipStream_t s,
               float* logits = nullptr, int32_t* pred = nullptr, int F = K0, int ldx = K0) {
-  mlp_fwd_head_v2_kernel<K0, INFER, XF><<<nwg, 512, V2_LDS, s>>>(X, W0, b0, W1, b1, Wo, bo, labels, B, C, scale,
-                                                                 h1, dact, slab, block_loss, block_correct, logits,
-                                                                 pred, F, ldx);
+  auto kern = (INFER || h1) ? mlp_fwd_head_v2_kernel<K0, INFER, XF, true> : mlp_fwd_head_v2_kernel<K0, INFER, XF, false>;
+  kern<<<nwg, 512, V2_LDS, s>>>(X, W0, b0, W1, b1, Wo, bo, labels, B, C, scale, h1, dact, slab, block_loss,
+                                block_correct, logits, pred, F, ldx);
   HAR_CHECK_LAUNCH();
   return 0;
 }
@@ -812,22 +819,29 @@ __device__ __forceinline__ bf16x8_t frag_rows(const bf16_t* img, int pitch, int 
   return __builtin_bit_cast(bf16x8_t, v);
 }
 
-template <int K0> struct BwdLds {
+// RH1: the h1 quadrant tiles are recomputed from the X tiles (h1 = relu(W0 . x + b0), the forward's
+// operands, accumulation order and rounding: bit-identical) instead of read from HBM; X is then
+// staged two tiles ahead through four buffers so tile i+1's h1 is computed during tile i.
+template <int K0, bool RH1 = false> struct BwdLds {
   static constexpr int XP = K0 + 16;
+  static constexpr int NXB = RH1 ? 4 : 3;  // X tile buffers
   static constexpr int DSM = BF_RT * BF_DP, HS = BF_RT * BF_UP, XS = BF_RT * XP;  // elements per buffer
-  static constexpr size_t bytes = (size_t)(2 * DSM + 2 * HS + 2 * HS + 3 * XS) * sizeof(bf16_t) +
+  static constexpr size_t bytes = (size_t)(2 * DSM + 2 * HS + 2 * HS + NXB * XS) * sizeof(bf16_t) +
                                   4 * BF_QU * sizeof(float);
 };
 
-template <int K0>
+template <int K0, bool RH1 = false>
 __global__ __launch_bounds__(512) void mlp_bwd_fused_kernel(const bf16_t* __restrict__ dact2,
                                                            const bf16_t* __restrict__ h1,
                                                            const bf16_t* __restrict__ X,
                                                            const bf16_t* __restrict__ W1, int B, int S,
                                                            float* __restrict__ gw1, float* __restrict__ gw0,
                                                            float* __restrict__ gb0, int64_t slab_stride,
-                                                           int32_t* __restrict__ tick) {
-  using L = BwdLds<K0>;
+                                                           int32_t* __restrict__ tick,
+                                                           const bf16_t* __restrict__ W0,
+                                                           const float* __restrict__ b0) {
+  using L = BwdLds<K0, RH1>;
+  constexpr int NXB = L::NXB;
   // the training step counter ticks here (one thread, before the reduction kernel reads it for Adam)
   if (tick && blockIdx.x == 0 && threadIdx.x == 0) *tick += 1;
   constexpr int H = V2_H, KC = H / 32, XP = L::XP, NFW = K0 / 32;
@@ -860,6 +874,17 @@ __global__ __launch_bounds__(512) void mlp_bwd_fused_kernel(const bf16_t* __rest
       for (int i = 0; i < 8; ++i) v[i] = (short)W1[(size_t)(kc * 32 + 8 * g + i) * H + qu0 + 16 * (up + e) + c16];
       w1t[e][kc] = __builtin_bit_cast(bf16x8_t, v);
     }
+  // (RH1) h1 recompute: wave w -> unit block w & 3 of the quadrant, row blocks 2 (w >> 2) + {0, 1};
+  // A = W0 rows of those units (the forward's stage-1 fragments), bias as the initial accumulator
+  const int ubh = wave & 3, rbh = 2 * (wave >> 2);
+  bf16x8_t w0q[NFW];
+  float4 b0q = make_float4(0.f, 0.f, 0.f, 0.f);
+  if constexpr (RH1) {
+#pragma unroll
+    for (int kc = 0; kc < NFW; ++kc)
+      w0q[kc] = *reinterpret_cast<const bf16x8_t*>(W0 + (size_t)(qu0 + 16 * ubh + c16) * K0 + kc * 32 + 8 * g);
+    b0q = *reinterpret_cast<const float4*>(b0 + qu0 + 16 * ubh + 4 * g);
+  }
   f32x4_t acc1[4][2], acc0[NFW];
 #pragma unroll
   for (int i = 0; i < 4; ++i) acc1[i][0] = acc1[i][1] = f32x4_t{0.f, 0.f, 0.f, 0.f};
@@ -879,8 +904,8 @@ __global__ __launch_bounds__(512) void mlp_bwd_fused_kernel(const bf16_t* __rest
   const int sdh = (tid >> 3) * BF_UP + (tid & 7) * 8;
   const int sdx = ((tid & (XV - 1)) / (K0 / 8)) * XP + ((tid & (XV - 1)) % (K0 / 8)) * 8;
   const int tlast = ntiles - 1;
-  uint4 r0, r1, r2, r3, r4, r5;
-#define HAR_BWD_LOAD(t)                                                      \
+  uint4 r0, r1, r2, r3, r4 = make_uint4(0, 0, 0, 0), r5;
+#define HAR_BWD_LOAD_D(t)                                                    \
   {                                                                          \
     const int64_t tt_ = min(t, tlast);                                       \
     const bf16_t* d_ = ldd + tt_ * BF_RT * H;                                \
@@ -888,18 +913,28 @@ __global__ __launch_bounds__(512) void mlp_bwd_fused_kernel(const bf16_t* __rest
     r1 = *reinterpret_cast<const uint4*>(d_ + 16 * H);                       \
     r2 = *reinterpret_cast<const uint4*>(d_ + 32 * H);                       \
     r3 = *reinterpret_cast<const uint4*>(d_ + 48 * H);                       \
-    r4 = *reinterpret_cast<const uint4*>(ldh + tt_ * BF_RT * H);             \
-    r5 = *reinterpret_cast<const uint4*>(ldx + tt_ * BF_RT * K0);            \
   }
-#define HAR_BWD_STAGE(i)                                                     \
+#define HAR_BWD_LOAD_X(t) r5 = *reinterpret_cast<const uint4*>(ldx + (int64_t)min(t, tlast) * BF_RT * K0);
+#define HAR_BWD_LOAD(t)                                                      \
+  {                                                                          \
+    HAR_BWD_LOAD_D(t)                                                        \
+    r4 = *reinterpret_cast<const uint4*>(ldh + (int64_t)min(t, tlast) * BF_RT * H); \
+    HAR_BWD_LOAD_X(t)                                                        \
+  }
+#define HAR_BWD_STAGE_D(i)                                                   \
   {                                                                          \
     bf16_t* d_ = dsm0 + ((i) & 1) * L::DSM + sdd;                            \
     *reinterpret_cast<uint4*>(d_) = r0;                                      \
     *reinterpret_cast<uint4*>(d_ + 16 * BF_DP) = r1;                         \
     *reinterpret_cast<uint4*>(d_ + 32 * BF_DP) = r2;                         \
     *reinterpret_cast<uint4*>(d_ + 48 * BF_DP) = r3;                         \
+  }
+#define HAR_BWD_STAGE_X(i) *reinterpret_cast<uint4*>(xs0 + ((i) % NXB) * L::XS + sdx) = r5;
+#define HAR_BWD_STAGE(i)                                                     \
+  {                                                                          \
+    HAR_BWD_STAGE_D(i)                                                       \
     *reinterpret_cast<uint4*>(hs0 + ((i) & 1) * L::HS + sdh) = r4;           \
-    *reinterpret_cast<uint4*>(xs0 + ((i) % 3) * L::XS + sdx) = r5;           \
+    HAR_BWD_STAGE_X(i)                                                       \
   }
 
   // (a) + (b) of local tile i (LDS buffers i & 1)
@@ -940,10 +975,10 @@ __global__ __launch_bounds__(512) void mlp_bwd_fused_kernel(const bf16_t* __rest
       }
     }
   };
-  // (c) of local tile i (its dact1 buffer i & 1, X buffer i % 3)
+  // (c) of local tile i (its dact1 buffer i & 1, X buffer i % NXB)
   auto tile_c = [&](int i) __attribute__((always_inline)) {
     const bf16_t* d1s = d1s0 + (i & 1) * L::HS;
-    const bf16_t* xs = xs0 + (i % 3) * L::XS;
+    const bf16_t* xs = xs0 + (i % NXB) * L::XS;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       const bf16x8_t A = frag_rows(d1s + 32 * ks * BF_UP, BF_UP, 16 * ub, lane);
@@ -953,22 +988,69 @@ __global__ __launch_bounds__(512) void mlp_bwd_fused_kernel(const bf16_t* __rest
     }
   };
 
-  HAR_BWD_LOAD(t0)
-  HAR_BWD_STAGE(0)
-  HAR_BWD_LOAD(t0 + 1)
-  __builtin_amdgcn_sched_barrier(0);
-  __syncthreads();  // tile 0 is in LDS
-  for (int i = 0; i < n; ++i) {
-    HAR_BWD_STAGE(i + 1)          // waits for the refill issued one iteration ago
-    HAR_BWD_LOAD(t0 + i + 2)
-    __builtin_amdgcn_sched_barrier(0);  // the refill is issued before the compute
-    tile_ab(i);
-    if (i > 0) tile_c(i - 1);     // wave-uniform
-    __syncthreads();              // tile i+1 staged; tile i's dact1 complete; buffers of i-1 free
+  // (RH1) h1 quadrant tile i from X tile i (buffer i % NXB) into h1 buffer i & 1
+  auto tile_h1 = [&](int i) __attribute__((always_inline)) {
+    const bf16_t* xs = xs0 + (i % NXB) * L::XS;
+    bf16_t* hs = hs0 + (i & 1) * L::HS;
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int row = 16 * (rbh + e) + c16;
+      f32x4_t a = {b0q.x, b0q.y, b0q.z, b0q.w};
+#pragma unroll
+      for (int kc = 0; kc < NFW; ++kc)
+        a = mma32(w0q[kc], *reinterpret_cast<const bf16x8_t*>(xs + row * XP + kc * 32 + 8 * g), a);
+      *reinterpret_cast<uint2*>(hs + row * BF_UP + 16 * ubh + 4 * g) =
+          make_uint2(relu2(pack2(a[0], a[1])), relu2(pack2(a[2], a[3])));
+    }
+  };
+
+  if constexpr (RH1) {
+    // invariant at the top of iteration i: r0..r3 = dact2 tile i+1, r5 = X tile i+2 (loaded)
+    HAR_BWD_LOAD_D(t0)
+    HAR_BWD_LOAD_X(t0)
+    HAR_BWD_STAGE_D(0)
+    HAR_BWD_STAGE_X(0)
+    HAR_BWD_LOAD_X(t0 + 1)
+    HAR_BWD_STAGE_X(1)
+    HAR_BWD_LOAD_D(t0 + 1)
+    HAR_BWD_LOAD_X(t0 + 2)
+    __builtin_amdgcn_sched_barrier(0);
+    __syncthreads();  // dact2 tile 0, X tiles 0 and 1 are in LDS
+    tile_h1(0);
+    __syncthreads();  // h1 tile 0 complete
+    for (int i = 0; i < n; ++i) {
+      HAR_BWD_STAGE_D(i + 1)        // waits for the refills issued one iteration ago
+      HAR_BWD_STAGE_X(i + 2)
+      HAR_BWD_LOAD_D(t0 + i + 2)
+      HAR_BWD_LOAD_X(t0 + i + 3)
+      __builtin_amdgcn_sched_barrier(0);  // the refills are issued before the compute
+      tile_h1(i + 1);               // X tile i+1 has been in LDS since the last barrier
+      tile_ab(i);
+      if (i > 0) tile_c(i - 1);     // wave-uniform
+      __syncthreads();              // dact2 i+1 / X i+2 staged, h1 i+1 and dact1 i complete
+    }
+  } else {
+    HAR_BWD_LOAD(t0)
+    HAR_BWD_STAGE(0)
+    HAR_BWD_LOAD(t0 + 1)
+    __builtin_amdgcn_sched_barrier(0);
+    __syncthreads();  // tile 0 is in LDS
+    for (int i = 0; i < n; ++i) {
+      HAR_BWD_STAGE(i + 1)          // waits for the refill issued one iteration ago
+      HAR_BWD_LOAD(t0 + i + 2)
+      __builtin_amdgcn_sched_barrier(0);  // the refill is issued before the compute
+      tile_ab(i);
+      if (i > 0) tile_c(i - 1);     // wave-uniform
+      __syncthreads();              // tile i+1 staged; tile i's dact1 complete; buffers of i-1 free
+    }
   }
   if (n > 0) tile_c(n - 1);
 #undef HAR_BWD_LOAD
+#undef HAR_BWD_LOAD_D
+#undef HAR_BWD_LOAD_X
 #undef HAR_BWD_STAGE
+#undef HAR_BWD_STAGE_D
+#undef HAR_BWD_STAGE_X
 
   // ---- this workgroup's parts of slab `slice` ----
   float* w1o = gw1 + (size_t)slice * slab_stride;
@@ -1074,18 +1156,32 @@ extern "C" int har_mlp_bwd_fused_slices(int B) { return std::max(1, std::min(64,
 
 // dW1 / dW0 / db0 of the 2-hidden-layer step (H = 256, B % 64 == 0): per-slice partials written at
 // gw1 / gw0 / gb0 + s * slab_stride (s < har_mlp_bwd_fused_slices(B)).
+// h1 == nullptr: recompute h1 from X with W0 / b0 (the forward then skips its h1 store).
 extern "C" int har_mlp_bwd_fused(const uint16_t* dact2, const uint16_t* h1, const uint16_t* X, int K0,
                                  const uint16_t* W1, int H, int B, float* gw1, float* gw0, float* gb0,
-                                 int64_t slab_stride, int32_t* tick, hipStream_t s) {
+                                 int64_t slab_stride, int32_t* tick, const uint16_t* W0, const float* b0,
+                                 hipStream_t s) {
   if (H != V2_H || B <= 0 || B % BF_RT || (K0 != 32 && K0 != 64) || slab_stride < (int64_t)H * H) return -2;
-  if (((uintptr_t)dact2 | (uintptr_t)h1 | (uintptr_t)X | (uintptr_t)W1) & 15) return -3;
+  if (((uintptr_t)dact2 | (uintptr_t)h1 | (uintptr_t)X | (uintptr_t)W1 | (uintptr_t)W0 | (uintptr_t)b0) & 15)
+    return -3;
+  if (!h1 && (!W0 || !b0)) return -4;
   const int S = har_mlp_bwd_fused_slices(B);
-  if (K0 == 64)
-    mlp_bwd_fused_kernel<64><<<S * BF_Q, 512, BwdLds<64>::bytes, s>>>(dact2, h1, X, W1, B, S, gw1, gw0, gb0,
-                                                                      slab_stride, tick);
-  else
-    mlp_bwd_fused_kernel<32><<<S * BF_Q, 512, BwdLds<32>::bytes, s>>>(dact2, h1, X, W1, B, S, gw1, gw0, gb0,
-                                                                      slab_stride, tick);
+  const dim3 grid(S * BF_Q);
+  if (h1) {
+    if (K0 == 64)
+      mlp_bwd_fused_kernel<64, false><<<grid, 512, BwdLds<64, false>::bytes, s>>>(dact2, h1, X, W1, B, S, gw1, gw0,
+                                                                                  gb0, slab_stride, tick, W0, b0);
+    else
+      mlp_bwd_fused_kernel<32, false><<<grid, 512, BwdLds<32, false>::bytes, s>>>(dact2, h1, X, W1, B, S, gw1, gw0,
+                                                                                  gb0, slab_stride, tick, W0, b0);
+  } else {
+    if (K0 == 64)
+      mlp_bwd_fused_kernel<64, true><<<grid, 512, BwdLds<64, true>::bytes, s>>>(dact2, h1, X, W1, B, S, gw1, gw0,
+                                                                                gb0, slab_stride, tick, W0, b0);
+    else
+      mlp_bwd_fused_kernel<32, true><<<grid, 512, BwdLds<32, true>::bytes, s>>>(dact2, h1, X, W1, B, S, gw1, gw0,
+                                                                                gb0, slab_stride, tick, W0, b0);
+  }
   HAR_CHECK_LAUNCH();
   return 0;
 }

@@ -296,10 +296,14 @@ def test_column_stats_and_binning(cuda):
 
 
 @pytest.mark.parametrize("H,F", [(256, 43), (256, 20), (128, 20)])
-def test_mlp_fused_fwd_head_matches_unfused(cuda, H, F):
+def test_mlp_fused_fwd_head_matches_unfused(cuda, monkeypatch, H, F):
     """mlp_fused.hip (fwd L1 + fwd L2 + head + dWout/dbout in one kernel) against the unfused
-    kernel chain: same h1 / dact2 / reduced gradients / loss up to bf16 summation-order noise."""
+    kernel chain: same h1 / dact2 / reduced gradients / loss up to bf16 summation-order noise
+    (h1 stored by the forward here so it can be compared; the default recomputes it in the backward)."""
+    from har.models import mlp as mlp_mod
     from har.models.mlp import MLPEngine, pad_input_bf16
+
+    monkeypatch.setattr(mlp_mod, "RECOMPUTE_H1", False)
 
     B = 4096
     layers = [F, H, H, 6]
@@ -335,6 +339,31 @@ def test_mlp_fused_fwd_head_matches_unfused(cuda, H, F):
     assert not a.last_fused
 
 
+@pytest.mark.parametrize("F,B", [(43, 4096), (20, 4160), (43, 65536)])
+def test_mlp_backward_h1_recompute_is_bit_identical(cuda, monkeypatch, F, B):
+    """The fused backward recomputing h1 = relu(W0 x + b0) from its X tiles (forward skips the h1
+    store) produces exactly the gradients and parameters of the stored-h1 path: the recompute uses
+    the forward's operands, accumulation order and rounding.  K0 = 64 and 32, a batch that is not a
+    multiple of the slice size, and the flagship batch."""
+    from har.models import mlp as mlp_mod
+    from har.models.mlp import MLPEngine, pad_input_bf16
+
+    g = torch.Generator(device=cuda).manual_seed(3)
+    X = pad_input_bf16(torch.randn(B, F, device=cuda, generator=g), MLPEngine([F, 256, 256, 6], B, cuda).layout.in_pad)
+    y = torch.randint(0, 6, (B,), device=cuda, generator=g).to(torch.int32)
+    out = {}
+    for rh in (False, True):
+        monkeypatch.setattr(mlp_mod, "RECOMPUTE_H1", rh)
+        e = MLPEngine([F, 256, 256, 6], B, cuda, lr=1e-3, seed=8)
+        for _ in range(3):
+            e.train_step(X, y, B)
+        torch.cuda.synchronize()
+        assert e.last_fused and e.last_bwd
+        out[rh] = (e.G.clone(), e.P.clone())
+    assert torch.equal(out[False][0], out[True][0])
+    assert torch.equal(out[False][1], out[True][1])
+
+
 @pytest.mark.parametrize("H,F", [(256, 43), (128, 20)])
 def test_mlp_fused_infer_matches_fp32(cuda, H, F):
     """Serving variant of the fused kernel (logits + argmax only) vs the fp32 PyTorch forward
@@ -363,8 +392,12 @@ def test_mlp_fused_infer_matches_fp32(cuda, H, F):
 def test_mlp_fused_v2_matches_v1(cuda, monkeypatch):
     """The 8-wave fused forward (W1 distributed over the waves' registers, H = 256) against the
     4-wave LDS-resident-W1 kernel on the same batch: same h1, dact2, gradient slabs and loss up
-    to bf16 / summation-order noise (HAR_MLP_FUSED_V1 selects the kernel per launch)."""
+    to bf16 / summation-order noise (HAR_MLP_FUSED_V1 selects the kernel per launch; h1 stored by
+    the forward so it can be compared)."""
+    from har.models import mlp as mlp_mod
     from har.models.mlp import MLPEngine, pad_input_bf16
+
+    monkeypatch.setattr(mlp_mod, "RECOMPUTE_H1", False)
 
     B, H, F = 8192, 256, 43
     g = torch.Generator(device=cuda).manual_seed(12)
