@@ -118,14 +118,10 @@ class ForestBuilder:
         if thresholds is None:
             # GPU: device findSplits (one sort, one small copy back; the same thresholds)
             thresholds = T.thresholds_for(X, self.max_bins, seed=self.seed)
-        self.thresholds = thresholds
-        F = X.shape[1]
-        self.nbins = torch.tensor([len(t) + 1 for t in self.thresholds], dtype=torch.int32, device=X.device)
-        thr_mat = np.full((F, self.max_bins), np.inf, dtype=np.float32)
-        for f, t in enumerate(self.thresholds):
-            thr_mat[f, : len(t)] = t
-        self.thr_mat = torch.from_numpy(thr_mat).to(X.device)
-        self.bins = bin_features(X, self.thresholds).to(X.device).contiguous()  # [F, N] uint8 (HIP on the GPU)
+        self.thresholds = tt = T.ThresholdTable.from_any(thresholds)  # one padded matrix, no per-feature loop
+        self.nbins = torch.from_numpy((tt.counts + 1).astype(np.int32)).to(X.device)
+        self.thr_mat = torch.from_numpy(tt.padded(self.max_bins)).to(X.device)
+        self.bins = bin_features(X, tt).to(X.device).contiguous()  # [F, N] uint8 (HIP on the GPU)
 
     def bootstrap_weights(self, N: int, device, row_offset: int = 0) -> torch.Tensor:
         """Host oracle of the device tree_init draws (same Philox keys, same CDF table)."""

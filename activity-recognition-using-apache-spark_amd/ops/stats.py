@@ -50,12 +50,10 @@ def bin_features(X: torch.Tensor, thresholds) -> torch.Tensor:
     if not X.is_cuda:
         return torch.from_numpy(T.bin_features(X.detach().float().cpu().numpy(), thresholds))
     F = X.shape[1]
-    maxb = max(1, max(len(t) for t in thresholds))
-    thr = np.full((F, maxb), np.inf, dtype=np.float32)
-    for f, t in enumerate(thresholds):
-        thr[f, : len(t)] = t
-    nthr = torch.tensor([len(t) for t in thresholds], dtype=torch.int32, device=X.device)
-    thr_t = torch.from_numpy(thr).to(X.device)
+    tt = T.ThresholdTable.from_any(thresholds)
+    maxb = max(1, int(tt.counts.max(initial=0)))
+    nthr = torch.from_numpy(tt.counts.astype(np.int32)).to(X.device)
+    thr_t = torch.from_numpy(tt.padded(maxb)).to(X.device)
     Xc = X.float().contiguous()
     out = torch.empty(F, Xc.shape[0], dtype=torch.uint8, device=X.device)
     _native.kernels().bin_features(Xc.data_ptr(), Xc.shape[0], F, Xc.stride(0), thr_t.data_ptr(), maxb,
