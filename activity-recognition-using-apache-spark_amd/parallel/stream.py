@@ -67,11 +67,13 @@ def exchange_halo(ctx: DistContext, local: torch.Tensor, halo: int, lens: Option
 
 
 def sharded_window_features(ctx: DistContext, local: torch.Tensor, featurizer: WindowFeaturizer,
-                            offset: Optional[int] = None, total: Optional[int] = None):
+                            offset: Optional[int] = None, total: Optional[int] = None, transform=None):
     """Featurize this rank's shard ``local`` [S_r, A] of a global stream.
 
     Returns ``(features [n_owned, F], first_window)`` where ``first_window`` is the
-    global index of the first owned window (labels / ids line up with it)."""
+    global index of the first owned window (labels / ids line up with it).  ``transform``
+    (segment -> rows) replaces ``featurizer.transform``, e.g. the window kernel's fused
+    MLP-input mode (``window_features_mlp``)."""
     W, st = featurizer.window, featurizer.stride
     lens = shard_lengths(ctx, local.shape[0], local.device)
     if offset is None or total is None:
@@ -85,4 +87,4 @@ def sharded_window_features(ctx: DistContext, local: torch.Tensor, featurizer: W
     if n == 0:
         return local.new_zeros(0, len(featurizer.names)), p0 // st
     seg = ext[p0 - offset: p0 - offset + (n - 1) * st + W]
-    return featurizer.transform(seg), p0 // st
+    return (transform or featurizer.transform)(seg), p0 // st

@@ -371,6 +371,8 @@ def bench_stream(args, ctx):
             feat.copy_(featurize(s))
             eng.train_step(pad_input_bf16(feat, eng.layout.in_pad), y32[j * B:(j + 1) * B], global_batch)
 
+    if args.stream_pass:
+        return _stream_full_pass(args, ctx, spec, stream, labels, eng, mean, inv_std, samples_local)
     elapsed = timed(ctx, step, args.steps, args.warmup, dev)
     st_, yt = generate_stream(8192, spec, dev, first_window=10 ** 9)
     Xt = featurize(st_)
@@ -384,6 +386,61 @@ def bench_stream(args, ctx):
                                 f"({F}-{args.hidden}-{args.hidden}-{N_CLASSES})",
                        "global_batch": global_batch, "seq_len": W, "parallelism": f"dp{world}"},
             "test_accuracy": hdist.mean_over_ranks(ctx, acc), "test_accuracy_data": "held-out synthetic stream"}
+
+
+def _stream_full_pass(args, ctx, spec, stream, labels, eng, mean, inv_std, samples_local):
+    """``--config stream --stream-pass``: one timed step = one FULL pass over every resident
+    sample (1B per 8 GPUs): the rank's shard is featurized with 50%-overlapping windows — windows
+    that straddle a shard cut take the right neighbour's first W-1 samples by one point-to-point
+    halo exchange (parallel/stream.py) — straight into standardized bf16 MLP rows (window kernel
+    MLP-input mode), then the MLP trains one epoch over them (every rank the same step count)."""
+    import torch.distributed as tdist
+
+    from har.features.window import WindowFeaturizer, n_features, window_features, window_features_mlp
+    from har.models.mlp import pad_input_bf16
+    from har.parallel.stream import shard_offsets, sharded_window_features
+
+    dev, world, B, W = ctx.device, ctx.world_size, args.batch, spec.window
+    fz = WindowFeaturizer(hz=spec.hz, seconds=W / spec.hz, overlap=0.5)
+    offset, total = shard_offsets(ctx, stream.shape[0], dev)
+    xin_rows = {}
+
+    def inputs(seg):
+        if eng.native:  # one kernel: featurize + NaN fill + standardize + bf16 + pad
+            return window_features_mlp(seg, fz.window, fz.stride, spec.hz, mean, inv_std, eng.layout.in_pad, -1.0)
+        X = torch.nan_to_num(window_features(seg, fz.window, fz.stride, spec.hz), nan=-1.0)
+        return pad_input_bf16((X - mean) * inv_std, eng.layout.in_pad)
+
+    X0, _ = sharded_window_features(ctx, stream, fz, offset, total, transform=inputs)  # untimed: the owned count
+    nbt = torch.tensor([X0.shape[0] // B], device=dev)
+    del X0
+    if world > 1:
+        tdist.all_reduce(nbt, op=tdist.ReduceOp.MIN, group=ctx.group)
+    nb = int(nbt.item())  # MLP steps per pass (the same on every rank)
+    gb = B * world
+
+    def one_pass(i):
+        X, first_w = sharded_window_features(ctx, stream, fz, offset, total, transform=inputs)
+        xin_rows["n"] = X.shape[0]
+        # window j starts at j * stride; its label is that of the generated segment it starts in
+        lab = labels[(torch.arange(first_w, first_w + nb * B, device=dev) * fz.stride) // W - offset // W]
+        y32 = lab.to(torch.int32)
+        for j in range(nb):
+            eng.train_step(X[j * B:(j + 1) * B], y32[j * B:(j + 1) * B], gb)
+
+    elapsed = timed(ctx, one_pass, args.steps, args.warmup, dev)
+    trained = nb * gb
+    return {"value": trained * args.steps / elapsed, "ms_per_step": elapsed * 1e3 / args.steps,
+            "vs_baseline": None, "vs_baseline_note": BASELINE_NOTE,
+            "samples_per_s": samples_local * world * args.steps / elapsed,
+            "windows_featurized_per_pass": xin_rows.get("n", 0) * world, "mlp_steps_per_pass": nb,
+            "data": f"synthetic 3-axis {spec.hz:g} Hz stream, {samples_local * world / 1e9:.2f}B samples resident "
+                    f"({samples_local / 1e6:.0f}M per GPU); one step = one full pass: sharded featurization with "
+                    f"{fz.window}-sample windows at stride {fz.stride} (halo exchange between ranks) + one MLP epoch",
+            "config": {"model": f"raw stream full pass -> window features -> MLP bf16 "
+                                f"({n_features(3)}-{args.hidden}-{args.hidden}-{N_CLASSES})",
+                       "global_batch": gb, "seq_len": fz.window, "parallelism": f"dp{world}"},
+            "test_accuracy": None, "test_accuracy_data": "not measured in --stream-pass mode"}
 
 
 def main():
@@ -408,6 +465,9 @@ def main():
     ap.add_argument("--rf-reduce", default="owner", choices=["owner", "allreduce"],
                     help="DP forest histograms: reduce-scatter by node owner + all-gather of splits, or all-reduce")
     ap.add_argument("--samples", type=int, default=1_000_000_000, help="stream samples per 8 GPUs")
+    ap.add_argument("--stream-pass", action="store_true",
+                    help="--config stream: time full passes over every resident sample (halo-sharded featurization "
+                         "+ one MLP epoch) instead of per-batch steps")
     ap.add_argument("--out", type=str, default="")
     args = ap.parse_args()
 

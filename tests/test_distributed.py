@@ -211,7 +211,8 @@ def test_tree_parallel_forest_equals_single(world):
     torch.testing.assert_close(outs[0], single.predict_raw(X))
 
 
-@pytest.mark.parametrize("config,extra", [("mlp", ["--batch", "512"]), ("rf", ["--rows", "3000", "--trees", "3"])])
+@pytest.mark.parametrize("config,extra", [("mlp", ["--batch", "512"]), ("rf", ["--rows", "3000", "--trees", "3"]),
+                                          ("stream", ["--stream-pass", "--samples", "8000000", "--batch", "512"])])
 def test_bench_contract_torchrun(config, extra):
     """The driver's N>1 launch (``torch.distributed.run ... bench.py --gpus N``) on 2 gloo ranks:
     exactly one JSON line (rank 0), whole-job aggregate value, dp2 config."""
@@ -230,5 +231,7 @@ def test_bench_contract_torchrun(config, extra):
     assert len(lines) == 1, r.stdout[-2000:]
     rec = json.loads(lines[0])
     assert rec["n_gpus"] == 2 and rec["config"]["parallelism"] == "dp2" and rec["value"] > 0
+    if config == "stream":  # full pass: both shards featurized (halo exchange across the cut), same step count
+        assert rec["windows_featurized_per_pass"] >= 9990 and rec["mlp_steps_per_pass"] >= 9
     if config == "mlp":  # value = whole-job windows per second = global batch / step time
         assert abs(rec["value"] - rec["config"]["global_batch"] / (rec["ms_per_step"] * 1e-3)) <= 1e-6 * rec["value"]
