@@ -242,10 +242,20 @@ class DeviceLogregSolver:
 
     def _args(self, init: int = 0, head: int = 0, filled: int = 0, fin: int = 0, fin_init: int = 0,
               fin_head: int = 0, fin_it: int = 0):
+        # the buffers never move during a solve: their pointers are read once (~40 data_ptr calls per
+        # launch were most of the host time of a 20-iteration fit), only the iteration scalars change
+        base = getattr(self, "_arg_base", None)
+        if base is None:
+            base = self._arg_base = self._pointer_args()
+        a = dict(base)
+        a.update(head=head, filled=filled, init=init, fin=fin, fin_init=fin_init, fin_head=fin_head, fin_it=fin_it)
+        return a
+
+    def _pointer_args(self):
         p = lambda t: 0 if t is None else t.data_ptr()  # noqa: E731
-        return {"B": self.B, "T": self.T, "K": self.d.K, "F": self.d.F, "m": self.m, "head": head,
-                "filled": filled, "init": init, "nch": self.nch, "fin": fin, "fin_init": fin_init,
-                "fin_head": fin_head, "fin_it": fin_it, "D": self.D, "x": p(self.x), "g": p(self.g),
+        return {"B": self.B, "T": self.T, "K": self.d.K, "F": self.d.F, "m": self.m, "head": 0,
+                "filled": 0, "init": 0, "nch": self.nch, "fin": 0, "fin_init": 0,
+                "fin_head": 0, "fin_it": 0, "D": self.D, "x": p(self.x), "g": p(self.g),
                 "fobj": p(self.fobj), "l1": p(self.l1v), "l2": p(self.l2v), "pmask": p(self.pmask),
                 "inv_std": p(self.inv_std), "S": p(self.S), "Y": p(self.Y), "rho": p(self.rho),
                 "SY": p(self.SY), "YY": p(self.YY), "P1": p(self.P1), "P2": p(self.P2), "P3": p(self.P3),
