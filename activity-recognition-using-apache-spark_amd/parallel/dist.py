@@ -63,8 +63,8 @@ def init(expected_world: Optional[int] = None, backend: Optional[str] = None, de
         kw = dict(backend=be, rank=rank, world_size=world, timeout=datetime.timedelta(seconds=timeout_s))
         if be == "nccl":
             kw["device_id"] = dev
-        restart = os.environ.get("TORCHELASTIC_RESTART_COUNT")
-        if restart is not None and not dist.is_initialized():
+        restart = int(os.environ.get("TORCHELASTIC_RESTART_COUNT", "0"))
+        if restart > 0 and not dist.is_initialized():
             # under torchrun --max-restarts the rendezvous store can outlive a failed attempt: key
             # this attempt's process group under its own prefix, or a restarted rank may read a dead
             # peer's (stale) transport address from the previous attempt and fail to connect
