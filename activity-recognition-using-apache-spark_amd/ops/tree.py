@@ -140,14 +140,18 @@ def find_thresholds_device(X: torch.Tensor, max_bins: int, sample_rows: int = 10
     ns = max_bins - 1
     if n == 0 or ns <= 0:
         return [np.zeros(0, dtype=np.float32) for _ in range(F)]
-    s = torch.sort(Xs.t().contiguous(), dim=1).values  # [F, n], NaN sorted last
     if X.is_cuda and n <= 16384 and ns <= 63:
-        # tree.hip find_splits_post_sort: distinct ranks, quantile cut points, dedup — one kernel
+        # tree.hip: one LDS bitonic sort per feature column (NaN last), then find_splits_post_sort:
+        # distinct ranks, quantile cut points, dedup — two kernels
+        Xc = Xs.contiguous()
+        s = torch.empty(F, n, dtype=torch.float32, device=X.device)
+        _native.kernels().sort_columns(Xc.data_ptr(), n, F, F, s.data_ptr(), _native.stream_ptr())
         out = torch.empty(F, ns + 1, dtype=torch.float32, device=X.device)
         _native.kernels().find_splits_post_sort(s.data_ptr(), F, n, ns, out.data_ptr(), _native.stream_ptr())
         h = out.cpu().numpy()  # the one device -> host copy
         cnt = h[:, ns].astype(np.int64)
         return ThresholdTable(np.where(np.arange(ns)[None, :] < cnt[:, None], h[:, :ns], np.float32(np.inf)), cnt)
+    s = torch.sort(Xs.t().contiguous(), dim=1).values  # [F, n], NaN sorted last
     nvalid = (~torch.isnan(s)).sum(1)  # [F]
     pos = torch.arange(n, device=X.device)
     valid = pos.view(1, n) < nvalid.view(F, 1)

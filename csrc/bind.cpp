@@ -315,6 +315,9 @@ PYBIND11_MODULE(_har_native, m) {
                         P<int32_t>(bad), S(stream)),
           "tree_init");
   });
+  m.def("sort_columns", [](u X, int n, int F, int ld, u out, u stream) {
+    check(har_sort_columns(P<const float>(X), n, F, ld, P<float>(out), S(stream)), "sort_columns");
+  });
   m.def("find_splits_post_sort", [](u sorted, int F, int n, int ns, u out, u stream) {
     check(har_find_splits_post_sort(P<const float>(sorted), F, n, ns, P<float>(out), S(stream)),
           "find_splits_post_sort");

@@ -116,6 +116,9 @@ int har_tree_init(uint64_t seed, int tree0, int ntrees, int64_t row0, int64_t n,
 // findSplits cut points from the per-feature sorted sample [F][n] (NaN last), n <= 16384, ns <= 63:
 // out [F][ns + 1] = thresholds then their count.
 int har_find_splits_post_sort(const float* sorted, int F, int n, int ns, float* out, hipStream_t s);
+// findSplits sample sort: columns of the row-major X [n][ld] (F of them) -> out [F][n] ascending, NaN
+// last (n <= 16384: one LDS bitonic sort per column).
+int har_sort_columns(const float* X, int n, int F, int ld, float* out, hipStream_t s);
 int har_poisson_bootstrap(uint64_t seed, int tree0, int ntrees, int64_t row0, int64_t n, uint8_t* out,
                           hipStream_t s);
 

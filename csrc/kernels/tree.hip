@@ -522,6 +522,39 @@ __global__ __launch_bounds__(256) void tree_init_kernel(uint64_t seed, int tree0
 // sorted position ceil(t) - 1 — are deduplicated and written in order.  out [F][ns + 1]: the
 // thresholds, then their count (as float): the ONE device -> host copy of findSplits.
 constexpr int FS_MAXN = 16384;
+
+// findSplits sample sort: column f of the row-major sample X [n][ld] -> ascending out[f][0..n) with
+// NaN last (torch.sort's order), one workgroup per feature: order-preserving uint32 keys (NaN ->
+// 0xFFFFFFFF, also the padding up to the power of two N2 <= FS_MAXN) bitonic-sorted in LDS.
+__device__ __forceinline__ uint32_t sort_key(float x) {
+  const uint32_t u = __float_as_uint(x);
+  return isnan(x) ? 0xFFFFFFFFu : ((u >> 31) ? ~u : (u | 0x80000000u));
+}
+__device__ __forceinline__ float sort_val(uint32_t k) {
+  return k == 0xFFFFFFFFu ? __uint_as_float(0x7FC00000u) : __uint_as_float((k >> 31) ? (k & 0x7FFFFFFFu) : ~k);
+}
+__global__ __launch_bounds__(1024) void sort_columns_kernel(const float* __restrict__ X, int n, int ld, int N2,
+                                                            float* __restrict__ out) {
+  extern __shared__ uint32_t skey[];
+  const int f = blockIdx.x, tid = threadIdx.x;
+  for (int i = tid; i < N2; i += 1024) skey[i] = i < n ? sort_key(X[(size_t)i * ld + f]) : 0xFFFFFFFFu;
+  __syncthreads();
+  for (int k = 2; k <= N2; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int i = tid; i < (N2 >> 1); i += 1024) {
+        const int a = ((i & ~(j - 1)) << 1) | (i & (j - 1)), b = a + j;
+        const uint32_t ka = skey[a], kb = skey[b];
+        if ((ka > kb) == ((a & k) == 0)) {
+          skey[a] = kb;
+          skey[b] = ka;
+        }
+      }
+      __syncthreads();
+    }
+  }
+  float* o = out + (size_t)f * n;
+  for (int i = tid; i < n; i += 1024) o[i] = sort_val(skey[i]);
+}
 __global__ __launch_bounds__(256) void find_splits_post_sort_kernel(const float* __restrict__ sorted, int n, int ns,
                                                                     float* __restrict__ out) {
   extern __shared__ __attribute__((aligned(16))) int fs_smem[];
@@ -746,6 +779,16 @@ extern "C" int har_tree_init(uint64_t seed, int tree0, int ntrees, int64_t row0,
   dim3 grid((unsigned)((n + INIT_ROWS - 1) / INIT_ROWS), (unsigned)ntrees);
   tree_init_kernel<<<grid, 256, 0, s>>>(seed, tree0, row0, n, tab, rw, y, K, W, node_of, stats, stats_tree_stride,
                                         bad);
+  HAR_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int har_sort_columns(const float* X, int n, int F, int ld, float* out, hipStream_t s) {
+  if (n <= 0 || n > FS_MAXN || F < 0 || ld < F) return -2;
+  if (F == 0) return 0;
+  int N2 = 2;
+  while (N2 < n) N2 <<= 1;
+  sort_columns_kernel<<<F, 1024, (size_t)N2 * sizeof(uint32_t), s>>>(X, n, ld, N2, out);
   HAR_CHECK_LAUNCH();
   return 0;
 }

@@ -466,3 +466,24 @@ def test_find_thresholds_device_matches_numpy():
         b = T.find_thresholds_device(X.cuda(), 32, seed=5, row_offset=row0, n_total=n_total)
         for f in range(X.shape[1]):
             assert np.array_equal(a[f], b[f]), f
+
+
+@pytest.mark.parametrize("n,F", [(10000, 43), (3853, 300), (1, 3), (16384, 5), (777, 1)])
+def test_sort_columns_matches_torch_sort(cuda, n, F):
+    """findSplits' per-feature LDS bitonic sort (tree.hip sort_columns) against torch.sort of the
+    transposed sample: same ascending values, NaN last; ties, +-0 and constant columns included."""
+    from har.ops import _native
+
+    g = torch.Generator(device=cuda).manual_seed(n + F)
+    X = torch.randn(n, F, device=cuda, generator=g)
+    X[torch.rand(n, F, device=cuda, generator=g) < 0.1] = float("nan")
+    X[:, 0] = torch.round(X[:, 0] * 2) / 2  # heavy ties
+    if F > 1:
+        X[:, 1] = 3.0  # constant column
+    if F > 2:
+        X[: n // 2, 2] = -0.0
+    out = torch.empty(F, n, device=cuda)
+    _native.kernels().sort_columns(X.data_ptr(), n, F, F, out.data_ptr(), _native.stream_ptr())
+    ref = torch.sort(X.t().contiguous(), dim=1).values
+    assert torch.equal(torch.isnan(out), torch.isnan(ref))
+    assert torch.equal(torch.nan_to_num(out, nan=0.0), torch.nan_to_num(ref, nan=0.0))
