@@ -697,6 +697,17 @@ class DecisionTreeClassifier(_TreeEstimatorBase):
                                                 device=X.device) for f in range(masks.shape[0])]
 
 
+
+# (tree, row) slots of one lock-step forest build: row lists, counts and scans in tree_level.hip
+# are int32, so one build never holds more slots than this (bigger forests grow in tree waves)
+LOCKSTEP_SLOT_LIMIT = 2 ** 31 - 1
+
+
+def max_lockstep_trees(n_rows: int) -> int:
+    """Most trees one lock-step build may grow over ``n_rows`` rows (>= 1)."""
+    return max(1, LOCKSTEP_SLOT_LIMIT // max(1, n_rows))
+
+
 class RandomForestClassifier(_TreeEstimatorBase):
     _param_names = _TreeEstimatorBase._param_names + ("numTrees", "featureSubsetStrategy", "subsamplingRate")
 
@@ -734,8 +745,8 @@ class RandomForestClassifier(_TreeEstimatorBase):
         total = self.numTrees if num_trees is None else int(num_trees)
         wave = tree_wave if tree_wave and tree_wave < total else total
         # (tree, row) slots of one lock-step build are int32-indexed on the device
-        # (tree_level.hip row lists / scans): cap a wave at 2^31 - 1 slots
-        max_wave = max(1, (2 ** 31 - 1) // max(1, X.shape[0]))
+        # (tree_level.hip row lists / scans): cap a wave at LOCKSTEP_SLOT_LIMIT slots
+        max_wave = max_lockstep_trees(int(X.shape[0]))
         if wave > max_wave:
             wave = max_wave
         ckpt = None

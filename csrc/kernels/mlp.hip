@@ -189,6 +189,17 @@ __global__ __launch_bounds__(1024) void grad_reduce_adam_kernel(GradRegions rg, 
   __shared__ float4 part[GR_W][64];
   const int q = threadIdx.x >> 6, k = threadIdx.x & 63;
   const int64_t i4 = (int64_t)blockIdx.x * 64 + k, e = i4 * 4;
+  // the Adam operands do not depend on the reduction: wave 0 issues their loads first, so their
+  // latency overlaps the slab loads instead of following them
+  const bool do_adam = q == 0 && e < n && (mode & GR_ADAM);
+  float4 pp = make_float4(0.f, 0.f, 0.f, 0.f), mm = pp, vv = pp;
+  int32_t t_int = 0;
+  if (do_adam) {
+    pp = reinterpret_cast<const float4*>(param)[i4];
+    mm = reinterpret_cast<const float4*>(m)[i4];
+    vv = reinterpret_cast<const float4*>(v)[i4];
+    t_int = *step;
+  }
   if (mode & GR_REDUCE) {
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
     if (e < n) {
@@ -231,7 +242,6 @@ __global__ __launch_bounds__(1024) void grad_reduce_adam_kernel(GradRegions rg, 
     }
     __syncthreads();
   }
-  const int32_t t_int = (mode & GR_ADAM) ? *step : 0;
   if (q == 0 && e < n) {
     float4 g;
     if (mode & GR_REDUCE) {
@@ -242,12 +252,9 @@ __global__ __launch_bounds__(1024) void grad_reduce_adam_kernel(GradRegions rg, 
       g = reinterpret_cast<const float4*>(G)[i4];
     }
     if (mode & GR_STORE) reinterpret_cast<float4*>(G)[i4] = g;
-    if (mode & GR_ADAM) {
+    if (do_adam) {
       const float t = (float)t_int;
       const float bc1 = 1.f - powf(b1, t), bc2 = 1.f - powf(b2, t);
-      float4 pp = reinterpret_cast<float4*>(param)[i4];
-      float4 mm = reinterpret_cast<float4*>(m)[i4];
-      float4 vv = reinterpret_cast<float4*>(v)[i4];
       float* pa = &pp.x; float* ma = &mm.x; float* va = &vv.x; const float* ga = &g.x;
       ushort4 ob;
       unsigned short* oa = &ob.x;

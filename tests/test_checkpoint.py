@@ -106,6 +106,34 @@ def test_rf_waves_equal_one_shot():
     assert torch.equal(one.arrs.feature, wav.arrs.feature)
 
 
+def test_rf_int32_slot_cap_waves_automatically(monkeypatch):
+    """(tree, row) slots are int32 on the device: a forest whose lock-step build would exceed
+    the slot limit grows in waves by itself, equal to the one-shot forest."""
+    import har.models.tree as tree_mod
+
+    assert tree_mod.max_lockstep_trees(4_300_000) == (2 ** 31 - 1) // 4_300_000
+    assert tree_mod.max_lockstep_trees(2 ** 32) == 1
+    g = torch.Generator().manual_seed(3)
+    mu = torch.randn(3, 8, generator=g) * 2
+    y = torch.randint(0, 3, (600,), generator=g)
+    X = mu[y] + torch.randn(600, 8, generator=g)
+    one = RandomForestClassifier(numTrees=7, maxDepth=4, seed=5, device="cpu").fit_tensors(X, y, 3)
+    built = []
+    real = tree_mod.ForestBuilder
+
+    class Spy(real):
+        def __init__(self, K, nt, *a, **kw):
+            built.append(nt)
+            super().__init__(K, nt, *a, **kw)
+
+    monkeypatch.setattr(tree_mod, "LOCKSTEP_SLOT_LIMIT", 600 * 3)
+    monkeypatch.setattr(tree_mod, "ForestBuilder", Spy)
+    capped = RandomForestClassifier(numTrees=7, maxDepth=4, seed=5, device="cpu").fit_tensors(X, y, 3)
+    assert built == [3, 3, 1]
+    assert torch.equal(one.arrs.feature, capped.arrs.feature)
+    assert torch.equal(one.predict_all(X)[0], capped.predict_all(X)[0])
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("kind,fault", [("mlp", 10), ("rf", 8)])
 def test_fault_then_resume_gpu(tmp_path, kind, fault):
