@@ -169,6 +169,7 @@ __global__ __launch_bounds__(256) void csv_parse_rows(const uint8_t* __restrict_
 }  // namespace
 
 extern "C" int har_csv_count_newlines(const uint8_t* buf, int64_t n, int32_t* counts, hipStream_t s) {
+  if (n < 0) return -2;
   const int64_t blocks = (n + CHUNK - 1) / CHUNK;
   if (blocks == 0) return 0;
   csv_count_newlines<<<(unsigned)blocks, 256, 0, s>>>(buf, n, counts);

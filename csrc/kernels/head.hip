@@ -240,7 +240,7 @@ extern "C" int har_reduce_slabs_multi(int nseg, const float* const* slabs, const
   return 0;
 }
 
-extern "C" int har_head_fused_blocks(int B) { return (B + ROWS - 1) / ROWS; }
+extern "C" int har_head_fused_blocks(int B) { return (int)(((int64_t)B + ROWS - 1) / ROWS); }
 
 extern "C" int har_head_fused(const uint16_t* H, const uint16_t* W, const float* bias, const int32_t* labels, int B,
                               int D, int C, float scale, uint16_t* dlogits, uint16_t* dH, float* block_loss,

@@ -66,7 +66,7 @@ __global__ __launch_bounds__(256) void moments_kernel(const float* __restrict__ 
 
 extern "C" int har_confusion_matrix(const int32_t* label, const int32_t* pred, int64_t n, int K, int64_t* cm,
                                     hipStream_t s) {
-  if (K * K > MAXK2) return -2;
+  if (K <= 0 || (int64_t)K * K > MAXK2 || n < 0) return -2;
   if (n == 0) return 0;
   int blocks = (int)std::min<int64_t>(1024, (n + 255) / 256);
   confusion_kernel<<<blocks, 256, 0, s>>>(label, pred, n, K, reinterpret_cast<unsigned long long*>(cm));
@@ -75,6 +75,7 @@ extern "C" int har_confusion_matrix(const int32_t* label, const int32_t* pred, i
 }
 
 extern "C" int har_regression_moments(const float* y, const float* yhat, int64_t n, double* out6, hipStream_t s) {
+  if (n < 0) return -2;
   if (n == 0) return 0;
   int blocks = (int)std::min<int64_t>(1024, (n + 255) / 256);
   moments_kernel<<<blocks, 256, 0, s>>>(y, yhat, n, out6);
@@ -83,8 +84,8 @@ extern "C" int har_regression_moments(const float* y, const float* yhat, int64_t
 }
 
 extern "C" int har_value_counts(const int64_t* codes, int64_t n, int V, int64_t* out, hipStream_t s) {
-  if (V <= 0 || V > 32768) return -2;  // LDS counters: <= 128 KB
-  hipMemsetAsync(out, 0, sizeof(int64_t) * (size_t)V, s);
+  if (V <= 0 || V > 32768 || n < 0) return -2;  // LDS counters: <= 128 KB
+  if (const hipError_t e = hipMemsetAsync(out, 0, sizeof(int64_t) * (size_t)V, s); e != hipSuccess) return (int)e;
   if (n == 0) return 0;
   const int blocks = (int)std::min<int64_t>(256, (n + 255) / 256);
   value_counts_kernel<<<blocks, 256, sizeof(unsigned int) * (size_t)V, s>>>(codes, n, V,

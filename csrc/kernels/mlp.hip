@@ -278,7 +278,9 @@ int grid_for(int64_t n4) { return (int)std::max<int64_t>(1, std::min<int64_t>(20
 
 }  // namespace
 
-extern "C" int har_softmax_ce_head_blocks(int B) { return (B + HEAD_ROWS_PER_BLOCK - 1) / HEAD_ROWS_PER_BLOCK; }
+extern "C" int har_softmax_ce_head_blocks(int B) {
+  return (int)(((int64_t)B + HEAD_ROWS_PER_BLOCK - 1) / HEAD_ROWS_PER_BLOCK);
+}
 
 extern "C" int har_softmax_ce_head(const uint16_t* H, const uint16_t* W, const float* bias, const int32_t* labels,
                                    int B, int D, int C, float scale, uint16_t* dlogits, float* block_loss,

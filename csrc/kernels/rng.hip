@@ -21,6 +21,7 @@ __global__ __launch_bounds__(256) void philox_buckets_kernel(uint64_t seed, uint
 
 extern "C" int har_philox_buckets(uint64_t seed, uint32_t stream, int64_t row0, int64_t n, const uint32_t* thr,
                                   int nthr, int32_t* out, hipStream_t s) {
+  if (n < 0 || nthr < 0) return -2;
   if (n == 0) return 0;
   int blocks = (int)std::min<int64_t>(4096, (n + 255) / 256);
   philox_buckets_kernel<<<blocks, 256, 0, s>>>(seed, stream, row0, n, thr, nthr, out);

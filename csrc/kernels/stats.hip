@@ -111,6 +111,7 @@ __global__ __launch_bounds__(256) void bin_features_kernel(const float* __restri
 
 extern "C" int har_column_stats(const float* X, int64_t n, int ncols, int ld, const float* w, double* stats,
                                 double* workspace, hipStream_t s) {
+  if (n < 0 || ncols < 0 || ld < ncols) return -2;
   if (n == 0 || ncols == 0) return 0;
   const int nb = (int)((n + ROWS_PER_BLOCK - 1) / ROWS_PER_BLOCK);
   dim3 grid((ncols + 255) / 256, nb);
@@ -123,6 +124,7 @@ extern "C" int har_column_stats(const float* X, int64_t n, int ncols, int ld, co
 // fp64 input, column-major [ncols][n] (one device-CSV value plane per column); center as above
 extern "C" int har_column_stats_f64(const double* X, int64_t n, int ncols, const double* center, double* stats,
                                     double* workspace, hipStream_t s) {
+  if (n < 0 || ncols < 0) return -2;
   if (n == 0 || ncols == 0) return 0;
   const int nb = (int)((n + ROWS_PER_BLOCK - 1) / ROWS_PER_BLOCK);
   // column-major planes: one workgroup column per input column, lanes walk rows
@@ -139,8 +141,8 @@ extern "C" int64_t har_column_stats_workspace(int64_t n, int ncols) {
 
 extern "C" int har_bin_features(const float* X, int64_t n, int F, int ld, const float* thr, int maxb,
                                 const int32_t* nthr, uint8_t* bins, hipStream_t s) {
+  if (n < 0 || F < 0 || F > 65535 || ld < F) return -2;
   if (n == 0 || F == 0) return 0;
-  if (F > 65535) return -2;
   dim3 grid((unsigned)std::min<int64_t>(1024, (n + 255) / 256), F);
   bin_features_kernel<<<grid, 256, 0, s>>>(X, n, F, ld, thr, maxb, nthr, bins);
   HAR_CHECK_LAUNCH();

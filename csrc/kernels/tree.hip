@@ -760,6 +760,7 @@ extern "C" int har_forest_predict(const float* X, int64_t n, int F, int ld, cons
 
 extern "C" int har_poisson_bootstrap(uint64_t seed, int tree0, int ntrees, int64_t row0, int64_t n, uint8_t* out,
                                      hipStream_t s) {
+  if (ntrees < 0 || n < 0) return -2;
   int64_t total = (int64_t)ntrees * n;
   if (total == 0) return 0;
   int blocks = (int)std::min<int64_t>(4096, (total + 255) / 256);

@@ -552,7 +552,8 @@ int launch_axes(const float* stream, int64_t n_samples, int window, int stride, 
 
 extern "C" int har_window_features(const float* stream, int64_t n_samples, int axes, int window, int stride,
                                    int64_t n_windows, float hz, int nbins, float* out, int ld_out, hipStream_t s) {
-  if (axes > MAXA || axes % 3 || nbins != NB || window < 3 || window >= 65536 || stride <= 0) return -2;
+  if (axes > MAXA || axes % 3 || nbins != NB || window < 3 || window >= 65536 || stride <= 0 || n_windows < 0)
+    return -2;
   if ((n_windows - 1) * (int64_t)stride + window > n_samples) return -3;  // every window must be in bounds
   if (ld_out < 17 * axes + 4 * (axes / 3)) return -4;
   if (n_windows == 0) return 0;
@@ -568,7 +569,7 @@ extern "C" int har_window_features(const float* stream, int64_t n_samples, int a
 extern "C" int har_window_features_mlp(const float* stream, int64_t n_samples, int axes, int window, int stride,
                                        int64_t n_windows, float hz, const float* mean, const float* inv_std,
                                        float nan_value, uint16_t* out, int ld_out, hipStream_t s) {
-  if (axes > MAXA || axes % 3 || window < 3 || window >= 65536 || stride <= 0) return -2;
+  if (axes > MAXA || axes % 3 || window < 3 || window >= 65536 || stride <= 0 || n_windows < 0) return -2;
   if ((n_windows - 1) * (int64_t)stride + window > n_samples) return -3;
   if (ld_out < 17 * axes + 4 * (axes / 3) || !mean || !inv_std || !out) return -4;
   if (n_windows == 0) return 0;
