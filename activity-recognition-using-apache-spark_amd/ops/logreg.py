@@ -230,7 +230,7 @@ class DeviceLogregSolver:
         self.iters = torch.zeros(B, **i32)
         self.steep = torch.zeros(B, **i32)
         self.pick = torch.zeros(B, **i32)
-        self.nch = _native.kernels().qn_chunks(D)
+        self.nch = _native.kernels().qn_chunks(D, B)
         self.P1 = torch.zeros(B, self.nch, 2 * 10 + 1, **f64)   # chunk partials (QN_MAX_M = 10)
         self.P2 = torch.zeros(B, self.nch, 3 * 4 + 2, **f64)    # (QN_MAX_TRIALS = 4)
         self.P3 = torch.zeros(B, self.nch, 5 + 3 * 10, **f64)
@@ -264,18 +264,31 @@ class DeviceLogregSolver:
                 "fails": p(self.fails), "iters": p(self.iters), "steep": p(self.steep), "pick": p(self.pick),
                 "hist": p(self.hist), "c1": float(self.c1), "tol": float(self.tol)}
 
+    def _eval_args(self, tstride: int):
+        """Positional arguments (but the stream) of the evaluate + gradient launches, built once per
+        tstride: the buffers never move during a solve."""
+        cache = self.__dict__.setdefault("_eval_arg_cache", {})
+        if tstride not in cache:
+            d = self.d
+            n_models = (self.B * self.T) // tstride
+            R = 0 if self.R is None else self.R.data_ptr()
+            ev = (d.dense.data_ptr(), d.dense.stride(0), d.Fd, d.dense_cols.data_ptr(), d.cat.data_ptr(), d.C,
+                  d.y32.data_ptr(), d.rw.data_ptr(), self.inv_wsum.data_ptr(), self.weff.data_ptr(), d.N, d.F,
+                  d.K, self.T, tstride, 0, R, self.slab.data_ptr(), d.KP, n_models)
+            slice_lo, col_slice, blk_col, blk_slice, nb = d.grad_partition()
+            gr = (self.slab.data_ptr(), R, d.col_map.data_ptr(), d.csc_rows.data_ptr(), slice_lo.data_ptr(),
+                  col_slice.data_ptr(), blk_col.data_ptr(), blk_slice.data_ptr(), nb, self.inv_std.data_ptr(),
+                  self.pmask.data_ptr(), d.N, d.F, d.Fd, d.K, self.T, tstride, self.ntiles, self.G.data_ptr(),
+                  self.loss.data_ptr(), d.KP, n_models)
+            cache[tstride] = (ev, gr)
+        return cache[tstride]
+
     def _evaluate(self, tstride: int):
-        d, mod, s = self.d, _native.kernels(), _native.stream_ptr()
-        n_models = (self.B * self.T) // tstride
-        mod.logreg_eval(d.dense.data_ptr(), d.dense.stride(0), d.Fd, d.dense_cols.data_ptr(), d.cat.data_ptr(), d.C,
-                        d.y32.data_ptr(), d.rw.data_ptr(), self.inv_wsum.data_ptr(), self.weff.data_ptr(), d.N, d.F,
-                        d.K, self.T, tstride, 0, 0 if self.R is None else self.R.data_ptr(), self.slab.data_ptr(),
-                        d.KP, n_models, s)
-        slice_lo, col_slice, blk_col, blk_slice, nb = d.grad_partition()
-        mod.logreg_grad(self.slab.data_ptr(), 0 if self.R is None else self.R.data_ptr(), d.col_map.data_ptr(),
-                        d.csc_rows.data_ptr(), slice_lo.data_ptr(), col_slice.data_ptr(), blk_col.data_ptr(),
-                        blk_slice.data_ptr(), nb, self.inv_std.data_ptr(), self.pmask.data_ptr(), d.N, d.F, d.Fd,
-                        d.K, self.T, tstride, self.ntiles, self.G.data_ptr(), self.loss.data_ptr(), d.KP, n_models, s)
+        mod = _native.kernels()
+        ev, gr = self._eval_args(tstride)
+        s = _native.stream_ptr()
+        mod.logreg_eval(*ev, s)
+        mod.logreg_grad(*gr, s)
         if self.allreduce is not None:  # data parallel: the flat fp32 gradient bucket + the fp64 losses
             self.allreduce(self.G)
             self.allreduce(self.loss)
@@ -286,28 +299,33 @@ class DeviceLogregSolver:
         + T trial points), evaluate + gradient of the B*T trials, phase 2 (pick + history).  The
         host polls ``active`` (one sync) every ``poll`` iterations only."""
         mod, s, KP = _native.kernels(), _native.stream_ptr(), self.d.KP
+        qa = getattr(self, "_qn_args", None)
+        if qa is None:  # pointers / shapes converted once; a launch passes only the iteration scalars
+            qa = self._qn_args = mod.qn_args(self._args())
+
+        def phase(ph, head=0, filled=0, init=0, fin=0, fin_init=0, fin_head=0, fin_it=0):
+            mod.lbfgs_phase_h(qa, ph, head, filled, init, fin, fin_init, fin_head, fin_it, KP, s)
+
         self.x.copy_(x0.reshape(self.B, self.D))
-        mod.lbfgs_phase(1, self._args(init=1), KP, s)
+        phase(1, init=1)
         self._evaluate(self.T)
-        mod.lbfgs_phase(2, self._args(init=1), KP, s)
+        phase(2, init=1)
         head = filled = 0
         prev = -1  # history slot written by the previous phase 2 (-1: the init update)
         finalized = False
         for it in range(self.max_iter):
-            mod.lbfgs_phase(0, self._args(head=head, filled=filled, fin=1, fin_init=int(prev < 0),
-                                          fin_head=max(prev, 0), fin_it=it), KP, s)
+            phase(0, head, filled, fin=1, fin_init=int(prev < 0), fin_head=max(prev, 0), fin_it=it)
             if poll and it and it % poll == 0 and not bool(self.active.any()):
                 finalized = True
                 break
-            mod.lbfgs_phase(1, self._args(head=head, filled=filled), KP, s)
+            phase(1, head, filled)
             self._evaluate(1)
-            mod.lbfgs_phase(2, self._args(head=head, filled=filled), KP, s)
+            phase(2, head, filled)
             prev = head
             head = (head + 1) % self.m
             filled = min(filled + 1, self.m)
         if not finalized:
-            mod.lbfgs_phase(3, self._args(fin=1, fin_init=int(prev < 0), fin_head=max(prev, 0),
-                                          fin_it=self.max_iter), KP, s)
+            phase(3, fin=1, fin_init=int(prev < 0), fin_head=max(prev, 0), fin_it=self.max_iter)
         return self.x, self.fobj, self.iters
 
     def margins(self, W_models: torch.Tensor, hm, n_models: int) -> torch.Tensor:

@@ -99,6 +99,65 @@ static GemmParams make_gemm(u A, u B, u C, u bias, u mask, u rowsum, int M, int 
 #define HAR_SOURCE_HASH "unknown"
 #endif
 
+static QnArgs qn_args_from_dict(py::dict d) {
+  auto I = [&](const char* k) { return d[k].cast<int64_t>(); };
+  auto U = [&](const char* k) { return d[k].cast<u>(); };
+  QnArgs a;
+  a.B = (int)I("B");
+  a.T = (int)I("T");
+  a.K = (int)I("K");
+  a.F = (int)I("F");
+  a.m = (int)I("m");
+  a.head = (int)I("head");
+  a.filled = (int)I("filled");
+  a.init = (int)I("init");
+  a.nch = (int)I("nch");
+  a.fin = (int)I("fin");
+  a.fin_only = 0;
+  a.fin_init = (int)I("fin_init");
+  a.fin_head = (int)I("fin_head");
+  a.fin_it = (int)I("fin_it");
+  a.D = I("D");
+  a.x = P<float>(U("x"));
+  a.g = P<float>(U("g"));
+  a.fobj = P<double>(U("fobj"));
+  a.l1 = P<const float>(U("l1"));
+  a.l2 = P<const float>(U("l2"));
+  a.pmask = P<const float>(U("pmask"));
+  a.inv_std = P<const float>(U("inv_std"));
+  a.S = P<float>(U("S"));
+  a.Y = P<float>(U("Y"));
+  a.rho = P<double>(U("rho"));
+  a.SY = P<double>(U("SY"));
+  a.YY = P<double>(U("YY"));
+  a.P1 = P<double>(U("P1"));
+  a.P2 = P<double>(U("P2"));
+  a.P3 = P<double>(U("P3"));
+  a.xtrial = P<float>(U("xtrial"));
+  a.weff = P<float>(U("weff"));
+  a.reg = P<double>(U("reg"));
+  a.decr = P<double>(U("decr"));
+  a.G = P<const float>(U("G"));
+  a.loss = P<const double>(U("loss"));
+  a.step_scale = P<float>(U("step_scale"));
+  a.active = P<int32_t>(U("active"));
+  a.fails = P<int32_t>(U("fails"));
+  a.iters = P<int32_t>(U("iters"));
+  a.steep = P<int32_t>(U("steep"));
+  a.pick = P<int32_t>(U("pick"));
+  a.hist = P<double>(U("hist"));
+  a.c1 = d["c1"].cast<double>();
+  a.tol = d["tol"].cast<double>();
+  return a;
+}
+
+// The pointer / shape fields of a solve's L-BFGS arguments, converted from the Python dict ONCE per
+// solve; each phase launch then passes only the iteration scalars (a dict conversion per launch cost
+// ~20 us of host time, three launches per iteration).
+struct QnArgsHolder {
+  QnArgs a;
+};
+
 PYBIND11_MODULE(_har_native, m) {
   m.doc() = "har native runtime: host CSV parser + gfx950 HIP kernel launchers";
   // content hash of every source / header / flag the library was built from (tools/build_native.py);
@@ -198,54 +257,22 @@ PYBIND11_MODULE(_har_native, m) {
   // 3 finalize only); the QnArgs fields come from a dict of ints / floats / device pointers
   m.def("qn_chunks", &har_qn_chunks);
   m.def("lbfgs_phase", [](int phase, py::dict d, int KP, u stream) {
-    auto I = [&](const char* k) { return d[k].cast<int64_t>(); };
-    auto U = [&](const char* k) { return d[k].cast<u>(); };
-    QnArgs a;
-    a.B = (int)I("B");
-    a.T = (int)I("T");
-    a.K = (int)I("K");
-    a.F = (int)I("F");
-    a.m = (int)I("m");
-    a.head = (int)I("head");
-    a.filled = (int)I("filled");
-    a.init = (int)I("init");
-    a.nch = (int)I("nch");
-    a.fin = (int)I("fin");
+    QnArgs a = qn_args_from_dict(d);
+    check(har_lbfgs_phase(&a, KP, phase, S(stream)), "lbfgs_phase");
+  });
+  py::class_<QnArgsHolder>(m, "QnArgs");
+  m.def("qn_args", [](py::dict d) { return QnArgsHolder{qn_args_from_dict(d)}; });
+  m.def("lbfgs_phase_h", [](const QnArgsHolder& h, int phase, int head, int filled, int init, int fin, int fin_init,
+                            int fin_head, int fin_it, int KP, u stream) {
+    QnArgs a = h.a;
+    a.head = head;
+    a.filled = filled;
+    a.init = init;
+    a.fin = fin;
     a.fin_only = 0;
-    a.fin_init = (int)I("fin_init");
-    a.fin_head = (int)I("fin_head");
-    a.fin_it = (int)I("fin_it");
-    a.D = I("D");
-    a.x = P<float>(U("x"));
-    a.g = P<float>(U("g"));
-    a.fobj = P<double>(U("fobj"));
-    a.l1 = P<const float>(U("l1"));
-    a.l2 = P<const float>(U("l2"));
-    a.pmask = P<const float>(U("pmask"));
-    a.inv_std = P<const float>(U("inv_std"));
-    a.S = P<float>(U("S"));
-    a.Y = P<float>(U("Y"));
-    a.rho = P<double>(U("rho"));
-    a.SY = P<double>(U("SY"));
-    a.YY = P<double>(U("YY"));
-    a.P1 = P<double>(U("P1"));
-    a.P2 = P<double>(U("P2"));
-    a.P3 = P<double>(U("P3"));
-    a.xtrial = P<float>(U("xtrial"));
-    a.weff = P<float>(U("weff"));
-    a.reg = P<double>(U("reg"));
-    a.decr = P<double>(U("decr"));
-    a.G = P<const float>(U("G"));
-    a.loss = P<const double>(U("loss"));
-    a.step_scale = P<float>(U("step_scale"));
-    a.active = P<int32_t>(U("active"));
-    a.fails = P<int32_t>(U("fails"));
-    a.iters = P<int32_t>(U("iters"));
-    a.steep = P<int32_t>(U("steep"));
-    a.pick = P<int32_t>(U("pick"));
-    a.hist = P<double>(U("hist"));
-    a.c1 = d["c1"].cast<double>();
-    a.tol = d["tol"].cast<double>();
+    a.fin_init = fin_init;
+    a.fin_head = fin_head;
+    a.fin_it = fin_it;
     check(har_lbfgs_phase(&a, KP, phase, S(stream)), "lbfgs_phase");
   });
 

@@ -219,7 +219,7 @@ typedef struct QnArgs {
 int har_logreg_eval(const LogregEvalArgs* a, int KP, int n_models, hipStream_t s);
 int har_logreg_eval_tiles(int64_t n);
 int har_logreg_grad(const LogregGradArgs* a, int KP, int n_models, hipStream_t s);
-int har_qn_chunks(int64_t D);
+int har_qn_chunks(int64_t D, int B);
 int har_lbfgs_phase(const QnArgs* a, int KP, int phase, hipStream_t s);
 
 int har_logreg_softmax_grad(const float* Z, int64_t n, int nmodels, int K, int ld, const int32_t* y,

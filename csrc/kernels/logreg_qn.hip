@@ -227,7 +227,7 @@ __global__ __launch_bounds__(256) void logreg_grad_kernel(LogregGradArgs a) {
 // ---------------------------------------------------------------------------------------------
 // Batched L-BFGS / OWL-QN, chunked over the whole chip.
 //
-// Every model's parameter vector (D = K (F+1) = 18,606 for WISDM) is cut into QN_CHUNK-element
+// Every model's parameter vector (D = K (F+1) = 18,606 for WISDM) is cut into har_qn_chunks(D, B)
 // chunks and each phase runs one 256-thread workgroup per (chunk, model), so a single fit
 // streams its history (m = 10 pairs of D floats) with tens of CUs instead of one.  Cross-chunk
 // sums go through per-chunk fp64 partial slabs reduced in chunk order by the consumer (fixed
@@ -250,7 +250,6 @@ __global__ __launch_bounds__(256) void logreg_grad_kernel(LogregGradArgs a) {
 //   phase 3  (B)           finalize only (after the last iteration)
 // ---------------------------------------------------------------------------------------------
 constexpr int QN_BLOCK = 256;
-constexpr int QN_CHUNK = 2048;
 constexpr int QN_MAX_TRIALS = 4;
 constexpr int QN_MAX_M = 10;
 constexpr int NP1 = 2 * QN_MAX_M + 1;        // s_j.pg, y_j.pg, pg.pg
@@ -278,13 +277,17 @@ __device__ __forceinline__ void block_sum(double (&v)[NV], double* sh) {
   __syncthreads();
 }
 
+// Chunk sums in chunk order (fixed: bitwise reproducible), one lane per value q into the shared vs[NV]
+// (the loads of a lane pipeline, instead of one serial lane paying a round trip per chunk).
+// The caller synchronizes before reading vs.
 template <int NV>
-__device__ __forceinline__ void reduce_chunks(const double* P, int nch, double (&v)[NV]) {
-#pragma unroll
-  for (int q = 0; q < NV; ++q) v[q] = 0.0;
-  for (int c = 0; c < nch; ++c) {
-#pragma unroll
-    for (int q = 0; q < NV; ++q) v[q] += P[c * NV + q];
+__device__ __forceinline__ void reduce_chunks_shared(const double* P, int nch, double* vs) {
+  const int q = threadIdx.x;
+  if (q < NV) {
+    double t = 0.0;
+#pragma unroll 8
+    for (int c = 0; c < nch; ++c) t += P[c * NV + q];
+    vs[q] = t;
   }
 }
 
@@ -308,7 +311,7 @@ __device__ __forceinline__ float sgnf(float v) { return v > 0.f ? 1.f : (v < 0.f
 
 // the previous phase 2 of model b, completed by one lane (pick[b]: >= 0 accepted trial, -1 no
 // trial accepted / inactive, -2 non-descent direction)
-__device__ void qn_finalize(const QnArgs& a, int b) {
+__device__ void qn_finalize(const QnArgs& a, int b, const double* v) {
   const int mm = a.m;
   const int p = a.pick[b];
   if (a.fin_init) {
@@ -317,9 +320,7 @@ __device__ void qn_finalize(const QnArgs& a, int b) {
     return;
   }
   const int h = a.fin_head;
-  if (p >= 0) {
-    double v[NP3];
-    reduce_chunks<NP3>(a.P3 + (int64_t)b * a.nch * NP3, a.nch, v);
+  if (p >= 0) {  // v: the P3 chunk sums (LDS)
     double* SY = a.SY + (int64_t)b * mm * mm;
     double* YY = a.YY + (int64_t)b * mm * mm;
     SY[h * mm + h] = v[0];
@@ -358,8 +359,13 @@ __device__ void qn_finalize(const QnArgs& a, int b) {
 // phase 0
 __global__ __launch_bounds__(QN_BLOCK) void qn_dots_kernel(QnArgs a) {
   __shared__ double sh[4 * NP1];
+  __shared__ double fin_v[NP3];
   const int c = blockIdx.x, b = blockIdx.y;
-  if (a.fin && c == 0 && threadIdx.x == 0) qn_finalize(a, b);
+  if (a.fin && c == 0) {  // block-uniform
+    if (!a.fin_init && a.pick[b] >= 0) reduce_chunks_shared<NP3>(a.P3 + (int64_t)b * a.nch * NP3, a.nch, fin_v);
+    __syncthreads();
+    if (threadIdx.x == 0) qn_finalize(a, b, fin_v);
+  }
   if (a.fin_only) return;
   const int D = (int)a.D;
   const int mm = a.m;
@@ -369,12 +375,12 @@ __global__ __launch_bounds__(QN_BLOCK) void qn_dots_kernel(QnArgs a) {
   const float* __restrict__ l1v = a.l1 ? a.l1 + (int64_t)b * D : nullptr;
   const float* __restrict__ Sb = a.S + (int64_t)b * D;
   const float* __restrict__ Yb = a.Y + (int64_t)b * D;
-  const int e1 = min(D, (c + 1) * QN_CHUNK);
+  const int csz = (D + a.nch - 1) / a.nch, e1 = min(D, (c + 1) * csz);
   float acc[NP1];
 #pragma unroll
   for (int j = 0; j < NP1; ++j) acc[j] = 0.f;
 #pragma unroll 2
-  for (int e = c * QN_CHUNK + threadIdx.x; e < e1; e += QN_BLOCK) {
+  for (int e = c * csz + threadIdx.x; e < e1; e += QN_BLOCK) {
     const float pg = pseudo_grad(x[e], g[e], l1v ? l1v[e] : 0.f);
     acc[2 * QN_MAX_M] = fmaf(pg, pg, acc[2 * QN_MAX_M]);
 #pragma unroll
@@ -403,38 +409,52 @@ __global__ __launch_bounds__(QN_BLOCK) void qn_direction_kernel(QnArgs a) {
   const int mm = a.m;
   const int Fp1 = a.F + 1;
   const bool steep = a.steep[b] != 0;
+  // the recursion's operands live in LDS: the P1 chunk sums (reduced by NP1 lanes), the Gram
+  // matrices, rho and the coefficient vectors (per-lane arrays indexed by slot would spill to scratch)
+  __shared__ double p1v[NP1], SY[QN_MAX_M * QN_MAX_M], YY[QN_MAX_M * QN_MAX_M], rho_s[QN_MAX_M];
+  __shared__ double u[QN_MAX_M], w[QN_MAX_M], al[QN_MAX_M];
+  const bool rec = !a.init && !steep;  // block-uniform
+  if (rec) {
+    reduce_chunks_shared<NP1>(a.P1 + (int64_t)b * a.nch * NP1, a.nch, p1v);
+    const double* SYg = a.SY + (int64_t)b * mm * mm;
+    const double* YYg = a.YY + (int64_t)b * mm * mm;
+    for (int i = threadIdx.x; i < mm * mm; i += QN_BLOCK) {
+      SY[i] = SYg[i];
+      YY[i] = YYg[i];
+    }
+    if (threadIdx.x < QN_MAX_M) {
+      const int j = threadIdx.x;
+      rho_s[j] = j < mm ? a.rho[j * a.B + b] : 0.0;
+      u[j] = w[j] = al[j] = 0.0;
+    }
+    __syncthreads();
+  }
   if (threadIdx.x == 0) {
     float gamma = 0.f;
     for (int j = 0; j < QN_MAX_M; ++j) cS[j] = cY[j] = 0.f;
-    if (!a.init && !steep) {  // the two-loop recursion on coefficients
-      double v[NP1];
-      reduce_chunks<NP1>(a.P1 + (int64_t)b * a.nch * NP1, a.nch, v);
-      const double* SY = a.SY + (int64_t)b * mm * mm;
-      const double* YY = a.YY + (int64_t)b * mm * mm;
-      double u[QN_MAX_M], w[QN_MAX_M], al[QN_MAX_M];
-      for (int j = 0; j < QN_MAX_M; ++j) u[j] = w[j] = al[j] = 0.0;
+    if (rec) {  // the two-loop recursion on coefficients
       for (int i = 0; i < a.filled; ++i) {  // newest -> oldest: q = pg + sum u_k y_k
         const int j = (a.head - 1 - i + mm) % mm;
-        const double rho = a.rho[j * a.B + b];
+        const double rho = rho_s[j];
         if (rho == 0.0) continue;
-        double sq = v[j];
+        double sq = p1v[j];
         for (int k = 0; k < mm; ++k) sq += u[k] * SY[j * mm + k];
         al[j] = rho * sq;
         u[j] -= al[j];
       }
       double gm;
       if (a.filled == 0) {
-        gm = 1.0 / fmax(sqrt(v[2 * QN_MAX_M]), 1e-12);
+        gm = 1.0 / fmax(sqrt(p1v[2 * QN_MAX_M]), 1e-12);
       } else {
         const int n = (a.head - 1 + mm) % mm;
         const double yy = YY[n * mm + n];
-        gm = (a.rho[n * a.B + b] > 0.0 && yy > 0.0) ? SY[n * mm + n] / yy : 1.0;
+        gm = (rho_s[n] > 0.0 && yy > 0.0) ? SY[n * mm + n] / yy : 1.0;
       }
       for (int i = a.filled - 1; i >= 0; --i) {  // oldest -> newest: r = gamma q + sum w_k s_k
         const int j = (a.head - 1 - i + mm) % mm;
-        const double rho = a.rho[j * a.B + b];
+        const double rho = rho_s[j];
         if (rho == 0.0) continue;
-        double yr = v[QN_MAX_M + j];
+        double yr = p1v[QN_MAX_M + j];
         for (int k = 0; k < mm; ++k) yr += u[k] * YY[j * mm + k];
         yr *= gm;
         for (int k = 0; k < mm; ++k) yr += w[k] * SY[k * mm + j];
@@ -459,12 +479,12 @@ __global__ __launch_bounds__(QN_BLOCK) void qn_direction_kernel(QnArgs a) {
   const int T = a.init ? 1 : a.T;
   const float s0 = a.init ? 0.f : a.step_scale[b];
   const float gamma = gam;
-  const int e1 = min(D, (c + 1) * QN_CHUNK);
+  const int csz = (D + a.nch - 1) / a.nch, e1 = min(D, (c + 1) * csz);
   float r[NP2];
 #pragma unroll
   for (int t = 0; t < NP2; ++t) r[t] = 0.f;
 #pragma unroll 2
-  for (int e = c * QN_CHUNK + threadIdx.x; e < e1; e += QN_BLOCK) {
+  for (int e = c * csz + threadIdx.x; e < e1; e += QN_BLOCK) {
     const float xe = x[e];
     const float l1e = l1v ? l1v[e] : 0.f;
     const float pg = a.init ? 0.f : pseudo_grad(xe, g[e], l1e);
@@ -518,16 +538,17 @@ __global__ __launch_bounds__(QN_BLOCK) void qn_direction_kernel(QnArgs a) {
 // phase 2
 __global__ __launch_bounds__(QN_BLOCK) void qn_update_kernel(QnArgs a) {
   __shared__ double sh[4 * NP3];
+  __shared__ double p2v[NP2];
   __shared__ int pick;
   const int c = blockIdx.x, b = blockIdx.y;
   const int D = (int)a.D;
   const int mm = a.m;
   const bool active = a.active[b] != 0;
+  reduce_chunks_shared<NP2>(a.P2 + (int64_t)b * a.nch * NP2, a.nch, p2v);
+  __syncthreads();
   if (threadIdx.x == 0) {
-    double v[NP2];
-    reduce_chunks<NP2>(a.P2 + (int64_t)b * a.nch * NP2, a.nch, v);
     const bool steep = a.steep[b] != 0;
-    const double dd = steep ? -v[3 * QN_MAX_TRIALS + 1] : v[3 * QN_MAX_TRIALS];
+    const double dd = steep ? -p2v[3 * QN_MAX_TRIALS + 1] : p2v[3 * QN_MAX_TRIALS];
     const int T = a.init ? 1 : a.T;
     const float s0 = a.init ? 0.f : a.step_scale[b];
     int p = -1;
@@ -540,8 +561,8 @@ __global__ __launch_bounds__(QN_BLOCK) void qn_update_kernel(QnArgs a) {
         const double F0 = a.fobj[b];
         for (int t = 0; t < T && p < 0; ++t) {
           const int bt = b * a.T + t;
-          const double decr = a.l1 ? v[3 * t + 2] : (double)(s0 * ldexpf(1.f, -t)) * dd;
-          const double Ft = a.loss[bt] + v[3 * t] + v[3 * t + 1];
+          const double decr = a.l1 ? p2v[3 * t + 2] : (double)(s0 * ldexpf(1.f, -t)) * dd;
+          const double Ft = a.loss[bt] + p2v[3 * t] + p2v[3 * t + 1];
           if (isfinite(Ft) && Ft <= F0 + a.c1 * decr) p = t;
         }
       }
@@ -549,8 +570,8 @@ __global__ __launch_bounds__(QN_BLOCK) void qn_update_kernel(QnArgs a) {
     if (c == 0) {
       a.pick[b] = p;
       for (int t = 0; t < T; ++t) {
-        a.reg[b * a.T + t] = v[3 * t] + v[3 * t + 1];
-        a.decr[b * a.T + t] = a.l1 ? v[3 * t + 2] : (double)(s0 * ldexpf(1.f, -t)) * dd;
+        a.reg[b * a.T + t] = p2v[3 * t] + p2v[3 * t + 1];
+        a.decr[b * a.T + t] = a.l1 ? p2v[3 * t + 2] : (double)(s0 * ldexpf(1.f, -t)) * dd;
       }
     }
     pick = p;
@@ -570,12 +591,12 @@ __global__ __launch_bounds__(QN_BLOCK) void qn_update_kernel(QnArgs a) {
   const float* __restrict__ xt = a.xtrial + (int64_t)bt * D;
   const float* __restrict__ Gt = a.G + (int64_t)bt * D;
   const float* __restrict__ l2 = a.l2 + (int64_t)b * D;
-  const int e1 = min(D, (c + 1) * QN_CHUNK);
+  const int csz = (D + a.nch - 1) / a.nch, e1 = min(D, (c + 1) * csz);
   float ps[NP3];
 #pragma unroll
   for (int q = 0; q < NP3; ++q) ps[q] = 0.f;
 #pragma unroll 2
-  for (int e = c * QN_CHUNK + threadIdx.x; e < e1; e += QN_BLOCK) {
+  for (int e = c * csz + threadIdx.x; e < e1; e += QN_BLOCK) {
     const float xn = xt[e];
     const float gn = Gt[e] + l2[e] * xn;  // data gradient (masked, scaled) + L2 term
     if (!a.init) {
@@ -644,12 +665,20 @@ extern "C" int har_logreg_grad(const LogregGradArgs* args, int KP, int n_models,
   return 0;
 }
 
-extern "C" int har_qn_chunks(int64_t D) { return (int)((D + QN_CHUNK - 1) / QN_CHUNK); }
+// Chunks per model: at most 512 workgroups over the B models of a solve — what the chip holds at
+// once at the phases' 228-256 VGPRs (two 4-wave workgroups per CU); one more workgroup than that
+// runs as a second round (45 models x 12 chunks: 88 us per phase vs 72 at 10) — so a single fit
+// streams its history with 32 CUs and a 45-model CrossValidator batch with 11 chunks per model;
+// at least 256 elements per chunk.
+extern "C" int har_qn_chunks(int64_t D, int B) {
+  const int64_t by_b = 512 / std::max(B, 1), by_d = (D + 255) / 256;
+  return (int)std::max<int64_t>(1, std::min<int64_t>(32, std::min(by_b, by_d)));
+}
 
 extern "C" int har_lbfgs_phase(const QnArgs* args, int KP, int phase, hipStream_t s) {
   const QnArgs& a = *args;
   if ((KP != 8 && KP != 16) || a.K > KP || a.m < 1 || a.m > QN_MAX_M || a.T < 1 || a.T > QN_MAX_TRIALS ||
-      a.D != (int64_t)a.K * (a.F + 1) || a.D >= (1LL << 31) || a.nch != har_qn_chunks(a.D) || phase < 0 ||
+      a.D != (int64_t)a.K * (a.F + 1) || a.D >= (1LL << 31) || a.nch != har_qn_chunks(a.D, a.B) || phase < 0 ||
       phase > 3)
     return -2;
   if (a.B == 0) return 0;

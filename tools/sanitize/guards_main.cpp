@@ -163,7 +163,7 @@ static void sizing_helpers() {
   for (int64_t n : ns) {
     EXPECT_TRUE(har_column_stats_workspace(n, 3100) >= 0);
     EXPECT_TRUE(har_logreg_eval_tiles(n) >= 0);
-    EXPECT_TRUE(har_qn_chunks(n) >= 0);
+    EXPECT_TRUE(har_qn_chunks(n, 1) >= 1 && har_qn_chunks(n, 45) >= 1 && har_qn_chunks(n, 0) >= 1);
     EXPECT_TRUE(har_tree_level_group_chunks(n) >= 0);
   }
 }
