@@ -356,7 +356,10 @@ __device__ void qn_finalize(const QnArgs& a, int b, const double* v) {
   if (a.hist) a.hist[(int64_t)a.fin_it * a.B + b] = a.fobj[b];
 }
 
+// FULLM (history of QN_MAX_M pairs, the default m): the per-element history loops are unrolled with no
+// slot conditions, so a lane issues all 2 m history loads of an element before it waits
 // phase 0
+template <bool FULLM>
 __global__ __launch_bounds__(QN_BLOCK) void qn_dots_kernel(QnArgs a) {
   __shared__ double sh[4 * NP1];
   __shared__ double fin_v[NP3];
@@ -385,7 +388,7 @@ __global__ __launch_bounds__(QN_BLOCK) void qn_dots_kernel(QnArgs a) {
     acc[2 * QN_MAX_M] = fmaf(pg, pg, acc[2 * QN_MAX_M]);
 #pragma unroll
     for (int j = 0; j < QN_MAX_M; ++j) {
-      if (j < mm) {
+      if (FULLM || j < mm) {
         acc[j] = fmaf(Sb[j * sstride + e], pg, acc[j]);
         acc[QN_MAX_M + j] = fmaf(Yb[j * sstride + e], pg, acc[QN_MAX_M + j]);
       }
@@ -399,7 +402,7 @@ __global__ __launch_bounds__(QN_BLOCK) void qn_dots_kernel(QnArgs a) {
 }
 
 // phase 1
-template <int KP>
+template <int KP, bool FULLM>
 __global__ __launch_bounds__(QN_BLOCK) void qn_direction_kernel(QnArgs a) {
   __shared__ double sh[4 * NP2];
   __shared__ float cS[QN_MAX_M], cY[QN_MAX_M];
@@ -496,7 +499,7 @@ __global__ __launch_bounds__(QN_BLOCK) void qn_direction_kernel(QnArgs a) {
         float acc = gamma * pg;
 #pragma unroll
         for (int j = 0; j < QN_MAX_M; ++j) {
-          if (j < mm) {
+          if (FULLM || j < mm) {
             acc = fmaf(cY[j], Yb[j * sstride + e], acc);
             acc = fmaf(cS[j], Sb[j * sstride + e], acc);
           }
@@ -536,6 +539,7 @@ __global__ __launch_bounds__(QN_BLOCK) void qn_direction_kernel(QnArgs a) {
 }
 
 // phase 2
+template <bool FULLM>
 __global__ __launch_bounds__(QN_BLOCK) void qn_update_kernel(QnArgs a) {
   __shared__ double sh[4 * NP3];
   __shared__ double p2v[NP2];
@@ -583,10 +587,10 @@ __global__ __launch_bounds__(QN_BLOCK) void qn_update_kernel(QnArgs a) {
   float* __restrict__ x = a.x + (int64_t)b * D;
   float* __restrict__ g = a.g + (int64_t)b * D;
   const float* __restrict__ l1v = a.l1 ? a.l1 + (int64_t)b * D : nullptr;
-  float* __restrict__ Sh = a.S + (int64_t)a.head * sstride + (int64_t)b * D;
-  float* __restrict__ Yh = a.Y + (int64_t)a.head * sstride + (int64_t)b * D;
-  const float* __restrict__ Sb = a.S + (int64_t)b * D;
-  const float* __restrict__ Yb = a.Y + (int64_t)b * D;
+  float* Sh = a.S + (int64_t)a.head * sstride + (int64_t)b * D;  // aliases slot `head` of Sb / Yb
+  float* Yh = a.Y + (int64_t)a.head * sstride + (int64_t)b * D;
+  const float* Sb = a.S + (int64_t)b * D;
+  const float* Yb = a.Y + (int64_t)b * D;
   const int bt = b * a.T + p;
   const float* __restrict__ xt = a.xtrial + (int64_t)bt * D;
   const float* __restrict__ Gt = a.G + (int64_t)bt * D;
@@ -601,20 +605,22 @@ __global__ __launch_bounds__(QN_BLOCK) void qn_update_kernel(QnArgs a) {
     const float gn = Gt[e] + l2[e] * xn;  // data gradient (masked, scaled) + L2 term
     if (!a.init) {
       const float se = xn - x[e], ye = gn - g[e];
-      Sh[e] = se;
-      Yh[e] = ye;
       ps[0] = fmaf(se, ye, ps[0]);
       ps[1] = fmaf(se, se, ps[1]);
       ps[2] = fmaf(ye, ye, ps[2]);
 #pragma unroll
       for (int j = 0; j < QN_MAX_M; ++j) {
-        if (j < mm && j != a.head) {
+        // FULLM also accumulates slot `head` (its OLD pair: the loads precede the stores below);
+        // finalize never reads those sums
+        if (FULLM || (j < mm && j != a.head)) {
           const float sj = Sb[j * sstride + e], yj = Yb[j * sstride + e];
           ps[5 + 3 * j] = fmaf(se, yj, ps[5 + 3 * j]);
           ps[6 + 3 * j] = fmaf(sj, ye, ps[6 + 3 * j]);
           ps[7 + 3 * j] = fmaf(ye, yj, ps[7 + 3 * j]);
         }
       }
+      Sh[e] = se;
+      Yh[e] = ye;
     }
     const float pg = pseudo_grad(xn, gn, l1v ? l1v[e] : 0.f);
     ps[3] = fmaf(xn, xn, ps[3]);
@@ -682,20 +688,32 @@ extern "C" int har_lbfgs_phase(const QnArgs* args, int KP, int phase, hipStream_
       phase > 3)
     return -2;
   if (a.B == 0) return 0;
+  const bool full = a.m == QN_MAX_M;
+  const dim3 grid(a.nch, a.B);
   if (phase == 3) {
     QnArgs f = a;
     f.fin = 1;
     f.fin_only = 1;
-    qn_dots_kernel<<<dim3(1, a.B), QN_BLOCK, 0, s>>>(f);
+    qn_dots_kernel<false><<<dim3(1, a.B), QN_BLOCK, 0, s>>>(f);
   } else if (phase == 0) {
-    qn_dots_kernel<<<dim3(a.nch, a.B), QN_BLOCK, 0, s>>>(a);
-  } else if (phase == 1) {
-    if (KP == 8)
-      qn_direction_kernel<8><<<dim3(a.nch, a.B), QN_BLOCK, 0, s>>>(a);
+    if (full)
+      qn_dots_kernel<true><<<grid, QN_BLOCK, 0, s>>>(a);
     else
-      qn_direction_kernel<16><<<dim3(a.nch, a.B), QN_BLOCK, 0, s>>>(a);
+      qn_dots_kernel<false><<<grid, QN_BLOCK, 0, s>>>(a);
+  } else if (phase == 1) {
+    if (KP == 8 && full)
+      qn_direction_kernel<8, true><<<grid, QN_BLOCK, 0, s>>>(a);
+    else if (KP == 8)
+      qn_direction_kernel<8, false><<<grid, QN_BLOCK, 0, s>>>(a);
+    else if (full)
+      qn_direction_kernel<16, true><<<grid, QN_BLOCK, 0, s>>>(a);
+    else
+      qn_direction_kernel<16, false><<<grid, QN_BLOCK, 0, s>>>(a);
   } else {
-    qn_update_kernel<<<dim3(a.nch, a.B), QN_BLOCK, 0, s>>>(a);
+    if (full)
+      qn_update_kernel<true><<<grid, QN_BLOCK, 0, s>>>(a);
+    else
+      qn_update_kernel<false><<<grid, QN_BLOCK, 0, s>>>(a);
   }
   HAR_CHECK_LAUNCH();
   return 0;
