@@ -23,6 +23,7 @@ in one lock-stepped batched optimization on the device — the CrossValidator's
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass
 from typing import List, Optional, Sequence
 
@@ -132,6 +133,40 @@ class LogisticRegressionModel(ClassificationModel):
                 "binomial": self.binomial}
 
 
+def _check_trials(t) -> None:
+    if not isinstance(t, (int, np.integer)) or not 1 <= int(t) <= 4:
+        raise ValueError(f"lineSearchTrials must be an integer in [1, 4] (the device solver evaluates at most 4 "
+                         f"step lengths per line search), got {t!r}")
+
+
+def _content_checksums(hm: HybridMatrix, y: torch.Tensor, specs, allreduce=None) -> List[float]:
+    """Position-weighted fp64 checksums of the fit's data (dense features, one-hot column ids,
+    labels and every spec's row weights — the CV fold masks), summed over ranks: a checkpoint
+    fingerprint that changes with the data content and the fold assignment, not just its shape.
+    Computed on the data's device."""
+    dev = hm.device
+    n = hm.n_rows
+    pos = torch.arange(n, device=dev, dtype=torch.float64)  # shard-local: the fingerprint records the world size
+    wr = torch.cos(pos * 0.6180339887) + 1.5  # distinct, bounded weight per row
+
+    def cs(t: torch.Tensor) -> torch.Tensor:
+        t = t.double().reshape(n, -1)
+        t = torch.nan_to_num(t, nan=-7.0)
+        colw = torch.sin(torch.arange(t.shape[1], device=dev, dtype=torch.float64) * 0.7548776662) + 2.0
+        return (t * wr[:, None] * colw[None, :]).sum()
+
+    parts = [cs(hm.dense) if hm.dense.numel() else torch.zeros((), dtype=torch.float64, device=dev),
+             cs(hm.cat) if hm.cat.numel() else torch.zeros((), dtype=torch.float64, device=dev),
+             cs(y)]
+    for s in specs:
+        parts.append(cs(s.row_weight) if s.row_weight is not None else torch.zeros((), dtype=torch.float64,
+                                                                                   device=dev))
+    v = torch.stack(parts)
+    if allreduce is not None:
+        allreduce(v)
+    return [float(f"{x:.12g}") for x in v.cpu().tolist()]
+
+
 class LogisticRegression(Estimator, ClassifierParams):
     _param_names = ("maxIter", "regParam", "elasticNetParam", "tol", "fitIntercept", "standardization", "family",
                     "featuresCol", "labelCol", "weightCol", "device", "lineSearchTrials", "threshold", "thresholds",
@@ -154,6 +189,7 @@ class LogisticRegression(Estimator, ClassifierParams):
         self.tol, self.fitIntercept, self.standardization = tol, fitIntercept, standardization
         self.family, self.weightCol, self.device = family, weightCol, device
         self.lineSearchTrials = lineSearchTrials  # step lengths 2^-t evaluated together per line search
+        _check_trials(lineSearchTrials)
 
     # ------------------------------------------------------------------
     def fit(self, table: Table) -> LogisticRegressionModel:
@@ -244,16 +280,25 @@ class LogisticRegression(Estimator, ClassifierParams):
         dev = hm.device
         F = hm.n_features
         K = int(num_classes or int(y.max()) + 1)
+        _check_trials(self.lineSearchTrials)
         ckpt = fp = None
         if self.checkpointDir:
+            import hashlib
+            import json
+
             from ..utils.checkpoint import Checkpointer
 
-            ckpt = Checkpointer(self.checkpointDir)
+            ctx = dp_context() if allreduce is not None else None
             fp = {"rows": int(hm.n_rows), "features": int(F), "classes": K, "maxIter": self.maxIter,
                   "tol": self.tol, "fitIntercept": self.fitIntercept, "standardization": self.standardization,
                   "family": self.family, "lineSearchTrials": self.lineSearchTrials,
                   "specs": [[s.regParam, s.elasticNetParam, s.row_weight is None] for s in specs],
-                  "labels_sum": int(y.long().sum()), "world": 0 if allreduce is None else 1}
+                  "content": _content_checksums(hm, y, specs, allreduce),
+                  "world": ctx.world_size if ctx else 1}
+            # one directory per fingerprint: the CV fits and the final refit of one job (and any
+            # other fit sharing checkpointDir) never overwrite or resume each other
+            key = hashlib.sha256(json.dumps(fp, sort_keys=True, default=str).encode()).hexdigest()[:16]
+            ckpt = Checkpointer(os.path.join(self.checkpointDir, f"lr-{key}"), rank=ctx.rank if ctx else 0)
             last = ckpt.latest(fingerprint=fp)
             if last is not None:
                 return self._models_from_state(last[0], last[1], len(specs), dev)

@@ -215,7 +215,8 @@ class MLPEngine:
         s = self.layout.by_name[name]
         return self.slabs.view(-1)[s.offset:]
 
-    def forward_backward_native(self, Xb: torch.Tensor, y32: torch.Tensor, scale: float, on_grad=None):
+    def forward_backward_native(self, Xb: torch.Tensor, y32: torch.Tensor, scale: float, on_grad=None,
+                                _record=None):
         """Xb: [B, in_pad] bf16 (contiguous slice), y32: [B] int32.  Leaves the gradient partials
         in the slabs (``_grad_regions``); ``on_grad(name)`` is called as soon as layer ``name``'s
         weight/bias gradient slabs are enqueued (a hook for tracing / tests)."""
@@ -229,7 +230,7 @@ class MLPEngine:
         nh = len(L.hidden)
         acts = [Xb] + [a[:B] for a in self.acts[1:]]
         if self.fused_ok and B % 16 == 0:
-            return self._forward_backward_fused(Xb, y32, scale, on_grad, ks, acts)
+            return self._forward_backward_fused(Xb, y32, scale, on_grad, ks, acts, _record)
         self.last_fused = False
         self.last_bwd = False
         for i in range(nh):
@@ -268,10 +269,11 @@ class MLPEngine:
                           mask=acts[i], tile=dgrad_tile(B, hp, h))
                 dact = prev
 
-    def _forward_backward_fused(self, Xb, y32, scale, on_grad, ks, acts):
+    def _forward_backward_fused(self, Xb, y32, scale, on_grad, ks, acts, record=None):
         """2-hidden-layer step: ONE kernel for fwd L1 + fwd L2 + head + dWout/dbout (+ db1) (h2 and
         the logit gradients stay on chip), then ONE kernel for dW1 + dgrad + dW0 / db0 (H = 256),
-        or dW1, dgrad and dW0 as split-K MFMA GEMMs."""
+        or dW1, dgrad and dW0 as split-K MFMA GEMMs.  ``record`` (a list) receives one re-launchable
+        closure per kernel (tools/mlp_phase_probe.py)."""
         L, mod, s = self.layout, _native.kernels(), _native.stream_ptr()
         B, H, K0 = Xb.shape[0], self.dims[-1], L.in_pad
         total = L.total
@@ -281,11 +283,18 @@ class MLPEngine:
         self.last_bwd = self.bwd_ok and B % 64 == 0 and mod.mlp_fwd_head_variant(H, B) == 2
         # with the fused backward, h1 never reaches HBM: that kernel recomputes it from X (same bits)
         rh1 = self.last_bwd and RECOMPUTE_H1
-        mod.mlp_fwd_head(Xb.data_ptr(), K0, self._w(self.Pb, "W0").data_ptr(), self._w(self.P, "b0").data_ptr(),
-                         self._w(self.Pb, "W1").data_ptr(), self._w(self.P, "b1").data_ptr(), H,
-                         self._w(self.Pb, "Wout").data_ptr(), self._w(self.P, "bout").data_ptr(), y32.data_ptr(),
-                         B, L.num_classes, float(scale), 0 if rh1 else h1.data_ptr(), dact.data_ptr(),
-                         self.fslab.data_ptr(), self.fblock_loss.data_ptr(), self.fblock_correct.data_ptr(), s)
+
+        def fwd():
+            mod.mlp_fwd_head(Xb.data_ptr(), K0, self._w(self.Pb, "W0").data_ptr(), self._w(self.P, "b0").data_ptr(),
+                             self._w(self.Pb, "W1").data_ptr(), self._w(self.P, "b1").data_ptr(), H,
+                             self._w(self.Pb, "Wout").data_ptr(), self._w(self.P, "bout").data_ptr(),
+                             y32.data_ptr(), B, L.num_classes, float(scale), 0 if rh1 else h1.data_ptr(),
+                             dact.data_ptr(), self.fslab.data_ptr(), self.fblock_loss.data_ptr(),
+                             self.fblock_correct.data_ptr(), s)
+
+        fwd()
+        if record is not None:
+            record.append(fwd)
         self.last_fused = True
         self.last_batch = B
         if on_grad is not None:
@@ -295,11 +304,17 @@ class MLPEngine:
             # dW1 + dgrad + relu' + dW0 / db0: one kernel, one partial per row slice in self.slabs
             self.bwd_S = mod.mlp_bwd_fused_slices(B)
             sb = self.slabs.data_ptr()
-            mod.mlp_bwd_fused(dact.data_ptr(), 0 if rh1 else h1.data_ptr(), Xb.data_ptr(), K0,
-                              self._w(self.Pb, "W1").data_ptr(), H, B, sb + 4 * L.by_name["W1"].offset,
-                              sb + 4 * L.by_name["W0"].offset, sb + 4 * L.by_name["b0"].offset, total,
-                              self.step_count.data_ptr(), self._w(self.Pb, "W0").data_ptr(),
-                              self._w(self.P, "b0").data_ptr(), s)
+
+            def bwd():
+                mod.mlp_bwd_fused(dact.data_ptr(), 0 if rh1 else h1.data_ptr(), Xb.data_ptr(), K0,
+                                  self._w(self.Pb, "W1").data_ptr(), H, B, sb + 4 * L.by_name["W1"].offset,
+                                  sb + 4 * L.by_name["W0"].offset, sb + 4 * L.by_name["b0"].offset, total,
+                                  self.step_count.data_ptr(), self._w(self.Pb, "W0").data_ptr(),
+                                  self._w(self.P, "b0").data_ptr(), s)
+
+            bwd()
+            if record is not None:
+                record.append(bwd)
             if on_grad is not None:
                 on_grad("W1")
                 on_grad("W0")
@@ -331,6 +346,25 @@ class MLPEngine:
             on_grad("W0")
         if self.side is not None:  # join: the W1 slabs (and the next step's h1 / dact2 reuse) are ordered
             main.wait_event(self.ev_join)
+
+    def phase_fns(self, Xb: torch.Tensor, y32: torch.Tensor, global_batch: int):
+        """One callable per kernel of the fused step (forward, backward, reduction + Adam), for
+        tools/mlp_phase_probe.py: each re-launches exactly one kernel on the state the last full
+        step left behind."""
+        self.forward_backward_native(Xb, y32, 1.0 / global_batch)
+        calls = []
+
+        def fb():
+            self.forward_backward_native(Xb, y32, 1.0 / global_batch, _record=calls)
+
+        fb()
+        out = {}
+        if calls:
+            out["fwd"] = calls[0]
+            if len(calls) > 1:
+                out["bwd"] = calls[1]
+        out["reduce"] = lambda: self._grad_kernel(self.GR_REDUCE | self.GR_ADAM, tick=not self.last_bwd)
+        return out
 
     def _grad_regions(self):
         """Sources of the flat gradient after the last native batch, in flat order: (start, end,

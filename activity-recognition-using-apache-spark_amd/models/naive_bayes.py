@@ -17,7 +17,7 @@ from typing import Optional
 import torch
 
 from ..data.table import Table
-from ..ops.gemm import EPI_BIAS_F32, EPI_F32_ATOMIC, gemm_f32
+from ..ops.gemm import EPI_BIAS_F32, EPI_F32_SLAB, auto_k_split, gemm_f32
 from .base import ClassificationModel, ClassifierParams, Estimator, dp_allreduce, dp_context, dp_owner, dp_rows, \
     features_tensor, labels_tensor, new_uid, resolve_device
 
@@ -38,8 +38,15 @@ def class_moments(X: torch.Tensor, y: torch.Tensor, K: int, w: Optional[torch.Te
         XX = torch.zeros(N, Fp, device=X.device)
         XX[:, :F] = X
         XX[:, F:2 * F] = X * X
-        S = torch.zeros(Kp, Fp, device=X.device)
-        gemm_f32(Yp, XX, S, M=Kp, N=Fp, K=N, layout=3, epi=EPI_F32_ATOMIC)
+        # deterministic split-K: every batch slice writes its partial [Kp, Fp] tile into its own
+        # slab (plain stores), then one fixed-order sum over the slabs — bitwise reproducible,
+        # unlike float atomics
+        ks = auto_k_split(Kp, Fp, N)
+        splits = (N + ks - 1) // ks
+        slabs = torch.empty(splits, Kp, Fp, device=X.device)
+        gemm_f32(Yp, XX, slabs, M=Kp, N=Fp, K=N, layout=3, epi=EPI_F32_SLAB, k_split=ks, ldc=Fp,
+                 slab_stride=Kp * Fp)
+        S = slabs.sum(0)
         return Y.sum(0), S[:K, :F], S[:K, F:2 * F]
     return Y.sum(0), Y.T @ X, Y.T @ (X * X)
 

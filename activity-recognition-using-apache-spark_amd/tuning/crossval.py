@@ -97,6 +97,19 @@ class CrossValidatorModel(Model):
         return self.uid
 
 
+def _batched_predictions(models, raw: torch.Tensor) -> torch.Tensor:
+    """Predicted classes of a stack of models' raw outputs ``raw`` [n, N, K], as each model's
+    ``transform`` would give them: argmax of the probabilities, or of the probabilities scaled by
+    the model's ``thresholds`` when it has them (Spark scores CV folds through
+    ``model.transform``, which applies the thresholds; ``Main/main.py:209-215``)."""
+    if all(getattr(m, "thresholds", None) is None for m in models):
+        return torch.argmax(raw, dim=2)  # probabilities are monotone in the raw scores per row
+    preds = []
+    for m, r in zip(models, raw):
+        preds.append(m._predict_from_probability(m.raw_to_probability(r)))
+    return torch.stack(preds)
+
+
 class CrossValidator(Estimator):
     def __init__(self, estimator=None, estimatorParamMaps: Optional[List[Dict]] = None, evaluator=None,
                  numFolds: int = 3, seed: int = 0, parallelism: int = 1, collectSubModels: bool = False):
@@ -132,7 +145,7 @@ class CrossValidator(Estimator):
             models = base.fit_many(hm.rows(lo, hi), y[lo:hi], specs, K, allreduce=dp_allreduce())
             # every (map, fold) model scored on its validation fold in ONE batched pass
             raw = _lr_margins(models, hm)                                          # [n, N, K]
-            pred = torch.argmax(raw, dim=2)
+            pred = _batched_predictions(models, raw)
             mask = torch.stack([fold_t == f for _, f in index])
             vals = ev.evaluate_batched(y, pred, mask, K, raw)
             for (mi, f), v in zip(index, vals):
@@ -145,8 +158,7 @@ class CrossValidator(Estimator):
             for mi, pm in enumerate(maps):
                 fms = est.copy(pm).fit_folds(X, y, K, masks)
                 raws = [m.predict_raw(X) for m in fms]
-                raw = torch.stack([m.raw_to_probability(r) for m, r in zip(fms, raws)])
-                pred = torch.argmax(raw, dim=2)
+                pred = _batched_predictions(fms, torch.stack(raws))
                 vals = ev.evaluate_batched(y, pred, masks == 0, K, torch.stack(raws))
                 metrics[mi, :] = vals
         else:

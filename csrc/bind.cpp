@@ -405,6 +405,7 @@ PYBIND11_MODULE(_har_native, m) {
   m.def("mlp_fwd_head_grid", &har_mlp_fwd_head_grid);
   m.def("mlp_bwd_fused_slices", &har_mlp_bwd_fused_slices);
   m.def("mlp_fwd_head_variant", &har_mlp_fwd_head_variant);
+  m.def("mlp_set_stamps", [](u p) { har_mlp_set_stamps(P<uint64_t>(p)); });
   m.def("mlp_bwd_fused", [](u dact2, u h1, u X, int K0, u W1, int H, int B, u gw1, u gw0, u gb0, int64_t stride,
                             u tick, u W0, u b0, u stream) {
     check(har_mlp_bwd_fused(P<const uint16_t>(dact2), P<const uint16_t>(h1), P<const uint16_t>(X), K0,

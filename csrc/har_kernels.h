@@ -80,6 +80,8 @@ int har_mlp_bwd_fused(const uint16_t* dact2, const uint16_t* h1, const uint16_t*
                       const uint16_t* W0, const float* b0, hipStream_t s);
 int har_mlp_bwd_fused_slices(int B);
 int har_mlp_fwd_head_variant(int H, int B);
+// diagnostic phase stamps of the fused training kernels (nullptr = off); see mlp_fused.hip
+void har_mlp_set_stamps(uint64_t* p);
 // Serving variant of the same kernel: logits [B][C] fp32 + argmax class [B] int32, nothing else.
 int har_mlp_fwd_infer_f32(const float* X, int ldx, int F, int K0, const uint16_t* W0, const float* b0,
                           const uint16_t* W1, const float* b1, int H, const uint16_t* Wo, const float* bo, int B, int C,

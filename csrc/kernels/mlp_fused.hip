@@ -32,6 +32,23 @@
 
 namespace {
 
+// Diagnostic phase stamps (tools/mlp_phase_probe.py --stamps): a separate STAMP instantiation of
+// the training kernels, launched only while a stamp buffer is set, has lane 0 of every wave store
+// s_memtime (shader clock) at fixed points into its own 40-slot row of that buffer (slots 38 / 39:
+// s_memrealtime at entry / exit, 100 MHz, one clock for the whole chip).  Nothing else reads them.
+uint64_t* g_stamps = nullptr;
+constexpr size_t STAMP_BWD_OFF = (size_t)256 * 8 * 40;  // the backward's rows follow the forward's
+#define HAR_STAMP(NW, k)                                                                     \
+  if constexpr (STAMP) {                                                                     \
+    if ((threadIdx.x & 63) == 0)                                                             \
+      stamps[((size_t)blockIdx.x * (NW) + (threadIdx.x >> 6)) * 40 + (k)] = __builtin_amdgcn_s_memtime(); \
+  }
+#define HAR_STAMP_REAL(NW, k)                                                                \
+  if constexpr (STAMP) {                                                                     \
+    if ((threadIdx.x & 63) == 0)                                                             \
+      stamps[((size_t)blockIdx.x * (NW) + (threadIdx.x >> 6)) * 40 + (k)] = __builtin_amdgcn_s_memrealtime(); \
+  }
+
 typedef __attribute__((ext_vector_type(4))) short s16x4_t;
 typedef __attribute__((address_space(3))) s16x4_t lds_s16x4_t;
 typedef __attribute__((ext_vector_type(4))) uint32_t u32x4_t;
@@ -469,14 +486,14 @@ __device__ __forceinline__ bf16x8_t frag_tr(const bf16_t* img, int pitch, int co
 
 // SH1 = false: h1 is not written (the fused backward recomputes it from X: 2 x B x 256 bf16 of HBM
 // traffic saved per step for ~2 GFLOP of MFMA work)
-template <int K0, bool INFER, int XF = 0, bool SH1 = true>
+template <int K0, bool INFER, int XF = 0, bool SH1 = true, bool STAMP = false>
 __global__ __launch_bounds__(512) void mlp_fwd_head_v2_kernel(
     const bf16_t* __restrict__ X, const bf16_t* __restrict__ W0, const float* __restrict__ b0,
     const bf16_t* __restrict__ W1, const float* __restrict__ b1, const bf16_t* __restrict__ Wo,
     const float* __restrict__ bo, const int32_t* __restrict__ labels, int B, int C, float scale,
     bf16_t* __restrict__ h1out, bf16_t* __restrict__ dact, float* __restrict__ slab,
     float* __restrict__ block_loss, int32_t* __restrict__ block_correct, float* __restrict__ logits_out,
-    int32_t* __restrict__ pred_out, int F, int ldx) {
+    int32_t* __restrict__ pred_out, int F, int ldx, uint64_t* __restrict__ stamps) {
   constexpr int H = V2_H, K0C = K0 / 32, KC = H / 32;
   extern __shared__ __attribute__((aligned(16))) bf16_t lds[];
   bf16_t* h1s = lds;                                          // [32][V2_HP] h1 tile
@@ -488,6 +505,8 @@ __global__ __launch_bounds__(512) void mlp_fwd_head_v2_kernel(
   const int u0 = wave * V2_U;
   bf16_t* img = reinterpret_cast<bf16_t*>(dzs + 2 * 64 * 2) + wave * 3 * V2_IMG;  // h2 t=0, t=1, dz
   const LaneSwap swp(lane);
+  HAR_STAMP_REAL(V2_W, 38)
+  HAR_STAMP(V2_W, 0)
 
   // ---- this wave's weight slices, in registers for the whole kernel ----
   bf16x8_t w0f[2][K0C], w1f[2][KC];
@@ -521,6 +540,8 @@ __global__ __launch_bounds__(512) void mlp_fwd_head_v2_kernel(
 #pragma unroll
   for (int r = 0; r < 4; ++r) bo_r[r] = (4 * g + r < C) ? bo[4 * g + r] : 0.f;
 
+  if constexpr (STAMP) __builtin_amdgcn_s_waitcnt(0x0f70);
+  HAR_STAMP(V2_W, 1)
   f32x4_t acc5[2] = {f32x4_t{0.f, 0.f, 0.f, 0.f}, f32x4_t{0.f, 0.f, 0.f, 0.f}};
   float db1[2][4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};  // column sums of this lane's dact2 values
   float dbo[4] = {0.f, 0.f, 0.f, 0.f};
@@ -537,8 +558,11 @@ __global__ __launch_bounds__(512) void mlp_fwd_head_v2_kernel(
       for (int kc = 0; kc < K0C; ++kc) xb[h][kc] = load_x<K0, XF>(X, T * V2_RT + 16 * h + c16, kc, g, F, ldx);
     }
   }
+  int it_ = 0;
   for (; T < ntiles; T += gridDim.x) {
     const int r0 = T * V2_RT;
+    if (it_ < 32) HAR_STAMP(V2_W, 2 + it_)
+    ++it_;
     // ---- stage 1: h1^T = W0 . X^T for this wave's units ----
 #pragma unroll
     for (int h = 0; h < 2; ++h)
@@ -723,6 +747,7 @@ __global__ __launch_bounds__(512) void mlp_fwd_head_v2_kernel(
   }
 
   if constexpr (INFER) return;
+  HAR_STAMP(V2_W, 34)
   __syncthreads();  // the last tile's dact2 tile is complete
   if (prev_r0 >= 0) v2_store_tile(dts, dact, prev_r0, tid);
   // ---- this wave's units of the workgroup slab: dWout rows 0..15 x units, dbout, loss ----
@@ -763,6 +788,9 @@ __global__ __launch_bounds__(512) void mlp_fwd_head_v2_kernel(
     block_loss[blockIdx.x] = red[2 * NCLS] + red[2 * NCLS + 1];
     block_correct[blockIdx.x] = (int)(red[2 * NCLS + 2] + red[2 * NCLS + 3]);
   }
+  if constexpr (STAMP) __builtin_amdgcn_s_waitcnt(0x0f70);
+  HAR_STAMP(V2_W, 35)
+  HAR_STAMP_REAL(V2_W, 39)
 }
 
 template <int K0, bool INFER = false, int XF = 0>
@@ -771,8 +799,9 @@ int launch_v2(const bf16_t* X, const bf16_t* W0, const float* b0, const bf16_t* 
               bf16_t* dact, float* slab, float* block_loss, int32_t* block_correct, int nwg, hipStream_t s,
               float* logits = nullptr, int32_t* pred = nullptr, int F = K0, int ldx = K0) {
   auto kern = (INFER || h1) ? mlp_fwd_head_v2_kernel<K0, INFER, XF, true> : mlp_fwd_head_v2_kernel<K0, INFER, XF, false>;
+  if (!INFER && !h1 && g_stamps) kern = mlp_fwd_head_v2_kernel<K0, INFER, XF, false, true>;
   kern<<<nwg, 512, V2_LDS, s>>>(X, W0, b0, W1, b1, Wo, bo, labels, B, C, scale, h1, dact, slab, block_loss,
-                                block_correct, logits, pred, F, ldx);
+                                block_correct, logits, pred, F, ldx, g_stamps);
   HAR_CHECK_LAUNCH();
   return 0;
 }
@@ -830,7 +859,7 @@ template <int K0, bool RH1 = false> struct BwdLds {
                                   4 * BF_QU * sizeof(float);
 };
 
-template <int K0, bool RH1 = false>
+template <int K0, bool RH1 = false, bool STAMP = false>
 __global__ __launch_bounds__(512) void mlp_bwd_fused_kernel(const bf16_t* __restrict__ dact2,
                                                            const bf16_t* __restrict__ h1,
                                                            const bf16_t* __restrict__ X,
@@ -839,7 +868,8 @@ __global__ __launch_bounds__(512) void mlp_bwd_fused_kernel(const bf16_t* __rest
                                                            float* __restrict__ gb0, int64_t slab_stride,
                                                            int32_t* __restrict__ tick,
                                                            const bf16_t* __restrict__ W0,
-                                                           const float* __restrict__ b0) {
+                                                           const float* __restrict__ b0,
+                                                           uint64_t* __restrict__ stamps) {
   using L = BwdLds<K0, RH1>;
   constexpr int NXB = L::NXB;
   // the training step counter ticks here (one thread, before the reduction kernel reads it for Adam)
@@ -854,6 +884,8 @@ __global__ __launch_bounds__(512) void mlp_bwd_fused_kernel(const bf16_t* __rest
   float* const red = reinterpret_cast<float*>(xs0 + 3 * L::XS);  // [4][64] db0 of the row blocks
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int c16 = lane & 15, g = lane >> 4;
+  HAR_STAMP_REAL(8, 38)
+  HAR_STAMP(8, 0)
   const int b = xcd_remap(blockIdx.x, gridDim.x);
   const int slice = b / BF_Q, qu0 = (b % BF_Q) * BF_QU;
   const int rb = wave & 3, up = 2 * (wave >> 2);            // (a)
@@ -885,6 +917,8 @@ __global__ __launch_bounds__(512) void mlp_bwd_fused_kernel(const bf16_t* __rest
       w0q[kc] = *reinterpret_cast<const bf16x8_t*>(W0 + (size_t)(qu0 + 16 * ubh + c16) * K0 + kc * 32 + 8 * g);
     b0q = *reinterpret_cast<const float4*>(b0 + qu0 + 16 * ubh + 4 * g);
   }
+  if constexpr (STAMP) __builtin_amdgcn_s_waitcnt(0x0f70);
+  HAR_STAMP(8, 1)
   f32x4_t acc1[4][2], acc0[NFW];
 #pragma unroll
   for (int i = 0; i < 4; ++i) acc1[i][0] = acc1[i][1] = f32x4_t{0.f, 0.f, 0.f, 0.f};
@@ -1019,6 +1053,7 @@ __global__ __launch_bounds__(512) void mlp_bwd_fused_kernel(const bf16_t* __rest
     tile_h1(0);
     __syncthreads();  // h1 tile 0 complete
     for (int i = 0; i < n; ++i) {
+      if (i < 32) HAR_STAMP(8, 2 + i)
       HAR_BWD_STAGE_D(i + 1)        // waits for the refills issued one iteration ago
       HAR_BWD_STAGE_X(i + 2)
       HAR_BWD_LOAD_D(t0 + i + 2)
@@ -1044,6 +1079,7 @@ __global__ __launch_bounds__(512) void mlp_bwd_fused_kernel(const bf16_t* __rest
       __syncthreads();              // tile i+1 staged; tile i's dact1 complete; buffers of i-1 free
     }
   }
+  HAR_STAMP(8, 34)
   if (n > 0) tile_c(n - 1);
 #undef HAR_BWD_LOAD
 #undef HAR_BWD_LOAD_D
@@ -1078,6 +1114,9 @@ __global__ __launch_bounds__(512) void mlp_bwd_fused_kernel(const bf16_t* __rest
   __syncthreads();
   if (tid < BF_QU)
     gb0[(size_t)slice * slab_stride + qu0 + tid] = (red[tid] + red[BF_QU + tid]) + (red[2 * BF_QU + tid] + red[3 * BF_QU + tid]);
+  if constexpr (STAMP) __builtin_amdgcn_s_waitcnt(0x0f70);
+  HAR_STAMP(8, 35)
+  HAR_STAMP_REAL(8, 39)
 }
 
 // Training only: serving (stages 1-3) keeps v1 — without the backward stages, v2's two barriers
@@ -1149,6 +1188,11 @@ extern "C" int har_mlp_fwd_infer_f32(const float* X, int ldx, int F, int K0, con
   return -4;
 }
 
+// Diagnostic: while p != nullptr the training launches of the fused forward (h1 recomputed) and
+// the fused backward (K0 = 64) run their stamped instantiations into p (>= 2 x 256 x 8 x 40
+// uint64, forward rows first); grids are at most 256 workgroups of 8 waves.
+extern "C" void har_mlp_set_stamps(uint64_t* p) { g_stamps = p; }
+
 extern "C" int har_mlp_fwd_head_variant(int H, int B) { return use_v2(H, B) ? 2 : 1; }
 
 // Row slices of the fused backward: >= 4 tiles (256 rows) per slice, <= 64 slices (one slab each).
@@ -1170,17 +1214,20 @@ extern "C" int har_mlp_bwd_fused(const uint16_t* dact2, const uint16_t* h1, cons
   if (h1) {
     if (K0 == 64)
       mlp_bwd_fused_kernel<64, false><<<grid, 512, BwdLds<64, false>::bytes, s>>>(dact2, h1, X, W1, B, S, gw1, gw0,
-                                                                                  gb0, slab_stride, tick, W0, b0);
+                                                                                  gb0, slab_stride, tick, W0, b0, nullptr);
     else
       mlp_bwd_fused_kernel<32, false><<<grid, 512, BwdLds<32, false>::bytes, s>>>(dact2, h1, X, W1, B, S, gw1, gw0,
-                                                                                  gb0, slab_stride, tick, W0, b0);
+                                                                                  gb0, slab_stride, tick, W0, b0, nullptr);
+  } else if (g_stamps && K0 == 64) {
+    mlp_bwd_fused_kernel<64, true, true><<<grid, 512, BwdLds<64, true>::bytes, s>>>(
+        dact2, h1, X, W1, B, S, gw1, gw0, gb0, slab_stride, tick, W0, b0, g_stamps + STAMP_BWD_OFF);
   } else {
     if (K0 == 64)
       mlp_bwd_fused_kernel<64, true><<<grid, 512, BwdLds<64, true>::bytes, s>>>(dact2, h1, X, W1, B, S, gw1, gw0,
-                                                                                gb0, slab_stride, tick, W0, b0);
+                                                                                gb0, slab_stride, tick, W0, b0, nullptr);
     else
       mlp_bwd_fused_kernel<32, true><<<grid, 512, BwdLds<32, true>::bytes, s>>>(dact2, h1, X, W1, B, S, gw1, gw0,
-                                                                                gb0, slab_stride, tick, W0, b0);
+                                                                                gb0, slab_stride, tick, W0, b0, nullptr);
   }
   HAR_CHECK_LAUNCH();
   return 0;

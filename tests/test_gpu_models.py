@@ -152,6 +152,21 @@ def test_naive_bayes_gpu_matches_cpu(cuda):
         torch.testing.assert_close(g.predict_raw(xx.to(cuda)).cpu(), c.predict_raw(xx), rtol=1e-4, atol=1e-3)
 
 
+def test_naive_bayes_gpu_bitwise_deterministic(cuda):
+    """NB class moments reduce split-K slabs in a fixed order (no float atomics): two fits of the
+    same data give bit-identical parameters."""
+    from har.models.naive_bayes import NaiveBayes
+
+    x, y = _blobs(20000, 24, 5, seed=9)
+    xg, yg = x.to(cuda), y.to(cuda)
+    for mt, xx in (("gaussian", xg), ("multinomial", xg.abs())):
+        a = NaiveBayes(modelType=mt).fit_tensors(xx, yg, 5)
+        b = NaiveBayes(modelType=mt).fit_tensors(xx, yg, 5)
+        assert torch.equal(a.theta, b.theta) and torch.equal(a.pi, b.pi)
+        if a.sigma is not None:
+            assert torch.equal(a.sigma, b.sigma)
+
+
 def test_main_reference_run_gpu(cuda, tmp_path, wisdm_csv):
     import main
 

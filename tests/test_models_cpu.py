@@ -318,3 +318,52 @@ def test_logreg_checkpoint_resume(tmp_path, monkeypatch):
         assert mb.summary["resumed"] and mb.summary["iterations"] == ma.summary["iterations"]
     with pytest.raises(AssertionError):  # a different fit (maxIter) is not resumed from the stale checkpoint
         LogisticRegression(maxIter=21, device="cpu", checkpointDir=ck).fit_many(X, y, specs, 3)
+
+
+def test_crossvalidator_scores_with_thresholds():
+    """CV folds are scored as model.transform would predict them: a LogisticRegression(threshold=t)
+    inside CrossValidator is scored at t, not at 0.5 (Spark scores folds through transform)."""
+    from har.data.table import Column, Table
+    from har.tuning.crossval import _batched_predictions
+
+    g = torch.Generator().manual_seed(3)
+    X = torch.randn(900, 3, generator=g)
+    y = (X[:, 0] + 0.8 * torch.randn(900, generator=g) > 0).long()
+    lr = LogisticRegression(maxIter=25, device="cpu", threshold=0.85)
+    models = lr.fit_many(X, y, [FitSpec(None, 0.0, 0.0), FitSpec(None, 0.1, 0.0)], 2)
+    raw = torch.stack([m.predict_raw(X) for m in models])
+    pred = _batched_predictions(models, raw)
+    for m, p in zip(models, pred):
+        assert torch.equal(p, m.predict(X))
+    assert int(pred.sum()) < int(torch.argmax(raw, 2).sum())  # the threshold moved predictions
+    t = Table([Column("features", "vector", X.numpy().astype(np.float64)),
+               Column("label", "double", y.numpy().astype(np.float64))])
+    ev = MulticlassClassificationEvaluator(metricName="accuracy")
+    plain = CrossValidator(estimator=LogisticRegression(maxIter=25, device="cpu"), evaluator=ev, numFolds=3,
+                           seed=1).fit(t)
+    strict = CrossValidator(estimator=lr, evaluator=ev, numFolds=3, seed=1).fit(t)
+    assert strict.avgMetrics[0] < plain.avgMetrics[0]
+
+
+def test_logreg_checkpoint_keys_on_content(tmp_path):
+    """The LR checkpoint fingerprint carries the data content and the fold masks: a rerun on other
+    data of the same shape / label sum, or with other fold masks, does not resume a stale fit; fits
+    with different fingerprints in one directory do not overwrite each other."""
+    g = torch.Generator().manual_seed(5)
+    X = torch.randn(400, 4, generator=g)
+    y = torch.randint(0, 3, (400,), generator=g)
+    ck = str(tmp_path / "lr")
+    w1 = (torch.arange(400) % 5 != 0).float()
+    w2 = (torch.arange(400) % 5 != 1).float()
+    lr = LogisticRegression(maxIter=15, device="cpu", checkpointDir=ck)
+    a = lr.fit_many(X, y, [FitSpec(w1, 0.1, 0.0)], 3)[0]
+    b = lr.fit_many(X, y, [FitSpec(w2, 0.1, 0.0)], 3)[0]      # other fold mask: solved, not resumed
+    assert not b.summary.get("resumed")
+    X2 = X.clone()
+    X2[0, 0] += 1.0                                            # same shape and labels, other content
+    c = lr.fit_many(X2, y, [FitSpec(w1, 0.1, 0.0)], 3)[0]
+    assert not c.summary.get("resumed")
+    a2 = lr.fit_many(X, y, [FitSpec(w1, 0.1, 0.0)], 3)[0]     # the first fit is still there
+    assert a2.summary.get("resumed") and torch.equal(a2.coefficientMatrix, a.coefficientMatrix)
+    with pytest.raises(ValueError):
+        LogisticRegression(lineSearchTrials=5)
