@@ -34,8 +34,7 @@ from ..data.table import Table
 from ..ops import _native
 from ..features.hybrid import HybridMatrix, hybrid_features
 from ..features.hybrid import from_dense as hybrid_from_dense
-from ..ops.logreg import (DeviceLogregSolver, LogregDesign, LogregWorkspace, logreg_loss_grad_native,
-                          logreg_margins_native)
+from ..ops.logreg import DeviceLogregSolver, LogregDesign, logreg_margins_native, pack_bucket, unpack_bucket
 from ..optim import lbfgs
 from .base import ClassificationModel, ClassifierParams, Estimator, dp_allreduce, dp_context, dp_owner, dp_rows, \
     features_tensor, labels_tensor, new_uid, resolve_device
@@ -83,36 +82,17 @@ class LogisticRegressionModel(ClassificationModel):
 
     def predict_raw(self, X) -> torch.Tensor:
         """Margins (binomial: ``[-m, m]``).  ``X``: dense ``[N, F]`` or a HybridMatrix.  On the GPU
-        the logreg_qn.hip evaluation kernel (prediction mode) runs for any hybrid input and for
-        dense inputs up to its LDS tile width; wider dense inputs use the exact-fp32 MFMA GEMM."""
+        the logreg_qn.hip evaluation kernel (prediction mode) runs for every input (dense columns of
+        any width are staged through LDS in chunks)."""
         k = self.coefficientMatrix.shape[0]
         if isinstance(X, HybridMatrix) or X.is_cuda:
-            hm = X if isinstance(X, HybridMatrix) else None
-            dense_w = X.shape[1] if hm is None else int(hm.dense.shape[1])
-            if hm is None and dense_w <= _native.kernels().logreg_max_dense():
-                hm = hybrid_from_dense(X.float(), [])
-            if hm is not None and hm.device.type == "cuda" and int(hm.dense.shape[1]) <= \
-                    _native.kernels().logreg_max_dense():
+            hm = X if isinstance(X, HybridMatrix) else hybrid_from_dense(X.float(), [])
+            if hm.device.type == "cuda":
                 KP = 8 if k <= 8 else 16
                 m = logreg_margins_native(hm, self.weight_table(KP).to(hm.device), k, 1)[0, :, :k]
-            elif hm is not None and hm.device.type != "cuda":
+            else:
                 Xd = hm.to_dense()
                 m = Xd @ self.coefficientMatrix.to(Xd.device).T + self.interceptVector.to(Xd.device)
-            else:
-                from ..ops.gemm import EPI_BIAS_F32, gemm_f32
-                Xd = X if hm is None else hm.to_dense()
-                W = self.coefficientMatrix.to(Xd.device)
-                F4 = (Xd.shape[1] + 3) // 4 * 4
-                if F4 != Xd.shape[1]:
-                    Xd = torch.nn.functional.pad(Xd, (0, F4 - Xd.shape[1]))
-                rows = max(8, (k + 7) // 8 * 8)
-                Wp = torch.zeros(rows, F4, device=Xd.device)
-                Wp[:k, :W.shape[1]] = W
-                bp = torch.zeros(rows, device=Xd.device)
-                bp[:k] = self.interceptVector.to(Xd.device)
-                Z = torch.empty(Xd.shape[0], rows, device=Xd.device)
-                gemm_f32(Xd.contiguous(), Wp, Z, M=Xd.shape[0], N=rows, K=F4, layout=0, epi=EPI_BIAS_F32, bias=bp)
-                m = Z[:, :k]
         else:
             m = X @ self.coefficientMatrix.to(X.device).T + self.interceptVector.to(X.device)
         if self.binomial:
@@ -215,18 +195,41 @@ class LogisticRegression(Estimator, ClassifierParams):
         return model
 
     def _setup(self, hm: HybridMatrix, y: torch.Tensor, specs: Sequence[FitSpec], K: int, allreduce):
-        """Summarizer (+ its one all-reduce) -> standardization, masks, regularization vectors, x0."""
+        """Summarizer (+ its one all-reduce) -> standardization, masks, regularization vectors, x0.
+        GPU: three HIP launches (logreg_setup.hip), no host round trip; CPU: the same math in torch."""
         dev = hm.device
         N, F = hm.n_rows, hm.n_features
         binomial = self.family == "binomial" or (self.family == "auto" and K <= 2)
         Kp = 2 if binomial else K
         B = len(specs)
-        rw = torch.stack([torch.ones(N, device=dev) if s.row_weight is None else s.row_weight.to(dev).float()
-                          for s in specs])                                            # [B, N]
+        if all(s.row_weight is None for s in specs) and dev.type == "cuda":
+            rw = None                                                               # every row weight 1
+        else:
+            rw = torch.stack([torch.ones(N, device=dev) if s.row_weight is None else s.row_weight.to(dev).float()
+                              for s in specs])                                        # [B, N]
         design = LogregDesign(hm, y, rw, Kp)
         summ = design.summary()
         if allreduce is not None:
             allreduce(summ)
+        D = Kp * (F + 1)
+        if dev.type == "cuda":
+            reg_a = torch.tensor([[s.regParam for s in specs], [s.elasticNetParam for s in specs]],
+                                 dtype=torch.float32).to(dev, non_blocking=True)
+            has_l1 = any(s.regParam * s.elasticNetParam > 0 for s in specs)
+            if design.S != B:  # unweighted: one summary row serves every spec
+                summ = summ.expand(B, -1).contiguous()
+            inv_std = torch.empty(B, F, device=dev)
+            inv_wsum = torch.empty(B, device=dev)
+            pmask = torch.empty(B, Kp, F + 1, device=dev)
+            l2v = torch.empty(B, D, device=dev)
+            l1v = torch.empty(B, D, device=dev) if has_l1 else None
+            x0 = torch.empty(B, Kp, F + 1, device=dev)
+            _native.kernels().logreg_prepare(summ.data_ptr(), reg_a[0].data_ptr(), reg_a[1].data_ptr(), B, F, Kp, Kp,
+                                             int(self.standardization), int(self.fitIntercept), int(binomial),
+                                             inv_std.data_ptr(), inv_wsum.data_ptr(), pmask.data_ptr(),
+                                             l2v.data_ptr(), 0 if l1v is None else l1v.data_ptr(), x0.data_ptr(),
+                                             _native.stream_ptr())
+            return design, binomial, Kp, inv_std, inv_wsum, pmask, l2v, l1v, x0
         wsum = summ[:, 0]
         mean = summ[:, 1:1 + F] / wsum[:, None]
         ex2 = summ[:, 1 + F:1 + 2 * F] / wsum[:, None]
@@ -240,7 +243,6 @@ class LogisticRegression(Estimator, ClassifierParams):
             inv_std = torch.where(std > 0, torch.ones_like(std), torch.zeros_like(std))
         reg = torch.tensor([s.regParam for s in specs], device=dev, dtype=torch.float32)
         alpha = torch.tensor([s.elasticNetParam for s in specs], device=dev, dtype=torch.float32)
-        D = Kp * (F + 1)
         # parameters x[b] = [K, F+1] in standardized space (last column = intercept)
         x0 = torch.zeros(B, Kp, F + 1, device=dev)
         if self.fitIntercept:
@@ -306,26 +308,30 @@ class LogisticRegression(Estimator, ClassifierParams):
         B, D = len(specs), Kp * (F + 1)
         T = max(1, int(self.lineSearchTrials))
         poll = 10 if self.maxIter > 20 else 0
-        if dev.type == "cuda" and design.Fd <= _native.kernels().logreg_max_dense() and Kp <= 16:
+        if dev.type == "cuda":
+            if Kp > 16:
+                raise ValueError(f"the device LogisticRegression supports at most 16 classes, got {Kp}")
             solver = DeviceLogregSolver(design, B, T, 10, inv_std, pmask, inv_wsum, l2v, l1v, self.maxIter, self.tol,
                                         allreduce=allreduce)
             xs, fobj, iters = solver.solve(x0, poll=poll)
-            n_evals, history = solver.n_evals, solver.hist
-        elif dev.type == "cuda":
-            xs, fobj, iters, n_evals, history = self._fit_wide_dense(hm, y, design, inv_std, inv_wsum, pmask, l2v,
-                                                                     l1v, x0, allreduce)
+            n_evals = solver.n_evals
+            hist_h = solver.hist.cpu()
+            history = [solver.history(bi, hist_h) for bi in range(B)]
         else:
             def evaluate(xt):
                 loss, G = design.eval_torch(xt.view(-1, Kp, F + 1), T if xt.shape[0] != B else 1, inv_std, pmask,
                                             inv_wsum)
-                if allreduce is not None:
-                    allreduce(G)
-                    allreduce(loss)
+                if allreduce is not None:  # ONE collective per evaluation: [gradients | exact losses]
+                    bucket = pack_bucket(G, loss)
+                    allreduce(bucket)
+                    G2, loss = unpack_bucket(bucket, loss.numel(), G.shape)
+                    G = G2.to(G.dtype)
                 return loss, G
 
             res = lbfgs.minimize_trials(evaluate, x0.reshape(B, D), l2v, l1v, max_iter=self.maxIter, m=10,
                                         tol=self.tol, trials=T, poll=poll)
             xs, fobj, iters, n_evals, history = res.x, res.f, res.iterations, res.n_evals, res.history
+            history = [list(history) for _ in range(B)]  # per-model lists (the batch mean per iteration)
         xs = xs.view(B, Kp, F + 1) * pmask
         models = []
         fobj_h = fobj.double().cpu()
@@ -338,7 +344,7 @@ class LogisticRegression(Estimator, ClassifierParams):
             elif self.fitIntercept:
                 icpt = icpt - icpt.mean()
             summary = {"objective": float(fobj_h[bi]), "iterations": int(iters_h[bi]), "n_evals": n_evals,
-                       "objectiveHistory": history}
+                       "objectiveHistory": history[bi]}
             models.append(self._apply_thresholds(LogisticRegressionModel(coef.detach(), icpt.detach(), binomial,
                                                                          device=dev, summary=summary)))
         if ckpt is not None:
@@ -357,35 +363,6 @@ class LogisticRegression(Estimator, ClassifierParams):
                 st[f"coef{bi}"].to(dev), st[f"icpt{bi}"].to(dev), bool(meta["binomial"]), device=dev,
                 summary=summary)))
         return out
-
-    def _fit_wide_dense(self, hm, y, design, inv_std, inv_wsum, pmask, l2v, l1v, x0, allreduce):
-        """GPU objective for dense blocks wider than the fused kernel's LDS tile: exact-fp32 MFMA
-        GEMMs (ops.logreg.logreg_loss_grad_native, F padded to a multiple of 4) driven by the
-        serial-backtracking L-BFGS."""
-        X = hm.to_dense()
-        B, Kp, Fp1 = x0.shape
-        F = Fp1 - 1
-        F4 = (F + 3) // 4 * 4
-        if F4 != F:
-            X = torch.nn.functional.pad(X, (0, F4 - F))
-        ws = LogregWorkspace(X, B, Kp)
-        y32 = y.to(torch.int32).contiguous()
-        rw = design.rw
-
-        def objective(xflat):
-            xv = xflat.view(B, Kp, F + 1) * pmask
-            W_eff = torch.nn.functional.pad(xv[:, :, :F] * inv_std[:, None, :], (0, F4 - F))
-            loss, gW, gb = logreg_loss_grad_native(X, y32, W_eff, xv[:, :, F], rw, inv_wsum, ws)
-            G = torch.cat([gW[:, :, :F] * inv_std[:, None, :], gb.unsqueeze(2)], dim=2) * pmask
-            G = G.reshape(B, -1)
-            if allreduce is not None:
-                allreduce(G)
-                allreduce(loss)
-            xr = xflat
-            return loss + 0.5 * (l2v * xr * xr).sum(1), G + l2v * xr
-
-        res = lbfgs.minimize(objective, x0.reshape(B, -1), max_iter=self.maxIter, m=10, tol=self.tol, l1=l1v)
-        return res.x, res.f, res.iterations, res.n_evals, res.history
 
 
 __all__ = ["LogisticRegression", "LogisticRegressionModel", "FitSpec"]

@@ -1,32 +1,34 @@
-"""Batched multinomial logistic-regression loss/gradient (kernel K9).
+"""Batched multinomial logistic-regression objective + device L-BFGS (kernels K8-K10).
 
 For B models with effective weights ``W [B, K, F]`` and intercepts ``b [B, K]``
 over one resident feature matrix ``X [N, F]``:
 
-    Z   = X . W^T + b                  (one GEMM for all B*K columns)
+    Z   = X . W^T + b
     P   = softmax over each model's K columns
     R   = rw[b, i] / sum_i rw[b, i] * (P - onehot(y))
     loss[b] = sum_i rw[b,i] * CE_i / sum_i rw[b,i]
     dW  = R^T . X ,   db = sum_i R
 
 ``rw`` carries the per-model row weights (fold membership in CrossValidator,
-Spark's instance weights otherwise), so 45 CV fits share the two GEMMs.
+Spark's instance weights otherwise), so 45 CV fits share one evaluation.
 
-GPU path (gfx950): ``har_gemm_f32`` (exact-fp32 ``v_mfma_f32_16x16x4_f32``,
-bias fused in the epilogue) -> ``har_logreg_softmax_grad`` (fused softmax + CE +
-residual + per-model loss reduction) -> ``har_gemm_f32`` split-K with fp32
-atomics for ``R^T . X``.  CPU path: the same math in PyTorch (test oracle).
+GPU path (gfx950, csrc/kernels/logreg_qn.hip + logreg_setup.hip): the features stay in
+the HYBRID layout (one-hot index blocks + dense columns of any width, staged through LDS
+in 32-column chunks); the summarizer, the standardization / masks / regularization
+vectors, the CSC slice index of the gradient kernel and every L-BFGS / OWL-QN phase are
+HIP kernels — a fit enqueues with no host synchronization.  Data parallel: ONE fp32
+all-reduce per evaluation carries the gradient bucket and the exact (fixed-point) losses.
+CPU path: the same math in PyTorch (test oracle).
 """
 from __future__ import annotations
+
+import os
 
 import torch
 
 from . import _native
-from .gemm import EPI_BIAS_F32, EPI_F32_ATOMIC, gemm_f32
 
-
-def _pad8(x: int) -> int:
-    return (x + 7) // 8 * 8
+SLICE_ROWS = 32  # rows per CSC slice of the gradient / summary kernels
 
 
 def logreg_loss_grad_torch(X, y, W, b, rw, inv_wsum):
@@ -45,110 +47,126 @@ def logreg_loss_grad_torch(X, y, W, b, rw, inv_wsum):
     return loss, gW, gb
 
 
-class LogregWorkspace:
-    """Device buffers reused across the ~30-60 objective evaluations of a fit."""
-
-    def __init__(self, X: torch.Tensor, B: int, K: int):
-        N, F = X.shape
-        self.N, self.F, self.B, self.K = N, F, B, K
-        self.cols = _pad8(B * K)
-        dev = X.device
-        self.Wflat = torch.zeros(self.cols, F, device=dev, dtype=torch.float32)
-        self.bflat = torch.zeros(self.cols, device=dev, dtype=torch.float32)
-        self.Z = torch.empty(N, self.cols, device=dev, dtype=torch.float32)
-        self.R = torch.empty(N, self.cols, device=dev, dtype=torch.float32)
-        self.G = torch.empty(self.cols, F, device=dev, dtype=torch.float32)
-        self.loss = torch.empty(B, device=dev, dtype=torch.float64)
-
-
-def logreg_loss_grad_native(X, y32, W, b, rw, inv_wsum, ws: LogregWorkspace):
-    B, K, F = W.shape
-    N = X.shape[0]
-    if F % 4:
-        raise ValueError("native logreg path needs F % 4 == 0 (pad the feature matrix)")
-    mod = _native.kernels()
-    s = _native.stream_ptr()
-    ws.Wflat[: B * K].copy_(W.reshape(B * K, F))
-    ws.bflat[: B * K].copy_(b.reshape(-1))
-    # Z = X . W^T + b        (A = X K-major, B = W K-major)
-    gemm_f32(X, ws.Wflat, ws.Z, M=N, N=ws.cols, K=F, layout=0, epi=EPI_BIAS_F32, bias=ws.bflat)
-    ws.loss.zero_()
-    mod.logreg_softmax_grad(ws.Z.data_ptr(), N, B, K, ws.cols, y32.data_ptr(), rw.data_ptr(),
-                            inv_wsum.data_ptr(), ws.R.data_ptr(), ws.loss.data_ptr(), s)
-    # G = R^T . X            (A = R M-major [N][cols], B = X N-major [N][F]); split-K over rows
-    ws.G.zero_()
-    gemm_f32(ws.R, X, ws.G, M=ws.cols, N=F, K=N, layout=3, epi=EPI_F32_ATOMIC,
-             k_split=max(32, ((N + 63) // 64 + 31) // 32 * 32))
-    gW = ws.G[: B * K].view(B, K, F)
-    gb = ws.R[:, : B * K].sum(dim=0).view(B, K)
-    return ws.loss.to(torch.float32), gW, gb
-
-
 # ------------------------------------------------------------------------------------------
 # Hybrid-layout objective + device L-BFGS (csrc/kernels/logreg_qn.hip)
 # ------------------------------------------------------------------------------------------
+LOSS_FX = float(2 ** 40)
+
+
+def pack_bucket(G: torch.Tensor, loss: torch.Tensor) -> torch.Tensor:
+    """[gradients (fp32) | each loss as 2^-40 fixed point in four 16-bit pieces + a non-finite
+    flag (fp32 integers)]: the data-parallel all-reduce bucket of one evaluation.  Summing the
+    pieces in fp32 is exact (|sum| < 2^24), so ``unpack_bucket`` returns the exact sum of the
+    ranks' fixed-point losses — the torch twin of logreg_qn.hip's loss_encode / loss_decode."""
+    ld = loss.double()
+    bad = ~(ld.abs() < 8388608.0)
+    q = torch.round(torch.where(bad, torch.zeros_like(ld), ld) * LOSS_FX).to(torch.int64)
+    pieces = [q & 0xffff, (q >> 16) & 0xffff, (q >> 32) & 0xffff, q >> 48, bad.to(torch.int64)]
+    enc = torch.stack(pieces, 1).to(torch.float32)
+    return torch.cat([G.reshape(-1).float(), enc.reshape(-1)])
+
+
+def unpack_bucket(bucket: torch.Tensor, n_loss: int, g_shape):
+    n = bucket.numel() - 5 * n_loss
+    enc = bucket[n:].view(n_loss, 5).to(torch.int64)
+    q = enc[:, 0] + (enc[:, 1] << 16) + (enc[:, 2] << 32) + (enc[:, 3] << 48)
+    loss = q.double() / LOSS_FX
+    loss = torch.where(enc[:, 4] != 0, torch.full_like(loss, float("nan")), loss)
+    return bucket[:n].view(g_shape), loss
+
+
 def _kp(K: int) -> int:
     return 8 if K <= 8 else 16
 
 
+def hybrid_index(hm):
+    """(CSC offsets [F+2], CSC rows, column map [F+1]) of a hybrid matrix, cached on it: derived from
+    the resident (immutable) features, so every fit / CV fold / evaluation over the same matrix
+    reuses one index (one sort per dataset, not per fit)."""
+    idx = getattr(hm, "_lr_index", None)
+    if idx is None:
+        off, rows = hm.csc()
+        if rows.numel() == 0:
+            rows = torch.zeros(1, dtype=torch.int32, device=hm.device)
+        idx = (off, rows, hm.col_map())
+        hm._lr_index = idx
+    return idx
+
+
 class LogregDesign:
     """Device data of one fit: the hybrid feature layout, labels, per-spec row weights, the
-    one-hot CSC row lists and the column map of the gradient kernel."""
+    one-hot CSC row lists (+ their row slices) and the column map of the gradient kernel."""
 
-    def __init__(self, hm, y: torch.Tensor, rw: torch.Tensor, K: int):
+    def __init__(self, hm, y: torch.Tensor, rw, K: int):
         self.hm = hm
         self.N, self.F = hm.n_rows, hm.n_features
         self.Fd, self.C = int(hm.dense.shape[1]), int(hm.cat.shape[1])
         self.K = K
         self.KP = _kp(K)
         self.y32 = y.to(torch.int32).contiguous()
-        self.rw = rw.float().contiguous()                       # [S, N]
-        self.csc_off, self.csc_rows = hm.csc()
-        if self.csc_rows.numel() == 0:
-            self.csc_rows = torch.zeros(1, dtype=torch.int32, device=hm.device)
-        self.col_map = hm.col_map()
+        # [S, N] float32 row weights, or None (every spec unweighted: the kernels read 1)
+        self.rw = None if rw is None else rw.float().contiguous()
+        self.S = 1 if rw is None else int(rw.shape[0])
+        self.csc_off, self.csc_rows, self.col_map = hybrid_index(hm)
         self.dense = hm.dense if self.Fd else torch.zeros(max(1, self.N), 1, device=hm.device)
         self.dense_cols = hm.dense_cols if self.Fd else torch.zeros(1, dtype=torch.int32, device=hm.device)
         self.cat = hm.cat if self.C else torch.zeros(max(1, self.N), 1, dtype=torch.int32, device=hm.device)
+        self.SL = SLICE_ROWS
+        self._col_slice = None
 
-    def grad_partition(self, cols_per_block: int = 128):
-        """Work partition of the gradient kernel (one host read of the CSC offsets per fit):
-        every one-hot column's row list is cut into slices of <= SL rows, SL chosen so no
-        ``cols_per_block``-column window holds more than 256 slices; returns device int32
-        (slice_lo [n_slices+1], col_slice [F+2], blk_col [nb+1], blk_slice [nb+1]) and nb."""
-        if getattr(self, "_part", None) is not None:
-            return self._part
-        import numpy as np
+    @property
+    def device(self):
+        return self.hm.device
 
-        F = self.F
-        off = self.csc_off.cpu().numpy().astype(np.int64)
-        L = off[1:F + 2] - off[:F + 1]                                   # rows per column (F+1)
-        starts = np.arange(0, F + 1, cols_per_block)
-        win = np.add.reduceat(L, starts) if L.size else np.zeros(1, np.int64)
-        SL = max(16, int(-(-int(win.max()) // cols_per_block)) if win.size else 16)
-        ns = -(-L // SL)
-        col_slice = np.zeros(F + 2, np.int64)
-        col_slice[1:] = np.cumsum(ns)
-        total = int(col_slice[-1])
-        col_of = np.repeat(np.arange(F + 1), ns)
-        within = np.arange(total) - col_slice[col_of]
-        slice_lo = np.concatenate([off[col_of] + within * SL, [off[F + 1]]])
-        blk_col = np.concatenate([starts, [F + 1]])
-        blk_slice = col_slice[blk_col]
-        assert int(np.max(np.diff(blk_slice), initial=0)) <= 256 and int(np.max(np.diff(blk_col))) <= 256
-        dev = self.rw.device
-        t = lambda a: torch.as_tensor(a.astype(np.int32)).to(dev)  # noqa: E731
-        self._part = (t(slice_lo), t(col_slice), t(blk_col), t(blk_slice), len(starts))
-        return self._part
+    def col_slice(self) -> torch.Tensor:
+        """[F+2] int32: first CSC row slice (of SL rows) of every column — the work index of the
+        gradient and summary kernels, built on the device (no host read)."""
+        if self._col_slice is None:
+            F = self.F
+            if self.device.type == "cuda":
+                cs = torch.empty(F + 2, dtype=torch.int32, device=self.device)
+                _native.kernels().logreg_col_slices(self.csc_off.data_ptr(), F, self.SL, cs.data_ptr(),
+                                                    _native.stream_ptr())
+            else:
+                L = (self.csc_off[1:].long() - self.csc_off[:-1].long())
+                ns = (L + self.SL - 1) // self.SL
+                cs = torch.zeros(F + 2, dtype=torch.int64)
+                cs[1:] = torch.cumsum(ns, 0)
+                cs = cs.to(torch.int32)
+            self._col_slice = cs
+        return self._col_slice
+
+    def rw_ptr(self) -> int:
+        return 0 if self.rw is None else self.rw.data_ptr()
+
+    def rw_rows(self) -> torch.Tensor:
+        """[S, N] row weights (materialized ones when unweighted; CPU oracle only)."""
+        if self.rw is None:
+            return torch.ones(self.S, self.N, device=self.device)
+        return self.rw
 
     def summary(self):
         """Weighted summarizer per spec (Spark MultivariateOnlineSummarizer + MultiClassSummarizer):
-        [S, 1 + 2F + K] float64 = (sum w, sum w x, sum w x^2, class counts).  One-hot columns are
-        segment sums of the weights over their CSC row lists (fp64 scan), dense columns one fp64
-        product — every sum in a fixed order."""
-        S_, N, F, K = self.rw.shape[0], self.N, self.F, self.K
-        dev = self.rw.device
-        rwd = self.rw.double()
+        [S, 1 + 2F + K] float64 = (sum w, sum w x, sum w x^2, class counts).  GPU: two HIP kernels
+        (logreg_setup.hip: per-tile fp64 partials of the dense columns + class sums, then one lane
+        per column: tile partials in order / w over the CSC row slices of a one-hot column).
+        CPU: one-hot columns are segment sums over their CSC rows (fp64 scan), dense columns one
+        fp64 product.  Every sum in a fixed order."""
+        S_, N, F, K = self.S, self.N, self.F, self.K
+        dev = self.device
+        if dev.type == "cuda":
+            mod, st = _native.kernels(), _native.stream_ptr()
+            nt = mod.logreg_summary_tiles(N)
+            part = torch.empty(S_, max(1, nt), 2 * self.Fd + K + 1, dtype=torch.float64, device=dev)
+            out = torch.empty(S_, 1 + 2 * F + K, dtype=torch.float64, device=dev)
+            cs = self.col_slice()
+            for ph in (0, 1):
+                mod.logreg_summary(ph, self.dense.data_ptr(), self.dense.stride(0), self.Fd, self.y32.data_ptr(),
+                                   self.rw_ptr(), N, F, K, S_, self.col_map.data_ptr(), self.csc_rows.data_ptr(),
+                                   self.csc_off.data_ptr(), cs.data_ptr(), self.SL, nt, part.data_ptr(),
+                                   out.data_ptr(), st)
+            return out
+        rwd = self.rw_rows().double()
         out = torch.zeros(S_, 1 + 2 * F + K, dtype=torch.float64, device=dev)
         out[:, 0] = rwd.sum(1)
         if self.C:
@@ -180,10 +198,27 @@ class LogregDesign:
         if getattr(self, "_X", None) is None:
             self._X = self.hm.to_dense()
         X = self._X.to(xt.dtype)
-        rw = self.rw[spec].to(xt.dtype)
+        rw = self.rw_rows()[spec].to(xt.dtype)
         loss, gW, gb = logreg_loss_grad_torch(X, self.y32.long(), Weff, b, rw, inv_wsum[spec])
         G = torch.cat([gW * inv_std[spec][:, None, :], gb.unsqueeze(2)], dim=2) * pmask[spec]
         return loss.double(), G.reshape(BT, -1)
+
+
+def _arena(specs, dev, into: dict) -> torch.Tensor:
+    """One zero-filled device allocation carved into 256-byte aligned views ``(name, shape, dtype)``,
+    stored into ``into``; returns the backing buffer."""
+    offs, off = [], 0
+    for _, shape, dt in specs:
+        n = 1
+        for v in shape:
+            n *= int(v)
+        nb = n * torch.empty((), dtype=dt).element_size()
+        offs.append((off, nb))
+        off = (off + nb + 255) // 256 * 256
+    buf = torch.zeros(max(off, 256), dtype=torch.uint8, device=dev)
+    for (name, shape, dt), (o, nb) in zip(specs, offs):
+        into[name] = buf[o:o + nb].view(dt).view(shape)
+    return buf
 
 
 class DeviceLogregSolver:
@@ -200,9 +235,6 @@ class DeviceLogregSolver:
         self.D = K * (F + 1)
         D = self.D
         BT = B * T
-        f32 = dict(dtype=torch.float32, device=dev)
-        f64 = dict(dtype=torch.float64, device=dev)
-        i32 = dict(dtype=torch.int32, device=dev)
         self.inv_std = inv_std.float().contiguous()
         self.pmask = pmask.float().reshape(B, D).contiguous()
         self.inv_wsum = inv_wsum.float().contiguous()
@@ -210,34 +242,35 @@ class DeviceLogregSolver:
         self.l1v = None if l1v is None else l1v.float().contiguous()
         self.max_iter, self.tol, self.c1 = max_iter, tol, c1
         self.allreduce = allreduce
-        self.x = torch.zeros(B, D, **f32)
-        self.g = torch.zeros(B, D, **f32)
-        self.fobj = torch.zeros(B, **f64)
-        self.S = torch.zeros(m, B, D, **f32)
-        self.Y = torch.zeros(m, B, D, **f32)
-        self.rho = torch.zeros(m, B, **f64)
-        self.SY = torch.zeros(B, m, m, **f64)   # history Gram matrices (compact two-loop recursion)
-        self.YY = torch.zeros(B, m, m, **f64)
-        self.xtrial = torch.zeros(BT, D, **f32)
-        self.weff = torch.zeros(BT, F + 1, design.KP, **f32)   # padded classes stay 0
-        self.reg = torch.zeros(BT, **f64)
-        self.decr = torch.zeros(BT, **f64)
-        self.G = torch.zeros(BT, D, **f32)        # data gradient of every trial (the DP all-reduce bucket)
-        self.loss = torch.zeros(BT, **f64)        # data loss of every trial (fp64, its own small all-reduce)
-        self.step_scale = torch.ones(B, **f32)
-        self.active = torch.ones(B, **i32)
-        self.fails = torch.zeros(B, **i32)
-        self.iters = torch.zeros(B, **i32)
-        self.steep = torch.zeros(B, **i32)
-        self.pick = torch.zeros(B, **i32)
         self.nch = _native.kernels().qn_chunks(D, B)
-        self.P1 = torch.zeros(B, self.nch, 2 * 10 + 1, **f64)   # chunk partials (QN_MAX_M = 10)
-        self.P2 = torch.zeros(B, self.nch, 3 * 4 + 2, **f64)    # (QN_MAX_TRIALS = 4)
-        self.P3 = torch.zeros(B, self.nch, 5 + 3 * 10, **f64)
-        self.hist = torch.zeros(max_iter + 1, B, **f64)
         self.ntiles = _native.kernels().logreg_eval_tiles(design.N)
-        self.slab = torch.zeros(BT, max(1, self.ntiles), design.Fd * design.KP + design.KP + 1, **f32)
-        self.R = torch.zeros(BT, max(1, design.N), design.KP, **f32) if design.C else None
+        KP, N = design.KP, max(1, design.N)
+        # trial models whose residual rows [N][KP] are held at once (the one-hot gradient reads them):
+        # evaluations are launched in chunks of rchunk models so R stays within HAR_LR_R_BUDGET_MB
+        budget = int(os.environ.get("HAR_LR_R_BUDGET_MB", "1024")) << 20
+        self.rchunk = max(1, min(BT, budget // (N * KP * 4)))
+        f32, f64, i32 = torch.float32, torch.float64, torch.int32
+        # every buffer of the solve is a view of ONE zeroed arena (one allocation + one fill per fit
+        # instead of ~30); the data-parallel bucket G is followed by the fixed-point losses so ONE
+        # all-reduce carries both
+        specs = [("x", (B, D), f32), ("g", (B, D), f32), ("fobj", (B,), f64), ("S", (m, B, D), f32),
+                 ("Y", (m, B, D), f32), ("rho", (m, B), f64), ("SY", (B, m, m), f64), ("YY", (B, m, m), f64),
+                 ("xtrial", (BT, D), f32), ("weff", (BT, F + 1, KP), f32), ("reg", (BT,), f64),
+                 ("decr", (BT,), f64), ("bucket", (BT * D + 5 * BT,), f32), ("loss", (BT,), f64),
+                 ("step_scale", (B,), f32), ("active", (B,), i32), ("fails", (B,), i32), ("iters", (B,), i32),
+                 ("steep", (B,), i32), ("pick", (B,), i32), ("P1", (B, self.nch, 2 * 10 + 1), f64),
+                 ("P2", (B, self.nch, 3 * 4 + 2), f64), ("P3", (B, self.nch, 5 + 3 * 10), f64),
+                 ("hist", (max_iter + 1, B), f64),
+                 ("slab", (BT, max(1, self.ntiles), design.Fd * KP + KP + 1), f32)]
+        if design.C:
+            specs.append(("R", (self.rchunk, N, KP), f32))
+        else:
+            self.R = None
+        self.arena = _arena(specs, dev, self.__dict__)
+        self.G = self.bucket[: BT * D].view(BT, D)          # data gradient of every trial
+        self.loss_fx = self.bucket[BT * D:].view(BT, 5)     # DP only: fixed-point loss pieces
+        self.step_scale.fill_(1.0)
+        self.active.fill_(1)
         self.n_evals = 0
 
     def _args(self, init: int = 0, head: int = 0, filled: int = 0, fin: int = 0, fin_init: int = 0,
@@ -265,33 +298,41 @@ class DeviceLogregSolver:
                 "hist": p(self.hist), "c1": float(self.c1), "tol": float(self.tol)}
 
     def _eval_args(self, tstride: int):
-        """Positional arguments (but the stream) of the evaluate + gradient launches, built once per
-        tstride: the buffers never move during a solve."""
+        """Per launch chunk: positional arguments (but the stream) of the evaluate + gradient
+        launches, built once per tstride: the buffers never move during a solve."""
         cache = self.__dict__.setdefault("_eval_arg_cache", {})
         if tstride not in cache:
             d = self.d
             n_models = (self.B * self.T) // tstride
             R = 0 if self.R is None else self.R.data_ptr()
-            ev = (d.dense.data_ptr(), d.dense.stride(0), d.Fd, d.dense_cols.data_ptr(), d.cat.data_ptr(), d.C,
-                  d.y32.data_ptr(), d.rw.data_ptr(), self.inv_wsum.data_ptr(), self.weff.data_ptr(), d.N, d.F,
-                  d.K, self.T, tstride, 0, R, self.slab.data_ptr(), d.KP, n_models)
-            slice_lo, col_slice, blk_col, blk_slice, nb = d.grad_partition()
-            gr = (self.slab.data_ptr(), R, d.col_map.data_ptr(), d.csc_rows.data_ptr(), slice_lo.data_ptr(),
-                  col_slice.data_ptr(), blk_col.data_ptr(), blk_slice.data_ptr(), nb, self.inv_std.data_ptr(),
-                  self.pmask.data_ptr(), d.N, d.F, d.Fd, d.K, self.T, tstride, self.ntiles, self.G.data_ptr(),
-                  self.loss.data_ptr(), d.KP, n_models)
-            cache[tstride] = (ev, gr)
+            cs = d.col_slice()
+            dp = self.allreduce is not None
+            launches = []
+            for c0 in range(0, n_models, self.rchunk):
+                n = min(self.rchunk, n_models - c0)
+                m0 = c0 * tstride
+                ev = (d.dense.data_ptr(), d.dense.stride(0), d.Fd, d.dense_cols.data_ptr(), d.cat.data_ptr(), d.C,
+                      d.y32.data_ptr(), d.rw_ptr(), self.inv_wsum.data_ptr(), self.weff.data_ptr(), d.N, d.F,
+                      d.K, self.T, tstride, m0, 0, R, self.slab.data_ptr(), d.KP, n)
+                gr = (self.slab.data_ptr(), R, d.col_map.data_ptr(), d.csc_rows.data_ptr(), d.csc_off.data_ptr(),
+                      cs.data_ptr(), d.SL, self.inv_std.data_ptr(), self.pmask.data_ptr(), d.N, d.F, d.Fd, d.K,
+                      self.T, tstride, m0, self.ntiles, self.G.data_ptr(), self.loss.data_ptr(),
+                      self.loss_fx.data_ptr() if dp else 0, d.KP, n)
+                launches.append((ev, gr))
+            cache[tstride] = launches
         return cache[tstride]
 
     def _evaluate(self, tstride: int):
         mod = _native.kernels()
-        ev, gr = self._eval_args(tstride)
         s = _native.stream_ptr()
-        mod.logreg_eval(*ev, s)
-        mod.logreg_grad(*gr, s)
-        if self.allreduce is not None:  # data parallel: the flat fp32 gradient bucket + the fp64 losses
-            self.allreduce(self.G)
-            self.allreduce(self.loss)
+        for ev, gr in self._eval_args(tstride):
+            mod.logreg_eval(*ev, s)
+            mod.logreg_grad(*gr, s)
+        if self.allreduce is not None:
+            # data parallel: ONE fp32 all-reduce of [gradients | fixed-point losses], then the exact
+            # loss sums back to fp64 (every rank then takes the identical optimizer step)
+            self.allreduce(self.bucket)
+            mod.logreg_loss_decode(self.loss_fx.data_ptr(), self.loss.data_ptr(), self.B * self.T, s)
         self.n_evals += 1
 
     def solve(self, x0: torch.Tensor, poll: int = 0):
@@ -317,6 +358,7 @@ class DeviceLogregSolver:
             phase(0, head, filled, fin=1, fin_init=int(prev < 0), fin_head=max(prev, 0), fin_it=it)
             if poll and it and it % poll == 0 and not bool(self.active.any()):
                 finalized = True
+                self.hist_rows = it + 1
                 break
             phase(1, head, filled)
             self._evaluate(1)
@@ -326,7 +368,17 @@ class DeviceLogregSolver:
             filled = min(filled + 1, self.m)
         if not finalized:
             phase(3, fin=1, fin_init=int(prev < 0), fin_head=max(prev, 0), fin_it=self.max_iter)
+            self.hist_rows = self.max_iter + 1
         return self.x, self.fobj, self.iters
+
+    def history(self, b: int, hist_host=None):
+        """Objective history of model ``b`` (a list like Spark's ``objectiveHistory``: the objective
+        after each iteration, trailing repeats of the final value — iterations after convergence —
+        dropped).  ``hist_host``: this solver's ``hist`` already on the host."""
+        h = (self.hist if hist_host is None else hist_host)[: self.hist_rows, b].tolist()
+        while len(h) > 1 and h[-1] == h[-2]:
+            h.pop()
+        return h
 
     def margins(self, W_models: torch.Tensor, hm, n_models: int) -> torch.Tensor:
         """Raw margins of ``n_models`` weight tables ``[n, F+1, KP]`` over ``hm`` rows: [n, N, KP]."""
@@ -347,5 +399,5 @@ def logreg_margins_native(hm, W_models: torch.Tensor, K: int, n_models: int) -> 
     out = torch.empty(n_models, max(1, N), KP, device=dev)
     ones = torch.ones(1, device=dev)
     mod.logreg_eval(dense.data_ptr(), dense.stride(0), Fd, dcols.data_ptr(), cat.data_ptr(), C, 0, 0, ones.data_ptr(),
-                    W_models.contiguous().data_ptr(), N, F, K, 1, 1, 1, out.data_ptr(), 0, KP, n_models, s)
+                    W_models.contiguous().data_ptr(), N, F, K, 1, 1, 0, 1, out.data_ptr(), 0, KP, n_models, s)
     return out[:, :N]

@@ -69,14 +69,12 @@ def _lr_margins(models, hm) -> torch.Tensor:
     launch of the evaluation kernel in prediction mode on the GPU."""
     k = models[0].coefficientMatrix.shape[0]
     if hm.device.type == "cuda":
-        from ..ops import _native
         from ..ops.logreg import logreg_margins_native
 
-        if int(hm.dense.shape[1]) <= _native.kernels().logreg_max_dense():
-            KP = 8 if k <= 8 else 16
-            W = torch.cat([m.weight_table(KP).to(hm.device) for m in models])
-            m = logreg_margins_native(hm, W, k, len(models))[:, :, :k]
-            return torch.cat([-m, m], dim=2) if models[0].binomial else m
+        KP = 8 if k <= 8 else 16
+        W = torch.cat([m.weight_table(KP).to(hm.device) for m in models])
+        m = logreg_margins_native(hm, W, k, len(models))[:, :, :k]
+        return torch.cat([-m, m], dim=2) if models[0].binomial else m
     return torch.stack([mm.predict_raw(hm) for mm in models])
 
 

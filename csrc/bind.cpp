@@ -193,18 +193,10 @@ PYBIND11_MODULE(_har_native, m) {
     check(har_reduce_slabs(P<const float>(slabs), nslabs, n, P<float>(dst), S(stream)), "reduce_slabs");
   });
 
-  m.def("logreg_softmax_grad", [](u Z, int64_t n, int B, int K, int ld, u y, u rw, u inv_wsum, u R, u loss,
-                                  u stream) {
-    check(har_logreg_softmax_grad(P<const float>(Z), n, B, K, ld, P<const int32_t>(y), P<const float>(rw),
-                                  P<const float>(inv_wsum), P<float>(R), P<double>(loss), S(stream)),
-          "logreg_softmax_grad");
-  });
-
-  // ---- device logistic regression + batched L-BFGS / OWL-QN (logreg_qn.hip) ----
   m.def("logreg_eval_tiles", &har_logreg_eval_tiles);
-  m.def("logreg_max_dense", []() { return HAR_LOGREG_MAX_DENSE; });
   m.def("logreg_eval", [](u dense, int64_t ldd, int Fd, u dense_cols, u cat, int C, u y, u rw, u inv_wsum, u W,
-                          int64_t N, int F, int K, int T, int tstride, int mode, u R, u slab, int KP, int n_models,
+                          int64_t N, int F, int K, int T, int tstride, int model0, int mode, u R, u slab, int KP,
+                          int n_models,
                           u stream) {
     LogregEvalArgs a;
     a.dense = P<const float>(dense);
@@ -222,24 +214,23 @@ PYBIND11_MODULE(_har_native, m) {
     a.K = K;
     a.T = T;
     a.tstride = tstride;
+    a.model0 = model0;
     a.mode = mode;
     a.R = P<float>(R);
     a.slab = P<float>(slab);
     check(har_logreg_eval(&a, KP, n_models, S(stream)), "logreg_eval");
   });
-  m.def("logreg_grad", [](u slab, u R, u col_map, u csc_rows, u slice_lo, u col_slice, u blk_col, u blk_slice,
-                          int n_blocks, u inv_std, u pmask, int64_t N, int F, int Fd, int K, int T, int tstride,
-                          int ntiles, u G, u loss, int KP, int n_models, u stream) {
+  m.def("logreg_grad", [](u slab, u R, u col_map, u csc_rows, u csc_off, u col_slice, int SL, u inv_std, u pmask,
+                          int64_t N, int F, int Fd, int K, int T, int tstride, int model0, int ntiles, u G, u loss,
+                          u loss_fx, int KP, int n_models, u stream) {
     LogregGradArgs a;
     a.slab = P<const float>(slab);
     a.R = P<const float>(R);
     a.col_map = P<const int32_t>(col_map);
     a.csc_rows = P<const int32_t>(csc_rows);
-    a.slice_lo = P<const int32_t>(slice_lo);
+    a.csc_off = P<const int32_t>(csc_off);
     a.col_slice = P<const int32_t>(col_slice);
-    a.blk_col = P<const int32_t>(blk_col);
-    a.blk_slice = P<const int32_t>(blk_slice);
-    a.n_blocks = n_blocks;
+    a.SL = SL;
     a.inv_std = P<const float>(inv_std);
     a.pmask = P<const float>(pmask);
     a.N = N;
@@ -248,10 +239,65 @@ PYBIND11_MODULE(_har_native, m) {
     a.K = K;
     a.T = T;
     a.tstride = tstride;
+    a.model0 = model0;
     a.ntiles = ntiles;
     a.G = P<float>(G);
     a.loss = P<double>(loss);
+    a.loss_fx = P<float>(loss_fx);
     check(har_logreg_grad(&a, KP, n_models, S(stream)), "logreg_grad");
+  });
+  m.def("logreg_col_slices", [](u csc_off, int F, int SL, u col_slice, u stream) {
+    check(har_logreg_col_slices(P<const int32_t>(csc_off), F, SL, P<int32_t>(col_slice), S(stream)),
+          "logreg_col_slices");
+  });
+  m.def("logreg_summary_tiles", &har_logreg_summary_tiles);
+  m.def("logreg_summary", [](int phase, u dense, int64_t ldd, int Fd, u y, u rw, int64_t N, int F, int K, int nspec,
+                             u col_map, u csc_rows, u csc_off, u col_slice, int SL, int ntiles, u part, u summ,
+                             u stream) {
+    LogregSummaryArgs a;
+    a.dense = P<const float>(dense);
+    a.ldd = ldd;
+    a.Fd = Fd;
+    a.y = P<const int32_t>(y);
+    a.rw = P<const float>(rw);
+    a.N = N;
+    a.F = F;
+    a.K = K;
+    a.S = nspec;
+    a.col_map = P<const int32_t>(col_map);
+    a.csc_rows = P<const int32_t>(csc_rows);
+    a.csc_off = P<const int32_t>(csc_off);
+    a.col_slice = P<const int32_t>(col_slice);
+    a.SL = SL;
+    a.ntiles = ntiles;
+    a.part = P<double>(part);
+    a.summ = P<double>(summ);
+    check(har_logreg_summary(&a, phase, S(stream)), "logreg_summary");
+  });
+  m.def("logreg_prepare", [](u summ, u reg, u alpha, int B, int F, int K, int Kp, int standardization,
+                             int fit_intercept, int binomial, u inv_std, u inv_wsum, u pmask, u l2, u l1, u x0,
+                             u stream) {
+    LogregPrepareArgs a;
+    a.summ = P<const double>(summ);
+    a.reg = P<const float>(reg);
+    a.alpha = P<const float>(alpha);
+    a.B = B;
+    a.F = F;
+    a.K = K;
+    a.Kp = Kp;
+    a.standardization = standardization;
+    a.fit_intercept = fit_intercept;
+    a.binomial = binomial;
+    a.inv_std = P<float>(inv_std);
+    a.inv_wsum = P<float>(inv_wsum);
+    a.pmask = P<float>(pmask);
+    a.l2 = P<float>(l2);
+    a.l1 = P<float>(l1);
+    a.x0 = P<float>(x0);
+    check(har_logreg_prepare(&a, S(stream)), "logreg_prepare");
+  });
+  m.def("logreg_loss_decode", [](u fx, u loss, int n, u stream) {
+    check(har_logreg_loss_decode(P<const float>(fx), P<double>(loss), n, S(stream)), "logreg_loss_decode");
   });
   // one L-BFGS phase (logreg_qn.hip: 0 finalize + dots, 1 direction + trials, 2 pick + history,
   // 3 finalize only); the QnArgs fields come from a dict of ints / floats / device pointers

@@ -146,7 +146,6 @@ int har_roc_pr_sums(const float* sorted_scores, const float* labels, int64_t n, 
 
 // ---- logistic regression (batched over B models, K classes padded to 8) ----
 // ---- device logistic regression + batched L-BFGS / OWL-QN (logreg_qn.hip) ----
-#define HAR_LOGREG_MAX_DENSE 48
 typedef struct LogregEvalArgs {
   const float* dense;       // [N][ldd] dense feature columns (Fd used)
   int64_t ldd;
@@ -159,7 +158,8 @@ typedef struct LogregEvalArgs {
   const float* inv_wsum;    // [S]
   const float* W;           // [n_trial_models][F+1][KP] effective weights (row F = intercept)
   int64_t N;
-  int F, K, T, tstride;     // model bt = blockIdx.y * tstride, spec = bt / T
+  int F, K, T, tstride;     // model bt = model0 + blockIdx.y * tstride, spec = bt / T
+  int model0;               // first model of the launch (R holds one [N][KP] slot per launched model)
   int mode;                 // 0 = loss/gradient, 1 = margins into R
   float* R;                 // [n_trial_models][N][KP] residuals (mode 0, needed when C > 0) / margins
   float* slab;              // [n_trial_models][tiles][Fd*KP + KP + 1]
@@ -170,17 +170,17 @@ typedef struct LogregGradArgs {
   const float* R;
   const int32_t* col_map;   // [F+1]: >= 0 dense index, -1 intercept, <= -2 one-hot (CSC rows)
   const int32_t* csc_rows;  // row ids of the one-hot columns, column-major, ascending per column
-  const int32_t* slice_lo;  // [n_slices + 1] CSC range of every row slice (<= SL rows, one column each)
-  const int32_t* col_slice; // [F+2] first slice of each column
-  const int32_t* blk_col;   // [n_blocks + 1] column range of every workgroup (<= 256 columns)
-  const int32_t* blk_slice; // [n_blocks + 1] slice range of every workgroup (<= 256 slices)
-  int n_blocks;
+  const int32_t* csc_off;   // [F+2] CSC offsets of every column
+  const int32_t* col_slice; // [F+2] first row slice of each column (har_logreg_col_slices)
+  int SL;                   // rows per slice
   const float* inv_std;     // [S][F]
   const float* pmask;       // [S][K][F+1]
   int64_t N;
   int F, Fd, K, T, tstride, ntiles;
+  int model0;               // as LogregEvalArgs: model bt = model0 + blockIdx.y * tstride, R slot blockIdx.y
   float* G;                 // [n_trial_models][K][F+1]
-  double* loss;             // [n_trial_models]
+  double* loss;             // [n_trial_models] (loss_fx == null)
+  float* loss_fx;           // [n_trial_models][5] fixed-point loss pieces for the DP bucket, or null
 } LogregGradArgs;
 
 typedef struct QnArgs {
@@ -221,12 +221,48 @@ typedef struct QnArgs {
 int har_logreg_eval(const LogregEvalArgs* a, int KP, int n_models, hipStream_t s);
 int har_logreg_eval_tiles(int64_t n);
 int har_logreg_grad(const LogregGradArgs* a, int KP, int n_models, hipStream_t s);
+typedef struct LogregSummaryArgs {
+  const float* dense;       // [N][ldd] dense feature columns
+  int64_t ldd;
+  int Fd;
+  const int32_t* y;         // [N]
+  const float* rw;          // [S][N] row weights (null = 1)
+  int64_t N;
+  int F, K, S;
+  const int32_t* col_map;   // [F+1] (HybridMatrix.col_map)
+  const int32_t* csc_rows;
+  const int32_t* csc_off;   // [F+2]
+  const int32_t* col_slice; // [F+2] (har_logreg_col_slices)
+  int SL;
+  int ntiles;               // har_logreg_summary_tiles(N)
+  double* part;             // [S][ntiles][2 Fd + K + 1] tile partials
+  double* summ;             // [S][1 + 2F + K] (sum w, sum w x, sum w x^2, class sums)
+} LogregSummaryArgs;
+
+typedef struct LogregPrepareArgs {
+  const double* summ;       // [B][1 + 2F + K] (all-reduced in data-parallel fits)
+  const float* reg;         // [B] regParam
+  const float* alpha;       // [B] elasticNetParam
+  int B, F, K, Kp;
+  int standardization, fit_intercept, binomial;
+  float* inv_std;           // [B][F]
+  float* inv_wsum;          // [B]
+  float* pmask;             // [B][Kp][F+1]
+  float* l2;                // [B][Kp (F+1)]
+  float* l1;                // [B][Kp (F+1)] or null (no L1 term)
+  float* x0;                // [B][Kp][F+1]
+} LogregPrepareArgs;
+
+// phase 0: tile partials, phase 1: column sums
+int har_logreg_summary(const LogregSummaryArgs* a, int phase, hipStream_t s);
+int har_logreg_summary_tiles(int64_t n);
+int har_logreg_prepare(const LogregPrepareArgs* a, hipStream_t s);
+int har_logreg_col_slices(const int32_t* csc_off, int F, int SL, int32_t* col_slice, hipStream_t s);
+int har_logreg_loss_decode(const float* fx, double* loss, int n, hipStream_t s);
 int har_qn_chunks(int64_t D, int B);
 int har_lbfgs_phase(const QnArgs* a, int KP, int phase, hipStream_t s);
 
-int har_logreg_softmax_grad(const float* Z, int64_t n, int nmodels, int K, int ld, const int32_t* y,
-                            const float* rw, const float* inv_wsum, float* R, double* loss,
-                            hipStream_t s);
+
 
 // ---- windowed feature extraction over raw [S, A] streams ----
 // Training-input variant: bf16 ((isnan(v) ? nan_value : v) - mean) * inv_std rows, zero-padded to ld_out.

@@ -36,50 +36,65 @@ namespace {
 constexpr int EVAL_ROWS = 256;
 
 // ---------------------------------------------------------------------------------------------
-// logreg_eval: one workgroup = EVAL_ROWS rows x one (trial) model
+// logreg_eval: one workgroup = EVAL_ROWS rows x one (trial) model.  The dense columns go through
+// LDS in chunks of EVAL_DCH (any width: a 165-column 9-axis design or an un-one-hot numeric design
+// uses the same kernel as the 10 dense columns of the reference encoding): pass A accumulates the
+// margins chunk by chunk (column order = the order of one unchunked sweep), pass B re-stages the
+// chunks newest-first (the last one is still in LDS) for the tile's dense gradient R^T X.
 // ---------------------------------------------------------------------------------------------
+constexpr int EVAL_DCH = 32;                       // dense columns per LDS chunk
+constexpr int EVAL_XLD = EVAL_DCH + 1;             // odd row stride: conflict-free row reads
+
+template <int KP>
+__device__ __forceinline__ void eval_stage_chunk(const LogregEvalArgs& a, const float* W, float* wd, float* xs,
+                                                 int c0, int nc, int64_t r0, int64_t nrow_tile, bool weights) {
+  const int tid = threadIdx.x;
+  if (weights)
+    for (int e = tid; e < nc * KP; e += EVAL_ROWS) wd[e] = W[(int64_t)a.dense_cols[c0 + e / KP] * KP + (e % KP)];
+  for (int e = tid; e < EVAL_ROWS * nc; e += EVAL_ROWS) {
+    const int rr = e / nc, j = e % nc;
+    xs[rr * EVAL_XLD + j] = rr < nrow_tile ? a.dense[(r0 + rr) * a.ldd + c0 + j] : 0.f;
+  }
+}
+
 template <int KP>
 __global__ __launch_bounds__(EVAL_ROWS) void logreg_eval_kernel(LogregEvalArgs a) {
   extern __shared__ float smem[];
   const int Fd = a.Fd;
-  const int xs_ld = Fd | 1;                        // odd row stride: conflict-free row reads
-  float* wd = smem;                                // [Fd + 1][KP] dense weights + intercept
-  float* xs = wd + (Fd + 1) * KP;                  // [EVAL_ROWS][xs_ld]
-  float* rs = xs + EVAL_ROWS * xs_ld;              // [EVAL_ROWS][KP]
+  float* wd = smem;                                // [EVAL_DCH][KP] dense weights of the chunk
+  float* xs = wd + EVAL_DCH * KP;                  // [EVAL_ROWS][EVAL_XLD] dense row tile, one chunk
+  float* rs = xs + EVAL_ROWS * EVAL_XLD;           // [EVAL_ROWS][KP]
   float* red = rs + EVAL_ROWS * KP;                // [EVAL_ROWS / 64]
 
   const int tid = threadIdx.x;
-  const int bt = blockIdx.y * a.tstride;           // trial model
+  const int bt = a.model0 + blockIdx.y * a.tstride;  // trial model (its residual rows: R slot blockIdx.y)
   const int s = bt / a.T;                          // spec (row-weight vector) of the model
   const int64_t r0 = (int64_t)blockIdx.x * EVAL_ROWS;
   const int64_t row = r0 + tid;
   const bool ok = row < a.N;
   const float* W = a.W + (int64_t)bt * (a.F + 1) * KP;
-
-  // stage the dense weights (+ intercept row) and the dense row tile
-  for (int e = tid; e < Fd * KP; e += EVAL_ROWS) wd[e] = W[(int64_t)a.dense_cols[e / KP] * KP + (e % KP)];
-  if (tid < KP) wd[Fd * KP + tid] = W[(int64_t)a.F * KP + tid];
   const int64_t nrow_tile = min((int64_t)EVAL_ROWS, a.N - r0);
-  for (int64_t e = tid; e < nrow_tile * Fd; e += EVAL_ROWS) {
-    const int64_t rr = e / Fd, j = e % Fd;
-    xs[rr * xs_ld + j] = a.dense[(r0 + rr) * a.ldd + j];
-  }
-  for (int64_t e = nrow_tile * Fd + tid; e < (int64_t)EVAL_ROWS * Fd; e += EVAL_ROWS) {
-    const int64_t rr = e / Fd, j = e % Fd;
-    xs[rr * xs_ld + j] = 0.f;
-  }
-  __syncthreads();
+  const int nchunk = (Fd + EVAL_DCH - 1) / EVAL_DCH;
 
+  // ---- pass A: margins ----
   float z[KP];
 #pragma unroll
-  for (int k = 0; k < KP; ++k) z[k] = wd[Fd * KP + k];
+  for (int k = 0; k < KP; ++k) z[k] = W[(int64_t)a.F * KP + k];  // intercept row
+  for (int ch = 0; ch < nchunk; ++ch) {
+    const int c0 = ch * EVAL_DCH, nc = min(EVAL_DCH, Fd - c0);
+    if (ch) __syncthreads();                       // the previous chunk is consumed
+    eval_stage_chunk<KP>(a, W, wd, xs, c0, nc, r0, nrow_tile, true);
+    __syncthreads();
+    if (ok) {
+      for (int j = 0; j < nc; ++j) {
+        const float xv = xs[tid * EVAL_XLD + j];
+#pragma unroll
+        for (int k = 0; k < KP; ++k) z[k] = fmaf(xv, wd[j * KP + k], z[k]);
+      }
+    }
+  }
   float lossv = 0.f;
   if (ok) {
-    for (int j = 0; j < Fd; ++j) {
-      const float xv = xs[tid * xs_ld + j];
-#pragma unroll
-      for (int k = 0; k < KP; ++k) z[k] = fmaf(xv, wd[j * KP + k], z[k]);
-    }
     for (int c = 0; c < a.C; ++c) {
       const int col = a.cat[row * a.C + c];
       if (col >= 0) {
@@ -125,7 +140,7 @@ __global__ __launch_bounds__(EVAL_ROWS) void logreg_eval_kernel(LogregEvalArgs a
 #pragma unroll
   for (int k = 0; k < KP; ++k) rs[tid * KP + k] = rv[k];
   if (a.R != nullptr && ok) {
-    f32x4_t* rp = reinterpret_cast<f32x4_t*>(a.R + ((int64_t)bt * a.N + row) * KP);
+    f32x4_t* rp = reinterpret_cast<f32x4_t*>(a.R + ((int64_t)blockIdx.y * a.N + row) * KP);
 #pragma unroll
     for (int q = 0; q < KP / 4; ++q) rp[q] = f32x4_t{rv[4 * q], rv[4 * q + 1], rv[4 * q + 2], rv[4 * q + 3]};
   }
@@ -133,37 +148,78 @@ __global__ __launch_bounds__(EVAL_ROWS) void logreg_eval_kernel(LogregEvalArgs a
   // tile loss: wave sums, then the 4 wave partials in a fixed order
   lossv = wave_sum(lossv);
   if ((tid & 63) == 0) red[tid >> 6] = lossv;
-  __syncthreads();
+  __syncthreads();                                 // rs / red complete; the last chunk is in xs
   const int SW = Fd * KP + KP + 1;
   float* slab = a.slab + ((int64_t)bt * gridDim.x + blockIdx.x) * SW;
-  // dense gradient R^T X and intercept gradient sum R of the tile (fixed row order)
-  for (int o = tid; o < Fd * KP + KP; o += EVAL_ROWS) {
-    const int k = o % KP;
-    float acc = 0.f;
-    if (o < Fd * KP) {
-      const int j = o / KP;
-      for (int i = 0; i < EVAL_ROWS; ++i) acc = fmaf(rs[i * KP + k], xs[i * xs_ld + j], acc);
-    } else {
-      for (int i = 0; i < EVAL_ROWS; ++i) acc += rs[i * KP + k];
+  // ---- pass B: dense gradient R^T X of the tile, chunks newest-first (fixed row order) ----
+  for (int ch = nchunk - 1; ch >= 0; --ch) {
+    const int c0 = ch * EVAL_DCH, nc = min(EVAL_DCH, Fd - c0);
+    if (ch != nchunk - 1) {
+      __syncthreads();
+      eval_stage_chunk<KP>(a, W, wd, xs, c0, nc, r0, nrow_tile, false);
+      __syncthreads();
     }
-    slab[o] = acc;
+    for (int o = tid; o < nc * KP; o += EVAL_ROWS) {
+      const int j = o / KP, k = o % KP;
+      float acc = 0.f;
+      for (int i = 0; i < EVAL_ROWS; ++i) acc = fmaf(rs[i * KP + k], xs[i * EVAL_XLD + j], acc);
+      slab[(int64_t)c0 * KP + o] = acc;
+    }
+  }
+  // intercept gradient sum R of the tile
+  for (int k = tid; k < KP; k += EVAL_ROWS) {
+    float acc = 0.f;
+    for (int i = 0; i < EVAL_ROWS; ++i) acc += rs[i * KP + k];
+    slab[Fd * KP + k] = acc;
   }
   if (tid == 0) slab[SW - 1] = (red[0] + red[1]) + (red[2] + red[3]);
 }
 
 // ---------------------------------------------------------------------------------------------
-// logreg_grad: G[bt][k][col], loss[bt].  Workgroup w owns the column range
-// [blk_col[w], blk_col[w+1]) and the row SLICES of its one-hot columns [blk_slice[w],
-// blk_slice[w+1]) (<= 256 of each; a column's CSC row list is cut into slices of <= SL rows on
-// the host, so a frequent category — '?' in XPEAK, hundreds of rows — is spread over many lanes
-// instead of serializing one).  Phase 1: one lane per slice sums its rows' residuals into LDS;
-// phase 2: one lane per column sums its slices (or the tile slabs of a dense column / the
-// intercept) in order.  Fixed summation order everywhere: bitwise reproducible.
+// logreg_grad: G[bt][k][col], loss[bt].  Workgroup w owns the columns [256 w, 256 w + 256) and the
+// row SLICES of its one-hot columns: a column's CSC row list is cut into slices of a.SL rows
+// (col_slice = exclusive scan of ceil(rows / SL), built on the device by logreg_col_slices), so a
+// frequent category — '?' in XPEAK, hundreds of rows — is spread over many lanes instead of
+// serializing one.  The workgroup walks its slices in rounds of 256: one lane per slice sums its
+// rows' residuals into LDS, then one lane per column adds its slices of the round in order (or
+// the tile slabs of a dense column / the intercept).  Fixed summation order everywhere: bitwise
+// reproducible, and no host-side partition (the grid is ceil((F+1) / 256) x models).
 // ---------------------------------------------------------------------------------------------
+// Exact loss transport for the data-parallel bucket: a rank's fp64 loss as a 2^-40 fixed-point
+// int64 in four 16-bit pieces (three unsigned, the top one signed) carried as fp32 integers, plus
+// a non-finite flag.  The fp32 SUM all-reduce adds every piece exactly (|sum| < 2^24 for up to
+// 256 ranks), so the decoded total is the exact sum of the ranks' fixed-point losses: one
+// collective per evaluation carries the gradient AND a loss good to ~1e-12.
+constexpr double LOSS_FX = 1099511627776.0;  // 2^40
+
+__device__ __forceinline__ void loss_encode(double l, float* out) {
+  if (!(fabs(l) < 8388608.0)) {  // non-finite or out of range: flag it
+    out[0] = out[1] = out[2] = out[3] = 0.f;
+    out[4] = 1.f;
+    return;
+  }
+  long long q = llrint(l * LOSS_FX);
+  out[0] = (float)(q & 0xffff);
+  q >>= 16;
+  out[1] = (float)(q & 0xffff);
+  q >>= 16;
+  out[2] = (float)(q & 0xffff);
+  q >>= 16;
+  out[3] = (float)q;
+  out[4] = 0.f;
+}
+
+__device__ __forceinline__ double loss_decode(const float* in) {
+  if (in[4] != 0.f) return __builtin_nan("");
+  const long long q = (long long)in[0] + ((long long)in[1] << 16) + ((long long)in[2] << 32) +
+                      ((long long)in[3] << 48);
+  return (double)q / LOSS_FX;
+}
+
 template <int KP>
 __global__ __launch_bounds__(256) void logreg_grad_kernel(LogregGradArgs a) {
   __shared__ float part[256 * KP];
-  const int bt = blockIdx.y * a.tstride;
+  const int bt = a.model0 + blockIdx.y * a.tstride;
   const int s = bt / a.T;
   const int Fp1 = a.F + 1;
   const int SW = a.Fd * KP + KP + 1;
@@ -171,39 +227,58 @@ __global__ __launch_bounds__(256) void logreg_grad_kernel(LogregGradArgs a) {
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     double l = 0.0;
     for (int t = 0; t < a.ntiles; ++t) l += (double)slab[(int64_t)t * SW + SW - 1];
-    a.loss[bt] = l;
+    if (a.loss_fx)
+      loss_encode(l, a.loss_fx + (int64_t)bt * 5);
+    else
+      a.loss[bt] = l;
   }
-  const int s0 = a.blk_slice[blockIdx.x], s1 = a.blk_slice[blockIdx.x + 1];
-  const int c0 = a.blk_col[blockIdx.x], c1 = a.blk_col[blockIdx.x + 1];
-  const float* R = a.R + (int64_t)bt * a.N * KP;
-  if (threadIdx.x < s1 - s0) {
-    const int sl = s0 + threadIdx.x;
-    const int lo = a.slice_lo[sl], hi = a.slice_lo[sl + 1];
-    float g[KP];
-#pragma unroll
-    for (int k = 0; k < KP; ++k) g[k] = 0.f;
-#pragma unroll 4
-    for (int i = lo; i < hi; ++i) {
-      const f32x4_t* rp = reinterpret_cast<const f32x4_t*>(R + (int64_t)a.csc_rows[i] * KP);
-#pragma unroll
-      for (int q = 0; q < KP / 4; ++q) {
-        const f32x4_t r4 = rp[q];
-        g[4 * q + 0] += r4[0];
-        g[4 * q + 1] += r4[1];
-        g[4 * q + 2] += r4[2];
-        g[4 * q + 3] += r4[3];
-      }
-    }
-#pragma unroll
-    for (int k = 0; k < KP; ++k) part[threadIdx.x * KP + k] = g[k];
-  }
-  __syncthreads();
+  const int c0 = blockIdx.x * 256, c1 = min(Fp1, c0 + 256);
   const int col = c0 + threadIdx.x;
-  if (col >= c1) return;
-  const int cm = a.col_map[col];
+  const int s0 = a.col_slice[c0], s1 = a.col_slice[c1];
+  const int cs0 = col < c1 ? a.col_slice[col] : 0, cs1 = col < c1 ? a.col_slice[col + 1] : 0;
+  const float* R = a.R + (int64_t)blockIdx.y * a.N * KP;  // this launch's residual slot of the model
   float g[KP];
 #pragma unroll
   for (int k = 0; k < KP; ++k) g[k] = 0.f;
+  for (int base = s0; base < s1; base += 256) {
+    if (base > s0) __syncthreads();  // the previous round's partials are consumed
+    const int sl = base + threadIdx.x;
+    if (sl < s1) {
+      // the slice's column: the last column of the block whose first slice is <= sl
+      int lo = c0, hi = c1 - 1;
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (a.col_slice[mid] <= sl) lo = mid; else hi = mid - 1;
+      }
+      const int r0 = a.csc_off[lo] + (sl - a.col_slice[lo]) * a.SL;
+      const int r1 = min(r0 + a.SL, a.csc_off[lo + 1]);
+      float gs[KP];
+#pragma unroll
+      for (int k = 0; k < KP; ++k) gs[k] = 0.f;
+#pragma unroll 4
+      for (int i = r0; i < r1; ++i) {
+        const f32x4_t* rp = reinterpret_cast<const f32x4_t*>(R + (int64_t)a.csc_rows[i] * KP);
+#pragma unroll
+        for (int q = 0; q < KP / 4; ++q) {
+          const f32x4_t r4 = rp[q];
+          gs[4 * q + 0] += r4[0];
+          gs[4 * q + 1] += r4[1];
+          gs[4 * q + 2] += r4[2];
+          gs[4 * q + 3] += r4[3];
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < KP; ++k) part[threadIdx.x * KP + k] = gs[k];
+    }
+    __syncthreads();
+    const int e0 = max(cs0, base), e1 = min(cs1, base + 256);
+    for (int e = e0; e < e1; ++e) {  // this column's slices of the round, in order
+#pragma unroll
+      for (int k = 0; k < KP; ++k) g[k] += part[(e - base) * KP + k];
+    }
+  }
+  if (col >= c1) return;
+  const int cm = a.col_map[col];
   if (cm >= 0 || cm == -1) {  // dense column j = cm, or the intercept (slab entries after the dense block)
     const int off = cm >= 0 ? cm * KP : a.Fd * KP;
     for (int t = 0; t < a.ntiles; ++t) {
@@ -211,17 +286,48 @@ __global__ __launch_bounds__(256) void logreg_grad_kernel(LogregGradArgs a) {
 #pragma unroll
       for (int k = 0; k < KP; ++k) g[k] += p[k];
     }
-  } else {  // one-hot column: its slices, in row order
-    for (int sl = a.col_slice[col]; sl < a.col_slice[col + 1]; ++sl) {
-#pragma unroll
-      for (int k = 0; k < KP; ++k) g[k] += part[(sl - s0) * KP + k];
-    }
   }
   const float sc = col < a.F ? a.inv_std[(int64_t)s * a.F + col] : 1.f;
   const int64_t D = (int64_t)a.K * Fp1;
   float* G = a.G + (int64_t)bt * D;
   const float* pm = a.pmask + (int64_t)s * D;
   for (int k = 0; k < a.K; ++k) G[(int64_t)k * Fp1 + col] = g[k] * sc * pm[(int64_t)k * Fp1 + col];
+}
+
+// after the data-parallel all-reduce of the bucket: the summed fixed-point losses -> fp64
+__global__ void logreg_loss_decode_kernel(const float* __restrict__ fx, double* __restrict__ loss, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) loss[i] = loss_decode(fx + (int64_t)i * 5);
+}
+
+// col_slice [F+2] = exclusive scan over the F+1 columns of ceil((csc_off[c+1] - csc_off[c]) / SL):
+// one 1024-thread workgroup, chunked block scan (integer: exact)
+__global__ __launch_bounds__(1024) void logreg_col_slices_kernel(const int32_t* __restrict__ off, int F1, int SL,
+                                                                 int32_t* __restrict__ col_slice) {
+  __shared__ int wsum[16];
+  __shared__ int carry;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  if (tid == 0) carry = 0;
+  __syncthreads();
+  for (int base = 0; base < F1; base += 1024) {
+    const int c = base + tid;
+    const int n = c < F1 ? (off[c + 1] - off[c] + SL - 1) / SL : 0;
+    int v = n;  // inclusive wave scan
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int t = __shfl_up(v, o, 64);
+      if (lane >= o) v += t;
+    }
+    if (lane == 63) wsum[w] = v;
+    __syncthreads();
+    int pre = carry;
+    for (int i = 0; i < w; ++i) pre += wsum[i];
+    if (c < F1) col_slice[c] = pre + v - n;
+    __syncthreads();
+    if (tid == 1023) carry = pre + v;
+    __syncthreads();
+  }
+  if (tid == 0) col_slice[F1] = carry;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -639,12 +745,12 @@ __global__ __launch_bounds__(QN_BLOCK) void qn_update_kernel(QnArgs a) {
 
 extern "C" int har_logreg_eval(const LogregEvalArgs* args, int KP, int n_models, hipStream_t s) {
   const LogregEvalArgs& a = *args;
-  if (a.Fd < 0 || a.Fd > HAR_LOGREG_MAX_DENSE || a.K < 1 || a.K > KP || (KP != 8 && KP != 16) || a.T < 1 ||
+  if (a.Fd < 0 || a.K < 1 || a.K > KP || (KP != 8 && KP != 16) || a.T < 1 ||
       a.tstride < 1 || (a.mode == 0 && a.slab == nullptr) || (a.C > 0 && a.cat == nullptr))
     return -2;
   if (a.N == 0 || n_models == 0) return 0;
   const int tiles = (int)((a.N + EVAL_ROWS - 1) / EVAL_ROWS);
-  const size_t lds = sizeof(float) * ((a.Fd + 1) * KP + EVAL_ROWS * (a.Fd | 1) + EVAL_ROWS * KP + EVAL_ROWS / 64);
+  const size_t lds = sizeof(float) * (EVAL_DCH * KP + EVAL_ROWS * EVAL_XLD + EVAL_ROWS * KP + EVAL_ROWS / 64);
   dim3 grid(tiles, n_models);
   if (KP == 8)
     logreg_eval_kernel<8><<<grid, EVAL_ROWS, lds, s>>>(a);
@@ -658,15 +764,29 @@ extern "C" int har_logreg_eval_tiles(int64_t n) { return (int)((n + EVAL_ROWS - 
 
 extern "C" int har_logreg_grad(const LogregGradArgs* args, int KP, int n_models, hipStream_t s) {
   const LogregGradArgs& a = *args;
-  if (a.K < 1 || a.K > KP || (KP != 8 && KP != 16) || a.T < 1 || a.tstride < 1 || a.n_blocks < 1 ||
-      a.blk_col == nullptr || a.blk_slice == nullptr || a.col_slice == nullptr || a.slice_lo == nullptr)
+  if (a.K < 1 || a.K > KP || (KP != 8 && KP != 16) || a.T < 1 || a.tstride < 1 || a.SL < 1 ||
+      a.col_slice == nullptr || a.csc_off == nullptr || (a.loss == nullptr && a.loss_fx == nullptr))
     return -2;
   if (n_models == 0) return 0;
-  dim3 grid(a.n_blocks, n_models);
+  dim3 grid((a.F + 1 + 255) / 256, n_models);
   if (KP == 8)
     logreg_grad_kernel<8><<<grid, 256, 0, s>>>(a);
   else
     logreg_grad_kernel<16><<<grid, 256, 0, s>>>(a);
+  HAR_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int har_logreg_col_slices(const int32_t* csc_off, int F, int SL, int32_t* col_slice, hipStream_t s) {
+  if (F < 0 || SL < 1) return -2;
+  logreg_col_slices_kernel<<<1, 1024, 0, s>>>(csc_off, F + 1, SL, col_slice);
+  HAR_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int har_logreg_loss_decode(const float* fx, double* loss, int n, hipStream_t s) {
+  if (n <= 0) return n < 0 ? -2 : 0;
+  logreg_loss_decode_kernel<<<(n + 255) / 256, 256, 0, s>>>(fx, loss, n);
   HAR_CHECK_LAUNCH();
   return 0;
 }

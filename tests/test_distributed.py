@@ -41,11 +41,25 @@ def _worker(rank, world, port, out_dir, what):
     X, y = _data()
     Xs, ys, off = dp.shard(X, y, ctx)
     if what == "lr":
+        import torch.distributed as tdist
+
         from har.models.logreg import FitSpec, LogisticRegression
 
-        ms = dp.fit_logreg_dp(LogisticRegression(maxIter=15), Xs, ys,
-                              [FitSpec(None, 0.1, 0.0), FitSpec(None, 0.05, 0.3)], 4, ctx)
+        n_coll = [0]
+        real = tdist.all_reduce
+
+        def counting(*a, **kw):  # every collective of the fit goes through all_reduce
+            n_coll[0] += 1
+            return real(*a, **kw)
+
+        tdist.all_reduce = counting
+        try:
+            ms = dp.fit_logreg_dp(LogisticRegression(maxIter=15), Xs, ys,
+                                  [FitSpec(None, 0.1, 0.0), FitSpec(None, 0.05, 0.3)], 4, ctx)
+        finally:
+            tdist.all_reduce = real
         res = torch.stack([m.coefficientMatrix for m in ms])
+        torch.save(torch.tensor([n_coll[0], ms[0].summary["n_evals"]]), os.path.join(out_dir, f"lrcoll_{rank}.pt"))
     elif what in ("rf", "rf_allreduce"):
         from har.models.tree import RandomForestClassifier
 
@@ -105,9 +119,14 @@ def _run(what, world=2):
 def test_dp_logreg_equals_single(world):
     from har.models.logreg import FitSpec, LogisticRegression
 
-    outs = _run("lr", world)
+    d = tempfile.mkdtemp()
+    mp.spawn(_worker, args=(world, _free_port(), d, "lr"), nprocs=world, join=True)
+    outs = [torch.load(os.path.join(d, f"lr_{r}.pt"), weights_only=True) for r in range(world)]
     for o in outs[1:]:
         torch.testing.assert_close(outs[0], o)
+    for r in range(world):  # ONE all-reduce per objective evaluation (+ the summarizer's)
+        n_coll, n_evals = torch.load(os.path.join(d, f"lrcoll_{r}.pt"), weights_only=True).tolist()
+        assert n_evals > 5 and n_coll == n_evals + 1, (n_coll, n_evals)
     X, y = _data()
     ms = LogisticRegression(maxIter=15).fit_many(X, y, [FitSpec(None, 0.1, 0.0), FitSpec(None, 0.05, 0.3)], 4)
     torch.testing.assert_close(outs[0], torch.stack([m.coefficientMatrix for m in ms]), rtol=1e-3, atol=1e-4)

@@ -219,23 +219,35 @@ def test_mlp_step_matches_torch(cuda):
     assert abs(lsum - float(ref_loss)) / float(ref_loss) < 1e-2
 
 
-def test_logreg_objective_native_vs_torch(cuda):
-    from har.ops.logreg import LogregWorkspace, logreg_loss_grad_native, logreg_loss_grad_torch
+def test_logreg_wide_dense_eval_vs_torch(cuda):
+    """The LR evaluation + gradient kernels on a wide all-dense design (124 columns: four LDS chunks,
+    the last one partial) vs the fp64 torch objective, several row-weighted trial models."""
+    from har.features.hybrid import from_dense
+    from har.ops.logreg import DeviceLogregSolver, LogregDesign
 
-    N, F, B, K = 777, 124, 5, 6
-    g = torch.Generator(device=cuda).manual_seed(4)
-    X = torch.randn(N, F, device=cuda, generator=g)
-    y = torch.randint(0, K, (N,), device=cuda, generator=g)
-    W = torch.randn(B, K, F, device=cuda, generator=g) * 0.1
-    b = torch.randn(B, K, device=cuda, generator=g)
-    rw = (torch.rand(B, N, device=cuda, generator=g) > 0.2).float()
-    inv = 1.0 / rw.sum(1)
-    ws = LogregWorkspace(X, B, K)
-    l1, g1, b1 = logreg_loss_grad_native(X, y.to(torch.int32), W, b, rw, inv, ws)
-    l2, g2, b2 = logreg_loss_grad_torch(X.double(), y, W.double(), b.double(), rw.double(), inv.double())
-    torch.testing.assert_close(l1.double(), l2, rtol=1e-5, atol=1e-5)
-    torch.testing.assert_close(g1.double(), g2, rtol=1e-4, atol=1e-5)
-    torch.testing.assert_close(b1.double(), b2, rtol=1e-4, atol=1e-5)
+    N, F, S, T, K = 777, 124, 2, 3, 6
+    g = torch.Generator().manual_seed(4)
+    X = torch.randn(N, F, generator=g)
+    y = torch.randint(0, K, (N,), generator=g)
+    hm = from_dense(X.to(cuda), [])
+    rw = (torch.rand(S, N, generator=g) > 0.2).float().to(cuda)
+    design = LogregDesign(hm, y.to(cuda), rw, K)
+    inv_std = (torch.rand(S, F, generator=g) + 0.5).to(cuda)
+    pmask = torch.ones(S, K, F + 1, device=cuda)
+    inv_wsum = 1.0 / rw.sum(1)
+    D = K * (F + 1)
+    solver = DeviceLogregSolver(design, S, T, 4, inv_std, pmask, inv_wsum, torch.zeros(S, D, device=cuda), None, 1,
+                                1e-6)
+    xt = torch.randn(S * T, K, F + 1, generator=g).to(cuda) * 0.1
+    spec = torch.arange(S * T, device=cuda) // T
+    solver.weff.zero_()
+    solver.weff[:, :F, :K] = (xt[:, :, :F] * inv_std[spec][:, None, :]).transpose(1, 2)
+    solver.weff[:, F, :K] = xt[:, :, F]
+    solver._evaluate(1)
+    ref_loss, ref_G = LogregDesign(hm, y.to(cuda), rw.double(), K).eval_torch(
+        xt.double(), T, inv_std.double(), pmask.double(), inv_wsum.double())
+    torch.testing.assert_close(solver.loss, ref_loss, rtol=2e-5, atol=1e-6)
+    torch.testing.assert_close(solver.G.double(), ref_G, rtol=2e-4, atol=2e-6)
 
 
 def test_metrics_kernels(cuda):

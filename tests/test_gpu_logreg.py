@@ -132,3 +132,48 @@ def test_wisdm_reference_lr_and_cv_on_device(cuda, wisdm_csv):
                         evaluator=RegressionEvaluator(metricName="mae"), numFolds=5, seed=2018).fit(tr)
     acc_cv = float((cv.bestModel.predict(cv.bestModel.features_input(te)) == yt).float().mean())
     assert acc_cv >= 0.70 and len(cv.avgMetrics) == 9
+
+
+def test_device_solver_wide_dense_165(cuda):
+    """A 165-column all-dense design (the 9-axis feature width) on the device solver — no width cap,
+    no host-synced fallback — against the torch algorithm (minimize_trials) on the same data."""
+    from har.features.hybrid import from_dense
+    from har.models.logreg import FitSpec, LogisticRegression
+
+    g = torch.Generator().manual_seed(11)
+    N, F, K = 3000, 165, 12
+    mu = torch.randn(K, F, generator=g) * 0.4
+    y = torch.randint(0, K, (N,), generator=g)
+    X = mu[y] + torch.randn(N, F, generator=g)
+    est = LogisticRegression(maxIter=25, regParam=0.01)
+    specs = [FitSpec(None, 0.01, 0.0), FitSpec((torch.arange(N) % 4 != 0).float(), 0.02, 0.3)]
+    cpu = est.fit_many(X, y, specs, K)
+    hm = from_dense(X.to(cuda), [])
+    gpu = est.fit_many(hm, y.to(cuda), [FitSpec(None if s.row_weight is None else s.row_weight.to(cuda),
+                                                 s.regParam, s.elasticNetParam) for s in specs], K)
+    for c, gm in zip(cpu, gpu):
+        assert abs(c.summary["objective"] - gm.summary["objective"]) <= 2e-4 * max(1.0, abs(c.summary["objective"]))
+        agree = (c.predict(X) == gm.predict(hm).cpu()).float().mean()
+        assert agree > 0.99
+        assert isinstance(gm.summary["objectiveHistory"], list) and len(gm.summary["objectiveHistory"]) >= 2
+
+
+def test_device_setup_matches_torch(cuda):
+    """The device summarizer + prepare kernels (logreg_setup.hip) == the torch setup: standardization,
+    masks, regularization vectors and the initial point, for weighted and unweighted specs."""
+    from har.models.logreg import FitSpec, LogisticRegression
+
+    X, y, hm = _hybrid_problem(cuda, N=1800, seed=12)
+    specs = [FitSpec(None, 0.1, 0.0), FitSpec((torch.arange(1800) % 3 != 0).float(), 0.3, 0.2)]
+    est = LogisticRegression()
+    from har.features.hybrid import from_dense
+
+    hm_cpu = from_dense(X, list(hm.blocks))
+    c = est._setup(hm_cpu, y, specs, 6, None)
+    g = est._setup(hm, y.to(cuda), [FitSpec(None if s.row_weight is None else s.row_weight.to(cuda), s.regParam,
+                                            s.elasticNetParam) for s in specs], 6, None)
+    torch.testing.assert_close(g[0].summary().cpu()[:1].expand(2, -1) if g[0].S == 1 else g[0].summary().cpu(),
+                               c[0].summary(), rtol=1e-12, atol=1e-9)
+    for i in (3, 4, 5, 6, 8):  # inv_std, inv_wsum, pmask, l2v, x0
+        torch.testing.assert_close(g[i].cpu().reshape(c[i].shape), c[i], rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(g[7].cpu(), c[7], rtol=1e-5, atol=1e-6)  # l1v
