@@ -12,12 +12,13 @@ Engine layout (MI355X-first):
   buffer — so data-parallel training issues exactly one RCCL all-reduce per step
   (the whole gradient is ~0.3 MB: latency-bound on xGMI, so one bucket);
 * one training step of the 2-hidden-layer (H = 256) network = THREE kernels
-  (mlp_fused.hip, mlp.hip): fused forward (layer 1, layer 2, softmax-CE head, dlogits,
-  dact2, dWout / dbout / db1 partials; h2 and the logits never leave the CU) ->
-  fused backward (dW1, dgrad, relu', dW0 / db0 in one pass over dact2 / h1 / X; dact1
-  never leaves the CU) -> one deterministic gradient reduction with Adam fused in
-  (N > 1: the reduction stores G, ONE RCCL all-reduce, then Adam from G).  Other
-  shapes run the same math as split-K MFMA GEMMs (gemm.hip) + the fused head.
+  (mlp_step.hip, mlp.hip): the forward (layer 1, layer 2, softmax-CE head, dWout / dbout
+  partials; h1, h2 and the logits never leave the CU) writes only the logit gradients dz
+  and the relu' bits of h2 (64 B per row) -> the backward rebuilds dact2 and h1 on chip
+  and does dW1, dgrad, relu', dW0 / db0 / db1 in one pass (dact1 never leaves the CU) ->
+  one deterministic gradient reduction with Adam fused in (N > 1: the reduction stores
+  G, ONE RCCL all-reduce, then Adam from G).  Other shapes run the fused forward
+  (mlp_fused.hip) + split-K MFMA GEMMs (gemm.hip).
   No host synchronization inside a step; the loss and correct-count accumulators are
   read only when asked for;
 * input rows are kept resident in HBM as padded bf16 ([N, F_pad]); a step reads a
@@ -42,10 +43,6 @@ from .base import ClassificationModel, ClassifierParams, Estimator, dp_allreduce
     features_tensor, labels_tensor, new_uid, resolve_device
 
 HEAD_PAD = 32  # classes padded to 32 rows (two 16-wide MFMA column tiles)
-# The fused backward recomputes h1 = relu(W0 x + b0) from the X tiles it reads anyway (bit-identical
-# to the forward's h1) instead of the forward writing and the backward reading B x 256 bf16 through
-# HBM; HAR_MLP_RECOMPUTE_H1=0 restores the stored h1 (A/B switch).
-RECOMPUTE_H1 = os.environ.get("HAR_MLP_RECOMPUTE_H1", "1") != "0"
 
 
 def _pad(x: int, m: int) -> int:
@@ -177,8 +174,8 @@ class MLPEngine:
             # <= n_splits slices and writes plain partial tiles into slab z of a
             # [n_splits, total] workspace laid out like the flat parameter buffer.
             self.n_splits = n_splits_for(self.B)
-            # the fused backward (mlp_bwd_fused) writes one partial per row slice into the same slabs
-            n_slab = max(self.n_splits, _native.kernels().mlp_bwd_fused_slices(self.B))
+            # the step backward (mlp_step.hip) writes one partial per row slice into the same slabs
+            n_slab = max(self.n_splits, _native.kernels().mlp_step_slices(self.B))
             self.slabs = torch.zeros(n_slab, L.total, dtype=torch.float32, device=dev)
             # one-kernel forward + head + dWout (mlp_fused.hip) for the 2-hidden-layer shapes it covers
             self.fused_ok = (len(L.hidden) == 2 and L.hidden[0] == L.hidden[1] and L.hidden[0] in (128, 256)
@@ -186,17 +183,26 @@ class MLPEngine:
                              and os.environ.get("HAR_MLP_FUSED", "1") != "0")
             if self.fused_ok:
                 nwg = _native.kernels().mlp_fwd_head_grid(self.B)
-                H = L.hidden[-1]  # per workgroup: dWout rows 0..15 [16][H], dbout [16], db1 [H] (8-wave variant)
+                H = L.hidden[-1]  # per workgroup: dWout rows 0..15 [16][H], dbout [16] (+ an unused db1 slot)
                 self.fslab = torch.zeros(nwg, 16 * H + 16 + H, dtype=torch.float32, device=dev)
                 self.fblock_loss = torch.zeros(nwg, dtype=torch.float32, device=dev)
                 self.fblock_correct = torch.zeros(nwg, dtype=torch.int32, device=dev)
             self.last_fused = False
-            # fused backward (mlp_fused.hip mlp_bwd_fused): dW1, dgrad -> relu' -> dW0 / db0 in ONE pass
-            # over dact2 / h1 / X, dact1 never reaches HBM (H = 256, batch % 32, after the 8-wave
-            # forward, which supplies db1; HAR_MLP_BWD_FUSED=0 keeps the split-K GEMMs)
-            self.bwd_ok = (self.fused_ok and L.hidden[0] == 256
-                           and os.environ.get("HAR_MLP_BWD_FUSED", "1") != "0")
+            # the three-kernel step (mlp_step.hip: forward -> dz + relu' mask, backward rebuilding dact2
+            # and h1 on chip, then grad_reduce_adam) for H = 256 and batches % 64; HAR_MLP_STEP=0 keeps
+            # the fused forward + split-K GEMM backward (the reference path of the tests)
+            self.step_ok = (self.fused_ok and L.hidden[0] == 256
+                            and os.environ.get("HAR_MLP_STEP", "1") != "0")
+            if self.step_ok:
+                mod = _native.kernels()
+                nwg = mod.mlp_step_grid(self.B)
+                self.sslab = torch.zeros(nwg, mod.mlp_step_fwd_slab_width(256), dtype=torch.float32, device=dev)
+                self.sblock_loss = torch.zeros(nwg, dtype=torch.float32, device=dev)
+                self.sblock_correct = torch.zeros(nwg, dtype=torch.int32, device=dev)
+                self.dz = torch.zeros(self.B * 8, dtype=torch.int32, device=dev)      # 16 bf16 per row
+                self.h2mask = torch.zeros(self.B * 8, dtype=torch.int32, device=dev)  # 256 bits per row
             self.last_bwd = False
+            self.last_path = None
             # optional: the two backward branches after the fused forward — dW1 (split-K over the
             # batch) and dgrad -> dW0 — are independent, so HAR_MLP_STREAMS=1 runs dW1 on a second
             # HIP stream (fork/join with events; graph-capturable).  Measured on MI355X at batch
@@ -229,10 +235,13 @@ class MLPEngine:
         total = L.total
         nh = len(L.hidden)
         acts = [Xb] + [a[:B] for a in self.acts[1:]]
+        if self.step_ok and B % 64 == 0:
+            return self._step(Xb, y32, scale, on_grad, _record)
         if self.fused_ok and B % 16 == 0:
             return self._forward_backward_fused(Xb, y32, scale, on_grad, ks, acts, _record)
         self.last_fused = False
         self.last_bwd = False
+        self.last_path = "gemm"
         for i in range(nh):
             gemm_bf16(acts[i], self._w(self.Pb, f"W{i}"), acts[i + 1], M=B, N=self.dims[i + 1], K=self.dims[i],
                       layout=0, epi=EPI_BIAS_RELU, bias=self._w(self.P, f"b{i}"),
@@ -269,56 +278,73 @@ class MLPEngine:
                           mask=acts[i], tile=dgrad_tile(B, hp, h))
                 dact = prev
 
+    def _step(self, Xb, y32, scale, on_grad, record=None):
+        """The three-kernel step of the H = 256 network (mlp_step.hip): mlp_step_fwd (layer 1, layer 2,
+        softmax-CE head, dWout / dbout; writes only dz and the relu' mask of h2), mlp_step_bwd (dact2
+        rebuilt from them, h1 recomputed, dW1 + dgrad + relu' + dW0 / db0 / db1 in one pass).  The
+        gradient reduction + Adam follow in ``train_step``.  ``record`` (a list) receives one
+        re-launchable closure per kernel (tools/mlp_phase_probe.py)."""
+        L, mod, s = self.layout, _native.kernels(), _native.stream_ptr()
+        B, H, K0 = Xb.shape[0], self.dims[-1], L.in_pad
+        total = L.total
+        self.step_nwg = mod.mlp_step_grid(B)
+        self.step_S = mod.mlp_step_slices(B)
+        P, Pb, sb = self.P, self.Pb, self.slabs.data_ptr()
+        w = lambda t, n: self._w(t, n).data_ptr()  # noqa: E731
+
+        def fwd():
+            mod.mlp_step_fwd(Xb.data_ptr(), K0, w(Pb, "W0"), w(P, "b0"), w(Pb, "W1"), w(P, "b1"), H, w(Pb, "Wout"),
+                             w(P, "bout"), y32.data_ptr(), B, L.num_classes, float(scale), self.dz.data_ptr(),
+                             self.h2mask.data_ptr(), self.sslab.data_ptr(), self.sblock_loss.data_ptr(),
+                             self.sblock_correct.data_ptr(), s)
+
+        def bwd():
+            off = lambda n: sb + 4 * L.by_name[n].offset  # noqa: E731
+            mod.mlp_step_bwd(self.dz.data_ptr(), self.h2mask.data_ptr(), Xb.data_ptr(), K0, w(Pb, "W1"), H,
+                             w(Pb, "W0"), w(P, "b0"), w(Pb, "Wout"), B, off("W1"), off("W0"), off("b0"), off("b1"),
+                             total, self.step_count.data_ptr(), s)
+
+        fwd()
+        if on_grad is not None:
+            on_grad("Wout")
+        bwd()
+        if on_grad is not None:
+            on_grad("W1")
+            on_grad("W0")
+        if record is not None:
+            record += [fwd, bwd]
+        self.last_fused = self.last_bwd = True
+        self.last_path = "step"
+        self.last_batch = B
+
     def _forward_backward_fused(self, Xb, y32, scale, on_grad, ks, acts, record=None):
-        """2-hidden-layer step: ONE kernel for fwd L1 + fwd L2 + head + dWout/dbout (+ db1) (h2 and
-        the logit gradients stay on chip), then ONE kernel for dW1 + dgrad + dW0 / db0 (H = 256),
-        or dW1, dgrad and dW0 as split-K MFMA GEMMs.  ``record`` (a list) receives one re-launchable
-        closure per kernel (tools/mlp_phase_probe.py)."""
+        """2-hidden-layer step of the shapes the three-kernel step does not take (H = 128, or a batch
+        that is not a multiple of 64): ONE kernel for fwd L1 + fwd L2 + head + dWout/dbout (h2 and
+        the logit gradients stay on chip; h1 and dact2 are written), then dW1, dgrad and dW0 as
+        split-K MFMA GEMMs."""
         L, mod, s = self.layout, _native.kernels(), _native.stream_ptr()
         B, H, K0 = Xb.shape[0], self.dims[-1], L.in_pad
         total = L.total
         h1 = acts[1]
         dact = self.dbuf[1][: B * H].view(B, H)
         self.fused_nwg = mod.mlp_fwd_head_grid(B)
-        self.last_bwd = self.bwd_ok and B % 64 == 0 and mod.mlp_fwd_head_variant(H, B) == 2
-        # with the fused backward, h1 never reaches HBM: that kernel recomputes it from X (same bits)
-        rh1 = self.last_bwd and RECOMPUTE_H1
 
         def fwd():
             mod.mlp_fwd_head(Xb.data_ptr(), K0, self._w(self.Pb, "W0").data_ptr(), self._w(self.P, "b0").data_ptr(),
                              self._w(self.Pb, "W1").data_ptr(), self._w(self.P, "b1").data_ptr(), H,
                              self._w(self.Pb, "Wout").data_ptr(), self._w(self.P, "bout").data_ptr(),
-                             y32.data_ptr(), B, L.num_classes, float(scale), 0 if rh1 else h1.data_ptr(),
-                             dact.data_ptr(), self.fslab.data_ptr(), self.fblock_loss.data_ptr(),
-                             self.fblock_correct.data_ptr(), s)
+                             y32.data_ptr(), B, L.num_classes, float(scale), h1.data_ptr(), dact.data_ptr(),
+                             self.fslab.data_ptr(), self.fblock_loss.data_ptr(), self.fblock_correct.data_ptr(), s)
 
         fwd()
         if record is not None:
             record.append(fwd)
         self.last_fused = True
+        self.last_bwd = False
+        self.last_path = "fused_fwd"
         self.last_batch = B
         if on_grad is not None:
             on_grad("Wout")
-
-        if self.last_bwd:
-            # dW1 + dgrad + relu' + dW0 / db0: one kernel, one partial per row slice in self.slabs
-            self.bwd_S = mod.mlp_bwd_fused_slices(B)
-            sb = self.slabs.data_ptr()
-
-            def bwd():
-                mod.mlp_bwd_fused(dact.data_ptr(), 0 if rh1 else h1.data_ptr(), Xb.data_ptr(), K0,
-                                  self._w(self.Pb, "W1").data_ptr(), H, B, sb + 4 * L.by_name["W1"].offset,
-                                  sb + 4 * L.by_name["W0"].offset, sb + 4 * L.by_name["b0"].offset, total,
-                                  self.step_count.data_ptr(), self._w(self.Pb, "W0").data_ptr(),
-                                  self._w(self.P, "b0").data_ptr(), s)
-
-            bwd()
-            if record is not None:
-                record.append(bwd)
-            if on_grad is not None:
-                on_grad("W1")
-                on_grad("W0")
-            return
 
         def dw1():
             gemm_bf16(dact, h1, self._slab("W1"), M=H, N=H, K=B, layout=3, epi=EPI_F32_SLAB, k_split=ks, ldc=H,
@@ -368,23 +394,25 @@ class MLPEngine:
 
     def _grad_regions(self):
         """Sources of the flat gradient after the last native batch, in flat order: (start, end,
-        pointer of slab 0 at start, #slabs, slab stride) — the split-K GEMM slabs or the fused
-        backward's per-slice partials, and after a fused step the forward kernel's per-workgroup
-        slabs (dWout / dbout, and db1 when the fused backward ran)."""
+        pointer of slab 0 at start, #slabs, slab stride) — the step backward's per-slice partials
+        (W0, b0, W1, b1) and the step forward's per-workgroup dWout / dbout slabs, or the split-K
+        GEMM slabs (+ the fused forward's dWout / dbout slabs)."""
         L, total = self.layout, self.layout.total
         regions = []
-        fs = self.fslab.data_ptr() if self.last_fused else 0
-        if self.last_bwd:
-            H = self.dims[-1]
+        wo, bo = L.by_name["Wout"].offset, L.by_name["bout"].offset
+        if self.last_path == "step":
+            H, w = self.dims[-1], self.sslab.shape[1]
             w0, b1 = L.by_name["W0"].offset, L.by_name["b1"].offset
-            regions.append((w0, b1, self.slabs.data_ptr() + 4 * w0, self.bwd_S, total))  # W0, b0, W1
-            regions.append((b1, b1 + H, fs + 4 * (16 * H + 16), self.fused_nwg, self.fslab.shape[1]))
-        else:
-            end = L.by_name["Wout"].offset if self.last_fused else total
-            regions.append((0, end, self.slabs.data_ptr(), self.active_splits, total))
+            fs = self.sslab.data_ptr()
+            regions.append((w0, b1 + H, self.slabs.data_ptr() + 4 * w0, self.step_S, total))  # W0, b0, W1, b1
+            regions.append((wo, wo + 16 * H, fs, self.step_nwg, w))
+            regions.append((bo, bo + 16, fs + 4 * 16 * H, self.step_nwg, w))
+            return regions
+        end = wo if self.last_fused else total
+        regions.append((0, end, self.slabs.data_ptr(), self.active_splits, total))
         if self.last_fused:
             H, w = self.dims[-1], self.fslab.shape[1]
-            wo, bo = L.by_name["Wout"].offset, L.by_name["bout"].offset
+            fs = self.fslab.data_ptr()
             regions.append((wo, wo + 16 * H, fs, self.fused_nwg, w))
             regions.append((bo, bo + 16, fs + 4 * 16 * H, self.fused_nwg, w))
         return regions
@@ -466,6 +494,9 @@ class MLPEngine:
 
     def last_loss_and_correct(self):
         """(sum of CE, #correct) of the last native batch — one host sync."""
+        if self.last_path == "step":
+            n = self.step_nwg
+            return float(self.sblock_loss[:n].sum().item()), int(self.sblock_correct[:n].sum().item())
         if self.last_fused:
             n = self.fused_nwg
             return float(self.fblock_loss[:n].sum().item()), int(self.fblock_correct[:n].sum().item())

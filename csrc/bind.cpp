@@ -449,15 +449,25 @@ PYBIND11_MODULE(_har_native, m) {
   });
   m.def("head_fused_blocks", &har_head_fused_blocks);
   m.def("mlp_fwd_head_grid", &har_mlp_fwd_head_grid);
-  m.def("mlp_bwd_fused_slices", &har_mlp_bwd_fused_slices);
-  m.def("mlp_fwd_head_variant", &har_mlp_fwd_head_variant);
   m.def("mlp_set_stamps", [](u p) { har_mlp_set_stamps(P<uint64_t>(p)); });
-  m.def("mlp_bwd_fused", [](u dact2, u h1, u X, int K0, u W1, int H, int B, u gw1, u gw0, u gb0, int64_t stride,
-                            u tick, u W0, u b0, u stream) {
-    check(har_mlp_bwd_fused(P<const uint16_t>(dact2), P<const uint16_t>(h1), P<const uint16_t>(X), K0,
-                            P<const uint16_t>(W1), H, B, P<float>(gw1), P<float>(gw0), P<float>(gb0), stride,
-                            P<int32_t>(tick), P<const uint16_t>(W0), P<const float>(b0), S(stream)),
-          "mlp_bwd_fused");
+  m.def("mlp_step_grid", &har_mlp_step_grid);
+  m.def("mlp_step_slices", &har_mlp_step_slices);
+  m.def("mlp_step_fwd_slab_width", &har_mlp_step_fwd_slab_width);
+  m.def("mlp_step_fwd", [](u X, int K0, u W0, u b0, u W1, u b1, int H, u Wo, u bo, u labels, int B, int C,
+                           float scale, u dz, u mask, u slab, u block_loss, u block_correct, u stream) {
+    check(har_mlp_step_fwd(P<const uint16_t>(X), K0, P<const uint16_t>(W0), P<const float>(b0),
+                           P<const uint16_t>(W1), P<const float>(b1), H, P<const uint16_t>(Wo), P<const float>(bo),
+                           P<const int32_t>(labels), B, C, scale, P<uint32_t>(dz), P<uint32_t>(mask), P<float>(slab),
+                           P<float>(block_loss), P<int32_t>(block_correct), S(stream)),
+          "mlp_step_fwd");
+  });
+  m.def("mlp_step_bwd", [](u dz, u mask, u X, int K0, u W1, int H, u W0, u b0, u Wo, int B, u gw1, u gw0, u gb0,
+                           u gb1, int64_t stride, u tick, u stream) {
+    check(har_mlp_step_bwd(P<const uint32_t>(dz), P<const uint32_t>(mask), P<const uint16_t>(X), K0,
+                           P<const uint16_t>(W1), H, P<const uint16_t>(W0), P<const float>(b0), P<const uint16_t>(Wo),
+                           B, P<float>(gw1), P<float>(gw0), P<float>(gb0), P<float>(gb1), stride, P<int32_t>(tick),
+                           S(stream)),
+          "mlp_step_bwd");
   });
   m.def("mlp_fwd_head", [](u X, int K0, u W0, u b0, u W1, u b1, int H, u Wo, u bo, u labels, int B, int C,
                            float scale, u h1, u dact, u slab, u block_loss, u block_correct, u stream) {

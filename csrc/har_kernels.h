@@ -71,16 +71,23 @@ int har_mlp_fwd_head(const uint16_t* X, int K0, const uint16_t* W0, const float*
                      int C, float scale, uint16_t* h1, uint16_t* dact, float* slab, float* block_loss,
                      int32_t* block_correct, hipStream_t s);
 int har_mlp_fwd_head_grid(int B);
-// Fused backward after the fused forward (H = 256, B % 32 == 0): dW1 = dact2^T h1, dact1 = (dact2 W1) *
-// relu'(h1), dW0 = dact1^T X, db0 in one pass; per-slice partials at gw1 / gw0 / gb0 + s * slab_stride for
-// s < har_mlp_bwd_fused_slices(B).  har_mlp_fwd_head_variant: 2 = the 8-wave forward (writes db1 too).
-// h1 = nullptr: h1 is recomputed from X with W0 / b0 (pass h1 = nullptr to har_mlp_fwd_head too).
-int har_mlp_bwd_fused(const uint16_t* dact2, const uint16_t* h1, const uint16_t* X, int K0, const uint16_t* W1,
-                      int H, int B, float* gw1, float* gw0, float* gb0, int64_t slab_stride, int32_t* tick,
-                      const uint16_t* W0, const float* b0, hipStream_t s);
-int har_mlp_bwd_fused_slices(int B);
-int har_mlp_fwd_head_variant(int H, int B);
-// diagnostic phase stamps of the fused training kernels (nullptr = off); see mlp_fused.hip
+// Fused training step of the H = 256 MLP (mlp_step.hip; K0 = 32/64, C <= 16, B % 64 == 0):
+// har_mlp_step_fwd writes dz [B][8] u32 (16 bf16 logit gradients), the relu'(h2) mask [B][8] u32, per
+// workgroup slabs [har_mlp_step_grid(B)][har_mlp_step_fwd_slab_width(H)] (dWout rows 0..15, dbout) and
+// per-workgroup loss / #correct; har_mlp_step_bwd rebuilds dact2 from them and writes per row slice
+// s < har_mlp_step_slices(B) the partials of dW1, dW0, db0, db1 at gw1 / gw0 / gb0 / gb1 + s * slab_stride
+// (h1 recomputed from X).
+int har_mlp_step_fwd(const uint16_t* X, int K0, const uint16_t* W0, const float* b0, const uint16_t* W1,
+                     const float* b1, int H, const uint16_t* Wo, const float* bo, const int32_t* labels, int B, int C,
+                     float scale, uint32_t* dz, uint32_t* mask, float* slab, float* block_loss,
+                     int32_t* block_correct, hipStream_t s);
+int har_mlp_step_bwd(const uint32_t* dz, const uint32_t* mask, const uint16_t* X, int K0, const uint16_t* W1, int H,
+                     const uint16_t* W0, const float* b0, const uint16_t* Wo, int B, float* gw1, float* gw0,
+                     float* gb0, float* gb1, int64_t slab_stride, int32_t* tick, hipStream_t s);
+int har_mlp_step_grid(int B);
+int har_mlp_step_slices(int B);
+int har_mlp_step_fwd_slab_width(int H);
+// diagnostic phase stamps of the step kernels (nullptr = off); see mlp_step.hip
 void har_mlp_set_stamps(uint64_t* p);
 // Serving variant of the same kernel: logits [B][C] fp32 + argmax class [B] int32, nothing else.
 int har_mlp_fwd_infer_f32(const float* X, int ldx, int F, int K0, const uint16_t* W0, const float* b0,

@@ -1,0 +1,67 @@
+// MFMA fragment helpers shared by the fused MLP kernels (mlp_fused.hip, mlp_step.hip).
+//
+// gfx950 16x16x32 bf16 MFMA (v_mfma_f32_16x16x32_bf16): lane l holds A[row l & 15][k = 8 (l >> 4) + i]
+// and B[k = 8 (l >> 4) + i][col l & 15] (i < 8); C/D: col = l & 15, row = 4 (l >> 4) + reg.  The
+// 16x16x16 form (_1k) takes 4 k per lane: k = 4 (l >> 4) + i.
+#pragma once
+#include "common.h"
+
+namespace mlpf {
+
+typedef __attribute__((ext_vector_type(4))) short s16x4_t;
+typedef __attribute__((ext_vector_type(8))) short s16x8_t;
+typedef __attribute__((address_space(3))) s16x4_t lds_s16x4_t;
+typedef __attribute__((ext_vector_type(4))) uint32_t u32x4_t;
+typedef __attribute__((ext_vector_type(2))) uint32_t u32x2_t;
+typedef __attribute__((ext_vector_type(2))) short s16x2_t;
+typedef __attribute__((ext_vector_type(2))) unsigned short u16x2_t;
+
+__device__ __forceinline__ uint32_t pack2(float a, float b) {
+  return (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16);
+}
+
+__device__ __forceinline__ f32x4_t mma32(bf16x8_t a, bf16x8_t b, f32x4_t c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ f32x4_t mma16(s16x4_t a, s16x4_t b, f32x4_t c) {
+  return __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ bf16x8_t cat8(uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+  return __builtin_bit_cast(bf16x8_t, u32x4_t{a, b, c, d});
+}
+
+// relu of two packed bf16 (sign bit set = negative, -0 -> +0): one v_pk_max_i16
+__device__ __forceinline__ uint32_t relu2(uint32_t p) {
+  return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(s16x2_t, p), s16x2_t{0, 0}));
+}
+
+// Non-temporal 16-byte store (one global_store_dwordx4 ... nt; the consumer is the next kernel)
+__device__ __forceinline__ void nt_store16(void* p, u32x4_t v) {
+  __builtin_nontemporal_store(v, reinterpret_cast<u32x4_t*>(p));
+}
+
+// MFMA operand fragment (8 consecutive k of column lane & 15, natural k order) of a [k][cols] bf16
+// LDS image: two transposing 4 x 16 reads per lane
+__device__ __forceinline__ bf16x8_t frag_tr(const bf16_t* img, int pitch, int col0, int lane) {
+  const int li = lane & 15, g = lane >> 4;
+  const bf16_t* p0 = img + (8 * g + (li >> 2)) * pitch + col0 + 4 * (li & 3);
+  const s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)p0);
+  const s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(p0 + 4 * pitch));
+  const s16x8_t v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8_t, v);
+}
+
+// Same with the permuted k order of a 32-row step: lane group g supplies rows 4g..4g+3 and
+// 16+4g..16+4g+3 (both operands of a product must use it).  With a row pitch of an odd multiple
+// of 8 dwords the 32 lanes of an LDS bank group read 8 consecutive rows: conflict-free.
+__device__ __forceinline__ bf16x8_t frag_rows(const bf16_t* img, int pitch, int col0, int lane) {
+  const int li = lane & 15, g = lane >> 4;
+  const bf16_t* p0 = img + (4 * g + (li >> 2)) * pitch + col0 + 4 * (li & 3);
+  const s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)p0);
+  const s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(p0 + 16 * pitch));
+  const s16x8_t v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8_t, v);
+}
+
+}  // namespace mlpf

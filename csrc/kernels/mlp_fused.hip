@@ -32,23 +32,6 @@
 
 namespace {
 
-// Diagnostic phase stamps (tools/mlp_phase_probe.py --stamps): a separate STAMP instantiation of
-// the training kernels, launched only while a stamp buffer is set, has lane 0 of every wave store
-// s_memtime (shader clock) at fixed points into its own 40-slot row of that buffer (slots 38 / 39:
-// s_memrealtime at entry / exit, 100 MHz, one clock for the whole chip).  Nothing else reads them.
-uint64_t* g_stamps = nullptr;
-constexpr size_t STAMP_BWD_OFF = (size_t)256 * 8 * 40;  // the backward's rows follow the forward's
-#define HAR_STAMP(NW, k)                                                                     \
-  if constexpr (STAMP) {                                                                     \
-    if ((threadIdx.x & 63) == 0)                                                             \
-      stamps[((size_t)blockIdx.x * (NW) + (threadIdx.x >> 6)) * 40 + (k)] = __builtin_amdgcn_s_memtime(); \
-  }
-#define HAR_STAMP_REAL(NW, k)                                                                \
-  if constexpr (STAMP) {                                                                     \
-    if ((threadIdx.x & 63) == 0)                                                             \
-      stamps[((size_t)blockIdx.x * (NW) + (threadIdx.x >> 6)) * 40 + (k)] = __builtin_amdgcn_s_memrealtime(); \
-  }
-
 typedef __attribute__((ext_vector_type(4))) short s16x4_t;
 typedef __attribute__((address_space(3))) s16x4_t lds_s16x4_t;
 typedef __attribute__((ext_vector_type(4))) uint32_t u32x4_t;
@@ -392,741 +375,6 @@ int launch(const bf16_t* X, const bf16_t* W0, const float* b0, const bf16_t* W1,
   return 0;
 }
 
-// ---------------------------------------------------------------------------------------------
-// v2 (training step; H = 256, batch a multiple of 32; the default for those shapes,
-// HAR_MLP_FUSED_V1=1 keeps v1): 8 waves per workgroup; wave w owns hidden units [32w, 32w + 32) of BOTH hidden layers,
-// so its slices of W0, W1 (64 VGPRs per lane) and Wout stay in registers and the LDS holds only
-// per-tile data — the 32-row h1 tile (written by all 8 waves, read by all), the partial logits
-// and the stage-5 transpose images (~69 KB).  At <= 256 registers per lane two waves share each
-// SIMD (v1: one; its resident W1 image filled the LDS), so one wave's LDS / VALU / store
-// latency runs under the other's MFMAs.
-//
-//   stage 1  h1^T[u][r] = W0[u] . x_r        A = W0 (registers), B = X rows (16-byte loads)
-//            -> h1 (global) and the LDS h1 tile                                  | barrier
-//   stage 2  h2^T[u] = W1[u] . h1^T          A = W1 (registers), B = 16-byte LDS reads
-//   stage 3  partial z^T = Wout[:, u] . h2^T over the wave's 32 units -> LDS    | barrier
-//            z = sum of the 8 partials in a fixed order (identical bits in every wave), then
-//            softmax / CE / argmax per wave; wave 0 counts loss, #correct and dbout
-//   stage 4  dact2^T[u] = Wout^T[u] . dz^T, masked by relu'(h2)      16x16x16, K = classes
-//   stage 5  dWout^T[u] += h2^T . dz over the tile's 32 rows          16x16x32, K = rows: both
-//            operands transposed through a per-wave [32][16] LDS image + ds_read_b64_tr_b16
-constexpr int V2_W = 8, V2_U = 32, V2_RT = 32, V2_H = 256;
-constexpr int V2_HP = V2_H + 8;        // h1 tile pitch (bf16 elements)
-constexpr int V2_SP = 16 + 8;          // transpose image pitch
-constexpr int V2_IMG = V2_RT * V2_SP;  // elements per transpose image
-constexpr size_t V2_LDS = (size_t)2 * V2_RT * V2_HP * 2 + (size_t)V2_W * 2 * 64 * 16 + 2 * 64 * 8 +
-                          (size_t)V2_W * 3 * V2_IMG * 2;
-
-// The value lane ^ 16 / lane ^ 32 holds, by the gfx950 row / half swaps (VALU, no LDS round trip
-// like ds_bpermute).  `self` is the swap's result for the lane's own id: it fixes which of the
-// two outputs carries the partner, independent of the operand order convention.
-struct LaneSwap {
-  bool hi16, hi32;
-  __device__ __forceinline__ explicit LaneSwap(int lane) {
-    const auto a = __builtin_amdgcn_permlane16_swap((uint32_t)lane, (uint32_t)lane, false, false);
-    const auto b = __builtin_amdgcn_permlane32_swap((uint32_t)lane, (uint32_t)lane, false, false);
-    hi16 = a[0] == (uint32_t)(lane ^ 16);
-    hi32 = b[0] == (uint32_t)(lane ^ 32);
-  }
-  __device__ __forceinline__ uint32_t x16(uint32_t v) const {
-    const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
-    return hi16 ? r[0] : r[1];
-  }
-  __device__ __forceinline__ uint32_t x32(uint32_t v) const {
-    const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
-    return hi32 ? r[0] : r[1];
-  }
-  __device__ __forceinline__ float x16(float v) const { return __uint_as_float(x16(__float_as_uint(v))); }
-  __device__ __forceinline__ float x32(float v) const { return __uint_as_float(x32(__float_as_uint(v))); }
-};
-
-// Non-temporal 16-byte store (streaming: no L2 allocation; the consumer is the next kernel)
-__device__ __forceinline__ void nt_store4(uint4* p, uint4 v) {
-  __builtin_nontemporal_store(v.x, reinterpret_cast<uint32_t*>(p));
-  __builtin_nontemporal_store(v.y, reinterpret_cast<uint32_t*>(p) + 1);
-  __builtin_nontemporal_store(v.z, reinterpret_cast<uint32_t*>(p) + 2);
-  __builtin_nontemporal_store(v.w, reinterpret_cast<uint32_t*>(p) + 3);
-}
-
-// Copy a [32][V2_HP] LDS tile to rows r0.. of a [B][256] global matrix: two 16-byte vectors per
-// thread, every row one contiguous 512-byte run (row-per-lane dwordx2 stores are issue-bound)
-__device__ __forceinline__ void v2_store_tile(const bf16_t* tile, bf16_t* __restrict__ dst, int r0, int tid) {
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int v = tid + 512 * i, row = v >> 5, col = (v & 31) * 8;
-    const uint4 v4 = *reinterpret_cast<const uint4*>(tile + row * V2_HP + col);
-    nt_store4(reinterpret_cast<uint4*>(dst + (size_t)(r0 + row) * V2_H + col), v4);
-  }
-}
-
-typedef __attribute__((ext_vector_type(2))) short s16x2_t;
-typedef __attribute__((ext_vector_type(2))) unsigned short u16x2_t;
-// relu of two packed bf16 (sign bit set = negative, -0 -> +0): one v_pk_max_i16
-__device__ __forceinline__ uint32_t relu2(uint32_t p) {
-  return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(s16x2_t, p), s16x2_t{0, 0}));
-}
-// d where the packed activation m (relu2 output: never negative) is nonzero, else 0, per half:
-// v_pk_min_u16 -> {0, 1}, v_pk_mul_lo_u16
-__device__ __forceinline__ uint32_t mask2(uint32_t d, uint32_t m) {
-  const u16x2_t nz = __builtin_elementwise_min(__builtin_bit_cast(u16x2_t, m), u16x2_t{1, 1});
-  return __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2_t, d) * nz);
-}
-
-// MFMA operand fragment (8 consecutive k of column lane & 15) of a [k][cols] bf16 LDS image:
-// two transposing 4 x 16 reads per lane
-__device__ __forceinline__ bf16x8_t frag_tr(const bf16_t* img, int pitch, int col0, int lane) {
-  const int li = lane & 15, g = lane >> 4;
-  const bf16_t* p0 = img + (8 * g + (li >> 2)) * pitch + col0 + 4 * (li & 3);
-  const s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)p0);
-  const s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(p0 + 4 * pitch));
-  typedef __attribute__((ext_vector_type(8))) short s16x8_t;
-  const s16x8_t v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-  return __builtin_bit_cast(bf16x8_t, v);
-}
-
-// SH1 = false: h1 is not written (the fused backward recomputes it from X: 2 x B x 256 bf16 of HBM
-// traffic saved per step for ~2 GFLOP of MFMA work)
-template <int K0, bool INFER, int XF = 0, bool SH1 = true, bool STAMP = false>
-__global__ __launch_bounds__(512) void mlp_fwd_head_v2_kernel(
-    const bf16_t* __restrict__ X, const bf16_t* __restrict__ W0, const float* __restrict__ b0,
-    const bf16_t* __restrict__ W1, const float* __restrict__ b1, const bf16_t* __restrict__ Wo,
-    const float* __restrict__ bo, const int32_t* __restrict__ labels, int B, int C, float scale,
-    bf16_t* __restrict__ h1out, bf16_t* __restrict__ dact, float* __restrict__ slab,
-    float* __restrict__ block_loss, int32_t* __restrict__ block_correct, float* __restrict__ logits_out,
-    int32_t* __restrict__ pred_out, int F, int ldx, uint64_t* __restrict__ stamps) {
-  constexpr int H = V2_H, K0C = K0 / 32, KC = H / 32;
-  extern __shared__ __attribute__((aligned(16))) bf16_t lds[];
-  bf16_t* h1s = lds;                                          // [32][V2_HP] h1 tile
-  bf16_t* dts = h1s + V2_RT * V2_HP;                          // [32][V2_HP] dact2 tile (copied out a tile later)
-  float* zs = reinterpret_cast<float*>(dts + V2_RT * V2_HP);  // [8 waves][2 halves][64 lanes][4]
-  uint32_t* dzs = reinterpret_cast<uint32_t*>(zs + V2_W * 2 * 64 * 4);  // [2 halves][64 lanes][2]
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int c16 = lane & 15, g = lane >> 4;
-  const int u0 = wave * V2_U;
-  bf16_t* img = reinterpret_cast<bf16_t*>(dzs + 2 * 64 * 2) + wave * 3 * V2_IMG;  // h2 t=0, t=1, dz
-  const LaneSwap swp(lane);
-  HAR_STAMP_REAL(V2_W, 38)
-  HAR_STAMP(V2_W, 0)
-
-  // ---- this wave's weight slices, in registers for the whole kernel ----
-  bf16x8_t w0f[2][K0C], w1f[2][KC];
-#pragma unroll
-  for (int t = 0; t < 2; ++t) {
-#pragma unroll
-    for (int kc = 0; kc < K0C; ++kc)
-      w0f[t][kc] = *reinterpret_cast<const bf16x8_t*>(W0 + (size_t)(u0 + 16 * t + c16) * K0 + kc * 32 + g * 8);
-#pragma unroll
-    for (int kc = 0; kc < KC; ++kc)
-      w1f[t][kc] = *reinterpret_cast<const bf16x8_t*>(W1 + (size_t)(u0 + 16 * t + c16) * H + kc * 32 + g * 8);
-  }
-  // stage-3 A fragment: Wout[class c16][u0 + 4g + j] (j < 4), [u0 + 16 + 4g + j - 4] (j >= 4) —
-  // the k permutation of the h2 register pairs (see "Operand trick" at the top)
-  const uint2 wlo = *reinterpret_cast<const uint2*>(Wo + (size_t)c16 * H + u0 + 4 * g);
-  const uint2 whi = *reinterpret_cast<const uint2*>(Wo + (size_t)c16 * H + u0 + 16 + 4 * g);
-  const bf16x8_t wo3 = cat8(wlo.x, wlo.y, whi.x, whi.y);
-  // stage-4 A fragments: Wout[class 4g + j][u0 + 16t + c16], j < 4
-  s16x4_t wo4[2];
-#pragma unroll
-  for (int t = 0; t < 2; ++t)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) wo4[t][j] = (short)Wo[(size_t)(4 * g + j) * H + u0 + 16 * t + c16];
-  float4 b0r[2], b1r[2];
-#pragma unroll
-  for (int t = 0; t < 2; ++t) {
-    b0r[t] = *reinterpret_cast<const float4*>(b0 + u0 + 16 * t + 4 * g);
-    b1r[t] = *reinterpret_cast<const float4*>(b1 + u0 + 16 * t + 4 * g);
-  }
-  float bo_r[4];
-#pragma unroll
-  for (int r = 0; r < 4; ++r) bo_r[r] = (4 * g + r < C) ? bo[4 * g + r] : 0.f;
-
-  if constexpr (STAMP) __builtin_amdgcn_s_waitcnt(0x0f70);
-  HAR_STAMP(V2_W, 1)
-  f32x4_t acc5[2] = {f32x4_t{0.f, 0.f, 0.f, 0.f}, f32x4_t{0.f, 0.f, 0.f, 0.f}};
-  float db1[2][4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};  // column sums of this lane's dact2 values
-  float dbo[4] = {0.f, 0.f, 0.f, 0.f};
-  float lsum = 0.f;
-  int ncorr = 0;
-  const int ntiles = B / V2_RT;
-  int T = blockIdx.x;
-  bf16x8_t xb[2][K0C];
-  int prev_r0 = -1;
-  if (T < ntiles) {
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-#pragma unroll
-      for (int kc = 0; kc < K0C; ++kc) xb[h][kc] = load_x<K0, XF>(X, T * V2_RT + 16 * h + c16, kc, g, F, ldx);
-    }
-  }
-  int it_ = 0;
-  for (; T < ntiles; T += gridDim.x) {
-    const int r0 = T * V2_RT;
-    if (it_ < 32) HAR_STAMP(V2_W, 2 + it_)
-    ++it_;
-    // ---- stage 1: h1^T = W0 . X^T for this wave's units ----
-#pragma unroll
-    for (int h = 0; h < 2; ++h)
-#pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        f32x4_t a = {b0r[t].x, b0r[t].y, b0r[t].z, b0r[t].w};  // bias as the initial accumulator
-#pragma unroll
-        for (int kc = 0; kc < K0C; ++kc) a = mma32(w0f[t][kc], xb[h][kc], a);
-        const uint2 v = make_uint2(relu2(pack2(a[0], a[1])), relu2(pack2(a[2], a[3])));
-        *reinterpret_cast<uint2*>(h1s + (16 * h + c16) * V2_HP + u0 + 16 * t + 4 * g) = v;
-      }
-    // this tile's labels, loaded after stage 1 (whose X reads the compiler waits for) and first
-    // used by the softmax two barriers later (a label prefetched one tile ahead is loop-carried in
-    // a renamed register: the copy at the back edge made every tile wait for its own X prefetch).
-    // The loads are inline asm so the compiler cannot sink them next to their use (it did, and
-    // then drained vmcnt(0) there, X prefetch included); the explicit counted wait before the
-    // softmax (label_wait) retires them while the 2 * K0C X loads and the 4 tile stores issued
-    // after them stay in flight.
-    int yc0 = 0, yc1 = 0;
-    if (!INFER) {
-      const int32_t* lp = labels + r0 + c16;
-      asm volatile("global_load_dword %0, %2, off\n\tglobal_load_dword %1, %2, off offset:64"
-                   : "=&v"(yc0), "=&v"(yc1)
-                   : "v"(lp)
-                   : "memory");
-    }
-    __syncthreads();  // the h1 tile (and the previous tile's dact2 tile) is complete
-    if (!INFER) {  // coalesced row stores of h1 (this tile) and dact2 (the previous tile)
-      if constexpr (SH1) v2_store_tile(h1s, h1out, r0, tid);
-      // unconditional (same store count every tile, so the waits stay counted): the first tile
-      // writes its not-yet-computed dact2 rows, which the same threads overwrite a tile later
-      v2_store_tile(dts, dact, prev_r0 >= 0 ? prev_r0 : r0, tid);
-      prev_r0 = r0;
-    }
-    // prefetch the next tile's X rows, after this tile's stores: the loop-top wait for them is then
-    // the same on the first and on every later tile (the youngest ops either way), and it comes a
-    // whole tile later.  Unconditional (index clamped to a valid tile): a conditional load merges
-    // paths with different outstanding-load counts and the compiler then drains vmcnt(0) mid-tile
-    const int Tn = min(T + (int)gridDim.x, ntiles - 1);
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-#pragma unroll
-      for (int kc = 0; kc < K0C; ++kc) xb[h][kc] = load_x<K0, XF>(X, Tn * V2_RT + 16 * h + c16, kc, g, F, ldx);
-    }
-
-    // ---- stage 2: h2^T = W1 . h1^T (4 independent accumulators) ----
-    f32x4_t acc[2][2];
-#pragma unroll
-    for (int h = 0; h < 2; ++h)
-#pragma unroll
-      for (int t = 0; t < 2; ++t) acc[h][t] = f32x4_t{b1r[t].x, b1r[t].y, b1r[t].z, b1r[t].w};
-#pragma unroll
-    for (int kc = 0; kc < KC; ++kc) {
-      bf16x8_t hb[2];
-#pragma unroll
-      for (int h = 0; h < 2; ++h)
-        hb[h] = *reinterpret_cast<const bf16x8_t*>(h1s + (16 * h + c16) * V2_HP + kc * 32 + 8 * g);
-#pragma unroll
-      for (int h = 0; h < 2; ++h)
-#pragma unroll
-        for (int t = 0; t < 2; ++t) acc[h][t] = mma32(w1f[t][kc], hb[h], acc[h][t]);
-    }
-    uint32_t h2p[2][2][2];
-#pragma unroll
-    for (int h = 0; h < 2; ++h)
-#pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        h2p[h][t][0] = relu2(pack2(acc[h][t][0], acc[h][t][1]));
-        h2p[h][t][1] = relu2(pack2(acc[h][t][2], acc[h][t][3]));
-      }
-    // ---- stage 3: partial logits over this wave's 32 units ----
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const f32x4_t zp = mma32(wo3, cat8(h2p[h][0][0], h2p[h][0][1], h2p[h][1][0], h2p[h][1][1]),
-                               f32x4_t{0.f, 0.f, 0.f, 0.f});
-      *reinterpret_cast<f32x4_t*>(zs + ((wave * 2 + h) * 64 + lane) * 4) = zp;
-    }
-    __syncthreads();  // every wave's partial logits are in
-    if (!INFER) {  // the labels (issued first this tile) are in: vmcnt(2 * K0C X loads + 4 stores)
-      if constexpr (SH1) {
-        if constexpr (K0C == 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-      } else {  // two tile stores fewer behind the labels
-        if constexpr (K0C == 2) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-      }
-    }
-    // ---- logits, softmax, CE of half h in wave h < 2 (the other waves only need dz) ----
-    if (wave < 2) {
-      const int h = wave;
-      f32x4_t z = *reinterpret_cast<const f32x4_t*>(zs + (h * 64 + lane) * 4);
-#pragma unroll
-      for (int w = 1; w < V2_W; ++w) z += *reinterpret_cast<const f32x4_t*>(zs + ((w * 2 + h) * 64 + lane) * 4);
-      const int row = r0 + 16 * h + c16;
-      const int yc = h ? yc1 : yc0;
-      float zz[4];
-      float mx = -INFINITY;
-      int amx = 1 << 30;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int cls = 4 * g + r;
-        zz[r] = cls < C ? z[r] + bo_r[r] : -INFINITY;
-        if (zz[r] > mx) { mx = zz[r]; amx = cls; }
-      }
-      {
-        float om = swp.x16(mx);
-        int oa = (int)swp.x16((uint32_t)amx);
-        if (om > mx || (om == mx && oa < amx)) { mx = om; amx = oa; }
-        om = swp.x32(mx);
-        oa = (int)swp.x32((uint32_t)amx);
-        if (om > mx || (om == mx && oa < amx)) { mx = om; amx = oa; }
-      }
-      if constexpr (INFER) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          if (4 * g + r < C) logits_out[(size_t)row * C + 4 * g + r] = zz[r];
-        if (g == 0) pred_out[row] = amx;
-      } else {
-        float e[4], se = 0.f;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          e[r] = (4 * g + r < C) ? __expf(zz[r] - mx) : 0.f;
-          se += e[r];
-        }
-        se += swp.x16(se);
-        se += swp.x32(se);
-        const float inv = 1.f / se, lse = mx + __logf(se);
-        float dl[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int cls = 4 * g + r;
-          dl[r] = cls < C ? (e[r] * inv - (cls == yc ? 1.f : 0.f)) * scale : 0.f;
-          if (cls == yc) lsum += lse - zz[r];
-        }
-        if (g == 0 && amx == yc) ncorr += 1;
-        const uint32_t dz01 = pack2(dl[0], dl[1]), dz23 = pack2(dl[2], dl[3]);
-        dbo[0] += __uint_as_float(dz01 << 16);
-        dbo[1] += __uint_as_float(dz01 & 0xffff0000u);
-        dbo[2] += __uint_as_float(dz23 << 16);
-        dbo[3] += __uint_as_float(dz23 & 0xffff0000u);
-        *reinterpret_cast<uint2*>(dzs + (h * 64 + lane) * 2) = make_uint2(dz01, dz23);
-      }
-    }
-    if constexpr (INFER) continue;
-    __syncthreads();  // dz of both halves is in
-    uint32_t dz[2][2];
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const uint2 v = *reinterpret_cast<const uint2*>(dzs + (h * 64 + lane) * 2);
-      dz[h][0] = v.x;
-      dz[h][1] = v.y;
-    }
-    // ---- stage 4: dact2^T = Wout^T . dz^T, masked by relu'(h2) ----
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const s16x4_t dzv = __builtin_bit_cast(s16x4_t, make_uint2(dz[h][0], dz[h][1]));
-#pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        const f32x4_t d = mma16(wo4[t], dzv, f32x4_t{0.f, 0.f, 0.f, 0.f});
-        const uint32_t q0 = mask2(pack2(d[0], d[1]), h2p[h][t][0]), q1 = mask2(pack2(d[2], d[3]), h2p[h][t][1]);
-        *reinterpret_cast<uint2*>(dts + (16 * h + c16) * V2_HP + u0 + 16 * t + 4 * g) = make_uint2(q0, q1);
-        db1[t][0] += __uint_as_float(q0 << 16);
-        db1[t][1] += __uint_as_float(q0 & 0xffff0000u);
-        db1[t][2] += __uint_as_float(q1 << 16);
-        db1[t][3] += __uint_as_float(q1 & 0xffff0000u);
-      }
-    }
-    // ---- stage 5: dWout^T += h2^T . dz over the tile's 32 rows (per-wave transposes) ----
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-#pragma unroll
-      for (int t = 0; t < 2; ++t)
-        *reinterpret_cast<uint2*>(img + t * V2_IMG + (16 * h + c16) * V2_SP + 4 * g) =
-            make_uint2(h2p[h][t][0], h2p[h][t][1]);
-      *reinterpret_cast<uint2*>(img + 2 * V2_IMG + (16 * h + c16) * V2_SP + 4 * g) = make_uint2(dz[h][0], dz[h][1]);
-    }
-    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's images are in LDS
-    __builtin_amdgcn_wave_barrier();
-    const bf16x8_t bz = frag_tr(img + 2 * V2_IMG, V2_SP, 0, lane);
-#pragma unroll
-    for (int t = 0; t < 2; ++t) acc5[t] = mma32(frag_tr(img + t * V2_IMG, V2_SP, 0, lane), bz, acc5[t]);
-  }
-
-  if constexpr (INFER) return;
-  HAR_STAMP(V2_W, 34)
-  __syncthreads();  // the last tile's dact2 tile is complete
-  if (prev_r0 >= 0) v2_store_tile(dts, dact, prev_r0, tid);
-  // ---- this wave's units of the workgroup slab: dWout rows 0..15 x units, dbout, loss ----
-  float* out = slab + (size_t)blockIdx.x * fwd_slab_width(H);
-#pragma unroll
-  for (int t = 0; t < 2; ++t)
-    nt_store4(reinterpret_cast<uint4*>(out + (size_t)c16 * H + u0 + 16 * t + 4 * g), __builtin_bit_cast(uint4, acc5[t]));
-  // db1 of this wave's units: sum over the 16 row lanes of each lane group
-#pragma unroll
-  for (int t = 0; t < 2; ++t)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      float v = db1[t][r];
-#pragma unroll
-      for (int o = 1; o < 16; o <<= 1) v += __shfl_xor(v, o, 64);
-      if (c16 == 0) out[NCLS * H + NCLS + u0 + 16 * t + 4 * g + r] = v;
-    }
-  float* red = zs;  // waves 0 / 1 (halves 0 / 1): dbout [2][16], loss [2], #correct [2]
-  if (wave < 2) {
-#pragma unroll
-    for (int r = 0; r < 4; ++r)
-#pragma unroll
-      for (int o = 1; o < 16; o <<= 1) dbo[r] += __shfl_xor(dbo[r], o, 64);
-    if (c16 == 0) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) red[wave * NCLS + 4 * g + r] = dbo[r];
-    }
-    lsum = wave_sum(lsum);
-    const float nc = wave_sum((float)ncorr);
-    if (lane == 0) {
-      red[2 * NCLS + wave] = lsum;
-      red[2 * NCLS + 2 + wave] = nc;
-    }
-  }
-  __syncthreads();
-  if (tid < NCLS) out[NCLS * H + tid] = red[tid] + red[NCLS + tid];
-  if (tid == 0) {
-    block_loss[blockIdx.x] = red[2 * NCLS] + red[2 * NCLS + 1];
-    block_correct[blockIdx.x] = (int)(red[2 * NCLS + 2] + red[2 * NCLS + 3]);
-  }
-  if constexpr (STAMP) __builtin_amdgcn_s_waitcnt(0x0f70);
-  HAR_STAMP(V2_W, 35)
-  HAR_STAMP_REAL(V2_W, 39)
-}
-
-template <int K0, bool INFER = false, int XF = 0>
-int launch_v2(const bf16_t* X, const bf16_t* W0, const float* b0, const bf16_t* W1, const float* b1,
-              const bf16_t* Wo, const float* bo, const int32_t* labels, int B, int C, float scale, bf16_t* h1,
-              bf16_t* dact, float* slab, float* block_loss, int32_t* block_correct, int nwg, hipStream_t s,
-              float* logits = nullptr, int32_t* pred = nullptr, int F = K0, int ldx = K0) {
-  auto kern = (INFER || h1) ? mlp_fwd_head_v2_kernel<K0, INFER, XF, true> : mlp_fwd_head_v2_kernel<K0, INFER, XF, false>;
-  if (!INFER && !h1 && g_stamps) kern = mlp_fwd_head_v2_kernel<K0, INFER, XF, false, true>;
-  kern<<<nwg, 512, V2_LDS, s>>>(X, W0, b0, W1, b1, Wo, bo, labels, B, C, scale, h1, dact, slab, block_loss,
-                                block_correct, logits, pred, F, ldx, g_stamps);
-  HAR_CHECK_LAUNCH();
-  return 0;
-}
-
-// ---------------------------------------------------------------------------------------------
-// Layer-2 weight gradient + layer-1 backward in ONE pass (H = 256, batch a multiple of 64):
-//   dW1 = dact2^T . h1,   dact1 = (dact2 . W1) * relu'(h1),   dW0 = dact1^T . X,   db0 = sum_rows dact1
-// (db1 = the column sums of dact2 come from the forward kernel, which produces dact2).  The
-// split-K dW1 GEMM and a separate layer-1 kernel each read dact2 and h1 (2 x 64 MB at batch
-// 65536); here they are read once, and dact1 never reaches HBM.
-//
-// Grid: S row slices x 4 h1-unit quadrants (64 units each).  After the XCD remap the four
-// quadrant workgroups of a slice are adjacent (same XCD), so the dact2 / X tiles they all read
-// come from that XCD's L2 after the first.  Workgroup (s, q) owns dW1[:, 64q..64q+64),
-// dW0[64q..64q+64, :] and db0[64q..64q+64) of slab s — one deterministic partial per slice, laid
-// out like the flat parameter buffer (reduced later in a fixed order).
-//
-// Software pipeline, ONE barrier per 64-row tile i (8 waves):
-//   stage tile i+1 (registers -> LDS buffer (i+1)&1) | refill the registers with tile i+2 |
-//   (a) dact1^T[u][r] = W1[:, u]^T . dact2^T   A = W1 columns (registers, two unit blocks per
-//       wave), B = dact2 rows (LDS b128); relu'(h1) mask; dact1 -> LDS buffer i&1
-//       wave: rows 16 (w & 3).., unit blocks 2 (w >> 2) + {0, 1}
-//   (b) dW1[j][u] += dact2^T . h1 (two K = 32 row steps; both operands transposed out of LDS)
-//       wave: unit blocks 2 (w & 1) + {0, 1} x j blocks 4 (w >> 1) + {0..3}
-//   (c) dW0[u][k] += dact1^T . X for tile i-1 (its dact1 is complete after the last barrier)
-//       wave: unit block w & 3, k blocks of half w >> 2  |  barrier
-// X tiles rotate through three buffers (tile i-1 is read by (c) while tile i+1 is staged).
-// Row order of the transposed operands (frag_rows): lane group g supplies rows 4g..4g+3 and
-// 16+4g..16+4g+3 of a 32-row step — one permutation of K, used by both operands of a product.
-// With row pitches of an odd multiple of 8 dwords the 32 lanes of an LDS bank group then read 8
-// consecutive rows: conflict-free, and the row-per-lane b128 reads of (a) are conflict-free too.
-constexpr int BF_Q = 4, BF_QU = V2_H / BF_Q;  // 64 h1 units per workgroup
-constexpr int BF_RT = 64;                     // rows per pipeline tile
-constexpr int BF_DP = V2_H + 16;              // dact2 tile pitch: 136 dwords (8 mod 64)
-constexpr int BF_UP = BF_QU + 16;             // h1 / dact1 quadrant tile pitch: 40 dwords
-
-__device__ __forceinline__ bf16x8_t frag_rows(const bf16_t* img, int pitch, int col0, int lane) {
-  const int li = lane & 15, g = lane >> 4;
-  const bf16_t* p0 = img + (4 * g + (li >> 2)) * pitch + col0 + 4 * (li & 3);
-  const s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)p0);
-  const s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(p0 + 16 * pitch));
-  typedef __attribute__((ext_vector_type(8))) short s16x8_t;
-  const s16x8_t v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-  return __builtin_bit_cast(bf16x8_t, v);
-}
-
-// RH1: the h1 quadrant tiles are recomputed from the X tiles (h1 = relu(W0 . x + b0), the forward's
-// operands, accumulation order and rounding: bit-identical) instead of read from HBM; X is then
-// staged two tiles ahead through four buffers so tile i+1's h1 is computed during tile i.
-template <int K0, bool RH1 = false> struct BwdLds {
-  static constexpr int XP = K0 + 16;
-  static constexpr int NXB = RH1 ? 4 : 3;  // X tile buffers
-  static constexpr int DSM = BF_RT * BF_DP, HS = BF_RT * BF_UP, XS = BF_RT * XP;  // elements per buffer
-  static constexpr size_t bytes = (size_t)(2 * DSM + 2 * HS + 2 * HS + NXB * XS) * sizeof(bf16_t) +
-                                  4 * BF_QU * sizeof(float);
-};
-
-template <int K0, bool RH1 = false, bool STAMP = false>
-__global__ __launch_bounds__(512) void mlp_bwd_fused_kernel(const bf16_t* __restrict__ dact2,
-                                                           const bf16_t* __restrict__ h1,
-                                                           const bf16_t* __restrict__ X,
-                                                           const bf16_t* __restrict__ W1, int B, int S,
-                                                           float* __restrict__ gw1, float* __restrict__ gw0,
-                                                           float* __restrict__ gb0, int64_t slab_stride,
-                                                           int32_t* __restrict__ tick,
-                                                           const bf16_t* __restrict__ W0,
-                                                           const float* __restrict__ b0,
-                                                           uint64_t* __restrict__ stamps) {
-  using L = BwdLds<K0, RH1>;
-  constexpr int NXB = L::NXB;
-  // the training step counter ticks here (one thread, before the reduction kernel reads it for Adam)
-  if (tick && blockIdx.x == 0 && threadIdx.x == 0) *tick += 1;
-  constexpr int H = V2_H, KC = H / 32, XP = L::XP, NFW = K0 / 32;
-  constexpr int XV = BF_RT * K0 / 8;  // 16-byte vectors of an X tile (512 / 256)
-  extern __shared__ __attribute__((aligned(16))) bf16_t lds[];
-  bf16_t* const dsm0 = lds;                 // [2][64][BF_DP] dact2 tiles
-  bf16_t* const hs0 = dsm0 + 2 * L::DSM;    // [2][64][BF_UP] h1 quadrant tiles
-  bf16_t* const d1s0 = hs0 + 2 * L::HS;     // [2][64][BF_UP] dact1 quadrant tiles
-  bf16_t* const xs0 = d1s0 + 2 * L::HS;     // [3][64][XP] X tiles
-  float* const red = reinterpret_cast<float*>(xs0 + 3 * L::XS);  // [4][64] db0 of the row blocks
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int c16 = lane & 15, g = lane >> 4;
-  HAR_STAMP_REAL(8, 38)
-  HAR_STAMP(8, 0)
-  const int b = xcd_remap(blockIdx.x, gridDim.x);
-  const int slice = b / BF_Q, qu0 = (b % BF_Q) * BF_QU;
-  const int rb = wave & 3, up = 2 * (wave >> 2);            // (a)
-  const int ubp = 2 * (wave & 1), jb0 = 4 * (wave >> 1);    // (b)
-  const int ub = wave & 3, fb = (wave >> 2) * NFW;          // (c)
-  const int ntiles = B / BF_RT, per = (ntiles + S - 1) / S;
-  const int t0 = slice * per, n = max(0, min(ntiles, t0 + per) - t0);
-
-  // (a) A fragments: A[u][k = j] = W1[kc * 32 + 8g + i][qu0 + 16 (up + e) + c16]
-  bf16x8_t w1t[2][KC];
-#pragma unroll
-  for (int e = 0; e < 2; ++e)
-#pragma unroll
-    for (int kc = 0; kc < KC; ++kc) {
-      typedef __attribute__((ext_vector_type(8))) short s16x8_t;
-      s16x8_t v;
-#pragma unroll
-      for (int i = 0; i < 8; ++i) v[i] = (short)W1[(size_t)(kc * 32 + 8 * g + i) * H + qu0 + 16 * (up + e) + c16];
-      w1t[e][kc] = __builtin_bit_cast(bf16x8_t, v);
-    }
-  // (RH1) h1 recompute: wave w -> unit block w & 3 of the quadrant, row blocks 2 (w >> 2) + {0, 1};
-  // A = W0 rows of those units (the forward's stage-1 fragments), bias as the initial accumulator
-  const int ubh = wave & 3, rbh = 2 * (wave >> 2);
-  bf16x8_t w0q[NFW];
-  float4 b0q = make_float4(0.f, 0.f, 0.f, 0.f);
-  if constexpr (RH1) {
-#pragma unroll
-    for (int kc = 0; kc < NFW; ++kc)
-      w0q[kc] = *reinterpret_cast<const bf16x8_t*>(W0 + (size_t)(qu0 + 16 * ubh + c16) * K0 + kc * 32 + 8 * g);
-    b0q = *reinterpret_cast<const float4*>(b0 + qu0 + 16 * ubh + 4 * g);
-  }
-  if constexpr (STAMP) __builtin_amdgcn_s_waitcnt(0x0f70);
-  HAR_STAMP(8, 1)
-  f32x4_t acc1[4][2], acc0[NFW];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) acc1[i][0] = acc1[i][1] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int f = 0; f < NFW; ++f) acc0[f] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-  float rs[2][4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
-
-  // Register staging of a tile: four dact2 vectors, one h1-quadrant vector and one X vector per
-  // thread (for K0 = 32 threads 256.. reload threads 0..255's X vector and store the same bytes
-  // to the same place).  Per-thread pointers are fixed once; every load is unconditional (a tile
-  // index past the slice is clamped to a valid tile whose bytes are staged but never used), so
-  // the compiler's vmcnt accounting is exact on every path.
-  const bf16_t* ldd = dact2 + (size_t)tid * 8;
-  const bf16_t* ldh = h1 + (size_t)(tid >> 3) * H + qu0 + (tid & 7) * 8;
-  const bf16_t* ldx = X + (size_t)(tid & (XV - 1)) * 8;
-  const int sdd = (tid >> 5) * BF_DP + (tid & 31) * 8;  // + 16 rows * BF_DP per dact2 vector
-  const int sdh = (tid >> 3) * BF_UP + (tid & 7) * 8;
-  const int sdx = ((tid & (XV - 1)) / (K0 / 8)) * XP + ((tid & (XV - 1)) % (K0 / 8)) * 8;
-  const int tlast = ntiles - 1;
-  uint4 r0, r1, r2, r3, r4 = make_uint4(0, 0, 0, 0), r5;
-#define HAR_BWD_LOAD_D(t)                                                    \
-  {                                                                          \
-    const int64_t tt_ = min(t, tlast);                                       \
-    const bf16_t* d_ = ldd + tt_ * BF_RT * H;                                \
-    r0 = *reinterpret_cast<const uint4*>(d_);                                \
-    r1 = *reinterpret_cast<const uint4*>(d_ + 16 * H);                       \
-    r2 = *reinterpret_cast<const uint4*>(d_ + 32 * H);                       \
-    r3 = *reinterpret_cast<const uint4*>(d_ + 48 * H);                       \
-  }
-#define HAR_BWD_LOAD_X(t) r5 = *reinterpret_cast<const uint4*>(ldx + (int64_t)min(t, tlast) * BF_RT * K0);
-#define HAR_BWD_LOAD(t)                                                      \
-  {                                                                          \
-    HAR_BWD_LOAD_D(t)                                                        \
-    r4 = *reinterpret_cast<const uint4*>(ldh + (int64_t)min(t, tlast) * BF_RT * H); \
-    HAR_BWD_LOAD_X(t)                                                        \
-  }
-#define HAR_BWD_STAGE_D(i)                                                   \
-  {                                                                          \
-    bf16_t* d_ = dsm0 + ((i) & 1) * L::DSM + sdd;                            \
-    *reinterpret_cast<uint4*>(d_) = r0;                                      \
-    *reinterpret_cast<uint4*>(d_ + 16 * BF_DP) = r1;                         \
-    *reinterpret_cast<uint4*>(d_ + 32 * BF_DP) = r2;                         \
-    *reinterpret_cast<uint4*>(d_ + 48 * BF_DP) = r3;                         \
-  }
-#define HAR_BWD_STAGE_X(i) *reinterpret_cast<uint4*>(xs0 + ((i) % NXB) * L::XS + sdx) = r5;
-#define HAR_BWD_STAGE(i)                                                     \
-  {                                                                          \
-    HAR_BWD_STAGE_D(i)                                                       \
-    *reinterpret_cast<uint4*>(hs0 + ((i) & 1) * L::HS + sdh) = r4;           \
-    HAR_BWD_STAGE_X(i)                                                       \
-  }
-
-  // (a) + (b) of local tile i (LDS buffers i & 1)
-  auto tile_ab = [&](int i) __attribute__((always_inline)) {
-    const bf16_t* dsm = dsm0 + (i & 1) * L::DSM;
-    const bf16_t* hs = hs0 + (i & 1) * L::HS;
-    bf16_t* d1s = d1s0 + (i & 1) * L::HS;
-    f32x4_t a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int kc = 0; kc < KC; ++kc) {
-      const bf16x8_t bv = *reinterpret_cast<const bf16x8_t*>(dsm + (16 * rb + c16) * BF_DP + kc * 32 + 8 * g);
-      a0 = mma32(w1t[0][kc], bv, a0);
-      a1 = mma32(w1t[1][kc], bv, a1);
-    }
-#pragma unroll
-    for (int e = 0; e < 2; ++e) {
-      const f32x4_t& a = e ? a1 : a0;
-      const int col = 16 * (up + e) + 4 * g;
-      const uint2 m = *reinterpret_cast<const uint2*>(hs + (16 * rb + c16) * BF_UP + col);
-      const float d0 = bf_pos(m.x) ? a[0] : 0.f, d1 = bf_pos(m.x >> 16) ? a[1] : 0.f;
-      const float d2 = bf_pos(m.y) ? a[2] : 0.f, d3 = bf_pos(m.y >> 16) ? a[3] : 0.f;
-      const uint32_t p0 = pack2(d0, d1), p1 = pack2(d2, d3);
-      rs[e][0] += __uint_as_float(p0 << 16);
-      rs[e][1] += __uint_as_float(p0 & 0xffff0000u);
-      rs[e][2] += __uint_as_float(p1 << 16);
-      rs[e][3] += __uint_as_float(p1 & 0xffff0000u);
-      *reinterpret_cast<uint2*>(d1s + (16 * rb + c16) * BF_UP + col) = make_uint2(p0, p1);
-    }
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      const bf16x8_t hb0 = frag_rows(hs + 32 * ks * BF_UP, BF_UP, 16 * ubp, lane);
-      const bf16x8_t hb1 = frag_rows(hs + 32 * ks * BF_UP, BF_UP, 16 * (ubp + 1), lane);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const bf16x8_t da = frag_rows(dsm + 32 * ks * BF_DP, BF_DP, 16 * (jb0 + j), lane);
-        acc1[j][0] = mma32(da, hb0, acc1[j][0]);
-        acc1[j][1] = mma32(da, hb1, acc1[j][1]);
-      }
-    }
-  };
-  // (c) of local tile i (its dact1 buffer i & 1, X buffer i % NXB)
-  auto tile_c = [&](int i) __attribute__((always_inline)) {
-    const bf16_t* d1s = d1s0 + (i & 1) * L::HS;
-    const bf16_t* xs = xs0 + (i % NXB) * L::XS;
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      const bf16x8_t A = frag_rows(d1s + 32 * ks * BF_UP, BF_UP, 16 * ub, lane);
-#pragma unroll
-      for (int f = 0; f < NFW; ++f)
-        acc0[f] = mma32(A, frag_rows(xs + 32 * ks * XP, XP, 16 * (fb + f), lane), acc0[f]);
-    }
-  };
-
-  // (RH1) h1 quadrant tile i from X tile i (buffer i % NXB) into h1 buffer i & 1
-  auto tile_h1 = [&](int i) __attribute__((always_inline)) {
-    const bf16_t* xs = xs0 + (i % NXB) * L::XS;
-    bf16_t* hs = hs0 + (i & 1) * L::HS;
-#pragma unroll
-    for (int e = 0; e < 2; ++e) {
-      const int row = 16 * (rbh + e) + c16;
-      f32x4_t a = {b0q.x, b0q.y, b0q.z, b0q.w};
-#pragma unroll
-      for (int kc = 0; kc < NFW; ++kc)
-        a = mma32(w0q[kc], *reinterpret_cast<const bf16x8_t*>(xs + row * XP + kc * 32 + 8 * g), a);
-      *reinterpret_cast<uint2*>(hs + row * BF_UP + 16 * ubh + 4 * g) =
-          make_uint2(relu2(pack2(a[0], a[1])), relu2(pack2(a[2], a[3])));
-    }
-  };
-
-  if constexpr (RH1) {
-    // invariant at the top of iteration i: r0..r3 = dact2 tile i+1, r5 = X tile i+2 (loaded)
-    HAR_BWD_LOAD_D(t0)
-    HAR_BWD_LOAD_X(t0)
-    HAR_BWD_STAGE_D(0)
-    HAR_BWD_STAGE_X(0)
-    HAR_BWD_LOAD_X(t0 + 1)
-    HAR_BWD_STAGE_X(1)
-    HAR_BWD_LOAD_D(t0 + 1)
-    HAR_BWD_LOAD_X(t0 + 2)
-    __builtin_amdgcn_sched_barrier(0);
-    __syncthreads();  // dact2 tile 0, X tiles 0 and 1 are in LDS
-    tile_h1(0);
-    __syncthreads();  // h1 tile 0 complete
-    for (int i = 0; i < n; ++i) {
-      if (i < 32) HAR_STAMP(8, 2 + i)
-      HAR_BWD_STAGE_D(i + 1)        // waits for the refills issued one iteration ago
-      HAR_BWD_STAGE_X(i + 2)
-      HAR_BWD_LOAD_D(t0 + i + 2)
-      HAR_BWD_LOAD_X(t0 + i + 3)
-      __builtin_amdgcn_sched_barrier(0);  // the refills are issued before the compute
-      tile_h1(i + 1);               // X tile i+1 has been in LDS since the last barrier
-      tile_ab(i);
-      if (i > 0) tile_c(i - 1);     // wave-uniform
-      __syncthreads();              // dact2 i+1 / X i+2 staged, h1 i+1 and dact1 i complete
-    }
-  } else {
-    HAR_BWD_LOAD(t0)
-    HAR_BWD_STAGE(0)
-    HAR_BWD_LOAD(t0 + 1)
-    __builtin_amdgcn_sched_barrier(0);
-    __syncthreads();  // tile 0 is in LDS
-    for (int i = 0; i < n; ++i) {
-      HAR_BWD_STAGE(i + 1)          // waits for the refill issued one iteration ago
-      HAR_BWD_LOAD(t0 + i + 2)
-      __builtin_amdgcn_sched_barrier(0);  // the refill is issued before the compute
-      tile_ab(i);
-      if (i > 0) tile_c(i - 1);     // wave-uniform
-      __syncthreads();              // tile i+1 staged; tile i's dact1 complete; buffers of i-1 free
-    }
-  }
-  HAR_STAMP(8, 34)
-  if (n > 0) tile_c(n - 1);
-#undef HAR_BWD_LOAD
-#undef HAR_BWD_LOAD_D
-#undef HAR_BWD_LOAD_X
-#undef HAR_BWD_STAGE
-#undef HAR_BWD_STAGE_D
-#undef HAR_BWD_STAGE_X
-
-  // ---- this workgroup's parts of slab `slice` ----
-  float* w1o = gw1 + (size_t)slice * slab_stride;
-#pragma unroll
-  for (int j = 0; j < 4; ++j)
-#pragma unroll
-    for (int uu = 0; uu < 2; ++uu)
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-        w1o[(size_t)(16 * (jb0 + j) + 4 * g + r) * H + qu0 + 16 * (ubp + uu) + c16] = acc1[j][uu][r];
-  float* w0o = gw0 + (size_t)slice * slab_stride;
-#pragma unroll
-  for (int f = 0; f < NFW; ++f)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) w0o[(size_t)(qu0 + 16 * ub + 4 * g + r) * K0 + 16 * (fb + f) + c16] = acc0[f][r];
-#pragma unroll
-  for (int e = 0; e < 2; ++e)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      float v = rs[e][r];
-#pragma unroll
-      for (int o = 1; o < 16; o <<= 1) v += __shfl_xor(v, o, 64);
-      if (c16 == 0) red[rb * BF_QU + 16 * (up + e) + 4 * g + r] = v;
-    }
-  __syncthreads();
-  if (tid < BF_QU)
-    gb0[(size_t)slice * slab_stride + qu0 + tid] = (red[tid] + red[BF_QU + tid]) + (red[2 * BF_QU + tid] + red[3 * BF_QU + tid]);
-  if constexpr (STAMP) __builtin_amdgcn_s_waitcnt(0x0f70);
-  HAR_STAMP(8, 35)
-  HAR_STAMP_REAL(8, 39)
-}
-
-// Training only: serving (stages 1-3) keeps v1 — without the backward stages, v2's two barriers
-// and partial-logit exchange per tile cost more than its occupancy gains (batch 1M: 0.67 vs
-// 0.43 ms on MI355X).
-bool use_v2(int H, int B) {
-  if (H != V2_H || B % V2_RT) return false;
-  const char* e = getenv("HAR_MLP_FUSED_V1");
-  return !(e && e[0] == '1');
-}
 
 }  // namespace
 
@@ -1145,10 +393,6 @@ extern "C" int har_mlp_fwd_head(const uint16_t* X, int K0, const uint16_t* W0, c
        (uintptr_t)b0 | (uintptr_t)b1 | (uintptr_t)slab) & 15)
     return -3;
   const int nwg = har_mlp_fwd_head_grid(B);
-  if (use_v2(H, B)) {
-    if (K0 == 64) return launch_v2<64>(X, W0, b0, W1, b1, Wo, bo, labels, B, C, scale, h1, dact, slab, block_loss, block_correct, nwg, s);
-    if (K0 == 32) return launch_v2<32>(X, W0, b0, W1, b1, Wo, bo, labels, B, C, scale, h1, dact, slab, block_loss, block_correct, nwg, s);
-  }
   if (H == 256 && K0 == 64) return launch<256, 64>(X, W0, b0, W1, b1, Wo, bo, labels, B, C, scale, h1, dact, slab, block_loss, block_correct, nwg, s);
   if (H == 256 && K0 == 32) return launch<256, 32>(X, W0, b0, W1, b1, Wo, bo, labels, B, C, scale, h1, dact, slab, block_loss, block_correct, nwg, s);
   if (H == 128 && K0 == 64) return launch<128, 64>(X, W0, b0, W1, b1, Wo, bo, labels, B, C, scale, h1, dact, slab, block_loss, block_correct, nwg, s);
@@ -1186,49 +430,4 @@ extern "C" int har_mlp_fwd_infer_f32(const float* X, int ldx, int F, int K0, con
   HAR_INFER_F32(256, 64) HAR_INFER_F32(256, 32) HAR_INFER_F32(128, 64) HAR_INFER_F32(128, 32)
 #undef HAR_INFER_F32
   return -4;
-}
-
-// Diagnostic: while p != nullptr the training launches of the fused forward (h1 recomputed) and
-// the fused backward (K0 = 64) run their stamped instantiations into p (>= 2 x 256 x 8 x 40
-// uint64, forward rows first); grids are at most 256 workgroups of 8 waves.
-extern "C" void har_mlp_set_stamps(uint64_t* p) { g_stamps = p; }
-
-extern "C" int har_mlp_fwd_head_variant(int H, int B) { return use_v2(H, B) ? 2 : 1; }
-
-// Row slices of the fused backward: >= 4 tiles (256 rows) per slice, <= 64 slices (one slab each).
-extern "C" int har_mlp_bwd_fused_slices(int B) { return std::max(1, std::min(64, B / BF_RT / 4)); }
-
-// dW1 / dW0 / db0 of the 2-hidden-layer step (H = 256, B % 64 == 0): per-slice partials written at
-// gw1 / gw0 / gb0 + s * slab_stride (s < har_mlp_bwd_fused_slices(B)).
-// h1 == nullptr: recompute h1 from X with W0 / b0 (the forward then skips its h1 store).
-extern "C" int har_mlp_bwd_fused(const uint16_t* dact2, const uint16_t* h1, const uint16_t* X, int K0,
-                                 const uint16_t* W1, int H, int B, float* gw1, float* gw0, float* gb0,
-                                 int64_t slab_stride, int32_t* tick, const uint16_t* W0, const float* b0,
-                                 hipStream_t s) {
-  if (H != V2_H || B <= 0 || B % BF_RT || (K0 != 32 && K0 != 64) || slab_stride < (int64_t)H * H) return -2;
-  if (((uintptr_t)dact2 | (uintptr_t)h1 | (uintptr_t)X | (uintptr_t)W1 | (uintptr_t)W0 | (uintptr_t)b0) & 15)
-    return -3;
-  if (!h1 && (!W0 || !b0)) return -4;
-  const int S = har_mlp_bwd_fused_slices(B);
-  const dim3 grid(S * BF_Q);
-  if (h1) {
-    if (K0 == 64)
-      mlp_bwd_fused_kernel<64, false><<<grid, 512, BwdLds<64, false>::bytes, s>>>(dact2, h1, X, W1, B, S, gw1, gw0,
-                                                                                  gb0, slab_stride, tick, W0, b0, nullptr);
-    else
-      mlp_bwd_fused_kernel<32, false><<<grid, 512, BwdLds<32, false>::bytes, s>>>(dact2, h1, X, W1, B, S, gw1, gw0,
-                                                                                  gb0, slab_stride, tick, W0, b0, nullptr);
-  } else if (g_stamps && K0 == 64) {
-    mlp_bwd_fused_kernel<64, true, true><<<grid, 512, BwdLds<64, true>::bytes, s>>>(
-        dact2, h1, X, W1, B, S, gw1, gw0, gb0, slab_stride, tick, W0, b0, g_stamps + STAMP_BWD_OFF);
-  } else {
-    if (K0 == 64)
-      mlp_bwd_fused_kernel<64, true><<<grid, 512, BwdLds<64, true>::bytes, s>>>(dact2, h1, X, W1, B, S, gw1, gw0,
-                                                                                gb0, slab_stride, tick, W0, b0, nullptr);
-    else
-      mlp_bwd_fused_kernel<32, true><<<grid, 512, BwdLds<32, true>::bytes, s>>>(dact2, h1, X, W1, B, S, gw1, gw0,
-                                                                                gb0, slab_stride, tick, W0, b0, nullptr);
-  }
-  HAR_CHECK_LAUNCH();
-  return 0;
 }

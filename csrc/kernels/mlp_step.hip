@@ -1,0 +1,637 @@
+// Fused training step of the flagship MLP (BASELINE.json config 3: 43-256-256-6, bf16 MFMA; SURVEY.md
+// K23), H = 256 hidden units, K0 = 32 / 64 padded inputs, <= 16 classes, batch a multiple of 64.
+// Three kernels per step: mlp_fwd3 -> mlp_bwd3 -> grad_reduce_adam (mlp.hip).
+//
+// The forward hands the backward only what it cannot recompute cheaply: the logit gradients dz
+// ([B][16] bf16, 32 B per row) and the relu' mask of h2 ([B][8] u32, 32 B per row) — 4 MB at batch
+// 65,536 instead of the 32 MB dact2 of the previous design.  The backward rebuilds each dact2 tile on
+// chip, dact2^T = (Wout^T . dz^T) * relu'(h2) (one 16x16x16 MFMA per 16 x 16 block, K = 16 classes),
+// and recomputes h1 = relu(W0 x + b0) from the X tiles it reads anyway.
+//
+// mlp_fwd3 (persistent, one 8-wave workgroup per CU, 32-row tiles).  Wave w owns hidden units
+// [32w, 32w + 32) of both layers; its slices of W0, W1 and Wout stay in registers.  Per tile:
+//   stage 1  h1^T = W0 . X^T (bias as the initial accumulator) -> LDS h1 tile        | B1
+//   stage 5  (previous tile) dWout^T += h2^T . dz over its 32 rows (operands from LDS images)
+//   stage 2  h2^T = W1 . h1^T (h1 from LDS, 16-byte reads); relu' bits of the wave's units -> mask
+//   stage 3  partial logits over the wave's 32 units -> LDS; h2 images for stage 5      | B2
+//   softmax  spread over ALL 512 lanes — lane = (row 4w + g, class c16): the 8 partials in a fixed
+//            order, max / sum over the 16 class lanes of the row, CE, argmax, dz -> LDS + global
+// Two barriers per tile and no serial section: stage 5 of a tile runs after the next tile's B1, so
+// the dz exchange needs no barrier of its own (dz and the h2 images are double-buffered).
+//
+// mlp_bwd3 (S row slices x 4 h1-unit quadrants of 64 units; 64-row tiles, one barrier per tile):
+//   dact2 tile i+1 (MFMA from dz / mask registers loaded a tile ahead) -> LDS | X tile i+2 -> LDS |
+//   h1 tile i+1 recomputed from X | (a) dact1^T = W1^T[u] . dact2^T, relu'(h1) | (b) dW1 += h1^T . dact2
+//   | (c) dW0 += dact1^T . X of tile i-1 | db1 = sum_rows dact2 (quadrant 0, a ones-row MFMA) | barrier
+// One deterministic partial per (slice, quadrant), laid out like the flat parameter buffer.
+#include <algorithm>
+#include <cstdlib>
+
+#include "common.h"
+#include "mlp_frag.h"
+#include "../har_kernels.h"
+
+using namespace mlpf;
+
+// Diagnostic phase stamps (tools/mlp_phase_probe.py --stamps): a separate STAMP instantiation of the
+// step kernels, launched only while a stamp buffer is set, has lane 0 of every wave store s_memtime
+// (shader clock) at fixed points into its own 40-slot row of that buffer (slots 38 / 39:
+// s_memrealtime at entry / exit, 100 MHz, one clock for the whole chip).  Nothing else reads them.
+uint64_t* g_har_mlp_stamps = nullptr;
+
+namespace {
+
+constexpr size_t STAMP_BWD_OFF = (size_t)256 * 8 * 40;  // the backward's rows follow the forward's
+#define HAR_STAMP(NW, k)                                                                                   \
+  if constexpr (STAMP) {                                                                                   \
+    if ((threadIdx.x & 63) == 0)                                                                           \
+      stamps[((size_t)blockIdx.x * (NW) + (threadIdx.x >> 6)) * 40 + (k)] = __builtin_amdgcn_s_memtime();  \
+  }
+#define HAR_STAMP_REAL(NW, k)                                                                                  \
+  if constexpr (STAMP) {                                                                                       \
+    if ((threadIdx.x & 63) == 0)                                                                               \
+      stamps[((size_t)blockIdx.x * (NW) + (threadIdx.x >> 6)) * 40 + (k)] = __builtin_amdgcn_s_memrealtime(); \
+  }
+
+constexpr int NCLS = 16;
+constexpr int HH = 256;
+
+// ------------------------------------------------------------------------------------------------
+// forward
+// ------------------------------------------------------------------------------------------------
+constexpr int FW = 8;                  // waves (2 per SIMD)
+constexpr int FRT = 32;                // rows per tile
+constexpr int FHP = HH + 8;            // h1 tile pitch (bf16)
+constexpr int FSP = 16 + 8;            // [32 rows][16 cols] transpose image pitch
+constexpr int FIMG = FRT * FSP;
+// partial logits of one (wave, half): lane group g's 16 lanes x 4 classes at dword 72 g + 4 c16: the
+// softmax lanes (row, class) then read 16 distinct banks per row and disjoint banks per row pair
+constexpr int ZREG = 4 * 72;
+constexpr int FWD_SLAB = NCLS * HH + NCLS;  // per workgroup: dWout rows 0..15 [16][H], dbout [16]
+constexpr size_t FWD_LDS = (size_t)FRT * FHP * 2 + (size_t)FW * 2 * ZREG * 4 + (size_t)2 * FIMG * 2 +
+                           (size_t)FW * 4 * FIMG * 2;
+
+template <int K0>
+__device__ __forceinline__ bf16x8_t ldx(const bf16_t* __restrict__ X, int row, int kc, int g) {
+  return *reinterpret_cast<const bf16x8_t*>(X + (size_t)row * K0 + kc * 32 + g * 8);
+}
+
+template <int K0, bool STAMP>
+__global__ __launch_bounds__(512) void mlp_fwd3_kernel(
+    const bf16_t* __restrict__ X, const bf16_t* __restrict__ W0, const float* __restrict__ b0,
+    const bf16_t* __restrict__ W1, const float* __restrict__ b1, const bf16_t* __restrict__ Wo,
+    const float* __restrict__ bo, const int32_t* __restrict__ labels, int B, int C, float scale,
+    uint32_t* __restrict__ dz_out, uint32_t* __restrict__ mask_out, float* __restrict__ slab,
+    float* __restrict__ block_loss, int32_t* __restrict__ block_correct, uint64_t* __restrict__ stamps) {
+  constexpr int K0C = K0 / 32, KC = HH / 32;
+  extern __shared__ __attribute__((aligned(16))) bf16_t lds[];
+  bf16_t* const h1s = lds;                                              // [32][FHP]
+  float* const zs = reinterpret_cast<float*>(h1s + FRT * FHP);          // [8 waves][2 halves][ZREG]
+  bf16_t* const dzs = reinterpret_cast<bf16_t*>(zs + FW * 2 * ZREG);    // [2 bufs][32 rows][FSP]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int c16 = lane & 15, g = lane >> 4;
+  const int u0 = wave * 32;
+  bf16_t* const img = dzs + 2 * FIMG + wave * 4 * FIMG;                 // [2 bufs][2 unit tiles][32][FSP]
+  HAR_STAMP_REAL(FW, 38)
+  HAR_STAMP(FW, 0)
+
+  // ---- this wave's weight slices, in registers for the whole kernel ----
+  bf16x8_t w0f[2][K0C], w1f[2][KC];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+#pragma unroll
+    for (int kc = 0; kc < K0C; ++kc)
+      w0f[t][kc] = *reinterpret_cast<const bf16x8_t*>(W0 + (size_t)(u0 + 16 * t + c16) * K0 + kc * 32 + g * 8);
+#pragma unroll
+    for (int kc = 0; kc < KC; ++kc)
+      w1f[t][kc] = *reinterpret_cast<const bf16x8_t*>(W1 + (size_t)(u0 + 16 * t + c16) * HH + kc * 32 + g * 8);
+  }
+  // stage-3 A fragment: Wout[class c16][u0 + 4g + j] (j < 4), [u0 + 16 + 4g + j - 4] (j >= 4): the k
+  // order of the h2 register pairs (C layout: unit 4g + r of a 16-unit tile in register r)
+  const uint2 wlo = *reinterpret_cast<const uint2*>(Wo + (size_t)c16 * HH + u0 + 4 * g);
+  const uint2 whi = *reinterpret_cast<const uint2*>(Wo + (size_t)c16 * HH + u0 + 16 + 4 * g);
+  const bf16x8_t wo3 = cat8(wlo.x, wlo.y, whi.x, whi.y);
+  float4 b0r[2], b1r[2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    b0r[t] = *reinterpret_cast<const float4*>(b0 + u0 + 16 * t + 4 * g);
+    b1r[t] = *reinterpret_cast<const float4*>(b1 + u0 + 16 * t + 4 * g);
+  }
+  // softmax lane: tile row sr = 4 wave + g (half sh, row srr of it), class c16
+  const int sr = 4 * wave + g, sh = sr >> 4, srr = sr & 15;
+  const float bo_s = c16 < C ? bo[c16] : 0.f;
+  if constexpr (STAMP) __builtin_amdgcn_s_waitcnt(0x0f70);
+  HAR_STAMP(FW, 1)
+
+  f32x4_t acc5[2] = {f32x4_t{0.f, 0.f, 0.f, 0.f}, f32x4_t{0.f, 0.f, 0.f, 0.f}};
+  float dbo = 0.f, lsum = 0.f, ncorr = 0.f;
+  const int ntiles = B / FRT;
+  int T = blockIdx.x;
+  bf16x8_t xb[2][K0C];
+  int ys = 0;
+  if (T < ntiles) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int kc = 0; kc < K0C; ++kc) xb[h][kc] = ldx<K0>(X, T * FRT + 16 * h + c16, kc, g);
+    ys = labels[T * FRT + sr];
+  }
+  int it = 0;
+  for (; T < ntiles; T += gridDim.x, ++it) {
+    const int r0 = T * FRT;
+    if (it < 32) HAR_STAMP(FW, 2 + it)
+    const int yc = ys;
+    // ---- stage 1: h1^T = W0 . X^T for this wave's units ----
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        f32x4_t a = {b0r[t].x, b0r[t].y, b0r[t].z, b0r[t].w};
+#pragma unroll
+        for (int kc = 0; kc < K0C; ++kc) a = mma32(w0f[t][kc], xb[h][kc], a);
+        *reinterpret_cast<uint2*>(h1s + (16 * h + c16) * FHP + u0 + 16 * t + 4 * g) =
+            make_uint2(relu2(pack2(a[0], a[1])), relu2(pack2(a[2], a[3])));
+      }
+    __syncthreads();  // B1: h1 tile complete; the previous tile's dz (dzs) complete
+    // prefetch the next tile (index clamped: the same loads on every path, so the waits stay counted)
+    {
+      const int Tn = min(T + (int)gridDim.x, ntiles - 1);
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int kc = 0; kc < K0C; ++kc) xb[h][kc] = ldx<K0>(X, Tn * FRT + 16 * h + c16, kc, g);
+      ys = labels[Tn * FRT + sr];
+    }
+    // ---- stage 5 of the previous tile: dWout^T += h2^T . dz over its 32 rows ----
+    if (it > 0) {
+      const bf16x8_t bz = frag_tr(dzs + ((it - 1) & 1) * FIMG, FSP, 0, lane);
+      const bf16_t* ip = img + ((it - 1) & 1) * 2 * FIMG;
+#pragma unroll
+      for (int t = 0; t < 2; ++t) acc5[t] = mma32(frag_tr(ip + t * FIMG, FSP, 0, lane), bz, acc5[t]);
+    }
+    // ---- stage 2: h2^T = W1 . h1^T (4 independent accumulators) ----
+    f32x4_t acc[2][2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int t = 0; t < 2; ++t) acc[h][t] = f32x4_t{b1r[t].x, b1r[t].y, b1r[t].z, b1r[t].w};
+#pragma unroll
+    for (int kc = 0; kc < KC; ++kc) {
+      bf16x8_t hb[2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+        hb[h] = *reinterpret_cast<const bf16x8_t*>(h1s + (16 * h + c16) * FHP + kc * 32 + 8 * g);
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int t = 0; t < 2; ++t) acc[h][t] = mma32(w1f[t][kc], hb[h], acc[h][t]);
+    }
+    uint32_t h2p[2][2][2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        h2p[h][t][0] = relu2(pack2(acc[h][t][0], acc[h][t][1]));
+        h2p[h][t][1] = relu2(pack2(acc[h][t][2], acc[h][t][3]));
+      }
+    // relu'(h2) of the wave's 32 units for rows 16h + c16 -> mask word `wave` of the row (every lane of
+    // the row stores the same word: unconditional stores keep the counted waits exact)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      uint32_t m = 0;
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          const uint32_t w2 = h2p[h][t][e];
+          m |= ((w2 & 0xffffu) ? 1u : 0u) << (16 * t + 4 * g + 2 * e);
+          m |= ((w2 >> 16) ? 1u : 0u) << (16 * t + 4 * g + 2 * e + 1);
+        }
+      m |= __shfl_xor(m, 16, 64);
+      m |= __shfl_xor(m, 32, 64);
+      mask_out[(size_t)(r0 + 16 * h + c16) * 8 + wave] = m;
+    }
+    // ---- stage 3: partial logits over this wave's 32 units ----
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const f32x4_t zp = mma32(wo3, cat8(h2p[h][0][0], h2p[h][0][1], h2p[h][1][0], h2p[h][1][1]),
+                               f32x4_t{0.f, 0.f, 0.f, 0.f});
+      *reinterpret_cast<f32x4_t*>(zs + (wave * 2 + h) * ZREG + 72 * g + 4 * c16) = zp;
+    }
+    // stage-5 images of this tile's h2 (this wave's units), consumed by the same wave next tile
+    {
+      bf16_t* ib = img + (it & 1) * 2 * FIMG;
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+          *reinterpret_cast<uint2*>(ib + t * FIMG + (16 * h + c16) * FSP + 4 * g) = make_uint2(h2p[h][t][0], h2p[h][t][1]);
+    }
+    __syncthreads();  // B2: every wave's partial logits are in
+    // ---- softmax / CE / argmax / dz: lane = (row sr, class c16) ----
+    {
+      float z = 0.f;
+#pragma unroll
+      for (int w = 0; w < FW; ++w) z += zs[(w * 2 + sh) * ZREG + 72 * (c16 >> 2) + 4 * srr + (c16 & 3)];
+      const float zz = c16 < C ? z + bo_s : -INFINITY;
+      float mx = zz;
+      int amx = c16 < C ? c16 : (1 << 30);
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) {
+        const float om = __shfl_xor(mx, o, 64);
+        const int oa = __shfl_xor(amx, o, 64);
+        const bool take = (om > mx) | ((om == mx) & (oa < amx));  // selects, no divergent branch
+        mx = take ? om : mx;
+        amx = take ? oa : amx;
+      }
+      const float e = c16 < C ? __expf(zz - mx) : 0.f;
+      float se = e;
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) se += __shfl_xor(se, o, 64);
+      const float dl = c16 < C ? (e * (1.f / se) - (c16 == yc ? 1.f : 0.f)) * scale : 0.f;
+      const bf16_t db = f2bf(dl);
+      lsum += c16 == yc ? (mx + __logf(se)) - zz : 0.f;
+      ncorr += (c16 == 0 && amx == yc) ? 1.f : 0.f;
+      dbo += bf2f(db);
+      dzs[(it & 1) * FIMG + sr * FSP + c16] = db;
+      const uint32_t other = (uint32_t)__shfl_xor((int)db, 1, 64) & 0xffffu;
+      const uint32_t pair = (c16 & 1) ? (other | ((uint32_t)db << 16)) : ((uint32_t)db | (other << 16));
+      dz_out[(size_t)(r0 + sr) * 8 + (c16 >> 1)] = pair;  // both lanes of a pair store the same word
+    }
+  }
+  HAR_STAMP(FW, 34)
+  __syncthreads();  // the last tile's dz
+  if (it > 0) {
+    const bf16x8_t bz = frag_tr(dzs + ((it - 1) & 1) * FIMG, FSP, 0, lane);
+    const bf16_t* ip = img + ((it - 1) & 1) * 2 * FIMG;
+#pragma unroll
+    for (int t = 0; t < 2; ++t) acc5[t] = mma32(frag_tr(ip + t * FIMG, FSP, 0, lane), bz, acc5[t]);
+  }
+  // ---- this workgroup's slab: dWout rows 0..15 x this wave's units, dbout; loss, #correct ----
+  float* out = slab + (size_t)blockIdx.x * FWD_SLAB;
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+    nt_store16(out + (size_t)c16 * HH + u0 + 16 * t + 4 * g, __builtin_bit_cast(u32x4_t, acc5[t]));
+  dbo += __shfl_xor(dbo, 16, 64);
+  dbo += __shfl_xor(dbo, 32, 64);
+  lsum = wave_sum(lsum);
+  ncorr = wave_sum(ncorr);
+  float* red = zs;  // free: its last reads (the softmax) precede the barrier above
+  if (g == 0) red[wave * NCLS + c16] = dbo;
+  if (lane == 0) {
+    red[FW * NCLS + wave] = lsum;
+    red[FW * NCLS + FW + wave] = ncorr;
+  }
+  __syncthreads();
+  if (tid < NCLS) {
+    float s = 0.f;
+#pragma unroll
+    for (int w = 0; w < FW; ++w) s += red[w * NCLS + tid];
+    out[NCLS * HH + tid] = s;
+  }
+  if (tid == 0) {
+    float l = 0.f, c = 0.f;
+#pragma unroll
+    for (int w = 0; w < FW; ++w) {
+      l += red[FW * NCLS + w];
+      c += red[FW * NCLS + FW + w];
+    }
+    block_loss[blockIdx.x] = l;
+    block_correct[blockIdx.x] = (int)c;
+  }
+  if constexpr (STAMP) __builtin_amdgcn_s_waitcnt(0x0f70);
+  HAR_STAMP(FW, 35)
+  HAR_STAMP_REAL(FW, 39)
+}
+
+// ------------------------------------------------------------------------------------------------
+// backward
+// ------------------------------------------------------------------------------------------------
+constexpr int BQ = 4, BQU = HH / BQ;  // 64 h1 units per workgroup
+constexpr int BRT = 64;               // rows per pipeline tile
+constexpr int BDP = HH + 16;          // dact2 tile pitch: 136 dwords (8 mod 64)
+constexpr int BUP = BQU + 16;         // h1 / dact1 quadrant tile pitch: 40 dwords
+constexpr int WQP = BQU + 8;          // prologue W1-quadrant image pitch
+
+template <int K0> struct Bwd3Lds {
+  static constexpr int XP = K0 + 16;
+  static constexpr int NXB = 4;  // X tile buffers (staged two tiles ahead; read by h1 / (c) two tiles apart)
+  static constexpr int DSM = BRT * BDP, HS = BRT * BUP, XS = BRT * XP;
+  static constexpr size_t bytes = (size_t)(2 * DSM + 2 * HS + 2 * HS + NXB * XS) * sizeof(bf16_t) +
+                                  4 * BQU * sizeof(float);
+  static_assert((size_t)HH * WQP + NCLS * HH <= (size_t)2 * DSM, "prologue images fit the dact2 buffers");
+};
+
+template <int K0, bool STAMP>
+__global__ __launch_bounds__(512) void mlp_bwd3_kernel(
+    const uint32_t* __restrict__ dz, const uint32_t* __restrict__ mask, const bf16_t* __restrict__ X,
+    const bf16_t* __restrict__ W1, const bf16_t* __restrict__ W0, const float* __restrict__ b0,
+    const bf16_t* __restrict__ Wo, int B, int S, float* __restrict__ gw1, float* __restrict__ gw0,
+    float* __restrict__ gb0, float* __restrict__ gb1, int64_t slab_stride, int32_t* __restrict__ tick,
+    uint64_t* __restrict__ stamps) {
+  using L = Bwd3Lds<K0>;
+  constexpr int NXB = L::NXB, KC = HH / 32, XP = L::XP, NFW = K0 / 32;
+  constexpr int XV = BRT * K0 / 8;  // 16-byte vectors of an X tile (512 / 256)
+  // the training step counter ticks here (one thread, before the reduction kernel reads it for Adam)
+  if (tick && blockIdx.x == 0 && threadIdx.x == 0) *tick += 1;
+  extern __shared__ __attribute__((aligned(16))) bf16_t lds[];
+  bf16_t* const dsm0 = lds;                // [2][64][BDP] dact2 tiles
+  bf16_t* const hs0 = dsm0 + 2 * L::DSM;   // [2][64][BUP] h1 quadrant tiles
+  bf16_t* const d1s0 = hs0 + 2 * L::HS;    // [2][64][BUP] dact1 quadrant tiles
+  bf16_t* const xs0 = d1s0 + 2 * L::HS;    // [NXB][64][XP] X tiles
+  float* const red = reinterpret_cast<float*>(xs0 + NXB * L::XS);  // [4][64] db0 of the row blocks
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int c16 = lane & 15, g = lane >> 4;
+  HAR_STAMP_REAL(8, 38)
+  HAR_STAMP(8, 0)
+  const int b = xcd_remap(blockIdx.x, gridDim.x);
+  const int slice = b / BQ, q = b % BQ, qu0 = q * BQU;
+  const int rb = wave & 3, up = 2 * (wave >> 2);            // (a): rows 16 rb, unit blocks up, up + 1
+  const int ubp = 2 * (wave & 1), jb0 = 4 * (wave >> 1);    // (b): unit blocks ubp, ubp + 1 x j blocks jb0..
+  const int ub = wave & 3, fb = (wave >> 2) * NFW;          // (c): unit block ub x input blocks fb..
+  const int rb2 = wave & 3, jh = wave >> 2;                 // dact2: rows 16 rb2, j in [128 jh, 128 jh + 128)
+  const int ubh = wave & 3, rbh = 2 * (wave >> 2);          // h1 recompute: unit block ubh, row blocks rbh..
+  const int ntiles = B / BRT, per = (ntiles + S - 1) / S;
+  const int t0 = slice * per, n = max(0, min(ntiles, t0 + per) - t0);
+
+  // ---- prologue: the W1 quadrant columns and Wout through LDS (coalesced rows in, transposed
+  // fragment reads out), then the recompute's W0 rows ----
+  bf16_t* const wq = lds;                  // [256 j][WQP]: W1[j][qu0 .. qu0 + 64)
+  bf16_t* const wos = wq + HH * WQP;       // [16][256] Wout
+#pragma unroll
+  for (int v = tid; v < HH * (BQU / 8); v += 512) {  // every load issued before the first LDS store
+    const int j = v / (BQU / 8), c = (v % (BQU / 8)) * 8;
+    *reinterpret_cast<uint4*>(wq + j * WQP + c) = *reinterpret_cast<const uint4*>(W1 + (size_t)j * HH + qu0 + c);
+  }
+#pragma unroll
+  for (int v = tid; v < NCLS * HH / 8; v += 512)
+    *reinterpret_cast<uint4*>(wos + v * 8) = *reinterpret_cast<const uint4*>(Wo + (size_t)v * 8);
+  bf16x8_t w0q[NFW];
+#pragma unroll
+  for (int kc = 0; kc < NFW; ++kc)
+    w0q[kc] = *reinterpret_cast<const bf16x8_t*>(W0 + (size_t)(qu0 + 16 * ubh + c16) * K0 + kc * 32 + 8 * g);
+  const float4 b0q = *reinterpret_cast<const float4*>(b0 + qu0 + 16 * ubh + 4 * g);
+  __syncthreads();
+  // (a) A fragments: A[u][k = j] = W1[32 kc + 8g + i][qu0 + 16 (up + e) + c16] (natural k order)
+  bf16x8_t w1t[2][KC];
+#pragma unroll
+  for (int e = 0; e < 2; ++e)
+#pragma unroll
+    for (int kc = 0; kc < KC; ++kc) w1t[e][kc] = frag_tr(wq + 32 * kc * WQP, WQP, 16 * (up + e), lane);
+  // dact2 A fragments (16x16x16): A[m = j][k = class] = Wout[4g + i][128 jh + 16 jt + c16]
+  s16x4_t woa[8];
+#pragma unroll
+  for (int jt = 0; jt < 8; ++jt)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) woa[jt][i] = (short)wos[(4 * g + i) * HH + 128 * jh + 16 * jt + c16];
+  // db1 (quadrant 0): A = a row of ones (row 0 of the 16 x 32 tile)
+  const bf16x8_t ones = __builtin_bit_cast(bf16x8_t, c16 == 0 ? s16x8_t{0x3f80, 0x3f80, 0x3f80, 0x3f80, 0x3f80,
+                                                                        0x3f80, 0x3f80, 0x3f80}
+                                                              : s16x8_t{0, 0, 0, 0, 0, 0, 0, 0});
+  if constexpr (STAMP) __builtin_amdgcn_s_waitcnt(0x0f70);
+  HAR_STAMP(8, 1)
+  __syncthreads();  // the prologue images are read: the tile buffers may be written
+
+  f32x4_t acc1[4][2], acc0[NFW], accb[2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) acc1[i][0] = acc1[i][1] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int f = 0; f < NFW; ++f) acc0[f] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  accb[0] = accb[1] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  float rs[2][4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+
+  // Register staging: one dz piece (8 B: classes 4g.. of row 16 rb2 + c16) + one mask piece (16 B:
+  // words 4 jh.. of the row) + one X vector per thread per tile.  Every load is unconditional (a tile
+  // index past the slice is clamped to a valid tile that is staged but never used), so the compiler's
+  // vmcnt accounting is exact on every path.
+  const int tlast = ntiles - 1;
+  const uint32_t* ldz = dz + (size_t)(16 * rb2 + c16) * 8 + 2 * g;
+  const uint32_t* lmk = mask + (size_t)(16 * rb2 + c16) * 8 + 4 * jh;
+  const bf16_t* lx = X + (size_t)(tid & (XV - 1)) * 8;
+  const int sdx = ((tid & (XV - 1)) / (K0 / 8)) * XP + ((tid & (XV - 1)) % (K0 / 8)) * 8;
+  uint2 dzr;
+  uint4 mkr, xr;
+#define HAR_B3_LOAD_D(t)                                                        \
+  {                                                                             \
+    const int64_t tt_ = min(t, tlast);                                          \
+    dzr = *reinterpret_cast<const uint2*>(ldz + tt_ * BRT * 8);                 \
+    mkr = *reinterpret_cast<const uint4*>(lmk + tt_ * BRT * 8);                 \
+  }
+#define HAR_B3_LOAD_X(t) xr = *reinterpret_cast<const uint4*>(lx + (int64_t)min(t, tlast) * BRT * K0);
+#define HAR_B3_STAGE_X(i) *reinterpret_cast<uint4*>(xs0 + ((i) % NXB) * L::XS + sdx) = xr;
+
+  // dact2 tile from the dz / mask registers -> LDS buffer `buf` (row-major [r][j])
+  auto stage_dact2 = [&](int buf) __attribute__((always_inline)) {
+    bf16_t* d = dsm0 + buf * L::DSM + (16 * rb2 + c16) * BDP + 128 * jh + 4 * g;
+    const s16x4_t dzv = __builtin_bit_cast(s16x4_t, dzr);
+    const uint32_t mw[4] = {mkr.x, mkr.y, mkr.z, mkr.w};
+#pragma unroll
+    for (int jt = 0; jt < 8; ++jt) {
+      const f32x4_t v = mma16(woa[jt], dzv, f32x4_t{0.f, 0.f, 0.f, 0.f});  // rows j = 16 jt + 4g + r, col row c16
+      const uint32_t m = mw[jt >> 1] >> (16 * (jt & 1) + 4 * g);
+      const float d0 = (m & 1u) ? v[0] : 0.f, d1 = (m & 2u) ? v[1] : 0.f;
+      const float d2 = (m & 4u) ? v[2] : 0.f, d3 = (m & 8u) ? v[3] : 0.f;
+      *reinterpret_cast<uint2*>(d + 16 * jt) = make_uint2(pack2(d0, d1), pack2(d2, d3));
+    }
+  };
+
+  // (a) + (b) (+ db1) of local tile i (LDS buffers i & 1)
+  auto tile_ab = [&](int i) __attribute__((always_inline)) {
+    const bf16_t* dsm = dsm0 + (i & 1) * L::DSM;
+    const bf16_t* hs = hs0 + (i & 1) * L::HS;
+    bf16_t* d1s = d1s0 + (i & 1) * L::HS;
+    f32x4_t a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kc = 0; kc < KC; ++kc) {
+      const bf16x8_t bv = *reinterpret_cast<const bf16x8_t*>(dsm + (16 * rb + c16) * BDP + kc * 32 + 8 * g);
+      a0 = mma32(w1t[0][kc], bv, a0);
+      a1 = mma32(w1t[1][kc], bv, a1);
+    }
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const f32x4_t& a = e ? a1 : a0;
+      const int col = 16 * (up + e) + 4 * g;
+      const uint2 m = *reinterpret_cast<const uint2*>(hs + (16 * rb + c16) * BUP + col);
+      const float d0 = (m.x & 0xffffu) ? a[0] : 0.f, d1 = (m.x >> 16) ? a[1] : 0.f;
+      const float d2 = (m.y & 0xffffu) ? a[2] : 0.f, d3 = (m.y >> 16) ? a[3] : 0.f;
+      const uint32_t p0 = pack2(d0, d1), p1 = pack2(d2, d3);
+      rs[e][0] += __uint_as_float(p0 << 16);
+      rs[e][1] += __uint_as_float(p0 & 0xffff0000u);
+      rs[e][2] += __uint_as_float(p1 << 16);
+      rs[e][3] += __uint_as_float(p1 & 0xffff0000u);
+      *reinterpret_cast<uint2*>(d1s + (16 * rb + c16) * BUP + col) = make_uint2(p0, p1);
+    }
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const bf16x8_t hb0 = frag_rows(hs + 32 * ks * BUP, BUP, 16 * ubp, lane);
+      const bf16x8_t hb1 = frag_rows(hs + 32 * ks * BUP, BUP, 16 * (ubp + 1), lane);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const bf16x8_t da = frag_rows(dsm + 32 * ks * BDP, BDP, 16 * (jb0 + j), lane);
+        acc1[j][0] = mma32(hb0, da, acc1[j][0]);  // C[u][j]: 4 consecutive units per lane
+        acc1[j][1] = mma32(hb1, da, acc1[j][1]);
+      }
+    }
+    if (q == 0) {  // workgroup-uniform: db1 = sum over the rows of dact2 (row 0 of ones . dact2)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int e = 0; e < 2; ++e)
+          accb[e] = mma32(ones, frag_rows(dsm + 32 * ks * BDP, BDP, 16 * (2 * wave + e), lane), accb[e]);
+    }
+  };
+  // (c) of local tile i (its dact1 buffer i & 1, X buffer i % NXB)
+  auto tile_c = [&](int i) __attribute__((always_inline)) {
+    const bf16_t* d1s = d1s0 + (i & 1) * L::HS;
+    const bf16_t* xs = xs0 + (i % NXB) * L::XS;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const bf16x8_t A = frag_rows(d1s + 32 * ks * BUP, BUP, 16 * ub, lane);
+#pragma unroll
+      for (int f = 0; f < NFW; ++f) acc0[f] = mma32(A, frag_rows(xs + 32 * ks * XP, XP, 16 * (fb + f), lane), acc0[f]);
+    }
+  };
+  // h1 quadrant tile i from X tile i (buffer i % NXB) into h1 buffer i & 1: the forward's operands,
+  // accumulation order and rounding (bit-identical h1)
+  auto tile_h1 = [&](int i) __attribute__((always_inline)) {
+    const bf16_t* xs = xs0 + (i % NXB) * L::XS;
+    bf16_t* hs = hs0 + (i & 1) * L::HS;
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int row = 16 * (rbh + e) + c16;
+      f32x4_t a = {b0q.x, b0q.y, b0q.z, b0q.w};
+#pragma unroll
+      for (int kc = 0; kc < NFW; ++kc) a = mma32(w0q[kc], *reinterpret_cast<const bf16x8_t*>(xs + row * XP + kc * 32 + 8 * g), a);
+      *reinterpret_cast<uint2*>(hs + row * BUP + 16 * ubh + 4 * g) =
+          make_uint2(relu2(pack2(a[0], a[1])), relu2(pack2(a[2], a[3])));
+    }
+  };
+
+  // invariant at the top of iteration i: dzr / mkr = tile i+1, xr = X tile i+2 (loaded)
+  HAR_B3_LOAD_D(t0)
+  HAR_B3_LOAD_X(t0)
+  stage_dact2(0);
+  HAR_B3_STAGE_X(0)
+  HAR_B3_LOAD_X(t0 + 1)
+  HAR_B3_STAGE_X(1)
+  HAR_B3_LOAD_D(t0 + 1)
+  HAR_B3_LOAD_X(t0 + 2)
+  __builtin_amdgcn_sched_barrier(0);
+  __syncthreads();  // dact2 tile 0, X tiles 0 and 1 are in LDS
+  tile_h1(0);
+  __syncthreads();  // h1 tile 0 complete
+  for (int i = 0; i < n; ++i) {
+    if (i < 32) HAR_STAMP(8, 2 + i)
+    stage_dact2((i + 1) & 1);       // waits for the dz / mask loads issued one iteration ago
+    HAR_B3_STAGE_X(i + 2)
+    HAR_B3_LOAD_D(t0 + i + 2)
+    HAR_B3_LOAD_X(t0 + i + 3)
+    __builtin_amdgcn_sched_barrier(0);  // the refills are issued before the compute
+    tile_h1(i + 1);                 // X tile i+1 has been in LDS since the last barrier
+    tile_ab(i);
+    if (i > 0) tile_c(i - 1);       // wave-uniform
+    __syncthreads();                // dact2 i+1 / X i+2 staged, h1 i+1 and dact1 i complete
+  }
+  HAR_STAMP(8, 34)
+  if (n > 0) tile_c(n - 1);
+#undef HAR_B3_LOAD_D
+#undef HAR_B3_LOAD_X
+#undef HAR_B3_STAGE_X
+
+  // ---- this workgroup's parts of slab `slice` (flat parameter layout) ----
+  float* w1o = gw1 + (size_t)slice * slab_stride;
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int uu = 0; uu < 2; ++uu)
+      *reinterpret_cast<f32x4_t*>(w1o + (size_t)(16 * (jb0 + j) + c16) * HH + qu0 + 16 * (ubp + uu) + 4 * g) =
+          acc1[j][uu];
+  float* w0o = gw0 + (size_t)slice * slab_stride;
+#pragma unroll
+  for (int f = 0; f < NFW; ++f)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) w0o[(size_t)(qu0 + 16 * ub + 4 * g + r) * K0 + 16 * (fb + f) + c16] = acc0[f][r];
+  if (q == 0 && g == 0) {
+#pragma unroll
+    for (int e = 0; e < 2; ++e) gb1[(size_t)slice * slab_stride + 16 * (2 * wave + e) + c16] = accb[e][0];
+  }
+#pragma unroll
+  for (int e = 0; e < 2; ++e)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float v = rs[e][r];
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) v += __shfl_xor(v, o, 64);
+      if (c16 == 0) red[rb * BQU + 16 * (up + e) + 4 * g + r] = v;
+    }
+  __syncthreads();
+  if (tid < BQU)
+    gb0[(size_t)slice * slab_stride + qu0 + tid] = (red[tid] + red[BQU + tid]) + (red[2 * BQU + tid] + red[3 * BQU + tid]);
+  if constexpr (STAMP) __builtin_amdgcn_s_waitcnt(0x0f70);
+  HAR_STAMP(8, 35)
+  HAR_STAMP_REAL(8, 39)
+}
+
+template <int K0>
+void launch_fwd3(const bf16_t* X, const bf16_t* W0, const float* b0, const bf16_t* W1, const float* b1,
+                 const bf16_t* Wo, const float* bo, const int32_t* labels, int B, int C, float scale, uint32_t* dz,
+                 uint32_t* mask, float* slab, float* bl, int32_t* bc, int nwg, hipStream_t s) {
+  auto k = g_har_mlp_stamps ? mlp_fwd3_kernel<K0, true> : mlp_fwd3_kernel<K0, false>;
+  k<<<nwg, 512, FWD_LDS, s>>>(X, W0, b0, W1, b1, Wo, bo, labels, B, C, scale, dz, mask, slab, bl, bc, g_har_mlp_stamps);
+}
+
+template <int K0>
+void launch_bwd3(const uint32_t* dz, const uint32_t* mask, const bf16_t* X, const bf16_t* W1, const bf16_t* W0,
+                 const float* b0, const bf16_t* Wo, int B, int S, float* gw1, float* gw0, float* gb0, float* gb1,
+                 int64_t stride, int32_t* tick, hipStream_t s) {
+  auto k = g_har_mlp_stamps ? mlp_bwd3_kernel<K0, true> : mlp_bwd3_kernel<K0, false>;
+  k<<<S * BQ, 512, Bwd3Lds<K0>::bytes, s>>>(dz, mask, X, W1, W0, b0, Wo, B, S, gw1, gw0, gb0, gb1, stride, tick,
+                                           g_har_mlp_stamps ? g_har_mlp_stamps + STAMP_BWD_OFF : nullptr);
+}
+
+}  // namespace
+
+extern "C" int har_mlp_step_grid(int B) { return std::max(1, std::min(256, B / FRT)); }
+extern "C" int har_mlp_step_slices(int B) { return std::max(1, std::min(64, B / BRT / 4)); }
+extern "C" int har_mlp_step_fwd_slab_width(int H) { return NCLS * H + NCLS; }
+
+// Forward of the step: dz [B][8] u32 (bf16 pairs, 16 classes), relu'(h2) mask [B][8] u32, and per
+// workgroup (har_mlp_step_grid(B) of them) dWout rows 0..15 + dbout (width har_mlp_step_fwd_slab_width),
+// loss and #correct.
+extern "C" int har_mlp_step_fwd(const uint16_t* X, int K0, const uint16_t* W0, const float* b0, const uint16_t* W1,
+                                const float* b1, int H, const uint16_t* Wo, const float* bo, const int32_t* labels,
+                                int B, int C, float scale, uint32_t* dz, uint32_t* mask, float* slab,
+                                float* block_loss, int32_t* block_correct, hipStream_t s) {
+  if (H != HH || (K0 != 32 && K0 != 64) || B <= 0 || B % 64 || C < 1 || C > NCLS) return -2;
+  if (((uintptr_t)X | (uintptr_t)W0 | (uintptr_t)W1 | (uintptr_t)Wo | (uintptr_t)b0 | (uintptr_t)b1 |
+       (uintptr_t)slab | (uintptr_t)dz | (uintptr_t)mask) & 15)
+    return -3;
+  const int nwg = har_mlp_step_grid(B);
+  if (K0 == 64)
+    launch_fwd3<64>(X, W0, b0, W1, b1, Wo, bo, labels, B, C, scale, dz, mask, slab, block_loss, block_correct, nwg, s);
+  else
+    launch_fwd3<32>(X, W0, b0, W1, b1, Wo, bo, labels, B, C, scale, dz, mask, slab, block_loss, block_correct, nwg, s);
+  HAR_CHECK_LAUNCH();
+  return 0;
+}
+
+// Backward of the step: per row slice s < har_mlp_step_slices(B) the partials of dW1, dW0, db0 (and db1)
+// at gw1 / gw0 / gb0 / gb1 + s * slab_stride.
+extern "C" int har_mlp_step_bwd(const uint32_t* dz, const uint32_t* mask, const uint16_t* X, int K0,
+                                const uint16_t* W1, int H, const uint16_t* W0, const float* b0, const uint16_t* Wo,
+                                int B, float* gw1, float* gw0, float* gb0, float* gb1, int64_t slab_stride,
+                                int32_t* tick, hipStream_t s) {
+  if (H != HH || B <= 0 || B % BRT || (K0 != 32 && K0 != 64) || slab_stride < (int64_t)H * H) return -2;
+  if (((uintptr_t)dz | (uintptr_t)mask | (uintptr_t)X | (uintptr_t)W1 | (uintptr_t)W0 | (uintptr_t)b0 |
+       (uintptr_t)Wo | (uintptr_t)gw1) & 15)
+    return -3;
+  const int S = har_mlp_step_slices(B);
+  if (K0 == 64)
+    launch_bwd3<64>(dz, mask, X, W1, W0, b0, Wo, B, S, gw1, gw0, gb0, gb1, slab_stride, tick, s);
+  else
+    launch_bwd3<32>(dz, mask, X, W1, W0, b0, Wo, B, S, gw1, gw0, gb0, gb1, slab_stride, tick, s);
+  HAR_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" void har_mlp_set_stamps(uint64_t* p) { g_har_mlp_stamps = p; }

@@ -174,13 +174,13 @@ def _bf_round(x):
     return x.to(torch.bfloat16).float()
 
 
-def test_mlp_step_matches_torch(cuda):
+@pytest.mark.parametrize("layers,B,path", [([43, 64, 96, 6], 512, "gemm"), ([43, 256, 256, 6], 4096, "step")])
+def test_mlp_step_matches_torch(cuda, layers, B, path):
     """Native step gradients vs a manual fp32 backprop that rounds to bf16 at the same
-    points as the kernels (activations, dlogits, data grads, weight copies)."""
+    points as the kernels (activations, dlogits, data grads, weight copies): the generic GEMM
+    path and the flagship three-kernel step."""
     from har.models.mlp import MLPEngine, pad_input_bf16
 
-    B = 512
-    layers = [43, 64, 96, 6]
     eng = MLPEngine(layers, B, cuda, lr=1e-3, seed=3)
     g = torch.Generator(device=cuda).manual_seed(9)
     X = torch.randn(B, 43, device=cuda, generator=g)
@@ -188,6 +188,7 @@ def test_mlp_step_matches_torch(cuda):
     Xb = pad_input_bf16(X, eng.layout.in_pad)
     eng.forward_backward_native(Xb, y.to(torch.int32), 1.0 / B)
     eng.reduce_grads_native()
+    assert eng.last_path == path
     L = eng.layout
     P = eng.P.double()
     W = {s.name: L.view(P, s.name) for s in L.segments}
@@ -311,11 +312,10 @@ def test_column_stats_and_binning(cuda):
 def test_mlp_fused_fwd_head_matches_unfused(cuda, monkeypatch, H, F):
     """mlp_fused.hip (fwd L1 + fwd L2 + head + dWout/dbout in one kernel) against the unfused
     kernel chain: same h1 / dact2 / reduced gradients / loss up to bf16 summation-order noise
-    (h1 stored by the forward here so it can be compared; the default recomputes it in the backward)."""
-    from har.models import mlp as mlp_mod
+    (HAR_MLP_STEP=0: the fused forward + GEMM backward path, the one that writes h1 / dact2)."""
     from har.models.mlp import MLPEngine, pad_input_bf16
 
-    monkeypatch.setattr(mlp_mod, "RECOMPUTE_H1", False)
+    monkeypatch.setenv("HAR_MLP_STEP", "0")
 
     B = 4096
     layers = [F, H, H, 6]
@@ -351,29 +351,62 @@ def test_mlp_fused_fwd_head_matches_unfused(cuda, monkeypatch, H, F):
     assert not a.last_fused
 
 
-@pytest.mark.parametrize("F,B", [(43, 4096), (20, 4160), (43, 65536)])
-def test_mlp_backward_h1_recompute_is_bit_identical(cuda, monkeypatch, F, B):
-    """The fused backward recomputing h1 = relu(W0 x + b0) from its X tiles (forward skips the h1
-    store) produces exactly the gradients and parameters of the stored-h1 path: the recompute uses
-    the forward's operands, accumulation order and rounding.  K0 = 64 and 32, a batch that is not a
-    multiple of the slice size, and the flagship batch."""
-    from har.models import mlp as mlp_mod
+@pytest.mark.parametrize("F,B", [(43, 4096), (20, 4160), (43, 8256), (43, 65536)])
+def test_mlp_step_matches_gemm_path_and_is_deterministic(cuda, monkeypatch, F, B):
+    """The three-kernel step (mlp_step.hip: forward -> dz + relu' mask, backward rebuilding dact2 and
+    h1 on chip) against the fused forward + split-K GEMM backward on the same batch: reduced
+    gradients, loss and #correct agree to bf16 summation-order noise; K0 = 64 and 32, a batch whose
+    last row slices are short (8256), the flagship batch.  Two runs of the step are bit-identical."""
     from har.models.mlp import MLPEngine, pad_input_bf16
 
-    g = torch.Generator(device=cuda).manual_seed(3)
-    X = pad_input_bf16(torch.randn(B, F, device=cuda, generator=g), MLPEngine([F, 256, 256, 6], B, cuda).layout.in_pad)
+    g = torch.Generator(device=cuda).manual_seed(13)
+    X = torch.randn(B, F, device=cuda, generator=g)
     y = torch.randint(0, 6, (B,), device=cuda, generator=g).to(torch.int32)
-    out = {}
-    for rh in (False, True):
-        monkeypatch.setattr(mlp_mod, "RECOMPUTE_H1", rh)
-        e = MLPEngine([F, 256, 256, 6], B, cuda, lr=1e-3, seed=8)
-        for _ in range(3):
-            e.train_step(X, y, B)
+    runs = []
+    for flag in ("1", "1", "0"):
+        monkeypatch.setenv("HAR_MLP_STEP", flag)
+        e = MLPEngine([F, 256, 256, 6], B, cuda, lr=1e-3, seed=7)
+        Xb = pad_input_bf16(X, e.layout.in_pad)
+        e.forward_backward_native(Xb, y, 1.0 / B)
+        e.reduce_grads_native()
         torch.cuda.synchronize()
-        assert e.last_fused and e.last_bwd
-        out[rh] = (e.G.clone(), e.P.clone())
-    assert torch.equal(out[False][0], out[True][0])
-    assert torch.equal(out[False][1], out[True][1])
+        assert (e.last_path == "step") == (flag == "1")
+        runs.append((e.G.clone(), e.last_loss_and_correct(), e.layout))
+    (g1, lc1, L), (g2, lc2, _), (gr, lcr, _) = runs
+    assert torch.equal(g1, g2) and lc1 == lc2
+    for s_ in L.segments:
+        a, b = L.view(g1, s_.name), L.view(gr, s_.name)
+        rel = float((a - b).norm() / b.norm().clamp_min(1e-12))
+        assert rel < 1e-2, f"{s_.name}: {rel:.3e}"
+    assert abs(lc1[0] - lcr[0]) / lcr[0] < 1e-3 and abs(lc1[1] - lcr[1]) <= 2
+
+
+def test_mlp_step_outputs(cuda):
+    """What the step forward hands the backward: dz = (softmax - onehot) * scale in bf16 and the
+    relu' bits of h2, against the fp32 PyTorch forward of the same (bf16-rounded) parameters."""
+    from har.models.mlp import MLPEngine, pad_input_bf16
+
+    B, F = 4096, 43
+    e = MLPEngine([F, 256, 256, 6], B, cuda, lr=1e-3, seed=3)
+    g = torch.Generator(device=cuda).manual_seed(5)
+    X = pad_input_bf16(torch.randn(B, F, device=cuda, generator=g), 64)
+    y = torch.randint(0, 6, (B,), device=cuda, generator=g).to(torch.int32)
+    e.forward_backward_native(X, y, 1.0 / B)
+    torch.cuda.synchronize()
+    assert e.last_path == "step"
+    P = e.Pb.float()
+    L = e.layout
+    h1 = torch.relu(X.float() @ L.view(P, "W0").T + L.view(e.P, "b0")).bfloat16().float()
+    h2 = torch.relu(h1 @ L.view(P, "W1").T + L.view(e.P, "b1"))
+    z = h2.bfloat16().float() @ L.view(P, "Wout")[:6].T + L.view(e.P, "bout")[:6]
+    ref_dz = (torch.softmax(z, 1) - torch.nn.functional.one_hot(y.long(), 6).float()) / B
+    dz = e.dz.view(B, 8).view(torch.bfloat16).float()  # [B][16] bf16
+    assert float(dz[:, 6:].abs().max()) == 0.0
+    assert float((dz[:, :6] - ref_dz).norm() / ref_dz.norm()) < 2e-2
+    bits = e.h2mask.view(B, 8)
+    got = ((bits.unsqueeze(2) >> torch.arange(32, device=cuda, dtype=torch.int32)) & 1).reshape(B, 256).bool()
+    agree = float((got == (h2 > 0)).float().mean())
+    assert agree > 0.995  # bf16 rounding flips a few near-zero units
 
 
 @pytest.mark.parametrize("H,F", [(256, 43), (128, 20)])
@@ -399,67 +432,6 @@ def test_mlp_fused_infer_matches_fp32(cuda, H, F):
     torch.testing.assert_close(lf, logits)
     assert torch.equal(pf, pred)
     torch.testing.assert_close(eng.logits(X), logits)  # logits() takes the fused fp32 path
-
-
-def test_mlp_fused_v2_matches_v1(cuda, monkeypatch):
-    """The 8-wave fused forward (W1 distributed over the waves' registers, H = 256) against the
-    4-wave LDS-resident-W1 kernel on the same batch: same h1, dact2, gradient slabs and loss up
-    to bf16 / summation-order noise (HAR_MLP_FUSED_V1 selects the kernel per launch; h1 stored by
-    the forward so it can be compared)."""
-    from har.models import mlp as mlp_mod
-    from har.models.mlp import MLPEngine, pad_input_bf16
-
-    monkeypatch.setattr(mlp_mod, "RECOMPUTE_H1", False)
-
-    B, H, F = 8192, 256, 43
-    g = torch.Generator(device=cuda).manual_seed(12)
-    X = pad_input_bf16(torch.randn(B, F, device=cuda, generator=g), 64)
-    y = torch.randint(0, 6, (B,), device=cuda, generator=g).to(torch.int32)
-    outs = []
-    for v1 in ("1", "0"):
-        monkeypatch.setenv("HAR_MLP_FUSED_V1", v1)
-        e = MLPEngine([F, H, H, 6], B, cuda, lr=1e-3, seed=5)
-        e.forward_backward_native(X, y, 1.0 / B)
-        e.reduce_grads_native()
-        torch.cuda.synchronize()
-        assert e.last_fused
-        outs.append((e.acts[1].float().clone(), e.dbuf[1][: B * H].float().clone(), e.G.clone(),
-                     e.last_loss_and_correct(), e))
-    (h_a, d_a, g_a, (l_a, c_a), ea), (h_b, d_b, g_b, (l_b, c_b), eb) = outs
-    assert torch.equal(h_a, h_b)  # stage 1 is the same bf16 product in both kernels
-    assert (d_a - d_b).norm() / d_b.norm() < 1e-2
-    for s in ea.layout.segments:
-        ga, gb = ea.layout.view(g_a, s.name), ea.layout.view(g_b, s.name)
-        assert float((ga - gb).norm() / gb.norm().clamp_min(1e-12)) < 1e-2, s.name
-    assert abs(l_a - l_b) / l_b < 1e-4 and abs(c_a - c_b) <= 2
-
-
-@pytest.mark.parametrize("F,B", [(43, 8192), (20, 8192), (43, 8256)])
-def test_mlp_bwd_fused_matches_gemms(cuda, monkeypatch, F, B):
-    """Fused backward (dW1 + dgrad + relu' + dW0 / db0 in one kernel, dact1 on chip, db1 from the
-    forward kernel) against the split-K dW1 GEMM + dgrad GEMM + dW0 GEMM chain on the same
-    fused-forward outputs; B = 8256 leaves the last row slices short / empty."""
-    from har.models.mlp import MLPEngine, pad_input_bf16
-
-    H = 256
-    g = torch.Generator(device=cuda).manual_seed(13)
-    X = torch.randn(B, F, device=cuda, generator=g)
-    y = torch.randint(0, 6, (B,), device=cuda, generator=g).to(torch.int32)
-    Gs = []
-    for flag in ("0", "1"):
-        monkeypatch.setenv("HAR_MLP_BWD_FUSED", flag)
-        e = MLPEngine([F, H, H, 6], B, cuda, lr=1e-3, seed=7)
-        Xb = pad_input_bf16(X, e.layout.in_pad)
-        e.forward_backward_native(Xb, y, 1.0 / B)
-        e.reduce_grads_native()
-        torch.cuda.synchronize()
-        assert e.last_bwd == (flag == "1")
-        Gs.append((e.G.clone(), e.layout))
-    (ga, L), (gb, _) = Gs
-    for s in L.segments:
-        a, b = L.view(ga, s.name), L.view(gb, s.name)
-        rel = float((a - b).norm() / b.norm().clamp_min(1e-12))
-        assert rel < 1e-2, f"{s.name}: {rel:.3e}"
 
 
 def test_find_thresholds_device_matches_numpy():

@@ -59,7 +59,7 @@ def main():
                           [(f"region {i} reduce+store", [rg], R | S) for i, rg in enumerate(regs)]:
         med, mn = timed(lambda: call(rs, mode))
         print(f"{name:28s} median {med:7.1f} us  min {mn:7.1f} us")
-    n_bwd = eng.bwd_S
+    n_bwd = eng.step_S
     w0, b1o = eng.layout.by_name["W0"].offset, eng.layout.by_name["b1"].offset
     sl = eng.slabs[:n_bwd, w0:b1o]
     out = torch.empty(sl.shape[1], device=dev)
