@@ -454,6 +454,12 @@ class MLPEngine:
 
     def grad_phase(self, Xb: torch.Tensor, yb: torch.Tensor, global_batch: int):
         """DP step, part 1 (graph-capturable): fwd + bwd + deterministic slab reduction into G."""
+        if self._plan_ok(Xb, yb):
+            B = Xb.shape[0]
+            plan, self.step_nwg, self.step_S = self._plan(B)
+            self.last_path, self.last_fused, self.last_bwd, self.last_batch = "step", True, True, B
+            plan.run(Xb.data_ptr(), yb.data_ptr(), B, 1.0 / global_batch, 2, _native.stream_ptr())
+            return
         self.forward_backward_native(Xb, yb, 1.0 / global_batch)
         self.reduce_grads_native()
 
@@ -462,10 +468,51 @@ class MLPEngine:
         all-reduce, issued eagerly between the two graph replays)."""
         self.optimizer_step_native()
 
+    def _plan(self, B: int):
+        """The native step plan (bind.cpp MlpStepPlan) of the three-kernel step at batch B: every
+        pointer, gradient region and hyper-parameter fixed once, so a step is ONE host call."""
+        plans = self.__dict__.setdefault("_plans", {})
+        if B not in plans:
+            L, mod = self.layout, _native.kernels()
+            self.step_nwg, self.step_S = mod.mlp_step_grid(B), mod.mlp_step_slices(B)
+            self.last_path, self.last_fused, self.last_bwd = "step", True, True
+            sb = self.slabs.data_ptr()
+            off = lambda n: sb + 4 * L.by_name[n].offset  # noqa: E731
+            w = lambda t, n: self._w(t, n).data_ptr()  # noqa: E731
+            P, Pb = self.P, self.Pb
+            d = dict(W0=w(Pb, "W0"), b0=w(P, "b0"), W1=w(Pb, "W1"), b1=w(P, "b1"), Wo=w(Pb, "Wout"), bo=w(P, "bout"),
+                     dz=self.dz.data_ptr(), mask=self.h2mask.data_ptr(), fslab=self.sslab.data_ptr(),
+                     bloss=self.sblock_loss.data_ptr(), bcorr=self.sblock_correct.data_ptr(), gw1=off("W1"),
+                     gw0=off("W0"), gb0=off("b0"), gb1=off("b1"), step=self.step_count.data_ptr(),
+                     G=self.G.data_ptr(), P=P.data_ptr(), m=self.m.data_ptr(), v=self.v.data_ptr(), Pb=Pb.data_ptr(),
+                     K0=L.in_pad, H=self.dims[-1], C=L.num_classes, stride=L.total, n=L.total, lr=float(self.lr),
+                     beta1=float(self.betas[0]), beta2=float(self.betas[1]), eps=float(self.eps), wd=float(self.wd),
+                     regions=[(a, e, p, ns, ld) for a, e, p, ns, ld in self._grad_regions()])
+            plans[B] = (mod.MlpStepPlan(d), self.step_nwg, self.step_S)
+        return plans[B]
+
+    def _plan_ok(self, Xb, yb):
+        return (self.step_ok and Xb.shape[0] % 64 == 0 and Xb.shape[0] <= self.B and Xb.shape[1] == self.layout.in_pad
+                and Xb.dtype == torch.bfloat16 and yb.dtype == torch.int32 and Xb.is_contiguous()
+                and os.environ.get("HAR_MLP_PLAN", "1") != "0")
+
     def train_step(self, Xb: torch.Tensor, yb: torch.Tensor, global_batch: int):
         """One step.  Native: fwd kernel + bwd kernel + ONE reduction kernel; at N = 1 the Adam
         update is fused into that kernel, at N > 1 it stores G, one RCCL all-reduce of G follows and
-        Adam runs from G — the same kernels and the same summation order at every N."""
+        Adam runs from G — the same kernels and the same summation order at every N.  The
+        three-kernel step goes through the native plan (one host call per phase)."""
+        if self.native and self._plan_ok(Xb, yb):
+            B = Xb.shape[0]
+            plan, self.step_nwg, self.step_S = self._plan(B)
+            self.last_path, self.last_fused, self.last_bwd, self.last_batch = "step", True, True, B
+            s = _native.stream_ptr()
+            if self.world > 1:
+                plan.run(Xb.data_ptr(), yb.data_ptr(), B, 1.0 / global_batch, 2, s)
+                self.allreduce_grads()
+                plan.run(0, 0, B, 0.0, 4, s)
+            else:
+                plan.run(Xb.data_ptr(), yb.data_ptr(), B, 1.0 / global_batch, 1, s)
+            return
         if self.native:
             self.forward_backward_native(Xb, yb, 1.0 / global_batch)
             if self.world > 1:

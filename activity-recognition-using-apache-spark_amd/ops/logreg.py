@@ -229,7 +229,7 @@ class DeviceLogregSolver:
     def __init__(self, design: LogregDesign, B: int, T: int, m: int, inv_std, pmask, inv_wsum, l2v, l1v,
                  max_iter: int, tol: float, c1: float = 1e-4, allreduce=None):
         self.d = design
-        dev = design.rw.device
+        dev = design.device
         K, F = design.K, design.F
         self.B, self.T, self.m = B, T, m
         self.D = K * (F + 1)

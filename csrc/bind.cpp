@@ -13,6 +13,7 @@
 #include <cstring>
 #include <stdexcept>
 #include <string>
+#include <vector>
 
 #include "har_kernels.h"
 #include "host/csv_parser.h"
@@ -156,6 +157,43 @@ static QnArgs qn_args_from_dict(py::dict d) {
 // ~20 us of host time, three launches per iteration).
 struct QnArgsHolder {
   QnArgs a;
+};
+
+// The flagship MLP training step as ONE host call: the buffers of an engine never move, so their
+// pointers, the gradient-reduction regions and the Adam hyper-parameters are fixed once per (engine,
+// batch size) and run() enqueues mlp_step_fwd -> mlp_step_bwd -> grad_reduce_adam with only the batch
+// pointers changing (three pybind calls with ~20 arguments each and a region list rebuilt in Python
+// every step were ~10 us of host time per 70 us step: enough to starve the GPU when not graph-captured).
+struct MlpStepPlan {
+  u W0, b0, W1, b1, Wo, bo, dz, mask, fslab, bloss, bcorr, gw1, gw0, gb0, gb1, step, G, Pw, m, v, Pb;
+  int K0, H, C;
+  int64_t stride, n;
+  float lr, b1c, b2c, eps, wd;
+  std::vector<const float*> src;
+  std::vector<int64_t> start, len, lds;
+  std::vector<int> S;
+  // mode: 1 reduce + Adam (N = 1), 2 reduce + store G (DP, before the all-reduce), 4 Adam from G
+  void run(u X, u y, int B, float scale, int mode, u stream) {
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    if (mode & 3) {
+      check(har_mlp_step_fwd(P<const uint16_t>(X), K0, P<const uint16_t>(W0), P<const float>(b0),
+                             P<const uint16_t>(W1), P<const float>(b1), H, P<const uint16_t>(Wo), P<const float>(bo),
+                             P<const int32_t>(y), B, C, scale, P<uint32_t>(dz), P<uint32_t>(mask), P<float>(fslab),
+                             P<float>(bloss), P<int32_t>(bcorr), s),
+            "mlp_step_fwd");
+      check(har_mlp_step_bwd(P<const uint32_t>(dz), P<const uint32_t>(mask), P<const uint16_t>(X), K0,
+                             P<const uint16_t>(W1), H, P<const uint16_t>(W0), P<const float>(b0),
+                             P<const uint16_t>(Wo), B, P<float>(gw1), P<float>(gw0), P<float>(gb0), P<float>(gb1),
+                             stride, P<int32_t>(step), s),
+            "mlp_step_bwd");
+    }
+    const int gm = mode == 1 ? 1 | 4 : mode == 2 ? 1 | 2 : 4;  // GR_REDUCE 1, GR_STORE 2, GR_ADAM 4
+    const int k = (gm & 1) ? (int)src.size() : 0;
+    check(har_grad_reduce_adam(k, src.data(), start.data(), len.data(), lds.data(), S.data(), n, P<float>(G),
+                               P<float>(Pw), P<float>(m), P<float>(v), P<uint16_t>(Pb), lr, b1c, b2c, eps, wd,
+                               P<int32_t>(step), 0, gm, s),
+          "grad_reduce_adam");
+  }
 };
 
 PYBIND11_MODULE(_har_native, m) {
@@ -450,6 +488,43 @@ PYBIND11_MODULE(_har_native, m) {
   m.def("head_fused_blocks", &har_head_fused_blocks);
   m.def("mlp_fwd_head_grid", &har_mlp_fwd_head_grid);
   m.def("mlp_set_stamps", [](u p) { har_mlp_set_stamps(P<uint64_t>(p)); });
+  py::class_<MlpStepPlan>(m, "MlpStepPlan")
+      .def(py::init([](py::dict d) {
+        MlpStepPlan p;
+        for (const char* k : {"W0", "b0", "W1", "b1", "Wo", "bo", "dz", "mask", "fslab", "bloss", "bcorr", "gw1", "gw0",
+                              "gb0", "gb1", "step", "G", "P", "m", "v", "Pb"}) {
+          const u x = d[k].cast<u>();
+          if (!strcmp(k, "W0")) p.W0 = x; else if (!strcmp(k, "b0")) p.b0 = x; else if (!strcmp(k, "W1")) p.W1 = x;
+          else if (!strcmp(k, "b1")) p.b1 = x; else if (!strcmp(k, "Wo")) p.Wo = x; else if (!strcmp(k, "bo")) p.bo = x;
+          else if (!strcmp(k, "dz")) p.dz = x; else if (!strcmp(k, "mask")) p.mask = x;
+          else if (!strcmp(k, "fslab")) p.fslab = x; else if (!strcmp(k, "bloss")) p.bloss = x;
+          else if (!strcmp(k, "bcorr")) p.bcorr = x; else if (!strcmp(k, "gw1")) p.gw1 = x;
+          else if (!strcmp(k, "gw0")) p.gw0 = x; else if (!strcmp(k, "gb0")) p.gb0 = x; else if (!strcmp(k, "gb1")) p.gb1 = x;
+          else if (!strcmp(k, "step")) p.step = x; else if (!strcmp(k, "G")) p.G = x; else if (!strcmp(k, "P")) p.Pw = x;
+          else if (!strcmp(k, "m")) p.m = x; else if (!strcmp(k, "v")) p.v = x; else p.Pb = x;
+        }
+        p.K0 = d["K0"].cast<int>();
+        p.H = d["H"].cast<int>();
+        p.C = d["C"].cast<int>();
+        p.stride = d["stride"].cast<int64_t>();
+        p.n = d["n"].cast<int64_t>();
+        p.lr = d["lr"].cast<float>();
+        p.b1c = d["beta1"].cast<float>();
+        p.b2c = d["beta2"].cast<float>();
+        p.eps = d["eps"].cast<float>();
+        p.wd = d["wd"].cast<float>();
+        for (auto r : d["regions"].cast<py::list>()) {  // (start, end, src pointer, #slabs, slab stride)
+          auto t = r.cast<py::tuple>();
+          const int64_t a = t[0].cast<int64_t>(), e = t[1].cast<int64_t>();
+          p.start.push_back(a);
+          p.len.push_back(e - a);
+          p.src.push_back(P<const float>(t[2].cast<u>()));
+          p.S.push_back(t[3].cast<int>());
+          p.lds.push_back(t[4].cast<int64_t>());
+        }
+        return p;
+      }))
+      .def("run", &MlpStepPlan::run);
   m.def("mlp_step_grid", &har_mlp_step_grid);
   m.def("mlp_step_slices", &har_mlp_step_slices);
   m.def("mlp_step_fwd_slab_width", &har_mlp_step_fwd_slab_width);

@@ -16,8 +16,14 @@ typedef __attribute__((ext_vector_type(2))) uint32_t u32x2_t;
 typedef __attribute__((ext_vector_type(2))) short s16x2_t;
 typedef __attribute__((ext_vector_type(2))) unsigned short u16x2_t;
 
+typedef __attribute__((ext_vector_type(2))) float f32x2_t;
+typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2_t;
+
+// two fp32 -> one packed bf16 pair: a single v_cvt_pk_bf16_f32 (round to nearest even).  Packing two
+// scalar conversions instead makes hipcc pair the wrong operands and re-assemble the halves with
+// shifts / ORs (~6 extra VALU per pair).
 __device__ __forceinline__ uint32_t pack2(float a, float b) {
-  return (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16);
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2_t{a, b}, bf16x2_t));
 }
 
 __device__ __forceinline__ f32x4_t mma32(bf16x8_t a, bf16x8_t b, f32x4_t c) {
@@ -63,5 +69,70 @@ __device__ __forceinline__ bf16x8_t frag_rows(const bf16_t* img, int pitch, int 
   const s16x8_t v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
   return __builtin_bit_cast(bf16x8_t, v);
 }
+
+// frag_rows of an image whose rows with bit 2 set have their 16-byte column chunks swapped in pairs
+// (column ^ 8; col0 a multiple of 16): the lane's rows 4g + (li >> 2) (+ 16) all have bit 2 = g & 1
+__device__ __forceinline__ bf16x8_t frag_rows_sw(const bf16_t* img, int pitch, int col0, int lane) {
+  const int li = lane & 15, g = lane >> 4;
+  const bf16_t* p0 = img + (4 * g + (li >> 2)) * pitch + col0 + ((4 * (li & 3)) ^ (8 * (g & 1)));
+  const s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)p0);
+  const s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(p0 + 16 * pitch));
+  const s16x8_t v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8_t, v);
+}
+
+// ---- cross-lane steps on the VALU (DPP / permlane), not through the LDS crossbar: __shfl_xor
+// lowers to ds_bpermute_b32, whose LDS round trip made a 13-step softmax chain ~1.4k cycles ----
+template <int CTRL>
+__device__ __forceinline__ int dpp_i(int v) {
+  return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xf, 0xf, false);
+}
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __builtin_bit_cast(float, dpp_i<CTRL>(__builtin_bit_cast(int, v)));
+}
+constexpr int DPP_ROR8 = 0x128, DPP_ROR4 = 0x124, DPP_ROR2 = 0x122, DPP_ROR1 = 0x121;  // row_ror:n (16-lane rows)
+constexpr int DPP_QUAD_XOR1 = 0xb1;                                                // quad_perm [1,0,3,2]
+
+// all-reduce over the 16 lanes of each DPP row (lanes 16r .. 16r + 15)
+__device__ __forceinline__ float row16_max(float v) {
+  v = fmaxf(v, dpp_f<DPP_ROR8>(v));
+  v = fmaxf(v, dpp_f<DPP_ROR4>(v));
+  v = fmaxf(v, dpp_f<DPP_ROR2>(v));
+  return fmaxf(v, dpp_f<DPP_ROR1>(v));
+}
+__device__ __forceinline__ float row16_sum(float v) {
+  v += dpp_f<DPP_ROR8>(v);
+  v += dpp_f<DPP_ROR4>(v);
+  v += dpp_f<DPP_ROR2>(v);
+  return v + dpp_f<DPP_ROR1>(v);
+}
+__device__ __forceinline__ int row16_min(int v) {
+  v = min(v, dpp_i<DPP_ROR8>(v));
+  v = min(v, dpp_i<DPP_ROR4>(v));
+  v = min(v, dpp_i<DPP_ROR2>(v));
+  return min(v, dpp_i<DPP_ROR1>(v));
+}
+
+// The value lane ^ 16 / lane ^ 32 holds, by the gfx950 row / half swaps (VALU).  `self` of the swap of
+// the lane's own id fixes which of the two outputs carries the partner, independent of the operand
+// order convention.
+struct LaneSwap {
+  bool hi16, hi32;
+  __device__ __forceinline__ explicit LaneSwap(int lane) {
+    const auto a = __builtin_amdgcn_permlane16_swap((uint32_t)lane, (uint32_t)lane, false, false);
+    const auto b = __builtin_amdgcn_permlane32_swap((uint32_t)lane, (uint32_t)lane, false, false);
+    hi16 = a[0] == (uint32_t)(lane ^ 16);
+    hi32 = b[0] == (uint32_t)(lane ^ 32);
+  }
+  __device__ __forceinline__ uint32_t x16(uint32_t v) const {
+    const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+    return hi16 ? r[0] : r[1];
+  }
+  __device__ __forceinline__ uint32_t x32(uint32_t v) const {
+    const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+    return hi32 ? r[0] : r[1];
+  }
+};
 
 }  // namespace mlpf

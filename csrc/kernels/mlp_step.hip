@@ -22,7 +22,7 @@
 // mlp_bwd3 (S row slices x 4 h1-unit quadrants of 64 units; 64-row tiles, one barrier per tile):
 //   dact2 tile i+1 (MFMA from dz / mask registers loaded a tile ahead) -> LDS | X tile i+2 -> LDS |
 //   h1 tile i+1 recomputed from X | (a) dact1^T = W1^T[u] . dact2^T, relu'(h1) | (b) dW1 += h1^T . dact2
-//   | (c) dW0 += dact1^T . X of tile i-1 | db1 = sum_rows dact2 (quadrant 0, a ones-row MFMA) | barrier
+//   | (c) dW0 += dact1^T . X of tile i-1 | db1 = sum_rows dact2 (a ones-row MFMA, 64 j per quadrant) | barrier
 // One deterministic partial per (slice, quadrant), laid out like the flat parameter buffer.
 #include <algorithm>
 #include <cstdlib>
@@ -61,14 +61,16 @@ constexpr int HH = 256;
 // ------------------------------------------------------------------------------------------------
 constexpr int FW = 8;                  // waves (2 per SIMD)
 constexpr int FRT = 32;                // rows per tile
-constexpr int FHP = HH + 8;            // h1 tile pitch (bf16)
+// h1 tile: pitch 136 dwords, and the 16-byte column chunks of rows with bit 2 set swapped in pairs
+// (column ^ 8): the 16-byte reads of stage 2 are conflict-free (the stage-1 8-byte stores 2-way)
+constexpr int FHP = HH + 16;
 constexpr int FSP = 16 + 8;            // [32 rows][16 cols] transpose image pitch
 constexpr int FIMG = FRT * FSP;
 // partial logits of one (wave, half): lane group g's 16 lanes x 4 classes at dword 72 g + 4 c16: the
 // softmax lanes (row, class) then read 16 distinct banks per row and disjoint banks per row pair
 constexpr int ZREG = 4 * 72;
 constexpr int FWD_SLAB = NCLS * HH + NCLS;  // per workgroup: dWout rows 0..15 [16][H], dbout [16]
-constexpr size_t FWD_LDS = (size_t)FRT * FHP * 2 + (size_t)FW * 2 * ZREG * 4 + (size_t)2 * FIMG * 2 +
+constexpr size_t FWD_LDS = (size_t)2 * FRT * FHP * 2 + (size_t)2 * FW * 2 * ZREG * 4 + (size_t)2 * FIMG * 2 +
                            (size_t)FW * 4 * FIMG * 2;
 
 template <int K0>
@@ -85,9 +87,9 @@ __global__ __launch_bounds__(512) void mlp_fwd3_kernel(
     float* __restrict__ block_loss, int32_t* __restrict__ block_correct, uint64_t* __restrict__ stamps) {
   constexpr int K0C = K0 / 32, KC = HH / 32;
   extern __shared__ __attribute__((aligned(16))) bf16_t lds[];
-  bf16_t* const h1s = lds;                                              // [32][FHP]
-  float* const zs = reinterpret_cast<float*>(h1s + FRT * FHP);          // [8 waves][2 halves][ZREG]
-  bf16_t* const dzs = reinterpret_cast<bf16_t*>(zs + FW * 2 * ZREG);    // [2 bufs][32 rows][FSP]
+  bf16_t* const h1s = lds;                                                // [2 bufs][32][FHP]
+  float* const zs = reinterpret_cast<float*>(h1s + 2 * FRT * FHP);        // [2 bufs][8 waves][2 halves][ZREG]
+  bf16_t* const dzs = reinterpret_cast<bf16_t*>(zs + 2 * FW * 2 * ZREG);  // [2 bufs][32 rows][FSP]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int c16 = lane & 15, g = lane >> 4;
   const int u0 = wave * 32;
@@ -119,6 +121,8 @@ __global__ __launch_bounds__(512) void mlp_fwd3_kernel(
   }
   // softmax lane: tile row sr = 4 wave + g (half sh, row srr of it), class c16
   const int sr = 4 * wave + g, sh = sr >> 4, srr = sr & 15;
+  const int hsw = 8 * ((c16 >> 2) & 1);  // h1 tile chunk swap of this lane's rows (16h + c16)
+  const LaneSwap swp(lane);
   const float bo_s = c16 < C ? bo[c16] : 0.f;
   if constexpr (STAMP) __builtin_amdgcn_s_waitcnt(0x0f70);
   HAR_STAMP(FW, 1)
@@ -126,22 +130,21 @@ __global__ __launch_bounds__(512) void mlp_fwd3_kernel(
   f32x4_t acc5[2] = {f32x4_t{0.f, 0.f, 0.f, 0.f}, f32x4_t{0.f, 0.f, 0.f, 0.f}};
   float dbo = 0.f, lsum = 0.f, ncorr = 0.f;
   const int ntiles = B / FRT;
-  int T = blockIdx.x;
+  const int nt = (int)blockIdx.x < ntiles ? (ntiles - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
+  // tile k of this workgroup; past the last one clamped to it (staged, computed, never consumed), so
+  // every load is unconditional and the compiler's counted waits stay exact on every path
+  auto tile_of = [&](int k) __attribute__((always_inline)) { return (int)blockIdx.x + min(k, nt - 1) * (int)gridDim.x; };
   bf16x8_t xb[2][K0C];
-  int ys = 0;
-  if (T < ntiles) {
+  auto load_x = [&](int k) __attribute__((always_inline)) {
+    const int r = tile_of(k) * FRT;
 #pragma unroll
     for (int h = 0; h < 2; ++h)
 #pragma unroll
-      for (int kc = 0; kc < K0C; ++kc) xb[h][kc] = ldx<K0>(X, T * FRT + 16 * h + c16, kc, g);
-    ys = labels[T * FRT + sr];
-  }
-  int it = 0;
-  for (; T < ntiles; T += gridDim.x, ++it) {
-    const int r0 = T * FRT;
-    if (it < 32) HAR_STAMP(FW, 2 + it)
-    const int yc = ys;
-    // ---- stage 1: h1^T = W0 . X^T for this wave's units ----
+      for (int kc = 0; kc < K0C; ++kc) xb[h][kc] = ldx<K0>(X, r + 16 * h + c16, kc, g);
+  };
+  // ---- stage 1: h1^T = W0 . X^T for this wave's units -> h1 buffer `buf` ----
+  auto stage1 = [&](int buf) __attribute__((always_inline)) {
+    bf16_t* hb = h1s + buf * FRT * FHP;
 #pragma unroll
     for (int h = 0; h < 2; ++h)
 #pragma unroll
@@ -149,27 +152,15 @@ __global__ __launch_bounds__(512) void mlp_fwd3_kernel(
         f32x4_t a = {b0r[t].x, b0r[t].y, b0r[t].z, b0r[t].w};
 #pragma unroll
         for (int kc = 0; kc < K0C; ++kc) a = mma32(w0f[t][kc], xb[h][kc], a);
-        *reinterpret_cast<uint2*>(h1s + (16 * h + c16) * FHP + u0 + 16 * t + 4 * g) =
+        *reinterpret_cast<uint2*>(hb + (16 * h + c16) * FHP + ((u0 + 16 * t + 4 * g) ^ hsw)) =
             make_uint2(relu2(pack2(a[0], a[1])), relu2(pack2(a[2], a[3])));
       }
-    __syncthreads();  // B1: h1 tile complete; the previous tile's dz (dzs) complete
-    // prefetch the next tile (index clamped: the same loads on every path, so the waits stay counted)
-    {
-      const int Tn = min(T + (int)gridDim.x, ntiles - 1);
-#pragma unroll
-      for (int h = 0; h < 2; ++h)
-#pragma unroll
-        for (int kc = 0; kc < K0C; ++kc) xb[h][kc] = ldx<K0>(X, Tn * FRT + 16 * h + c16, kc, g);
-      ys = labels[Tn * FRT + sr];
-    }
-    // ---- stage 5 of the previous tile: dWout^T += h2^T . dz over its 32 rows ----
-    if (it > 0) {
-      const bf16x8_t bz = frag_tr(dzs + ((it - 1) & 1) * FIMG, FSP, 0, lane);
-      const bf16_t* ip = img + ((it - 1) & 1) * 2 * FIMG;
-#pragma unroll
-      for (int t = 0; t < 2; ++t) acc5[t] = mma32(frag_tr(ip + t * FIMG, FSP, 0, lane), bz, acc5[t]);
-    }
-    // ---- stage 2: h2^T = W1 . h1^T (4 independent accumulators) ----
+  };
+  // ---- stages 2 + 3 of tile k from h1 buffer `buf`: h2^T = W1 . h1^T, relu' mask, partial logits
+  // -> zs buffer `buf`, h2 images for stage 5 -> image buffer `buf` ----
+  auto stage23 = [&](int k, int buf) __attribute__((always_inline)) {
+    const int r0 = tile_of(k) * FRT;
+    const bf16_t* hsrc = h1s + buf * FRT * FHP;
     f32x4_t acc[2][2];
 #pragma unroll
     for (int h = 0; h < 2; ++h)
@@ -180,7 +171,7 @@ __global__ __launch_bounds__(512) void mlp_fwd3_kernel(
       bf16x8_t hb[2];
 #pragma unroll
       for (int h = 0; h < 2; ++h)
-        hb[h] = *reinterpret_cast<const bf16x8_t*>(h1s + (16 * h + c16) * FHP + kc * 32 + 8 * g);
+        hb[h] = *reinterpret_cast<const bf16x8_t*>(hsrc + (16 * h + c16) * FHP + ((kc * 32 + 8 * g) ^ hsw));
 #pragma unroll
       for (int h = 0; h < 2; ++h)
 #pragma unroll
@@ -194,8 +185,8 @@ __global__ __launch_bounds__(512) void mlp_fwd3_kernel(
         h2p[h][t][0] = relu2(pack2(acc[h][t][0], acc[h][t][1]));
         h2p[h][t][1] = relu2(pack2(acc[h][t][2], acc[h][t][3]));
       }
-    // relu'(h2) of the wave's 32 units for rows 16h + c16 -> mask word `wave` of the row (every lane of
-    // the row stores the same word: unconditional stores keep the counted waits exact)
+    // relu'(h2) of the wave's 32 units for rows 16h + c16 -> mask word `wave` of the row (every lane
+    // of the row stores the same word)
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       uint32_t m = 0;
@@ -207,66 +198,90 @@ __global__ __launch_bounds__(512) void mlp_fwd3_kernel(
           m |= ((w2 & 0xffffu) ? 1u : 0u) << (16 * t + 4 * g + 2 * e);
           m |= ((w2 >> 16) ? 1u : 0u) << (16 * t + 4 * g + 2 * e + 1);
         }
-      m |= __shfl_xor(m, 16, 64);
-      m |= __shfl_xor(m, 32, 64);
+      m |= swp.x16(m);
+      m |= swp.x32(m);
       mask_out[(size_t)(r0 + 16 * h + c16) * 8 + wave] = m;
     }
-    // ---- stage 3: partial logits over this wave's 32 units ----
+    float* zb = zs + buf * FW * 2 * ZREG;
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const f32x4_t zp = mma32(wo3, cat8(h2p[h][0][0], h2p[h][0][1], h2p[h][1][0], h2p[h][1][1]),
                                f32x4_t{0.f, 0.f, 0.f, 0.f});
-      *reinterpret_cast<f32x4_t*>(zs + (wave * 2 + h) * ZREG + 72 * g + 4 * c16) = zp;
+      *reinterpret_cast<f32x4_t*>(zb + (wave * 2 + h) * ZREG + 72 * g + 4 * c16) = zp;
     }
-    // stage-5 images of this tile's h2 (this wave's units), consumed by the same wave next tile
-    {
-      bf16_t* ib = img + (it & 1) * 2 * FIMG;
+    bf16_t* ib = img + buf * 2 * FIMG;
 #pragma unroll
-      for (int h = 0; h < 2; ++h)
+    for (int h = 0; h < 2; ++h)
 #pragma unroll
-        for (int t = 0; t < 2; ++t)
-          *reinterpret_cast<uint2*>(ib + t * FIMG + (16 * h + c16) * FSP + 4 * g) = make_uint2(h2p[h][t][0], h2p[h][t][1]);
-    }
-    __syncthreads();  // B2: every wave's partial logits are in
-    // ---- softmax / CE / argmax / dz: lane = (row sr, class c16) ----
-    {
-      float z = 0.f;
+      for (int t = 0; t < 2; ++t)
+        *reinterpret_cast<uint2*>(ib + t * FIMG + (16 * h + c16) * FSP + 4 * g) = make_uint2(h2p[h][t][0], h2p[h][t][1]);
+  };
+  // ---- softmax / CE / argmax / dz of tile k (zs buffer `buf`): lane = (row sr, class c16) ----
+  auto softmax = [&](int k, int buf, int yc) __attribute__((always_inline)) {
+    const int r0 = tile_of(k) * FRT;
+    const float* zb = zs + buf * FW * 2 * ZREG;
+    float z = 0.f;
 #pragma unroll
-      for (int w = 0; w < FW; ++w) z += zs[(w * 2 + sh) * ZREG + 72 * (c16 >> 2) + 4 * srr + (c16 & 3)];
-      const float zz = c16 < C ? z + bo_s : -INFINITY;
-      float mx = zz;
-      int amx = c16 < C ? c16 : (1 << 30);
-#pragma unroll
-      for (int o = 1; o < 16; o <<= 1) {
-        const float om = __shfl_xor(mx, o, 64);
-        const int oa = __shfl_xor(amx, o, 64);
-        const bool take = (om > mx) | ((om == mx) & (oa < amx));  // selects, no divergent branch
-        mx = take ? om : mx;
-        amx = take ? oa : amx;
-      }
-      const float e = c16 < C ? __expf(zz - mx) : 0.f;
-      float se = e;
-#pragma unroll
-      for (int o = 1; o < 16; o <<= 1) se += __shfl_xor(se, o, 64);
-      const float dl = c16 < C ? (e * (1.f / se) - (c16 == yc ? 1.f : 0.f)) * scale : 0.f;
-      const bf16_t db = f2bf(dl);
-      lsum += c16 == yc ? (mx + __logf(se)) - zz : 0.f;
-      ncorr += (c16 == 0 && amx == yc) ? 1.f : 0.f;
-      dbo += bf2f(db);
-      dzs[(it & 1) * FIMG + sr * FSP + c16] = db;
-      const uint32_t other = (uint32_t)__shfl_xor((int)db, 1, 64) & 0xffffu;
-      const uint32_t pair = (c16 & 1) ? (other | ((uint32_t)db << 16)) : ((uint32_t)db | (other << 16));
-      dz_out[(size_t)(r0 + sr) * 8 + (c16 >> 1)] = pair;  // both lanes of a pair store the same word
-    }
-  }
-  HAR_STAMP(FW, 34)
-  __syncthreads();  // the last tile's dz
-  if (it > 0) {
-    const bf16x8_t bz = frag_tr(dzs + ((it - 1) & 1) * FIMG, FSP, 0, lane);
-    const bf16_t* ip = img + ((it - 1) & 1) * 2 * FIMG;
+    for (int w = 0; w < FW; ++w) z += zb[(w * 2 + sh) * ZREG + 72 * (c16 >> 2) + 4 * srr + (c16 & 3)];
+    const float zz = c16 < C ? z + bo_s : -INFINITY;
+    // the 16 class lanes of a row are one DPP row: max, argmax (smallest class at the max), sum
+    const float mx = row16_max(zz);
+    const int amx = row16_min(zz == mx && c16 < C ? c16 : (1 << 30));
+    const float e = c16 < C ? __expf(zz - mx) : 0.f;
+    const float se = row16_sum(e);
+    const float dl = c16 < C ? (e * (1.f / se) - (c16 == yc ? 1.f : 0.f)) * scale : 0.f;
+    const bf16_t db = f2bf(dl);
+    lsum += c16 == yc ? (mx + __logf(se)) - zz : 0.f;
+    ncorr += (c16 == 0 && amx == yc) ? 1.f : 0.f;
+    dbo += bf2f(db);
+    dzs[buf * FIMG + sr * FSP + c16] = db;
+    const uint32_t other = (uint32_t)dpp_i<DPP_QUAD_XOR1>((int)db) & 0xffffu;
+    const uint32_t pair = (c16 & 1) ? (other | ((uint32_t)db << 16)) : ((uint32_t)db | (other << 16));
+    dz_out[(size_t)(r0 + sr) * 8 + (c16 >> 1)] = pair;  // both lanes of a pair store the same word
+  };
+  // ---- stage 5 of a tile (dz buffer / image buffer `buf`): dWout^T += h2^T . dz over its 32 rows ----
+  auto stage5 = [&](int buf) __attribute__((always_inline)) {
+    const bf16x8_t bz = frag_tr(dzs + buf * FIMG, FSP, 0, lane);
+    const bf16_t* ip = img + buf * 2 * FIMG;
 #pragma unroll
     for (int t = 0; t < 2; ++t) acc5[t] = mma32(frag_tr(ip + t * FIMG, FSP, 0, lane), bz, acc5[t]);
+  };
+
+  // Software pipeline, ONE barrier per tile.  Iteration k: softmax of tile k | stage 5 of tile k-1 |
+  // stages 2 + 3 of tile k+1 | stage 1 of tile k+2 | barrier.  The softmax's dependent chain (LDS
+  // reads, cross-lane max / sum, exp / log) and the next tile's MFMAs share one barrier interval, so
+  // the scheduler interleaves them; h1, the partial logits, dz and the h2 images are double-buffered.
+  int ynext = 0;
+  if (nt > 0) {
+    load_x(0);
+    ynext = labels[tile_of(0) * FRT + sr];
+    stage1(0);
+    load_x(1);
+    __syncthreads();  // h1 of tile 0
+    stage23(0, 0);
+    stage1(1);
+    load_x(2);
+    __syncthreads();  // partial logits of tile 0, h1 of tile 1
   }
+  for (int k = 0; k < nt; ++k) {
+    if (k < 32) HAR_STAMP(FW, 2 + k)
+    const int yc = ynext;
+    ynext = labels[tile_of(k + 1) * FRT + sr];
+    softmax(k, k & 1, yc);
+    if (k == 4) HAR_STAMP(FW, 10)
+    if (k > 0) stage5((k - 1) & 1);
+    if (k == 4) HAR_STAMP(FW, 11)
+    if (k + 1 < nt) {  // workgroup-uniform
+      stage23(k + 1, (k + 1) & 1);
+      if (k == 4) HAR_STAMP(FW, 12)
+      stage1(k & 1);   // tile k+2 (clamped) into the buffer tile k left
+      load_x(k + 3);
+      if (k == 4) HAR_STAMP(FW, 13)
+    }
+    __syncthreads();
+  }
+  HAR_STAMP(FW, 34)
+  if (nt > 0) stage5((nt - 1) & 1);
   // ---- this workgroup's slab: dWout rows 0..15 x this wave's units, dbout; loss, #correct ----
   float* out = slab + (size_t)blockIdx.x * FWD_SLAB;
 #pragma unroll
@@ -318,7 +333,7 @@ template <int K0> struct Bwd3Lds {
   static constexpr int NXB = 4;  // X tile buffers (staged two tiles ahead; read by h1 / (c) two tiles apart)
   static constexpr int DSM = BRT * BDP, HS = BRT * BUP, XS = BRT * XP;
   static constexpr size_t bytes = (size_t)(2 * DSM + 2 * HS + 2 * HS + NXB * XS) * sizeof(bf16_t) +
-                                  4 * BQU * sizeof(float);
+                                  4 * BQU * sizeof(float) + 32 * sizeof(uint32_t);
   static_assert((size_t)HH * WQP + NCLS * HH <= (size_t)2 * DSM, "prologue images fit the dact2 buffers");
 };
 
@@ -342,6 +357,11 @@ __global__ __launch_bounds__(512) void mlp_bwd3_kernel(
   float* const red = reinterpret_cast<float*>(xs0 + NXB * L::XS);  // [4][64] db0 of the row blocks
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int c16 = lane & 15, g = lane >> 4;
+  // relu' nibble -> the two 32-bit AND masks of four packed bf16 (entry n: bit i of n keeps element i)
+  uint32_t* const lut = reinterpret_cast<uint32_t*>(red + 4 * BQU);  // [16][2]
+  if (tid < 16)
+    *reinterpret_cast<uint2*>(lut + 2 * tid) = make_uint2((tid & 1 ? 0xffffu : 0u) | (tid & 2 ? 0xffff0000u : 0u),
+                                                          (tid & 4 ? 0xffffu : 0u) | (tid & 8 ? 0xffff0000u : 0u));
   HAR_STAMP_REAL(8, 38)
   HAR_STAMP(8, 0)
   const int b = xcd_remap(blockIdx.x, gridDim.x);
@@ -378,12 +398,15 @@ __global__ __launch_bounds__(512) void mlp_bwd3_kernel(
   for (int e = 0; e < 2; ++e)
 #pragma unroll
     for (int kc = 0; kc < KC; ++kc) w1t[e][kc] = frag_tr(wq + 32 * kc * WQP, WQP, 16 * (up + e), lane);
-  // dact2 A fragments (16x16x16): A[m = j][k = class] = Wout[4g + i][128 jh + 16 jt + c16]
+  // dact2 A fragments (16x16x16): A[m][k = class] = Wout[4g + i][j(m)] with the row -> j map of block
+  // t = 2p + s: j = 128 jh + 32 p + 8 (m >> 2) + 4 s + (m & 3), so lane group g of the block pair p
+  // holds the 8 consecutive j = 128 jh + 32 p + 8 g .. + 7: one 16-byte LDS store per pair
   s16x4_t woa[8];
 #pragma unroll
-  for (int jt = 0; jt < 8; ++jt)
+  for (int t = 0; t < 8; ++t)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) woa[jt][i] = (short)wos[(4 * g + i) * HH + 128 * jh + 16 * jt + c16];
+    for (int i = 0; i < 4; ++i)
+      woa[t][i] = (short)wos[(4 * g + i) * HH + 128 * jh + 32 * (t >> 1) + 8 * (c16 >> 2) + 4 * (t & 1) + (c16 & 3)];
   // db1 (quadrant 0): A = a row of ones (row 0 of the 16 x 32 tile)
   const bf16x8_t ones = __builtin_bit_cast(bf16x8_t, c16 == 0 ? s16x8_t{0x3f80, 0x3f80, 0x3f80, 0x3f80, 0x3f80,
                                                                         0x3f80, 0x3f80, 0x3f80}
@@ -392,12 +415,12 @@ __global__ __launch_bounds__(512) void mlp_bwd3_kernel(
   HAR_STAMP(8, 1)
   __syncthreads();  // the prologue images are read: the tile buffers may be written
 
-  f32x4_t acc1[4][2], acc0[NFW], accb[2];
+  f32x4_t acc1[4][2], acc0[NFW], accb[1];
 #pragma unroll
   for (int i = 0; i < 4; ++i) acc1[i][0] = acc1[i][1] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int f = 0; f < NFW; ++f) acc0[f] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-  accb[0] = accb[1] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  accb[0] = f32x4_t{0.f, 0.f, 0.f, 0.f};
   float rs[2][4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
 
   // Register staging: one dz piece (8 B: classes 4g.. of row 16 rb2 + c16) + one mask piece (16 B:
@@ -420,18 +443,24 @@ __global__ __launch_bounds__(512) void mlp_bwd3_kernel(
 #define HAR_B3_LOAD_X(t) xr = *reinterpret_cast<const uint4*>(lx + (int64_t)min(t, tlast) * BRT * K0);
 #define HAR_B3_STAGE_X(i) *reinterpret_cast<uint4*>(xs0 + ((i) % NXB) * L::XS + sdx) = xr;
 
-  // dact2 tile from the dz / mask registers -> LDS buffer `buf` (row-major [r][j])
+  // dact2 tile from the dz / mask registers -> LDS buffer `buf`: row-major [r][j] with the 16-byte chunks
+  // of rows r with bit 2 set swapped in pairs (column ^ 8), which makes these 16-byte stores and the
+  // 16-byte row reads of (a) conflict-free; the transposed reads of (b) apply the same swap.  The relu'
+  // bits of a lane's four values of a block pick two AND masks from the LDS table (no per-element VALU).
   auto stage_dact2 = [&](int buf) __attribute__((always_inline)) {
-    bf16_t* d = dsm0 + buf * L::DSM + (16 * rb2 + c16) * BDP + 128 * jh + 4 * g;
+    const int sw = 8 * ((c16 >> 2) & 1);
+    bf16_t* d = dsm0 + buf * L::DSM + (16 * rb2 + c16) * BDP;
     const s16x4_t dzv = __builtin_bit_cast(s16x4_t, dzr);
-    const uint32_t mw[4] = {mkr.x, mkr.y, mkr.z, mkr.w};
+    const uint32_t mw[4] = {mkr.x >> (8 * g), mkr.y >> (8 * g), mkr.z >> (8 * g), mkr.w >> (8 * g)};
 #pragma unroll
-    for (int jt = 0; jt < 8; ++jt) {
-      const f32x4_t v = mma16(woa[jt], dzv, f32x4_t{0.f, 0.f, 0.f, 0.f});  // rows j = 16 jt + 4g + r, col row c16
-      const uint32_t m = mw[jt >> 1] >> (16 * (jt & 1) + 4 * g);
-      const float d0 = (m & 1u) ? v[0] : 0.f, d1 = (m & 2u) ? v[1] : 0.f;
-      const float d2 = (m & 4u) ? v[2] : 0.f, d3 = (m & 8u) ? v[3] : 0.f;
-      *reinterpret_cast<uint2*>(d + 16 * jt) = make_uint2(pack2(d0, d1), pack2(d2, d3));
+    for (int p = 0; p < 4; ++p) {
+      const f32x4_t v0 = mma16(woa[2 * p], dzv, f32x4_t{0.f, 0.f, 0.f, 0.f});
+      const f32x4_t v1 = mma16(woa[2 * p + 1], dzv, f32x4_t{0.f, 0.f, 0.f, 0.f});
+      const uint2 m0 = *reinterpret_cast<const uint2*>(lut + 2 * (mw[p] & 0xfu));
+      const uint2 m1 = *reinterpret_cast<const uint2*>(lut + 2 * ((mw[p] >> 4) & 0xfu));
+      *reinterpret_cast<u32x4_t*>(d + ((128 * jh + 32 * p + 8 * g) ^ sw)) =
+          u32x4_t{pack2(v0[0], v0[1]) & m0.x, pack2(v0[2], v0[3]) & m0.y, pack2(v1[0], v1[1]) & m1.x,
+                  pack2(v1[2], v1[3]) & m1.y};
     }
   };
 
@@ -443,7 +472,8 @@ __global__ __launch_bounds__(512) void mlp_bwd3_kernel(
     f32x4_t a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int kc = 0; kc < KC; ++kc) {
-      const bf16x8_t bv = *reinterpret_cast<const bf16x8_t*>(dsm + (16 * rb + c16) * BDP + kc * 32 + 8 * g);
+      const bf16x8_t bv =
+          *reinterpret_cast<const bf16x8_t*>(dsm + (16 * rb + c16) * BDP + ((kc * 32 + 8 * g) ^ (8 * ((c16 >> 2) & 1))));
       a0 = mma32(w1t[0][kc], bv, a0);
       a1 = mma32(w1t[1][kc], bv, a1);
     }
@@ -467,17 +497,16 @@ __global__ __launch_bounds__(512) void mlp_bwd3_kernel(
       const bf16x8_t hb1 = frag_rows(hs + 32 * ks * BUP, BUP, 16 * (ubp + 1), lane);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const bf16x8_t da = frag_rows(dsm + 32 * ks * BDP, BDP, 16 * (jb0 + j), lane);
+        const bf16x8_t da = frag_rows_sw(dsm + 32 * ks * BDP, BDP, 16 * (jb0 + j), lane);
         acc1[j][0] = mma32(hb0, da, acc1[j][0]);  // C[u][j]: 4 consecutive units per lane
         acc1[j][1] = mma32(hb1, da, acc1[j][1]);
       }
     }
-    if (q == 0) {  // workgroup-uniform: db1 = sum over the rows of dact2 (row 0 of ones . dact2)
+    if (wave < 4) {  // db1 = sum over the rows of dact2 (row 0 of ones . dact2): quadrant q, wave w < 4
+                     // own the 16 j of block 4q + w, so every workgroup does the same work
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-        for (int e = 0; e < 2; ++e)
-          accb[e] = mma32(ones, frag_rows(dsm + 32 * ks * BDP, BDP, 16 * (2 * wave + e), lane), accb[e]);
+        accb[0] = mma32(ones, frag_rows_sw(dsm + 32 * ks * BDP, BDP, 16 * (4 * q + wave), lane), accb[0]);
     }
   };
   // (c) of local tile i (its dact1 buffer i & 1, X buffer i % NXB)
@@ -551,10 +580,7 @@ __global__ __launch_bounds__(512) void mlp_bwd3_kernel(
   for (int f = 0; f < NFW; ++f)
 #pragma unroll
     for (int r = 0; r < 4; ++r) w0o[(size_t)(qu0 + 16 * ub + 4 * g + r) * K0 + 16 * (fb + f) + c16] = acc0[f][r];
-  if (q == 0 && g == 0) {
-#pragma unroll
-    for (int e = 0; e < 2; ++e) gb1[(size_t)slice * slab_stride + 16 * (2 * wave + e) + c16] = accb[e][0];
-  }
+  if (wave < 4 && g == 0) gb1[(size_t)slice * slab_stride + 16 * (4 * q + wave) + c16] = accb[0][0];
 #pragma unroll
   for (int e = 0; e < 2; ++e)
 #pragma unroll

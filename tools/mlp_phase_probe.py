@@ -60,7 +60,8 @@ def stamps(B=65536):
         live = s[:, 0] > 0
         s = s[live]
         print(f"--- {name}: {live.sum()} waves stamped")
-        ntile = int(((s[:, 2:34] > 0).sum(1)).max())
+        lim = 10 if (k == 0 and (s[:, 10] > 0).all()) else 34  # forward slots 10.. hold tile-4 sub-phases
+        ntile = int(((s[:, 2:lim] > 0).sum(1)).max())
         rows = [("prologue (weights in regs)", s[:, 1] - s[:, 0])]
         for t in range(min(ntile, 32)):
             end = s[:, 3 + t] if t + 1 < ntile else s[:, 34]
@@ -69,6 +70,12 @@ def stamps(B=65536):
         rows.append(("total (entry -> exit)", s[:, 35] - s[:, 0]))
         for nm, v in rows:
             print(f"  {nm:28s} median {np.median(v):9.0f}  max {v.max():9.0f} cycles")
+        if k == 0 and (s[:, 10] > 0).all():  # forward sub-phases of tile 4 (stamped slots 10..13)
+            sub = [("  tile 4: softmax", s[:, 10] - s[:, 6]), ("  tile 4: stage 5", s[:, 11] - s[:, 10]),
+                   ("  tile 4: stages 2+3 (next tile)", s[:, 12] - s[:, 11]),
+                   ("  tile 4: stage 1 + X loads", s[:, 13] - s[:, 12]), ("  tile 4: to next tile (barrier)", s[:, 7] - s[:, 13])]
+            for nm, v in sub:
+                print(f"  {nm:28s} median {np.median(v):9.0f}  max {v.max():9.0f} cycles")
         t0 = s[:, 38].min()
         ent, ex = (s[:, 38] - t0) * 10.0, (s[:, 39] - t0) * 10.0  # ns
         print(f"  real time: entry spread {ent.max():.0f} ns (median {np.median(ent):.0f}), "

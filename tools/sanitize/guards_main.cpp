@@ -80,14 +80,19 @@ static void mlp_contracts() {
   // unsupported hidden width -> no kernel instance
   EXPECT(har_mlp_fwd_infer(hbuf, 64, hbuf, fbuf, hbuf, fbuf, 192, hbuf, fbuf, 64, 6, fbuf, ibuf, 0), -4);
 
-  // fused backward: H != 256, B % 64, K0 not 32/64, short slab stride, misaligned, no h1 and no W0
+  // three-kernel step: H != 256, K0 not 32 / 64, B % 64, C outside [1, 16], short slab stride, misaligned
+  uint32_t* w = reinterpret_cast<uint32_t*>(ibuf);
   float* g = fbuf;
-  EXPECT(har_mlp_bwd_fused(hbuf, hbuf, hbuf, 64, hbuf, 128, 64, g, g, g, 1 << 20, ibuf, hbuf, fbuf, 0), -2);
-  EXPECT(har_mlp_bwd_fused(hbuf, hbuf, hbuf, 64, hbuf, 256, 96, g, g, g, 1 << 20, ibuf, hbuf, fbuf, 0), -2);
-  EXPECT(har_mlp_bwd_fused(hbuf, hbuf, hbuf, 48, hbuf, 256, 64, g, g, g, 1 << 20, ibuf, hbuf, fbuf, 0), -2);
-  EXPECT(har_mlp_bwd_fused(hbuf, hbuf, hbuf, 64, hbuf, 256, 64, g, g, g, 256 * 255, ibuf, hbuf, fbuf, 0), -2);
-  EXPECT(har_mlp_bwd_fused(hbuf + 4, hbuf, hbuf, 64, hbuf, 256, 64, g, g, g, 1 << 20, ibuf, hbuf, fbuf, 0), -3);
-  EXPECT(har_mlp_bwd_fused(hbuf, nullptr, hbuf, 64, hbuf, 256, 64, g, g, g, 1 << 20, ibuf, nullptr, fbuf, 0), -4);
+  EXPECT(har_mlp_step_fwd(hbuf, 64, hbuf, fbuf, hbuf, fbuf, 128, hbuf, fbuf, ibuf, 64, 6, 1.f, w, w, g, g, ibuf, 0), -2);
+  EXPECT(har_mlp_step_fwd(hbuf, 48, hbuf, fbuf, hbuf, fbuf, 256, hbuf, fbuf, ibuf, 64, 6, 1.f, w, w, g, g, ibuf, 0), -2);
+  EXPECT(har_mlp_step_fwd(hbuf, 64, hbuf, fbuf, hbuf, fbuf, 256, hbuf, fbuf, ibuf, 96, 6, 1.f, w, w, g, g, ibuf, 0), -2);
+  EXPECT(har_mlp_step_fwd(hbuf, 64, hbuf, fbuf, hbuf, fbuf, 256, hbuf, fbuf, ibuf, 64, 17, 1.f, w, w, g, g, ibuf, 0), -2);
+  EXPECT(har_mlp_step_fwd(hbuf + 4, 64, hbuf, fbuf, hbuf, fbuf, 256, hbuf, fbuf, ibuf, 64, 6, 1.f, w, w, g, g, ibuf, 0), -3);
+  EXPECT(har_mlp_step_bwd(w, w, hbuf, 64, hbuf, 128, hbuf, fbuf, hbuf, 64, g, g, g, g, 1 << 20, ibuf, 0), -2);
+  EXPECT(har_mlp_step_bwd(w, w, hbuf, 64, hbuf, 256, hbuf, fbuf, hbuf, 96, g, g, g, g, 1 << 20, ibuf, 0), -2);
+  EXPECT(har_mlp_step_bwd(w, w, hbuf, 48, hbuf, 256, hbuf, fbuf, hbuf, 64, g, g, g, g, 1 << 20, ibuf, 0), -2);
+  EXPECT(har_mlp_step_bwd(w, w, hbuf, 64, hbuf, 256, hbuf, fbuf, hbuf, 64, g, g, g, g, 256 * 255, ibuf, 0), -2);
+  EXPECT(har_mlp_step_bwd(w + 1, w, hbuf, 64, hbuf, 256, hbuf, fbuf, hbuf, 64, g, g, g, g, 1 << 20, ibuf, 0), -3);
 }
 
 static void window_contracts() {
@@ -153,7 +158,8 @@ static void data_contracts() {
 static void sizing_helpers() {
   const int Bs[] = {1, 15, 16, 31, 32, 63, 64, 65, 256, 4096, 65536, 1 << 20, INT_MAX / 2, INT_MAX};
   for (int B : Bs) {
-    const int grid = har_mlp_fwd_head_grid(B), sl = har_mlp_bwd_fused_slices(B);
+    const int grid = har_mlp_fwd_head_grid(B), sl = har_mlp_step_slices(B);
+    EXPECT_TRUE(har_mlp_step_grid(B) >= 1 && har_mlp_step_grid(B) <= 256);
     EXPECT_TRUE(grid >= 1 && grid <= 256);
     EXPECT_TRUE(sl >= 1 && sl <= 64);
     EXPECT_TRUE(har_softmax_ce_head_blocks(B) >= 1);
