@@ -284,7 +284,7 @@ class MLPEngine:
         rebuilt from them, h1 recomputed, dW1 + dgrad + relu' + dW0 / db0 / db1 in one pass).  The
         gradient reduction + Adam follow in ``train_step``.  ``record`` (a list) receives one
         re-launchable closure per kernel (tools/mlp_phase_probe.py)."""
-        L, mod, s = self.layout, _native.kernels(), _native.stream_ptr()
+        L, mod = self.layout, _native.kernels()
         B, H, K0 = Xb.shape[0], self.dims[-1], L.in_pad
         total = L.total
         self.step_nwg = mod.mlp_step_grid(B)
@@ -296,13 +296,14 @@ class MLPEngine:
             mod.mlp_step_fwd(Xb.data_ptr(), K0, w(Pb, "W0"), w(P, "b0"), w(Pb, "W1"), w(P, "b1"), H, w(Pb, "Wout"),
                              w(P, "bout"), y32.data_ptr(), B, L.num_classes, float(scale), self.dz.data_ptr(),
                              self.h2mask.data_ptr(), self.sslab.data_ptr(), self.sblock_loss.data_ptr(),
-                             self.sblock_correct.data_ptr(), s)
+                             self.sblock_correct.data_ptr(), _native.stream_ptr())
 
-        def bwd():
+        def bwd():  # also sums the forward's dWout / dbout slabs into G
             off = lambda n: sb + 4 * L.by_name[n].offset  # noqa: E731
             mod.mlp_step_bwd(self.dz.data_ptr(), self.h2mask.data_ptr(), Xb.data_ptr(), K0, w(Pb, "W1"), H,
                              w(Pb, "W0"), w(P, "b0"), w(Pb, "Wout"), B, off("W1"), off("W0"), off("b0"), off("b1"),
-                             total, self.step_count.data_ptr(), s)
+                             total, self.step_count.data_ptr(), self.sslab.data_ptr(), self.sslab.shape[1],
+                             w(self.G, "Wout"), w(self.G, "bout"), _native.stream_ptr())
 
         fwd()
         if on_grad is not None:
@@ -401,12 +402,12 @@ class MLPEngine:
         regions = []
         wo, bo = L.by_name["Wout"].offset, L.by_name["bout"].offset
         if self.last_path == "step":
-            H, w = self.dims[-1], self.sslab.shape[1]
+            H = self.dims[-1]
             w0, b1 = L.by_name["W0"].offset, L.by_name["b1"].offset
-            fs = self.sslab.data_ptr()
             regions.append((w0, b1 + H, self.slabs.data_ptr() + 4 * w0, self.step_S, total))  # W0, b0, W1, b1
-            regions.append((wo, wo + 16 * H, fs, self.step_nwg, w))
-            regions.append((bo, bo + 16, fs + 4 * 16 * H, self.step_nwg, w))
+            g = self.G.data_ptr()  # dWout / dbout: summed into G by the step backward
+            regions.append((wo, wo + 16 * H, g + 4 * wo, 1, 4))
+            regions.append((bo, bo + 16, g + 4 * bo, 1, 4))
             return regions
         end = wo if self.last_fused else total
         regions.append((0, end, self.slabs.data_ptr(), self.active_splits, total))
@@ -484,6 +485,7 @@ class MLPEngine:
                      dz=self.dz.data_ptr(), mask=self.h2mask.data_ptr(), fslab=self.sslab.data_ptr(),
                      bloss=self.sblock_loss.data_ptr(), bcorr=self.sblock_correct.data_ptr(), gw1=off("W1"),
                      gw0=off("W0"), gb0=off("b0"), gb1=off("b1"), step=self.step_count.data_ptr(),
+                     fslab_w=self.sslab.shape[1], gwo=w(self.G, "Wout"), gbo=w(self.G, "bout"),
                      G=self.G.data_ptr(), P=P.data_ptr(), m=self.m.data_ptr(), v=self.v.data_ptr(), Pb=Pb.data_ptr(),
                      K0=L.in_pad, H=self.dims[-1], C=L.num_classes, stride=L.total, n=L.total, lr=float(self.lr),
                      beta1=float(self.betas[0]), beta2=float(self.betas[1]), eps=float(self.eps), wd=float(self.wd),

@@ -166,7 +166,8 @@ struct QnArgsHolder {
 // every step were ~10 us of host time per 70 us step: enough to starve the GPU when not graph-captured).
 struct MlpStepPlan {
   u W0, b0, W1, b1, Wo, bo, dz, mask, fslab, bloss, bcorr, gw1, gw0, gb0, gb1, step, G, Pw, m, v, Pb;
-  int K0, H, C;
+  int K0, H, C, fslab_w;
+  u gwo, gbo;
   int64_t stride, n;
   float lr, b1c, b2c, eps, wd;
   std::vector<const float*> src;
@@ -184,7 +185,7 @@ struct MlpStepPlan {
       check(har_mlp_step_bwd(P<const uint32_t>(dz), P<const uint32_t>(mask), P<const uint16_t>(X), K0,
                              P<const uint16_t>(W1), H, P<const uint16_t>(W0), P<const float>(b0),
                              P<const uint16_t>(Wo), B, P<float>(gw1), P<float>(gw0), P<float>(gb0), P<float>(gb1),
-                             stride, P<int32_t>(step), s),
+                             stride, P<int32_t>(step), P<const float>(fslab), fslab_w, P<float>(gwo), P<float>(gbo), s),
             "mlp_step_bwd");
     }
     const int gm = mode == 1 ? 1 | 4 : mode == 2 ? 1 | 2 : 4;  // GR_REDUCE 1, GR_STORE 2, GR_ADAM 4
@@ -504,6 +505,9 @@ PYBIND11_MODULE(_har_native, m) {
           else if (!strcmp(k, "m")) p.m = x; else if (!strcmp(k, "v")) p.v = x; else p.Pb = x;
         }
         p.K0 = d["K0"].cast<int>();
+        p.fslab_w = d["fslab_w"].cast<int>();
+        p.gwo = d["gwo"].cast<u>();
+        p.gbo = d["gbo"].cast<u>();
         p.H = d["H"].cast<int>();
         p.C = d["C"].cast<int>();
         p.stride = d["stride"].cast<int64_t>();
@@ -537,11 +541,11 @@ PYBIND11_MODULE(_har_native, m) {
           "mlp_step_fwd");
   });
   m.def("mlp_step_bwd", [](u dz, u mask, u X, int K0, u W1, int H, u W0, u b0, u Wo, int B, u gw1, u gw0, u gb0,
-                           u gb1, int64_t stride, u tick, u stream) {
+                           u gb1, int64_t stride, u tick, u fslab, int fslab_w, u gwo, u gbo, u stream) {
     check(har_mlp_step_bwd(P<const uint32_t>(dz), P<const uint32_t>(mask), P<const uint16_t>(X), K0,
                            P<const uint16_t>(W1), H, P<const uint16_t>(W0), P<const float>(b0), P<const uint16_t>(Wo),
                            B, P<float>(gw1), P<float>(gw0), P<float>(gb0), P<float>(gb1), stride, P<int32_t>(tick),
-                           S(stream)),
+                           P<const float>(fslab), fslab_w, P<float>(gwo), P<float>(gbo), S(stream)),
           "mlp_step_bwd");
   });
   m.def("mlp_fwd_head", [](u X, int K0, u W0, u b0, u W1, u b1, int H, u Wo, u bo, u labels, int B, int C,

@@ -83,7 +83,8 @@ int har_mlp_step_fwd(const uint16_t* X, int K0, const uint16_t* W0, const float*
                      int32_t* block_correct, hipStream_t s);
 int har_mlp_step_bwd(const uint32_t* dz, const uint32_t* mask, const uint16_t* X, int K0, const uint16_t* W1, int H,
                      const uint16_t* W0, const float* b0, const uint16_t* Wo, int B, float* gw1, float* gw0,
-                     float* gb0, float* gb1, int64_t slab_stride, int32_t* tick, hipStream_t s);
+                     float* gb0, float* gb1, int64_t slab_stride, int32_t* tick, const float* fslab, int fslab_w,
+                     float* gwo, float* gbo, hipStream_t s);
 int har_mlp_step_grid(int B);
 int har_mlp_step_slices(int B);
 int har_mlp_step_fwd_slab_width(int H);

@@ -179,9 +179,8 @@ __global__ void cast_pad_kernel(const float* __restrict__ in, int rows, int cin,
 // GR_ADAM) and N > 1 (GR_REDUCE | GR_STORE, all-reduce, GR_ADAM) apply the same summation and the
 // same Adam arithmetic.
 constexpr int GR_REDUCE = 1, GR_STORE = 2, GR_ADAM = 4;
-constexpr int GR_W = 16;  // waves per workgroup
-
-__global__ __launch_bounds__(1024) void grad_reduce_adam_kernel(GradRegions rg, int64_t n, float* __restrict__ G,
+template <int GR_W>  // waves per workgroup
+__global__ __launch_bounds__(64 * GR_W) void grad_reduce_adam_kernel(GradRegions rg, int64_t n, float* __restrict__ G,
                                                                 float* __restrict__ param, float* __restrict__ m,
                                                                 float* __restrict__ v, bf16_t* __restrict__ pb,
                                                                 float lr, float b1, float b2, float eps, float wd,
@@ -235,12 +234,16 @@ __global__ __launch_bounds__(1024) void grad_reduce_adam_kernel(GradRegions rg, 
     }
     part[q][k] = acc;
     __syncthreads();
-    if (q < 4) {  // 16 -> 4 partials (fixed pairs)
+    if (GR_W == 16 && q < 4) {  // 16 -> 4 partials (fixed pairs)
       const float4 a = part[q][k], b = part[q + 4][k], c = part[q + 8][k], d = part[q + 12][k];
       part[q][k] = make_float4((a.x + b.x) + (c.x + d.x), (a.y + b.y) + (c.y + d.y), (a.z + b.z) + (c.z + d.z),
                                (a.w + b.w) + (c.w + d.w));
     }
-    __syncthreads();
+    if (GR_W == 8 && q < 4) {
+      const float4 a = part[q][k], b = part[q + 4][k];
+      part[q][k] = make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
+    }
+    if (GR_W > 4) __syncthreads();
   }
   if (q == 0 && e < n) {
     float4 g;
@@ -338,8 +341,17 @@ extern "C" int har_grad_reduce_adam(int nreg, const float* const* src, const int
   const int64_t blocks = (n / 4 + 63) / 64;
   if (blocks == 0) return 0;
   if (tick) adam_tick_kernel<<<1, 1, 0, s>>>(step);
-  grad_reduce_adam_kernel<<<(int)blocks, 64 * GR_W, 0, s>>>(rg, n, G, param, m, v, pb, lr, b1, b2, eps, wd, step,
-                                                            mode);
+  static const int w = [] {
+    const char* e = getenv("HAR_GR_W");
+    return e ? atoi(e) : 16;
+  }();
+  if (w == 4)
+    grad_reduce_adam_kernel<4><<<(int)blocks, 256, 0, s>>>(rg, n, G, param, m, v, pb, lr, b1, b2, eps, wd, step, mode);
+  else if (w == 8)
+    grad_reduce_adam_kernel<8><<<(int)blocks, 512, 0, s>>>(rg, n, G, param, m, v, pb, lr, b1, b2, eps, wd, step, mode);
+  else
+    grad_reduce_adam_kernel<16><<<(int)blocks, 1024, 0, s>>>(rg, n, G, param, m, v, pb, lr, b1, b2, eps, wd, step,
+                                                             mode);
   HAR_CHECK_LAUNCH();
   return 0;
 }

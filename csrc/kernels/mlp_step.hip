@@ -343,6 +343,7 @@ __global__ __launch_bounds__(512) void mlp_bwd3_kernel(
     const bf16_t* __restrict__ W1, const bf16_t* __restrict__ W0, const float* __restrict__ b0,
     const bf16_t* __restrict__ Wo, int B, int S, float* __restrict__ gw1, float* __restrict__ gw0,
     float* __restrict__ gb0, float* __restrict__ gb1, int64_t slab_stride, int32_t* __restrict__ tick,
+    const float* __restrict__ fslab, int fslab_w, int nfwd, float* __restrict__ gwo, float* __restrict__ gbo,
     uint64_t* __restrict__ stamps) {
   using L = Bwd3Lds<K0>;
   constexpr int NXB = L::NXB, KC = HH / 32, XP = L::XP, NFW = K0 / 32;
@@ -391,7 +392,33 @@ __global__ __launch_bounds__(512) void mlp_bwd3_kernel(
   for (int kc = 0; kc < NFW; ++kc)
     w0q[kc] = *reinterpret_cast<const bf16x8_t*>(W0 + (size_t)(qu0 + 16 * ubh + c16) * K0 + kc * 32 + 8 * g);
   const float4 b0q = *reinterpret_cast<const float4*>(b0 + qu0 + 16 * ubh + 4 * g);
+  // The forward's per-workgroup dWout / dbout partials are complete before this kernel starts: one
+  // wave per 16-byte gradient column sums them (lane l: slabs l, l + 64, ...; then a fixed xor tree)
+  // into G, so the reduction kernel reads one slab instead of har_mlp_step_grid(B).  The first
+  // column's loads are issued here and overlap the staging above.
+  constexpr int WO4 = NCLS * HH / 4, NC4 = WO4 + NCLS / 4;
+  const int gwv = blockIdx.x * 8 + wave, nwv = gridDim.x * 8;
+  f32x4_t px[4];
+  auto wo_load = [&](int c4) {
+    const float* src = fslab + (c4 < WO4 ? 4 * c4 : NCLS * HH + 4 * (c4 - WO4));
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      px[r] = lane + 64 * r < nfwd ? *reinterpret_cast<const f32x4_t*>(src + (size_t)(lane + 64 * r) * fslab_w)
+                                   : f32x4_t{0.f, 0.f, 0.f, 0.f};
+  };
+  if (fslab && gwv < NC4) wo_load(gwv);
   __syncthreads();
+  if (fslab) {
+    for (int c4 = gwv; c4 < NC4; c4 += nwv) {
+      if (c4 != gwv) wo_load(c4);
+      f32x4_t v = (px[0] + px[1]) + (px[2] + px[3]);
+#pragma unroll
+      for (int o = 32; o >= 1; o >>= 1)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] += __shfl_xor(v[e], o, 64);
+      if (lane == 0) *reinterpret_cast<f32x4_t*>(c4 < WO4 ? gwo + 4 * c4 : gbo + 4 * (c4 - WO4)) = v;
+    }
+  }
   // (a) A fragments: A[u][k = j] = W1[32 kc + 8g + i][qu0 + 16 (up + e) + c16] (natural k order)
   bf16x8_t w1t[2][KC];
 #pragma unroll
@@ -609,10 +636,11 @@ void launch_fwd3(const bf16_t* X, const bf16_t* W0, const float* b0, const bf16_
 template <int K0>
 void launch_bwd3(const uint32_t* dz, const uint32_t* mask, const bf16_t* X, const bf16_t* W1, const bf16_t* W0,
                  const float* b0, const bf16_t* Wo, int B, int S, float* gw1, float* gw0, float* gb0, float* gb1,
-                 int64_t stride, int32_t* tick, hipStream_t s) {
+                 int64_t stride, int32_t* tick, const float* fslab, int fslab_w, int nfwd, float* gwo, float* gbo,
+                 hipStream_t s) {
   auto k = g_har_mlp_stamps ? mlp_bwd3_kernel<K0, true> : mlp_bwd3_kernel<K0, false>;
   k<<<S * BQ, 512, Bwd3Lds<K0>::bytes, s>>>(dz, mask, X, W1, W0, b0, Wo, B, S, gw1, gw0, gb0, gb1, stride, tick,
-                                           g_har_mlp_stamps ? g_har_mlp_stamps + STAMP_BWD_OFF : nullptr);
+                                           fslab, fslab_w, nfwd, gwo, gbo, g_har_mlp_stamps ? g_har_mlp_stamps + STAMP_BWD_OFF : nullptr);
 }
 
 }  // namespace
@@ -642,20 +670,27 @@ extern "C" int har_mlp_step_fwd(const uint16_t* X, int K0, const uint16_t* W0, c
 }
 
 // Backward of the step: per row slice s < har_mlp_step_slices(B) the partials of dW1, dW0, db0 (and db1)
-// at gw1 / gw0 / gb0 / gb1 + s * slab_stride.
+// at gw1 / gw0 / gb0 / gb1 + s * slab_stride.  With fslab (the forward's har_mlp_step_grid(B)
+// per-workgroup slabs, row stride fslab_w) it also writes their sums: dWout rows 0..15 to gwo and
+// dbout to gbo (fixed summation order).
 extern "C" int har_mlp_step_bwd(const uint32_t* dz, const uint32_t* mask, const uint16_t* X, int K0,
                                 const uint16_t* W1, int H, const uint16_t* W0, const float* b0, const uint16_t* Wo,
                                 int B, float* gw1, float* gw0, float* gb0, float* gb1, int64_t slab_stride,
-                                int32_t* tick, hipStream_t s) {
+                                int32_t* tick, const float* fslab, int fslab_w, float* gwo, float* gbo,
+                                hipStream_t s) {
   if (H != HH || B <= 0 || B % BRT || (K0 != 32 && K0 != 64) || slab_stride < (int64_t)H * H) return -2;
   if (((uintptr_t)dz | (uintptr_t)mask | (uintptr_t)X | (uintptr_t)W1 | (uintptr_t)W0 | (uintptr_t)b0 |
-       (uintptr_t)Wo | (uintptr_t)gw1) & 15)
+       (uintptr_t)Wo | (uintptr_t)gw1 | (uintptr_t)fslab | (uintptr_t)gwo | (uintptr_t)gbo) & 15)
     return -3;
+  const int nfwd = har_mlp_step_grid(B);
+  if (fslab && (fslab_w < har_mlp_step_fwd_slab_width(H) || fslab_w % 4 || nfwd > 256 || !gwo || !gbo)) return -2;
   const int S = har_mlp_step_slices(B);
   if (K0 == 64)
-    launch_bwd3<64>(dz, mask, X, W1, W0, b0, Wo, B, S, gw1, gw0, gb0, gb1, slab_stride, tick, s);
+    launch_bwd3<64>(dz, mask, X, W1, W0, b0, Wo, B, S, gw1, gw0, gb0, gb1, slab_stride, tick, fslab, fslab_w, nfwd,
+                    gwo, gbo, s);
   else
-    launch_bwd3<32>(dz, mask, X, W1, W0, b0, Wo, B, S, gw1, gw0, gb0, gb1, slab_stride, tick, s);
+    launch_bwd3<32>(dz, mask, X, W1, W0, b0, Wo, B, S, gw1, gw0, gb0, gb1, slab_stride, tick, fslab, fslab_w, nfwd,
+                    gwo, gbo, s);
   HAR_CHECK_LAUNCH();
   return 0;
 }

@@ -16,16 +16,35 @@ from har.models.mlp import MLPEngine, pad_input_bf16  # noqa: E402
 from har.ops import _native  # noqa: E402
 
 
-def timed(fn, reps=100):
+def timed(fn, reps=100, graph=None):
+    """us per call: min over 3 runs of `reps` back-to-back calls.  graph=True captures the `reps`
+    calls in one HIP graph and times its replay (device time, no host launch cost: a short kernel
+    launched from Python is otherwise host-bound); default from HAR_PROBE_GRAPH (1)."""
+    if graph is None:
+        graph = os.environ.get("HAR_PROBE_GRAPH", "1") != "0"
     for _ in range(5):
         fn()
     torch.cuda.synchronize()
+    run = None
+    if graph:
+        g = torch.cuda.CUDAGraph()
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            with torch.cuda.graph(g, stream=s):
+                for _ in range(reps):
+                    fn()
+        torch.cuda.current_stream().wait_stream(s)
+        run = g.replay
+    else:
+        def run():
+            for _ in range(reps):
+                fn()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     best = 1e30
     for _ in range(3):
         e0.record()
-        for _ in range(reps):
-            fn()
+        run()
         e1.record()
         torch.cuda.synchronize()
         best = min(best, e0.elapsed_time(e1) * 1e3 / reps)
@@ -88,7 +107,8 @@ def main():
     if sys.argv[1:2] == ["--stamps"]:
         return stamps(int(sys.argv[2]) if len(sys.argv) > 2 else 65536)
     sizes = [int(a) for a in sys.argv[1:]] or [16384, 32768, 65536, 131072, 262144]
-    print(f"{'B':>8s} {'step':>8s} {'fwd':>8s} {'bwd':>8s} {'reduce':>8s}   (us, min of 3 x 100 launches)")
+    print(f"{'B':>8s} {'step':>8s} {'fwd':>8s} {'bwd':>8s} {'reduce':>8s} {'eager':>8s}  (us, min of 3 x 100 launches; "
+          "graph-replayed unless HAR_PROBE_GRAPH=0, eager = the step launched from Python)")
     for B in sizes:
         eng = MLPEngine([43, 256, 256, 6], B, dev, seed=1)
         g = torch.Generator(device=dev).manual_seed(0)
@@ -97,12 +117,13 @@ def main():
         eng.train_step(X, y, B)
         torch.cuda.synchronize()
         step = timed(lambda: eng.train_step(X, y, B))
+        step_eager = timed(lambda: eng.train_step(X, y, B), graph=False)
         phases = getattr(eng, "phase_fns", None)
         if phases is None:
             print(f"{B:8d} {step:8.1f}  (engine exposes no phase_fns)")
             continue
         t = {k: timed(f) for k, f in phases(X, y, B).items()}
-        print(f"{B:8d} {step:8.1f} " + " ".join(f"{t.get(k, float('nan')):8.1f}" for k in ("fwd", "bwd", "reduce")))
+        print(f"{B:8d} {step:8.1f} " + " ".join(f"{t.get(k, float('nan')):8.1f}" for k in ("fwd", "bwd", "reduce")) + f" {step_eager:8.1f}")
         del eng
         torch.cuda.empty_cache()
 

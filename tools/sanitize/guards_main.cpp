@@ -88,11 +88,12 @@ static void mlp_contracts() {
   EXPECT(har_mlp_step_fwd(hbuf, 64, hbuf, fbuf, hbuf, fbuf, 256, hbuf, fbuf, ibuf, 96, 6, 1.f, w, w, g, g, ibuf, 0), -2);
   EXPECT(har_mlp_step_fwd(hbuf, 64, hbuf, fbuf, hbuf, fbuf, 256, hbuf, fbuf, ibuf, 64, 17, 1.f, w, w, g, g, ibuf, 0), -2);
   EXPECT(har_mlp_step_fwd(hbuf + 4, 64, hbuf, fbuf, hbuf, fbuf, 256, hbuf, fbuf, ibuf, 64, 6, 1.f, w, w, g, g, ibuf, 0), -3);
-  EXPECT(har_mlp_step_bwd(w, w, hbuf, 64, hbuf, 128, hbuf, fbuf, hbuf, 64, g, g, g, g, 1 << 20, ibuf, 0), -2);
-  EXPECT(har_mlp_step_bwd(w, w, hbuf, 64, hbuf, 256, hbuf, fbuf, hbuf, 96, g, g, g, g, 1 << 20, ibuf, 0), -2);
-  EXPECT(har_mlp_step_bwd(w, w, hbuf, 48, hbuf, 256, hbuf, fbuf, hbuf, 64, g, g, g, g, 1 << 20, ibuf, 0), -2);
-  EXPECT(har_mlp_step_bwd(w, w, hbuf, 64, hbuf, 256, hbuf, fbuf, hbuf, 64, g, g, g, g, 256 * 255, ibuf, 0), -2);
-  EXPECT(har_mlp_step_bwd(w + 1, w, hbuf, 64, hbuf, 256, hbuf, fbuf, hbuf, 64, g, g, g, g, 1 << 20, ibuf, 0), -3);
+  EXPECT(har_mlp_step_bwd(w, w, hbuf, 64, hbuf, 128, hbuf, fbuf, hbuf, 64, g, g, g, g, 1 << 20, ibuf, nullptr, 0, g, g, 0), -2);
+  EXPECT(har_mlp_step_bwd(w, w, hbuf, 64, hbuf, 256, hbuf, fbuf, hbuf, 96, g, g, g, g, 1 << 20, ibuf, nullptr, 0, g, g, 0), -2);
+  EXPECT(har_mlp_step_bwd(w, w, hbuf, 48, hbuf, 256, hbuf, fbuf, hbuf, 64, g, g, g, g, 1 << 20, ibuf, nullptr, 0, g, g, 0), -2);
+  EXPECT(har_mlp_step_bwd(w, w, hbuf, 64, hbuf, 256, hbuf, fbuf, hbuf, 64, g, g, g, g, 256 * 255, ibuf, nullptr, 0, g, g, 0), -2);
+  EXPECT(har_mlp_step_bwd(w + 1, w, hbuf, 64, hbuf, 256, hbuf, fbuf, hbuf, 64, g, g, g, g, 1 << 20, ibuf, nullptr, 0, g, g, 0), -3);
+  EXPECT(har_mlp_step_bwd(w, w, hbuf, 64, hbuf, 256, hbuf, fbuf, hbuf, 64, g, g, g, g, 1 << 20, ibuf, g, 100, g, g, 0), -2);
 }
 
 static void window_contracts() {
