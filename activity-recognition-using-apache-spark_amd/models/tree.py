@@ -155,7 +155,7 @@ class ForestBuilder:
         n_nodes = np.ones(Tn, dtype=np.int64)
         if dev.type == "cuda":
             rw = None if row_weight is None else row_weight.to(device=dev, dtype=torch.float32).contiguous()
-            return _fit_device(self, y32, rw, row_offset, N, F, m, maxn)
+            return _fit_device(self, y32, rw, row_offset, N, F, m, maxn, n_all)
         # ---- CPU builder (PyTorch; the oracle of the device loop) ----
         W = self.bootstrap_weights(N, dev, row_offset)        # [T, N]
         if row_weight is not None:
@@ -275,10 +275,13 @@ FORCE_NODE_BLOCKS = False
 FORCE_LEVEL_SYNC = False
 # host timestamps of the last device level loop: (start, every level enqueued, node counts read back)
 LAST_LEVEL_TIMES = (0.0, 0.0, 0.0)
+# device -> host count reads the level loops have made (0 per fit when every level runs on the device
+# counts; tests/test_gpu_distributed.py checks the data-parallel fits)
+LEVEL_SYNCS = 0
 
 
 def _levels_device_frontier(b: "ForestBuilder", y32, W, N: int, F: int, m: int, maxn: int, stats, feature, thresh,
-                            left, right, gains, node_of):
+                            left, right, gains, node_of, n_all: Optional[int] = None):
     """Device level loop with the frontier resident on the GPU; returns the per-tree node counts
     (a device tensor: the caller reads them back once).
 
@@ -297,9 +300,18 @@ def _levels_device_frontier(b: "ForestBuilder", y32, W, N: int, F: int, m: int, 
     by a bound (next candidates <= 2 x this level's, per tree <= 2 x the per-tree maximum).  On one
     device the whole fit is therefore enqueued with no device -> host read until the final node
     counts.  A level whose bound would exceed ``ASYNC_MAX_NODES`` / ``ASYNC_MAX_COUNT_WS`` or the
-    grouping's LDS (``GROUP_MAX_NT`` per tree), and every level of a data-parallel fit (the
-    collectives are sized on the host), first reads the previous level's 16 bytes back — the
-    kernels then get the exact counts.  Both modes grow the same forest node for node."""
+    grouping's LDS (``GROUP_MAX_NT`` per tree) first reads the previous level's 16 bytes back — the
+    kernels then get the exact counts.  Both modes grow the same forest node for node.
+
+    Data parallel (``b.allreduce`` / ``b.owner``) runs this same loop: the same grouping, plan and
+    work items, with the level's histograms kept per node (``ops.tree.hist_split_planned_dp``) and
+    summed across ranks before the split search.  Every collective is sized by the host bound of
+    the level's node count, which all ranks share (the bounds use the global row count ``n_all``),
+    so a DP level reads nothing back either; the frontier is replicated (every rank applies the
+    same winners).  Sibling subtraction stays single-device (a derived node would need its
+    parent's summed histogram on the rank that owns it)."""
+    dp = b.owner is not None or b.allreduce is not None
+    n_all = N if n_all is None else n_all
     dev = W.device
     Tn, K, D = b.T, b.K, b.D
     mod = _native.kernels()
@@ -308,10 +320,11 @@ def _levels_device_frontier(b: "ForestBuilder", y32, W, N: int, F: int, m: int, 
     Wf = W.reshape(-1).contiguous()
     bins_rm = b.bins.t().contiguous()  # [N, F] for the histogram gathers (partition keeps [F, N])
     nch = mod.tree_level_group_chunks(N)
-    planned = b.owner is None and b.allreduce is None and not FORCE_NODE_BLOCKS
+    nch_g = mod.tree_level_group_chunks(n_all)  # rank-independent bound checks (DP: every rank decides alike)
+    planned = not FORCE_NODE_BLOCKS
     async_ok = planned and not FORCE_SORT_GROUPING and not FORCE_LEVEL_SYNC
     slot_bytes = 4 * F * b.max_bins * K
-    subtract = planned and m >= F and SIBLING_SUBTRACTION and Tn * N >= SUBTRACT_MIN_PAIRS
+    subtract = planned and not dp and m >= F and SIBLING_SUBTRACTION and Tn * N >= SUBTRACT_MIN_PAIRS
     hprev = parent_of = derive_from = None  # the previous level's store and this level's derive info
 
     # root frontier on the device: scal_all row 0 = [0, root candidates, 1, max root weight bits]
@@ -330,9 +343,11 @@ def _levels_device_frontier(b: "ForestBuilder", y32, W, N: int, F: int, m: int, 
     tlo_next = torch.empty(Tn + 1, **i32)
     scal_h = None
     max_w = 0.0
-    if not async_ok:  # exact counts from the start (data parallel / test hooks): read row 0 back
+    global LEVEL_SYNCS
+    if not async_ok:  # exact counts from the start (test hooks): read row 0 back
         scal_h = torch.empty(4, dtype=torch.int32).pin_memory()
         scal_h.copy_(scal_all[:4])
+        LEVEL_SYNCS += 1
         A, wbits = int(scal_h[1]), int(scal_h[3])
         max_w = float(np.array([wbits], dtype=np.int32).view(np.float32)[0])
         exact = True
@@ -369,7 +384,13 @@ def _levels_device_frontier(b: "ForestBuilder", y32, W, N: int, F: int, m: int, 
         store = None
         if subtract and A * slot_bytes <= SUBTRACT_MAX_BYTES:
             store = torch.empty(A * slot_bytes // 4, dtype=torch.float32, device=dev)
-        if planned:
+        if planned and dp:
+            # data parallel: the same work items, histograms summed across ranks by the bound A
+            res = T.hist_split_planned_dp(b.bins, b.nbins, y32, rows, row_w, starts, counts, feats, K, b.max_bins,
+                                          b.min_inst, b.min_gain, b.impurity, rows_bound=Tn * N, a_dev=a_dev,
+                                          allreduce=None if b.owner is not None else b.allreduce, owner=b.owner,
+                                          bins_rm=bins_rm)
+        elif planned:
             # one device: work items by rows (big nodes chunked), no host sync (ops/tree.py)
             res = T.hist_split_planned(b.bins, b.nbins, y32, rows, row_w, starts, counts, feats, K, b.max_bins,
                                        b.min_inst, b.min_gain, b.impurity, rows_bound=Tn * N, bins_rm=bins_rm,
@@ -390,7 +411,7 @@ def _levels_device_frontier(b: "ForestBuilder", y32, W, N: int, F: int, m: int, 
         front = torch.empty(2 * A, dtype=torch.float32, device=dev)
         q = torch.empty(2 * A + 1, **i32)
         ct_next, cn_next = torch.empty(2 * A, **i32), torch.empty(2 * A, **i32)
-        A_b = min(2 * A, Tn * N)
+        A_b = min(2 * A, Tn * n_all)
         # the next level derives siblings when this level kept its histograms and the next one can
         derive = store is not None and A_b * slot_bytes <= SUBTRACT_MAX_BYTES
         par_n = torch.empty(2 * A, **i32) if derive else None
@@ -401,7 +422,7 @@ def _levels_device_frontier(b: "ForestBuilder", y32, W, N: int, F: int, m: int, 
                           tlo_next.data_ptr(), cand_idx.data_ptr(), scal.data_ptr(), a_dev,
                           par_n.data_ptr() if derive else 0, der_n.data_ptr() if derive else 0, st)
         # the last level commits on the device count too (nothing after it needs the host)
-        bounds_ok = A_b <= ASYNC_MAX_NODES and nch * A_b <= ASYNC_MAX_COUNT_WS and 2 * nt_max <= GROUP_MAX_NT
+        bounds_ok = A_b <= ASYNC_MAX_NODES and nch_g * A_b <= ASYNC_MAX_COUNT_WS and 2 * nt_max <= GROUP_MAX_NT
         stay_async = async_ok and (depth + 1 == D or bounds_ok)
         if stay_async:  # the next level runs on the device counts in scal
             S, s_dev, A_next, nt_next = A, scal.data_ptr(), A_b, 2 * nt_max
@@ -409,6 +430,7 @@ def _levels_device_frontier(b: "ForestBuilder", y32, W, N: int, F: int, m: int, 
             if scal_h is None:
                 scal_h = torch.empty(4, dtype=torch.int32).pin_memory()
             scal_h.copy_(scal)  # this level's one sync
+            LEVEL_SYNCS += 1
             S, A_next, nt_next, wbits = (int(v) for v in scal_h.tolist())
             s_dev = 0
             max_w = float(np.array([wbits], dtype=np.int32).view(np.float32)[0])
@@ -434,17 +456,17 @@ def _levels_device_frontier(b: "ForestBuilder", y32, W, N: int, F: int, m: int, 
     return nn
 
 
-def levels_all_async(b: "ForestBuilder", N: int, F: int, m: int) -> bool:
+def levels_all_async(b: "ForestBuilder", N: int, F: int, m: int, n_all: Optional[int] = None) -> bool:
     """True when every level of this fit runs on device-side counts (no host read inside the
     loop): the condition for capturing the fit in a HIP graph.  The loop's decisions depend only
     on the bounds, so this replays them."""
-    if b.owner is not None or b.allreduce is not None or FORCE_NODE_BLOCKS or FORCE_SORT_GROUPING \
-            or FORCE_LEVEL_SYNC:
+    if FORCE_NODE_BLOCKS or FORCE_SORT_GROUPING or FORCE_LEVEL_SYNC:
         return False
-    nch = _native.kernels().tree_level_group_chunks(N)
+    n_all = N if n_all is None else n_all
+    nch = _native.kernels().tree_level_group_chunks(n_all)
     A, nt = b.T, 1
     for depth in range(b.D - 1):
-        A_b = min(2 * A, b.T * N)
+        A_b = min(2 * A, b.T * n_all)
         if A_b > ASYNC_MAX_NODES or nch * A_b > ASYNC_MAX_COUNT_WS or 2 * nt > GROUP_MAX_NT:
             return False
         A, nt = A_b, 2 * nt
@@ -495,7 +517,8 @@ def _alloc_fit_buffers(Tn: int, N: int, K: int, maxn: int, dev) -> dict:
                 gains=torch.empty(Tn, maxn, dtype=torch.float32, device=dev))
 
 
-def _enqueue_fit(b: "ForestBuilder", bufs: dict, y32, rw, row_offset: int, N: int, F: int, m: int, maxn: int):
+def _enqueue_fit(b: "ForestBuilder", bufs: dict, y32, rw, row_offset: int, N: int, F: int, m: int, maxn: int,
+                 n_all: Optional[int] = None):
     """Every launch of one device fit into ``bufs`` (no host read on one device): initial node
     arrays, tree_init (bootstrap weights x row weights, node ids, root class counts, label check), the
     DP all-reduce of the root counts, the level loop.  Returns the node-count tensor."""
@@ -513,7 +536,7 @@ def _enqueue_fit(b: "ForestBuilder", bufs: dict, y32, rw, row_offset: int, N: in
         b.allreduce(root)
         bufs["stats"][:, 0] = root
     return _levels_device_frontier(b, y32, bufs["W"], N, F, m, maxn, bufs["stats"], bufs["feature"], bufs["thresh"],
-                                   bufs["left"], bufs["right"], bufs["gains"], bufs["node_of"])
+                                   bufs["left"], bufs["right"], bufs["gains"], bufs["node_of"], n_all=n_all)
 
 
 def _finish_fit(b: "ForestBuilder", bufs: dict, nn, clone: bool) -> ForestArrays:
@@ -525,10 +548,12 @@ def _finish_fit(b: "ForestBuilder", bufs: dict, nn, clone: bool) -> ForestArrays
                         o["gains"])
 
 
-def _fit_device(b: "ForestBuilder", y32, rw, row_offset: int, N: int, F: int, m: int, maxn: int) -> ForestArrays:
+def _fit_device(b: "ForestBuilder", y32, rw, row_offset: int, N: int, F: int, m: int, maxn: int,
+                n_all: Optional[int] = None) -> ForestArrays:
     dev = y32.device
+    n_all = N if n_all is None else n_all
     key = None
-    if FIT_GRAPHS and levels_all_async(b, N, F, m):
+    if FIT_GRAPHS and not (b.allreduce or b.owner) and levels_all_async(b, N, F, m, n_all):
         key = (dev.index, b.T, b.K, b.D, N, F, m, maxn, b.max_bins, b.impurity, b.min_inst, b.min_gain, b.seed,
                b.tree_offset, None if b.cdf is None else tuple(int(v) for v in b.cdf), rw is not None, row_offset,
                SIBLING_SUBTRACTION, SUBTRACT_MIN_PAIRS, SUBTRACT_MAX_BYTES, ASYNC_MAX_NODES, ASYNC_MAX_COUNT_WS,
@@ -544,7 +569,7 @@ def _fit_device(b: "ForestBuilder", y32, rw, row_offset: int, N: int, F: int, m:
             torch.cuda.synchronize(dev)
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
-                ent.nn = _enqueue_fit(b, ent.bufs, ent.y32, ent.rw, row_offset, N, F, m, maxn)
+                ent.nn = _enqueue_fit(b, ent.bufs, ent.y32, ent.rw, row_offset, N, F, m, maxn, n_all)
             ent.graph = g
         finally:
             b.bins, b.nbins, b.thr_mat = own
@@ -556,7 +581,7 @@ def _fit_device(b: "ForestBuilder", y32, rw, row_offset: int, N: int, F: int, m:
     if key is not None:
         _fit_graph_seen[key] = _fit_graph_seen.get(key, 0) + 1
     bufs = _alloc_fit_buffers(b.T, N, b.K, maxn, dev)
-    nn = _enqueue_fit(b, bufs, y32, rw, row_offset, N, F, m, maxn)
+    nn = _enqueue_fit(b, bufs, y32, rw, row_offset, N, F, m, maxn, n_all)
     return _finish_fit(b, bufs, nn, clone=False)
 
 

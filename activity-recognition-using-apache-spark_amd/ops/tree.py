@@ -423,6 +423,68 @@ def hist_split_planned(bins, nbins_feat, label, rows, row_w, node_start, node_co
     return _best_chunk(gain, feat, bin_, left, total, A, chunks, K)
 
 
+def hist_split_planned_dp(bins, nbins_feat, label, rows, row_w, node_start, node_count, feats, K, max_bins,
+                          min_instances, min_info_gain, impurity, rows_bound: int, a_dev: int, allreduce=None,
+                          owner=None, bins_rm=None, prows: int = PLAN_ROWS) -> LevelResult:
+    """The data-parallel level on the planned path, with no host read: ``feats.shape[0]`` = A is the
+    host-known node BOUND of the level (identical on every rank), ``a_dev`` the device count.
+
+    1. the row-balanced work items of ``hist_split_planned`` add this rank's histograms into a
+       zeroed per-node store [A, m, bins, K] (kernel mode 6: histogram only);
+    2. the store is summed across ranks — ``allreduce`` (every rank then searches every node) or
+       ``owner.reduce_scatter`` (rank r receives the summed slice of nodes [a0, a1));
+    3. split search from the (slice of the) reduced store (mode 7; nodes >= the device count exit);
+    4. owner: the slice's winners, packed [n, 3 + 2K] (``pack_level``), travel in ONE all-gather.
+    Every collective is sized by the bound A, so the loop never needs the real count on the host;
+    winners of the bound's surplus rows are never read (the decide / frontier kernels stop at the
+    device count)."""
+    A, m = feats.shape
+    F, N = bins.shape
+    fc = max(1, min(m, LDS_BUDGET // (max_bins * K * 4)))
+    chunks = (m + fc - 1) // fc
+    dev = bins.device
+    items_ub = A + rows_bound // prows
+    plan = torch.empty(4 + (A + 1) + 3 * A + items_ub, dtype=torch.int32, device=dev)
+    slot = m * max_bins * K
+    store = torch.zeros(A * slot, dtype=torch.float32, device=dev)
+    mod, st = _native.kernels(), _native.stream_ptr()
+    mod.tree_plan(node_count.data_ptr(), A, prows, plan.data_ptr(), slot, store.data_ptr(), max(1, A), 1, a_dev, st)
+    bptr, row_major = (bins_rm.data_ptr(), 1) if bins_rm is not None else (bins.data_ptr(), 0)
+
+    def launch(mode, n, a0, hist_ptr, fptr, outs, bound):
+        g, f, b, lf, tot = outs
+        mod.tree_hist_split_planned(bptr, N, F, row_major, nbins_feat.data_ptr(), rows.data_ptr(), row_w.data_ptr(),
+                                    node_start.data_ptr(), node_count.data_ptr(), n, fptr, m, fc, label.data_ptr(),
+                                    K, max_bins, float(min_instances), float(min_info_gain), impurity, g.data_ptr(),
+                                    f.data_ptr(), b.data_ptr(), lf.data_ptr(), tot.data_ptr(), mode, hist_ptr,
+                                    1, plan.data_ptr(), a0 if mode == 7 else prows, bound, 1, 0, 0, 0, st)
+
+    def outs(n):
+        return (torch.empty(n * chunks, dtype=torch.float32, device=dev),
+                torch.empty(n * chunks, dtype=torch.int32, device=dev),
+                torch.empty(n * chunks, dtype=torch.int32, device=dev),
+                torch.empty(n * chunks, K, dtype=torch.float32, device=dev),
+                torch.empty(n, K, dtype=torch.float32, device=dev))
+
+    full = outs(A)
+    launch(6, A, 0, store.data_ptr(), feats.data_ptr(), full, items_ub)
+    if owner is None:
+        if allreduce is not None:
+            allreduce(store)
+        launch(7, A, 0, store.data_ptr(), feats.data_ptr(), full, A)
+        return _best_chunk(*full, A, chunks, K)
+    local, a0, a1 = owner.reduce_scatter(store.view(A, slot))
+    n = a1 - a0
+    if n > 0:
+        loc = local[:n].contiguous()
+        part = outs(n)
+        launch(7, n, a0, loc.data_ptr(), feats.data_ptr() + 4 * a0 * m, part, n)
+        packed = pack_level(_best_chunk(*part, n, chunks, K))
+    else:
+        packed = torch.zeros(0, 3 + 2 * K, dtype=torch.float32, device=dev)
+    return unpack_level(owner.all_gather(packed, A), K)
+
+
 def _best_chunk(gain, feat, bin_, left, total, A, chunks, K) -> LevelResult:
     if chunks == 1:  # every sampled feature in one workgroup: the kernel's winner is the node's
         return LevelResult(gain=gain, feat=feat, bin=bin_, left=left.view(A, K), total=total)

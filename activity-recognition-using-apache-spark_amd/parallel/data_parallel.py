@@ -41,12 +41,12 @@ def allreduce_sum(ctx: Optional[DistContext]):
         return None
 
     def _ar(t: torch.Tensor):
-        if t.is_cuda or ctx.backend != "nccl":
+        if t.is_cuda == (ctx.backend == "nccl"):
             dist.all_reduce(t, group=ctx.group)
-        else:  # host tensor under RCCL: stage through the device
-            d = t.to(ctx.device)
+        else:  # host tensor under RCCL, or a device tensor under gloo (GPU tests): stage it
+            d = t.to(ctx.device if ctx.backend == "nccl" else "cpu")
             dist.all_reduce(d, group=ctx.group)
-            t.copy_(d.cpu())
+            t.copy_(d)
     return _ar
 
 
@@ -119,8 +119,8 @@ class NodeOwner:
         return t[:numel]
 
     def _dev(self):
-        # RCCL needs device tensors; host tensors are staged through HBM
-        return self.ctx.device if self.ctx.backend == "nccl" else None
+        # RCCL needs device tensors (host tensors are staged through HBM), gloo host tensors
+        return self.ctx.device if self.ctx.backend == "nccl" else torch.device("cpu")
 
     def reduce_scatter(self, hist: torch.Tensor):
         P, r = self.ctx.world_size, self.ctx.rank

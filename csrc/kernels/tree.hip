@@ -125,6 +125,9 @@ __global__ __launch_bounds__(256) void tree_hist_split_kernel(
   //   fused node's LDS histogram to its store slot, and merges big-node chunks into slot a;
   //   mode 5: blockIdx.y = node a with derive_from[a] = sibling s: hist = hprev[parent_of[a]] -
   //   store[s] (integer-valued weights: exact), kept in store[a], then the split search (mode 2).
+  // Data parallel (by_node = 1, the store zeroed): mode 6 = the work items of mode 3, histogram only
+  // (every item adds into its node's slot); the store is then summed across ranks (all-reduce, or
+  // reduce-scatter by node owner); mode 7 = split search from the rank's slice of it.
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int c = blockIdx.x, chunks = gridDim.x;
   int a = blockIdx.y, gslot = blockIdx.y;
@@ -136,13 +139,20 @@ __global__ __launch_bounds__(256) void tree_hist_split_kernel(
   __shared__ int red_idx[4];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   int start, cnt;
-  if (mode == 3 || mode == 4) {
+  if (mode == 7) {
+    // data parallel: split search from the rank's slice of the reduced store (ghist, feats, outputs
+    // all start at global node prows = a0); nodes at or past the level's device count exit
+    if (prows + (int)blockIdx.y >= plan[2]) return;
+    mode = 2;
+    start = 0;
+    cnt = 0;
+  } else if (mode == 3 || mode == 4 || mode == 6) {
     const int A = plan[2];
     const int32_t* item_start = plan + 4;            // [A + 1]
     const int32_t* big_rank = item_start + A + 1;    // [A]  (-1: not big)
     const int32_t* big_list = big_rank + A;          // [A]
     const int32_t* item_node = big_list + A;         // [items]
-    if (mode == 3) {
+    if (mode != 4) {
       if ((int)blockIdx.y >= plan[0]) return;        // beyond this level's work items
       a = item_node[blockIdx.y];
       if (derive_from && derive_from[a] >= 0) return;  // histogram = parent - sibling (mode 5)
@@ -151,7 +161,9 @@ __global__ __launch_bounds__(256) void tree_hist_split_kernel(
       const int cnt_all = node_count[a];
       start = node_start[a] + z * prows;
       cnt = gslot < 0 ? cnt_all : min(prows, cnt_all - z * prows);
-      if (gslot >= 0) mode = 1;                      // a chunk of a big node: histogram only
+      // mode 6 (data parallel): every item only adds its histogram into the node's zeroed store
+      // slot; the split search follows the cross-rank reduction (mode 7)
+      if (gslot >= 0 || mode == 6) mode = 1;         // a chunk of a big node: histogram only
       else mode = 0;
       if (by_node) gslot = a;
     } else {
@@ -706,7 +718,8 @@ extern "C" int har_tree_hist_split(const uint8_t* bins, int64_t N, int F, int ro
                                      nullptr, nullptr, nullptr, s);
 }
 
-// mode 3 / 4 (plan != nullptr): grid.y = `bound` (items for mode 3, big-node slots for mode 4)
+// planned modes (plan != nullptr): grid.y = `bound` (work items for modes 3 / 6, big-node slots for
+// mode 4, nodes for mode 5, the rank's node slice for mode 7, whose first global node is `prows`)
 extern "C" int har_tree_hist_split_planned(const uint8_t* bins, int64_t N, int F, int row_major,
                                            const int32_t* nbins_feat, const int32_t* rows, const float* row_w,
                                            const int32_t* node_start, const int32_t* node_count, int A,
@@ -719,9 +732,10 @@ extern "C" int har_tree_hist_split_planned(const uint8_t* bins, int64_t N, int F
                                            const int32_t* parent_of, hipStream_t s) {
   if (K > KMAX || maxbins > 64 || fc <= 0 || m <= 0) return -2;
   if (mode != 0 && !ghist) return -4;
-  const bool planned = mode == 3 || mode == 4 || mode == 5;
-  if (planned && (!plan || prows <= 0)) return -6;
+  const bool planned = mode >= 3 && mode <= 7;
+  if (planned && (!plan || (mode != 7 && prows <= 0) || prows < 0)) return -6;
   if (mode == 5 && (!by_node || !hprev || !derive_from || !parent_of)) return -7;
+  if ((mode == 6 || mode == 7) && (!by_node || derive_from)) return -7;
   if (by_node && !planned) return -7;
   if (A == 0) return 0;
   const int chunks = (m + fc - 1) / fc;
