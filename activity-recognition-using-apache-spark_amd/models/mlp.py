@@ -455,6 +455,8 @@ class MLPEngine:
 
     def grad_phase(self, Xb: torch.Tensor, yb: torch.Tensor, global_batch: int):
         """DP step, part 1 (graph-capturable): fwd + bwd + deterministic slab reduction into G."""
+        if not self.native:
+            return self._grad_torch(Xb, yb, global_batch)
         if self._plan_ok(Xb, yb):
             B = Xb.shape[0]
             plan, self.step_nwg, self.step_S = self._plan(B)
@@ -467,6 +469,8 @@ class MLPEngine:
     def apply_phase(self):
         """DP step, part 3 (graph-capturable): Adam from the all-reduced G (part 2 is the RCCL
         all-reduce, issued eagerly between the two graph replays)."""
+        if not self.native:
+            return self._adam_torch()
         self.optimizer_step_native()
 
     def _plan(self, B: int):
@@ -564,12 +568,19 @@ class MLPEngine:
 
     def train_step_torch(self, X: torch.Tensor, y: torch.Tensor, global_batch: int):
         """fp32 reference step (CPU path / oracle); same Adam math as the kernel."""
+        self._grad_torch(X, y, global_batch)
+        self.allreduce_grads()
+        self._adam_torch()
+
+    def _grad_torch(self, X: torch.Tensor, y: torch.Tensor, global_batch: int):
         P = self.P.detach().requires_grad_(True)
         z = self.torch_forward(P, X.float())
         loss = torch.nn.functional.cross_entropy(z, y.long(), reduction="sum") / global_batch
         (g,) = torch.autograd.grad(loss, P)
         self.G.copy_(g)
-        self.allreduce_grads()
+        self.last_loss = float(loss.detach()) * global_batch / X.shape[0]
+
+    def _adam_torch(self):
         self.t_step += 1
         b1, b2 = self.betas
         with torch.no_grad():
@@ -577,7 +588,6 @@ class MLPEngine:
             self.v.mul_(b2).add_((1 - b2) * self.G * self.G)
             upd = (self.m / (1 - b1 ** self.t_step)) / ((self.v / (1 - b2 ** self.t_step)).sqrt() + self.eps)
             self.P.sub_(self.lr * (upd + self.wd * self.P))
-        self.last_loss = float(loss.detach()) * global_batch / X.shape[0]
 
     # ---------------------------------------------------------------- inference
     def infer_fused(self, Xb: torch.Tensor):

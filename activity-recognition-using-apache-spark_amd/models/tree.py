@@ -479,6 +479,9 @@ def levels_all_async(b: "ForestBuilder", N: int, F: int, m: int, n_all: Optional
 # copied into the graph's static buffers.  HAR_TREE_GRAPH=0 disables it.
 FIT_GRAPHS = os.environ.get("HAR_TREE_GRAPH", "1") != "0"
 FIT_GRAPH_MAX = 8
+# how the last device fit ran: "eager" (launched from Python), "capture" (launched while recorded
+# into a HIP graph) or "replay" (the graph of an earlier fit of the same signature)
+LAST_FIT_KIND = "eager"
 _fit_graph_seen: dict = {}
 _fit_graphs: dict = {}
 
@@ -550,6 +553,7 @@ def _finish_fit(b: "ForestBuilder", bufs: dict, nn, clone: bool) -> ForestArrays
 
 def _fit_device(b: "ForestBuilder", y32, rw, row_offset: int, N: int, F: int, m: int, maxn: int,
                 n_all: Optional[int] = None) -> ForestArrays:
+    global LAST_FIT_KIND
     dev = y32.device
     n_all = N if n_all is None else n_all
     key = None
@@ -574,6 +578,11 @@ def _fit_device(b: "ForestBuilder", y32, rw, row_offset: int, N: int, F: int, m:
         finally:
             b.bins, b.nbins, b.thr_mat = own
         _fit_graphs[key] = ent
+        LAST_FIT_KIND = "capture"
+    elif ent is not None:
+        LAST_FIT_KIND = "replay"
+    else:
+        LAST_FIT_KIND = "eager"
     if ent is not None:
         ent.load(b, y32, rw)
         ent.graph.replay()

@@ -153,6 +153,7 @@ def bench_mlp(args, ctx):
     else:
         run = step
     elapsed = timed(ctx, run, args.steps, args.warmup, dev)
+    phases = mlp_phase_times(ctx, eng, Xin, y32, B, nb, global_batch, n=max(10, min(50, args.steps)))
     Xt, yt = synthetic_windows(65536, seed=999, device=dev)
     acc = float((torch.argmax(eng.logits(Xt), dim=1) == yt).float().mean())
     rec = {"value": global_batch * args.steps / elapsed, "ms_per_step": elapsed * 1e3 / args.steps,
@@ -164,9 +165,55 @@ def bench_mlp(args, ctx):
                       "parallelism": f"dp{world}"},
            "synthetic_test_accuracy": hdist.mean_over_ranks(ctx, acc),
            "hip_graph": {0: "off", 1: "whole-step", 2: "segmented"}[mode if graphs else 0],
-           "collectives_per_step": eng.collective_stats() if hasattr(eng, "collective_stats") else None}
+           "collectives_per_step": eng.collective_stats() if hasattr(eng, "collective_stats") else None,
+           "phase_ms": phases}
     rec.update(wisdm_accuracy_fields(args, ctx, hidden=(args.hidden, args.hidden)))
     return rec
+
+
+def mlp_phase_times(ctx, eng, Xin, y32, B, nb, global_batch, n=50):
+    """Per-phase time of the DP step, measured AFTER the timed loop on n extra (untimed) steps run
+    as the three phases of the N > 1 step: compute (forward + backward + slab reduction into the
+    flat fp32 gradient G), the RCCL all-reduce of G, Adam.  Device time from HIP events around each
+    phase on the compute stream (host clock on the CPU path); mean per step, max over ranks.  At
+    N = 1 the all-reduce is absent and the N = 1 step fuses Adam into the reduction kernel, so
+    compute + adam there is the split form of the timed step (one extra launch)."""
+    from har.parallel import dist as hdist
+
+    cuda = Xin.is_cuda
+    tot = {"compute": 0.0, "allreduce": 0.0, "adam": 0.0}
+    if cuda:
+        ev = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(n)]
+    for i in range(n):
+        j = i % nb
+        xb, yb = Xin[j * B:(j + 1) * B], y32[j * B:(j + 1) * B]
+        if cuda:
+            e = ev[i]
+            e[0].record()
+            eng.grad_phase(xb, yb, global_batch)
+            e[1].record()
+            eng.allreduce_grads()
+            e[2].record()
+            eng.apply_phase()
+            e[3].record()
+        else:
+            t0 = time.perf_counter()
+            eng.grad_phase(xb, yb, global_batch)
+            t1 = time.perf_counter()
+            eng.allreduce_grads()
+            t2 = time.perf_counter()
+            eng.apply_phase()
+            t3 = time.perf_counter()
+            for k, dt in zip(tot, (t1 - t0, t2 - t1, t3 - t2)):
+                tot[k] += dt * 1e3
+    if cuda:
+        torch.cuda.synchronize()
+        for e in ev:
+            for k, (a, b) in zip(tot, ((0, 1), (1, 2), (2, 3))):
+                tot[k] += e[a].elapsed_time(e[b])
+    out = {k: hdist.max_over_ranks(ctx, v / n) for k, v in tot.items()}
+    out.update(steps=n, clock="HIP events" if cuda else "host", world=ctx.world_size)
+    return out
 
 
 def wisdm_accuracy_fields(args, ctx, hidden):
@@ -325,7 +372,9 @@ def bench_stream(args, ctx):
     spec = StreamSpec(seed=2018)
     W = spec.window
     B = args.batch
-    samples_local = args.samples // 8  # 1B samples per 8-GPU node: 125M per GPU (weak scaling)
+    # 1B samples per 8-GPU node: 125M per GPU (weak scaling); --samples-per-gpu N holds N on every GPU
+    # (1e9: config 4's whole 1B-sample stream, 12 GB of fp32 x/y/z, resident on ONE MI355X)
+    samples_local = args.samples_per_gpu or args.samples // 8
     nw_local = samples_local // W
     stream = torch.empty(nw_local * W, 3, device=dev)
     labels = torch.empty(nw_local, dtype=torch.long, device=dev)
@@ -371,12 +420,18 @@ def bench_stream(args, ctx):
             feat.copy_(featurize(s))
             eng.train_step(pad_input_bf16(feat, eng.layout.in_pad), y32[j * B:(j + 1) * B], global_batch)
 
+    def held_out_accuracy():
+        # 8192 windows of the stream beyond every rank's shard, featurized the same way
+        st_, yt = generate_stream(8192, spec, dev, first_window=10 ** 9)
+        return hdist.mean_over_ranks(ctx, float((torch.argmax(eng.logits(featurize(st_)), 1) == yt).float().mean()))
+
     if args.stream_pass:
-        return _stream_full_pass(args, ctx, spec, stream, labels, eng, mean, inv_std, samples_local)
+        rec = _stream_full_pass(args, ctx, spec, stream, labels, eng, mean, inv_std, samples_local)
+        rec.update(test_accuracy=held_out_accuracy(),
+                   test_accuracy_data="held-out synthetic stream (8192 windows past every shard), after the timed passes")
+        return rec
     elapsed = timed(ctx, step, args.steps, args.warmup, dev)
-    st_, yt = generate_stream(8192, spec, dev, first_window=10 ** 9)
-    Xt = featurize(st_)
-    acc = float((torch.argmax(eng.logits(Xt), 1) == yt).float().mean())
+    acc = held_out_accuracy()
     return {"value": global_batch * args.steps / elapsed, "ms_per_step": elapsed * 1e3 / args.steps,
             "vs_baseline": None, "vs_baseline_note": BASELINE_NOTE,
             "samples_per_s": global_batch * W * args.steps / elapsed,
@@ -385,7 +440,7 @@ def bench_stream(args, ctx):
             "config": {"model": f"raw stream -> window features ({F}) -> MLP bf16 "
                                 f"({F}-{args.hidden}-{args.hidden}-{N_CLASSES})",
                        "global_batch": global_batch, "seq_len": W, "parallelism": f"dp{world}"},
-            "test_accuracy": hdist.mean_over_ranks(ctx, acc), "test_accuracy_data": "held-out synthetic stream"}
+            "test_accuracy": acc, "test_accuracy_data": "held-out synthetic stream"}
 
 
 def _stream_full_pass(args, ctx, spec, stream, labels, eng, mean, inv_std, samples_local):
@@ -440,7 +495,7 @@ def _stream_full_pass(args, ctx, spec, stream, labels, eng, mean, inv_std, sampl
             "config": {"model": f"raw stream full pass -> window features -> MLP bf16 "
                                 f"({n_features(3)}-{args.hidden}-{args.hidden}-{N_CLASSES})",
                        "global_batch": gb, "seq_len": fz.window, "parallelism": f"dp{world}"},
-            "test_accuracy": None, "test_accuracy_data": "not measured in --stream-pass mode"}
+            "samples_per_gpu": samples_local}
 
 
 def main():
@@ -465,6 +520,8 @@ def main():
     ap.add_argument("--rf-reduce", default="owner", choices=["owner", "allreduce"],
                     help="DP forest histograms: reduce-scatter by node owner + all-gather of splits, or all-reduce")
     ap.add_argument("--samples", type=int, default=1_000_000_000, help="stream samples per 8 GPUs")
+    ap.add_argument("--samples-per-gpu", type=int, default=0,
+                    help="--config stream: samples resident on EVERY GPU (overrides --samples / 8)")
     ap.add_argument("--stream-pass", action="store_true",
                     help="--config stream: time full passes over every resident sample (halo-sharded featurization "
                          "+ one MLP epoch) instead of per-batch steps")

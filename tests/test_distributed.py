@@ -254,3 +254,5 @@ def test_bench_contract_torchrun(config, extra):
         assert rec["windows_featurized_per_pass"] >= 9990 and rec["mlp_steps_per_pass"] >= 9
     if config == "mlp":  # value = whole-job windows per second = global batch / step time
         assert abs(rec["value"] - rec["config"]["global_batch"] / (rec["ms_per_step"] * 1e-3)) <= 1e-6 * rec["value"]
+        ph = rec["phase_ms"]  # the DP step's split: compute, the all-reduce of G, Adam
+        assert ph["world"] == 2 and all(ph[k] >= 0 for k in ("compute", "allreduce", "adam")) and ph["allreduce"] > 0
