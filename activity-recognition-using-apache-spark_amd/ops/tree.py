@@ -457,7 +457,7 @@ def hist_split_planned_dp(bins, nbins_feat, label, rows, row_w, node_start, node
                                     node_start.data_ptr(), node_count.data_ptr(), n, fptr, m, fc, label.data_ptr(),
                                     K, max_bins, float(min_instances), float(min_info_gain), impurity, g.data_ptr(),
                                     f.data_ptr(), b.data_ptr(), lf.data_ptr(), tot.data_ptr(), mode, hist_ptr,
-                                    1, plan.data_ptr(), a0 if mode == 7 else prows, bound, 1, 0, 0, 0, st)
+                                    plan.data_ptr(), a0 if mode == 7 else prows, bound, 1, 0, 0, 0, st)
 
     def outs(n):
         return (torch.empty(n * chunks, dtype=torch.float32, device=dev),
