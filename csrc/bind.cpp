@@ -451,6 +451,7 @@ PYBIND11_MODULE(_har_native, m) {
                                   S(stream_)),
           "window_features_mlp");
   });
+  m.def("window_set_legacy", [](int on) { har_window_set_legacy(on); });
   m.def("window_features", [](u stream, int64_t n_samples, int axes, int window, int stride, int64_t n_windows,
                               float hz, int nbins, u out, int ld_out, u st) {
     check(har_window_features(P<const float>(stream), n_samples, axes, window, stride, n_windows, hz, nbins,
@@ -489,6 +490,7 @@ PYBIND11_MODULE(_har_native, m) {
   m.def("head_fused_blocks", &har_head_fused_blocks);
   m.def("mlp_fwd_head_grid", &har_mlp_fwd_head_grid);
   m.def("mlp_set_stamps", [](u p) { har_mlp_set_stamps(P<uint64_t>(p)); });
+  m.def("mlp_set_bwd_variant", [](int v) { har_mlp_set_bwd_variant(v); });
   py::class_<MlpStepPlan>(m, "MlpStepPlan")
       .def(py::init([](py::dict d) {
         MlpStepPlan p;

@@ -38,6 +38,9 @@ using namespace mlpf;
 // (shader clock) at fixed points into its own 40-slot row of that buffer (slots 38 / 39:
 // s_memrealtime at entry / exit, 100 MHz, one clock for the whole chip).  Nothing else reads them.
 uint64_t* g_har_mlp_stamps = nullptr;
+// Backward scheduling variant (probe A/B): 1 = no scheduling barrier between the refills + dact2
+// build and the tile's MFMA phases
+int g_har_mlp_bwd_ilv = 0;
 
 namespace {
 
@@ -97,36 +100,10 @@ __global__ __launch_bounds__(512) void mlp_fwd3_kernel(
   HAR_STAMP_REAL(FW, 38)
   HAR_STAMP(FW, 0)
 
-  // ---- this wave's weight slices, in registers for the whole kernel ----
-  bf16x8_t w0f[2][K0C], w1f[2][KC];
-#pragma unroll
-  for (int t = 0; t < 2; ++t) {
-#pragma unroll
-    for (int kc = 0; kc < K0C; ++kc)
-      w0f[t][kc] = *reinterpret_cast<const bf16x8_t*>(W0 + (size_t)(u0 + 16 * t + c16) * K0 + kc * 32 + g * 8);
-#pragma unroll
-    for (int kc = 0; kc < KC; ++kc)
-      w1f[t][kc] = *reinterpret_cast<const bf16x8_t*>(W1 + (size_t)(u0 + 16 * t + c16) * HH + kc * 32 + g * 8);
-  }
-  // stage-3 A fragment: Wout[class c16][u0 + 4g + j] (j < 4), [u0 + 16 + 4g + j - 4] (j >= 4): the k
-  // order of the h2 register pairs (C layout: unit 4g + r of a 16-unit tile in register r)
-  const uint2 wlo = *reinterpret_cast<const uint2*>(Wo + (size_t)c16 * HH + u0 + 4 * g);
-  const uint2 whi = *reinterpret_cast<const uint2*>(Wo + (size_t)c16 * HH + u0 + 16 + 4 * g);
-  const bf16x8_t wo3 = cat8(wlo.x, wlo.y, whi.x, whi.y);
-  float4 b0r[2], b1r[2];
-#pragma unroll
-  for (int t = 0; t < 2; ++t) {
-    b0r[t] = *reinterpret_cast<const float4*>(b0 + u0 + 16 * t + 4 * g);
-    b1r[t] = *reinterpret_cast<const float4*>(b1 + u0 + 16 * t + 4 * g);
-  }
   // softmax lane: tile row sr = 4 wave + g (half sh, row srr of it), class c16
   const int sr = 4 * wave + g, sh = sr >> 4, srr = sr & 15;
   const int hsw = 8 * ((c16 >> 2) & 1);  // h1 tile chunk swap of this lane's rows (16h + c16)
   const LaneSwap swp(lane);
-  const float bo_s = c16 < C ? bo[c16] : 0.f;
-  if constexpr (STAMP) __builtin_amdgcn_s_waitcnt(0x0f70);
-  HAR_STAMP(FW, 1)
-
   f32x4_t acc5[2] = {f32x4_t{0.f, 0.f, 0.f, 0.f}, f32x4_t{0.f, 0.f, 0.f, 0.f}};
   float dbo = 0.f, lsum = 0.f, ncorr = 0.f;
   const int ntiles = B / FRT;
@@ -142,6 +119,41 @@ __global__ __launch_bounds__(512) void mlp_fwd3_kernel(
 #pragma unroll
       for (int kc = 0; kc < K0C; ++kc) xb[h][kc] = ldx<K0>(X, r + 16 * h + c16, kc, g);
   };
+
+  // ---- this wave's weight slices, in registers for the whole kernel.  Issue order: W0, b0, the
+  // first X tile and its labels, THEN W1 / Wout / b1 (the bulk: 16 KB per wave, L2-bandwidth-bound
+  // with every CU fetching it at once), so stage 1 of tile 0 waits only for what it reads ----
+  bf16x8_t w0f[2][K0C], w1f[2][KC];
+  float4 b0r[2], b1r[2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+#pragma unroll
+    for (int kc = 0; kc < K0C; ++kc)
+      w0f[t][kc] = *reinterpret_cast<const bf16x8_t*>(W0 + (size_t)(u0 + 16 * t + c16) * K0 + kc * 32 + g * 8);
+    b0r[t] = *reinterpret_cast<const float4*>(b0 + u0 + 16 * t + 4 * g);
+  }
+  int ynext = 0;
+  if (nt > 0) {
+    load_x(0);
+    ynext = labels[tile_of(0) * FRT + sr];
+  }
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+#pragma unroll
+    for (int kc = 0; kc < KC; ++kc)
+      w1f[t][kc] = *reinterpret_cast<const bf16x8_t*>(W1 + (size_t)(u0 + 16 * t + c16) * HH + kc * 32 + g * 8);
+    b1r[t] = *reinterpret_cast<const float4*>(b1 + u0 + 16 * t + 4 * g);
+  }
+  // stage-3 A fragment: Wout[class c16][u0 + 4g + j] (j < 4), [u0 + 16 + 4g + j - 4] (j >= 4): the k
+  // order of the h2 register pairs (C layout: unit 4g + r of a 16-unit tile in register r)
+  const uint2 wlo = *reinterpret_cast<const uint2*>(Wo + (size_t)c16 * HH + u0 + 4 * g);
+  const uint2 whi = *reinterpret_cast<const uint2*>(Wo + (size_t)c16 * HH + u0 + 16 + 4 * g);
+  const bf16x8_t wo3 = cat8(wlo.x, wlo.y, whi.x, whi.y);
+  const float bo_s = c16 < C ? bo[c16] : 0.f;
+  __builtin_amdgcn_sched_barrier(0);
+  if constexpr (STAMP) __builtin_amdgcn_s_waitcnt(0x0f70);
+  HAR_STAMP(FW, 1)
   // ---- stage 1: h1^T = W0 . X^T for this wave's units -> h1 buffer `buf` ----
   auto stage1 = [&](int buf) __attribute__((always_inline)) {
     bf16_t* hb = h1s + buf * FRT * FHP;
@@ -223,13 +235,17 @@ __global__ __launch_bounds__(512) void mlp_fwd3_kernel(
     float z = 0.f;
 #pragma unroll
     for (int w = 0; w < FW; ++w) z += zb[(w * 2 + sh) * ZREG + 72 * (c16 >> 2) + 4 * srr + (c16 & 3)];
+    asm volatile("" : "+v"(z));  // computed by every lane: no exec-masked branch splits the loop body
     const float zz = c16 < C ? z + bo_s : -INFINITY;
     // the 16 class lanes of a row are one DPP row: max, argmax (smallest class at the max), sum
     const float mx = row16_max(zz);
     const int amx = row16_min(zz == mx && c16 < C ? c16 : (1 << 30));
     const float e = c16 < C ? __expf(zz - mx) : 0.f;
     const float se = row16_sum(e);
-    const float dl = c16 < C ? (e * (1.f / se) - (c16 == yc ? 1.f : 0.f)) * scale : 0.f;
+    // v_rcp_f32 (1 ulp) rather than the IEEE division sequence, which hipcc sinks into an
+    // exec-masked branch; dz is rounded to bf16 right after
+    const float dl0 = (e * __builtin_amdgcn_rcpf(se) - (c16 == yc ? 1.f : 0.f)) * scale;
+    const float dl = c16 < C ? dl0 : 0.f;
     const bf16_t db = f2bf(dl);
     lsum += c16 == yc ? (mx + __logf(se)) - zz : 0.f;
     ncorr += (c16 == 0 && amx == yc) ? 1.f : 0.f;
@@ -251,10 +267,7 @@ __global__ __launch_bounds__(512) void mlp_fwd3_kernel(
   // stages 2 + 3 of tile k+1 | stage 1 of tile k+2 | barrier.  The softmax's dependent chain (LDS
   // reads, cross-lane max / sum, exp / log) and the next tile's MFMAs share one barrier interval, so
   // the scheduler interleaves them; h1, the partial logits, dz and the h2 images are double-buffered.
-  int ynext = 0;
   if (nt > 0) {
-    load_x(0);
-    ynext = labels[tile_of(0) * FRT + sr];
     stage1(0);
     load_x(1);
     __syncthreads();  // h1 of tile 0
@@ -263,15 +276,19 @@ __global__ __launch_bounds__(512) void mlp_fwd3_kernel(
     load_x(2);
     __syncthreads();  // partial logits of tile 0, h1 of tile 1
   }
-  for (int k = 0; k < nt; ++k) {
+  // iteration k: softmax(k) | stage5(k-1) | stages 2+3 (k+1) | stage1 (k+2).  The first and the last
+  // iterations are peeled so the steady-state body is ONE basic block (no k > 0 / k + 1 < nt
+  // branches): the scheduler can then interleave the softmax's VALU / DPP chain with the stage-2
+  // MFMAs instead of running them back to back.
+  auto iter = [&](int k, bool first, bool last) __attribute__((always_inline)) {
     if (k < 32) HAR_STAMP(FW, 2 + k)
     const int yc = ynext;
     ynext = labels[tile_of(k + 1) * FRT + sr];
     softmax(k, k & 1, yc);
     if (k == 4) HAR_STAMP(FW, 10)
-    if (k > 0) stage5((k - 1) & 1);
+    if (!first) stage5((k - 1) & 1);
     if (k == 4) HAR_STAMP(FW, 11)
-    if (k + 1 < nt) {  // workgroup-uniform
+    if (!last) {
       stage23(k + 1, (k + 1) & 1);
       if (k == 4) HAR_STAMP(FW, 12)
       stage1(k & 1);   // tile k+2 (clamped) into the buffer tile k left
@@ -279,7 +296,10 @@ __global__ __launch_bounds__(512) void mlp_fwd3_kernel(
       if (k == 4) HAR_STAMP(FW, 13)
     }
     __syncthreads();
-  }
+  };
+  if (nt > 0) iter(0, true, nt == 1);
+  for (int k = 1; k < nt - 1; ++k) iter(k, false, false);
+  if (nt > 1) iter(nt - 1, false, true);
   HAR_STAMP(FW, 34)
   if (nt > 0) stage5((nt - 1) & 1);
   // ---- this workgroup's slab: dWout rows 0..15 x this wave's units, dbout; loss, #correct ----
@@ -337,7 +357,7 @@ template <int K0> struct Bwd3Lds {
   static_assert((size_t)HH * WQP + NCLS * HH <= (size_t)2 * DSM, "prologue images fit the dact2 buffers");
 };
 
-template <int K0, bool STAMP>
+template <int K0, bool STAMP, bool ILV>
 __global__ __launch_bounds__(512) void mlp_bwd3_kernel(
     const uint32_t* __restrict__ dz, const uint32_t* __restrict__ mask, const bf16_t* __restrict__ X,
     const bf16_t* __restrict__ W1, const bf16_t* __restrict__ W0, const float* __restrict__ b0,
@@ -529,12 +549,12 @@ __global__ __launch_bounds__(512) void mlp_bwd3_kernel(
         acc1[j][1] = mma32(hb1, da, acc1[j][1]);
       }
     }
-    if (wave < 4) {  // db1 = sum over the rows of dact2 (row 0 of ones . dact2): quadrant q, wave w < 4
-                     // own the 16 j of block 4q + w, so every workgroup does the same work
+    // db1 = sum over the rows of dact2 (row 0 of ones . dact2): j block 4q + (w & 3), so every
+    // workgroup does the same work; waves 4..7 repeat waves 0..3's (never stored) instead of
+    // branching, which keeps the tile body one basic block
 #pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
-        accb[0] = mma32(ones, frag_rows_sw(dsm + 32 * ks * BDP, BDP, 16 * (4 * q + wave), lane), accb[0]);
-    }
+    for (int ks = 0; ks < 2; ++ks)
+      accb[0] = mma32(ones, frag_rows_sw(dsm + 32 * ks * BDP, BDP, 16 * (4 * q + (wave & 3)), lane), accb[0]);
   };
   // (c) of local tile i (its dact1 buffer i & 1, X buffer i % NXB)
   auto tile_c = [&](int i) __attribute__((always_inline)) {
@@ -576,18 +596,29 @@ __global__ __launch_bounds__(512) void mlp_bwd3_kernel(
   __syncthreads();  // dact2 tile 0, X tiles 0 and 1 are in LDS
   tile_h1(0);
   __syncthreads();  // h1 tile 0 complete
-  for (int i = 0; i < n; ++i) {
-    if (i < 32) HAR_STAMP(8, 2 + i)
+  // iteration 0 is peeled (no (c) yet) so the steady-state body after the refill point is one
+  // basic block the scheduler can interleave
+  auto iter = [&](int i, bool first) __attribute__((always_inline)) {
+    if (i < 24) HAR_STAMP(8, 2 + i)
     stage_dact2((i + 1) & 1);       // waits for the dz / mask loads issued one iteration ago
+    if (i == 4) HAR_STAMP(8, 26)
     HAR_B3_STAGE_X(i + 2)
     HAR_B3_LOAD_D(t0 + i + 2)
     HAR_B3_LOAD_X(t0 + i + 3)
-    __builtin_amdgcn_sched_barrier(0);  // the refills are issued before the compute
+    // the refills are issued before the compute; ILV lets the scheduler interleave the dact2
+    // build (VALU / LDS stores) with the MFMAs of h1 / (a) / (b) / (c) instead
+    if constexpr (!ILV) __builtin_amdgcn_sched_barrier(0);
+    if (i == 4) HAR_STAMP(8, 27)
     tile_h1(i + 1);                 // X tile i+1 has been in LDS since the last barrier
+    if (i == 4) HAR_STAMP(8, 28)
     tile_ab(i);
-    if (i > 0) tile_c(i - 1);       // wave-uniform
+    if (i == 4) HAR_STAMP(8, 29)
+    if (!first) tile_c(i - 1);
+    if (i == 4) HAR_STAMP(8, 30)
     __syncthreads();                // dact2 i+1 / X i+2 staged, h1 i+1 and dact1 i complete
-  }
+  };
+  if (n > 0) iter(0, true);
+  for (int i = 1; i < n; ++i) iter(i, false);
   HAR_STAMP(8, 34)
   if (n > 0) tile_c(n - 1);
 #undef HAR_B3_LOAD_D
@@ -638,7 +669,8 @@ void launch_bwd3(const uint32_t* dz, const uint32_t* mask, const bf16_t* X, cons
                  const float* b0, const bf16_t* Wo, int B, int S, float* gw1, float* gw0, float* gb0, float* gb1,
                  int64_t stride, int32_t* tick, const float* fslab, int fslab_w, int nfwd, float* gwo, float* gbo,
                  hipStream_t s) {
-  auto k = g_har_mlp_stamps ? mlp_bwd3_kernel<K0, true> : mlp_bwd3_kernel<K0, false>;
+  auto k = g_har_mlp_bwd_ilv ? (g_har_mlp_stamps ? mlp_bwd3_kernel<K0, true, true> : mlp_bwd3_kernel<K0, false, true>)
+                             : (g_har_mlp_stamps ? mlp_bwd3_kernel<K0, true, false> : mlp_bwd3_kernel<K0, false, false>);
   k<<<S * BQ, 512, Bwd3Lds<K0>::bytes, s>>>(dz, mask, X, W1, W0, b0, Wo, B, S, gw1, gw0, gb0, gb1, stride, tick,
                                            fslab, fslab_w, nfwd, gwo, gbo, g_har_mlp_stamps ? g_har_mlp_stamps + STAMP_BWD_OFF : nullptr);
 }
@@ -696,3 +728,4 @@ extern "C" int har_mlp_step_bwd(const uint32_t* dz, const uint32_t* mask, const 
 }
 
 extern "C" void har_mlp_set_stamps(uint64_t* p) { g_har_mlp_stamps = p; }
+extern "C" void har_mlp_set_bwd_variant(int v) { g_har_mlp_bwd_ilv = v; }

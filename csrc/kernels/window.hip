@@ -31,7 +31,11 @@
 #include <type_traits>
 
 #include "common.h"
+#include "mlp_frag.h"
 #include "../har_kernels.h"
+
+// A/B switch for probes: the pre-v3 kernels only (window_features_kernel / _persistent_kernel)
+bool g_window_legacy = false;
 
 namespace {
 
@@ -466,6 +470,248 @@ __global__ __launch_bounds__(256) void window_features_persistent_kernel(
   }
 }
 
+// ------------------------------------------------------------------------------------------------
+// Register-resident variant: a group of LPW = 16 / 32 / 64 lanes per (window, triad), lane `sub`
+// owning the CONTIGUOUS run of C samples t = sub*C .. sub*C + C - 1 (C odd, LPW*C >= W), read once
+// from LDS into registers.  Both passes then run on registers: the neighbours of the peak test are
+// the lane's own x[k-1] / x[k+1] (only the run's first prev comes from LDS, and the run's last
+// "rising" bit from the next lane), so a sample costs one LDS read per axis instead of four, and no
+// pass carries a per-sample mask: the run positions past the window hold copies of sample W - 1,
+// whose contributions are subtracted once per window (D = LPW*C - W of them), and the peak bits
+// of t = 0 / t >= W - 1 are cleared with one per-lane mask.  The block stages the CONTIGUOUS
+// sample span of its windows (overlapping windows share it), so a batch of stride < W windows
+// reads every sample once.  One-shot blocks, several per CU: the loads of one block overlap the
+// arithmetic of the others.
+// ------------------------------------------------------------------------------------------------
+constexpr int RCMAX = 17;  // samples per lane held in registers (C <= RCMAX)
+
+// reduction over a group of LPW = 16 / 32 / 64 lanes: 16-lane DPP butterflies, then the gfx950 row
+// (lane ^ 16) and half (lane ^ 32) swaps on the VALU
+template <int LPW, typename T, typename Op>
+__device__ __forceinline__ T greduce(T v, Op op, const mlpf::LaneSwap& sw) {
+  v = rreduce<16, T>(v, op);
+  if constexpr (LPW >= 32) v = op(v, __builtin_bit_cast(T, sw.x16(__builtin_bit_cast(uint32_t, v))));
+  if constexpr (LPW >= 64) v = op(v, __builtin_bit_cast(T, sw.x32(__builtin_bit_cast(uint32_t, v))));
+  return v;
+}
+
+// bin of a sample: fma instead of (x - lo) * scale (a boundary sample may move by one bin, within
+// the 1/W the tests allow), clamped in float (med3) so the conversion never sees a negative
+__device__ __forceinline__ uint32_t bin_of(float x, float sc, float off) {
+  return (uint32_t)__builtin_amdgcn_fmed3f(fmaf(x, sc, off), 0.f, (float)(NB - 1));
+}
+
+template <int A, int LPW, bool MLP>
+__global__ __launch_bounds__(256) void window_features_reg_kernel(const float* __restrict__ stream, int W,
+                                                                  int stride, int64_t n_windows, float ms_per_sample,
+                                                                  float* __restrict__ out, int ld_out, MlpOut mo,
+                                                                  int C, int wpb) {
+  static_assert(LPW == 16 || LPW == 32 || LPW == 64, "groups of 16, 32 or 64 lanes");
+  constexpr int T3 = A / 3, GPW = 64 / LPW;
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int nt = (int)blockDim.x, tid = (int)threadIdx.x;
+  const int64_t w0 = (int64_t)blockIdx.x * wpb;
+  const int nwin = (int)min<int64_t>(wpb, n_windows - w0);
+  float* const span = lds + PAD;
+
+  // ---- stage the span: samples [w0 * stride, (w0 + nwin - 1) * stride + W), A floats each ----
+  {
+    const float* src = stream + w0 * stride * A;
+    const int nspan = ((nwin - 1) * stride + W) * A;
+    int done = 0;
+    if ((reinterpret_cast<uintptr_t>(src) & 15) == 0) {
+      const int n4 = nspan >> 2;
+      const v4f* s4 = reinterpret_cast<const v4f*>(src);
+      v4f* d4 = reinterpret_cast<v4f*>(span);
+      // unconditional (clamped) loads and stores: no exec-masked branches between them, so all eight
+      // loads are in flight before the first store waits (a clamped slot rewrites the last float4)
+      for (int f0 = tid; f0 < n4; f0 += 8 * nt) {
+        v4f r[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) r[u] = s4[min(f0 + u * nt, n4 - 1)];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) d4[min(f0 + u * nt, n4 - 1)] = r[u];
+      }
+      done = n4 * 4;
+    }
+    for (int e = done + tid; e < nspan; e += nt) span[e] = src[e];
+  }
+  __syncthreads();
+
+  const int lane = tid & 63, wave = tid >> 6, sub = lane % LPW;
+  const int g = wave % T3;
+  const int wi = GPW * (wave / T3) + lane / LPW;
+  const bool valid = wi < nwin;
+  const int64_t win = w0 + (valid ? wi : 0);
+  const float* img = span + (valid ? wi : 0) * stride * A + 3 * g;  // the group's triad
+  const mlpf::LaneSwap sw(lane);
+  const int tb = sub * C;
+  const float invW = 1.f / (float)W;
+  const float D = (float)(LPW * C - W);  // copies of sample W - 1 in the runs
+
+  // Runtime C <= RCMAX: every k-step is guarded by the uniform k < C, which also keeps the
+  // scheduler from hoisting all 3*RCMAX loads and their consumers at once (register pressure)
+  float x[3][RCMAX];
+#pragma unroll
+  for (int k = 0; k < RCMAX; ++k)
+    if (k < C) {
+      const float* p = img + min(tb + k, W - 1) * A;
+#pragma unroll
+      for (int c = 0; c < 3; ++c) x[c][k] = p[c];
+    }
+  float xl[3], pv0[3];
+  {
+    const float* pl = img + (W - 1) * A;
+    const float* pp = img + (min(tb, W) - 1) * A;  // sample before the run (t = -1: the PAD / previous window)
+#pragma unroll
+    for (int c = 0; c < 3; ++c) { xl[c] = pl[c]; pv0[c] = pp[c]; }
+  }
+
+  // ---- pass 1 ----
+  float mean[3], mn[3], mx[3], en[3];
+  {
+    float s[3], q[3], lo[3], hi[3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) { s[c] = 0.f; q[c] = 0.f; lo[c] = x[c][0]; hi[c] = x[c][0]; }
+#pragma unroll
+    for (int k = 0; k < RCMAX; ++k)
+      if (k < C) {
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+          const float v = x[c][k];
+          s[c] += v; q[c] = fmaf(v, v, q[c]); lo[c] = fminf(lo[c], v); hi[c] = fmaxf(hi[c], v);
+        }
+      }
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      const float S = greduce<LPW, float>(s[c], [](float a, float b) { return a + b; }, sw) - D * xl[c];
+      const float Q = greduce<LPW, float>(q[c], [](float a, float b) { return a + b; }, sw) - D * xl[c] * xl[c];
+      mean[c] = S * invW; en[c] = Q * invW;
+      mn[c] = greduce<LPW, float>(lo[c], [](float a, float b) { return fminf(a, b); }, sw);
+      mx[c] = greduce<LPW, float>(hi[c], [](float a, float b) { return fmaxf(a, b); }, sw);
+    }
+  }
+
+  // ---- pass 2 ----
+  float sc[3], off[3], thr[3];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    const float range = mx[c] - mn[c];
+    sc[c] = range > 0.f ? (float)NB / range : 0.f;
+    off[c] = -mn[c] * sc[c];
+    thr[c] = mean[c] + 0.5f * (mx[c] - mean[c]);
+  }
+  float ad[3] = {0.f, 0.f, 0.f}, v2[3] = {0.f, 0.f, 0.f}, res = 0.f, cxy = 0.f, cxz = 0.f, cyz = 0.f;
+  uint64_t h[3] = {0, 0, 0};
+  uint32_t R[3] = {0, 0, 0}, PT[3] = {0, 0, 0};  // bit j <-> run sample k = C - 1 - j
+#pragma unroll
+  for (int k = 0; k < RCMAX; ++k)
+    if (k < C) {
+      float d[3];
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        const float xv = x[c][k], pv = k ? x[c][k - 1] : pv0[c];
+        const float dc = xv - mean[c];
+        d[c] = dc;
+        ad[c] += fabsf(dc);
+        v2[c] = fmaf(dc, dc, v2[c]);
+        h[c] += 1ull << __umul24(bin_of(xv, sc[c], off[c]), 6u);  // v_mul_u32_u24, not the quarter-rate mul_lo
+        const bool r = xv > pv;
+        R[c] = (R[c] << 1) + (r ? 1u : 0u);
+        PT[c] = (PT[c] << 1) + ((r && xv > thr[c]) ? 1u : 0u);
+      }
+      res += __builtin_amdgcn_sqrtf(fmaf(x[0][k], x[0][k], fmaf(x[1][k], x[1][k], x[2][k] * x[2][k])));
+      cxy = fmaf(d[0], d[1], cxy);
+      cxz = fmaf(d[0], d[2], cxz);
+      cyz = fmaf(d[1], d[2], cyz);
+    }
+
+  // peak positions: 0 < t < W - 1 (t = tb + k), i.e. bits j in [C - 1 - kh, C - 1 - kl]
+  const int kl = sub == 0 ? 1 : 0, kh = min(C - 1, W - 2 - tb);
+  const uint32_t pmask = kh >= kl ? ((1u << (C - kl)) - 1u) & ~((1u << (C - 1 - kh)) - 1u) : 0u;
+
+  // ---- reduce + write ----
+  float* o = MLP ? nullptr : out + win * (int64_t)ld_out;
+  uint16_t* ob = MLP ? mo.out + win * (int64_t)ld_out : nullptr;
+  auto emit = [&](bool on, int f, float v) {
+    if (!(on && valid)) return;
+    if constexpr (MLP) {
+      const float xv = v != v ? mo.nan_value : v;
+      ob[f] = f2bf((xv - mo.mean[f]) * mo.inv_std[f]);
+    } else {
+      o[f] = v;
+    }
+  };
+  constexpr int F = 17 * A + 4 * T3;
+  if constexpr (MLP) {  // zero the pad columns of the row (triad 0's group)
+    if (g == 0 && valid)
+      for (int f = F + sub; f < ld_out; f += LPW) ob[f] = 0;
+  }
+  const int off_avg = A * NB, off_peak = off_avg + A, off_abs = off_peak + A, off_std = off_abs + A;
+  const int off_res = off_std + A, off_min = off_res + T3, off_max = off_min + A, off_en = off_max + A;
+  const int off_corr = off_en + A;
+  const auto fsum = [](float a, float b) { return a + b; };
+  const auto usum = [](uint32_t a, uint32_t b) { return a + b; };
+  float sd[3], dl[3];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    const int ax = 3 * g + c;
+    dl[c] = xl[c] - mean[c];
+    const float adv = (greduce<LPW, float>(ad[c], fsum, sw) - D * fabsf(dl[c])) * invW;
+    const float var = fmaxf(greduce<LPW, float>(v2[c], fsum, sw) - D * dl[c] * dl[c], 0.f) * invW;
+    sd[c] = __builtin_amdgcn_sqrtf(var);
+    // the next lane's first rising bit closes this lane's run (the group's last lane: masked)
+    const uint32_t rC = (uint32_t)__shfl((int)(R[c] >> (C - 1)) & 1, (lane + 1) & 63, 64);
+    const uint32_t P = PT[c] & ~((R[c] << 1) | rC) & pmask;
+    const int npk = (int)greduce<LPW, uint32_t>((uint32_t)__builtin_popcount(P), usum, sw);
+    const int first = greduce<LPW, int>(P ? tb + C - 1 - (31 - __builtin_clz(P)) : 0x7fffffff,
+                                         [](int a, int b) { return min(a, b); }, sw);
+    const int last = greduce<LPW, int>(P ? tb + C - 1 - __builtin_ctz(P) : -1, [](int a, int b) { return max(a, b); }, sw);
+    // bins: packed 6-bit counts -> five words of two 16-bit bins; lane `sub` < NB writes bin `sub`
+    uint32_t hw[5];
+#pragma unroll
+    for (int j = 0; j < 5; ++j)
+      hw[j] = greduce<LPW, uint32_t>((uint32_t)((h[c] >> (12 * j)) & 63) | ((uint32_t)((h[c] >> (12 * j + 6)) & 63) << 16),
+                                     usum, sw);
+    {
+      uint32_t word = hw[0];
+#pragma unroll
+      for (int j = 1; j < 5; ++j) word = (sub >> 1) == j ? hw[j] : word;
+      uint32_t cnt = (sub & 1) ? word >> 16 : word & 0xffffu;
+      cnt -= (uint32_t)sub == bin_of(xl[c], sc[c], off[c]) ? (uint32_t)(LPW * C - W) : 0u;
+      emit(sub < NB, ax * NB + sub, (float)cnt * invW);
+    }
+    const float peak =
+        npk >= 2 ? (float)(last - first) * __builtin_amdgcn_rcpf((float)(npk - 1)) * ms_per_sample : NAN;
+    float v = mean[c];
+    int f = off_avg + ax;
+    v = sub == 1 ? peak : v;       f = sub == 1 ? off_peak + ax : f;
+    v = sub == 2 ? adv : v;        f = sub == 2 ? off_abs + ax : f;
+    v = sub == 3 ? sd[c] : v;      f = sub == 3 ? off_std + ax : f;
+    v = sub == 4 ? mn[c] : v;      f = sub == 4 ? off_min + ax : f;
+    v = sub == 5 ? mx[c] : v;      f = sub == 5 ? off_max + ax : f;
+    v = sub == 6 ? en[c] : v;      f = sub == 6 ? off_en + ax : f;
+    emit(sub < 7, f, v);
+  }
+  // triad: resultant (lane 0) and the three correlations (lanes 1..3)
+  {
+    const float rl = __builtin_amdgcn_sqrtf(fmaf(xl[0], xl[0], fmaf(xl[1], xl[1], xl[2] * xl[2])));
+    const float rs = (greduce<LPW, float>(res, fsum, sw) - D * rl) * invW;
+    const float sxy = (greduce<LPW, float>(cxy, fsum, sw) - D * dl[0] * dl[1]) * invW;
+    const float sxz = (greduce<LPW, float>(cxz, fsum, sw) - D * dl[0] * dl[2]) * invW;
+    const float syz = (greduce<LPW, float>(cyz, fsum, sw) - D * dl[1] * dl[2]) * invW;
+    const float rxy = (sd[0] > 0.f && sd[1] > 0.f) ? sxy * __builtin_amdgcn_rcpf(sd[0] * sd[1]) : 0.f;
+    const float rxz = (sd[0] > 0.f && sd[2] > 0.f) ? sxz * __builtin_amdgcn_rcpf(sd[0] * sd[2]) : 0.f;
+    const float ryz = (sd[1] > 0.f && sd[2] > 0.f) ? syz * __builtin_amdgcn_rcpf(sd[1] * sd[2]) : 0.f;
+    float v = rs;
+    int f = off_res + g;
+    v = sub == 1 ? rxy : v;  f = sub == 1 ? off_corr + 3 * g : f;
+    v = sub == 2 ? rxz : v;  f = sub == 2 ? off_corr + 3 * g + 1 : f;
+    v = sub == 3 ? ryz : v;  f = sub == 3 ? off_corr + 3 * g + 2 : f;
+    emit(sub < 4, f, v);
+  }
+}
+
 int cu_count() {
   static int n = 0;
   if (!n) {
@@ -529,6 +775,42 @@ int launch_axes(const float* stream, int64_t n_samples, int window, int stride, 
     HAR_CHECK_LAUNCH();
     return 0;
   };
+  // register-resident kernel: the smallest group (16 / 32 / 64 lanes) whose runs of C <= RCMAX
+  // samples (C odd: lanes C*A floats apart hit distinct LDS banks for odd A) cover the window
+  if (!g_window_legacy) {
+    // the smallest group (16 / 32 / 64 lanes), then the shortest odd run C in {5, 9, 13, 17} (lanes
+    // C*A floats apart hit distinct LDS banks for odd A) with LPW * C >= W (W <= 1088)
+    int lpw = 0, C = 0;
+    for (int l = 16; l <= 64 && !lpw; l *= 2)
+      for (int c : {5, 9, 13, 17})
+        if (l * c >= window) { lpw = l; C = c; break; }
+    if (lpw) {
+      const int gpw = 64 / lpw;
+      auto span_bytes = [&](int wpb) -> int64_t {
+        return (PAD + ((int64_t)(wpb - 1) * stride + window) * A + SLACK) * (int64_t)sizeof(float);
+      };
+      // waves per block: a multiple of T3, at most 4; the most whose span fits 48 KB (>= 3 blocks per CU)
+      int m = 0;
+      for (int mm = 4 / T3; mm >= 1; --mm)
+        if (span_bytes(mm * gpw) <= 48 * 1024) { m = mm; break; }
+      if (!m && span_bytes(gpw) <= 160 * 1024) m = 1;
+      if (m) {
+        const int wpb = m * gpw, nt = 64 * T3 * m;
+        const int64_t nblk = (n_windows + wpb - 1) / wpb;
+        const size_t bytes = (size_t)span_bytes(wpb);
+        const unsigned grid = (unsigned)nblk;  // one-shot blocks (a persistent DMA-prefetch variant measured slower)
+#define HAR_WIN_R(L)                                                                                         \
+  window_features_reg_kernel<A, L, MLP><<<grid, nt, bytes, s>>>(stream, window, stride, n_windows, ms, out, ld_out, \
+                                                                mo, C, wpb)
+        if (lpw == 16) HAR_WIN_R(16);
+        else if (lpw == 32) HAR_WIN_R(32);
+        else HAR_WIN_R(64);
+#undef HAR_WIN_R
+        HAR_CHECK_LAUNCH();
+        return 0;
+      }
+    }
+  }
   // 8-lane groups (half the reduction and write-out work per window) when two waves' sixteen
   // 3-axis windows fit 64 KB — the short-window WISDM case; else 16-lane groups
   if constexpr (A == 3) {
@@ -549,6 +831,8 @@ int launch_axes(const float* stream, int64_t n_samples, int window, int stride, 
 
 
 }  // namespace
+
+extern "C" void har_window_set_legacy(int on) { g_window_legacy = on != 0; }
 
 extern "C" int har_window_features(const float* stream, int64_t n_samples, int axes, int window, int stride,
                                    int64_t n_windows, float hz, int nbins, float* out, int ld_out, hipStream_t s) {

@@ -51,7 +51,7 @@ def test_synth_stream_shard_invariant():
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("axes,window,stride", [(3, 200, 200), (3, 500, 250), (9, 500, 500), (6, 97, 31), (3, 97, 40),
-                                               (9, 37, 37)])
+                                               (9, 37, 37), (3, 700, 350), (6, 1100, 1100)])
 def test_window_kernel_matches_torch(cuda, axes, window, stride):
     from har.features.window import window_features
 

@@ -79,7 +79,8 @@ def stamps(B=65536):
         live = s[:, 0] > 0
         s = s[live]
         print(f"--- {name}: {live.sum()} waves stamped")
-        lim = 10 if (k == 0 and (s[:, 10] > 0).all()) else 34  # forward slots 10.. hold tile-4 sub-phases
+        # forward slots 10.. / backward slots 26.. hold tile-4 sub-phases
+        lim = 10 if (k == 0 and (s[:, 10] > 0).all()) else 26 if (k == 1 and (s[:, 26] > 0).all()) else 34
         ntile = int(((s[:, 2:lim] > 0).sum(1)).max())
         rows = [("prologue (weights in regs)", s[:, 1] - s[:, 0])]
         for t in range(min(ntile, 32)):
@@ -95,6 +96,12 @@ def stamps(B=65536):
                    ("  tile 4: stage 1 + X loads", s[:, 13] - s[:, 12]), ("  tile 4: to next tile (barrier)", s[:, 7] - s[:, 13])]
             for nm, v in sub:
                 print(f"  {nm:28s} median {np.median(v):9.0f}  max {v.max():9.0f} cycles")
+        if k == 1 and (s[:, 26] > 0).all():  # backward sub-phases of tile 4 (stamped slots 26..30)
+            sub = [("  tile 4: dact2 -> LDS", s[:, 26] - s[:, 6]), ("  tile 4: X stage + refills", s[:, 27] - s[:, 26]),
+                   ("  tile 4: h1 recompute", s[:, 28] - s[:, 27]), ("  tile 4: (a) + (b) + db1", s[:, 29] - s[:, 28]),
+                   ("  tile 4: (c) dW0", s[:, 30] - s[:, 29]), ("  tile 4: barrier", s[:, 7] - s[:, 30])]
+            for nm, v in sub:
+                print(f"  {nm:28s} median {np.median(v):9.0f}  max {v.max():9.0f} cycles")
         t0 = s[:, 38].min()
         ent, ex = (s[:, 38] - t0) * 10.0, (s[:, 39] - t0) * 10.0  # ns
         print(f"  real time: entry spread {ent.max():.0f} ns (median {np.median(ent):.0f}), "
@@ -104,6 +111,8 @@ def stamps(B=65536):
 
 def main():
     dev = torch.device("cuda")
+    # backward scheduling variant under test (HAR_BWD_VARIANT, csrc/kernels/mlp_step.hip)
+    _native.kernels().mlp_set_bwd_variant(int(os.environ.get("HAR_BWD_VARIANT", "0")))
     if sys.argv[1:2] == ["--stamps"]:
         return stamps(int(sys.argv[2]) if len(sys.argv) > 2 else 65536)
     sizes = [int(a) for a in sys.argv[1:]] or [16384, 32768, 65536, 131072, 262144]

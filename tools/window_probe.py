@@ -32,10 +32,38 @@ while time.time() - t0 < 0.5:
         a @ a
     torch.cuda.synchronize()
 
-for s, W, hz in streams:
-    for _ in range(20):
-        window_features(s, W, W, hz)
-for _ in range(20):
-    window_features_mlp(s3, 200, 200, 20.0, mean, inv, 64, -1.0, out=out)
+from har.ops import _native  # noqa: E402
+
+mod = _native.kernels()
+
+
+def timed(fn, reps=20):
+    """us per launch (HIP events around `reps` back-to-back launches, best of 3)"""
+    fn()
+    torch.cuda.synchronize()
+    best = 1e30
+    for _ in range(3):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            fn()
+        e1.record()
+        torch.cuda.synchronize()
+        best = min(best, e0.elapsed_time(e1) * 1e3 / reps)
+    return best
+
+
+modes = [("v3", 0), ("legacy", 1)] if os.environ.get("HAR_WINDOW_AB", "1") != "0" else [("v3", 0)]
+for name, legacy in modes:
+    mod.window_set_legacy(legacy)
+    for s, W, hz in streams:
+        us = timed(lambda: window_features(s, W, W, hz))
+        gb = s.numel() * 4 / 1e9
+        print(f"{name:7s} {s.shape[1]} axes W={W} stride={W}: {us:8.1f} us  {gb / us * 1e3:6.2f} TB/s ({gb:.3f} GB)")
+    us = timed(lambda: window_features_mlp(s3, 200, 200, 20.0, mean, inv, 64, -1.0, out=out))
+    print(f"{name:7s} 3 axes W=200 MLP rows : {us:8.1f} us  {s3.numel() * 4 / us / 1e3:6.2f} TB/s")
+    us = timed(lambda: window_features(s3, 200, 100, 20.0))
+    print(f"{name:7s} 3 axes W=200 stride=100: {us:8.1f} us  {s3.numel() * 4 / us / 1e3:6.2f} TB/s")
+mod.window_set_legacy(0)
 torch.cuda.synchronize()
 print("ok")
