@@ -38,9 +38,10 @@ using namespace mlpf;
 // (shader clock) at fixed points into its own 40-slot row of that buffer (slots 38 / 39:
 // s_memrealtime at entry / exit, 100 MHz, one clock for the whole chip).  Nothing else reads them.
 uint64_t* g_har_mlp_stamps = nullptr;
-// Backward scheduling variant (probe A/B): 1 = no scheduling barrier between the refills + dact2
-// build and the tile's MFMA phases
+// Scheduling variants (probe A/B, har_mlp_set_bwd_variant): bit 0 = the backend's IGLP small-GEMM
+// interleave in the backward tile, bit 1 = its exp / MFMA interleave in the forward tile
 int g_har_mlp_bwd_ilv = 0;
+int g_har_mlp_fwd_variant = 0;
 
 namespace {
 
@@ -81,7 +82,7 @@ __device__ __forceinline__ bf16x8_t ldx(const bf16_t* __restrict__ X, int row, i
   return *reinterpret_cast<const bf16x8_t*>(X + (size_t)row * K0 + kc * 32 + g * 8);
 }
 
-template <int K0, bool STAMP>
+template <int K0, bool STAMP, bool IGLP>
 __global__ __launch_bounds__(512) void mlp_fwd3_kernel(
     const bf16_t* __restrict__ X, const bf16_t* __restrict__ W0, const float* __restrict__ b0,
     const bf16_t* __restrict__ W1, const float* __restrict__ b1, const bf16_t* __restrict__ Wo,
@@ -295,6 +296,8 @@ __global__ __launch_bounds__(512) void mlp_fwd3_kernel(
       load_x(k + 3);
       if (k == 4) HAR_STAMP(FW, 13)
     }
+    // IGLP: the backend's exp / MFMA interleave strategy over the steady-state body (probe A/B)
+    if constexpr (IGLP) if (!first && !last) __builtin_amdgcn_iglp_opt(2);
     __syncthreads();
   };
   if (nt > 0) iter(0, true, nt == 1);
@@ -605,15 +608,15 @@ __global__ __launch_bounds__(512) void mlp_bwd3_kernel(
     HAR_B3_STAGE_X(i + 2)
     HAR_B3_LOAD_D(t0 + i + 2)
     HAR_B3_LOAD_X(t0 + i + 3)
-    // the refills are issued before the compute; ILV lets the scheduler interleave the dact2
-    // build (VALU / LDS stores) with the MFMAs of h1 / (a) / (b) / (c) instead
-    if constexpr (!ILV) __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_sched_barrier(0);  // the refills are issued before the compute
     if (i == 4) HAR_STAMP(8, 27)
     tile_h1(i + 1);                 // X tile i+1 has been in LDS since the last barrier
     if (i == 4) HAR_STAMP(8, 28)
     tile_ab(i);
     if (i == 4) HAR_STAMP(8, 29)
     if (!first) tile_c(i - 1);
+    // ILV: the backend's small-GEMM DS / MFMA interleave over the tile's compute (probe A/B)
+    if constexpr (ILV) if (!first) __builtin_amdgcn_iglp_opt(0);
     if (i == 4) HAR_STAMP(8, 30)
     __syncthreads();                // dact2 i+1 / X i+2 staged, h1 i+1 and dact1 i complete
   };
@@ -660,7 +663,8 @@ template <int K0>
 void launch_fwd3(const bf16_t* X, const bf16_t* W0, const float* b0, const bf16_t* W1, const float* b1,
                  const bf16_t* Wo, const float* bo, const int32_t* labels, int B, int C, float scale, uint32_t* dz,
                  uint32_t* mask, float* slab, float* bl, int32_t* bc, int nwg, hipStream_t s) {
-  auto k = g_har_mlp_stamps ? mlp_fwd3_kernel<K0, true> : mlp_fwd3_kernel<K0, false>;
+  auto k = g_har_mlp_fwd_variant ? (g_har_mlp_stamps ? mlp_fwd3_kernel<K0, true, true> : mlp_fwd3_kernel<K0, false, true>)
+                                 : (g_har_mlp_stamps ? mlp_fwd3_kernel<K0, true, false> : mlp_fwd3_kernel<K0, false, false>);
   k<<<nwg, 512, FWD_LDS, s>>>(X, W0, b0, W1, b1, Wo, bo, labels, B, C, scale, dz, mask, slab, bl, bc, g_har_mlp_stamps);
 }
 
@@ -728,4 +732,7 @@ extern "C" int har_mlp_step_bwd(const uint32_t* dz, const uint32_t* mask, const 
 }
 
 extern "C" void har_mlp_set_stamps(uint64_t* p) { g_har_mlp_stamps = p; }
-extern "C" void har_mlp_set_bwd_variant(int v) { g_har_mlp_bwd_ilv = v; }
+extern "C" void har_mlp_set_bwd_variant(int v) {
+  g_har_mlp_bwd_ilv = v & 1;
+  g_har_mlp_fwd_variant = (v >> 1) & 1;  // bit 1: forward variant
+}
