@@ -336,17 +336,19 @@ class LogisticRegression(Estimator, ClassifierParams):
         models = []
         fobj_h = fobj.double().cpu()
         iters_h = iters.cpu()
+        # every model's coefficients / intercepts in a few batched ops (per-model views below): a
+        # 45-model CrossValidator otherwise pays ~4 small launches per model on the host
+        coef_all = xs[:, :, :F] * inv_std[:, None, :]
+        icpt_all = xs[:, :, F].clone()
+        if binomial:
+            coef_all, icpt_all = coef_all[:, 1:2], icpt_all[:, 1:2]
+        elif self.fitIntercept:
+            icpt_all = icpt_all - icpt_all.mean(dim=1, keepdim=True)
         for bi in range(B):
-            coef = xs[bi, :, :F] * inv_std[bi][None, :]
-            icpt = xs[bi, :, F].clone()
-            if binomial:
-                coef, icpt = coef[1:2], icpt[1:2]
-            elif self.fitIntercept:
-                icpt = icpt - icpt.mean()
             summary = {"objective": float(fobj_h[bi]), "iterations": int(iters_h[bi]), "n_evals": n_evals,
                        "objectiveHistory": history[bi]}
-            models.append(self._apply_thresholds(LogisticRegressionModel(coef.detach(), icpt.detach(), binomial,
-                                                                         device=dev, summary=summary)))
+            models.append(self._apply_thresholds(LogisticRegressionModel(coef_all[bi].detach(), icpt_all[bi].detach(),
+                                                                         binomial, device=dev, summary=summary)))
         if ckpt is not None:
             st = {}
             for bi, mo in enumerate(models):

@@ -348,6 +348,17 @@ class DeviceLogregSolver:
             mod.lbfgs_phase_h(qa, ph, head, filled, init, fin, fin_init, fin_head, fin_it, KP, s)
 
         self.x.copy_(x0.reshape(self.B, self.D))
+        if not poll and self.allreduce is None and os.environ.get("HAR_LR_NATIVE_SOLVE", "1") != "0":
+            # the fixed launch sequence below as ONE native call (bind.cpp logreg_solve): no
+            # convergence poll and no collective, so nothing needs the host between launches
+            plan = getattr(self, "_solve_plan", None)
+            if plan is None:
+                chunks = lambda ts: [mod.logreg_eval_chunk(ev, gr) for ev, gr in self._eval_args(ts)]  # noqa: E731
+                plan = self._solve_plan = mod.logreg_solve_plan(qa, chunks(self.T), chunks(1), KP)
+            mod.logreg_solve(plan, self.max_iter, self.m, s)
+            self.n_evals += 1 + self.max_iter
+            self.hist_rows = self.max_iter + 1
+            return self.x, self.fobj, self.iters
         phase(1, init=1)
         self._evaluate(self.T)
         phase(2, init=1)

@@ -72,7 +72,12 @@ def _lr_margins(models, hm) -> torch.Tensor:
         from ..ops.logreg import logreg_margins_native
 
         KP = 8 if k <= 8 else 16
-        W = torch.cat([m.weight_table(KP).to(hm.device) for m in models])
+        # one batched weight table [n, F+1, KP] (row F = intercepts) instead of one per model
+        coef = torch.stack([m.coefficientMatrix for m in models]).to(hm.device)
+        F = coef.shape[2]
+        W = torch.zeros(len(models), F + 1, KP, device=hm.device)
+        W[:, :F, :k] = coef.transpose(1, 2)
+        W[:, F, :k] = torch.stack([m.interceptVector for m in models]).to(hm.device)
         m = logreg_margins_native(hm, W, k, len(models))[:, :, :k]
         return torch.cat([-m, m], dim=2) if models[0].binomial else m
     return torch.stack([mm.predict_raw(hm) for mm in models])
@@ -129,11 +134,13 @@ class CrossValidator(Estimator):
             y = labels_tensor(table, est.labelCol, dev)
             K = int(max(int(y.max()) + 1, len((table[est.labelCol].meta or {}).get("vocab") or [])))
             fold_t = torch.as_tensor(fold, device=dev)
+            in_fold = fold_t[None, :] == torch.arange(k, device=dev)[:, None]  # [k, N]: ONE launch, not k
+            train_w = (~in_fold).float()
             specs, index = [], []
             for mi, pm in enumerate(maps):
                 sub = est.copy(pm)
                 for f in range(k):
-                    specs.append(FitSpec((fold_t != f).float(), sub.regParam, sub.elasticNetParam))
+                    specs.append(FitSpec(train_w[f], sub.regParam, sub.elasticNetParam))
                     index.append((mi, f))
             # maxIter / tol / family etc. may differ per map only through regParam/elasticNetParam
             base = est.copy(maps[0]) if maps else est
@@ -144,7 +151,7 @@ class CrossValidator(Estimator):
             # every (map, fold) model scored on its validation fold in ONE batched pass
             raw = _lr_margins(models, hm)                                          # [n, N, K]
             pred = _batched_predictions(models, raw)
-            mask = torch.stack([fold_t == f for _, f in index])
+            mask = in_fold[torch.tensor([f for _, f in index], device=dev)]
             vals = ev.evaluate_batched(y, pred, mask, K, raw)
             for (mi, f), v in zip(index, vals):
                 metrics[mi, f] = v

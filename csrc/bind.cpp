@@ -159,6 +159,58 @@ struct QnArgsHolder {
   QnArgs a;
 };
 
+// One launch chunk of a LogisticRegression objective evaluation: the evaluate + gradient kernels'
+// arguments (pointers fixed for the life of a DeviceLogregSolver).
+struct LogregEvalChunk {
+  LogregEvalArgs ev;
+  LogregGradArgs gr;
+  int KP, n_models;
+};
+
+// The whole device L-BFGS / OWL-QN solve of a fit as ONE host call (no convergence poll, no
+// collective): the same launch sequence as ops/logreg.py DeviceLogregSolver.solve enqueues from
+// Python, minus ~60 pybind round trips per fit (the host, not the GPU, bounded a WISDM fit).
+struct LogregSolvePlan {
+  QnArgs q;
+  std::vector<LogregEvalChunk> evT, ev1;  // evaluations of the T trials (first) / 1 per model
+  int KP = 8;
+};
+
+static void logreg_solve_run(const LogregSolvePlan& p, int max_iter, int m, hipStream_t s) {
+  auto phase = [&](int ph, int head, int filled, int init, int fin, int fin_init, int fin_head, int fin_it) {
+    QnArgs a = p.q;
+    a.head = head;
+    a.filled = filled;
+    a.init = init;
+    a.fin = fin;
+    a.fin_only = 0;
+    a.fin_init = fin_init;
+    a.fin_head = fin_head;
+    a.fin_it = fin_it;
+    check(har_lbfgs_phase(&a, p.KP, ph, s), "lbfgs_phase");
+  };
+  auto evaluate = [&](const std::vector<LogregEvalChunk>& v) {
+    for (const auto& c : v) {
+      check(har_logreg_eval(&c.ev, c.KP, c.n_models, s), "logreg_eval");
+      check(har_logreg_grad(&c.gr, c.KP, c.n_models, s), "logreg_grad");
+    }
+  };
+  phase(1, 0, 0, 1, 0, 0, 0, 0);
+  evaluate(p.evT);
+  phase(2, 0, 0, 1, 0, 0, 0, 0);
+  int head = 0, filled = 0, prev = -1;
+  for (int it = 0; it < max_iter; ++it) {
+    phase(0, head, filled, 0, 1, prev < 0 ? 1 : 0, prev > 0 ? prev : 0, it);
+    phase(1, head, filled, 0, 0, 0, 0, 0);
+    evaluate(p.ev1);
+    phase(2, head, filled, 0, 0, 0, 0, 0);
+    prev = head;
+    head = (head + 1) % m;
+    filled = filled + 1 < m ? filled + 1 : m;
+  }
+  phase(3, 0, 0, 0, 1, prev < 0 ? 1 : 0, prev > 0 ? prev : 0, max_iter);
+}
+
 // The flagship MLP training step as ONE host call: the buffers of an engine never move, so their
 // pointers, the gradient-reduction regions and the Adam hyper-parameters are fixed once per (engine,
 // batch size) and run() enqueues mlp_step_fwd -> mlp_step_bwd -> grad_reduce_adam with only the batch
@@ -258,6 +310,70 @@ PYBIND11_MODULE(_har_native, m) {
     a.R = P<float>(R);
     a.slab = P<float>(slab);
     check(har_logreg_eval(&a, KP, n_models, S(stream)), "logreg_eval");
+  });
+  // argument holders for logreg_solve_plan: the same positional arguments as logreg_eval /
+  // logreg_grad below, without the stream
+  py::class_<LogregEvalChunk>(m, "LogregEvalChunk");
+  m.def("logreg_eval_chunk", [](py::tuple e, py::tuple g) {
+    LogregEvalChunk c{};
+    auto U = [](py::handle h) { return h.cast<u>(); };
+    auto I = [](py::handle h) { return h.cast<int64_t>(); };
+    c.ev.dense = P<const float>(U(e[0]));
+    c.ev.ldd = I(e[1]);
+    c.ev.Fd = (int)I(e[2]);
+    c.ev.dense_cols = P<const int32_t>(U(e[3]));
+    c.ev.cat = P<const int32_t>(U(e[4]));
+    c.ev.C = (int)I(e[5]);
+    c.ev.y = P<const int32_t>(U(e[6]));
+    c.ev.rw = P<const float>(U(e[7]));
+    c.ev.inv_wsum = P<const float>(U(e[8]));
+    c.ev.W = P<const float>(U(e[9]));
+    c.ev.N = I(e[10]);
+    c.ev.F = (int)I(e[11]);
+    c.ev.K = (int)I(e[12]);
+    c.ev.T = (int)I(e[13]);
+    c.ev.tstride = (int)I(e[14]);
+    c.ev.model0 = (int)I(e[15]);
+    c.ev.mode = (int)I(e[16]);
+    c.ev.R = P<float>(U(e[17]));
+    c.ev.slab = P<float>(U(e[18]));
+    c.KP = (int)I(e[19]);
+    c.n_models = (int)I(e[20]);
+    c.gr.slab = P<const float>(U(g[0]));
+    c.gr.R = P<const float>(U(g[1]));
+    c.gr.col_map = P<const int32_t>(U(g[2]));
+    c.gr.csc_rows = P<const int32_t>(U(g[3]));
+    c.gr.csc_off = P<const int32_t>(U(g[4]));
+    c.gr.col_slice = P<const int32_t>(U(g[5]));
+    c.gr.SL = (int)I(g[6]);
+    c.gr.inv_std = P<const float>(U(g[7]));
+    c.gr.pmask = P<const float>(U(g[8]));
+    c.gr.N = I(g[9]);
+    c.gr.F = (int)I(g[10]);
+    c.gr.Fd = (int)I(g[11]);
+    c.gr.K = (int)I(g[12]);
+    c.gr.T = (int)I(g[13]);
+    c.gr.tstride = (int)I(g[14]);
+    c.gr.model0 = (int)I(g[15]);
+    c.gr.ntiles = (int)I(g[16]);
+    c.gr.G = P<float>(U(g[17]));
+    c.gr.loss = P<double>(U(g[18]));
+    c.gr.loss_fx = P<float>(U(g[19]));
+    if ((int)I(g[20]) != c.KP || (int)I(g[21]) != c.n_models) throw std::runtime_error("logreg_eval_chunk: KP / n mismatch");
+    return c;
+  });
+  py::class_<LogregSolvePlan>(m, "LogregSolvePlan");
+  m.def("logreg_solve_plan", [](const QnArgsHolder& h, std::vector<LogregEvalChunk> evT,
+                                std::vector<LogregEvalChunk> ev1, int KP) {
+    LogregSolvePlan p;
+    p.q = h.a;
+    p.evT = std::move(evT);
+    p.ev1 = std::move(ev1);
+    p.KP = KP;
+    return p;
+  });
+  m.def("logreg_solve", [](const LogregSolvePlan& p, int max_iter, int m, u stream) {
+    logreg_solve_run(p, max_iter, m, S(stream));
   });
   m.def("logreg_grad", [](u slab, u R, u col_map, u csc_rows, u csc_off, u col_slice, int SL, u inv_std, u pmask,
                           int64_t N, int F, int Fd, int K, int T, int tstride, int model0, int ntiles, u G, u loss,
@@ -490,7 +606,6 @@ PYBIND11_MODULE(_har_native, m) {
   m.def("head_fused_blocks", &har_head_fused_blocks);
   m.def("mlp_fwd_head_grid", &har_mlp_fwd_head_grid);
   m.def("mlp_set_stamps", [](u p) { har_mlp_set_stamps(P<uint64_t>(p)); });
-  m.def("mlp_set_bwd_variant", [](int v) { har_mlp_set_bwd_variant(v); });
   py::class_<MlpStepPlan>(m, "MlpStepPlan")
       .def(py::init([](py::dict d) {
         MlpStepPlan p;

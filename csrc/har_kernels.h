@@ -90,7 +90,6 @@ int har_mlp_step_slices(int B);
 int har_mlp_step_fwd_slab_width(int H);
 // diagnostic phase stamps of the step kernels (nullptr = off); see mlp_step.hip
 void har_mlp_set_stamps(uint64_t* p);
-void har_mlp_set_bwd_variant(int v);
 // Serving variant of the same kernel: logits [B][C] fp32 + argmax class [B] int32, nothing else.
 int har_mlp_fwd_infer_f32(const float* X, int ldx, int F, int K0, const uint16_t* W0, const float* b0,
                           const uint16_t* W1, const float* b1, int H, const uint16_t* Wo, const float* bo, int B, int C,

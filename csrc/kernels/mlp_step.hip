@@ -38,10 +38,6 @@ using namespace mlpf;
 // (shader clock) at fixed points into its own 40-slot row of that buffer (slots 38 / 39:
 // s_memrealtime at entry / exit, 100 MHz, one clock for the whole chip).  Nothing else reads them.
 uint64_t* g_har_mlp_stamps = nullptr;
-// Scheduling variants (probe A/B, har_mlp_set_bwd_variant): bit 0 = the backend's IGLP small-GEMM
-// interleave in the backward tile, bit 1 = its exp / MFMA interleave in the forward tile
-int g_har_mlp_bwd_ilv = 0;
-int g_har_mlp_fwd_variant = 0;
 
 namespace {
 
@@ -82,7 +78,7 @@ __device__ __forceinline__ bf16x8_t ldx(const bf16_t* __restrict__ X, int row, i
   return *reinterpret_cast<const bf16x8_t*>(X + (size_t)row * K0 + kc * 32 + g * 8);
 }
 
-template <int K0, bool STAMP, bool IGLP>
+template <int K0, bool STAMP>
 __global__ __launch_bounds__(512) void mlp_fwd3_kernel(
     const bf16_t* __restrict__ X, const bf16_t* __restrict__ W0, const float* __restrict__ b0,
     const bf16_t* __restrict__ W1, const float* __restrict__ b1, const bf16_t* __restrict__ Wo,
@@ -296,8 +292,6 @@ __global__ __launch_bounds__(512) void mlp_fwd3_kernel(
       load_x(k + 3);
       if (k == 4) HAR_STAMP(FW, 13)
     }
-    // IGLP: the backend's exp / MFMA interleave strategy over the steady-state body (probe A/B)
-    if constexpr (IGLP) if (!first && !last) __builtin_amdgcn_iglp_opt(2);
     __syncthreads();
   };
   if (nt > 0) iter(0, true, nt == 1);
@@ -360,7 +354,7 @@ template <int K0> struct Bwd3Lds {
   static_assert((size_t)HH * WQP + NCLS * HH <= (size_t)2 * DSM, "prologue images fit the dact2 buffers");
 };
 
-template <int K0, bool STAMP, bool ILV>
+template <int K0, bool STAMP>
 __global__ __launch_bounds__(512) void mlp_bwd3_kernel(
     const uint32_t* __restrict__ dz, const uint32_t* __restrict__ mask, const bf16_t* __restrict__ X,
     const bf16_t* __restrict__ W1, const bf16_t* __restrict__ W0, const float* __restrict__ b0,
@@ -615,8 +609,6 @@ __global__ __launch_bounds__(512) void mlp_bwd3_kernel(
     tile_ab(i);
     if (i == 4) HAR_STAMP(8, 29)
     if (!first) tile_c(i - 1);
-    // ILV: the backend's small-GEMM DS / MFMA interleave over the tile's compute (probe A/B)
-    if constexpr (ILV) if (!first) __builtin_amdgcn_iglp_opt(0);
     if (i == 4) HAR_STAMP(8, 30)
     __syncthreads();                // dact2 i+1 / X i+2 staged, h1 i+1 and dact1 i complete
   };
@@ -663,8 +655,7 @@ template <int K0>
 void launch_fwd3(const bf16_t* X, const bf16_t* W0, const float* b0, const bf16_t* W1, const float* b1,
                  const bf16_t* Wo, const float* bo, const int32_t* labels, int B, int C, float scale, uint32_t* dz,
                  uint32_t* mask, float* slab, float* bl, int32_t* bc, int nwg, hipStream_t s) {
-  auto k = g_har_mlp_fwd_variant ? (g_har_mlp_stamps ? mlp_fwd3_kernel<K0, true, true> : mlp_fwd3_kernel<K0, false, true>)
-                                 : (g_har_mlp_stamps ? mlp_fwd3_kernel<K0, true, false> : mlp_fwd3_kernel<K0, false, false>);
+  auto k = g_har_mlp_stamps ? mlp_fwd3_kernel<K0, true> : mlp_fwd3_kernel<K0, false>;
   k<<<nwg, 512, FWD_LDS, s>>>(X, W0, b0, W1, b1, Wo, bo, labels, B, C, scale, dz, mask, slab, bl, bc, g_har_mlp_stamps);
 }
 
@@ -673,8 +664,7 @@ void launch_bwd3(const uint32_t* dz, const uint32_t* mask, const bf16_t* X, cons
                  const float* b0, const bf16_t* Wo, int B, int S, float* gw1, float* gw0, float* gb0, float* gb1,
                  int64_t stride, int32_t* tick, const float* fslab, int fslab_w, int nfwd, float* gwo, float* gbo,
                  hipStream_t s) {
-  auto k = g_har_mlp_bwd_ilv ? (g_har_mlp_stamps ? mlp_bwd3_kernel<K0, true, true> : mlp_bwd3_kernel<K0, false, true>)
-                             : (g_har_mlp_stamps ? mlp_bwd3_kernel<K0, true, false> : mlp_bwd3_kernel<K0, false, false>);
+  auto k = g_har_mlp_stamps ? mlp_bwd3_kernel<K0, true> : mlp_bwd3_kernel<K0, false>;
   k<<<S * BQ, 512, Bwd3Lds<K0>::bytes, s>>>(dz, mask, X, W1, W0, b0, Wo, B, S, gw1, gw0, gb0, gb1, stride, tick,
                                            fslab, fslab_w, nfwd, gwo, gbo, g_har_mlp_stamps ? g_har_mlp_stamps + STAMP_BWD_OFF : nullptr);
 }
@@ -732,7 +722,3 @@ extern "C" int har_mlp_step_bwd(const uint32_t* dz, const uint32_t* mask, const 
 }
 
 extern "C" void har_mlp_set_stamps(uint64_t* p) { g_har_mlp_stamps = p; }
-extern "C" void har_mlp_set_bwd_variant(int v) {
-  g_har_mlp_bwd_ilv = v & 1;
-  g_har_mlp_fwd_variant = (v >> 1) & 1;  // bit 1: forward variant
-}

@@ -472,32 +472,3 @@ def test_sort_columns_matches_torch_sort(cuda, n, F):
     assert torch.equal(torch.isnan(out), torch.isnan(ref))
     assert torch.equal(torch.nan_to_num(out, nan=0.0), torch.nan_to_num(ref, nan=0.0))
 
-
-@pytest.mark.parametrize("B", [4096, 65536])
-def test_mlp_step_variants_agree(cuda, B):
-    """The step's scheduling variants (mlp_step.hip, har_mlp_set_bwd_variant: the backend's IGLP
-    interleave strategies in the backward / forward tile bodies) run the same arithmetic in the same
-    order: gradients, loss, #correct, dz and the relu' mask are bit-identical to the default."""
-    from har.models.mlp import MLPEngine, pad_input_bf16
-    from har.ops import _native
-
-    mod = _native.kernels()
-    g = torch.Generator(device=cuda).manual_seed(21)
-    X = torch.randn(B, 43, device=cuda, generator=g)
-    y = torch.randint(0, 6, (B,), device=cuda, generator=g).to(torch.int32)
-    out = {}
-    try:
-        for v in (0, 1, 2, 3):
-            mod.mlp_set_bwd_variant(v)
-            e = MLPEngine([43, 256, 256, 6], B, cuda, lr=1e-3, seed=7)
-            Xb = pad_input_bf16(X, e.layout.in_pad)
-            e.forward_backward_native(Xb, y, 1.0 / B)
-            e.reduce_grads_native()
-            torch.cuda.synchronize()
-            assert e.last_path == "step"
-            out[v] = (e.G.clone(), e.last_loss_and_correct(), e.dz.clone(), e.h2mask.clone())
-    finally:
-        mod.mlp_set_bwd_variant(0)
-    for v in (1, 2, 3):
-        assert torch.equal(out[v][0], out[0][0]) and out[v][1] == out[0][1], v
-        assert torch.equal(out[v][2], out[0][2]) and torch.equal(out[v][3], out[0][3]), v

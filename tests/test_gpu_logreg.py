@@ -108,6 +108,25 @@ def test_device_fit_is_bitwise_deterministic(cuda):
         assert torch.equal(m1.interceptVector, m2.interceptVector)
 
 
+def test_native_solve_plan_equals_python_loop(cuda, monkeypatch):
+    """The whole-solve native call (bind.cpp logreg_solve) enqueues the launch sequence of the Python
+    loop in DeviceLogregSolver.solve: bit-identical coefficients, objectives and histories."""
+    from har.models.logreg import FitSpec, LogisticRegression
+
+    _, y, hm = _hybrid_problem(cuda, N=3000, seed=8)
+    est = LogisticRegression(maxIter=20, regParam=0.1)
+    specs = [FitSpec(None, 0.1, 0.0), FitSpec(None, 0.3, 0.1)]
+    out = []
+    for flag in ("1", "0"):
+        monkeypatch.setenv("HAR_LR_NATIVE_SOLVE", flag)
+        out.append(est.fit_many(hm, y.to(cuda), specs, 6))
+    for m1, m2 in zip(*out):
+        assert torch.equal(m1.coefficientMatrix, m2.coefficientMatrix)
+        assert torch.equal(m1.interceptVector, m2.interceptVector)
+        assert m1.summary["objective"] == m2.summary["objective"]
+        assert m1.summary["objectiveHistory"] == m2.summary["objectiveHistory"]
+
+
 def test_wisdm_reference_lr_and_cv_on_device(cuda, wisdm_csv):
     from har.data.csv_io import read_csv
     from har.data.split import random_split

@@ -111,8 +111,6 @@ def stamps(B=65536):
 
 def main():
     dev = torch.device("cuda")
-    # backward scheduling variant under test (HAR_BWD_VARIANT, csrc/kernels/mlp_step.hip)
-    _native.kernels().mlp_set_bwd_variant(int(os.environ.get("HAR_BWD_VARIANT", "0")))
     if sys.argv[1:2] == ["--stamps"]:
         return stamps(int(sys.argv[2]) if len(sys.argv) > 2 else 65536)
     sizes = [int(a) for a in sys.argv[1:]] or [16384, 32768, 65536, 131072, 262144]
