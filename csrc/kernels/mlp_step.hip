@@ -121,6 +121,9 @@ __global__ __launch_bounds__(512) void mlp_fwd3_kernel(
   // first X tile and its labels, THEN W1 / Wout / b1 (the bulk: 16 KB per wave, L2-bandwidth-bound
   // with every CU fetching it at once), so stage 1 of tile 0 waits only for what it reads ----
   bf16x8_t w0f[2][K0C], w1f[2][KC];
+  // k-chunk rotation per workgroup: every CU fetches all of W1 at once in the prologue, and a
+  // common order makes them request the same lines together; register kc holds chunk (kc + krot)
+  const int krot = (int)blockIdx.x & (KC - 1);
   float4 b0r[2], b1r[2];
 #pragma unroll
   for (int t = 0; t < 2; ++t) {
@@ -139,7 +142,7 @@ __global__ __launch_bounds__(512) void mlp_fwd3_kernel(
   for (int t = 0; t < 2; ++t) {
 #pragma unroll
     for (int kc = 0; kc < KC; ++kc)
-      w1f[t][kc] = *reinterpret_cast<const bf16x8_t*>(W1 + (size_t)(u0 + 16 * t + c16) * HH + kc * 32 + g * 8);
+      w1f[t][kc] = *reinterpret_cast<const bf16x8_t*>(W1 + (size_t)(u0 + 16 * t + c16) * HH + ((kc + krot) & (KC - 1)) * 32 + g * 8);
     b1r[t] = *reinterpret_cast<const float4*>(b1 + u0 + 16 * t + 4 * g);
   }
   // stage-3 A fragment: Wout[class c16][u0 + 4g + j] (j < 4), [u0 + 16 + 4g + j - 4] (j >= 4): the k
@@ -180,7 +183,7 @@ __global__ __launch_bounds__(512) void mlp_fwd3_kernel(
       bf16x8_t hb[2];
 #pragma unroll
       for (int h = 0; h < 2; ++h)
-        hb[h] = *reinterpret_cast<const bf16x8_t*>(hsrc + (16 * h + c16) * FHP + ((kc * 32 + 8 * g) ^ hsw));
+        hb[h] = *reinterpret_cast<const bf16x8_t*>(hsrc + (16 * h + c16) * FHP + ((((kc + krot) & (KC - 1)) * 32 + 8 * g) ^ hsw));
 #pragma unroll
       for (int h = 0; h < 2; ++h)
 #pragma unroll
@@ -397,7 +400,9 @@ __global__ __launch_bounds__(512) void mlp_bwd3_kernel(
   bf16_t* const wq = lds;                  // [256 j][WQP]: W1[j][qu0 .. qu0 + 64)
   bf16_t* const wos = wq + HH * WQP;       // [16][256] Wout
 #pragma unroll
-  for (int v = tid; v < HH * (BQU / 8); v += 512) {  // every load issued before the first LDS store
+  for (int v0 = tid; v0 < HH * (BQU / 8); v0 += 512) {  // every load issued before the first LDS store
+    // rotated by slice: the 64 workgroups of a quadrant do not request the same lines together
+    const int v = (v0 + 512 * slice) & (HH * (BQU / 8) - 1);
     const int j = v / (BQU / 8), c = (v % (BQU / 8)) * 8;
     *reinterpret_cast<uint4*>(wq + j * WQP + c) = *reinterpret_cast<const uint4*>(W1 + (size_t)j * HH + qu0 + c);
   }
