@@ -127,9 +127,10 @@ def bench_mlp(args, ctx):
         j = i % nb
         eng.train_step(Xin[j * B:(j + 1) * B], y32[j * B:(j + 1) * B], global_batch)
 
-    # default eager: the three-kernel step is GPU-bound (round 2 on MI355X, 200 steps: eager
-    # 0.0821 / 0.0825 ms, whole-step graph 0.0860 / 0.0872 ms, segmented graphs 0.0930 ms), and in
-    # DP the one flat all-reduce sits between the reduction and Adam kernels
+    # default eager at every N: the three-kernel step is GPU-bound; graph modes measured slower at
+    # N = 1 (profiles/r3/bench_graph_modes.md: eager 0.0740-0.0757, whole-step 0.0801, segmented 0.0884,
+    # one graph per 8-step cycle 0.0757 ms), and in DP the one flat all-reduce sits between the
+    # reduction and Adam kernels
     mode = args.graph if args.graph >= 0 else 0
     graphs = None
     if eng.native and mode == 1:  # whole step (collective included) in one graph per slot
@@ -152,6 +153,9 @@ def bench_mlp(args, ctx):
             gB.replay()
     else:
         run = step
+    # the untimed WISDM accuracy run (a separate engine) goes first: the timed steps then start on a
+    # GPU already out of its idle power state instead of ramping its clock inside a 20-step window
+    extras = wisdm_accuracy_fields(args, ctx, hidden=(args.hidden, args.hidden))
     elapsed = timed(ctx, run, args.steps, args.warmup, dev)
     phases = mlp_phase_times(ctx, eng, Xin, y32, B, nb, global_batch, n=max(10, min(50, args.steps)))
     Xt, yt = synthetic_windows(65536, seed=999, device=dev)
@@ -167,7 +171,7 @@ def bench_mlp(args, ctx):
            "hip_graph": {0: "off", 1: "whole-step", 2: "segmented"}[mode if graphs else 0],
            "collectives_per_step": eng.collective_stats() if hasattr(eng, "collective_stats") else None,
            "phase_ms": phases}
-    rec.update(wisdm_accuracy_fields(args, ctx, hidden=(args.hidden, args.hidden)))
+    rec.update(extras)
     return rec
 
 
@@ -226,7 +230,7 @@ def wisdm_accuracy_fields(args, ctx, hidden):
     return {"test_accuracy": r["accuracy"], "test_accuracy_data": "WISDM v1.1 transformed table, "
             f"{r['encoding']}, {r['split']}: {r['n_train']} train / {r['n_test']} test windows; same MLP "
             f"architecture ({'-'.join(map(str, r['layers']))}), {r['epochs']} epochs of batch {r['batch']}, "
-            "trained after the timed steps", "wisdm_mlp_fit_s": r["fit_s"]}
+            "a separate engine trained before the timed steps (untimed)", "wisdm_mlp_fit_s": r["fit_s"]}
 
 
 def bench_reference(args, ctx):
@@ -511,8 +515,9 @@ def main():
     ap.add_argument("--hidden", type=int, default=256)
     ap.add_argument("--lr", type=float, default=1e-3)
     ap.add_argument("--graph", type=int, default=-1,
-                    help="HIP graphs for the MLP step: 0 eager (default; DP overlaps the bucketed all-reduce with "
-                         "backward), 1 whole step in one graph, 2 graphs around an eager RCCL all-reduce")
+                    help="HIP graphs for the MLP step: 0 eager (default; in DP one flat all-reduce per step between "
+                         "the reduction and Adam kernels), 1 whole step in one graph per batch slot, 2 graphs around "
+                         "an eager RCCL all-reduce")
     ap.add_argument("--rows", type=int, default=60000, help="windows per GPU (forest configs)")
     ap.add_argument("--trees", type=int, default=0)
     ap.add_argument("--depth", type=int, default=10)
