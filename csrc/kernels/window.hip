@@ -495,10 +495,41 @@ __device__ __forceinline__ T greduce(T v, Op op, const mlpf::LaneSwap& sw) {
   return v;
 }
 
-// bin of a sample: fma instead of (x - lo) * scale (a boundary sample may move by one bin, within
-// the 1/W the tests allow), clamped in float (med3) so the conversion never sees a negative
-__device__ __forceinline__ uint32_t bin_of(float x, float sc, float off) {
-  return (uint32_t)__builtin_amdgcn_fmed3f(fmaf(x, sc, off), 0.f, (float)(NB - 1));
+// min / max as one v_min_f32 / v_max_f32: fminf / fmaxf make hipcc quiet BOTH operands first in
+// IEEE mode (a v_max_f32 x, x each, also on the running accumulator across the guarded k-steps:
+// 6 VALU per sample and axis for min + max instead of 2; fmed3 with an infinity folds back to that);
+// the samples are finite sensor data
+__device__ __forceinline__ float vmin(float a, float b) {
+  float r;
+  asm("v_min_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ float vmax(float a, float b) {
+  float r;
+  asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+
+// One sample's peak flags into the two shift registers: R = 2R + (x > prev), PT = 2PT + (x > prev &&
+// x > thr), as two compares into SGPR masks and two v_addc (R + R + carry); written by hipcc it is a
+// v_cndmask + v_lshl_or per flag
+__device__ __forceinline__ void flag_step(uint32_t& R, uint32_t& PT, float x, float prev, float thr) {
+  uint64_t m1, m2, cc;
+  asm("v_cmp_gt_f32_e64 %[m1], %[x], %[p]\n\t"
+      "v_cmp_gt_f32_e64 %[m2], %[x], %[t]\n\t"
+      "s_and_b64 %[m2], %[m1], %[m2]\n\t"
+      "v_addc_co_u32_e64 %[R], %[cc], %[R], %[R], %[m1]\n\t"
+      "v_addc_co_u32_e64 %[PT], %[cc], %[PT], %[PT], %[m2]"
+      : [R] "+v"(R), [PT] "+v"(PT), [m1] "=&s"(m1), [m2] "=&s"(m2), [cc] "=&s"(cc)
+      : [x] "v"(x), [p] "v"(prev), [t] "v"(thr)
+      : "scc");
+}
+
+// bin of a sample: (x - lo) * (10 / range) in fp32, the legacy kernel's arithmetic (x >= lo, so the
+// conversion never sees a negative), clamped to bin 9
+__device__ __forceinline__ uint32_t bin_of(float x, float sc, float lo) {
+  const uint32_t b = (uint32_t)((x - lo) * sc);
+  return b < (uint32_t)(NB - 1) ? b : (uint32_t)(NB - 1);
 }
 
 template <int A, int LPW, bool MLP>
@@ -579,7 +610,7 @@ __global__ __launch_bounds__(256) void window_features_reg_kernel(const float* _
 #pragma unroll
         for (int c = 0; c < 3; ++c) {
           const float v = x[c][k];
-          s[c] += v; q[c] = fmaf(v, v, q[c]); lo[c] = fminf(lo[c], v); hi[c] = fmaxf(hi[c], v);
+          s[c] += v; q[c] = fmaf(v, v, q[c]); lo[c] = vmin(lo[c], v); hi[c] = vmax(hi[c], v);
         }
       }
 #pragma unroll
@@ -587,8 +618,8 @@ __global__ __launch_bounds__(256) void window_features_reg_kernel(const float* _
       const float S = greduce<LPW, float>(s[c], [](float a, float b) { return a + b; }, sw) - D * xl[c];
       const float Q = greduce<LPW, float>(q[c], [](float a, float b) { return a + b; }, sw) - D * xl[c] * xl[c];
       mean[c] = S * invW; en[c] = Q * invW;
-      mn[c] = greduce<LPW, float>(lo[c], [](float a, float b) { return fminf(a, b); }, sw);
-      mx[c] = greduce<LPW, float>(hi[c], [](float a, float b) { return fmaxf(a, b); }, sw);
+      mn[c] = greduce<LPW, float>(lo[c], [](float a, float b) { return vmin(a, b); }, sw);
+      mx[c] = greduce<LPW, float>(hi[c], [](float a, float b) { return vmax(a, b); }, sw);
     }
   }
 
@@ -598,7 +629,7 @@ __global__ __launch_bounds__(256) void window_features_reg_kernel(const float* _
   for (int c = 0; c < 3; ++c) {
     const float range = mx[c] - mn[c];
     sc[c] = range > 0.f ? (float)NB / range : 0.f;
-    off[c] = -mn[c] * sc[c];
+    off[c] = mn[c];  // bin_of's lo
     thr[c] = mean[c] + 0.5f * (mx[c] - mean[c]);
   }
   float ad[3] = {0.f, 0.f, 0.f}, v2[3] = {0.f, 0.f, 0.f}, res = 0.f, cxy = 0.f, cxz = 0.f, cyz = 0.f;
@@ -616,9 +647,7 @@ __global__ __launch_bounds__(256) void window_features_reg_kernel(const float* _
         ad[c] += fabsf(dc);
         v2[c] = fmaf(dc, dc, v2[c]);
         h[c] += 1ull << __umul24(bin_of(xv, sc[c], off[c]), 6u);  // v_mul_u32_u24, not the quarter-rate mul_lo
-        const bool r = xv > pv;
-        R[c] = (R[c] << 1) + (r ? 1u : 0u);
-        PT[c] = (PT[c] << 1) + ((r && xv > thr[c]) ? 1u : 0u);
+        flag_step(R[c], PT[c], xv, pv, thr[c]);
       }
       res += __builtin_amdgcn_sqrtf(fmaf(x[0][k], x[0][k], fmaf(x[1][k], x[1][k], x[2][k] * x[2][k])));
       cxy = fmaf(d[0], d[1], cxy);
