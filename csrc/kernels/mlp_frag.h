@@ -94,12 +94,19 @@ __device__ __forceinline__ float dpp_f(float v) {
 constexpr int DPP_ROR8 = 0x128, DPP_ROR4 = 0x124, DPP_ROR2 = 0x122, DPP_ROR1 = 0x121;  // row_ror:n (16-lane rows)
 constexpr int DPP_QUAD_XOR1 = 0xb1;                                                // quad_perm [1,0,3,2]
 
+// max as one v_max_f32: fmaxf of a DPP-moved value makes hipcc quiet both operands first (IEEE mode),
+// two extra VALU per step on the softmax's dependent chain
+__device__ __forceinline__ float vmaxf(float a, float b) {
+  float r;
+  asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
 // all-reduce over the 16 lanes of each DPP row (lanes 16r .. 16r + 15)
 __device__ __forceinline__ float row16_max(float v) {
-  v = fmaxf(v, dpp_f<DPP_ROR8>(v));
-  v = fmaxf(v, dpp_f<DPP_ROR4>(v));
-  v = fmaxf(v, dpp_f<DPP_ROR2>(v));
-  return fmaxf(v, dpp_f<DPP_ROR1>(v));
+  v = vmaxf(v, dpp_f<DPP_ROR8>(v));
+  v = vmaxf(v, dpp_f<DPP_ROR4>(v));
+  v = vmaxf(v, dpp_f<DPP_ROR2>(v));
+  return vmaxf(v, dpp_f<DPP_ROR1>(v));
 }
 __device__ __forceinline__ float row16_sum(float v) {
   v += dpp_f<DPP_ROR8>(v);
