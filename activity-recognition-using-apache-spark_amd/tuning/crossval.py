@@ -126,6 +126,7 @@ class CrossValidator(Estimator):
         metrics = np.zeros((len(maps), k), dtype=np.float64)
         from ..models.logreg import FitSpec, LogisticRegression
 
+        batch_refit = False
         if isinstance(est, LogisticRegression):
             from ..features.hybrid import hybrid_features
 
@@ -142,12 +143,23 @@ class CrossValidator(Estimator):
                 for f in range(k):
                     specs.append(FitSpec(train_w[f], sub.regParam, sub.elasticNetParam))
                     index.append((mi, f))
+            # the refit of every candidate on the full data rides along in the same batched solve
+            # (one more model per param map): the final model is then the winner's full-data fit,
+            # with no separate fit after the selection — the same model Spark's refit produces
+            n_cv = len(specs)
+            batch_refit = not est.weightCol and all(set(pm) <= {"regParam", "elasticNetParam"} for pm in maps)
+            if batch_refit:
+                for pm in maps:
+                    sub = est.copy(pm)
+                    specs.append(FitSpec(None, sub.regParam, sub.elasticNetParam))
             # maxIter / tol / family etc. may differ per map only through regParam/elasticNetParam
             base = est.copy(maps[0]) if maps else est
-            lo, hi = dp_rows(hm.n_rows)  # data parallel: all 45 fits on this rank's row shard
+            lo, hi = dp_rows(hm.n_rows)  # data parallel: every fit on this rank's row shard
             if dp_context() is not None:
-                specs = [FitSpec(s.row_weight[lo:hi], s.regParam, s.elasticNetParam) for s in specs]
-            models = base.fit_many(hm.rows(lo, hi), y[lo:hi], specs, K, allreduce=dp_allreduce())
+                specs = [FitSpec(None if s.row_weight is None else s.row_weight[lo:hi], s.regParam, s.elasticNetParam)
+                         for s in specs]
+            models_all = base.fit_many(hm.rows(lo, hi), y[lo:hi], specs, K, allreduce=dp_allreduce())
+            models, refits = models_all[:n_cv], models_all[n_cv:]
             # every (map, fold) model scored on its validation fold in ONE batched pass
             raw = _lr_margins(models, hm)                                          # [n, N, K]
             pred = _batched_predictions(models, raw)
@@ -175,7 +187,11 @@ class CrossValidator(Estimator):
                     metrics[mi, f] = ev.evaluate(m.transform(va))
         avg = metrics.mean(axis=1)
         best = int(np.argmax(avg) if ev.isLargerBetter() else np.argmin(avg))
-        best_model = est.copy(maps[best]).fit(table)
+        if isinstance(est, LogisticRegression) and batch_refit:
+            best_model = refits[best]
+            best_model.uid = est.uid
+        else:
+            best_model = est.copy(maps[best]).fit(table)
         return CrossValidatorModel(best_model, avg.tolist(), best)
 
 
