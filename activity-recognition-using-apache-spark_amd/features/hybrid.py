@@ -39,8 +39,15 @@ class HybridMatrix:
         return self.dense.device
 
     def rows(self, lo: int, hi: int) -> "HybridMatrix":
-        return HybridMatrix(self.dense[lo:hi].contiguous(), self.dense_cols, self.cat[lo:hi].contiguous(),
-                            self.blocks, self.n_features)
+        """Rows [lo, hi) — memoized per range (the matrix is immutable), so a fit's derived device
+        index (the CSC row lists cached on the matrix) is built once per shard, not once per fit."""
+        if lo == 0 and hi == self.n_rows:
+            return self
+        memo = self.__dict__.setdefault("_row_shards", {})
+        if (lo, hi) not in memo:
+            memo[(lo, hi)] = HybridMatrix(self.dense[lo:hi].contiguous(), self.dense_cols,
+                                          self.cat[lo:hi].contiguous(), self.blocks, self.n_features)
+        return memo[(lo, hi)]
 
     def take(self, idx: torch.Tensor) -> "HybridMatrix":
         return HybridMatrix(self.dense[idx].contiguous(), self.dense_cols, self.cat[idx].contiguous(), self.blocks,

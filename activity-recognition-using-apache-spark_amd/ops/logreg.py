@@ -260,7 +260,7 @@ class DeviceLogregSolver:
                  ("step_scale", (B,), f32), ("active", (B,), i32), ("fails", (B,), i32), ("iters", (B,), i32),
                  ("steep", (B,), i32), ("pick", (B,), i32), ("P1", (B, self.nch, 2 * 10 + 1), f64),
                  ("P2", (B, self.nch, 3 * 4 + 2), f64), ("P3", (B, self.nch, 5 + 3 * 10), f64),
-                 ("hist", (max_iter + 1, B), f64),
+                 ("hist", (max_iter + 1, B), f64), ("done", (B,), i32),
                  ("slab", (BT, max(1, self.ntiles), design.Fd * KP + KP + 1), f32)]
         if design.C:
             specs.append(("R", (self.rchunk, N, KP), f32))
@@ -273,29 +273,27 @@ class DeviceLogregSolver:
         self.active.fill_(1)
         self.n_evals = 0
 
-    def _args(self, init: int = 0, head: int = 0, filled: int = 0, fin: int = 0, fin_init: int = 0,
-              fin_head: int = 0, fin_it: int = 0):
+    def _args(self, init: int = 0, head: int = 0, filled: int = 0, fin_it: int = 0):
         # the buffers never move during a solve: their pointers are read once (~40 data_ptr calls per
         # launch were most of the host time of a 20-iteration fit), only the iteration scalars change
         base = getattr(self, "_arg_base", None)
         if base is None:
             base = self._arg_base = self._pointer_args()
         a = dict(base)
-        a.update(head=head, filled=filled, init=init, fin=fin, fin_init=fin_init, fin_head=fin_head, fin_it=fin_it)
+        a.update(head=head, filled=filled, init=init, fin_it=fin_it)
         return a
 
     def _pointer_args(self):
         p = lambda t: 0 if t is None else t.data_ptr()  # noqa: E731
         return {"B": self.B, "T": self.T, "K": self.d.K, "F": self.d.F, "m": self.m, "head": 0,
-                "filled": 0, "init": 0, "nch": self.nch, "fin": 0, "fin_init": 0,
-                "fin_head": 0, "fin_it": 0, "D": self.D, "x": p(self.x), "g": p(self.g),
+                "filled": 0, "init": 0, "nch": self.nch, "fin_it": 0, "D": self.D, "x": p(self.x), "g": p(self.g),
                 "fobj": p(self.fobj), "l1": p(self.l1v), "l2": p(self.l2v), "pmask": p(self.pmask),
                 "inv_std": p(self.inv_std), "S": p(self.S), "Y": p(self.Y), "rho": p(self.rho),
                 "SY": p(self.SY), "YY": p(self.YY), "P1": p(self.P1), "P2": p(self.P2), "P3": p(self.P3),
                 "xtrial": p(self.xtrial), "weff": p(self.weff), "reg": p(self.reg), "decr": p(self.decr),
                 "G": p(self.G), "loss": p(self.loss), "step_scale": p(self.step_scale), "active": p(self.active),
                 "fails": p(self.fails), "iters": p(self.iters), "steep": p(self.steep), "pick": p(self.pick),
-                "hist": p(self.hist), "c1": float(self.c1), "tol": float(self.tol)}
+                "hist": p(self.hist), "done": p(self.done), "c1": float(self.c1), "tol": float(self.tol)}
 
     def _eval_args(self, tstride: int):
         """Per launch chunk: positional arguments (but the stream) of the evaluate + gradient
@@ -336,18 +334,20 @@ class DeviceLogregSolver:
         self.n_evals += 1
 
     def solve(self, x0: torch.Tensor, poll: int = 0):
-        """Per iteration: phase 0 (finalize the previous update + history dots), phase 1 (direction
-        + T trial points), evaluate + gradient of the B*T trials, phase 2 (pick + history).  The
-        host polls ``active`` (one sync) every ``poll`` iterations only."""
+        """Per iteration: phase 1 (direction + T trial points), evaluate + gradient of the B*T
+        trials, phase 2 (pick + history + the next direction's dots; each model's last chunk
+        finalizes it on the device).  The host polls ``active`` (one sync) every ``poll``
+        iterations only."""
         mod, s, KP = _native.kernels(), _native.stream_ptr(), self.d.KP
         qa = getattr(self, "_qn_args", None)
         if qa is None:  # pointers / shapes converted once; a launch passes only the iteration scalars
             qa = self._qn_args = mod.qn_args(self._args())
 
-        def phase(ph, head=0, filled=0, init=0, fin=0, fin_init=0, fin_head=0, fin_it=0):
-            mod.lbfgs_phase_h(qa, ph, head, filled, init, fin, fin_init, fin_head, fin_it, KP, s)
+        def phase(ph, head=0, filled=0, init=0, fin_it=0):
+            mod.lbfgs_phase_h(qa, ph, head, filled, init, fin_it, KP, s)
 
         self.x.copy_(x0.reshape(self.B, self.D))
+        self.hist_rows = self.max_iter + 1
         if not poll and self.allreduce is None and os.environ.get("HAR_LR_NATIVE_SOLVE", "1") != "0":
             # the fixed launch sequence below as ONE native call (bind.cpp logreg_solve): no
             # convergence poll and no collective, so nothing needs the host between launches
@@ -357,29 +357,20 @@ class DeviceLogregSolver:
                 plan = self._solve_plan = mod.logreg_solve_plan(qa, chunks(self.T), chunks(1), KP)
             mod.logreg_solve(plan, self.max_iter, self.m, s)
             self.n_evals += 1 + self.max_iter
-            self.hist_rows = self.max_iter + 1
             return self.x, self.fobj, self.iters
         phase(1, init=1)
         self._evaluate(self.T)
         phase(2, init=1)
         head = filled = 0
-        prev = -1  # history slot written by the previous phase 2 (-1: the init update)
-        finalized = False
         for it in range(self.max_iter):
-            phase(0, head, filled, fin=1, fin_init=int(prev < 0), fin_head=max(prev, 0), fin_it=it)
             if poll and it and it % poll == 0 and not bool(self.active.any()):
-                finalized = True
                 self.hist_rows = it + 1
                 break
             phase(1, head, filled)
             self._evaluate(1)
-            phase(2, head, filled)
-            prev = head
+            phase(2, head, filled, fin_it=it + 1)
             head = (head + 1) % self.m
             filled = min(filled + 1, self.m)
-        if not finalized:
-            phase(3, fin=1, fin_init=int(prev < 0), fin_head=max(prev, 0), fin_it=self.max_iter)
-            self.hist_rows = self.max_iter + 1
         return self.x, self.fobj, self.iters
 
     def history(self, b: int, hist_host=None):

@@ -176,7 +176,7 @@ def run_reference_suite(dev, path: str, models: Sequence[str] = ("lr", "lrcv", "
         best = model.bestModel if hasattr(model, "bestModel") else model
         device_sync(dev)
         t0 = time.perf_counter()
-        pred = best.predict(X_test)
+        pred = best.predict(best.features_input(test) if hasattr(best, "features_input") else X_test)
         device_sync(dev)
         pred_s = time.perf_counter() - t0
         acc = float((pred.to(y_test.device) == y_test).float().mean())

@@ -113,10 +113,6 @@ static QnArgs qn_args_from_dict(py::dict d) {
   a.filled = (int)I("filled");
   a.init = (int)I("init");
   a.nch = (int)I("nch");
-  a.fin = (int)I("fin");
-  a.fin_only = 0;
-  a.fin_init = (int)I("fin_init");
-  a.fin_head = (int)I("fin_head");
   a.fin_it = (int)I("fin_it");
   a.D = I("D");
   a.x = P<float>(U("x"));
@@ -147,6 +143,7 @@ static QnArgs qn_args_from_dict(py::dict d) {
   a.steep = P<int32_t>(U("steep"));
   a.pick = P<int32_t>(U("pick"));
   a.hist = P<double>(U("hist"));
+  a.done = P<int32_t>(U("done"));
   a.c1 = d["c1"].cast<double>();
   a.tol = d["tol"].cast<double>();
   return a;
@@ -177,15 +174,11 @@ struct LogregSolvePlan {
 };
 
 static void logreg_solve_run(const LogregSolvePlan& p, int max_iter, int m, hipStream_t s) {
-  auto phase = [&](int ph, int head, int filled, int init, int fin, int fin_init, int fin_head, int fin_it) {
+  auto phase = [&](int ph, int head, int filled, int init, int fin_it) {
     QnArgs a = p.q;
     a.head = head;
     a.filled = filled;
     a.init = init;
-    a.fin = fin;
-    a.fin_only = 0;
-    a.fin_init = fin_init;
-    a.fin_head = fin_head;
     a.fin_it = fin_it;
     check(har_lbfgs_phase(&a, p.KP, ph, s), "lbfgs_phase");
   };
@@ -195,20 +188,17 @@ static void logreg_solve_run(const LogregSolvePlan& p, int max_iter, int m, hipS
       check(har_logreg_grad(&c.gr, c.KP, c.n_models, s), "logreg_grad");
     }
   };
-  phase(1, 0, 0, 1, 0, 0, 0, 0);
+  phase(1, 0, 0, 1, 0);
   evaluate(p.evT);
-  phase(2, 0, 0, 1, 0, 0, 0, 0);
-  int head = 0, filled = 0, prev = -1;
+  phase(2, 0, 0, 1, 0);
+  int head = 0, filled = 0;
   for (int it = 0; it < max_iter; ++it) {
-    phase(0, head, filled, 0, 1, prev < 0 ? 1 : 0, prev > 0 ? prev : 0, it);
-    phase(1, head, filled, 0, 0, 0, 0, 0);
+    phase(1, head, filled, 0, 0);
     evaluate(p.ev1);
-    phase(2, head, filled, 0, 0, 0, 0, 0);
-    prev = head;
+    phase(2, head, filled, 0, it + 1);
     head = (head + 1) % m;
     filled = filled + 1 < m ? filled + 1 : m;
   }
-  phase(3, 0, 0, 0, 1, prev < 0 ? 1 : 0, prev > 0 ? prev : 0, max_iter);
 }
 
 // The flagship MLP training step as ONE host call: the buffers of an engine never move, so their
@@ -454,8 +444,9 @@ PYBIND11_MODULE(_har_native, m) {
   m.def("logreg_loss_decode", [](u fx, u loss, int n, u stream) {
     check(har_logreg_loss_decode(P<const float>(fx), P<double>(loss), n, S(stream)), "logreg_loss_decode");
   });
-  // one L-BFGS phase (logreg_qn.hip: 0 finalize + dots, 1 direction + trials, 2 pick + history,
-  // 3 finalize only); the QnArgs fields come from a dict of ints / floats / device pointers
+  // one L-BFGS phase (logreg_qn.hip: 1 direction + trials, 2 pick + history + the next direction's
+  // dots, finalized by the model's last chunk); the QnArgs fields come from a dict of ints / floats /
+  // device pointers
   m.def("qn_chunks", &har_qn_chunks);
   m.def("lbfgs_phase", [](int phase, py::dict d, int KP, u stream) {
     QnArgs a = qn_args_from_dict(d);
@@ -463,16 +454,12 @@ PYBIND11_MODULE(_har_native, m) {
   });
   py::class_<QnArgsHolder>(m, "QnArgs");
   m.def("qn_args", [](py::dict d) { return QnArgsHolder{qn_args_from_dict(d)}; });
-  m.def("lbfgs_phase_h", [](const QnArgsHolder& h, int phase, int head, int filled, int init, int fin, int fin_init,
-                            int fin_head, int fin_it, int KP, u stream) {
+  m.def("lbfgs_phase_h", [](const QnArgsHolder& h, int phase, int head, int filled, int init, int fin_it, int KP,
+                            u stream) {
     QnArgs a = h.a;
     a.head = head;
     a.filled = filled;
     a.init = init;
-    a.fin = fin;
-    a.fin_only = 0;
-    a.fin_init = fin_init;
-    a.fin_head = fin_head;
     a.fin_it = fin_it;
     check(har_lbfgs_phase(&a, KP, phase, S(stream)), "lbfgs_phase");
   });

@@ -193,7 +193,7 @@ typedef struct LogregGradArgs {
 
 typedef struct QnArgs {
   int B, T, K, F, m, head, filled, init, nch;
-  int fin, fin_only, fin_init, fin_head, fin_it;  // phase 0 / 3: finalize the previous phase 2
+  int fin_it;               // phase 2: hist row of the objective it leaves (0 for the init update)
   int64_t D;                // K * (F + 1)
   float* x;                 // [B][D] standardized parameters
   float* g;                 // [B][D] smooth gradient at x
@@ -207,7 +207,7 @@ typedef struct QnArgs {
   double* rho;              // [m][B] (0 = empty / rejected slot)
   double* SY;               // [B][m][m] history Gram matrix s_i . y_j
   double* YY;               // [B][m][m] history Gram matrix y_i . y_j
-  double* P1;               // [B][nch][2m+1] chunk partials (phase 0)
+  double* P1;               // [B][nch][2m+1] chunk partials of the next direction's dots (phase 2)
   double* P2;               // [B][nch][3T+2] chunk partials (phase 1)
   double* P3;               // [B][nch][5+3m] chunk partials (phase 2)
   float* xtrial;            // [B*T][D]
@@ -223,6 +223,7 @@ typedef struct QnArgs {
   int32_t* steep;           // [B] steepest descent this iteration (the last direction was not descent)
   int32_t* pick;            // [B] trial taken by the last phase 2 (-1 none, -2 non-descent)
   double* hist;             // [max_iter + 1][B] objective per iteration (nullable)
+  int32_t* done;            // [B] phase-2 chunks done (zeroed; the last chunk resets it)
   double c1, tol;
 } QnArgs;
 

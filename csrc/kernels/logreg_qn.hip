@@ -341,19 +341,22 @@ __global__ __launch_bounds__(1024) void logreg_col_slices_kernel(const int32_t* 
 // Gram matrices SY[i][j] = s_i.y_j and YY[i][j] = y_i.y_j (maintained as pairs enter), so a
 // direction costs two streaming sweeps instead of 4m dependent ones.
 //
-//   phase 0  (chunks x B)  lane 0 of chunk 0 finalizes the previous update of its model (Gram
-//                          rows of the new pair, rho, objective, convergence / failure flags);
-//                          every chunk: pg and the partial dots s_j.pg, y_j.pg, pg.pg -> P1
 //   phase 1  (chunks x B)  reduce P1 -> recursion coefficients (lane 0) -> per element
 //                          d = -(gamma pg + sum cY_j y_j + cS_j s_j) (orthant-restricted), the T
 //                          trial points x + a0 2^-t d and their W_eff; partial reg / decrease /
 //                          pg.d -> P2
-//   (logreg_eval + logreg_grad evaluate the B*T trial models)
+//   (logreg_eval + logreg_grad evaluate the B*T trials)
 //   phase 2  (chunks x B)  reduce P2 -> pick the largest Armijo-satisfying trial (or reject a
 //                          non-descent direction: steepest descent next iteration) -> per element
 //                          s, y into the history slot, x, g; partial dots of the new pair with
-//                          every slot -> P3
-//   phase 3  (B)           finalize only (after the last iteration)
+//                          every slot -> P3, and the NEXT direction's dots s_j.pg, y_j.pg, pg.pg
+//                          (new pg, new pair in its slot) -> P1.  The last chunk of a model to
+//                          finish (a device-scope counter: release fence + atomic, no spinning)
+//                          finalizes the model: Gram rows of the new pair, rho, objective,
+//                          convergence / failure flags.  A rejected step (no trial taken) changes
+//                          neither x, g nor the history, so the P1 of the previous update stays
+//                          exact.  Two launches per iteration between the evaluations, no
+//                          separate dots / finalize pass.
 // ---------------------------------------------------------------------------------------------
 constexpr int QN_BLOCK = 256;
 constexpr int QN_MAX_TRIALS = 4;
@@ -405,6 +408,28 @@ __device__ __forceinline__ void store_partial(double (&v)[NV], double* P) {
   }
 }
 
+// The phase-2 chunk partials cross workgroups inside the kernel (the model's last chunk reduces
+// them): agent-scope stores / loads (write-through, coherent across the XCDs' L2s) instead of a
+// device-scope release fence, whose L2 write-back of every dirty line cost more than the pass it saves
+template <int NV>
+__device__ __forceinline__ void store_partial_agent(const double (&v)[NV], double* P) {
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int q = 0; q < NV; ++q) __hip_atomic_store(P + q, v[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+template <int NV>
+__device__ __forceinline__ void reduce_chunks_agent(const double* P, int nch, double* vs) {
+  const int q = threadIdx.x;
+  if (q < NV) {
+    double t = 0.0;
+#pragma unroll 8
+    for (int c = 0; c < nch; ++c) t += __hip_atomic_load(P + c * NV + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    vs[q] = t;
+  }
+}
+
 __device__ __forceinline__ float pseudo_grad(float x, float g, float l1) {
   if (l1 == 0.f) return g;
   const float gp = g + l1, gm = g - l1;
@@ -415,17 +440,18 @@ __device__ __forceinline__ float pseudo_grad(float x, float g, float l1) {
 
 __device__ __forceinline__ float sgnf(float v) { return v > 0.f ? 1.f : (v < 0.f ? -1.f : 0.f); }
 
-// the previous phase 2 of model b, completed by one lane (pick[b]: >= 0 accepted trial, -1 no
-// trial accepted / inactive, -2 non-descent direction)
-__device__ void qn_finalize(const QnArgs& a, int b, const double* v) {
+// phase 2 of model b, completed by one lane of its last chunk (p: >= 0 accepted trial, -1 no
+// trial accepted / inactive, -2 non-descent direction; regp: the regularization of trial p, from the
+// block's own P2 sums — reg[] is stored by chunk 0 of this launch, not visible to the last chunk);
+// the objective goes to hist row fin_it
+__device__ void qn_finalize(const QnArgs& a, int b, int p, double regp, const double* v) {
   const int mm = a.m;
-  const int p = a.pick[b];
-  if (a.fin_init) {
-    a.fobj[b] = a.loss[b * a.T] + a.reg[b * a.T];
+  if (a.init) {
+    a.fobj[b] = a.loss[b * a.T] + regp;
     if (a.hist) a.hist[b] = a.fobj[b];
     return;
   }
-  const int h = a.fin_head;
+  const int h = a.head;
   if (p >= 0) {  // v: the P3 chunk sums (LDS)
     double* SY = a.SY + (int64_t)b * mm * mm;
     double* YY = a.YY + (int64_t)b * mm * mm;
@@ -439,8 +465,7 @@ __device__ void qn_finalize(const QnArgs& a, int b, const double* v) {
     }
     const bool good = v[0] > 1e-10 * fmax(sqrt(v[1]) * sqrt(v[2]), 1e-300);
     a.rho[h * a.B + b] = good ? 1.0 / v[0] : 0.0;
-    const int bt = b * a.T + p;
-    const double Fn = a.loss[bt] + a.reg[bt];
+    const double Fn = a.loss[b * a.T + p] + regp;
     const double F0 = a.fobj[b];
     const double rel = fabs(F0 - Fn) / fmax(fmax(fabs(F0), fabs(Fn)), 1.0);
     a.fobj[b] = Fn;
@@ -460,51 +485,6 @@ __device__ void qn_finalize(const QnArgs& a, int b, const double* v) {
     }
   }
   if (a.hist) a.hist[(int64_t)a.fin_it * a.B + b] = a.fobj[b];
-}
-
-// FULLM (history of QN_MAX_M pairs, the default m): the per-element history loops are unrolled with no
-// slot conditions, so a lane issues all 2 m history loads of an element before it waits
-// phase 0
-template <bool FULLM>
-__global__ __launch_bounds__(QN_BLOCK) void qn_dots_kernel(QnArgs a) {
-  __shared__ double sh[4 * NP1];
-  __shared__ double fin_v[NP3];
-  const int c = blockIdx.x, b = blockIdx.y;
-  if (a.fin && c == 0) {  // block-uniform
-    if (!a.fin_init && a.pick[b] >= 0) reduce_chunks_shared<NP3>(a.P3 + (int64_t)b * a.nch * NP3, a.nch, fin_v);
-    __syncthreads();
-    if (threadIdx.x == 0) qn_finalize(a, b, fin_v);
-  }
-  if (a.fin_only) return;
-  const int D = (int)a.D;
-  const int mm = a.m;
-  const int64_t sstride = (int64_t)a.B * D;
-  const float* __restrict__ x = a.x + (int64_t)b * D;
-  const float* __restrict__ g = a.g + (int64_t)b * D;
-  const float* __restrict__ l1v = a.l1 ? a.l1 + (int64_t)b * D : nullptr;
-  const float* __restrict__ Sb = a.S + (int64_t)b * D;
-  const float* __restrict__ Yb = a.Y + (int64_t)b * D;
-  const int csz = (D + a.nch - 1) / a.nch, e1 = min(D, (c + 1) * csz);
-  float acc[NP1];
-#pragma unroll
-  for (int j = 0; j < NP1; ++j) acc[j] = 0.f;
-#pragma unroll 2
-  for (int e = c * csz + threadIdx.x; e < e1; e += QN_BLOCK) {
-    const float pg = pseudo_grad(x[e], g[e], l1v ? l1v[e] : 0.f);
-    acc[2 * QN_MAX_M] = fmaf(pg, pg, acc[2 * QN_MAX_M]);
-#pragma unroll
-    for (int j = 0; j < QN_MAX_M; ++j) {
-      if (FULLM || j < mm) {
-        acc[j] = fmaf(Sb[j * sstride + e], pg, acc[j]);
-        acc[QN_MAX_M + j] = fmaf(Yb[j * sstride + e], pg, acc[QN_MAX_M + j]);
-      }
-    }
-  }
-  double v[NP1];
-#pragma unroll
-  for (int j = 0; j < NP1; ++j) v[j] = (double)acc[j];
-  block_sum<NP1>(v, sh);
-  store_partial<NP1>(v, a.P1 + ((int64_t)b * a.nch + c) * NP1);
 }
 
 // phase 1
@@ -649,7 +629,8 @@ template <bool FULLM>
 __global__ __launch_bounds__(QN_BLOCK) void qn_update_kernel(QnArgs a) {
   __shared__ double sh[4 * NP3];
   __shared__ double p2v[NP2];
-  __shared__ int pick;
+  __shared__ double fin_v[NP3];
+  __shared__ int pick, last;
   const int c = blockIdx.x, b = blockIdx.y;
   const int D = (int)a.D;
   const int mm = a.m;
@@ -688,57 +669,90 @@ __global__ __launch_bounds__(QN_BLOCK) void qn_update_kernel(QnArgs a) {
   }
   __syncthreads();
   const int p = pick;
-  if (p < 0) return;
-  const int64_t sstride = (int64_t)a.B * D;
-  float* __restrict__ x = a.x + (int64_t)b * D;
-  float* __restrict__ g = a.g + (int64_t)b * D;
-  const float* __restrict__ l1v = a.l1 ? a.l1 + (int64_t)b * D : nullptr;
-  float* Sh = a.S + (int64_t)a.head * sstride + (int64_t)b * D;  // aliases slot `head` of Sb / Yb
-  float* Yh = a.Y + (int64_t)a.head * sstride + (int64_t)b * D;
-  const float* Sb = a.S + (int64_t)b * D;
-  const float* Yb = a.Y + (int64_t)b * D;
-  const int bt = b * a.T + p;
-  const float* __restrict__ xt = a.xtrial + (int64_t)bt * D;
-  const float* __restrict__ Gt = a.G + (int64_t)bt * D;
-  const float* __restrict__ l2 = a.l2 + (int64_t)b * D;
-  const int csz = (D + a.nch - 1) / a.nch, e1 = min(D, (c + 1) * csz);
-  float ps[NP3];
+  if (p >= 0) {  // block-uniform
+    const int64_t sstride = (int64_t)a.B * D;
+    float* __restrict__ x = a.x + (int64_t)b * D;
+    float* __restrict__ g = a.g + (int64_t)b * D;
+    const float* __restrict__ l1v = a.l1 ? a.l1 + (int64_t)b * D : nullptr;
+    float* Sh = a.S + (int64_t)a.head * sstride + (int64_t)b * D;  // aliases slot `head` of Sb / Yb
+    float* Yh = a.Y + (int64_t)a.head * sstride + (int64_t)b * D;
+    const float* Sb = a.S + (int64_t)b * D;
+    const float* Yb = a.Y + (int64_t)b * D;
+    const int bt = b * a.T + p;
+    const float* __restrict__ xt = a.xtrial + (int64_t)bt * D;
+    const float* __restrict__ Gt = a.G + (int64_t)bt * D;
+    const float* __restrict__ l2 = a.l2 + (int64_t)b * D;
+    const int csz = (D + a.nch - 1) / a.nch, e1 = min(D, (c + 1) * csz);
+    float ps[NP3];
+    float pd[2 * QN_MAX_M];  // the next direction's s_j.pg, y_j.pg (pg.pg is ps[4])
 #pragma unroll
-  for (int q = 0; q < NP3; ++q) ps[q] = 0.f;
+    for (int q = 0; q < NP3; ++q) ps[q] = 0.f;
+#pragma unroll
+    for (int q = 0; q < 2 * QN_MAX_M; ++q) pd[q] = 0.f;
 #pragma unroll 2
-  for (int e = c * csz + threadIdx.x; e < e1; e += QN_BLOCK) {
-    const float xn = xt[e];
-    const float gn = Gt[e] + l2[e] * xn;  // data gradient (masked, scaled) + L2 term
-    if (!a.init) {
-      const float se = xn - x[e], ye = gn - g[e];
-      ps[0] = fmaf(se, ye, ps[0]);
-      ps[1] = fmaf(se, se, ps[1]);
-      ps[2] = fmaf(ye, ye, ps[2]);
+    for (int e = c * csz + threadIdx.x; e < e1; e += QN_BLOCK) {
+      const float xn = xt[e];
+      const float gn = Gt[e] + l2[e] * xn;  // data gradient (masked, scaled) + L2 term
+      const float pg = pseudo_grad(xn, gn, l1v ? l1v[e] : 0.f);
+      if (!a.init) {
+        const float se = xn - x[e], ye = gn - g[e];
+        ps[0] = fmaf(se, ye, ps[0]);
+        ps[1] = fmaf(se, se, ps[1]);
+        ps[2] = fmaf(ye, ye, ps[2]);
 #pragma unroll
-      for (int j = 0; j < QN_MAX_M; ++j) {
-        // FULLM also accumulates slot `head` (its OLD pair: the loads precede the stores below);
-        // finalize never reads those sums
-        if (FULLM || (j < mm && j != a.head)) {
-          const float sj = Sb[j * sstride + e], yj = Yb[j * sstride + e];
-          ps[5 + 3 * j] = fmaf(se, yj, ps[5 + 3 * j]);
-          ps[6 + 3 * j] = fmaf(sj, ye, ps[6 + 3 * j]);
-          ps[7 + 3 * j] = fmaf(ye, yj, ps[7 + 3 * j]);
+        for (int j = 0; j < QN_MAX_M; ++j) {
+          if (FULLM || j < mm) {
+            const bool hj = j == a.head;
+            // FULLM also loads slot `head` (its OLD pair: the loads precede the stores below) and
+            // accumulates its P3 sums, which finalize never reads
+            float sj = 0.f, yj = 0.f;
+            if (FULLM || !hj) {
+              sj = Sb[j * sstride + e];
+              yj = Yb[j * sstride + e];
+              ps[5 + 3 * j] = fmaf(se, yj, ps[5 + 3 * j]);
+              ps[6 + 3 * j] = fmaf(sj, ye, ps[6 + 3 * j]);
+              ps[7 + 3 * j] = fmaf(ye, yj, ps[7 + 3 * j]);
+            }
+            pd[j] = fmaf(hj ? se : sj, pg, pd[j]);
+            pd[QN_MAX_M + j] = fmaf(hj ? ye : yj, pg, pd[QN_MAX_M + j]);
+          }
         }
+        Sh[e] = se;
+        Yh[e] = ye;
       }
-      Sh[e] = se;
-      Yh[e] = ye;
+      ps[3] = fmaf(xn, xn, ps[3]);
+      ps[4] = fmaf(pg, pg, ps[4]);
+      x[e] = xn;
+      g[e] = gn;
     }
-    const float pg = pseudo_grad(xn, gn, l1v ? l1v[e] : 0.f);
-    ps[3] = fmaf(xn, xn, ps[3]);
-    ps[4] = fmaf(pg, pg, ps[4]);
-    x[e] = xn;
-    g[e] = gn;
-  }
-  double v[NP3];
+    double v[NP3];
 #pragma unroll
-  for (int q = 0; q < NP3; ++q) v[q] = (double)ps[q];
-  block_sum<NP3>(v, sh);
-  store_partial<NP3>(v, a.P3 + ((int64_t)b * a.nch + c) * NP3);
+    for (int q = 0; q < NP3; ++q) v[q] = (double)ps[q];
+    block_sum<NP3>(v, sh);
+    store_partial_agent<NP3>(v, a.P3 + ((int64_t)b * a.nch + c) * NP3);
+    double w[NP1];
+#pragma unroll
+    for (int q = 0; q < 2 * QN_MAX_M; ++q) w[q] = (double)pd[q];
+    w[2 * QN_MAX_M] = 0.0;
+    block_sum<NP1>(w, sh);
+    w[2 * QN_MAX_M] = v[4];
+    store_partial<NP1>(w, a.P1 + ((int64_t)b * a.nch + c) * NP1);
+  }
+  // the last chunk of model b to get here finalizes the model: lane 0 counts the chunk only once its
+  // agent-scope P3 stores have completed (vmcnt drained), and the last chunk reads every chunk's
+  // partials with agent-scope loads
+  if (threadIdx.x == 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    last = __hip_atomic_fetch_add(a.done + b, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == a.nch - 1;
+  }
+  __syncthreads();
+  if (!last) return;
+  if (!a.init && p >= 0) reduce_chunks_agent<NP3>(a.P3 + (int64_t)b * a.nch * NP3, a.nch, fin_v);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    qn_finalize(a, b, p, p >= 0 ? p2v[3 * p] + p2v[3 * p + 1] : 0.0, fin_v);
+    a.done[b] = 0;
+  }
 }
 
 }  // namespace
@@ -804,23 +818,13 @@ extern "C" int har_qn_chunks(int64_t D, int B) {
 extern "C" int har_lbfgs_phase(const QnArgs* args, int KP, int phase, hipStream_t s) {
   const QnArgs& a = *args;
   if ((KP != 8 && KP != 16) || a.K > KP || a.m < 1 || a.m > QN_MAX_M || a.T < 1 || a.T > QN_MAX_TRIALS ||
-      a.D != (int64_t)a.K * (a.F + 1) || a.D >= (1LL << 31) || a.nch != har_qn_chunks(a.D, a.B) || phase < 0 ||
-      phase > 3)
+      a.D != (int64_t)a.K * (a.F + 1) || a.D >= (1LL << 31) || a.nch != har_qn_chunks(a.D, a.B) || phase < 1 ||
+      phase > 2 || a.head < 0 || a.head >= a.m || a.done == nullptr)
     return -2;
   if (a.B == 0) return 0;
   const bool full = a.m == QN_MAX_M;
   const dim3 grid(a.nch, a.B);
-  if (phase == 3) {
-    QnArgs f = a;
-    f.fin = 1;
-    f.fin_only = 1;
-    qn_dots_kernel<false><<<dim3(1, a.B), QN_BLOCK, 0, s>>>(f);
-  } else if (phase == 0) {
-    if (full)
-      qn_dots_kernel<true><<<grid, QN_BLOCK, 0, s>>>(a);
-    else
-      qn_dots_kernel<false><<<grid, QN_BLOCK, 0, s>>>(a);
-  } else if (phase == 1) {
+  if (phase == 1) {
     if (KP == 8 && full)
       qn_direction_kernel<8, true><<<grid, QN_BLOCK, 0, s>>>(a);
     else if (KP == 8)

@@ -6,7 +6,7 @@ ROOT="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 OUT="$ROOT/gpurun_out/lrq_${1:-x}"
 mkdir -p "$OUT"
 cd "$ROOT"
-timeout -k 10 400 python -m pytest tests/test_gpu_logreg.py tests/test_gpu_models.py -m gpu -q -x -k "logreg or lr or LogisticRegression or crossval or cv" > "$OUT/pytest.log" 2>&1
+timeout -k 10 400 python -m pytest tests/test_gpu_logreg.py tests/test_gpu_models.py tests/test_gpu_distributed.py -m gpu --timeout 120 --timeout-method thread -q -x -k "logreg or lr or LogisticRegression or crossval or cv" > "$OUT/pytest.log" 2>&1
 rc=$?; tail -2 "$OUT/pytest.log"; [ $rc -ne 0 ] && [ $rc -ne 5 ] && exit $rc
 timeout -k 10 300 python bench.py --config reference --steps 3 --warmup 1 --out "$OUT/bench_reference.json" > "$OUT/bench.log" 2>&1 || exit $?
 python -c "import json;d=json.load(open('$OUT/bench_reference.json'))['reference_suite']['models'];print({k:(round(v['fit_s']*1e3,2),round(v['accuracy'],4)) for k,v in d.items()})"

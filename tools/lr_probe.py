@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Host profile of the reference LogisticRegression fit (WISDM, 3100-dim encoding) on the GPU:
 wall time per fit, then cProfile of 5 more fits (where the host spends the fit).
-usage: python tools/lr_probe.py [--model lr|lrcv] [--fits 5]"""
+With --cold: main.py's order instead (device warm-up, then the FIRST fit of each model profiled).
+usage: python tools/lr_probe.py [--model lr|lrcv] [--fits 5] [--cold]"""
 import argparse
 import cProfile
 import os
@@ -16,25 +17,36 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--model", default="lr")
     ap.add_argument("--fits", type=int, default=5)
+    ap.add_argument("--cold", action="store_true")
     a = ap.parse_args()
     import torch
 
     from har.config import DEFAULT_WISDM, RunConfig
-    from har.suite import build_estimator, load_wisdm, n_feature_columns
+    from har.suite import build_estimator, load_wisdm, n_feature_columns, warm_up_device
 
     dev = torch.device("cuda")
     cfg = RunConfig(cv_metric="mae")
     train, test, _ = load_wisdm(DEFAULT_WISDM, "reference", cfg.seed, device=dev)
     nf, nc = n_feature_columns(train), len(train["label"].meta["vocab"])
 
-    def fit():
-        est = build_estimator(a.model, cfg, dev, nf, nc)
+    def fit(model=a.model):
+        est = build_estimator(model, cfg, dev, nf, nc)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         est.fit(train)
         torch.cuda.synchronize()
         return time.perf_counter() - t0
 
+    if a.cold:
+        warm_up_device(dev, train, cfg)
+        for model in ("lr", "lrcv"):
+            pr = cProfile.Profile()
+            pr.enable()
+            t = fit(model)
+            pr.disable()
+            print(f"first {model} fit: {1e3 * t:.3f} ms", flush=True)
+            pstats.Stats(pr).sort_stats("cumtime").print_stats(35)
+        return
     for i in range(3):
         print(f"fit {i}: {1e3 * fit():.3f} ms", flush=True)
     pr = cProfile.Profile()
