@@ -315,7 +315,11 @@ class LogisticRegression(Estimator, ClassifierParams):
                                         allreduce=allreduce)
             xs, fobj, iters = solver.solve(x0, poll=poll)
             n_evals = solver.n_evals
-            hist_h = solver.hist.cpu()
+            # objective history, objectives and iteration counts to the host in ONE transfer
+            packed = torch.cat([solver.hist.reshape(-1), fobj.double(), iters.double()]).cpu()
+            nh = solver.hist.numel()
+            hist_h = packed[:nh].view(solver.hist.shape)
+            fobj, iters = packed[nh:nh + B], packed[nh + B:].to(torch.int64)
             history = [solver.history(bi, hist_h) for bi in range(B)]
         else:
             def evaluate(xt):

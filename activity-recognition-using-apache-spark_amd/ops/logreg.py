@@ -112,7 +112,7 @@ class LogregDesign:
         self.dense_cols = hm.dense_cols if self.Fd else torch.zeros(1, dtype=torch.int32, device=hm.device)
         self.cat = hm.cat if self.C else torch.zeros(max(1, self.N), 1, dtype=torch.int32, device=hm.device)
         self.SL = SLICE_ROWS
-        self._col_slice = None
+        self._col_slice = getattr(hm, "_lr_col_slice", None)  # cached on the (immutable) matrix
 
     @property
     def device(self):
@@ -133,7 +133,7 @@ class LogregDesign:
                 cs = torch.zeros(F + 2, dtype=torch.int64)
                 cs[1:] = torch.cumsum(ns, 0)
                 cs = cs.to(torch.int32)
-            self._col_slice = cs
+            self._col_slice = self.hm._lr_col_slice = cs
         return self._col_slice
 
     def rw_ptr(self) -> int:

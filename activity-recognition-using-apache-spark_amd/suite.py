@@ -102,6 +102,14 @@ def warm_up_device(dev, train, cfg: RunConfig, classifiers: Optional[Sequence[st
             if hasattr(est, attr):
                 setattr(est, attr, v)
         est.fit(small).predict_all(features_tensor(small, "features", dev))
+    if dev.type == "cuda" and any(c.startswith("lr") for c in (classifiers or cfg.classifiers)):
+        # a LogisticRegression fit over the whole table sorts its one-hot CSC keys with a larger
+        # radix-sort configuration than the 256-row fits above select (its first launch cost ~15 ms
+        # inside the first timed fit): warm that configuration on synthetic keys of the same count
+        from ..features.hybrid import hybrid_features
+
+        n_keys = train.count() * max(1, int(hybrid_features(small, "features", dev).cat.shape[1]))
+        torch.sort(torch.arange(n_keys, 0, -1, device=dev, dtype=torch.int64))
     device_sync(dev)
 
 
