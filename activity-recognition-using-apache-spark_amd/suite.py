@@ -96,17 +96,20 @@ def warm_up_device(dev, train, cfg: RunConfig, classifiers: Optional[Sequence[st
     small = train.head(min(256, train.count()))
     n_classes = len(train["label"].meta["vocab"])
     for name in classifiers or cfg.classifiers:
-        base = name[:-2] if name.endswith("cv") else name
-        est = build_estimator(base, cfg, dev, n_feature_columns(small), n_classes)
+        # the CrossValidators too (on the same 256 rows): their batched solve, fold scoring and
+        # evaluator run code (torch reductions, batched metrics) a plain fit never touches
+        est = build_estimator(name, cfg, dev, n_feature_columns(small), n_classes)
+        inner = getattr(est, "estimator", None) or est
         for attr, v in (("maxIter", 2), ("numTrees", 2)):
-            if hasattr(est, attr):
-                setattr(est, attr, v)
-        est.fit(small).predict_all(features_tensor(small, "features", dev))
+            if hasattr(inner, attr):
+                setattr(inner, attr, v)
+        m = est.fit(small)
+        getattr(m, "bestModel", m).predict_all(features_tensor(small, "features", dev))
     if dev.type == "cuda" and any(c.startswith("lr") for c in (classifiers or cfg.classifiers)):
         # a LogisticRegression fit over the whole table sorts its one-hot CSC keys with a larger
         # radix-sort configuration than the 256-row fits above select (its first launch cost ~15 ms
         # inside the first timed fit): warm that configuration on synthetic keys of the same count
-        from ..features.hybrid import hybrid_features
+        from .features.hybrid import hybrid_features
 
         n_keys = train.count() * max(1, int(hybrid_features(small, "features", dev).cat.shape[1]))
         torch.sort(torch.arange(n_keys, 0, -1, device=dev, dtype=torch.int64))
@@ -155,7 +158,7 @@ def run_reference_suite(dev, path: str, models: Sequence[str] = ("lr", "lrcv", "
     y_test = labels_tensor(test, "label", dev)
     t_w = time.perf_counter()
     if dev.type == "cuda":
-        warm_up_device(dev, train, cfg, [m[:-2] if m.endswith("cv") else m for m in models])
+        warm_up_device(dev, train, cfg, list(models))
     warm_s = time.perf_counter() - t_w
     from .models import tree as tree_mod
 

@@ -28,6 +28,7 @@
 // A one-hot feature of the reference's 3,100-dim encoding (Main/main.py:51-66) is one gathered
 // weight column per row instead of 3,090 multiplications by zero: the WISDM objective reads
 // ~60 bytes per row instead of 12.4 KB.
+#include <algorithm>
 #include <cstdlib>
 
 #include "common.h"
@@ -45,9 +46,14 @@ constexpr int EVAL_ROWS = 256;
 // chunks newest-first (the last one is still in LDS) for the tile's dense gradient R^T X.
 // ---------------------------------------------------------------------------------------------
 constexpr int EVAL_DCH = 32;                       // dense columns per LDS chunk
-constexpr int EVAL_XLD = EVAL_DCH + 1;             // odd row stride: conflict-free row reads
+// LDS row stride of the dense tile (a compile-time constant: the tile's row addresses fold into
+// immediate offsets): 33 in general, 11 for designs of at most 10 dense columns (the reference
+// encoding) — an 11 KB tile instead of 34 KB, so three times as many evaluation workgroups fit a CU
+// (the 54-model CrossValidator batch: 62 -> 49 us per evaluation)
+constexpr int EVAL_XLD_NARROW = 11;
+__host__ __device__ constexpr int eval_xld(int Fd) { return Fd <= EVAL_XLD_NARROW - 1 ? EVAL_XLD_NARROW : EVAL_DCH + 1; }
 
-template <int KP>
+template <int KP, int XLD>
 __device__ __forceinline__ void eval_stage_chunk(const LogregEvalArgs& a, const float* W, float* wd, float* xs,
                                                  int c0, int nc, int64_t r0, int64_t nrow_tile, bool weights) {
   const int tid = threadIdx.x;
@@ -55,17 +61,18 @@ __device__ __forceinline__ void eval_stage_chunk(const LogregEvalArgs& a, const 
     for (int e = tid; e < nc * KP; e += EVAL_ROWS) wd[e] = W[(int64_t)a.dense_cols[c0 + e / KP] * KP + (e % KP)];
   for (int e = tid; e < EVAL_ROWS * nc; e += EVAL_ROWS) {
     const int rr = e / nc, j = e % nc;
-    xs[rr * EVAL_XLD + j] = rr < nrow_tile ? a.dense[(r0 + rr) * a.ldd + c0 + j] : 0.f;
+    xs[rr * XLD + j] = rr < nrow_tile ? a.dense[(r0 + rr) * a.ldd + c0 + j] : 0.f;
   }
 }
 
-template <int KP>
+template <int KP, int XLD>
 __global__ __launch_bounds__(EVAL_ROWS) void logreg_eval_kernel(LogregEvalArgs a) {
   extern __shared__ float smem[];
   const int Fd = a.Fd;
   float* wd = smem;                                // [EVAL_DCH][KP] dense weights of the chunk
-  float* xs = wd + EVAL_DCH * KP;                  // [EVAL_ROWS][EVAL_XLD] dense row tile, one chunk
-  float* rs = xs + EVAL_ROWS * EVAL_XLD;           // [EVAL_ROWS][KP]
+  constexpr int xld = XLD;
+  float* xs = wd + EVAL_DCH * KP;                  // [EVAL_ROWS][xld] dense row tile, one chunk
+  float* rs = xs + EVAL_ROWS * xld;                // [EVAL_ROWS][KP]
   float* red = rs + EVAL_ROWS * KP;                // [EVAL_ROWS / 64]
 
   const int tid = threadIdx.x;
@@ -85,11 +92,11 @@ __global__ __launch_bounds__(EVAL_ROWS) void logreg_eval_kernel(LogregEvalArgs a
   for (int ch = 0; ch < nchunk; ++ch) {
     const int c0 = ch * EVAL_DCH, nc = min(EVAL_DCH, Fd - c0);
     if (ch) __syncthreads();                       // the previous chunk is consumed
-    eval_stage_chunk<KP>(a, W, wd, xs, c0, nc, r0, nrow_tile, true);
+    eval_stage_chunk<KP, XLD>(a, W, wd, xs, c0, nc, r0, nrow_tile, true);
     __syncthreads();
     if (ok) {
       for (int j = 0; j < nc; ++j) {
-        const float xv = xs[tid * EVAL_XLD + j];
+        const float xv = xs[tid * xld + j];
 #pragma unroll
         for (int k = 0; k < KP; ++k) z[k] = fmaf(xv, wd[j * KP + k], z[k]);
       }
@@ -158,13 +165,13 @@ __global__ __launch_bounds__(EVAL_ROWS) void logreg_eval_kernel(LogregEvalArgs a
     const int c0 = ch * EVAL_DCH, nc = min(EVAL_DCH, Fd - c0);
     if (ch != nchunk - 1) {
       __syncthreads();
-      eval_stage_chunk<KP>(a, W, wd, xs, c0, nc, r0, nrow_tile, false);
+      eval_stage_chunk<KP, XLD>(a, W, wd, xs, c0, nc, r0, nrow_tile, false);
       __syncthreads();
     }
     for (int o = tid; o < nc * KP; o += EVAL_ROWS) {
       const int j = o / KP, k = o % KP;
       float acc = 0.f;
-      for (int i = 0; i < EVAL_ROWS; ++i) acc = fmaf(rs[i * KP + k], xs[i * EVAL_XLD + j], acc);
+      for (int i = 0; i < EVAL_ROWS; ++i) acc = fmaf(rs[i * KP + k], xs[i * xld + j], acc);
       slab[(int64_t)c0 * KP + o] = acc;
     }
   }
@@ -790,12 +797,18 @@ extern "C" int har_logreg_eval(const LogregEvalArgs* args, int KP, int n_models,
     return -2;
   if (a.N == 0 || n_models == 0) return 0;
   const int tiles = (int)((a.N + EVAL_ROWS - 1) / EVAL_ROWS);
-  const size_t lds = sizeof(float) * (EVAL_DCH * KP + EVAL_ROWS * EVAL_XLD + EVAL_ROWS * KP + EVAL_ROWS / 64);
+  const int xld = eval_xld(a.Fd);
+  const size_t lds = sizeof(float) * (EVAL_DCH * KP + EVAL_ROWS * xld + EVAL_ROWS * KP + EVAL_ROWS / 64);
   dim3 grid(tiles, n_models);
-  if (KP == 8)
-    logreg_eval_kernel<8><<<grid, EVAL_ROWS, lds, s>>>(a);
+  const bool narrow = xld == EVAL_XLD_NARROW;
+  if (KP == 8 && narrow)
+    logreg_eval_kernel<8, EVAL_XLD_NARROW><<<grid, EVAL_ROWS, lds, s>>>(a);
+  else if (KP == 8)
+    logreg_eval_kernel<8, EVAL_DCH + 1><<<grid, EVAL_ROWS, lds, s>>>(a);
+  else if (narrow)
+    logreg_eval_kernel<16, EVAL_XLD_NARROW><<<grid, EVAL_ROWS, lds, s>>>(a);
   else
-    logreg_eval_kernel<16><<<grid, EVAL_ROWS, lds, s>>>(a);
+    logreg_eval_kernel<16, EVAL_DCH + 1><<<grid, EVAL_ROWS, lds, s>>>(a);
   HAR_CHECK_LAUNCH();
   return 0;
 }
