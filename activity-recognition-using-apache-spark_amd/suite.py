@@ -104,7 +104,8 @@ def warm_up_device(dev, train, cfg: RunConfig, classifiers: Optional[Sequence[st
             if hasattr(inner, attr):
                 setattr(inner, attr, v)
         m = est.fit(small)
-        getattr(m, "bestModel", m).predict_all(features_tensor(small, "features", dev))
+        m = getattr(m, "bestModel", m)
+        m.predict_all(m.features_input(small))  # the model's own feature layout, as transform() uses
     if dev.type == "cuda" and any(c.startswith("lr") for c in (classifiers or cfg.classifiers)):
         # a LogisticRegression fit over the whole table sorts its one-hot CSC keys with a larger
         # radix-sort configuration than the 256-row fits above select (its first launch cost ~15 ms
