@@ -463,14 +463,36 @@ __device__ __forceinline__ float sgnf(float v) { return v > 0.f ? 1.f : (v < 0.f
 // trial accepted / inactive, -2 non-descent direction; regp: the regularization of trial p, from the
 // block's own P2 sums — reg[] is stored by chunk 0 of this launch, not visible to the last chunk);
 // the objective goes to hist row fin_it
-__device__ void qn_finalize(const QnArgs& a, int b, int p, double regp, const double* v) {
+// The per-model scalars phase 2 reads (objective, trial losses, step scale, flags, counters) are
+// loaded at the start of the launch, uniform (scalar loads): their round trip overlaps the P2
+// partials' instead of following the pick and again the last-chunk count.
+struct QnScalars {
+  double F0, L0, L1, L2, L3;  // objective at x, data loss of trials 0..3
+  float step_scale;
+  int steep, active, fails, iters;
+};
+
+__device__ __forceinline__ double trial_loss(const QnScalars& q, int t) {
+  return t == 0 ? q.L0 : t == 1 ? q.L1 : t == 2 ? q.L2 : q.L3;
+}
+
+__device__ __forceinline__ QnScalars qn_load_scalars(const QnArgs& a, int b) {
+  const double* L = a.loss + b * a.T;
+  return QnScalars{a.fobj[b], L[0], a.T > 1 ? L[1] : 0.0, a.T > 2 ? L[2] : 0.0, a.T > 3 ? L[3] : 0.0,
+                   a.step_scale[b], a.steep[b], a.active[b], a.fails[b], a.iters[b]};
+}
+
+__device__ __forceinline__ void qn_finalize(const QnArgs& a, int b, int p, double regp, const QnScalars& q,
+                                            const double* v) {
   const int mm = a.m;
   if (a.init) {
-    a.fobj[b] = a.loss[b * a.T] + regp;
-    if (a.hist) a.hist[b] = a.fobj[b];
+    const double F = q.L0 + regp;
+    a.fobj[b] = F;
+    if (a.hist) a.hist[b] = F;
     return;
   }
   const int h = a.head;
+  double Fout = q.F0;
   if (p >= 0) {  // v: the P3 chunk sums (LDS)
     double* SY = a.SY + (int64_t)b * mm * mm;
     double* YY = a.YY + (int64_t)b * mm * mm;
@@ -484,11 +506,11 @@ __device__ void qn_finalize(const QnArgs& a, int b, int p, double regp, const do
     }
     const bool good = v[0] > 1e-10 * fmax(sqrt(v[1]) * sqrt(v[2]), 1e-300);
     a.rho[h * a.B + b] = good ? 1.0 / v[0] : 0.0;
-    const double Fn = a.loss[b * a.T + p] + regp;
-    const double F0 = a.fobj[b];
+    const double Fn = trial_loss(q, p) + regp;
+    const double F0 = q.F0;
     const double rel = fabs(F0 - Fn) / fmax(fmax(fabs(F0), fabs(Fn)), 1.0);
-    a.fobj[b] = Fn;
-    a.iters[b] += 1;
+    a.fobj[b] = Fout = Fn;
+    a.iters[b] = q.iters + 1;
     a.fails[b] = 0;
     a.steep[b] = 0;
     a.step_scale[b] = 1.0f;
@@ -498,12 +520,42 @@ __device__ void qn_finalize(const QnArgs& a, int b, int p, double regp, const do
     a.steep[b] = 1;
   } else {
     a.rho[h * a.B + b] = 0.0;
-    if (a.active[b]) {
-      a.step_scale[b] *= 1.0f / 16.0f;
-      if (++a.fails[b] >= 2) a.active[b] = 0;
+    if (q.active) {
+      a.step_scale[b] = q.step_scale * (1.0f / 16.0f);
+      a.fails[b] = q.fails + 1;
+      if (q.fails + 1 >= 2) a.active[b] = 0;
     }
   }
-  if (a.hist) a.hist[(int64_t)a.fin_it * a.B + b] = a.fobj[b];
+  if (a.hist) a.hist[(int64_t)a.fin_it * a.B + b] = Fout;
+}
+
+// One parameter element's operands for phase 1 (x, g, L1 / L2 weights, the W_eff scale and the
+// m history values), loaded at a clamped (always valid) index so the loads are unconditional: the
+// kernel keeps the next element's loads in flight while it computes the current one, and the
+// first element's while lane 0 runs the recursion.
+struct DirElem {
+  float x, g, l1, hl2, wsc;
+  float s[QN_MAX_M], y[QN_MAX_M];
+};
+
+__device__ __forceinline__ DirElem dir_load(const QnArgs& a, int b, int e) {
+  const int64_t D = a.D, sstride = (int64_t)a.B * D;
+  const int Fp1 = a.F + 1;
+  const int k = e / Fp1, col = e - k * Fp1;
+  DirElem v;
+  v.x = a.x[b * D + e];
+  v.g = a.g[b * D + e];
+  v.l1 = a.l1 ? a.l1[b * D + e] : 0.f;
+  v.hl2 = 0.5f * a.l2[b * D + e];
+  const float isd = a.inv_std[(int64_t)b * a.F + min(col, a.F - 1)];
+  v.wsc = a.pmask[b * D + e] * (col < a.F ? isd : 1.f);
+#pragma unroll
+  for (int j = 0; j < QN_MAX_M; ++j) {  // slots >= m: allocated ([QN_MAX_M ... ] not read), see below
+    const int jj = j < a.m ? j : 0;
+    v.s[j] = a.S[jj * sstride + b * D + e];
+    v.y[j] = a.Y[jj * sstride + b * D + e];
+  }
+  return v;
 }
 
 // phase 1
@@ -523,6 +575,9 @@ __global__ __launch_bounds__(QN_BLOCK) void qn_direction_kernel(QnArgs a) {
   __shared__ double u[QN_MAX_M], w[QN_MAX_M], al[QN_MAX_M];
   __shared__ double stage[QN_MAX_CHUNKS * NP1];
   const bool rec = !a.init && !steep;  // block-uniform
+  const int csz = (D + a.nch - 1) / a.nch, e1 = min(D, (c + 1) * csz);
+  const int e0 = c * csz + threadIdx.x;
+  DirElem cur = dir_load(a, b, min(e0, D - 1));  // in flight during the prologue + recursion
   if (rec) {
     // the Gram matrices and rho (one element per lane: m^2 <= 100 < QN_BLOCK) are loaded to
     // registers first, so their round trip overlaps the P1 partials'
@@ -584,25 +639,19 @@ __global__ __launch_bounds__(QN_BLOCK) void qn_direction_kernel(QnArgs a) {
     gam = gamma;
   }
   __syncthreads();
-  const int64_t sstride = (int64_t)a.B * D;
-  const float* __restrict__ x = a.x + (int64_t)b * D;
-  const float* __restrict__ g = a.g + (int64_t)b * D;
-  const float* __restrict__ l1v = a.l1 ? a.l1 + (int64_t)b * D : nullptr;
-  const float* __restrict__ Sb = a.S + (int64_t)b * D;
-  const float* __restrict__ Yb = a.Y + (int64_t)b * D;
+  const bool l1on = a.l1 != nullptr;
   const bool active = a.active[b] != 0;
   const int T = a.init ? 1 : a.T;
   const float s0 = a.init ? 0.f : a.step_scale[b];
   const float gamma = gam;
-  const int csz = (D + a.nch - 1) / a.nch, e1 = min(D, (c + 1) * csz);
   float r[NP2];
 #pragma unroll
   for (int t = 0; t < NP2; ++t) r[t] = 0.f;
-#pragma unroll 2
-  for (int e = c * csz + threadIdx.x; e < e1; e += QN_BLOCK) {
-    const float xe = x[e];
-    const float l1e = l1v ? l1v[e] : 0.f;
-    const float pg = a.init ? 0.f : pseudo_grad(xe, g[e], l1e);
+  for (int e = e0; e < e1; e += QN_BLOCK) {
+    const DirElem nxt = dir_load(a, b, min(e + QN_BLOCK, e1 - 1));  // next element, in flight
+    const float xe = cur.x;
+    const float l1e = cur.l1;
+    const float pg = a.init ? 0.f : pseudo_grad(xe, cur.g, l1e);
     float d = 0.f;
     if (!a.init) {
       if (steep) {
@@ -612,25 +661,25 @@ __global__ __launch_bounds__(QN_BLOCK) void qn_direction_kernel(QnArgs a) {
 #pragma unroll
         for (int j = 0; j < QN_MAX_M; ++j) {
           if (FULLM || j < mm) {
-            acc = fmaf(cY[j], Yb[j * sstride + e], acc);
-            acc = fmaf(cS[j], Sb[j * sstride + e], acc);
+            acc = fmaf(cY[j], cur.y[j], acc);
+            acc = fmaf(cS[j], cur.s[j], acc);
           }
         }
         d = -acc;
-        if (l1v && d * pg >= 0.f) d = 0.f;  // OWL-QN: keep the direction in pg's orthant
+        if (l1on && d * pg >= 0.f) d = 0.f;  // OWL-QN: keep the direction in pg's orthant
       }
     }
     r[3 * QN_MAX_TRIALS] = fmaf(pg, d, r[3 * QN_MAX_TRIALS]);
     r[3 * QN_MAX_TRIALS + 1] = fmaf(pg, pg, r[3 * QN_MAX_TRIALS + 1]);
     const float xi = xe != 0.f ? sgnf(xe) : sgnf(-pg);
-    const float hl2 = 0.5f * a.l2[(int64_t)b * D + e];
+    const float hl2 = cur.hl2;
     const int k = e / Fp1, col = e - k * Fp1;
-    const float wsc = a.pmask[(int64_t)b * D + e] * (col < a.F ? a.inv_std[(int64_t)b * a.F + col] : 1.f);
+    const float wsc = cur.wsc;
 #pragma unroll
     for (int t = 0; t < QN_MAX_TRIALS; ++t) {
       if (t < T) {
         float xn = xe + s0 * ldexpf(1.f, -t) * d;
-        if (l1v && !a.init) {  // stay in the orthant of x (or of -pg where x == 0)
+        if (l1on && !a.init) {  // stay in the orthant of x (or of -pg where x == 0)
           if (sgnf(xn) != xi) xn = 0.f;
           r[3 * t + 2] = fmaf(pg, xn - xe, r[3 * t + 2]);
         }
@@ -642,6 +691,7 @@ __global__ __launch_bounds__(QN_BLOCK) void qn_direction_kernel(QnArgs a) {
         a.weff[((int64_t)bt * Fp1 + col) * KP + k] = xn * wsc;
       }
     }
+    cur = nxt;
   }
   __shared__ double tot2[NP2];
   block_sum_f<NP2>(r, sh, tot2);
@@ -664,27 +714,28 @@ __global__ __launch_bounds__(QN_BLOCK) void qn_update_kernel(QnArgs a) {
   const int c = blockIdx.x, b = blockIdx.y;
   const int D = (int)a.D;
   const int mm = a.m;
-  const bool active = a.active[b] != 0;
+  const QnScalars qs = qn_load_scalars(a, b);  // uniform (scalar) loads, in flight with the P2 partials
   reduce_chunks_shared<NP2>(a.P2 + (int64_t)b * a.nch * NP2, a.nch, p2v, stage);
   __syncthreads();
   if (threadIdx.x == 0) {
-    const bool steep = a.steep[b] != 0;
+    const bool steep = qs.steep != 0;
     const double dd = steep ? -p2v[3 * QN_MAX_TRIALS + 1] : p2v[3 * QN_MAX_TRIALS];
     const int T = a.init ? 1 : a.T;
-    const float s0 = a.init ? 0.f : a.step_scale[b];
+    const float s0 = a.init ? 0.f : qs.step_scale;
     int p = -1;
     if (a.init) {
       p = 0;
-    } else if (active) {
+    } else if (qs.active) {
       if (dd >= 0.0) {
         p = steep ? -1 : -2;
       } else {
-        const double F0 = a.fobj[b];
-        for (int t = 0; t < T && p < 0; ++t) {
-          const int bt = b * a.T + t;
-          const double decr = a.l1 ? p2v[3 * t + 2] : (double)(s0 * ldexpf(1.f, -t)) * dd;
-          const double Ft = a.loss[bt] + p2v[3 * t] + p2v[3 * t + 1];
-          if (isfinite(Ft) && Ft <= F0 + a.c1 * decr) p = t;
+#pragma unroll
+        for (int t = 0; t < QN_MAX_TRIALS; ++t) {
+          if (t < T && p < 0) {
+            const double decr = a.l1 ? p2v[3 * t + 2] : (double)(s0 * ldexpf(1.f, -t)) * dd;
+            const double Ft = trial_loss(qs, t) + p2v[3 * t] + p2v[3 * t + 1];
+            if (isfinite(Ft) && Ft <= qs.F0 + a.c1 * decr) p = t;
+          }
         }
       }
     }
@@ -783,7 +834,7 @@ __global__ __launch_bounds__(QN_BLOCK) void qn_update_kernel(QnArgs a) {
   if (!a.init && p >= 0) reduce_chunks_shared<NP3, true>(a.P3 + (int64_t)b * a.nch * NP3, a.nch, fin_v, stage);
   __syncthreads();
   if (threadIdx.x == 0) {
-    qn_finalize(a, b, p, p >= 0 ? p2v[3 * p] + p2v[3 * p + 1] : 0.0, fin_v);
+    qn_finalize(a, b, p, p >= 0 ? p2v[3 * p] + p2v[3 * p + 1] : 0.0, qs, fin_v);
     a.done[b] = 0;
   }
 }
