@@ -224,7 +224,8 @@ def _arena(specs, dev, into: dict) -> torch.Tensor:
 class DeviceLogregSolver:
     """Runs ``optim.lbfgs.minimize_trials``' algorithm for the LR objective entirely with the
     logreg_qn.hip kernels: 4 launches per iteration (direction + trials, evaluate, gradient,
-    pick + history), no host synchronization unless ``poll`` asks for a convergence check."""
+    pick + history + the next direction's dots, each model finalized on the device by its last
+    chunk), no host synchronization unless ``poll`` asks for a convergence check."""
 
     def __init__(self, design: LogregDesign, B: int, T: int, m: int, inv_std, pmask, inv_wsum, l2v, l1v,
                  max_iter: int, tol: float, c1: float = 1e-4, allreduce=None):
