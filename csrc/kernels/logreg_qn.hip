@@ -274,7 +274,7 @@ __global__ __launch_bounds__(256) void logreg_grad_kernel(LogregGradArgs a) {
       float gs[KP];
 #pragma unroll
       for (int k = 0; k < KP; ++k) gs[k] = 0.f;
-#pragma unroll 4
+#pragma unroll 8  // 8 row indices, then their 8 residual rows in flight: 8 dependent round trips per 32-row slice instead of 16
       for (int i = r0; i < r1; ++i) {
         const f32x4_t* rp = reinterpret_cast<const f32x4_t*>(R + (int64_t)a.csc_rows[i] * KP);
 #pragma unroll
