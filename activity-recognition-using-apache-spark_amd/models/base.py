@@ -150,10 +150,34 @@ def features_tensor(table: Table, col: str, device, dtype=torch.float32) -> torc
 
 
 def labels_tensor(table: Table, col: str, device) -> torch.Tensor:
+    """int64 label tensor of ``col`` on ``device``, cached on the (immutable) column."""
     c = table[col]
+    key = ("labels", str(device))
+    cache = getattr(c, "cache", None)
+    if cache is not None and key in cache:
+        return cache[key]
     if isinstance(c, DeviceColumn):
-        return c.tensor.to(device=device, dtype=torch.int64)
-    return torch.as_tensor(c.data.astype(np.int64)).to(device)
+        t = c.tensor.to(device=device, dtype=torch.int64)
+    else:
+        t = torch.as_tensor(c.data.astype(np.int64)).to(device)
+    if cache is not None:
+        cache[key] = t
+    return t
+
+
+def num_label_classes(table: Table, col: str, device) -> int:
+    """max(label) + 1, at least the indexer vocabulary size — cached on the column, so a fit on a
+    resident table does not wait on a device -> host read before its first launch."""
+    c = table[col]
+    cache = getattr(c, "cache", None)
+    key = ("num_classes", str(device))
+    if cache is not None and key in cache:
+        return cache[key]
+    y = labels_tensor(table, col, device)
+    k = int(max(int(y.max()) + 1 if y.numel() else 0, len((c.meta or {}).get("vocab") or [])))
+    if cache is not None:
+        cache[key] = k
+    return k
 
 
 class ClassifierParams(Params):

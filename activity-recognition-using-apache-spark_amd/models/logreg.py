@@ -37,7 +37,7 @@ from ..features.hybrid import from_dense as hybrid_from_dense
 from ..ops.logreg import DeviceLogregSolver, LogregDesign, logreg_margins_native, pack_bucket, unpack_bucket
 from ..optim import lbfgs
 from .base import ClassificationModel, ClassifierParams, Estimator, dp_allreduce, dp_context, dp_owner, dp_rows, \
-    features_tensor, labels_tensor, new_uid, resolve_device
+    features_tensor, labels_tensor, new_uid, num_label_classes, resolve_device
 
 
 @dataclass
@@ -179,7 +179,7 @@ class LogisticRegression(Estimator, ClassifierParams):
         w = None
         if self.weightCol:
             w = torch.as_tensor(table[self.weightCol].data.astype(np.float32), device=dev)
-        num_classes = int(max(int(y.max()) + 1, len((table[self.labelCol].meta or {}).get("vocab") or [])))
+        num_classes = num_label_classes(table, self.labelCol, dev)
         lo, hi = dp_rows(hm.n_rows)  # data parallel: this rank's row shard + one all-reduce per evaluation
         model = self.fit_many(hm.rows(lo, hi), y[lo:hi], [FitSpec(None if w is None else w[lo:hi], self.regParam,
                                                                   self.elasticNetParam)], num_classes,

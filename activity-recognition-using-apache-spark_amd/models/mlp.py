@@ -40,7 +40,7 @@ from ..data.table import Table
 from ..ops import _native, rng
 from ..ops.gemm import EPI_BIAS_RELU, EPI_F32_SLAB, EPI_RELU_GRAD, gemm_bf16, tile_counts
 from .base import ClassificationModel, ClassifierParams, Estimator, dp_allreduce, dp_context, dp_owner, dp_rows, \
-    features_tensor, labels_tensor, new_uid, resolve_device
+    features_tensor, labels_tensor, new_uid, num_label_classes, resolve_device
 
 HEAD_PAD = 32  # classes padded to 32 rows (two 16-wide MFMA column tiles)
 
@@ -712,8 +712,7 @@ class MultilayerPerceptronClassifier(Estimator, ClassifierParams):
         dev = resolve_device(self.device)
         X = features_tensor(table, self.featuresCol, dev)
         y = labels_tensor(table, self.labelCol, dev)
-        vocab = (table[self.labelCol].meta or {}).get("vocab")
-        K = int(max(int(y.max()) + 1, len(vocab) if vocab else 0))
+        K = num_label_classes(table, self.labelCol, dev)
         ctx = dp_context()
         if ctx is None:
             return self.fit_tensors(X, y, num_classes=K)

@@ -19,7 +19,7 @@ import torch
 from ..data.table import Table
 from ..ops.gemm import EPI_BIAS_F32, EPI_F32_SLAB, auto_k_split, gemm_f32
 from .base import ClassificationModel, ClassifierParams, Estimator, dp_allreduce, dp_context, dp_owner, dp_rows, \
-    features_tensor, labels_tensor, new_uid, resolve_device
+    features_tensor, labels_tensor, new_uid, num_label_classes, resolve_device
 
 
 def _pad4(x: int) -> int:
@@ -121,8 +121,7 @@ class NaiveBayes(Estimator, ClassifierParams):
         dev = resolve_device(self.device)
         X = features_tensor(table, self.featuresCol, dev)
         y = labels_tensor(table, self.labelCol, dev)
-        vocab = (table[self.labelCol].meta or {}).get("vocab")
-        K = int(max(int(y.max()) + 1, len(vocab) if vocab else 0))
+        K = num_label_classes(table, self.labelCol, dev)
         w = None
         if self.weightCol:
             w = torch.as_tensor(table[self.weightCol].data, dtype=torch.float32, device=dev)

@@ -40,7 +40,7 @@ from ..data.table import Table
 from ..ops import _native, rng
 from ..ops import tree as T
 from .base import ClassificationModel, ClassifierParams, Estimator, dp_allreduce, dp_context, dp_owner, dp_rows, \
-    features_tensor, labels_tensor, new_uid, resolve_device
+    features_tensor, labels_tensor, new_uid, num_label_classes, resolve_device
 
 
 @dataclass
@@ -692,8 +692,7 @@ class _TreeEstimatorBase(Estimator, ClassifierParams):
         dev = resolve_device(self.device)
         X = features_tensor(table, self.featuresCol, dev)
         y = labels_tensor(table, self.labelCol, dev)
-        vocab = (table[self.labelCol].meta or {}).get("vocab")
-        K = int(max(int(y.max()) + 1, len(vocab) if vocab else 0))
+        K = num_label_classes(table, self.labelCol, dev)
         return X, y, K
 
 

@@ -32,7 +32,7 @@ import torch
 from ..data.split import kfold_ids, split_ids
 from ..data.table import Column, Table
 from ..models.base import Estimator, Model, dp_allreduce, dp_context, dp_rows, features_tensor, labels_tensor, \
-    new_uid, resolve_device
+    new_uid, num_label_classes, resolve_device
 
 
 def _pname(p) -> str:
@@ -133,7 +133,7 @@ class CrossValidator(Estimator):
             dev = resolve_device(est.device)
             hm = hybrid_features(table, est.featuresCol, dev)
             y = labels_tensor(table, est.labelCol, dev)
-            K = int(max(int(y.max()) + 1, len((table[est.labelCol].meta or {}).get("vocab") or [])))
+            K = num_label_classes(table, est.labelCol, dev)
             fold_t = torch.as_tensor(fold, device=dev)
             in_fold = fold_t[None, :] == torch.arange(k, device=dev)[:, None]  # [k, N]: ONE launch, not k
             train_w = (~in_fold).float()
