@@ -176,3 +176,20 @@ def test_plots_hexbin_grid_and_scatter_matrix(tmp_path, wisdm_csv):
     assert "Scatter_Matrix.png" in names and "Fig YAVG_ZAVG.png" in names
     assert len([n for n in names if n.startswith("Fig ")]) == len(cols) ** 2
     assert all(os.path.getsize(p) > 1000 for p in written)
+
+
+def test_warm_up_device_covers_every_classifier(wisdm_csv):
+    """The device warm-up (suite.warm_up_device, run by main.py and the reference suite before any
+    timer) fits every configured classifier — the CrossValidators included — on 256 rows and
+    predicts through each model's own feature layout; on the CPU it must run the same code."""
+    from har.config import RunConfig
+    from har.models.base import labels_tensor, num_label_classes
+    from har.suite import load_wisdm, warm_up_device
+
+    cfg = RunConfig(cv_metric="mae")
+    train, _, _ = load_wisdm(wisdm_csv, "reference", cfg.seed, device=torch.device("cpu"))
+    warm_up_device(torch.device("cpu"), train, cfg, ["lr", "lrcv", "dt", "dtcv", "rf", "nb"])
+    # the label tensor and class count are cached on the column (no device -> host read per fit)
+    y = labels_tensor(train, "label", "cpu")
+    assert labels_tensor(train, "label", "cpu") is y
+    assert num_label_classes(train, "label", "cpu") == max(int(y.max()) + 1, len(train["label"].meta["vocab"]))
