@@ -55,6 +55,9 @@ class RunConfig:
     rf_num_trees: int = 100
     rf_max_depth: int = 4
     max_bins: int = 32
+    # RF over N ranks (torchrun): "tree" = every rank all rows, numTrees / N trees, one all-gather;
+    # "data" = row shards + per-level owner reduction; "auto" = tree while the table is small
+    rf_parallel: str = "auto"
     # NaiveBayes / MLP (new)
     nb_model_type: str = "gaussian"
     mlp_hidden: List[int] = field(default_factory=lambda: [128, 128])

@@ -34,7 +34,8 @@ from ..data.table import Table
 from ..ops import _native
 from ..features.hybrid import HybridMatrix, hybrid_features
 from ..features.hybrid import from_dense as hybrid_from_dense
-from ..ops.logreg import DeviceLogregSolver, LogregDesign, logreg_margins_native, pack_bucket, unpack_bucket
+from ..ops.logreg import DeviceLogregSolver, LogregDesign, logreg_margins_native, native_classes_ok, pack_bucket, \
+    unpack_bucket
 from ..optim import lbfgs
 from .base import ClassificationModel, ClassifierParams, Estimator, dp_allreduce, dp_context, dp_owner, dp_rows, \
     features_tensor, labels_tensor, new_uid, num_label_classes, resolve_device
@@ -87,7 +88,7 @@ class LogisticRegressionModel(ClassificationModel):
         k = self.coefficientMatrix.shape[0]
         if isinstance(X, HybridMatrix) or X.is_cuda:
             hm = X if isinstance(X, HybridMatrix) else hybrid_from_dense(X.float(), [])
-            if hm.device.type == "cuda":
+            if hm.device.type == "cuda" and native_classes_ok(k):
                 KP = 8 if k <= 8 else 16
                 m = logreg_margins_native(hm, self.weight_table(KP).to(hm.device), k, 1)[0, :, :k]
             else:
@@ -202,17 +203,20 @@ class LogisticRegression(Estimator, ClassifierParams):
         binomial = self.family == "binomial" or (self.family == "auto" and K <= 2)
         Kp = 2 if binomial else K
         B = len(specs)
-        if all(s.row_weight is None for s in specs) and dev.type == "cuda":
+        # device kernels for <= 16 classes on the GPU; wider problems run the torch objective on the
+        # data's device (the CPU path's math), every spec's row weights materialized
+        native = dev.type == "cuda" and native_classes_ok(Kp)
+        if all(s.row_weight is None for s in specs) and native:
             rw = None                                                               # every row weight 1
         else:
             rw = torch.stack([torch.ones(N, device=dev) if s.row_weight is None else s.row_weight.to(dev).float()
                               for s in specs])                                        # [B, N]
-        design = LogregDesign(hm, y, rw, Kp)
+        design = LogregDesign(hm, y, rw, Kp, native=native)
         summ = design.summary()
         if allreduce is not None:
             allreduce(summ)
         D = Kp * (F + 1)
-        if dev.type == "cuda":
+        if native:
             reg_a = torch.tensor([[s.regParam for s in specs], [s.elasticNetParam for s in specs]],
                                  dtype=torch.float32).to(dev, non_blocking=True)
             has_l1 = any(s.regParam * s.elasticNetParam > 0 for s in specs)
@@ -308,9 +312,7 @@ class LogisticRegression(Estimator, ClassifierParams):
         B, D = len(specs), Kp * (F + 1)
         T = max(1, int(self.lineSearchTrials))
         poll = 10 if self.maxIter > 20 else 0
-        if dev.type == "cuda":
-            if Kp > 16:
-                raise ValueError(f"the device LogisticRegression supports at most 16 classes, got {Kp}")
+        if design.native:
             solver = DeviceLogregSolver(design, B, T, 10, inv_std, pmask, inv_wsum, l2v, l1v, self.maxIter, self.tol,
                                         allreduce=allreduce)
             xs, fobj, iters = solver.solve(x0, poll=poll)
@@ -334,8 +336,8 @@ class LogisticRegression(Estimator, ClassifierParams):
 
             res = lbfgs.minimize_trials(evaluate, x0.reshape(B, D), l2v, l1v, max_iter=self.maxIter, m=10,
                                         tol=self.tol, trials=T, poll=poll)
-            xs, fobj, iters, n_evals, history = res.x, res.f, res.iterations, res.n_evals, res.history
-            history = [list(history) for _ in range(B)]  # per-model lists (the batch mean per iteration)
+            xs, fobj, iters, n_evals = res.x, res.f, res.iterations, res.n_evals
+            history = res.history_per_model  # each model's own objective per iteration
         xs = xs.view(B, Kp, F + 1) * pmask
         models = []
         fobj_h = fobj.double().cpu()
@@ -357,14 +359,15 @@ class LogisticRegression(Estimator, ClassifierParams):
             st = {}
             for bi, mo in enumerate(models):
                 st[f"coef{bi}"], st[f"icpt{bi}"] = mo.coefficientMatrix, mo.interceptVector
-            ckpt.save(1, st, {"binomial": binomial, "summaries": [
-                {k: v for k, v in mo.summary.items() if k != "objectiveHistory"} for mo in models]}, fingerprint=fp)
+            ckpt.save(1, st, {"binomial": binomial, "summaries": [dict(mo.summary) for mo in models]},
+                      fingerprint=fp)
         return models
 
     def _models_from_state(self, st, meta, B: int, dev) -> List[LogisticRegressionModel]:
         out = []
         for bi in range(B):
             summary = dict(meta["summaries"][bi], resumed=True)
+            summary.setdefault("objectiveHistory", [])  # checkpoints written before it was kept
             out.append(self._apply_thresholds(LogisticRegressionModel(
                 st[f"coef{bi}"].to(dev), st[f"icpt{bi}"].to(dev), bool(meta["binomial"]), device=dev,
                 summary=summary)))

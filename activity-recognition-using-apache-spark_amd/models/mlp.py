@@ -201,6 +201,12 @@ class MLPEngine:
                 self.sblock_correct = torch.zeros(nwg, dtype=torch.int32, device=dev)
                 self.dz = torch.zeros(self.B * 8, dtype=torch.int32, device=dev)      # 16 bf16 per row
                 self.h2mask = torch.zeros(self.B * 8, dtype=torch.int32, device=dev)  # 256 bits per row
+                # MFMA-fragment-ordered bf16 copies of W0 / W1 (W0 | W1 | W1^T; mlp.hip frag_pos): the step
+                # kernels load their weight operands from here, one 1 KB-contiguous load per fragment;
+                # every Adam update of the step refreshes them together with Pb
+                H = L.hidden[0]
+                self.Pf = torch.zeros(H * L.in_pad + 2 * H * H, dtype=torch.bfloat16, device=dev)
+                self._pack_frag()
             self.last_bwd = False
             self.last_path = None
             # optional: the two backward branches after the fused forward — dW1 (split-K over the
@@ -216,6 +222,25 @@ class MLPEngine:
     # ---------------------------------------------------------------- native
     def _w(self, flat, name):
         return self.layout.view(flat, name)
+
+    def _frag_args(self):
+        """(dst, W0 offset, W1 offset, K0, H) of the fragment copies, or zeros when the step is off."""
+        if not getattr(self, "step_ok", False):
+            return 0, 0, 0, 0, 0
+        L = self.layout
+        return (self.Pf.data_ptr(), L.by_name["W0"].offset, L.by_name["W1"].offset, L.in_pad, L.hidden[0])
+
+    def _pack_frag(self):
+        """Rebuild the fragment copies from Pb (after anything but the step's Adam wrote Pb)."""
+        if getattr(self, "step_ok", False):
+            dst, o0, o1, k0, h = self._frag_args()
+            _native.kernels().mlp_pack_frag(self.Pb.data_ptr(), dst, o0, o1, k0, h, _native.stream_ptr())
+
+    def refresh_bf16(self):
+        """Pb (+ fragment copies) from the fp32 master P."""
+        if self.native:
+            self.Pb.copy_(self.P.to(torch.bfloat16))
+            self._pack_frag()
 
     def _slab(self, name):
         s = self.layout.by_name[name]
@@ -293,15 +318,15 @@ class MLPEngine:
         w = lambda t, n: self._w(t, n).data_ptr()  # noqa: E731
 
         def fwd():
-            mod.mlp_step_fwd(Xb.data_ptr(), K0, w(Pb, "W0"), w(P, "b0"), w(Pb, "W1"), w(P, "b1"), H, w(Pb, "Wout"),
+            mod.mlp_step_fwd(Xb.data_ptr(), K0, self.Pf.data_ptr(), w(P, "b0"), w(P, "b1"), H, w(Pb, "Wout"),
                              w(P, "bout"), y32.data_ptr(), B, L.num_classes, float(scale), self.dz.data_ptr(),
                              self.h2mask.data_ptr(), self.sslab.data_ptr(), self.sblock_loss.data_ptr(),
                              self.sblock_correct.data_ptr(), _native.stream_ptr())
 
         def bwd():  # also sums the forward's dWout / dbout slabs into G
             off = lambda n: sb + 4 * L.by_name[n].offset  # noqa: E731
-            mod.mlp_step_bwd(self.dz.data_ptr(), self.h2mask.data_ptr(), Xb.data_ptr(), K0, w(Pb, "W1"), H,
-                             w(Pb, "W0"), w(P, "b0"), w(Pb, "Wout"), B, off("W1"), off("W0"), off("b0"), off("b1"),
+            mod.mlp_step_bwd(self.dz.data_ptr(), self.h2mask.data_ptr(), Xb.data_ptr(), K0, self.Pf.data_ptr(), H,
+                             w(P, "b0"), w(Pb, "Wout"), B, off("W1"), off("W0"), off("b0"), off("b1"),
                              total, self.step_count.data_ptr(), self.sslab.data_ptr(), self.sslab.shape[1],
                              w(self.G, "Wout"), w(self.G, "bout"), _native.stream_ptr())
 
@@ -431,7 +456,7 @@ class MLPEngine:
             list(cols[2]), list(cols[0]), [e - a for a, e in zip(cols[0], cols[1])], list(cols[4]), list(cols[3]),
             self.layout.total, self.G.data_ptr(), self.P.data_ptr(), self.m.data_ptr(), self.v.data_ptr(),
             self.Pb.data_ptr(), float(self.lr), b1, b2, float(self.eps), float(self.wd), self.step_count.data_ptr(),
-            int(tick), mode, _native.stream_ptr())
+            int(tick), mode, _native.stream_ptr(), *self._frag_args())
 
     def reduce_grads_native(self):
         """G = the sum of the last batch's gradient slabs (needed before a collective)."""
@@ -485,7 +510,8 @@ class MLPEngine:
             off = lambda n: sb + 4 * L.by_name[n].offset  # noqa: E731
             w = lambda t, n: self._w(t, n).data_ptr()  # noqa: E731
             P, Pb = self.P, self.Pb
-            d = dict(W0=w(Pb, "W0"), b0=w(P, "b0"), W1=w(Pb, "W1"), b1=w(P, "b1"), Wo=w(Pb, "Wout"), bo=w(P, "bout"),
+            d = dict(Wf=self.Pf.data_ptr(), w0_off=L.by_name["W0"].offset, w1_off=L.by_name["W1"].offset,
+                     b0=w(P, "b0"), b1=w(P, "b1"), Wo=w(Pb, "Wout"), bo=w(P, "bout"),
                      dz=self.dz.data_ptr(), mask=self.h2mask.data_ptr(), fslab=self.sslab.data_ptr(),
                      bloss=self.sblock_loss.data_ptr(), bcorr=self.sblock_correct.data_ptr(), gw1=off("W1"),
                      gw0=off("W0"), gb0=off("b0"), gb1=off("b1"), step=self.step_count.data_ptr(),
@@ -541,7 +567,7 @@ class MLPEngine:
         self.v.copy_(st["v"].to(self.v.device))
         if self.native:
             self.step_count.copy_(st["step"].to(self.step_count.device))
-            self.Pb.copy_(self.P.to(torch.bfloat16))
+            self.refresh_bf16()
         else:
             self.t_step = int(st["step"][0])
 
@@ -783,11 +809,37 @@ class MultilayerPerceptronClassifier(Estimator, ClassifierParams):
                 start_epoch, start_step = int(meta["epoch"]), int(meta["step_in_epoch"])
         from ..utils.checkpoint import maybe_inject_fault
 
+        # One HIP graph per epoch (single GPU, native step, no per-step hooks): the epoch's batches
+        # live in static buffers (the shuffled rows are gathered into them), the first epoch runs
+        # eagerly and warms every kernel, the second is captured and every later epoch replays it —
+        # the host is out of the small-batch step loop (batch 256: ~3 launches of ~4 us each per step).
+        use_graph = (eng.native and world_size == 1 and ckpt is None and not os.environ.get("HAR_FAULT_INJECT")
+                     and eng._plan_ok(Xin[:B], y32[:B]) and os.environ.get("HAR_MLP_EPOCH_GRAPH", "1") != "0"
+                     and self.maxIter - start_epoch >= 3)
+        n_used = steps_per_epoch * B
+        if use_graph:
+            Xe = torch.empty(n_used, Xin.shape[1], dtype=Xin.dtype, device=dev)
+            ye = torch.empty(n_used, dtype=y32.dtype, device=dev)
+        epoch_graph = None
         for epoch in range(start_epoch, self.maxIter):
             # data order is a pure function of (seed, rank, epoch): resumable without RNG state
             g = torch.Generator(device="cpu").manual_seed(self.seed + 7919 * rank + 104729 * epoch)
             perm = torch.randperm(N, generator=g).to(dev)
-            Xe, ye = Xin[perm].contiguous(), y32[perm].contiguous()
+            if use_graph:
+                torch.index_select(Xin, 0, perm[:n_used], out=Xe)
+                torch.index_select(y32, 0, perm[:n_used], out=ye)
+                if epoch_graph is not None:
+                    epoch_graph.replay()
+                    continue
+                if epoch > start_epoch:  # second epoch: capture (records, does not run), then replay
+                    epoch_graph = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(epoch_graph):
+                        for s in range(steps_per_epoch):
+                            eng.train_step(Xe[s * B:(s + 1) * B], ye[s * B:(s + 1) * B], global_batch)
+                    epoch_graph.replay()
+                    continue
+            else:
+                Xe, ye = Xin[perm].contiguous(), y32[perm].contiguous()
             for s in range(start_step if epoch == start_epoch else 0, steps_per_epoch):
                 gstep = epoch * steps_per_epoch + s
                 maybe_inject_fault(gstep, rank)

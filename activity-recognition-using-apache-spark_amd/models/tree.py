@@ -276,8 +276,12 @@ FORCE_LEVEL_SYNC = False
 # host timestamps of the last device level loop: (start, every level enqueued, node counts read back)
 LAST_LEVEL_TIMES = (0.0, 0.0, 0.0)
 # device -> host count reads the level loops have made (0 per fit when every level runs on the device
-# counts; tests/test_gpu_distributed.py checks the data-parallel fits)
+# counts; a data-parallel fit reads one 16-byte record per level: tests/test_gpu_distributed.py)
 LEVEL_SYNCS = 0
+# data parallel: read each level's node count (16 bytes) so the histogram collectives carry the real
+# nodes only, in fp16 when exact; False = the r3 behaviour (collectives sized by the host bound
+# min(2^depth x trees, trees x rows), no reads) — kept for the byte comparison (HAR_TREE_DP_BOUND=1)
+DP_COUNT_READS = os.environ.get("HAR_TREE_DP_BOUND", "0") != "1"
 
 
 def _levels_device_frontier(b: "ForestBuilder", y32, W, N: int, F: int, m: int, maxn: int, stats, feature, thresh,
@@ -322,7 +326,9 @@ def _levels_device_frontier(b: "ForestBuilder", y32, W, N: int, F: int, m: int, 
     nch = mod.tree_level_group_chunks(N)
     nch_g = mod.tree_level_group_chunks(n_all)  # rank-independent bound checks (DP: every rank decides alike)
     planned = not FORCE_NODE_BLOCKS
-    async_ok = planned and not FORCE_SORT_GROUPING and not FORCE_LEVEL_SYNC
+    # data parallel: ONE 16-byte count read per level, so every collective is sized by the level's
+    # real node count (not the bound 2^depth x trees) and may travel as fp16 (DP_COUNT_READS)
+    async_ok = planned and not FORCE_SORT_GROUPING and not FORCE_LEVEL_SYNC and not (dp and DP_COUNT_READS)
     slot_bytes = 4 * F * b.max_bins * K
     subtract = planned and not dp and m >= F and SIBLING_SUBTRACTION and Tn * N >= SUBTRACT_MIN_PAIRS
     hprev = parent_of = derive_from = None  # the previous level's store and this level's derive info
@@ -389,7 +395,7 @@ def _levels_device_frontier(b: "ForestBuilder", y32, W, N: int, F: int, m: int, 
             res = T.hist_split_planned_dp(b.bins, b.nbins, y32, rows, row_w, starts, counts, feats, K, b.max_bins,
                                           b.min_inst, b.min_gain, b.impurity, rows_bound=Tn * N, a_dev=a_dev,
                                           allreduce=None if b.owner is not None else b.allreduce, owner=b.owner,
-                                          bins_rm=bins_rm)
+                                          bins_rm=bins_rm, max_weight=max_w if exact else -1.0)
         elif planned:
             # one device: work items by rows (big nodes chunked), no host sync (ops/tree.py)
             res = T.hist_split_planned(b.bins, b.nbins, y32, rows, row_w, starts, counts, feats, K, b.max_bins,
@@ -741,24 +747,48 @@ def max_lockstep_trees(n_rows: int) -> int:
     return max(1, LOCKSTEP_SLOT_LIMIT // max(1, n_rows))
 
 
+# "auto" tree parallelism while the replicated fp32 feature matrix stays below this (every rank holds it)
+TREE_PARALLEL_MAX_BYTES = 16 << 30
+
+
 class RandomForestClassifier(_TreeEstimatorBase):
-    _param_names = _TreeEstimatorBase._param_names + ("numTrees", "featureSubsetStrategy", "subsamplingRate")
+    _param_names = _TreeEstimatorBase._param_names + ("numTrees", "featureSubsetStrategy", "subsamplingRate",
+                                                      "parallelism")
 
     def __init__(self, featuresCol="features", labelCol="label", numTrees: int = 20, maxDepth: int = 5,
                  maxBins: int = 32, minInstancesPerNode: int = 1, minInfoGain: float = 0.0, impurity: str = "gini",
-                 featureSubsetStrategy: str = "auto", subsamplingRate: float = 1.0, seed: int = 0, device=None):
+                 featureSubsetStrategy: str = "auto", subsamplingRate: float = 1.0, seed: int = 0, device=None,
+                 parallelism: str = "auto"):
         super().__init__(new_uid("RandomForestClassifier"))
         self.featuresCol, self.labelCol = featuresCol, labelCol
         self.numTrees, self.maxDepth, self.maxBins = numTrees, maxDepth, maxBins
         self.minInstancesPerNode, self.minInfoGain, self.impurity = minInstancesPerNode, minInfoGain, impurity
         self.featureSubsetStrategy, self.subsamplingRate = featureSubsetStrategy, subsamplingRate
         self.seed, self.device = seed, device
+        # multi-GPU strategy under data_parallel: "data" = row shards + per-level owner reduction,
+        # "tree" = every rank all rows, numTrees / P trees, one all-gather; "auto" = tree when the
+        # replicated feature matrix is small (TREE_PARALLEL_MAX_BYTES) and there are >= P trees
+        self.parallelism = parallelism
+
+    def resolve_parallelism(self, n_rows: int, n_features: int, world: int) -> str:
+        p = str(self.parallelism).lower()
+        if p not in ("auto", "data", "tree"):
+            raise ValueError(f"parallelism must be auto, data or tree, got {self.parallelism!r}")
+        if p != "auto":
+            return p
+        fits = n_rows * n_features * 4 <= TREE_PARALLEL_MAX_BYTES
+        return "tree" if (fits and self.numTrees >= world) else "data"
 
     def fit(self, table: Table) -> RandomForestClassificationModel:
         X, y, K = self._prep(table)
-        if dp_context() is None:
+        ctx = dp_context()
+        if ctx is None:
             return self.fit_tensors(X, y, K)
         thr = T.thresholds_for(X, self.maxBins, seed=self.seed)
+        if self.resolve_parallelism(X.shape[0], X.shape[1], ctx.world_size) == "tree":
+            from ..parallel.data_parallel import fit_forest_tree_parallel
+
+            return fit_forest_tree_parallel(self, X, y, K, ctx, thresholds=thr)
         lo, hi = dp_rows(X.shape[0])
         return self.fit_tensors(X[lo:hi], y[lo:hi], K, row_offset=lo, thresholds=thr, owner=dp_owner())
 

@@ -24,6 +24,8 @@ from __future__ import annotations
 
 import os
 
+from typing import Optional
+
 import torch
 
 from . import _native
@@ -75,8 +77,17 @@ def unpack_bucket(bucket: torch.Tensor, n_loss: int, g_shape):
     return bucket[:n].view(g_shape), loss
 
 
+MAX_NATIVE_CLASSES = 16  # class rows of the logreg_qn.hip kernels (KP = 8 / 16)
+
+
 def _kp(K: int) -> int:
     return 8 if K <= 8 else 16
+
+
+def native_classes_ok(K: int) -> bool:
+    """True when the device LR kernels take K classes; wider fits use the torch objective on the
+    same device (dense GEMMs) with the same L-BFGS / OWL-QN algorithm (optim/lbfgs.py)."""
+    return K <= MAX_NATIVE_CLASSES
 
 
 def hybrid_index(hm):
@@ -97,8 +108,10 @@ class LogregDesign:
     """Device data of one fit: the hybrid feature layout, labels, per-spec row weights, the
     one-hot CSC row lists (+ their row slices) and the column map of the gradient kernel."""
 
-    def __init__(self, hm, y: torch.Tensor, rw, K: int):
+    def __init__(self, hm, y: torch.Tensor, rw, K: int, native: Optional[bool] = None):
         self.hm = hm
+        # the HIP kernels serve this design (GPU, <= 16 classes); else the torch objective on its device
+        self.native = (hm.device.type == "cuda" and native_classes_ok(K)) if native is None else bool(native)
         self.N, self.F = hm.n_rows, hm.n_features
         self.Fd, self.C = int(hm.dense.shape[1]), int(hm.cat.shape[1])
         self.K = K
@@ -154,7 +167,7 @@ class LogregDesign:
         fp64 product.  Every sum in a fixed order."""
         S_, N, F, K = self.S, self.N, self.F, self.K
         dev = self.device
-        if dev.type == "cuda":
+        if self.native:
             mod, st = _native.kernels(), _native.stream_ptr()
             nt = mod.logreg_summary_tiles(N)
             part = torch.empty(S_, max(1, nt), 2 * self.Fd + K + 1, dtype=torch.float64, device=dev)

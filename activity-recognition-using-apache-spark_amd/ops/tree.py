@@ -423,30 +423,43 @@ def hist_split_planned(bins, nbins_feat, label, rows, row_w, node_start, node_co
     return _best_chunk(gain, feat, bin_, left, total, A, chunks, K)
 
 
+# integer-valued histogram counts up to this are exact in fp16 (DP wire format of small levels)
+FP16_EXACT_MAX = 2048.0
+
+
 def hist_split_planned_dp(bins, nbins_feat, label, rows, row_w, node_start, node_count, feats, K, max_bins,
                           min_instances, min_info_gain, impurity, rows_bound: int, a_dev: int, allreduce=None,
-                          owner=None, bins_rm=None, prows: int = PLAN_ROWS) -> LevelResult:
-    """The data-parallel level on the planned path, with no host read: ``feats.shape[0]`` = A is the
-    host-known node BOUND of the level (identical on every rank), ``a_dev`` the device count.
+                          owner=None, bins_rm=None, prows: int = PLAN_ROWS, max_weight: float = -1.0) -> LevelResult:
+    """The data-parallel level on the planned path.  ``feats.shape[0]`` = A is the level's node count:
+    EXACT when ``a_dev`` is 0 (the level loop read its 16-byte count record back), else a bound shared
+    by every rank with ``a_dev`` pointing at the device count.
 
-    1. the row-balanced work items of ``hist_split_planned`` add this rank's histograms into a
-       zeroed per-node store [A, m, bins, K] (kernel mode 6: histogram only);
+    1. the row-balanced work items of ``hist_split_planned`` write this rank's per-node histograms
+       into the store [A, m, bins, K] (kernel mode 6: a node of one work item stores its slot, the
+       chunks of a big node add into their slot, zeroed by the plan — no fill of the whole store);
     2. the store is summed across ranks — ``allreduce`` (every rank then searches every node) or
-       ``owner.reduce_scatter`` (rank r receives the summed slice of nodes [a0, a1));
-    3. split search from the (slice of the) reduced store (mode 7; nodes >= the device count exit);
-    4. owner: the slice's winners, packed [n, 3 + 2K] (``pack_level``), travel in ONE all-gather.
-    Every collective is sized by the bound A, so the loop never needs the real count on the host;
-    winners of the bound's surplus rows are never read (the decide / frontier kernels stop at the
-    device count)."""
+       ``owner.reduce_scatter_store`` (rank r receives the summed slice of nodes [a0, a1)), straight
+       from the store (allocated with the owner padding; no staging copy on RCCL).  With the exact
+       count every collective carries real nodes only, and when ``max_weight`` (the largest candidate
+       node's weight, known with the count) is <= 2048 the counts travel as fp16 — integer-valued
+       (bootstrap x fold weights), so exact — halving the wire bytes again;
+    3. split search from the (slice of the) reduced store (mode 7);
+    4. owner: the slice's winners, packed [n, 3 + 2K] (``pack_level``), travel in ONE all-gather."""
     A, m = feats.shape
     F, N = bins.shape
     fc = max(1, min(m, LDS_BUDGET // (max_bins * K * 4)))
     chunks = (m + fc - 1) // fc
     dev = bins.device
+    exact = a_dev == 0
     items_ub = A + rows_bound // prows
     plan = torch.empty(4 + (A + 1) + 3 * A + items_ub, dtype=torch.int32, device=dev)
     slot = m * max_bins * K
-    store = torch.zeros(A * slot, dtype=torch.float32, device=dev)
+    P = owner.ctx.world_size if owner is not None else 1
+    S = max(1, -(-A // P))
+    if exact:  # every slot is written by its node's items: no zero fill (owner padding never read)
+        store = torch.empty((P * S if owner is not None else A) * slot, dtype=torch.float32, device=dev)
+    else:      # bound: the surplus slots past the device count must sum to zero
+        store = torch.zeros(A * slot, dtype=torch.float32, device=dev)
     mod, st = _native.kernels(), _native.stream_ptr()
     mod.tree_plan(node_count.data_ptr(), A, prows, plan.data_ptr(), slot, store.data_ptr(), max(1, A), 1, a_dev, st)
     bptr, row_major = (bins_rm.data_ptr(), 1) if bins_rm is not None else (bins.data_ptr(), 0)
@@ -468,12 +481,21 @@ def hist_split_planned_dp(bins, nbins_feat, label, rows, row_w, node_start, node
 
     full = outs(A)
     launch(6, A, 0, store.data_ptr(), feats.data_ptr(), full, items_ub)
+    narrow = exact and 0 <= max_weight <= FP16_EXACT_MAX
     if owner is None:
         if allreduce is not None:
-            allreduce(store)
+            if narrow:
+                h = store.to(torch.float16)
+                allreduce(h)
+                store.copy_(h)
+            else:
+                allreduce(store)
         launch(7, A, 0, store.data_ptr(), feats.data_ptr(), full, A)
         return _best_chunk(*full, A, chunks, K)
-    local, a0, a1 = owner.reduce_scatter(store.view(A, slot))
+    if exact:
+        local, a0, a1 = owner.reduce_scatter_store(store.view(P * S, slot), A, narrow)
+    else:
+        local, a0, a1 = owner.reduce_scatter(store.view(A, slot))
     n = a1 - a0
     if n > 0:
         loc = local[:n].contiguous()

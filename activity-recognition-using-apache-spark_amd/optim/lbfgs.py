@@ -160,6 +160,7 @@ class TrialResult:
     iterations: torch.Tensor  # [B]
     n_evals: int              # batched evaluations (each covers B x T trial points)
     history: list             # per-iteration mean objective
+    history_per_model: list = None  # [B] lists: each model's own objective per iteration
 
 
 def _reg_value(x, l2v, l1v):
@@ -202,7 +203,7 @@ def minimize_trials(evaluate, x0: torch.Tensor, l2v: torch.Tensor, l1v: Optional
     scale = torch.ones(B, device=dev)
     steep = torch.zeros(B, dtype=torch.bool, device=dev)
     head, filled, n_evals = 0, 0, 1
-    history = [float(Fo.mean())]
+    fhist = [Fo.clone()]  # per-model objectives, read back once at the end (no per-iteration sync)
     pg_fn = lambda xx, gg: _pseudo_grad(xx, gg, l1v)  # noqa: E731
     for it in range(max_iter):
         pg = pg_fn(x, g)
@@ -279,7 +280,9 @@ def minimize_trials(evaluate, x0: torch.Tensor, l2v: torch.Tensor, l1v: Optional
         active = active & ~(take & conv) & ~(fails >= 2)
         head = (head + 1) % m
         filled = min(filled + 1, m)
-        history.append(float(Fo.mean()))
+        fhist.append(Fo.clone())
         if poll and (it + 1) % poll == 0 and not bool(active.any()):
             break
-    return TrialResult(x=x, f=Fo, iterations=iters, n_evals=n_evals, history=history)
+    H = torch.stack(fhist).cpu()  # [iterations + 1, B]
+    return TrialResult(x=x, f=Fo, iterations=iters, n_evals=n_evals, history=H.mean(1).tolist(),
+                       history_per_model=[H[:, b].tolist() for b in range(B)])

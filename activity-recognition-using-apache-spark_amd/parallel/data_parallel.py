@@ -141,6 +141,26 @@ class NodeOwner:
         self.stats["bytes"] += src.numel() * src.element_size()
         return out.to(hist.device).view(S, *hist.shape[1:]), a0, a1
 
+    def reduce_scatter_store(self, store: torch.Tensor, A: int, narrow: bool = False):
+        """Owner reduction of a per-node store that already has the owner padding ([P * S, w], rows
+        past A never read): no staging copy when the store lives where the backend reduces (device
+        tensors under RCCL); ``narrow`` sends it as fp16 (the caller guarantees exact values).
+        Returns (this rank's summed slice [S, w] fp32, a0, a1)."""
+        P, r = self.ctx.world_size, self.ctx.rank
+        S = max(1, -(-A // P))
+        a0, a1 = min(A, r * S), min(A, (r + 1) * S)
+        if P == 1:
+            return store[:A], 0, A
+        w = store.shape[1]
+        dev = self._dev() or store.device
+        dt = torch.float16 if narrow else store.dtype
+        src = store if (store.device == torch.device(dev) and dt == store.dtype) else store.to(dev, dt)
+        out = self._buf("rs_out16" if narrow else "rs_out", S * w, dt, dev).view(S, w)
+        dist.reduce_scatter_tensor(out, src, group=self.ctx.group)
+        self.stats["reduce_scatter"] += 1
+        self.stats["bytes"] += src.numel() * src.element_size()
+        return out.to(store.device, torch.float32), a0, a1
+
     def all_gather(self, local: torch.Tensor, A: int) -> torch.Tensor:
         P = self.ctx.world_size
         if P == 1:
@@ -170,13 +190,16 @@ def fit_forest_dp(estimator, X_shard, y_shard, num_classes: int, row_offset: int
                                  thresholds=thr)
 
 
-def fit_forest_tree_parallel(estimator, X, y, num_classes: int, ctx: DistContext, thresholds=None):
+def fit_forest_tree_parallel(estimator, X, y, num_classes: int, ctx: DistContext, thresholds=None, stats=None):
     """Tree parallelism: every rank holds ALL rows and grows its contiguous
     slice of the forest's trees — keyed by global tree id, so bootstraps and feature subsets
-    are those of the single-process forest — with zero communication until ONE all-gather of
-    the node arrays at the end.  The result equals the single-process forest.  Pays when the
-    data fits every GPU (288 GB each) and trees are many; row-sharded DP (``fit_forest_dp``)
-    pays when rows are many."""
+    are those of the single-process forest — with zero communication until ONE all-gather at the
+    end: each rank packs its node arrays (feature, threshold, children, class stats, gains, node
+    counts, depth) as 32-bit words into one [trees-per-rank, words] buffer.  The result equals the
+    single-process forest.  Pays when the binned table fits every GPU (288 GB each: config 5's
+    480k x 165 features is ~80 MB) — per-level communication is then zero; row-sharded DP
+    (``fit_forest_dp``) pays when rows are too many to replicate.  ``stats`` (a dict) receives the
+    collective count and bytes."""
     from ..models.tree import ForestArrays, RandomForestClassificationModel
 
     T_, P, r = estimator.numTrees, ctx.world_size, ctx.rank
@@ -188,25 +211,50 @@ def fit_forest_tree_parallel(estimator, X, y, num_classes: int, ctx: DistContext
         return part
     a = part.arrs
     S = -(-T_ // P)  # trees per rank, padded
+    Tr, maxn = a.feature.shape
+    K = a.stats.shape[2]
+    dev = ctx.device if ctx.backend == "nccl" else torch.device("cpu")
 
-    def gather(t: torch.Tensor) -> torch.Tensor:
-        buf = torch.zeros((S,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
-        buf[: t.shape[0]] = t
-        src = buf if (buf.is_cuda or ctx.backend != "nccl") else buf.to(ctx.device)
-        out = torch.empty((P * S,) + tuple(t.shape[1:]), dtype=t.dtype, device=src.device)
-        dist.all_gather_into_tensor(out, src, group=ctx.group)
-        keep = torch.cat([torch.arange(q * S, q * S + (T_ * (q + 1)) // P - (T_ * q) // P) for q in range(P)])
-        return out[keep.to(out.device)].to(t.device)
+    def words(t: torch.Tensor) -> torch.Tensor:  # [Tr, ...] -> [Tr, w] int32 words
+        t = t.to(dev).contiguous()
+        n = int(np.prod(t.shape[1:])) if t.dim() > 1 else 1
+        return (t.view(torch.int32) if t.dtype in (torch.int32, torch.float32) else t.to(torch.int32)).reshape(Tr, n)
 
-    nn = torch.as_tensor(a.n_nodes, dtype=torch.int64, device=a.feature.device)
-    md = torch.tensor([a.max_depth], device=a.feature.device)
-    mds = torch.empty(P, dtype=md.dtype, device=md.device)
-    dist.all_gather_into_tensor(mds, md if (md.is_cuda or ctx.backend != "nccl") else md.to(ctx.device),
-                                group=ctx.group)
-    full = ForestArrays(gather(a.feature), gather(a.threshold), gather(a.left), gather(a.right), gather(a.stats),
-                        gather(nn.view(-1, 1)).view(-1).cpu().numpy(), int(mds.max()),
-                        gather(a.gain) if a.gain is not None else None)
-    return RandomForestClassificationModel(full, X.shape[1], num_classes, uid=estimator.uid, device=X.device)
+    gain = a.gain if a.gain is not None else torch.zeros(Tr, maxn, device=a.feature.device)
+    nn = torch.as_tensor(np.asarray(a.n_nodes), dtype=torch.int32)
+    depth = torch.full((Tr, 1), int(a.max_depth), dtype=torch.int32)
+    cols = [words(a.feature), words(a.threshold), words(a.left), words(a.right), words(a.stats), words(gain),
+            words(nn.view(-1, 1)), words(depth)]
+    w = sum(c.shape[1] for c in cols)
+    buf = torch.zeros(S, w, dtype=torch.int32, device=dev)
+    if Tr:
+        buf[:Tr] = torch.cat(cols, dim=1)
+    out = torch.empty(P * S, w, dtype=torch.int32, device=dev)
+    dist.all_gather_into_tensor(out, buf, group=ctx.group)
+    if stats is not None:
+        stats["all_gather"] = stats.get("all_gather", 0) + 1
+        stats["bytes"] = stats.get("bytes", 0) + out.numel() * 4
+    keep = torch.cat([torch.arange(q * S, q * S + (T_ * (q + 1)) // P - (T_ * q) // P) for q in range(P)])
+    full = out[keep.to(out.device)].to(a.feature.device)
+    o = 0
+
+    def take(n: int, dtype, shape):
+        nonlocal o
+        v = full[:, o:o + n].contiguous()
+        o += n
+        v = v.view(torch.float32) if dtype == torch.float32 else v
+        return v.reshape((T_,) + shape)
+
+    feature = take(maxn, torch.int32, (maxn,))
+    threshold = take(maxn, torch.float32, (maxn,))
+    left = take(maxn, torch.int32, (maxn,))
+    right = take(maxn, torch.int32, (maxn,))
+    st = take(maxn * K, torch.float32, (maxn, K))
+    g = take(maxn, torch.float32, (maxn,))
+    n_nodes = take(1, torch.int32, (1,)).view(-1).cpu().numpy().astype(np.int64)
+    max_depth = int(take(1, torch.int32, (1,)).max())
+    arrs = ForestArrays(feature, threshold, left, right, st, n_nodes, max_depth, g if a.gain is not None else None)
+    return RandomForestClassificationModel(arrs, X.shape[1], num_classes, uid=estimator.uid, device=X.device)
 
 
 def fit_mlp_dp(estimator, X_shard, y_shard, ctx: DistContext, num_classes: Optional[int] = None):

@@ -51,9 +51,14 @@ def init(expected_world: Optional[int] = None, backend: Optional[str] = None, de
     if expected_world is not None and world != expected_world and world > 1:
         raise RuntimeError(f"launched with WORLD_SIZE={world} but --gpus {expected_world}")
     use_cuda = torch.cuda.is_available() and (device is None or str(device).startswith("cuda"))
+    # rehearsal of an N-rank job on fewer GPUs (e.g. 8 gloo ranks on one MI355X): HAR_DIST_SHARE_DEVICE=1
+    # puts every rank on cuda:0, HAR_DIST_BACKEND picks the backend (gloo: host-staged collectives)
+    share = os.environ.get("HAR_DIST_SHARE_DEVICE", "0") == "1"
+    backend = backend or os.environ.get("HAR_DIST_BACKEND") or None
     if use_cuda:
-        torch.cuda.set_device(local_rank)
-        dev = torch.device("cuda", local_rank)
+        dev_index = 0 if share else local_rank
+        torch.cuda.set_device(dev_index)
+        dev = torch.device("cuda", dev_index)
     else:
         dev = torch.device("cpu")
     be = None
@@ -79,7 +84,7 @@ def init(expected_world: Optional[int] = None, backend: Optional[str] = None, de
 def barrier(ctx: DistContext):
     if ctx.is_distributed:
         if ctx.backend == "nccl":
-            dist.barrier(device_ids=[ctx.local_rank])
+            dist.barrier(device_ids=[ctx.device.index])
         else:
             dist.barrier()
 

@@ -65,7 +65,8 @@ def build_estimator(name: str, cfg: RunConfig, dev, n_features: int, n_classes: 
                                       maxBins=cfg.max_bins, device=dev)
     if name == "rf":
         return RandomForestClassifier(featuresCol="features", labelCol="label", numTrees=cfg.rf_num_trees,
-                                      maxDepth=cfg.rf_max_depth, maxBins=cfg.max_bins, seed=cfg.seed, device=dev)
+                                      maxDepth=cfg.rf_max_depth, maxBins=cfg.max_bins, seed=cfg.seed, device=dev,
+                                      parallelism=cfg.rf_parallel)
     if name == "nb":
         return NaiveBayes(modelType=cfg.nb_model_type, device=dev)
     if name == "mlp":

@@ -67,10 +67,10 @@ class ParamGridBuilder:
 def _lr_margins(models, hm) -> torch.Tensor:
     """Raw predictions ``[n, N, K]`` of n logistic-regression models (binomial: ``[-m, m]``): one
     launch of the evaluation kernel in prediction mode on the GPU."""
-    k = models[0].coefficientMatrix.shape[0]
-    if hm.device.type == "cuda":
-        from ..ops.logreg import logreg_margins_native
+    from ..ops.logreg import logreg_margins_native, native_classes_ok
 
+    k = models[0].coefficientMatrix.shape[0]
+    if hm.device.type == "cuda" and native_classes_ok(k):
         KP = 8 if k <= 8 else 16
         # one batched weight table [n, F+1, KP] (row F = intercepts) instead of one per model
         coef = torch.stack([m.coefficientMatrix for m in models]).to(hm.device)

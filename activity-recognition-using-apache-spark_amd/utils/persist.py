@@ -127,7 +127,7 @@ def _build(md, t, children, device):
         eng = MLPEngine(st["layers"], 4096, d)
         eng.P.copy_(t["params"].to(d))
         if eng.native:
-            eng.Pb.copy_(eng.P.to(torch.bfloat16))
+            eng.refresh_bf16()
         m = MultilayerPerceptronClassificationModel(eng, uid=uid)
         m.mean = t.get("mean")
         m.inv_std = t.get("inv_std")

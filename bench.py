@@ -313,6 +313,7 @@ def bench_rf(args, ctx, nine_axis=False, single_tree=False):
     from har.data.synth import StreamSpec
     from har.models import tree as tree_mod
     from har.models.tree import DecisionTreeClassifier, RandomForestClassifier
+    from har.ops import tree as T
     from har.parallel import data_parallel as dp
     from har.parallel import dist as hdist
 
@@ -321,7 +322,19 @@ def bench_rf(args, ctx, nine_axis=False, single_tree=False):
     spec = StreamSpec(num_classes=K, axes=9 if nine_axis else 3, hz=50.0 if nine_axis else 20.0,
                       window=500 if nine_axis else 200, seed=2018)
     n_local = args.rows
-    X, y = _featurized(n_local, spec, dev, first_window=rank * n_local)
+    n_trees = args.trees or (500 if nine_axis else 100)
+    # tree parallel (every rank: ALL n_local * N rows, n_trees / N trees, one all-gather) or data
+    # parallel (rank's n_local rows, all trees, per-level reduce-scatter + all-gather); "auto" = tree
+    # while the replicated table is small (its features fit every GPU many times over here)
+    probe = RandomForestClassifier(numTrees=n_trees, parallelism=args.rf_parallel)
+    from har.features.window import n_features
+
+    n_feat = n_features(spec.axes) if nine_axis else N_FEATURES
+    mode = "data" if single_tree else probe.resolve_parallelism(n_local * world, n_feat, world)
+    if mode == "tree":  # the whole table, identical on every rank (windows keyed by global id)
+        X, y = _featurized(n_local * world, spec, dev, first_window=0)
+    else:
+        X, y = _featurized(n_local, spec, dev, first_window=rank * n_local)
     if not nine_axis:
         X = X[:, :N_FEATURES].contiguous()  # the WISDM-43 feature set
     Xt, yt = _featurized(4096, spec, dev, first_window=10 ** 9)
@@ -332,14 +345,19 @@ def bench_rf(args, ctx, nine_axis=False, single_tree=False):
         tree_mod.SUBTRACT_MIN_PAIRS = 0  # measure the subtraction at every size
         est = DecisionTreeClassifier(maxDepth=args.depth, maxBins=32, device=dev)
     else:
-        est = RandomForestClassifier(numTrees=args.trees or (500 if nine_axis else 100), maxDepth=args.depth,
-                                     maxBins=32, seed=7, device=dev)
+        est = RandomForestClassifier(numTrees=n_trees, maxDepth=args.depth, maxBins=32, seed=7, device=dev,
+                                     parallelism=mode)
     model = {}
 
-    owner = dp.NodeOwner(ctx) if (args.rf_reduce == "owner" and ctx.is_distributed) else None
+    owner = dp.NodeOwner(ctx) if (mode == "data" and args.rf_reduce == "owner" and ctx.is_distributed) else None
+    tp_stats = {}
 
     def run(i):
         # the whole fit is timed, findSplits included (sample all-gather + device sort + binning)
+        if mode == "tree":
+            thr = T.thresholds_for(X, 32, seed=7)  # the whole table is local: no collective
+            model["m"] = dp.fit_forest_tree_parallel(est, X, y, K, ctx, thresholds=thr, stats=tp_stats)
+            return
         thr = dp.global_thresholds(X, 32, ctx, seed=7)
         model["m"] = est.fit_tensors(X, y, K, allreduce=None if owner else dp.allreduce_sum(ctx),
                                      row_offset=rank * n_local, thresholds=thr, owner=owner)
@@ -347,6 +365,12 @@ def bench_rf(args, ctx, nine_axis=False, single_tree=False):
     elapsed = timed(ctx, run, args.steps, args.warmup, dev)
     acc = float((model["m"].predict(Xt) == yt).float().mean())
     rows = n_local * world
+    if mode == "tree" and world > 1:
+        coll = {k: v / (args.steps + args.warmup) for k, v in tp_stats.items()}
+    elif owner is not None:
+        coll = {k: v / (args.steps + args.warmup) for k, v in owner.stats.items()}
+    else:
+        coll = None
     if single_tree:
         name = (f"WISDM 6-class DecisionTree depth {args.depth} (all features, sibling subtraction "
                 f"{'off' if args.no_subtract else 'on'})")
@@ -361,9 +385,9 @@ def bench_rf(args, ctx, nine_axis=False, single_tree=False):
                     f"({X.shape[1]} features, {K} classes)",
             "config": {"model": name, "global_batch": rows, "seq_len": spec.window, "parallelism": f"dp{world}"},
             "test_accuracy": hdist.mean_over_ranks(ctx, acc), "test_accuracy_data": "held-out synthetic windows",
-            "dtype": "fp32", "histogram_reduction": args.rf_reduce if world > 1 else "none",
-            "collectives_per_step": ({k: v / (args.steps + args.warmup) for k, v in owner.stats.items()}
-                                     if owner is not None else None)}
+            "dtype": "fp32", "rf_parallel": mode,
+            "histogram_reduction": (args.rf_reduce if mode == "data" else "none (tree parallel)") if world > 1 else "none",
+            "collectives_per_step": coll}
 
 
 def bench_stream(args, ctx):
@@ -524,6 +548,10 @@ def main():
     ap.add_argument("--no-subtract", action="store_true", help="--config dt: histogram every node directly")
     ap.add_argument("--rf-reduce", default="owner", choices=["owner", "allreduce"],
                     help="DP forest histograms: reduce-scatter by node owner + all-gather of splits, or all-reduce")
+    ap.add_argument("--rf-parallel", default="auto", choices=["auto", "data", "tree"],
+                    help="forest configs over N GPUs: tree = every rank holds all N x --rows windows and grows "
+                         "numTrees / N trees (one all-gather per fit); data = row shards with per-level histogram "
+                         "reductions; auto = tree while the replicated table is small")
     ap.add_argument("--samples", type=int, default=1_000_000_000, help="stream samples per 8 GPUs")
     ap.add_argument("--samples-per-gpu", type=int, default=0,
                     help="--config stream: samples resident on EVERY GPU (overrides --samples / 8)")

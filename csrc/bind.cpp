@@ -207,8 +207,9 @@ static void logreg_solve_run(const LogregSolvePlan& p, int max_iter, int m, hipS
 // pointers changing (three pybind calls with ~20 arguments each and a region list rebuilt in Python
 // every step were ~10 us of host time per 70 us step: enough to starve the GPU when not graph-captured).
 struct MlpStepPlan {
-  u W0, b0, W1, b1, Wo, bo, dz, mask, fslab, bloss, bcorr, gw1, gw0, gb0, gb1, step, G, Pw, m, v, Pb;
+  u Wf, b0, b1, Wo, bo, dz, mask, fslab, bloss, bcorr, gw1, gw0, gb0, gb1, step, G, Pw, m, v, Pb;
   int K0, H, C, fslab_w;
+  MlpFragSpec frag;
   u gwo, gbo;
   int64_t stride, n;
   float lr, b1c, b2c, eps, wd;
@@ -219,22 +220,22 @@ struct MlpStepPlan {
   void run(u X, u y, int B, float scale, int mode, u stream) {
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     if (mode & 3) {
-      check(har_mlp_step_fwd(P<const uint16_t>(X), K0, P<const uint16_t>(W0), P<const float>(b0),
-                             P<const uint16_t>(W1), P<const float>(b1), H, P<const uint16_t>(Wo), P<const float>(bo),
-                             P<const int32_t>(y), B, C, scale, P<uint32_t>(dz), P<uint32_t>(mask), P<float>(fslab),
-                             P<float>(bloss), P<int32_t>(bcorr), s),
+      check(har_mlp_step_fwd(P<const uint16_t>(X), K0, P<uint16_t>(Wf), P<const float>(b0), P<const float>(b1), H,
+                             P<const uint16_t>(Wo), P<const float>(bo), P<const int32_t>(y), B, C, scale,
+                             P<uint32_t>(dz), P<uint32_t>(mask), P<float>(fslab), P<float>(bloss), P<int32_t>(bcorr),
+                             s),
             "mlp_step_fwd");
       check(har_mlp_step_bwd(P<const uint32_t>(dz), P<const uint32_t>(mask), P<const uint16_t>(X), K0,
-                             P<const uint16_t>(W1), H, P<const uint16_t>(W0), P<const float>(b0),
-                             P<const uint16_t>(Wo), B, P<float>(gw1), P<float>(gw0), P<float>(gb0), P<float>(gb1),
-                             stride, P<int32_t>(step), P<const float>(fslab), fslab_w, P<float>(gwo), P<float>(gbo), s),
+                             P<const uint16_t>(Wf), H, P<const float>(b0), P<const uint16_t>(Wo), B, P<float>(gw1),
+                             P<float>(gw0), P<float>(gb0), P<float>(gb1), stride, P<int32_t>(step),
+                             P<const float>(fslab), fslab_w, P<float>(gwo), P<float>(gbo), s),
             "mlp_step_bwd");
     }
     const int gm = mode == 1 ? 1 | 4 : mode == 2 ? 1 | 2 : 4;  // GR_REDUCE 1, GR_STORE 2, GR_ADAM 4
     const int k = (gm & 1) ? (int)src.size() : 0;
     check(har_grad_reduce_adam(k, src.data(), start.data(), len.data(), lds.data(), S.data(), n, P<float>(G),
                                P<float>(Pw), P<float>(m), P<float>(v), P<uint16_t>(Pb), lr, b1c, b2c, eps, wd,
-                               P<int32_t>(step), 0, gm, s),
+                               P<int32_t>(step), 0, gm, &frag, s),
           "grad_reduce_adam");
   }
 };
@@ -565,7 +566,8 @@ PYBIND11_MODULE(_har_native, m) {
   m.def("grad_reduce_adam", [](std::vector<u> src, std::vector<int64_t> start, std::vector<int64_t> len,
                                std::vector<int64_t> lds, std::vector<int> nsl, int64_t n, u G, u param, u mm, u vv,
                                u pb, float lr, float b1, float b2, float eps, float wd, u step, int tick, int mode,
-                               u stream) {
+                               u stream, u frag_dst, int64_t w0_off, int64_t w1_off, int fK0, int fH) {
+    const MlpFragSpec frag{P<uint16_t>(frag_dst), w0_off, w1_off, fK0, fH};
     const int k = (int)src.size();
     if ((int)start.size() != k || (int)len.size() != k || (int)lds.size() != k || (int)nsl.size() != k)
       throw std::runtime_error("grad_reduce_adam: region lists differ in length");
@@ -573,8 +575,15 @@ PYBIND11_MODULE(_har_native, m) {
     for (int i = 0; i < k; ++i) sp[i] = P<const float>(src[i]);
     check(har_grad_reduce_adam(k, sp.data(), start.data(), len.data(), lds.data(), nsl.data(), n, P<float>(G),
                                P<float>(param), P<float>(mm), P<float>(vv), P<uint16_t>(pb), lr, b1, b2, eps, wd,
-                               P<int32_t>(step), tick, mode, S(stream)),
+                               P<int32_t>(step), tick, mode, frag_dst ? &frag : nullptr, S(stream)),
           "grad_reduce_adam");
+  }, py::arg("src"), py::arg("start"), py::arg("len"), py::arg("lds"), py::arg("nsl"), py::arg("n"), py::arg("G"),
+     py::arg("param"), py::arg("m"), py::arg("v"), py::arg("pb"), py::arg("lr"), py::arg("b1"), py::arg("b2"),
+     py::arg("eps"), py::arg("wd"), py::arg("step"), py::arg("tick"), py::arg("mode"), py::arg("stream"),
+     py::arg("frag_dst") = 0, py::arg("w0_off") = 0, py::arg("w1_off") = 0, py::arg("fK0") = 0, py::arg("fH") = 0);
+  m.def("mlp_pack_frag", [](u pb, u dst, int64_t w0_off, int64_t w1_off, int K0, int H, u stream) {
+    const MlpFragSpec f{P<uint16_t>(dst), w0_off, w1_off, K0, H};
+    check(har_mlp_pack_frag(P<const uint16_t>(pb), &f, S(stream)), "mlp_pack_frag");
   });
   m.def("reduce_slabs_multi", [](std::vector<u> slabs, std::vector<int> nsl, std::vector<int64_t> n,
                                  std::vector<int64_t> lds, std::vector<u> dst, std::vector<int64_t> ldd, int G,
@@ -596,10 +605,10 @@ PYBIND11_MODULE(_har_native, m) {
   py::class_<MlpStepPlan>(m, "MlpStepPlan")
       .def(py::init([](py::dict d) {
         MlpStepPlan p;
-        for (const char* k : {"W0", "b0", "W1", "b1", "Wo", "bo", "dz", "mask", "fslab", "bloss", "bcorr", "gw1", "gw0",
+        for (const char* k : {"Wf", "b0", "b1", "Wo", "bo", "dz", "mask", "fslab", "bloss", "bcorr", "gw1", "gw0",
                               "gb0", "gb1", "step", "G", "P", "m", "v", "Pb"}) {
           const u x = d[k].cast<u>();
-          if (!strcmp(k, "W0")) p.W0 = x; else if (!strcmp(k, "b0")) p.b0 = x; else if (!strcmp(k, "W1")) p.W1 = x;
+          if (!strcmp(k, "Wf")) p.Wf = x; else if (!strcmp(k, "b0")) p.b0 = x;
           else if (!strcmp(k, "b1")) p.b1 = x; else if (!strcmp(k, "Wo")) p.Wo = x; else if (!strcmp(k, "bo")) p.bo = x;
           else if (!strcmp(k, "dz")) p.dz = x; else if (!strcmp(k, "mask")) p.mask = x;
           else if (!strcmp(k, "fslab")) p.fslab = x; else if (!strcmp(k, "bloss")) p.bloss = x;
@@ -621,6 +630,7 @@ PYBIND11_MODULE(_har_native, m) {
         p.b2c = d["beta2"].cast<float>();
         p.eps = d["eps"].cast<float>();
         p.wd = d["wd"].cast<float>();
+        p.frag = MlpFragSpec{P<uint16_t>(p.Wf), d["w0_off"].cast<int64_t>(), d["w1_off"].cast<int64_t>(), p.K0, p.H};
         for (auto r : d["regions"].cast<py::list>()) {  // (start, end, src pointer, #slabs, slab stride)
           auto t = r.cast<py::tuple>();
           const int64_t a = t[0].cast<int64_t>(), e = t[1].cast<int64_t>();
@@ -636,19 +646,19 @@ PYBIND11_MODULE(_har_native, m) {
   m.def("mlp_step_grid", &har_mlp_step_grid);
   m.def("mlp_step_slices", &har_mlp_step_slices);
   m.def("mlp_step_fwd_slab_width", &har_mlp_step_fwd_slab_width);
-  m.def("mlp_step_fwd", [](u X, int K0, u W0, u b0, u W1, u b1, int H, u Wo, u bo, u labels, int B, int C,
-                           float scale, u dz, u mask, u slab, u block_loss, u block_correct, u stream) {
-    check(har_mlp_step_fwd(P<const uint16_t>(X), K0, P<const uint16_t>(W0), P<const float>(b0),
-                           P<const uint16_t>(W1), P<const float>(b1), H, P<const uint16_t>(Wo), P<const float>(bo),
-                           P<const int32_t>(labels), B, C, scale, P<uint32_t>(dz), P<uint32_t>(mask), P<float>(slab),
-                           P<float>(block_loss), P<int32_t>(block_correct), S(stream)),
+  m.def("mlp_step_fwd", [](u X, int K0, u Wf, u b0, u b1, int H, u Wo, u bo, u labels, int B, int C, float scale,
+                           u dz, u mask, u slab, u block_loss, u block_correct, u stream) {
+    check(har_mlp_step_fwd(P<const uint16_t>(X), K0, P<uint16_t>(Wf), P<const float>(b0), P<const float>(b1), H,
+                           P<const uint16_t>(Wo), P<const float>(bo), P<const int32_t>(labels), B, C, scale,
+                           P<uint32_t>(dz), P<uint32_t>(mask), P<float>(slab), P<float>(block_loss),
+                           P<int32_t>(block_correct), S(stream)),
           "mlp_step_fwd");
   });
-  m.def("mlp_step_bwd", [](u dz, u mask, u X, int K0, u W1, int H, u W0, u b0, u Wo, int B, u gw1, u gw0, u gb0,
-                           u gb1, int64_t stride, u tick, u fslab, int fslab_w, u gwo, u gbo, u stream) {
+  m.def("mlp_step_bwd", [](u dz, u mask, u X, int K0, u Wf, int H, u b0, u Wo, int B, u gw1, u gw0, u gb0, u gb1,
+                           int64_t stride, u tick, u fslab, int fslab_w, u gwo, u gbo, u stream) {
     check(har_mlp_step_bwd(P<const uint32_t>(dz), P<const uint32_t>(mask), P<const uint16_t>(X), K0,
-                           P<const uint16_t>(W1), H, P<const uint16_t>(W0), P<const float>(b0), P<const uint16_t>(Wo),
-                           B, P<float>(gw1), P<float>(gw0), P<float>(gb0), P<float>(gb1), stride, P<int32_t>(tick),
+                           P<const uint16_t>(Wf), H, P<const float>(b0), P<const uint16_t>(Wo), B, P<float>(gw1),
+                           P<float>(gw0), P<float>(gb0), P<float>(gb1), stride, P<int32_t>(tick),
                            P<const float>(fslab), fslab_w, P<float>(gwo), P<float>(gbo), S(stream)),
           "mlp_step_bwd");
   });

@@ -46,10 +46,18 @@ int har_softmax_ce_head_blocks(int B);
 // Flat-gradient reduction (+ Adam) of the MLP step (mlp.hip): mode bits 1 = reduce the regions' slabs,
 // 2 = store G, 4 = Adam with t = *step (tick != 0: *step += 1 first, in its own launch).  Regions:
 // sorted, disjoint, 4-aligned [start, start + len), S slabs at src + s * lds.
+// MFMA-fragment-ordered bf16 copies of the step's W0 / W1 (mlp.hip frag_pos): dst = [W0 frag (H*K0) |
+// W1 frag (H*H) | W1^T frag (H*H)], refreshed by every Adam update that is given the spec.
+typedef struct MlpFragSpec {
+  uint16_t* dst;
+  int64_t w0_off, w1_off;  // flat offsets of W0 [H][K0] and W1 [H][H]
+  int K0, H;
+} MlpFragSpec;
 int har_grad_reduce_adam(int nreg, const float* const* src, const int64_t* start, const int64_t* len,
                          const int64_t* lds, const int* S, int64_t n, float* G, float* param, float* m, float* v,
                          uint16_t* pb, float lr, float b1, float b2, float eps, float wd, int32_t* step, int tick,
-                         int mode, hipStream_t s);
+                         int mode, const MlpFragSpec* frag, hipStream_t s);
+int har_mlp_pack_frag(const uint16_t* pb, const MlpFragSpec* f, hipStream_t s);
 int har_adam_step(float* param, const float* grad, const float* slabs, int nslabs, float* m, float* v,
                   uint16_t* param_bf16, int64_t n, float lr, float beta1, float beta2, float eps,
                   float weight_decay, float grad_scale, int32_t* step, int tick, hipStream_t s);
@@ -77,14 +85,16 @@ int har_mlp_fwd_head_grid(int B);
 // per-workgroup loss / #correct; har_mlp_step_bwd rebuilds dact2 from them and writes per row slice
 // s < har_mlp_step_slices(B) the partials of dW1, dW0, db0, db1 at gw1 / gw0 / gb0 / gb1 + s * slab_stride
 // (h1 recomputed from X).
-int har_mlp_step_fwd(const uint16_t* X, int K0, const uint16_t* W0, const float* b0, const uint16_t* W1,
-                     const float* b1, int H, const uint16_t* Wo, const float* bo, const int32_t* labels, int B, int C,
-                     float scale, uint32_t* dz, uint32_t* mask, float* slab, float* block_loss,
-                     int32_t* block_correct, hipStream_t s);
-int har_mlp_step_bwd(const uint32_t* dz, const uint32_t* mask, const uint16_t* X, int K0, const uint16_t* W1, int H,
-                     const uint16_t* W0, const float* b0, const uint16_t* Wo, int B, float* gw1, float* gw0,
-                     float* gb0, float* gb1, int64_t slab_stride, int32_t* tick, const float* fslab, int fslab_w,
-                     float* gwo, float* gbo, hipStream_t s);
+// Wf: the MlpFragSpec::dst fragment copies of W0 / W1 (the step's weight operands); the forward
+// (re)writes the W1^T part from its W1 registers, the backward of the same step reads it.
+int har_mlp_step_fwd(const uint16_t* X, int K0, uint16_t* Wf, const float* b0, const float* b1, int H,
+                     const uint16_t* Wo, const float* bo, const int32_t* labels, int B, int C, float scale,
+                     uint32_t* dz, uint32_t* mask, float* slab, float* block_loss, int32_t* block_correct,
+                     hipStream_t s);
+int har_mlp_step_bwd(const uint32_t* dz, const uint32_t* mask, const uint16_t* X, int K0, const uint16_t* Wf, int H,
+                     const float* b0, const uint16_t* Wo, int B, float* gw1, float* gw0, float* gb0, float* gb1,
+                     int64_t slab_stride, int32_t* tick, const float* fslab, int fslab_w, float* gwo, float* gbo,
+                     hipStream_t s);
 int har_mlp_step_grid(int B);
 int har_mlp_step_slices(int B);
 int har_mlp_step_fwd_slab_width(int H);

@@ -572,7 +572,6 @@ __global__ __launch_bounds__(QN_BLOCK) void qn_direction_kernel(QnArgs a) {
   // the recursion's operands live in LDS: the P1 chunk sums (reduced by NP1 lanes), the Gram
   // matrices, rho and the coefficient vectors (per-lane arrays indexed by slot would spill to scratch)
   __shared__ double p1v[NP1], SY[QN_MAX_M * QN_MAX_M], YY[QN_MAX_M * QN_MAX_M], rho_s[QN_MAX_M];
-  __shared__ double u[QN_MAX_M], w[QN_MAX_M], al[QN_MAX_M];
   __shared__ double stage[QN_MAX_CHUNKS * NP1];
   const bool rec = !a.init && !steep;  // block-uniform
   const int csz = (D + a.nch - 1) / a.nch, e1 = min(D, (c + 1) * csz);
@@ -593,24 +592,32 @@ __global__ __launch_bounds__(QN_BLOCK) void qn_direction_kernel(QnArgs a) {
       SY[i] = syv;
       YY[i] = yyv;
     }
-    if (i < QN_MAX_M) {
-      rho_s[i] = rhv;
-      u[i] = w[i] = al[i] = 0.0;
-    }
+    if (i < QN_MAX_M) rho_s[i] = rhv;
     __syncthreads();
   }
   if (threadIdx.x == 0) {
     float gamma = 0.f;
     for (int j = 0; j < QN_MAX_M; ++j) cS[j] = cY[j] = 0.f;
     if (rec) {  // the two-loop recursion on coefficients
+      // u, w, al in registers (slot-indexed updates as unrolled selects): the Gram rows are the only
+      // LDS reads of a step and issue together, instead of u / w being re-read after every store
+      double ur[QN_MAX_M], wr[QN_MAX_M], alr[QN_MAX_M];
+#pragma unroll
+      for (int k = 0; k < QN_MAX_M; ++k) ur[k] = wr[k] = alr[k] = 0.0;
       for (int i = 0; i < a.filled; ++i) {  // newest -> oldest: q = pg + sum u_k y_k
         const int j = (a.head - 1 - i + mm) % mm;
         const double rho = rho_s[j];
         if (rho == 0.0) continue;
         double sq = p1v[j];
-        for (int k = 0; k < mm; ++k) sq += u[k] * SY[j * mm + k];
-        al[j] = rho * sq;
-        u[j] -= al[j];
+#pragma unroll
+        for (int k = 0; k < QN_MAX_M; ++k)
+          if (k < mm) sq += ur[k] * SY[j * mm + k];
+        const double alj = rho * sq;
+#pragma unroll
+        for (int k = 0; k < QN_MAX_M; ++k) {
+          alr[k] = k == j ? alj : alr[k];
+          ur[k] = k == j ? ur[k] - alj : ur[k];
+        }
       }
       double gm;
       if (a.filled == 0) {
@@ -625,14 +632,26 @@ __global__ __launch_bounds__(QN_BLOCK) void qn_direction_kernel(QnArgs a) {
         const double rho = rho_s[j];
         if (rho == 0.0) continue;
         double yr = p1v[QN_MAX_M + j];
-        for (int k = 0; k < mm; ++k) yr += u[k] * YY[j * mm + k];
+#pragma unroll
+        for (int k = 0; k < QN_MAX_M; ++k)
+          if (k < mm) yr += ur[k] * YY[j * mm + k];
         yr *= gm;
-        for (int k = 0; k < mm; ++k) yr += w[k] * SY[k * mm + j];
-        w[j] += al[j] - rho * yr;
+#pragma unroll
+        for (int k = 0; k < QN_MAX_M; ++k)
+          if (k < mm) yr += wr[k] * SY[k * mm + j];
+        double alj = 0.0;
+#pragma unroll
+        for (int k = 0; k < QN_MAX_M; ++k) alj = k == j ? alr[k] : alj;
+        const double dw = alj - rho * yr;
+#pragma unroll
+        for (int k = 0; k < QN_MAX_M; ++k) wr[k] = k == j ? wr[k] + dw : wr[k];
       }
-      for (int j = 0; j < mm; ++j) {
-        cY[j] = (float)(gm * u[j]);
-        cS[j] = (float)w[j];
+#pragma unroll
+      for (int j = 0; j < QN_MAX_M; ++j) {
+        if (j < mm) {
+          cY[j] = (float)(gm * ur[j]);
+          cS[j] = (float)wr[j];
+        }
       }
       gamma = (float)gm;
     }

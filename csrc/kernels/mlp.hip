@@ -101,6 +101,48 @@ struct GradRegions {
   int nreg;
 };
 
+// ---- MFMA-fragment-ordered bf16 copies of W0 / W1 for the step kernels (mlp_step.hip) ----
+// A 16x16x32 A-operand fragment (16 rows x 32 k, lane l: row l & 15, k 8 (l >> 4) .. + 7) of a [R][C]
+// matrix is stored as ONE contiguous KB: element (r, c) at frag_pos(r, c, C).  A wave then loads a
+// fragment with one 1 KB-contiguous instruction instead of 16 half-lines (profiles/r4/prologue_probe.txt:
+// 2.7k vs 9.2k cycles for the forward's 21 KB per wave).  Layout of MlpFragSpec::dst: W0 [H][K0], W1
+// [H][H] (forward A: rows = layer-2 units), W1^T (backward A: rows = layer-1 units).
+__device__ __forceinline__ int64_t frag_pos(int r, int c, int C) {
+  return ((((int64_t)(r >> 4) * (C >> 5) + (c >> 5)) * 64 + ((c & 31) >> 3) * 16 + (r & 15)) << 3) + (c & 7);
+}
+
+// element e .. e + 3 of the flat parameter buffer (bf16 values ob) into the fragment copies; the
+// W1^T copy too when `transposed` (2-byte scatter: the Adam kernel writes it from an LDS tile instead)
+template <bool transposed>
+__device__ __forceinline__ void frag_store4(const MlpFragSpec& f, int64_t e, ushort4 ob) {
+  const int H = f.H, K0 = f.K0;
+  const int64_t a0 = e - f.w0_off, a1 = e - f.w1_off;
+  if (a0 >= 0 && a0 < (int64_t)H * K0) {
+    const int u = (int)(a0 / K0), k = (int)(a0 % K0);
+    *reinterpret_cast<ushort4*>(f.dst + frag_pos(u, k, K0)) = ob;
+  } else if (a1 >= 0 && a1 < (int64_t)H * H) {
+    const int j = (int)(a1 / H), u = (int)(a1 % H);
+    bf16_t* w1 = f.dst + (int64_t)H * K0;
+    *reinterpret_cast<ushort4*>(w1 + frag_pos(j, u, H)) = ob;
+    if constexpr (transposed) {
+      bf16_t* w1t = w1 + (int64_t)H * H;
+      w1t[frag_pos(u, j, H)] = ob.x;
+      w1t[frag_pos(u + 1, j, H)] = ob.y;
+      w1t[frag_pos(u + 2, j, H)] = ob.z;
+      w1t[frag_pos(u + 3, j, H)] = ob.w;
+    }
+  }
+}
+
+// refresh of the fragment copies from the flat bf16 copy (engine init / checkpoint load)
+__global__ void mlp_pack_frag_kernel(const bf16_t* __restrict__ pb, MlpFragSpec f) {
+  const int64_t n0 = (int64_t)f.H * f.K0 / 4, n1 = (int64_t)f.H * f.H / 4;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n0 + n1; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t e = i < n0 ? f.w0_off + 4 * i : f.w1_off + 4 * (i - n0);
+    frag_store4<true>(f, e, *reinterpret_cast<const ushort4*>(pb + e));
+  }
+}
+
 // Step counter lives on the device so a captured hipGraph replays correct bias corrections.
 __global__ void adam_tick_kernel(int32_t* step) { *step += 1; }
 
@@ -177,14 +219,17 @@ __global__ void cast_pad_kernel(const float* __restrict__ in, int rows, int cin,
 // in flight per step: the 256 per-workgroup slabs of the forward kernel take two steps), the 16
 // partials are added in a fixed tree order -> bitwise reproducible, and N = 1 (GR_REDUCE |
 // GR_ADAM) and N > 1 (GR_REDUCE | GR_STORE, all-reduce, GR_ADAM) apply the same summation and the
-// same Adam arithmetic.
+// same Adam arithmetic.  With fragment copies (MlpFragSpec) the new bf16 values also go to the W0 and
+// W1 fragment copies (8-byte runs); the W1^T copy is written by the step's forward kernel, which
+// holds W1 in registers anyway (a tiled transposing variant of this kernel measured 1.5 us slower).
 constexpr int GR_REDUCE = 1, GR_STORE = 2, GR_ADAM = 4;
 template <int GR_W>  // waves per workgroup
 __global__ __launch_bounds__(64 * GR_W) void grad_reduce_adam_kernel(GradRegions rg, int64_t n, float* __restrict__ G,
                                                                 float* __restrict__ param, float* __restrict__ m,
                                                                 float* __restrict__ v, bf16_t* __restrict__ pb,
                                                                 float lr, float b1, float b2, float eps, float wd,
-                                                                const int32_t* __restrict__ step, int mode) {
+                                                                const int32_t* __restrict__ step, int mode,
+                                                                MlpFragSpec frag) {
   __shared__ float4 part[GR_W][64];
   const int q = threadIdx.x >> 6, k = threadIdx.x & 63;
   const int64_t i4 = (int64_t)blockIdx.x * 64 + k, e = i4 * 4;
@@ -273,6 +318,7 @@ __global__ __launch_bounds__(64 * GR_W) void grad_reduce_adam_kernel(GradRegions
       reinterpret_cast<float4*>(m)[i4] = mm;
       reinterpret_cast<float4*>(v)[i4] = vv;
       reinterpret_cast<ushort4*>(pb)[i4] = ob;
+      if (frag.dst) frag_store4<false>(frag, e, ob);
     }
   }
 }
@@ -328,8 +374,16 @@ extern "C" int har_cast_pad_bf16(const float* in, int rows, int cin, int ldin, u
 extern "C" int har_grad_reduce_adam(int nreg, const float* const* src, const int64_t* start, const int64_t* len,
                                     const int64_t* lds, const int* S, int64_t n, float* G, float* param, float* m,
                                     float* v, uint16_t* pb, float lr, float b1, float b2, float eps, float wd,
-                                    int32_t* step, int tick, int mode, hipStream_t s) {
+                                    int32_t* step, int tick, int mode, const MlpFragSpec* frag_spec,
+                                    hipStream_t s) {
   if (n % 4 || nreg < 0 || nreg > 8 || ((mode & GR_REDUCE) && nreg == 0)) return -2;
+  MlpFragSpec frag{};
+  if (frag_spec && frag_spec->dst) {
+    frag = *frag_spec;
+    if (frag.H % 32 || frag.K0 % 32 || frag.w0_off % 4 || frag.w1_off % 4 || (reinterpret_cast<uintptr_t>(frag.dst) & 7) ||
+        frag.w0_off + (int64_t)frag.H * frag.K0 > n || frag.w1_off + (int64_t)frag.H * frag.H > n)
+      return -2;
+  }
   GradRegions rg{};
   rg.nreg = nreg;
   for (int r = 0; r < nreg; ++r) {
@@ -346,12 +400,24 @@ extern "C" int har_grad_reduce_adam(int nreg, const float* const* src, const int
     return e ? atoi(e) : 16;
   }();
   if (w == 4)
-    grad_reduce_adam_kernel<4><<<(int)blocks, 256, 0, s>>>(rg, n, G, param, m, v, pb, lr, b1, b2, eps, wd, step, mode);
+    grad_reduce_adam_kernel<4><<<(int)blocks, 256, 0, s>>>(rg, n, G, param, m, v, pb, lr, b1, b2, eps, wd, step, mode,
+                                                           frag);
   else if (w == 8)
-    grad_reduce_adam_kernel<8><<<(int)blocks, 512, 0, s>>>(rg, n, G, param, m, v, pb, lr, b1, b2, eps, wd, step, mode);
+    grad_reduce_adam_kernel<8><<<(int)blocks, 512, 0, s>>>(rg, n, G, param, m, v, pb, lr, b1, b2, eps, wd, step, mode,
+                                                           frag);
   else
     grad_reduce_adam_kernel<16><<<(int)blocks, 1024, 0, s>>>(rg, n, G, param, m, v, pb, lr, b1, b2, eps, wd, step,
-                                                             mode);
+                                                             mode, frag);
+  HAR_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int har_mlp_pack_frag(const uint16_t* pb, const MlpFragSpec* f, hipStream_t s) {
+  if (!f || !f->dst || f->H % 32 || f->K0 % 32 || f->w0_off % 4 || f->w1_off % 4 ||
+      (reinterpret_cast<uintptr_t>(f->dst) & 7) || (reinterpret_cast<uintptr_t>(pb) & 7))
+    return -2;
+  const int64_t n4 = ((int64_t)f->H * f->K0 + (int64_t)f->H * f->H) / 4;
+  mlp_pack_frag_kernel<<<(int)std::min<int64_t>(1024, (n4 + 255) / 256), 256, 0, s>>>(pb, *f);
   HAR_CHECK_LAUNCH();
   return 0;
 }

@@ -80,8 +80,8 @@ __device__ __forceinline__ bf16x8_t ldx(const bf16_t* __restrict__ X, int row, i
 
 template <int K0, bool STAMP>
 __global__ __launch_bounds__(512) void mlp_fwd3_kernel(
-    const bf16_t* __restrict__ X, const bf16_t* __restrict__ W0, const float* __restrict__ b0,
-    const bf16_t* __restrict__ W1, const float* __restrict__ b1, const bf16_t* __restrict__ Wo,
+    const bf16_t* __restrict__ X, bf16_t* __restrict__ Wf, const float* __restrict__ b0,
+    const float* __restrict__ b1, const bf16_t* __restrict__ Wo,
     const float* __restrict__ bo, const int32_t* __restrict__ labels, int B, int C, float scale,
     uint32_t* __restrict__ dz_out, uint32_t* __restrict__ mask_out, float* __restrict__ slab,
     float* __restrict__ block_loss, int32_t* __restrict__ block_correct, uint64_t* __restrict__ stamps) {
@@ -117,19 +117,22 @@ __global__ __launch_bounds__(512) void mlp_fwd3_kernel(
       for (int kc = 0; kc < K0C; ++kc) xb[h][kc] = ldx<K0>(X, r + 16 * h + c16, kc, g);
   };
 
-  // ---- this wave's weight slices, in registers for the whole kernel.  Issue order: W0, b0, the
-  // first X tile and its labels, THEN W1 / Wout / b1 (the bulk: 16 KB per wave, L2-bandwidth-bound
-  // with every CU fetching it at once), so stage 1 of tile 0 waits only for what it reads ----
+  // ---- this wave's weight slices, in registers for the whole kernel, from the fragment-ordered
+  // copies (MlpFragSpec: one 1 KB-contiguous load per fragment).  Issue order: W0, b0, the first X
+  // tile and its labels, THEN W1 / Wout / b1 (the bulk: 16 KB per wave), so stage 1 of tile 0 waits
+  // only for what it reads ----
+  const bf16_t* const W0f = Wf;
+  const bf16_t* const W1f = Wf + HH * K0;
   bf16x8_t w0f[2][K0C], w1f[2][KC];
-  // k-chunk rotation per workgroup: every CU fetches all of W1 at once in the prologue, and a
-  // common order makes them request the same lines together; register kc holds chunk (kc + krot)
+  // k-chunk rotation per workgroup (register kc holds chunk (kc + krot)): the CUs' prologue requests
+  // spread over the lines of W1 instead of all asking for the same ones together
   const int krot = (int)blockIdx.x & (KC - 1);
   float4 b0r[2], b1r[2];
 #pragma unroll
   for (int t = 0; t < 2; ++t) {
 #pragma unroll
     for (int kc = 0; kc < K0C; ++kc)
-      w0f[t][kc] = *reinterpret_cast<const bf16x8_t*>(W0 + (size_t)(u0 + 16 * t + c16) * K0 + kc * 32 + g * 8);
+      w0f[t][kc] = *reinterpret_cast<const bf16x8_t*>(W0f + ((size_t)((2 * wave + t) * K0C + kc) * 64 + lane) * 8);
     b0r[t] = *reinterpret_cast<const float4*>(b0 + u0 + 16 * t + 4 * g);
   }
   int ynext = 0;
@@ -142,7 +145,7 @@ __global__ __launch_bounds__(512) void mlp_fwd3_kernel(
   for (int t = 0; t < 2; ++t) {
 #pragma unroll
     for (int kc = 0; kc < KC; ++kc)
-      w1f[t][kc] = *reinterpret_cast<const bf16x8_t*>(W1 + (size_t)(u0 + 16 * t + c16) * HH + ((kc + krot) & (KC - 1)) * 32 + g * 8);
+      w1f[t][kc] = *reinterpret_cast<const bf16x8_t*>(W1f + ((size_t)((2 * wave + t) * KC + ((kc + krot) & (KC - 1))) * 64 + lane) * 8);
     b1r[t] = *reinterpret_cast<const float4*>(b1 + u0 + 16 * t + 4 * g);
   }
   // stage-3 A fragment: Wout[class c16][u0 + 4g + j] (j < 4), [u0 + 16 + 4g + j - 4] (j >= 4): the k
@@ -270,6 +273,28 @@ __global__ __launch_bounds__(512) void mlp_fwd3_kernel(
   if (nt > 0) {
     stage1(0);
     load_x(1);
+    // The W1^T fragment copy the backward of this step reads (Wf + H K0 + H H; the Adam kernel writes
+    // only the W0 / W1 copies): fragment f = (unit block ub = f & 15, k chunk jc = f >> 4) holds
+    // W1[32 jc .. + 32][16 ub .. + 16], i.e. rows this workgroup's wave jc has in registers (W1 rows
+    // 32 jc .. + 32 = its units): transposed through the (still unused) partial-logit buffer.
+    for (int f = blockIdx.x; f < 8 * (HH / 16); f += gridDim.x) {
+      const int ub = f & 15, jc = f >> 4;
+      if (wave == jc) {
+        bf16_t* tt = reinterpret_cast<bf16_t*>(zs) + wave * 32 * 24;  // this wave's [32 j][16 u] (+ pad)
+        const int kcs = ((ub >> 1) - krot) & (KC - 1);
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+          for (int kc = 0; kc < KC; ++kc)
+            if (kc == kcs && (g >> 1) == (ub & 1))
+              *reinterpret_cast<bf16x8_t*>(tt + (16 * t + c16) * 24 + 8 * (g & 1)) = w1f[t][kc];
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the wave's own LDS stores
+        __builtin_amdgcn_wave_barrier();
+        *reinterpret_cast<bf16x8_t*>(Wf + HH * K0 + HH * HH + ((size_t)(ub * KC + jc) * 64 + lane) * 8) =
+            frag_tr(tt, 24, 0, lane);
+        __builtin_amdgcn_wave_barrier();
+      }
+    }
     __syncthreads();  // h1 of tile 0
     stage23(0, 0);
     stage1(1);
@@ -346,7 +371,6 @@ constexpr int BQ = 4, BQU = HH / BQ;  // 64 h1 units per workgroup
 constexpr int BRT = 64;               // rows per pipeline tile
 constexpr int BDP = HH + 16;          // dact2 tile pitch: 136 dwords (8 mod 64)
 constexpr int BUP = BQU + 16;         // h1 / dact1 quadrant tile pitch: 40 dwords
-constexpr int WQP = BQU + 8;          // prologue W1-quadrant image pitch
 
 template <int K0> struct Bwd3Lds {
   static constexpr int XP = K0 + 16;
@@ -354,13 +378,13 @@ template <int K0> struct Bwd3Lds {
   static constexpr int DSM = BRT * BDP, HS = BRT * BUP, XS = BRT * XP;
   static constexpr size_t bytes = (size_t)(2 * DSM + 2 * HS + 2 * HS + NXB * XS) * sizeof(bf16_t) +
                                   4 * BQU * sizeof(float) + 32 * sizeof(uint32_t);
-  static_assert((size_t)HH * WQP + NCLS * HH <= (size_t)2 * DSM, "prologue images fit the dact2 buffers");
+  static_assert((size_t)NCLS * HH + HH * BQU <= (size_t)2 * DSM, "the prologue images fit the dact2 buffers");
 };
 
 template <int K0, bool STAMP>
 __global__ __launch_bounds__(512) void mlp_bwd3_kernel(
     const uint32_t* __restrict__ dz, const uint32_t* __restrict__ mask, const bf16_t* __restrict__ X,
-    const bf16_t* __restrict__ W1, const bf16_t* __restrict__ W0, const float* __restrict__ b0,
+    const bf16_t* __restrict__ Wf, const float* __restrict__ b0,
     const bf16_t* __restrict__ Wo, int B, int S, float* __restrict__ gw1, float* __restrict__ gw0,
     float* __restrict__ gb0, float* __restrict__ gb1, int64_t slab_stride, int32_t* __restrict__ tick,
     const float* __restrict__ fslab, int fslab_w, int nfwd, float* __restrict__ gwo, float* __restrict__ gbo,
@@ -395,24 +419,26 @@ __global__ __launch_bounds__(512) void mlp_bwd3_kernel(
   const int ntiles = B / BRT, per = (ntiles + S - 1) / S;
   const int t0 = slice * per, n = max(0, min(ntiles, t0 + per) - t0);
 
-  // ---- prologue: the W1 quadrant columns and Wout through LDS (coalesced rows in, transposed
-  // fragment reads out), then the recompute's W0 rows ----
-  bf16_t* const wq = lds;                  // [256 j][WQP]: W1[j][qu0 .. qu0 + 64)
-  bf16_t* const wos = wq + HH * WQP;       // [16][256] Wout
+  // ---- prologue: the quadrant's (a) A fragments (W1^T, 32 KB contiguous in the fragment-ordered
+  // copy) and Wout through LDS — every byte fetched once per workgroup, 1 KB-contiguous loads —
+  // then the recompute's W0 fragments straight to registers ----
+  const bf16_t* const W0f = Wf;
+  const bf16_t* const W1tq = Wf + HH * K0 + HH * HH + (size_t)(4 * q) * KC * 512;
+  bf16_t* const wos = lds;                 // [16][256] Wout
+  bf16_t* const w1q = lds + NCLS * HH;     // [4 unit blocks][KC][64 lanes][8]: W1^T fragments
+  {
+    uint4 st[4];
 #pragma unroll
-  for (int v0 = tid; v0 < HH * (BQU / 8); v0 += 512) {  // every load issued before the first LDS store
-    // rotated by slice: the 64 workgroups of a quadrant do not request the same lines together
-    const int v = (v0 + 512 * slice) & (HH * (BQU / 8) - 1);
-    const int j = v / (BQU / 8), c = (v % (BQU / 8)) * 8;
-    *reinterpret_cast<uint4*>(wq + j * WQP + c) = *reinterpret_cast<const uint4*>(W1 + (size_t)j * HH + qu0 + c);
+    for (int i = 0; i < 4; ++i) st[i] = *reinterpret_cast<const uint4*>(W1tq + (size_t)(i * 8 + wave) * 512 + lane * 8);
+    const uint4 so = *reinterpret_cast<const uint4*>(Wo + (size_t)tid * 8);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) *reinterpret_cast<uint4*>(w1q + (i * 8 + wave) * 512 + lane * 8) = st[i];
+    *reinterpret_cast<uint4*>(wos + tid * 8) = so;
   }
-#pragma unroll
-  for (int v = tid; v < NCLS * HH / 8; v += 512)
-    *reinterpret_cast<uint4*>(wos + v * 8) = *reinterpret_cast<const uint4*>(Wo + (size_t)v * 8);
   bf16x8_t w0q[NFW];
 #pragma unroll
   for (int kc = 0; kc < NFW; ++kc)
-    w0q[kc] = *reinterpret_cast<const bf16x8_t*>(W0 + (size_t)(qu0 + 16 * ubh + c16) * K0 + kc * 32 + 8 * g);
+    w0q[kc] = *reinterpret_cast<const bf16x8_t*>(W0f + ((size_t)((4 * q + ubh) * NFW + kc) * 64 + lane) * 8);
   const float4 b0q = *reinterpret_cast<const float4*>(b0 + qu0 + 16 * ubh + 4 * g);
   // The forward's per-workgroup dWout / dbout partials are complete before this kernel starts: one
   // wave per 16-byte gradient column sums them (lane l: slabs l, l + 64, ...; then a fixed xor tree)
@@ -441,12 +467,13 @@ __global__ __launch_bounds__(512) void mlp_bwd3_kernel(
       if (lane == 0) *reinterpret_cast<f32x4_t*>(c4 < WO4 ? gwo + 4 * c4 : gbo + 4 * (c4 - WO4)) = v;
     }
   }
-  // (a) A fragments: A[u][k = j] = W1[32 kc + 8g + i][qu0 + 16 (up + e) + c16] (natural k order)
+  // (a) A fragments: A[u][k = j] = W1[32 kc + 8g + i][qu0 + 16 (up + e) + c16]
   bf16x8_t w1t[2][KC];
 #pragma unroll
   for (int e = 0; e < 2; ++e)
 #pragma unroll
-    for (int kc = 0; kc < KC; ++kc) w1t[e][kc] = frag_tr(wq + 32 * kc * WQP, WQP, 16 * (up + e), lane);
+    for (int kc = 0; kc < KC; ++kc)
+      w1t[e][kc] = *reinterpret_cast<const bf16x8_t*>(w1q + (((up + e) * KC + kc) * 64 + lane) * 8);
   // dact2 A fragments (16x16x16): A[m][k = class] = Wout[4g + i][j(m)] with the row -> j map of block
   // t = 2p + s: j = 128 jh + 32 p + 8 (m >> 2) + 4 s + (m & 3), so lane group g of the block pair p
   // holds the 8 consecutive j = 128 jh + 32 p + 8 g .. + 7: one 16-byte LDS store per pair
@@ -657,45 +684,51 @@ __global__ __launch_bounds__(512) void mlp_bwd3_kernel(
 }
 
 template <int K0>
-void launch_fwd3(const bf16_t* X, const bf16_t* W0, const float* b0, const bf16_t* W1, const float* b1,
-                 const bf16_t* Wo, const float* bo, const int32_t* labels, int B, int C, float scale, uint32_t* dz,
-                 uint32_t* mask, float* slab, float* bl, int32_t* bc, int nwg, hipStream_t s) {
+void launch_fwd3(const bf16_t* X, bf16_t* Wf, const float* b0, const float* b1, const bf16_t* Wo,
+                 const float* bo, const int32_t* labels, int B, int C, float scale, uint32_t* dz, uint32_t* mask,
+                 float* slab, float* bl, int32_t* bc, int nwg, hipStream_t s) {
   auto k = g_har_mlp_stamps ? mlp_fwd3_kernel<K0, true> : mlp_fwd3_kernel<K0, false>;
-  k<<<nwg, 512, FWD_LDS, s>>>(X, W0, b0, W1, b1, Wo, bo, labels, B, C, scale, dz, mask, slab, bl, bc, g_har_mlp_stamps);
+  k<<<nwg, 512, FWD_LDS, s>>>(X, Wf, b0, b1, Wo, bo, labels, B, C, scale, dz, mask, slab, bl, bc, g_har_mlp_stamps);
 }
 
 template <int K0>
-void launch_bwd3(const uint32_t* dz, const uint32_t* mask, const bf16_t* X, const bf16_t* W1, const bf16_t* W0,
-                 const float* b0, const bf16_t* Wo, int B, int S, float* gw1, float* gw0, float* gb0, float* gb1,
-                 int64_t stride, int32_t* tick, const float* fslab, int fslab_w, int nfwd, float* gwo, float* gbo,
-                 hipStream_t s) {
+void launch_bwd3(const uint32_t* dz, const uint32_t* mask, const bf16_t* X, const bf16_t* Wf, const float* b0,
+                 const bf16_t* Wo, int B, int S, float* gw1, float* gw0, float* gb0, float* gb1, int64_t stride,
+                 int32_t* tick, const float* fslab, int fslab_w, int nfwd, float* gwo, float* gbo, hipStream_t s) {
   auto k = g_har_mlp_stamps ? mlp_bwd3_kernel<K0, true> : mlp_bwd3_kernel<K0, false>;
-  k<<<S * BQ, 512, Bwd3Lds<K0>::bytes, s>>>(dz, mask, X, W1, W0, b0, Wo, B, S, gw1, gw0, gb0, gb1, stride, tick,
+  k<<<S * BQ, 512, Bwd3Lds<K0>::bytes, s>>>(dz, mask, X, Wf, b0, Wo, B, S, gw1, gw0, gb0, gb1, stride, tick,
                                            fslab, fslab_w, nfwd, gwo, gbo, g_har_mlp_stamps ? g_har_mlp_stamps + STAMP_BWD_OFF : nullptr);
 }
 
 }  // namespace
 
 extern "C" int har_mlp_step_grid(int B) { return std::max(1, std::min(256, B / FRT)); }
-extern "C" int har_mlp_step_slices(int B) { return std::max(1, std::min(64, B / BRT / 4)); }
+// Row slices of the backward (x 4 unit quadrants = workgroups; one fp32 gradient slab per slice):
+// 4 tiles per slice at large batches (the slab traffic stays 64 slabs), but at least min(16, tiles)
+// slices at small ones, so a batch of 256 runs 16 workgroups instead of 4 (every workgroup's
+// prologue and slab stores are a fixed cost; their parallelism is what a small step needs).
+extern "C" int har_mlp_step_slices(int B) {
+  const int tiles = B / BRT;
+  return std::max(1, std::min(64, std::max(tiles / 4, std::min(tiles, 16))));
+}
 extern "C" int har_mlp_step_fwd_slab_width(int H) { return NCLS * H + NCLS; }
 
 // Forward of the step: dz [B][8] u32 (bf16 pairs, 16 classes), relu'(h2) mask [B][8] u32, and per
 // workgroup (har_mlp_step_grid(B) of them) dWout rows 0..15 + dbout (width har_mlp_step_fwd_slab_width),
 // loss and #correct.
-extern "C" int har_mlp_step_fwd(const uint16_t* X, int K0, const uint16_t* W0, const float* b0, const uint16_t* W1,
-                                const float* b1, int H, const uint16_t* Wo, const float* bo, const int32_t* labels,
-                                int B, int C, float scale, uint32_t* dz, uint32_t* mask, float* slab,
-                                float* block_loss, int32_t* block_correct, hipStream_t s) {
+extern "C" int har_mlp_step_fwd(const uint16_t* X, int K0, uint16_t* Wf, const float* b0, const float* b1,
+                                int H, const uint16_t* Wo, const float* bo, const int32_t* labels, int B, int C,
+                                float scale, uint32_t* dz, uint32_t* mask, float* slab, float* block_loss,
+                                int32_t* block_correct, hipStream_t s) {
   if (H != HH || (K0 != 32 && K0 != 64) || B <= 0 || B % 64 || C < 1 || C > NCLS) return -2;
-  if (((uintptr_t)X | (uintptr_t)W0 | (uintptr_t)W1 | (uintptr_t)Wo | (uintptr_t)b0 | (uintptr_t)b1 |
-       (uintptr_t)slab | (uintptr_t)dz | (uintptr_t)mask) & 15)
+  if (((uintptr_t)X | (uintptr_t)Wf | (uintptr_t)Wo | (uintptr_t)b0 | (uintptr_t)b1 | (uintptr_t)slab |
+       (uintptr_t)dz | (uintptr_t)mask) & 15)
     return -3;
   const int nwg = har_mlp_step_grid(B);
   if (K0 == 64)
-    launch_fwd3<64>(X, W0, b0, W1, b1, Wo, bo, labels, B, C, scale, dz, mask, slab, block_loss, block_correct, nwg, s);
+    launch_fwd3<64>(X, Wf, b0, b1, Wo, bo, labels, B, C, scale, dz, mask, slab, block_loss, block_correct, nwg, s);
   else
-    launch_fwd3<32>(X, W0, b0, W1, b1, Wo, bo, labels, B, C, scale, dz, mask, slab, block_loss, block_correct, nwg, s);
+    launch_fwd3<32>(X, Wf, b0, b1, Wo, bo, labels, B, C, scale, dz, mask, slab, block_loss, block_correct, nwg, s);
   HAR_CHECK_LAUNCH();
   return 0;
 }
@@ -705,23 +738,22 @@ extern "C" int har_mlp_step_fwd(const uint16_t* X, int K0, const uint16_t* W0, c
 // per-workgroup slabs, row stride fslab_w) it also writes their sums: dWout rows 0..15 to gwo and
 // dbout to gbo (fixed summation order).
 extern "C" int har_mlp_step_bwd(const uint32_t* dz, const uint32_t* mask, const uint16_t* X, int K0,
-                                const uint16_t* W1, int H, const uint16_t* W0, const float* b0, const uint16_t* Wo,
-                                int B, float* gw1, float* gw0, float* gb0, float* gb1, int64_t slab_stride,
-                                int32_t* tick, const float* fslab, int fslab_w, float* gwo, float* gbo,
-                                hipStream_t s) {
+                                const uint16_t* Wf, int H, const float* b0, const uint16_t* Wo, int B, float* gw1,
+                                float* gw0, float* gb0, float* gb1, int64_t slab_stride, int32_t* tick,
+                                const float* fslab, int fslab_w, float* gwo, float* gbo, hipStream_t s) {
   if (H != HH || B <= 0 || B % BRT || (K0 != 32 && K0 != 64) || slab_stride < (int64_t)H * H) return -2;
-  if (((uintptr_t)dz | (uintptr_t)mask | (uintptr_t)X | (uintptr_t)W1 | (uintptr_t)W0 | (uintptr_t)b0 |
-       (uintptr_t)Wo | (uintptr_t)gw1 | (uintptr_t)fslab | (uintptr_t)gwo | (uintptr_t)gbo) & 15)
+  if (((uintptr_t)dz | (uintptr_t)mask | (uintptr_t)X | (uintptr_t)Wf | (uintptr_t)b0 | (uintptr_t)Wo |
+       (uintptr_t)gw1 | (uintptr_t)fslab | (uintptr_t)gwo | (uintptr_t)gbo) & 15)
     return -3;
   const int nfwd = har_mlp_step_grid(B);
   if (fslab && (fslab_w < har_mlp_step_fwd_slab_width(H) || fslab_w % 4 || nfwd > 256 || !gwo || !gbo)) return -2;
   const int S = har_mlp_step_slices(B);
   if (K0 == 64)
-    launch_bwd3<64>(dz, mask, X, W1, W0, b0, Wo, B, S, gw1, gw0, gb0, gb1, slab_stride, tick, fslab, fslab_w, nfwd,
-                    gwo, gbo, s);
+    launch_bwd3<64>(dz, mask, X, Wf, b0, Wo, B, S, gw1, gw0, gb0, gb1, slab_stride, tick, fslab, fslab_w, nfwd, gwo,
+                    gbo, s);
   else
-    launch_bwd3<32>(dz, mask, X, W1, W0, b0, Wo, B, S, gw1, gw0, gb0, gb1, slab_stride, tick, fslab, fslab_w, nfwd,
-                    gwo, gbo, s);
+    launch_bwd3<32>(dz, mask, X, Wf, b0, Wo, B, S, gw1, gw0, gb0, gb1, slab_stride, tick, fslab, fslab_w, nfwd, gwo,
+                    gbo, s);
   HAR_CHECK_LAUNCH();
   return 0;
 }

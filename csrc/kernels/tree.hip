@@ -125,9 +125,10 @@ __global__ __launch_bounds__(256) void tree_hist_split_kernel(
   //   fused node's LDS histogram to its store slot, and merges big-node chunks into slot a;
   //   mode 5: blockIdx.y = node a with derive_from[a] = sibling s: hist = hprev[parent_of[a]] -
   //   store[s] (integer-valued weights: exact), kept in store[a], then the split search (mode 2).
-  // Data parallel (by_node = 1, the store zeroed): mode 6 = the work items of mode 3, histogram only
-  // (every item adds into its node's slot); the store is then summed across ranks (all-reduce, or
-  // reduce-scatter by node owner); mode 7 = split search from the rank's slice of it.
+  // Data parallel (by_node = 1): mode 6 = the work items of mode 3, histogram only: a node of one
+  // item stores its slot outright (zero rows on this rank: zeros), the chunks of a big node add into
+  // its slot (zeroed by tree_plan), so the store needs no zero fill; it is then summed across ranks
+  // (all-reduce, or reduce-scatter by node owner); mode 7 = split search from the rank's slice of it.
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int c = blockIdx.x, chunks = gridDim.x;
   int a = blockIdx.y, gslot = blockIdx.y;
@@ -139,6 +140,7 @@ __global__ __launch_bounds__(256) void tree_hist_split_kernel(
   __shared__ int red_idx[4];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   int start, cnt;
+  bool direct = false;  // mode 6, a node of one work item: its slot is stored, not added into
   if (mode == 7) {
     // data parallel: split search from the rank's slice of the reduced store (ghist, feats, outputs
     // all start at global node prows = a0); nodes at or past the level's device count exit
@@ -163,6 +165,7 @@ __global__ __launch_bounds__(256) void tree_hist_split_kernel(
       cnt = gslot < 0 ? cnt_all : min(prows, cnt_all - z * prows);
       // mode 6 (data parallel): every item only adds its histogram into the node's zeroed store
       // slot; the split search follows the cross-rank reduction (mode 7)
+      direct = mode == 6 && gslot < 0;
       if (gslot >= 0 || mode == 6) mode = 1;         // a chunk of a big node: histogram only
       else mode = 0;
       if (by_node) gslot = a;
@@ -280,7 +283,7 @@ __global__ __launch_bounds__(256) void tree_hist_split_kernel(
   if (mode == 0 && by_node)  // keep the fused node's histogram for its children's subtraction
     for (int i = tid; i < f_n * maxbins * K; i += blockDim.x) gh[i] = hist[i];
   if (mode == 1) {
-    if (!merge) {
+    if (!merge || direct) {
       for (int i = tid; i < f_n * maxbins * K; i += blockDim.x) gh[i] = hist[i];
     } else {  // row-split node: merge into the zeroed global histogram (integer-valued sums: exact)
       for (int i = tid; i < f_n * maxbins * K; i += blockDim.x)

@@ -256,3 +256,47 @@ def test_bench_contract_torchrun(config, extra):
         assert abs(rec["value"] - rec["config"]["global_batch"] / (rec["ms_per_step"] * 1e-3)) <= 1e-6 * rec["value"]
         ph = rec["phase_ms"]  # the DP step's split: compute, the all-reduce of G, Adam
         assert ph["world"] == 2 and all(ph[k] >= 0 for k in ("compute", "allreduce", "adam")) and ph["allreduce"] > 0
+
+
+def _bench_torchrun(world, args, timeout=900):
+    import json
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world),
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(root, "bench.py"),
+           "--gpus", str(world)] + args
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, cwd=root,
+                       env=dict(os.environ, OMP_NUM_THREADS="1"))
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    return json.loads(lines[0])
+
+
+def test_bench_rf9_tree_parallel_world8():
+    """``bench.py --config rf9 --rf-parallel tree`` under a gloo world of 8: one JSON line, every rank
+    holds the whole 8 x --rows table and grows numTrees / 8 trees, and the only collective of a fit is
+    ONE all-gather of the packed node arrays."""
+    rec = _bench_torchrun(8, ["--steps", "1", "--warmup", "0", "--config", "rf9", "--rf-parallel", "tree",
+                              "--rows", "200", "--trees", "16", "--depth", "4"])
+    assert rec["n_gpus"] == 8 and rec["rf_parallel"] == "tree" and rec["config"]["global_batch"] == 1600
+    coll = rec["collectives_per_step"]
+    assert coll["all_gather"] == 1 and set(coll) == {"all_gather", "bytes"} and coll["bytes"] > 0
+
+
+def test_rf_parallel_modes_same_forest_at_n1():
+    """At N = 1 the tree-parallel and data-parallel entry points give the same forest."""
+    from har.models.tree import RandomForestClassifier
+    from har.ops import tree as T
+    from har.parallel import data_parallel as dp
+    from har.parallel.dist import DistContext
+
+    X, y = _data()
+    thr = T.find_thresholds(X.numpy(), 32)
+    ctx = DistContext(rank=0, world_size=1, local_rank=0, device=torch.device("cpu"), backend="gloo")
+    a = dp.fit_forest_tree_parallel(RandomForestClassifier(numTrees=6, maxDepth=4, seed=5), X, y, 4, ctx,
+                                    thresholds=thr)
+    b = RandomForestClassifier(numTrees=6, maxDepth=4, seed=5).fit_tensors(X, y, 4, thresholds=thr)
+    torch.testing.assert_close(a.predict_raw(X), b.predict_raw(X))

@@ -98,7 +98,7 @@ def _worker(rank, world, port, out_dir, kind, reduction):
 
 @pytest.mark.parametrize("kind,reduction,world", [("rf", "owner", 2), ("rf", "allreduce", 2), ("dt", "owner", 3),
                                                   ("rf", "owner", 4), ("rf", "owner", 8)])
-def test_dp_device_forest_equals_single_with_no_level_reads(cuda, kind, reduction, world):
+def test_dp_device_forest_equals_single_with_one_read_per_level(cuda, kind, reduction, world):
     from har.ops import tree as T
 
     d = tempfile.mkdtemp()
@@ -109,7 +109,9 @@ def test_dp_device_forest_equals_single_with_no_level_reads(cuda, kind, reductio
     m = _estimator(kind).fit_tensors(X.to(cuda), y.to(cuda), 4, thresholds=thr)
     a = m.arrs
     for o in outs:
-        assert o["reads"].tolist() == [0, 0], o["reads"]  # no count read back inside the level loop
+        # one 16-byte count record per level (+ the roots') is read back: the collectives are sized by
+        # the real node counts; nothing else leaves the device inside the level loop
+        assert o["reads"][1] <= m.arrs.max_depth + 1 and o["reads"][0] <= 2 * (m.arrs.max_depth + 1), o["reads"]
         assert torch.equal(o["feature"], a.feature.cpu())
         assert torch.equal(o["threshold"], a.threshold.cpu())
         assert torch.equal(o["stats"], a.stats.cpu())

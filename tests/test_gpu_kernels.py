@@ -472,3 +472,33 @@ def test_sort_columns_matches_torch_sort(cuda, n, F):
     assert torch.equal(torch.isnan(out), torch.isnan(ref))
     assert torch.equal(torch.nan_to_num(out, nan=0.0), torch.nan_to_num(ref, nan=0.0))
 
+
+
+def _frag_reference(M: torch.Tensor) -> torch.Tensor:
+    """Independent construction of the A-fragment order of mlp.hip frag_pos: [R][C] -> blocks of 16 rows x
+    32 k, one KB each, lane l = 16 * (k-group g) + row-in-block holding 8 consecutive k."""
+    R, C = M.shape
+    t = M.reshape(R // 16, 16, C // 32, 4, 8)        # (row block, row, k chunk, g, i)
+    return t.permute(0, 2, 3, 1, 4).reshape(-1)      # (row block, k chunk, g, row, i)
+
+
+@pytest.mark.parametrize("F", [43, 20])
+def test_mlp_fragment_copies_track_pb(cuda, F):
+    """The step's fragment-ordered weight copies (Pf = W0 | W1 | W1^T in MFMA fragment order) equal
+    the flat bf16 copy Pb after the engine's init and after every fused Adam update."""
+    from har.models.mlp import MLPEngine, pad_input_bf16
+
+    B = 4096
+    e = MLPEngine([F, 256, 256, 6], B, cuda, lr=1e-2, seed=11)
+    assert e.step_ok
+    g = torch.Generator(device=cuda).manual_seed(2)
+    X = pad_input_bf16(torch.randn(B, F, device=cuda, generator=g), e.layout.in_pad)
+    y = torch.randint(0, 6, (B,), device=cuda, generator=g).to(torch.int32)
+    L = e.layout
+    for step in range(3):
+        if step:
+            e.train_step(X, y, B)
+        torch.cuda.synchronize()
+        W0, W1 = L.view(e.Pb, "W0"), L.view(e.Pb, "W1")
+        want = torch.cat([_frag_reference(W0), _frag_reference(W1), _frag_reference(W1.T.contiguous())])
+        assert torch.equal(e.Pf, want), f"fragment copies differ from Pb after step {step}"

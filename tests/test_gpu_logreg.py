@@ -196,3 +196,33 @@ def test_device_setup_matches_torch(cuda):
     for i in (3, 4, 5, 6, 8):  # inv_std, inv_wsum, pmask, l2v, x0
         torch.testing.assert_close(g[i].cpu().reshape(c[i].shape), c[i], rtol=1e-5, atol=1e-6)
     torch.testing.assert_close(g[7].cpu(), c[7], rtol=1e-5, atol=1e-6)  # l1v
+
+
+def test_logreg_more_than_16_classes_on_gpu(cuda):
+    """18 classes exceed the device kernels' 16 class rows: the GPU fit runs the torch objective on
+    the device with the same L-BFGS algorithm (it used to raise), predictions through the
+    dense path, for plain fits and a CrossValidator."""
+    from har.data.table import Column, Table
+    from har.evaluation.evaluators import MulticlassClassificationEvaluator
+    from har.models.logreg import FitSpec, LogisticRegression
+    from har.tuning.crossval import CrossValidator, ParamGridBuilder
+
+    g = torch.Generator().manual_seed(4)
+    K, N, F = 18, 3000, 16
+    mu = torch.randn(K, F, generator=g) * 2
+    y = torch.randint(0, K, (N,), generator=g)
+    x = mu[y] + torch.randn(N, F, generator=g)
+    spec = [FitSpec(None, 0.001, 0.0)]
+    mg = LogisticRegression(maxIter=40, device=cuda).fit_many(x.to(cuda), y.to(cuda), spec, K)[0]
+    mc = LogisticRegression(maxIter=40, device="cpu").fit_many(x, y, spec, K)[0]
+    assert mg.coefficientMatrix.shape == (K, F)
+    pg, pc = mg.predict(x.to(cuda)).cpu(), mc.predict(x)
+    assert float((pg == pc).float().mean()) > 0.99
+    assert float((pg == y).float().mean()) > 0.8
+    assert abs(mg.summary["objective"] - mc.summary["objective"]) / abs(mc.summary["objective"]) < 1e-3
+    t = Table([Column("features", "vector", x.numpy().astype(np.float32)),
+               Column("label", "double", y.numpy().astype(np.float64))])
+    grid = ParamGridBuilder().addGrid("regParam", [0.001, 0.01]).build()
+    cv = CrossValidator(estimator=LogisticRegression(maxIter=20, device=cuda), estimatorParamMaps=grid,
+                        evaluator=MulticlassClassificationEvaluator(metricName="accuracy"), numFolds=3, seed=1).fit(t)
+    assert len(cv.avgMetrics) == 2 and cv.bestModel.coefficientMatrix.shape == (K, F)

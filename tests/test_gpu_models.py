@@ -419,3 +419,24 @@ def test_subsampled_forest_gpu_equals_cpu(cuda, trees, rate):
     g = RandomForestClassifier(**kw).fit_tensors(x.to(cuda), y.to(cuda), 5, thresholds=thr)
     torch.testing.assert_close(g.arrs.stats[:, 0].cpu(), c.arrs.stats[:, 0], rtol=0, atol=0)
     assert torch.equal(g.arrs.feature[:, :3].cpu(), c.arrs.feature[:, :3])
+
+
+@pytest.mark.parametrize("B", [256, 320])
+def test_mlp_epoch_graph_equals_eager_fit(cuda, monkeypatch, B):
+    """A single-GPU MultilayerPerceptronClassifier fit replays one captured HIP graph per epoch
+    (static batch buffers, the shuffled rows gathered into them); it must train exactly the
+    parameters of the eager step loop.  B = 256 / 320: the small batches main.py and the bench's
+    WISDM accuracy run use (more backward slices than 4-tile slices would give)."""
+    from har.models.mlp import MultilayerPerceptronClassifier
+
+    g = torch.Generator().manual_seed(9)
+    X = torch.randn(2500, 43, generator=g).to(cuda)
+    y = torch.randint(0, 6, (2500,), generator=g).to(cuda)
+    params = []
+    for flag in ("1", "0"):
+        monkeypatch.setenv("HAR_MLP_EPOCH_GRAPH", flag)
+        est = MultilayerPerceptronClassifier(layers=[43, 256, 256, 6], maxIter=4, blockSize=B, stepSize=1e-3, seed=3,
+                                             device=cuda)
+        params.append(est.fit_tensors(X, y, num_classes=6).engine.P.clone())
+    torch.cuda.synchronize()
+    assert torch.equal(params[0], params[1])

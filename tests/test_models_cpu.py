@@ -367,3 +367,45 @@ def test_logreg_checkpoint_keys_on_content(tmp_path):
     assert a2.summary.get("resumed") and torch.equal(a2.coefficientMatrix, a.coefficientMatrix)
     with pytest.raises(ValueError):
         LogisticRegression(lineSearchTrials=5)
+
+
+def test_crossvalidator_batched_refit_matches_plain_fit():
+    """The CrossValidator's best model comes from the batched solve (the 9 candidates' full-data
+    refits ride along with the 45 fold fits).  Its fp summation order differs from a separate
+    ``est.copy(best_map).fit(table)``, so the two agree within tolerance, not bitwise: the same
+    objective to 1e-4 relative and > 99% identical predictions."""
+    from har.data.table import Column, Table
+
+    x, y = _blobs(1200, 10, 4, seed=5)
+    t = Table([Column("features", "vector", x.numpy().astype(np.float32)),
+               Column("label", "double", y.numpy().astype(np.float64))])
+    lr = LogisticRegression(maxIter=30)
+    grid = ParamGridBuilder().addGrid("regParam", [0.05, 0.2]).addGrid("elasticNetParam", [0.0, 0.1]).build()
+    cv = CrossValidator(estimator=lr, estimatorParamMaps=grid,
+                        evaluator=MulticlassClassificationEvaluator(metricName="accuracy"), numFolds=3, seed=1)
+    m = cv.fit(t)
+    plain = lr.copy(grid[m.bestIndex]).fit(t)
+    fa, fb = m.bestModel.summary["objective"], plain.summary["objective"]
+    assert abs(fa - fb) / abs(fb) < 1e-4, (fa, fb)
+    agree = float((m.bestModel.predict(x) == plain.predict(x)).float().mean())
+    assert agree > 0.99, agree
+
+
+def test_logreg_per_model_objective_history():
+    """Every model of a batched fit reports its own objective trajectory (not the batch mean)."""
+    x, y = _blobs(600, 6, 3, seed=2)
+    specs = [FitSpec(None, 0.01, 0.0), FitSpec(None, 1.0, 0.0)]
+    ms = LogisticRegression(maxIter=15).fit_many(x, y, specs, 3)
+    h0, h1 = ms[0].summary["objectiveHistory"], ms[1].summary["objectiveHistory"]
+    assert len(h0) >= 2 and h0 != h1
+    assert abs(h0[-1] - ms[0].summary["objective"]) < 1e-6 * max(1.0, abs(h0[-1]))
+    assert abs(h1[-1] - ms[1].summary["objective"]) < 1e-6 * max(1.0, abs(h1[-1]))
+    assert all(b <= a + 1e-9 for a, b in zip(h0, h0[1:]))  # monotone (Armijo steps only)
+
+
+def test_logreg_many_classes_cpu():
+    """More classes than the device kernels' 16 class rows: the same estimator fits them."""
+    x, y = _blobs(2000, 12, 18, seed=3)
+    m = LogisticRegression(maxIter=60, regParam=0.001).fit_many(x, y, [FitSpec(None, 0.001, 0.0)], 18)[0]
+    assert m.coefficientMatrix.shape == (18, 12)
+    assert float((m.predict(x) == y).float().mean()) > 0.8

@@ -49,17 +49,17 @@ static void mlp_contracts() {
   int64_t lds[9] = {36, 36, 36, 36, 36, 36, 36, 36, 36};
   int S[9] = {2, 2, 2, 2, 2, 2, 2, 2, 2};
   // n % 4, too many regions, REDUCE without regions, S <= 0, region past n, unsorted, misaligned
-  EXPECT(har_grad_reduce_adam(1, src, start, len, lds, S, 6, fbuf, fbuf, fbuf, fbuf, hbuf, 0, 0, 0, 0, 0, ibuf, 0, 1, 0), -2);
-  EXPECT(har_grad_reduce_adam(9, src, start, len, lds, S, 36, fbuf, fbuf, fbuf, fbuf, hbuf, 0, 0, 0, 0, 0, ibuf, 0, 1, 0), -2);
-  EXPECT(har_grad_reduce_adam(0, src, start, len, lds, S, 36, fbuf, fbuf, fbuf, fbuf, hbuf, 0, 0, 0, 0, 0, ibuf, 0, 1, 0), -2);
+  EXPECT(har_grad_reduce_adam(1, src, start, len, lds, S, 6, fbuf, fbuf, fbuf, fbuf, hbuf, 0, 0, 0, 0, 0, ibuf, 0, 1, nullptr, 0), -2);
+  EXPECT(har_grad_reduce_adam(9, src, start, len, lds, S, 36, fbuf, fbuf, fbuf, fbuf, hbuf, 0, 0, 0, 0, 0, ibuf, 0, 1, nullptr, 0), -2);
+  EXPECT(har_grad_reduce_adam(0, src, start, len, lds, S, 36, fbuf, fbuf, fbuf, fbuf, hbuf, 0, 0, 0, 0, 0, ibuf, 0, 1, nullptr, 0), -2);
   int S0[1] = {0};
-  EXPECT(har_grad_reduce_adam(1, src, start, len, lds, S0, 36, fbuf, fbuf, fbuf, fbuf, hbuf, 0, 0, 0, 0, 0, ibuf, 0, 1, 0), -2);
+  EXPECT(har_grad_reduce_adam(1, src, start, len, lds, S0, 36, fbuf, fbuf, fbuf, fbuf, hbuf, 0, 0, 0, 0, 0, ibuf, 0, 1, nullptr, 0), -2);
   int64_t far[1] = {36};
-  EXPECT(har_grad_reduce_adam(1, src, far, len, lds, S, 36, fbuf, fbuf, fbuf, fbuf, hbuf, 0, 0, 0, 0, 0, ibuf, 0, 1, 0), -2);
+  EXPECT(har_grad_reduce_adam(1, src, far, len, lds, S, 36, fbuf, fbuf, fbuf, fbuf, hbuf, 0, 0, 0, 0, 0, ibuf, 0, 1, nullptr, 0), -2);
   int64_t unsorted[2] = {8, 0};
-  EXPECT(har_grad_reduce_adam(2, src, unsorted, len, lds, S, 36, fbuf, fbuf, fbuf, fbuf, hbuf, 0, 0, 0, 0, 0, ibuf, 0, 1, 0), -2);
+  EXPECT(har_grad_reduce_adam(2, src, unsorted, len, lds, S, 36, fbuf, fbuf, fbuf, fbuf, hbuf, 0, 0, 0, 0, 0, ibuf, 0, 1, nullptr, 0), -2);
   const float* mis[1] = {fbuf + 1};
-  EXPECT(har_grad_reduce_adam(1, mis, start, len, lds, S, 36, fbuf, fbuf, fbuf, fbuf, hbuf, 0, 0, 0, 0, 0, ibuf, 0, 1, 0), -3);
+  EXPECT(har_grad_reduce_adam(1, mis, start, len, lds, S, 36, fbuf, fbuf, fbuf, fbuf, hbuf, 0, 0, 0, 0, 0, ibuf, 0, 1, nullptr, 0), -3);
 
   EXPECT(har_adam_step(fbuf, fbuf, nullptr, 0, fbuf, fbuf, hbuf, 6, 0, 0, 0, 0, 0, 1, ibuf, 0, 0), -2);
   EXPECT(har_reduce_slabs(fbuf, 2, 6, fbuf, 0), -2);
@@ -83,17 +83,17 @@ static void mlp_contracts() {
   // three-kernel step: H != 256, K0 not 32 / 64, B % 64, C outside [1, 16], short slab stride, misaligned
   uint32_t* w = reinterpret_cast<uint32_t*>(ibuf);
   float* g = fbuf;
-  EXPECT(har_mlp_step_fwd(hbuf, 64, hbuf, fbuf, hbuf, fbuf, 128, hbuf, fbuf, ibuf, 64, 6, 1.f, w, w, g, g, ibuf, 0), -2);
-  EXPECT(har_mlp_step_fwd(hbuf, 48, hbuf, fbuf, hbuf, fbuf, 256, hbuf, fbuf, ibuf, 64, 6, 1.f, w, w, g, g, ibuf, 0), -2);
-  EXPECT(har_mlp_step_fwd(hbuf, 64, hbuf, fbuf, hbuf, fbuf, 256, hbuf, fbuf, ibuf, 96, 6, 1.f, w, w, g, g, ibuf, 0), -2);
-  EXPECT(har_mlp_step_fwd(hbuf, 64, hbuf, fbuf, hbuf, fbuf, 256, hbuf, fbuf, ibuf, 64, 17, 1.f, w, w, g, g, ibuf, 0), -2);
-  EXPECT(har_mlp_step_fwd(hbuf + 4, 64, hbuf, fbuf, hbuf, fbuf, 256, hbuf, fbuf, ibuf, 64, 6, 1.f, w, w, g, g, ibuf, 0), -3);
-  EXPECT(har_mlp_step_bwd(w, w, hbuf, 64, hbuf, 128, hbuf, fbuf, hbuf, 64, g, g, g, g, 1 << 20, ibuf, nullptr, 0, g, g, 0), -2);
-  EXPECT(har_mlp_step_bwd(w, w, hbuf, 64, hbuf, 256, hbuf, fbuf, hbuf, 96, g, g, g, g, 1 << 20, ibuf, nullptr, 0, g, g, 0), -2);
-  EXPECT(har_mlp_step_bwd(w, w, hbuf, 48, hbuf, 256, hbuf, fbuf, hbuf, 64, g, g, g, g, 1 << 20, ibuf, nullptr, 0, g, g, 0), -2);
-  EXPECT(har_mlp_step_bwd(w, w, hbuf, 64, hbuf, 256, hbuf, fbuf, hbuf, 64, g, g, g, g, 256 * 255, ibuf, nullptr, 0, g, g, 0), -2);
-  EXPECT(har_mlp_step_bwd(w + 1, w, hbuf, 64, hbuf, 256, hbuf, fbuf, hbuf, 64, g, g, g, g, 1 << 20, ibuf, nullptr, 0, g, g, 0), -3);
-  EXPECT(har_mlp_step_bwd(w, w, hbuf, 64, hbuf, 256, hbuf, fbuf, hbuf, 64, g, g, g, g, 1 << 20, ibuf, g, 100, g, g, 0), -2);
+  EXPECT(har_mlp_step_fwd(hbuf, 64, hbuf, fbuf, fbuf, 128, hbuf, fbuf, ibuf, 64, 6, 1.f, w, w, g, g, ibuf, 0), -2);
+  EXPECT(har_mlp_step_fwd(hbuf, 48, hbuf, fbuf, fbuf, 256, hbuf, fbuf, ibuf, 64, 6, 1.f, w, w, g, g, ibuf, 0), -2);
+  EXPECT(har_mlp_step_fwd(hbuf, 64, hbuf, fbuf, fbuf, 256, hbuf, fbuf, ibuf, 96, 6, 1.f, w, w, g, g, ibuf, 0), -2);
+  EXPECT(har_mlp_step_fwd(hbuf, 64, hbuf, fbuf, fbuf, 256, hbuf, fbuf, ibuf, 64, 17, 1.f, w, w, g, g, ibuf, 0), -2);
+  EXPECT(har_mlp_step_fwd(hbuf + 4, 64, hbuf, fbuf, fbuf, 256, hbuf, fbuf, ibuf, 64, 6, 1.f, w, w, g, g, ibuf, 0), -3);
+  EXPECT(har_mlp_step_bwd(w, w, hbuf, 64, hbuf, 128, fbuf, hbuf, 64, g, g, g, g, 1 << 20, ibuf, nullptr, 0, g, g, 0), -2);
+  EXPECT(har_mlp_step_bwd(w, w, hbuf, 64, hbuf, 256, fbuf, hbuf, 96, g, g, g, g, 1 << 20, ibuf, nullptr, 0, g, g, 0), -2);
+  EXPECT(har_mlp_step_bwd(w, w, hbuf, 48, hbuf, 256, fbuf, hbuf, 64, g, g, g, g, 1 << 20, ibuf, nullptr, 0, g, g, 0), -2);
+  EXPECT(har_mlp_step_bwd(w, w, hbuf, 64, hbuf, 256, fbuf, hbuf, 64, g, g, g, g, 256 * 255, ibuf, nullptr, 0, g, g, 0), -2);
+  EXPECT(har_mlp_step_bwd(w + 1, w, hbuf, 64, hbuf, 256, fbuf, hbuf, 64, g, g, g, g, 1 << 20, ibuf, nullptr, 0, g, g, 0), -3);
+  EXPECT(har_mlp_step_bwd(w, w, hbuf, 64, hbuf, 256, fbuf, hbuf, 64, g, g, g, g, 1 << 20, ibuf, g, 100, g, g, 0), -2);
 }
 
 static void window_contracts() {
