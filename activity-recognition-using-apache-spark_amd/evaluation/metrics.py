@@ -111,12 +111,17 @@ def batched_metrics(metric: str, label: torch.Tensor, pred: torch.Tensor, mask: 
                     raw: torch.Tensor = None) -> np.ndarray:
     """One metric for B models at once: ``pred`` / ``mask`` are ``[B, N]`` (mask = the rows each
     model is scored on, e.g. its CrossValidator validation fold); returns ``[B]`` with the same
-    definitions as the single-model functions above.  Multiclass metrics come from a batched
-    confusion matrix (one einsum), regression metrics from masked moments; one host read.
-    Binary metrics (``raw [B, N, K]``) fall back to one sort per model."""
+    definitions as the single-model functions above.  On the GPU multiclass metrics come from ONE
+    batched confusion-matrix launch (metrics.hip) and binary metrics from ONE segmented sort + ONE
+    batched roc.hip launch; regression metrics from masked moments; one host read.  On the CPU the
+    same definitions in torch (one-hot einsum, one sort per model for the binary areas)."""
     B, N = pred.shape
     y = label.to(pred.device).long().view(1, N)
     w = mask.to(torch.float64)
+    if metric in ("areaUnderROC", "areaUnderPR") and pred.is_cuda:
+        sc = raw[:, :, 1] if raw.shape[-1] > 1 else raw.reshape(B, N)
+        auroc, aupr = mops.roc_pr_auc_batched(sc, label, mask.bool())
+        return np.asarray(auroc if metric == "areaUnderROC" else aupr, dtype=np.float64)
     if metric in ("areaUnderROC", "areaUnderPR"):
         out = []
         for b in range(B):
@@ -137,9 +142,12 @@ def batched_metrics(metric: str, label: torch.Tensor, pred: torch.Tensor, mask: 
         res["r2"] = torch.where(ss_tot > 0, 1.0 - se / ss_tot.clamp_min(1e-300), torch.full_like(se, float("nan")))
         return res[metric].cpu().numpy()
     K = num_classes
-    Y1 = torch.nn.functional.one_hot(y.view(N), K).double()                  # [N, K]
-    P1 = torch.nn.functional.one_hot(pred.long().clamp(0, K - 1), K).double()  # [B, N, K]
-    cm = torch.einsum("bn,nk,bnj->bkj", w, Y1, P1)                            # [B, true, pred]
+    if pred.is_cuda and K * K <= 4096:
+        cm = mops.confusion_matrix_batched(y.view(N), pred.long().clamp(0, K - 1), mask.bool(), K).double()
+    else:
+        Y1 = torch.nn.functional.one_hot(y.view(N), K).double()                  # [N, K]
+        P1 = torch.nn.functional.one_hot(pred.long().clamp(0, K - 1), K).double()  # [B, N, K]
+        cm = torch.einsum("bn,nk,bnj->bkj", w, Y1, P1)                            # [B, true, pred]
     n = cm.sum((1, 2))
     tp = torch.diagonal(cm, dim1=1, dim2=2)
     lc, pc = cm.sum(2), cm.sum(1)

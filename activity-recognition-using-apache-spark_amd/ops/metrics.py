@@ -38,9 +38,45 @@ def roc_pr_auc(score: torch.Tensor, label: torch.Tensor):
     roc, pr, P, N = out.cpu().tolist()
     # the curve closes at (1, 1); without negatives its last point is (0, 1) and the closing
     # segment is the whole area (without positives tpr is 0 everywhere)
+    return _auc_from_sums(roc, pr, P, N)
+
+
+def _auc_from_sums(roc, pr, P, N):
     auroc = (roc / (2.0 * P * N) if P > 0 and N > 0 else 0.0) + (0.0 if N > 0 else (1.0 + (P > 0)) / 2.0)
     aupr = pr / (2.0 * P) if P > 0 else 0.0
     return auroc, aupr
+
+
+def confusion_matrix_batched(label: torch.Tensor, pred: torch.Tensor, mask: torch.Tensor, K: int) -> torch.Tensor:
+    """[B, K, K] int64 confusion matrices of B models' predictions ``pred [B, N]`` over the rows
+    ``mask [B, N]`` selects (CrossValidator validation folds): one HIP launch (grid row chunks x B)."""
+    B, N = pred.shape
+    lab = label.to(device=pred.device, dtype=torch.int32).contiguous()
+    prd = pred.to(torch.int32).contiguous()
+    msk = mask.to(device=pred.device, dtype=torch.uint8).contiguous()
+    cm = torch.empty(B, K, K, dtype=torch.int64, device=pred.device)
+    _native.kernels().confusion_matrix_batched(lab.data_ptr(), prd.data_ptr(), msk.data_ptr(), N, B, K, cm.data_ptr(),
+                                               _native.stream_ptr())
+    return cm
+
+
+def roc_pr_auc_batched(score: torch.Tensor, label: torch.Tensor, mask: torch.Tensor):
+    """(areaUnderROC [B], areaUnderPR [B]) of B models' scores ``score [B, N]`` vs ``label > 0.5`` over
+    the rows ``mask [B, N]`` selects: ONE segmented descending sort of all B rows (the unselected rows
+    keyed -inf sort to the back), ONE roc.hip launch with a workgroup per model, ONE host read."""
+    B, N = score.shape
+    s = torch.where(mask.to(score.device), score.to(torch.float32), torch.full_like(score, float("-inf"),
+                                                                                     dtype=torch.float32))
+    vals, order = torch.sort(s, dim=1, descending=True, stable=True)
+    y = label.to(device=score.device, dtype=torch.float32).reshape(1, N).expand(B, N)
+    ys = torch.gather(y, 1, order).contiguous()
+    ns = mask.to(score.device).sum(1).to(torch.int32).contiguous()
+    out = torch.zeros(B, 4, dtype=torch.float64, device=score.device)
+    _native.kernels().roc_pr_sums_batched(vals.contiguous().data_ptr(), ys.data_ptr(), ns.data_ptr(), B, N,
+                                          out.data_ptr(), _native.stream_ptr())
+    o = out.cpu().tolist()
+    res = [_auc_from_sums(*r) for r in o]
+    return [r[0] for r in res], [r[1] for r in res]
 
 
 def regression_moments(y: torch.Tensor, yhat: torch.Tensor):

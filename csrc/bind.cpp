@@ -478,6 +478,16 @@ PYBIND11_MODULE(_har_native, m) {
           "regression_moments");
   });
 
+  m.def("confusion_matrix_batched", [](u label, u pred, u mask, int64_t n, int B, int K, u cm, u stream) {
+    check(har_confusion_matrix_batched(P<const int32_t>(label), P<const int32_t>(pred), P<const uint8_t>(mask), n, B,
+                                       K, P<int64_t>(cm), S(stream)),
+          "confusion_matrix_batched");
+  });
+  m.def("roc_pr_sums_batched", [](u s, u y, u ns, int B, int64_t ld, u out, u stream) {
+    check(har_roc_pr_sums_batched(P<const float>(s), P<const float>(y), P<const int32_t>(ns), B, ld, P<double>(out),
+                                  S(stream)),
+          "roc_pr_sums_batched");
+  });
   m.def("roc_pr_sums", [](u s, u y, int64_t n, u out, u stream) {
     check(har_roc_pr_sums(P<const float>(s), P<const float>(y), n, P<double>(out), S(stream)), "roc_pr_sums");
   });

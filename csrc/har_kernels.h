@@ -158,9 +158,15 @@ int har_value_counts(const int64_t* codes, int64_t n, int V, int64_t* out, hipSt
 int har_confusion_matrix(const int32_t* label, const int32_t* pred, int64_t n, int K, int64_t* cm,
                          hipStream_t s);
 int har_regression_moments(const float* y, const float* yhat, int64_t n, double* out6, hipStream_t s);
+// B models' confusion matrices over masked rows: pred / mask [B][n] (mask != 0 = scored), cm [B][K][K]
+// (zeroed here)
+int har_confusion_matrix_batched(const int32_t* label, const int32_t* pred, const uint8_t* mask, int64_t n, int B,
+                                 int K, int64_t* cm, hipStream_t s);
 // scores sorted descending, labels permuted alike (positive iff > 0.5):
 // out4 = {sum dFP (TP + TP_prev), sum dTP (prec + prec_prev), P, N} over tie-group end points
 int har_roc_pr_sums(const float* sorted_scores, const float* labels, int64_t n, double* out4, hipStream_t s);
+int har_roc_pr_sums_batched(const float* sorted_scores, const float* labels, const int32_t* ns, int B, int64_t ld,
+                            double* out, hipStream_t s);
 
 // ---- logistic regression (batched over B models, K classes padded to 8) ----
 // ---- device logistic regression + batched L-BFGS / OWL-QN (logreg_qn.hip) ----

@@ -25,6 +25,27 @@ __global__ __launch_bounds__(256) void confusion_kernel(const int32_t* __restric
 
 // codes in [0, V) (others ignored: -1 = null); LDS-privatized 32-bit counters, one 64-bit global
 // atomic per non-zero counter per workgroup (integer adds: order-independent, exact)
+// B models at once (CrossValidator scoring): cm[b] over the rows with mask[b][i] != 0; grid (row
+// chunks, B).  Out-of-range labels / predictions are skipped (the host checks the ranges).
+__global__ __launch_bounds__(256) void confusion_batched_kernel(const int32_t* __restrict__ label,
+                                                                const int32_t* __restrict__ pred,
+                                                                const uint8_t* __restrict__ mask, int64_t n, int K,
+                                                                unsigned long long* __restrict__ cm) {
+  __shared__ unsigned int h[MAXK2];
+  const int KK = K * K, b = blockIdx.y;
+  const int32_t* pb = pred + (size_t)b * n;
+  const uint8_t* mb = mask + (size_t)b * n;
+  for (int i = threadIdx.x; i < KK; i += blockDim.x) h[i] = 0;
+  __syncthreads();
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int l = label[i], p = pb[i];
+    if (mb[i] && (unsigned)l < (unsigned)K && (unsigned)p < (unsigned)K) atomicAdd(&h[l * K + p], 1u);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < KK; i += blockDim.x)
+    if (h[i]) atomicAdd(cm + (size_t)b * KK + i, (unsigned long long)h[i]);
+}
+
 __global__ __launch_bounds__(256) void value_counts_kernel(const int64_t* __restrict__ codes, int64_t n, int V,
                                                            unsigned long long* __restrict__ out) {
   extern __shared__ unsigned int hv[];
@@ -70,6 +91,18 @@ extern "C" int har_confusion_matrix(const int32_t* label, const int32_t* pred, i
   if (n == 0) return 0;
   int blocks = (int)std::min<int64_t>(1024, (n + 255) / 256);
   confusion_kernel<<<blocks, 256, 0, s>>>(label, pred, n, K, reinterpret_cast<unsigned long long*>(cm));
+  HAR_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int har_confusion_matrix_batched(const int32_t* label, const int32_t* pred, const uint8_t* mask, int64_t n,
+                                            int B, int K, int64_t* cm, hipStream_t s) {
+  if (K <= 0 || (int64_t)K * K > MAXK2 || n < 0 || B <= 0 || B > 65535) return -2;
+  if (const hipError_t e = hipMemsetAsync(cm, 0, sizeof(int64_t) * (size_t)B * K * K, s); e != hipSuccess) return (int)e;
+  if (n == 0) return 0;
+  const int chunks = (int)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, std::max(1, 1024 / B)));
+  confusion_batched_kernel<<<dim3(chunks, B), 256, 0, s>>>(label, pred, mask, n, K,
+                                                             reinterpret_cast<unsigned long long*>(cm));
   HAR_CHECK_LAUNCH();
   return 0;
 }

@@ -375,6 +375,7 @@ constexpr int BUP = BQU + 16;         // h1 / dact1 quadrant tile pitch: 40 dwor
 template <int K0> struct Bwd3Lds {
   static constexpr int XP = K0 + 16;
   static constexpr int NXB = 4;  // X tile buffers (staged two tiles ahead; read by h1 / (c) two tiles apart)
+  static_assert((NXB & (NXB - 1)) == 0, "buffer indices are taken with & (NXB - 1)");
   static constexpr int DSM = BRT * BDP, HS = BRT * BUP, XS = BRT * XP;
   static constexpr size_t bytes = (size_t)(2 * DSM + 2 * HS + 2 * HS + NXB * XS) * sizeof(bf16_t) +
                                   4 * BQU * sizeof(float) + 32 * sizeof(uint32_t);
@@ -497,7 +498,7 @@ __global__ __launch_bounds__(512) void mlp_bwd3_kernel(
 #pragma unroll
   for (int f = 0; f < NFW; ++f) acc0[f] = f32x4_t{0.f, 0.f, 0.f, 0.f};
   accb[0] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-  float rs[2][4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+  f32x4_t accd0 = {0.f, 0.f, 0.f, 0.f};  // db0 of unit block ub (column 0: lanes c16 == 0)
 
   // Register staging: one dz piece (8 B: classes 4g.. of row 16 rb2 + c16) + one mask piece (16 B:
   // words 4 jh.. of the row) + one X vector per thread per tile.  Every load is unconditional (a tile
@@ -517,7 +518,7 @@ __global__ __launch_bounds__(512) void mlp_bwd3_kernel(
     mkr = *reinterpret_cast<const uint4*>(lmk + tt_ * BRT * 8);                 \
   }
 #define HAR_B3_LOAD_X(t) xr = *reinterpret_cast<const uint4*>(lx + (int64_t)min(t, tlast) * BRT * K0);
-#define HAR_B3_STAGE_X(i) *reinterpret_cast<uint4*>(xs0 + ((i) % NXB) * L::XS + sdx) = xr;
+#define HAR_B3_STAGE_X(i) *reinterpret_cast<uint4*>(xs0 + ((i) & (NXB - 1)) * L::XS + sdx) = xr;
 
   // dact2 tile from the dz / mask registers -> LDS buffer `buf`: row-major [r][j] with the 16-byte chunks
   // of rows r with bit 2 set swapped in pairs (column ^ 8), which makes these 16-byte stores and the
@@ -561,10 +562,6 @@ __global__ __launch_bounds__(512) void mlp_bwd3_kernel(
       const float d0 = (m.x & 0xffffu) ? a[0] : 0.f, d1 = (m.x >> 16) ? a[1] : 0.f;
       const float d2 = (m.y & 0xffffu) ? a[2] : 0.f, d3 = (m.y >> 16) ? a[3] : 0.f;
       const uint32_t p0 = pack2(d0, d1), p1 = pack2(d2, d3);
-      rs[e][0] += __uint_as_float(p0 << 16);
-      rs[e][1] += __uint_as_float(p0 & 0xffff0000u);
-      rs[e][2] += __uint_as_float(p1 << 16);
-      rs[e][3] += __uint_as_float(p1 & 0xffff0000u);
       *reinterpret_cast<uint2*>(d1s + (16 * rb + c16) * BUP + col) = make_uint2(p0, p1);
     }
 #pragma unroll
@@ -588,18 +585,21 @@ __global__ __launch_bounds__(512) void mlp_bwd3_kernel(
   // (c) of local tile i (its dact1 buffer i & 1, X buffer i % NXB)
   auto tile_c = [&](int i) __attribute__((always_inline)) {
     const bf16_t* d1s = d1s0 + (i & 1) * L::HS;
-    const bf16_t* xs = xs0 + (i % NXB) * L::XS;
+    const bf16_t* xs = xs0 + (i & (NXB - 1)) * L::XS;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       const bf16x8_t A = frag_rows(d1s + 32 * ks * BUP, BUP, 16 * ub, lane);
 #pragma unroll
       for (int f = 0; f < NFW; ++f) acc0[f] = mma32(A, frag_rows(xs + 32 * ks * XP, XP, 16 * (fb + f), lane), acc0[f]);
+      // db0 = sum over the rows of dact1: the same A against a column of ones (waves 4..7 repeat
+      // waves 0..3's block, never stored, so the body stays one basic block)
+      accd0 = mma32(A, ones, accd0);
     }
   };
   // h1 quadrant tile i from X tile i (buffer i % NXB) into h1 buffer i & 1: the forward's operands,
   // accumulation order and rounding (bit-identical h1)
   auto tile_h1 = [&](int i) __attribute__((always_inline)) {
-    const bf16_t* xs = xs0 + (i % NXB) * L::XS;
+    const bf16_t* xs = xs0 + (i & (NXB - 1)) * L::XS;
     bf16_t* hs = hs0 + (i & 1) * L::HS;
 #pragma unroll
     for (int e = 0; e < 2; ++e) {
@@ -645,6 +645,8 @@ __global__ __launch_bounds__(512) void mlp_bwd3_kernel(
     __syncthreads();                // dact2 i+1 / X i+2 staged, h1 i+1 and dact1 i complete
   };
   if (n > 0) iter(0, true);
+  // (not unrolled: a 4x unroll makes every buffer offset an immediate, -34 address VALU per tile,
+  // but the hoisted per-phase bases push the kernel past 256 VGPRs: 50 spilled registers)
   for (int i = 1; i < n; ++i) iter(i, false);
   HAR_STAMP(8, 34)
   if (n > 0) tile_c(n - 1);
@@ -666,18 +668,8 @@ __global__ __launch_bounds__(512) void mlp_bwd3_kernel(
 #pragma unroll
     for (int r = 0; r < 4; ++r) w0o[(size_t)(qu0 + 16 * ub + 4 * g + r) * K0 + 16 * (fb + f) + c16] = acc0[f][r];
   if (wave < 4 && g == 0) gb1[(size_t)slice * slab_stride + 16 * (4 * q + wave) + c16] = accb[0][0];
-#pragma unroll
-  for (int e = 0; e < 2; ++e)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      float v = rs[e][r];
-#pragma unroll
-      for (int o = 1; o < 16; o <<= 1) v += __shfl_xor(v, o, 64);
-      if (c16 == 0) red[rb * BQU + 16 * (up + e) + 4 * g + r] = v;
-    }
-  __syncthreads();
-  if (tid < BQU)
-    gb0[(size_t)slice * slab_stride + qu0 + tid] = (red[tid] + red[BQU + tid]) + (red[2 * BQU + tid] + red[3 * BQU + tid]);
+  if (wave < 4 && c16 == 0)
+    *reinterpret_cast<f32x4_t*>(gb0 + (size_t)slice * slab_stride + qu0 + 16 * ub + 4 * g) = accd0;
   if constexpr (STAMP) __builtin_amdgcn_s_waitcnt(0x0f70);
   HAR_STAMP(8, 35)
   HAR_STAMP_REAL(8, 39)

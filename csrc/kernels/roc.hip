@@ -17,7 +17,15 @@ namespace {
 constexpr int ROC_T = 1024, ROC_I = 4, ROC_W = ROC_T / 64;
 
 __global__ __launch_bounds__(ROC_T) void roc_pr_kernel(const float* __restrict__ s, const float* __restrict__ y,
-                                                      int n, double* __restrict__ out) {
+                                                      int n, double* __restrict__ out, const int32_t* __restrict__ ns,
+                                                      int64_t ld) {
+  // batched (grid = models): model b's scores / labels at + b * ld, its first ns[b] entries
+  if (ns) {
+    s += (size_t)blockIdx.x * ld;
+    y += (size_t)blockIdx.x * ld;
+    n = ns[blockIdx.x];
+    out += 4 * (size_t)blockIdx.x;
+  }
   __shared__ int wtot[ROC_W], whas[ROC_W], wtp[ROC_W], wfp[ROC_W];
   __shared__ int carry[4];  // has point, TP, FP of the last point; positives so far
   __shared__ double wred[2][ROC_W];
@@ -112,7 +120,17 @@ __global__ __launch_bounds__(ROC_T) void roc_pr_kernel(const float* __restrict__
 extern "C" int har_roc_pr_sums(const float* sorted_scores, const float* labels, int64_t n, double* out4,
                                hipStream_t s) {
   if (n < 0 || n >= ((int64_t)1 << 30)) return -2;
-  roc_pr_kernel<<<1, ROC_T, 0, s>>>(sorted_scores, labels, (int)n, out4);
+  roc_pr_kernel<<<1, ROC_T, 0, s>>>(sorted_scores, labels, (int)n, out4, nullptr, 0);
+  HAR_CHECK_LAUNCH();
+  return 0;
+}
+
+// B models: row b of sorted_scores / labels ([B][ld], scores descending) holds ns[b] valid entries
+// (a CrossValidator fold's validation rows, sorted to the front); out [B][4].
+extern "C" int har_roc_pr_sums_batched(const float* sorted_scores, const float* labels, const int32_t* ns, int B,
+                                       int64_t ld, double* out, hipStream_t s) {
+  if (B <= 0 || ld < 0 || ld >= ((int64_t)1 << 30) || !ns) return -2;
+  roc_pr_kernel<<<B, ROC_T, 0, s>>>(sorted_scores, labels, 0, out, ns, ld);
   HAR_CHECK_LAUNCH();
   return 0;
 }

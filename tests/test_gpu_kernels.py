@@ -1,4 +1,5 @@
 """Numerics of every HIP kernel vs. a plain PyTorch fp32/fp64 reference (GPU only)."""
+import numpy as np
 import pytest
 import torch
 
@@ -502,3 +503,21 @@ def test_mlp_fragment_copies_track_pb(cuda, F):
         W0, W1 = L.view(e.Pb, "W0"), L.view(e.Pb, "W1")
         want = torch.cat([_frag_reference(W0), _frag_reference(W1), _frag_reference(W1.T.contiguous())])
         assert torch.equal(e.Pf, want), f"fragment copies differ from Pb after step {step}"
+
+
+@pytest.mark.parametrize("metric", ["accuracy", "f1", "weightedPrecision", "areaUnderROC", "areaUnderPR", "mae"])
+def test_batched_cv_metrics_gpu_match_cpu(cuda, metric):
+    """CrossValidator scoring of B models at once: the batched confusion-matrix kernel and the
+    segmented-sort + batched roc.hip pass give the CPU definitions (one-hot einsum, one sort per
+    model) for every model / fold mask, ties in the scores included."""
+    from har.evaluation.metrics import batched_metrics
+
+    g = torch.Generator().manual_seed(21)
+    B, N, K = 7, 3001, 6
+    label = torch.randint(0, K, (N,), generator=g)
+    pred = torch.randint(0, K, (B, N), generator=g)
+    mask = torch.rand(B, N, generator=g) < 0.3
+    raw = torch.round(torch.randn(B, N, K, generator=g) * 4) / 4  # coarse scores: many ties
+    cpu = batched_metrics(metric, label, pred, mask, K, raw)
+    gpu = batched_metrics(metric, label.to(cuda), pred.to(cuda), mask.to(cuda), K, raw.to(cuda))
+    np.testing.assert_allclose(gpu, cpu, rtol=1e-9, atol=1e-12)
