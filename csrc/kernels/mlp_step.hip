@@ -675,6 +675,325 @@ __global__ __launch_bounds__(512) void mlp_bwd3_kernel(
   HAR_STAMP_REAL(8, 39)
 }
 
+// ------------------------------------------------------------------------------------------------
+// backward, wave-specialized (mlp_bwd4): the same work items, products and summation orders as
+// mlp_bwd3, but the 8 waves split by role instead of by data.  Waves 0..3 PRODUCE the next tile's
+// operands (the dact2 tile from dz / mask, the X tile staging and the h1 recompute: VALU, LDS stores
+// and a few small MFMAs); waves 4..7 CONSUME the current tile (the (a) dact1, (b) dW1, (c) dW0, db0 /
+// db1 products: MFMA with LDS fragment reads).  Each SIMD hosts one producer and one consumer, so
+// the producer's VALU / LDS-store stream issues beside the consumer's MFMA stream instead of both
+// waves of a SIMD running the same phase at the same time (mlp_bwd3: 36% MFMA busy per tile).
+// Each role runs its own loop (disjoint register live ranges: max, not sum, of the two roles'
+// state) with the same barrier sequence: one workgroup barrier per tile.
+//   consumer c: (a) unit blocks 2 (c & 1) .. + 1 x row blocks 2 (c >> 1) .. + 1 (W1^T fragments in
+//               registers, dact2 rows from LDS); (b) all 4 unit blocks x j blocks 4c .. 4c + 3
+//               (64 dW1 accumulators); (c) unit block c x every input block; db0 of unit block c;
+//               db1 of j block 4q + c
+//   producer p: dact2 rows 16p .. + 16 x all 256 j; h1 unit block p x all 4 row blocks; X staging
+template <int K0, bool STAMP>
+__global__ __launch_bounds__(512) void mlp_bwd4_kernel(
+    const uint32_t* __restrict__ dz, const uint32_t* __restrict__ mask, const bf16_t* __restrict__ X,
+    const bf16_t* __restrict__ Wf, const float* __restrict__ b0,
+    const bf16_t* __restrict__ Wo, int B, int S, float* __restrict__ gw1, float* __restrict__ gw0,
+    float* __restrict__ gb0, float* __restrict__ gb1, int64_t slab_stride, int32_t* __restrict__ tick,
+    const float* __restrict__ fslab, int fslab_w, int nfwd, float* __restrict__ gwo, float* __restrict__ gbo,
+    uint64_t* __restrict__ stamps) {
+  using L = Bwd3Lds<K0>;
+  constexpr int NXB = L::NXB, KC = HH / 32, XP = L::XP, NFW = K0 / 32, NFB = K0 / 16;
+  constexpr int XV = BRT * K0 / 8;  // 16-byte vectors of an X tile (512 / 256)
+  constexpr int XPT = XV / 256;     // per producer thread (2 / 1)
+  if (tick && blockIdx.x == 0 && threadIdx.x == 0) *tick += 1;
+  extern __shared__ __attribute__((aligned(16))) bf16_t lds[];
+  bf16_t* const dsm0 = lds;                // [2][64][BDP] dact2 tiles
+  bf16_t* const hs0 = dsm0 + 2 * L::DSM;   // [2][64][BUP] h1 quadrant tiles
+  bf16_t* const d1s0 = hs0 + 2 * L::HS;    // [2][64][BUP] dact1 quadrant tiles
+  bf16_t* const xs0 = d1s0 + 2 * L::HS;    // [NXB][64][XP] X tiles
+  float* const red = reinterpret_cast<float*>(xs0 + NXB * L::XS);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // scalar: the role branches are s_cbranch
+  const int c16 = lane & 15, g = lane >> 4;
+  uint32_t* const lut = reinterpret_cast<uint32_t*>(red + 4 * BQU);  // [16][2] relu' nibble -> AND masks
+  if (tid < 16)
+    *reinterpret_cast<uint2*>(lut + 2 * tid) = make_uint2((tid & 1 ? 0xffffu : 0u) | (tid & 2 ? 0xffff0000u : 0u),
+                                                          (tid & 4 ? 0xffffu : 0u) | (tid & 8 ? 0xffff0000u : 0u));
+  HAR_STAMP_REAL(8, 38)
+  HAR_STAMP(8, 0)
+  const int b = xcd_remap(blockIdx.x, gridDim.x);
+  const int slice = b / BQ, q = b % BQ, qu0 = q * BQU;
+  const bool prod = wave < 4;
+  const int pw = wave & 3;
+  const int ntiles = B / BRT, per = (ntiles + S - 1) / S;
+  const int t0 = slice * per, n = max(0, min(ntiles, t0 + per) - t0);
+
+  // ---- prologue (all waves): W1^T quadrant fragments and Wout into LDS, the forward's dWout slabs ----
+  const bf16_t* const W0f = Wf;
+  const bf16_t* const W1tq = Wf + HH * K0 + HH * HH + (size_t)(4 * q) * KC * 512;
+  bf16_t* const wos = lds;
+  bf16_t* const w1q = lds + NCLS * HH;
+  {
+    uint4 st[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) st[i] = *reinterpret_cast<const uint4*>(W1tq + (size_t)(i * 8 + wave) * 512 + lane * 8);
+    const uint4 so = *reinterpret_cast<const uint4*>(Wo + (size_t)tid * 8);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) *reinterpret_cast<uint4*>(w1q + (i * 8 + wave) * 512 + lane * 8) = st[i];
+    *reinterpret_cast<uint4*>(wos + tid * 8) = so;
+  }
+  constexpr int WO4 = NCLS * HH / 4, NC4 = WO4 + NCLS / 4;
+  const int gwv = blockIdx.x * 8 + wave, nwv = gridDim.x * 8;
+  f32x4_t px[4];
+  auto wo_load = [&](int c4) {
+    const float* src = fslab + (c4 < WO4 ? 4 * c4 : NCLS * HH + 4 * (c4 - WO4));
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      px[r] = lane + 64 * r < nfwd ? *reinterpret_cast<const f32x4_t*>(src + (size_t)(lane + 64 * r) * fslab_w)
+                                   : f32x4_t{0.f, 0.f, 0.f, 0.f};
+  };
+  if (fslab && gwv < NC4) wo_load(gwv);
+  __syncthreads();
+  if (fslab) {
+    for (int c4 = gwv; c4 < NC4; c4 += nwv) {
+      if (c4 != gwv) wo_load(c4);
+      f32x4_t v = (px[0] + px[1]) + (px[2] + px[3]);
+#pragma unroll
+      for (int o = 32; o >= 1; o >>= 1)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] += __shfl_xor(v[e], o, 64);
+      if (lane == 0) *reinterpret_cast<f32x4_t*>(c4 < WO4 ? gwo + 4 * c4 : gbo + 4 * (c4 - WO4)) = v;
+    }
+  }
+  // a row of ones (A operand: row 0) / a column of ones (B operand: column 0): the same registers
+  const bf16x8_t ones = __builtin_bit_cast(bf16x8_t, c16 == 0 ? s16x8_t{0x3f80, 0x3f80, 0x3f80, 0x3f80, 0x3f80,
+                                                                        0x3f80, 0x3f80, 0x3f80}
+                                                              : s16x8_t{0, 0, 0, 0, 0, 0, 0, 0});
+  const int tlast = ntiles - 1;
+
+  if (prod) {
+    // ================================ producer ================================
+    // dact2 A fragments for all 256 j: block t = 2 pp + s holds j = 32 pp + 8 (m >> 2) + 4 s + (m & 3),
+    // so lane group g of pair pp holds the 8 consecutive j = 32 pp + 8 g .. + 7 (one 16-byte store)
+    s16x4_t woa[16];
+#pragma unroll
+    for (int t = 0; t < 16; ++t)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        woa[t][i] = (short)wos[(4 * g + i) * HH + 32 * (t >> 1) + 8 * (c16 >> 2) + 4 * (t & 1) + (c16 & 3)];
+    bf16x8_t w0q[NFW];
+#pragma unroll
+    for (int kc = 0; kc < NFW; ++kc)
+      w0q[kc] = *reinterpret_cast<const bf16x8_t*>(W0f + ((size_t)((4 * q + pw) * NFW + kc) * 64 + lane) * 8);
+    const float4 b0q = *reinterpret_cast<const float4*>(b0 + qu0 + 16 * pw + 4 * g);
+    if constexpr (STAMP) __builtin_amdgcn_s_waitcnt(0x0f70);
+    HAR_STAMP(8, 1)
+    __syncthreads();  // the prologue images are read: the tile buffers may be written
+
+    const uint32_t* ldz = dz + (size_t)(16 * pw + c16) * 8 + 2 * g;
+    const uint32_t* lmk = mask + (size_t)(16 * pw + c16) * 8;
+    const int ptid = tid;  // 0..255
+    static_assert(XPT == 1 || XPT == 2, "one or two X vectors per producer thread");
+    // (macros, not lambdas: a lambda-captured register array is kept in scratch)
+    uint2 dzr;
+    uint4 mk0, mk1, xr0, xr1;
+#define HAR_B4_LOAD_D(t)                                                      \
+  {                                                                           \
+    const int64_t tt_ = min(t, tlast);                                        \
+    dzr = *reinterpret_cast<const uint2*>(ldz + tt_ * BRT * 8);               \
+    mk0 = *reinterpret_cast<const uint4*>(lmk + tt_ * BRT * 8);               \
+    mk1 = *reinterpret_cast<const uint4*>(lmk + tt_ * BRT * 8 + 4);           \
+  }
+#define HAR_B4_LOAD_X(t)                                                                      \
+  {                                                                                           \
+    const int64_t tt_ = min(t, tlast);                                                        \
+    xr0 = *reinterpret_cast<const uint4*>(X + (tt_ * XV + ptid) * 8);                         \
+    if constexpr (XPT == 2) xr1 = *reinterpret_cast<const uint4*>(X + (tt_ * XV + ptid + 256) * 8); \
+  }
+#define HAR_B4_STAGE_X(i)                                                                                  \
+  {                                                                                                        \
+    bf16_t* xb_ = xs0 + ((i) & (NXB - 1)) * L::XS;                                                         \
+    *reinterpret_cast<uint4*>(xb_ + (ptid / (K0 / 8)) * XP + (ptid % (K0 / 8)) * 8) = xr0;                 \
+    if constexpr (XPT == 2)                                                                                \
+      *reinterpret_cast<uint4*>(xb_ + ((ptid + 256) / (K0 / 8)) * XP + ((ptid + 256) % (K0 / 8)) * 8) = xr1; \
+  }
+    // dact2 rows 16 pw + c16 -> LDS buffer `buf` (row-major, 16-byte chunks of rows with bit 2 set
+    // swapped in pairs), relu'(h2) applied by AND masks from the nibble table
+    auto stage_dact2 = [&](int buf) __attribute__((always_inline)) {
+      const int sw = 8 * ((c16 >> 2) & 1);
+      bf16_t* d = dsm0 + buf * L::DSM + (16 * pw + c16) * BDP;
+      const s16x4_t dzv = __builtin_bit_cast(s16x4_t, dzr);
+#pragma unroll
+      for (int pp = 0; pp < 8; ++pp) {
+        const uint4 mk = pp < 4 ? mk0 : mk1;
+        const uint32_t mword = (pp & 3) == 0 ? mk.x : (pp & 3) == 1 ? mk.y : (pp & 3) == 2 ? mk.z : mk.w;
+        const uint32_t mw = mword >> (8 * g);
+        const f32x4_t v0 = mma16(woa[2 * pp], dzv, f32x4_t{0.f, 0.f, 0.f, 0.f});
+        const f32x4_t v1 = mma16(woa[2 * pp + 1], dzv, f32x4_t{0.f, 0.f, 0.f, 0.f});
+        const uint2 m0 = *reinterpret_cast<const uint2*>(lut + 2 * (mw & 0xfu));
+        const uint2 m1 = *reinterpret_cast<const uint2*>(lut + 2 * ((mw >> 4) & 0xfu));
+        *reinterpret_cast<u32x4_t*>(d + ((32 * pp + 8 * g) ^ sw)) =
+            u32x4_t{pack2(v0[0], v0[1]) & m0.x, pack2(v0[2], v0[3]) & m0.y, pack2(v1[0], v1[1]) & m1.x,
+                    pack2(v1[2], v1[3]) & m1.y};
+      }
+    };
+    // h1 unit block pw x 4 row blocks of tile i (X buffer i & 3) -> h1 buffer i & 1 (the forward's
+    // operands, accumulation order and rounding: bit-identical h1)
+    auto tile_h1 = [&](int i) __attribute__((always_inline)) {
+      const bf16_t* xs = xs0 + (i & (NXB - 1)) * L::XS;
+      bf16_t* hs = hs0 + (i & 1) * L::HS;
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const int row = 16 * rr + c16;
+        f32x4_t a = {b0q.x, b0q.y, b0q.z, b0q.w};
+#pragma unroll
+        for (int kc = 0; kc < NFW; ++kc)
+          a = mma32(w0q[kc], *reinterpret_cast<const bf16x8_t*>(xs + row * XP + kc * 32 + 8 * g), a);
+        *reinterpret_cast<uint2*>(hs + row * BUP + 16 * pw + 4 * g) =
+            make_uint2(relu2(pack2(a[0], a[1])), relu2(pack2(a[2], a[3])));
+      }
+    };
+    // invariant at the top of iteration i: dzr / mkr = tile i+1, xr = X tile i+2 (loaded)
+    HAR_B4_LOAD_D(t0)
+    HAR_B4_LOAD_X(t0)
+    stage_dact2(0);
+    HAR_B4_STAGE_X(0)
+    HAR_B4_LOAD_X(t0 + 1)
+    HAR_B4_STAGE_X(1)
+    HAR_B4_LOAD_D(t0 + 1)
+    HAR_B4_LOAD_X(t0 + 2)
+    __builtin_amdgcn_sched_barrier(0);
+    __syncthreads();  // dact2 tile 0, X tiles 0 and 1 are in LDS
+    tile_h1(0);
+    __syncthreads();  // h1 tile 0 complete
+    for (int i = 0; i < n; ++i) {
+      if (i < 24) HAR_STAMP(8, 2 + i)
+      stage_dact2((i + 1) & 1);  // waits for the dz / mask loads issued one iteration ago
+      if (i == 4) HAR_STAMP(8, 26)
+      HAR_B4_STAGE_X(i + 2)
+      HAR_B4_LOAD_D(t0 + i + 2)
+      HAR_B4_LOAD_X(t0 + i + 3)
+      __builtin_amdgcn_sched_barrier(0);  // the refills are issued before the h1 recompute
+      if (i == 4) HAR_STAMP(8, 27)
+      tile_h1(i + 1);  // X tile i+1 has been in LDS since the last barrier
+      if (i == 4) HAR_STAMP(8, 28)
+      __syncthreads();  // dact2 i+1 / X i+2 staged, h1 i+1 complete; the consumers finished tile i
+    }
+    HAR_STAMP(8, 34)
+#undef HAR_B4_LOAD_D
+#undef HAR_B4_LOAD_X
+#undef HAR_B4_STAGE_X
+  } else {
+    // ================================ consumer ================================
+    const int ua0 = 2 * (pw & 1), ra0 = 2 * (pw >> 1);
+    bf16x8_t w1t[2][KC];  // (a) A fragments: A[u][k = j] = W1[32 kc + 8g + i][qu0 + 16 (ua0 + e) + c16]
+#pragma unroll
+    for (int e = 0; e < 2; ++e)
+#pragma unroll
+      for (int kc = 0; kc < KC; ++kc)
+        w1t[e][kc] = *reinterpret_cast<const bf16x8_t*>(w1q + (((ua0 + e) * KC + kc) * 64 + lane) * 8);
+    if constexpr (STAMP) __builtin_amdgcn_s_waitcnt(0x0f70);
+    HAR_STAMP(8, 1)
+    // (paired with the producers' "prologue images are read" barrier: the W1^T image is read above,
+    // the producers then overwrite it with dact2 tile 0)
+    __syncthreads();
+    f32x4_t acc1[4][4], acc0[NFB], accb = {0.f, 0.f, 0.f, 0.f}, accd0 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) acc1[j][u] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int f = 0; f < NFB; ++f) acc0[f] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    // (a) dact1^T = W1^T[u] . dact2^T over row blocks ra0, ra0 + 1; relu'(h1); dact1 -> LDS
+    auto tile_a = [&](int i) __attribute__((always_inline)) {
+      const bf16_t* dsm = dsm0 + (i & 1) * L::DSM;
+      const bf16_t* hs = hs0 + (i & 1) * L::HS;
+      bf16_t* d1s = d1s0 + (i & 1) * L::HS;
+#pragma unroll
+      for (int rr = 0; rr < 2; ++rr) {
+        const int row = 16 * (ra0 + rr) + c16;
+        f32x4_t a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kc = 0; kc < KC; ++kc) {
+          const bf16x8_t bv =
+              *reinterpret_cast<const bf16x8_t*>(dsm + row * BDP + ((kc * 32 + 8 * g) ^ (8 * ((c16 >> 2) & 1))));
+          a0 = mma32(w1t[0][kc], bv, a0);
+          a1 = mma32(w1t[1][kc], bv, a1);
+        }
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          const f32x4_t& a = e ? a1 : a0;
+          const int col = 16 * (ua0 + e) + 4 * g;
+          const uint2 m = *reinterpret_cast<const uint2*>(hs + row * BUP + col);
+          const float d0 = (m.x & 0xffffu) ? a[0] : 0.f, d1 = (m.x >> 16) ? a[1] : 0.f;
+          const float d2 = (m.y & 0xffffu) ? a[2] : 0.f, d3 = (m.y >> 16) ? a[3] : 0.f;
+          *reinterpret_cast<uint2*>(d1s + row * BUP + col) = make_uint2(pack2(d0, d1), pack2(d2, d3));
+        }
+      }
+    };
+    // (b) dW1[j][u] += dact2^T . h1 for j blocks 4 pw .. + 3 x all unit blocks; db1 of j block 4q + pw
+    auto tile_b = [&](int i) __attribute__((always_inline)) {
+      const bf16_t* dsm = dsm0 + (i & 1) * L::DSM;
+      const bf16_t* hs = hs0 + (i & 1) * L::HS;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        bf16x8_t hb[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) hb[u] = frag_rows(hs + 32 * ks * BUP, BUP, 16 * u, lane);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const bf16x8_t da = frag_rows_sw(dsm + 32 * ks * BDP, BDP, 16 * (4 * pw + j), lane);
+#pragma unroll
+          for (int u = 0; u < 4; ++u) acc1[j][u] = mma32(hb[u], da, acc1[j][u]);  // C[u][j]
+        }
+        accb = mma32(ones, frag_rows_sw(dsm + 32 * ks * BDP, BDP, 16 * (4 * q + pw), lane), accb);
+      }
+    };
+    // (c) dW0[u][f] += dact1^T . X of tile i (unit block pw, every input block) and db0
+    auto tile_c = [&](int i) __attribute__((always_inline)) {
+      const bf16_t* d1s = d1s0 + (i & 1) * L::HS;
+      const bf16_t* xs = xs0 + (i & (NXB - 1)) * L::XS;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const bf16x8_t A = frag_rows(d1s + 32 * ks * BUP, BUP, 16 * pw, lane);
+#pragma unroll
+        for (int f = 0; f < NFB; ++f) acc0[f] = mma32(A, frag_rows(xs + 32 * ks * XP, XP, 16 * f, lane), acc0[f]);
+        accd0 = mma32(A, ones, accd0);
+      }
+    };
+    __builtin_amdgcn_s_setprio(1);  // the consumers' MFMA stream is the critical path of a tile
+    __syncthreads();  // (paired with the producers' barrier: dact2 0, X 0 / 1 staged)
+    __syncthreads();  // (paired: h1 tile 0 complete)
+    for (int i = 0; i < n; ++i) {
+      if (i < 24) HAR_STAMP(8, 2 + i)
+      tile_a(i);
+      if (i == 4) HAR_STAMP(8, 29)
+      tile_b(i);
+      if (i == 4) HAR_STAMP(8, 30)
+      if (i > 0) tile_c(i - 1);
+      if (i == 4) HAR_STAMP(8, 31)
+      __syncthreads();  // dact1 i complete; the buffers of tile i may be overwritten
+    }
+    HAR_STAMP(8, 34)
+    if (n > 0) tile_c(n - 1);
+    __builtin_amdgcn_s_setprio(0);
+    // ---- this wave's parts of slab `slice` (flat parameter layout) ----
+    float* w1o = gw1 + (size_t)slice * slab_stride;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        *reinterpret_cast<f32x4_t*>(w1o + (size_t)(16 * (4 * pw + j) + c16) * HH + qu0 + 16 * u + 4 * g) = acc1[j][u];
+    float* w0o = gw0 + (size_t)slice * slab_stride;
+#pragma unroll
+    for (int f = 0; f < NFB; ++f)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) w0o[(size_t)(qu0 + 16 * pw + 4 * g + r) * K0 + 16 * f + c16] = acc0[f][r];
+    if (g == 0) gb1[(size_t)slice * slab_stride + 16 * (4 * q + pw) + c16] = accb[0];
+    if (c16 == 0) *reinterpret_cast<f32x4_t*>(gb0 + (size_t)slice * slab_stride + qu0 + 16 * pw + 4 * g) = accd0;
+  }
+  if constexpr (STAMP) __builtin_amdgcn_s_waitcnt(0x0f70);
+  HAR_STAMP(8, 35)
+  HAR_STAMP_REAL(8, 39)
+}
+
 template <int K0>
 void launch_fwd3(const bf16_t* X, bf16_t* Wf, const float* b0, const float* b1, const bf16_t* Wo,
                  const float* bo, const int32_t* labels, int B, int C, float scale, uint32_t* dz, uint32_t* mask,
@@ -687,7 +1006,12 @@ template <int K0>
 void launch_bwd3(const uint32_t* dz, const uint32_t* mask, const bf16_t* X, const bf16_t* Wf, const float* b0,
                  const bf16_t* Wo, int B, int S, float* gw1, float* gw0, float* gb0, float* gb1, int64_t stride,
                  int32_t* tick, const float* fslab, int fslab_w, int nfwd, float* gwo, float* gbo, hipStream_t s) {
-  auto k = g_har_mlp_stamps ? mlp_bwd3_kernel<K0, true> : mlp_bwd3_kernel<K0, false>;
+  static const bool v4 = [] {
+    const char* e = getenv("HAR_MLP_BWD");
+    return !e || atoi(e) != 3;
+  }();
+  auto k = v4 ? (g_har_mlp_stamps ? mlp_bwd4_kernel<K0, true> : mlp_bwd4_kernel<K0, false>)
+              : (g_har_mlp_stamps ? mlp_bwd3_kernel<K0, true> : mlp_bwd3_kernel<K0, false>);
   k<<<S * BQ, 512, Bwd3Lds<K0>::bytes, s>>>(dz, mask, X, Wf, b0, Wo, B, S, gw1, gw0, gb0, gb1, stride, tick,
                                            fslab, fslab_w, nfwd, gwo, gbo, g_har_mlp_stamps ? g_har_mlp_stamps + STAMP_BWD_OFF : nullptr);
 }

@@ -17,8 +17,10 @@ timeout -k 10 600 python -u -m pytest tests -m gpu -k "$KEXPR" -q -x --timeout 2
 rc=$?; tail -4 "$OUT/pytest.log"; fatal $rc pytest
 timeout -k 10 200 python -u tools/mlp_phase_probe.py 65536 256 > "$OUT/probe.txt" 2>&1
 rc=$?; grep -v amdgpu.ids "$OUT/probe.txt"; fatal $rc probe
+HAR_MLP_BWD=3 timeout -k 10 200 python -u tools/mlp_phase_probe.py 65536 > "$OUT/probe_bwd3.txt" 2>&1
+rc=$?; grep -v amdgpu.ids "$OUT/probe_bwd3.txt" | sed 's/^/[bwd3] /'; fatal $rc probe_bwd3
 timeout -k 10 200 python -u tools/mlp_phase_probe.py --stamps > "$OUT/stamps.txt" 2>&1
-rc=$?; grep -E "prologue|epilogue|total|clock|tile 4" "$OUT/stamps.txt"; fatal $rc stamps
+rc=$?; grep -E -- "---|prologue|epilogue|total|clock|tile 4" "$OUT/stamps.txt"; fatal $rc stamps
 for i in 1 2 3; do
   timeout -k 10 180 python bench.py --no-wisdm --steps 200 --warmup 20 --out "$OUT/bench_$i.json" > "$OUT/bench_$i.log" 2>&1
   rc=$?; fatal $rc bench

@@ -74,13 +74,21 @@ def stamps(B=65536):
     finally:
         mod.mlp_set_stamps(0)
     st = buf.cpu().numpy().view(np.uint64).astype(np.float64).reshape(2, 256 * 8, 40)
-    for k, name in enumerate(("forward", "backward")):
+    bwd4 = os.environ.get("HAR_MLP_BWD", "4") != "3"
+    roles = [("forward", 0, None)]
+    if bwd4:  # mlp_bwd4: waves 0..3 of a workgroup produce, 4..7 consume (own loops, own phase stamps)
+        roles += [("backward producers (waves 0-3)", 1, True), ("backward consumers (waves 4-7)", 1, False)]
+    else:
+        roles += [("backward", 1, None)]
+    for name, k, producer in roles:
         s = st[k]
         live = s[:, 0] > 0
+        if producer is not None:
+            live &= ((np.arange(s.shape[0]) % 8) < 4) == producer
         s = s[live]
         print(f"--- {name}: {live.sum()} waves stamped")
         # forward slots 10.. / backward slots 26.. hold tile-4 sub-phases
-        lim = 10 if (k == 0 and (s[:, 10] > 0).all()) else 26 if (k == 1 and (s[:, 26] > 0).all()) else 34
+        lim = 10 if (k == 0 and (s[:, 10] > 0).all()) else 26 if (k == 1 and ((s[:, 26] > 0) | (s[:, 29] > 0)).all()) else 34
         ntile = int(((s[:, 2:lim] > 0).sum(1)).max())
         rows = [("prologue (weights in regs)", s[:, 1] - s[:, 0])]
         for t in range(min(ntile, 32)):
@@ -96,7 +104,17 @@ def stamps(B=65536):
                    ("  tile 4: stage 1 + X loads", s[:, 13] - s[:, 12]), ("  tile 4: to next tile (barrier)", s[:, 7] - s[:, 13])]
             for nm, v in sub:
                 print(f"  {nm:28s} median {np.median(v):9.0f}  max {v.max():9.0f} cycles")
-        if k == 1 and (s[:, 26] > 0).all():  # backward sub-phases of tile 4 (stamped slots 26..30)
+        if k == 1 and bwd4 and producer and (s[:, 26] > 0).all():  # mlp_bwd4 producer phases of tile 4
+            sub = [("  tile 4: dact2 (tile 5) -> LDS", s[:, 26] - s[:, 6]), ("  tile 4: X stage + refills", s[:, 27] - s[:, 26]),
+                   ("  tile 4: h1 recompute (tile 5)", s[:, 28] - s[:, 27]), ("  tile 4: barrier", s[:, 7] - s[:, 28])]
+            for nm, v in sub:
+                print(f"  {nm:28s} median {np.median(v):9.0f}  max {v.max():9.0f} cycles")
+        if k == 1 and bwd4 and producer is False and (s[:, 29] > 0).all():  # mlp_bwd4 consumer phases
+            sub = [("  tile 4: (a) dact1", s[:, 29] - s[:, 6]), ("  tile 4: (b) dW1 + db1", s[:, 30] - s[:, 29]),
+                   ("  tile 4: (c) dW0 + db0 (tile 3)", s[:, 31] - s[:, 30]), ("  tile 4: barrier", s[:, 7] - s[:, 31])]
+            for nm, v in sub:
+                print(f"  {nm:28s} median {np.median(v):9.0f}  max {v.max():9.0f} cycles")
+        if k == 1 and not bwd4 and (s[:, 26] > 0).all():  # backward sub-phases of tile 4 (stamped slots 26..30)
             sub = [("  tile 4: dact2 -> LDS", s[:, 26] - s[:, 6]), ("  tile 4: X stage + refills", s[:, 27] - s[:, 26]),
                    ("  tile 4: h1 recompute", s[:, 28] - s[:, 27]), ("  tile 4: (a) + (b) + db1", s[:, 29] - s[:, 28]),
                    ("  tile 4: (c) dW0", s[:, 30] - s[:, 29]), ("  tile 4: barrier", s[:, 7] - s[:, 30])]
