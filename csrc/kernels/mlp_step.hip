@@ -201,18 +201,20 @@ __global__ __launch_bounds__(512) void mlp_fwd3_kernel(
         h2p[h][t][1] = relu2(pack2(acc[h][t][2], acc[h][t][3]));
       }
     // relu'(h2) of the wave's 32 units for rows 16h + c16 -> mask word `wave` of the row (every lane
-    // of the row stores the same word)
+    // of the row stores the same word).  Bit 16 t + 4 g + 2 e + b = element b of pair h2p[h][t][e]
+    // is nonzero: after relu each 16-bit half is in [0, 0x7fff], so adding 0x7fff carries into the
+    // half's bit 15 exactly when it is nonzero (no carry crosses the halves); the four bits of a
+    // (t) pair of words are then gathered with shifts instead of a compare + select per element.
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       uint32_t m = 0;
 #pragma unroll
-      for (int t = 0; t < 2; ++t)
-#pragma unroll
-        for (int e = 0; e < 2; ++e) {
-          const uint32_t w2 = h2p[h][t][e];
-          m |= ((w2 & 0xffffu) ? 1u : 0u) << (16 * t + 4 * g + 2 * e);
-          m |= ((w2 >> 16) ? 1u : 0u) << (16 * t + 4 * g + 2 * e + 1);
-        }
+      for (int t = 0; t < 2; ++t) {
+        const uint32_t ta = h2p[h][t][0] + 0x7fff7fffu, tb = h2p[h][t][1] + 0x7fff7fffu;
+        // c: bit 0 = (e 0, lo), 16 = (e 0, hi), 2 = (e 1, lo), 18 = (e 1, hi)
+        const uint32_t c = ((ta >> 15) & 0x10001u) | ((tb >> 13) & 0x40004u);
+        m |= ((c | (c >> 15)) & 0xfu) << (16 * t + 4 * g);
+      }
       m |= swp.x16(m);
       m |= swp.x32(m);
       mask_out[(size_t)(r0 + 16 * h + c16) * 8 + wave] = m;
