@@ -132,7 +132,7 @@ __global__ __launch_bounds__(512) void mlp_fwd3_kernel(
   for (int t = 0; t < 2; ++t) {
 #pragma unroll
     for (int kc = 0; kc < K0C; ++kc)
-      w0f[t][kc] = *reinterpret_cast<const bf16x8_t*>(W0f + ((size_t)((2 * wave + t) * K0C + kc) * 64 + lane) * 8);
+      w0f[t][kc] = *reinterpret_cast<const bf16x8_t*>(W0f + (size_t)((2 * wave + t) * K0C + kc) * 512 + frag_lane_off(lane));
     b0r[t] = *reinterpret_cast<const float4*>(b0 + u0 + 16 * t + 4 * g);
   }
   int ynext = 0;
@@ -145,7 +145,7 @@ __global__ __launch_bounds__(512) void mlp_fwd3_kernel(
   for (int t = 0; t < 2; ++t) {
 #pragma unroll
     for (int kc = 0; kc < KC; ++kc)
-      w1f[t][kc] = *reinterpret_cast<const bf16x8_t*>(W1f + ((size_t)((2 * wave + t) * KC + ((kc + krot) & (KC - 1))) * 64 + lane) * 8);
+      w1f[t][kc] = *reinterpret_cast<const bf16x8_t*>(W1f + (size_t)((2 * wave + t) * KC + ((kc + krot) & (KC - 1))) * 512 + frag_lane_off(lane));
     b1r[t] = *reinterpret_cast<const float4*>(b1 + u0 + 16 * t + 4 * g);
   }
   // stage-3 A fragment: Wout[class c16][u0 + 4g + j] (j < 4), [u0 + 16 + 4g + j - 4] (j >= 4): the k
@@ -292,7 +292,7 @@ __global__ __launch_bounds__(512) void mlp_fwd3_kernel(
               *reinterpret_cast<bf16x8_t*>(tt + (16 * t + c16) * 24 + 8 * (g & 1)) = w1f[t][kc];
         __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the wave's own LDS stores
         __builtin_amdgcn_wave_barrier();
-        *reinterpret_cast<bf16x8_t*>(Wf + HH * K0 + HH * HH + ((size_t)(ub * KC + jc) * 64 + lane) * 8) =
+        *reinterpret_cast<bf16x8_t*>(Wf + HH * K0 + HH * HH + (size_t)(ub * KC + jc) * 512 + frag_lane_off(lane)) =
             frag_tr(tt, 24, 0, lane);
         __builtin_amdgcn_wave_barrier();
       }
@@ -441,7 +441,7 @@ __global__ __launch_bounds__(512) void mlp_bwd3_kernel(
   bf16x8_t w0q[NFW];
 #pragma unroll
   for (int kc = 0; kc < NFW; ++kc)
-    w0q[kc] = *reinterpret_cast<const bf16x8_t*>(W0f + ((size_t)((4 * q + ubh) * NFW + kc) * 64 + lane) * 8);
+    w0q[kc] = *reinterpret_cast<const bf16x8_t*>(W0f + (size_t)((4 * q + ubh) * NFW + kc) * 512 + frag_lane_off(lane));
   const float4 b0q = *reinterpret_cast<const float4*>(b0 + qu0 + 16 * ubh + 4 * g);
   // The forward's per-workgroup dWout / dbout partials are complete before this kernel starts: one
   // wave per 16-byte gradient column sums them (lane l: slabs l, l + 64, ...; then a fixed xor tree)
@@ -476,7 +476,7 @@ __global__ __launch_bounds__(512) void mlp_bwd3_kernel(
   for (int e = 0; e < 2; ++e)
 #pragma unroll
     for (int kc = 0; kc < KC; ++kc)
-      w1t[e][kc] = *reinterpret_cast<const bf16x8_t*>(w1q + (((up + e) * KC + kc) * 64 + lane) * 8);
+      w1t[e][kc] = *reinterpret_cast<const bf16x8_t*>(w1q + ((up + e) * KC + kc) * 512 + frag_lane_off(lane));
   // dact2 A fragments (16x16x16): A[m][k = class] = Wout[4g + i][j(m)] with the row -> j map of block
   // t = 2p + s: j = 128 jh + 32 p + 8 (m >> 2) + 4 s + (m & 3), so lane group g of the block pair p
   // holds the 8 consecutive j = 128 jh + 32 p + 8 g .. + 7: one 16-byte LDS store per pair
@@ -783,7 +783,7 @@ __global__ __launch_bounds__(512) void mlp_bwd4_kernel(
     bf16x8_t w0q[NFW];
 #pragma unroll
     for (int kc = 0; kc < NFW; ++kc)
-      w0q[kc] = *reinterpret_cast<const bf16x8_t*>(W0f + ((size_t)((4 * q + pw) * NFW + kc) * 64 + lane) * 8);
+      w0q[kc] = *reinterpret_cast<const bf16x8_t*>(W0f + (size_t)((4 * q + pw) * NFW + kc) * 512 + frag_lane_off(lane));
     const float4 b0q = *reinterpret_cast<const float4*>(b0 + qu0 + 16 * pw + 4 * g);
     if constexpr (STAMP) __builtin_amdgcn_s_waitcnt(0x0f70);
     HAR_STAMP(8, 1)
@@ -890,7 +890,7 @@ __global__ __launch_bounds__(512) void mlp_bwd4_kernel(
     for (int e = 0; e < 2; ++e)
 #pragma unroll
       for (int kc = 0; kc < KC; ++kc)
-        w1t[e][kc] = *reinterpret_cast<const bf16x8_t*>(w1q + (((ua0 + e) * KC + kc) * 64 + lane) * 8);
+        w1t[e][kc] = *reinterpret_cast<const bf16x8_t*>(w1q + ((ua0 + e) * KC + kc) * 512 + frag_lane_off(lane));
     if constexpr (STAMP) __builtin_amdgcn_s_waitcnt(0x0f70);
     HAR_STAMP(8, 1)
     // (paired with the producers' "prologue images are read" barrier: the W1^T image is read above,
