@@ -157,9 +157,10 @@ def bench_mlp(args, ctx):
     # GPU already out of its idle power state instead of ramping its clock inside a 20-step window
     extras = wisdm_accuracy_fields(args, ctx, hidden=(args.hidden, args.hidden))
     elapsed = timed(ctx, run, args.steps, args.warmup, dev)
-    phases = mlp_phase_times(ctx, eng, Xin, y32, B, nb, global_batch, n=max(10, min(50, args.steps)))
+    # accuracy of the model the timed steps trained, before the phase probe's extra steps move it
     Xt, yt = synthetic_windows(65536, seed=999, device=dev)
     acc = float((torch.argmax(eng.logits(Xt), dim=1) == yt).float().mean())
+    phases = mlp_phase_times(ctx, eng, Xin, y32, B, nb, global_batch, n=max(10, min(50, args.steps)))
     rec = {"value": global_batch * args.steps / elapsed, "ms_per_step": elapsed * 1e3 / args.steps,
            "vs_baseline": None, "vs_baseline_note": BASELINE_NOTE,
            "data": "synthetic WISDM-shaped windows (43 features, 6 classes, class-conditional Gaussian); "

@@ -841,12 +841,15 @@ __global__ __launch_bounds__(QN_BLOCK) void qn_update_kernel(QnArgs a) {
       P1[2 * QN_MAX_M] = tot3[4];  // pg.pg
     }
   }
-  // the last chunk of model b to get here finalizes the model: lane 0 counts the chunk only once its
-  // agent-scope P3 stores have completed (vmcnt drained), and the last chunk reads every chunk's
-  // partials with agent-scope loads
+  // the last chunk of model b to get here finalizes the model.  Memory model: lane 0 publishes the
+  // chunk's P3 / P1 partials with an agent-scope RELEASE fence before counting it (the stores are
+  // complete and written back past this XCD's L2), and the block that counts last takes an agent-scope
+  // ACQUIRE fence before reading any other chunk's partials (its own L2 / L1 copies invalidated), so
+  // the handoff holds across the 8 XCDs without relying on the counter's relaxed ordering
   if (threadIdx.x == 0) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     last = __hip_atomic_fetch_add(a.done + b, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == a.nch - 1;
+    if (last) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   }
   __syncthreads();
   if (!last) return;
