@@ -318,15 +318,25 @@ __global__ __launch_bounds__(512) void mlp_fwd3_kernel(
     if (!last) {
       stage23(k + 1, (k + 1) & 1);
       if (k == 4) HAR_STAMP(FW, 12)
+      // stage 1 reads the X tile whose loads were issued just before the last barrier: hoisted to the
+      // top of the body (as the scheduler likes, to fill the MFMA pipe beside the softmax) it waits out
+      // their whole latency there; here the softmax and stages 2 + 3 cover it
+      __builtin_amdgcn_sched_barrier(0);
       stage1(k & 1);   // tile k+2 (clamped) into the buffer tile k left
       load_x(k + 3);
       if (k == 4) HAR_STAMP(FW, 13)
     }
     __syncthreads();
   };
-  if (nt > 0) iter(0, true, nt == 1);
-  for (int k = 1; k < nt - 1; ++k) iter(k, false, false);
-  if (nt > 1) iter(nt - 1, false, true);
+  // (nt == 1 apart, so that every path into the loop issues its loads in the loop body's order: a
+  // path with other pending loads makes the counted wait for the label at the loop top conservative)
+  if (nt == 1) {
+    iter(0, true, true);
+  } else if (nt > 1) {
+    iter(0, true, false);
+    for (int k = 1; k < nt - 1; ++k) iter(k, false, false);
+    iter(nt - 1, false, true);
+  }
   HAR_STAMP(FW, 34)
   if (nt > 0) stage5((nt - 1) & 1);
   // ---- this workgroup's slab: dWout rows 0..15 x this wave's units, dbout; loss, #correct ----
@@ -794,14 +804,18 @@ __global__ __launch_bounds__(512) void mlp_bwd4_kernel(
     const int ptid = tid;  // 0..255
     static_assert(XPT == 1 || XPT == 2, "one or two X vectors per producer thread");
     // (macros, not lambdas: a lambda-captured register array is kept in scratch)
-    uint2 dzr;
-    uint4 mk0, mk1, xr0, xr1;
+    // the loop-carried dz / mask pieces are single dwords: with 2- / 4-dword tuples the register
+    // allocator re-packs the phi and the back-edge copy then waits out the refill's whole latency
+    uint32_t dz0, dz1, mw0, mw1, mw2, mw3, mw4, mw5, mw6, mw7;
+    uint4 xr0, xr1;
 #define HAR_B4_LOAD_D(t)                                                      \
   {                                                                           \
     const int64_t tt_ = min(t, tlast);                                        \
-    dzr = *reinterpret_cast<const uint2*>(ldz + tt_ * BRT * 8);               \
-    mk0 = *reinterpret_cast<const uint4*>(lmk + tt_ * BRT * 8);               \
-    mk1 = *reinterpret_cast<const uint4*>(lmk + tt_ * BRT * 8 + 4);           \
+    const uint32_t* dp_ = ldz + tt_ * BRT * 8;                                \
+    const uint32_t* mp_ = lmk + tt_ * BRT * 8;                                \
+    dz0 = dp_[0]; dz1 = dp_[1];                                               \
+    mw0 = mp_[0]; mw1 = mp_[1]; mw2 = mp_[2]; mw3 = mp_[3];                   \
+    mw4 = mp_[4]; mw5 = mp_[5]; mw6 = mp_[6]; mw7 = mp_[7];                   \
   }
 #define HAR_B4_LOAD_X(t)                                                                      \
   {                                                                                           \
@@ -821,12 +835,11 @@ __global__ __launch_bounds__(512) void mlp_bwd4_kernel(
     auto stage_dact2 = [&](int buf) __attribute__((always_inline)) {
       const int sw = 8 * ((c16 >> 2) & 1);
       bf16_t* d = dsm0 + buf * L::DSM + (16 * pw + c16) * BDP;
-      const s16x4_t dzv = __builtin_bit_cast(s16x4_t, dzr);
+      const s16x4_t dzv = __builtin_bit_cast(s16x4_t, make_uint2(dz0, dz1));
+      const uint32_t mws[8] = {mw0, mw1, mw2, mw3, mw4, mw5, mw6, mw7};
 #pragma unroll
       for (int pp = 0; pp < 8; ++pp) {
-        const uint4 mk = pp < 4 ? mk0 : mk1;
-        const uint32_t mword = (pp & 3) == 0 ? mk.x : (pp & 3) == 1 ? mk.y : (pp & 3) == 2 ? mk.z : mk.w;
-        const uint32_t mw = mword >> (8 * g);
+        const uint32_t mw = mws[pp] >> (8 * g);
         const f32x4_t v0 = mma16(woa[2 * pp], dzv, f32x4_t{0.f, 0.f, 0.f, 0.f});
         const f32x4_t v1 = mma16(woa[2 * pp + 1], dzv, f32x4_t{0.f, 0.f, 0.f, 0.f});
         const uint2 m0 = *reinterpret_cast<const uint2*>(lut + 2 * (mw & 0xfu));
@@ -870,6 +883,9 @@ __global__ __launch_bounds__(512) void mlp_bwd4_kernel(
       stage_dact2((i + 1) & 1);  // waits for the dz / mask loads issued one iteration ago
       if (i == 4) HAR_STAMP(8, 26)
       HAR_B4_STAGE_X(i + 2)
+      // the refills may not be hoisted above the last reads of the registers they overwrite: a hoisted
+      // load gets fresh registers, and the loop-carried copy back then waits out its whole latency
+      __builtin_amdgcn_sched_barrier(0);
       HAR_B4_LOAD_D(t0 + i + 2)
       HAR_B4_LOAD_X(t0 + i + 3)
       __builtin_amdgcn_sched_barrier(0);  // the refills are issued before the h1 recompute

@@ -485,8 +485,10 @@ def _frag_reference(M: torch.Tensor) -> torch.Tensor:
 
 @pytest.mark.parametrize("F", [43, 20])
 def test_mlp_fragment_copies_track_pb(cuda, F):
-    """The step's fragment-ordered weight copies (Pf = W0 | W1 | W1^T in MFMA fragment order) equal
-    the flat bf16 copy Pb after the engine's init and after every fused Adam update."""
+    """The step's fragment-ordered weight copies (Pf = W0 | W1 | W1^T in MFMA fragment order): the W0 /
+    W1 copies equal the flat bf16 copy Pb after the engine's init and after every fused Adam update;
+    the W1^T copy is written by the step's forward from the W1 it ran with (the backward of the same
+    step reads it), so after a step it holds the W1 from BEFORE that step's update."""
     from har.models.mlp import MLPEngine, pad_input_bf16
 
     B = 4096
@@ -496,13 +498,17 @@ def test_mlp_fragment_copies_track_pb(cuda, F):
     X = pad_input_bf16(torch.randn(B, F, device=cuda, generator=g), e.layout.in_pad)
     y = torch.randint(0, 6, (B,), device=cuda, generator=g).to(torch.int32)
     L = e.layout
+    W1_used = L.view(e.Pb, "W1").clone()
     for step in range(3):
         if step:
+            W1_used = L.view(e.Pb, "W1").clone()
             e.train_step(X, y, B)
         torch.cuda.synchronize()
         W0, W1 = L.view(e.Pb, "W0"), L.view(e.Pb, "W1")
-        want = torch.cat([_frag_reference(W0), _frag_reference(W1), _frag_reference(W1.T.contiguous())])
+        want = torch.cat([_frag_reference(W0), _frag_reference(W1), _frag_reference(W1_used.T.contiguous())])
         assert torch.equal(e.Pf, want), f"fragment copies differ from Pb after step {step}"
+        if step:
+            assert not torch.equal(W1, W1_used), "the update did not move W1"
 
 
 @pytest.mark.parametrize("metric", ["accuracy", "f1", "weightedPrecision", "areaUnderROC", "areaUnderPR", "mae"])

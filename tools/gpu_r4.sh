@@ -21,6 +21,8 @@ HAR_MLP_BWD=3 timeout -k 10 200 python -u tools/mlp_phase_probe.py 65536 > "$OUT
 rc=$?; grep -v amdgpu.ids "$OUT/probe_bwd3.txt" | sed 's/^/[bwd3] /'; fatal $rc probe_bwd3
 timeout -k 10 200 python -u tools/mlp_phase_probe.py --stamps > "$OUT/stamps.txt" 2>&1
 rc=$?; grep -E -- "---|prologue|epilogue|total|clock|tile 4" "$OUT/stamps.txt"; fatal $rc stamps
+timeout -k 10 240 python -u tools/mlp_fit_probe.py > "$OUT/fit_probe.txt" 2>&1
+rc=$?; grep -v amdgpu.ids "$OUT/fit_probe.txt"; fatal $rc fit_probe
 for i in 1 2 3; do
   timeout -k 10 180 python bench.py --no-wisdm --steps 200 --warmup 20 --out "$OUT/bench_$i.json" > "$OUT/bench_$i.log" 2>&1
   rc=$?; fatal $rc bench
