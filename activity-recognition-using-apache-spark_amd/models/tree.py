@@ -392,10 +392,13 @@ def _levels_device_frontier(b: "ForestBuilder", y32, W, N: int, F: int, m: int, 
             store = torch.empty(A * slot_bytes // 4, dtype=torch.float32, device=dev)
         if planned and dp:
             # data parallel: the same work items, histograms summed across ranks by the bound A
+            # the candidates' global class counts (replicated stats): the packed wire format's layout
+            node_cc = (stats.view(Tn * maxn, K)[ct[:A].long() * maxn + cn[:A].long()]
+                       if exact and b.owner is not None and getattr(b, "int_weights", False) else None)
             res = T.hist_split_planned_dp(b.bins, b.nbins, y32, rows, row_w, starts, counts, feats, K, b.max_bins,
                                           b.min_inst, b.min_gain, b.impurity, rows_bound=Tn * N, a_dev=a_dev,
                                           allreduce=None if b.owner is not None else b.allreduce, owner=b.owner,
-                                          bins_rm=bins_rm, max_weight=max_w if exact else -1.0)
+                                          bins_rm=bins_rm, max_weight=max_w if exact else -1.0, node_cc=node_cc)
         elif planned:
             # one device: work items by rows (big nodes chunked), no host sync (ops/tree.py)
             res = T.hist_split_planned(b.bins, b.nbins, y32, rows, row_w, starts, counts, feats, K, b.max_bins,
@@ -544,6 +547,9 @@ def _enqueue_fit(b: "ForestBuilder", bufs: dict, y32, rw, row_offset: int, N: in
         root = bufs["stats"][:, 0].contiguous()
         b.allreduce(root)
         bufs["stats"][:, 0] = root
+        # integer row weights (bootstrap counts x 0/1 folds): histogram counts are integers, so the DP
+        # levels may ship them as packed integer fields (ops.tree.dp_wire_plan)
+        b.int_weights = rw is None or bool(torch.equal(rw, torch.round(rw)))
     return _levels_device_frontier(b, y32, bufs["W"], N, F, m, maxn, bufs["stats"], bufs["feature"], bufs["thresh"],
                                    bufs["left"], bufs["right"], bufs["gains"], bufs["node_of"], n_all=n_all)
 

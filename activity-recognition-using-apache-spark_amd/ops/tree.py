@@ -16,7 +16,9 @@
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass
+from typing import Optional
 
 import numpy as np
 import torch
@@ -427,9 +429,48 @@ def hist_split_planned(bins, nbins_feat, label, rows, row_w, node_start, node_co
 FP16_EXACT_MAX = 2048.0
 
 
+# DP wire format of the per-node histograms (HAR_TREE_DP_WIRE): "packed" = present classes only, each
+# count in an 8 / 16 / 32-bit field of int32 words by its node's total weight (tree_dp.hip); "fp16" =
+# the dense store, fp16 when every count is < 2048, else fp32
+DP_WIRE = os.environ.get("HAR_TREE_DP_WIRE", "packed")
+
+
+def dp_wire_plan(node_cc: torch.Tensor, mb: int, P: int):
+    """The packed wire layout of one DP level from the candidates' GLOBAL class counts ``node_cc``
+    [A, K] (identical on every rank): per node the present classes ``cls`` [A, K] (ascending, first
+    ``kp`` valid), the field width ``bw`` in bytes (1 / 2 / 4: the node's total weight < 2^8 / 2^16 /
+    else) and its words; nodes go to owner ranks in contiguous word-balanced ranges.  Returns
+    (cls, kp, bw, woff, bounds, wmax): ``woff`` [A] int64 = the node's word offset in the [P, wmax]
+    send buffer, ``bounds`` (host list, P + 1) = rank r owns nodes bounds[r] .. bounds[r + 1] - 1.
+    One small device -> host read (the bounds and the widest rank's words)."""
+    A, K = node_cc.shape
+    dev = node_cc.device
+    present = node_cc > 0
+    kp = present.sum(1).to(torch.int32)
+    w = node_cc.sum(1)
+    bw = torch.where(w < 256, 1, torch.where(w < 65536, 2, 4)).to(torch.int32)
+    per = (4 // bw).long()
+    words = (mb * kp.long() + per - 1) // per
+    ar = torch.arange(K, device=dev)
+    cls = (torch.sort(torch.where(present, ar, ar + K), dim=1).values % K).to(torch.int32).contiguous()
+    incl = torch.cumsum(words, 0)
+    excl = incl - words
+    total = incl[-1:].clamp_min(1)
+    own = torch.minimum(excl * P // total, torch.tensor(P - 1, device=dev))
+    bounds_d = torch.searchsorted(own, torch.arange(P + 1, device=dev))
+    bounds_d[-1] = A
+    start = torch.cat([excl, incl[-1:]])[bounds_d]          # first word of each rank's range
+    seg = start[1:] - start[:-1]
+    hdr = torch.cat([bounds_d, seg]).cpu().tolist()
+    bounds, wmax = [int(v) for v in hdr[:P + 1]], max(1, max(int(v) for v in hdr[P + 1:]))
+    woff = (own * wmax + excl - start[own]).contiguous()
+    return cls, kp, bw, woff, bounds, wmax
+
+
 def hist_split_planned_dp(bins, nbins_feat, label, rows, row_w, node_start, node_count, feats, K, max_bins,
                           min_instances, min_info_gain, impurity, rows_bound: int, a_dev: int, allreduce=None,
-                          owner=None, bins_rm=None, prows: int = PLAN_ROWS, max_weight: float = -1.0) -> LevelResult:
+                          owner=None, bins_rm=None, prows: int = PLAN_ROWS, max_weight: float = -1.0,
+                          node_cc: Optional[torch.Tensor] = None) -> LevelResult:
     """The data-parallel level on the planned path.  ``feats.shape[0]`` = A is the level's node count:
     EXACT when ``a_dev`` is 0 (the level loop read its 16-byte count record back), else a bound shared
     by every rank with ``a_dev`` pointing at the device count.
@@ -444,7 +485,12 @@ def hist_split_planned_dp(bins, nbins_feat, label, rows, row_w, node_start, node
        node's weight, known with the count) is <= 2048 the counts travel as fp16 — integer-valued
        (bootstrap x fold weights), so exact — halving the wire bytes again;
     3. split search from the (slice of the) reduced store (mode 7);
-    4. owner: the slice's winners, packed [n, 3 + 2K] (``pack_level``), travel in ONE all-gather."""
+    4. owner: the slice's winners, packed [n, 3 + 2K] (``pack_level``), travel in ONE all-gather.
+
+    With ``node_cc`` (the candidates' global class counts, exact level, integer weights) the owner
+    reduction ships the PACKED wire format instead (``dp_wire_plan`` / tree_dp.hip): present classes
+    only, 8 / 16 / 32-bit integer fields by node weight, one int32 reduce-scatter of word-balanced
+    rank rows; the owner unpacks its summed row into the fp32 store the split kernel reads."""
     A, m = feats.shape
     F, N = bins.shape
     fc = max(1, min(m, LDS_BUDGET // (max_bins * K * 4)))
@@ -492,6 +538,26 @@ def hist_split_planned_dp(bins, nbins_feat, label, rows, row_w, node_start, node
                 allreduce(store)
         launch(7, A, 0, store.data_ptr(), feats.data_ptr(), full, A)
         return _best_chunk(*full, A, chunks, K)
+    if exact and node_cc is not None and DP_WIRE == "packed" and P > 1:
+        mb = m * max_bins
+        cls, kp, bw, woff, bounds, wmax = dp_wire_plan(node_cc[:A].contiguous(), mb, P)
+        send = owner.words_buffer(P * wmax, dev)
+        mod.tree_dp_pack(store.data_ptr(), A, slot, mb, K, cls.data_ptr(), kp.data_ptr(), bw.data_ptr(),
+                         woff.data_ptr(), send.data_ptr(), st)
+        recv = owner.reduce_scatter_words(send, wmax, dev)
+        r = owner.ctx.rank
+        a0, a1 = bounds[r], bounds[r + 1]
+        n = a1 - a0
+        if n > 0:
+            loc = torch.empty(n * slot, dtype=torch.float32, device=dev)
+            mod.tree_dp_unpack(recv.data_ptr(), a0, n, slot, mb, K, cls.data_ptr(), kp.data_ptr(), bw.data_ptr(),
+                               woff.data_ptr(), r * wmax, loc.data_ptr(), st)
+            part = outs(n)
+            launch(7, n, a0, loc.data_ptr(), feats.data_ptr() + 4 * a0 * m, part, n)
+            packed = pack_level(_best_chunk(*part, n, chunks, K))
+        else:
+            packed = torch.zeros(0, 3 + 2 * K, dtype=torch.float32, device=dev)
+        return unpack_level(owner.all_gather_ranges(packed, bounds), K)
     if exact:
         local, a0, a1 = owner.reduce_scatter_store(store.view(P * S, slot), A, narrow)
     else:

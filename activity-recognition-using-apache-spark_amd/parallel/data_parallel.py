@@ -161,6 +161,41 @@ class NodeOwner:
         self.stats["bytes"] += src.numel() * src.element_size()
         return out.to(store.device, torch.float32), a0, a1
 
+    def words_buffer(self, numel: int, device) -> torch.Tensor:
+        """The packed DP send buffer (int32 words, on the device the pack kernel writes)."""
+        return self._buf("pk_src", numel, torch.int32, device)
+
+    def reduce_scatter_words(self, send: torch.Tensor, wmax: int, device) -> torch.Tensor:
+        """Integer-sum reduce-scatter of the packed [P, wmax] int32 rows (field-exact: see
+        csrc/kernels/tree_dp.hip); returns this rank's summed row on ``device``."""
+        P = self.ctx.world_size
+        dev = self._dev() or device
+        src = send if send.device == torch.device(dev) else send.to(dev)
+        out = self._buf("pk_out", wmax, torch.int32, dev)
+        dist.reduce_scatter_tensor(out, src, group=self.ctx.group)
+        self.stats["reduce_scatter"] += 1
+        self.stats["bytes"] += src.numel() * src.element_size()
+        return out.to(device)
+
+    def all_gather_ranges(self, local: torch.Tensor, bounds) -> torch.Tensor:
+        """All-gather of per-rank rows of unequal counts (rank r holds rows bounds[r] .. bounds[r+1]-1):
+        every rank pads to the largest range; returns the [bounds[-1], ...] concatenation."""
+        P = self.ctx.world_size
+        sizes = [bounds[q + 1] - bounds[q] for q in range(P)]
+        S = max(1, max(sizes))
+        inner = tuple(local.shape[1:])
+        w = int(np.prod(inner)) if inner else 1
+        dev = self._dev() or local.device
+        buf = self._buf("ag_src", S * w, local.dtype, dev).view(S, w)
+        buf[: local.shape[0]].copy_(local.reshape(local.shape[0], w))
+        buf[local.shape[0]:].zero_()
+        out = self._buf("ag_out", P * S * w, local.dtype, dev).view(P, S, w)
+        dist.all_gather_into_tensor(out.view(P * S, w), buf, group=self.ctx.group)
+        self.stats["all_gather"] += 1
+        self.stats["bytes"] += out.numel() * out.element_size()
+        full = torch.cat([out[q, :sizes[q]] for q in range(P)], 0)
+        return full.view((bounds[-1],) + inner).to(local.device).clone()
+
     def all_gather(self, local: torch.Tensor, A: int) -> torch.Tensor:
         P = self.ctx.world_size
         if P == 1:

@@ -478,6 +478,17 @@ PYBIND11_MODULE(_har_native, m) {
           "regression_moments");
   });
 
+  m.def("tree_dp_pack", [](u store, int A, int64_t slot, int mb, int K, u cls, u kp, u bw, u woff, u out, u stream) {
+    check(har_tree_dp_pack(P<const float>(store), A, slot, mb, K, P<const int32_t>(cls), P<const int32_t>(kp),
+                           P<const int32_t>(bw), P<const int64_t>(woff), P<int32_t>(out), S(stream)),
+          "tree_dp_pack");
+  });
+  m.def("tree_dp_unpack", [](u in, int a0, int n, int64_t slot, int mb, int K, u cls, u kp, u bw, u woff,
+                             int64_t base, u local, u stream) {
+    check(har_tree_dp_unpack(P<const int32_t>(in), a0, n, slot, mb, K, P<const int32_t>(cls), P<const int32_t>(kp),
+                             P<const int32_t>(bw), P<const int64_t>(woff), base, P<float>(local), S(stream)),
+          "tree_dp_unpack");
+  });
   m.def("confusion_matrix_batched", [](u label, u pred, u mask, int64_t n, int B, int K, u cm, u stream) {
     check(har_confusion_matrix_batched(P<const int32_t>(label), P<const int32_t>(pred), P<const uint8_t>(mask), n, B,
                                        K, P<int64_t>(cm), S(stream)),

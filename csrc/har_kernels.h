@@ -160,6 +160,13 @@ int har_confusion_matrix(const int32_t* label, const int32_t* pred, int64_t n, i
 int har_regression_moments(const float* y, const float* yhat, int64_t n, double* out6, hipStream_t s);
 // B models' confusion matrices over masked rows: pred / mask [B][n] (mask != 0 = scored), cm [B][K][K]
 // (zeroed here)
+// DP forest level wire format (tree_dp.hip): per-node present classes / field widths packed into
+// int32 words (sum-exact), and the owner's unpack back to an fp32 [n][mb][K] store
+int har_tree_dp_pack(const float* store, int A, int64_t slot, int mb, int K, const int32_t* cls, const int32_t* kp,
+                     const int32_t* bw, const int64_t* woff, int32_t* out, hipStream_t s);
+int har_tree_dp_unpack(const int32_t* in, int a0, int n, int64_t slot, int mb, int K, const int32_t* cls,
+                       const int32_t* kp, const int32_t* bw, const int64_t* woff, int64_t base, float* local,
+                       hipStream_t s);
 int har_confusion_matrix_batched(const int32_t* label, const int32_t* pred, const uint8_t* mask, int64_t n, int B,
                                  int K, int64_t* cm, hipStream_t s);
 // scores sorted descending, labels permuted alike (positive iff > 0.5):
