@@ -232,14 +232,19 @@ def wisdm_mlp_accuracy(dev, path: str, layers_hidden=(256, 256), epochs: int = 6
     F = train["features"].data.shape[1]
     est = MultilayerPerceptronClassifier(layers=[F] + list(layers_hidden) + [K], maxIter=epochs, blockSize=batch,
                                          stepSize=lr, seed=seed, device=dev)
-    device_sync(dev)
-    t0 = time.perf_counter()
-    model = est.fit(train)
-    device_sync(dev)
-    fit_s = time.perf_counter() - t0
+    # two fits of the same estimator: the first in the process pays the one-time costs (code-object
+    # loads of the step kernels, allocator growth) and is reported as first_fit_s; fit_s is the
+    # second, the cost of every later fit (the reference suite's fit_s / first_fit_s convention)
+    times = []
+    for _ in range(2):
+        device_sync(dev)
+        t0 = time.perf_counter()
+        model = est.fit(train)
+        device_sync(dev)
+        times.append(time.perf_counter() - t0)
     X_test = features_tensor(test, "features", dev)
     y_test = labels_tensor(test, "label", dev)
     acc = float((model.predict(X_test) == y_test).float().mean())
-    return {"accuracy": acc, "fit_s": fit_s, "n_train": train.count(), "n_test": test.count(),
+    return {"accuracy": acc, "fit_s": times[1], "first_fit_s": times[0], "n_train": train.count(), "n_test": test.count(),
             "layers": [F] + list(layers_hidden) + [K], "epochs": epochs, "batch": batch,
             "encoding": "numeric43 (all 43 WISDM features, '?' -> -1)", "split": "70/30 Philox seed 2018"}

@@ -109,9 +109,10 @@ def test_dp_device_forest_equals_single_with_one_read_per_level(cuda, kind, redu
     m = _estimator(kind).fit_tensors(X.to(cuda), y.to(cuda), 4, thresholds=thr)
     a = m.arrs
     for o in outs:
-        # one 16-byte count record per level (+ the roots') is read back: the collectives are sized by
-        # the real node counts; nothing else leaves the device inside the level loop
-        assert o["reads"][1] <= m.arrs.max_depth + 1 and o["reads"][0] <= 2 * (m.arrs.max_depth + 1), o["reads"]
+        # per level one 16-byte count record (+ the roots') and, on the packed owner path, one
+        # (2P + 1)-int layout header (ops.tree.dp_wire_plan) are read back: the collectives are sized
+        # by the real node counts and present classes; nothing else leaves the device inside the loop
+        assert o["reads"][1] <= m.arrs.max_depth + 1 and o["reads"][0] <= 3 * (m.arrs.max_depth + 1), o["reads"]
         assert torch.equal(o["feature"], a.feature.cpu())
         assert torch.equal(o["threshold"], a.threshold.cpu())
         assert torch.equal(o["stats"], a.stats.cpu())

@@ -421,12 +421,13 @@ def test_subsampled_forest_gpu_equals_cpu(cuda, trees, rate):
     assert torch.equal(g.arrs.feature[:, :3].cpu(), c.arrs.feature[:, :3])
 
 
-@pytest.mark.parametrize("B", [256, 320])
-def test_mlp_epoch_graph_equals_eager_fit(cuda, monkeypatch, B):
+@pytest.mark.parametrize("B,H", [(256, 256), (320, 256), (256, 128), (144, 128)])
+def test_mlp_epoch_graph_equals_eager_fit(cuda, monkeypatch, B, H):
     """A single-GPU MultilayerPerceptronClassifier fit replays one captured HIP graph per epoch
     (static batch buffers, the shuffled rows gathered into them); it must train exactly the
     parameters of the eager step loop.  B = 256 / 320: the small batches main.py and the bench's
-    WISDM accuracy run use (more backward slices than 4-tile slices would give)."""
+    WISDM accuracy run use (more backward slices than 4-tile slices would give); H = 128: main.py's
+    43-128-128-6 on the fused forward + split-K backward (B = 144: not a multiple of 64)."""
     from har.models.mlp import MultilayerPerceptronClassifier
 
     g = torch.Generator().manual_seed(9)
@@ -435,7 +436,7 @@ def test_mlp_epoch_graph_equals_eager_fit(cuda, monkeypatch, B):
     params = []
     for flag in ("1", "0"):
         monkeypatch.setenv("HAR_MLP_EPOCH_GRAPH", flag)
-        est = MultilayerPerceptronClassifier(layers=[43, 256, 256, 6], maxIter=4, blockSize=B, stepSize=1e-3, seed=3,
+        est = MultilayerPerceptronClassifier(layers=[43, H, H, 6], maxIter=4, blockSize=B, stepSize=1e-3, seed=3,
                                              device=cuda)
         params.append(est.fit_tensors(X, y, num_classes=6).engine.P.clone())
     torch.cuda.synchronize()

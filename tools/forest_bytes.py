@@ -65,37 +65,45 @@ def main():
             n, d = stack.pop()
             split = feat[t, n] >= 0
             if split or (d < args.depth and gini[t, n] > 1e-12 and weight[t, n] >= 2):
-                c, w = per_level.get(d, (0, 0.0))
-                per_level[d] = (c + 1, max(w, float(weight[t, n])))
+                c, w, pk = per_level.get(d, (0, 0.0, 0))
+                # packed wire words of the node: m x bins x present classes, fields by node weight
+                kp = int((st[t, n] > 0).sum())
+                wt = float(weight[t, n])
+                bw = 1 if wt < 256 else 2 if wt < 65536 else 4
+                per_level[d] = (c + 1, max(w, wt), pk + -(-m * 32 * kp // (4 // bw)))
             if split:
                 stack += [(left[t, n], d + 1), (right[t, n], d + 1)]
     P = args.world
     slot = m * 32 * K
     rows = []
-    tot_old = tot_new = 0
+    tot_old = tot_new = tot_pk = 0
     A_bound = Tn
     for d in range(args.depth):
-        A, wmax = per_level.get(d, (0, 0.0))
+        A, wmax, words = per_level.get(d, (0, 0.0, 0))
         if A == 0:
             break
         old = A_bound * slot * 4
         S = -(-A // P)
         narrow = wmax <= 2048
         new = P * S * slot * (2 if narrow else 4)
+        pk = words * 4  # word-balanced owner rows: ~ the total words (+ < one node's words per rank)
         tot_old += old
         tot_new += new
+        tot_pk += pk
         rows.append(f"| {d} | {A_bound} | {A} | {wmax:.0f} | {'fp16' if narrow else 'fp32'} | {old / 2**20:.1f} | "
-                    f"{new / 2**20:.2f} | {old / max(new, 1):.1f}x |")
+                    f"{new / 2**20:.2f} | {pk / 2**20:.2f} | {old / max(pk, 1):.1f}x |")
         A_bound = min(2 * A_bound, Tn * n_all)
     print(f"# DP forest histogram wire volume per rank, {args.config}: {Tn} trees, depth {args.depth}, {K} classes, "
           f"{F} features (m = {m} per node), {args.rows_per_gpu} rows x {P} ranks\n")
     print("Level = split level d; bound = r3 store nodes min(2^d T, T N); real = the level's candidates in the fitted forest; "
-          "max w = largest node weight at d (fp16 exact <= 2048). Bytes: one rank's reduce-scatter input.\n")
-    print("| level | r3 bound nodes | real nodes | max w | r4 wire | r3 MiB | r4 MiB | ratio |")
-    print("|---:|---:|---:|---:|---|---:|---:|---:|")
+          "max w = largest node weight at d (fp16 exact <= 2048). Bytes: one rank's reduce-scatter input. "
+          "exact = the dense store sized by the real node count (fp16 when max w <= 2048, HAR_TREE_DP_WIRE=fp16); "
+          "packed = present classes only, 8 / 16 / 32-bit integer fields by node weight (default).\n")
+    print("| level | r3 bound nodes | real nodes | max w | exact wire | r3 MiB | exact MiB | packed MiB | r3 / packed |")
+    print("|---:|---:|---:|---:|---|---:|---:|---:|---:|")
     print("\n".join(rows))
-    print(f"\nper forest: r3 {tot_old / 2**20:.1f} MiB, r4 {tot_new / 2**20:.2f} MiB ({tot_old / max(tot_new, 1):.1f}x less); "
-          f"device {dev}, test accuracy of the fit not measured here")
+    print(f"\nper forest: r3 {tot_old / 2**20:.1f} MiB, exact {tot_new / 2**20:.2f} MiB ({tot_old / max(tot_new, 1):.1f}x less), "
+          f"packed {tot_pk / 2**20:.2f} MiB ({tot_old / max(tot_pk, 1):.1f}x less); device {dev}")
 
 
 if __name__ == "__main__":

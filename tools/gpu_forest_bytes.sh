@@ -16,7 +16,7 @@ timeout -k 10 240 python -u tools/forest_bytes.py rf --rows-per-gpu 60000 --worl
 rc=$?; tail -3 "$OUT/table_rf.md"; fatal $rc table_rf
 run8() {  # $1 = tag, $2 = HAR_TREE_DP_BOUND (0 / 1), rest = bench args
   local tag=$1 bound=$2; shift 2
-  timeout -k 10 400 env HAR_DIST_BACKEND=gloo HAR_DIST_SHARE_DEVICE=1 OMP_NUM_THREADS=2 HAR_TREE_DP_BOUND=$bound \
+  timeout -k 10 400 env HAR_TREE_DP_WIRE=${HAR_TREE_DP_WIRE:-packed} HAR_DIST_BACKEND=gloo HAR_DIST_SHARE_DEVICE=1 OMP_NUM_THREADS=2 HAR_TREE_DP_BOUND=$bound \
       python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29611 \
       bench.py --gpus 8 --steps 1 --warmup 0 --no-wisdm "$@" --out "$OUT/$tag.json" > "$OUT/$tag.log" 2>&1
   local rc=$?
@@ -25,12 +25,16 @@ run8() {  # $1 = tag, $2 = HAR_TREE_DP_BOUND (0 / 1), rest = bench args
 }
 run8 rf9_exact 0 --config rf9 --rows 4000 --trees 100 --rf-parallel data
 rc=$?; fatal $rc rf9_exact
+HAR_TREE_DP_WIRE=fp16 run8 rf9_fp16 0 --config rf9 --rows 4000 --trees 100 --rf-parallel data
+rc=$?; fatal $rc rf9_fp16
 run8 rf9_bound 1 --config rf9 --rows 4000 --trees 100 --rf-parallel data
 rc=$?; fatal $rc rf9_bound
 run8 rf9_tree 0 --config rf9 --rows 4000 --trees 100 --rf-parallel tree
 rc=$?; fatal $rc rf9_tree
 run8 rf_exact 0 --config rf --rows 8000 --rf-parallel data
 rc=$?; fatal $rc rf_exact
+HAR_TREE_DP_WIRE=fp16 run8 rf_fp16 0 --config rf --rows 8000 --rf-parallel data
+rc=$?; fatal $rc rf_fp16
 run8 rf_bound 1 --config rf --rows 8000 --rf-parallel data
 rc=$?; fatal $rc rf_bound
 echo done

@@ -23,6 +23,8 @@ timeout -k 10 200 python -u tools/mlp_phase_probe.py --stamps > "$OUT/stamps.txt
 rc=$?; grep -E -- "---|prologue|epilogue|total|clock|tile 4" "$OUT/stamps.txt"; fatal $rc stamps
 timeout -k 10 240 python -u tools/mlp_fit_probe.py > "$OUT/fit_probe.txt" 2>&1
 rc=$?; grep -v amdgpu.ids "$OUT/fit_probe.txt"; fatal $rc fit_probe
+timeout -k 10 240 python -u tools/mlp_fit_probe.py --hidden 128 > "$OUT/fit_probe128.txt" 2>&1
+rc=$?; grep -v amdgpu.ids "$OUT/fit_probe128.txt"; fatal $rc fit_probe128
 for i in 1 2 3; do
   timeout -k 10 180 python bench.py --no-wisdm --steps 200 --warmup 20 --out "$OUT/bench_$i.json" > "$OUT/bench_$i.log" 2>&1
   rc=$?; fatal $rc bench
