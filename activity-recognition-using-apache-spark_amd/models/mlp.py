@@ -815,7 +815,7 @@ class MultilayerPerceptronClassifier(Estimator, ClassifierParams):
         # the host is out of the small-batch step loop (batch 256: ~3 launches of ~4 us each per step).
         # (the three-kernel step, or the fused forward + split-K backward of the other H = 128 / 256
         # shapes: both enqueue a fixed kernel sequence with no host read)
-        capturable = eng._plan_ok(Xin[:B], y32[:B]) or (eng.native and eng.fused_ok and B % 16 == 0)
+        capturable = eng.native and (eng._plan_ok(Xin[:B], y32[:B]) or (eng.fused_ok and B % 16 == 0))
         use_graph = (eng.native and world_size == 1 and ckpt is None and not os.environ.get("HAR_FAULT_INJECT")
                      and capturable and os.environ.get("HAR_MLP_EPOCH_GRAPH", "1") != "0"
                      and self.maxIter - start_epoch >= 3)
