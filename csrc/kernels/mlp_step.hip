@@ -837,33 +837,53 @@ __global__ __launch_bounds__(512) void mlp_bwd4_kernel(
       bf16_t* d = dsm0 + buf * L::DSM + (16 * pw + c16) * BDP;
       const s16x4_t dzv = __builtin_bit_cast(s16x4_t, make_uint2(dz0, dz1));
       const uint32_t mws[8] = {mw0, mw1, mw2, mw3, mw4, mw5, mw6, mw7};
+      // all 16 table reads first, then the 16 MFMAs, then the masked stores: interleaved per pp, each
+      // read -> AND -> store waited out a full LDS round trip (8 serialized trips per tile)
+      uint2 m0[8], m1[8];
 #pragma unroll
       for (int pp = 0; pp < 8; ++pp) {
         const uint32_t mw = mws[pp] >> (8 * g);
-        const f32x4_t v0 = mma16(woa[2 * pp], dzv, f32x4_t{0.f, 0.f, 0.f, 0.f});
-        const f32x4_t v1 = mma16(woa[2 * pp + 1], dzv, f32x4_t{0.f, 0.f, 0.f, 0.f});
-        const uint2 m0 = *reinterpret_cast<const uint2*>(lut + 2 * (mw & 0xfu));
-        const uint2 m1 = *reinterpret_cast<const uint2*>(lut + 2 * ((mw >> 4) & 0xfu));
-        *reinterpret_cast<u32x4_t*>(d + ((32 * pp + 8 * g) ^ sw)) =
-            u32x4_t{pack2(v0[0], v0[1]) & m0.x, pack2(v0[2], v0[3]) & m0.y, pack2(v1[0], v1[1]) & m1.x,
-                    pack2(v1[2], v1[3]) & m1.y};
+        m0[pp] = *reinterpret_cast<const uint2*>(lut + 2 * (mw & 0xfu));
+        m1[pp] = *reinterpret_cast<const uint2*>(lut + 2 * ((mw >> 4) & 0xfu));
       }
+      f32x4_t v0[8], v1[8];
+#pragma unroll
+      for (int pp = 0; pp < 8; ++pp) {
+        v0[pp] = mma16(woa[2 * pp], dzv, f32x4_t{0.f, 0.f, 0.f, 0.f});
+        v1[pp] = mma16(woa[2 * pp + 1], dzv, f32x4_t{0.f, 0.f, 0.f, 0.f});
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int pp = 0; pp < 8; ++pp)
+        *reinterpret_cast<u32x4_t*>(d + ((32 * pp + 8 * g) ^ sw)) =
+            u32x4_t{pack2(v0[pp][0], v0[pp][1]) & m0[pp].x, pack2(v0[pp][2], v0[pp][3]) & m0[pp].y,
+                    pack2(v1[pp][0], v1[pp][1]) & m1[pp].x, pack2(v1[pp][2], v1[pp][3]) & m1[pp].y};
     };
     // h1 unit block pw x 4 row blocks of tile i (X buffer i & 3) -> h1 buffer i & 1 (the forward's
     // operands, accumulation order and rounding: bit-identical h1)
     auto tile_h1 = [&](int i) __attribute__((always_inline)) {
       const bf16_t* xs = xs0 + (i & (NXB - 1)) * L::XS;
       bf16_t* hs = hs0 + (i & 1) * L::HS;
+      // every X fragment read first (one LDS round trip per tile, not one per row block)
+      bf16x8_t xf[4][NFW];
 #pragma unroll
-      for (int rr = 0; rr < 4; ++rr) {
-        const int row = 16 * rr + c16;
-        f32x4_t a = {b0q.x, b0q.y, b0q.z, b0q.w};
+      for (int rr = 0; rr < 4; ++rr)
 #pragma unroll
         for (int kc = 0; kc < NFW; ++kc)
-          a = mma32(w0q[kc], *reinterpret_cast<const bf16x8_t*>(xs + row * XP + kc * 32 + 8 * g), a);
-        *reinterpret_cast<uint2*>(hs + row * BUP + 16 * pw + 4 * g) =
-            make_uint2(relu2(pack2(a[0], a[1])), relu2(pack2(a[2], a[3])));
+          xf[rr][kc] = *reinterpret_cast<const bf16x8_t*>(xs + (16 * rr + c16) * XP + kc * 32 + 8 * g);
+      __builtin_amdgcn_sched_barrier(0);
+      f32x4_t a[4];
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        a[rr] = f32x4_t{b0q.x, b0q.y, b0q.z, b0q.w};
+#pragma unroll
+        for (int kc = 0; kc < NFW; ++kc) a[rr] = mma32(w0q[kc], xf[rr][kc], a[rr]);
       }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr)
+        *reinterpret_cast<uint2*>(hs + (16 * rr + c16) * BUP + 16 * pw + 4 * g) =
+            make_uint2(relu2(pack2(a[rr][0], a[rr][1])), relu2(pack2(a[rr][2], a[rr][3])));
     };
     // invariant at the top of iteration i: dzr / mkr = tile i+1, xr = X tile i+2 (loaded)
     HAR_B4_LOAD_D(t0)
@@ -880,6 +900,12 @@ __global__ __launch_bounds__(512) void mlp_bwd4_kernel(
     __syncthreads();  // h1 tile 0 complete
     for (int i = 0; i < n; ++i) {
       if (i < 24) HAR_STAMP(8, 2 + i)
+      if constexpr (STAMP) {  // (stamped build only: how long the dz / mask refill is still in flight)
+        if (i == 4) {
+          __builtin_amdgcn_s_waitcnt(0x0f70 | XPT);
+          HAR_STAMP(8, 32)
+        }
+      }
       stage_dact2((i + 1) & 1);  // waits for the dz / mask loads issued one iteration ago
       if (i == 4) HAR_STAMP(8, 26)
       HAR_B4_STAGE_X(i + 2)
@@ -920,31 +946,59 @@ __global__ __launch_bounds__(512) void mlp_bwd4_kernel(
 #pragma unroll
     for (int f = 0; f < NFB; ++f) acc0[f] = f32x4_t{0.f, 0.f, 0.f, 0.f};
     // (a) dact1^T = W1^T[u] . dact2^T over row blocks ra0, ra0 + 1; relu'(h1); dact1 -> LDS
+    // Software-pipelined: the dact2 fragments of k chunk kc + 3 are read while the MFMAs of chunk kc
+    // run (pinned by scheduling groups: 2 LDS reads, then 4 MFMAs, per chunk), and the relu'(h1)
+    // words are read first; written plainly, each chunk's reads were issued right before their MFMAs
+    // and every chunk waited out an LDS round trip
     auto tile_a = [&](int i) __attribute__((always_inline)) {
       const bf16_t* dsm = dsm0 + (i & 1) * L::DSM;
       const bf16_t* hs = hs0 + (i & 1) * L::HS;
       bf16_t* d1s = d1s0 + (i & 1) * L::HS;
+      constexpr int PD = 3;  // prefetch distance (k chunks)
+      const int swz = 8 * ((c16 >> 2) & 1);
+      uint2 hm[2][2];
 #pragma unroll
-      for (int rr = 0; rr < 2; ++rr) {
-        const int row = 16 * (ra0 + rr) + c16;
-        f32x4_t a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
+      for (int rr = 0; rr < 2; ++rr)
 #pragma unroll
-        for (int kc = 0; kc < KC; ++kc) {
-          const bf16x8_t bv =
-              *reinterpret_cast<const bf16x8_t*>(dsm + row * BDP + ((kc * 32 + 8 * g) ^ (8 * ((c16 >> 2) & 1))));
-          a0 = mma32(w1t[0][kc], bv, a0);
-          a1 = mma32(w1t[1][kc], bv, a1);
+        for (int e = 0; e < 2; ++e)
+          hm[rr][e] = *reinterpret_cast<const uint2*>(hs + (16 * (ra0 + rr) + c16) * BUP + 16 * (ua0 + e) + 4 * g);
+      bf16x8_t bv[2][KC];
+#pragma unroll
+      for (int kc = 0; kc < PD; ++kc)
+#pragma unroll
+        for (int rr = 0; rr < 2; ++rr)
+          bv[rr][kc] = *reinterpret_cast<const bf16x8_t*>(dsm + (16 * (ra0 + rr) + c16) * BDP + ((kc * 32 + 8 * g) ^ swz));
+      f32x4_t acc[2][2];
+#pragma unroll
+      for (int rr = 0; rr < 2; ++rr)
+#pragma unroll
+        for (int e = 0; e < 2; ++e) acc[rr][e] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kc = 0; kc < KC; ++kc) {
+        if (kc + PD < KC) {
+#pragma unroll
+          for (int rr = 0; rr < 2; ++rr)
+            bv[rr][kc + PD] =
+                *reinterpret_cast<const bf16x8_t*>(dsm + (16 * (ra0 + rr) + c16) * BDP + (((kc + PD) * 32 + 8 * g) ^ swz));
+          __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);  // the 2 LDS reads of chunk kc + PD
         }
+#pragma unroll
+        for (int rr = 0; rr < 2; ++rr)
+#pragma unroll
+          for (int e = 0; e < 2; ++e) acc[rr][e] = mma32(w1t[e][kc], bv[rr][kc], acc[rr][e]);
+        __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);  // then the 4 MFMAs of chunk kc
+      }
+#pragma unroll
+      for (int rr = 0; rr < 2; ++rr)
 #pragma unroll
         for (int e = 0; e < 2; ++e) {
-          const f32x4_t& a = e ? a1 : a0;
-          const int col = 16 * (ua0 + e) + 4 * g;
-          const uint2 m = *reinterpret_cast<const uint2*>(hs + row * BUP + col);
+          const f32x4_t& a = acc[rr][e];
+          const uint2 m = hm[rr][e];
           const float d0 = (m.x & 0xffffu) ? a[0] : 0.f, d1 = (m.x >> 16) ? a[1] : 0.f;
           const float d2 = (m.y & 0xffffu) ? a[2] : 0.f, d3 = (m.y >> 16) ? a[3] : 0.f;
-          *reinterpret_cast<uint2*>(d1s + row * BUP + col) = make_uint2(pack2(d0, d1), pack2(d2, d3));
+          *reinterpret_cast<uint2*>(d1s + (16 * (ra0 + rr) + c16) * BUP + 16 * (ua0 + e) + 4 * g) =
+              make_uint2(pack2(d0, d1), pack2(d2, d3));
         }
-      }
     };
     // (b) dW1[j][u] += dact2^T . h1 for j blocks 4 pw .. + 3 x all unit blocks; db1 of j block 4q + pw
     auto tile_b = [&](int i) __attribute__((always_inline)) {

@@ -483,15 +483,26 @@ __global__ __launch_bounds__(256) void window_features_persistent_kernel(
 // reads every sample once.  One-shot blocks, several per CU: the loads of one block overlap the
 // arithmetic of the others.
 // ------------------------------------------------------------------------------------------------
-constexpr int RCMAX = 17;  // samples per lane held in registers (C <= RCMAX)
+constexpr int RCMAX_LONG = 31;  // samples per lane held in registers (C <= 31: the flag words hold C bits);
+                                // runs of C <= 17 use a 17-register instantiation (fewer VGPRs)
 
-// reduction over a group of LPW = 16 / 32 / 64 lanes: 16-lane DPP butterflies, then the gfx950 row
-// (lane ^ 16) and half (lane ^ 32) swaps on the VALU
+// reduction over a group of LPW = 8 / 16 / 32 / 64 lanes: 8- / 16-lane DPP butterflies, then the
+// gfx950 row (lane ^ 16) and half (lane ^ 32) swaps on the VALU.  A swap of v with itself leaves
+// {own, partner} in its two outputs (which is which depends on the lane's row / half), so the
+// commutative op takes both outputs directly: no select of the partner
 template <int LPW, typename T, typename Op>
-__device__ __forceinline__ T greduce(T v, Op op, const mlpf::LaneSwap& sw) {
-  v = rreduce<16, T>(v, op);
-  if constexpr (LPW >= 32) v = op(v, __builtin_bit_cast(T, sw.x16(__builtin_bit_cast(uint32_t, v))));
-  if constexpr (LPW >= 64) v = op(v, __builtin_bit_cast(T, sw.x32(__builtin_bit_cast(uint32_t, v))));
+__device__ __forceinline__ T greduce(T v, Op op, const mlpf::LaneSwap&) {
+  v = rreduce<(LPW < 16 ? LPW : 16), T>(v, op);
+  if constexpr (LPW >= 32) {
+    const uint32_t u = __builtin_bit_cast(uint32_t, v);
+    const auto r = __builtin_amdgcn_permlane16_swap(u, u, false, false);
+    v = op(__builtin_bit_cast(T, (uint32_t)r[0]), __builtin_bit_cast(T, (uint32_t)r[1]));
+  }
+  if constexpr (LPW >= 64) {
+    const uint32_t u = __builtin_bit_cast(uint32_t, v);
+    const auto r = __builtin_amdgcn_permlane32_swap(u, u, false, false);
+    v = op(__builtin_bit_cast(T, (uint32_t)r[0]), __builtin_bit_cast(T, (uint32_t)r[1]));
+  }
   return v;
 }
 
@@ -532,12 +543,12 @@ __device__ __forceinline__ uint32_t bin_of(float x, float sc, float lo) {
   return b < (uint32_t)(NB - 1) ? b : (uint32_t)(NB - 1);
 }
 
-template <int A, int LPW, bool MLP>
+template <int A, int LPW, bool MLP, int RCMAX>
 __global__ __launch_bounds__(256) void window_features_reg_kernel(const float* __restrict__ stream, int W,
                                                                   int stride, int64_t n_windows, float ms_per_sample,
                                                                   float* __restrict__ out, int ld_out, MlpOut mo,
                                                                   int C, int wpb) {
-  static_assert(LPW == 16 || LPW == 32 || LPW == 64, "groups of 16, 32 or 64 lanes");
+  static_assert(LPW == 8 || LPW == 16 || LPW == 32 || LPW == 64, "groups of 8, 16, 32 or 64 lanes");
   constexpr int T3 = A / 3, GPW = 64 / LPW;
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int nt = (int)blockDim.x, tid = (int)threadIdx.x;
@@ -702,13 +713,16 @@ __global__ __launch_bounds__(256) void window_features_reg_kernel(const float* _
     for (int j = 0; j < 5; ++j)
       hw[j] = greduce<LPW, uint32_t>((uint32_t)((h[c] >> (12 * j)) & 63) | ((uint32_t)((h[c] >> (12 * j + 6)) & 63) << 16),
                                      usum, sw);
-    {
+    // lane `sub` writes bin `sub` (and bin sub + 8 for 8-lane groups)
+#pragma unroll
+    for (int b0 = 0; b0 < NB; b0 += LPW) {
+      const int bn = b0 + sub;
       uint32_t word = hw[0];
 #pragma unroll
-      for (int j = 1; j < 5; ++j) word = (sub >> 1) == j ? hw[j] : word;
-      uint32_t cnt = (sub & 1) ? word >> 16 : word & 0xffffu;
-      cnt -= (uint32_t)sub == bin_of(xl[c], sc[c], off[c]) ? (uint32_t)(LPW * C - W) : 0u;
-      emit(sub < NB, ax * NB + sub, (float)cnt * invW);
+      for (int j = 1; j < 5; ++j) word = (bn >> 1) == j ? hw[j] : word;
+      uint32_t cnt = (bn & 1) ? word >> 16 : word & 0xffffu;
+      cnt -= (uint32_t)bn == bin_of(xl[c], sc[c], off[c]) ? (uint32_t)(LPW * C - W) : 0u;
+      emit(bn < NB, ax * NB + bn, (float)cnt * invW);
     }
     const float peak =
         npk >= 2 ? (float)(last - first) * __builtin_amdgcn_rcpf((float)(npk - 1)) * ms_per_sample : NAN;
@@ -804,14 +818,18 @@ int launch_axes(const float* stream, int64_t n_samples, int window, int stride, 
     HAR_CHECK_LAUNCH();
     return 0;
   };
-  // register-resident kernel: the smallest group (16 / 32 / 64 lanes) whose runs of C <= RCMAX
+  // register-resident kernel: the smallest group (8 / 16 / 32 / 64 lanes) whose runs of C <= RCMAX
   // samples (C odd: lanes C*A floats apart hit distinct LDS banks for odd A) cover the window
   if (!g_window_legacy) {
-    // the smallest group (16 / 32 / 64 lanes), then the shortest odd run C in {5, 9, 13, 17} (lanes
-    // C*A floats apart hit distinct LDS banks for odd A) with LPW * C >= W (W <= 1088)
+    // the smallest group (8 / 16 / 32 / 64 lanes), then the shortest odd run C <= 31 (lanes C*A
+    // floats apart hit distinct LDS banks for odd A) with LPW * C >= W (W <= 1984): the fewer lanes
+    // per window, the fewer cross-lane reductions per sample (~a third of the VALU at 32 lanes)
+    // (8-lane groups only for overlapping windows: their span is shared, so the LDS per window — which
+    // bounds the waves per CU — stays small; measured: W = 200 stride 100 69 vs 77 us, stride 200 54
+    // vs 47 us with 8- vs 16-lane groups)
     int lpw = 0, C = 0;
-    for (int l = 16; l <= 64 && !lpw; l *= 2)
-      for (int c : {5, 9, 13, 17})
+    for (int l = stride < window ? 8 : 16; l <= 64 && !lpw; l *= 2)
+      for (int c = 5; c <= RCMAX_LONG; c += 2)
         if (l * c >= window) { lpw = l; C = c; break; }
     if (lpw) {
       const int gpw = 64 / lpw;
@@ -828,12 +846,17 @@ int launch_axes(const float* stream, int64_t n_samples, int window, int stride, 
         const int64_t nblk = (n_windows + wpb - 1) / wpb;
         const size_t bytes = (size_t)span_bytes(wpb);
         const unsigned grid = (unsigned)nblk;  // one-shot blocks (a persistent DMA-prefetch variant measured slower)
-#define HAR_WIN_R(L)                                                                                         \
-  window_features_reg_kernel<A, L, MLP><<<grid, nt, bytes, s>>>(stream, window, stride, n_windows, ms, out, ld_out, \
-                                                                mo, C, wpb)
-        if (lpw == 16) HAR_WIN_R(16);
-        else if (lpw == 32) HAR_WIN_R(32);
-        else HAR_WIN_R(64);
+#define HAR_WIN_R(L)                                                                                          \
+  if (C <= 17)                                                                                             \
+    window_features_reg_kernel<A, L, MLP, 17><<<grid, nt, bytes, s>>>(stream, window, stride, n_windows, ms, out, \
+                                                                      ld_out, mo, C, wpb);                 \
+  else                                                                                                     \
+    window_features_reg_kernel<A, L, MLP, RCMAX_LONG><<<grid, nt, bytes, s>>>(stream, window, stride, n_windows, \
+                                                                              ms, out, ld_out, mo, C, wpb)
+        if (lpw == 8) { HAR_WIN_R(8); }
+        else if (lpw == 16) { HAR_WIN_R(16); }
+        else if (lpw == 32) { HAR_WIN_R(32); }
+        else { HAR_WIN_R(64); }
 #undef HAR_WIN_R
         HAR_CHECK_LAUNCH();
         return 0;
