@@ -588,7 +588,9 @@ __global__ __launch_bounds__(QN_BLOCK) void qn_direction_kernel(QnArgs a) {
     }
     if (i < mm) rhv = a.rho[i * a.B + b];
     reduce_chunks_shared<NP1>(a.P1 + (int64_t)b * a.nch * NP1, a.nch, p1v, stage);
-    if (i < mm * mm) {
+    // every entry of the [QN_MAX_M]^2 images written (zeros past m^2): the recursion below reads whole
+    // rows / columns unconditionally, its products with the zero coefficients of unused slots exact
+    if (i < QN_MAX_M * QN_MAX_M) {
       SY[i] = syv;
       YY[i] = yyv;
     }
@@ -607,12 +609,14 @@ __global__ __launch_bounds__(QN_BLOCK) void qn_direction_kernel(QnArgs a) {
       for (int i = 0; i < a.filled; ++i) {  // newest -> oldest: q = pg + sum u_k y_k
         const int j = (a.head - 1 - i + mm) % mm;
         const double rho = rho_s[j];
-        if (rho == 0.0) continue;
+        // (a rejected pair, rho = 0: alj = 0 leaves u and al as the skipped step did; a select, not a
+        // branch, so rho's read issues with the row's)
+        // unconditional reads (j mm + k < QN_MAX_M^2; ur[k] = 0 for k >= mm): no branch per k, so the
+        // ten LDS reads issue together instead of one round trip per term; the sum order is unchanged
         double sq = p1v[j];
 #pragma unroll
-        for (int k = 0; k < QN_MAX_M; ++k)
-          if (k < mm) sq += ur[k] * SY[j * mm + k];
-        const double alj = rho * sq;
+        for (int k = 0; k < QN_MAX_M; ++k) sq += ur[k] * SY[j * mm + k];
+        const double alj = rho == 0.0 ? 0.0 : rho * sq;
 #pragma unroll
         for (int k = 0; k < QN_MAX_M; ++k) {
           alr[k] = k == j ? alj : alr[k];
@@ -630,19 +634,16 @@ __global__ __launch_bounds__(QN_BLOCK) void qn_direction_kernel(QnArgs a) {
       for (int i = a.filled - 1; i >= 0; --i) {  // oldest -> newest: r = gamma q + sum w_k s_k
         const int j = (a.head - 1 - i + mm) % mm;
         const double rho = rho_s[j];
-        if (rho == 0.0) continue;
         double yr = p1v[QN_MAX_M + j];
 #pragma unroll
-        for (int k = 0; k < QN_MAX_M; ++k)
-          if (k < mm) yr += ur[k] * YY[j * mm + k];
+        for (int k = 0; k < QN_MAX_M; ++k) yr += ur[k] * YY[j * mm + k];
         yr *= gm;
 #pragma unroll
-        for (int k = 0; k < QN_MAX_M; ++k)
-          if (k < mm) yr += wr[k] * SY[k * mm + j];
+        for (int k = 0; k < QN_MAX_M; ++k) yr += wr[k] * SY[k * mm + j];
         double alj = 0.0;
 #pragma unroll
         for (int k = 0; k < QN_MAX_M; ++k) alj = k == j ? alr[k] : alj;
-        const double dw = alj - rho * yr;
+        const double dw = rho == 0.0 ? 0.0 : alj - rho * yr;  // (rho = 0: the skipped step, w unchanged)
 #pragma unroll
         for (int k = 0; k < QN_MAX_M; ++k) wr[k] = k == j ? wr[k] + dw : wr[k];
       }
