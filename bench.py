@@ -507,9 +507,12 @@ def _stream_full_pass(args, ctx, spec, stream, labels, eng, mean, inv_std, sampl
     def one_pass(i):
         X, first_w = sharded_window_features(ctx, stream, fz, offset, total, transform=inputs)
         xin_rows["n"] = X.shape[0]
-        # window j starts at j * stride; its label is that of the generated segment it starts in
-        lab = labels[(torch.arange(first_w, first_w + nb * B, device=dev) * fz.stride) // W - offset // W]
-        y32 = lab.to(torch.int32)
+        # window j starts at j * stride; its label is that of the generated segment it starts in (the
+        # same windows every pass: the int32 label vector is built by the first (warm-up) pass only)
+        y32 = xin_rows.get(("y", first_w))
+        if y32 is None:
+            lab = labels[(torch.arange(first_w, first_w + nb * B, device=dev) * fz.stride) // W - offset // W]
+            y32 = xin_rows[("y", first_w)] = lab.to(torch.int32)
         for j in range(nb):
             eng.train_step(X[j * B:(j + 1) * B], y32[j * B:(j + 1) * B], gb)
 

@@ -61,9 +61,9 @@ for name, legacy in modes:
         gb = s.numel() * 4 / 1e9
         print(f"{name:7s} {s.shape[1]} axes W={W} stride={W}: {us:8.1f} us  {gb / us * 1e3:6.2f} TB/s ({gb:.3f} GB)")
     us = timed(lambda: window_features_mlp(s3, 200, 200, 20.0, mean, inv, 64, -1.0, out=out))
-    print(f"{name:7s} 3 axes W=200 MLP rows : {us:8.1f} us  {s3.numel() * 4 / us / 1e3:6.2f} TB/s")
+    print(f"{name:7s} 3 axes W=200 MLP rows : {us:8.1f} us  {s3.numel() * 4 / us / 1e6:6.2f} TB/s")
     us = timed(lambda: window_features(s3, 200, 100, 20.0))
-    print(f"{name:7s} 3 axes W=200 stride=100: {us:8.1f} us  {s3.numel() * 4 / us / 1e3:6.2f} TB/s")
+    print(f"{name:7s} 3 axes W=200 stride=100: {us:8.1f} us  {s3.numel() * 4 / us / 1e6:6.2f} TB/s ({s3.shape[0] // 100 - 1} windows)")
 mod.window_set_legacy(0)
 torch.cuda.synchronize()
 print("ok")
