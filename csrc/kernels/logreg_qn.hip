@@ -52,17 +52,31 @@ constexpr int EVAL_DCH = 32;                       // dense columns per LDS chun
 // (the 54-model CrossValidator batch: 62 -> 49 us per evaluation)
 constexpr int EVAL_XLD_NARROW = 11;
 __host__ __device__ constexpr int eval_xld(int Fd) { return Fd <= EVAL_XLD_NARROW - 1 ? EVAL_XLD_NARROW : EVAL_DCH + 1; }
+// Dense designs wider than the narrow tile run both dense products on the matrix cores (MF kernels,
+// v_mfma_f32_16x16x4_f32: fp32 operands, fp32 accumulation): the margins of the tile's 256 rows as
+// W^T . X^T (16 classes x 4 columns per step; KP = 8 pads the class rows with zeros) and the tile's
+// dense gradient R^T . X (16 classes x 16 columns, the rows split over the 4 waves, their partials
+// added in a fixed order: still bitwise reproducible).  Row pitch 36: the chunk zero-padded to a
+// multiple of 4 columns, and the 16 rows x 4 columns of an operand read hit 64 distinct banks.
+constexpr int EVAL_XLD_MF = 36;
 
 template <int KP, int XLD>
 __device__ __forceinline__ void eval_stage_chunk(const LogregEvalArgs& a, const float* W, float* wd, float* xs,
                                                  int c0, int nc, int64_t r0, int64_t nrow_tile, bool weights) {
   const int tid = threadIdx.x;
+  // (MF pitch: columns nc .. nc4 - 1 of the chunk staged as zeros, the MFMA k steps are 4 wide)
+  const int ncs = XLD == EVAL_XLD_MF ? (nc + 3) & ~3 : nc;
   if (weights)
-    for (int e = tid; e < nc * KP; e += EVAL_ROWS) wd[e] = W[(int64_t)a.dense_cols[c0 + e / KP] * KP + (e % KP)];
-  for (int e = tid; e < EVAL_ROWS * nc; e += EVAL_ROWS) {
-    const int rr = e / nc, j = e % nc;
-    xs[rr * XLD + j] = rr < nrow_tile ? a.dense[(r0 + rr) * a.ldd + c0 + j] : 0.f;
+    for (int e = tid; e < ncs * KP; e += EVAL_ROWS)
+      wd[e] = e / KP < nc ? W[(int64_t)a.dense_cols[c0 + e / KP] * KP + (e % KP)] : 0.f;
+  for (int e = tid; e < EVAL_ROWS * ncs; e += EVAL_ROWS) {
+    const int rr = e / ncs, j = e % ncs;
+    xs[rr * XLD + j] = (rr < nrow_tile && j < nc) ? a.dense[(r0 + rr) * a.ldd + c0 + j] : 0.f;
   }
+}
+
+__device__ __forceinline__ f32x4_t mfma4(float a, float b, f32x4_t c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
 template <int KP, int XLD>
@@ -74,6 +88,10 @@ __global__ __launch_bounds__(EVAL_ROWS) void logreg_eval_kernel(LogregEvalArgs a
   float* xs = wd + EVAL_DCH * KP;                  // [EVAL_ROWS][xld] dense row tile, one chunk
   float* rs = xs + EVAL_ROWS * xld;                // [EVAL_ROWS][KP]
   float* red = rs + EVAL_ROWS * KP;                // [EVAL_ROWS / 64]
+  constexpr bool MF = XLD == EVAL_XLD_MF;          // matrix-core dense products
+  float* pb = red + EVAL_ROWS / 64;                // MF: [4 waves][EVAL_DCH][KP] gradient partials
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int l16 = lane & 15, kq = lane >> 4;
 
   const int tid = threadIdx.x;
   const int bt = a.model0 + blockIdx.y * a.tstride;  // trial model (its residual rows: R slot blockIdx.y)
@@ -89,18 +107,39 @@ __global__ __launch_bounds__(EVAL_ROWS) void logreg_eval_kernel(LogregEvalArgs a
   float z[KP];
 #pragma unroll
   for (int k = 0; k < KP; ++k) z[k] = W[(int64_t)a.F * KP + k];  // intercept row
+  f32x4_t za[4] = {f32x4_t{0.f, 0.f, 0.f, 0.f}, f32x4_t{0.f, 0.f, 0.f, 0.f}, f32x4_t{0.f, 0.f, 0.f, 0.f},
+                   f32x4_t{0.f, 0.f, 0.f, 0.f}};  // MF: z^T of the wave's 4 row blocks (lane: row l16, classes 4 kq + r)
   for (int ch = 0; ch < nchunk; ++ch) {
     const int c0 = ch * EVAL_DCH, nc = min(EVAL_DCH, Fd - c0);
     if (ch) __syncthreads();                       // the previous chunk is consumed
     eval_stage_chunk<KP, XLD>(a, W, wd, xs, c0, nc, r0, nrow_tile, true);
     __syncthreads();
-    if (ok) {
+    if constexpr (MF) {
+      const int nc4 = (nc + 3) & ~3;
+      for (int j0 = 0; j0 < nc4; j0 += 4) {
+        const float av = l16 < KP ? wd[(j0 + kq) * KP + l16] : 0.f;  // A = W^T [class l16][column j0 + kq]
+#pragma unroll
+        for (int rb = 0; rb < 4; ++rb)                                   // B = X^T [column j0 + kq][row l16]
+          za[rb] = mfma4(av, xs[(wv * 64 + rb * 16 + l16) * XLD + j0 + kq], za[rb]);
+      }
+    } else if (ok) {
       for (int j = 0; j < nc; ++j) {
         const float xv = xs[tid * xld + j];
 #pragma unroll
         for (int k = 0; k < KP; ++k) z[k] = fmaf(xv, wd[j * KP + k], z[k]);
       }
     }
+  }
+  if constexpr (MF) {  // the margins through LDS to their rows' threads
+#pragma unroll
+    for (int rb = 0; rb < 4; ++rb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (4 * kq + r < KP) rs[(wv * 64 + rb * 16 + l16) * KP + 4 * kq + r] = za[rb][r];
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < KP; ++k) z[k] += rs[tid * KP + k];
+    __syncthreads();                               // rs is rewritten with the residuals below
   }
   float lossv = 0.f;
   if (ok) {
@@ -168,11 +207,31 @@ __global__ __launch_bounds__(EVAL_ROWS) void logreg_eval_kernel(LogregEvalArgs a
       eval_stage_chunk<KP, XLD>(a, W, wd, xs, c0, nc, r0, nrow_tile, false);
       __syncthreads();
     }
-    for (int o = tid; o < nc * KP; o += EVAL_ROWS) {
-      const int j = o / KP, k = o % KP;
-      float acc = 0.f;
-      for (int i = 0; i < EVAL_ROWS; ++i) acc = fmaf(rs[i * KP + k], xs[i * xld + j], acc);
-      slab[(int64_t)c0 * KP + o] = acc;
+    if constexpr (MF) {
+      // wave wv: rows 64 wv .. + 63 of R^T . X for every 16-column block of the chunk -> pb[wv]
+      for (int fb = 0; fb * 16 < nc; ++fb) {
+        f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 4
+        for (int i0 = 0; i0 < 64; i0 += 4) {
+          const int row = wv * 64 + i0 + kq;
+          const float av = l16 < KP ? rs[row * KP + l16] : 0.f;   // A = R^T [class l16][row]
+          acc = mfma4(av, xs[row * XLD + fb * 16 + l16], acc);     // B = X [row][column fb 16 + l16]
+        }
+        const int j = fb * 16 + l16;                               // D: column j, classes 4 kq + r
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (j < nc && 4 * kq + r < KP) pb[(wv * EVAL_DCH + j) * KP + 4 * kq + r] = acc[r];
+      }
+      __syncthreads();
+      for (int o = tid; o < nc * KP; o += EVAL_ROWS)
+        slab[(int64_t)c0 * KP + o] = (pb[o] + pb[EVAL_DCH * KP + o]) + (pb[2 * EVAL_DCH * KP + o] + pb[3 * EVAL_DCH * KP + o]);
+    } else {
+      for (int o = tid; o < nc * KP; o += EVAL_ROWS) {
+        const int j = o / KP, k = o % KP;
+        float acc = 0.f;
+        for (int i = 0; i < EVAL_ROWS; ++i) acc = fmaf(rs[i * KP + k], xs[i * xld + j], acc);
+        slab[(int64_t)c0 * KP + o] = acc;
+      }
     }
   }
   // intercept gradient sum R of the tile
@@ -871,11 +930,21 @@ extern "C" int har_logreg_eval(const LogregEvalArgs* args, int KP, int n_models,
     return -2;
   if (a.N == 0 || n_models == 0) return 0;
   const int tiles = (int)((a.N + EVAL_ROWS - 1) / EVAL_ROWS);
-  const int xld = eval_xld(a.Fd);
-  const size_t lds = sizeof(float) * (EVAL_DCH * KP + EVAL_ROWS * xld + EVAL_ROWS * KP + EVAL_ROWS / 64);
+  static const bool mf_on = [] {
+    const char* e = std::getenv("HAR_LR_EVAL_MFMA");
+    return !e || std::atoi(e) != 0;
+  }();
+  const bool narrow = eval_xld(a.Fd) == EVAL_XLD_NARROW;
+  const bool mf = mf_on && !narrow;
+  const int xld = mf ? EVAL_XLD_MF : eval_xld(a.Fd);
+  const size_t lds = sizeof(float) * (EVAL_DCH * KP + EVAL_ROWS * xld + EVAL_ROWS * KP + EVAL_ROWS / 64 +
+                                      (mf ? 4 * EVAL_DCH * KP : 0));
   dim3 grid(tiles, n_models);
-  const bool narrow = xld == EVAL_XLD_NARROW;
-  if (KP == 8 && narrow)
+  if (mf && KP == 8)
+    logreg_eval_kernel<8, EVAL_XLD_MF><<<grid, EVAL_ROWS, lds, s>>>(a);
+  else if (mf)
+    logreg_eval_kernel<16, EVAL_XLD_MF><<<grid, EVAL_ROWS, lds, s>>>(a);
+  else if (KP == 8 && narrow)
     logreg_eval_kernel<8, EVAL_XLD_NARROW><<<grid, EVAL_ROWS, lds, s>>>(a);
   else if (KP == 8)
     logreg_eval_kernel<8, EVAL_DCH + 1><<<grid, EVAL_ROWS, lds, s>>>(a);

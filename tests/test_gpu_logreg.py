@@ -62,6 +62,38 @@ def test_hybrid_eval_kernel_matches_fp64(cuda):
     assert float(solver.G.view(S * T, K, F + 1)[:, :, 3].abs().max()) == 0.0
 
 
+@pytest.mark.parametrize("Fd,K", [(43, 6), (70, 12), (16, 3)])
+def test_wide_dense_eval_mfma_matches_fp64(cuda, Fd, K):
+    """Dense designs wider than the narrow tile run the evaluation's two dense products on the matrix
+    cores (fp32 MFMA: margins W^T X^T, gradient R^T X; KP = 8 and 16; one and several 32-column LDS
+    chunks, a ragged last chunk): loss and gradient equal the fp64 oracle."""
+    from har.ops.logreg import DeviceLogregSolver, LogregDesign
+
+    X, y, hm = _hybrid_problem(cuda, N=1300, seed=Fd, blocks=((0, 12),), Fd=Fd, K=K)
+    N, F = X.shape
+    S, T = 2, 3
+    g = torch.Generator().manual_seed(7)
+    rw = (torch.rand(S, N, generator=g) > 0.2).float().to(cuda)
+    design = LogregDesign(hm, y.to(cuda), rw, K)
+    inv_std = (torch.rand(S, F, generator=g) + 0.5).to(cuda)
+    pmask = torch.ones(S, K, F + 1, device=cuda)
+    inv_wsum = 1.0 / rw.sum(1)
+    D = K * (F + 1)
+    solver = DeviceLogregSolver(design, S, T, 4, inv_std, pmask, inv_wsum, torch.zeros(S, D, device=cuda), None, 1,
+                                1e-6)
+    xt = torch.randn(S * T, K, F + 1, generator=g).to(cuda) * 0.2
+    spec = torch.arange(S * T, device=cuda) // T
+    W = xt[:, :, :F] * inv_std[spec][:, None, :] * pmask[spec][:, :, :F]
+    solver.weff.zero_()
+    solver.weff[:, :F, :K] = W.transpose(1, 2)
+    solver.weff[:, F, :K] = xt[:, :, F] * pmask[spec][:, :, F]
+    solver._evaluate(1)
+    ref_loss, ref_G = LogregDesign(hm, y.to(cuda), rw.double(), K).eval_torch(
+        xt.double(), T, inv_std.double(), pmask.double(), inv_wsum.double())
+    torch.testing.assert_close(solver.loss, ref_loss, rtol=2e-5, atol=1e-6)
+    torch.testing.assert_close(solver.G.double(), ref_G, rtol=2e-4, atol=2e-6)
+
+
 def test_margins_kernel_matches_dense(cuda):
     from har.ops.logreg import logreg_margins_native
 
@@ -226,3 +258,33 @@ def test_logreg_more_than_16_classes_on_gpu(cuda):
     cv = CrossValidator(estimator=LogisticRegression(maxIter=20, device=cuda), estimatorParamMaps=grid,
                         evaluator=MulticlassClassificationEvaluator(metricName="accuracy"), numFolds=3, seed=1).fit(t)
     assert len(cv.avgMetrics) == 2 and cv.bestModel.coefficientMatrix.shape == (K, F)
+
+
+def test_crossvalidator_batched_refit_matches_plain_fit_gpu(cuda):
+    """GPU twin of ``test_models_cpu.py::test_crossvalidator_batched_refit_matches_plain_fit``: the best
+    model of the batched device solve (its refit rides in the 54-model batch, ~9 chunks per model, a
+    materialized all-ones weight row) against a separate single device fit of the winning parameters:
+    the same objective within 1e-4 relative and > 99% identical predictions."""
+    from har.data.table import Column, Table
+    from har.evaluation.evaluators import MulticlassClassificationEvaluator
+    from har.models.logreg import LogisticRegression
+    from har.tuning.crossval import CrossValidator, ParamGridBuilder
+
+    g = torch.Generator().manual_seed(5)
+    K, F, N = 4, 10, 1200
+    mu = torch.randn(K, F, generator=g) * 1.5
+    y = torch.randint(0, K, (N,), generator=g)
+    x = mu[y] + torch.randn(N, F, generator=g)
+    t = Table([Column("features", "vector", x.numpy().astype(np.float32)),
+               Column("label", "double", y.numpy().astype(np.float64))])
+    lr = LogisticRegression(maxIter=30, device=cuda)
+    grid = ParamGridBuilder().addGrid("regParam", [0.05, 0.2]).addGrid("elasticNetParam", [0.0, 0.1]).build()
+    cv = CrossValidator(estimator=lr, estimatorParamMaps=grid,
+                        evaluator=MulticlassClassificationEvaluator(metricName="accuracy"), numFolds=3, seed=1)
+    m = cv.fit(t)
+    plain = lr.copy(grid[m.bestIndex]).fit(t)
+    fa, fb = m.bestModel.summary["objective"], plain.summary["objective"]
+    assert abs(fa - fb) / abs(fb) < 1e-4, (fa, fb)
+    xd = x.to(cuda)
+    agree = float((m.bestModel.predict(xd) == plain.predict(xd)).float().mean())
+    assert agree > 0.99, agree

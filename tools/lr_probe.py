@@ -18,6 +18,7 @@ def main():
     ap.add_argument("--model", default="lr")
     ap.add_argument("--fits", type=int, default=5)
     ap.add_argument("--cold", action="store_true")
+    ap.add_argument("--encoding", default="reference", help="reference (3100-dim one-hot) or numeric43 (dense)")
     a = ap.parse_args()
     import torch
 
@@ -26,7 +27,7 @@ def main():
 
     dev = torch.device("cuda")
     cfg = RunConfig(cv_metric="mae")
-    train, test, _ = load_wisdm(DEFAULT_WISDM, "reference", cfg.seed, device=dev)
+    train, test, _ = load_wisdm(DEFAULT_WISDM, a.encoding, cfg.seed, device=dev)
     nf, nc = n_feature_columns(train), len(train["label"].meta["vocab"])
 
     def fit(model=a.model):
