@@ -543,7 +543,15 @@ __device__ __forceinline__ uint32_t bin_of(float x, float sc, float lo) {
   return b < (uint32_t)(NB - 1) ? b : (uint32_t)(NB - 1);
 }
 
-template <int A, int LPW, bool MLP, int RCMAX>
+// P32: non-overlapping windows (stride == W) with 32-sample runs (C = 32, even): every window gets its
+// own LDS image with a 4-float pad after each 32 samples (sample t at t A + 4 (t >> 5)), so the lanes of a
+// group, 32 A + 4 floats apart, still read distinct banks (an unpadded 32 A stride would put 16 lanes on
+// 2 - 4 banks).  The pads keep every float4 of the copy 16-byte aligned (32 A is a multiple of 4).  It
+// lets a 500-sample 9-axis window run on 16-lane groups (16 x 32 >= 500) instead of 32 x 17.
+__host__ __device__ constexpr int p32_pos(int t, int A) { return t * A + 4 * (t >> 5); }
+__host__ __device__ inline int p32_pitch(int W, int A) { return (p32_pos(W, A) + 4 + 3) & ~3; }
+
+template <int A, int LPW, bool MLP, int RCMAX, bool P32 = false>
 __global__ __launch_bounds__(256) void window_features_reg_kernel(const float* __restrict__ stream, int W,
                                                                   int stride, int64_t n_windows, float ms_per_sample,
                                                                   float* __restrict__ out, int ld_out, MlpOut mo,
@@ -555,7 +563,23 @@ __global__ __launch_bounds__(256) void window_features_reg_kernel(const float* _
   const int64_t w0 = (int64_t)blockIdx.x * wpb;
   const int nwin = (int)min<int64_t>(wpb, n_windows - w0);
   float* const span = lds + PAD;
+  const int ip = P32 ? p32_pitch(W, A) : stride * A;  // image pitch (floats) between consecutive windows
+  auto pos = [&](int t) { return P32 ? p32_pos(t, A) : t * A; };
 
+  if constexpr (P32) {  // ---- stage the windows, one padded image each (float4 granules) ----
+    const v4f* s4 = reinterpret_cast<const v4f*>(stream + w0 * (int64_t)W * A);
+    const int n4w = W * A / 4, n4 = nwin * n4w;
+    for (int f0 = tid; f0 < n4; f0 += 8 * nt) {
+      v4f r[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) r[u] = s4[min(f0 + u * nt, n4 - 1)];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int f = min(f0 + u * nt, n4 - 1), wl = f / n4w, e = 4 * (f - wl * n4w);
+        *reinterpret_cast<v4f*>(span + wl * ip + e + 4 * (e / (32 * A))) = r[u];
+      }
+    }
+  } else {
   // ---- stage the span: samples [w0 * stride, (w0 + nwin - 1) * stride + W), A floats each ----
   {
     const float* src = stream + w0 * stride * A;
@@ -578,6 +602,7 @@ __global__ __launch_bounds__(256) void window_features_reg_kernel(const float* _
     }
     for (int e = done + tid; e < nspan; e += nt) span[e] = src[e];
   }
+  }
   __syncthreads();
 
   const int lane = tid & 63, wave = tid >> 6, sub = lane % LPW;
@@ -585,7 +610,7 @@ __global__ __launch_bounds__(256) void window_features_reg_kernel(const float* _
   const int wi = GPW * (wave / T3) + lane / LPW;
   const bool valid = wi < nwin;
   const int64_t win = w0 + (valid ? wi : 0);
-  const float* img = span + (valid ? wi : 0) * stride * A + 3 * g;  // the group's triad
+  const float* img = span + (valid ? wi : 0) * ip + 3 * g;  // the group's triad
   const mlpf::LaneSwap sw(lane);
   const int tb = sub * C;
   const float invW = 1.f / (float)W;
@@ -597,14 +622,16 @@ __global__ __launch_bounds__(256) void window_features_reg_kernel(const float* _
 #pragma unroll
   for (int k = 0; k < RCMAX; ++k)
     if (k < C) {
-      const float* p = img + min(tb + k, W - 1) * A;
+      const float* p = img + pos(min(tb + k, W - 1));
 #pragma unroll
       for (int c = 0; c < 3; ++c) x[c][k] = p[c];
     }
   float xl[3], pv0[3];
   {
-    const float* pl = img + (W - 1) * A;
-    const float* pp = img + (min(tb, W) - 1) * A;  // sample before the run (t = -1: the PAD / previous window)
+    const float* pl = img + pos(W - 1);
+    // sample before the run (t = -1: the PAD / previous window; P32: sample 0 — lane 0's t = 0 peak
+    // bit is masked either way)
+    const float* pp = img + (P32 ? pos(max(min(tb, W) - 1, 0)) : (min(tb, W) - 1) * A);
 #pragma unroll
     for (int c = 0; c < 3; ++c) { xl[c] = pl[c]; pv0[c] = pp[c]; }
   }
@@ -668,7 +695,8 @@ __global__ __launch_bounds__(256) void window_features_reg_kernel(const float* _
 
   // peak positions: 0 < t < W - 1 (t = tb + k), i.e. bits j in [C - 1 - kh, C - 1 - kl]
   const int kl = sub == 0 ? 1 : 0, kh = min(C - 1, W - 2 - tb);
-  const uint32_t pmask = kh >= kl ? ((1u << (C - kl)) - 1u) & ~((1u << (C - 1 - kh)) - 1u) : 0u;
+  const uint32_t pmask =
+      kh >= kl ? (uint32_t)(((1ull << (C - kl)) - 1ull) & ~((1ull << (C - 1 - kh)) - 1ull)) : 0u;  // (C <= 32)
 
   // ---- reduce + write ----
   float* o = MLP ? nullptr : out + win * (int64_t)ld_out;
@@ -831,9 +859,21 @@ int launch_axes(const float* stream, int64_t n_samples, int window, int stride, 
     for (int l = stride < window ? 8 : 16; l <= 64 && !lpw; l *= 2)
       for (int c = 5; c <= RCMAX_LONG; c += 2)
         if (l * c >= window) { lpw = l; C = c; break; }
+    // non-overlapping windows of (16 x 31, 16 x 32] samples: 16-lane groups of 32-sample runs on padded
+    // per-window images (P32) instead of 32-lane groups (fewer cross-lane reductions per window).  Opt-in
+    // (HAR_WINDOW_P32=1): measured 364 vs 328 us on the 9-axis 500-sample shape — four windows' images per
+    // 3-wave block (73 KB) halve the resident waves, which costs more than the saved reductions
+    static const bool p32_on = [] {
+      const char* e = std::getenv("HAR_WINDOW_P32");
+      return e && std::atoi(e) != 0;
+    }();
+    const bool p32 = p32_on && stride == window && (window * A) % 4 == 0 &&
+                     (reinterpret_cast<uintptr_t>(stream) & 15) == 0 && lpw > 16 && window <= 16 * 32;
+    if (p32) { lpw = 16; C = 32; }
     if (lpw) {
       const int gpw = 64 / lpw;
       auto span_bytes = [&](int wpb) -> int64_t {
+        if (p32) return (PAD + (int64_t)wpb * p32_pitch(window, A) + SLACK) * (int64_t)sizeof(float);
         return (PAD + ((int64_t)(wpb - 1) * stride + window) * A + SLACK) * (int64_t)sizeof(float);
       };
       // waves per block: a multiple of T3, at most 4; the most whose span fits 48 KB (>= 3 blocks per CU)
@@ -853,7 +893,10 @@ int launch_axes(const float* stream, int64_t n_samples, int window, int stride, 
   else                                                                                                     \
     window_features_reg_kernel<A, L, MLP, RCMAX_LONG><<<grid, nt, bytes, s>>>(stream, window, stride, n_windows, \
                                                                               ms, out, ld_out, mo, C, wpb)
-        if (lpw == 8) { HAR_WIN_R(8); }
+        if (p32)
+          window_features_reg_kernel<A, 16, MLP, 32, true><<<grid, nt, bytes, s>>>(stream, window, stride, n_windows,
+                                                                                   ms, out, ld_out, mo, C, wpb);
+        else if (lpw == 8) { HAR_WIN_R(8); }
         else if (lpw == 16) { HAR_WIN_R(16); }
         else if (lpw == 32) { HAR_WIN_R(32); }
         else { HAR_WIN_R(64); }
