@@ -207,6 +207,23 @@ class MLPEngine:
                 H = L.hidden[0]
                 self.Pf = torch.zeros(H * L.in_pad + 2 * H * H, dtype=torch.bfloat16, device=dev)
                 self._pack_frag()
+            # small batches (B <= 512, B % 32 == 0, one GPU): the whole forward + backward of each 32-row
+            # tile in one workgroup (mlp_small.hip) + the reduction / Adam kernel — two launches per step
+            self.small_ok = (self.fused_ok and L.hidden[0] in (128, 256) and self.world == 1
+                             and os.environ.get("HAR_MLP_SMALL", "1") != "0")
+            self.small_max = _native.kernels().mlp_small_step_max_batch() if self.small_ok else 0
+            if self.small_ok:
+                H = L.hidden[0]
+                if not getattr(self, "step_ok", False):  # (the step path allocated them already)
+                    self.Pf = torch.zeros(H * L.in_pad + 2 * H * H, dtype=torch.bfloat16, device=dev)
+                self.small_loss = torch.zeros(self.small_max // 32, dtype=torch.float32, device=dev)
+                self.small_correct = torch.zeros(self.small_max // 32, dtype=torch.int32, device=dev)
+                if self.slabs.shape[0] < self.small_max // 32:
+                    self.slabs = torch.zeros(self.small_max // 32, L.total, dtype=torch.float32, device=dev)
+                self._pack_frag()
+            # the W1^T fragment copy equals the current W1 (only the small path's Adam keeps it so; the
+            # step path's forward writes it from the pre-update W1, the other paths leave it)
+            self._pf_fresh = True
             self.last_bwd = False
             self.last_path = None
             # optional: the two backward branches after the fused forward — dW1 (split-K over the
@@ -231,10 +248,36 @@ class MLPEngine:
         return (self.Pf.data_ptr(), L.by_name["W0"].offset, L.by_name["W1"].offset, L.in_pad, L.hidden[0])
 
     def _pack_frag(self):
-        """Rebuild the fragment copies from Pb (after anything but the step's Adam wrote Pb)."""
-        if getattr(self, "step_ok", False):
-            dst, o0, o1, k0, h = self._frag_args()
-            _native.kernels().mlp_pack_frag(self.Pb.data_ptr(), dst, o0, o1, k0, h, _native.stream_ptr())
+        """Rebuild the fragment copies (W0 | W1 | W1^T) from Pb (after anything but the step's Adam wrote Pb)."""
+        if getattr(self, "Pf", None) is not None:
+            L = self.layout
+            _native.kernels().mlp_pack_frag(self.Pb.data_ptr(), self.Pf.data_ptr(), L.by_name["W0"].offset,
+                                            L.by_name["W1"].offset, L.in_pad, L.hidden[0], _native.stream_ptr())
+            self._pf_fresh = True
+
+    def _small_ok(self, Xb, yb) -> bool:
+        B = Xb.shape[0]
+        return (getattr(self, "small_ok", False) and 0 < B <= self.small_max and B % 32 == 0
+                and Xb.shape[1] == self.layout.in_pad and Xb.dtype == torch.bfloat16 and Xb.is_contiguous()
+                and yb.dtype == torch.int32)
+
+    def _small_step(self, Xb, yb, global_batch: int):
+        """mlp_small.hip: the fused tile kernel + the reduction / Adam of its B / 32 slabs (one host call)."""
+        L, B = self.layout, Xb.shape[0]
+        if not self._pf_fresh:  # a step of another path ran since: W1^T (and for H = 128 W0 / W1) re-packed
+            self._pack_frag()
+        b1, b2 = self.betas
+        o = {n: L.by_name[n].offset for n in ("W0", "b0", "W1", "b1", "Wout", "bout")}
+        _native.kernels().mlp_small_step(
+            Xb.data_ptr(), L.in_pad, self.Pf.data_ptr(), self._w(self.P, "b0").data_ptr(),
+            self._w(self.P, "b1").data_ptr(), L.hidden[0], self._w(self.Pb, "Wout").data_ptr(),
+            self._w(self.P, "bout").data_ptr(), yb.data_ptr(), B, L.num_classes, 1.0 / global_batch,
+            self.slabs.data_ptr(), L.total, o["W0"], o["b0"], o["W1"], o["b1"], o["Wout"], o["bout"],
+            self.small_loss.data_ptr(), self.small_correct.data_ptr(), self.step_count.data_ptr(), self.G.data_ptr(),
+            self.P.data_ptr(), self.m.data_ptr(), self.v.data_ptr(), self.Pb.data_ptr(), float(self.lr), b1, b2,
+            float(self.eps), float(self.wd), self.step_count.data_ptr(), _native.stream_ptr())
+        self.last_path, self.last_fused, self.last_bwd, self.last_batch = "small", False, True, B
+        self._pf_fresh = True
 
     def refresh_bf16(self):
         """Pb (+ fragment copies) from the fp32 master P."""
@@ -533,6 +576,10 @@ class MLPEngine:
         update is fused into that kernel, at N > 1 it stores G, one RCCL all-reduce of G follows and
         Adam runs from G — the same kernels and the same summation order at every N.  The
         three-kernel step goes through the native plan (one host call per phase)."""
+        if self.native and self.world == 1 and self._small_ok(Xb, yb):
+            return self._small_step(Xb, yb, global_batch)
+        if self.native:
+            self._pf_fresh = False  # (every other native path leaves the W1^T copy behind W1)
         if self.native and self._plan_ok(Xb, yb):
             B = Xb.shape[0]
             plan, self.step_nwg, self.step_S = self._plan(B)
@@ -576,6 +623,9 @@ class MLPEngine:
         if self.last_path == "step":
             n = self.step_nwg
             return float(self.sblock_loss[:n].sum().item()), int(self.sblock_correct[:n].sum().item())
+        if self.last_path == "small":
+            n = self.last_batch // 32
+            return float(self.small_loss[:n].sum().item()), int(self.small_correct[:n].sum().item())
         if self.last_fused:
             n = self.fused_nwg
             return float(self.fblock_loss[:n].sum().item()), int(self.fblock_correct[:n].sum().item())

@@ -602,6 +602,28 @@ PYBIND11_MODULE(_har_native, m) {
      py::arg("param"), py::arg("m"), py::arg("v"), py::arg("pb"), py::arg("lr"), py::arg("b1"), py::arg("b2"),
      py::arg("eps"), py::arg("wd"), py::arg("step"), py::arg("tick"), py::arg("mode"), py::arg("stream"),
      py::arg("frag_dst") = 0, py::arg("w0_off") = 0, py::arg("w1_off") = 0, py::arg("fK0") = 0, py::arg("fH") = 0);
+  // small-batch step: the fused tile kernel, then ONE region reduction of its B / 32 slabs + Adam that
+  // refreshes Pb and all three fragment copies (mlp_small.hip)
+  m.def("mlp_small_step_max_batch", &har_mlp_small_step_max_batch);
+  m.def("mlp_small_step", [](u X, int K0, u Wf, u b0, u b1, int H, u Wo, u bo, u labels, int B, int C, float scale,
+                             u slab, int64_t total, int64_t off_w0, int64_t off_b0, int64_t off_w1, int64_t off_b1,
+                             int64_t off_wo, int64_t off_bo, u block_loss, u block_correct, u tick, u G, u param,
+                             u mm, u vv, u pb, float lr, float b1c, float b2c, float eps, float wd, u step,
+                             u stream) {
+    const MlpSmallStepArgs a{P<const uint16_t>(X), P<const uint16_t>(Wf), P<const float>(b0), P<const float>(b1),
+                             P<const uint16_t>(Wo), P<const float>(bo), P<const int32_t>(labels), B, C, scale,
+                             P<float>(slab), total, off_w0, off_b0, off_w1, off_b1, off_wo, off_bo,
+                             P<float>(block_loss), P<int32_t>(block_correct), P<int32_t>(tick)};
+    check(har_mlp_small_step(&a, K0, H, S(stream)), "mlp_small_step");
+    const float* src = P<const float>(slab);
+    const int64_t start = 0;
+    const int nsl = B / 32;
+    const MlpFragSpec frag{P<uint16_t>(Wf), off_w0, off_w1, K0, H, 1};
+    check(har_grad_reduce_adam(1, &src, &start, &total, &total, &nsl, total, P<float>(G), P<float>(param),
+                               P<float>(mm), P<float>(vv), P<uint16_t>(pb), lr, b1c, b2c, eps, wd, P<int32_t>(step),
+                               0, 1 | 4, &frag, S(stream)),
+          "mlp_small_step reduce+adam");
+  });
   m.def("mlp_pack_frag", [](u pb, u dst, int64_t w0_off, int64_t w1_off, int K0, int H, u stream) {
     const MlpFragSpec f{P<uint16_t>(dst), w0_off, w1_off, K0, H};
     check(har_mlp_pack_frag(P<const uint16_t>(pb), &f, S(stream)), "mlp_pack_frag");

@@ -52,7 +52,30 @@ typedef struct MlpFragSpec {
   uint16_t* dst;
   int64_t w0_off, w1_off;  // flat offsets of W0 [H][K0] and W1 [H][H]
   int K0, H;
+  int w1t;                 // the Adam update also writes the W1^T copy (paths with no step forward)
 } MlpFragSpec;
+// Small-batch step (mlp_small.hip): the whole forward + backward of a 32-row tile per workgroup (B / 32
+// of them, B <= har_mlp_small_step_max_batch()), each writing its partial gradient to slab blockIdx.x in
+// the flat parameter layout (segment offsets off_*), loss / #correct per workgroup; `tick` (optional)
+// advances Adam's step counter.  Wf: the MlpFragSpec fragment copies (W0 | W1 | W1^T, all read).
+typedef struct MlpSmallStepArgs {
+  const uint16_t* X;        // [B][K0] bf16 (padded inputs)
+  const uint16_t* Wf;       // fragment copies
+  const float* b0;
+  const float* b1;
+  const uint16_t* Wo;       // [16][H] bf16
+  const float* bo;          // [16]
+  const int32_t* labels;    // [B]
+  int B, C;
+  float scale;              // 1 / global batch
+  float* slab;              // [B / 32][total]
+  int64_t total, off_w0, off_b0, off_w1, off_b1, off_wo, off_bo;
+  float* block_loss;        // [B / 32]
+  int32_t* block_correct;   // [B / 32]
+  int32_t* tick;
+} MlpSmallStepArgs;
+int har_mlp_small_step(const MlpSmallStepArgs* args, int K0, int H, hipStream_t s);
+int har_mlp_small_step_max_batch();
 int har_grad_reduce_adam(int nreg, const float* const* src, const int64_t* start, const int64_t* len,
                          const int64_t* lds, const int* S, int64_t n, float* G, float* param, float* m, float* v,
                          uint16_t* pb, float lr, float b1, float b2, float eps, float wd, int32_t* step, int tick,

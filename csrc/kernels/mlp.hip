@@ -321,7 +321,10 @@ __global__ __launch_bounds__(64 * GR_W) void grad_reduce_adam_kernel(GradRegions
       reinterpret_cast<float4*>(m)[i4] = mm;
       reinterpret_cast<float4*>(v)[i4] = vv;
       reinterpret_cast<ushort4*>(pb)[i4] = ob;
-      if (frag.dst) frag_store4<false>(frag, e, ob);
+      if (frag.dst) {
+        if (frag.w1t) frag_store4<true>(frag, e, ob);
+        else frag_store4<false>(frag, e, ob);
+      }
     }
   }
 }

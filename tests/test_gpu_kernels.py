@@ -511,6 +511,38 @@ def test_mlp_fragment_copies_track_pb(cuda, F):
             assert not torch.equal(W1, W1_used), "the update did not move W1"
 
 
+@pytest.mark.parametrize("H,F,B", [(256, 43, 256), (128, 43, 256), (256, 20, 512), (128, 20, 64)])
+def test_mlp_small_step_matches_other_paths(cuda, monkeypatch, H, F, B):
+    """The small-batch step (mlp_small.hip: one workgroup per 32-row tile + the reduction / Adam kernel)
+    against the engine's other native path on the same batches (the three-kernel step for H = 256, the
+    fused forward + GEMM backward for H = 128): parameters after three Adam steps, loss and #correct;
+    the fragment copies (W0, W1 and the W1^T copy the small path's Adam keeps current) equal Pb; two
+    small-path engines are bit-identical."""
+    from har.models.mlp import MLPEngine, pad_input_bf16
+
+    g = torch.Generator(device=cuda).manual_seed(17)
+    X = torch.randn(B, F, device=cuda, generator=g)
+    y = torch.randint(0, 6, (B,), device=cuda, generator=g).to(torch.int32)
+    engines = []
+    for flag in ("1", "1", "0"):
+        monkeypatch.setenv("HAR_MLP_SMALL", flag)
+        e = MLPEngine([F, H, H, 6], B, cuda, lr=1e-3, seed=5)
+        Xb = pad_input_bf16(X, e.layout.in_pad)
+        for _ in range(3):
+            e.train_step(Xb, y, B)
+        torch.cuda.synchronize()
+        assert (e.last_path == "small") == (flag == "1")
+        engines.append((e, e.last_loss_and_correct()))
+    (a, lca), (a2, lca2), (b, lcb) = engines
+    assert torch.equal(a.P, a2.P) and lca == lca2
+    torch.testing.assert_close(a.P, b.P, rtol=0, atol=5e-4)
+    assert abs(lca[0] - lcb[0]) / lcb[0] < 2e-3 and abs(lca[1] - lcb[1]) <= 2
+    L = a.layout
+    W0, W1 = L.view(a.Pb, "W0"), L.view(a.Pb, "W1")
+    want = torch.cat([_frag_reference(W0), _frag_reference(W1), _frag_reference(W1.T.contiguous())])
+    assert torch.equal(a.Pf, want), "small-path fragment copies differ from Pb"
+
+
 @pytest.mark.parametrize("metric", ["accuracy", "f1", "weightedPrecision", "areaUnderROC", "areaUnderPR", "mae"])
 def test_batched_cv_metrics_gpu_match_cpu(cuda, metric):
     """CrossValidator scoring of B models at once: the batched confusion-matrix kernel and the
