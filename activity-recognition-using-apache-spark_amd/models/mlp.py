@@ -796,6 +796,29 @@ class MultilayerPerceptronClassifier(Estimator, ClassifierParams):
         return self.fit_tensors(X[lo:hi], y[lo:hi], process_group=ctx.group, rank=ctx.rank,
                                 world_size=ctx.world_size, num_classes=K)
 
+    def _prep(self, table: Table):
+        dev = resolve_device(self.device)
+        return (features_tensor(table, self.featuresCol, dev), labels_tensor(table, self.labelCol, dev),
+                num_label_classes(table, self.labelCol, dev))
+
+    def fit_folds(self, X: torch.Tensor, y: torch.Tensor, K: int, masks: torch.Tensor):
+        """CrossValidator's folds: fold f trains on the rows with ``masks[f] != 0``, gathered on the
+        device from the resident matrix (no host row subset, no re-upload); the rows and their order
+        are those of ``fit(table.take_rows(...))``, so the model is the same (minibatches included)."""
+        ctx = dp_context()
+        out = []
+        for f in range(masks.shape[0]):
+            idx = torch.nonzero(masks[f]).squeeze(1)
+            Xf, yf = X.index_select(0, idx), y.index_select(0, idx)
+            if ctx is None:
+                m = self.fit_tensors(Xf, yf, num_classes=K)
+            else:
+                lo, hi = dp_rows(Xf.shape[0])
+                m = self.fit_tensors(Xf[lo:hi], yf[lo:hi], process_group=ctx.group, rank=ctx.rank,
+                                     world_size=ctx.world_size, num_classes=K)
+            out.append(m)
+        return out
+
     def fit_tensors(self, X: torch.Tensor, y: torch.Tensor, process_group=None, rank: int = 0,
                     world_size: int = 1, num_classes: Optional[int] = None) -> MultilayerPerceptronClassificationModel:
         """DP-ready fit: every rank passes its own shard (X, y); the standardization

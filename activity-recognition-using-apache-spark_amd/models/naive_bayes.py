@@ -130,6 +130,24 @@ class NaiveBayes(Estimator, ClassifierParams):
         m.uid = self.uid
         return m
 
+    def _prep(self, table: Table):
+        dev = resolve_device(self.device)
+        return (features_tensor(table, self.featuresCol, dev), labels_tensor(table, self.labelCol, dev),
+                num_label_classes(table, self.labelCol, dev))
+
+    def fit_folds(self, X, y, K, masks: torch.Tensor):
+        """One model per CrossValidator fold (``masks`` [k, N]: 1 = training row of fold f) from the
+        full device matrices with the fold mask as row weights — no per-fold row gather; the
+        CrossValidator then scores every fold's validation rows in one batched pass (data parallel:
+        each rank's row shard, moments all-reduced)."""
+        lo, hi = dp_rows(X.shape[0])
+        out = []
+        for f in range(masks.shape[0]):
+            m = self.fit_tensors(X[lo:hi], y[lo:hi], K, masks[f, lo:hi], allreduce=dp_allreduce())
+            m.uid = self.uid
+            out.append(m)
+        return out
+
     def fit_tensors(self, X, y, K, w=None, allreduce=None) -> NaiveBayesModel:
         """``allreduce`` (in-place SUM over ranks): X/y/w are this rank's shard and the
         class counts / first / second moments are summed in ONE flat bucket."""

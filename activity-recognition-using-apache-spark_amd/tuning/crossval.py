@@ -167,7 +167,8 @@ class CrossValidator(Estimator):
             vals = ev.evaluate_batched(y, pred, mask, K, raw)
             for (mi, f), v in zip(index, vals):
                 metrics[mi, f] = v
-        elif hasattr(est, "fit_folds"):  # trees: every fold's tree(s) in one lock-step build
+        elif hasattr(est, "fit_folds") and not getattr(est, "weightCol", None):
+            # trees: every fold's tree(s) in one lock-step build; NaiveBayes: fold masks as row weights
             dev = resolve_device(est.device)
             X, y, K = est._prep(table)
             fold_t = torch.as_tensor(fold, device=dev)

@@ -409,3 +409,53 @@ def test_logreg_many_classes_cpu():
     m = LogisticRegression(maxIter=60, regParam=0.001).fit_many(x, y, [FitSpec(None, 0.001, 0.0)], 18)[0]
     assert m.coefficientMatrix.shape == (18, 12)
     assert float((m.predict(x) == y).float().mean()) > 0.8
+
+
+@pytest.mark.parametrize("model_type", ["multinomial", "gaussian"])
+def test_naive_bayes_crossvalidator_fold_masks_match_row_subsets(model_type):
+    """CrossValidator over NaiveBayes fits every fold from the full matrix with the fold mask as row
+    weights (``NaiveBayes.fit_folds``) and scores the folds in one batched pass; the metrics equal the
+    per-fold row-subset fits (``take_rows``) of the generic loop."""
+    from har.data.split import kfold_ids
+    from har.data.table import Column, Table
+    from har.tuning.crossval import CrossValidator, ParamGridBuilder
+
+    x, y = _blobs(900, 8, 3, seed=4)
+    x = x.abs() if model_type == "multinomial" else x
+    t = Table([Column("features", "vector", x.numpy().astype(np.float32)),
+               Column("label", "double", y.numpy().astype(np.float64))])
+    nb = NaiveBayes(modelType=model_type)
+    grid = ParamGridBuilder().addGrid("smoothing", [0.5, 1.0]).build()
+    ev = MulticlassClassificationEvaluator(metricName="accuracy")
+    cv = CrossValidator(estimator=nb, estimatorParamMaps=grid, evaluator=ev, numFolds=3, seed=2).fit(t)
+    fold = kfold_ids(t.count(), 3, 2)
+    want = []
+    for pm in grid:
+        vals = []
+        for f in range(3):
+            tr, va = t.take_rows(np.nonzero(fold != f)[0]), t.take_rows(np.nonzero(fold == f)[0])
+            vals.append(ev.evaluate(nb.copy(pm).fit(tr).transform(va)))
+        want.append(float(np.mean(vals)))
+    np.testing.assert_allclose(cv.avgMetrics, want, rtol=0, atol=1e-9)
+
+
+def test_mlp_crossvalidator_device_fold_rows_match_row_subsets():
+    """CrossValidator over the MLP gathers each fold's training rows on the device
+    (``fit_folds``) instead of building host row subsets; same rows, same order, same model."""
+    from har.data.split import kfold_ids
+    from har.data.table import Column, Table
+
+    x, y = _blobs(600, 8, 3, seed=5)
+    t = Table([Column("features", "vector", x.numpy().astype(np.float32)),
+               Column("label", "double", y.numpy().astype(np.float64))])
+    mlp = MultilayerPerceptronClassifier(layers=[8, 32, 3], maxIter=3, blockSize=64, stepSize=1e-2, device="cpu")
+    grid = ParamGridBuilder().addGrid("stepSize", [1e-2, 3e-2]).build()
+    ev = MulticlassClassificationEvaluator(metricName="f1")
+    cv = CrossValidator(estimator=mlp, estimatorParamMaps=grid, evaluator=ev, numFolds=3, seed=1).fit(t)
+    fold = kfold_ids(t.count(), 3, 1)
+    want = []
+    for pm in grid:
+        vals = [ev.evaluate(mlp.copy(pm).fit(t.take_rows(np.nonzero(fold != f)[0]))
+                            .transform(t.take_rows(np.nonzero(fold == f)[0]))) for f in range(3)]
+        want.append(float(np.mean(vals)))
+    np.testing.assert_allclose(cv.avgMetrics, want, rtol=0, atol=1e-6)
