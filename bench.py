@@ -89,6 +89,30 @@ def timed(ctx, run, steps, warmup, dev):
     return hdist.max_over_ranks(ctx, time.perf_counter() - t0)
 
 
+def settle_clocks(ctx, run, ms, dev):
+    """Untimed training steps for ``ms`` of wall time before the warm-up steps (the same step the
+    timed loop runs, so the model just trains longer): the timed window then starts at the clocks a
+    running job holds instead of inside the power-state ramp of a GPU that was idle a moment ago
+    (profiles/r4/bench_settle_ab.md: the driver's 20-step window read 0.0747-0.0758 ms per step
+    without, 0.0674-0.0681 ms with >= 100 ms, the 500-step run 0.0689).  Ranks stop together (the
+    elapsed time is agreed over the group after every 16 steps), so the DP steps' collectives pair
+    up.  Returns the settle time spent (ms)."""
+    from har.parallel import dist as hdist
+
+    if ms <= 0 or dev.type != "cuda":
+        return 0.0
+    t0 = time.perf_counter()
+    i = 0
+    while True:
+        for _ in range(16):
+            run(i)
+            i += 1
+        torch.cuda.synchronize(dev)
+        el = hdist.max_over_ranks(ctx, (time.perf_counter() - t0) * 1e3)
+        if el >= ms:
+            return el
+
+
 def capture_steps(step, nslots, enable):
     """HIP-graph capture of one training step per batch slot (launch-bound inner loop)."""
     if not enable:
@@ -156,6 +180,7 @@ def bench_mlp(args, ctx):
     # the untimed WISDM accuracy run (a separate engine) goes first: the timed steps then start on a
     # GPU already out of its idle power state instead of ramping its clock inside a 20-step window
     extras = wisdm_accuracy_fields(args, ctx, hidden=(args.hidden, args.hidden))
+    settle_ms = settle_clocks(ctx, run, args.settle_ms, dev)
     elapsed = timed(ctx, run, args.steps, args.warmup, dev)
     # accuracy of the model the timed steps trained, before the phase probe's extra steps move it
     Xt, yt = synthetic_windows(65536, seed=999, device=dev)
@@ -171,7 +196,7 @@ def bench_mlp(args, ctx):
            "synthetic_test_accuracy": hdist.mean_over_ranks(ctx, acc),
            "hip_graph": {0: "off", 1: "whole-step", 2: "segmented"}[mode if graphs else 0],
            "collectives_per_step": eng.collective_stats() if hasattr(eng, "collective_stats") else None,
-           "phase_ms": phases}
+           "phase_ms": phases, "settle_ms": settle_ms}
     rec.update(extras)
     return rec
 
@@ -564,6 +589,8 @@ def main():
                     help="--config stream: time full passes over every resident sample (halo-sharded featurization "
                          "+ one MLP epoch) instead of per-batch steps")
     ap.add_argument("--out", type=str, default="")
+    ap.add_argument("--settle-ms", type=float, default=float(os.environ.get("HAR_BENCH_SETTLE_MS", "200")),
+                    help="MLP configs: untimed training steps for this long before the warm-up (clock settle)")
     args = ap.parse_args()
 
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
