@@ -234,6 +234,10 @@ def _arena(specs, dev, into: dict) -> torch.Tensor:
     return buf
 
 
+# how the last native solve ran: 1 = one persistent cooperative launch, 0 = the launch sequence (tests)
+LAST_SOLVE_MODE = -1
+
+
 class DeviceLogregSolver:
     """Runs ``optim.lbfgs.minimize_trials``' algorithm for the LR objective entirely with the
     logreg_qn.hip kernels: 4 launches per iteration (direction + trials, evaluate, gradient,
@@ -369,7 +373,10 @@ class DeviceLogregSolver:
             if plan is None:
                 chunks = lambda ts: [mod.logreg_eval_chunk(ev, gr) for ev, gr in self._eval_args(ts)]  # noqa: E731
                 plan = self._solve_plan = mod.logreg_solve_plan(qa, chunks(self.T), chunks(1), KP)
-            mod.logreg_solve(plan, self.max_iter, self.m, s)
+            # the launch sequence, or (HAR_LR_PERSISTENT=1) one cooperative launch for the whole solve
+            # (logreg_solve_persistent_kernel, bitwise the same; measured slower); 1 = persistent ran
+            global LAST_SOLVE_MODE
+            self.solve_mode = LAST_SOLVE_MODE = mod.logreg_solve(plan, self.max_iter, self.m, s)
             self.n_evals += 1 + self.max_iter
             return self.x, self.fobj, self.iters
         phase(1, init=1)

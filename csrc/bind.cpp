@@ -10,7 +10,9 @@
 
 #include <hip/hip_runtime_api.h>
 
+#include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -171,9 +173,46 @@ struct LogregSolvePlan {
   QnArgs q;
   std::vector<LogregEvalChunk> evT, ev1;  // evaluations of the T trials (first) / 1 per model
   int KP = 8;
+  // the persistent solve's barrier counter + timeout flag (2 device words, allocated on first use)
+  std::shared_ptr<uint32_t> sync;
+  int last_mode = 0;  // 1 = the last solve ran persistent, 0 = as the launch sequence
 };
 
-static void logreg_solve_run(const LogregSolvePlan& p, int max_iter, int m, hipStream_t s) {
+// HAR_LR_PERSISTENT: 0 (default) = the launch sequence, 1 = one cooperative launch when every phase's
+// workgroups are co-resident in one round, 2 = one cooperative launch whenever possible.  Measured
+// (profiles/r4/lr_persistent.md): the persistent solve is bitwise the sequence but SLOWER on MI355X —
+// 1.46 ms vs 1.36 ms of solve kernels for the WISDM fit — back-to-back dependent launches cost less
+// than a grid barrier (release fence + counter + acquire fence), so the phases' own latency chains,
+// not kernel boundaries, bound an iteration
+static int g_lr_persistent = [] {
+  const char* e = std::getenv("HAR_LR_PERSISTENT");
+  return e ? std::atoi(e) : 0;
+}();
+static int lr_persistent_mode() { return g_lr_persistent; }
+
+static bool logreg_solve_persistent(LogregSolvePlan& p, int max_iter, hipStream_t s) {
+  const int mode = lr_persistent_mode();
+  if (mode == 0 || p.evT.size() != 1 || p.ev1.size() != 1) return false;
+  if (!p.sync) {
+    void* d = nullptr;
+    if (hipMalloc(&d, 2 * sizeof(uint32_t)) != hipSuccess) return false;
+    p.sync = std::shared_ptr<uint32_t>(static_cast<uint32_t*>(d), [](uint32_t* q) { (void)hipFree(q); });
+  }
+  const LogregEvalChunk &cT = p.evT[0], &c1 = p.ev1[0];
+  // mode 1: only when the widest phase fits one co-resident round (max_grid = 0: the launcher caps
+  // the grid at the co-resident count; a wider phase then loops, which the batched CV fits lose on)
+  const int rc = har_logreg_solve_persistent(&p.q, &cT.ev, &cT.gr, cT.n_models, &c1.ev, &c1.gr, c1.n_models, p.KP,
+                                             max_iter, p.sync.get(), mode == 1 ? -1 : 0, s);
+  if (rc == -2) throw std::runtime_error("logreg_solve_persistent: invalid arguments");
+  return rc == 0;
+}
+
+static void logreg_solve_run(LogregSolvePlan& p, int max_iter, int m, hipStream_t s) {
+  if (logreg_solve_persistent(p, max_iter, s)) {
+    p.last_mode = 1;
+    return;
+  }
+  p.last_mode = 0;
   auto phase = [&](int ph, int head, int filled, int init, int fin_it) {
     QnArgs a = p.q;
     a.head = head;
@@ -363,8 +402,21 @@ PYBIND11_MODULE(_har_native, m) {
     p.KP = KP;
     return p;
   });
-  m.def("logreg_solve", [](const LogregSolvePlan& p, int max_iter, int m, u stream) {
+  m.def("logreg_solve", [](LogregSolvePlan& p, int max_iter, int m, u stream) {
     logreg_solve_run(p, max_iter, m, S(stream));
+    return p.last_mode;
+  });
+  m.def("logreg_set_persistent", [](int mode) {
+    const int old = g_lr_persistent;
+    g_lr_persistent = mode;
+    return old;
+  });
+  // the persistent solve's timeout flag (blocking 4-byte read; tests / diagnostics)
+  m.def("logreg_solve_flag", [](const LogregSolvePlan& p) {
+    uint32_t f = 0;
+    if (p.sync) check(hipMemcpy(&f, p.sync.get() + 1, sizeof f, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1,
+                      "logreg_solve_flag");
+    return (int)f;
   });
   m.def("logreg_grad", [](u slab, u R, u col_map, u csc_rows, u csc_off, u col_slice, int SL, u inv_std, u pmask,
                           int64_t N, int F, int Fd, int K, int T, int tstride, int model0, int ntiles, u G, u loss,

@@ -316,6 +316,11 @@ int har_logreg_col_slices(const int32_t* csc_off, int F, int SL, int32_t* col_sl
 int har_logreg_loss_decode(const float* fx, double* loss, int n, hipStream_t s);
 int har_qn_chunks(int64_t D, int B);
 int har_lbfgs_phase(const QnArgs* a, int KP, int phase, hipStream_t s);
+// the whole L-BFGS / OWL-QN solve as one cooperative launch: 0 ran, -4 not available here (use
+// the launch sequence), -2 invalid; sync = 2 device words (barrier counter, timeout flag)
+int har_logreg_solve_persistent(const QnArgs* q, const LogregEvalArgs* evT, const LogregGradArgs* grT, int nT,
+                                const LogregEvalArgs* ev1, const LogregGradArgs* gr1, int n1, int KP, int max_iter,
+                                uint32_t* sync, int max_grid, hipStream_t s);
 
 
 

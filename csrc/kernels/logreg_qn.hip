@@ -79,9 +79,10 @@ __device__ __forceinline__ f32x4_t mfma4(float a, float b, f32x4_t c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
+// The kernel bodies below take their workgroup coordinates as arguments: the stand-alone kernels pass
+// blockIdx / gridDim, the persistent solve (logreg_solve_persistent_kernel) its virtual blocks.
 template <int KP, int XLD>
-__global__ __launch_bounds__(EVAL_ROWS) void logreg_eval_kernel(LogregEvalArgs a) {
-  extern __shared__ float smem[];
+__device__ __forceinline__ void logreg_eval_body(const LogregEvalArgs& a, int bx, int by, int gdx, float* smem) {
   const int Fd = a.Fd;
   float* wd = smem;                                // [EVAL_DCH][KP] dense weights of the chunk
   constexpr int xld = XLD;
@@ -94,9 +95,9 @@ __global__ __launch_bounds__(EVAL_ROWS) void logreg_eval_kernel(LogregEvalArgs a
   const int l16 = lane & 15, kq = lane >> 4;
 
   const int tid = threadIdx.x;
-  const int bt = a.model0 + blockIdx.y * a.tstride;  // trial model (its residual rows: R slot blockIdx.y)
+  const int bt = a.model0 + by * a.tstride;  // trial model (its residual rows: R slot by)
   const int s = bt / a.T;                          // spec (row-weight vector) of the model
-  const int64_t r0 = (int64_t)blockIdx.x * EVAL_ROWS;
+  const int64_t r0 = (int64_t)bx * EVAL_ROWS;
   const int64_t row = r0 + tid;
   const bool ok = row < a.N;
   const float* W = a.W + (int64_t)bt * (a.F + 1) * KP;
@@ -188,7 +189,7 @@ __global__ __launch_bounds__(EVAL_ROWS) void logreg_eval_kernel(LogregEvalArgs a
 #pragma unroll
   for (int k = 0; k < KP; ++k) rs[tid * KP + k] = rv[k];
   if (a.R != nullptr && ok) {
-    f32x4_t* rp = reinterpret_cast<f32x4_t*>(a.R + ((int64_t)blockIdx.y * a.N + row) * KP);
+    f32x4_t* rp = reinterpret_cast<f32x4_t*>(a.R + ((int64_t)by * a.N + row) * KP);
 #pragma unroll
     for (int q = 0; q < KP / 4; ++q) rp[q] = f32x4_t{rv[4 * q], rv[4 * q + 1], rv[4 * q + 2], rv[4 * q + 3]};
   }
@@ -198,7 +199,7 @@ __global__ __launch_bounds__(EVAL_ROWS) void logreg_eval_kernel(LogregEvalArgs a
   if ((tid & 63) == 0) red[tid >> 6] = lossv;
   __syncthreads();                                 // rs / red complete; the last chunk is in xs
   const int SW = Fd * KP + KP + 1;
-  float* slab = a.slab + ((int64_t)bt * gridDim.x + blockIdx.x) * SW;
+  float* slab = a.slab + ((int64_t)bt * gdx + bx) * SW;
   // ---- pass B: dense gradient R^T X of the tile, chunks newest-first (fixed row order) ----
   for (int ch = nchunk - 1; ch >= 0; --ch) {
     const int c0 = ch * EVAL_DCH, nc = min(EVAL_DCH, Fd - c0);
@@ -243,6 +244,12 @@ __global__ __launch_bounds__(EVAL_ROWS) void logreg_eval_kernel(LogregEvalArgs a
   if (tid == 0) slab[SW - 1] = (red[0] + red[1]) + (red[2] + red[3]);
 }
 
+template <int KP, int XLD>
+__global__ __launch_bounds__(EVAL_ROWS) void logreg_eval_kernel(LogregEvalArgs a) {
+  extern __shared__ float smem[];
+  logreg_eval_body<KP, XLD>(a, blockIdx.x, blockIdx.y, gridDim.x, smem);
+}
+
 // ---------------------------------------------------------------------------------------------
 // logreg_grad: G[bt][k][col], loss[bt].  Workgroup w owns the columns [256 w, 256 w + 256) and the
 // row SLICES of its one-hot columns: a column's CSC row list is cut into slices of a.SL rows
@@ -285,22 +292,22 @@ __device__ __forceinline__ double loss_decode(const float* in) {
 }
 
 template <int KP>
-__global__ __launch_bounds__(256) void logreg_grad_kernel(LogregGradArgs a) {
+__device__ __forceinline__ void logreg_grad_body(const LogregGradArgs& a, int bx, int by) {
   __shared__ float part[256 * KP];
   __shared__ int cs_l[257];                        // col_slice[c0 .. c1] of the block
   __shared__ float tl[256];                        // tile losses (block 0)
-  const int bt = a.model0 + blockIdx.y * a.tstride;
+  const int bt = a.model0 + by * a.tstride;
   const int s = bt / a.T;
   const int Fp1 = a.F + 1;
   const int SW = a.Fd * KP + KP + 1;
   const float* slab = a.slab + (int64_t)bt * a.ntiles * SW;
-  const int c0 = blockIdx.x * 256, c1 = min(Fp1, c0 + 256);
+  const int c0 = bx * 256, c1 = min(Fp1, c0 + 256);
   const int col = c0 + threadIdx.x;
   // one round of independent loads instead of dependent chains: the block's slice index (the
   // slice -> column search below runs in LDS) and, in block 0, the tile losses
   if (c0 + (int)threadIdx.x <= c1) cs_l[threadIdx.x] = a.col_slice[c0 + threadIdx.x];
   if (threadIdx.x == 0 && c1 - c0 == 256) cs_l[256] = a.col_slice[c1];
-  const bool loss_block = blockIdx.x == 0;
+  const bool loss_block = bx == 0;
   if (loss_block && (int)threadIdx.x < a.ntiles) tl[threadIdx.x] = slab[(int64_t)threadIdx.x * SW + SW - 1];
   __syncthreads();
   if (loss_block && threadIdx.x == 0) {
@@ -314,7 +321,7 @@ __global__ __launch_bounds__(256) void logreg_grad_kernel(LogregGradArgs a) {
   }
   const int s0 = cs_l[0], s1 = cs_l[c1 - c0];
   const int cs0 = col < c1 ? cs_l[threadIdx.x] : 0, cs1 = col < c1 ? cs_l[threadIdx.x + 1] : 0;
-  const float* R = a.R + (int64_t)blockIdx.y * a.N * KP;  // this launch's residual slot of the model
+  const float* R = a.R + (int64_t)by * a.N * KP;  // this launch's residual slot of the model
   float g[KP];
 #pragma unroll
   for (int k = 0; k < KP; ++k) g[k] = 0.f;
@@ -371,6 +378,11 @@ __global__ __launch_bounds__(256) void logreg_grad_kernel(LogregGradArgs a) {
   float* G = a.G + (int64_t)bt * D;
   const float* pm = a.pmask + (int64_t)s * D;
   for (int k = 0; k < a.K; ++k) G[(int64_t)k * Fp1 + col] = g[k] * sc * pm[(int64_t)k * Fp1 + col];
+}
+
+template <int KP>
+__global__ __launch_bounds__(256) void logreg_grad_kernel(LogregGradArgs a) {
+  logreg_grad_body<KP>(a, blockIdx.x, blockIdx.y);
 }
 
 // after the data-parallel all-reduce of the bucket: the summed fixed-point losses -> fp64
@@ -619,11 +631,10 @@ __device__ __forceinline__ DirElem dir_load(const QnArgs& a, int b, int e) {
 
 // phase 1
 template <int KP, bool FULLM>
-__global__ __launch_bounds__(QN_BLOCK) void qn_direction_kernel(QnArgs a) {
+__device__ __forceinline__ void qn_direction_body(const QnArgs& a, int c, int b) {
   __shared__ double sh[4 * NP2];
   __shared__ float cS[QN_MAX_M], cY[QN_MAX_M];
   __shared__ float gam;
-  const int c = blockIdx.x, b = blockIdx.y;
   const int D = (int)a.D;
   const int mm = a.m;
   const int Fp1 = a.F + 1;
@@ -781,16 +792,20 @@ __global__ __launch_bounds__(QN_BLOCK) void qn_direction_kernel(QnArgs a) {
   }
 }
 
+template <int KP, bool FULLM>
+__global__ __launch_bounds__(QN_BLOCK) void qn_direction_kernel(QnArgs a) {
+  qn_direction_body<KP, FULLM>(a, blockIdx.x, blockIdx.y);
+}
+
 // phase 2
 template <bool FULLM, bool WIDE>
-__global__ __launch_bounds__(QN_BLOCK) void qn_update_kernel(QnArgs a) {
+__device__ __forceinline__ void qn_update_body(const QnArgs& a, int c, int b) {
   __shared__ double sh[4 * NP3];
   __shared__ double p2v[NP2];
   __shared__ double fin_v[NP3];
   __shared__ double stage[QN_MAX_CHUNKS * NP3];
   __shared__ double tot3[NP3], tot1[NP1];
   __shared__ int pick, last;
-  const int c = blockIdx.x, b = blockIdx.y;
   const int D = (int)a.D;
   const int mm = a.m;
   const QnScalars qs = qn_load_scalars(a, b);  // uniform (scalar) loads, in flight with the P2 partials
@@ -917,7 +932,103 @@ __global__ __launch_bounds__(QN_BLOCK) void qn_update_kernel(QnArgs a) {
   __syncthreads();
   if (threadIdx.x == 0) {
     qn_finalize(a, b, p, p >= 0 ? p2v[3 * p] + p2v[3 * p + 1] : 0.0, qs, fin_v);
-    a.done[b] = 0;
+    __hip_atomic_store(a.done + b, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+template <bool FULLM, bool WIDE>
+__global__ __launch_bounds__(QN_BLOCK) void qn_update_kernel(QnArgs a) {
+  qn_update_body<FULLM, WIDE>(a, blockIdx.x, blockIdx.y);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Persistent solve: the whole fit's launch sequence (logreg_solve_run in bind.cpp: init direction,
+// evaluate, gradient, init update, then max_iter x [direction, evaluate, gradient, update]) as ONE
+// cooperative launch.  Every phase runs the SAME body as its stand-alone kernel over virtual blocks
+// (workgroup g takes blocks g, g + grid, ...), so the solve is bitwise the launch sequence's; a
+// grid barrier replaces each kernel boundary.  Barrier: an agent-scope release fence (this XCD's
+// L2 written back), one counter increment, a bounded spin on the counter, an agent-scope acquire
+// fence (stale L1 / L2 lines dropped).  The spin is bounded and a timed-out barrier raises a flag
+// that every later barrier checks first, so a fault can never leave waves spinning: the launcher
+// reports the flag and the caller falls back to the launch sequence.
+// ---------------------------------------------------------------------------------------------
+struct SolvePersistArgs {
+  QnArgs q;
+  LogregEvalArgs evT, ev1;  // the init evaluation (trial 0 of every model) / the per-iteration one
+  LogregGradArgs grT, gr1;
+  int nT, n1, max_iter;
+  uint32_t* sync;           // [0] barrier counter (zeroed by the launcher), [1] timeout flag
+};
+
+constexpr uint32_t SOLVE_SPIN_LIMIT = 1u << 22;
+
+__device__ __forceinline__ void grid_barrier(uint32_t* sync, uint32_t& gen) {
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    __hip_atomic_fetch_add(sync, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t target = (gen + 1) * gridDim.x;
+    uint32_t spins = 0;
+    while (__hip_atomic_load(sync, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+      if (__hip_atomic_load(sync + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) break;
+      if (++spins > SOLVE_SPIN_LIMIT) {
+        __hip_atomic_store(sync + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  }
+  ++gen;
+  __syncthreads();
+}
+
+template <int KP, int XLD, bool FULLM>
+__global__ __launch_bounds__(QN_BLOCK) void logreg_solve_persistent_kernel(SolvePersistArgs p) {
+  extern __shared__ float smem[];
+  uint32_t gen = 0;
+  const int G = gridDim.x, g0 = blockIdx.x;
+  const int nqb = p.q.nch * p.q.B;
+  const int tiles = (int)((p.ev1.N + EVAL_ROWS - 1) / EVAL_ROWS);
+  const int cols = (p.gr1.F + 1 + 255) / 256;
+  auto qn = [&](int phase, int head, int filled, int init, int fin_it) {
+    QnArgs a = p.q;
+    a.head = head;
+    a.filled = filled;
+    a.init = init;
+    a.fin_it = fin_it;
+    for (int v = g0; v < nqb; v += G) {
+      if (phase == 1)
+        qn_direction_body<KP, FULLM>(a, v % a.nch, v / a.nch);
+      else
+        qn_update_body<FULLM, FULLM>(a, v % a.nch, v / a.nch);
+      __syncthreads();  // the next virtual block reuses the LDS
+    }
+    grid_barrier(p.sync, gen);
+  };
+  auto evaluate = [&](const LogregEvalArgs& ev, const LogregGradArgs& gr, int n) {
+    for (int v = g0; v < tiles * n; v += G) {
+      logreg_eval_body<KP, XLD>(ev, v % tiles, v / tiles, tiles, smem);
+      __syncthreads();
+    }
+    grid_barrier(p.sync, gen);
+    for (int v = g0; v < cols * n; v += G) {
+      logreg_grad_body<KP>(gr, v % cols, v / cols);
+      __syncthreads();
+    }
+    grid_barrier(p.sync, gen);
+  };
+  qn(1, 0, 0, 1, 0);
+  evaluate(p.evT, p.grT, p.nT);
+  qn(2, 0, 0, 1, 0);
+  const int mm = p.q.m;
+  int head = 0, filled = 0;
+  for (int it = 0; it < p.max_iter; ++it) {
+    qn(1, head, filled, 0, 0);
+    evaluate(p.ev1, p.gr1, p.n1);
+    qn(2, head, filled, 0, it + 1);
+    head = (head + 1) % mm;
+    filled = filled + 1 < mm ? filled + 1 : mm;
   }
 }
 
@@ -1000,6 +1111,70 @@ extern "C" int har_qn_chunks(int64_t D, int B) {
   }();
   const int64_t by_b = budget / std::max(B, 1), by_d = (D + 255) / 256;
   return (int)std::max<int64_t>(1, std::min<int64_t>(QN_MAX_CHUNKS, std::min(by_b, by_d)));
+}
+
+// Host-side validation of one evaluation's arguments (the checks of har_logreg_eval / har_logreg_grad).
+static bool eval_args_ok(const LogregEvalArgs& a, const LogregGradArgs& g, int KP, int n) {
+  return a.Fd >= 0 && a.K >= 1 && a.K <= KP && a.T >= 1 && a.tstride >= 1 && a.slab != nullptr &&
+         (a.C == 0 || a.cat != nullptr) && a.mode == 0 && g.K == a.K && g.T == a.T && g.SL >= 1 &&
+         g.col_slice != nullptr && g.csc_off != nullptr && g.loss != nullptr && g.loss_fx == nullptr &&
+         g.N == a.N && g.F == a.F && g.Fd == a.Fd && g.tstride == a.tstride && g.model0 == a.model0 &&
+         g.ntiles == (int)((a.N + EVAL_ROWS - 1) / EVAL_ROWS) && n >= 1 && a.N > 0 && (a.C == 0 || a.R != nullptr);
+}
+
+// The whole solve as one cooperative launch (logreg_solve_persistent_kernel).  Returns 0 when it ran
+// (the caller then checks the timeout flag sync[1] with its results), -4 when this configuration
+// has no persistent instantiation (m != QN_MAX_M) or the grid cannot be co-resident (the caller uses
+// the launch sequence), -2 on invalid arguments.
+extern "C" int har_logreg_solve_persistent(const QnArgs* q, const LogregEvalArgs* evT, const LogregGradArgs* grT,
+                                           int nT, const LogregEvalArgs* ev1, const LogregGradArgs* gr1, int n1,
+                                           int KP, int max_iter, uint32_t* sync, int max_grid, hipStream_t s) {
+  const QnArgs& a = *q;
+  if ((KP != 8 && KP != 16) || a.K > KP || a.m < 1 || a.m > QN_MAX_M || a.T < 1 || a.T > QN_MAX_TRIALS ||
+      a.D != (int64_t)a.K * (a.F + 1) || a.D >= (1LL << 31) || a.nch != har_qn_chunks(a.D, a.B) || a.B < 1 ||
+      a.done == nullptr || sync == nullptr || max_iter < 0 || !eval_args_ok(*evT, *grT, KP, nT) ||
+      !eval_args_ok(*ev1, *gr1, KP, n1) || evT->N != ev1->N || evT->Fd != ev1->Fd || ev1->F != a.F ||
+      ev1->K != a.K || n1 != a.B * a.T || nT != a.B || ev1->tstride != 1 || evT->tstride != a.T)
+    return -2;
+  if (a.m != QN_MAX_M) return -4;
+  SolvePersistArgs p{*q, *evT, *ev1, *grT, *gr1, nT, n1, max_iter, sync};
+  p.q.head = p.q.filled = p.q.init = p.q.fin_it = 0;
+  static const bool mf_on = [] {
+    const char* e = std::getenv("HAR_LR_EVAL_MFMA");
+    return !e || std::atoi(e) != 0;
+  }();
+  const bool narrow = eval_xld(ev1->Fd) == EVAL_XLD_NARROW;
+  const bool mf = mf_on && !narrow;
+  const int xld = mf ? EVAL_XLD_MF : eval_xld(ev1->Fd);
+  const size_t lds = sizeof(float) * (EVAL_DCH * KP + EVAL_ROWS * xld + EVAL_ROWS * KP + EVAL_ROWS / 64 +
+                                      (mf ? 4 * EVAL_DCH * KP : 0));
+  const void* fn;
+  if (KP == 8)
+    fn = mf ? (const void*)logreg_solve_persistent_kernel<8, EVAL_XLD_MF, true>
+            : narrow ? (const void*)logreg_solve_persistent_kernel<8, EVAL_XLD_NARROW, true>
+                     : (const void*)logreg_solve_persistent_kernel<8, EVAL_DCH + 1, true>;
+  else
+    fn = mf ? (const void*)logreg_solve_persistent_kernel<16, EVAL_XLD_MF, true>
+            : narrow ? (const void*)logreg_solve_persistent_kernel<16, EVAL_XLD_NARROW, true>
+                     : (const void*)logreg_solve_persistent_kernel<16, EVAL_DCH + 1, true>;
+  // grid: every phase's virtual blocks once if they fit co-resident, else as many as are
+  int dev = 0, cus = 0, per_cu = 0;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, QN_BLOCK, lds) != hipSuccess || per_cu < 1)
+    return -4;
+  const int tiles = (int)((ev1->N + EVAL_ROWS - 1) / EVAL_ROWS), cols = (a.F + 1 + 255) / 256;
+  const int64_t want = std::max<int64_t>({(int64_t)a.nch * a.B, (int64_t)tiles * n1, (int64_t)cols * n1});
+  if (max_grid < 0 && want > (int64_t)per_cu * cus) return -4;  // one co-resident round required
+  int64_t grid = std::min<int64_t>(want, (int64_t)per_cu * cus);
+  if (max_grid > 0) grid = std::min<int64_t>(grid, max_grid);
+  if (grid < 1) return -4;
+  if (hipMemsetAsync(sync, 0, 2 * sizeof(uint32_t), s) != hipSuccess) return -4;
+  void* kargs[] = {&p};
+  if (hipLaunchCooperativeKernel(fn, dim3((unsigned)grid), dim3(QN_BLOCK), kargs, (unsigned)lds, s) != hipSuccess) {
+    (void)hipGetLastError();
+    return -4;
+  }
+  return 0;
 }
 
 extern "C" int har_lbfgs_phase(const QnArgs* args, int KP, int phase, hipStream_t s) {

@@ -288,3 +288,45 @@ def test_crossvalidator_batched_refit_matches_plain_fit_gpu(cuda):
     xd = x.to(cuda)
     agree = float((m.bestModel.predict(xd) == plain.predict(xd)).float().mean())
     assert agree > 0.99, agree
+
+
+@pytest.mark.parametrize("specs_kind", ["pair", "wisdm"])
+def test_persistent_solve_equals_launch_sequence(cuda, wisdm_csv, specs_kind):
+    """The whole solve as ONE cooperative launch (logreg_solve_persistent_kernel: the same phase
+    bodies over virtual blocks, grid barriers for the kernel boundaries) is bitwise the launch
+    sequence: coefficients, intercepts and objective histories."""
+    from har.models.logreg import FitSpec, LogisticRegression
+    from har.ops import _native
+    from har.ops import logreg as L
+
+    mod = _native.kernels()
+    if specs_kind == "pair":
+        _, y, hm = _hybrid_problem(cuda, N=3000, seed=9)
+        est = LogisticRegression(maxIter=20, regParam=0.1)
+        specs, K = [FitSpec(None, 0.1, 0.0), FitSpec(None, 0.3, 0.1)], 6
+        y = y.to(cuda)
+    else:
+        from har.features.hybrid import hybrid_features
+        from har.suite import load_wisdm
+        from har.models.base import labels_tensor, num_label_classes
+
+        train, _, _ = load_wisdm(wisdm_csv, "reference", 2018, device=cuda)
+        hm = hybrid_features(train, "features", cuda)
+        y = labels_tensor(train, "label", cuda)
+        K = num_label_classes(train, "label", cuda)
+        est = LogisticRegression(maxIter=20, regParam=0.3, elasticNetParam=0.8)
+        specs = [FitSpec(None, 0.3, 0.8)]
+    out, modes = [], []
+    old = mod.logreg_set_persistent(1)
+    try:
+        for mode in (1, 0):
+            mod.logreg_set_persistent(mode)
+            out.append(est.fit_many(hm, y, specs, K))
+            modes.append(L.LAST_SOLVE_MODE)
+    finally:
+        mod.logreg_set_persistent(old)
+    assert modes == [1, 0]
+    for m1, m2 in zip(*out):
+        assert torch.equal(m1.coefficientMatrix, m2.coefficientMatrix)
+        assert torch.equal(m1.interceptVector, m2.interceptVector)
+        assert m1.summary["objectiveHistory"] == m2.summary["objectiveHistory"]
