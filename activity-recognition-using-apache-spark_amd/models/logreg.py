@@ -34,7 +34,8 @@ from ..data.table import Table
 from ..ops import _native
 from ..features.hybrid import HybridMatrix, hybrid_features
 from ..features.hybrid import from_dense as hybrid_from_dense
-from ..ops.logreg import DeviceLogregSolver, LogregDesign, logreg_margins_native, native_classes_ok, pack_bucket, \
+from ..ops.logreg import DeviceLogregSolver, LogregDesign, SolverCacheEntry, logreg_margins_native, \
+    native_classes_ok, pack_bucket, solver_cache_get, solver_cache_put, \
     unpack_bucket
 from ..optim import lbfgs
 from .base import ClassificationModel, ClassifierParams, Estimator, dp_allreduce, dp_context, dp_owner, dp_rows, \
@@ -195,9 +196,10 @@ class LogisticRegression(Estimator, ClassifierParams):
             model.setThresholds([1.0 - float(self.threshold), float(self.threshold)])
         return model
 
-    def _setup(self, hm: HybridMatrix, y: torch.Tensor, specs: Sequence[FitSpec], K: int, allreduce):
+    def _setup(self, hm: HybridMatrix, y: torch.Tensor, specs: Sequence[FitSpec], K: int, allreduce, reuse=None):
         """Summarizer (+ its one all-reduce) -> standardization, masks, regularization vectors, x0.
-        GPU: three HIP launches (logreg_setup.hip), no host round trip; CPU: the same math in torch."""
+        GPU: three HIP launches (logreg_setup.hip), no host round trip; CPU: the same math in torch.
+        ``reuse`` (a solver-cache entry): its design, and its input buffers as the outputs."""
         dev = hm.device
         N, F = hm.n_rows, hm.n_features
         binomial = self.family == "binomial" or (self.family == "auto" and K <= 2)
@@ -211,7 +213,12 @@ class LogisticRegression(Estimator, ClassifierParams):
         else:
             rw = torch.stack([torch.ones(N, device=dev) if s.row_weight is None else s.row_weight.to(dev).float()
                               for s in specs])                                        # [B, N]
-        design = LogregDesign(hm, y, rw, Kp, native=native)
+        if reuse is not None:  # the cached design: this fit's row weights into its buffer
+            design = reuse.design
+            if rw is not None:
+                design.rw.copy_(rw)
+        else:
+            design = LogregDesign(hm, y, rw, Kp, native=native)
         summ = design.summary()
         if allreduce is not None:
             allreduce(summ)
@@ -222,12 +229,15 @@ class LogisticRegression(Estimator, ClassifierParams):
             has_l1 = any(s.regParam * s.elasticNetParam > 0 for s in specs)
             if design.S != B:  # unweighted: one summary row serves every spec
                 summ = summ.expand(B, -1).contiguous()
-            inv_std = torch.empty(B, F, device=dev)
-            inv_wsum = torch.empty(B, device=dev)
-            pmask = torch.empty(B, Kp, F + 1, device=dev)
-            l2v = torch.empty(B, D, device=dev)
-            l1v = torch.empty(B, D, device=dev) if has_l1 else None
-            x0 = torch.empty(B, Kp, F + 1, device=dev)
+            if reuse is not None:
+                inv_std, inv_wsum, pmask, l2v, l1v, x0 = reuse.bufs
+            else:
+                inv_std = torch.empty(B, F, device=dev)
+                inv_wsum = torch.empty(B, device=dev)
+                pmask = torch.empty(B, Kp, F + 1, device=dev)
+                l2v = torch.empty(B, D, device=dev)
+                l1v = torch.empty(B, D, device=dev) if has_l1 else None
+                x0 = torch.empty(B, Kp, F + 1, device=dev)
             _native.kernels().logreg_prepare(summ.data_ptr(), reg_a[0].data_ptr(), reg_a[1].data_ptr(), B, F, Kp, Kp,
                                              int(self.standardization), int(self.fitIntercept), int(binomial),
                                              inv_std.data_ptr(), inv_wsum.data_ptr(), pmask.data_ptr(),
@@ -308,13 +318,29 @@ class LogisticRegression(Estimator, ClassifierParams):
             last = ckpt.latest(fingerprint=fp)
             if last is not None:
                 return self._models_from_state(last[0], last[1], len(specs), dev)
-        design, binomial, Kp, inv_std, inv_wsum, pmask, l2v, l1v, x0 = self._setup(hm, y, specs, K, allreduce)
-        B, D = len(specs), Kp * (F + 1)
         T = max(1, int(self.lineSearchTrials))
+        # repeated single-device fits on one resident design reuse the solver (ops/logreg.py)
+        ckey = ent = None
+        if (dev.type == "cuda" and allreduce is None and ckpt is None
+                and native_classes_ok(2 if self.family == "binomial" or (self.family == "auto" and K <= 2) else K)):
+            ckey = (id(hm), K, len(specs), T, self.maxIter, float(self.tol), self.family, self.fitIntercept,
+                    self.standardization, any(s.regParam * s.elasticNetParam > 0 for s in specs),
+                    any(s.row_weight is not None for s in specs), str(dev))
+            ent = solver_cache_get(ckey, hm, y)
+        design, binomial, Kp, inv_std, inv_wsum, pmask, l2v, l1v, x0 = self._setup(hm, y, specs, K, allreduce,
+                                                                                    reuse=ent)
+        B, D = len(specs), Kp * (F + 1)
         poll = 10 if self.maxIter > 20 else 0
         if design.native:
-            solver = DeviceLogregSolver(design, B, T, 10, inv_std, pmask, inv_wsum, l2v, l1v, self.maxIter, self.tol,
-                                        allreduce=allreduce)
+            if ent is not None:
+                solver = ent.solver
+                solver.reset()
+            else:
+                solver = DeviceLogregSolver(design, B, T, 10, inv_std, pmask, inv_wsum, l2v, l1v, self.maxIter,
+                                            self.tol, allreduce=allreduce)
+                if ckey is not None:
+                    solver_cache_put(ckey, SolverCacheEntry(hm, y, design, solver,
+                                                            (inv_std, inv_wsum, pmask, l2v, l1v, x0)))
             xs, fobj, iters = solver.solve(x0, poll=poll)
             n_evals = solver.n_evals
             # objective history, objectives and iteration counts to the host in ONE transfer

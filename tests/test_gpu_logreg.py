@@ -330,3 +330,56 @@ def test_persistent_solve_equals_launch_sequence(cuda, wisdm_csv, specs_kind):
         assert torch.equal(m1.coefficientMatrix, m2.coefficientMatrix)
         assert torch.equal(m1.interceptVector, m2.interceptVector)
         assert m1.summary["objectiveHistory"] == m2.summary["objectiveHistory"]
+
+
+def test_solver_cache_refit_is_bitwise_a_fresh_fit(cuda, wisdm_csv):
+    """A repeated fit on the same resident table reuses the cached solver (arena, argument blocks,
+    solve plan): its model is bitwise the model of a fit with the cache cleared, and a fit with other
+    hyper-parameters in between leaves it unchanged."""
+    from har.models.logreg import LogisticRegression
+    from har.ops import logreg as L
+    from har.suite import load_wisdm
+
+    train, _, _ = load_wisdm(wisdm_csv, "reference", 2018, device=cuda)
+    est = LogisticRegression(maxIter=20, regParam=0.3, elasticNetParam=0.8)
+    L.solver_cache_clear()
+    a = est.fit(train)
+    assert len(L._SOLVER_CACHE) == 1
+    other = LogisticRegression(maxIter=20, regParam=0.05, elasticNetParam=0.5).fit(train)  # same key, new inputs
+    b = est.fit(train)
+    assert len(L._SOLVER_CACHE) == 1
+    L.solver_cache_clear()
+    c = est.fit(train)
+    for m in (b, c):
+        assert torch.equal(m.coefficientMatrix, a.coefficientMatrix)
+        assert torch.equal(m.interceptVector, a.interceptVector)
+        assert m.summary["objectiveHistory"] == a.summary["objectiveHistory"]
+    assert not torch.equal(other.coefficientMatrix, a.coefficientMatrix)
+
+
+def test_solver_cache_crossvalidator_repeat_is_bitwise(cuda, wisdm_csv):
+    """The CrossValidator's batched weighted fit reuses its cached solver on a repeat (new fold row
+    weights copied into the cached design): the same metrics and model as with the cache cleared."""
+    from har.evaluation.evaluators import RegressionEvaluator
+    from har.models.logreg import LogisticRegression
+    from har.ops import logreg as L
+    from har.suite import load_wisdm
+    from har.tuning.crossval import CrossValidator, ParamGridBuilder
+
+    train, _, _ = load_wisdm(wisdm_csv, "reference", 2018, device=cuda)
+    lr = LogisticRegression(maxIter=10)
+    grid = ParamGridBuilder().addGrid("regParam", [0.1, 0.3]).addGrid("elasticNetParam", [0.0, 0.5]).build()
+
+    def run(seed):
+        return CrossValidator(estimator=lr, estimatorParamMaps=grid, evaluator=RegressionEvaluator(metricName="mae"),
+                              numFolds=3, seed=seed).fit(train)
+
+    L.solver_cache_clear()
+    a = run(1)
+    run(5)  # other folds through the cached solver
+    b = run(1)
+    L.solver_cache_clear()
+    c = run(1)
+    for m in (b, c):
+        assert m.avgMetrics == a.avgMetrics
+        assert torch.equal(m.bestModel.coefficientMatrix, a.bestModel.coefficientMatrix)
