@@ -130,17 +130,28 @@ def batched_metrics(metric: str, label: torch.Tensor, pred: torch.Tensor, mask: 
             out.append(binary_metrics(sc, label.to(rows.device)[rows])[metric])
         return np.asarray(out, dtype=np.float64)
     if metric in ("rmse", "mse", "r2", "mae", "var"):
+        # only the requested metric's terms (each is a few [B, N] launches; the CrossValidator asks one)
         yd = y.double().expand(B, N)
-        e = pred.double() - yd
         n = w.sum(1).clamp_min(1e-300)
+        if metric == "mae":
+            return ((w * (pred.double() - yd).abs()).sum(1) / n).cpu().numpy()
+
+        def var_y():
+            my = (w * yd).sum(1) / n
+            return (w * yd * yd).sum(1) / n - my * my
+
+        if metric == "var":
+            return var_y().cpu().numpy()
+        e = pred.double() - yd
         se = (w * e * e).sum(1)
-        res = {"mse": se / n, "rmse": (se / n).sqrt(), "mae": (w * e.abs()).sum(1) / n}
-        my = (w * yd).sum(1) / n
-        var_y = (w * yd * yd).sum(1) / n - my * my
-        res["var"] = var_y
-        ss_tot = var_y * n
-        res["r2"] = torch.where(ss_tot > 0, 1.0 - se / ss_tot.clamp_min(1e-300), torch.full_like(se, float("nan")))
-        return res[metric].cpu().numpy()
+        if metric == "mse":
+            out = se / n
+        elif metric == "rmse":
+            out = (se / n).sqrt()
+        else:  # r2
+            ss_tot = var_y() * n
+            out = torch.where(ss_tot > 0, 1.0 - se / ss_tot.clamp_min(1e-300), torch.full_like(se, float("nan")))
+        return out.cpu().numpy()
     K = num_classes
     if pred.is_cuda and K * K <= 4096:
         cm = mops.confusion_matrix_batched(y.view(N), pred.long().clamp(0, K - 1), mask.bool(), K).double()

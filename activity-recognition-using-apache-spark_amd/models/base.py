@@ -4,6 +4,7 @@
 from __future__ import annotations
 
 import copy
+import random
 import secrets
 from typing import Dict, Optional, Tuple
 
@@ -13,12 +14,19 @@ import torch
 from ..data.table import Column, DeviceColumn, Table
 
 
+# uid generator: seeded once from the OS entropy pool, then 80 random bits per uid (a urandom
+# syscall per uid cost ~5 us, paid 54 times by a CrossValidator's batched LR fit)
+_UID_RNG = random.Random(secrets.randbits(128))
+
+
 def new_uid(prefix: str) -> str:
     """Spark-style uid: ``<Class>_<20 hex chars>`` (e.g. ``LogisticRegression_446cab28d15c5195e1ba``)."""
-    return f"{prefix}_{secrets.token_hex(10)}"
+    return f"{prefix}_{_UID_RNG.getrandbits(80):020x}"
 
 
 def resolve_device(device=None) -> torch.device:
+    if isinstance(device, torch.device):
+        return device
     if device is None or device == "auto":
         return torch.device("cuda" if torch.cuda.is_available() else "cpu")
     return torch.device(device)

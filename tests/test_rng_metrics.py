@@ -91,3 +91,21 @@ def test_evaluate_all_reference_identities():
     assert r.correct + r.wrong == r.count_total == 1625
     assert r.ratio_correct == pytest.approx(r.accuracy)
     assert r.mse == pytest.approx(r.rmse ** 2)
+
+
+@pytest.mark.parametrize("metric", ["mse", "rmse", "mae", "r2", "var"])
+def test_batched_regression_metrics_match_single(metric):
+    """The CrossValidator's batched regression metric (one requested metric, masked rows per model)
+    equals the single-model definition on each model's rows."""
+    from har.evaluation.metrics import batched_metrics, regression_metrics
+
+    g = torch.Generator().manual_seed(3)
+    N, B = 400, 4
+    label = torch.randint(0, 6, (N,), generator=g)
+    pred = torch.randint(0, 6, (B, N), generator=g)
+    mask = torch.rand(B, N, generator=g) < 0.4
+    got = batched_metrics(metric, label, pred, mask, 6)
+    for b in range(B):
+        rows = torch.nonzero(mask[b]).squeeze(1)
+        want = regression_metrics(label[rows].numpy(), pred[b, rows].numpy())[metric]
+        assert abs(got[b] - want) < 1e-9 * max(1.0, abs(want))
