@@ -102,7 +102,7 @@ def settle_clocks(ctx, run, ms, dev):
     if ms <= 0 or dev.type != "cuda":
         return 0.0
     t0 = time.perf_counter()
-    i = 0
+    i = 1 << 20  # step indices past every warm-up / timed index (steps keyed on small i stay untouched)
     while True:
         for _ in range(16):
             run(i)
@@ -314,6 +314,7 @@ def bench_infer(args, ctx):
         if i < nb:
             correct.add_((pred.long() == y[j * B:(j + 1) * B]).sum())
 
+    settle_ms = settle_clocks(ctx, step, args.settle_ms, dev)
     elapsed = timed(ctx, step, args.steps, args.warmup, dev)
     acc = float(correct) / (B * min(nb, args.steps + args.warmup))
     return {"value": B * world * args.steps / elapsed, "ms_per_step": elapsed * 1e3 / args.steps,
@@ -324,7 +325,7 @@ def bench_infer(args, ctx):
                        "global_batch": B * world, "seq_len": None, "features": N_FEATURES,
                        "parallelism": f"dp{world}"},
             "test_accuracy": hdist.mean_over_ranks(ctx, acc), "test_accuracy_data": "held-out synthetic windows",
-            "mode": "inference"}
+            "mode": "inference", "settle_ms": settle_ms}
 
 
 def _featurized(n_windows, spec, dev, first_window):
@@ -389,6 +390,10 @@ def bench_rf(args, ctx, nine_axis=False, single_tree=False):
         model["m"] = est.fit_tensors(X, y, K, allreduce=None if owner else dp.allreduce_sum(ctx),
                                      row_offset=rank * n_local, thresholds=thr, owner=owner)
 
+    settle_ms = settle_clocks(ctx, run, args.settle_ms, dev)
+    for st in (tp_stats, owner.stats if owner is not None else {}):  # per-fit collective counts: timed fits only
+        for k in st:
+            st[k] = 0
     elapsed = timed(ctx, run, args.steps, args.warmup, dev)
     acc = float((model["m"].predict(Xt) == yt).float().mean())
     rows = n_local * world
@@ -412,7 +417,7 @@ def bench_rf(args, ctx, nine_axis=False, single_tree=False):
                     f"({X.shape[1]} features, {K} classes)",
             "config": {"model": name, "global_batch": rows, "seq_len": spec.window, "parallelism": f"dp{world}"},
             "test_accuracy": hdist.mean_over_ranks(ctx, acc), "test_accuracy_data": "held-out synthetic windows",
-            "dtype": "fp32", "rf_parallel": mode,
+            "dtype": "fp32", "rf_parallel": mode, "settle_ms": settle_ms,
             "histogram_reduction": (args.rf_reduce if mode == "data" else "none (tree parallel)") if world > 1 else "none",
             "collectives_per_step": coll}
 
@@ -485,6 +490,7 @@ def bench_stream(args, ctx):
         rec.update(test_accuracy=held_out_accuracy(),
                    test_accuracy_data="held-out synthetic stream (8192 windows past every shard), after the timed passes")
         return rec
+    settle_ms = settle_clocks(ctx, step, args.settle_ms, dev)
     elapsed = timed(ctx, step, args.steps, args.warmup, dev)
     acc = held_out_accuracy()
     return {"value": global_batch * args.steps / elapsed, "ms_per_step": elapsed * 1e3 / args.steps,
@@ -495,7 +501,7 @@ def bench_stream(args, ctx):
             "config": {"model": f"raw stream -> window features ({F}) -> MLP bf16 "
                                 f"({F}-{args.hidden}-{args.hidden}-{N_CLASSES})",
                        "global_batch": global_batch, "seq_len": W, "parallelism": f"dp{world}"},
-            "test_accuracy": acc, "test_accuracy_data": "held-out synthetic stream"}
+            "test_accuracy": acc, "test_accuracy_data": "held-out synthetic stream", "settle_ms": settle_ms}
 
 
 def _stream_full_pass(args, ctx, spec, stream, labels, eng, mean, inv_std, samples_local):
@@ -541,6 +547,7 @@ def _stream_full_pass(args, ctx, spec, stream, labels, eng, mean, inv_std, sampl
         for j in range(nb):
             eng.train_step(X[j * B:(j + 1) * B], y32[j * B:(j + 1) * B], gb)
 
+    settle_ms = settle_clocks(ctx, one_pass, args.settle_ms, dev)
     elapsed = timed(ctx, one_pass, args.steps, args.warmup, dev)
     trained = nb * gb
     return {"value": trained * args.steps / elapsed, "ms_per_step": elapsed * 1e3 / args.steps,
@@ -553,7 +560,7 @@ def _stream_full_pass(args, ctx, spec, stream, labels, eng, mean, inv_std, sampl
             "config": {"model": f"raw stream full pass -> window features -> MLP bf16 "
                                 f"({n_features(3)}-{args.hidden}-{args.hidden}-{N_CLASSES})",
                        "global_batch": gb, "seq_len": fz.window, "parallelism": f"dp{world}"},
-            "samples_per_gpu": samples_local}
+            "samples_per_gpu": samples_local, "settle_ms": settle_ms}
 
 
 def main():
