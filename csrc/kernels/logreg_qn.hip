@@ -621,8 +621,11 @@ __device__ __forceinline__ DirElem dir_load(const QnArgs& a, int b, int e) {
   const float isd = a.inv_std[(int64_t)b * a.F + min(col, a.F - 1)];
   v.wsc = a.pmask[b * D + e] * (col < a.F ? isd : 1.f);
 #pragma unroll
-  for (int j = 0; j < QN_MAX_M; ++j) {  // slots >= m: allocated ([QN_MAX_M ... ] not read), see below
-    const int jj = j < a.m ? j : 0;
+  for (int j = 0; j < QN_MAX_M; ++j) {
+    // slots not filled yet (j >= filled; the ring fills 0, 1, ... before it wraps) re-read slot 0: the
+    // same lines, so they cost no HBM traffic (the batched CV direction is bandwidth-bound while the
+    // history fills), and their coefficients cS / cY are 0; slots >= m are never valid either
+    const int jj = j < a.filled ? j : 0;
     v.s[j] = a.S[jj * sstride + b * D + e];
     v.y[j] = a.Y[jj * sstride + b * D + e];
   }
@@ -882,8 +885,11 @@ __device__ __forceinline__ void qn_update_body(const QnArgs& a, int c, int b) {
             // accumulates its P3 sums, which finalize never reads
             float sj = 0.f, yj = 0.f;
             if (FULLM || !hj) {
-              sj = Sb[j * sstride + e];
-              yj = Yb[j * sstride + e];
+              // (unfilled slots re-read slot 0 — cached lines, no HBM traffic; their dots are never
+              // read: a slot's Gram row / column is rewritten when its first pair enters)
+              const int jl = j < a.filled ? j : 0;
+              sj = Sb[jl * sstride + e];
+              yj = Yb[jl * sstride + e];
               ps[5 + 3 * j] = fmaf(se, yj, ps[5 + 3 * j]);
               ps[6 + 3 * j] = fmaf(sj, ye, ps[6 + 3 * j]);
               ps[7 + 3 * j] = fmaf(ye, yj, ps[7 + 3 * j]);

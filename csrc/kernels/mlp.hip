@@ -218,9 +218,9 @@ __global__ void cast_pad_kernel(const float* __restrict__ in, int rows, int cin,
 //   GR_STORE   G[i] = g                                         (DP: before the all-reduce)
 //   GR_ADAM    Adam update of param / m / v / bf16 copy with t = *step (ticked earlier in the step
 //              by the fused backward kernel or adam_tick_kernel: no kernel both ticks and reads it)
-// A workgroup = 16 waves x 64 float4 columns: wave q sums slabs q, q + 16, q + 32, ... (eight loads
-// in flight per step: the 256 per-workgroup slabs of the forward kernel take two steps), the 16
-// partials are added in a fixed tree order -> bitwise reproducible, and N = 1 (GR_REDUCE |
+// A workgroup = GR_W (4 by default; 8 / 16 by HAR_GR_W) waves x 64 float4 columns: wave q sums slabs
+// q, q + GR_W, q + 2 GR_W, ... (eight loads in flight per step), the GR_W partials are added in a
+// fixed tree order -> bitwise reproducible, and N = 1 (GR_REDUCE |
 // GR_ADAM) and N > 1 (GR_REDUCE | GR_STORE, all-reduce, GR_ADAM) apply the same summation and the
 // same Adam arithmetic.  With fragment copies (MlpFragSpec) the new bf16 values also go to the W0 and
 // W1 fragment copies (8-byte runs); the W1^T copy is written by the step's forward kernel, which
@@ -401,9 +401,11 @@ extern "C" int har_grad_reduce_adam(int nreg, const float* const* src, const int
   const int64_t blocks = (n / 4 + 63) / 64;
   if (blocks == 0) return 0;
   if (tick) adam_tick_kernel<<<1, 1, 0, s>>>(step);
+  // waves per workgroup: 4 (tools/gpu_qnwg_ab.sh a: flagship reduction + Adam 6.6 -> 4.9 us with 64 slabs,
+  // the small-batch step 21.7 -> 20.8 us with 8; 8 waves 5.4 / 20.9; 16 was the round-3 choice)
   static const int w = [] {
     const char* e = getenv("HAR_GR_W");
-    return e ? atoi(e) : 16;
+    return e ? atoi(e) : 4;
   }();
   if (w == 4)
     grad_reduce_adam_kernel<4><<<(int)blocks, 256, 0, s>>>(rg, n, G, param, m, v, pb, lr, b1, b2, eps, wd, step, mode,
