@@ -480,6 +480,36 @@ def bench_stream(args, ctx):
             feat.copy_(featurize(s))
             eng.train_step(pad_input_bf16(feat, eng.layout.in_pad), y32[j * B:(j + 1) * B], global_batch)
 
+    if eng.native and args.stream_overlap:
+        # software pipeline: step i trains on batch i (featurized during step i - 1) while a side
+        # stream featurizes batch i + 1 into the other buffer (events order the buffer reuse), so the
+        # memory-bound featurizer runs beside the MLP kernels instead of between them.  A timed window
+        # of K steps still featurizes K batches and trains K batches.
+        xb = [torch.empty_like(xin), torch.empty_like(xin)]
+        fstream = torch.cuda.Stream(device=dev)
+        ready = [torch.cuda.Event(), torch.cuda.Event()]
+        consumed = [torch.cuda.Event(), torch.cuda.Event()]
+        pending = {"i": None}
+
+        def featurize_into(i):
+            j, buf = i % nb, i % 2
+            fstream.wait_event(consumed[buf])  # the train step that read this buffer has run
+            with torch.cuda.stream(fstream):
+                window_features_mlp(stream[j * B * W:(j + 1) * B * W], W, W, spec.hz, mean, inv_std,
+                                    eng.layout.in_pad, -1.0, out=xb[buf])
+                ready[buf].record(fstream)
+
+        def step(i):  # noqa: F811
+            if pending["i"] != i:  # not prefetched (the first step, or a jump in the step index)
+                featurize_into(i)
+            featurize_into(i + 1)
+            pending["i"] = i + 1
+            cur = torch.cuda.current_stream()
+            cur.wait_event(ready[i % 2])
+            j = i % nb
+            eng.train_step(xb[i % 2], y32[j * B:(j + 1) * B], global_batch)
+            consumed[i % 2].record(cur)
+
     def held_out_accuracy():
         # 8192 windows of the stream beyond every rank's shard, featurized the same way
         st_, yt = generate_stream(8192, spec, dev, first_window=10 ** 9)
@@ -501,7 +531,8 @@ def bench_stream(args, ctx):
             "config": {"model": f"raw stream -> window features ({F}) -> MLP bf16 "
                                 f"({F}-{args.hidden}-{args.hidden}-{N_CLASSES})",
                        "global_batch": global_batch, "seq_len": W, "parallelism": f"dp{world}"},
-            "test_accuracy": acc, "test_accuracy_data": "held-out synthetic stream", "settle_ms": settle_ms}
+            "test_accuracy": acc, "test_accuracy_data": "held-out synthetic stream", "settle_ms": settle_ms,
+            "stream_overlap": bool(eng.native and args.stream_overlap)}
 
 
 def _stream_full_pass(args, ctx, spec, stream, labels, eng, mean, inv_std, samples_local):
@@ -596,6 +627,9 @@ def main():
                     help="--config stream: time full passes over every resident sample (halo-sharded featurization "
                          "+ one MLP epoch) instead of per-batch steps")
     ap.add_argument("--out", type=str, default="")
+    ap.add_argument("--stream-overlap", type=int, default=int(os.environ.get("HAR_STREAM_OVERLAP", "0")),
+                    help="--config stream: featurize batch i+1 on a side stream while batch i trains (1) or "
+                         "featurize then train in one stream (0)")
     ap.add_argument("--settle-ms", type=float, default=float(os.environ.get("HAR_BENCH_SETTLE_MS", "200")),
                     help="MLP configs: untimed training steps for this long before the warm-up (clock settle)")
     args = ap.parse_args()

@@ -25,6 +25,7 @@ PY
 b rf --config rf --steps 5 --warmup 2 || exit $?
 b rf9 --config rf9 --steps 5 --warmup 2 || exit $?
 b stream --config stream --steps 50 --warmup 10 || exit $?
+b stream_ov --config stream --steps 50 --warmup 10 --stream-overlap 1 || exit $?
 b infer --config infer --steps 50 --warmup 10 || exit $?
 HAR_WINDOW_AB=0 timeout -k 10 200 python -u tools/window_probe.py > "$OUT/window.txt" 2>&1 || exit $?
 grep -v amdgpu.ids "$OUT/window.txt"
