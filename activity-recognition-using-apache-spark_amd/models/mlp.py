@@ -691,6 +691,21 @@ class MLPEngine:
             raise ValueError("infer_fused_f32: unsupported shape")
         out = torch.empty(B, L.num_classes, dtype=torch.float32, device=X.device)
         pred = torch.empty(B, dtype=torch.int32, device=X.device)
+        if (getattr(self, "Pf", None) is not None and L.hidden[0] == 256 and B % 64 == 0
+                and os.environ.get("HAR_MLP_STEP_INFER", "1") != "0"):
+            # the training step's forward pipeline in its serving instantiation (mlp_step.hip INFER:
+            # weights in registers from the fragment copies, one barrier per 32-row tile) after the
+            # fp32 -> padded bf16 cast
+            mod = _native.kernels()
+            if not self._pf_fresh:
+                self._pack_frag()
+            Xb = torch.empty(B, L.in_pad, dtype=torch.bfloat16, device=X.device)
+            mod.cast_pad_bf16(X.data_ptr(), B, F, X.stride(0), Xb.data_ptr(), L.in_pad, _native.stream_ptr())
+            mod.mlp_step_fwd_infer(Xb.data_ptr(), L.in_pad, self.Pf.data_ptr(), self._w(self.P, "b0").data_ptr(),
+                                   self._w(self.P, "b1").data_ptr(), 256, self._w(self.Pb, "Wout").data_ptr(),
+                                   self._w(self.P, "bout").data_ptr(), B, L.num_classes, out.data_ptr(),
+                                   pred.data_ptr(), _native.stream_ptr())
+            return out, pred
         _native.kernels().mlp_fwd_infer_f32(X.data_ptr(), X.stride(0), F, L.in_pad, self._w(self.Pb, "W0").data_ptr(),
                                             self._w(self.P, "b0").data_ptr(), self._w(self.Pb, "W1").data_ptr(),
                                             self._w(self.P, "b1").data_ptr(), self.dims[-1],

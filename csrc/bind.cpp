@@ -749,6 +749,13 @@ PYBIND11_MODULE(_har_native, m) {
                            P<int32_t>(block_correct), S(stream)),
           "mlp_step_fwd");
   });
+  m.def("mlp_step_fwd_infer", [](u X, int K0, u Wf, u b0, u b1, int H, u Wo, u bo, int B, int C, u logits, u pred,
+                                 u stream) {
+    check(har_mlp_step_fwd_infer(P<const uint16_t>(X), K0, P<const uint16_t>(Wf), P<const float>(b0),
+                                 P<const float>(b1), H, P<const uint16_t>(Wo), P<const float>(bo), B, C,
+                                 P<float>(logits), P<int32_t>(pred), S(stream)),
+          "mlp_step_fwd_infer");
+  });
   m.def("mlp_step_bwd", [](u dz, u mask, u X, int K0, u Wf, int H, u b0, u Wo, int B, u gw1, u gw0, u gb0, u gb1,
                            int64_t stride, u tick, u fslab, int fslab_w, u gwo, u gbo, u stream) {
     check(har_mlp_step_bwd(P<const uint32_t>(dz), P<const uint32_t>(mask), P<const uint16_t>(X), K0,

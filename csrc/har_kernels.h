@@ -114,6 +114,10 @@ int har_mlp_step_fwd(const uint16_t* X, int K0, uint16_t* Wf, const float* b0, c
                      const uint16_t* Wo, const float* bo, const int32_t* labels, int B, int C, float scale,
                      uint32_t* dz, uint32_t* mask, float* slab, float* block_loss, int32_t* block_correct,
                      hipStream_t s);
+// serving forward on the same pipeline: logits [B][C] fp32 + argmax [B] (B % 64 == 0, H == 256)
+int har_mlp_step_fwd_infer(const uint16_t* X, int K0, const uint16_t* Wf, const float* b0, const float* b1, int H,
+                           const uint16_t* Wo, const float* bo, int B, int C, float* logits, int32_t* pred,
+                           hipStream_t s);
 int har_mlp_step_bwd(const uint32_t* dz, const uint32_t* mask, const uint16_t* X, int K0, const uint16_t* Wf, int H,
                      const float* b0, const uint16_t* Wo, int B, float* gw1, float* gw0, float* gb0, float* gb1,
                      int64_t slab_stride, int32_t* tick, const float* fslab, int fslab_w, float* gwo, float* gbo,

@@ -78,7 +78,9 @@ __device__ __forceinline__ bf16x8_t ldx(const bf16_t* __restrict__ X, int row, i
   return *reinterpret_cast<const bf16x8_t*>(X + (size_t)row * K0 + kc * 32 + g * 8);
 }
 
-template <int K0, bool STAMP>
+// INFER: the serving forward of the same pipeline — no labels, no dz / relu' mask / dWout / W1^T copy;
+// `slab` receives the logits [B][C] (fp32, bias included) and `block_correct` the argmax [B].
+template <int K0, bool STAMP, bool INFER = false>
 __global__ __launch_bounds__(512) void mlp_fwd3_kernel(
     const bf16_t* __restrict__ X, bf16_t* __restrict__ Wf, const float* __restrict__ b0,
     const float* __restrict__ b1, const bf16_t* __restrict__ Wo,
@@ -138,7 +140,7 @@ __global__ __launch_bounds__(512) void mlp_fwd3_kernel(
   int ynext = 0;
   if (nt > 0) {
     load_x(0);
-    ynext = labels[tile_of(0) * FRT + sr];
+    if constexpr (!INFER) ynext = labels[tile_of(0) * FRT + sr];
   }
   __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -217,7 +219,7 @@ __global__ __launch_bounds__(512) void mlp_fwd3_kernel(
       }
       m |= swp.x16(m);
       m |= swp.x32(m);
-      mask_out[(size_t)(r0 + 16 * h + c16) * 8 + wave] = m;
+      if constexpr (!INFER) mask_out[(size_t)(r0 + 16 * h + c16) * 8 + wave] = m;
     }
     float* zb = zs + buf * FW * 2 * ZREG;
 #pragma unroll
@@ -226,12 +228,14 @@ __global__ __launch_bounds__(512) void mlp_fwd3_kernel(
                                f32x4_t{0.f, 0.f, 0.f, 0.f});
       *reinterpret_cast<f32x4_t*>(zb + (wave * 2 + h) * ZREG + 72 * g + 4 * c16) = zp;
     }
-    bf16_t* ib = img + buf * 2 * FIMG;
+    if constexpr (!INFER) {
+      bf16_t* ib = img + buf * 2 * FIMG;
 #pragma unroll
-    for (int h = 0; h < 2; ++h)
+      for (int h = 0; h < 2; ++h)
 #pragma unroll
-      for (int t = 0; t < 2; ++t)
-        *reinterpret_cast<uint2*>(ib + t * FIMG + (16 * h + c16) * FSP + 4 * g) = make_uint2(h2p[h][t][0], h2p[h][t][1]);
+        for (int t = 0; t < 2; ++t)
+          *reinterpret_cast<uint2*>(ib + t * FIMG + (16 * h + c16) * FSP + 4 * g) = make_uint2(h2p[h][t][0], h2p[h][t][1]);
+    }
   };
   // ---- softmax / CE / argmax / dz of tile k (zs buffer `buf`): lane = (row sr, class c16) ----
   auto softmax = [&](int k, int buf, int yc) __attribute__((always_inline)) {
@@ -245,6 +249,11 @@ __global__ __launch_bounds__(512) void mlp_fwd3_kernel(
     // the 16 class lanes of a row are one DPP row: max, argmax (smallest class at the max), sum
     const float mx = row16_max(zz);
     const int amx = row16_min(zz == mx && c16 < C ? c16 : (1 << 30));
+    if constexpr (INFER) {
+      if (c16 < C) slab[(size_t)(r0 + sr) * C + c16] = zz;
+      if (c16 == 0) block_correct[r0 + sr] = amx;
+      return;
+    }
     const float e = c16 < C ? __expf(zz - mx) : 0.f;
     const float se = row16_sum(e);
     // v_rcp_f32 (1 ulp) rather than the IEEE division sequence, which hipcc sinks into an
@@ -279,7 +288,7 @@ __global__ __launch_bounds__(512) void mlp_fwd3_kernel(
     // only the W0 / W1 copies): fragment f = (unit block ub = f & 15, k chunk jc = f >> 4) holds
     // W1[32 jc .. + 32][16 ub .. + 16], i.e. rows this workgroup's wave jc has in registers (W1 rows
     // 32 jc .. + 32 = its units): transposed through the (still unused) partial-logit buffer.
-    for (int f = blockIdx.x; f < 8 * (HH / 16); f += gridDim.x) {
+    for (int f = blockIdx.x; !INFER && f < 8 * (HH / 16); f += gridDim.x) {
       const int ub = f & 15, jc = f >> 4;
       if (wave == jc) {
         bf16_t* tt = reinterpret_cast<bf16_t*>(zs) + wave * 32 * 24;  // this wave's [32 j][16 u] (+ pad)
@@ -310,10 +319,10 @@ __global__ __launch_bounds__(512) void mlp_fwd3_kernel(
   auto iter = [&](int k, bool first, bool last) __attribute__((always_inline)) {
     if (k < 32) HAR_STAMP(FW, 2 + k)
     const int yc = ynext;
-    ynext = labels[tile_of(k + 1) * FRT + sr];
+    if constexpr (!INFER) ynext = labels[tile_of(k + 1) * FRT + sr];
     softmax(k, k & 1, yc);
     if (k == 4) HAR_STAMP(FW, 10)
-    if (!first) stage5((k - 1) & 1);
+    if (!INFER && !first) stage5((k - 1) & 1);
     if (k == 4) HAR_STAMP(FW, 11)
     if (!last) {
       stage23(k + 1, (k + 1) & 1);
@@ -338,6 +347,7 @@ __global__ __launch_bounds__(512) void mlp_fwd3_kernel(
     iter(nt - 1, false, true);
   }
   HAR_STAMP(FW, 34)
+  if constexpr (INFER) return;
   if (nt > 0) stage5((nt - 1) & 1);
   // ---- this workgroup's slab: dWout rows 0..15 x this wave's units, dbout; loss, #correct ----
   float* out = slab + (size_t)blockIdx.x * FWD_SLAB;
@@ -1075,6 +1085,13 @@ void launch_fwd3(const bf16_t* X, bf16_t* Wf, const float* b0, const float* b1, 
 }
 
 template <int K0>
+void launch_fwd3_infer(const bf16_t* X, bf16_t* Wf, const float* b0, const float* b1, const bf16_t* Wo,
+                       const float* bo, int B, int C, float* logits, int32_t* pred, int nwg, hipStream_t s) {
+  mlp_fwd3_kernel<K0, false, true><<<nwg, 512, FWD_LDS, s>>>(X, Wf, b0, b1, Wo, bo, nullptr, B, C, 1.f, nullptr, nullptr,
+                                                              logits, nullptr, pred, nullptr);
+}
+
+template <int K0>
 void launch_bwd3(const uint32_t* dz, const uint32_t* mask, const bf16_t* X, const bf16_t* Wf, const float* b0,
                  const bf16_t* Wo, int B, int S, float* gw1, float* gw0, float* gb0, float* gb1, int64_t stride,
                  int32_t* tick, const float* fslab, int fslab_w, int nfwd, float* gwo, float* gbo, hipStream_t s) {
@@ -1117,6 +1134,26 @@ extern "C" int har_mlp_step_fwd(const uint16_t* X, int K0, uint16_t* Wf, const f
     launch_fwd3<64>(X, Wf, b0, b1, Wo, bo, labels, B, C, scale, dz, mask, slab, block_loss, block_correct, nwg, s);
   else
     launch_fwd3<32>(X, Wf, b0, b1, Wo, bo, labels, B, C, scale, dz, mask, slab, block_loss, block_correct, nwg, s);
+  HAR_CHECK_LAUNCH();
+  return 0;
+}
+
+// Serving forward on the step's pipeline (the INFER instantiation of mlp_fwd3): X bf16 [B][K0] padded,
+// the W0 / W1 fragment copies in Wf (as the training step keeps them); logits [B][C] fp32 and the argmax
+// [B] int32 out.
+extern "C" int har_mlp_step_fwd_infer(const uint16_t* X, int K0, const uint16_t* Wf, const float* b0, const float* b1,
+                                      int H, const uint16_t* Wo, const float* bo, int B, int C, float* logits,
+                                      int32_t* pred, hipStream_t s) {
+  if (H != HH || (K0 != 32 && K0 != 64) || B <= 0 || B % 64 || C < 1 || C > NCLS || !logits || !pred) return -2;
+  if (((uintptr_t)X | (uintptr_t)Wf | (uintptr_t)Wo | (uintptr_t)b0 | (uintptr_t)b1) & 15) return -3;
+  const int nwg = har_mlp_step_grid(B);
+  bf16_t* wf = const_cast<bf16_t*>(reinterpret_cast<const bf16_t*>(Wf));  // read only in INFER
+  if (K0 == 64)
+    launch_fwd3_infer<64>(reinterpret_cast<const bf16_t*>(X), wf, b0, b1, reinterpret_cast<const bf16_t*>(Wo), bo, B, C,
+                          logits, pred, nwg, s);
+  else
+    launch_fwd3_infer<32>(reinterpret_cast<const bf16_t*>(X), wf, b0, b1, reinterpret_cast<const bf16_t*>(Wo), bo, B, C,
+                          logits, pred, nwg, s);
   HAR_CHECK_LAUNCH();
   return 0;
 }
