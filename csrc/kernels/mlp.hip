@@ -202,6 +202,27 @@ __global__ __launch_bounds__(256) void reduce_slabs_kernel(const float* __restri
     reinterpret_cast<float4*>(dst)[i] = load_grad4(nullptr, slabs, nslabs, n, i);
 }
 
+// 8 outputs per thread (one 16-byte store): thread t = (row t / (cout / 8), chunk t % (cout / 8)), so
+// consecutive threads read consecutive 32-byte runs of a row and write consecutive 16-byte runs (the
+// element-per-thread form below did an integer division per element)
+__global__ __launch_bounds__(256) void cast_pad8_kernel(const float* __restrict__ in, int rows, int cin, int ldin,
+                                                        bf16_t* __restrict__ out, int cout) {
+  const int cpr = cout / 8;
+  const int64_t n = (int64_t)rows * cpr;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n; t += (int64_t)gridDim.x * blockDim.x) {
+    const int r = (int)(t / cpr), c0 = (int)(t - (int64_t)r * cpr) * 8;
+    const float* p = in + (size_t)r * ldin;
+    uint32_t w[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int c = c0 + 2 * i;
+      const float a = c < cin ? p[c] : 0.f, b = c + 1 < cin ? p[c + 1] : 0.f;
+      w[i] = (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16);
+    }
+    *reinterpret_cast<uint4*>(out + (size_t)r * cout + c0) = make_uint4(w[0], w[1], w[2], w[3]);
+  }
+}
+
 __global__ void cast_pad_kernel(const float* __restrict__ in, int rows, int cin, int ldin,
                                 bf16_t* __restrict__ out, int cout) {
   int64_t total = (int64_t)rows * cout;
@@ -370,6 +391,14 @@ extern "C" int har_reduce_slabs(const float* slabs, int nslabs, int64_t n, float
 extern "C" int har_cast_pad_bf16(const float* in, int rows, int cin, int ldin, uint16_t* out, int cout,
                                  hipStream_t s) {
   int64_t total = (int64_t)rows * cout;
+  if (cout % 8 == 0 && (reinterpret_cast<uintptr_t>(out) & 15) == 0) {
+    const int64_t n8 = total / 8;
+    const int blocks = (int)std::min<int64_t>(8192, (n8 + 255) / 256);
+    if (blocks == 0) return 0;
+    cast_pad8_kernel<<<blocks, 256, 0, s>>>(in, rows, cin, ldin, reinterpret_cast<bf16_t*>(out), cout);
+    HAR_CHECK_LAUNCH();
+    return 0;
+  }
   int blocks = (int)std::min<int64_t>(4096, (total + 255) / 256);
   if (blocks == 0) return 0;
   cast_pad_kernel<<<blocks, 256, 0, s>>>(in, rows, cin, ldin, out, cout);
