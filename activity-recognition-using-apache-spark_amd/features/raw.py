@@ -98,8 +98,7 @@ def featurize_starts(xyz: torch.Tensor, starts: torch.Tensor, window: int, hz: f
 def _featurize_dp(ctx, xyz_host: np.ndarray, starts: np.ndarray, window: int, hz: float, device) -> torch.Tensor:
     """Rank r featurizes the windows starting in its contiguous sample shard; the last window of a
     shard may run into the next rank's samples: one halo exchange of window - 1 samples."""
-    import torch.distributed as dist
-
+    from ..parallel import comm
     from ..parallel.stream import exchange_halo, shard_lengths
 
     S = xyz_host.shape[0]
@@ -114,7 +113,7 @@ def _featurize_dp(ctx, xyz_host: np.ndarray, starts: np.ndarray, window: int, hz
     pad = torch.zeros(max(counts), f.shape[1], dtype=f.dtype, device=f.device)
     pad[: f.shape[0]] = f
     allf = torch.zeros(ctx.world_size * pad.shape[0], f.shape[1], dtype=f.dtype, device=f.device)
-    dist.all_gather_into_tensor(allf, pad, group=ctx.group)
+    comm.all_gather_into_tensor(allf, pad, group=ctx.group)
     allf = allf.view(ctx.world_size, -1, f.shape[1])
     return torch.cat([allf[r, :counts[r]] for r in range(ctx.world_size)], 0)
 

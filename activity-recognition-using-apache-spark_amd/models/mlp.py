@@ -153,10 +153,27 @@ class MLPEngine:
         self.world = world_size
         L = self.layout
         dev = self.device
-        self.P = init_params(L, seed).to(dev)
-        self.G = torch.zeros_like(self.P)
+        # Data parallel, sharded optimizer (ZeRO-1 style, the default for world > 1;
+        # HAR_MLP_SHARDED_OPT=0 keeps the all-reduce step): the flat buffers are padded to world x
+        # chunk (chunk a multiple of 64 elements: 256-byte aligned slices), rank r owns
+        # [r chunk, (r + 1) chunk) of P / m / v, the step is reduce-scatter(G) -> Adam on the owned
+        # slice -> all-gather(P) -> bf16 / fragment refresh
+        self.sharded = world_size > 1 and os.environ.get("HAR_MLP_SHARDED_OPT", "1") != "0"
+        n = L.total
+        self.chunk = -(-n // (64 * world_size)) * 64 if world_size > 1 else n
+        npad = self.chunk * world_size if world_size > 1 else n
+        self.Pfull = torch.zeros(npad, dtype=torch.float32, device=dev)
+        self.Gfull = torch.zeros(npad, dtype=torch.float32, device=dev)
+        self.P = self.Pfull[:n]
+        self.P.copy_(init_params(L, seed).to(dev))
+        self.G = self.Gfull[:n]
         self.m = torch.zeros_like(self.P)
         self.v = torch.zeros_like(self.P)
+        if self.sharded:
+            self.rank = _pg_rank(process_group)
+            self.lo = self.rank * self.chunk
+            self.n_own = max(0, min(n, self.lo + self.chunk) - self.lo)
+            self.Gsh = torch.zeros(self.chunk, dtype=torch.float32, device=dev)
         self.step_count = torch.zeros(1, dtype=torch.int32, device=dev)
         self.native = self.device.type == "cuda"
         if self.native:
@@ -510,16 +527,84 @@ class MLPEngine:
         self._grad_kernel(self.GR_ADAM)
 
     def collective_stats(self):
-        """Collectives of one DP training step: ONE flat all-reduce of the whole fp32 gradient
-        (~0.34 MB for 43-256-256-6: latency-bound on xGMI, so no bucketing)."""
+        """Collectives of one DP training step and the bytes each rank hands to them: the sharded
+        step (default) is ONE reduce-scatter of the fp32 gradient + ONE all-gather of the fp32
+        parameters (world x chunk elements each, ~0.34 MB for 43-256-256-6: latency-bound on xGMI,
+        so one flat message each, no bucketing); HAR_MLP_SHARDED_OPT=0: ONE all-reduce of G."""
         if self.world <= 1:
             return {"all_reduce": 0, "bytes": 0}
+        if self.sharded:
+            nb = int(self.Gfull.numel() * 4)
+            return {"all_reduce": 0, "reduce_scatter": 1, "all_gather": 1, "bytes": 2 * nb,
+                    "reduce_scatter_bytes": nb, "all_gather_bytes": nb, "world": self.world}
         return {"all_reduce": 1, "bytes": int(self.G.numel() * 4), "world": self.world}
 
     def allreduce_grads(self):
         if self.world > 1:
-            import torch.distributed as dist
-            dist.all_reduce(self.G, group=self.pg)
+            from ..parallel import comm
+            comm.all_reduce(self.G, group=self.pg)
+
+    def sharded_update(self):
+        """DP step after G holds this rank's gradient (the slab reduction, GR_STORE): reduce-scatter
+        -> Adam on the owned slice of (P, m, v) -> all-gather of P -> Pb / fragment copies.  Every
+        rank applies Adam to 1/N of the parameters; each element's update is the one the
+        all-reduce step computes (same summed gradient, same Adam arithmetic)."""
+        self.comm_phase()
+        self.apply_phase()
+        self.gather_phase()
+
+    def comm_phase(self):
+        """The gradient collective of the DP step: reduce-scatter (sharded) or all-reduce of G."""
+        if self.world <= 1:
+            return
+        if not self.sharded:
+            return self.allreduce_grads()
+        from ..parallel import comm
+
+        comm.reduce_scatter_tensor(self.Gsh, self.Gfull, group=self.pg)
+
+    def _adam_shard(self):
+        lo, n = self.lo, self.n_own
+        if n <= 0:
+            if not self.native:
+                self.t_step += 1
+            return
+        if self.native:
+            b1, b2 = self.betas
+            _native.kernels().grad_reduce_adam(
+                [], [], [], [], [], n, self.Gsh.data_ptr(), self.P.data_ptr() + 4 * lo,
+                self.m.data_ptr() + 4 * lo, self.v.data_ptr() + 4 * lo, self.Pb.data_ptr() + 2 * lo,
+                float(self.lr), b1, b2, float(self.eps), float(self.wd), self.step_count.data_ptr(), 0,
+                self.GR_ADAM, _native.stream_ptr(), 0, 0, 0, 0, 0)
+        else:
+            self._adam_torch(sl=slice(lo, lo + n), g=self.Gsh[:n])
+
+    def gather_phase(self):
+        """Sharded DP step, last part: all-gather of the owned fp32 parameter slices (every rank
+        then holds the identical P) and the bf16 / fragment copies rebuilt from it."""
+        if not (self.world > 1 and self.sharded):
+            return
+        from ..parallel import comm
+
+        comm.all_gather_into_tensor(self.Pfull, self.Pfull[self.rank * self.chunk:(self.rank + 1) * self.chunk],
+                                    group=self.pg)
+        if self.native:
+            self.Pb.copy_(self.P)  # round-to-nearest-even, as the Adam kernel's own bf16 copy
+            self._pack_frag()
+
+    def _gather_moments(self):
+        """Sharded optimizer: every rank's owned slices of m / v into the full vectors (a checkpoint
+        of the moments; two all-gathers)."""
+        from ..parallel import comm
+
+        out = []
+        for t in (self.m, self.v):
+            full = torch.zeros_like(self.Pfull)
+            full[:t.numel()] = t
+            comm.all_gather_into_tensor(full, full[self.rank * self.chunk:(self.rank + 1) * self.chunk].clone(),
+                                        group=self.pg)
+            out.append(full[:t.numel()])
+        return out
 
     def grad_phase(self, Xb: torch.Tensor, yb: torch.Tensor, global_batch: int):
         """DP step, part 1 (graph-capturable): fwd + bwd + deterministic slab reduction into G."""
@@ -536,7 +621,10 @@ class MLPEngine:
 
     def apply_phase(self):
         """DP step, part 3 (graph-capturable): Adam from the all-reduced G (part 2 is the RCCL
-        all-reduce, issued eagerly between the two graph replays)."""
+        collective, ``comm_phase``, issued eagerly between the two graph replays); sharded: Adam on
+        this rank's slice, then ``gather_phase``."""
+        if self.world > 1 and self.sharded:
+            return self._adam_shard()
         if not self.native:
             return self._adam_torch()
         self.optimizer_step_native()
@@ -587,8 +675,11 @@ class MLPEngine:
             s = _native.stream_ptr()
             if self.world > 1:
                 plan.run(Xb.data_ptr(), yb.data_ptr(), B, 1.0 / global_batch, 2, s)
-                self.allreduce_grads()
-                plan.run(0, 0, B, 0.0, 4, s)
+                if self.sharded:
+                    self.sharded_update()
+                else:
+                    self.allreduce_grads()
+                    plan.run(0, 0, B, 0.0, 4, s)
             else:
                 plan.run(Xb.data_ptr(), yb.data_ptr(), B, 1.0 / global_batch, 1, s)
             return
@@ -596,17 +687,22 @@ class MLPEngine:
             self.forward_backward_native(Xb, yb, 1.0 / global_batch)
             if self.world > 1:
                 self.reduce_grads_native()
-                self.allreduce_grads()
-                self.optimizer_step_native()
+                if self.sharded:
+                    self.sharded_update()
+                else:
+                    self.allreduce_grads()
+                    self.optimizer_step_native()
             else:
                 self._grad_kernel(self.GR_REDUCE | self.GR_ADAM, tick=not self.last_bwd)
         else:
             self.train_step_torch(Xb, yb, global_batch)
 
     def state_tensors(self):
-        """Everything needed to resume training bit-for-bit."""
+        """Everything needed to resume training bit-for-bit (sharded optimizer: the moments are
+        gathered from their owners first — every rank calls this)."""
         step = self.step_count.clone() if self.native else torch.tensor([self.t_step], dtype=torch.int32)
-        return {"P": self.P, "m": self.m, "v": self.v, "step": step}
+        m, v = self._gather_moments() if self.sharded else (self.m, self.v)
+        return {"P": self.P, "m": m, "v": v, "step": step}
 
     def load_state(self, st):
         self.P.copy_(st["P"].to(self.P.device))
@@ -645,6 +741,9 @@ class MLPEngine:
     def train_step_torch(self, X: torch.Tensor, y: torch.Tensor, global_batch: int):
         """fp32 reference step (CPU path / oracle); same Adam math as the kernel."""
         self._grad_torch(X, y, global_batch)
+        if self.sharded:
+            self.sharded_update()
+            return
         self.allreduce_grads()
         self._adam_torch()
 
@@ -656,14 +755,16 @@ class MLPEngine:
         self.G.copy_(g)
         self.last_loss = float(loss.detach()) * global_batch / X.shape[0]
 
-    def _adam_torch(self):
+    def _adam_torch(self, sl: slice = slice(None), g: Optional[torch.Tensor] = None):
         self.t_step += 1
         b1, b2 = self.betas
+        G = self.G[sl] if g is None else g
+        m, v, P = self.m[sl], self.v[sl], self.P[sl]
         with torch.no_grad():
-            self.m.mul_(b1).add_((1 - b1) * self.G)
-            self.v.mul_(b2).add_((1 - b2) * self.G * self.G)
-            upd = (self.m / (1 - b1 ** self.t_step)) / ((self.v / (1 - b2 ** self.t_step)).sqrt() + self.eps)
-            self.P.sub_(self.lr * (upd + self.wd * self.P))
+            m.mul_(b1).add_((1 - b1) * G)
+            v.mul_(b2).add_((1 - b2) * G * G)
+            upd = (m / (1 - b1 ** self.t_step)) / ((v / (1 - b2 ** self.t_step)).sqrt() + self.eps)
+            P.sub_(self.lr * (upd + self.wd * P))
 
     # ---------------------------------------------------------------- inference
     def infer_fused(self, Xb: torch.Tensor):
@@ -738,6 +839,12 @@ class MLPEngine:
         Xp[:, : X.shape[1]] = X
         with torch.no_grad():
             return self.torch_forward(self.P.to(X.device), Xp)
+
+
+def _pg_rank(group) -> int:
+    import torch.distributed as dist
+
+    return dist.get_rank(group) if dist.is_initialized() else 0
 
 
 def pad_input_bf16(X: torch.Tensor, in_pad: int) -> torch.Tensor:
@@ -843,8 +950,10 @@ class MultilayerPerceptronClassifier(Estimator, ClassifierParams):
         K = int(num_classes) if num_classes else int(y.max()) + 1
         if world_size > 1 and not num_classes:
             import torch.distributed as dist
+
+            from ..parallel import comm
             kt = torch.tensor([K], device=dev)
-            dist.all_reduce(kt, op=dist.ReduceOp.MAX, group=process_group)
+            comm.all_reduce(kt, op=dist.ReduceOp.MAX, group=process_group)
             K = int(kt.item())
         layers = self.layers or [X.shape[1], 128, 128, K]
         if layers[0] != X.shape[1]:
@@ -855,9 +964,9 @@ class MultilayerPerceptronClassifier(Estimator, ClassifierParams):
             s1 = X.double().sum(0)
             s2 = (X.double() ** 2).sum(0)
             if world_size > 1:
-                import torch.distributed as dist
+                from ..parallel import comm
                 buf = torch.cat([n, s1, s2])
-                dist.all_reduce(buf, group=process_group)
+                comm.all_reduce(buf, group=process_group)
                 n, s1, s2 = buf[:1], buf[1:1 + X.shape[1]], buf[1 + X.shape[1]:]
             mean = (s1 / n).float()
             var = (s2 / n - (s1 / n) ** 2).clamp_min(0).float()
@@ -866,8 +975,10 @@ class MultilayerPerceptronClassifier(Estimator, ClassifierParams):
         B = min(self.blockSize, X.shape[0])
         if world_size > 1:  # every rank must run the same number of steps (collectives!)
             import torch.distributed as dist
+
+            from ..parallel import comm
             bt = torch.tensor([B], device=dev)
-            dist.all_reduce(bt, op=dist.ReduceOp.MIN, group=process_group)
+            comm.all_reduce(bt, op=dist.ReduceOp.MIN, group=process_group)
             B = int(bt.item())
         eng = MLPEngine(layers, B, dev, lr=self.stepSize, seed=self.seed, process_group=process_group,
                         world_size=world_size, weight_decay=self.weightDecay)
@@ -878,8 +989,10 @@ class MultilayerPerceptronClassifier(Estimator, ClassifierParams):
         steps_per_epoch = max(1, N // B)
         if world_size > 1:
             import torch.distributed as dist
+
+            from ..parallel import comm
             st = torch.tensor([steps_per_epoch], device=dev)
-            dist.all_reduce(st, op=dist.ReduceOp.MIN, group=process_group)
+            comm.all_reduce(st, op=dist.ReduceOp.MIN, group=process_group)
             steps_per_epoch = int(st.item())
         ckpt = None
         start_epoch, start_step = 0, 0

@@ -30,9 +30,9 @@ from typing import Optional
 
 import numpy as np
 import torch
-import torch.distributed as dist
 
 from ..ops import tree as T
+from . import comm
 from .dist import DistContext, shard_range
 
 
@@ -41,12 +41,7 @@ def allreduce_sum(ctx: Optional[DistContext]):
         return None
 
     def _ar(t: torch.Tensor):
-        if t.is_cuda == (ctx.backend == "nccl"):
-            dist.all_reduce(t, group=ctx.group)
-        else:  # host tensor under RCCL, or a device tensor under gloo (GPU tests): stage it
-            d = t.to(ctx.device if ctx.backend == "nccl" else "cpu")
-            dist.all_reduce(d, group=ctx.group)
-            t.copy_(d)
+        comm.all_reduce(t, group=ctx.group)  # (staged when the placement is not the backend's)
     return _ar
 
 
@@ -78,7 +73,7 @@ def global_thresholds(X_shard: torch.Tensor, max_bins: int, ctx: DistContext, sa
         # one all-gather of a [1] tensor per rank, ONE host read of all P sizes
         t = torch.tensor([v], dtype=torch.int64, device=X.device)
         out = torch.empty(P, dtype=torch.int64, device=X.device)
-        dist.all_gather_into_tensor(out, t, group=ctx.group)
+        comm.all_gather_into_tensor(out, t, group=ctx.group)
         return out.tolist()
 
     shard_rows = gather_sizes(X.shape[0])
@@ -89,7 +84,7 @@ def global_thresholds(X_shard: torch.Tensor, max_bins: int, ctx: DistContext, sa
     buf = torch.zeros(max(counts), X.shape[1], dtype=X.dtype, device=X.device)
     buf[:take.shape[0]] = take
     parts = torch.empty(P * buf.shape[0], X.shape[1], dtype=X.dtype, device=X.device)
-    dist.all_gather_into_tensor(parts, buf, group=ctx.group)
+    comm.all_gather_into_tensor(parts, buf, group=ctx.group)
     parts = parts.view(P, buf.shape[0], X.shape[1])
     sample = torch.cat([parts[q, :c] for q, c in enumerate(counts)], 0)
     # already sampled: no second draw (n_total <= sample_rows disables it)
@@ -136,7 +131,7 @@ class NodeOwner:
         src[:A].copy_(flat)
         src[A:].zero_()  # only the pad rows of the last owner's slice
         out = self._buf("rs_out", S * w, flat.dtype, dev).view(S, w)
-        dist.reduce_scatter_tensor(out, src, group=self.ctx.group)
+        comm.reduce_scatter_tensor(out, src, group=self.ctx.group)
         self.stats["reduce_scatter"] += 1
         self.stats["bytes"] += src.numel() * src.element_size()
         return out.to(hist.device).view(S, *hist.shape[1:]), a0, a1
@@ -156,7 +151,7 @@ class NodeOwner:
         dt = torch.float16 if narrow else store.dtype
         src = store if (store.device == torch.device(dev) and dt == store.dtype) else store.to(dev, dt)
         out = self._buf("rs_out16" if narrow else "rs_out", S * w, dt, dev).view(S, w)
-        dist.reduce_scatter_tensor(out, src, group=self.ctx.group)
+        comm.reduce_scatter_tensor(out, src, group=self.ctx.group)
         self.stats["reduce_scatter"] += 1
         self.stats["bytes"] += src.numel() * src.element_size()
         return out.to(store.device, torch.float32), a0, a1
@@ -172,7 +167,7 @@ class NodeOwner:
         dev = self._dev() or device
         src = send if send.device == torch.device(dev) else send.to(dev)
         out = self._buf("pk_out", wmax, torch.int32, dev)
-        dist.reduce_scatter_tensor(out, src, group=self.ctx.group)
+        comm.reduce_scatter_tensor(out, src, group=self.ctx.group)
         self.stats["reduce_scatter"] += 1
         self.stats["bytes"] += src.numel() * src.element_size()
         return out.to(device)
@@ -190,7 +185,7 @@ class NodeOwner:
         buf[: local.shape[0]].copy_(local.reshape(local.shape[0], w))
         buf[local.shape[0]:].zero_()
         out = self._buf("ag_out", P * S * w, local.dtype, dev).view(P, S, w)
-        dist.all_gather_into_tensor(out.view(P * S, w), buf, group=self.ctx.group)
+        comm.all_gather_into_tensor(out.view(P * S, w), buf, group=self.ctx.group)
         self.stats["all_gather"] += 1
         self.stats["bytes"] += out.numel() * out.element_size()
         full = torch.cat([out[q, :sizes[q]] for q in range(P)], 0)
@@ -208,7 +203,7 @@ class NodeOwner:
         buf[: local.shape[0]].copy_(local.reshape(local.shape[0], w))
         buf[local.shape[0]:].zero_()
         out = self._buf("ag_out", P * S * w, local.dtype, dev).view(P * S, w)
-        dist.all_gather_into_tensor(out, buf, group=self.ctx.group)
+        comm.all_gather_into_tensor(out, buf, group=self.ctx.group)
         self.stats["all_gather"] += 1
         self.stats["bytes"] += out.numel() * out.element_size()
         return out[:A].view((A,) + inner).to(local.device).clone()
@@ -265,7 +260,7 @@ def fit_forest_tree_parallel(estimator, X, y, num_classes: int, ctx: DistContext
     if Tr:
         buf[:Tr] = torch.cat(cols, dim=1)
     out = torch.empty(P * S, w, dtype=torch.int32, device=dev)
-    dist.all_gather_into_tensor(out, buf, group=ctx.group)
+    comm.all_gather_into_tensor(out, buf, group=ctx.group)
     if stats is not None:
         stats["all_gather"] = stats.get("all_gather", 0) + 1
         stats["bytes"] = stats.get("bytes", 0) + out.numel() * 4

@@ -86,7 +86,7 @@ def barrier(ctx: DistContext):
         if ctx.backend == "nccl":
             dist.barrier(device_ids=[ctx.device.index])
         else:
-            dist.barrier()
+            dist.barrier(group=ctx.group)
 
 
 def sync(device):
@@ -97,8 +97,10 @@ def sync(device):
 def _reduce_scalar(ctx: DistContext, x: float, op) -> float:
     if not ctx.is_distributed:
         return x
-    t = torch.tensor([x], dtype=torch.float64, device=ctx.device)
-    dist.all_reduce(t, op=op, group=ctx.group)
+    from . import comm
+
+    t = torch.tensor([x], dtype=torch.float64)
+    comm.all_reduce(t, op=op, group=ctx.group)  # (staged to the device under RCCL)
     return float(t.item())
 
 

@@ -18,9 +18,9 @@ from __future__ import annotations
 from typing import List, Optional, Tuple
 
 import torch
-import torch.distributed as dist
 
 from ..features.window import WindowFeaturizer, window_count
+from . import comm
 from .dist import DistContext
 
 
@@ -30,7 +30,7 @@ def shard_lengths(ctx: DistContext, local_len: int, device) -> List[int]:
         return [local_len]
     t = torch.tensor([local_len], dtype=torch.long, device=device)
     allv = torch.zeros(ctx.world_size, dtype=torch.long, device=device)
-    dist.all_gather_into_tensor(allv, t, group=ctx.group)
+    comm.all_gather_into_tensor(allv, t, group=ctx.group)
     return [int(v) for v in allv.cpu().tolist()]
 
 
@@ -54,15 +54,14 @@ def exchange_halo(ctx: DistContext, local: torch.Tensor, halo: int, lens: Option
     if short:
         raise ValueError(f"shard(s) of rank(s) {short} ({[lens[r] for r in short]} samples) are shorter than "
                          f"the halo ({halo} samples)")
-    ops = []
+    sends, recvs = [], []
     recv = None
     if ctx.rank > 0:
-        ops.append(dist.P2POp(dist.isend, local[:halo].contiguous(), ctx.rank - 1, group=ctx.group))
+        sends.append((local[:halo].contiguous(), ctx.rank - 1))
     if ctx.rank < ctx.world_size - 1:
         recv = local.new_empty(halo, A)
-        ops.append(dist.P2POp(dist.irecv, recv, ctx.rank + 1, group=ctx.group))
-    for req in dist.batch_isend_irecv(ops):
-        req.wait()
+        recvs.append((recv, ctx.rank + 1))
+    comm.send_recv(sends, recvs, group=ctx.group)
     return recv if recv is not None else local.new_zeros(0, A)
 
 

@@ -173,8 +173,9 @@ def bench_mlp(args, ctx):
 
         def run(i):
             gA[i % nb].replay()
-            eng.allreduce_grads()
+            eng.comm_phase()
             gB.replay()
+            eng.gather_phase()
     else:
         run = step
     # the untimed WISDM accuracy run (a separate engine) goes first: the timed steps then start on a
@@ -203,44 +204,42 @@ def bench_mlp(args, ctx):
 
 def mlp_phase_times(ctx, eng, Xin, y32, B, nb, global_batch, n=50):
     """Per-phase time of the DP step, measured AFTER the timed loop on n extra (untimed) steps run
-    as the three phases of the N > 1 step: compute (forward + backward + slab reduction into the
-    flat fp32 gradient G), the RCCL all-reduce of G, Adam.  Device time from HIP events around each
-    phase on the compute stream (host clock on the CPU path); mean per step, max over ranks.  At
-    N = 1 the all-reduce is absent and the N = 1 step fuses Adam into the reduction kernel, so
-    compute + adam there is the split form of the timed step (one extra launch)."""
+    as the phases of the N > 1 step: compute (forward + backward + slab reduction into the flat fp32
+    gradient G), the gradient collective (``allreduce``: the RCCL reduce-scatter of G under the
+    sharded optimizer, the all-reduce otherwise), Adam (on this rank's slice when sharded), and
+    ``all_gather`` (sharded: the all-gather of P + the bf16 / fragment refresh).  Device time from
+    HIP events around each phase on the compute stream (host clock on the CPU path); mean per step,
+    max over ranks.  At N = 1 the collectives are absent and the N = 1 step fuses Adam into the
+    reduction kernel, so compute + adam there is the split form of the timed step (one extra launch)."""
     from har.parallel import dist as hdist
 
     cuda = Xin.is_cuda
-    tot = {"compute": 0.0, "allreduce": 0.0, "adam": 0.0}
+    tot = {"compute": 0.0, "allreduce": 0.0, "adam": 0.0, "all_gather": 0.0}
+    phases = (lambda xb, yb: eng.grad_phase(xb, yb, global_batch), lambda xb, yb: eng.comm_phase(),
+              lambda xb, yb: eng.apply_phase(), lambda xb, yb: eng.gather_phase())
     if cuda:
-        ev = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(n)]
+        ev = [[torch.cuda.Event(enable_timing=True) for _ in range(5)] for _ in range(n)]
     for i in range(n):
         j = i % nb
         xb, yb = Xin[j * B:(j + 1) * B], y32[j * B:(j + 1) * B]
         if cuda:
             e = ev[i]
             e[0].record()
-            eng.grad_phase(xb, yb, global_batch)
-            e[1].record()
-            eng.allreduce_grads()
-            e[2].record()
-            eng.apply_phase()
-            e[3].record()
+            for q, ph in enumerate(phases):
+                ph(xb, yb)
+                e[q + 1].record()
         else:
-            t0 = time.perf_counter()
-            eng.grad_phase(xb, yb, global_batch)
-            t1 = time.perf_counter()
-            eng.allreduce_grads()
-            t2 = time.perf_counter()
-            eng.apply_phase()
-            t3 = time.perf_counter()
-            for k, dt in zip(tot, (t1 - t0, t2 - t1, t3 - t2)):
-                tot[k] += dt * 1e3
+            t = [time.perf_counter()]
+            for ph in phases:
+                ph(xb, yb)
+                t.append(time.perf_counter())
+            for q, k in enumerate(tot):
+                tot[k] += (t[q + 1] - t[q]) * 1e3
     if cuda:
         torch.cuda.synchronize()
         for e in ev:
-            for k, (a, b) in zip(tot, ((0, 1), (1, 2), (2, 3))):
-                tot[k] += e[a].elapsed_time(e[b])
+            for q, k in enumerate(tot):
+                tot[k] += e[q].elapsed_time(e[q + 1])
     out = {k: hdist.max_over_ranks(ctx, v / n) for k, v in tot.items()}
     out.update(steps=n, clock="HIP events" if cuda else "host", world=ctx.world_size)
     return out
@@ -458,8 +457,8 @@ def bench_stream(args, ctx):
     ns = min(nw_local, 16384)
     st = column_stats(torch.nan_to_num(window_features(stream[:ns * W], W, W, spec.hz), nan=-1.0))[:3].contiguous()
     if world > 1:
-        import torch.distributed as tdist
-        tdist.all_reduce(st, group=ctx.group)
+        from har.parallel import comm
+        comm.all_reduce(st, group=ctx.group)
     mean = (st[1] / st[0]).float()
     var = (st[2] / st[0]).float() - mean * mean
     inv_std = torch.where(var > 1e-12, var.clamp_min(1e-12).rsqrt(), torch.ones_like(var))
@@ -545,6 +544,7 @@ def _stream_full_pass(args, ctx, spec, stream, labels, eng, mean, inv_std, sampl
 
     from har.features.window import WindowFeaturizer, n_features, window_features, window_features_mlp
     from har.models.mlp import pad_input_bf16
+    from har.parallel import comm
     from har.parallel.stream import shard_offsets, sharded_window_features
 
     dev, world, B, W = ctx.device, ctx.world_size, args.batch, spec.window
@@ -562,7 +562,7 @@ def _stream_full_pass(args, ctx, spec, stream, labels, eng, mean, inv_std, sampl
     nbt = torch.tensor([X0.shape[0] // B], device=dev)
     del X0
     if world > 1:
-        tdist.all_reduce(nbt, op=tdist.ReduceOp.MIN, group=ctx.group)
+        comm.all_reduce(nbt, op=tdist.ReduceOp.MIN, group=ctx.group)
     nb = int(nbt.item())  # MLP steps per pass (the same on every rank)
     gb = B * world
 

@@ -98,6 +98,7 @@ def _worker(rank, world, port, out_dir, what):
     else:
         from har.models.mlp import MLPEngine
 
+        os.environ["HAR_MLP_SHARDED_OPT"] = "0" if what == "mlp_ar" else "1"
         per = 128 // world
         eng = MLPEngine([12, 32, 4], per, "cpu", lr=1e-2, seed=1, process_group=ctx.group, world_size=ctx.world_size)
         lo = rank * per
@@ -162,6 +163,24 @@ def test_dp_mlp_equals_single(world):
     for s in range(3):
         eng.train_step(X[s * 128:(s + 1) * 128], y[s * 128:(s + 1) * 128], 128)
     torch.testing.assert_close(outs[0], eng.P, rtol=1e-4, atol=1e-5)
+
+
+@pytest.mark.parametrize("world", [2, 8])
+def test_dp_mlp_sharded_optimizer_matches_allreduce(world):
+    """Sharded optimizer (reduce-scatter of G, Adam on the owned 1/N slice, all-gather of P) vs the
+    all-reduce step: every rank bit-identical in both, and the two steps equal — bitwise at world 2
+    (a two-rank sum is one commutative add in either collective), to rounding at world 8 (the
+    reduce-scatter and the all-reduce may pair the rank partials in different orders)."""
+    sh = _run("mlp", world)
+    ar = _run("mlp_ar", world)
+    for o in sh[1:]:
+        assert torch.equal(sh[0], o)
+    for o in ar[1:]:
+        assert torch.equal(ar[0], o)
+    if world == 2:
+        assert torch.equal(sh[0], ar[0])
+    else:
+        torch.testing.assert_close(sh[0], ar[0], rtol=1e-5, atol=1e-7)
 
 
 @pytest.mark.parametrize("world", [2, 8])

@@ -207,43 +207,6 @@ def test_dictionary_encode_device(cuda, wisdm_csv):
     assert int(codes.min()) == 0 and codes.device.type == "cuda"
 
 
-def test_mlp_dp_step_equals_single_gpu_step(cuda):
-    """The DP step (slab reduction -> G, RCCL all-reduce of G on a 1-rank group, Adam from G)
-    gives bitwise the parameters, moments and step counter of the N = 1 step (the same reduction
-    kernel with Adam fused in): N > 1 runs the N = 1 kernels plus one collective."""
-    import socket
-
-    import torch.distributed as dist
-
-    from har.models.mlp import MLPEngine, pad_input_bf16
-
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
-    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1, device_id=cuda)
-    try:
-        B = 4096
-        layers = [43, 256, 256, 6]
-        a = MLPEngine(layers, B, cuda, lr=1e-3, seed=4)
-        b = MLPEngine(layers, B, cuda, lr=1e-3, seed=4, process_group=dist.group.WORLD, world_size=1)
-        b.world = 2  # take the DP branch of train_step on the 1-rank group (the all-reduce is an identity)
-        g = torch.Generator(device=cuda).manual_seed(2)
-        for _ in range(3):
-            X = pad_input_bf16(torch.randn(B, 43, device=cuda, generator=g), a.layout.in_pad)
-            y = torch.randint(0, 6, (B,), device=cuda, generator=g).to(torch.int32)
-            a.train_step(X, y, B)
-            b.train_step(X, y, B)
-        torch.cuda.synchronize()
-        assert a.last_bwd and b.last_bwd
-        assert torch.equal(a.P, b.P) and torch.equal(a.m, b.m) and torch.equal(a.v, b.v)
-        assert torch.equal(a.Pb, b.Pb) and torch.equal(a.step_count, b.step_count)
-        assert int(b.step_count[0]) == 3
-        assert b.collective_stats()["all_reduce"] == 1
-    finally:
-        dist.destroy_process_group()
-
-
 @pytest.mark.parametrize("F,m", [(165, 13), (3100, 56), (43, 7), (20, 20)])
 def test_feature_subsets_device_matches_host(cuda, F, m):
     """tree_level.hip Floyd sampler == har.ops.rng.feature_subsets (the CPU oracle), bit for bit."""
