@@ -118,6 +118,10 @@ def batched_metrics(metric: str, label: torch.Tensor, pred: torch.Tensor, mask: 
     B, N = pred.shape
     y = label.to(pred.device).long().view(1, N)
     w = mask.to(torch.float64)
+    if metric not in ("areaUnderROC", "areaUnderPR", "rmse", "mse", "r2", "mae", "var") and N:
+        lo, hi = torch.stack([y.min(), y.max()]).tolist()
+        if lo < 0 or hi >= num_classes:  # as the single-model confusion matrix (one_hot raises there)
+            raise ValueError(f"labels out of range [0, {num_classes}): min {lo}, max {hi}")
     if metric in ("areaUnderROC", "areaUnderPR") and pred.is_cuda:
         sc = raw[:, :, 1] if raw.shape[-1] > 1 else raw.reshape(B, N)
         auroc, aupr = mops.roc_pr_auc_batched(sc, label, mask.bool())
@@ -153,7 +157,9 @@ def batched_metrics(metric: str, label: torch.Tensor, pred: torch.Tensor, mask: 
             out = torch.where(ss_tot > 0, 1.0 - se / ss_tot.clamp_min(1e-300), torch.full_like(se, float("nan")))
         return out.cpu().numpy()
     K = num_classes
-    if pred.is_cuda and K * K <= 4096:
+    # the batched kernel counts rows (0/1 masks: CrossValidator folds); fractional row weights take
+    # the weighted einsum below, as on the CPU
+    if pred.is_cuda and K * K <= 4096 and bool(((mask == 0) | (mask == 1)).all()):
         cm = mops.confusion_matrix_batched(y.view(N), pred.long().clamp(0, K - 1), mask.bool(), K).double()
     else:
         Y1 = torch.nn.functional.one_hot(y.view(N), K).double()                  # [N, K]

@@ -22,8 +22,10 @@ level the rows of all active (tree, node) pairs are grouped on the device, one
 fused HIP kernel builds the LDS histograms and picks every node's best split
 (``har_tree_hist_split``), and a vectorized partition step moves rows to the
 children.  Bootstrap weights are Philox(seed, tree, global row) so forests are
-identical for any sharding.  In data-parallel mode (``parallel.forest``) the
-per-rank histograms are all-reduced before split selection.
+identical for any sharding.  In data-parallel mode (``parallel.data_parallel``:
+``fit_forest_dp`` / ``NodeOwner``) the per-rank histograms are reduce-scattered by node
+owner (packed integer wire format) or all-reduced before split selection;
+``fit_forest_tree_parallel`` grows disjoint tree slices per rank instead.
 """
 from __future__ import annotations
 
@@ -398,7 +400,10 @@ def _levels_device_frontier(b: "ForestBuilder", y32, W, N: int, F: int, m: int, 
             res = T.hist_split_planned_dp(b.bins, b.nbins, y32, rows, row_w, starts, counts, feats, K, b.max_bins,
                                           b.min_inst, b.min_gain, b.impurity, rows_bound=Tn * N, a_dev=a_dev,
                                           allreduce=None if b.owner is not None else b.allreduce, owner=b.owner,
-                                          bins_rm=bins_rm, max_weight=max_w if exact else -1.0, node_cc=node_cc)
+                                          bins_rm=bins_rm,
+                                          # fp16 transport only for integer counts (exact below 2048)
+                                          max_weight=max_w if exact and getattr(b, "int_weights", False) else -1.0,
+                                          node_cc=node_cc)
         elif planned:
             # one device: work items by rows (big nodes chunked), no host sync (ops/tree.py)
             res = T.hist_split_planned(b.bins, b.nbins, y32, rows, row_w, starts, counts, feats, K, b.max_bins,
@@ -544,12 +549,17 @@ def _enqueue_fit(b: "ForestBuilder", bufs: dict, y32, rw, row_offset: int, N: in
                                 y32.data_ptr(), K, bufs["W"].data_ptr(), bufs["node_of"].data_ptr(),
                                 bufs["stats"].data_ptr(), maxn * K, bufs["bad"].data_ptr(), _native.stream_ptr())
     if b.allreduce is not None:
-        root = bufs["stats"][:, 0].contiguous()
-        b.allreduce(root)
-        bufs["stats"][:, 0] = root
         # integer row weights (bootstrap counts x 0/1 folds): histogram counts are integers, so the DP
-        # levels may ship them as packed integer fields (ops.tree.dp_wire_plan)
-        b.int_weights = rw is None or bool(torch.equal(rw, torch.round(rw)))
+        # levels may ship them as packed integer fields (ops.tree.dp_wire_plan) or as fp16.  Every rank
+        # must take the SAME wire path (mismatched collectives hang or corrupt the sums), so the
+        # shard-local "some weight is fractional" flag rides in the root-count all-reduce: integer
+        # only when no rank has a fractional weight
+        nonint = (torch.zeros(1, device=y32.device) if rw is None
+                  else (rw != torch.round(rw)).any().float().reshape(1))
+        root = torch.cat([bufs["stats"][:, 0].reshape(-1), nonint])
+        b.allreduce(root)
+        bufs["stats"][:, 0] = root[:-1].view(Tn, K)
+        b.int_weights = bool(root[-1].item() == 0)
     return _levels_device_frontier(b, y32, bufs["W"], N, F, m, maxn, bufs["stats"], bufs["feature"], bufs["thresh"],
                                    bufs["left"], bufs["right"], bufs["gains"], bufs["node_of"], n_all=n_all)
 

@@ -234,7 +234,8 @@ def _arena(specs, dev, into: dict) -> torch.Tensor:
     return buf
 
 
-# how the last native solve ran: 1 = one persistent cooperative launch, 0 = the launch sequence (tests)
+# how the last native solve ran: 1 = one persistent cooperative launch, 0 = the launch sequence, 3 = the
+# persistent launch timed out in a grid barrier and the fit was rerun as the sequence (tests)
 LAST_SOLVE_MODE = -1
 
 
@@ -386,6 +387,20 @@ class DeviceLogregSolver:
             # (logreg_solve_persistent_kernel, bitwise the same; measured slower); 1 = persistent ran
             global LAST_SOLVE_MODE
             self.solve_mode = LAST_SOLVE_MODE = mod.logreg_solve(plan, self.max_iter, self.m, s)
+            if self.solve_mode == 2:
+                # a grid barrier of the persistent solve timed out (its blocks went on unsynchronized):
+                # the results are garbage — rerun the whole fit as the launch sequence, loudly
+                import warnings
+
+                warnings.warn("persistent LR solve: grid barrier timed out; rerunning as the launch sequence")
+                self.reset()
+                self.x.copy_(x0.reshape(self.B, self.D))
+                old = mod.logreg_set_persistent(0)
+                try:
+                    mod.logreg_solve(plan, self.max_iter, self.m, s)
+                finally:
+                    mod.logreg_set_persistent(old)
+                self.solve_mode = LAST_SOLVE_MODE = 3  # 3 = timed out, rerun as the sequence
             self.n_evals += 1 + self.max_iter
             return self.x, self.fobj, self.iters
         phase(1, init=1)
@@ -442,13 +457,25 @@ def logreg_margins_native(hm, W_models: torch.Tensor, K: int, n_models: int) -> 
 # kernel of the fit still runs; only the host-side construction (~0.15 ms of Python per fit, the GPU
 # idle meanwhile) is skipped.  Entries hold the matrix and labels they were built for (identity
 # checked, so a freed tensor's reused address can never alias a stale entry).
+# Bounded twice: at most SOLVER_CACHE_MAX entries AND at most HAR_LR_CACHE_MB (default 1024) MB of
+# device memory held by them (arena + design + per-fit inputs; least recently used evicted first);
+# main.run / the reference suite clear it when they finish, so tables a caller has dropped do not
+# stay resident for the life of the process.
 SOLVER_CACHE_MAX = 4
+SOLVER_CACHE_MAX_BYTES = int(os.environ.get("HAR_LR_CACHE_MB", "1024")) << 20
 _SOLVER_CACHE: "dict" = {}
+
+
+def _nbytes(*ts) -> int:
+    return sum(t.numel() * t.element_size() for t in ts if isinstance(t, torch.Tensor))
 
 
 class SolverCacheEntry:
     def __init__(self, hm, y, design, solver, bufs):
         self.hm, self.y, self.design, self.solver, self.bufs = hm, y, design, solver, bufs
+        d = design
+        self.nbytes = (_nbytes(solver.arena, getattr(solver, "R", None), d.rw, d.y32, d.csc_rows, d.csc_off)
+                       + _nbytes(*[b for b in bufs if b is not None]))
 
 
 def solver_cache_get(key, hm, y) -> Optional[SolverCacheEntry]:
@@ -464,9 +491,16 @@ def solver_cache_get(key, hm, y) -> Optional[SolverCacheEntry]:
 
 def solver_cache_put(key, ent: SolverCacheEntry):
     _SOLVER_CACHE.pop(key, None)
-    while len(_SOLVER_CACHE) >= SOLVER_CACHE_MAX:
+    if ent.nbytes > SOLVER_CACHE_MAX_BYTES:
+        return  # larger than the whole budget: not cached
+    while _SOLVER_CACHE and (len(_SOLVER_CACHE) >= SOLVER_CACHE_MAX or
+                             sum(e.nbytes for e in _SOLVER_CACHE.values()) + ent.nbytes > SOLVER_CACHE_MAX_BYTES):
         _SOLVER_CACHE.pop(next(iter(_SOLVER_CACHE)))
     _SOLVER_CACHE[key] = ent
+
+
+def solver_cache_bytes() -> int:
+    return sum(e.nbytes for e in _SOLVER_CACHE.values())
 
 
 def solver_cache_clear():

@@ -51,6 +51,9 @@ def confusion_matrix_batched(label: torch.Tensor, pred: torch.Tensor, mask: torc
     """[B, K, K] int64 confusion matrices of B models' predictions ``pred [B, N]`` over the rows
     ``mask [B, N]`` selects (CrossValidator validation folds): one HIP launch (grid row chunks x B)."""
     B, N = pred.shape
+    lo_hi = torch.stack([label.min(), label.max()]).tolist() if label.numel() else [0, 0]
+    if lo_hi[0] < 0 or lo_hi[1] >= K:  # (the kernel would drop such rows silently)
+        raise ValueError(f"labels out of range [0, {K}): min {lo_hi[0]}, max {lo_hi[1]}")
     lab = label.to(device=pred.device, dtype=torch.int32).contiguous()
     prd = pred.to(torch.int32).contiguous()
     msk = mask.to(device=pred.device, dtype=torch.uint8).contiguous()
@@ -65,9 +68,13 @@ def roc_pr_auc_batched(score: torch.Tensor, label: torch.Tensor, mask: torch.Ten
     the rows ``mask [B, N]`` selects: ONE segmented descending sort of all B rows (the unselected rows
     keyed -inf sort to the back), ONE roc.hip launch with a workgroup per model, ONE host read."""
     B, N = score.shape
-    s = torch.where(mask.to(score.device), score.to(torch.float32), torch.full_like(score, float("-inf"),
-                                                                                     dtype=torch.float32))
-    vals, order = torch.sort(s, dim=1, descending=True, stable=True)
+    # two stable sorts: by score (descending), then selected rows first — an unselected row can never
+    # be counted in place of a selected one, not even when a selected score is -inf itself
+    m = mask.to(device=score.device, dtype=torch.bool)
+    vals, order = torch.sort(score.to(torch.float32), dim=1, descending=True, stable=True)
+    _, sel_first = torch.sort((~torch.gather(m, 1, order)).to(torch.uint8), dim=1, stable=True)
+    order = torch.gather(order, 1, sel_first)
+    vals = torch.gather(vals, 1, sel_first)
     y = label.to(device=score.device, dtype=torch.float32).reshape(1, N).expand(B, N)
     ys = torch.gather(y, 1, order).contiguous()
     ns = mask.to(score.device).sum(1).to(torch.int32).contiguous()

@@ -218,6 +218,9 @@ def run_reference_suite(dev, path: str, models: Sequence[str] = ("lr", "lrcv", "
         summary["ref_suite_fit_s"] = ref_tot
         summary["ref_suite_train_windows_per_s"] = len(models) * REFERENCE_N_TRAIN / ref_tot
         summary["suite_vs_baseline"] = summary["suite_train_windows_per_s"] / summary["ref_suite_train_windows_per_s"]
+    from .ops.logreg import solver_cache_clear
+
+    solver_cache_clear()  # the suite's resident tables go out of scope with it
     return summary
 
 

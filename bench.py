@@ -282,8 +282,10 @@ def bench_reference(args, ctx):
 
 def bench_infer(args, ctx):
     """Serving throughput: the MLP of config 3 (trained ``--train-steps`` steps first, untimed)
-    classifies ``--batch`` fp32 feature windows per GPU per step with ONE fused forward+head
-    kernel that reads the fp32 features directly (bf16 cast in its loads; logits and argmax).  The reference has no measurable inference path
+    classifies ``--batch`` fp32 feature windows per GPU per step: for the H = 256 network and
+    batches that are multiples of 64, one vectorized fp32 -> bf16 cast kernel, then the INFER
+    instantiation of the training step's forward (mlp_step.hip mlp_fwd3: logits and argmax out);
+    other shapes run the fused forward+head kernel (mlp_fused.hip).  The reference has no measurable inference path
     (its "Prediction made in" timer is lazy-plan time, Main/main.py:121-123)."""
     from har.models.mlp import MLPEngine, pad_input_bf16
     from har.parallel import dist as hdist
@@ -307,7 +309,7 @@ def bench_infer(args, ctx):
         j = i % nb
         xb = X[j * B:(j + 1) * B]
         if eng.native:
-            _, pred = eng.infer_fused_f32(xb)  # raw fp32 features in, cast in the kernel's loads
+            _, pred = eng.infer_fused_f32(xb)  # raw fp32 features in: cast kernel + the step's INFER forward
         else:
             pred = torch.argmax(eng.logits(xb), 1)
         if i < nb:

@@ -207,9 +207,17 @@ static bool logreg_solve_persistent(LogregSolvePlan& p, int max_iter, hipStream_
   return rc == 0;
 }
 
+// last_mode: 1 = the persistent solve ran and completed, 2 = it ran but a grid barrier timed out
+// (sync[1] set: blocks went on with unsynchronized x / g / history, so the results are garbage and
+// the caller must rerun the fit as the launch sequence — ops/logreg.py does), 0 = the sequence ran
 static void logreg_solve_run(LogregSolvePlan& p, int max_iter, int m, hipStream_t s) {
   if (logreg_solve_persistent(p, max_iter, s)) {
-    p.last_mode = 1;
+    uint32_t flag = 0;  // one blocking 4-byte read: only the opt-in persistent mode pays it
+    check(hipMemcpyAsync(&flag, p.sync.get() + 1, sizeof flag, hipMemcpyDeviceToHost, s) == hipSuccess &&
+                  hipStreamSynchronize(s) == hipSuccess
+              ? 0 : -1,
+          "logreg_solve flag read");
+    p.last_mode = flag ? 2 : 1;
     return;
   }
   p.last_mode = 0;
@@ -411,6 +419,7 @@ PYBIND11_MODULE(_har_native, m) {
     g_lr_persistent = mode;
     return old;
   });
+  m.def("logreg_set_spin_limit", [](uint32_t n) { return har_logreg_set_spin_limit(n); });
   // the persistent solve's timeout flag (blocking 4-byte read; tests / diagnostics)
   m.def("logreg_solve_flag", [](const LogregSolvePlan& p) {
     uint32_t f = 0;

@@ -322,6 +322,7 @@ int har_qn_chunks(int64_t D, int B);
 int har_lbfgs_phase(const QnArgs* a, int KP, int phase, hipStream_t s);
 // the whole L-BFGS / OWL-QN solve as one cooperative launch: 0 ran, -4 not available here (use
 // the launch sequence), -2 invalid; sync = 2 device words (barrier counter, timeout flag)
+uint32_t har_logreg_set_spin_limit(uint32_t n);
 int har_logreg_solve_persistent(const QnArgs* q, const LogregEvalArgs* evT, const LogregGradArgs* grT, int nT,
                                 const LogregEvalArgs* ev1, const LogregGradArgs* gr1, int n1, int KP, int max_iter,
                                 uint32_t* sync, int max_grid, hipStream_t s);

@@ -964,11 +964,14 @@ struct SolvePersistArgs {
   LogregGradArgs grT, gr1;
   int nT, n1, max_iter;
   uint32_t* sync;           // [0] barrier counter (zeroed by the launcher), [1] timeout flag
+  uint32_t spin_limit;      // polls per barrier before the timeout flag is raised
 };
 
 constexpr uint32_t SOLVE_SPIN_LIMIT = 1u << 22;
+// (tests shrink it to force the timeout path: har_logreg_set_spin_limit)
+uint32_t g_solve_spin_limit = SOLVE_SPIN_LIMIT;
 
-__device__ __forceinline__ void grid_barrier(uint32_t* sync, uint32_t& gen) {
+__device__ __forceinline__ void grid_barrier(uint32_t* sync, uint32_t& gen, uint32_t spin_limit) {
   __syncthreads();
   if (threadIdx.x == 0) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
@@ -977,7 +980,7 @@ __device__ __forceinline__ void grid_barrier(uint32_t* sync, uint32_t& gen) {
     uint32_t spins = 0;
     while (__hip_atomic_load(sync, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
       if (__hip_atomic_load(sync + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) break;
-      if (++spins > SOLVE_SPIN_LIMIT) {
+      if (++spins > spin_limit) {
         __hip_atomic_store(sync + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         break;
       }
@@ -1010,19 +1013,19 @@ __global__ __launch_bounds__(QN_BLOCK) void logreg_solve_persistent_kernel(Solve
         qn_update_body<FULLM, FULLM>(a, v % a.nch, v / a.nch);
       __syncthreads();  // the next virtual block reuses the LDS
     }
-    grid_barrier(p.sync, gen);
+    grid_barrier(p.sync, gen, p.spin_limit);
   };
   auto evaluate = [&](const LogregEvalArgs& ev, const LogregGradArgs& gr, int n) {
     for (int v = g0; v < tiles * n; v += G) {
       logreg_eval_body<KP, XLD>(ev, v % tiles, v / tiles, tiles, smem);
       __syncthreads();
     }
-    grid_barrier(p.sync, gen);
+    grid_barrier(p.sync, gen, p.spin_limit);
     for (int v = g0; v < cols * n; v += G) {
       logreg_grad_body<KP>(gr, v % cols, v / cols);
       __syncthreads();
     }
-    grid_barrier(p.sync, gen);
+    grid_barrier(p.sync, gen, p.spin_limit);
   };
   qn(1, 0, 0, 1, 0);
   evaluate(p.evT, p.grT, p.nT);
@@ -1143,7 +1146,7 @@ extern "C" int har_logreg_solve_persistent(const QnArgs* q, const LogregEvalArgs
       ev1->K != a.K || n1 != a.B * a.T || nT != a.B || ev1->tstride != 1 || evT->tstride != a.T)
     return -2;
   if (a.m != QN_MAX_M) return -4;
-  SolvePersistArgs p{*q, *evT, *ev1, *grT, *gr1, nT, n1, max_iter, sync};
+  SolvePersistArgs p{*q, *evT, *ev1, *grT, *gr1, nT, n1, max_iter, sync, g_solve_spin_limit};
   p.q.head = p.q.filled = p.q.init = p.q.fin_it = 0;
   static const bool mf_on = [] {
     const char* e = std::getenv("HAR_LR_EVAL_MFMA");
@@ -1181,6 +1184,12 @@ extern "C" int har_logreg_solve_persistent(const QnArgs* q, const LogregEvalArgs
     return -4;
   }
   return 0;
+}
+
+extern "C" uint32_t har_logreg_set_spin_limit(uint32_t n) {
+  const uint32_t old = g_solve_spin_limit;
+  g_solve_spin_limit = n ? n : SOLVE_SPIN_LIMIT;
+  return old;
 }
 
 extern "C" int har_lbfgs_phase(const QnArgs* args, int KP, int phase, hipStream_t s) {

@@ -5,6 +5,7 @@
 // 16x16x16 form (_1k) takes 4 k per lane: k = 4 (l >> 4) + i.
 #pragma once
 #include "common.h"
+#include "wave_ops.h"
 
 namespace mlpf {
 
@@ -85,65 +86,7 @@ __device__ __forceinline__ bf16x8_t frag_rows_sw(const bf16_t* img, int pitch, i
   return __builtin_bit_cast(bf16x8_t, v);
 }
 
-// ---- cross-lane steps on the VALU (DPP / permlane), not through the LDS crossbar: __shfl_xor
-// lowers to ds_bpermute_b32, whose LDS round trip made a 13-step softmax chain ~1.4k cycles ----
-template <int CTRL>
-__device__ __forceinline__ int dpp_i(int v) {
-  return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xf, 0xf, false);
-}
-template <int CTRL>
-__device__ __forceinline__ float dpp_f(float v) {
-  return __builtin_bit_cast(float, dpp_i<CTRL>(__builtin_bit_cast(int, v)));
-}
-constexpr int DPP_ROR8 = 0x128, DPP_ROR4 = 0x124, DPP_ROR2 = 0x122, DPP_ROR1 = 0x121;  // row_ror:n (16-lane rows)
-constexpr int DPP_QUAD_XOR1 = 0xb1;                                                // quad_perm [1,0,3,2]
-
-// max as one v_max_f32: fmaxf of a DPP-moved value makes hipcc quiet both operands first (IEEE mode),
-// two extra VALU per step on the softmax's dependent chain
-__device__ __forceinline__ float vmaxf(float a, float b) {
-  float r;
-  asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
-  return r;
-}
-// all-reduce over the 16 lanes of each DPP row (lanes 16r .. 16r + 15)
-__device__ __forceinline__ float row16_max(float v) {
-  v = vmaxf(v, dpp_f<DPP_ROR8>(v));
-  v = vmaxf(v, dpp_f<DPP_ROR4>(v));
-  v = vmaxf(v, dpp_f<DPP_ROR2>(v));
-  return vmaxf(v, dpp_f<DPP_ROR1>(v));
-}
-__device__ __forceinline__ float row16_sum(float v) {
-  v += dpp_f<DPP_ROR8>(v);
-  v += dpp_f<DPP_ROR4>(v);
-  v += dpp_f<DPP_ROR2>(v);
-  return v + dpp_f<DPP_ROR1>(v);
-}
-__device__ __forceinline__ int row16_min(int v) {
-  v = min(v, dpp_i<DPP_ROR8>(v));
-  v = min(v, dpp_i<DPP_ROR4>(v));
-  v = min(v, dpp_i<DPP_ROR2>(v));
-  return min(v, dpp_i<DPP_ROR1>(v));
-}
-
-// The value lane ^ 16 / lane ^ 32 holds, by the gfx950 row / half swaps (VALU).  `self` of the swap of
-// the lane's own id fixes which of the two outputs carries the partner, independent of the operand
-// order convention.
-struct LaneSwap {
-  bool hi16, hi32;
-  __device__ __forceinline__ explicit LaneSwap(int lane) {
-    const auto a = __builtin_amdgcn_permlane16_swap((uint32_t)lane, (uint32_t)lane, false, false);
-    const auto b = __builtin_amdgcn_permlane32_swap((uint32_t)lane, (uint32_t)lane, false, false);
-    hi16 = a[0] == (uint32_t)(lane ^ 16);
-    hi32 = b[0] == (uint32_t)(lane ^ 32);
-  }
-  __device__ __forceinline__ uint32_t x16(uint32_t v) const {
-    const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
-    return hi16 ? r[0] : r[1];
-  }
-  __device__ __forceinline__ uint32_t x32(uint32_t v) const {
-    const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
-    return hi32 ? r[0] : r[1];
-  }
-};
+// cross-lane steps on the VALU (DPP / permlane): wave_ops.h (dpp_i / dpp_f, vmaxf, row16_*, LaneSwap)
+using namespace wops;
 
 }  // namespace mlpf

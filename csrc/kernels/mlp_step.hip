@@ -1,6 +1,7 @@
 // Fused training step of the flagship MLP (BASELINE.json config 3: 43-256-256-6, bf16 MFMA; SURVEY.md
 // K23), H = 256 hidden units, K0 = 32 / 64 padded inputs, <= 16 classes, batch a multiple of 64.
-// Three kernels per step: mlp_fwd3 -> mlp_bwd3 -> grad_reduce_adam (mlp.hip).
+// Three kernels per step: mlp_fwd3 -> mlp_bwd4 (the wave-specialized backward; mlp_bwd3, the
+// data-split form, stays selectable with HAR_MLP_BWD=3) -> grad_reduce_adam (mlp.hip).
 //
 // The forward hands the backward only what it cannot recompute cheaply: the logit gradients dz
 // ([B][16] bf16, 32 B per row) and the relu' mask of h2 ([B][8] u32, 32 B per row) — 4 MB at batch

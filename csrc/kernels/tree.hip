@@ -14,6 +14,7 @@
 //   Poisson(1) counts, identical to har/ops/rng.py.
 #include "common.h"
 #include "philox.h"
+#include "wave_ops.h"
 #include "../har_kernels.h"
 
 namespace {
@@ -34,11 +35,14 @@ __device__ __forceinline__ void split_search_pairs(const float* hist, const int*
                                                    int f_n, int maxbins, int K, float min_inst, int impurity,
                                                    int wave, int nwaves, int lane, double& best_g, int& best_i) {
   const int half = lane >> 5, bl = lane & 31;
+  const wops::LaneSwap sw(lane);
   for (int fp = wave; 2 * fp < f_n; fp += nwaves) {
     const int fs = 2 * fp + half;
     const bool fv = fs < f_n;
     const int nb = fv ? nbins_feat[fid[fs]] : 0;
-    const int src = (lane & 32) + max(nb - 1, 0);
+    // each half's last bin (uniform per half): the totals are two scalar lane reads, not a permute
+    const int last0 = max(__builtin_amdgcn_readlane(nb, 0) - 1, 0);
+    const int last1 = 32 + max(__builtin_amdgcn_readlane(nb, 32) - 1, 0);
     double wl = 0.0, wt = 0.0, ql = 0.0, qr = 0.0, qt = 0.0;
     // classes in groups of KC (registers), accumulated in class order
     for (int k0 = 0; k0 < K; k0 += KC) {
@@ -46,17 +50,13 @@ __device__ __forceinline__ void split_search_pairs(const float* hist, const int*
 #pragma unroll
       for (int k = 0; k < KC; ++k)
         c[k] = (k0 + k < K && bl < nb && bl < maxbins) ? hist[(fs * maxbins + bl) * K + k0 + k] : 0.f;
+      // inclusive bin scans of the KC classes over each 32-lane half (DPP row shifts + row broadcast:
+      // VALU, independent chains pipeline)
 #pragma unroll
-      for (int o = 1; o < 32; o <<= 1) {
-#pragma unroll
-        for (int k = 0; k < KC; ++k) {
-          const float u = __shfl_up(c[k], o, 32);
-          if (bl >= o) c[k] += u;
-        }
-      }
+      for (int k = 0; k < KC; ++k) c[k] = wops::scan32_add(c[k]);
 #pragma unroll
       for (int k = 0; k < KC; ++k) {
-        const float tf = __shfl(c[k], src, 64);
+        const float tf = half ? wops::lane_f(c[k], last1) : wops::lane_f(c[k], last0);
         if (k0 + k < K) {
           const double v = (double)c[k], t = (double)tf, r = t - v;
           wl += v;
@@ -83,12 +83,7 @@ __device__ __forceinline__ void split_search_pairs(const float* hist, const int*
       g = ip - (wl / wt) * il - (wr / wt) * ir;
     }
     int idx = fs * maxbins + bl;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      const double og = __shfl_xor(g, o, 64);
-      const int oi = __shfl_xor(idx, o, 64);
-      if (og > g || (og == g && oi < idx)) { g = og; idx = oi; }
-    }
+    wops::wave_argmax(g, idx, sw);
     if (g > best_g || (g == best_g && idx < best_i)) { best_g = g; best_i = idx; }
   }
 }
@@ -303,21 +298,18 @@ __global__ __launch_bounds__(256) void tree_hist_split_kernel(
   if (pairs)
     split_search_pairs<8>(hist, fid, nbins_feat, f_n, maxbins, K, min_inst, impurity, wave, nwaves, lane, best_g,
                           best_i);
+  const wops::LaneSwap swl(lane);
   for (int fs = wave; !pairs && fs < f_n; fs += nwaves) {
-    const int nb = nbins_feat[fid[fs]];
+    const int nb = __builtin_amdgcn_readfirstlane(nbins_feat[fid[fs]]);
     double wl = 0.0, wt = 0.0, ql = 0.0, qr = 0.0, qt = 0.0;
     for (int k = 0; k < K; ++k) {
-      // the bin scan runs in fp32 (one ds_bpermute per step instead of two): the sums are exact
-      // for integer-valued weights below 2^24 (bootstrap counts, fold masks) and are what the
-      // CPU oracle's float32 cumsum computes anyway; the gains below are fp64
+      // the bin scan runs in fp32 on the VALU (DPP): the sums are exact for integer-valued weights
+      // below 2^24 (bootstrap counts, fold masks), as the CPU oracle's float32 cumsum; the gains
+      // below are fp64
       float vf = (lane < nb && lane < maxbins) ? hist[(fs * maxbins + lane) * K + k] : 0.f;
-#pragma unroll
-      for (int o = 1; o < 64; o <<= 1) {
-        const float u = __shfl_up(vf, o, 64);
-        if (lane >= o) vf += u;
-      }
+      vf = wops::scan64_add(vf);
       const double v = (double)vf;
-      const double t = (double)__shfl(vf, max(nb - 1, 0), 64);
+      const double t = (double)wops::lane_f(vf, max(nb - 1, 0));
       const double r = t - v;
       wl += v;
       wt += t;
@@ -341,13 +333,7 @@ __global__ __launch_bounds__(256) void tree_hist_split_kernel(
       g = ip - (wl / wt) * il - (wr / wt) * ir;
     }
     int idx = fs * maxbins + lane;
-    // wave argmax, lowest index on ties
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      double og = __shfl_xor(g, o, 64);
-      int oi = __shfl_xor(idx, o, 64);
-      if (og > g || (og == g && oi < idx)) { g = og; idx = oi; }
-    }
+    wops::wave_argmax(g, idx, swl);  // lowest index on ties
     if (g > best_g || (g == best_g && idx < best_i)) { best_g = g; best_i = idx; }
   }
   if (lane == 0) { red_gain[wave] = best_g; red_idx[wave] = best_i; }
@@ -372,11 +358,8 @@ __global__ __launch_bounds__(256) void tree_hist_split_kernel(
     for (int k = 0; k < K; ++k) {
       float vl = (ok && lane <= b) ? hist[(fs * maxbins + lane) * K + k] : 0.f;
       float vt = (c == 0 && lane < maxbins) ? hist[lane * K + k] : 0.f;
-#pragma unroll
-      for (int off = 32; off > 0; off >>= 1) {
-        vl += __shfl_xor(vl, off, 64);
-        vt += __shfl_xor(vt, off, 64);
-      }
+      vl = wops::wave_sum_dpp(vl, swl);
+      vt = wops::wave_sum_dpp(vt, swl);
       if (lane == 0) {
         out_left[o * K + k] = vl;
         if (c == 0) out_total[(size_t)a * K + k] = vt;
@@ -446,11 +429,10 @@ __global__ __launch_bounds__(256) void forest_predict_wave_kernel(
   const float* x = X + i * (int64_t)ld;
   for (int t = lane; t < T; t += 64)
     add_tree<KC>(x, (size_t)t * maxn, feature, thr, left, right, leaf, K, max_depth, normalize, acc);
+  const wops::LaneSwap sw(lane);
 #pragma unroll
   for (int k = 0; k < KC; ++k) {
-    float v = acc[k];
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    const float v = wops::wave_sum_dpp(acc[k], sw);
     if (lane == k && k < K) out[i * K + k] = v;
   }
 }
@@ -656,12 +638,7 @@ __global__ __launch_bounds__(1024) void tree_plan_kernel(const int32_t* __restri
     tb += big;
   }
   // exclusive block scan of (items, big nodes): wave shuffles, then the 16 wave totals
-  int si = ti, sb = tb;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const int ui = __shfl_up(si, o, 64), ub = __shfl_up(sb, o, 64);
-    if (lane >= o) { si += ui; sb += ub; }
-  }
+  const int si = wops::scan64_add(ti), sb = wops::scan64_add(tb);
   if (lane == 63) { wsum_i[wave] = si; wsum_b[wave] = sb; }
   __syncthreads();
   int oi = si - ti, ob = sb - tb, all_i = 0, all_b = 0;

@@ -187,6 +187,9 @@ def main(argv=None):
     if int(os.environ.get("WORLD_SIZE", "1")) > 1:  # launched by torch.distributed.run: one rank per GPU
         ctx = hdist.init(device=None if cfg.device == "auto" else cfg.device)
     summary = run(cfg, ctx)
+    from har.ops.logreg import solver_cache_clear
+
+    solver_cache_clear()  # the run's tables are dropped: release the cached LR solvers' device memory
     if ctx is not None:
         hdist.shutdown(ctx)
         if not ctx.is_main:

@@ -574,3 +574,37 @@ def test_batched_cv_metrics_gpu_match_cpu(cuda, metric):
     cpu = batched_metrics(metric, label, pred, mask, K, raw)
     gpu = batched_metrics(metric, label.to(cuda), pred.to(cuda), mask.to(cuda), K, raw.to(cuda))
     np.testing.assert_allclose(gpu, cpu, rtol=1e-9, atol=1e-12)
+
+
+def test_batched_roc_with_minus_inf_scores_matches_cpu(cuda):
+    """Selected rows whose score is -inf (a margin that overflowed) sort among the unselected rows
+    under a -inf sentinel; the batched pass must still score exactly the selected rows."""
+    from har.evaluation.metrics import batched_metrics
+
+    g = torch.Generator().manual_seed(5)
+    B, N, K = 5, 1201, 6
+    label = torch.randint(0, K, (N,), generator=g)
+    pred = torch.randint(0, K, (B, N), generator=g)
+    mask = torch.rand(B, N, generator=g) < 0.4
+    raw = torch.round(torch.randn(B, N, K, generator=g) * 4) / 4
+    raw[:, ::7, 1] = float("-inf")  # selected and unselected rows alike
+    for metric in ("areaUnderROC", "areaUnderPR"):
+        cpu = batched_metrics(metric, label, pred, mask, K, raw)
+        gpu = batched_metrics(metric, label.to(cuda), pred.to(cuda), mask.to(cuda), K, raw.to(cuda))
+        np.testing.assert_allclose(gpu, cpu, rtol=1e-9, atol=1e-12)
+
+
+def test_batched_confusion_rejects_out_of_range_labels_and_weights_rows(cuda):
+    from har.evaluation.metrics import batched_metrics
+
+    g = torch.Generator().manual_seed(6)
+    B, N, K = 3, 500, 4
+    label = torch.randint(0, K, (N,), generator=g)
+    pred = torch.randint(0, K, (B, N), generator=g)
+    w = torch.rand(B, N, generator=g)  # fractional row weights: the weighted definition, as on the CPU
+    np.testing.assert_allclose(batched_metrics("accuracy", label.to(cuda), pred.to(cuda), w.to(cuda), K),
+                               batched_metrics("accuracy", label, pred, w, K), rtol=1e-9)
+    bad = label.clone()
+    bad[3] = K
+    with pytest.raises(ValueError):
+        batched_metrics("accuracy", bad.to(cuda), pred.to(cuda), (w > 0.5).to(cuda), K)

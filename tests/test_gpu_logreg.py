@@ -332,6 +332,43 @@ def test_persistent_solve_equals_launch_sequence(cuda, wisdm_csv, specs_kind):
         assert m1.summary["objectiveHistory"] == m2.summary["objectiveHistory"]
 
 
+def test_persistent_solve_timeout_falls_back_to_the_sequence(cuda):
+    """A grid barrier of the persistent solve that runs out of polls raises the timeout flag; the
+    fit must not return the unsynchronized results: it is rerun as the launch sequence (mode 3) and
+    equals a plain launch-sequence fit bit for bit (the flag was never read)."""
+    import warnings
+
+    from har.models.logreg import FitSpec, LogisticRegression
+    from har.ops import _native
+    from har.ops import logreg as L
+
+    mod = _native.kernels()
+    _, y, hm = _hybrid_problem(cuda, N=3000, seed=9)
+    est = LogisticRegression(maxIter=20, regParam=0.1)
+    specs, K = [FitSpec(None, 0.1, 0.0), FitSpec(None, 0.3, 0.1)], 6
+    y = y.to(cuda)
+    old, old_lim = mod.logreg_set_persistent(2), mod.logreg_set_spin_limit(1)
+    try:
+        L.solver_cache_clear()
+        with warnings.catch_warnings(record=True) as w:
+            warnings.simplefilter("always")
+            a = est.fit_many(hm, y, specs, K)
+        mode_a = L.LAST_SOLVE_MODE
+        mod.logreg_set_persistent(0)
+        L.solver_cache_clear()
+        b = est.fit_many(hm, y, specs, K)
+    finally:
+        mod.logreg_set_persistent(old)
+        mod.logreg_set_spin_limit(old_lim)
+        L.solver_cache_clear()
+    if mode_a == -1 or mode_a == 0:
+        pytest.skip("the persistent solve was not co-resident on this device")
+    assert mode_a == 3 and any("timed out" in str(x.message) for x in w), mode_a
+    for m1, m2 in zip(a, b):
+        assert torch.equal(m1.coefficientMatrix, m2.coefficientMatrix)
+        assert torch.equal(m1.interceptVector, m2.interceptVector)
+
+
 def test_solver_cache_refit_is_bitwise_a_fresh_fit(cuda, wisdm_csv):
     """A repeated fit on the same resident table reuses the cached solver (arena, argument blocks,
     solve plan): its model is bitwise the model of a fit with the cache cleared, and a fit with other

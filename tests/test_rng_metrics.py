@@ -109,3 +109,14 @@ def test_batched_regression_metrics_match_single(metric):
         rows = torch.nonzero(mask[b]).squeeze(1)
         want = regression_metrics(label[rows].numpy(), pred[b, rows].numpy())[metric]
         assert abs(got[b] - want) < 1e-9 * max(1.0, abs(want))
+
+
+def test_batched_metrics_rejects_out_of_range_labels():
+    import pytest
+
+    from har.evaluation.metrics import batched_metrics
+
+    label = torch.tensor([0, 1, 2, 6])
+    pred = torch.zeros(2, 4, dtype=torch.long)
+    with pytest.raises(ValueError):
+        batched_metrics("accuracy", label, pred, torch.ones(2, 4), 6)
