@@ -103,15 +103,16 @@ struct GradRegions {
 
 // ---- MFMA-fragment-ordered bf16 copies of W0 / W1 for the step kernels (mlp_step.hip) ----
 // A 16x16x32 A-operand fragment (16 rows x 32 k, lane l: row l & 15, k 8 (l >> 4) .. + 7) of a [R][C]
-// matrix is stored as ONE contiguous KB, row-major inside (row r & 15 at 64 (r & 15) bytes): element
-// (r, c) at frag_pos(r, c, C).  A wave then loads a fragment with one 1 KB-contiguous instruction
-// (lane l at frag_lane_off(l), mlp_frag.h) instead of 16 half-lines (profiles/r4/prologue_probe.txt:
-// 2.7k vs 9.2k cycles for the forward's 21 KB per wave), and the optimizer's row-wise update writes
-// 64-byte runs (a lane-major order put the 64 lanes of an Adam store on 64 different lines).  Layout
-// of MlpFragSpec::dst: W0 [H][K0], W1 [H][H] (forward A: rows = layer-2 units), W1^T (backward A:
-// rows = layer-1 units).
+// matrix is stored as ONE contiguous KB in LANE order (lane l's 16 bytes at 16 l): element (r, c) at
+// frag_pos(r, c, C).  A wave loads a fragment with one instruction whose 64 lanes read consecutive
+// 16-byte pieces (frag_lane_off(l) = 8 l, mlp_frag.h): every quarter-wave touches 2 cache lines.  The
+// row-major order inside the block (r4) put the 16 lanes of a quarter-wave on 16 lines 64 bytes apart
+// and the forward's weight prologue stayed at ~8.7k cycles (profiles/r4/mlp_stamps_bwd4.txt) against
+// 2.7k for a lane-sequential load (profiles/r4/prologue_probe.txt); the price is the optimizer's
+// fragment stores (8-byte pieces, ~160 KB per step).  Layout of MlpFragSpec::dst: W0 [H][K0], W1 [H][H]
+// (forward A: rows = layer-2 units), W1^T (backward A: rows = layer-1 units).
 __device__ __forceinline__ int64_t frag_pos(int r, int c, int C) {
-  return ((((int64_t)(r >> 4) * (C >> 5) + (c >> 5)) * 16 + (r & 15)) << 5) + (c & 31);
+  return ((((int64_t)(r >> 4) * (C >> 5) + (c >> 5)) * 64 + ((c & 31) >> 3) * 16 + (r & 15)) << 3) + (c & 7);
 }
 
 // element e .. e + 3 of the flat parameter buffer (bf16 values ob) into the fragment copies; the

@@ -27,9 +27,9 @@ __device__ __forceinline__ uint32_t pack2(float a, float b) {
   return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2_t{a, b}, bf16x2_t));
 }
 
-// element offset of lane l's 16 bytes inside a 1 KB fragment block of the fragment-ordered weight
-// copies (mlp.hip frag_pos: 16 rows x 32 k, row-major): row l & 15, k 8 (l >> 4) .. + 7
-__device__ __forceinline__ int frag_lane_off(int lane) { return (lane & 15) * 32 + (lane >> 4) * 8; }
+// element offset of lane l's 16 bytes (row l & 15, k 8 (l >> 4) .. + 7) inside a 1 KB fragment block
+// of the fragment-ordered weight copies (mlp.hip frag_pos: lane order)
+__device__ __forceinline__ int frag_lane_off(int lane) { return lane * 8; }
 
 __device__ __forceinline__ f32x4_t mma32(bf16x8_t a, bf16x8_t b, f32x4_t c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);

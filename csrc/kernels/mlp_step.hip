@@ -26,6 +26,7 @@
 //   | (c) dW0 += dact1^T . X of tile i-1 | db1 = sum_rows dact2 (a ones-row MFMA, 64 j per quadrant) | barrier
 // One deterministic partial per (slice, quadrant), laid out like the flat parameter buffer.
 #include <algorithm>
+#include <type_traits>
 #include <cstdlib>
 
 #include "common.h"
@@ -87,7 +88,8 @@ __global__ __launch_bounds__(512) void mlp_fwd3_kernel(
     const float* __restrict__ b1, const bf16_t* __restrict__ Wo,
     const float* __restrict__ bo, const int32_t* __restrict__ labels, int B, int C, float scale,
     uint32_t* __restrict__ dz_out, uint32_t* __restrict__ mask_out, float* __restrict__ slab,
-    float* __restrict__ block_loss, int32_t* __restrict__ block_correct, uint64_t* __restrict__ stamps) {
+    float* __restrict__ block_loss, int32_t* __restrict__ block_correct, uint64_t* __restrict__ stamps,
+    int stagger) {
   constexpr int K0C = K0 / 32, KC = HH / 32;
   extern __shared__ __attribute__((aligned(16))) bf16_t lds[];
   bf16_t* const h1s = lds;                                                // [2 bufs][32][FHP]
@@ -317,11 +319,19 @@ __global__ __launch_bounds__(512) void mlp_fwd3_kernel(
   // iterations are peeled so the steady-state body is ONE basic block (no k > 0 / k + 1 < nt
   // branches): the scheduler can then interleave the softmax's VALU / DPP chain with the stage-2
   // MFMAs instead of running them back to back.
-  auto iter = [&](int k, bool first, bool last) __attribute__((always_inline)) {
+  // Staggered roles (stagger != 0): the two waves of a SIMD (w and w + 4) run the SAME phases of an
+  // iteration in a different ORDER — waves 0..3 softmax(k) first, waves 4..7 last (after stage 5 and
+  // the next tile's MFMA stages) — so one wave's VALU / DPP softmax chain issues beside its partner's
+  // stage-2 MFMAs instead of both SIMD partners reaching the softmax (MFMA pipe idle) and then the
+  // MFMAs (pipe shared) together.  Legal: within an iteration the phases touch disjoint buffers
+  // (softmax: zs[k], dzs[k]; stage 5: dzs[k-1], the wave's own img[k-1]; stages 2 + 3: h1[k+1] ->
+  // zs[k+1], own img[k+1]; stage 1: h1[k+2]) and the wave's own img[k-1] is read before its img[k+1]
+  // (the same buffer) is written in both orders.
+  auto iter = [&](int k, bool first, bool last, auto late) __attribute__((always_inline)) {
     if (k < 32) HAR_STAMP(FW, 2 + k)
     const int yc = ynext;
     if constexpr (!INFER) ynext = labels[tile_of(k + 1) * FRT + sr];
-    softmax(k, k & 1, yc);
+    if constexpr (!decltype(late)::value) softmax(k, k & 1, yc);
     if (k == 4) HAR_STAMP(FW, 10)
     if (!INFER && !first) stage5((k - 1) & 1);
     if (k == 4) HAR_STAMP(FW, 11)
@@ -336,17 +346,24 @@ __global__ __launch_bounds__(512) void mlp_fwd3_kernel(
       load_x(k + 3);
       if (k == 4) HAR_STAMP(FW, 13)
     }
+    if constexpr (decltype(late)::value) softmax(k, k & 1, yc);
     __syncthreads();
   };
   // (nt == 1 apart, so that every path into the loop issues its loads in the loop body's order: a
   // path with other pending loads makes the counted wait for the label at the loop top conservative)
-  if (nt == 1) {
-    iter(0, true, true);
-  } else if (nt > 1) {
-    iter(0, true, false);
-    for (int k = 1; k < nt - 1; ++k) iter(k, false, false);
-    iter(nt - 1, false, true);
-  }
+  auto run = [&](auto late) __attribute__((always_inline)) {
+    if (nt == 1) {
+      iter(0, true, true, late);
+    } else if (nt > 1) {
+      iter(0, true, false, late);
+      for (int k = 1; k < nt - 1; ++k) iter(k, false, false, late);
+      iter(nt - 1, false, true, late);
+    }
+  };
+  if (stagger && __builtin_amdgcn_readfirstlane(wave) >= FW / 2)
+    run(std::true_type{});
+  else
+    run(std::false_type{});
   HAR_STAMP(FW, 34)
   if constexpr (INFER) return;
   if (nt > 0) stage5((nt - 1) & 1);
@@ -1077,19 +1094,29 @@ __global__ __launch_bounds__(512) void mlp_bwd4_kernel(
   HAR_STAMP_REAL(8, 39)
 }
 
+// HAR_MLP_FWD_STAGGER=0 runs every wave of the forward in one phase order (the round-4 kernel)
+static int fwd_stagger() {
+  static const int v = [] {
+    const char* e = getenv("HAR_MLP_FWD_STAGGER");
+    return e ? atoi(e) : 1;
+  }();
+  return v;
+}
+
 template <int K0>
 void launch_fwd3(const bf16_t* X, bf16_t* Wf, const float* b0, const float* b1, const bf16_t* Wo,
                  const float* bo, const int32_t* labels, int B, int C, float scale, uint32_t* dz, uint32_t* mask,
                  float* slab, float* bl, int32_t* bc, int nwg, hipStream_t s) {
   auto k = g_har_mlp_stamps ? mlp_fwd3_kernel<K0, true> : mlp_fwd3_kernel<K0, false>;
-  k<<<nwg, 512, FWD_LDS, s>>>(X, Wf, b0, b1, Wo, bo, labels, B, C, scale, dz, mask, slab, bl, bc, g_har_mlp_stamps);
+  k<<<nwg, 512, FWD_LDS, s>>>(X, Wf, b0, b1, Wo, bo, labels, B, C, scale, dz, mask, slab, bl, bc, g_har_mlp_stamps,
+                              fwd_stagger());
 }
 
 template <int K0>
 void launch_fwd3_infer(const bf16_t* X, bf16_t* Wf, const float* b0, const float* b1, const bf16_t* Wo,
                        const float* bo, int B, int C, float* logits, int32_t* pred, int nwg, hipStream_t s) {
   mlp_fwd3_kernel<K0, false, true><<<nwg, 512, FWD_LDS, s>>>(X, Wf, b0, b1, Wo, bo, nullptr, B, C, 1.f, nullptr, nullptr,
-                                                              logits, nullptr, pred, nullptr);
+                                                              logits, nullptr, pred, nullptr, fwd_stagger());
 }
 
 template <int K0>

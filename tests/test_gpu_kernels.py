@@ -492,10 +492,11 @@ def test_sort_columns_matches_torch_sort(cuda, n, F):
 
 def _frag_reference(M: torch.Tensor) -> torch.Tensor:
     """Independent construction of the fragment order of mlp.hip frag_pos: [R][C] -> blocks of 16 rows x
-    32 k, one KB each, row-major inside (lane l = 16 g + row reads the 16 bytes at row * 64 + g * 16)."""
+    32 k, one KB each, in MFMA lane order inside (lane l = 16 g + row reads the 16 bytes at 16 l: row,
+    k = 8 g .. 8 g + 7)."""
     R, C = M.shape
-    t = M.reshape(R // 16, 16, C // 32, 32)          # (row block, row, k chunk, k)
-    return t.permute(0, 2, 1, 3).reshape(-1)         # (row block, k chunk, row, k)
+    t = M.reshape(R // 16, 16, C // 32, 4, 8)        # (row block, row, k chunk, k group g, k)
+    return t.permute(0, 2, 3, 1, 4).reshape(-1)      # (row block, k chunk, g, row, k)
 
 
 @pytest.mark.parametrize("F", [43, 20])
