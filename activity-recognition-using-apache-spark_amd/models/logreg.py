@@ -152,14 +152,15 @@ def _content_checksums(hm: HybridMatrix, y: torch.Tensor, specs, allreduce=None)
 
 class LogisticRegression(Estimator, ClassifierParams):
     _param_names = ("maxIter", "regParam", "elasticNetParam", "tol", "fitIntercept", "standardization", "family",
-                    "featuresCol", "labelCol", "weightCol", "device", "lineSearchTrials", "threshold", "thresholds",
-                    "checkpointDir")
+                    "featuresCol", "labelCol", "weightCol", "device", "lineSearchTrials", "lineSearch", "threshold",
+                    "thresholds", "checkpointDir")
 
     def __init__(self, featuresCol="features", labelCol="label", maxIter: int = 100, regParam: float = 0.0,
                  elasticNetParam: float = 0.0, tol: float = 1e-6, fitIntercept: bool = True,
                  standardization: bool = True, family: str = "auto", weightCol: Optional[str] = None,
                  device=None, lineSearchTrials: int = 4, threshold: float = 0.5,
-                 thresholds: Optional[Sequence[float]] = None, checkpointDir: Optional[str] = None):
+                 thresholds: Optional[Sequence[float]] = None, checkpointDir: Optional[str] = None,
+                 lineSearch: str = "armijo"):
         super().__init__(new_uid("LogisticRegression"))
         # Spark: binary ``threshold`` t == thresholds [1 - t, t]; ``thresholds`` (any K) wins if set
         self.threshold, self.thresholds = threshold, thresholds
@@ -173,6 +174,13 @@ class LogisticRegression(Estimator, ClassifierParams):
         self.family, self.weightCol, self.device = family, weightCol, device
         self.lineSearchTrials = lineSearchTrials  # step lengths 2^-t evaluated together per line search
         _check_trials(lineSearchTrials)
+        # "armijo" (default, fast): lineSearchTrials step lengths per iteration in ONE batched evaluation,
+        # the largest that satisfies Armijo; "wolfe": Breeze's searches — strong Wolfe (bracketing +
+        # cubic zoom) for L-BFGS, projected backtracking with the Wolfe curvature condition for OWL-QN —
+        # one trial per model per batched evaluation round (optim.lbfgs.minimize_wolfe)
+        if lineSearch not in ("armijo", "wolfe"):
+            raise ValueError(f"lineSearch must be 'armijo' or 'wolfe', got {lineSearch!r}")
+        self.lineSearch = lineSearch
 
     # ------------------------------------------------------------------
     def fit(self, table: Table) -> LogisticRegressionModel:
@@ -309,6 +317,7 @@ class LogisticRegression(Estimator, ClassifierParams):
             fp = {"rows": int(hm.n_rows), "features": int(F), "classes": K, "maxIter": self.maxIter,
                   "tol": self.tol, "fitIntercept": self.fitIntercept, "standardization": self.standardization,
                   "family": self.family, "lineSearchTrials": self.lineSearchTrials,
+                  "lineSearch": getattr(self, "lineSearch", "armijo"),
                   "specs": [[s.regParam, s.elasticNetParam, s.row_weight is None] for s in specs],
                   "content": _content_checksums(hm, y, specs, allreduce),
                   "world": ctx.world_size if ctx else 1}
@@ -319,10 +328,11 @@ class LogisticRegression(Estimator, ClassifierParams):
             last = ckpt.latest(fingerprint=fp)
             if last is not None:
                 return self._models_from_state(last[0], last[1], len(specs), dev)
-        T = max(1, int(self.lineSearchTrials))
+        wolfe = getattr(self, "lineSearch", "armijo") == "wolfe"
+        T = 1 if wolfe else max(1, int(self.lineSearchTrials))
         # repeated single-device fits on one resident design reuse the solver (ops/logreg.py)
         ckey = ent = None
-        if (dev.type == "cuda" and allreduce is None and ckpt is None
+        if (dev.type == "cuda" and allreduce is None and ckpt is None and not wolfe
                 and native_classes_ok(2 if self.family == "binomial" or (self.family == "auto" and K <= 2) else K)):
             ckey = (id(hm), K, len(specs), T, self.maxIter, float(self.tol), self.family, self.fitIntercept,
                     self.standardization, any(s.regParam * s.elasticNetParam > 0 for s in specs),
@@ -332,7 +342,32 @@ class LogisticRegression(Estimator, ClassifierParams):
                                                                                     reuse=ent)
         B, D = len(specs), Kp * (F + 1)
         poll = 10 if self.maxIter > 20 else 0
-        if design.native:
+        rounds = None
+        if wolfe:
+            if design.native:  # the evaluation kernels at each round's trial points (+ the DP all-reduce)
+                solver = DeviceLogregSolver(design, B, 1, 10, inv_std, pmask, inv_wsum, l2v, l1v, self.maxIter,
+                                            self.tol, allreduce=allreduce)
+                evaluate = solver.evaluate_at
+            else:
+                def evaluate(xt):
+                    loss, G = design.eval_torch(xt.view(-1, Kp, F + 1), 1, inv_std, pmask, inv_wsum)
+                    if allreduce is not None:
+                        bucket = pack_bucket(G, loss)
+                        allreduce(bucket)
+                        G2, loss = unpack_bucket(bucket, loss.numel(), G.shape)
+                        G = G2.to(G.dtype)
+                    return loss, G
+            res = lbfgs.minimize_wolfe(evaluate, x0.reshape(B, D), l2v, l1v, max_iter=self.maxIter, m=10,
+                                       tol=self.tol)
+            xs, fobj, iters, n_evals = res.x, res.f, res.iterations, res.n_evals
+            rounds = res.rounds_per_iter
+            history = []
+            for h in res.history_per_model:  # as Spark's objectiveHistory: no repeats after a model stopped
+                h = list(h)
+                while len(h) > 1 and h[-1] == h[-2]:
+                    h.pop()
+                history.append(h)
+        elif design.native:
             if ent is not None:
                 solver = ent.solver
                 solver.reset()
@@ -383,7 +418,9 @@ class LogisticRegression(Estimator, ClassifierParams):
         fobj_l, iters_l = fobj_h.tolist(), iters_h.tolist()
         for bi in range(B):
             summary = {"objective": float(fobj_l[bi]), "iterations": int(iters_l[bi]), "n_evals": n_evals,
-                       "objectiveHistory": history[bi]}
+                       "objectiveHistory": history[bi], "lineSearch": "wolfe" if wolfe else "armijo"}
+            if rounds is not None:
+                summary["lineSearchRounds"] = rounds  # batched evaluation rounds per iteration
             models.append(self._apply_thresholds(LogisticRegressionModel(coefs[bi], icpts[bi], binomial, device=dev,
                                                                          summary=summary)))
         if ckpt is not None:

@@ -361,6 +361,22 @@ class DeviceLogregSolver:
             mod.logreg_loss_decode(self.loss_fx.data_ptr(), self.loss.data_ptr(), self.B * self.T, s)
         self.n_evals += 1
 
+    def evaluate_at(self, x: torch.Tensor):
+        """The data objective at arbitrary points ``x [B, D]`` through the evaluation kernels
+        (T = 1 solvers: ``LogisticRegression(lineSearch="wolfe")``, whose line-search state machine
+        runs as batched tensor ops in ``optim.lbfgs.minimize_wolfe``): W_eff = x * inv_std * mask in
+        the evaluator's [F+1][KP] layout, then evaluate + gradient (+ the DP all-reduce).  Returns
+        (loss [B] float64, G [B, D] float32) — views of the solver's buffers, overwritten by the next
+        call."""
+        if self.T != 1:
+            raise ValueError("evaluate_at needs a one-trial solver")
+        B, K, F = self.B, self.d.K, self.d.F
+        xv = x.reshape(B, K, F + 1).float() * self.pmask.view(B, K, F + 1)
+        sc = torch.cat([self.inv_std.view(B, F), torch.ones(B, 1, device=xv.device)], 1)
+        self.weff[:, :, :K].copy_((xv * sc[:, None, :]).transpose(1, 2))
+        self._evaluate(1)
+        return self.loss, self.G
+
     def solve(self, x0: torch.Tensor, poll: int = 0):
         """Per iteration: phase 1 (direction + T trial points), evaluate + gradient of the B*T
         trials, phase 2 (pick + history + the next direction's dots; each model's last chunk

@@ -286,3 +286,228 @@ def minimize_trials(evaluate, x0: torch.Tensor, l2v: torch.Tensor, l1v: Optional
     H = torch.stack(fhist).cpu()  # [iterations + 1, B]
     return TrialResult(x=x, f=Fo, iterations=iters, n_evals=n_evals, history=H.mean(1).tolist(),
                        history_per_model=[H[:, b].tolist() for b in range(B)])
+
+
+# ------------------------------------------------------------------------------------------
+# Breeze-semantics line searches (LogisticRegression(lineSearch="wolfe"))
+# ------------------------------------------------------------------------------------------
+# Spark's LogisticRegression.train runs Breeze's LBFGS (elasticNetParam = 0) or OWLQN (> 0):
+#   * LBFGS.determineStepSize: StrongWolfeLineSearch(maxZoomIter = 10, maxLineSearchIter = 10),
+#     c1 = 1e-4, c2 = 0.9, initial step 1 / |dir| on the first iteration and 1 afterwards; the
+#     bracketing phase grows the step by 1.5, the zoom phase picks the safeguarded cubic
+#     interpolant of the bracket (clamped to its inner 80 %);
+#   * OWLQN.determineStepSize: BacktrackingLineSearch on the orthant-projected step, Armijo
+#     (c 1e-4) plus the weak Wolfe curvature condition (c 0.9: grow the step by 2.1 while it fails),
+#     shrink 0.1 on the first iteration and 0.5 afterwards, initial step 0.5 / |grad| on the first
+#     iteration and 1 afterwards, at most 20 trial steps; the directional derivative is the
+#     pseudo-gradient of the trial point along the search direction.
+# A search that fails (a bracket / zoom / backtracking budget spent, a non-descent direction)
+# resets that model's history and retries from steepest descent; a second consecutive failure stops
+# the model (Breeze: FirstOrderMinimizer's failedOnce).  Convergence, per model, Breeze's
+# defaultConvergenceCheck form: (max F over the last 20 iterates - F) / max(|F|, |that max|, 1e-6)
+# <= tol, or |adjusted gradient|_inf / max(|x|_2, 1) <= tol, or maxIter.
+# Breeze's source is not in this environment: the constants and control flow above are restated
+# from its documented algorithm, so coefficient / objectiveHistory parity with Spark stays
+# unpinned (no reference fixture holds them; PARITY.md).
+#
+# Batched: every model advances its own line-search state machine; each ROUND evaluates ONE trial
+# point per model still searching, all models in ONE evaluation call (the device kernels on the
+# GPU), so the rounds of an iteration are max over models, not the sum.
+
+
+def _cubic_step(lt, lf, ld, rt, rf, rd):
+    """Breeze CubicLineSearch.interp of brackets l < r: the cubic minimizer, clamped to
+    [l + 0.1 (r - l), l + 0.9 (r - l)]; a non-real / non-finite interpolant falls back to the midpoint."""
+    d1 = ld + rd - 3.0 * (lf - rf) / (lt - rt)
+    disc = d1 * d1 - ld * rd
+    d2 = torch.sqrt(disc.clamp_min(0.0))
+    t = rt - (rt - lt) * (rd + d2 - d1) / (rd - ld + 2.0 * d2)
+    lb, ub = lt + 0.1 * (rt - lt), lt + 0.9 * (rt - lt)
+    t = torch.minimum(torch.maximum(t, lb), ub)
+    return torch.where(torch.isfinite(t) & (disc >= 0), t, 0.5 * (lt + rt))
+
+
+def _interp_bracket(lo_t, lo_f, lo_d, hi_t, hi_f, hi_d):
+    """interp(low, hi) if low.t <= hi.t else interp(hi, low) (Breeze's zoom)."""
+    sw = lo_t > hi_t
+    a = [torch.where(sw, h, l) for l, h in ((lo_t, hi_t), (lo_f, hi_f), (lo_d, hi_d))]
+    b = [torch.where(sw, l, h) for l, h in ((lo_t, hi_t), (lo_f, hi_f), (lo_d, hi_d))]
+    return _cubic_step(*a, *b)
+
+
+def minimize_wolfe(evaluate, x0: torch.Tensor, l2v: torch.Tensor, l1v: Optional[torch.Tensor] = None,
+                   max_iter: int = 100, m: int = 10, tol: float = 1e-6, c1: float = 1e-4, c2: float = 0.9,
+                   max_ls: int = 10, max_zoom: int = 10, max_backtrack: int = 20, fval_memory: int = 20
+                   ) -> TrialResult:
+    """Minimize ``B`` problems ``data(x_b) + 0.5 sum l2v x^2 + sum l1v |x|`` with Breeze's line
+    searches (module comment above): strong Wolfe for the models without an L1 term (L-BFGS),
+    projected backtracking with the weak Wolfe condition for the models with one (OWL-QN).
+
+    ``evaluate(x [B, D]) -> (loss [B] float64, grad [B, D])`` is the DATA part (as in
+    ``minimize_trials`` with one trial).  float32 vectors, float64 reductions and line-search
+    scalars; every operation is a batched tensor op on x's device.  ``n_evals`` counts the
+    batched evaluations (the initial one plus one per line-search round)."""
+    B, D = x0.shape
+    dev = x0.device
+    f64 = torch.float64
+    x = x0.clone().float()
+    owl = (l1v > 0).any(1) if l1v is not None else torch.zeros(B, dtype=torch.bool, device=dev)
+    l1 = l1v if (l1v is not None and bool(owl.any())) else None
+    pg_fn = lambda xx, gg: _pseudo_grad(xx, gg, l1)  # noqa: E731
+    dot = lambda a, b: (a.double() * b.double()).sum(1)  # noqa: E731
+    loss, G = evaluate(x)
+    g = G.float() + l2v * x
+    F = loss.double() + _reg_value(x, l2v, l1)
+    S = torch.zeros(m, B, D, device=dev)
+    Y = torch.zeros(m, B, D, device=dev)
+    rho = torch.zeros(m, B, dtype=f64, device=dev)
+    active = torch.ones(B, dtype=torch.bool, device=dev)
+    failed_once = torch.zeros(B, dtype=torch.bool, device=dev)
+    iters = torch.zeros(B, dtype=torch.int64, device=dev)
+    head, filled, n_evals = 0, 0, 1
+    fhist = [F.clone()]
+    rounds_per_iter = []
+    for it in range(max_iter):
+        pg = pg_fn(x, g)
+        # ---- two-loop recursion (Breeze: unscaled -grad while the history is empty) ----
+        q = pg.clone()
+        alphas = []
+        for i in range(filled):
+            j = (head - 1 - i) % m
+            a = rho[j] * dot(S[j], q)
+            alphas.append(a)
+            q = torch.where((rho[j] != 0)[:, None], (q.double() - a[:, None] * Y[j].double()).float(), q)
+        if filled:
+            j = (head - 1) % m
+            yy = (Y[j].double() ** 2).sum(1)
+            sy = dot(S[j], Y[j])
+            gamma = torch.where((rho[j] > 0) & (yy > 0), sy / yy.clamp_min(1e-300), torch.ones_like(yy))
+            q = (gamma[:, None] * q.double()).float()
+        for i in reversed(range(filled)):
+            j = (head - 1 - i) % m
+            coef = alphas[i] - rho[j] * dot(Y[j], q)
+            q = torch.where((rho[j] != 0)[:, None], (q.double() + coef[:, None] * S[j].double()).float(), q)
+        d = -q
+        d = torch.where(owl[:, None] & ~(d * pg < 0), torch.zeros_like(d), d)
+        dd0 = dot(pg, d)
+        nondesc = active & ~(dd0 < 0)          # Breeze throws -> the retry from steepest descent
+        d = torch.where(nondesc[:, None], -pg, d)
+        dd0 = torch.where(nondesc, -dot(pg, pg), dd0)
+        xi = torch.where(x != 0, torch.sign(x), torch.sign(-pg))
+        first = iters == 0
+        dn = dot(d, d).sqrt().clamp_min(1e-300)
+        gn = dot(g, g).sqrt().clamp_min(1e-300)
+        t = torch.where(owl, torch.where(first, 0.5 / gn, torch.ones_like(gn)),
+                        torch.where(first, 1.0 / dn, torch.ones_like(dn)))
+        shrink = torch.where(first, torch.full_like(t, 0.1), torch.full_like(t, 0.5))
+        # ---- per-model line-search state ----
+        searching = active.clone()
+        success = torch.zeros(B, dtype=torch.bool, device=dev)
+        zoom = torch.zeros(B, dtype=torch.bool, device=dev)
+        n_try = torch.zeros(B, dtype=torch.int64, device=dev)   # bracket / backtracking trials
+        n_zoom = torch.zeros(B, dtype=torch.int64, device=dev)
+        lo_t, lo_f, lo_d = torch.zeros_like(t), F.clone(), dd0.clone()   # phi(0)
+        hi_t, hi_f, hi_d = torch.zeros_like(t), F.clone(), dd0.clone()
+        x_acc, g_acc, F_acc = x.clone(), g.clone(), F.clone()
+        rounds = 0
+        while bool(searching.any()):
+            rounds += 1
+            xt = x + t.float()[:, None] * d
+            xt = torch.where(owl[:, None] & (torch.sign(xt) != xi), torch.zeros_like(xt), xt)
+            xt = torch.where(searching[:, None], xt, x)
+            lt, Gt = evaluate(xt)
+            n_evals += 1
+            gt = Gt.float() + l2v * xt
+            Ft = lt.double() + _reg_value(xt, l2v, l1)
+            dt = torch.where(owl, dot(pg_fn(xt, gt), d), dot(gt, d))
+            fin = torch.isfinite(Ft)
+            armijo = Ft <= F + c1 * t * dd0
+            curv_strong = dt.abs() <= c2 * dd0.abs()
+            done_now = torch.zeros_like(searching)
+            fail_now = torch.zeros_like(searching)
+            # -- OWL-QN: backtracking with the weak Wolfe condition --
+            bt = searching & owl
+            bt_ok = bt & fin & armijo & (dt >= c2 * dd0)
+            mult = torch.where(~(fin & armijo), shrink, torch.full_like(t, 2.1))
+            done_now |= bt_ok
+            n_try = n_try + bt.long()
+            bt_next = bt & ~bt_ok
+            fail_now |= bt_next & ((n_try > max_backtrack) | (t * mult < 1e-10) | (t * mult > 1e10))
+            t_bt = t * mult
+            # -- L-BFGS: strong Wolfe, bracketing phase --
+            br = searching & ~owl & ~zoom
+            n_try = n_try + br.long()
+            halve = br & ~fin
+            to_zoom_a = br & fin & (~armijo | ((Ft >= lo_f) & (n_try > 1)))      # zoom(low, c)
+            ok_br = br & fin & ~to_zoom_a & curv_strong
+            to_zoom_b = br & fin & ~to_zoom_a & ~curv_strong & (dt >= 0)       # zoom(c, low)
+            grow = br & fin & ~to_zoom_a & ~ok_br & ~to_zoom_b
+            done_now |= ok_br
+            # zoom(low, c): low stays, hi = c;  zoom(c, low): hi = low, low = c
+            nhi_t = torch.where(to_zoom_a, t, torch.where(to_zoom_b, lo_t, hi_t))
+            nhi_f = torch.where(to_zoom_a, Ft, torch.where(to_zoom_b, lo_f, hi_f))
+            nhi_d = torch.where(to_zoom_a, dt, torch.where(to_zoom_b, lo_d, hi_d))
+            nlo_t = torch.where(to_zoom_b | grow, t, lo_t)
+            nlo_f = torch.where(to_zoom_b | grow, Ft, lo_f)
+            nlo_d = torch.where(to_zoom_b | grow, dt, lo_d)
+            # -- L-BFGS: zoom phase (the trial t was interpolated from the bracket) --
+            zm = searching & ~owl & zoom
+            n_zoom = n_zoom + zm.long()
+            z_hi = zm & (~fin | ~armijo | (Ft >= lo_f))
+            z_ok = zm & ~z_hi & curv_strong
+            z_mv = zm & ~z_hi & ~z_ok
+            z_swap = z_mv & (dt * (hi_t - lo_t) >= 0)                            # hi = low
+            done_now |= z_ok
+            nhi_t = torch.where(z_hi, t, torch.where(z_swap, lo_t, nhi_t))
+            nhi_f = torch.where(z_hi, Ft, torch.where(z_swap, lo_f, nhi_f))
+            nhi_d = torch.where(z_hi, dt, torch.where(z_swap, lo_d, nhi_d))
+            nlo_t = torch.where(z_mv, t, nlo_t)
+            nlo_f = torch.where(z_mv, Ft, nlo_f)
+            nlo_d = torch.where(z_mv, dt, nlo_d)
+            lo_t, lo_f, lo_d, hi_t, hi_f, hi_d = nlo_t, nlo_f, nlo_d, nhi_t, nhi_f, nhi_d
+            zoom = zoom | to_zoom_a | to_zoom_b
+            fail_now |= (br & ~done_now & ~to_zoom_a & ~to_zoom_b & (n_try >= max_ls))
+            fail_now |= ((zm | to_zoom_a | to_zoom_b) & ~done_now & (n_zoom >= max_zoom))
+            # next trial step
+            t_zoom = _interp_bracket(lo_t, lo_f, lo_d, hi_t, hi_f, hi_d)
+            t = torch.where(bt, t_bt, torch.where(halve, t / 2, torch.where(grow, t * 1.5,
+                                                                          torch.where(zoom, t_zoom, t))))
+            # accepted trial points
+            x_acc = torch.where(done_now[:, None], xt, x_acc)
+            g_acc = torch.where(done_now[:, None], gt, g_acc)
+            F_acc = torch.where(done_now, Ft, F_acc)
+            success |= done_now
+            searching = searching & ~done_now & ~fail_now
+        rounds_per_iter.append(rounds)
+        take = active & success
+        s_vec = x_acc - x
+        y_vec = g_acc - g
+        sy = dot(s_vec, y_vec)
+        good = take & (sy > 1e-10 * (dot(s_vec, s_vec).sqrt() * dot(y_vec, y_vec).sqrt()).clamp_min(1e-300))
+        # a failed search clears the model's history (Breeze: reset, retry from steepest descent)
+        failed = active & ~success
+        for j in range(m):
+            rho[j] = torch.where(failed, torch.zeros_like(rho[j]), rho[j])
+        S[head] = torch.where(take[:, None], s_vec, S[head])
+        Y[head] = torch.where(take[:, None], y_vec, Y[head])
+        rho[head] = torch.where(good, 1.0 / sy.clamp_min(1e-300), torch.where(take, torch.zeros_like(sy), rho[head]))
+        x = torch.where(take[:, None], x_acc, x)
+        g = torch.where(take[:, None], g_acc, g)
+        F = torch.where(take, F_acc, F)
+        iters = iters + take.long()
+        fhist.append(F.clone())
+        recent = torch.stack(fhist[-(fval_memory + 1):-1]).max(0).values if len(fhist) > 1 else F
+        fconv = (recent - F) / torch.maximum(torch.maximum(F.abs(), recent.abs()), torch.full_like(F, 1e-6)) <= tol
+        gconv = pg_fn(x, g).abs().amax(1).double() / dot(x, x).sqrt().clamp_min(1.0) <= tol
+        stop = (take & (fconv | gconv)) | (failed & failed_once)
+        failed_once = torch.where(take, torch.zeros_like(failed_once), failed_once | failed)
+        active = active & ~stop
+        head = (head + 1) % m
+        filled = min(filled + 1, m)
+        if not bool(active.any()):
+            break
+    H = torch.stack(fhist).cpu()
+    res = TrialResult(x=x, f=F, iterations=iters, n_evals=n_evals, history=H.mean(1).tolist(),
+                      history_per_model=[H[:, b].tolist() for b in range(B)])
+    res.rounds_per_iter = rounds_per_iter
+    return res
