@@ -420,3 +420,37 @@ def test_solver_cache_crossvalidator_repeat_is_bitwise(cuda, wisdm_csv):
     for m in (b, c):
         assert m.avgMetrics == a.avgMetrics
         assert torch.equal(m.bestModel.coefficientMatrix, a.bestModel.coefficientMatrix)
+
+
+@pytest.mark.parametrize("reg,alpha", [(0.3, 0.0), (0.1, 0.2)])
+def test_wolfe_line_search_device_matches_cpu_oracle(cuda, wisdm_csv, reg, alpha):
+    """LogisticRegression(lineSearch="wolfe") on the WISDM reference encoding: the device fit (the
+    evaluation kernels at each round's trial points, DeviceLogregSolver.evaluate_at) against the CPU
+    oracle (the same optim.lbfgs.minimize_wolfe with the torch objective): objective histories,
+    iterations and coefficients agree to the rounding of the two objective evaluations."""
+    from har.models.logreg import LogisticRegression
+    from har.ops import logreg as L
+    from har.suite import load_wisdm
+
+    n = {"at": 0}
+    real = L.DeviceLogregSolver.evaluate_at
+
+    def count(self, x):
+        n["at"] += 1
+        return real(self, x)
+
+    L.DeviceLogregSolver.evaluate_at = count
+    try:
+        trg, _, _ = load_wisdm(wisdm_csv, "reference", 2018, device=cuda)
+        mg = LogisticRegression(maxIter=20, regParam=reg, elasticNetParam=alpha, lineSearch="wolfe",
+                                device="cuda").fit(trg)
+    finally:
+        L.DeviceLogregSolver.evaluate_at = real
+    assert n["at"] >= mg.summary["iterations"] + 1
+    trc, _, _ = load_wisdm(wisdm_csv, "reference", 2018)
+    mc = LogisticRegression(maxIter=20, regParam=reg, elasticNetParam=alpha, lineSearch="wolfe",
+                            device="cpu").fit(trc)
+    hg, hc = mg.summary["objectiveHistory"], mc.summary["objectiveHistory"]
+    assert mg.summary["iterations"] == mc.summary["iterations"], (hg, hc)
+    np.testing.assert_allclose(hg, hc, rtol=2e-5)
+    torch.testing.assert_close(mg.coefficientMatrix.cpu(), mc.coefficientMatrix, rtol=2e-3, atol=2e-4)
