@@ -72,6 +72,14 @@ constexpr int FIMG = FRT * FSP;
 // softmax lanes (row, class) then read 16 distinct banks per row and disjoint banks per row pair
 constexpr int ZREG = 4 * 72;
 constexpr int FWD_SLAB = NCLS * HH + NCLS;  // per workgroup: dWout rows 0..15 [16][H], dbout [16]
+#ifndef HAR_FWD_PD
+#define HAR_FWD_PD 2
+#endif
+#ifndef HAR_FWD_PIN
+#define HAR_FWD_PIN 1
+#endif
+constexpr int FPD = HAR_FWD_PD;      // stage-2 h1 read prefetch distance (k chunks)
+constexpr bool FPIN = HAR_FWD_PIN;   // pin the read / MFMA interleave with scheduling groups
 constexpr size_t FWD_LDS = (size_t)2 * FRT * FHP * 2 + (size_t)2 * FW * 2 * ZREG * 4 + (size_t)2 * FIMG * 2 +
                            (size_t)FW * 4 * FIMG * 2;
 
@@ -186,17 +194,34 @@ __global__ __launch_bounds__(512) void mlp_fwd3_kernel(
     for (int h = 0; h < 2; ++h)
 #pragma unroll
       for (int t = 0; t < 2; ++t) acc[h][t] = f32x4_t{b1r[t].x, b1r[t].y, b1r[t].z, b1r[t].w};
+    // software-pipelined h1 reads (prefetch distance FPD k chunks, pinned by scheduling groups: the 2
+    // reads of chunk kc + FPD, then the 4 MFMAs of chunk kc).  Left to the scheduler each chunk's two
+    // reads were issued right before its MFMAs and every chunk waited out an LDS round trip (stage
+    // 2 + 3 ~1.9k cycles per wave for 34 MFMAs, profiles/r5)
+    bf16x8_t hb[KC][2];
+    if constexpr (FPIN) __builtin_amdgcn_sched_barrier(0);  // an isolated region: the groups take only these
+    auto ld_hb = [&](int kc) __attribute__((always_inline)) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+        hb[kc][h] = *reinterpret_cast<const bf16x8_t*>(hsrc + (16 * h + c16) * FHP +
+                                                        ((((kc + krot) & (KC - 1)) * 32 + 8 * g) ^ hsw));
+    };
+#pragma unroll
+    for (int kc = 0; kc < FPD; ++kc) ld_hb(kc);
+    if constexpr (FPIN) __builtin_amdgcn_sched_group_barrier(0x100, 2 * FPD, 0);  // the FPD chunks ahead
 #pragma unroll
     for (int kc = 0; kc < KC; ++kc) {
-      bf16x8_t hb[2];
+      if (kc + FPD < KC) {
+        ld_hb(kc + FPD);
+        if constexpr (FPIN) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+      }
 #pragma unroll
       for (int h = 0; h < 2; ++h)
-        hb[h] = *reinterpret_cast<const bf16x8_t*>(hsrc + (16 * h + c16) * FHP + ((((kc + krot) & (KC - 1)) * 32 + 8 * g) ^ hsw));
 #pragma unroll
-      for (int h = 0; h < 2; ++h)
-#pragma unroll
-        for (int t = 0; t < 2; ++t) acc[h][t] = mma32(w1f[t][kc], hb[h], acc[h][t]);
+        for (int t = 0; t < 2; ++t) acc[h][t] = mma32(w1f[t][kc], hb[kc][h], acc[h][t]);
+      if constexpr (FPIN) __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
     }
+    if constexpr (FPIN) __builtin_amdgcn_sched_barrier(0);
     uint32_t h2p[2][2][2];
 #pragma unroll
     for (int h = 0; h < 2; ++h)
@@ -984,6 +1009,10 @@ __global__ __launch_bounds__(512) void mlp_bwd4_kernel(
       bf16_t* d1s = d1s0 + (i & 1) * L::HS;
       constexpr int PD = 3;  // prefetch distance (k chunks)
       const int swz = 8 * ((c16 >> 2) & 1);
+      // (an isolated scheduling region whose first group is the hm reads + the PD chunks ahead: without
+      // it the scheduler put each chunk's own reads into the per-chunk read groups, right before their
+      // MFMAs — no prefetch at all, profiles/r5)
+      __builtin_amdgcn_sched_barrier(0);
       uint2 hm[2][2];
 #pragma unroll
       for (int rr = 0; rr < 2; ++rr)
@@ -996,6 +1025,7 @@ __global__ __launch_bounds__(512) void mlp_bwd4_kernel(
 #pragma unroll
         for (int rr = 0; rr < 2; ++rr)
           bv[rr][kc] = *reinterpret_cast<const bf16x8_t*>(dsm + (16 * (ra0 + rr) + c16) * BDP + ((kc * 32 + 8 * g) ^ swz));
+      __builtin_amdgcn_sched_group_barrier(0x100, 2 * PD + 4, 0);
       f32x4_t acc[2][2];
 #pragma unroll
       for (int rr = 0; rr < 2; ++rr)
@@ -1016,6 +1046,7 @@ __global__ __launch_bounds__(512) void mlp_bwd4_kernel(
           for (int e = 0; e < 2; ++e) acc[rr][e] = mma32(w1t[e][kc], bv[rr][kc], acc[rr][e]);
         __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);  // then the 4 MFMAs of chunk kc
       }
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int rr = 0; rr < 2; ++rr)
 #pragma unroll
@@ -1094,11 +1125,11 @@ __global__ __launch_bounds__(512) void mlp_bwd4_kernel(
   HAR_STAMP_REAL(8, 39)
 }
 
-// HAR_MLP_FWD_STAGGER=0 runs every wave of the forward in one phase order (the round-4 kernel)
+// HAR_MLP_FWD_STAGGER=1: waves 4..7 run their softmax after the MFMA stages (off by default)
 static int fwd_stagger() {
   static const int v = [] {
     const char* e = getenv("HAR_MLP_FWD_STAGGER");
-    return e ? atoi(e) : 1;
+    return e ? atoi(e) : 0;  // measured slower (fwd 21.9 vs 21.1 us, profiles/r5/mlp_fwd_variants.md)
   }();
   return v;
 }
