@@ -216,8 +216,9 @@ class MLPEngine:
                 self.sslab = torch.zeros(nwg, mod.mlp_step_fwd_slab_width(256), dtype=torch.float32, device=dev)
                 self.sblock_loss = torch.zeros(nwg, dtype=torch.float32, device=dev)
                 self.sblock_correct = torch.zeros(nwg, dtype=torch.int32, device=dev)
-                self.dz = torch.zeros(self.B * 8, dtype=torch.int32, device=dev)      # 16 bf16 per row
-                self.h2mask = torch.zeros(self.B * 8, dtype=torch.int32, device=dev)  # 256 bits per row
+                # the layer-2 gradient dact2 the forward writes for the backward (bf16 [B][256], the
+                # backward's LDS tile order: 16-byte chunks of rows with bit 2 set swapped in pairs)
+                self.dact2 = torch.zeros(self.B * L.hidden[-1], dtype=torch.bfloat16, device=dev)
                 # MFMA-fragment-ordered bf16 copies of W0 / W1 (W0 | W1 | W1^T; mlp.hip frag_pos): the step
                 # kernels load their weight operands from here, one 1 KB-contiguous load per fragment;
                 # every Adam update of the step refreshes them together with Pb
@@ -365,8 +366,8 @@ class MLPEngine:
 
     def _step(self, Xb, y32, scale, on_grad, record=None):
         """The three-kernel step of the H = 256 network (mlp_step.hip): mlp_step_fwd (layer 1, layer 2,
-        softmax-CE head, dWout / dbout; writes only dz and the relu' mask of h2), mlp_step_bwd (dact2
-        rebuilt from them, h1 recomputed, dW1 + dgrad + relu' + dW0 / db0 / db1 in one pass).  The
+        softmax-CE head, dWout / dbout, and dact2 = (dz . Wout) * relu'(h2) in bf16), mlp_step_bwd (h1
+        recomputed, dW1 + dgrad + relu' + dW0 / db0 / db1 in one pass).  The
         gradient reduction + Adam follow in ``train_step``.  ``record`` (a list) receives one
         re-launchable closure per kernel (tools/mlp_phase_probe.py)."""
         L, mod = self.layout, _native.kernels()
@@ -379,14 +380,14 @@ class MLPEngine:
 
         def fwd():
             mod.mlp_step_fwd(Xb.data_ptr(), K0, self.Pf.data_ptr(), w(P, "b0"), w(P, "b1"), H, w(Pb, "Wout"),
-                             w(P, "bout"), y32.data_ptr(), B, L.num_classes, float(scale), self.dz.data_ptr(),
-                             self.h2mask.data_ptr(), self.sslab.data_ptr(), self.sblock_loss.data_ptr(),
+                             w(P, "bout"), y32.data_ptr(), B, L.num_classes, float(scale), self.dact2.data_ptr(),
+                             self.sslab.data_ptr(), self.sblock_loss.data_ptr(),
                              self.sblock_correct.data_ptr(), _native.stream_ptr())
 
         def bwd():  # also sums the forward's dWout / dbout slabs into G
             off = lambda n: sb + 4 * L.by_name[n].offset  # noqa: E731
-            mod.mlp_step_bwd(self.dz.data_ptr(), self.h2mask.data_ptr(), Xb.data_ptr(), K0, self.Pf.data_ptr(), H,
-                             w(P, "b0"), w(Pb, "Wout"), B, off("W1"), off("W0"), off("b0"), off("b1"),
+            mod.mlp_step_bwd(self.dact2.data_ptr(), Xb.data_ptr(), K0, self.Pf.data_ptr(), H,
+                             w(P, "b0"), B, off("W1"), off("W0"), off("b0"), off("b1"),
                              total, self.step_count.data_ptr(), self.sslab.data_ptr(), self.sslab.shape[1],
                              w(self.G, "Wout"), w(self.G, "bout"), _native.stream_ptr())
 
@@ -643,7 +644,7 @@ class MLPEngine:
             P, Pb = self.P, self.Pb
             d = dict(Wf=self.Pf.data_ptr(), w0_off=L.by_name["W0"].offset, w1_off=L.by_name["W1"].offset,
                      b0=w(P, "b0"), b1=w(P, "b1"), Wo=w(Pb, "Wout"), bo=w(P, "bout"),
-                     dz=self.dz.data_ptr(), mask=self.h2mask.data_ptr(), fslab=self.sslab.data_ptr(),
+                     dact2=self.dact2.data_ptr(), fslab=self.sslab.data_ptr(),
                      bloss=self.sblock_loss.data_ptr(), bcorr=self.sblock_correct.data_ptr(), gw1=off("W1"),
                      gw0=off("W0"), gb0=off("b0"), gb1=off("b1"), step=self.step_count.data_ptr(),
                      fslab_w=self.sslab.shape[1], gwo=w(self.G, "Wout"), gbo=w(self.G, "bout"),

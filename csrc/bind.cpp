@@ -254,7 +254,7 @@ static void logreg_solve_run(LogregSolvePlan& p, int max_iter, int m, hipStream_
 // pointers changing (three pybind calls with ~20 arguments each and a region list rebuilt in Python
 // every step were ~10 us of host time per 70 us step: enough to starve the GPU when not graph-captured).
 struct MlpStepPlan {
-  u Wf, b0, b1, Wo, bo, dz, mask, fslab, bloss, bcorr, gw1, gw0, gb0, gb1, step, G, Pw, m, v, Pb;
+  u Wf, b0, b1, Wo, bo, dact2, fslab, bloss, bcorr, gw1, gw0, gb0, gb1, step, G, Pw, m, v, Pb;
   int K0, H, C, fslab_w;
   MlpFragSpec frag;
   u gwo, gbo;
@@ -269,13 +269,11 @@ struct MlpStepPlan {
     if (mode & 3) {
       check(har_mlp_step_fwd(P<const uint16_t>(X), K0, P<uint16_t>(Wf), P<const float>(b0), P<const float>(b1), H,
                              P<const uint16_t>(Wo), P<const float>(bo), P<const int32_t>(y), B, C, scale,
-                             P<uint32_t>(dz), P<uint32_t>(mask), P<float>(fslab), P<float>(bloss), P<int32_t>(bcorr),
-                             s),
+                             P<uint16_t>(dact2), P<float>(fslab), P<float>(bloss), P<int32_t>(bcorr), s),
             "mlp_step_fwd");
-      check(har_mlp_step_bwd(P<const uint32_t>(dz), P<const uint32_t>(mask), P<const uint16_t>(X), K0,
-                             P<const uint16_t>(Wf), H, P<const float>(b0), P<const uint16_t>(Wo), B, P<float>(gw1),
-                             P<float>(gw0), P<float>(gb0), P<float>(gb1), stride, P<int32_t>(step),
-                             P<const float>(fslab), fslab_w, P<float>(gwo), P<float>(gbo), s),
+      check(har_mlp_step_bwd(P<const uint16_t>(dact2), P<const uint16_t>(X), K0, P<const uint16_t>(Wf), H,
+                             P<const float>(b0), B, P<float>(gw1), P<float>(gw0), P<float>(gb0), P<float>(gb1),
+                             stride, P<int32_t>(step), P<const float>(fslab), fslab_w, P<float>(gwo), P<float>(gbo), s),
             "mlp_step_bwd");
     }
     const int gm = mode == 1 ? 1 | 4 : mode == 2 ? 1 | 2 : 4;  // GR_REDUCE 1, GR_STORE 2, GR_ADAM 4
@@ -709,12 +707,12 @@ PYBIND11_MODULE(_har_native, m) {
   py::class_<MlpStepPlan>(m, "MlpStepPlan")
       .def(py::init([](py::dict d) {
         MlpStepPlan p;
-        for (const char* k : {"Wf", "b0", "b1", "Wo", "bo", "dz", "mask", "fslab", "bloss", "bcorr", "gw1", "gw0",
+        for (const char* k : {"Wf", "b0", "b1", "Wo", "bo", "dact2", "fslab", "bloss", "bcorr", "gw1", "gw0",
                               "gb0", "gb1", "step", "G", "P", "m", "v", "Pb"}) {
           const u x = d[k].cast<u>();
           if (!strcmp(k, "Wf")) p.Wf = x; else if (!strcmp(k, "b0")) p.b0 = x;
           else if (!strcmp(k, "b1")) p.b1 = x; else if (!strcmp(k, "Wo")) p.Wo = x; else if (!strcmp(k, "bo")) p.bo = x;
-          else if (!strcmp(k, "dz")) p.dz = x; else if (!strcmp(k, "mask")) p.mask = x;
+          else if (!strcmp(k, "dact2")) p.dact2 = x;
           else if (!strcmp(k, "fslab")) p.fslab = x; else if (!strcmp(k, "bloss")) p.bloss = x;
           else if (!strcmp(k, "bcorr")) p.bcorr = x; else if (!strcmp(k, "gw1")) p.gw1 = x;
           else if (!strcmp(k, "gw0")) p.gw0 = x; else if (!strcmp(k, "gb0")) p.gb0 = x; else if (!strcmp(k, "gb1")) p.gb1 = x;
@@ -751,11 +749,11 @@ PYBIND11_MODULE(_har_native, m) {
   m.def("mlp_step_slices", &har_mlp_step_slices);
   m.def("mlp_step_fwd_slab_width", &har_mlp_step_fwd_slab_width);
   m.def("mlp_step_fwd", [](u X, int K0, u Wf, u b0, u b1, int H, u Wo, u bo, u labels, int B, int C, float scale,
-                           u dz, u mask, u slab, u block_loss, u block_correct, u stream) {
+                           u dact2, u slab, u block_loss, u block_correct, u stream) {
     check(har_mlp_step_fwd(P<const uint16_t>(X), K0, P<uint16_t>(Wf), P<const float>(b0), P<const float>(b1), H,
                            P<const uint16_t>(Wo), P<const float>(bo), P<const int32_t>(labels), B, C, scale,
-                           P<uint32_t>(dz), P<uint32_t>(mask), P<float>(slab), P<float>(block_loss),
-                           P<int32_t>(block_correct), S(stream)),
+                           P<uint16_t>(dact2), P<float>(slab), P<float>(block_loss), P<int32_t>(block_correct),
+                           S(stream)),
           "mlp_step_fwd");
   });
   m.def("mlp_step_fwd_infer", [](u X, int K0, u Wf, u b0, u b1, int H, u Wo, u bo, int B, int C, u logits, u pred,
@@ -765,12 +763,11 @@ PYBIND11_MODULE(_har_native, m) {
                                  P<float>(logits), P<int32_t>(pred), S(stream)),
           "mlp_step_fwd_infer");
   });
-  m.def("mlp_step_bwd", [](u dz, u mask, u X, int K0, u Wf, int H, u b0, u Wo, int B, u gw1, u gw0, u gb0, u gb1,
+  m.def("mlp_step_bwd", [](u dact2, u X, int K0, u Wf, int H, u b0, int B, u gw1, u gw0, u gb0, u gb1,
                            int64_t stride, u tick, u fslab, int fslab_w, u gwo, u gbo, u stream) {
-    check(har_mlp_step_bwd(P<const uint32_t>(dz), P<const uint32_t>(mask), P<const uint16_t>(X), K0,
-                           P<const uint16_t>(Wf), H, P<const float>(b0), P<const uint16_t>(Wo), B, P<float>(gw1),
-                           P<float>(gw0), P<float>(gb0), P<float>(gb1), stride, P<int32_t>(tick),
-                           P<const float>(fslab), fslab_w, P<float>(gwo), P<float>(gbo), S(stream)),
+    check(har_mlp_step_bwd(P<const uint16_t>(dact2), P<const uint16_t>(X), K0, P<const uint16_t>(Wf), H,
+                           P<const float>(b0), B, P<float>(gw1), P<float>(gw0), P<float>(gb0), P<float>(gb1), stride,
+                           P<int32_t>(tick), P<const float>(fslab), fslab_w, P<float>(gwo), P<float>(gbo), S(stream)),
           "mlp_step_bwd");
   });
   m.def("mlp_fwd_head", [](u X, int K0, u W0, u b0, u W1, u b1, int H, u Wo, u bo, u labels, int B, int C,

@@ -103,25 +103,24 @@ int har_mlp_fwd_head(const uint16_t* X, int K0, const uint16_t* W0, const float*
                      int32_t* block_correct, hipStream_t s);
 int har_mlp_fwd_head_grid(int B);
 // Fused training step of the H = 256 MLP (mlp_step.hip; K0 = 32/64, C <= 16, B % 64 == 0):
-// har_mlp_step_fwd writes dz [B][8] u32 (16 bf16 logit gradients), the relu'(h2) mask [B][8] u32, per
-// workgroup slabs [har_mlp_step_grid(B)][har_mlp_step_fwd_slab_width(H)] (dWout rows 0..15, dbout) and
-// per-workgroup loss / #correct; har_mlp_step_bwd rebuilds dact2 from them and writes per row slice
+// har_mlp_step_fwd writes dact2 [B][256] bf16 (the layer-2 gradient (dz . Wout) * relu'(h2), 16-byte
+// chunks of rows with bit 2 set swapped in pairs), per workgroup slabs
+// [har_mlp_step_grid(B)][har_mlp_step_fwd_slab_width(H)] (dWout rows 0..15, dbout) and per-workgroup
+// loss / #correct; har_mlp_step_bwd reads dact2 and X and writes per row slice
 // s < har_mlp_step_slices(B) the partials of dW1, dW0, db0, db1 at gw1 / gw0 / gb0 / gb1 + s * slab_stride
 // (h1 recomputed from X).
 // Wf: the MlpFragSpec::dst fragment copies of W0 / W1 (the step's weight operands); the forward
 // (re)writes the W1^T part from its W1 registers, the backward of the same step reads it.
 int har_mlp_step_fwd(const uint16_t* X, int K0, uint16_t* Wf, const float* b0, const float* b1, int H,
                      const uint16_t* Wo, const float* bo, const int32_t* labels, int B, int C, float scale,
-                     uint32_t* dz, uint32_t* mask, float* slab, float* block_loss, int32_t* block_correct,
-                     hipStream_t s);
+                     uint16_t* dact2, float* slab, float* block_loss, int32_t* block_correct, hipStream_t s);
 // serving forward on the same pipeline: logits [B][C] fp32 + argmax [B] (B % 64 == 0, H == 256)
 int har_mlp_step_fwd_infer(const uint16_t* X, int K0, const uint16_t* Wf, const float* b0, const float* b1, int H,
                            const uint16_t* Wo, const float* bo, int B, int C, float* logits, int32_t* pred,
                            hipStream_t s);
-int har_mlp_step_bwd(const uint32_t* dz, const uint32_t* mask, const uint16_t* X, int K0, const uint16_t* Wf, int H,
-                     const float* b0, const uint16_t* Wo, int B, float* gw1, float* gw0, float* gb0, float* gb1,
-                     int64_t slab_stride, int32_t* tick, const float* fslab, int fslab_w, float* gwo, float* gbo,
-                     hipStream_t s);
+int har_mlp_step_bwd(const uint16_t* dact2, const uint16_t* X, int K0, const uint16_t* Wf, int H, const float* b0,
+                     int B, float* gw1, float* gw0, float* gb0, float* gb1, int64_t slab_stride, int32_t* tick,
+                     const float* fslab, int fslab_w, float* gwo, float* gbo, hipStream_t s);
 int har_mlp_step_grid(int B);
 int har_mlp_step_slices(int B);
 int har_mlp_step_fwd_slab_width(int H);

@@ -95,7 +95,7 @@ __global__ __launch_bounds__(512) void mlp_fwd3_kernel(
     const bf16_t* __restrict__ X, bf16_t* __restrict__ Wf, const float* __restrict__ b0,
     const float* __restrict__ b1, const bf16_t* __restrict__ Wo,
     const float* __restrict__ bo, const int32_t* __restrict__ labels, int B, int C, float scale,
-    uint32_t* __restrict__ dz_out, uint32_t* __restrict__ mask_out, float* __restrict__ slab,
+    bf16_t* __restrict__ dact2_out, float* __restrict__ slab,
     float* __restrict__ block_loss, int32_t* __restrict__ block_correct, uint64_t* __restrict__ stamps,
     int stagger) {
   constexpr int K0C = K0 / 32, KC = HH / 32;
@@ -113,7 +113,6 @@ __global__ __launch_bounds__(512) void mlp_fwd3_kernel(
   // softmax lane: tile row sr = 4 wave + g (half sh, row srr of it), class c16
   const int sr = 4 * wave + g, sh = sr >> 4, srr = sr & 15;
   const int hsw = 8 * ((c16 >> 2) & 1);  // h1 tile chunk swap of this lane's rows (16h + c16)
-  const LaneSwap swp(lane);
   f32x4_t acc5[2] = {f32x4_t{0.f, 0.f, 0.f, 0.f}, f32x4_t{0.f, 0.f, 0.f, 0.f}};
   float dbo = 0.f, lsum = 0.f, ncorr = 0.f;
   const int ntiles = B / FRT;
@@ -167,6 +166,15 @@ __global__ __launch_bounds__(512) void mlp_fwd3_kernel(
   const uint2 whi = *reinterpret_cast<const uint2*>(Wo + (size_t)c16 * HH + u0 + 16 + 4 * g);
   const bf16x8_t wo3 = cat8(wlo.x, wlo.y, whi.x, whi.y);
   const float bo_s = c16 < C ? bo[c16] : 0.f;
+  // dact2 A fragments (16x16x16, K = the 16 classes): A[m = unit 16 t + c16][k = class 4 g + i] =
+  // Wout[4 g + i][u0 + 16 t + c16]
+  s16x4_t woT[2];
+  if constexpr (!INFER) {
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) woT[t][i] = (short)Wo[(size_t)(4 * g + i) * HH + u0 + 16 * t + c16];
+  }
   __builtin_amdgcn_sched_barrier(0);
   if constexpr (STAMP) __builtin_amdgcn_s_waitcnt(0x0f70);
   HAR_STAMP(FW, 1)
@@ -230,25 +238,6 @@ __global__ __launch_bounds__(512) void mlp_fwd3_kernel(
         h2p[h][t][0] = relu2(pack2(acc[h][t][0], acc[h][t][1]));
         h2p[h][t][1] = relu2(pack2(acc[h][t][2], acc[h][t][3]));
       }
-    // relu'(h2) of the wave's 32 units for rows 16h + c16 -> mask word `wave` of the row (every lane
-    // of the row stores the same word).  Bit 16 t + 4 g + 2 e + b = element b of pair h2p[h][t][e]
-    // is nonzero: after relu each 16-bit half is in [0, 0x7fff], so adding 0x7fff carries into the
-    // half's bit 15 exactly when it is nonzero (no carry crosses the halves); the four bits of a
-    // (t) pair of words are then gathered with shifts instead of a compare + select per element.
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      uint32_t m = 0;
-#pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        const uint32_t ta = h2p[h][t][0] + 0x7fff7fffu, tb = h2p[h][t][1] + 0x7fff7fffu;
-        // c: bit 0 = (e 0, lo), 16 = (e 0, hi), 2 = (e 1, lo), 18 = (e 1, hi)
-        const uint32_t c = ((ta >> 15) & 0x10001u) | ((tb >> 13) & 0x40004u);
-        m |= ((c | (c >> 15)) & 0xfu) << (16 * t + 4 * g);
-      }
-      m |= swp.x16(m);
-      m |= swp.x32(m);
-      if constexpr (!INFER) mask_out[(size_t)(r0 + 16 * h + c16) * 8 + wave] = m;
-    }
     float* zb = zs + buf * FW * 2 * ZREG;
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
@@ -293,16 +282,34 @@ __global__ __launch_bounds__(512) void mlp_fwd3_kernel(
     ncorr += (c16 == 0 && amx == yc) ? 1.f : 0.f;
     dbo += bf2f(db);
     dzs[buf * FIMG + sr * FSP + c16] = db;
-    const uint32_t other = (uint32_t)dpp_i<DPP_QUAD_XOR1>((int)db) & 0xffffu;
-    const uint32_t pair = (c16 & 1) ? (other | ((uint32_t)db << 16)) : ((uint32_t)db | (other << 16));
-    dz_out[(size_t)(r0 + sr) * 8 + (c16 >> 1)] = pair;  // both lanes of a pair store the same word
   };
-  // ---- stage 5 of a tile (dz buffer / image buffer `buf`): dWout^T += h2^T . dz over its 32 rows ----
-  auto stage5 = [&](int buf) __attribute__((always_inline)) {
-    const bf16x8_t bz = frag_tr(dzs + buf * FIMG, FSP, 0, lane);
+  // ---- stage 5 of a tile (dz buffer / image buffer `buf`, rows r0 ..): dWout^T += h2^T . dz over its
+  // 32 rows, and the backward's layer-2 gradient dact2 = (dz . Wout) * relu'(h2) of the wave's 32
+  // units -> dact2_out (bf16 [B][256], the 16-byte chunks of rows with bit 2 set swapped in pairs —
+  // the backward's LDS tile image, so its producers copy rows verbatim).  One 16x16x16 MFMA per
+  // (16 units x 16 rows) block, K = the 16 classes: C[unit 4 g + r][row c16], i.e. 4 consecutive
+  // units of one row per lane, the same (row, units) the lane's own h2 image words hold ----
+  bf16_t* const d2base = INFER ? nullptr : dact2_out + (size_t)c16 * HH + ((u0 + 4 * g) ^ hsw);
+  auto stage5 = [&](int buf, int r0) __attribute__((always_inline)) {
+    const bf16_t* zb = dzs + buf * FIMG;
+    const bf16x8_t bz = frag_tr(zb, FSP, 0, lane);
     const bf16_t* ip = img + buf * 2 * FIMG;
 #pragma unroll
     for (int t = 0; t < 2; ++t) acc5[t] = mma32(frag_tr(ip + t * FIMG, FSP, 0, lane), bz, acc5[t]);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const s16x4_t dzb = *reinterpret_cast<const s16x4_t*>(zb + (16 * h + c16) * FSP + 4 * g);
+      bf16_t* dst = d2base + (size_t)(r0 + 16 * h) * HH;
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const f32x4_t v = mma16(woT[t], dzb, f32x4_t{0.f, 0.f, 0.f, 0.f});
+        const uint2 hv = *reinterpret_cast<const uint2*>(ip + t * FIMG + (16 * h + c16) * FSP + 4 * g);
+        // relu'(h2): a relu'd bf16 half is in [0, 0x7fff]; adding 0x7fff carries into its bit 15 exactly
+        // when it is nonzero (no carry crosses the halves) -> 0xffff / 0 half masks
+        const uint32_t m0 = ((hv.x + 0x7fff7fffu) >> 15) & 0x00010001u, m1 = ((hv.y + 0x7fff7fffu) >> 15) & 0x00010001u;
+        *reinterpret_cast<uint2*>(dst + 16 * t) = make_uint2(pack2(v[0], v[1]) & (m0 * 0xffffu), pack2(v[2], v[3]) & (m1 * 0xffffu));
+      }
+    }
   };
 
   // Software pipeline, ONE barrier per tile.  Iteration k: softmax of tile k | stage 5 of tile k-1 |
@@ -358,7 +365,7 @@ __global__ __launch_bounds__(512) void mlp_fwd3_kernel(
     if constexpr (!INFER) ynext = labels[tile_of(k + 1) * FRT + sr];
     if constexpr (!decltype(late)::value) softmax(k, k & 1, yc);
     if (k == 4) HAR_STAMP(FW, 10)
-    if (!INFER && !first) stage5((k - 1) & 1);
+    if (!INFER && !first) stage5((k - 1) & 1, tile_of(k - 1) * FRT);
     if (k == 4) HAR_STAMP(FW, 11)
     if (!last) {
       stage23(k + 1, (k + 1) & 1);
@@ -391,7 +398,7 @@ __global__ __launch_bounds__(512) void mlp_fwd3_kernel(
     run(std::false_type{});
   HAR_STAMP(FW, 34)
   if constexpr (INFER) return;
-  if (nt > 0) stage5((nt - 1) & 1);
+  if (nt > 0) stage5((nt - 1) & 1, tile_of(nt - 1) * FRT);
   // ---- this workgroup's slab: dWout rows 0..15 x this wave's units, dbout; loss, #correct ----
   float* out = slab + (size_t)blockIdx.x * FWD_SLAB;
 #pragma unroll
@@ -437,350 +444,56 @@ constexpr int BRT = 64;               // rows per pipeline tile
 constexpr int BDP = HH + 16;          // dact2 tile pitch: 136 dwords (8 mod 64)
 constexpr int BUP = BQU + 16;         // h1 / dact1 quadrant tile pitch: 40 dwords
 
-template <int K0> struct Bwd3Lds {
+template <int K0> struct Bwd4Lds {
   static constexpr int XP = K0 + 16;
   static constexpr int NXB = 4;  // X tile buffers (staged two tiles ahead; read by h1 / (c) two tiles apart)
   static_assert((NXB & (NXB - 1)) == 0, "buffer indices are taken with & (NXB - 1)");
   static constexpr int DSM = BRT * BDP, HS = BRT * BUP, XS = BRT * XP;
-  static constexpr size_t bytes = (size_t)(2 * DSM + 2 * HS + 2 * HS + NXB * XS) * sizeof(bf16_t) +
-                                  4 * BQU * sizeof(float) + 32 * sizeof(uint32_t);
+  static constexpr size_t bytes = (size_t)(2 * DSM + 2 * HS + 2 * HS + NXB * XS) * sizeof(bf16_t);
   static_assert((size_t)NCLS * HH + HH * BQU <= (size_t)2 * DSM, "the prologue images fit the dact2 buffers");
 };
 
-template <int K0, bool STAMP>
-__global__ __launch_bounds__(512) void mlp_bwd3_kernel(
-    const uint32_t* __restrict__ dz, const uint32_t* __restrict__ mask, const bf16_t* __restrict__ X,
-    const bf16_t* __restrict__ Wf, const float* __restrict__ b0,
-    const bf16_t* __restrict__ Wo, int B, int S, float* __restrict__ gw1, float* __restrict__ gw0,
-    float* __restrict__ gb0, float* __restrict__ gb1, int64_t slab_stride, int32_t* __restrict__ tick,
-    const float* __restrict__ fslab, int fslab_w, int nfwd, float* __restrict__ gwo, float* __restrict__ gbo,
-    uint64_t* __restrict__ stamps) {
-  using L = Bwd3Lds<K0>;
-  constexpr int NXB = L::NXB, KC = HH / 32, XP = L::XP, NFW = K0 / 32;
-  constexpr int XV = BRT * K0 / 8;  // 16-byte vectors of an X tile (512 / 256)
-  // the training step counter ticks here (one thread, before the reduction kernel reads it for Adam)
-  if (tick && blockIdx.x == 0 && threadIdx.x == 0) *tick += 1;
-  extern __shared__ __attribute__((aligned(16))) bf16_t lds[];
-  bf16_t* const dsm0 = lds;                // [2][64][BDP] dact2 tiles
-  bf16_t* const hs0 = dsm0 + 2 * L::DSM;   // [2][64][BUP] h1 quadrant tiles
-  bf16_t* const d1s0 = hs0 + 2 * L::HS;    // [2][64][BUP] dact1 quadrant tiles
-  bf16_t* const xs0 = d1s0 + 2 * L::HS;    // [NXB][64][XP] X tiles
-  float* const red = reinterpret_cast<float*>(xs0 + NXB * L::XS);  // [4][64] db0 of the row blocks
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int c16 = lane & 15, g = lane >> 4;
-  // relu' nibble -> the two 32-bit AND masks of four packed bf16 (entry n: bit i of n keeps element i)
-  uint32_t* const lut = reinterpret_cast<uint32_t*>(red + 4 * BQU);  // [16][2]
-  if (tid < 16)
-    *reinterpret_cast<uint2*>(lut + 2 * tid) = make_uint2((tid & 1 ? 0xffffu : 0u) | (tid & 2 ? 0xffff0000u : 0u),
-                                                          (tid & 4 ? 0xffffu : 0u) | (tid & 8 ? 0xffff0000u : 0u));
-  HAR_STAMP_REAL(8, 38)
-  HAR_STAMP(8, 0)
-  const int b = xcd_remap(blockIdx.x, gridDim.x);
-  const int slice = b / BQ, q = b % BQ, qu0 = q * BQU;
-  const int rb = wave & 3, up = 2 * (wave >> 2);            // (a): rows 16 rb, unit blocks up, up + 1
-  const int ubp = 2 * (wave & 1), jb0 = 4 * (wave >> 1);    // (b): unit blocks ubp, ubp + 1 x j blocks jb0..
-  const int ub = wave & 3, fb = (wave >> 2) * NFW;          // (c): unit block ub x input blocks fb..
-  const int rb2 = wave & 3, jh = wave >> 2;                 // dact2: rows 16 rb2, j in [128 jh, 128 jh + 128)
-  const int ubh = wave & 3, rbh = 2 * (wave >> 2);          // h1 recompute: unit block ubh, row blocks rbh..
-  const int ntiles = B / BRT, per = (ntiles + S - 1) / S;
-  const int t0 = slice * per, n = max(0, min(ntiles, t0 + per) - t0);
-
-  // ---- prologue: the quadrant's (a) A fragments (W1^T, 32 KB contiguous in the fragment-ordered
-  // copy) and Wout through LDS — every byte fetched once per workgroup, 1 KB-contiguous loads —
-  // then the recompute's W0 fragments straight to registers ----
-  const bf16_t* const W0f = Wf;
-  const bf16_t* const W1tq = Wf + HH * K0 + HH * HH + (size_t)(4 * q) * KC * 512;
-  bf16_t* const wos = lds;                 // [16][256] Wout
-  bf16_t* const w1q = lds + NCLS * HH;     // [4 unit blocks][KC][64 lanes][8]: W1^T fragments
-  {
-    uint4 st[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) st[i] = *reinterpret_cast<const uint4*>(W1tq + (size_t)(i * 8 + wave) * 512 + lane * 8);
-    const uint4 so = *reinterpret_cast<const uint4*>(Wo + (size_t)tid * 8);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) *reinterpret_cast<uint4*>(w1q + (i * 8 + wave) * 512 + lane * 8) = st[i];
-    *reinterpret_cast<uint4*>(wos + tid * 8) = so;
-  }
-  bf16x8_t w0q[NFW];
-#pragma unroll
-  for (int kc = 0; kc < NFW; ++kc)
-    w0q[kc] = *reinterpret_cast<const bf16x8_t*>(W0f + (size_t)((4 * q + ubh) * NFW + kc) * 512 + frag_lane_off(lane));
-  const float4 b0q = *reinterpret_cast<const float4*>(b0 + qu0 + 16 * ubh + 4 * g);
-  // The forward's per-workgroup dWout / dbout partials are complete before this kernel starts: one
-  // wave per 16-byte gradient column sums them (lane l: slabs l, l + 64, ...; then a fixed xor tree)
-  // into G, so the reduction kernel reads one slab instead of har_mlp_step_grid(B).  The first
-  // column's loads are issued here and overlap the staging above.
-  constexpr int WO4 = NCLS * HH / 4, NC4 = WO4 + NCLS / 4;
-  const int gwv = blockIdx.x * 8 + wave, nwv = gridDim.x * 8;
-  f32x4_t px[4];
-  auto wo_load = [&](int c4) {
-    const float* src = fslab + (c4 < WO4 ? 4 * c4 : NCLS * HH + 4 * (c4 - WO4));
-#pragma unroll
-    for (int r = 0; r < 4; ++r)
-      px[r] = lane + 64 * r < nfwd ? *reinterpret_cast<const f32x4_t*>(src + (size_t)(lane + 64 * r) * fslab_w)
-                                   : f32x4_t{0.f, 0.f, 0.f, 0.f};
-  };
-  if (fslab && gwv < NC4) wo_load(gwv);
-  __syncthreads();
-  if (fslab) {
-    for (int c4 = gwv; c4 < NC4; c4 += nwv) {
-      if (c4 != gwv) wo_load(c4);
-      f32x4_t v = (px[0] + px[1]) + (px[2] + px[3]);
-#pragma unroll
-      for (int o = 32; o >= 1; o >>= 1)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] += __shfl_xor(v[e], o, 64);
-      if (lane == 0) *reinterpret_cast<f32x4_t*>(c4 < WO4 ? gwo + 4 * c4 : gbo + 4 * (c4 - WO4)) = v;
-    }
-  }
-  // (a) A fragments: A[u][k = j] = W1[32 kc + 8g + i][qu0 + 16 (up + e) + c16]
-  bf16x8_t w1t[2][KC];
-#pragma unroll
-  for (int e = 0; e < 2; ++e)
-#pragma unroll
-    for (int kc = 0; kc < KC; ++kc)
-      w1t[e][kc] = *reinterpret_cast<const bf16x8_t*>(w1q + ((up + e) * KC + kc) * 512 + frag_lane_off(lane));
-  // dact2 A fragments (16x16x16): A[m][k = class] = Wout[4g + i][j(m)] with the row -> j map of block
-  // t = 2p + s: j = 128 jh + 32 p + 8 (m >> 2) + 4 s + (m & 3), so lane group g of the block pair p
-  // holds the 8 consecutive j = 128 jh + 32 p + 8 g .. + 7: one 16-byte LDS store per pair
-  s16x4_t woa[8];
-#pragma unroll
-  for (int t = 0; t < 8; ++t)
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-      woa[t][i] = (short)wos[(4 * g + i) * HH + 128 * jh + 32 * (t >> 1) + 8 * (c16 >> 2) + 4 * (t & 1) + (c16 & 3)];
-  // db1 (quadrant 0): A = a row of ones (row 0 of the 16 x 32 tile)
-  const bf16x8_t ones = __builtin_bit_cast(bf16x8_t, c16 == 0 ? s16x8_t{0x3f80, 0x3f80, 0x3f80, 0x3f80, 0x3f80,
-                                                                        0x3f80, 0x3f80, 0x3f80}
-                                                              : s16x8_t{0, 0, 0, 0, 0, 0, 0, 0});
-  if constexpr (STAMP) __builtin_amdgcn_s_waitcnt(0x0f70);
-  HAR_STAMP(8, 1)
-  __syncthreads();  // the prologue images are read: the tile buffers may be written
-
-  f32x4_t acc1[4][2], acc0[NFW], accb[1];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) acc1[i][0] = acc1[i][1] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int f = 0; f < NFW; ++f) acc0[f] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-  accb[0] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-  f32x4_t accd0 = {0.f, 0.f, 0.f, 0.f};  // db0 of unit block ub (column 0: lanes c16 == 0)
-
-  // Register staging: one dz piece (8 B: classes 4g.. of row 16 rb2 + c16) + one mask piece (16 B:
-  // words 4 jh.. of the row) + one X vector per thread per tile.  Every load is unconditional (a tile
-  // index past the slice is clamped to a valid tile that is staged but never used), so the compiler's
-  // vmcnt accounting is exact on every path.
-  const int tlast = ntiles - 1;
-  const uint32_t* ldz = dz + (size_t)(16 * rb2 + c16) * 8 + 2 * g;
-  const uint32_t* lmk = mask + (size_t)(16 * rb2 + c16) * 8 + 4 * jh;
-  const bf16_t* lx = X + (size_t)(tid & (XV - 1)) * 8;
-  const int sdx = ((tid & (XV - 1)) / (K0 / 8)) * XP + ((tid & (XV - 1)) % (K0 / 8)) * 8;
-  uint2 dzr;
-  uint4 mkr, xr;
-#define HAR_B3_LOAD_D(t)                                                        \
-  {                                                                             \
-    const int64_t tt_ = min(t, tlast);                                          \
-    dzr = *reinterpret_cast<const uint2*>(ldz + tt_ * BRT * 8);                 \
-    mkr = *reinterpret_cast<const uint4*>(lmk + tt_ * BRT * 8);                 \
-  }
-#define HAR_B3_LOAD_X(t) xr = *reinterpret_cast<const uint4*>(lx + (int64_t)min(t, tlast) * BRT * K0);
-#define HAR_B3_STAGE_X(i) *reinterpret_cast<uint4*>(xs0 + ((i) & (NXB - 1)) * L::XS + sdx) = xr;
-
-  // dact2 tile from the dz / mask registers -> LDS buffer `buf`: row-major [r][j] with the 16-byte chunks
-  // of rows r with bit 2 set swapped in pairs (column ^ 8), which makes these 16-byte stores and the
-  // 16-byte row reads of (a) conflict-free; the transposed reads of (b) apply the same swap.  The relu'
-  // bits of a lane's four values of a block pick two AND masks from the LDS table (no per-element VALU).
-  auto stage_dact2 = [&](int buf) __attribute__((always_inline)) {
-    const int sw = 8 * ((c16 >> 2) & 1);
-    bf16_t* d = dsm0 + buf * L::DSM + (16 * rb2 + c16) * BDP;
-    const s16x4_t dzv = __builtin_bit_cast(s16x4_t, dzr);
-    const uint32_t mw[4] = {mkr.x >> (8 * g), mkr.y >> (8 * g), mkr.z >> (8 * g), mkr.w >> (8 * g)};
-#pragma unroll
-    for (int p = 0; p < 4; ++p) {
-      const f32x4_t v0 = mma16(woa[2 * p], dzv, f32x4_t{0.f, 0.f, 0.f, 0.f});
-      const f32x4_t v1 = mma16(woa[2 * p + 1], dzv, f32x4_t{0.f, 0.f, 0.f, 0.f});
-      const uint2 m0 = *reinterpret_cast<const uint2*>(lut + 2 * (mw[p] & 0xfu));
-      const uint2 m1 = *reinterpret_cast<const uint2*>(lut + 2 * ((mw[p] >> 4) & 0xfu));
-      *reinterpret_cast<u32x4_t*>(d + ((128 * jh + 32 * p + 8 * g) ^ sw)) =
-          u32x4_t{pack2(v0[0], v0[1]) & m0.x, pack2(v0[2], v0[3]) & m0.y, pack2(v1[0], v1[1]) & m1.x,
-                  pack2(v1[2], v1[3]) & m1.y};
-    }
-  };
-
-  // (a) + (b) (+ db1) of local tile i (LDS buffers i & 1)
-  auto tile_ab = [&](int i) __attribute__((always_inline)) {
-    const bf16_t* dsm = dsm0 + (i & 1) * L::DSM;
-    const bf16_t* hs = hs0 + (i & 1) * L::HS;
-    bf16_t* d1s = d1s0 + (i & 1) * L::HS;
-    f32x4_t a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int kc = 0; kc < KC; ++kc) {
-      const bf16x8_t bv =
-          *reinterpret_cast<const bf16x8_t*>(dsm + (16 * rb + c16) * BDP + ((kc * 32 + 8 * g) ^ (8 * ((c16 >> 2) & 1))));
-      a0 = mma32(w1t[0][kc], bv, a0);
-      a1 = mma32(w1t[1][kc], bv, a1);
-    }
-#pragma unroll
-    for (int e = 0; e < 2; ++e) {
-      const f32x4_t& a = e ? a1 : a0;
-      const int col = 16 * (up + e) + 4 * g;
-      const uint2 m = *reinterpret_cast<const uint2*>(hs + (16 * rb + c16) * BUP + col);
-      const float d0 = (m.x & 0xffffu) ? a[0] : 0.f, d1 = (m.x >> 16) ? a[1] : 0.f;
-      const float d2 = (m.y & 0xffffu) ? a[2] : 0.f, d3 = (m.y >> 16) ? a[3] : 0.f;
-      const uint32_t p0 = pack2(d0, d1), p1 = pack2(d2, d3);
-      *reinterpret_cast<uint2*>(d1s + (16 * rb + c16) * BUP + col) = make_uint2(p0, p1);
-    }
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      const bf16x8_t hb0 = frag_rows(hs + 32 * ks * BUP, BUP, 16 * ubp, lane);
-      const bf16x8_t hb1 = frag_rows(hs + 32 * ks * BUP, BUP, 16 * (ubp + 1), lane);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const bf16x8_t da = frag_rows_sw(dsm + 32 * ks * BDP, BDP, 16 * (jb0 + j), lane);
-        acc1[j][0] = mma32(hb0, da, acc1[j][0]);  // C[u][j]: 4 consecutive units per lane
-        acc1[j][1] = mma32(hb1, da, acc1[j][1]);
-      }
-    }
-    // db1 = sum over the rows of dact2 (row 0 of ones . dact2): j block 4q + (w & 3), so every
-    // workgroup does the same work; waves 4..7 repeat waves 0..3's (never stored) instead of
-    // branching, which keeps the tile body one basic block
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
-      accb[0] = mma32(ones, frag_rows_sw(dsm + 32 * ks * BDP, BDP, 16 * (4 * q + (wave & 3)), lane), accb[0]);
-  };
-  // (c) of local tile i (its dact1 buffer i & 1, X buffer i % NXB)
-  auto tile_c = [&](int i) __attribute__((always_inline)) {
-    const bf16_t* d1s = d1s0 + (i & 1) * L::HS;
-    const bf16_t* xs = xs0 + (i & (NXB - 1)) * L::XS;
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      const bf16x8_t A = frag_rows(d1s + 32 * ks * BUP, BUP, 16 * ub, lane);
-#pragma unroll
-      for (int f = 0; f < NFW; ++f) acc0[f] = mma32(A, frag_rows(xs + 32 * ks * XP, XP, 16 * (fb + f), lane), acc0[f]);
-      // db0 = sum over the rows of dact1: the same A against a column of ones (waves 4..7 repeat
-      // waves 0..3's block, never stored, so the body stays one basic block)
-      accd0 = mma32(A, ones, accd0);
-    }
-  };
-  // h1 quadrant tile i from X tile i (buffer i % NXB) into h1 buffer i & 1: the forward's operands,
-  // accumulation order and rounding (bit-identical h1)
-  auto tile_h1 = [&](int i) __attribute__((always_inline)) {
-    const bf16_t* xs = xs0 + (i & (NXB - 1)) * L::XS;
-    bf16_t* hs = hs0 + (i & 1) * L::HS;
-#pragma unroll
-    for (int e = 0; e < 2; ++e) {
-      const int row = 16 * (rbh + e) + c16;
-      f32x4_t a = {b0q.x, b0q.y, b0q.z, b0q.w};
-#pragma unroll
-      for (int kc = 0; kc < NFW; ++kc) a = mma32(w0q[kc], *reinterpret_cast<const bf16x8_t*>(xs + row * XP + kc * 32 + 8 * g), a);
-      *reinterpret_cast<uint2*>(hs + row * BUP + 16 * ubh + 4 * g) =
-          make_uint2(relu2(pack2(a[0], a[1])), relu2(pack2(a[2], a[3])));
-    }
-  };
-
-  // invariant at the top of iteration i: dzr / mkr = tile i+1, xr = X tile i+2 (loaded)
-  HAR_B3_LOAD_D(t0)
-  HAR_B3_LOAD_X(t0)
-  stage_dact2(0);
-  HAR_B3_STAGE_X(0)
-  HAR_B3_LOAD_X(t0 + 1)
-  HAR_B3_STAGE_X(1)
-  HAR_B3_LOAD_D(t0 + 1)
-  HAR_B3_LOAD_X(t0 + 2)
-  __builtin_amdgcn_sched_barrier(0);
-  __syncthreads();  // dact2 tile 0, X tiles 0 and 1 are in LDS
-  tile_h1(0);
-  __syncthreads();  // h1 tile 0 complete
-  // iteration 0 is peeled (no (c) yet) so the steady-state body after the refill point is one
-  // basic block the scheduler can interleave
-  auto iter = [&](int i, bool first) __attribute__((always_inline)) {
-    if (i < 24) HAR_STAMP(8, 2 + i)
-    stage_dact2((i + 1) & 1);       // waits for the dz / mask loads issued one iteration ago
-    if (i == 4) HAR_STAMP(8, 26)
-    HAR_B3_STAGE_X(i + 2)
-    HAR_B3_LOAD_D(t0 + i + 2)
-    HAR_B3_LOAD_X(t0 + i + 3)
-    __builtin_amdgcn_sched_barrier(0);  // the refills are issued before the compute
-    if (i == 4) HAR_STAMP(8, 27)
-    tile_h1(i + 1);                 // X tile i+1 has been in LDS since the last barrier
-    if (i == 4) HAR_STAMP(8, 28)
-    tile_ab(i);
-    if (i == 4) HAR_STAMP(8, 29)
-    if (!first) tile_c(i - 1);
-    if (i == 4) HAR_STAMP(8, 30)
-    __syncthreads();                // dact2 i+1 / X i+2 staged, h1 i+1 and dact1 i complete
-  };
-  if (n > 0) iter(0, true);
-  // (not unrolled: a 4x unroll makes every buffer offset an immediate, -34 address VALU per tile,
-  // but the hoisted per-phase bases push the kernel past 256 VGPRs: 50 spilled registers)
-  for (int i = 1; i < n; ++i) iter(i, false);
-  HAR_STAMP(8, 34)
-  if (n > 0) tile_c(n - 1);
-#undef HAR_B3_LOAD_D
-#undef HAR_B3_LOAD_X
-#undef HAR_B3_STAGE_X
-
-  // ---- this workgroup's parts of slab `slice` (flat parameter layout) ----
-  float* w1o = gw1 + (size_t)slice * slab_stride;
-#pragma unroll
-  for (int j = 0; j < 4; ++j)
-#pragma unroll
-    for (int uu = 0; uu < 2; ++uu)
-      *reinterpret_cast<f32x4_t*>(w1o + (size_t)(16 * (jb0 + j) + c16) * HH + qu0 + 16 * (ubp + uu) + 4 * g) =
-          acc1[j][uu];
-  float* w0o = gw0 + (size_t)slice * slab_stride;
-#pragma unroll
-  for (int f = 0; f < NFW; ++f)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) w0o[(size_t)(qu0 + 16 * ub + 4 * g + r) * K0 + 16 * (fb + f) + c16] = acc0[f][r];
-  if (wave < 4 && g == 0) gb1[(size_t)slice * slab_stride + 16 * (4 * q + wave) + c16] = accb[0][0];
-  if (wave < 4 && c16 == 0)
-    *reinterpret_cast<f32x4_t*>(gb0 + (size_t)slice * slab_stride + qu0 + 16 * ub + 4 * g) = accd0;
-  if constexpr (STAMP) __builtin_amdgcn_s_waitcnt(0x0f70);
-  HAR_STAMP(8, 35)
-  HAR_STAMP_REAL(8, 39)
-}
-
 // ------------------------------------------------------------------------------------------------
-// backward, wave-specialized (mlp_bwd4): the same work items, products and summation orders as
-// mlp_bwd3, but the 8 waves split by role instead of by data.  Waves 0..3 PRODUCE the next tile's
-// operands (the dact2 tile from dz / mask, the X tile staging and the h1 recompute: VALU, LDS stores
-// and a few small MFMAs); waves 4..7 CONSUME the current tile (the (a) dact1, (b) dW1, (c) dW0, db0 /
-// db1 products: MFMA with LDS fragment reads).  Each SIMD hosts one producer and one consumer, so
-// the producer's VALU / LDS-store stream issues beside the consumer's MFMA stream instead of both
-// waves of a SIMD running the same phase at the same time (mlp_bwd3: 36% MFMA busy per tile).
-// Each role runs its own loop (disjoint register live ranges: max, not sum, of the two roles'
-// state) with the same barrier sequence: one workgroup barrier per tile.
+// backward, wave-specialized (mlp_bwd4): the 8 waves split by role.  Waves 0..3 PRODUCE the next
+// tile's operands (the dact2 tile copied from the forward's dact2 rows, the X tile staging and the h1
+// recompute: loads, LDS stores and a few small MFMAs); waves 4..7 CONSUME the current tile (the (a)
+// dact1, (b) dW1, (c) dW0, db0 / db1 products: MFMA with LDS fragment reads).  Each SIMD hosts one
+// producer and one consumer, so the producer's load / LDS-store stream issues beside the consumer's
+// MFMA stream.  Each role runs its own loop (disjoint register live ranges: max, not sum, of the two
+// roles' state) with the same barrier sequence: one workgroup barrier per tile.
 //   consumer c: (a) unit blocks 2 (c & 1) .. + 1 x row blocks 2 (c >> 1) .. + 1 (W1^T fragments in
 //               registers, dact2 rows from LDS); (b) all 4 unit blocks x j blocks 4c .. 4c + 3
 //               (64 dW1 accumulators); (c) unit block c x every input block; db0 of unit block c;
 //               db1 of j block 4q + c
-//   producer p: dact2 rows 16p .. + 16 x all 256 j; h1 unit block p x all 4 row blocks; X staging
+//   producer p: dact2 / X staging (8 / 1-2 16-byte pieces per thread, loaded a tile ahead); h1 unit
+//               block p x all 4 row blocks
+// The forward computes dact2 = (dz . Wout) * relu'(h2) beside its dWout stage (16x16x16 MFMAs on data
+// it holds anyway) and writes it in this kernel's LDS tile order: the 4 quadrant workgroups of a row
+// slice then copy the same rows (one HBM read, three L2 / MALL hits) instead of each rebuilding them
+// from dz and a relu' bit mask (16 MFMAs + table-driven masking per producer wave and tile: the
+// producers had become the critical path, profiles/r5).
 template <int K0, bool STAMP>
 __global__ __launch_bounds__(512) void mlp_bwd4_kernel(
-    const uint32_t* __restrict__ dz, const uint32_t* __restrict__ mask, const bf16_t* __restrict__ X,
+    const bf16_t* __restrict__ dact2, const bf16_t* __restrict__ X,
     const bf16_t* __restrict__ Wf, const float* __restrict__ b0,
-    const bf16_t* __restrict__ Wo, int B, int S, float* __restrict__ gw1, float* __restrict__ gw0,
+    int B, int S, float* __restrict__ gw1, float* __restrict__ gw0,
     float* __restrict__ gb0, float* __restrict__ gb1, int64_t slab_stride, int32_t* __restrict__ tick,
     const float* __restrict__ fslab, int fslab_w, int nfwd, float* __restrict__ gwo, float* __restrict__ gbo,
     uint64_t* __restrict__ stamps) {
-  using L = Bwd3Lds<K0>;
+  using L = Bwd4Lds<K0>;
   constexpr int NXB = L::NXB, KC = HH / 32, XP = L::XP, NFW = K0 / 32, NFB = K0 / 16;
   constexpr int XV = BRT * K0 / 8;  // 16-byte vectors of an X tile (512 / 256)
   constexpr int XPT = XV / 256;     // per producer thread (2 / 1)
+  constexpr int DV = BRT * HH / 8 / 256;  // 16-byte dact2 pieces per producer thread and tile (8)
   if (tick && blockIdx.x == 0 && threadIdx.x == 0) *tick += 1;
   extern __shared__ __attribute__((aligned(16))) bf16_t lds[];
   bf16_t* const dsm0 = lds;                // [2][64][BDP] dact2 tiles
   bf16_t* const hs0 = dsm0 + 2 * L::DSM;   // [2][64][BUP] h1 quadrant tiles
   bf16_t* const d1s0 = hs0 + 2 * L::HS;    // [2][64][BUP] dact1 quadrant tiles
   bf16_t* const xs0 = d1s0 + 2 * L::HS;    // [NXB][64][XP] X tiles
-  float* const red = reinterpret_cast<float*>(xs0 + NXB * L::XS);
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // scalar: the role branches are s_cbranch
   const int c16 = lane & 15, g = lane >> 4;
-  uint32_t* const lut = reinterpret_cast<uint32_t*>(red + 4 * BQU);  // [16][2] relu' nibble -> AND masks
-  if (tid < 16)
-    *reinterpret_cast<uint2*>(lut + 2 * tid) = make_uint2((tid & 1 ? 0xffffu : 0u) | (tid & 2 ? 0xffff0000u : 0u),
-                                                          (tid & 4 ? 0xffffu : 0u) | (tid & 8 ? 0xffff0000u : 0u));
   HAR_STAMP_REAL(8, 38)
   HAR_STAMP(8, 0)
   const int b = xcd_remap(blockIdx.x, gridDim.x);
@@ -790,19 +503,16 @@ __global__ __launch_bounds__(512) void mlp_bwd4_kernel(
   const int ntiles = B / BRT, per = (ntiles + S - 1) / S;
   const int t0 = slice * per, n = max(0, min(ntiles, t0 + per) - t0);
 
-  // ---- prologue (all waves): W1^T quadrant fragments and Wout into LDS, the forward's dWout slabs ----
+  // ---- prologue (all waves): W1^T quadrant fragments into LDS, the forward's dWout slabs ----
   const bf16_t* const W0f = Wf;
   const bf16_t* const W1tq = Wf + HH * K0 + HH * HH + (size_t)(4 * q) * KC * 512;
-  bf16_t* const wos = lds;
   bf16_t* const w1q = lds + NCLS * HH;
   {
     uint4 st[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) st[i] = *reinterpret_cast<const uint4*>(W1tq + (size_t)(i * 8 + wave) * 512 + lane * 8);
-    const uint4 so = *reinterpret_cast<const uint4*>(Wo + (size_t)tid * 8);
 #pragma unroll
     for (int i = 0; i < 4; ++i) *reinterpret_cast<uint4*>(w1q + (i * 8 + wave) * 512 + lane * 8) = st[i];
-    *reinterpret_cast<uint4*>(wos + tid * 8) = so;
   }
   constexpr int WO4 = NCLS * HH / 4, NC4 = WO4 + NCLS / 4;
   const int gwv = blockIdx.x * 8 + wave, nwv = gridDim.x * 8;
@@ -835,14 +545,6 @@ __global__ __launch_bounds__(512) void mlp_bwd4_kernel(
 
   if (prod) {
     // ================================ producer ================================
-    // dact2 A fragments for all 256 j: block t = 2 pp + s holds j = 32 pp + 8 (m >> 2) + 4 s + (m & 3),
-    // so lane group g of pair pp holds the 8 consecutive j = 32 pp + 8 g .. + 7 (one 16-byte store)
-    s16x4_t woa[16];
-#pragma unroll
-    for (int t = 0; t < 16; ++t)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-        woa[t][i] = (short)wos[(4 * g + i) * HH + 32 * (t >> 1) + 8 * (c16 >> 2) + 4 * (t & 1) + (c16 & 3)];
     bf16x8_t w0q[NFW];
 #pragma unroll
     for (int kc = 0; kc < NFW; ++kc)
@@ -852,23 +554,28 @@ __global__ __launch_bounds__(512) void mlp_bwd4_kernel(
     HAR_STAMP(8, 1)
     __syncthreads();  // the prologue images are read: the tile buffers may be written
 
-    const uint32_t* ldz = dz + (size_t)(16 * pw + c16) * 8 + 2 * g;
-    const uint32_t* lmk = mask + (size_t)(16 * pw + c16) * 8;
     const int ptid = tid;  // 0..255
     static_assert(XPT == 1 || XPT == 2, "one or two X vectors per producer thread");
+    static_assert(DV == 8, "8 dact2 pieces per producer thread");
+    // dact2 piece i of a tile: row (ptid >> 5) + 8 i, 16-byte chunk ptid & 31 (a wave-instruction reads
+    // two whole 512-byte rows); LDS rows BDP apart (the forward wrote the chunk swizzle already)
+    const bf16_t* const d2src = dact2 + (size_t)(ptid >> 5) * HH + (ptid & 31) * 8;
+    const int d2dst = (ptid >> 5) * BDP + (ptid & 31) * 8;
     // (macros, not lambdas: a lambda-captured register array is kept in scratch)
-    // the loop-carried dz / mask pieces are single dwords: with 2- / 4-dword tuples the register
-    // allocator re-packs the phi and the back-edge copy then waits out the refill's whole latency
-    uint32_t dz0, dz1, mw0, mw1, mw2, mw3, mw4, mw5, mw6, mw7;
+    uint4 dr0, dr1, dr2, dr3, dr4, dr5, dr6, dr7;
     uint4 xr0, xr1;
 #define HAR_B4_LOAD_D(t)                                                      \
   {                                                                           \
     const int64_t tt_ = min(t, tlast);                                        \
-    const uint32_t* dp_ = ldz + tt_ * BRT * 8;                                \
-    const uint32_t* mp_ = lmk + tt_ * BRT * 8;                                \
-    dz0 = dp_[0]; dz1 = dp_[1];                                               \
-    mw0 = mp_[0]; mw1 = mp_[1]; mw2 = mp_[2]; mw3 = mp_[3];                   \
-    mw4 = mp_[4]; mw5 = mp_[5]; mw6 = mp_[6]; mw7 = mp_[7];                   \
+    const bf16_t* dp_ = d2src + tt_ * BRT * HH;                               \
+    dr0 = *reinterpret_cast<const uint4*>(dp_ + 0 * 8 * HH);                  \
+    dr1 = *reinterpret_cast<const uint4*>(dp_ + 1 * 8 * HH);                  \
+    dr2 = *reinterpret_cast<const uint4*>(dp_ + 2 * 8 * HH);                  \
+    dr3 = *reinterpret_cast<const uint4*>(dp_ + 3 * 8 * HH);                  \
+    dr4 = *reinterpret_cast<const uint4*>(dp_ + 4 * 8 * HH);                  \
+    dr5 = *reinterpret_cast<const uint4*>(dp_ + 5 * 8 * HH);                  \
+    dr6 = *reinterpret_cast<const uint4*>(dp_ + 6 * 8 * HH);                  \
+    dr7 = *reinterpret_cast<const uint4*>(dp_ + 7 * 8 * HH);                  \
   }
 #define HAR_B4_LOAD_X(t)                                                                      \
   {                                                                                           \
@@ -883,34 +590,17 @@ __global__ __launch_bounds__(512) void mlp_bwd4_kernel(
     if constexpr (XPT == 2)                                                                                \
       *reinterpret_cast<uint4*>(xb_ + ((ptid + 256) / (K0 / 8)) * XP + ((ptid + 256) % (K0 / 8)) * 8) = xr1; \
   }
-    // dact2 rows 16 pw + c16 -> LDS buffer `buf` (row-major, 16-byte chunks of rows with bit 2 set
-    // swapped in pairs), relu'(h2) applied by AND masks from the nibble table
+    // the dact2 tile (loaded a tile ahead) -> LDS buffer `buf`
     auto stage_dact2 = [&](int buf) __attribute__((always_inline)) {
-      const int sw = 8 * ((c16 >> 2) & 1);
-      bf16_t* d = dsm0 + buf * L::DSM + (16 * pw + c16) * BDP;
-      const s16x4_t dzv = __builtin_bit_cast(s16x4_t, make_uint2(dz0, dz1));
-      const uint32_t mws[8] = {mw0, mw1, mw2, mw3, mw4, mw5, mw6, mw7};
-      // all 16 table reads first, then the 16 MFMAs, then the masked stores: interleaved per pp, each
-      // read -> AND -> store waited out a full LDS round trip (8 serialized trips per tile)
-      uint2 m0[8], m1[8];
-#pragma unroll
-      for (int pp = 0; pp < 8; ++pp) {
-        const uint32_t mw = mws[pp] >> (8 * g);
-        m0[pp] = *reinterpret_cast<const uint2*>(lut + 2 * (mw & 0xfu));
-        m1[pp] = *reinterpret_cast<const uint2*>(lut + 2 * ((mw >> 4) & 0xfu));
-      }
-      f32x4_t v0[8], v1[8];
-#pragma unroll
-      for (int pp = 0; pp < 8; ++pp) {
-        v0[pp] = mma16(woa[2 * pp], dzv, f32x4_t{0.f, 0.f, 0.f, 0.f});
-        v1[pp] = mma16(woa[2 * pp + 1], dzv, f32x4_t{0.f, 0.f, 0.f, 0.f});
-      }
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int pp = 0; pp < 8; ++pp)
-        *reinterpret_cast<u32x4_t*>(d + ((32 * pp + 8 * g) ^ sw)) =
-            u32x4_t{pack2(v0[pp][0], v0[pp][1]) & m0[pp].x, pack2(v0[pp][2], v0[pp][3]) & m0[pp].y,
-                    pack2(v1[pp][0], v1[pp][1]) & m1[pp].x, pack2(v1[pp][2], v1[pp][3]) & m1[pp].y};
+      bf16_t* d = dsm0 + buf * L::DSM + d2dst;
+      *reinterpret_cast<uint4*>(d + 0 * 8 * BDP) = dr0;
+      *reinterpret_cast<uint4*>(d + 1 * 8 * BDP) = dr1;
+      *reinterpret_cast<uint4*>(d + 2 * 8 * BDP) = dr2;
+      *reinterpret_cast<uint4*>(d + 3 * 8 * BDP) = dr3;
+      *reinterpret_cast<uint4*>(d + 4 * 8 * BDP) = dr4;
+      *reinterpret_cast<uint4*>(d + 5 * 8 * BDP) = dr5;
+      *reinterpret_cast<uint4*>(d + 6 * 8 * BDP) = dr6;
+      *reinterpret_cast<uint4*>(d + 7 * 8 * BDP) = dr7;
     };
     // h1 unit block pw x 4 row blocks of tile i (X buffer i & 3) -> h1 buffer i & 1 (the forward's
     // operands, accumulation order and rounding: bit-identical h1)
@@ -938,7 +628,7 @@ __global__ __launch_bounds__(512) void mlp_bwd4_kernel(
         *reinterpret_cast<uint2*>(hs + (16 * rr + c16) * BUP + 16 * pw + 4 * g) =
             make_uint2(relu2(pack2(a[rr][0], a[rr][1])), relu2(pack2(a[rr][2], a[rr][3])));
     };
-    // invariant at the top of iteration i: dzr / mkr = tile i+1, xr = X tile i+2 (loaded)
+    // invariant at the top of iteration i: dr* = dact2 tile i+1, xr = X tile i+2 (loaded)
     HAR_B4_LOAD_D(t0)
     HAR_B4_LOAD_X(t0)
     stage_dact2(0);
@@ -953,13 +643,13 @@ __global__ __launch_bounds__(512) void mlp_bwd4_kernel(
     __syncthreads();  // h1 tile 0 complete
     for (int i = 0; i < n; ++i) {
       if (i < 24) HAR_STAMP(8, 2 + i)
-      if constexpr (STAMP) {  // (stamped build only: how long the dz / mask refill is still in flight)
+      if constexpr (STAMP) {  // (stamped build only: how long the dact2 refill is still in flight)
         if (i == 4) {
           __builtin_amdgcn_s_waitcnt(0x0f70 | XPT);
           HAR_STAMP(8, 32)
         }
       }
-      stage_dact2((i + 1) & 1);  // waits for the dz / mask loads issued one iteration ago
+      stage_dact2((i + 1) & 1);  // waits for the dact2 loads issued one iteration ago
       if (i == 4) HAR_STAMP(8, 26)
       HAR_B4_STAGE_X(i + 2)
       // the refills may not be hoisted above the last reads of the registers they overwrite: a hoisted
@@ -1136,32 +826,27 @@ static int fwd_stagger() {
 
 template <int K0>
 void launch_fwd3(const bf16_t* X, bf16_t* Wf, const float* b0, const float* b1, const bf16_t* Wo,
-                 const float* bo, const int32_t* labels, int B, int C, float scale, uint32_t* dz, uint32_t* mask,
+                 const float* bo, const int32_t* labels, int B, int C, float scale, bf16_t* dact2,
                  float* slab, float* bl, int32_t* bc, int nwg, hipStream_t s) {
   auto k = g_har_mlp_stamps ? mlp_fwd3_kernel<K0, true> : mlp_fwd3_kernel<K0, false>;
-  k<<<nwg, 512, FWD_LDS, s>>>(X, Wf, b0, b1, Wo, bo, labels, B, C, scale, dz, mask, slab, bl, bc, g_har_mlp_stamps,
+  k<<<nwg, 512, FWD_LDS, s>>>(X, Wf, b0, b1, Wo, bo, labels, B, C, scale, dact2, slab, bl, bc, g_har_mlp_stamps,
                               fwd_stagger());
 }
 
 template <int K0>
 void launch_fwd3_infer(const bf16_t* X, bf16_t* Wf, const float* b0, const float* b1, const bf16_t* Wo,
                        const float* bo, int B, int C, float* logits, int32_t* pred, int nwg, hipStream_t s) {
-  mlp_fwd3_kernel<K0, false, true><<<nwg, 512, FWD_LDS, s>>>(X, Wf, b0, b1, Wo, bo, nullptr, B, C, 1.f, nullptr, nullptr,
+  mlp_fwd3_kernel<K0, false, true><<<nwg, 512, FWD_LDS, s>>>(X, Wf, b0, b1, Wo, bo, nullptr, B, C, 1.f, nullptr,
                                                               logits, nullptr, pred, nullptr, fwd_stagger());
 }
 
 template <int K0>
-void launch_bwd3(const uint32_t* dz, const uint32_t* mask, const bf16_t* X, const bf16_t* Wf, const float* b0,
-                 const bf16_t* Wo, int B, int S, float* gw1, float* gw0, float* gb0, float* gb1, int64_t stride,
-                 int32_t* tick, const float* fslab, int fslab_w, int nfwd, float* gwo, float* gbo, hipStream_t s) {
-  static const bool v4 = [] {
-    const char* e = getenv("HAR_MLP_BWD");
-    return !e || atoi(e) != 3;
-  }();
-  auto k = v4 ? (g_har_mlp_stamps ? mlp_bwd4_kernel<K0, true> : mlp_bwd4_kernel<K0, false>)
-              : (g_har_mlp_stamps ? mlp_bwd3_kernel<K0, true> : mlp_bwd3_kernel<K0, false>);
-  k<<<S * BQ, 512, Bwd3Lds<K0>::bytes, s>>>(dz, mask, X, Wf, b0, Wo, B, S, gw1, gw0, gb0, gb1, stride, tick,
-                                           fslab, fslab_w, nfwd, gwo, gbo, g_har_mlp_stamps ? g_har_mlp_stamps + STAMP_BWD_OFF : nullptr);
+void launch_bwd4(const bf16_t* dact2, const bf16_t* X, const bf16_t* Wf, const float* b0, int B, int S, float* gw1,
+                 float* gw0, float* gb0, float* gb1, int64_t stride, int32_t* tick, const float* fslab, int fslab_w,
+                 int nfwd, float* gwo, float* gbo, hipStream_t s) {
+  auto k = g_har_mlp_stamps ? mlp_bwd4_kernel<K0, true> : mlp_bwd4_kernel<K0, false>;
+  k<<<S * BQ, 512, Bwd4Lds<K0>::bytes, s>>>(dact2, X, Wf, b0, B, S, gw1, gw0, gb0, gb1, stride, tick, fslab, fslab_w,
+                                           nfwd, gwo, gbo, g_har_mlp_stamps ? g_har_mlp_stamps + STAMP_BWD_OFF : nullptr);
 }
 
 }  // namespace
@@ -1177,22 +862,24 @@ extern "C" int har_mlp_step_slices(int B) {
 }
 extern "C" int har_mlp_step_fwd_slab_width(int H) { return NCLS * H + NCLS; }
 
-// Forward of the step: dz [B][8] u32 (bf16 pairs, 16 classes), relu'(h2) mask [B][8] u32, and per
-// workgroup (har_mlp_step_grid(B) of them) dWout rows 0..15 + dbout (width har_mlp_step_fwd_slab_width),
-// loss and #correct.
+// Forward of the step: dact2 [B][256] bf16 (the layer-2 gradient (dz . Wout) * relu'(h2), the 16-byte
+// chunks of rows with bit 2 set swapped in pairs: the backward's LDS tile image) and per workgroup
+// (har_mlp_step_grid(B) of them) dWout rows 0..15 + dbout (width har_mlp_step_fwd_slab_width), loss
+// and #correct.
 extern "C" int har_mlp_step_fwd(const uint16_t* X, int K0, uint16_t* Wf, const float* b0, const float* b1,
                                 int H, const uint16_t* Wo, const float* bo, const int32_t* labels, int B, int C,
-                                float scale, uint32_t* dz, uint32_t* mask, float* slab, float* block_loss,
+                                float scale, uint16_t* dact2, float* slab, float* block_loss,
                                 int32_t* block_correct, hipStream_t s) {
   if (H != HH || (K0 != 32 && K0 != 64) || B <= 0 || B % 64 || C < 1 || C > NCLS) return -2;
   if (((uintptr_t)X | (uintptr_t)Wf | (uintptr_t)Wo | (uintptr_t)b0 | (uintptr_t)b1 | (uintptr_t)slab |
-       (uintptr_t)dz | (uintptr_t)mask) & 15)
+       (uintptr_t)dact2) & 15)
     return -3;
   const int nwg = har_mlp_step_grid(B);
+  bf16_t* d2 = reinterpret_cast<bf16_t*>(dact2);
   if (K0 == 64)
-    launch_fwd3<64>(X, Wf, b0, b1, Wo, bo, labels, B, C, scale, dz, mask, slab, block_loss, block_correct, nwg, s);
+    launch_fwd3<64>(X, Wf, b0, b1, Wo, bo, labels, B, C, scale, d2, slab, block_loss, block_correct, nwg, s);
   else
-    launch_fwd3<32>(X, Wf, b0, b1, Wo, bo, labels, B, C, scale, dz, mask, slab, block_loss, block_correct, nwg, s);
+    launch_fwd3<32>(X, Wf, b0, b1, Wo, bo, labels, B, C, scale, d2, slab, block_loss, block_correct, nwg, s);
   HAR_CHECK_LAUNCH();
   return 0;
 }
@@ -1217,27 +904,28 @@ extern "C" int har_mlp_step_fwd_infer(const uint16_t* X, int K0, const uint16_t*
   return 0;
 }
 
-// Backward of the step: per row slice s < har_mlp_step_slices(B) the partials of dW1, dW0, db0 (and db1)
-// at gw1 / gw0 / gb0 / gb1 + s * slab_stride.  With fslab (the forward's har_mlp_step_grid(B)
-// per-workgroup slabs, row stride fslab_w) it also writes their sums: dWout rows 0..15 to gwo and
-// dbout to gbo (fixed summation order).
-extern "C" int har_mlp_step_bwd(const uint32_t* dz, const uint32_t* mask, const uint16_t* X, int K0,
-                                const uint16_t* Wf, int H, const float* b0, const uint16_t* Wo, int B, float* gw1,
-                                float* gw0, float* gb0, float* gb1, int64_t slab_stride, int32_t* tick,
-                                const float* fslab, int fslab_w, float* gwo, float* gbo, hipStream_t s) {
+// Backward of the step (from the forward's dact2 rows and X): per row slice s < har_mlp_step_slices(B)
+// the partials of dW1, dW0, db0 (and db1) at gw1 / gw0 / gb0 / gb1 + s * slab_stride.  With fslab (the
+// forward's har_mlp_step_grid(B) per-workgroup slabs, row stride fslab_w) it also writes their sums:
+// dWout rows 0..15 to gwo and dbout to gbo (fixed summation order).
+extern "C" int har_mlp_step_bwd(const uint16_t* dact2, const uint16_t* X, int K0, const uint16_t* Wf, int H,
+                                const float* b0, int B, float* gw1, float* gw0, float* gb0, float* gb1,
+                                int64_t slab_stride, int32_t* tick, const float* fslab, int fslab_w, float* gwo,
+                                float* gbo, hipStream_t s) {
   if (H != HH || B <= 0 || B % BRT || (K0 != 32 && K0 != 64) || slab_stride < (int64_t)H * H) return -2;
-  if (((uintptr_t)dz | (uintptr_t)mask | (uintptr_t)X | (uintptr_t)Wf | (uintptr_t)b0 | (uintptr_t)Wo |
-       (uintptr_t)gw1 | (uintptr_t)fslab | (uintptr_t)gwo | (uintptr_t)gbo) & 15)
+  if (((uintptr_t)dact2 | (uintptr_t)X | (uintptr_t)Wf | (uintptr_t)b0 | (uintptr_t)gw1 | (uintptr_t)fslab |
+       (uintptr_t)gwo | (uintptr_t)gbo) & 15)
     return -3;
   const int nfwd = har_mlp_step_grid(B);
   if (fslab && (fslab_w < har_mlp_step_fwd_slab_width(H) || fslab_w % 4 || nfwd > 256 || !gwo || !gbo)) return -2;
   const int S = har_mlp_step_slices(B);
+  const bf16_t* d2 = reinterpret_cast<const bf16_t*>(dact2);
+  const bf16_t* x = reinterpret_cast<const bf16_t*>(X);
+  const bf16_t* wf = reinterpret_cast<const bf16_t*>(Wf);
   if (K0 == 64)
-    launch_bwd3<64>(dz, mask, X, Wf, b0, Wo, B, S, gw1, gw0, gb0, gb1, slab_stride, tick, fslab, fslab_w, nfwd, gwo,
-                    gbo, s);
+    launch_bwd4<64>(d2, x, wf, b0, B, S, gw1, gw0, gb0, gb1, slab_stride, tick, fslab, fslab_w, nfwd, gwo, gbo, s);
   else
-    launch_bwd3<32>(dz, mask, X, Wf, b0, Wo, B, S, gw1, gw0, gb0, gb1, slab_stride, tick, fslab, fslab_w, nfwd, gwo,
-                    gbo, s);
+    launch_bwd4<32>(d2, x, wf, b0, B, S, gw1, gw0, gb0, gb1, slab_stride, tick, fslab, fslab_w, nfwd, gwo, gbo, s);
   HAR_CHECK_LAUNCH();
   return 0;
 }

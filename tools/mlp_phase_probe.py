@@ -105,7 +105,7 @@ def stamps(B=65536):
             for nm, v in sub:
                 print(f"  {nm:28s} median {np.median(v):9.0f}  max {v.max():9.0f} cycles")
         if k == 1 and bwd4 and producer and (s[:, 26] > 0).all():  # mlp_bwd4 producer phases of tile 4
-            sub = [("  tile 4: dz / mask refill wait", s[:, 32] - s[:, 6]),
+            sub = [("  tile 4: dact2 refill wait", s[:, 32] - s[:, 6]),
                    ("  tile 4: dact2 (tile 5) -> LDS", s[:, 26] - s[:, 32]), ("  tile 4: X stage + refills", s[:, 27] - s[:, 26]),
                    ("  tile 4: h1 recompute (tile 5)", s[:, 28] - s[:, 27]), ("  tile 4: barrier", s[:, 7] - s[:, 28])]
             for nm, v in sub:

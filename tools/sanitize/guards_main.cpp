@@ -81,19 +81,18 @@ static void mlp_contracts() {
   EXPECT(har_mlp_fwd_infer(hbuf, 64, hbuf, fbuf, hbuf, fbuf, 192, hbuf, fbuf, 64, 6, fbuf, ibuf, 0), -4);
 
   // three-kernel step: H != 256, K0 not 32 / 64, B % 64, C outside [1, 16], short slab stride, misaligned
-  uint32_t* w = reinterpret_cast<uint32_t*>(ibuf);
   float* g = fbuf;
-  EXPECT(har_mlp_step_fwd(hbuf, 64, hbuf, fbuf, fbuf, 128, hbuf, fbuf, ibuf, 64, 6, 1.f, w, w, g, g, ibuf, 0), -2);
-  EXPECT(har_mlp_step_fwd(hbuf, 48, hbuf, fbuf, fbuf, 256, hbuf, fbuf, ibuf, 64, 6, 1.f, w, w, g, g, ibuf, 0), -2);
-  EXPECT(har_mlp_step_fwd(hbuf, 64, hbuf, fbuf, fbuf, 256, hbuf, fbuf, ibuf, 96, 6, 1.f, w, w, g, g, ibuf, 0), -2);
-  EXPECT(har_mlp_step_fwd(hbuf, 64, hbuf, fbuf, fbuf, 256, hbuf, fbuf, ibuf, 64, 17, 1.f, w, w, g, g, ibuf, 0), -2);
-  EXPECT(har_mlp_step_fwd(hbuf + 4, 64, hbuf, fbuf, fbuf, 256, hbuf, fbuf, ibuf, 64, 6, 1.f, w, w, g, g, ibuf, 0), -3);
-  EXPECT(har_mlp_step_bwd(w, w, hbuf, 64, hbuf, 128, fbuf, hbuf, 64, g, g, g, g, 1 << 20, ibuf, nullptr, 0, g, g, 0), -2);
-  EXPECT(har_mlp_step_bwd(w, w, hbuf, 64, hbuf, 256, fbuf, hbuf, 96, g, g, g, g, 1 << 20, ibuf, nullptr, 0, g, g, 0), -2);
-  EXPECT(har_mlp_step_bwd(w, w, hbuf, 48, hbuf, 256, fbuf, hbuf, 64, g, g, g, g, 1 << 20, ibuf, nullptr, 0, g, g, 0), -2);
-  EXPECT(har_mlp_step_bwd(w, w, hbuf, 64, hbuf, 256, fbuf, hbuf, 64, g, g, g, g, 256 * 255, ibuf, nullptr, 0, g, g, 0), -2);
-  EXPECT(har_mlp_step_bwd(w + 1, w, hbuf, 64, hbuf, 256, fbuf, hbuf, 64, g, g, g, g, 1 << 20, ibuf, nullptr, 0, g, g, 0), -3);
-  EXPECT(har_mlp_step_bwd(w, w, hbuf, 64, hbuf, 256, fbuf, hbuf, 64, g, g, g, g, 1 << 20, ibuf, g, 100, g, g, 0), -2);
+  EXPECT(har_mlp_step_fwd(hbuf, 64, hbuf, fbuf, fbuf, 128, hbuf, fbuf, ibuf, 64, 6, 1.f, hbuf, g, g, ibuf, 0), -2);
+  EXPECT(har_mlp_step_fwd(hbuf, 48, hbuf, fbuf, fbuf, 256, hbuf, fbuf, ibuf, 64, 6, 1.f, hbuf, g, g, ibuf, 0), -2);
+  EXPECT(har_mlp_step_fwd(hbuf, 64, hbuf, fbuf, fbuf, 256, hbuf, fbuf, ibuf, 96, 6, 1.f, hbuf, g, g, ibuf, 0), -2);
+  EXPECT(har_mlp_step_fwd(hbuf, 64, hbuf, fbuf, fbuf, 256, hbuf, fbuf, ibuf, 64, 17, 1.f, hbuf, g, g, ibuf, 0), -2);
+  EXPECT(har_mlp_step_fwd(hbuf + 4, 64, hbuf, fbuf, fbuf, 256, hbuf, fbuf, ibuf, 64, 6, 1.f, hbuf, g, g, ibuf, 0), -3);
+  EXPECT(har_mlp_step_bwd(hbuf, hbuf, 64, hbuf, 128, fbuf, 64, g, g, g, g, 1 << 20, ibuf, nullptr, 0, g, g, 0), -2);
+  EXPECT(har_mlp_step_bwd(hbuf, hbuf, 64, hbuf, 256, fbuf, 96, g, g, g, g, 1 << 20, ibuf, nullptr, 0, g, g, 0), -2);
+  EXPECT(har_mlp_step_bwd(hbuf, hbuf, 48, hbuf, 256, fbuf, 64, g, g, g, g, 1 << 20, ibuf, nullptr, 0, g, g, 0), -2);
+  EXPECT(har_mlp_step_bwd(hbuf, hbuf, 64, hbuf, 256, fbuf, 64, g, g, g, g, 256 * 255, ibuf, nullptr, 0, g, g, 0), -2);
+  EXPECT(har_mlp_step_bwd(hbuf + 1, hbuf, 64, hbuf, 256, fbuf, 64, g, g, g, g, 1 << 20, ibuf, nullptr, 0, g, g, 0), -3);
+  EXPECT(har_mlp_step_bwd(hbuf, hbuf, 64, hbuf, 256, fbuf, 64, g, g, g, g, 1 << 20, ibuf, g, 100, g, g, 0), -2);
 }
 
 static void window_contracts() {
