@@ -166,14 +166,17 @@ __global__ __launch_bounds__(512) void mlp_fwd3_kernel(
   const uint2 whi = *reinterpret_cast<const uint2*>(Wo + (size_t)c16 * HH + u0 + 16 + 4 * g);
   const bf16x8_t wo3 = cat8(wlo.x, wlo.y, whi.x, whi.y);
   const float bo_s = c16 < C ? bo[c16] : 0.f;
-  // dact2 A fragments (16x16x16, K = the 16 classes): A[m = unit 16 t + c16][k = class 4 g + i] =
-  // Wout[4 g + i][u0 + 16 t + c16]
+  // dact2 A fragments (16x16x16, K = the 16 classes): row m of block t is unit 8 (m >> 2) + 4 t + (m & 3)
+  // of the wave's 32 (C row 4 g + r -> unit 8 g + 4 t + r: blocks t = 0, 1 give each lane the 8
+  // CONSECUTIVE units 8 g .. 8 g + 7 of a row, one 16-byte store); A[m][k = class 4 g + i] =
+  // Wout[4 g + i][u0 + 8 (c16 >> 2) + 4 t + (c16 & 3)]
   s16x4_t woT[2];
   if constexpr (!INFER) {
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) woT[t][i] = (short)Wo[(size_t)(4 * g + i) * HH + u0 + 16 * t + c16];
+      for (int i = 0; i < 4; ++i)
+        woT[t][i] = (short)Wo[(size_t)(4 * g + i) * HH + u0 + 8 * (c16 >> 2) + 4 * t + (c16 & 3)];
   }
   __builtin_amdgcn_sched_barrier(0);
   if constexpr (STAMP) __builtin_amdgcn_s_waitcnt(0x0f70);
@@ -286,10 +289,10 @@ __global__ __launch_bounds__(512) void mlp_fwd3_kernel(
   // ---- stage 5 of a tile (dz buffer / image buffer `buf`, rows r0 ..): dWout^T += h2^T . dz over its
   // 32 rows, and the backward's layer-2 gradient dact2 = (dz . Wout) * relu'(h2) of the wave's 32
   // units -> dact2_out (bf16 [B][256], the 16-byte chunks of rows with bit 2 set swapped in pairs —
-  // the backward's LDS tile image, so its producers copy rows verbatim).  One 16x16x16 MFMA per
-  // (16 units x 16 rows) block, K = the 16 classes: C[unit 4 g + r][row c16], i.e. 4 consecutive
-  // units of one row per lane, the same (row, units) the lane's own h2 image words hold ----
-  bf16_t* const d2base = INFER ? nullptr : dact2_out + (size_t)c16 * HH + ((u0 + 4 * g) ^ hsw);
+  // the backward's LDS tile image, so its producers copy rows verbatim).  Two 16x16x16 MFMAs per 16
+  // rows (K = the 16 classes, unit-permuted A rows: woT) give lane (c16, g) the units 8 g .. 8 g + 7 of
+  // row c16: one 16-byte relu' read of the wave's own h2 image, one 16-byte global store ----
+  bf16_t* const d2base = INFER ? nullptr : dact2_out + (size_t)c16 * HH + ((u0 + 8 * g) ^ hsw);
   auto stage5 = [&](int buf, int r0) __attribute__((always_inline)) {
     const bf16_t* zb = dzs + buf * FIMG;
     const bf16x8_t bz = frag_tr(zb, FSP, 0, lane);
@@ -299,16 +302,16 @@ __global__ __launch_bounds__(512) void mlp_fwd3_kernel(
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const s16x4_t dzb = *reinterpret_cast<const s16x4_t*>(zb + (16 * h + c16) * FSP + 4 * g);
-      bf16_t* dst = d2base + (size_t)(r0 + 16 * h) * HH;
+      // h2 units 8 g .. 8 g + 7 of row 16 h + c16: image block g >> 1, columns 8 (g & 1) ..
+      const u32x4_t hv = *reinterpret_cast<const u32x4_t*>(ip + (g >> 1) * FIMG + (16 * h + c16) * FSP + 8 * (g & 1));
+      const f32x4_t v0 = mma16(woT[0], dzb, f32x4_t{0.f, 0.f, 0.f, 0.f});
+      const f32x4_t v1 = mma16(woT[1], dzb, f32x4_t{0.f, 0.f, 0.f, 0.f});
+      // relu'(h2): a relu'd bf16 half is in [0, 0x7fff]; adding 0x7fff carries into its bit 15 exactly
+      // when it is nonzero (no carry crosses the halves) -> 0xffff / 0 half masks
+      u32x4_t o = {pack2(v0[0], v0[1]), pack2(v0[2], v0[3]), pack2(v1[0], v1[1]), pack2(v1[2], v1[3])};
 #pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        const f32x4_t v = mma16(woT[t], dzb, f32x4_t{0.f, 0.f, 0.f, 0.f});
-        const uint2 hv = *reinterpret_cast<const uint2*>(ip + t * FIMG + (16 * h + c16) * FSP + 4 * g);
-        // relu'(h2): a relu'd bf16 half is in [0, 0x7fff]; adding 0x7fff carries into its bit 15 exactly
-        // when it is nonzero (no carry crosses the halves) -> 0xffff / 0 half masks
-        const uint32_t m0 = ((hv.x + 0x7fff7fffu) >> 15) & 0x00010001u, m1 = ((hv.y + 0x7fff7fffu) >> 15) & 0x00010001u;
-        *reinterpret_cast<uint2*>(dst + 16 * t) = make_uint2(pack2(v[0], v[1]) & (m0 * 0xffffu), pack2(v[2], v[3]) & (m1 * 0xffffu));
-      }
+      for (int e = 0; e < 4; ++e) o[e] &= (((hv[e] + 0x7fff7fffu) >> 15) & 0x00010001u) * 0xffffu;
+      *reinterpret_cast<u32x4_t*>(d2base + (size_t)(r0 + 16 * h) * HH) = o;
     }
   };
 
@@ -562,21 +565,39 @@ __global__ __launch_bounds__(512) void mlp_bwd4_kernel(
     const bf16_t* const d2src = dact2 + (size_t)(ptid >> 5) * HH + (ptid & 31) * 8;
     const int d2dst = (ptid >> 5) * BDP + (ptid & 31) * 8;
     // (macros, not lambdas: a lambda-captured register array is kept in scratch)
-    uint4 dr0, dr1, dr2, dr3, dr4, dr5, dr6, dr7;
+    // two register sets of dact2 pieces: the tile staged at iteration i was loaded at iteration i - 2
+    // (one iteration ahead left ~700 cycles of the refill still in flight at its use, profiles/r5)
+    uint4 da0, da1, da2, da3, da4, da5, da6, da7, db0_, db1_, db2_, db3_, db4_, db5_, db6_, db7_;
     uint4 xr0, xr1;
-#define HAR_B4_LOAD_D(t)                                                      \
+#define HAR_B4_LOAD_D(t, ...) HAR_B4_LOAD_D_I(t, __VA_ARGS__)
+#define HAR_B4_LOAD_D_I(t, r0_, r1_, r2_, r3_, r4_, r5_, r6_, r7_)            \
   {                                                                           \
     const int64_t tt_ = min(t, tlast);                                        \
     const bf16_t* dp_ = d2src + tt_ * BRT * HH;                               \
-    dr0 = *reinterpret_cast<const uint4*>(dp_ + 0 * 8 * HH);                  \
-    dr1 = *reinterpret_cast<const uint4*>(dp_ + 1 * 8 * HH);                  \
-    dr2 = *reinterpret_cast<const uint4*>(dp_ + 2 * 8 * HH);                  \
-    dr3 = *reinterpret_cast<const uint4*>(dp_ + 3 * 8 * HH);                  \
-    dr4 = *reinterpret_cast<const uint4*>(dp_ + 4 * 8 * HH);                  \
-    dr5 = *reinterpret_cast<const uint4*>(dp_ + 5 * 8 * HH);                  \
-    dr6 = *reinterpret_cast<const uint4*>(dp_ + 6 * 8 * HH);                  \
-    dr7 = *reinterpret_cast<const uint4*>(dp_ + 7 * 8 * HH);                  \
+    r0_ = *reinterpret_cast<const uint4*>(dp_ + 0 * 8 * HH);                  \
+    r1_ = *reinterpret_cast<const uint4*>(dp_ + 1 * 8 * HH);                  \
+    r2_ = *reinterpret_cast<const uint4*>(dp_ + 2 * 8 * HH);                  \
+    r3_ = *reinterpret_cast<const uint4*>(dp_ + 3 * 8 * HH);                  \
+    r4_ = *reinterpret_cast<const uint4*>(dp_ + 4 * 8 * HH);                  \
+    r5_ = *reinterpret_cast<const uint4*>(dp_ + 5 * 8 * HH);                  \
+    r6_ = *reinterpret_cast<const uint4*>(dp_ + 6 * 8 * HH);                  \
+    r7_ = *reinterpret_cast<const uint4*>(dp_ + 7 * 8 * HH);                  \
   }
+#define HAR_B4_STAGE_D(buf, ...) HAR_B4_STAGE_D_I(buf, __VA_ARGS__)
+#define HAR_B4_STAGE_D_I(buf, r0_, r1_, r2_, r3_, r4_, r5_, r6_, r7_)         \
+  {                                                                           \
+    bf16_t* d_ = dsm0 + (buf) * L::DSM + d2dst;                               \
+    *reinterpret_cast<uint4*>(d_ + 0 * 8 * BDP) = r0_;                        \
+    *reinterpret_cast<uint4*>(d_ + 1 * 8 * BDP) = r1_;                        \
+    *reinterpret_cast<uint4*>(d_ + 2 * 8 * BDP) = r2_;                        \
+    *reinterpret_cast<uint4*>(d_ + 3 * 8 * BDP) = r3_;                        \
+    *reinterpret_cast<uint4*>(d_ + 4 * 8 * BDP) = r4_;                        \
+    *reinterpret_cast<uint4*>(d_ + 5 * 8 * BDP) = r5_;                        \
+    *reinterpret_cast<uint4*>(d_ + 6 * 8 * BDP) = r6_;                        \
+    *reinterpret_cast<uint4*>(d_ + 7 * 8 * BDP) = r7_;                        \
+  }
+#define HAR_DA da0, da1, da2, da3, da4, da5, da6, da7
+#define HAR_DB db0_, db1_, db2_, db3_, db4_, db5_, db6_, db7_
 #define HAR_B4_LOAD_X(t)                                                                      \
   {                                                                                           \
     const int64_t tt_ = min(t, tlast);                                                        \
@@ -590,18 +611,6 @@ __global__ __launch_bounds__(512) void mlp_bwd4_kernel(
     if constexpr (XPT == 2)                                                                                \
       *reinterpret_cast<uint4*>(xb_ + ((ptid + 256) / (K0 / 8)) * XP + ((ptid + 256) % (K0 / 8)) * 8) = xr1; \
   }
-    // the dact2 tile (loaded a tile ahead) -> LDS buffer `buf`
-    auto stage_dact2 = [&](int buf) __attribute__((always_inline)) {
-      bf16_t* d = dsm0 + buf * L::DSM + d2dst;
-      *reinterpret_cast<uint4*>(d + 0 * 8 * BDP) = dr0;
-      *reinterpret_cast<uint4*>(d + 1 * 8 * BDP) = dr1;
-      *reinterpret_cast<uint4*>(d + 2 * 8 * BDP) = dr2;
-      *reinterpret_cast<uint4*>(d + 3 * 8 * BDP) = dr3;
-      *reinterpret_cast<uint4*>(d + 4 * 8 * BDP) = dr4;
-      *reinterpret_cast<uint4*>(d + 5 * 8 * BDP) = dr5;
-      *reinterpret_cast<uint4*>(d + 6 * 8 * BDP) = dr6;
-      *reinterpret_cast<uint4*>(d + 7 * 8 * BDP) = dr7;
-    };
     // h1 unit block pw x 4 row blocks of tile i (X buffer i & 3) -> h1 buffer i & 1 (the forward's
     // operands, accumulation order and rounding: bit-identical h1)
     auto tile_h1 = [&](int i) __attribute__((always_inline)) {
@@ -628,43 +637,58 @@ __global__ __launch_bounds__(512) void mlp_bwd4_kernel(
         *reinterpret_cast<uint2*>(hs + (16 * rr + c16) * BUP + 16 * pw + 4 * g) =
             make_uint2(relu2(pack2(a[rr][0], a[rr][1])), relu2(pack2(a[rr][2], a[rr][3])));
     };
-    // invariant at the top of iteration i: dr* = dact2 tile i+1, xr = X tile i+2 (loaded)
-    HAR_B4_LOAD_D(t0)
+    // invariant at the top of iteration i: the dact2 set of i's parity (A even, B odd) holds tile i+1,
+    // the other set tile i+2; xr = X tile i+2 (loaded)
+    HAR_B4_LOAD_D(t0, HAR_DA)
     HAR_B4_LOAD_X(t0)
-    stage_dact2(0);
+    HAR_B4_STAGE_D(0, HAR_DA)
     HAR_B4_STAGE_X(0)
     HAR_B4_LOAD_X(t0 + 1)
     HAR_B4_STAGE_X(1)
-    HAR_B4_LOAD_D(t0 + 1)
+    HAR_B4_LOAD_D(t0 + 1, HAR_DA)
+    HAR_B4_LOAD_D(t0 + 2, HAR_DB)
     HAR_B4_LOAD_X(t0 + 2)
     __builtin_amdgcn_sched_barrier(0);
     __syncthreads();  // dact2 tile 0, X tiles 0 and 1 are in LDS
     tile_h1(0);
     __syncthreads();  // h1 tile 0 complete
-    for (int i = 0; i < n; ++i) {
-      if (i < 24) HAR_STAMP(8, 2 + i)
-      if constexpr (STAMP) {  // (stamped build only: how long the dact2 refill is still in flight)
-        if (i == 4) {
-          __builtin_amdgcn_s_waitcnt(0x0f70 | XPT);
-          HAR_STAMP(8, 32)
-        }
-      }
-      stage_dact2((i + 1) & 1);  // waits for the dact2 loads issued one iteration ago
-      if (i == 4) HAR_STAMP(8, 26)
-      HAR_B4_STAGE_X(i + 2)
-      // the refills may not be hoisted above the last reads of the registers they overwrite: a hoisted
-      // load gets fresh registers, and the loop-carried copy back then waits out its whole latency
-      __builtin_amdgcn_sched_barrier(0);
-      HAR_B4_LOAD_D(t0 + i + 2)
-      HAR_B4_LOAD_X(t0 + i + 3)
-      __builtin_amdgcn_sched_barrier(0);  // the refills are issued before the h1 recompute
-      if (i == 4) HAR_STAMP(8, 27)
-      tile_h1(i + 1);  // X tile i+1 has been in LDS since the last barrier
-      if (i == 4) HAR_STAMP(8, 28)
-      __syncthreads();  // dact2 i+1 / X i+2 staged, h1 i+1 complete; the consumers finished tile i
+#define HAR_B4_ITER(i, ...)                                                                             \
+  {                                                                                                     \
+    if ((i) < 24) HAR_STAMP(8, 2 + (i))                                                                 \
+    if constexpr (STAMP) { /* (stamped build only: how long the dact2 refill is still in flight) */    \
+      if ((i) == 4) {                                                                                   \
+        __builtin_amdgcn_s_waitcnt(0x0f70 | (8 + XPT));                                                 \
+        HAR_STAMP(8, 32)                                                                                \
+      }                                                                                                 \
+    }                                                                                                   \
+    HAR_B4_STAGE_D(((i) + 1) & 1, __VA_ARGS__) /* waits for the dact2 loads issued two iterations ago */ \
+    if ((i) == 4) HAR_STAMP(8, 26)                                                                      \
+    HAR_B4_STAGE_X((i) + 2)                                                                             \
+    /* the refills may not be hoisted above the last reads of the registers they overwrite: a hoisted  \
+       load gets fresh registers, and the loop-carried copy back then waits out its whole latency */   \
+    __builtin_amdgcn_sched_barrier(0);                                                                  \
+    HAR_B4_LOAD_D(t0 + (i) + 3, __VA_ARGS__)                                                            \
+    HAR_B4_LOAD_X(t0 + (i) + 3)                                                                         \
+    __builtin_amdgcn_sched_barrier(0); /* the refills are issued before the h1 recompute */           \
+    if ((i) == 4) HAR_STAMP(8, 27)                                                                      \
+    tile_h1((i) + 1); /* X tile i+1 has been in LDS since the last barrier */                         \
+    if ((i) == 4) HAR_STAMP(8, 28)                                                                      \
+    __syncthreads(); /* dact2 i+1 / X i+2 staged, h1 i+1 complete; the consumers finished tile i */    \
+  }
+    int i = 0;
+    for (; i + 1 < n; i += 2) {
+      HAR_B4_ITER(i, HAR_DA)
+      HAR_B4_ITER(i + 1, HAR_DB)
     }
+    if (i < n) HAR_B4_ITER(i, HAR_DA)
     HAR_STAMP(8, 34)
+#undef HAR_B4_ITER
+#undef HAR_B4_STAGE_D
+#undef HAR_B4_STAGE_D_I
+#undef HAR_DA
+#undef HAR_DB
 #undef HAR_B4_LOAD_D
+#undef HAR_B4_LOAD_D_I
 #undef HAR_B4_LOAD_X
 #undef HAR_B4_STAGE_X
   } else {
