@@ -1,29 +1,30 @@
 // Fused training step of the flagship MLP (BASELINE.json config 3: 43-256-256-6, bf16 MFMA; SURVEY.md
 // K23), H = 256 hidden units, K0 = 32 / 64 padded inputs, <= 16 classes, batch a multiple of 64.
-// Three kernels per step: mlp_fwd3 -> mlp_bwd4 (the wave-specialized backward; mlp_bwd3, the
-// data-split form, stays selectable with HAR_MLP_BWD=3) -> grad_reduce_adam (mlp.hip).
+// Three kernels per step: mlp_fwd3 -> mlp_bwd4 (the wave-specialized backward) -> grad_reduce_adam
+// (mlp.hip).
 //
-// The forward hands the backward only what it cannot recompute cheaply: the logit gradients dz
-// ([B][16] bf16, 32 B per row) and the relu' mask of h2 ([B][8] u32, 32 B per row) — 4 MB at batch
-// 65,536 instead of the 32 MB dact2 of the previous design.  The backward rebuilds each dact2 tile on
-// chip, dact2^T = (Wout^T . dz^T) * relu'(h2) (one 16x16x16 MFMA per 16 x 16 block, K = 16 classes),
-// and recomputes h1 = relu(W0 x + b0) from the X tiles it reads anyway.
+// The forward hands the backward dact2 = (dz . Wout) * relu'(h2) ([B][256] bf16, written in the
+// backward's LDS tile order with its chunk swizzle); the backward recomputes h1 = relu(W0 x + b0)
+// from the X tiles it reads anyway.
 //
 // mlp_fwd3 (persistent, one 8-wave workgroup per CU, 32-row tiles).  Wave w owns hidden units
 // [32w, 32w + 32) of both layers; its slices of W0, W1 and Wout stay in registers.  Per tile:
 //   stage 1  h1^T = W0 . X^T (bias as the initial accumulator) -> LDS h1 tile        | B1
-//   stage 5  (previous tile) dWout^T += h2^T . dz over its 32 rows (operands from LDS images)
-//   stage 2  h2^T = W1 . h1^T (h1 from LDS, 16-byte reads); relu' bits of the wave's units -> mask
+//   stage 5  (previous tile) dWout^T += h2^T . dz over its 32 rows (operands from LDS images) and
+//            dact2 of the wave's units (16x16x16 MFMAs, relu'(h2) from the h2 image) -> global
+//   stage 2  h2^T = W1 . h1^T (h1 from LDS, 16-byte reads, software-pipelined)
 //   stage 3  partial logits over the wave's 32 units -> LDS; h2 images for stage 5      | B2
 //   softmax  spread over ALL 512 lanes — lane = (row 4w + g, class c16): the 8 partials in a fixed
-//            order, max / sum over the 16 class lanes of the row, CE, argmax, dz -> LDS + global
+//            order, max / sum over the 16 class lanes of the row, CE, argmax, dz -> LDS
 // Two barriers per tile and no serial section: stage 5 of a tile runs after the next tile's B1, so
 // the dz exchange needs no barrier of its own (dz and the h2 images are double-buffered).
 //
-// mlp_bwd3 (S row slices x 4 h1-unit quadrants of 64 units; 64-row tiles, one barrier per tile):
-//   dact2 tile i+1 (MFMA from dz / mask registers loaded a tile ahead) -> LDS | X tile i+2 -> LDS |
-//   h1 tile i+1 recomputed from X | (a) dact1^T = W1^T[u] . dact2^T, relu'(h1) | (b) dW1 += h1^T . dact2
-//   | (c) dW0 += dact1^T . X of tile i-1 | db1 = sum_rows dact2 (a ones-row MFMA, 64 j per quadrant) | barrier
+// mlp_bwd4 (S row slices x 4 h1-unit quadrants of 64 units; 64-row tiles, one barrier per tile;
+// producer waves 0-3 / consumer waves 4-7, see the kernel's comment):
+//   producers: dact2 tile i+1 (copied, loaded two tiles ahead) -> LDS | X tile i+2 -> LDS | h1 tile
+//              i+1 recomputed from X | (c) dW0 += dact1^T . X and db0 of tile i-1
+//   consumers: (a) dact1^T = W1^T[u] . dact2^T, relu'(h1) | (b) dW1 += h1^T . dact2 | db1 = sum_rows
+//              dact2 (a ones-row MFMA, 64 j per quadrant)
 // One deterministic partial per (slice, quadrant), laid out like the flat parameter buffer.
 #include <algorithm>
 #include <type_traits>
@@ -459,17 +460,17 @@ template <int K0> struct Bwd4Lds {
 // ------------------------------------------------------------------------------------------------
 // backward, wave-specialized (mlp_bwd4): the 8 waves split by role.  Waves 0..3 PRODUCE the next
 // tile's operands (the dact2 tile copied from the forward's dact2 rows, the X tile staging and the h1
-// recompute: loads, LDS stores and a few small MFMAs); waves 4..7 CONSUME the current tile (the (a)
-// dact1, (b) dW1, (c) dW0, db0 / db1 products: MFMA with LDS fragment reads).  Each SIMD hosts one
+// recompute: loads, LDS stores and a few small MFMAs) and take the (c) dW0 / db0 products of the
+// previous tile; waves 4..7 CONSUME the current tile (the (a) dact1, (b) dW1, db1 products: MFMA with
+// LDS fragment reads).  Each SIMD hosts one
 // producer and one consumer, so the producer's load / LDS-store stream issues beside the consumer's
 // MFMA stream.  Each role runs its own loop (disjoint register live ranges: max, not sum, of the two
 // roles' state) with the same barrier sequence: one workgroup barrier per tile.
 //   consumer c: (a) unit blocks 2 (c & 1) .. + 1 x row blocks 2 (c >> 1) .. + 1 (W1^T fragments in
 //               registers, dact2 rows from LDS); (b) all 4 unit blocks x j blocks 4c .. 4c + 3
-//               (64 dW1 accumulators); (c) unit block c x every input block; db0 of unit block c;
-//               db1 of j block 4q + c
-//   producer p: dact2 / X staging (8 / 1-2 16-byte pieces per thread, loaded a tile ahead); h1 unit
-//               block p x all 4 row blocks
+//               (64 dW1 accumulators); db1 of j block 4q + c
+//   producer p: dact2 / X staging (8 / 1-2 16-byte pieces per thread, loaded two tiles ahead); h1
+//               unit block p x all 4 row blocks; (c) unit block p x every input block, db0 of unit block p
 // The forward computes dact2 = (dz . Wout) * relu'(h2) beside its dWout stage (16x16x16 MFMAs on data
 // it holds anyway) and writes it in this kernel's LDS tile order: the 4 quadrant workgroups of a row
 // slice then copy the same rows (one HBM read, three L2 / MALL hits) instead of each rebuilding them
@@ -637,6 +638,22 @@ __global__ __launch_bounds__(512) void mlp_bwd4_kernel(
         *reinterpret_cast<uint2*>(hs + (16 * rr + c16) * BUP + 16 * pw + 4 * g) =
             make_uint2(relu2(pack2(a[rr][0], a[rr][1])), relu2(pack2(a[rr][2], a[rr][3])));
     };
+    // (c) dW0[u][f] += dact1^T . X of tile i (unit block pw, every input block) and db0: on the producer
+    // side since the consumers' (a) + (b) MFMA stream had become the longer half of a tile (profiles/r5)
+    f32x4_t acc0[NFB], accd0 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int f = 0; f < NFB; ++f) acc0[f] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    auto tile_c = [&](int i) __attribute__((always_inline)) {
+      const bf16_t* d1s = d1s0 + (i & 1) * L::HS;
+      const bf16_t* xs = xs0 + (i & (NXB - 1)) * L::XS;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const bf16x8_t A = frag_rows(d1s + 32 * ks * BUP, BUP, 16 * pw, lane);
+#pragma unroll
+        for (int f = 0; f < NFB; ++f) acc0[f] = mma32(A, frag_rows(xs + 32 * ks * XP, XP, 16 * f, lane), acc0[f]);
+        accd0 = mma32(A, ones, accd0);
+      }
+    };
     // invariant at the top of iteration i: the dact2 set of i's parity (A even, B odd) holds tile i+1,
     // the other set tile i+2; xr = X tile i+2 (loaded)
     HAR_B4_LOAD_D(t0, HAR_DA)
@@ -673,6 +690,8 @@ __global__ __launch_bounds__(512) void mlp_bwd4_kernel(
     if ((i) == 4) HAR_STAMP(8, 27)                                                                      \
     tile_h1((i) + 1); /* X tile i+1 has been in LDS since the last barrier */                         \
     if ((i) == 4) HAR_STAMP(8, 28)                                                                      \
+    if ((i) > 0) tile_c((i) - 1); /* dact1 i-1 completed at the last barrier; X i-1 is still staged */  \
+    if ((i) == 4) HAR_STAMP(8, 33)                                                                      \
     __syncthreads(); /* dact2 i+1 / X i+2 staged, h1 i+1 complete; the consumers finished tile i */    \
   }
     int i = 0;
@@ -682,6 +701,13 @@ __global__ __launch_bounds__(512) void mlp_bwd4_kernel(
     }
     if (i < n) HAR_B4_ITER(i, HAR_DA)
     HAR_STAMP(8, 34)
+    if (n > 0) tile_c(n - 1);
+    float* w0o = gw0 + (size_t)slice * slab_stride;
+#pragma unroll
+    for (int f = 0; f < NFB; ++f)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) w0o[(size_t)(qu0 + 16 * pw + 4 * g + r) * K0 + 16 * f + c16] = acc0[f][r];
+    if (c16 == 0) *reinterpret_cast<f32x4_t*>(gb0 + (size_t)slice * slab_stride + qu0 + 16 * pw + 4 * g) = accd0;
 #undef HAR_B4_ITER
 #undef HAR_B4_STAGE_D
 #undef HAR_B4_STAGE_D_I
@@ -705,13 +731,11 @@ __global__ __launch_bounds__(512) void mlp_bwd4_kernel(
     // (paired with the producers' "prologue images are read" barrier: the W1^T image is read above,
     // the producers then overwrite it with dact2 tile 0)
     __syncthreads();
-    f32x4_t acc1[4][4], acc0[NFB], accb = {0.f, 0.f, 0.f, 0.f}, accd0 = {0.f, 0.f, 0.f, 0.f};
+    f32x4_t acc1[4][4], accb = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int j = 0; j < 4; ++j)
 #pragma unroll
       for (int u = 0; u < 4; ++u) acc1[j][u] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int f = 0; f < NFB; ++f) acc0[f] = f32x4_t{0.f, 0.f, 0.f, 0.f};
     // (a) dact1^T = W1^T[u] . dact2^T over row blocks ra0, ra0 + 1; relu'(h1); dact1 -> LDS
     // Software-pipelined: the dact2 fragments of k chunk kc + 3 are read while the MFMAs of chunk kc
     // run (pinned by scheduling groups: 2 LDS reads, then 4 MFMAs, per chunk), and the relu'(h1)
@@ -791,18 +815,6 @@ __global__ __launch_bounds__(512) void mlp_bwd4_kernel(
         accb = mma32(ones, frag_rows_sw(dsm + 32 * ks * BDP, BDP, 16 * (4 * q + pw), lane), accb);
       }
     };
-    // (c) dW0[u][f] += dact1^T . X of tile i (unit block pw, every input block) and db0
-    auto tile_c = [&](int i) __attribute__((always_inline)) {
-      const bf16_t* d1s = d1s0 + (i & 1) * L::HS;
-      const bf16_t* xs = xs0 + (i & (NXB - 1)) * L::XS;
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        const bf16x8_t A = frag_rows(d1s + 32 * ks * BUP, BUP, 16 * pw, lane);
-#pragma unroll
-        for (int f = 0; f < NFB; ++f) acc0[f] = mma32(A, frag_rows(xs + 32 * ks * XP, XP, 16 * f, lane), acc0[f]);
-        accd0 = mma32(A, ones, accd0);
-      }
-    };
     __builtin_amdgcn_s_setprio(1);  // the consumers' MFMA stream is the critical path of a tile
     __syncthreads();  // (paired with the producers' barrier: dact2 0, X 0 / 1 staged)
     __syncthreads();  // (paired: h1 tile 0 complete)
@@ -812,12 +824,9 @@ __global__ __launch_bounds__(512) void mlp_bwd4_kernel(
       if (i == 4) HAR_STAMP(8, 29)
       tile_b(i);
       if (i == 4) HAR_STAMP(8, 30)
-      if (i > 0) tile_c(i - 1);
-      if (i == 4) HAR_STAMP(8, 31)
       __syncthreads();  // dact1 i complete; the buffers of tile i may be overwritten
     }
     HAR_STAMP(8, 34)
-    if (n > 0) tile_c(n - 1);
     __builtin_amdgcn_s_setprio(0);
     // ---- this wave's parts of slab `slice` (flat parameter layout) ----
     float* w1o = gw1 + (size_t)slice * slab_stride;
@@ -826,13 +835,7 @@ __global__ __launch_bounds__(512) void mlp_bwd4_kernel(
 #pragma unroll
       for (int u = 0; u < 4; ++u)
         *reinterpret_cast<f32x4_t*>(w1o + (size_t)(16 * (4 * pw + j) + c16) * HH + qu0 + 16 * u + 4 * g) = acc1[j][u];
-    float* w0o = gw0 + (size_t)slice * slab_stride;
-#pragma unroll
-    for (int f = 0; f < NFB; ++f)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) w0o[(size_t)(qu0 + 16 * pw + 4 * g + r) * K0 + 16 * f + c16] = acc0[f][r];
     if (g == 0) gb1[(size_t)slice * slab_stride + 16 * (4 * q + pw) + c16] = accb[0];
-    if (c16 == 0) *reinterpret_cast<f32x4_t*>(gb0 + (size_t)slice * slab_stride + qu0 + 16 * pw + 4 * g) = accd0;
   }
   if constexpr (STAMP) __builtin_amdgcn_s_waitcnt(0x0f70);
   HAR_STAMP(8, 35)

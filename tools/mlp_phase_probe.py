@@ -107,12 +107,13 @@ def stamps(B=65536):
         if k == 1 and bwd4 and producer and (s[:, 26] > 0).all():  # mlp_bwd4 producer phases of tile 4
             sub = [("  tile 4: dact2 refill wait", s[:, 32] - s[:, 6]),
                    ("  tile 4: dact2 (tile 5) -> LDS", s[:, 26] - s[:, 32]), ("  tile 4: X stage + refills", s[:, 27] - s[:, 26]),
-                   ("  tile 4: h1 recompute (tile 5)", s[:, 28] - s[:, 27]), ("  tile 4: barrier", s[:, 7] - s[:, 28])]
+                   ("  tile 4: h1 recompute (tile 5)", s[:, 28] - s[:, 27]), ("  tile 4: (c) dW0 + db0 (tile 3)", s[:, 33] - s[:, 28]),
+                   ("  tile 4: barrier", s[:, 7] - s[:, 33])]
             for nm, v in sub:
                 print(f"  {nm:28s} median {np.median(v):9.0f}  max {v.max():9.0f} cycles")
         if k == 1 and bwd4 and producer is False and (s[:, 29] > 0).all():  # mlp_bwd4 consumer phases
             sub = [("  tile 4: (a) dact1", s[:, 29] - s[:, 6]), ("  tile 4: (b) dW1 + db1", s[:, 30] - s[:, 29]),
-                   ("  tile 4: (c) dW0 + db0 (tile 3)", s[:, 31] - s[:, 30]), ("  tile 4: barrier", s[:, 7] - s[:, 31])]
+                   ("  tile 4: barrier", s[:, 7] - s[:, 30])]
             for nm, v in sub:
                 print(f"  {nm:28s} median {np.median(v):9.0f}  max {v.max():9.0f} cycles")
         if k == 1 and not bwd4 and (s[:, 26] > 0).all():  # backward sub-phases of tile 4 (stamped slots 26..30)
