@@ -254,7 +254,7 @@ __global__ __launch_bounds__(64 * GR_W) void grad_reduce_adam_kernel(GradRegions
                                                                 float* __restrict__ v, bf16_t* __restrict__ pb,
                                                                 float lr, float b1, float b2, float eps, float wd,
                                                                 const int32_t* __restrict__ step, int mode,
-                                                                MlpFragSpec frag) {
+                                                                MlpFragSpec frag, int wide) {
   __shared__ float4 part[GR_W][64];
   const int q = threadIdx.x >> 6, k = threadIdx.x & 63;
   const int64_t i4 = (int64_t)blockIdx.x * 64 + k, e = i4 * 4;
@@ -278,6 +278,21 @@ __global__ __launch_bounds__(64 * GR_W) void grad_reduce_adam_kernel(GradRegions
         const int S = rg.S[r];
         const int64_t ld = rg.lds[r];
         int s = q;
+        if (wide) {  // 16 loads in flight per step (HAR_GR_NL=16)
+          for (; s + 15 * GR_W < S; s += 16 * GR_W) {
+            float4 x[16];
+#pragma unroll
+            for (int j = 0; j < 16; ++j) x[j] = *reinterpret_cast<const float4*>(p + (size_t)(s + j * GR_W) * ld);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+              x[j].x += x[j + 8].x; x[j].y += x[j + 8].y; x[j].z += x[j + 8].z; x[j].w += x[j + 8].w;
+            }
+            acc.x += ((x[0].x + x[1].x) + (x[2].x + x[3].x)) + ((x[4].x + x[5].x) + (x[6].x + x[7].x));
+            acc.y += ((x[0].y + x[1].y) + (x[2].y + x[3].y)) + ((x[4].y + x[5].y) + (x[6].y + x[7].y));
+            acc.z += ((x[0].z + x[1].z) + (x[2].z + x[3].z)) + ((x[4].z + x[5].z) + (x[6].z + x[7].z));
+            acc.w += ((x[0].w + x[1].w) + (x[2].w + x[3].w)) + ((x[4].w + x[5].w) + (x[6].w + x[7].w));
+          }
+        }
         for (; s + 7 * GR_W < S; s += 8 * GR_W) {
           float4 x[8];
 #pragma unroll
@@ -437,15 +452,19 @@ extern "C" int har_grad_reduce_adam(int nreg, const float* const* src, const int
     const char* e = getenv("HAR_GR_W");
     return e ? atoi(e) : 4;
   }();
+  static const int wide = [] {
+    const char* e = getenv("HAR_GR_NL");
+    return e && atoi(e) == 16 ? 1 : 0;
+  }();
   if (w == 4)
     grad_reduce_adam_kernel<4><<<(int)blocks, 256, 0, s>>>(rg, n, G, param, m, v, pb, lr, b1, b2, eps, wd, step, mode,
-                                                           frag);
+                                                           frag, wide);
   else if (w == 8)
     grad_reduce_adam_kernel<8><<<(int)blocks, 512, 0, s>>>(rg, n, G, param, m, v, pb, lr, b1, b2, eps, wd, step, mode,
-                                                           frag);
+                                                           frag, wide);
   else
     grad_reduce_adam_kernel<16><<<(int)blocks, 1024, 0, s>>>(rg, n, G, param, m, v, pb, lr, b1, b2, eps, wd, step,
-                                                             mode, frag);
+                                                             mode, frag, wide);
   HAR_CHECK_LAUNCH();
   return 0;
 }

@@ -483,7 +483,7 @@ __global__ __launch_bounds__(512) void mlp_bwd4_kernel(
     int B, int S, float* __restrict__ gw1, float* __restrict__ gw0,
     float* __restrict__ gb0, float* __restrict__ gb1, int64_t slab_stride, int32_t* __restrict__ tick,
     const float* __restrict__ fslab, int fslab_w, int nfwd, float* __restrict__ gwo, float* __restrict__ gbo,
-    uint64_t* __restrict__ stamps) {
+    uint64_t* __restrict__ stamps, int nt_slab) {
   using L = Bwd4Lds<K0>;
   constexpr int NXB = L::NXB, KC = HH / 32, XP = L::XP, NFW = K0 / 32, NFB = K0 / 16;
   constexpr int XV = BRT * K0 / 8;  // 16-byte vectors of an X tile (512 / 256)
@@ -834,7 +834,10 @@ __global__ __launch_bounds__(512) void mlp_bwd4_kernel(
     for (int j = 0; j < 4; ++j)
 #pragma unroll
       for (int u = 0; u < 4; ++u)
-        *reinterpret_cast<f32x4_t*>(w1o + (size_t)(16 * (4 * pw + j) + c16) * HH + qu0 + 16 * u + 4 * g) = acc1[j][u];
+        if (nt_slab)
+          nt_store16(w1o + (size_t)(16 * (4 * pw + j) + c16) * HH + qu0 + 16 * u + 4 * g, __builtin_bit_cast(u32x4_t, acc1[j][u]));
+        else
+          *reinterpret_cast<f32x4_t*>(w1o + (size_t)(16 * (4 * pw + j) + c16) * HH + qu0 + 16 * u + 4 * g) = acc1[j][u];
     if (g == 0) gb1[(size_t)slice * slab_stride + 16 * (4 * q + pw) + c16] = accb[0];
   }
   if constexpr (STAMP) __builtin_amdgcn_s_waitcnt(0x0f70);
@@ -871,9 +874,15 @@ template <int K0>
 void launch_bwd4(const bf16_t* dact2, const bf16_t* X, const bf16_t* Wf, const float* b0, int B, int S, float* gw1,
                  float* gw0, float* gb0, float* gb1, int64_t stride, int32_t* tick, const float* fslab, int fslab_w,
                  int nfwd, float* gwo, float* gbo, hipStream_t s) {
+  // HAR_MLP_BWD_NT=1: the dW1 partial slabs written with nontemporal stores
+  static const int nt = [] {
+    const char* e = getenv("HAR_MLP_BWD_NT");
+    return e ? atoi(e) : 0;
+  }();
   auto k = g_har_mlp_stamps ? mlp_bwd4_kernel<K0, true> : mlp_bwd4_kernel<K0, false>;
   k<<<S * BQ, 512, Bwd4Lds<K0>::bytes, s>>>(dact2, X, Wf, b0, B, S, gw1, gw0, gb0, gb1, stride, tick, fslab, fslab_w,
-                                           nfwd, gwo, gbo, g_har_mlp_stamps ? g_har_mlp_stamps + STAMP_BWD_OFF : nullptr);
+                                           nfwd, gwo, gbo, g_har_mlp_stamps ? g_har_mlp_stamps + STAMP_BWD_OFF : nullptr,
+                                           nt);
 }
 
 }  // namespace
