@@ -518,29 +518,7 @@ __global__ __launch_bounds__(512) void mlp_bwd4_kernel(
 #pragma unroll
     for (int i = 0; i < 4; ++i) *reinterpret_cast<uint4*>(w1q + (i * 8 + wave) * 512 + lane * 8) = st[i];
   }
-  constexpr int WO4 = NCLS * HH / 4, NC4 = WO4 + NCLS / 4;
-  const int gwv = blockIdx.x * 8 + wave, nwv = gridDim.x * 8;
-  f32x4_t px[4];
-  auto wo_load = [&](int c4) {
-    const float* src = fslab + (c4 < WO4 ? 4 * c4 : NCLS * HH + 4 * (c4 - WO4));
-#pragma unroll
-    for (int r = 0; r < 4; ++r)
-      px[r] = lane + 64 * r < nfwd ? *reinterpret_cast<const f32x4_t*>(src + (size_t)(lane + 64 * r) * fslab_w)
-                                   : f32x4_t{0.f, 0.f, 0.f, 0.f};
-  };
-  if (fslab && gwv < NC4) wo_load(gwv);
   __syncthreads();
-  if (fslab) {
-    for (int c4 = gwv; c4 < NC4; c4 += nwv) {
-      if (c4 != gwv) wo_load(c4);
-      f32x4_t v = (px[0] + px[1]) + (px[2] + px[3]);
-#pragma unroll
-      for (int o = 32; o >= 1; o >>= 1)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] += __shfl_xor(v[e], o, 64);
-      if (lane == 0) *reinterpret_cast<f32x4_t*>(c4 < WO4 ? gwo + 4 * c4 : gbo + 4 * (c4 - WO4)) = v;
-    }
-  }
   // a row of ones (A operand: row 0) / a column of ones (B operand: column 0): the same registers
   const bf16x8_t ones = __builtin_bit_cast(bf16x8_t, c16 == 0 ? s16x8_t{0x3f80, 0x3f80, 0x3f80, 0x3f80, 0x3f80,
                                                                         0x3f80, 0x3f80, 0x3f80}
@@ -708,6 +686,25 @@ __global__ __launch_bounds__(512) void mlp_bwd4_kernel(
 #pragma unroll
       for (int r = 0; r < 4; ++r) w0o[(size_t)(qu0 + 16 * pw + 4 * g + r) * K0 + 16 * f + c16] = acc0[f][r];
     if (c16 == 0) *reinterpret_cast<f32x4_t*>(gb0 + (size_t)slice * slab_stride + qu0 + 16 * pw + 4 * g) = accd0;
+    // the forward's dWout / dbout slabs (one per forward workgroup) -> gwo / gbo: one 4-column group per
+    // producer wave of the grid, after the producers' last tile (they finish ahead of the consumers;
+    // in the prologue the task waves of half the workgroups had started their tiles ~4k cycles late)
+    if (fslab) {
+      constexpr int WO4 = NCLS * HH / 4, NC4 = WO4 + NCLS / 4;
+      const LaneSwap lsw(lane);
+      for (int c4 = pw * (int)gridDim.x + (int)blockIdx.x; c4 < NC4; c4 += 4 * (int)gridDim.x) {
+        const float* src = fslab + (c4 < WO4 ? 4 * c4 : NCLS * HH + 4 * (c4 - WO4));
+        f32x4_t px[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          px[r] = lane + 64 * r < nfwd ? *reinterpret_cast<const f32x4_t*>(src + (size_t)(lane + 64 * r) * fslab_w)
+                                       : f32x4_t{0.f, 0.f, 0.f, 0.f};
+        f32x4_t v = (px[0] + px[1]) + (px[2] + px[3]);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = wave_sum_dpp(v[e], lsw);
+        if (lane == 0) *reinterpret_cast<f32x4_t*>(c4 < WO4 ? gwo + 4 * c4 : gbo + 4 * (c4 - WO4)) = v;
+      }
+    }
 #undef HAR_B4_ITER
 #undef HAR_B4_STAGE_D
 #undef HAR_B4_STAGE_D_I
