@@ -532,6 +532,16 @@ __global__ __launch_bounds__(512) void mlp_bwd4_kernel(
     for (int kc = 0; kc < NFW; ++kc)
       w0q[kc] = *reinterpret_cast<const bf16x8_t*>(W0f + (size_t)((4 * q + pw) * NFW + kc) * 512 + frag_lane_off(lane));
     const float4 b0q = *reinterpret_cast<const float4*>(b0 + qu0 + 16 * pw + 4 * g);
+    constexpr int WO4 = NCLS * HH / 4, NC4 = WO4 + NCLS / 4;
+    f32x4_t px[4];
+    auto wo_load = [&](int c4) __attribute__((always_inline)) {
+      const float* src = fslab + (c4 < WO4 ? 4 * c4 : NCLS * HH + 4 * (c4 - WO4));
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        px[r] = lane + 64 * r < nfwd ? *reinterpret_cast<const f32x4_t*>(src + (size_t)(lane + 64 * r) * fslab_w)
+                                     : f32x4_t{0.f, 0.f, 0.f, 0.f};
+    };
+    if (fslab && 4 * b + pw < NC4) wo_load(4 * b + pw);
     if constexpr (STAMP) __builtin_amdgcn_s_waitcnt(0x0f70);
     HAR_STAMP(8, 1)
     __syncthreads();  // the prologue images are read: the tile buffers may be written
@@ -686,34 +696,21 @@ __global__ __launch_bounds__(512) void mlp_bwd4_kernel(
 #pragma unroll
       for (int r = 0; r < 4; ++r) w0o[(size_t)(qu0 + 16 * pw + 4 * g + r) * K0 + 16 * f + c16] = acc0[f][r];
     if (c16 == 0) *reinterpret_cast<f32x4_t*>(gb0 + (size_t)slice * slab_stride + qu0 + 16 * pw + 4 * g) = accd0;
-    // the forward's dWout / dbout slabs (one per forward workgroup) -> gwo / gbo: one 4-column group per
-    // producer wave of the grid, after the producers' last tile (they finish ahead of the consumers;
-    // in the prologue the task waves of half the workgroups had started their tiles ~4k cycles late)
+    // the forward's dWout / dbout slabs (one per forward workgroup) -> gwo / gbo: 4-column group
+    // 4 b + pw per producer wave (b the XCD-remapped index: the 8 groups of a 128-byte line in two
+    // workgroups of one XCD), its loads issued in the prologue and summed here, after the last tile.
+    // (In the prologue proper the task waves started their tiles ~4k cycles late; loaded here, with
+    // neighbouring groups on other XCDs, the gather took ~17k cycles, profiles/r5)
     if (fslab) {
-      constexpr int WO4 = NCLS * HH / 4, NC4 = WO4 + NCLS / 4;
       const LaneSwap lsw(lane);
-      for (int c4 = pw * (int)gridDim.x + (int)blockIdx.x; c4 < NC4; c4 += 4 * (int)gridDim.x) {
-        const float* src = fslab + (c4 < WO4 ? 4 * c4 : NCLS * HH + 4 * (c4 - WO4));
-        f32x4_t px[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          px[r] = lane + 64 * r < nfwd ? *reinterpret_cast<const f32x4_t*>(src + (size_t)(lane + 64 * r) * fslab_w)
-                                       : f32x4_t{0.f, 0.f, 0.f, 0.f};
+      for (int c4 = 4 * b + pw; c4 < NC4; c4 += 4 * (int)gridDim.x) {
+        if (c4 != 4 * b + pw) wo_load(c4);
         f32x4_t v = (px[0] + px[1]) + (px[2] + px[3]);
 #pragma unroll
         for (int e = 0; e < 4; ++e) v[e] = wave_sum_dpp(v[e], lsw);
         if (lane == 0) *reinterpret_cast<f32x4_t*>(c4 < WO4 ? gwo + 4 * c4 : gbo + 4 * (c4 - WO4)) = v;
       }
     }
-#undef HAR_B4_ITER
-#undef HAR_B4_STAGE_D
-#undef HAR_B4_STAGE_D_I
-#undef HAR_DA
-#undef HAR_DB
-#undef HAR_B4_LOAD_D
-#undef HAR_B4_LOAD_D_I
-#undef HAR_B4_LOAD_X
-#undef HAR_B4_STAGE_X
   } else {
     // ================================ consumer ================================
     const int ua0 = 2 * (pw & 1), ra0 = 2 * (pw >> 1);

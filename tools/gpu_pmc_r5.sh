@@ -19,5 +19,5 @@ while read -r grp; do
   rc=$?; echo "mlp pass $i: rc=$rc"; [ $rc -ne 0 ] && exit $rc
 done < "$ROOT/tools/${2:-pmc_groups_step.txt}"
 cd "$ROOT"
-python3 tools/pmc_table.py $OUT/mlp[0-9] $OUT/mlp[0-9][0-9] > "$OUT/pmc.md" 2>&1; head -12 "$OUT/pmc.md"
+python3 tools/pmc_table.py $(ls -d $OUT/mlp[0-9]* | grep -v "\.log$") > "$OUT/pmc.md" 2>&1; head -12 "$OUT/pmc.md"
 echo done
