@@ -86,6 +86,20 @@ __device__ __forceinline__ bf16x8_t frag_rows_sw(const bf16_t* img, int pitch, i
   return __builtin_bit_cast(bf16x8_t, v);
 }
 
+// frag_rows of an image whose 4-column (8-byte) chunks are XOR-swizzled by row within each 16-column
+// block: the chunk of columns 4c .. 4c + 3 of row r lives at chunk c ^ ((r >> 2) & 3) (col0 a multiple
+// of 16).  The lane's rows 4g + (li >> 2) (+ 16, + 32 ks) all have (r >> 2) & 3 = g.  8-byte stores of
+// 16 consecutive rows at one column (bank group of 16 lanes) then hit 32 distinct banks at a pitch of
+// 40 dwords (unswizzled: 4-way), and these transposing reads stay conflict-free.
+__device__ __forceinline__ bf16x8_t frag_rows_q(const bf16_t* img, int pitch, int col0, int lane) {
+  const int li = lane & 15, g = lane >> 4;
+  const bf16_t* p0 = img + (4 * g + (li >> 2)) * pitch + col0 + 4 * ((li & 3) ^ g);
+  const s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)p0);
+  const s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(p0 + 16 * pitch));
+  const s16x8_t v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8_t, v);
+}
+
 // cross-lane steps on the VALU (DPP / permlane): wave_ops.h (dpp_i / dpp_f, vmaxf, row16_*, LaneSwap)
 using namespace wops;
 

@@ -446,7 +446,8 @@ __global__ __launch_bounds__(512) void mlp_fwd3_kernel(
 constexpr int BQ = 4, BQU = HH / BQ;  // 64 h1 units per workgroup
 constexpr int BRT = 64;               // rows per pipeline tile
 constexpr int BDP = HH + 16;          // dact2 tile pitch: 136 dwords (8 mod 64)
-constexpr int BUP = BQU + 16;         // h1 / dact1 quadrant tile pitch: 40 dwords
+constexpr int BUP = BQU + 16;         // h1 / dact1 quadrant tile pitch: 40 dwords; 8-byte chunks
+                                      // swizzled by row (frag_rows_q)
 
 template <int K0> struct Bwd4Lds {
   static constexpr int XP = K0 + 16;
@@ -623,7 +624,7 @@ __global__ __launch_bounds__(512) void mlp_bwd4_kernel(
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int rr = 0; rr < 4; ++rr)
-        *reinterpret_cast<uint2*>(hs + (16 * rr + c16) * BUP + 16 * pw + 4 * g) =
+        *reinterpret_cast<uint2*>(hs + (16 * rr + c16) * BUP + 16 * pw + 4 * (g ^ (c16 >> 2))) =
             make_uint2(relu2(pack2(a[rr][0], a[rr][1])), relu2(pack2(a[rr][2], a[rr][3])));
     };
     // (c) dW0[u][f] += dact1^T . X of tile i (unit block pw, every input block) and db0: on the producer
@@ -636,7 +637,7 @@ __global__ __launch_bounds__(512) void mlp_bwd4_kernel(
       const bf16_t* xs = xs0 + (i & (NXB - 1)) * L::XS;
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
-        const bf16x8_t A = frag_rows(d1s + 32 * ks * BUP, BUP, 16 * pw, lane);
+        const bf16x8_t A = frag_rows_q(d1s + 32 * ks * BUP, BUP, 16 * pw, lane);
 #pragma unroll
         for (int f = 0; f < NFB; ++f) acc0[f] = mma32(A, frag_rows(xs + 32 * ks * XP, XP, 16 * f, lane), acc0[f]);
         accd0 = mma32(A, ones, accd0);
@@ -750,7 +751,7 @@ __global__ __launch_bounds__(512) void mlp_bwd4_kernel(
       for (int rr = 0; rr < 2; ++rr)
 #pragma unroll
         for (int e = 0; e < 2; ++e)
-          hm[rr][e] = *reinterpret_cast<const uint2*>(hs + (16 * (ra0 + rr) + c16) * BUP + 16 * (ua0 + e) + 4 * g);
+          hm[rr][e] = *reinterpret_cast<const uint2*>(hs + (16 * (ra0 + rr) + c16) * BUP + 16 * (ua0 + e) + 4 * (g ^ (c16 >> 2)));
       bf16x8_t bv[2][KC];
 #pragma unroll
       for (int kc = 0; kc < PD; ++kc)
@@ -787,7 +788,7 @@ __global__ __launch_bounds__(512) void mlp_bwd4_kernel(
           const uint2 m = hm[rr][e];
           const float d0 = (m.x & 0xffffu) ? a[0] : 0.f, d1 = (m.x >> 16) ? a[1] : 0.f;
           const float d2 = (m.y & 0xffffu) ? a[2] : 0.f, d3 = (m.y >> 16) ? a[3] : 0.f;
-          *reinterpret_cast<uint2*>(d1s + (16 * (ra0 + rr) + c16) * BUP + 16 * (ua0 + e) + 4 * g) =
+          *reinterpret_cast<uint2*>(d1s + (16 * (ra0 + rr) + c16) * BUP + 16 * (ua0 + e) + 4 * (g ^ (c16 >> 2))) =
               make_uint2(pack2(d0, d1), pack2(d2, d3));
         }
     };
@@ -799,7 +800,7 @@ __global__ __launch_bounds__(512) void mlp_bwd4_kernel(
       for (int ks = 0; ks < 2; ++ks) {
         bf16x8_t hb[4];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) hb[u] = frag_rows(hs + 32 * ks * BUP, BUP, 16 * u, lane);
+        for (int u = 0; u < 4; ++u) hb[u] = frag_rows_q(hs + 32 * ks * BUP, BUP, 16 * u, lane);
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const bf16x8_t da = frag_rows_sw(dsm + 32 * ks * BDP, BDP, 16 * (4 * pw + j), lane);
