@@ -100,6 +100,17 @@ __device__ __forceinline__ bf16x8_t frag_rows_q(const bf16_t* img, int pitch, in
   return __builtin_bit_cast(bf16x8_t, v);
 }
 
+// frag_rows of an image whose 4-column chunks are XOR-permuted per row: `x` = the chunk XOR of the
+// lane's rows 4g + (li >> 2) (+ 16) (the caller's swizzle must give those rows one value)
+__device__ __forceinline__ bf16x8_t frag_rows_x(const bf16_t* img, int pitch, int col0, int lane, int x) {
+  const int li = lane & 15, g = lane >> 4;
+  const bf16_t* p0 = img + (4 * g + (li >> 2)) * pitch + col0 + 4 * ((li & 3) ^ x);
+  const s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)p0);
+  const s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(p0 + 16 * pitch));
+  const s16x8_t v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8_t, v);
+}
+
 // cross-lane steps on the VALU (DPP / permlane): wave_ops.h (dpp_i / dpp_f, vmaxf, row16_*, LaneSwap)
 using namespace wops;
 

@@ -67,7 +67,12 @@ constexpr int FRT = 32;                // rows per tile
 // h1 tile: pitch 136 dwords, and the 16-byte column chunks of rows with bit 2 set swapped in pairs
 // (column ^ 8): the 16-byte reads of stage 2 are conflict-free (the stage-1 8-byte stores 2-way)
 constexpr int FHP = HH + 16;
-constexpr int FSP = 16 + 8;            // [32 rows][16 cols] transpose image pitch
+// [32 rows][16 cols] images (dz, h2) read by stage 5: unpadded rows (8 dwords) with their four 4-column
+// chunks XOR-permuted by row — h2 images: chunk c of row r at c ^ fh(r), fh(r) = 2 ((r >> 2) & 1) +
+// ((r >> 3) & 1); dz: c ^ fz(r), fz(r) = 2 ((r >> 3) & 1).  The stage-3 8-byte stores (16 rows, one
+// chunk), the 16-byte relu' reads, the dz reads and the transposing fragment reads are all
+// conflict-free (the padded 12-dword pitch had 2-way conflicts on each, profiles/r5)
+constexpr int FSP = 16;
 constexpr int FIMG = FRT * FSP;
 // partial logits of one (wave, half): lane group g's 16 lanes x 4 classes at dword 72 g + 4 c16: the
 // softmax lanes (row, class) then read 16 distinct banks per row and disjoint banks per row pair
@@ -114,6 +119,8 @@ __global__ __launch_bounds__(512) void mlp_fwd3_kernel(
   // softmax lane: tile row sr = 4 wave + g (half sh, row srr of it), class c16
   const int sr = 4 * wave + g, sh = sr >> 4, srr = sr & 15;
   const int hsw = 8 * ((c16 >> 2) & 1);  // h1 tile chunk swap of this lane's rows (16h + c16)
+  // stage-5 image chunk XORs of this lane's rows 16 h + c16 (FSP)
+  const int fh_row = 2 * ((c16 >> 2) & 1) + ((c16 >> 3) & 1), fz_row = 2 * ((c16 >> 3) & 1);
   f32x4_t acc5[2] = {f32x4_t{0.f, 0.f, 0.f, 0.f}, f32x4_t{0.f, 0.f, 0.f, 0.f}};
   float dbo = 0.f, lsum = 0.f, ncorr = 0.f;
   const int ntiles = B / FRT;
@@ -255,7 +262,8 @@ __global__ __launch_bounds__(512) void mlp_fwd3_kernel(
       for (int h = 0; h < 2; ++h)
 #pragma unroll
         for (int t = 0; t < 2; ++t)
-          *reinterpret_cast<uint2*>(ib + t * FIMG + (16 * h + c16) * FSP + 4 * g) = make_uint2(h2p[h][t][0], h2p[h][t][1]);
+          *reinterpret_cast<uint2*>(ib + t * FIMG + (16 * h + c16) * FSP + 4 * (g ^ fh_row)) =
+              make_uint2(h2p[h][t][0], h2p[h][t][1]);
     }
   };
   // ---- softmax / CE / argmax / dz of tile k (zs buffer `buf`): lane = (row sr, class c16) ----
@@ -285,7 +293,7 @@ __global__ __launch_bounds__(512) void mlp_fwd3_kernel(
     lsum += c16 == yc ? (mx + __logf(se)) - zz : 0.f;
     ncorr += (c16 == 0 && amx == yc) ? 1.f : 0.f;
     dbo += bf2f(db);
-    dzs[buf * FIMG + sr * FSP + c16] = db;
+    dzs[buf * FIMG + sr * FSP + (c16 ^ (8 * ((sr >> 3) & 1)))] = db;
   };
   // ---- stage 5 of a tile (dz buffer / image buffer `buf`, rows r0 ..): dWout^T += h2^T . dz over its
   // 32 rows, and the backward's layer-2 gradient dact2 = (dz . Wout) * relu'(h2) of the wave's 32
@@ -296,15 +304,19 @@ __global__ __launch_bounds__(512) void mlp_fwd3_kernel(
   bf16_t* const d2base = INFER ? nullptr : dact2_out + (size_t)c16 * HH + ((u0 + 8 * g) ^ hsw);
   auto stage5 = [&](int buf, int r0) __attribute__((always_inline)) {
     const bf16_t* zb = dzs + buf * FIMG;
-    const bf16x8_t bz = frag_tr(zb, FSP, 0, lane);
+    // (the permuted k order of frag_rows on both operands: k runs over the 32 tile rows)
+    const bf16x8_t bz = frag_rows_x(zb, FSP, 0, lane, 2 * (g >> 1));
     const bf16_t* ip = img + buf * 2 * FIMG;
 #pragma unroll
-    for (int t = 0; t < 2; ++t) acc5[t] = mma32(frag_tr(ip + t * FIMG, FSP, 0, lane), bz, acc5[t]);
+    for (int t = 0; t < 2; ++t) acc5[t] = mma32(frag_rows_x(ip + t * FIMG, FSP, 0, lane, 2 * (g & 1) + (g >> 1)), bz, acc5[t]);
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      const s16x4_t dzb = *reinterpret_cast<const s16x4_t*>(zb + (16 * h + c16) * FSP + 4 * g);
-      // h2 units 8 g .. 8 g + 7 of row 16 h + c16: image block g >> 1, columns 8 (g & 1) ..
-      const u32x4_t hv = *reinterpret_cast<const u32x4_t*>(ip + (g >> 1) * FIMG + (16 * h + c16) * FSP + 8 * (g & 1));
+      const s16x4_t dzb = *reinterpret_cast<const s16x4_t*>(zb + (16 * h + c16) * FSP + 4 * (g ^ fz_row));
+      // h2 units 8 g .. 8 g + 7 of row 16 h + c16: image block g >> 1, columns 8 (g & 1) .. — chunks
+      // 2 (g & 1), + 1 at the 16-byte pair (g & 1) ^ (fh >> 1), in swapped order when fh is odd
+      u32x4_t hv = *reinterpret_cast<const u32x4_t*>(ip + (g >> 1) * FIMG + (16 * h + c16) * FSP +
+                                                     8 * ((g & 1) ^ (fh_row >> 1)));
+      if (fh_row & 1) hv = u32x4_t{hv[2], hv[3], hv[0], hv[1]};
       const f32x4_t v0 = mma16(woT[0], dzb, f32x4_t{0.f, 0.f, 0.f, 0.f});
       const f32x4_t v1 = mma16(woT[1], dzb, f32x4_t{0.f, 0.f, 0.f, 0.f});
       // relu'(h2): a relu'd bf16 half is in [0, 0x7fff]; adding 0x7fff carries into its bit 15 exactly
