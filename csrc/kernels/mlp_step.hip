@@ -86,6 +86,8 @@ constexpr int FWD_SLAB = NCLS * HH + NCLS;  // per workgroup: dWout rows 0..15 [
 #endif
 constexpr int FPD = HAR_FWD_PD;      // stage-2 h1 read prefetch distance (k chunks)
 constexpr bool FPIN = HAR_FWD_PIN;   // pin the read / MFMA interleave with scheduling groups
+// FILL (template argument, HAR_MLP_FWD_FILL): VALU instructions of the tile's softmax interleaved
+// after each stage-2 MFMA (0: the softmax runs on its own, before stage 5)
 constexpr size_t FWD_LDS = (size_t)2 * FRT * FHP * 2 + (size_t)2 * FW * 2 * ZREG * 4 + (size_t)2 * FIMG * 2 +
                            (size_t)FW * 4 * FIMG * 2;
 
@@ -96,7 +98,7 @@ __device__ __forceinline__ bf16x8_t ldx(const bf16_t* __restrict__ X, int row, i
 
 // INFER: the serving forward of the same pipeline — no labels, no dz / relu' mask / dWout / W1^T copy;
 // `slab` receives the logits [B][C] (fp32, bias included) and `block_correct` the argmax [B].
-template <int K0, bool STAMP, bool INFER = false>
+template <int K0, bool STAMP, bool INFER = false, int FFILL = 0>
 __global__ __launch_bounds__(512) void mlp_fwd3_kernel(
     const bf16_t* __restrict__ X, bf16_t* __restrict__ Wf, const float* __restrict__ b0,
     const float* __restrict__ b1, const bf16_t* __restrict__ Wo,
@@ -205,7 +207,7 @@ __global__ __launch_bounds__(512) void mlp_fwd3_kernel(
   };
   // ---- stages 2 + 3 of tile k from h1 buffer `buf`: h2^T = W1 . h1^T, relu' mask, partial logits
   // -> zs buffer `buf`, h2 images for stage 5 -> image buffer `buf` ----
-  auto stage23 = [&](int k, int buf) __attribute__((always_inline)) {
+  auto stage23 = [&](int k, int buf, auto&& fill) __attribute__((always_inline)) {
     const int r0 = tile_of(k) * FRT;
     const bf16_t* hsrc = h1s + buf * FRT * FHP;
     f32x4_t acc[2][2];
@@ -227,6 +229,9 @@ __global__ __launch_bounds__(512) void mlp_fwd3_kernel(
     };
 #pragma unroll
     for (int kc = 0; kc < FPD; ++kc) ld_hb(kc);
+    // the previous tile's softmax (a dependent VALU / DPP chain on partial logits read before stage 5):
+    // its VALU work goes into the MFMA shadow, FFILL instructions after each MFMA
+    fill();
     if constexpr (FPIN) __builtin_amdgcn_sched_group_barrier(0x100, 2 * FPD, 0);  // the FPD chunks ahead
 #pragma unroll
     for (int kc = 0; kc < KC; ++kc) {
@@ -238,7 +243,17 @@ __global__ __launch_bounds__(512) void mlp_fwd3_kernel(
       for (int h = 0; h < 2; ++h)
 #pragma unroll
         for (int t = 0; t < 2; ++t) acc[h][t] = mma32(w1f[t][kc], hb[kc][h], acc[h][t]);
-      if constexpr (FPIN) __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+      if constexpr (FPIN) {
+        if constexpr (FFILL > 0) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x002, FFILL, 0);
+          }
+        } else {
+          __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+        }
+      }
     }
     if constexpr (FPIN) __builtin_amdgcn_sched_barrier(0);
     uint32_t h2p[2][2][2];
@@ -267,12 +282,17 @@ __global__ __launch_bounds__(512) void mlp_fwd3_kernel(
     }
   };
   // ---- softmax / CE / argmax / dz of tile k (zs buffer `buf`): lane = (row sr, class c16) ----
-  auto softmax = [&](int k, int buf, int yc) __attribute__((always_inline)) {
-    const int r0 = tile_of(k) * FRT;
+  // (split: sm_load issues the 8 partial-logit reads, sm_compute the rest)
+  auto sm_load = [&](int buf, float (&zp)[FW]) __attribute__((always_inline)) {
     const float* zb = zs + buf * FW * 2 * ZREG;
+#pragma unroll
+    for (int w = 0; w < FW; ++w) zp[w] = zb[(w * 2 + sh) * ZREG + 72 * (c16 >> 2) + 4 * srr + (c16 & 3)];
+  };
+  auto sm_compute = [&](int k, int buf, int yc, const float (&zp)[FW]) __attribute__((always_inline)) {
+    const int r0 = tile_of(k) * FRT;
     float z = 0.f;
 #pragma unroll
-    for (int w = 0; w < FW; ++w) z += zb[(w * 2 + sh) * ZREG + 72 * (c16 >> 2) + 4 * srr + (c16 & 3)];
+    for (int w = 0; w < FW; ++w) z += zp[w];
     asm volatile("" : "+v"(z));  // computed by every lane: no exec-masked branch splits the loop body
     const float zz = c16 < C ? z + bo_s : -INFINITY;
     // the 16 class lanes of a row are one DPP row: max, argmax (smallest class at the max), sum
@@ -295,6 +315,12 @@ __global__ __launch_bounds__(512) void mlp_fwd3_kernel(
     dbo += bf2f(db);
     dzs[buf * FIMG + sr * FSP + (c16 ^ (8 * ((sr >> 3) & 1)))] = db;
   };
+  auto softmax = [&](int k, int buf, int yc) __attribute__((always_inline)) {
+    float zp[FW];
+    sm_load(buf, zp);
+    sm_compute(k, buf, yc, zp);
+  };
+  auto no_fill = [] {};
   // ---- stage 5 of a tile (dz buffer / image buffer `buf`, rows r0 ..): dWout^T += h2^T . dz over its
   // 32 rows, and the backward's layer-2 gradient dact2 = (dz . Wout) * relu'(h2) of the wave's 32
   // units -> dact2_out (bf16 [B][256], the 16-byte chunks of rows with bit 2 set swapped in pairs —
@@ -358,7 +384,7 @@ __global__ __launch_bounds__(512) void mlp_fwd3_kernel(
       }
     }
     __syncthreads();  // h1 of tile 0
-    stage23(0, 0);
+    stage23(0, 0, no_fill);
     stage1(1);
     load_x(2);
     __syncthreads();  // partial logits of tile 0, h1 of tile 1
@@ -379,12 +405,23 @@ __global__ __launch_bounds__(512) void mlp_fwd3_kernel(
     if (k < 32) HAR_STAMP(FW, 2 + k)
     const int yc = ynext;
     if constexpr (!INFER) ynext = labels[tile_of(k + 1) * FRT + sr];
-    if constexpr (!decltype(late)::value) softmax(k, k & 1, yc);
+    // softmax(k) inside the stage-2 region of tile k+1 (FFILL > 0; not in the stamped build, whose
+    // stamps would split it) or on its own
+    constexpr bool fill = FFILL > 0 && !STAMP && !decltype(late)::value;
+    float zp[FW];
+    if (fill && !last) {
+      sm_load(k & 1, zp);
+    } else if constexpr (!decltype(late)::value) {
+      softmax(k, k & 1, yc);
+    }
     if (k == 4) HAR_STAMP(FW, 10)
     if (!INFER && !first) stage5((k - 1) & 1, tile_of(k - 1) * FRT);
     if (k == 4) HAR_STAMP(FW, 11)
     if (!last) {
-      stage23(k + 1, (k + 1) & 1);
+      if (fill)
+        stage23(k + 1, (k + 1) & 1, [&] { sm_compute(k, k & 1, yc, zp); });
+      else
+        stage23(k + 1, (k + 1) & 1, no_fill);
       if (k == 4) HAR_STAMP(FW, 12)
       // stage 1 reads the X tile whose loads were issued just before the last barrier: hoisted to the
       // top of the body (as the scheduler likes, to fill the MFMA pipe beside the softmax) it waits out
@@ -865,7 +902,15 @@ template <int K0>
 void launch_fwd3(const bf16_t* X, bf16_t* Wf, const float* b0, const float* b1, const bf16_t* Wo,
                  const float* bo, const int32_t* labels, int B, int C, float scale, bf16_t* dact2,
                  float* slab, float* bl, int32_t* bc, int nwg, hipStream_t s) {
-  auto k = g_har_mlp_stamps ? mlp_fwd3_kernel<K0, true> : mlp_fwd3_kernel<K0, false>;
+  static const int fill = [] {
+    const char* e = getenv("HAR_MLP_FWD_FILL");
+    return e ? atoi(e) : 0;
+  }();
+  auto k = g_har_mlp_stamps ? mlp_fwd3_kernel<K0, true>
+           : fill == 1      ? mlp_fwd3_kernel<K0, false, false, 1>
+           : fill == 2      ? mlp_fwd3_kernel<K0, false, false, 2>
+           : fill >= 3      ? mlp_fwd3_kernel<K0, false, false, 3>
+                            : mlp_fwd3_kernel<K0, false>;
   k<<<nwg, 512, FWD_LDS, s>>>(X, Wf, b0, b1, Wo, bo, labels, B, C, scale, dact2, slab, bl, bc, g_har_mlp_stamps,
                               fwd_stagger());
 }
