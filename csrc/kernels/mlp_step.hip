@@ -81,6 +81,9 @@ constexpr int FWD_SLAB = NCLS * HH + NCLS;  // per workgroup: dWout rows 0..15 [
 #ifndef HAR_FWD_PD
 #define HAR_FWD_PD 2
 #endif
+#ifndef HAR_FWD_KROT
+#define HAR_FWD_KROT 0
+#endif
 #ifndef HAR_FWD_PIN
 #define HAR_FWD_PIN 1
 #endif
@@ -148,7 +151,9 @@ __global__ __launch_bounds__(512) void mlp_fwd3_kernel(
   bf16x8_t w0f[2][K0C], w1f[2][KC];
   // k-chunk rotation per workgroup (register kc holds chunk (kc + krot)): the CUs' prologue requests
   // spread over the lines of W1 instead of all asking for the same ones together
-  const int krot = (int)blockIdx.x & (KC - 1);
+  // (off: with a per-workgroup rotation every stage-2 LDS read needs a VALU address add; the rotation
+  // did not measurably shorten the prologue)
+  const int krot = HAR_FWD_KROT ? (int)blockIdx.x & (KC - 1) : 0;
   float4 b0r[2], b1r[2];
 #pragma unroll
   for (int t = 0; t < 2; ++t) {
@@ -225,7 +230,7 @@ __global__ __launch_bounds__(512) void mlp_fwd3_kernel(
 #pragma unroll
       for (int h = 0; h < 2; ++h)
         hb[kc][h] = *reinterpret_cast<const bf16x8_t*>(hsrc + (16 * h + c16) * FHP +
-                                                        ((((kc + krot) & (KC - 1)) * 32 + 8 * g) ^ hsw));
+                                                        ((8 * g) ^ hsw) + ((kc + krot) & (KC - 1)) * 32);
     };
 #pragma unroll
     for (int kc = 0; kc < FPD; ++kc) ld_hb(kc);
@@ -345,11 +350,14 @@ __global__ __launch_bounds__(512) void mlp_fwd3_kernel(
       if (fh_row & 1) hv = u32x4_t{hv[2], hv[3], hv[0], hv[1]};
       const f32x4_t v0 = mma16(woT[0], dzb, f32x4_t{0.f, 0.f, 0.f, 0.f});
       const f32x4_t v1 = mma16(woT[1], dzb, f32x4_t{0.f, 0.f, 0.f, 0.f});
-      // relu'(h2): a relu'd bf16 half is in [0, 0x7fff]; adding 0x7fff carries into its bit 15 exactly
-      // when it is nonzero (no carry crosses the halves) -> 0xffff / 0 half masks
+      // relu'(h2): a relu'd bf16 half is in [0, 0x7fff], so min(half, 1) is the 0 / 1 derivative and
+      // a 16-bit multiply applies it (v_pk_min_u16 + v_pk_mul_lo_u16: 2 VALU per dword, was 5)
       u32x4_t o = {pack2(v0[0], v0[1]), pack2(v0[2], v0[3]), pack2(v1[0], v1[1]), pack2(v1[2], v1[3])};
 #pragma unroll
-      for (int e = 0; e < 4; ++e) o[e] &= (((hv[e] + 0x7fff7fffu) >> 15) & 0x00010001u) * 0xffffu;
+      for (int e = 0; e < 4; ++e) {
+        const u16x2_t d = __builtin_elementwise_min(__builtin_bit_cast(u16x2_t, hv[e]), u16x2_t{1, 1});
+        o[e] = __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2_t, o[e]) * d);
+      }
       *reinterpret_cast<u32x4_t*>(d2base + (size_t)(r0 + 16 * h) * HH) = o;
     }
   };
