@@ -352,11 +352,15 @@ __global__ __launch_bounds__(512) void mlp_fwd3_kernel(
       const f32x4_t v1 = mma16(woT[1], dzb, f32x4_t{0.f, 0.f, 0.f, 0.f});
       // relu'(h2): a relu'd bf16 half is in [0, 0x7fff], so min(half, 1) is the 0 / 1 derivative and
       // a 16-bit multiply applies it (v_pk_min_u16 + v_pk_mul_lo_u16: 2 VALU per dword, was 5)
-      u32x4_t o = {pack2(v0[0], v0[1]), pack2(v0[2], v0[3]), pack2(v1[0], v1[1]), pack2(v1[2], v1[3])};
+      // (scalar temporaries: __builtin_bit_cast of a vector-element lvalue, hv[e] / o[e], reads
+      // element 0 for every e with this clang — checked on the host)
+      const uint32_t ov[4] = {pack2(v0[0], v0[1]), pack2(v0[2], v0[3]), pack2(v1[0], v1[1]), pack2(v1[2], v1[3])};
+      u32x4_t o;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const u16x2_t d = __builtin_elementwise_min(__builtin_bit_cast(u16x2_t, hv[e]), u16x2_t{1, 1});
-        o[e] = __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2_t, o[e]) * d);
+        const uint32_t he = hv[e];
+        const u16x2_t d = __builtin_elementwise_min(__builtin_bit_cast(u16x2_t, he), u16x2_t{1, 1});
+        o[e] = __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2_t, ov[e]) * d);
       }
       *reinterpret_cast<u32x4_t*>(d2base + (size_t)(r0 + 16 * h) * HH) = o;
     }
