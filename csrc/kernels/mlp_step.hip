@@ -68,10 +68,10 @@ constexpr int FRT = 32;                // rows per tile
 // (column ^ 8): the 16-byte reads of stage 2 are conflict-free (the stage-1 8-byte stores 2-way)
 constexpr int FHP = HH + 16;
 // [32 rows][16 cols] images (dz, h2) read by stage 5: unpadded rows (8 dwords) with their four 4-column
-// chunks XOR-permuted by row — h2 images: chunk c of row r at c ^ fh(r), fh(r) = 2 ((r >> 2) & 1) +
-// ((r >> 3) & 1); dz: c ^ fz(r), fz(r) = 2 ((r >> 3) & 1).  The stage-3 8-byte stores (16 rows, one
-// chunk), the 16-byte relu' reads, the dz reads and the transposing fragment reads are all
-// conflict-free (the padded 12-dword pitch had 2-way conflicts on each, profiles/r5)
+// chunks XOR-permuted by row — h2 images: chunk c of row r at c ^ fh(r), fh(r) = 2 ((r >> 2) & 1);
+// dz: c ^ fz(r), fz(r) = 2 ((r >> 3) & 1).  The 16-byte relu' reads, the dz reads and the transposing
+// fragment reads are conflict-free, the stage-3 8-byte stores 2-way (an odd fh making those
+// conflict-free too needs a lane-dependent swap of the relu' words: 8 more VALU per tile)
 constexpr int FSP = 16;
 constexpr int FIMG = FRT * FSP;
 // partial logits of one (wave, half): lane group g's 16 lanes x 4 classes at dword 72 g + 4 c16: the
@@ -125,7 +125,7 @@ __global__ __launch_bounds__(512) void mlp_fwd3_kernel(
   const int sr = 4 * wave + g, sh = sr >> 4, srr = sr & 15;
   const int hsw = 8 * ((c16 >> 2) & 1);  // h1 tile chunk swap of this lane's rows (16h + c16)
   // stage-5 image chunk XORs of this lane's rows 16 h + c16 (FSP)
-  const int fh_row = 2 * ((c16 >> 2) & 1) + ((c16 >> 3) & 1), fz_row = 2 * ((c16 >> 3) & 1);
+  const int fh_row = 2 * ((c16 >> 2) & 1), fz_row = 2 * ((c16 >> 3) & 1);
   f32x4_t acc5[2] = {f32x4_t{0.f, 0.f, 0.f, 0.f}, f32x4_t{0.f, 0.f, 0.f, 0.f}};
   float dbo = 0.f, lsum = 0.f, ncorr = 0.f;
   const int ntiles = B / FRT;
@@ -339,28 +339,30 @@ __global__ __launch_bounds__(512) void mlp_fwd3_kernel(
     const bf16x8_t bz = frag_rows_x(zb, FSP, 0, lane, 2 * (g >> 1));
     const bf16_t* ip = img + buf * 2 * FIMG;
 #pragma unroll
-    for (int t = 0; t < 2; ++t) acc5[t] = mma32(frag_rows_x(ip + t * FIMG, FSP, 0, lane, 2 * (g & 1) + (g >> 1)), bz, acc5[t]);
+    for (int t = 0; t < 2; ++t) acc5[t] = mma32(frag_rows_x(ip + t * FIMG, FSP, 0, lane, 2 * (g & 1)), bz, acc5[t]);
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const s16x4_t dzb = *reinterpret_cast<const s16x4_t*>(zb + (16 * h + c16) * FSP + 4 * (g ^ fz_row));
       // h2 units 8 g .. 8 g + 7 of row 16 h + c16: image block g >> 1, columns 8 (g & 1) .. — chunks
-      // 2 (g & 1), + 1 at the 16-byte pair (g & 1) ^ (fh >> 1), in swapped order when fh is odd
-      u32x4_t hv = *reinterpret_cast<const u32x4_t*>(ip + (g >> 1) * FIMG + (16 * h + c16) * FSP +
-                                                     8 * ((g & 1) ^ (fh_row >> 1)));
-      if (fh_row & 1) hv = u32x4_t{hv[2], hv[3], hv[0], hv[1]};
+      // 2 (g & 1), + 1 at the 16-byte pair (g & 1) ^ (fh >> 1)
+      const u32x4_t hv = *reinterpret_cast<const u32x4_t*>(ip + (g >> 1) * FIMG + (16 * h + c16) * FSP +
+                                                           8 * ((g & 1) ^ (fh_row >> 1)));
       const f32x4_t v0 = mma16(woT[0], dzb, f32x4_t{0.f, 0.f, 0.f, 0.f});
       const f32x4_t v1 = mma16(woT[1], dzb, f32x4_t{0.f, 0.f, 0.f, 0.f});
       // relu'(h2): a relu'd bf16 half is in [0, 0x7fff], so min(half, 1) is the 0 / 1 derivative and
       // a 16-bit multiply applies it (v_pk_min_u16 + v_pk_mul_lo_u16: 2 VALU per dword, was 5)
-      // (scalar temporaries: __builtin_bit_cast of a vector-element lvalue, hv[e] / o[e], reads
+      // (inline asm: written as vector min / multiply, clang turns them into 16-bit compares + selects +
+      // repacking, 7 VALU per dword; and __builtin_bit_cast of a vector-element lvalue, hv[e], read
       // element 0 for every e with this clang — checked on the host)
       const uint32_t ov[4] = {pack2(v0[0], v0[1]), pack2(v0[2], v0[3]), pack2(v1[0], v1[1]), pack2(v1[2], v1[3])};
       u32x4_t o;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const uint32_t he = hv[e];
-        const u16x2_t d = __builtin_elementwise_min(__builtin_bit_cast(u16x2_t, he), u16x2_t{1, 1});
-        o[e] = __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2_t, ov[e]) * d);
+        uint32_t d, r;
+        asm("v_pk_min_u16 %0, %1, %2" : "=v"(d) : "v"(he), "s"(0x00010001u));
+        asm("v_pk_mul_lo_u16 %0, %1, %2" : "=v"(r) : "v"(ov[e]), "v"(d));
+        o[e] = r;
       }
       *reinterpret_cast<u32x4_t*>(d2base + (size_t)(r0 + 16 * h) * HH) = o;
     }
