@@ -555,7 +555,7 @@ template <int A, int LPW, bool MLP, int RCMAX, bool P32 = false>
 __global__ __launch_bounds__(256) void window_features_reg_kernel(const float* __restrict__ stream, int W,
                                                                   int stride, int64_t n_windows, float ms_per_sample,
                                                                   float* __restrict__ out, int ld_out, MlpOut mo,
-                                                                  int C, int wpb) {
+                                                                  int C, int wpb, int ipw) {
   static_assert(LPW == 8 || LPW == 16 || LPW == 32 || LPW == 64, "groups of 8, 16, 32 or 64 lanes");
   constexpr int T3 = A / 3, GPW = 64 / LPW;
   extern __shared__ __attribute__((aligned(16))) float lds[];
@@ -563,20 +563,25 @@ __global__ __launch_bounds__(256) void window_features_reg_kernel(const float* _
   const int64_t w0 = (int64_t)blockIdx.x * wpb;
   const int nwin = (int)min<int64_t>(wpb, n_windows - w0);
   float* const span = lds + PAD;
-  const int ip = P32 ? p32_pitch(W, A) : stride * A;  // image pitch (floats) between consecutive windows
+  // image pitch (floats) between consecutive windows: P32 images, padded images (ipw > 0, non-overlapping
+  // windows: a pitch of 16 mod 32 floats puts the two 16-lane windows of a 32-lane LDS bank group on
+  // disjoint banks — the contiguous 600-float pitch of W = 200 x 3 axes had 32% bank-conflict cycles,
+  // profiles/r5/window_pmc.md), or the shared span (stride A floats per window)
+  const int ip = P32 ? p32_pitch(W, A) : ipw > 0 ? ipw : stride * A;
   auto pos = [&](int t) { return P32 ? p32_pos(t, A) : t * A; };
 
-  if constexpr (P32) {  // ---- stage the windows, one padded image each (float4 granules) ----
+  if (P32 || ipw > 0) {  // ---- stage the windows, one padded image each (float4 granules) ----
     const v4f* s4 = reinterpret_cast<const v4f*>(stream + w0 * (int64_t)W * A);
     const int n4w = W * A / 4, n4 = nwin * n4w;
+    const uint32_t magic = 0xffffffffu / (uint32_t)n4w + 1u;  // f / n4w = umulhi(f, magic) for f * n4w < 2^32
     for (int f0 = tid; f0 < n4; f0 += 8 * nt) {
       v4f r[8];
 #pragma unroll
       for (int u = 0; u < 8; ++u) r[u] = s4[min(f0 + u * nt, n4 - 1)];
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
-        const int f = min(f0 + u * nt, n4 - 1), wl = f / n4w, e = 4 * (f - wl * n4w);
-        *reinterpret_cast<v4f*>(span + wl * ip + e + 4 * (e / (32 * A))) = r[u];
+        const int f = min(f0 + u * nt, n4 - 1), wl = (int)__umulhi((uint32_t)f, magic), e = 4 * (f - wl * n4w);
+        *reinterpret_cast<v4f*>(span + wl * ip + e + (P32 ? 4 * (e / (32 * A)) : 0)) = r[u];
       }
     }
   } else {
@@ -872,8 +877,14 @@ int launch_axes(const float* stream, int64_t n_samples, int window, int stride, 
     if (p32) { lpw = 16; C = 32; }
     if (lpw) {
       const int gpw = 64 / lpw;
+      // non-overlapping 16-lane windows: padded images, pitch = 16 (mod 32) floats (see the kernel)
+      const bool pimg = !p32 && lpw == 16 && A % 2 == 1 && stride == window && (window * A) % 4 == 0 &&
+                        (reinterpret_cast<uintptr_t>(stream) & 15) == 0 && (window * A) % 32 != 16 &&
+                        !std::getenv("HAR_WINDOW_NOPAD");
+      const int ipw = pimg ? window * A + (((16 - window * A) % 32) + 32) % 32 : 0;
       auto span_bytes = [&](int wpb) -> int64_t {
         if (p32) return (PAD + (int64_t)wpb * p32_pitch(window, A) + SLACK) * (int64_t)sizeof(float);
+        if (ipw) return (PAD + (int64_t)wpb * ipw + SLACK) * (int64_t)sizeof(float);
         return (PAD + ((int64_t)(wpb - 1) * stride + window) * A + SLACK) * (int64_t)sizeof(float);
       };
       // waves per block: a multiple of T3, at most 4; the most whose span fits 48 KB (>= 3 blocks per CU)
@@ -889,13 +900,13 @@ int launch_axes(const float* stream, int64_t n_samples, int window, int stride, 
 #define HAR_WIN_R(L)                                                                                          \
   if (C <= 17)                                                                                             \
     window_features_reg_kernel<A, L, MLP, 17><<<grid, nt, bytes, s>>>(stream, window, stride, n_windows, ms, out, \
-                                                                      ld_out, mo, C, wpb);                 \
+                                                                      ld_out, mo, C, wpb, ipw);            \
   else                                                                                                     \
     window_features_reg_kernel<A, L, MLP, RCMAX_LONG><<<grid, nt, bytes, s>>>(stream, window, stride, n_windows, \
-                                                                              ms, out, ld_out, mo, C, wpb)
+                                                                              ms, out, ld_out, mo, C, wpb, ipw)
         if (p32)
           window_features_reg_kernel<A, 16, MLP, 32, true><<<grid, nt, bytes, s>>>(stream, window, stride, n_windows,
-                                                                                   ms, out, ld_out, mo, C, wpb);
+                                                                                   ms, out, ld_out, mo, C, wpb, ipw);
         else if (lpw == 8) { HAR_WIN_R(8); }
         else if (lpw == 16) { HAR_WIN_R(16); }
         else if (lpw == 32) { HAR_WIN_R(32); }
