@@ -139,7 +139,8 @@ __global__ __launch_bounds__(512) void mlp_fwd3_kernel(
 #pragma unroll
     for (int h = 0; h < 2; ++h)
 #pragma unroll
-      for (int kc = 0; kc < K0C; ++kc) xb[h][kc] = ldx<K0>(X, r + 16 * h + c16, kc, g);
+      for (int kc = 0; kc < K0C; ++kc)  // (uniform tile base + 32-bit lane offset: SGPR-base loads)
+        xb[h][kc] = *reinterpret_cast<const bf16x8_t*>((X + (size_t)r * K0) + ((16 * h + c16) * K0 + kc * 32 + g * 8));
   };
 
   // ---- this wave's weight slices, in registers for the whole kernel, from the fragment-ordered
@@ -165,7 +166,7 @@ __global__ __launch_bounds__(512) void mlp_fwd3_kernel(
   int ynext = 0;
   if (nt > 0) {
     load_x(0);
-    if constexpr (!INFER) ynext = labels[tile_of(0) * FRT + sr];
+    if constexpr (!INFER) ynext = (labels + (size_t)tile_of(0) * FRT)[sr];
   }
   __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -180,7 +181,8 @@ __global__ __launch_bounds__(512) void mlp_fwd3_kernel(
   const uint2 wlo = *reinterpret_cast<const uint2*>(Wo + (size_t)c16 * HH + u0 + 4 * g);
   const uint2 whi = *reinterpret_cast<const uint2*>(Wo + (size_t)c16 * HH + u0 + 16 + 4 * g);
   const bf16x8_t wo3 = cat8(wlo.x, wlo.y, whi.x, whi.y);
-  const float bo_s = c16 < C ? bo[c16] : 0.f;
+  // padded class lanes (c16 >= C): bias -inf, so their logit is -inf, exp 0, dz 0 with no per-lane selects
+  const float bo_s = c16 < C ? bo[c16] : -INFINITY;
   // dact2 A fragments (16x16x16, K = the 16 classes): row m of block t is unit 8 (m >> 2) + 4 t + (m & 3)
   // of the wave's 32 (C row 4 g + r -> unit 8 g + 4 t + r: blocks t = 0, 1 give each lane the 8
   // CONSECUTIVE units 8 g .. 8 g + 7 of a row, one 16-byte store); A[m][k = class 4 g + i] =
@@ -299,23 +301,23 @@ __global__ __launch_bounds__(512) void mlp_fwd3_kernel(
 #pragma unroll
     for (int w = 0; w < FW; ++w) z += zp[w];
     asm volatile("" : "+v"(z));  // computed by every lane: no exec-masked branch splits the loop body
-    const float zz = c16 < C ? z + bo_s : -INFINITY;
+    const float zz = z + bo_s;  // (-inf on the padded class lanes: their partial logits are 0)
     // the 16 class lanes of a row are one DPP row: max, argmax (smallest class at the max), sum
     const float mx = row16_max(zz);
-    const int amx = row16_min(zz == mx && c16 < C ? c16 : (1 << 30));
+    const int amx = row16_min(zz == mx ? c16 : (1 << 30));  // (mx is finite: C >= 1 real classes)
     if constexpr (INFER) {
       if (c16 < C) slab[(size_t)(r0 + sr) * C + c16] = zz;
       if (c16 == 0) block_correct[r0 + sr] = amx;
       return;
     }
-    const float e = c16 < C ? __expf(zz - mx) : 0.f;
+    const float e = __expf(zz - mx);  // exactly 0 on the padded class lanes
     const float se = row16_sum(e);
     // v_rcp_f32 (1 ulp) rather than the IEEE division sequence, which hipcc sinks into an
-    // exec-masked branch; dz is rounded to bf16 right after
-    const float dl0 = (e * __builtin_amdgcn_rcpf(se) - (c16 == yc ? 1.f : 0.f)) * scale;
-    const float dl = c16 < C ? dl0 : 0.f;
+    // exec-masked branch; dz is rounded to bf16 right after (0 on the padded class lanes: e = 0, yc < C)
+    const float dl = (e * __builtin_amdgcn_rcpf(se) - (c16 == yc ? 1.f : 0.f)) * scale;
     const bf16_t db = f2bf(dl);
-    lsum += c16 == yc ? (mx + __logf(se)) - zz : 0.f;
+    // ln se as v_log_f32 * ln 2: se >= 1 (the max term is exp 0), so no denormal range scaling
+    lsum += c16 == yc ? (mx + __builtin_amdgcn_logf(se) * 0.693147180559945f) - zz : 0.f;
     ncorr += (c16 == 0 && amx == yc) ? 1.f : 0.f;
     dbo += bf2f(db);
     dzs[buf * FIMG + sr * FSP + (c16 ^ (8 * ((sr >> 3) & 1)))] = db;
@@ -332,7 +334,9 @@ __global__ __launch_bounds__(512) void mlp_fwd3_kernel(
   // the backward's LDS tile image, so its producers copy rows verbatim).  Two 16x16x16 MFMAs per 16
   // rows (K = the 16 classes, unit-permuted A rows: woT) give lane (c16, g) the units 8 g .. 8 g + 7 of
   // row c16: one 16-byte relu' read of the wave's own h2 image, one 16-byte global store ----
-  bf16_t* const d2base = INFER ? nullptr : dact2_out + (size_t)c16 * HH + ((u0 + 8 * g) ^ hsw);
+  // (a wave-uniform row base + a 32-bit lane offset: the stores take the SGPR-base form, no 64-bit
+  // address arithmetic per store)
+  const int d2off = c16 * HH + ((u0 + 8 * g) ^ hsw);
   auto stage5 = [&](int buf, int r0) __attribute__((always_inline)) {
     const bf16_t* zb = dzs + buf * FIMG;
     // (the permuted k order of frag_rows on both operands: k runs over the 32 tile rows)
@@ -364,7 +368,8 @@ __global__ __launch_bounds__(512) void mlp_fwd3_kernel(
         asm("v_pk_mul_lo_u16 %0, %1, %2" : "=v"(r) : "v"(ov[e]), "v"(d));
         o[e] = r;
       }
-      *reinterpret_cast<u32x4_t*>(d2base + (size_t)(r0 + 16 * h) * HH) = o;
+      bf16_t* const rowp = dact2_out + (size_t)(r0 + 16 * h) * HH;
+      *reinterpret_cast<u32x4_t*>(rowp + d2off) = o;
     }
   };
 
@@ -418,7 +423,7 @@ __global__ __launch_bounds__(512) void mlp_fwd3_kernel(
   auto iter = [&](int k, bool first, bool last, auto late) __attribute__((always_inline)) {
     if (k < 32) HAR_STAMP(FW, 2 + k)
     const int yc = ynext;
-    if constexpr (!INFER) ynext = labels[tile_of(k + 1) * FRT + sr];
+    if constexpr (!INFER) ynext = (labels + (size_t)tile_of(k + 1) * FRT)[sr];
     // softmax(k) inside the stage-2 region of tile k+1 (FFILL > 0; not in the stamped build, whose
     // stamps would split it) or on its own
     constexpr bool fill = FFILL > 0 && !STAMP && !decltype(late)::value;

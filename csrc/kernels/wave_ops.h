@@ -37,12 +37,16 @@ __device__ __forceinline__ float vmaxf(float a, float b) {
   asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
   return r;
 }
-// all-reduce over the 16 lanes of each DPP row (lanes 16r .. 16r + 15)
+// all-reduce over the 16 lanes of each DPP row (lanes 16r .. 16r + 15).  The max steps are single
+// v_max_f32_dpp instructions (a DPP move + v_max_f32 is two): inline asm, with the s_nop 1 a DPP read
+// of a VGPR written by the previous VALU instruction needs (the compiler does not see inside the asm)
 __device__ __forceinline__ float row16_max(float v) {
-  v = vmaxf(v, dpp_f<DPP_ROR8>(v));
-  v = vmaxf(v, dpp_f<DPP_ROR4>(v));
-  v = vmaxf(v, dpp_f<DPP_ROR2>(v));
-  return vmaxf(v, dpp_f<DPP_ROR1>(v));
+  asm("s_nop 1\n\tv_max_f32_dpp %0, %0, %0 row_ror:8 row_mask:0xf bank_mask:0xf\n\t"
+      "s_nop 1\n\tv_max_f32_dpp %0, %0, %0 row_ror:4 row_mask:0xf bank_mask:0xf\n\t"
+      "s_nop 1\n\tv_max_f32_dpp %0, %0, %0 row_ror:2 row_mask:0xf bank_mask:0xf\n\t"
+      "s_nop 1\n\tv_max_f32_dpp %0, %0, %0 row_ror:1 row_mask:0xf bank_mask:0xf"
+      : "+v"(v));
+  return v;
 }
 __device__ __forceinline__ float row16_sum(float v) {
   v += dpp_f<DPP_ROR8>(v);
