@@ -111,6 +111,16 @@ __device__ __forceinline__ bf16x8_t frag_rows_x(const bf16_t* img, int pitch, in
   return __builtin_bit_cast(bf16x8_t, v);
 }
 
+// packed bf16 pair `v` times relu'(h) of the packed relu'd bf16 pair `h` (each half in [0, 0x7fff]):
+// min(half, 1) is the 0 / 1 derivative, a 16-bit multiply applies it — 2 VALU per pair.  Inline asm:
+// written as vector min / multiply, clang turns it into 16-bit compares + selects + repacking
+__device__ __forceinline__ uint32_t relu_d_mul(uint32_t v, uint32_t h) {
+  uint32_t d, r;
+  asm("v_pk_min_u16 %0, %1, 1 op_sel_hi:[1,0]" : "=v"(d) : "v"(h));
+  asm("v_pk_mul_lo_u16 %0, %1, %2" : "=v"(r) : "v"(v), "v"(d));
+  return r;
+}
+
 // cross-lane steps on the VALU (DPP / permlane): wave_ops.h (dpp_i / dpp_f, vmaxf, row16_*, LaneSwap)
 using namespace wops;
 

@@ -363,10 +363,7 @@ __global__ __launch_bounds__(512) void mlp_fwd3_kernel(
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const uint32_t he = hv[e];
-        uint32_t d, r;
-        asm("v_pk_min_u16 %0, %1, %2" : "=v"(d) : "v"(he), "s"(0x00010001u));
-        asm("v_pk_mul_lo_u16 %0, %1, %2" : "=v"(r) : "v"(ov[e]), "v"(d));
-        o[e] = r;
+        o[e] = relu_d_mul(ov[e], he);
       }
       bf16_t* const rowp = dact2_out + (size_t)(r0 + 16 * h) * HH;
       *reinterpret_cast<u32x4_t*>(rowp + d2off) = o;
@@ -476,10 +473,13 @@ __global__ __launch_bounds__(512) void mlp_fwd3_kernel(
 #pragma unroll
   for (int t = 0; t < 2; ++t)
     nt_store16(out + (size_t)c16 * HH + u0 + 16 * t + 4 * g, __builtin_bit_cast(u32x4_t, acc5[t]));
-  dbo += __shfl_xor(dbo, 16, 64);
-  dbo += __shfl_xor(dbo, 32, 64);
-  lsum = wave_sum(lsum);
-  ncorr = wave_sum(ncorr);
+  {  // (VALU lane swaps / DPP, not LDS-routed shuffles)
+    const LaneSwap sw(lane);
+    dbo += sw.x16f(dbo);
+    dbo += sw.x32f(dbo);
+    lsum = wave_sum_dpp(lsum, sw);
+    ncorr = wave_sum_dpp(ncorr, sw);
+  }
   float* red = zs;  // free: its last reads (the softmax) precede the barrier above
   if (g == 0) red[wave * NCLS + c16] = dbo;
   if (lane == 0) {
@@ -620,7 +620,8 @@ __global__ __launch_bounds__(512) void mlp_bwd4_kernel(
     static_assert(DV == 8, "8 dact2 pieces per producer thread");
     // dact2 piece i of a tile: row (ptid >> 5) + 8 i, 16-byte chunk ptid & 31 (a wave-instruction reads
     // two whole 512-byte rows); LDS rows BDP apart (the forward wrote the chunk swizzle already)
-    const bf16_t* const d2src = dact2 + (size_t)(ptid >> 5) * HH + (ptid & 31) * 8;
+    // (lane offsets 32-bit, tile bases wave-uniform: the loads take the SGPR-base form)
+    const uint32_t d2src = (uint32_t)((ptid >> 5) * HH + (ptid & 31) * 8);  // (unsigned: zero-extended offsets)
     const int d2dst = (ptid >> 5) * BDP + (ptid & 31) * 8;
     // (macros, not lambdas: a lambda-captured register array is kept in scratch)
     // two register sets of dact2 pieces: the tile staged at iteration i was loaded at iteration i - 2
@@ -630,16 +631,16 @@ __global__ __launch_bounds__(512) void mlp_bwd4_kernel(
 #define HAR_B4_LOAD_D(t, ...) HAR_B4_LOAD_D_I(t, __VA_ARGS__)
 #define HAR_B4_LOAD_D_I(t, r0_, r1_, r2_, r3_, r4_, r5_, r6_, r7_)            \
   {                                                                           \
-    const int64_t tt_ = min(t, tlast);                                        \
-    const bf16_t* dp_ = d2src + tt_ * BRT * HH;                               \
-    r0_ = *reinterpret_cast<const uint4*>(dp_ + 0 * 8 * HH);                  \
-    r1_ = *reinterpret_cast<const uint4*>(dp_ + 1 * 8 * HH);                  \
-    r2_ = *reinterpret_cast<const uint4*>(dp_ + 2 * 8 * HH);                  \
-    r3_ = *reinterpret_cast<const uint4*>(dp_ + 3 * 8 * HH);                  \
-    r4_ = *reinterpret_cast<const uint4*>(dp_ + 4 * 8 * HH);                  \
-    r5_ = *reinterpret_cast<const uint4*>(dp_ + 5 * 8 * HH);                  \
-    r6_ = *reinterpret_cast<const uint4*>(dp_ + 6 * 8 * HH);                  \
-    r7_ = *reinterpret_cast<const uint4*>(dp_ + 7 * 8 * HH);                  \
+    const int tt_ = min(t, tlast);                                            \
+    const bf16_t* dp_ = dact2 + (size_t)tt_ * (BRT * HH);                     \
+    r0_ = *reinterpret_cast<const uint4*>(dp_ + (d2src + 0 * 8 * HH));        \
+    r1_ = *reinterpret_cast<const uint4*>(dp_ + (d2src + 1 * 8 * HH));        \
+    r2_ = *reinterpret_cast<const uint4*>(dp_ + (d2src + 2 * 8 * HH));        \
+    r3_ = *reinterpret_cast<const uint4*>(dp_ + (d2src + 3 * 8 * HH));        \
+    r4_ = *reinterpret_cast<const uint4*>(dp_ + (d2src + 4 * 8 * HH));        \
+    r5_ = *reinterpret_cast<const uint4*>(dp_ + (d2src + 5 * 8 * HH));        \
+    r6_ = *reinterpret_cast<const uint4*>(dp_ + (d2src + 6 * 8 * HH));        \
+    r7_ = *reinterpret_cast<const uint4*>(dp_ + (d2src + 7 * 8 * HH));        \
   }
 #define HAR_B4_STAGE_D(buf, ...) HAR_B4_STAGE_D_I(buf, __VA_ARGS__)
 #define HAR_B4_STAGE_D_I(buf, r0_, r1_, r2_, r3_, r4_, r5_, r6_, r7_)         \
@@ -658,9 +659,10 @@ __global__ __launch_bounds__(512) void mlp_bwd4_kernel(
 #define HAR_DB db0_, db1_, db2_, db3_, db4_, db5_, db6_, db7_
 #define HAR_B4_LOAD_X(t)                                                                      \
   {                                                                                           \
-    const int64_t tt_ = min(t, tlast);                                                        \
-    xr0 = *reinterpret_cast<const uint4*>(X + (tt_ * XV + ptid) * 8);                         \
-    if constexpr (XPT == 2) xr1 = *reinterpret_cast<const uint4*>(X + (tt_ * XV + ptid + 256) * 8); \
+    const int tt_ = min(t, tlast);                                                            \
+    const bf16_t* xp_ = X + (size_t)tt_ * (XV * 8);                                           \
+    xr0 = *reinterpret_cast<const uint4*>(xp_ + (uint32_t)(ptid * 8));                        \
+    if constexpr (XPT == 2) xr1 = *reinterpret_cast<const uint4*>(xp_ + (uint32_t)((ptid + 256) * 8)); \
   }
 #define HAR_B4_STAGE_X(i)                                                                                  \
   {                                                                                                        \
@@ -804,10 +806,12 @@ __global__ __launch_bounds__(512) void mlp_bwd4_kernel(
     // run (pinned by scheduling groups: 2 LDS reads, then 4 MFMAs, per chunk), and the relu'(h1)
     // words are read first; written plainly, each chunk's reads were issued right before their MFMAs
     // and every chunk waited out an LDS round trip
-    auto tile_a = [&](int i) __attribute__((always_inline)) {
-      const bf16_t* dsm = dsm0 + (i & 1) * L::DSM;
-      const bf16_t* hs = hs0 + (i & 1) * L::HS;
-      bf16_t* d1s = d1s0 + (i & 1) * L::HS;
+    // (par = the tile's buffer parity, a compile-time constant in the 2-unrolled loop below: every LDS
+    // address is a lane base + an immediate offset, no per-tile address arithmetic)
+    auto tile_a = [&](int par) __attribute__((always_inline)) {
+      const bf16_t* dsm = dsm0 + par * L::DSM;
+      const bf16_t* hs = hs0 + par * L::HS;
+      bf16_t* d1s = d1s0 + par * L::HS;
       constexpr int PD = 3;  // prefetch distance (k chunks)
       const int swz = 8 * ((c16 >> 2) & 1);
       // (an isolated scheduling region whose first group is the hm reads + the PD chunks ahead: without
@@ -853,17 +857,15 @@ __global__ __launch_bounds__(512) void mlp_bwd4_kernel(
 #pragma unroll
         for (int e = 0; e < 2; ++e) {
           const f32x4_t& a = acc[rr][e];
-          const uint2 m = hm[rr][e];
-          const float d0 = (m.x & 0xffffu) ? a[0] : 0.f, d1 = (m.x >> 16) ? a[1] : 0.f;
-          const float d2 = (m.y & 0xffffu) ? a[2] : 0.f, d3 = (m.y >> 16) ? a[3] : 0.f;
+          const uint2 m = hm[rr][e];  // relu'd h1 (bf16 pairs): dact1 = dact1_pre * relu'(h1)
           *reinterpret_cast<uint2*>(d1s + (16 * (ra0 + rr) + c16) * BUP + 16 * (ua0 + e) + 4 * (g ^ (c16 >> 2))) =
-              make_uint2(pack2(d0, d1), pack2(d2, d3));
+              make_uint2(relu_d_mul(pack2(a[0], a[1]), m.x), relu_d_mul(pack2(a[2], a[3]), m.y));
         }
     };
     // (b) dW1[j][u] += dact2^T . h1 for j blocks 4 pw .. + 3 x all unit blocks; db1 of j block 4q + pw
-    auto tile_b = [&](int i) __attribute__((always_inline)) {
-      const bf16_t* dsm = dsm0 + (i & 1) * L::DSM;
-      const bf16_t* hs = hs0 + (i & 1) * L::HS;
+    auto tile_b = [&](int par) __attribute__((always_inline)) {
+      const bf16_t* dsm = dsm0 + par * L::DSM;
+      const bf16_t* hs = hs0 + par * L::HS;
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
         bf16x8_t hb[4];
@@ -881,14 +883,21 @@ __global__ __launch_bounds__(512) void mlp_bwd4_kernel(
     __builtin_amdgcn_s_setprio(1);  // the consumers' MFMA stream is the critical path of a tile
     __syncthreads();  // (paired with the producers' barrier: dact2 0, X 0 / 1 staged)
     __syncthreads();  // (paired: h1 tile 0 complete)
-    for (int i = 0; i < n; ++i) {
+    auto citer = [&](int i, auto parc) __attribute__((always_inline)) {
+      constexpr int par = decltype(parc)::value;
       if (i < 24) HAR_STAMP(8, 2 + i)
-      tile_a(i);
+      tile_a(par);
       if (i == 4) HAR_STAMP(8, 29)
-      tile_b(i);
+      tile_b(par);
       if (i == 4) HAR_STAMP(8, 30)
       __syncthreads();  // dact1 i complete; the buffers of tile i may be overwritten
+    };
+    int i = 0;
+    for (; i + 1 < n; i += 2) {
+      citer(i, std::integral_constant<int, 0>{});
+      citer(i + 1, std::integral_constant<int, 1>{});
     }
+    if (i < n) citer(i, std::integral_constant<int, 0>{});
     HAR_STAMP(8, 34)
     __builtin_amdgcn_s_setprio(0);
     // ---- this wave's parts of slab `slice` (flat parameter layout) ----
