@@ -27,6 +27,20 @@ def _import():
             return _MOD
         try:
             import sys
+            alt = os.environ.get("HAR_NATIVE_SO")
+            if alt:
+                # A/B tooling only (tools/gpu_ab.sh): load another build of the extension, e.g. the
+                # previous commit's, so two builds are compared on the same GPU box; no source check
+                from importlib.machinery import ExtensionFileLoader
+                from importlib.util import module_from_spec, spec_from_file_location
+
+                loader = ExtensionFileLoader("har._har_native", alt)
+                spec = spec_from_file_location("har._har_native", alt, loader=loader)
+                mod = module_from_spec(spec)
+                loader.exec_module(mod)
+                sys.modules["har._har_native"] = mod
+                _MOD = mod
+                return _MOD
             root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
             tools = os.path.join(root, "tools")
             bn = None
