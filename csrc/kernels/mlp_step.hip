@@ -423,15 +423,17 @@ __global__ __launch_bounds__(512) void mlp_fwd3_kernel(
     if constexpr (!INFER) ynext = (labels + (size_t)tile_of(k + 1) * FRT)[sr];
     // softmax(k) inside the stage-2 region of tile k+1 (FFILL > 0; not in the stamped build, whose
     // stamps would split it) or on its own
-    constexpr bool fill = FFILL > 0 && !STAMP && !decltype(late)::value;
+    constexpr int SMP = decltype(late)::value;  // where the softmax runs: 0 first, 1 after stage 5, 2 last
+    constexpr bool fill = FFILL > 0 && !STAMP && SMP == 0;
     float zp[FW];
     if (fill && !last) {
       sm_load(k & 1, zp);
-    } else if constexpr (!decltype(late)::value) {
+    } else if constexpr (SMP == 0) {
       softmax(k, k & 1, yc);
     }
     if (k == 4) HAR_STAMP(FW, 10)
     if (!INFER && !first) stage5((k - 1) & 1, tile_of(k - 1) * FRT);
+    if constexpr (SMP == 1) softmax(k, k & 1, yc);
     if (k == 4) HAR_STAMP(FW, 11)
     if (!last) {
       if (fill)
@@ -447,7 +449,7 @@ __global__ __launch_bounds__(512) void mlp_fwd3_kernel(
       load_x(k + 3);
       if (k == 4) HAR_STAMP(FW, 13)
     }
-    if constexpr (decltype(late)::value) softmax(k, k & 1, yc);
+    if constexpr (SMP == 2) softmax(k, k & 1, yc);
     __syncthreads();
   };
   // (nt == 1 apart, so that every path into the loop issues its loads in the loop body's order: a
@@ -461,10 +463,17 @@ __global__ __launch_bounds__(512) void mlp_fwd3_kernel(
       iter(nt - 1, false, true, late);
     }
   };
-  if (stagger && __builtin_amdgcn_readfirstlane(wave) >= FW / 2)
-    run(std::true_type{});
-  else
-    run(std::false_type{});
+  // stagger 1: waves 4..7 run their softmax last; 2: right after stage 5 (while waves 0..3, which ran
+  // theirs first, are in stage 5: the DPP / transcendental chain of one SIMD partner beside the LDS
+  // reads and MFMAs of the other, in both halves)
+  if (stagger && __builtin_amdgcn_readfirstlane(wave) >= FW / 2) {
+    if (stagger == 2)
+      run(std::integral_constant<int, 1>{});
+    else
+      run(std::integral_constant<int, 2>{});
+  } else {
+    run(std::integral_constant<int, 0>{});
+  }
   HAR_STAMP(FW, 34)
   if constexpr (INFER) return;
   if (nt > 0) stage5((nt - 1) & 1, tile_of(nt - 1) * FRT);
