@@ -297,9 +297,9 @@ __global__ __launch_bounds__(512) void mlp_fwd3_kernel(
   };
   auto sm_compute = [&](int k, int buf, int yc, const float (&zp)[FW]) __attribute__((always_inline)) {
     const int r0 = tile_of(k) * FRT;
-    // pairwise (3 dependent adds on the softmax chain, not 8)
-    static_assert(FW == 8, "eight partial logits");
-    float z = ((zp[0] + zp[1]) + (zp[2] + zp[3])) + ((zp[4] + zp[5]) + (zp[6] + zp[7]));
+    float z = 0.f;
+#pragma unroll
+    for (int w = 0; w < FW; ++w) z += zp[w];
     asm volatile("" : "+v"(z));  // computed by every lane: no exec-masked branch splits the loop body
     const float zz = z + bo_s;  // (-inf on the padded class lanes: their partial logits are 0)
     // the 16 class lanes of a row are one DPP row: max, argmax (smallest class at the max), sum
