@@ -21,8 +21,9 @@ xGMI, weak scaling (fixed per-GPU work).  Every line is ONE JSON record.
 ``--config rf9``    (config 5) 12-class 9-axis IMU RandomForest, 500 trees.
 ``--config dt``     DecisionTree (every feature at every node) on config 2's windows; sibling
                    histogram subtraction on (``--no-subtract``: every node histogrammed directly).
-``--config infer``  serving: windows/s classified by the trained config-3 MLP (fused
-                    forward + head kernel, logits + argmax); no reference number exists.
+``--config infer``  serving: windows/s classified by the trained config-3 MLP (an fp32 -> bf16 cast
+                    kernel + the INFER instantiation of the training forward, logits + argmax); no
+                    reference number exists.
 
 ``--config reference`` the reference's own four fits on the REAL WISDM table (3100-dim
                     StringIndexer/OneHot encoding, 70/30 split, seed 2018): LogisticRegression
