@@ -551,11 +551,14 @@ __device__ __forceinline__ uint32_t bin_of(float x, float sc, float lo) {
 __host__ __device__ constexpr int p32_pos(int t, int A) { return t * A + 4 * (t >> 5); }
 __host__ __device__ inline int p32_pitch(int W, int A) { return (p32_pos(W, A) + 4 + 3) & ~3; }
 
-template <int A, int LPW, bool MLP, int RCMAX, bool P32 = false, int WPE = 1>
+// FIXC: the run length is RCMAX itself (a compile-time constant): no per-k-step `k < C` guards, whose
+// compare + branch cost ~6 instructions per step and sample pass, and only the registers the runs use
+template <int A, int LPW, bool MLP, int RCMAX, bool P32 = false, int WPE = 1, bool FIXC = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void window_features_reg_kernel(const float* __restrict__ stream, int W,
                                                                   int stride, int64_t n_windows, float ms_per_sample,
                                                                   float* __restrict__ out, int ld_out, MlpOut mo,
-                                                                  int C, int wpb, int ipw) {
+                                                                  int Carg, int wpb, int ipw) {
+  const int C = FIXC ? RCMAX : Carg;
   static_assert(LPW == 8 || LPW == 16 || LPW == 32 || LPW == 64, "groups of 8, 16, 32 or 64 lanes");
   constexpr int T3 = A / 3, GPW = 64 / LPW;
   extern __shared__ __attribute__((aligned(16))) float lds[];
@@ -907,10 +910,13 @@ int launch_axes(const float* stream, int64_t n_samples, int window, int stride, 
         if (p32)
           window_features_reg_kernel<A, 16, MLP, 32, true><<<grid, nt, bytes, s>>>(stream, window, stride, n_windows,
                                                                                    ms, out, ld_out, mo, C, wpb, ipw);
-        else if (lpw == 8 && C > 17 && C <= 25)  // (the stride-100 200-sample shape: 8 x 25; a 25-register
-                                                 // instantiation held to 128 VGPRs: 4 waves per SIMD, not 3)
+        else if (lpw == 8 && C > 17 && C <= 25)  // (the stride-100 200-sample shape: 8 x 25, held to 128 VGPRs:
+                                                 // 4 waves per SIMD, not 3; fixed-length runs spilled 65 VGPRs there)
           window_features_reg_kernel<A, 8, MLP, 25, false, 4><<<grid, nt, bytes, s>>>(stream, window, stride, n_windows,
                                                                                      ms, out, ld_out, mo, C, wpb, ipw);
+        else if (lpw == 16 && C == 13)  // (the 200-sample non-overlapping shape: 16 x 13, fixed-length runs)
+          window_features_reg_kernel<A, 16, MLP, 13, false, 1, true><<<grid, nt, bytes, s>>>(
+              stream, window, stride, n_windows, ms, out, ld_out, mo, C, wpb, ipw);
         else if (lpw == 8) { HAR_WIN_R(8); }
         else if (lpw == 16) { HAR_WIN_R(16); }
         else if (lpw == 32) { HAR_WIN_R(32); }
