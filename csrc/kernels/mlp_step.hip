@@ -605,25 +605,6 @@ __global__ __launch_bounds__(512) void mlp_bwd4_kernel(
 
   if (prod) {
     // ================================ producer ================================
-    bf16x8_t w0q[NFW];
-#pragma unroll
-    for (int kc = 0; kc < NFW; ++kc)
-      w0q[kc] = *reinterpret_cast<const bf16x8_t*>(W0f + (size_t)((4 * q + pw) * NFW + kc) * 512 + frag_lane_off(lane));
-    const float4 b0q = *reinterpret_cast<const float4*>(b0 + qu0 + 16 * pw + 4 * g);
-    constexpr int WO4 = NCLS * HH / 4, NC4 = WO4 + NCLS / 4;
-    f32x4_t px[4];
-    auto wo_load = [&](int c4) __attribute__((always_inline)) {
-      const float* src = fslab + (c4 < WO4 ? 4 * c4 : NCLS * HH + 4 * (c4 - WO4));
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-        px[r] = lane + 64 * r < nfwd ? *reinterpret_cast<const f32x4_t*>(src + (size_t)(lane + 64 * r) * fslab_w)
-                                     : f32x4_t{0.f, 0.f, 0.f, 0.f};
-    };
-    if (fslab && 4 * b + pw < NC4) wo_load(4 * b + pw);
-    if constexpr (STAMP) __builtin_amdgcn_s_waitcnt(0x0f70);
-    HAR_STAMP(8, 1)
-    __syncthreads();  // the prologue images are read: the tile buffers may be written
-
     const int ptid = tid;  // 0..255
     static_assert(XPT == 1 || XPT == 2, "one or two X vectors per producer thread");
     static_assert(DV == 8, "8 dact2 pieces per producer thread");
@@ -636,7 +617,7 @@ __global__ __launch_bounds__(512) void mlp_bwd4_kernel(
     // two register sets of dact2 pieces: the tile staged at iteration i was loaded at iteration i - 2
     // (one iteration ahead left ~700 cycles of the refill still in flight at its use, profiles/r5)
     uint4 da0, da1, da2, da3, da4, da5, da6, da7, db0_, db1_, db2_, db3_, db4_, db5_, db6_, db7_;
-    uint4 xr0, xr1;
+    uint4 xr0, xr1, xq0, xq1;  // xq: X tile t0 + 1, loaded with tile t0
 #define HAR_B4_LOAD_D(t, ...) HAR_B4_LOAD_D_I(t, __VA_ARGS__)
 #define HAR_B4_LOAD_D_I(t, r0_, r1_, r2_, r3_, r4_, r5_, r6_, r7_)            \
   {                                                                           \
@@ -666,20 +647,45 @@ __global__ __launch_bounds__(512) void mlp_bwd4_kernel(
   }
 #define HAR_DA da0, da1, da2, da3, da4, da5, da6, da7
 #define HAR_DB db0_, db1_, db2_, db3_, db4_, db5_, db6_, db7_
-#define HAR_B4_LOAD_X(t)                                                                      \
+#define HAR_B4_LOAD_XR(t, xa_, xb2_)                                                          \
   {                                                                                           \
     const int tt_ = min(t, tlast);                                                            \
     const bf16_t* xp_ = X + (size_t)tt_ * (XV * 8);                                           \
-    xr0 = *reinterpret_cast<const uint4*>(xp_ + (uint32_t)(ptid * 8));                        \
-    if constexpr (XPT == 2) xr1 = *reinterpret_cast<const uint4*>(xp_ + (uint32_t)((ptid + 256) * 8)); \
+    xa_ = *reinterpret_cast<const uint4*>(xp_ + (uint32_t)(ptid * 8));                        \
+    if constexpr (XPT == 2) xb2_ = *reinterpret_cast<const uint4*>(xp_ + (uint32_t)((ptid + 256) * 8)); \
   }
-#define HAR_B4_STAGE_X(i)                                                                                  \
+#define HAR_B4_STAGE_XR(i, xa_, xb2_)                                                                      \
   {                                                                                                        \
     bf16_t* xb_ = xs0 + ((i) & (NXB - 1)) * L::XS;                                                         \
-    *reinterpret_cast<uint4*>(xb_ + (ptid / (K0 / 8)) * XP + (ptid % (K0 / 8)) * 8) = xr0;                 \
+    *reinterpret_cast<uint4*>(xb_ + (ptid / (K0 / 8)) * XP + (ptid % (K0 / 8)) * 8) = xa_;                 \
     if constexpr (XPT == 2)                                                                                \
-      *reinterpret_cast<uint4*>(xb_ + ((ptid + 256) / (K0 / 8)) * XP + ((ptid + 256) % (K0 / 8)) * 8) = xr1; \
+      *reinterpret_cast<uint4*>(xb_ + ((ptid + 256) / (K0 / 8)) * XP + ((ptid + 256) % (K0 / 8)) * 8) = xb2_; \
   }
+#define HAR_B4_LOAD_X(t) HAR_B4_LOAD_XR(t, xr0, xr1)
+#define HAR_B4_STAGE_X(i) HAR_B4_STAGE_XR(i, xr0, xr1)
+    // the first tiles' loads go out before anything else of the prologue (W0 fragments, the dWout
+    // slabs): dact2 tile 0 and X tiles 0 / 1 land in one round trip, staged after the barrier below
+    HAR_B4_LOAD_D(t0, HAR_DA)
+    HAR_B4_LOAD_X(t0)
+    HAR_B4_LOAD_XR(t0 + 1, xq0, xq1)
+    bf16x8_t w0q[NFW];
+#pragma unroll
+    for (int kc = 0; kc < NFW; ++kc)
+      w0q[kc] = *reinterpret_cast<const bf16x8_t*>(W0f + (size_t)((4 * q + pw) * NFW + kc) * 512 + frag_lane_off(lane));
+    const float4 b0q = *reinterpret_cast<const float4*>(b0 + qu0 + 16 * pw + 4 * g);
+    constexpr int WO4 = NCLS * HH / 4, NC4 = WO4 + NCLS / 4;
+    f32x4_t px[4];
+    auto wo_load = [&](int c4) __attribute__((always_inline)) {
+      const float* src = fslab + (c4 < WO4 ? 4 * c4 : NCLS * HH + 4 * (c4 - WO4));
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        px[r] = lane + 64 * r < nfwd ? *reinterpret_cast<const f32x4_t*>(src + (size_t)(lane + 64 * r) * fslab_w)
+                                     : f32x4_t{0.f, 0.f, 0.f, 0.f};
+    };
+    if (fslab && 4 * b + pw < NC4) wo_load(4 * b + pw);
+    if constexpr (STAMP) __builtin_amdgcn_s_waitcnt(0x0f70);
+    HAR_STAMP(8, 1)
+
     // h1 unit block pw x 4 row blocks of tile i (X buffer i & 3) -> h1 buffer i & 1 (the forward's
     // operands, accumulation order and rounding: bit-identical h1)
     auto tile_h1 = [&](int i) __attribute__((always_inline)) {
@@ -724,12 +730,10 @@ __global__ __launch_bounds__(512) void mlp_bwd4_kernel(
     };
     // invariant at the top of iteration i: the dact2 set of i's parity (A even, B odd) holds tile i+1,
     // the other set tile i+2; xr = X tile i+2 (loaded)
-    HAR_B4_LOAD_D(t0, HAR_DA)
-    HAR_B4_LOAD_X(t0)
+    __syncthreads();  // the prologue images are read: the tile buffers may be written
     HAR_B4_STAGE_D(0, HAR_DA)
     HAR_B4_STAGE_X(0)
-    HAR_B4_LOAD_X(t0 + 1)
-    HAR_B4_STAGE_X(1)
+    HAR_B4_STAGE_XR(1, xq0, xq1)
     HAR_B4_LOAD_D(t0 + 1, HAR_DA)
     HAR_B4_LOAD_D(t0 + 2, HAR_DB)
     HAR_B4_LOAD_X(t0 + 2)
@@ -768,6 +772,17 @@ __global__ __launch_bounds__(512) void mlp_bwd4_kernel(
       HAR_B4_ITER(i + 1, HAR_DB)
     }
     if (i < n) HAR_B4_ITER(i, HAR_DA)
+#undef HAR_B4_ITER
+#undef HAR_B4_STAGE_D
+#undef HAR_B4_STAGE_D_I
+#undef HAR_DA
+#undef HAR_DB
+#undef HAR_B4_LOAD_D
+#undef HAR_B4_LOAD_D_I
+#undef HAR_B4_LOAD_X
+#undef HAR_B4_STAGE_X
+#undef HAR_B4_LOAD_XR
+#undef HAR_B4_STAGE_XR
     HAR_STAMP(8, 34)
     if (n > 0) tile_c(n - 1);
     float* w0o = gw0 + (size_t)slice * slab_stride;
