@@ -248,27 +248,17 @@ __device__ __forceinline__ void logreg_eval_body(const LogregEvalArgs& a, int bx
     } else {
       for (int o = tid; o < nc * KP; o += EVAL_ROWS) {
         const int j = o / KP, k = o % KP;
-        // four interleaved row chains (rows i = 4 m + r), combined in a fixed order: a quarter of the
-        // dependent FMA latency of one 256-long chain (deterministic, not the single chain's bits)
-        float acc[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll 4
-        for (int i = 0; i < EVAL_ROWS; i += 4) {
-#pragma unroll
-          for (int r = 0; r < 4; ++r) acc[r] = fmaf(rs[(i + r) * KP + k], xs[(i + r) * xld + j], acc[r]);
-        }
-        slab[(int64_t)c0 * KP + o] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+        float acc = 0.f;
+        for (int i = 0; i < EVAL_ROWS; ++i) acc = fmaf(rs[i * KP + k], xs[i * xld + j], acc);
+        slab[(int64_t)c0 * KP + o] = acc;
       }
     }
   }
   // intercept gradient sum R of the tile
   for (int k = tid; k < KP; k += EVAL_ROWS) {
-    float acc[4] = {0.f, 0.f, 0.f, 0.f};  // (four interleaved chains, as above)
-#pragma unroll 4
-    for (int i = 0; i < EVAL_ROWS; i += 4) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) acc[r] += rs[(i + r) * KP + k];
-    }
-    slab[Fd * KP + k] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+    float acc = 0.f;
+    for (int i = 0; i < EVAL_ROWS; ++i) acc += rs[i * KP + k];
+    slab[Fd * KP + k] = acc;
   }
   if (tid == 0) slab[SW - 1] = (red[0] + red[1]) + (red[2] + red[3]);
 }
