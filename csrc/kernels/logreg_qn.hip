@@ -69,9 +69,26 @@ __device__ __forceinline__ void eval_stage_chunk(const LogregEvalArgs& a, const 
   if (weights)
     for (int e = tid; e < ncs * KP; e += EVAL_ROWS)
       wd[e] = e / KP < nc ? W[(int64_t)a.dense_cols[c0 + e / KP] * KP + (e % KP)] : 0.f;
-  for (int e = tid; e < EVAL_ROWS * ncs; e += EVAL_ROWS) {
-    const int rr = e / ncs, j = e % ncs;
-    xs[rr * XLD + j] = (rr < nrow_tile && j < nc) ? a.dense[(r0 + rr) * a.ldd + c0 + j] : 0.f;
+  // U loads in flight per thread (clamped to a valid element, zeroed by a select), then the U stores:
+  // the plain loop waited out one global round trip per element (10 per tile at 10 dense columns,
+  // most of the evaluation's latency)
+  constexpr int U = 8;
+  const int tot = EVAL_ROWS * ncs;
+  for (int e0 = tid; e0 < tot; e0 += U * EVAL_ROWS) {
+    float v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int e = e0 + u * EVAL_ROWS;
+      const int rr = e / ncs, j = e % ncs;
+      const bool in = e < tot && rr < nrow_tile && j < nc;
+      const float x = a.dense[(r0 + (in ? rr : 0)) * a.ldd + c0 + (in ? j : 0)];
+      v[u] = in ? x : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int e = e0 + u * EVAL_ROWS;
+      if (e < tot) xs[(e / ncs) * XLD + (e % ncs)] = v[u];
+    }
   }
 }
 
