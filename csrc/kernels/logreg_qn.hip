@@ -34,7 +34,18 @@
 #include "common.h"
 #include "../har_kernels.h"
 
+// Diagnostic phase stamps (tools/lr_stamps.py): a STAMP instantiation of the evaluation / direction /
+// update kernels, launched only while har_lr_set_stamps() holds a buffer, has thread 0 of every
+// workgroup store s_memtime at fixed points into its 16-slot row (workgroup = y * gridDim.x + x).
+uint64_t* g_lr_stamps = nullptr;       // evaluation kernel rows
+uint64_t* g_lr_stamps_dir = nullptr;   // direction kernel rows
+uint64_t* g_lr_stamps_upd = nullptr;   // update kernel rows
 namespace {
+#define HAR_LR_STAMP(k)                                                                                  \
+  if constexpr (STAMP) {                                                                                 \
+    if (threadIdx.x == 0)                                                                                \
+      st[((size_t)blockIdx.y * gridDim.x + blockIdx.x) * 16 + (k)] = __builtin_amdgcn_s_memtime();      \
+  }
 
 constexpr int EVAL_ROWS = 256;
 
@@ -98,8 +109,10 @@ __device__ __forceinline__ f32x4_t mfma4(float a, float b, f32x4_t c) {
 
 // The kernel bodies below take their workgroup coordinates as arguments: the stand-alone kernels pass
 // blockIdx / gridDim, the persistent solve (logreg_solve_persistent_kernel) its virtual blocks.
-template <int KP, int XLD>
-__device__ __forceinline__ void logreg_eval_body(const LogregEvalArgs& a, int bx, int by, int gdx, float* smem) {
+template <int KP, int XLD, bool STAMP = false>
+__device__ __forceinline__ void logreg_eval_body(const LogregEvalArgs& a, int bx, int by, int gdx, float* smem,
+                                                 uint64_t* st = nullptr) {
+  HAR_LR_STAMP(0)
   const int Fd = a.Fd;
   float* wd = smem;                                // [EVAL_DCH][KP] dense weights of the chunk
   constexpr int xld = XLD;
@@ -148,6 +161,7 @@ __device__ __forceinline__ void logreg_eval_body(const LogregEvalArgs& a, int bx
       }
     }
   }
+  HAR_LR_STAMP(1)
   if constexpr (MF) {  // the margins through LDS to their rows' threads
 #pragma unroll
     for (int rb = 0; rb < 4; ++rb)
@@ -195,6 +209,7 @@ __device__ __forceinline__ void logreg_eval_body(const LogregEvalArgs& a, int bx
       }
     }
   }
+  HAR_LR_STAMP(2)
   float rv[KP];
   if (a.mode == 1) {  // prediction: raw margins out
 #pragma unroll
@@ -230,12 +245,14 @@ __device__ __forceinline__ void logreg_eval_body(const LogregEvalArgs& a, int bx
     for (int q = 0; q < KP / 4; ++q) rp[q] = f32x4_t{rv[4 * q], rv[4 * q + 1], rv[4 * q + 2], rv[4 * q + 3]};
   }
   if (a.mode == 1) return;
+  HAR_LR_STAMP(3)
   // tile loss: wave sums, then the 4 wave partials in a fixed order
   lossv = wave_sum(lossv);
   if ((tid & 63) == 0) red[tid >> 6] = lossv;
   __syncthreads();                                 // rs / red complete; the last chunk is in xs
   const int SW = Fd * KP + KP + 1;
   float* slab = a.slab + ((int64_t)bt * gdx + bx) * SW;
+  HAR_LR_STAMP(4)
   // ---- pass B: dense gradient R^T X of the tile, chunks newest-first (fixed row order) ----
   for (int ch = nchunk - 1; ch >= 0; --ch) {
     const int c0 = ch * EVAL_DCH, nc = min(EVAL_DCH, Fd - c0);
@@ -271,6 +288,7 @@ __device__ __forceinline__ void logreg_eval_body(const LogregEvalArgs& a, int bx
       }
     }
   }
+  HAR_LR_STAMP(5)
   // intercept gradient sum R of the tile
   for (int k = tid; k < KP; k += EVAL_ROWS) {
     float acc = 0.f;
@@ -278,12 +296,13 @@ __device__ __forceinline__ void logreg_eval_body(const LogregEvalArgs& a, int bx
     slab[Fd * KP + k] = acc;
   }
   if (tid == 0) slab[SW - 1] = (red[0] + red[1]) + (red[2] + red[3]);
+  HAR_LR_STAMP(6)
 }
 
-template <int KP, int XLD>
-__global__ __launch_bounds__(EVAL_ROWS) void logreg_eval_kernel(LogregEvalArgs a) {
+template <int KP, int XLD, bool STAMP = false>
+__global__ __launch_bounds__(EVAL_ROWS) void logreg_eval_kernel(LogregEvalArgs a, uint64_t* st) {
   extern __shared__ float smem[];
-  logreg_eval_body<KP, XLD>(a, blockIdx.x, blockIdx.y, gridDim.x, smem);
+  logreg_eval_body<KP, XLD, STAMP>(a, blockIdx.x, blockIdx.y, gridDim.x, smem, st);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -669,8 +688,9 @@ __device__ __forceinline__ DirElem dir_load(const QnArgs& a, int b, int e) {
 }
 
 // phase 1
-template <int KP, bool FULLM>
-__device__ __forceinline__ void qn_direction_body(const QnArgs& a, int c, int b) {
+template <int KP, bool FULLM, bool STAMP = false>
+__device__ __forceinline__ void qn_direction_body(const QnArgs& a, int c, int b, uint64_t* st = nullptr) {
+  HAR_LR_STAMP(0)
   __shared__ double sh[4 * NP2];
   __shared__ float cS[QN_MAX_M], cY[QN_MAX_M];
   __shared__ float gam;
@@ -706,6 +726,7 @@ __device__ __forceinline__ void qn_direction_body(const QnArgs& a, int c, int b)
     if (i < QN_MAX_M) rho_s[i] = rhv;
     __syncthreads();
   }
+  HAR_LR_STAMP(1)
   if (threadIdx.x == 0) {
     float gamma = 0.f;
     for (int j = 0; j < QN_MAX_M; ++j) cS[j] = cY[j] = 0.f;
@@ -768,6 +789,7 @@ __device__ __forceinline__ void qn_direction_body(const QnArgs& a, int c, int b)
     gam = gamma;
   }
   __syncthreads();
+  HAR_LR_STAMP(2)
   const bool l1on = a.l1 != nullptr;
   const bool active = a.active[b] != 0;
   const int T = a.init ? 1 : a.T;
@@ -822,23 +844,27 @@ __device__ __forceinline__ void qn_direction_body(const QnArgs& a, int c, int b)
     }
     cur = nxt;
   }
+  HAR_LR_STAMP(3)
   __shared__ double tot2[NP2];
   block_sum_f<NP2>(r, sh, tot2);
+  HAR_LR_STAMP(4)
   if (threadIdx.x == 0) {
     double* P2 = a.P2 + ((int64_t)b * a.nch + c) * NP2;
 #pragma unroll
     for (int q = 0; q < NP2; ++q) P2[q] = tot2[q];
   }
+  HAR_LR_STAMP(5)
 }
 
-template <int KP, bool FULLM>
-__global__ __launch_bounds__(QN_BLOCK) void qn_direction_kernel(QnArgs a) {
-  qn_direction_body<KP, FULLM>(a, blockIdx.x, blockIdx.y);
+template <int KP, bool FULLM, bool STAMP = false>
+__global__ __launch_bounds__(QN_BLOCK) void qn_direction_kernel(QnArgs a, uint64_t* st) {
+  qn_direction_body<KP, FULLM, STAMP>(a, blockIdx.x, blockIdx.y, st);
 }
 
 // phase 2
-template <bool FULLM, bool WIDE>
-__device__ __forceinline__ void qn_update_body(const QnArgs& a, int c, int b) {
+template <bool FULLM, bool WIDE, bool STAMP = false>
+__device__ __forceinline__ void qn_update_body(const QnArgs& a, int c, int b, uint64_t* st = nullptr) {
+  HAR_LR_STAMP(0)
   __shared__ double sh[4 * NP3];
   __shared__ double p2v[NP2];
   __shared__ double fin_v[NP3];
@@ -850,6 +876,7 @@ __device__ __forceinline__ void qn_update_body(const QnArgs& a, int c, int b) {
   const QnScalars qs = qn_load_scalars(a, b);  // uniform (scalar) loads, in flight with the P2 partials
   reduce_chunks_shared<NP2>(a.P2 + (int64_t)b * a.nch * NP2, a.nch, p2v, stage);
   __syncthreads();
+  HAR_LR_STAMP(1)
   if (threadIdx.x == 0) {
     const bool steep = qs.steep != 0;
     const double dd = steep ? -p2v[3 * QN_MAX_TRIALS + 1] : p2v[3 * QN_MAX_TRIALS];
@@ -882,6 +909,7 @@ __device__ __forceinline__ void qn_update_body(const QnArgs& a, int c, int b) {
     pick = p;
   }
   __syncthreads();
+  HAR_LR_STAMP(2)
   const int p = pick;
   if (p >= 0) {  // block-uniform
     const int64_t sstride = (int64_t)a.B * D;
@@ -942,6 +970,7 @@ __device__ __forceinline__ void qn_update_body(const QnArgs& a, int c, int b) {
       x[e] = xn;
       g[e] = gn;
     }
+    HAR_LR_STAMP(3)
     block_sum_f<NP3, WIDE>(ps, sh, tot3);
     float pd1[NP1];
 #pragma unroll
@@ -963,24 +992,28 @@ __device__ __forceinline__ void qn_update_body(const QnArgs& a, int c, int b) {
   // complete and written back past this XCD's L2), and the block that counts last takes an agent-scope
   // ACQUIRE fence before reading any other chunk's partials (its own L2 / L1 copies invalidated), so
   // the handoff holds across the 8 XCDs without relying on the counter's relaxed ordering
+  HAR_LR_STAMP(4)
   if (threadIdx.x == 0) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     last = __hip_atomic_fetch_add(a.done + b, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == a.nch - 1;
     if (last) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   }
   __syncthreads();
+  HAR_LR_STAMP(5)
   if (!last) return;
   if (!a.init && p >= 0) reduce_chunks_shared<NP3, true>(a.P3 + (int64_t)b * a.nch * NP3, a.nch, fin_v, stage);
   __syncthreads();
+  HAR_LR_STAMP(6)
   if (threadIdx.x == 0) {
     qn_finalize(a, b, p, p >= 0 ? p2v[3 * p] + p2v[3 * p + 1] : 0.0, qs, fin_v);
     __hip_atomic_store(a.done + b, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
+  HAR_LR_STAMP(7)
 }
 
-template <bool FULLM, bool WIDE>
-__global__ __launch_bounds__(QN_BLOCK) void qn_update_kernel(QnArgs a) {
-  qn_update_body<FULLM, WIDE>(a, blockIdx.x, blockIdx.y);
+template <bool FULLM, bool WIDE, bool STAMP = false>
+__global__ __launch_bounds__(QN_BLOCK) void qn_update_kernel(QnArgs a, uint64_t* st) {
+  qn_update_body<FULLM, WIDE, STAMP>(a, blockIdx.x, blockIdx.y, st);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1097,17 +1130,20 @@ extern "C" int har_logreg_eval(const LogregEvalArgs* args, int KP, int n_models,
                                       (mf ? 4 * EVAL_DCH * KP : 0));
   dim3 grid(tiles, n_models);
   if (mf && KP == 8)
-    logreg_eval_kernel<8, EVAL_XLD_MF><<<grid, EVAL_ROWS, lds, s>>>(a);
+    logreg_eval_kernel<8, EVAL_XLD_MF><<<grid, EVAL_ROWS, lds, s>>>(a, nullptr);
   else if (mf)
-    logreg_eval_kernel<16, EVAL_XLD_MF><<<grid, EVAL_ROWS, lds, s>>>(a);
+    logreg_eval_kernel<16, EVAL_XLD_MF><<<grid, EVAL_ROWS, lds, s>>>(a, nullptr);
   else if (KP == 8 && narrow)
-    logreg_eval_kernel<8, EVAL_XLD_NARROW><<<grid, EVAL_ROWS, lds, s>>>(a);
+    if (g_lr_stamps)
+      logreg_eval_kernel<8, EVAL_XLD_NARROW, true><<<grid, EVAL_ROWS, lds, s>>>(a, g_lr_stamps);
+    else
+      logreg_eval_kernel<8, EVAL_XLD_NARROW><<<grid, EVAL_ROWS, lds, s>>>(a, nullptr);
   else if (KP == 8)
-    logreg_eval_kernel<8, EVAL_DCH + 1><<<grid, EVAL_ROWS, lds, s>>>(a);
+    logreg_eval_kernel<8, EVAL_DCH + 1><<<grid, EVAL_ROWS, lds, s>>>(a, nullptr);
   else if (narrow)
-    logreg_eval_kernel<16, EVAL_XLD_NARROW><<<grid, EVAL_ROWS, lds, s>>>(a);
+    logreg_eval_kernel<16, EVAL_XLD_NARROW><<<grid, EVAL_ROWS, lds, s>>>(a, nullptr);
   else
-    logreg_eval_kernel<16, EVAL_DCH + 1><<<grid, EVAL_ROWS, lds, s>>>(a);
+    logreg_eval_kernel<16, EVAL_DCH + 1><<<grid, EVAL_ROWS, lds, s>>>(a, nullptr);
   HAR_CHECK_LAUNCH();
   return 0;
 }
@@ -1239,19 +1275,31 @@ extern "C" int har_lbfgs_phase(const QnArgs* args, int KP, int phase, hipStream_
   const dim3 grid(a.nch, a.B);
   if (phase == 1) {
     if (KP == 8 && full)
-      qn_direction_kernel<8, true><<<grid, QN_BLOCK, 0, s>>>(a);
+      if (g_lr_stamps)
+        qn_direction_kernel<8, true, true><<<grid, QN_BLOCK, 0, s>>>(a, g_lr_stamps_dir);
+      else
+        qn_direction_kernel<8, true><<<grid, QN_BLOCK, 0, s>>>(a, nullptr);
     else if (KP == 8)
-      qn_direction_kernel<8, false><<<grid, QN_BLOCK, 0, s>>>(a);
+      qn_direction_kernel<8, false><<<grid, QN_BLOCK, 0, s>>>(a, nullptr);
     else if (full)
-      qn_direction_kernel<16, true><<<grid, QN_BLOCK, 0, s>>>(a);
+      qn_direction_kernel<16, true><<<grid, QN_BLOCK, 0, s>>>(a, nullptr);
     else
-      qn_direction_kernel<16, false><<<grid, QN_BLOCK, 0, s>>>(a);
+      qn_direction_kernel<16, false><<<grid, QN_BLOCK, 0, s>>>(a, nullptr);
   } else {
     if (full)  // 170 VGPRs: the 54-model CV batch at 9 chunks still fits one round (40.6 us vs 42.5 lean)
-      qn_update_kernel<true, true><<<grid, QN_BLOCK, 0, s>>>(a);
+      if (g_lr_stamps)
+        qn_update_kernel<true, true, true><<<grid, QN_BLOCK, 0, s>>>(a, g_lr_stamps_upd);
+      else
+        qn_update_kernel<true, true><<<grid, QN_BLOCK, 0, s>>>(a, nullptr);
     else
-      qn_update_kernel<false, false><<<grid, QN_BLOCK, 0, s>>>(a);
+      qn_update_kernel<false, false><<<grid, QN_BLOCK, 0, s>>>(a, nullptr);
   }
   HAR_CHECK_LAUNCH();
   return 0;
+}
+
+extern "C" void har_lr_set_stamps(uint64_t* ev, uint64_t* dir, uint64_t* upd) {
+  g_lr_stamps = ev;
+  g_lr_stamps_dir = dir;
+  g_lr_stamps_upd = upd;
 }
