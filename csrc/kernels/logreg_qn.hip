@@ -32,6 +32,7 @@
 #include <cstdlib>
 
 #include "common.h"
+#include "wave_ops.h"
 #include "../har_kernels.h"
 
 // Diagnostic phase stamps (tools/lr_stamps.py): a STAMP instantiation of the evaluation / direction /
@@ -247,7 +248,7 @@ __device__ __forceinline__ void logreg_eval_body(const LogregEvalArgs& a, int bx
   if (a.mode == 1) return;
   HAR_LR_STAMP(3)
   // tile loss: wave sums, then the 4 wave partials in a fixed order
-  lossv = wave_sum(lossv);
+  lossv = wops::wave_sum_f_dpp(lossv);
   if ((tid & 63) == 0) red[tid >> 6] = lossv;
   __syncthreads();                                 // rs / red complete; the last chunk is in xs
   const int SW = Fd * KP + KP + 1;
@@ -514,7 +515,8 @@ constexpr int NP3 = 5 + 3 * QN_MAX_M;        // s.y, s.s, y.y, x.x, pg.pg, then 
 
 constexpr int QN_MAX_CHUNKS = 32;
 
-// Block sum of fp32 per-lane partials (wave DPP sums, then the 4 wave partials in a fixed order),
+// Block sum of fp32 per-lane partials (wave DPP / lane-swap sums — wops::wave_sum_d_dpp; the __shfl_xor
+// form took ~20k cycles for the update's 56 values, profiles/r5/lr_stamps.md — then the 4 wave partials in a fixed order),
 // fp64 totals into the shared tot[NV].  WIDE: every value widened first, so all NV reductions
 // interleave (the full-history update pass: 170 VGPRs, 20.4 us single fit / 40.6 us 54-model batch
 // against 25.9 / 42.5 with each value widened as its own reduction starts — the lean form, kept
@@ -528,7 +530,7 @@ __device__ __forceinline__ void block_sum_f(const float (&p)[NV], double* sh, do
 #pragma unroll
     for (int q = 0; q < NV; ++q) v[q] = (double)p[q];
 #pragma unroll
-    for (int q = 0; q < NV; ++q) v[q] = wave_sum_d(v[q]);
+    for (int q = 0; q < NV; ++q) v[q] = wops::wave_sum_d_dpp(v[q]);
     if (lane == 0) {
 #pragma unroll
       for (int q = 0; q < NV; ++q) sh[w * NV + q] = v[q];
@@ -536,7 +538,7 @@ __device__ __forceinline__ void block_sum_f(const float (&p)[NV], double* sh, do
   } else {
 #pragma unroll
     for (int q = 0; q < NV; ++q) {
-      const double t = wave_sum_d((double)p[q]);
+      const double t = wops::wave_sum_d_dpp((double)p[q]);
       if (lane == 0) sh[w * NV + q] = t;
     }
   }
@@ -727,31 +729,31 @@ __device__ __forceinline__ void qn_direction_body(const QnArgs& a, int c, int b,
     __syncthreads();
   }
   HAR_LR_STAMP(1)
-  if (threadIdx.x == 0) {
+  if (threadIdx.x < 64) {
+    // the two-loop recursion on coefficients, spread over the 16 lanes of each DPP row of wave 0: lane k
+    // holds u_k, w_k, al_k (slot k < m; zero above), each step's 10-term dot product is a lane product
+    // plus a row sum by DPP rotations (fp64), the slot update a select on lane == j.  (Thread 0 alone,
+    // serial fp64 chains with a register select per slot, took ~17k cycles, profiles/r5/lr_stamps.md.)
+    // The same fixed order on every run; the sums' order differs from the serial form in the last bits.
+    const int k = threadIdx.x & 15;
+    if (threadIdx.x < QN_MAX_M) cS[threadIdx.x] = cY[threadIdx.x] = 0.f;
     float gamma = 0.f;
-    for (int j = 0; j < QN_MAX_M; ++j) cS[j] = cY[j] = 0.f;
-    if (rec) {  // the two-loop recursion on coefficients
-      // u, w, al in registers (slot-indexed updates as unrolled selects): the Gram rows are the only
-      // LDS reads of a step and issue together, instead of u / w being re-read after every store
-      double ur[QN_MAX_M], wr[QN_MAX_M], alr[QN_MAX_M];
-#pragma unroll
-      for (int k = 0; k < QN_MAX_M; ++k) ur[k] = wr[k] = alr[k] = 0.0;
+    if (rec) {
+      auto row_sum = [](double v) {
+        v += wops::dpp_d<wops::DPP_ROR8>(v);
+        v += wops::dpp_d<wops::DPP_ROR4>(v);
+        v += wops::dpp_d<wops::DPP_ROR2>(v);
+        return v + wops::dpp_d<wops::DPP_ROR1>(v);
+      };
+      const bool kin = k < mm;
+      double ur = 0.0, wr = 0.0, al = 0.0;
       for (int i = 0; i < a.filled; ++i) {  // newest -> oldest: q = pg + sum u_k y_k
         const int j = (a.head - 1 - i + mm) % mm;
         const double rho = rho_s[j];
-        // (a rejected pair, rho = 0: alj = 0 leaves u and al as the skipped step did; a select, not a
-        // branch, so rho's read issues with the row's)
-        // unconditional reads (j mm + k < QN_MAX_M^2; ur[k] = 0 for k >= mm): no branch per k, so the
-        // ten LDS reads issue together instead of one round trip per term; the sum order is unchanged
-        double sq = p1v[j];
-#pragma unroll
-        for (int k = 0; k < QN_MAX_M; ++k) sq += ur[k] * SY[j * mm + k];
-        const double alj = rho == 0.0 ? 0.0 : rho * sq;
-#pragma unroll
-        for (int k = 0; k < QN_MAX_M; ++k) {
-          alr[k] = k == j ? alj : alr[k];
-          ur[k] = k == j ? ur[k] - alj : ur[k];
-        }
+        const double sq = p1v[j] + row_sum(kin ? ur * SY[j * mm + k] : 0.0);
+        const double alj = rho == 0.0 ? 0.0 : rho * sq;  // (a rejected pair: rho = 0, u / al unchanged)
+        al = k == j ? alj : al;
+        ur = k == j ? ur - alj : ur;
       }
       double gm;
       if (a.filled == 0) {
@@ -764,29 +766,24 @@ __device__ __forceinline__ void qn_direction_body(const QnArgs& a, int c, int b,
       for (int i = a.filled - 1; i >= 0; --i) {  // oldest -> newest: r = gamma q + sum w_k s_k
         const int j = (a.head - 1 - i + mm) % mm;
         const double rho = rho_s[j];
-        double yr = p1v[QN_MAX_M + j];
-#pragma unroll
-        for (int k = 0; k < QN_MAX_M; ++k) yr += ur[k] * YY[j * mm + k];
+        double yr = p1v[QN_MAX_M + j] + row_sum(kin ? ur * YY[j * mm + k] : 0.0);
         yr *= gm;
-#pragma unroll
-        for (int k = 0; k < QN_MAX_M; ++k) yr += wr[k] * SY[k * mm + j];
-        double alj = 0.0;
-#pragma unroll
-        for (int k = 0; k < QN_MAX_M; ++k) alj = k == j ? alr[k] : alj;
+        yr += row_sum(kin ? wr * SY[k * mm + j] : 0.0);
+        const uint64_t alb = __builtin_bit_cast(uint64_t, al);  // al_j from lane j of the row
+        const double alj = __builtin_bit_cast(double, ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(alb >> 32), j) << 32) |
+                                                          (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)alb, j));
         const double dw = rho == 0.0 ? 0.0 : alj - rho * yr;  // (rho = 0: the skipped step, w unchanged)
-#pragma unroll
-        for (int k = 0; k < QN_MAX_M; ++k) wr[k] = k == j ? wr[k] + dw : wr[k];
+        wr = k == j ? wr + dw : wr;
       }
-#pragma unroll
-      for (int j = 0; j < QN_MAX_M; ++j) {
-        if (j < mm) {
-          cY[j] = (float)(gm * ur[j]);
-          cS[j] = (float)wr[j];
-        }
+      if (threadIdx.x < mm) {
+        cY[threadIdx.x] = (float)(gm * ur);
+        cS[threadIdx.x] = (float)wr;
       }
       gamma = (float)gm;
     }
-    gam = gamma;
+    if (threadIdx.x == 0) {
+      gam = gamma;
+    }
   }
   __syncthreads();
   HAR_LR_STAMP(2)

@@ -122,6 +122,39 @@ __device__ __forceinline__ float wave_sum_dpp(float v, const LaneSwap& sw) {
   return v + sw.x32f(v);
 }
 
+// all-reduce sums over the wave on the VALU (the __shfl_xor butterfly of common.h's wave_sum / wave_sum_d
+// is an LDS round trip per step, two per step for a double): row sums by DPP rotations, then the row and
+// half swaps.  A swap of v with itself leaves {own, partner} in its two outputs, so the sum takes both
+// outputs directly (no select; a + b == b + a, every lane ends with the same bits)
+__device__ __forceinline__ float wave_sum_f_dpp(float v) {
+  v = row16_sum(v);
+  const uint32_t u = __builtin_bit_cast(uint32_t, v);
+  const auto a = __builtin_amdgcn_permlane16_swap(u, u, false, false);
+  v = __builtin_bit_cast(float, (uint32_t)a[0]) + __builtin_bit_cast(float, (uint32_t)a[1]);
+  const uint32_t w = __builtin_bit_cast(uint32_t, v);
+  const auto b = __builtin_amdgcn_permlane32_swap(w, w, false, false);
+  return __builtin_bit_cast(float, (uint32_t)b[0]) + __builtin_bit_cast(float, (uint32_t)b[1]);
+}
+__device__ __forceinline__ double wave_sum_d_dpp(double v) {
+  v += dpp_d<DPP_ROR8>(v);
+  v += dpp_d<DPP_ROR4>(v);
+  v += dpp_d<DPP_ROR2>(v);
+  v += dpp_d<DPP_ROR1>(v);
+  auto swap_add = [](double x, bool half) {
+    const uint64_t u = __builtin_bit_cast(uint64_t, x);
+    const uint32_t lo = (uint32_t)u, hi = (uint32_t)(u >> 32);
+    const auto l = half ? __builtin_amdgcn_permlane32_swap(lo, lo, false, false)
+                        : __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+    const auto h = half ? __builtin_amdgcn_permlane32_swap(hi, hi, false, false)
+                        : __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+    const double x0 = __builtin_bit_cast(double, ((uint64_t)(uint32_t)h[0] << 32) | (uint32_t)l[0]);
+    const double x1 = __builtin_bit_cast(double, ((uint64_t)(uint32_t)h[1] << 32) | (uint32_t)l[1]);
+    return x0 + x1;
+  };
+  v = swap_add(v, false);
+  return swap_add(v, true);
+}
+
 // wave argmax of (gain, index): the largest gain, the lowest index among equal gains — an
 // associative, commutative combine, so the butterfly order (half swap, row swap, row rotations)
 // does not change the winner; every lane ends with it
