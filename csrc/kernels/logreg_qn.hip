@@ -515,41 +515,37 @@ constexpr int NP3 = 5 + 3 * QN_MAX_M;        // s.y, s.s, y.y, x.x, pg.pg, then 
 
 constexpr int QN_MAX_CHUNKS = 32;
 
-// Block sum of fp32 per-lane partials (wave DPP / lane-swap sums — wops::wave_sum_d_dpp; the __shfl_xor
-// form took ~20k cycles for the update's 56 values, profiles/r5/lr_stamps.md — then the 4 wave partials in a fixed order),
-// fp64 totals into the shared tot[NV].  WIDE: every value widened first, so all NV reductions
-// interleave (the full-history update pass: 170 VGPRs, 20.4 us single fit / 40.6 us 54-model batch
-// against 25.9 / 42.5 with each value widened as its own reduction starts — the lean form, kept
-// for the partial-history variant whose loads already fill the register file).  The former
-// double-array block_sum cost 314 VGPRs incl. AGPRs (one workgroup per CU).
+// Block sum of fp32 per-lane partials, fp64 totals into the shared tot[NV], through an LDS transpose:
+// every thread stores its NV partials, then thread 4 q + w adds value q over the 64 threads of
+// segment w (four fp64 chains of 16, fixed order), and thread q adds the four segments in order.
+// (Per-value wave reductions — 6 butterfly steps each, 56 values in the update pass — took 12-20k
+// cycles with LDS shuffles or fp64 DPP, profiles/r5/lr_stamps.md.)  `sh` holds the [NV][4] segment
+// sums; WIDE is kept for the call sites' signatures.
 template <int NV, bool WIDE = false>
 __device__ __forceinline__ void block_sum_f(const float (&p)[NV], double* sh, double* tot) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  if (WIDE) {  // every value widened first: all NV reductions interleave (latency, not registers)
-    double v[NV];
+  static_assert(QN_BLOCK == 256 && 4 * NV <= QN_BLOCK, "four 64-thread segments, one thread per (value, segment)");
+  constexpr int TP = QN_BLOCK + 4;  // row pitch (16-byte rows)
+  __shared__ __attribute__((aligned(16))) float tr[NV * TP];
+  const int t = threadIdx.x;
 #pragma unroll
-    for (int q = 0; q < NV; ++q) v[q] = (double)p[q];
+  for (int q = 0; q < NV; ++q) tr[q * TP + t] = p[q];
+  __syncthreads();
+  if (t < 4 * NV) {
+    const int q = t >> 2, w = t & 3;
+    const float4* r = reinterpret_cast<const float4*>(tr + q * TP + 64 * w);
+    double c0 = 0.0, c1 = 0.0, c2 = 0.0, c3 = 0.0;
 #pragma unroll
-    for (int q = 0; q < NV; ++q) v[q] = wops::wave_sum_d_dpp(v[q]);
-    if (lane == 0) {
-#pragma unroll
-      for (int q = 0; q < NV; ++q) sh[w * NV + q] = v[q];
+    for (int i = 0; i < 16; ++i) {
+      const float4 v = r[i];
+      c0 += (double)v.x;
+      c1 += (double)v.y;
+      c2 += (double)v.z;
+      c3 += (double)v.w;
     }
-  } else {
-#pragma unroll
-    for (int q = 0; q < NV; ++q) {
-      const double t = wops::wave_sum_d_dpp((double)p[q]);
-      if (lane == 0) sh[w * NV + q] = t;
-    }
+    sh[q * 4 + w] = (c0 + c1) + (c2 + c3);
   }
   __syncthreads();
-  if ((int)threadIdx.x < NV) {
-    const int q = threadIdx.x;
-    double t = 0.0;
-#pragma unroll
-    for (int i = 0; i < QN_BLOCK / 64; ++i) t += sh[i * NV + q];  // fixed order
-    tot[q] = t;
-  }
+  if (t < NV) tot[t] = (sh[t * 4] + sh[t * 4 + 1]) + (sh[t * 4 + 2] + sh[t * 4 + 3]);
   __syncthreads();
 }
 
@@ -746,14 +742,26 @@ __device__ __forceinline__ void qn_direction_body(const QnArgs& a, int c, int b,
         return v + wops::dpp_d<wops::DPP_ROR1>(v);
       };
       const bool kin = k < mm;
+      // every Gram element a lane needs, read before the dependent steps (step i uses slot j_i)
+      double sy1[QN_MAX_M], yy2[QN_MAX_M], sy2[QN_MAX_M];
+#pragma unroll
+      for (int i = 0; i < QN_MAX_M; ++i) {
+        const int j = (a.head - 1 - i + 2 * QN_MAX_M * mm) % mm;  // (any slot for i >= filled: unused)
+        sy1[i] = kin ? SY[j * mm + k] : 0.0;
+        yy2[i] = kin ? YY[j * mm + k] : 0.0;
+        sy2[i] = kin ? SY[k * mm + j] : 0.0;
+      }
       double ur = 0.0, wr = 0.0, al = 0.0;
-      for (int i = 0; i < a.filled; ++i) {  // newest -> oldest: q = pg + sum u_k y_k
-        const int j = (a.head - 1 - i + mm) % mm;
-        const double rho = rho_s[j];
-        const double sq = p1v[j] + row_sum(kin ? ur * SY[j * mm + k] : 0.0);
-        const double alj = rho == 0.0 ? 0.0 : rho * sq;  // (a rejected pair: rho = 0, u / al unchanged)
-        al = k == j ? alj : al;
-        ur = k == j ? ur - alj : ur;
+#pragma unroll
+      for (int i = 0; i < QN_MAX_M; ++i) {  // newest -> oldest: q = pg + sum u_k y_k
+        if (i < a.filled) {
+          const int j = (a.head - 1 - i + mm) % mm;
+          const double rho = rho_s[j];
+          const double sq = p1v[j] + row_sum(ur * sy1[i]);
+          const double alj = rho == 0.0 ? 0.0 : rho * sq;  // (a rejected pair: rho = 0, u / al unchanged)
+          al = k == j ? alj : al;
+          ur = k == j ? ur - alj : ur;
+        }
       }
       double gm;
       if (a.filled == 0) {
@@ -763,12 +771,14 @@ __device__ __forceinline__ void qn_direction_body(const QnArgs& a, int c, int b,
         const double yy = YY[n * mm + n];
         gm = (rho_s[n] > 0.0 && yy > 0.0) ? SY[n * mm + n] / yy : 1.0;
       }
-      for (int i = a.filled - 1; i >= 0; --i) {  // oldest -> newest: r = gamma q + sum w_k s_k
+#pragma unroll
+      for (int i = QN_MAX_M - 1; i >= 0; --i) {  // oldest -> newest: r = gamma q + sum w_k s_k
+        if (i >= a.filled) continue;
         const int j = (a.head - 1 - i + mm) % mm;
         const double rho = rho_s[j];
-        double yr = p1v[QN_MAX_M + j] + row_sum(kin ? ur * YY[j * mm + k] : 0.0);
+        double yr = p1v[QN_MAX_M + j] + row_sum(ur * yy2[i]);
         yr *= gm;
-        yr += row_sum(kin ? wr * SY[k * mm + j] : 0.0);
+        yr += row_sum(wr * sy2[i]);
         const uint64_t alb = __builtin_bit_cast(uint64_t, al);  // al_j from lane j of the row
         const double alj = __builtin_bit_cast(double, ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(alb >> 32), j) << 32) |
                                                           (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)alb, j));
