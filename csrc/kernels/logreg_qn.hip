@@ -176,11 +176,11 @@ __device__ __forceinline__ void logreg_eval_body(const LogregEvalArgs& a, int bx
   }
   float lossv = 0.f;
   if (ok) {
-    // one-hot columns in groups of CG: the group's indices in one round of independent loads, then its
+    // one-hot columns in groups of CG = 16: the group's indices in one round of independent loads, then its
     // weight rows in another (clamped, unconditional), added in column order with a select — two
     // round trips per group instead of two dependent ones per column (a per-column `if (col >= 0)`
     // load serialized ~2 C L2 round trips per evaluation; the sums and their order are unchanged)
-    constexpr int CG = 8;
+    constexpr int CG = 16;
     const int32_t* cr = a.cat + row * a.C;
     for (int c0 = 0; c0 < a.C; c0 += CG) {
       int cols[CG];
@@ -743,21 +743,30 @@ __device__ __forceinline__ void qn_direction_body(const QnArgs& a, int c, int b,
       };
       const bool kin = k < mm;
       // every Gram element a lane needs, read before the dependent steps (step i uses slot j_i)
-      double sy1[QN_MAX_M], yy2[QN_MAX_M], sy2[QN_MAX_M];
+      // (and the slot index j_i = head - 1 - i mod m by a conditional add: an integer modulo by the
+      // runtime m is a ~40-instruction division per step)
+      double sy1[QN_MAX_M], yy2[QN_MAX_M], sy2[QN_MAX_M], rh[QN_MAX_M], pa[QN_MAX_M], pb[QN_MAX_M];
+      int js[QN_MAX_M];
 #pragma unroll
       for (int i = 0; i < QN_MAX_M; ++i) {
-        const int j = (a.head - 1 - i + 2 * QN_MAX_M * mm) % mm;  // (any slot for i >= filled: unused)
+        int j = a.head - 1 - i;
+        j = j < 0 ? j + mm : j;
+        j = j < 0 ? 0 : j;  // (i >= filled may run below slot 0: any slot, unused)
+        js[i] = j;
         sy1[i] = kin ? SY[j * mm + k] : 0.0;
         yy2[i] = kin ? YY[j * mm + k] : 0.0;
         sy2[i] = kin ? SY[k * mm + j] : 0.0;
+        rh[i] = rho_s[j];
+        pa[i] = p1v[j];
+        pb[i] = p1v[QN_MAX_M + j];
       }
       double ur = 0.0, wr = 0.0, al = 0.0;
 #pragma unroll
       for (int i = 0; i < QN_MAX_M; ++i) {  // newest -> oldest: q = pg + sum u_k y_k
         if (i < a.filled) {
-          const int j = (a.head - 1 - i + mm) % mm;
-          const double rho = rho_s[j];
-          const double sq = p1v[j] + row_sum(ur * sy1[i]);
+          const int j = js[i];
+          const double rho = rh[i];
+          const double sq = pa[i] + row_sum(ur * sy1[i]);
           const double alj = rho == 0.0 ? 0.0 : rho * sq;  // (a rejected pair: rho = 0, u / al unchanged)
           al = k == j ? alj : al;
           ur = k == j ? ur - alj : ur;
@@ -767,16 +776,16 @@ __device__ __forceinline__ void qn_direction_body(const QnArgs& a, int c, int b,
       if (a.filled == 0) {
         gm = 1.0 / fmax(sqrt(p1v[2 * QN_MAX_M]), 1e-12);
       } else {
-        const int n = (a.head - 1 + mm) % mm;
+        const int n = js[0];
         const double yy = YY[n * mm + n];
         gm = (rho_s[n] > 0.0 && yy > 0.0) ? SY[n * mm + n] / yy : 1.0;
       }
 #pragma unroll
       for (int i = QN_MAX_M - 1; i >= 0; --i) {  // oldest -> newest: r = gamma q + sum w_k s_k
         if (i >= a.filled) continue;
-        const int j = (a.head - 1 - i + mm) % mm;
-        const double rho = rho_s[j];
-        double yr = p1v[QN_MAX_M + j] + row_sum(ur * yy2[i]);
+        const int j = js[i];
+        const double rho = rh[i];
+        double yr = pb[i] + row_sum(ur * yy2[i]);
         yr *= gm;
         yr += row_sum(wr * sy2[i]);
         const uint64_t alb = __builtin_bit_cast(uint64_t, al);  // al_j from lane j of the row
