@@ -176,11 +176,11 @@ __device__ __forceinline__ void logreg_eval_body(const LogregEvalArgs& a, int bx
   }
   float lossv = 0.f;
   if (ok) {
-    // one-hot columns in groups of CG = 16: the group's indices in one round of independent loads, then its
+    // one-hot columns in groups of CG: the group's indices in one round of independent loads, then its
     // weight rows in another (clamped, unconditional), added in column order with a select — two
     // round trips per group instead of two dependent ones per column (a per-column `if (col >= 0)`
     // load serialized ~2 C L2 round trips per evaluation; the sums and their order are unchanged)
-    constexpr int CG = 16;
+    constexpr int CG = 8;  // (16: slower, r5 stamps)
     const int32_t* cr = a.cat + row * a.C;
     for (int c0 = 0; c0 < a.C; c0 += CG) {
       int cols[CG];
@@ -283,18 +283,36 @@ __device__ __forceinline__ void logreg_eval_body(const LogregEvalArgs& a, int bx
     } else {
       for (int o = tid; o < nc * KP; o += EVAL_ROWS) {
         const int j = o / KP, k = o % KP;
-        float acc = 0.f;
-        for (int i = 0; i < EVAL_ROWS; ++i) acc = fmaf(rs[i * KP + k], xs[i * xld + j], acc);
-        slab[(int64_t)c0 * KP + o] = acc;
+        // four interleaved row chains (rows i = 4 m + r), combined in a fixed order: a quarter of the
+        // dependent FMA latency of one 256-long chain (deterministic, not the single chain's bits)
+        float acc[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 4
+        for (int i = 0; i < EVAL_ROWS; i += 4) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) acc[r] = fmaf(rs[(i + r) * KP + k], xs[(i + r) * xld + j], acc[r]);
+        }
+        slab[(int64_t)c0 * KP + o] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
       }
     }
   }
   HAR_LR_STAMP(5)
   // intercept gradient sum R of the tile
-  for (int k = tid; k < KP; k += EVAL_ROWS) {
+  // intercept: the 8 class sums over the 256 rows on 32 threads per class (8-row chains, then a
+  // fixed-order tree of the 32 through LDS), not one 256-long chain per class
+  {
+    const int k = tid & (KP - 1), part = tid / KP;  // KP classes x (EVAL_ROWS / KP) parts of KP rows
     float acc = 0.f;
-    for (int i = 0; i < EVAL_ROWS; ++i) acc += rs[i * KP + k];
-    slab[Fd * KP + k] = acc;
+#pragma unroll
+    for (int i = 0; i < KP; ++i) acc += rs[(part * KP + i) * KP + k];
+    __syncthreads();  // (every thread's pass-B reads of rs / xs are done: red2 reuses xs)
+    float* red2 = xs;
+    red2[tid] = acc;
+    __syncthreads();
+    if (tid < KP) {
+      float t = 0.f;
+      for (int q = 0; q < EVAL_ROWS / KP; ++q) t += red2[q * KP + tid];
+      slab[Fd * KP + tid] = t;
+    }
   }
   if (tid == 0) slab[SW - 1] = (red[0] + red[1]) + (red[2] + red[3]);
   HAR_LR_STAMP(6)
