@@ -418,8 +418,9 @@ PYBIND11_MODULE(_har_native, m) {
     return old;
   });
   m.def("logreg_set_spin_limit", [](uint32_t n) { return har_logreg_set_spin_limit(n); });
-  m.def("lr_set_stamps", [](uint64_t ev, uint64_t dir, uint64_t upd) {
-    har_lr_set_stamps(reinterpret_cast<uint64_t*>(ev), reinterpret_cast<uint64_t*>(dir), reinterpret_cast<uint64_t*>(upd));
+  m.def("lr_set_stamps", [](uint64_t ev, uint64_t dir, uint64_t upd, uint64_t grd) {
+    har_lr_set_stamps(reinterpret_cast<uint64_t*>(ev), reinterpret_cast<uint64_t*>(dir), reinterpret_cast<uint64_t*>(upd),
+                      reinterpret_cast<uint64_t*>(grd));
   });
   // the persistent solve's timeout flag (blocking 4-byte read; tests / diagnostics)
   m.def("logreg_solve_flag", [](const LogregSolvePlan& p) {

@@ -323,7 +323,7 @@ int har_lbfgs_phase(const QnArgs* a, int KP, int phase, hipStream_t s);
 // the launch sequence), -2 invalid; sync = 2 device words (barrier counter, timeout flag)
 uint32_t har_logreg_set_spin_limit(uint32_t n);
 // diagnostic phase stamps of the evaluation / direction / update kernels (tools/lr_stamps.py); null = off
-void har_lr_set_stamps(uint64_t* ev, uint64_t* dir, uint64_t* upd);
+void har_lr_set_stamps(uint64_t* ev, uint64_t* dir, uint64_t* upd, uint64_t* grd);
 int har_logreg_solve_persistent(const QnArgs* q, const LogregEvalArgs* evT, const LogregGradArgs* grT, int nT,
                                 const LogregEvalArgs* ev1, const LogregGradArgs* gr1, int n1, int KP, int max_iter,
                                 uint32_t* sync, int max_grid, hipStream_t s);

@@ -41,6 +41,7 @@
 uint64_t* g_lr_stamps = nullptr;       // evaluation kernel rows
 uint64_t* g_lr_stamps_dir = nullptr;   // direction kernel rows
 uint64_t* g_lr_stamps_upd = nullptr;   // update kernel rows
+uint64_t* g_lr_stamps_grd = nullptr;   // gradient kernel rows
 namespace {
 #define HAR_LR_STAMP(k)                                                                                  \
   if constexpr (STAMP) {                                                                                 \
@@ -365,8 +366,9 @@ __device__ __forceinline__ double loss_decode(const float* in) {
   return (double)q / LOSS_FX;
 }
 
-template <int KP>
-__device__ __forceinline__ void logreg_grad_body(const LogregGradArgs& a, int bx, int by) {
+template <int KP, bool STAMP = false>
+__device__ __forceinline__ void logreg_grad_body(const LogregGradArgs& a, int bx, int by, uint64_t* st = nullptr) {
+  HAR_LR_STAMP(0)
   __shared__ float part[256 * KP];
   __shared__ int cs_l[257];                        // col_slice[c0 .. c1] of the block
   __shared__ float tl[256];                        // tile losses (block 0)
@@ -393,6 +395,7 @@ __device__ __forceinline__ void logreg_grad_body(const LogregGradArgs& a, int bx
     else
       a.loss[bt] = l;
   }
+  HAR_LR_STAMP(1)
   const int s0 = cs_l[0], s1 = cs_l[c1 - c0];
   const int cs0 = col < c1 ? cs_l[threadIdx.x] : 0, cs1 = col < c1 ? cs_l[threadIdx.x + 1] : 0;
   const float* R = a.R + (int64_t)by * a.N * KP;  // this launch's residual slot of the model
@@ -436,6 +439,7 @@ __device__ __forceinline__ void logreg_grad_body(const LogregGradArgs& a, int bx
       for (int k = 0; k < KP; ++k) g[k] += part[(e - base) * KP + k];
     }
   }
+  HAR_LR_STAMP(2)
   if (col >= c1) return;
   const int cm = a.col_map[col];
   if (cm >= 0 || cm == -1) {  // dense column j = cm, or the intercept (slab entries after the dense block)
@@ -447,16 +451,18 @@ __device__ __forceinline__ void logreg_grad_body(const LogregGradArgs& a, int bx
       for (int k = 0; k < KP; ++k) g[k] += p[k];
     }
   }
+  HAR_LR_STAMP(3)
   const float sc = col < a.F ? a.inv_std[(int64_t)s * a.F + col] : 1.f;
   const int64_t D = (int64_t)a.K * Fp1;
   float* G = a.G + (int64_t)bt * D;
   const float* pm = a.pmask + (int64_t)s * D;
   for (int k = 0; k < a.K; ++k) G[(int64_t)k * Fp1 + col] = g[k] * sc * pm[(int64_t)k * Fp1 + col];
+  HAR_LR_STAMP(4)
 }
 
-template <int KP>
-__global__ __launch_bounds__(256) void logreg_grad_kernel(LogregGradArgs a) {
-  logreg_grad_body<KP>(a, blockIdx.x, blockIdx.y);
+template <int KP, bool STAMP = false>
+__global__ __launch_bounds__(256) void logreg_grad_kernel(LogregGradArgs a, uint64_t* st) {
+  logreg_grad_body<KP, STAMP>(a, blockIdx.x, blockIdx.y, st);
 }
 
 // after the data-parallel all-reduce of the bucket: the summed fixed-point losses -> fp64
@@ -1192,9 +1198,12 @@ extern "C" int har_logreg_grad(const LogregGradArgs* args, int KP, int n_models,
   if (n_models == 0) return 0;
   dim3 grid((a.F + 1 + 255) / 256, n_models);
   if (KP == 8)
-    logreg_grad_kernel<8><<<grid, 256, 0, s>>>(a);
+    if (g_lr_stamps_grd)
+      logreg_grad_kernel<8, true><<<grid, 256, 0, s>>>(a, g_lr_stamps_grd);
+    else
+      logreg_grad_kernel<8><<<grid, 256, 0, s>>>(a, nullptr);
   else
-    logreg_grad_kernel<16><<<grid, 256, 0, s>>>(a);
+    logreg_grad_kernel<16><<<grid, 256, 0, s>>>(a, nullptr);
   HAR_CHECK_LAUNCH();
   return 0;
 }
@@ -1332,7 +1341,8 @@ extern "C" int har_lbfgs_phase(const QnArgs* args, int KP, int phase, hipStream_
   return 0;
 }
 
-extern "C" void har_lr_set_stamps(uint64_t* ev, uint64_t* dir, uint64_t* upd) {
+extern "C" void har_lr_set_stamps(uint64_t* ev, uint64_t* dir, uint64_t* upd, uint64_t* grd) {
+  g_lr_stamps_grd = grd;
   g_lr_stamps = ev;
   g_lr_stamps_dir = dir;
   g_lr_stamps_upd = upd;

@@ -16,6 +16,8 @@ PHASES = {
              "pass B (dense gradient)", "intercept sums + slab"],
     "direction": ["P1 / Gram / rho loads", "recursion (thread 0) + barrier", "element sweep (trial points)",
                   "block sums", "P2 stores"],
+    "grad": ["col_slice + tile-loss loads", "one-hot slices (row lists)", "dense / intercept slab sums",
+             "scale + store"],
     "update": ["P2 reduce", "pick (thread 0)", "element sweep (history)", "block sums + P3 / P1 stores",
                "release fence + counter", "(last chunk) P3 reduce", "(last chunk) finalize"],
 }
@@ -41,12 +43,12 @@ def main():
     torch.cuda.synchronize()
     rows = 1 << 16
     bufs = {k: torch.zeros(rows * 16, dtype=torch.int64, device=dev) for k in PHASES}
-    mod.lr_set_stamps(bufs["eval"].data_ptr(), bufs["direction"].data_ptr(), bufs["update"].data_ptr())
+    mod.lr_set_stamps(bufs["eval"].data_ptr(), bufs["direction"].data_ptr(), bufs["update"].data_ptr(), bufs["grad"].data_ptr())
     try:
         build_estimator(a.model, cfg, dev, nf, nc).fit(train)
         torch.cuda.synchronize()
     finally:
-        mod.lr_set_stamps(0, 0, 0)
+        mod.lr_set_stamps(0, 0, 0, 0)
     for k, names in PHASES.items():
         st = bufs[k].view(rows, 16).cpu().numpy().astype(np.int64)
         live = st[:, 0] != 0
