@@ -282,34 +282,17 @@ __device__ __forceinline__ void logreg_eval_body(const LogregEvalArgs& a, int bx
       for (int o = tid; o < nc * KP; o += EVAL_ROWS)
         slab[(int64_t)c0 * KP + o] = (pb[o] + pb[EVAL_DCH * KP + o]) + (pb[2 * EVAL_DCH * KP + o] + pb[3 * EVAL_DCH * KP + o]);
     } else {
-      const int NO = nc * KP;  // outputs of the chunk
-      if (NO <= EVAL_ROWS) {
-        // P row ranges per output on P x NO threads, partials added in range order: each wave issues
-        // 1 / P of the LDS reads (one thread per output left most waves idle and the few busy ones
-        // LDS-issue-bound: ~4.6k cycles for the 80 outputs of the reference encoding, r5 stamps)
-        __shared__ float pbuf[EVAL_ROWS];
-        const int P = EVAL_ROWS / NO, RP = (EVAL_ROWS + P - 1) / P;
-        if (tid < P * NO) {
-          const int o = tid % NO, pr = tid / NO, j = o / KP, k = o % KP;
-          const int i0 = pr * RP, i1 = min(EVAL_ROWS, i0 + RP);
-          float acc = 0.f;
-          for (int i = i0; i < i1; ++i) acc = fmaf(rs[i * KP + k], xs[i * xld + j], acc);
-          pbuf[tid] = acc;
+      for (int o = tid; o < nc * KP; o += EVAL_ROWS) {
+        const int j = o / KP, k = o % KP;
+        // four interleaved row chains (rows i = 4 m + r), combined in a fixed order: a quarter of the
+        // dependent FMA latency of one 256-long chain (deterministic, not the single chain's bits)
+        float acc[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 4
+        for (int i = 0; i < EVAL_ROWS; i += 4) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) acc[r] = fmaf(rs[(i + r) * KP + k], xs[(i + r) * xld + j], acc[r]);
         }
-        __syncthreads();
-        if (tid < NO) {
-          float t = pbuf[tid];
-          for (int pr = 1; pr < P; ++pr) t += pbuf[pr * NO + tid];
-          slab[(int64_t)c0 * KP + tid] = t;
-        }
-        __syncthreads();  // (pbuf is rewritten by the next chunk)
-      } else {
-        for (int o = tid; o < NO; o += EVAL_ROWS) {
-          const int j = o / KP, k = o % KP;
-          float acc = 0.f;
-          for (int i = 0; i < EVAL_ROWS; ++i) acc = fmaf(rs[i * KP + k], xs[i * xld + j], acc);
-          slab[(int64_t)c0 * KP + o] = acc;
-        }
+        slab[(int64_t)c0 * KP + o] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
       }
     }
   }
@@ -434,47 +417,16 @@ __device__ __forceinline__ void logreg_grad_body(const LogregGradArgs& a, int bx
       float gs[KP];
 #pragma unroll
       for (int k = 0; k < KP; ++k) gs[k] = 0.f;
-      if (a.SL <= 32) {
-        // all of the slice's row indices in one round of loads, then its residual rows in four groups
-        // of 8 (clamped loads past the slice's end, added under a mask): five round trips per 32-row
-        // slice instead of eight (index, then rows, per group); rows added in order: the same sums
-        const int nr = r1 - r0;
-        int ridx[32];
+#pragma unroll 8  // 8 row indices, then their 8 residual rows in flight: 8 dependent round trips per 32-row slice instead of 16
+      for (int i = r0; i < r1; ++i) {
+        const f32x4_t* rp = reinterpret_cast<const f32x4_t*>(R + (int64_t)a.csc_rows[i] * KP);
 #pragma unroll
-        for (int u = 0; u < 32; ++u) ridx[u] = a.csc_rows[r0 + min(u, nr - 1)];
-#pragma unroll
-        for (int grp = 0; grp < 4; ++grp) {
-          f32x4_t rv[8][KP / 4];
-#pragma unroll
-          for (int u = 0; u < 8; ++u) {
-            const f32x4_t* rp = reinterpret_cast<const f32x4_t*>(R + (int64_t)ridx[8 * grp + u] * KP);
-#pragma unroll
-            for (int q = 0; q < KP / 4; ++q) rv[u][q] = rp[q];
-          }
-#pragma unroll
-          for (int u = 0; u < 8; ++u) {
-            const bool on = 8 * grp + u < nr;
-#pragma unroll
-            for (int q = 0; q < KP / 4; ++q) {
-              gs[4 * q + 0] = on ? gs[4 * q + 0] + rv[u][q][0] : gs[4 * q + 0];
-              gs[4 * q + 1] = on ? gs[4 * q + 1] + rv[u][q][1] : gs[4 * q + 1];
-              gs[4 * q + 2] = on ? gs[4 * q + 2] + rv[u][q][2] : gs[4 * q + 2];
-              gs[4 * q + 3] = on ? gs[4 * q + 3] + rv[u][q][3] : gs[4 * q + 3];
-            }
-          }
-        }
-      } else {
-#pragma unroll 8  // 8 row indices, then their 8 residual rows in flight
-        for (int i = r0; i < r1; ++i) {
-          const f32x4_t* rp = reinterpret_cast<const f32x4_t*>(R + (int64_t)a.csc_rows[i] * KP);
-#pragma unroll
-          for (int q = 0; q < KP / 4; ++q) {
-            const f32x4_t r4 = rp[q];
-            gs[4 * q + 0] += r4[0];
-            gs[4 * q + 1] += r4[1];
-            gs[4 * q + 2] += r4[2];
-            gs[4 * q + 3] += r4[3];
-          }
+        for (int q = 0; q < KP / 4; ++q) {
+          const f32x4_t r4 = rp[q];
+          gs[4 * q + 0] += r4[0];
+          gs[4 * q + 1] += r4[1];
+          gs[4 * q + 2] += r4[2];
+          gs[4 * q + 3] += r4[3];
         }
       }
 #pragma unroll
