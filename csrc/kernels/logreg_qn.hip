@@ -282,17 +282,13 @@ __device__ __forceinline__ void logreg_eval_body(const LogregEvalArgs& a, int bx
       for (int o = tid; o < nc * KP; o += EVAL_ROWS)
         slab[(int64_t)c0 * KP + o] = (pb[o] + pb[EVAL_DCH * KP + o]) + (pb[2 * EVAL_DCH * KP + o] + pb[3 * EVAL_DCH * KP + o]);
     } else {
+      // (one 256-row chain per output: four interleaved chains and row ranges on more threads both
+      // measured slower, the reads being the bound — r5 stamps)
       for (int o = tid; o < nc * KP; o += EVAL_ROWS) {
         const int j = o / KP, k = o % KP;
-        // four interleaved row chains (rows i = 4 m + r), combined in a fixed order: a quarter of the
-        // dependent FMA latency of one 256-long chain (deterministic, not the single chain's bits)
-        float acc[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll 4
-        for (int i = 0; i < EVAL_ROWS; i += 4) {
-#pragma unroll
-          for (int r = 0; r < 4; ++r) acc[r] = fmaf(rs[(i + r) * KP + k], xs[(i + r) * xld + j], acc[r]);
-        }
-        slab[(int64_t)c0 * KP + o] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+        float acc = 0.f;
+        for (int i = 0; i < EVAL_ROWS; ++i) acc = fmaf(rs[i * KP + k], xs[i * xld + j], acc);
+        slab[(int64_t)c0 * KP + o] = acc;
       }
     }
   }
