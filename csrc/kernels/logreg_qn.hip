@@ -533,7 +533,7 @@ constexpr int NP2 = 3 * QN_MAX_TRIALS + 2;   // per trial: 0.5 l2 x^2, l1 |x|, p
 constexpr int NP3 = 5 + 3 * QN_MAX_M;        // s.y, s.s, y.y, x.x, pg.pg, then s.y_j, s_j.y, y.y_j
 
 
-constexpr int QN_MAX_CHUNKS = 64;  // (32 -> 64: a single fit's 18.6k-element sweeps one or two elements per thread)
+constexpr int QN_MAX_CHUNKS = 32;
 
 // Block sum of fp32 per-lane partials, fp64 totals into the shared tot[NV], through an LDS transpose:
 // every thread stores its NV partials, then thread 4 q + w adds value q over the 64 threads of
