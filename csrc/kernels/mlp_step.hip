@@ -169,13 +169,15 @@ __global__ __launch_bounds__(512) void mlp_fwd3_kernel(
     if constexpr (!INFER) ynext = (labels + (size_t)tile_of(0) * FRT)[sr];
   }
   __builtin_amdgcn_sched_barrier(0);
+  // b1 first, then W1 k-chunk-major (both unit tiles of chunk kc together): tile 0's stage 2 waits, at
+  // chunk kc, only for the loads up to that chunk, so the tail of the W1 stream overlaps its MFMAs
 #pragma unroll
-  for (int t = 0; t < 2; ++t) {
+  for (int t = 0; t < 2; ++t) b1r[t] = *reinterpret_cast<const float4*>(b1 + u0 + 16 * t + 4 * g);
 #pragma unroll
-    for (int kc = 0; kc < KC; ++kc)
+  for (int kc = 0; kc < KC; ++kc)
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
       w1f[t][kc] = *reinterpret_cast<const bf16x8_t*>(W1f + (size_t)((2 * wave + t) * KC + ((kc + krot) & (KC - 1))) * 512 + frag_lane_off(lane));
-    b1r[t] = *reinterpret_cast<const float4*>(b1 + u0 + 16 * t + 4 * g);
-  }
   // stage-3 A fragment: Wout[class c16][u0 + 4g + j] (j < 4), [u0 + 16 + 4g + j - 4] (j >= 4): the k
   // order of the h2 register pairs (C layout: unit 4g + r of a 16-unit tile in register r)
   const uint2 wlo = *reinterpret_cast<const uint2*>(Wo + (size_t)c16 * HH + u0 + 4 * g);
