@@ -30,7 +30,7 @@ import torch
 
 from . import _native
 
-SLICE_ROWS = 32  # rows per CSC slice of the gradient / summary kernels
+SLICE_ROWS = int(os.environ.get("HAR_LR_SL", "32"))  # rows per CSC slice of the gradient / summary kernels
 
 
 def logreg_loss_grad_torch(X, y, W, b, rw, inv_wsum):
@@ -148,6 +148,45 @@ class LogregDesign:
                 cs = cs.to(torch.int32)
             self._col_slice = self.hm._lr_col_slice = cs
         return self._col_slice
+
+    def col_blocks(self):
+        """(blk, nblk, srow) of the gradient kernel: consecutive column blocks of at most 256 columns
+        and 256 CSC row slices each (a lone column with more slices takes a block of its own) as
+        [nblk][4] int32 (c0, c1, first slice, end slice), and srow [slices + 1] = the first CSC row of
+        every slice (the row lists are contiguous across columns, so slice sl covers rows
+        [srow[sl], srow[sl + 1])).  The kernel then loads everything a lane needs in one round at
+        entry instead of searching the slice's column and reading its offsets (grad stamps,
+        profiles/r5/lr_kernel_medians.md).  A column's slices are still summed in order by one lane:
+        the gradient is bitwise the fixed-block one.  Built once per matrix (one host read of
+        col_slice, cached on it); HAR_LR_COLBLK=0 keeps the fixed 256-column blocks."""
+        if os.environ.get("HAR_LR_COLBLK", "1") == "0" or self.device.type != "cuda":
+            return None, 0, None
+        cached = getattr(self.hm, "_lr_col_blk", None)
+        if cached is None or cached[3] != self.SL:
+            F1 = self.F + 1
+            cs = self.col_slice()[:F1 + 1].long()
+            csh = cs.cpu().tolist()
+            bounds, c0, sl = [0], 0, 0
+            for c in range(F1):
+                n = csh[c + 1] - csh[c]
+                if c > c0 and (c - c0 == 256 or sl + n > 256):
+                    bounds.append(c)
+                    c0, sl = c, 0
+                sl += n
+            bounds.append(F1)
+            blk = [(bounds[i], bounds[i + 1], csh[bounds[i]], csh[bounds[i + 1]]) for i in range(len(bounds) - 1)]
+            blk_t = torch.tensor(blk, dtype=torch.int32, device=self.device).contiguous()
+            total = csh[F1]
+            off = self.csc_off.long()
+            ns = cs[1:] - cs[:-1]
+            col_of = torch.repeat_interleave(torch.arange(F1, device=self.device), ns)
+            j = torch.arange(total, device=self.device) - cs[col_of]
+            srow = torch.empty(total + 1, dtype=torch.int32, device=self.device)
+            srow[:total] = (off[col_of] + j * self.SL).to(torch.int32)
+            srow[total] = off[F1].to(torch.int32)
+            cached = (blk_t, len(blk), srow, self.SL)
+            self.hm._lr_col_blk = cached
+        return cached[0], cached[1], cached[2]
 
     def rw_ptr(self) -> int:
         return 0 if self.rw is None else self.rw.data_ptr()
@@ -332,6 +371,7 @@ class DeviceLogregSolver:
             n_models = (self.B * self.T) // tstride
             R = 0 if self.R is None else self.R.data_ptr()
             cs = d.col_slice()
+            cb, nblk, srow = d.col_blocks()
             dp = self.allreduce is not None
             launches = []
             for c0 in range(0, n_models, self.rchunk):
@@ -343,7 +383,8 @@ class DeviceLogregSolver:
                 gr = (self.slab.data_ptr(), R, d.col_map.data_ptr(), d.csc_rows.data_ptr(), d.csc_off.data_ptr(),
                       cs.data_ptr(), d.SL, self.inv_std.data_ptr(), self.pmask.data_ptr(), d.N, d.F, d.Fd, d.K,
                       self.T, tstride, m0, self.ntiles, self.G.data_ptr(), self.loss.data_ptr(),
-                      self.loss_fx.data_ptr() if dp else 0, d.KP, n)
+                      self.loss_fx.data_ptr() if dp else 0, d.KP, n, 0 if cb is None else cb.data_ptr(), nblk,
+                      0 if srow is None else srow.data_ptr())
                 launches.append((ev, gr))
             cache[tstride] = launches
         return cache[tstride]

@@ -396,6 +396,9 @@ PYBIND11_MODULE(_har_native, m) {
     c.gr.loss = P<double>(U(g[18]));
     c.gr.loss_fx = P<float>(U(g[19]));
     if ((int)I(g[20]) != c.KP || (int)I(g[21]) != c.n_models) throw std::runtime_error("logreg_eval_chunk: KP / n mismatch");
+    c.gr.col_blk = P<const int32_t>(U(g[22]));
+    c.gr.nblk = (int)I(g[23]);
+    c.gr.srow = P<const int32_t>(U(g[24]));
     return c;
   });
   py::class_<LogregSolvePlan>(m, "LogregSolvePlan");
@@ -431,8 +434,11 @@ PYBIND11_MODULE(_har_native, m) {
   });
   m.def("logreg_grad", [](u slab, u R, u col_map, u csc_rows, u csc_off, u col_slice, int SL, u inv_std, u pmask,
                           int64_t N, int F, int Fd, int K, int T, int tstride, int model0, int ntiles, u G, u loss,
-                          u loss_fx, int KP, int n_models, u stream) {
+                          u loss_fx, int KP, int n_models, u col_blk, int nblk, u srow, u stream) {
     LogregGradArgs a;
+    a.col_blk = P<const int32_t>(col_blk);
+    a.nblk = nblk;
+    a.srow = P<const int32_t>(srow);
     a.slab = P<const float>(slab);
     a.R = P<const float>(R);
     a.col_map = P<const int32_t>(col_map);

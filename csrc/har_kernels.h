@@ -238,6 +238,9 @@ typedef struct LogregGradArgs {
   float* G;                 // [n_trial_models][K][F+1]
   double* loss;             // [n_trial_models] (loss_fx == null)
   float* loss_fx;           // [n_trial_models][5] fixed-point loss pieces for the DP bucket, or null
+  const int32_t* col_blk;   // [nblk][4] column blocks (c0, c1, first slice, end slice): <= 256 columns and
+  int nblk;                 // <= 256 slices each (a lone heavier column excepted), or null: fixed 256 columns
+  const int32_t* srow;      // [slices + 1] first CSC row of every slice (with col_blk)
 } LogregGradArgs;
 
 typedef struct QnArgs {

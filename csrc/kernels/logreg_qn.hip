@@ -373,12 +373,40 @@ __device__ __forceinline__ void logreg_grad_body(const LogregGradArgs& a, int bx
   const int Fp1 = a.F + 1;
   const int SW = a.Fd * KP + KP + 1;
   const float* slab = a.slab + (int64_t)bt * a.ntiles * SW;
-  const int c0 = bx * 256, c1 = min(Fp1, c0 + 256);
+  // col_blk (balanced blocks, ops/logreg.py LogregDesign.col_blocks): block bx = columns [c0, c1), slices
+  // [s0, s1), and slice sl covers the CSC rows [srow[sl], srow[sl + 1]) — no slice -> column search;
+  // everything a lane needs is loaded in ONE round at entry (its slice's rows, its column's slice range,
+  // inv_std and pmask).  Without it: fixed 256-column blocks, the slice's column searched in LDS
+  const bool fast = a.col_blk != nullptr;
+  int c0, c1, s0 = 0, s1 = 0;
+  if (fast) {
+    const int4 bk = reinterpret_cast<const int4*>(a.col_blk)[bx];
+    c0 = bk.x; c1 = bk.y; s0 = bk.z; s1 = bk.w;
+  } else {
+    c0 = bx * 256;
+    c1 = min(Fp1, c0 + 256);
+  }
   const int col = c0 + threadIdx.x;
-  // one round of independent loads instead of dependent chains: the block's slice index (the
-  // slice -> column search below runs in LDS) and, in block 0, the tile losses
-  if (c0 + (int)threadIdx.x <= c1) cs_l[threadIdx.x] = a.col_slice[c0 + threadIdx.x];
-  if (threadIdx.x == 0 && c1 - c0 == 256) cs_l[256] = a.col_slice[c1];
+  int cs0 = 0, cs1 = 0, r0f = 0, r1f = 0;
+  if (fast) {
+    if (col < c1) { cs0 = a.col_slice[col]; cs1 = a.col_slice[col + 1]; }
+    if (s0 + (int)threadIdx.x < s1) { r0f = a.srow[s0 + threadIdx.x]; r1f = a.srow[s0 + threadIdx.x + 1]; }
+  } else {
+    if (c0 + (int)threadIdx.x <= c1) cs_l[threadIdx.x] = a.col_slice[c0 + threadIdx.x];
+    if (threadIdx.x == 0 && c1 - c0 == 256) cs_l[256] = a.col_slice[c1];
+  }
+  // the output scaling of this lane's column, loaded now (its latency hides behind the sums)
+  const int64_t D = (int64_t)a.K * Fp1;
+  float sc = 1.f, pmv[KP];
+#pragma unroll
+  for (int k = 0; k < KP; ++k) pmv[k] = 0.f;
+  if (col < c1) {
+    if (col < a.F) sc = a.inv_std[(int64_t)s * a.F + col];
+    const float* pm = a.pmask + (int64_t)s * D;
+#pragma unroll
+    for (int k = 0; k < KP; ++k)
+      if (k < a.K) pmv[k] = pm[(int64_t)k * Fp1 + col];
+  }
   const bool loss_block = bx == 0;
   if (loss_block && (int)threadIdx.x < a.ntiles) tl[threadIdx.x] = slab[(int64_t)threadIdx.x * SW + SW - 1];
   __syncthreads();
@@ -392,8 +420,12 @@ __device__ __forceinline__ void logreg_grad_body(const LogregGradArgs& a, int bx
       a.loss[bt] = l;
   }
   HAR_LR_STAMP(1)
-  const int s0 = cs_l[0], s1 = cs_l[c1 - c0];
-  const int cs0 = col < c1 ? cs_l[threadIdx.x] : 0, cs1 = col < c1 ? cs_l[threadIdx.x + 1] : 0;
+  if (!fast) {
+    s0 = cs_l[0];
+    s1 = cs_l[c1 - c0];
+    cs0 = col < c1 ? cs_l[threadIdx.x] : 0;
+    cs1 = col < c1 ? cs_l[threadIdx.x + 1] : 0;
+  }
   const float* R = a.R + (int64_t)by * a.N * KP;  // this launch's residual slot of the model
   float g[KP];
 #pragma unroll
@@ -402,27 +434,47 @@ __device__ __forceinline__ void logreg_grad_body(const LogregGradArgs& a, int bx
     if (base > s0) __syncthreads();  // the previous round's partials are consumed
     const int sl = base + threadIdx.x;
     if (sl < s1) {
-      // the slice's column: the last column of the block whose first slice is <= sl
-      int lo = 0, hi = c1 - c0 - 1;
-      while (lo < hi) {
-        const int mid = (lo + hi + 1) >> 1;
-        if (cs_l[mid] <= sl) lo = mid; else hi = mid - 1;
+      int r0, r1;
+      if (fast) {
+        r0 = base == s0 ? r0f : a.srow[sl];
+        r1 = base == s0 ? r1f : a.srow[sl + 1];
+      } else {
+        // the slice's column: the last column of the block whose first slice is <= sl
+        int lo = 0, hi = c1 - c0 - 1;
+        while (lo < hi) {
+          const int mid = (lo + hi + 1) >> 1;
+          if (cs_l[mid] <= sl) lo = mid; else hi = mid - 1;
+        }
+        r0 = a.csc_off[c0 + lo] + (sl - cs_l[lo]) * a.SL;
+        r1 = min(r0 + a.SL, a.csc_off[c0 + lo + 1]);
       }
-      const int r0 = a.csc_off[c0 + lo] + (sl - cs_l[lo]) * a.SL;
-      const int r1 = min(r0 + a.SL, a.csc_off[c0 + lo + 1]);
       float gs[KP];
 #pragma unroll
       for (int k = 0; k < KP; ++k) gs[k] = 0.f;
-#pragma unroll 8  // 8 row indices, then their 8 residual rows in flight: 8 dependent round trips per 32-row slice instead of 16
-      for (int i = r0; i < r1; ++i) {
-        const f32x4_t* rp = reinterpret_cast<const f32x4_t*>(R + (int64_t)a.csc_rows[i] * KP);
+      // groups of RG rows: RG row indices, then their RG residual rows in flight (two dependent round
+      // trips per group, the slice's last partial group included: rows past r1 re-read row r1 - 1 and
+      // add +0, an exact identity since gs is never -0 — the sums are bitwise the row-by-row ones;
+      // a row-at-a-time tail cost two round trips PER ROW, up to 14 for a 7-row tail: grad stamps)
+      constexpr int RG = KP == 8 ? 8 : 4;
+      for (int i0 = r0; i0 < r1; i0 += RG) {
+        int rid[RG];
 #pragma unroll
-        for (int q = 0; q < KP / 4; ++q) {
-          const f32x4_t r4 = rp[q];
-          gs[4 * q + 0] += r4[0];
-          gs[4 * q + 1] += r4[1];
-          gs[4 * q + 2] += r4[2];
-          gs[4 * q + 3] += r4[3];
+        for (int j = 0; j < RG; ++j) rid[j] = a.csc_rows[min(i0 + j, r1 - 1)];
+        f32x4_t rr[RG][KP / 4];
+#pragma unroll
+        for (int j = 0; j < RG; ++j)
+#pragma unroll
+          for (int q = 0; q < KP / 4; ++q) rr[j][q] = reinterpret_cast<const f32x4_t*>(R + (int64_t)rid[j] * KP)[q];
+#pragma unroll
+        for (int j = 0; j < RG; ++j) {
+          const bool on = i0 + j < r1;
+#pragma unroll
+          for (int q = 0; q < KP / 4; ++q) {
+            gs[4 * q + 0] += on ? rr[j][q][0] : 0.f;
+            gs[4 * q + 1] += on ? rr[j][q][1] : 0.f;
+            gs[4 * q + 2] += on ? rr[j][q][2] : 0.f;
+            gs[4 * q + 3] += on ? rr[j][q][3] : 0.f;
+          }
         }
       }
 #pragma unroll
@@ -448,11 +500,10 @@ __device__ __forceinline__ void logreg_grad_body(const LogregGradArgs& a, int bx
     }
   }
   HAR_LR_STAMP(3)
-  const float sc = col < a.F ? a.inv_std[(int64_t)s * a.F + col] : 1.f;
-  const int64_t D = (int64_t)a.K * Fp1;
   float* G = a.G + (int64_t)bt * D;
-  const float* pm = a.pmask + (int64_t)s * D;
-  for (int k = 0; k < a.K; ++k) G[(int64_t)k * Fp1 + col] = g[k] * sc * pm[(int64_t)k * Fp1 + col];
+#pragma unroll
+  for (int k = 0; k < KP; ++k)
+    if (k < a.K) G[(int64_t)k * Fp1 + col] = g[k] * sc * pmv[k];
   HAR_LR_STAMP(4)
 }
 
@@ -1104,7 +1155,7 @@ __global__ __launch_bounds__(QN_BLOCK) void logreg_solve_persistent_kernel(Solve
   const int G = gridDim.x, g0 = blockIdx.x;
   const int nqb = p.q.nch * p.q.B;
   const int tiles = (int)((p.ev1.N + EVAL_ROWS - 1) / EVAL_ROWS);
-  const int cols = (p.gr1.F + 1 + 255) / 256;
+  const int cols = p.gr1.col_blk ? p.gr1.nblk : (p.gr1.F + 1 + 255) / 256;  // (grT: the same design)
   auto qn = [&](int phase, int head, int filled, int init, int fin_it) {
     QnArgs a = p.q;
     a.head = head;
@@ -1192,7 +1243,8 @@ extern "C" int har_logreg_grad(const LogregGradArgs* args, int KP, int n_models,
       a.col_slice == nullptr || a.csc_off == nullptr || (a.loss == nullptr && a.loss_fx == nullptr))
     return -2;
   if (n_models == 0) return 0;
-  dim3 grid((a.F + 1 + 255) / 256, n_models);
+  if (a.col_blk && (a.nblk < 1 || a.srow == nullptr)) return -2;
+  dim3 grid(a.col_blk ? a.nblk : (a.F + 1 + 255) / 256, n_models);
   if (KP == 8)
     if (g_lr_stamps_grd)
       logreg_grad_kernel<8, true><<<grid, 256, 0, s>>>(a, g_lr_stamps_grd);
@@ -1239,7 +1291,7 @@ static bool eval_args_ok(const LogregEvalArgs& a, const LogregGradArgs& g, int K
          (a.C == 0 || a.cat != nullptr) && a.mode == 0 && g.K == a.K && g.T == a.T && g.SL >= 1 &&
          g.col_slice != nullptr && g.csc_off != nullptr && g.loss != nullptr && g.loss_fx == nullptr &&
          g.N == a.N && g.F == a.F && g.Fd == a.Fd && g.tstride == a.tstride && g.model0 == a.model0 &&
-         g.ntiles == (int)((a.N + EVAL_ROWS - 1) / EVAL_ROWS) && n >= 1 && a.N > 0 && (a.C == 0 || a.R != nullptr);
+         g.ntiles == (int)((a.N + EVAL_ROWS - 1) / EVAL_ROWS) && (g.col_blk == nullptr || (g.nblk >= 1 && g.srow != nullptr)) && n >= 1 && a.N > 0 && (a.C == 0 || a.R != nullptr);
 }
 
 // The whole solve as one cooperative launch (logreg_solve_persistent_kernel).  Returns 0 when it ran
@@ -1253,7 +1305,7 @@ extern "C" int har_logreg_solve_persistent(const QnArgs* q, const LogregEvalArgs
   if ((KP != 8 && KP != 16) || a.K > KP || a.m < 1 || a.m > QN_MAX_M || a.T < 1 || a.T > QN_MAX_TRIALS ||
       a.D != (int64_t)a.K * (a.F + 1) || a.D >= (1LL << 31) || a.nch != har_qn_chunks(a.D, a.B) || a.B < 1 ||
       a.done == nullptr || sync == nullptr || max_iter < 0 || !eval_args_ok(*evT, *grT, KP, nT) ||
-      !eval_args_ok(*ev1, *gr1, KP, n1) || evT->N != ev1->N || evT->Fd != ev1->Fd || ev1->F != a.F ||
+      !eval_args_ok(*ev1, *gr1, KP, n1) || grT->col_blk != gr1->col_blk || grT->nblk != gr1->nblk || evT->N != ev1->N || evT->Fd != ev1->Fd || ev1->F != a.F ||
       ev1->K != a.K || n1 != a.B * a.T || nT != a.B || ev1->tstride != 1 || evT->tstride != a.T)
     return -2;
   if (a.m != QN_MAX_M) return -4;
@@ -1282,7 +1334,7 @@ extern "C" int har_logreg_solve_persistent(const QnArgs* q, const LogregEvalArgs
   if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
       hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, QN_BLOCK, lds) != hipSuccess || per_cu < 1)
     return -4;
-  const int tiles = (int)((ev1->N + EVAL_ROWS - 1) / EVAL_ROWS), cols = (a.F + 1 + 255) / 256;
+  const int tiles = (int)((ev1->N + EVAL_ROWS - 1) / EVAL_ROWS), cols = gr1->col_blk ? gr1->nblk : (a.F + 1 + 255) / 256;
   const int64_t want = std::max<int64_t>({(int64_t)a.nch * a.B, (int64_t)tiles * n1, (int64_t)cols * n1});
   if (max_grid < 0 && want > (int64_t)per_cu * cus) return -4;  // one co-resident round required
   int64_t grid = std::min<int64_t>(want, (int64_t)per_cu * cus);
