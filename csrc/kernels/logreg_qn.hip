@@ -72,13 +72,21 @@ __host__ __device__ constexpr int eval_xld(int Fd) { return Fd <= EVAL_XLD_NARRO
 // added in a fixed order: still bitwise reproducible).  Row pitch 36: the chunk zero-padded to a
 // multiple of 4 columns, and the 16 rows x 4 columns of an operand read hit 64 distinct banks.
 constexpr int EVAL_XLD_MF = 36;
+// ... and the narrow designs (<= 10 dense columns, the reference encoding) on the matrix cores too, at
+// row pitch 12 (the chunk padded to 12 columns; 16 rows x 4 columns of a pass-A operand read still hit
+// 64 distinct banks): pass B's 80 scalar 256-long LDS chains (~5.3k cycles, eval stamps) become 16
+// MFMAs per wave.  Opt-in (HAR_LR_EVAL_MFN=1): pass B 4.7k -> 2.5k cycles, but the evaluation only
+// ~1.1k shorter and the 54-model CrossValidator batch ~1% slower (tile pitch 12 + the 4 KB of MFMA
+// partials per workgroup: fewer resident workgroups), profiles/r5/lr_grad_blocks.md
+constexpr int EVAL_XLD_MFN = 12;
+template <int XLD> constexpr bool eval_mf() { return XLD == EVAL_XLD_MF || XLD == EVAL_XLD_MFN; }
 
 template <int KP, int XLD>
 __device__ __forceinline__ void eval_stage_chunk(const LogregEvalArgs& a, const float* W, float* wd, float* xs,
                                                  int c0, int nc, int64_t r0, int64_t nrow_tile, bool weights) {
   const int tid = threadIdx.x;
   // (MF pitch: columns nc .. nc4 - 1 of the chunk staged as zeros, the MFMA k steps are 4 wide)
-  const int ncs = XLD == EVAL_XLD_MF ? (nc + 3) & ~3 : nc;
+  const int ncs = eval_mf<XLD>() ? (nc + 3) & ~3 : nc;
   if (weights)
     for (int e = tid; e < ncs * KP; e += EVAL_ROWS)
       wd[e] = e / KP < nc ? W[(int64_t)a.dense_cols[c0 + e / KP] * KP + (e % KP)] : 0.f;
@@ -121,7 +129,7 @@ __device__ __forceinline__ void logreg_eval_body(const LogregEvalArgs& a, int bx
   float* xs = wd + EVAL_DCH * KP;                  // [EVAL_ROWS][xld] dense row tile, one chunk
   float* rs = xs + EVAL_ROWS * xld;                // [EVAL_ROWS][KP]
   float* red = rs + EVAL_ROWS * KP;                // [EVAL_ROWS / 64]
-  constexpr bool MF = XLD == EVAL_XLD_MF;          // matrix-core dense products
+  constexpr bool MF = eval_mf<XLD>();              // matrix-core dense products
   float* pb = red + EVAL_ROWS / 64;                // MF: [4 waves][EVAL_DCH][KP] gradient partials
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int l16 = lane & 15, kq = lane >> 4;
@@ -677,13 +685,19 @@ __device__ __forceinline__ QnScalars qn_load_scalars(const QnArgs& a, int b) {
                    a.step_scale[b], a.steep[b], a.active[b], a.fails[b], a.iters[b]};
 }
 
+// Run by the first three waves (t = threadIdx.x): thread j < m writes row / column j of the history Gram
+// matrices, thread 64 (wave 1) the curvature test, thread 128 (wave 2) the objective and the flags, so
+// the three parts run side by side instead of as one lane's serial ~35 stores + fp64 square roots and
+// divisions (~5k cycles of the update kernel's last chunk, profiles/r5/lr_kernel_medians.md)
 __device__ __forceinline__ void qn_finalize(const QnArgs& a, int b, int p, double regp, const QnScalars& q,
-                                            const double* v) {
+                                            const double* v, int t) {
   const int mm = a.m;
   if (a.init) {
-    const double F = q.L0 + regp;
-    a.fobj[b] = F;
-    if (a.hist) a.hist[b] = F;
+    if (t == 128) {
+      const double F = q.L0 + regp;
+      a.fobj[b] = F;
+      if (a.hist) a.hist[b] = F;
+    }
     return;
   }
   const int h = a.head;
@@ -691,37 +705,46 @@ __device__ __forceinline__ void qn_finalize(const QnArgs& a, int b, int p, doubl
   if (p >= 0) {  // v: the P3 chunk sums (LDS)
     double* SY = a.SY + (int64_t)b * mm * mm;
     double* YY = a.YY + (int64_t)b * mm * mm;
-    SY[h * mm + h] = v[0];
-    YY[h * mm + h] = v[2];
-    for (int j = 0; j < mm; ++j) {
-      if (j == h) continue;
-      SY[h * mm + j] = v[5 + 3 * j];
-      SY[j * mm + h] = v[6 + 3 * j];
-      YY[h * mm + j] = YY[j * mm + h] = v[7 + 3 * j];
+    if (t < mm) {
+      const int j = t;
+      if (j == h) {
+        SY[h * mm + h] = v[0];
+        YY[h * mm + h] = v[2];
+      } else {
+        SY[h * mm + j] = v[5 + 3 * j];
+        SY[j * mm + h] = v[6 + 3 * j];
+        YY[h * mm + j] = YY[j * mm + h] = v[7 + 3 * j];
+      }
     }
-    const bool good = v[0] > 1e-10 * fmax(sqrt(v[1]) * sqrt(v[2]), 1e-300);
-    a.rho[h * a.B + b] = good ? 1.0 / v[0] : 0.0;
-    const double Fn = trial_loss(q, p) + regp;
-    const double F0 = q.F0;
-    const double rel = fabs(F0 - Fn) / fmax(fmax(fabs(F0), fabs(Fn)), 1.0);
-    a.fobj[b] = Fout = Fn;
-    a.iters[b] = q.iters + 1;
-    a.fails[b] = 0;
-    a.steep[b] = 0;
-    a.step_scale[b] = 1.0f;
-    if (rel < a.tol || sqrt(v[4]) <= a.tol * fmax(sqrt(v[3]), 1.0)) a.active[b] = 0;
-  } else if (p == -2) {  // the recursion produced no descent direction: steepest descent next
-    a.rho[h * a.B + b] = 0.0;
-    a.steep[b] = 1;
-  } else {
-    a.rho[h * a.B + b] = 0.0;
-    if (q.active) {
-      a.step_scale[b] = q.step_scale * (1.0f / 16.0f);
-      a.fails[b] = q.fails + 1;
-      if (q.fails + 1 >= 2) a.active[b] = 0;
+    if (t == 64) {
+      const bool good = v[0] > 1e-10 * fmax(sqrt(v[1]) * sqrt(v[2]), 1e-300);
+      a.rho[h * a.B + b] = good ? 1.0 / v[0] : 0.0;
+    }
+    if (t == 128) {
+      const double Fn = trial_loss(q, p) + regp;
+      const double F0 = q.F0;
+      const double rel = fabs(F0 - Fn) / fmax(fmax(fabs(F0), fabs(Fn)), 1.0);
+      a.fobj[b] = Fout = Fn;
+      a.iters[b] = q.iters + 1;
+      a.fails[b] = 0;
+      a.steep[b] = 0;
+      a.step_scale[b] = 1.0f;
+      if (rel < a.tol || sqrt(v[4]) <= a.tol * fmax(sqrt(v[3]), 1.0)) a.active[b] = 0;
+    }
+  } else if (t == 128) {
+    if (p == -2) {  // the recursion produced no descent direction: steepest descent next
+      a.rho[h * a.B + b] = 0.0;
+      a.steep[b] = 1;
+    } else {
+      a.rho[h * a.B + b] = 0.0;
+      if (q.active) {
+        a.step_scale[b] = q.step_scale * (1.0f / 16.0f);
+        a.fails[b] = q.fails + 1;
+        if (q.fails + 1 >= 2) a.active[b] = 0;
+      }
     }
   }
-  if (a.hist) a.hist[(int64_t)a.fin_it * a.B + b] = Fout;
+  if (t == 128 && a.hist) a.hist[(int64_t)a.fin_it * a.B + b] = Fout;
 }
 
 // One parameter element's operands for phase 1 (x, g, L1 / L2 weights, the W_eff scale and the
@@ -1091,9 +1114,9 @@ __device__ __forceinline__ void qn_update_body(const QnArgs& a, int c, int b, ui
   if (!a.init && p >= 0) reduce_chunks_shared<NP3, true>(a.P3 + (int64_t)b * a.nch * NP3, a.nch, fin_v, stage);
   __syncthreads();
   HAR_LR_STAMP(6)
-  if (threadIdx.x == 0) {
-    qn_finalize(a, b, p, p >= 0 ? p2v[3 * p] + p2v[3 * p + 1] : 0.0, qs, fin_v);
-    __hip_atomic_store(a.done + b, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (threadIdx.x <= 128) {
+    qn_finalize(a, b, p, p >= 0 ? p2v[3 * p] + p2v[3 * p + 1] : 0.0, qs, fin_v, threadIdx.x);
+    if (threadIdx.x == 0) __hip_atomic_store(a.done + b, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   HAR_LR_STAMP(7)
 }
@@ -1210,13 +1233,24 @@ extern "C" int har_logreg_eval(const LogregEvalArgs* args, int KP, int n_models,
     const char* e = std::getenv("HAR_LR_EVAL_MFMA");
     return !e || std::atoi(e) != 0;
   }();
+  static const bool mfn_on = [] {
+    const char* e = std::getenv("HAR_LR_EVAL_MFN");
+    return e && std::atoi(e) != 0;
+  }();
   const bool narrow = eval_xld(a.Fd) == EVAL_XLD_NARROW;
-  const bool mf = mf_on && !narrow;
-  const int xld = mf ? EVAL_XLD_MF : eval_xld(a.Fd);
+  const bool mf = mf_on && (!narrow || mfn_on);
+  const int xld = mf ? (narrow ? EVAL_XLD_MFN : EVAL_XLD_MF) : eval_xld(a.Fd);
   const size_t lds = sizeof(float) * (EVAL_DCH * KP + EVAL_ROWS * xld + EVAL_ROWS * KP + EVAL_ROWS / 64 +
                                       (mf ? 4 * EVAL_DCH * KP : 0));
   dim3 grid(tiles, n_models);
-  if (mf && KP == 8)
+  if (mf && narrow && KP == 8)
+    if (g_lr_stamps)
+      logreg_eval_kernel<8, EVAL_XLD_MFN, true><<<grid, EVAL_ROWS, lds, s>>>(a, g_lr_stamps);
+    else
+      logreg_eval_kernel<8, EVAL_XLD_MFN><<<grid, EVAL_ROWS, lds, s>>>(a, nullptr);
+  else if (mf && narrow)
+    logreg_eval_kernel<16, EVAL_XLD_MFN><<<grid, EVAL_ROWS, lds, s>>>(a, nullptr);
+  else if (mf && KP == 8)
     logreg_eval_kernel<8, EVAL_XLD_MF><<<grid, EVAL_ROWS, lds, s>>>(a, nullptr);
   else if (mf)
     logreg_eval_kernel<16, EVAL_XLD_MF><<<grid, EVAL_ROWS, lds, s>>>(a, nullptr);
@@ -1315,18 +1349,24 @@ extern "C" int har_logreg_solve_persistent(const QnArgs* q, const LogregEvalArgs
     const char* e = std::getenv("HAR_LR_EVAL_MFMA");
     return !e || std::atoi(e) != 0;
   }();
+  static const bool mfn_on = [] {
+    const char* e = std::getenv("HAR_LR_EVAL_MFN");
+    return e && std::atoi(e) != 0;
+  }();
   const bool narrow = eval_xld(ev1->Fd) == EVAL_XLD_NARROW;
-  const bool mf = mf_on && !narrow;
-  const int xld = mf ? EVAL_XLD_MF : eval_xld(ev1->Fd);
+  const bool mf = mf_on && (!narrow || mfn_on);
+  const int xld = mf ? (narrow ? EVAL_XLD_MFN : EVAL_XLD_MF) : eval_xld(ev1->Fd);
   const size_t lds = sizeof(float) * (EVAL_DCH * KP + EVAL_ROWS * xld + EVAL_ROWS * KP + EVAL_ROWS / 64 +
                                       (mf ? 4 * EVAL_DCH * KP : 0));
   const void* fn;
   if (KP == 8)
-    fn = mf ? (const void*)logreg_solve_persistent_kernel<8, EVAL_XLD_MF, true>
+    fn = mf && narrow ? (const void*)logreg_solve_persistent_kernel<8, EVAL_XLD_MFN, true>
+       : mf ? (const void*)logreg_solve_persistent_kernel<8, EVAL_XLD_MF, true>
             : narrow ? (const void*)logreg_solve_persistent_kernel<8, EVAL_XLD_NARROW, true>
                      : (const void*)logreg_solve_persistent_kernel<8, EVAL_DCH + 1, true>;
   else
-    fn = mf ? (const void*)logreg_solve_persistent_kernel<16, EVAL_XLD_MF, true>
+    fn = mf && narrow ? (const void*)logreg_solve_persistent_kernel<16, EVAL_XLD_MFN, true>
+       : mf ? (const void*)logreg_solve_persistent_kernel<16, EVAL_XLD_MF, true>
             : narrow ? (const void*)logreg_solve_persistent_kernel<16, EVAL_XLD_NARROW, true>
                      : (const void*)logreg_solve_persistent_kernel<16, EVAL_DCH + 1, true>;
   // grid: every phase's virtual blocks once if they fit co-resident, else as many as are

@@ -17,7 +17,7 @@ for v in "${VS[@]}"; do
       --out "$OUT/bench_$i.json" > "$OUT/bench_$i.log" 2>&1 || exit $?
   python -c "import json;d=json.load(open('$OUT/bench_$i.json'))['reference_suite']['models'];print('$v', {k:(round(v['fit_s']*1e3,3),round(v['accuracy'],4)) for k,v in d.items() if k in ('lr','lrcv','LR','LR-CV') or 'lr' in k.lower()})"
   env $v timeout -k 10 200 python tools/lr_stamps.py --model lr > "$OUT/stamps_$i.txt" 2>&1 || exit $?
-  grep -A6 -- "--- grad" "$OUT/stamps_$i.txt" || true
+  grep -E -- "^---|entry -> last|finalize|pass B|one-hot slices|element sweep" "$OUT/stamps_$i.txt" || true
   i=$((i+1))
 done
 echo done
