@@ -30,7 +30,7 @@ import torch
 
 from . import _native
 
-SLICE_ROWS = int(os.environ.get("HAR_LR_SL", "32"))  # rows per CSC slice of the gradient / summary kernels
+SLICE_ROWS = int(os.environ.get("HAR_LR_SL", "16"))  # rows per CSC slice of the gradient / summary kernels (16: profiles/r5/lr_grad_blocks.md)
 
 
 def logreg_loss_grad_torch(X, y, W, b, rw, inv_wsum):

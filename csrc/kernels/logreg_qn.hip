@@ -628,6 +628,35 @@ __device__ __forceinline__ void block_sum_f(const float (&p)[NV], double* sh, do
   __syncthreads();
 }
 
+// block_sum_f with the totals handed to out(q, total) by thread q < NV (all in wave 0 for NV <= 64: the
+// caller's stores then need no barrier before wave 0 publishes them) instead of a shared array + barrier
+template <int NV, typename Out>
+__device__ __forceinline__ void block_sum_out(const float (&p)[NV], double* sh, Out&& out) {
+  static_assert(QN_BLOCK == 256 && 4 * NV <= QN_BLOCK && NV <= 64, "four 64-thread segments; totals in wave 0");
+  constexpr int TP = QN_BLOCK + 4;
+  __shared__ __attribute__((aligned(16))) float tr[NV * TP];
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int q = 0; q < NV; ++q) tr[q * TP + t] = p[q];
+  __syncthreads();
+  if (t < 4 * NV) {
+    const int q = t >> 2, w = t & 3;
+    const float4* r = reinterpret_cast<const float4*>(tr + q * TP + 64 * w);
+    double c0 = 0.0, c1 = 0.0, c2 = 0.0, c3 = 0.0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const float4 v = r[i];
+      c0 += (double)v.x;
+      c1 += (double)v.y;
+      c2 += (double)v.z;
+      c3 += (double)v.w;
+    }
+    sh[q * 4 + w] = (c0 + c1) + (c2 + c3);
+  }
+  __syncthreads();
+  if (t < NV) out(t, (sh[t * 4] + sh[t * 4 + 1]) + (sh[t * 4 + 2] + sh[t * 4 + 3]));
+}
+
 // Chunk sums in chunk order (fixed: bitwise reproducible) into the shared vs[NV]: every lane of the
 // block loads part of the nch x NV partials into LDS (ONE round of independent loads, not a chain of
 // nch / 8 dependent rounds per lane), then one lane per value q adds them in chunk order.  AGENT:
@@ -975,11 +1004,10 @@ __global__ __launch_bounds__(QN_BLOCK) void qn_direction_kernel(QnArgs a, uint64
 template <bool FULLM, bool WIDE, bool STAMP = false>
 __device__ __forceinline__ void qn_update_body(const QnArgs& a, int c, int b, uint64_t* st = nullptr) {
   HAR_LR_STAMP(0)
-  __shared__ double sh[4 * NP3];
+  __shared__ double sh[4 * (NP3 + 2 * QN_MAX_M)];
   __shared__ double p2v[NP2];
   __shared__ double fin_v[NP3];
   __shared__ double stage[QN_MAX_CHUNKS * NP3];
-  __shared__ double tot3[NP3], tot1[NP1];
   __shared__ int pick, last;
   const int D = (int)a.D;
   const int mm = a.m;
@@ -1081,21 +1109,20 @@ __device__ __forceinline__ void qn_update_body(const QnArgs& a, int c, int b, ui
       g[e] = gn;
     }
     HAR_LR_STAMP(3)
-    block_sum_f<NP3, WIDE>(ps, sh, tot3);
-    float pd1[NP1];
+    // the P3 and P1 partials in ONE block sum (one LDS transpose and barrier pair), each total stored
+    // by its own wave-0 thread (P3: agent-scope, read by the model's last chunk in this launch)
+    float pc[NP3 + 2 * QN_MAX_M];
 #pragma unroll
-    for (int q = 0; q < 2 * QN_MAX_M; ++q) pd1[q] = pd[q];
-    pd1[2 * QN_MAX_M] = 0.f;
-    block_sum_f<NP1, WIDE>(pd1, sh, tot1);
-    if (threadIdx.x == 0) {
-      double* P3 = a.P3 + ((int64_t)b * a.nch + c) * NP3;
-      double* P1 = a.P1 + ((int64_t)b * a.nch + c) * NP1;
+    for (int q = 0; q < NP3; ++q) pc[q] = ps[q];
 #pragma unroll
-      for (int q = 0; q < NP3; ++q) __hip_atomic_store(P3 + q, tot3[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#pragma unroll
-      for (int q = 0; q < 2 * QN_MAX_M; ++q) P1[q] = tot1[q];
-      P1[2 * QN_MAX_M] = tot3[4];  // pg.pg
-    }
+    for (int q = 0; q < 2 * QN_MAX_M; ++q) pc[NP3 + q] = pd[q];
+    double* P3 = a.P3 + ((int64_t)b * a.nch + c) * NP3;
+    double* P1 = a.P1 + ((int64_t)b * a.nch + c) * NP1;
+    block_sum_out<NP3 + 2 * QN_MAX_M>(pc, sh, [&](int q, double v) {
+      if (q < NP3) __hip_atomic_store(P3 + q, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      else P1[q - NP3] = v;
+      if (q == 4) P1[2 * QN_MAX_M] = v;  // pg.pg
+    });
   }
   // the last chunk of model b to get here finalizes the model.  Memory model: lane 0 publishes the
   // chunk's P3 / P1 partials with an agent-scope RELEASE fence before counting it (the stores are
