@@ -628,6 +628,31 @@ __device__ __forceinline__ void block_sum_f(const float (&p)[NV], double* sh, do
   __syncthreads();
 }
 
+// reduce_chunks_shared of two partial slabs at once (agent-scope loads, one round, one barrier): threads
+// q < NA sum slab A into va, threads 64 + q (q < NB) slab B into vb, side by side in chunk order
+template <int NA, int NB>
+__device__ __forceinline__ void reduce_chunks2_shared(const double* PA, const double* PB, int nch, double* va,
+                                                      double* vb, double* stage) {
+  static_assert(NA <= 64 && NB <= 64, "one wave per slab");
+  for (int i = threadIdx.x; i < nch * (NA + NB); i += QN_BLOCK)
+    stage[i] = i < nch * NA ? __hip_atomic_load(PA + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                            : __hip_atomic_load(PB + (i - nch * NA), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  const int t = threadIdx.x;
+  if (t < NA) {
+    double acc = 0.0;
+#pragma unroll 8
+    for (int c = 0; c < nch; ++c) acc += stage[c * NA + t];
+    va[t] = acc;
+  } else if (t >= 64 && t < 64 + NB) {
+    const double* sb = stage + nch * NA;
+    double acc = 0.0;
+#pragma unroll 8
+    for (int c = 0; c < nch; ++c) acc += sb[c * NB + (t - 64)];
+    vb[t - 64] = acc;
+  }
+}
+
 // block_sum_f with the totals handed to out(q, total) by thread q < NV (all in wave 0 for NV <= 64: the
 // caller's stores then need no barrier before wave 0 publishes them) instead of a shared array + barrier
 template <int NV, typename Out>
@@ -822,7 +847,6 @@ __device__ __forceinline__ void qn_direction_body(const QnArgs& a, int c, int b,
   // the recursion's operands live in LDS: the P1 chunk sums (reduced by NP1 lanes), the Gram
   // matrices, rho and the coefficient vectors (per-lane arrays indexed by slot would spill to scratch)
   __shared__ double p1v[NP1], SY[QN_MAX_M * QN_MAX_M], YY[QN_MAX_M * QN_MAX_M], rho_s[QN_MAX_M];
-  __shared__ double stage[QN_MAX_CHUNKS * NP1];
   const bool rec = !a.init && !steep;  // block-uniform
   const int csz = (D + a.nch - 1) / a.nch, e1 = min(D, (c + 1) * csz);
   const int e0 = c * csz + threadIdx.x;
@@ -837,7 +861,7 @@ __device__ __forceinline__ void qn_direction_body(const QnArgs& a, int c, int b,
       yyv = a.YY[(int64_t)b * mm * mm + i];
     }
     if (i < mm) rhv = a.rho[i * a.B + b];
-    reduce_chunks_shared<NP1>(a.P1 + (int64_t)b * a.nch * NP1, a.nch, p1v, stage);
+    if (i < NP1) p1v[i] = a.P1[(int64_t)b * a.nch * NP1 + i];  // the totals (the last update's last chunk)
     // every entry of the [QN_MAX_M]^2 images written (zeros past m^2): the recursion below reads whole
     // rows / columns unconditionally, its products with the zero coefficients of unused slots exact
     if (i < QN_MAX_M * QN_MAX_M) {
@@ -849,77 +873,78 @@ __device__ __forceinline__ void qn_direction_body(const QnArgs& a, int c, int b,
   }
   HAR_LR_STAMP(1)
   if (threadIdx.x < 64) {
-    // the two-loop recursion on coefficients, spread over the 16 lanes of each DPP row of wave 0: lane k
-    // holds u_k, w_k, al_k (slot k < m; zero above), each step's 10-term dot product is a lane product
-    // plus a row sum by DPP rotations (fp64), the slot update a select on lane == j.  (Thread 0 alone,
-    // serial fp64 chains with a register select per slot, took ~17k cycles, profiles/r5/lr_stamps.md.)
-    // The same fixed order on every run; the sums' order differs from the serial form in the last bits.
-    const int k = threadIdx.x & 15;
+    // the two-loop recursion on coefficients, lane L of each 16-lane row of wave 0 owning STEP L (slot
+    // j_L = head - 1 - L mod m): both loops are triangular recurrences, so each lane keeps the running dot
+    // product of its own step — step i's coefficient is computed on lane i, broadcast by readlane, and
+    // every lane adds its product with its Gram element (one fp64 fma).  A step is then readlane + fma +
+    // the next lane's update instead of a 10-term product and a 4-stage fp64 DPP row sum (recursion
+    // 6.9k -> see profiles/r5/lr_grad_blocks.md).  The loop-2 products with the final q (y_j . q for
+    // every j) do not depend on loop 2 and run as independent per-lane dots.  Fixed order on every run.
+    const int L = threadIdx.x & 15;
     if (threadIdx.x < QN_MAX_M) cS[threadIdx.x] = cY[threadIdx.x] = 0.f;
     float gamma = 0.f;
     if (rec) {
-      auto row_sum = [](double v) {
-        v += wops::dpp_d<wops::DPP_ROR8>(v);
-        v += wops::dpp_d<wops::DPP_ROR4>(v);
-        v += wops::dpp_d<wops::DPP_ROR2>(v);
-        return v + wops::dpp_d<wops::DPP_ROR1>(v);
+      auto readlane_d = [](double v, int lane) {
+        const uint64_t u = __builtin_bit_cast(uint64_t, v);
+        return __builtin_bit_cast(double, ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(u >> 32), lane) << 32) |
+                                              (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)u, lane));
       };
-      const bool kin = k < mm;
-      // every Gram element a lane needs, read before the dependent steps (step i uses slot j_i)
-      // (and the slot index j_i = head - 1 - i mod m by a conditional add: an integer modulo by the
-      // runtime m is a ~40-instruction division per step)
-      double sy1[QN_MAX_M], yy2[QN_MAX_M], sy2[QN_MAX_M], rh[QN_MAX_M], pa[QN_MAX_M], pb[QN_MAX_M];
-      int js[QN_MAX_M];
-#pragma unroll
-      for (int i = 0; i < QN_MAX_M; ++i) {
+      // slot index j_i = head - 1 - i mod m by a conditional add (an integer modulo by the runtime m is a
+      // ~40-instruction division); steps i >= filled may run below slot 0: any slot, unused
+      auto slot = [&](int i) {
         int j = a.head - 1 - i;
         j = j < 0 ? j + mm : j;
-        j = j < 0 ? 0 : j;  // (i >= filled may run below slot 0: any slot, unused)
-        js[i] = j;
-        sy1[i] = kin ? SY[j * mm + k] : 0.0;
-        yy2[i] = kin ? YY[j * mm + k] : 0.0;
-        sy2[i] = kin ? SY[k * mm + j] : 0.0;
-        rh[i] = rho_s[j];
-        pa[i] = p1v[j];
-        pb[i] = p1v[QN_MAX_M + j];
-      }
-      double ur = 0.0, wr = 0.0, al = 0.0;
+        return j < 0 ? 0 : j;
+      };
+      const int jL = slot(L);
+      // every Gram element this lane's step needs, read before the dependent steps
+      double m1[QN_MAX_M], m2[QN_MAX_M], m3[QN_MAX_M];
 #pragma unroll
-      for (int i = 0; i < QN_MAX_M; ++i) {  // newest -> oldest: q = pg + sum u_k y_k
+      for (int i = 0; i < QN_MAX_M; ++i) {
+        const int ji = slot(i);
+        m1[i] = SY[jL * mm + ji];  // s_jL . y_ji
+        m2[i] = YY[jL * mm + ji];  // y_jL . y_ji
+        m3[i] = SY[ji * mm + jL];  // s_ji . y_jL
+      }
+      const double paL = p1v[jL], pbL = p1v[QN_MAX_M + jL], rhL = rho_s[jL];
+      // loop 1, newest -> oldest: al_i = rho_i s_i . q, q = pg - sum al_l y_l (a rejected pair: rho = 0, al 0)
+      double acc = 0.0, alL = 0.0, als[QN_MAX_M];
+#pragma unroll
+      for (int i = 0; i < QN_MAX_M; ++i) {
+        als[i] = 0.0;
         if (i < a.filled) {
-          const int j = js[i];
-          const double rho = rh[i];
-          const double sq = pa[i] + row_sum(ur * sy1[i]);
-          const double alj = rho == 0.0 ? 0.0 : rho * sq;  // (a rejected pair: rho = 0, u / al unchanged)
-          al = k == j ? alj : al;
-          ur = k == j ? ur - alj : ur;
+          const double ali = readlane_d(rhL == 0.0 ? 0.0 : rhL * (paL + acc), i);
+          als[i] = ali;
+          alL = L == i ? ali : alL;
+          acc = fma(-ali, m1[i], acc);
         }
       }
       double gm;
       if (a.filled == 0) {
         gm = 1.0 / fmax(sqrt(p1v[2 * QN_MAX_M]), 1e-12);
       } else {
-        const int n = js[0];
+        const int n = slot(0);
         const double yy = YY[n * mm + n];
         gm = (rho_s[n] > 0.0 && yy > 0.0) ? SY[n * mm + n] / yy : 1.0;
       }
+      // y_jL . q with the final q
+      double yq = pbL;
 #pragma unroll
-      for (int i = QN_MAX_M - 1; i >= 0; --i) {  // oldest -> newest: r = gamma q + sum w_k s_k
-        if (i >= a.filled) continue;
-        const int j = js[i];
-        const double rho = rh[i];
-        double yr = pb[i] + row_sum(ur * yy2[i]);
-        yr *= gm;
-        yr += row_sum(wr * sy2[i]);
-        const uint64_t alb = __builtin_bit_cast(uint64_t, al);  // al_j from lane j of the row
-        const double alj = __builtin_bit_cast(double, ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(alb >> 32), j) << 32) |
-                                                          (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)alb, j));
-        const double dw = rho == 0.0 ? 0.0 : alj - rho * yr;  // (rho = 0: the skipped step, w unchanged)
-        wr = k == j ? wr + dw : wr;
+      for (int l = 0; l < QN_MAX_M; ++l)
+        if (l < a.filled) yq = fma(-als[l], m2[l], yq);
+      // loop 2, oldest -> newest: w_i = al_i - rho_i y_i . r, r = gm q + sum w_l s_l
+      double acc2 = 0.0, wL = 0.0;
+#pragma unroll
+      for (int i = QN_MAX_M - 1; i >= 0; --i) {
+        if (i < a.filled) {
+          const double wi = readlane_d(rhL == 0.0 ? 0.0 : als[i] - rhL * fma(gm, yq, acc2), i);
+          wL = L == i ? wi : wL;
+          acc2 = fma(wi, m3[i], acc2);
+        }
       }
-      if (threadIdx.x < mm) {
-        cY[threadIdx.x] = (float)(gm * ur);
-        cS[threadIdx.x] = (float)wr;
+      if (threadIdx.x < 16 && L < a.filled) {
+        cY[jL] = (float)(gm * -alL);
+        cS[jL] = (float)wL;
       }
       gamma = (float)gm;
     }
@@ -1006,8 +1031,8 @@ __device__ __forceinline__ void qn_update_body(const QnArgs& a, int c, int b, ui
   HAR_LR_STAMP(0)
   __shared__ double sh[4 * (NP3 + 2 * QN_MAX_M)];
   __shared__ double p2v[NP2];
-  __shared__ double fin_v[NP3];
-  __shared__ double stage[QN_MAX_CHUNKS * NP3];
+  __shared__ double fin_v[NP3], p1t[NP1];
+  __shared__ double stage[QN_MAX_CHUNKS * (NP3 + NP1)];
   __shared__ int pick, last;
   const int D = (int)a.D;
   const int mm = a.m;
@@ -1119,9 +1144,10 @@ __device__ __forceinline__ void qn_update_body(const QnArgs& a, int c, int b, ui
     double* P3 = a.P3 + ((int64_t)b * a.nch + c) * NP3;
     double* P1 = a.P1 + ((int64_t)b * a.nch + c) * NP1;
     block_sum_out<NP3 + 2 * QN_MAX_M>(pc, sh, [&](int q, double v) {
+      // (P1 too is reduced by the model's last chunk in this launch: agent-scope as well)
       if (q < NP3) __hip_atomic_store(P3 + q, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      else P1[q - NP3] = v;
-      if (q == 4) P1[2 * QN_MAX_M] = v;  // pg.pg
+      else __hip_atomic_store(P1 + (q - NP3), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (q == 4) __hip_atomic_store(P1 + 2 * QN_MAX_M, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // pg.pg
     });
   }
   // the last chunk of model b to get here finalizes the model.  Memory model: lane 0 publishes the
@@ -1138,7 +1164,19 @@ __device__ __forceinline__ void qn_update_body(const QnArgs& a, int c, int b, ui
   __syncthreads();
   HAR_LR_STAMP(5)
   if (!last) return;
-  if (!a.init && p >= 0) reduce_chunks_shared<NP3, true>(a.P3 + (int64_t)b * a.nch * NP3, a.nch, fin_v, stage);
+  // the P3 sums (finalize) and the next direction's P1 sums, side by side; the P1 totals replace chunk
+  // 0's partials (P1[b][0]), which the direction kernel then reads as they are — one load round instead
+  // of every direction workgroup reducing the nch partials again (a rejected step writes no partials:
+  // the totals of the last accepted one stay, as the history does)
+  if (p >= 0) {
+    double* P1b = a.P1 + (int64_t)b * a.nch * NP1;
+    if (!a.init)
+      reduce_chunks2_shared<NP3, NP1>(a.P3 + (int64_t)b * a.nch * NP3, P1b, a.nch, fin_v, p1t, stage);
+    else
+      reduce_chunks2_shared<0, NP1>(nullptr, P1b, a.nch, fin_v, p1t, stage);
+    __syncthreads();
+    if (threadIdx.x < NP1) P1b[threadIdx.x] = p1t[threadIdx.x];
+  }
   __syncthreads();
   HAR_LR_STAMP(6)
   if (threadIdx.x <= 128) {
