@@ -850,20 +850,29 @@ __device__ __forceinline__ void qn_direction_body(const QnArgs& a, int c, int b,
   const bool rec = !a.init && !steep;  // block-uniform
   const int csz = (D + a.nch - 1) / a.nch, e1 = min(D, (c + 1) * csz);
   const int e0 = c * csz + threadIdx.x;
-  DirElem cur = dir_load(a, b, min(e0, D - 1));  // in flight during the prologue + recursion
+  // each thread's first three elements in flight during the prologue + recursion (a refill three ahead),
+  // issued AFTER the recursion's operand loads (Gram, rho, P1 totals): a counted wait for those then
+  // does not also wait for the 75 element loads behind them
+  auto dclamp = [&](int e) { return max(min(e, e1 - 1), 0); };
+  const int i = threadIdx.x;
+  double syv = 0.0, yyv = 0.0, rhv = 0.0, p1x = 0.0;
   if (rec) {
-    // the Gram matrices and rho (one element per lane: m^2 <= 100 < QN_BLOCK) are loaded to
-    // registers first, so their round trip overlaps the P1 partials'
-    const int i = threadIdx.x;
-    double syv = 0.0, yyv = 0.0, rhv = 0.0;
+    // the Gram matrices and rho (one element per lane: m^2 <= 100 < QN_BLOCK)
     if (i < mm * mm) {
       syv = a.SY[(int64_t)b * mm * mm + i];
       yyv = a.YY[(int64_t)b * mm * mm + i];
     }
     if (i < mm) rhv = a.rho[i * a.B + b];
-    if (i < NP1) p1v[i] = a.P1[(int64_t)b * a.nch * NP1 + i];  // the totals (the last update's last chunk)
+    if (i < NP1) p1x = a.P1[(int64_t)b * a.nch * NP1 + i];  // the totals (the last update's last chunk)
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  DirElem d0 = dir_load(a, b, dclamp(e0)), d1 = dir_load(a, b, dclamp(e0 + QN_BLOCK)),
+          d2 = dir_load(a, b, dclamp(e0 + 2 * QN_BLOCK));
+  __builtin_amdgcn_sched_barrier(0);
+  if (rec) {
     // every entry of the [QN_MAX_M]^2 images written (zeros past m^2): the recursion below reads whole
     // rows / columns unconditionally, its products with the zero coefficients of unused slots exact
+    if (i < NP1) p1v[i] = p1x;
     if (i < QN_MAX_M * QN_MAX_M) {
       SY[i] = syv;
       YY[i] = yyv;
@@ -962,8 +971,7 @@ __device__ __forceinline__ void qn_direction_body(const QnArgs& a, int c, int b,
   float r[NP2];
 #pragma unroll
   for (int t = 0; t < NP2; ++t) r[t] = 0.f;
-  for (int e = e0; e < e1; e += QN_BLOCK) {
-    const DirElem nxt = dir_load(a, b, min(e + QN_BLOCK, e1 - 1));  // next element, in flight
+  auto proc = [&](const DirElem& cur, int e) __attribute__((always_inline)) {
     const float xe = cur.x;
     const float l1e = cur.l1;
     const float pg = a.init ? 0.f : pseudo_grad(xe, cur.g, l1e);
@@ -1006,7 +1014,18 @@ __device__ __forceinline__ void qn_direction_body(const QnArgs& a, int c, int b,
         a.weff[((int64_t)bt * Fp1 + col) * KP + k] = xn * wsc;
       }
     }
-    cur = nxt;
+  };
+  for (int e = e0; e < e1; e += 3 * QN_BLOCK) {
+    proc(d0, e);
+    if (e + 3 * QN_BLOCK < e1) d0 = dir_load(a, b, e + 3 * QN_BLOCK);
+    if (e + QN_BLOCK < e1) {
+      proc(d1, e + QN_BLOCK);
+      if (e + 4 * QN_BLOCK < e1) d1 = dir_load(a, b, e + 4 * QN_BLOCK);
+    }
+    if (e + 2 * QN_BLOCK < e1) {
+      proc(d2, e + 2 * QN_BLOCK);
+      if (e + 5 * QN_BLOCK < e1) d2 = dir_load(a, b, e + 5 * QN_BLOCK);
+    }
   }
   HAR_LR_STAMP(3)
   __shared__ double tot2[NP2];
@@ -1025,6 +1044,38 @@ __global__ __launch_bounds__(QN_BLOCK) void qn_direction_kernel(QnArgs a, uint64
   qn_direction_body<KP, FULLM, STAMP>(a, blockIdx.x, blockIdx.y, st);
 }
 
+// One parameter element's phase-2 operands that do not depend on the picked trial (x, g, L1 / L2
+// weights, the history values), loaded at a clamped (valid) index: the first three elements of every
+// thread go out at the start of the launch, under the P2 reduction and the pick, and a refill three
+// elements ahead while the current ones are processed (the history stores of an element may alias the
+// next element's loads for the compiler, so a plain loop waited out one round trip per element)
+struct UpdElem {
+  float x, g, l2, l1;
+  float s[QN_MAX_M], y[QN_MAX_M];
+};
+
+template <bool FULLM>
+__device__ __forceinline__ UpdElem upd_load(const QnArgs& a, int b, int e) {
+  const int64_t D = a.D, sstride = (int64_t)a.B * D, o = (int64_t)b * D + e;
+  UpdElem v;
+  v.x = a.x[o];
+  v.g = a.g[o];
+  v.l2 = a.l2[o];
+  v.l1 = a.l1 ? a.l1[o] : 0.f;
+#pragma unroll
+  for (int j = 0; j < QN_MAX_M; ++j) {
+    v.s[j] = v.y[j] = 0.f;
+    // FULLM also loads slot `head` (its OLD pair) and accumulates its P3 sums, which finalize never reads;
+    // unfilled slots re-read slot 0 (cached lines; their dots are never read)
+    if (!a.init && (FULLM || (j < a.m && j != a.head))) {
+      const int jl = j < a.filled ? j : 0;
+      v.s[j] = a.S[jl * sstride + o];
+      v.y[j] = a.Y[jl * sstride + o];
+    }
+  }
+  return v;
+}
+
 // phase 2
 template <bool FULLM, bool WIDE, bool STAMP = false>
 __device__ __forceinline__ void qn_update_body(const QnArgs& a, int c, int b, uint64_t* st = nullptr) {
@@ -1037,7 +1088,28 @@ __device__ __forceinline__ void qn_update_body(const QnArgs& a, int c, int b, ui
   const int D = (int)a.D;
   const int mm = a.m;
   const QnScalars qs = qn_load_scalars(a, b);  // uniform (scalar) loads, in flight with the P2 partials
-  reduce_chunks_shared<NP2>(a.P2 + (int64_t)b * a.nch * NP2, a.nch, p2v, stage);
+  const int csz = (D + a.nch - 1) / a.nch, e1 = min(D, (c + 1) * csz), eb = c * csz + (int)threadIdx.x;
+  auto eclamp = [&](int e) { return max(min(e, e1 - 1), 0); };
+  // the P2 partials (reduce_chunks_shared, its loads split out) BEFORE the element prefetch, so the
+  // counted wait for them does not also wait for the element loads
+  static_assert(QN_MAX_CHUNKS * NP2 <= 2 * QN_BLOCK, "two P2 partials per thread at most");
+  const double* P2b = a.P2 + (int64_t)b * a.nch * NP2;
+  const int n2 = a.nch * NP2, t2 = (int)threadIdx.x;
+  const double p2a = t2 < n2 ? P2b[t2] : 0.0, p2b = t2 + QN_BLOCK < n2 ? P2b[t2 + QN_BLOCK] : 0.0;
+  __builtin_amdgcn_sched_barrier(0);
+  UpdElem u0 = upd_load<FULLM>(a, b, eclamp(eb));
+  UpdElem u1 = upd_load<FULLM>(a, b, eclamp(eb + QN_BLOCK));
+  UpdElem u2 = upd_load<FULLM>(a, b, eclamp(eb + 2 * QN_BLOCK));
+  __builtin_amdgcn_sched_barrier(0);
+  if (t2 < n2) stage[t2] = p2a;
+  if (t2 + QN_BLOCK < n2) stage[t2 + QN_BLOCK] = p2b;
+  __syncthreads();
+  if (t2 < NP2) {
+    double acc = 0.0;
+#pragma unroll 8
+    for (int cc = 0; cc < a.nch; ++cc) acc += stage[cc * NP2 + t2];  // chunk order
+    p2v[t2] = acc;
+  }
   __syncthreads();
   HAR_LR_STAMP(1)
   if (threadIdx.x == 0) {
@@ -1078,29 +1150,22 @@ __device__ __forceinline__ void qn_update_body(const QnArgs& a, int c, int b, ui
     const int64_t sstride = (int64_t)a.B * D;
     float* __restrict__ x = a.x + (int64_t)b * D;
     float* __restrict__ g = a.g + (int64_t)b * D;
-    const float* __restrict__ l1v = a.l1 ? a.l1 + (int64_t)b * D : nullptr;
-    float* Sh = a.S + (int64_t)a.head * sstride + (int64_t)b * D;  // aliases slot `head` of Sb / Yb
+    float* Sh = a.S + (int64_t)a.head * sstride + (int64_t)b * D;  // aliases slot `head` of the history
     float* Yh = a.Y + (int64_t)a.head * sstride + (int64_t)b * D;
-    const float* Sb = a.S + (int64_t)b * D;
-    const float* Yb = a.Y + (int64_t)b * D;
     const int bt = b * a.T + p;
     const float* __restrict__ xt = a.xtrial + (int64_t)bt * D;
     const float* __restrict__ Gt = a.G + (int64_t)bt * D;
-    const float* __restrict__ l2 = a.l2 + (int64_t)b * D;
-    const int csz = (D + a.nch - 1) / a.nch, e1 = min(D, (c + 1) * csz);
     float ps[NP3];
     float pd[2 * QN_MAX_M];  // the next direction's s_j.pg, y_j.pg (pg.pg is ps[4])
 #pragma unroll
     for (int q = 0; q < NP3; ++q) ps[q] = 0.f;
 #pragma unroll
     for (int q = 0; q < 2 * QN_MAX_M; ++q) pd[q] = 0.f;
-#pragma unroll 2
-    for (int e = c * csz + threadIdx.x; e < e1; e += QN_BLOCK) {
-      const float xn = xt[e];
-      const float gn = Gt[e] + l2[e] * xn;  // data gradient (masked, scaled) + L2 term
-      const float pg = pseudo_grad(xn, gn, l1v ? l1v[e] : 0.f);
+    auto proc = [&](const UpdElem& u, int e, float xn, float gt) __attribute__((always_inline)) {
+      const float gn = gt + u.l2 * xn;  // data gradient (masked, scaled) + L2 term
+      const float pg = pseudo_grad(xn, gn, u.l1);
       if (!a.init) {
-        const float se = xn - x[e], ye = gn - g[e];
+        const float se = xn - u.x, ye = gn - u.g;
         ps[0] = fmaf(se, ye, ps[0]);
         ps[1] = fmaf(se, se, ps[1]);
         ps[2] = fmaf(ye, ye, ps[2]);
@@ -1108,15 +1173,8 @@ __device__ __forceinline__ void qn_update_body(const QnArgs& a, int c, int b, ui
         for (int j = 0; j < QN_MAX_M; ++j) {
           if (FULLM || j < mm) {
             const bool hj = j == a.head;
-            // FULLM also loads slot `head` (its OLD pair: the loads precede the stores below) and
-            // accumulates its P3 sums, which finalize never reads
-            float sj = 0.f, yj = 0.f;
+            const float sj = u.s[j], yj = u.y[j];
             if (FULLM || !hj) {
-              // (unfilled slots re-read slot 0 — cached lines, no HBM traffic; their dots are never
-              // read: a slot's Gram row / column is rewritten when its first pair enters)
-              const int jl = j < a.filled ? j : 0;
-              sj = Sb[jl * sstride + e];
-              yj = Yb[jl * sstride + e];
               ps[5 + 3 * j] = fmaf(se, yj, ps[5 + 3 * j]);
               ps[6 + 3 * j] = fmaf(sj, ye, ps[6 + 3 * j]);
               ps[7 + 3 * j] = fmaf(ye, yj, ps[7 + 3 * j]);
@@ -1132,6 +1190,22 @@ __device__ __forceinline__ void qn_update_body(const QnArgs& a, int c, int b, ui
       ps[4] = fmaf(pg, pg, ps[4]);
       x[e] = xn;
       g[e] = gn;
+    };
+    // three elements per thread and round: their trial values in one round of loads, then each processed
+    // and its slot refilled three elements ahead (the element order and every sum's order are unchanged)
+    for (int e = eb; e < e1; e += 3 * QN_BLOCK) {
+      const int ea = eclamp(e), eb1 = eclamp(e + QN_BLOCK), eb2 = eclamp(e + 2 * QN_BLOCK);
+      const float xn0 = xt[ea], gt0 = Gt[ea], xn1 = xt[eb1], gt1 = Gt[eb1], xn2 = xt[eb2], gt2 = Gt[eb2];
+      proc(u0, e, xn0, gt0);
+      if (e + 3 * QN_BLOCK < e1) u0 = upd_load<FULLM>(a, b, e + 3 * QN_BLOCK);
+      if (e + QN_BLOCK < e1) {
+        proc(u1, e + QN_BLOCK, xn1, gt1);
+        if (e + 4 * QN_BLOCK < e1) u1 = upd_load<FULLM>(a, b, e + 4 * QN_BLOCK);
+      }
+      if (e + 2 * QN_BLOCK < e1) {
+        proc(u2, e + 2 * QN_BLOCK, xn2, gt2);
+        if (e + 5 * QN_BLOCK < e1) u2 = upd_load<FULLM>(a, b, e + 5 * QN_BLOCK);
+      }
     }
     HAR_LR_STAMP(3)
     // the P3 and P1 partials in ONE block sum (one LDS transpose and barrier pair), each total stored
