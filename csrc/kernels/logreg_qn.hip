@@ -75,9 +75,10 @@ constexpr int EVAL_XLD_MF = 36;
 // ... and the narrow designs (<= 10 dense columns, the reference encoding) on the matrix cores too, at
 // row pitch 12 (the chunk padded to 12 columns; 16 rows x 4 columns of a pass-A operand read still hit
 // 64 distinct banks): pass B's 80 scalar 256-long LDS chains (~5.3k cycles, eval stamps) become 16
-// MFMAs per wave.  Opt-in (HAR_LR_EVAL_MFN=1): pass B 4.7k -> 2.5k cycles, but the evaluation only
-// ~1.1k shorter and the 54-model CrossValidator batch ~1% slower (tile pitch 12 + the 4 KB of MFMA
-// partials per workgroup: fewer resident workgroups), profiles/r5/lr_grad_blocks.md
+// MFMAs per wave (4.7k -> 2.5k cycles).  With the row-owned staging of the narrow tile it is the default
+// for both the single fit and the 54-model CrossValidator batch (same-box A/B: LR 0.93 vs 0.94-0.99 ms,
+// LR-CV 4.28-4.34 vs 4.36-4.60 ms, profiles/r5/lr_grad_blocks.md); HAR_LR_EVAL_MFN=0 keeps the scalar
+// narrow kernel, -1 uses the MFMA one for launches of <= 256 workgroups only
 constexpr int EVAL_XLD_MFN = 12;
 template <int XLD> constexpr bool eval_mf() { return XLD == EVAL_XLD_MF || XLD == EVAL_XLD_MFN; }
 
@@ -90,6 +91,21 @@ __device__ __forceinline__ void eval_stage_chunk(const LogregEvalArgs& a, const 
   if (weights)
     for (int e = tid; e < ncs * KP; e += EVAL_ROWS)
       wd[e] = e / KP < nc ? W[(int64_t)a.dense_cols[c0 + e / KP] * KP + (e % KP)] : 0.f;
+  if constexpr (XLD == EVAL_XLD_NARROW || XLD == EVAL_XLD_MFN) {
+    // narrow tile (<= 10 columns): thread = row, its nc values in ONE round of loads (the flat loop
+    // below takes two rounds of 8 for the 10 x 256 tile, with an integer division per element);
+    // the MFMA pitch's columns nc .. ncs - 1 as zeros
+    constexpr int NW = EVAL_XLD_NARROW - 1;
+    const bool in = tid < nrow_tile;
+    const float* rp = a.dense + (r0 + (in ? tid : 0)) * a.ldd + c0;
+    float v[NW];
+#pragma unroll
+    for (int j = 0; j < NW; ++j) v[j] = j < nc ? rp[j] : 0.f;
+#pragma unroll
+    for (int j = 0; j < XLD; ++j)
+      if (j < ncs) xs[tid * XLD + j] = in && j < nc ? v[j < NW ? j : 0] : 0.f;
+    return;
+  }
   // U loads in flight per thread (clamped to a valid element, zeroed by a select), then the U stores:
   // the plain loop waited out one global round trip per element (10 per tile at 10 dense columns,
   // most of the evaluation's latency)
@@ -144,6 +160,26 @@ __device__ __forceinline__ void logreg_eval_body(const LogregEvalArgs& a, int bx
   const int64_t nrow_tile = min((int64_t)EVAL_ROWS, a.N - r0);
   const int nchunk = (Fd + EVAL_DCH - 1) / EVAL_DCH;
 
+  // designs with <= 4 one-hot features (the reference encoding: 3): this row's category indices and
+  // their weight rows are loaded now, under the dense staging (added below in the same order as the
+  // grouped gathers: the same sums)
+  constexpr int CP = 4;
+  const bool cpre = a.C <= CP;
+  f32x4_t wpre[CP][KP / 4];
+  bool onp[CP];
+  if (cpre) {
+    const int32_t* cr = a.cat + (ok ? row : 0) * a.C;
+    int cp[CP];
+#pragma unroll
+    for (int u = 0; u < CP; ++u) cp[u] = u < a.C ? cr[u] : -1;
+#pragma unroll
+    for (int u = 0; u < CP; ++u) {
+      onp[u] = ok && cp[u] >= 0;
+      const f32x4_t* wp = reinterpret_cast<const f32x4_t*>(W + (int64_t)max(cp[u], 0) * KP);
+#pragma unroll
+      for (int q = 0; q < KP / 4; ++q) wpre[u][q] = wp[q];
+    }
+  }
   // ---- pass A: margins ----
   float z[KP];
 #pragma unroll
@@ -191,7 +227,19 @@ __device__ __forceinline__ void logreg_eval_body(const LogregEvalArgs& a, int bx
     // load serialized ~2 C L2 round trips per evaluation; the sums and their order are unchanged)
     constexpr int CG = 8;  // (16: slower, r5 stamps)
     const int32_t* cr = a.cat + row * a.C;
-    for (int c0 = 0; c0 < a.C; c0 += CG) {
+    if (cpre) {
+#pragma unroll
+      for (int u = 0; u < CP; ++u) {
+#pragma unroll
+        for (int q = 0; q < KP / 4; ++q) {
+          z[4 * q + 0] = onp[u] ? z[4 * q + 0] + wpre[u][q][0] : z[4 * q + 0];
+          z[4 * q + 1] = onp[u] ? z[4 * q + 1] + wpre[u][q][1] : z[4 * q + 1];
+          z[4 * q + 2] = onp[u] ? z[4 * q + 2] + wpre[u][q][2] : z[4 * q + 2];
+          z[4 * q + 3] = onp[u] ? z[4 * q + 3] + wpre[u][q][3] : z[4 * q + 3];
+        }
+      }
+    }
+    for (int c0 = 0; c0 < (cpre ? 0 : a.C); c0 += CG) {
       int cols[CG];
 #pragma unroll
       for (int u = 0; u < CG; ++u) {
@@ -1372,12 +1420,12 @@ extern "C" int har_logreg_eval(const LogregEvalArgs* args, int KP, int n_models,
     const char* e = std::getenv("HAR_LR_EVAL_MFMA");
     return !e || std::atoi(e) != 0;
   }();
-  static const bool mfn_on = [] {
+  static const int mfn_mode = [] {  // narrow designs on the MFMA kernel: 1 always, 0 never, -1 small launches
     const char* e = std::getenv("HAR_LR_EVAL_MFN");
-    return e && std::atoi(e) != 0;
+    return e ? std::atoi(e) : 1;
   }();
   const bool narrow = eval_xld(a.Fd) == EVAL_XLD_NARROW;
-  const bool mf = mf_on && (!narrow || mfn_on);
+  const bool mf = mf_on && (!narrow || mfn_mode == 1 || (mfn_mode < 0 && (int64_t)tiles * n_models <= 256));
   const int xld = mf ? (narrow ? EVAL_XLD_MFN : EVAL_XLD_MF) : eval_xld(a.Fd);
   const size_t lds = sizeof(float) * (EVAL_DCH * KP + EVAL_ROWS * xld + EVAL_ROWS * KP + EVAL_ROWS / 64 +
                                       (mf ? 4 * EVAL_DCH * KP : 0));
@@ -1488,12 +1536,12 @@ extern "C" int har_logreg_solve_persistent(const QnArgs* q, const LogregEvalArgs
     const char* e = std::getenv("HAR_LR_EVAL_MFMA");
     return !e || std::atoi(e) != 0;
   }();
-  static const bool mfn_on = [] {
+  static const int mfn_mode = [] {
     const char* e = std::getenv("HAR_LR_EVAL_MFN");
-    return e && std::atoi(e) != 0;
+    return e ? std::atoi(e) : 1;
   }();
   const bool narrow = eval_xld(ev1->Fd) == EVAL_XLD_NARROW;
-  const bool mf = mf_on && (!narrow || mfn_on);
+  const bool mf = mf_on && (!narrow || mfn_mode == 1);
   const int xld = mf ? (narrow ? EVAL_XLD_MFN : EVAL_XLD_MF) : eval_xld(ev1->Fd);
   const size_t lds = sizeof(float) * (EVAL_DCH * KP + EVAL_ROWS * xld + EVAL_ROWS * KP + EVAL_ROWS / 64 +
                                       (mf ? 4 * EVAL_DCH * KP : 0));
