@@ -24,10 +24,15 @@ constexpr int SROWS = 256;
 constexpr int SDCH = 32;
 constexpr int SXLD = SDCH + 1;
 
+// thread = row: a chunk's values of the row in one round of loads (the flat element loop was one
+// dependent round trip per element); each sum is 4 chains of 64 rows added in a fixed order (a single
+// 256-long fp64 chain per value was most of the kernel's ~36 us, profiles/r5/lr_grad_blocks.md)
 __global__ __launch_bounds__(SROWS) void logreg_summary_tiles_kernel(LogregSummaryArgs a) {
+  constexpr int NP = 4, PR = SROWS / NP;  // row parts per sum, rows per part
   __shared__ float xs[SROWS * SXLD];
   __shared__ double ws[SROWS];
   __shared__ int ys[SROWS];
+  __shared__ double red[SROWS];  // >= NP * 2 * SDCH partial chains
   const int tid = threadIdx.x, s = blockIdx.y;
   const int64_t r0 = (int64_t)blockIdx.x * SROWS, row = r0 + tid;
   const int64_t nrow = min((int64_t)SROWS, a.N - r0);
@@ -38,26 +43,45 @@ __global__ __launch_bounds__(SROWS) void logreg_summary_tiles_kernel(LogregSumma
   for (int c0 = 0; c0 < a.Fd; c0 += SDCH) {
     const int nc = min(SDCH, a.Fd - c0);
     __syncthreads();
-    for (int e = tid; e < SROWS * nc; e += SROWS) {
-      const int rr = e / nc, j = e % nc;
-      xs[rr * SXLD + j] = rr < nrow ? a.dense[(r0 + rr) * a.ldd + c0 + j] : 0.f;
+    {
+      const bool in = tid < nrow;
+      const float* rp = a.dense + (r0 + (in ? tid : 0)) * a.ldd + c0;
+      float v[SDCH];
+#pragma unroll
+      for (int j = 0; j < SDCH; ++j) v[j] = j < nc ? rp[j] : 0.f;
+#pragma unroll
+      for (int j = 0; j < SDCH; ++j)
+        if (j < nc) xs[tid * SXLD + j] = in ? v[j] : 0.f;
     }
     __syncthreads();
-    if (tid < 2 * nc) {
-      const int j = tid >> 1, sq = tid & 1;
+    if (tid < NP * 2 * nc) {
+      const int q = tid / NP, part = tid % NP, j = q >> 1, sq = q & 1;
       double acc = 0.0;
-      for (int i = 0; i < SROWS; ++i) {
+      for (int i = part * PR; i < (part + 1) * PR; ++i) {
         const double x = (double)xs[i * SXLD + j];
         acc = fma(ws[i], sq ? x * x : x, acc);
       }
-      out[2 * (c0 + j) + sq] = acc;
+      red[tid] = acc;
+    }
+    __syncthreads();
+    if (tid < 2 * nc) {
+      const double* r = red + NP * tid;
+      out[2 * c0 + tid] = (r[0] + r[1]) + (r[2] + r[3]);  // value tid = 2 j + sq
     }
   }
   __syncthreads();
-  if (tid <= a.K) {  // class sums (tid < K) and the weight sum (tid == K)
+  // class sums (k < K) and the weight sum (k == K): 4 row parts each (one 256-row chain when K >= 64)
+  const int npk = NP * (a.K + 1) <= SROWS ? NP : 1, prk = SROWS / npk;
+  if (tid < npk * (a.K + 1)) {
+    const int k = tid / npk, part = tid % npk;
     double acc = 0.0;
-    for (int i = 0; i < SROWS; ++i) acc += (tid == a.K || ys[i] == tid) ? ws[i] : 0.0;
-    out[2 * a.Fd + tid] = acc;
+    for (int i = part * prk; i < (part + 1) * prk; ++i) acc += (k == a.K || ys[i] == k) ? ws[i] : 0.0;
+    red[tid] = acc;
+  }
+  __syncthreads();
+  if (tid <= a.K) {
+    const double* r = red + npk * tid;
+    out[2 * a.Fd + tid] = npk == NP ? (r[0] + r[1]) + (r[2] + r[3]) : r[0];
   }
 }
 
