@@ -212,11 +212,12 @@ class LogregDesign:
             part = torch.empty(S_, max(1, nt), 2 * self.Fd + K + 1, dtype=torch.float64, device=dev)
             out = torch.empty(S_, 1 + 2 * F + K, dtype=torch.float64, device=dev)
             cs = self.col_slice()
+            srow = self.col_blocks()[2]
             for ph in (0, 1):
                 mod.logreg_summary(ph, self.dense.data_ptr(), self.dense.stride(0), self.Fd, self.y32.data_ptr(),
                                    self.rw_ptr(), N, F, K, S_, self.col_map.data_ptr(), self.csc_rows.data_ptr(),
                                    self.csc_off.data_ptr(), cs.data_ptr(), self.SL, nt, part.data_ptr(),
-                                   out.data_ptr(), st)
+                                   out.data_ptr(), 0 if srow is None else srow.data_ptr(), st)
             return out
         rwd = self.rw_rows().double()
         out = torch.zeros(S_, 1 + 2 * F + K, dtype=torch.float64, device=dev)

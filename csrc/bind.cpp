@@ -468,8 +468,9 @@ PYBIND11_MODULE(_har_native, m) {
   m.def("logreg_summary_tiles", &har_logreg_summary_tiles);
   m.def("logreg_summary", [](int phase, u dense, int64_t ldd, int Fd, u y, u rw, int64_t N, int F, int K, int nspec,
                              u col_map, u csc_rows, u csc_off, u col_slice, int SL, int ntiles, u part, u summ,
-                             u stream) {
+                             u srow, u stream) {
     LogregSummaryArgs a;
+    a.srow = P<const int32_t>(srow);
     a.dense = P<const float>(dense);
     a.ldd = ldd;
     a.Fd = Fd;

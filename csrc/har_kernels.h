@@ -296,6 +296,7 @@ typedef struct LogregSummaryArgs {
   const int32_t* col_slice; // [F+2] (har_logreg_col_slices)
   int SL;
   int ntiles;               // har_logreg_summary_tiles(N)
+  const int32_t* srow;      // [slices + 1] first CSC row of every slice, or null (search the slice's column)
   double* part;             // [S][ntiles][2 Fd + K + 1] tile partials
   double* summ;             // [S][1 + 2F + K] (sum w, sum w x, sum w x^2, class sums)
 } LogregSummaryArgs;

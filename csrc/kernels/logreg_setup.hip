@@ -102,13 +102,19 @@ __global__ __launch_bounds__(256) void logreg_summary_cols_kernel(LogregSummaryA
       if (base > s0) __syncthreads();
       const int sl = base + threadIdx.x;
       if (sl < s1) {
-        int lo = c0, hi = c1 - 1;
-        while (lo < hi) {
-          const int mid = (lo + hi + 1) >> 1;
-          if (a.col_slice[mid] <= sl) lo = mid; else hi = mid - 1;
+        int r0, r1;
+        if (a.srow) {  // the slice's rows from the per-slice table: no dependent search
+          r0 = a.srow[sl];
+          r1 = a.srow[sl + 1];
+        } else {  // the slice's column by a binary search over col_slice (a chain of global loads)
+          int lo = c0, hi = c1 - 1;
+          while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (a.col_slice[mid] <= sl) lo = mid; else hi = mid - 1;
+          }
+          r0 = a.csc_off[lo] + (sl - a.col_slice[lo]) * a.SL;
+          r1 = min(r0 + a.SL, a.csc_off[lo + 1]);
         }
-        const int r0 = a.csc_off[lo] + (sl - a.col_slice[lo]) * a.SL;
-        const int r1 = min(r0 + a.SL, a.csc_off[lo + 1]);
         double acc = 0.0;
         for (int i = r0; i < r1; ++i) acc += a.rw ? (double)a.rw[(int64_t)s * a.N + a.csc_rows[i]] : 1.0;
         part[threadIdx.x] = acc;
