@@ -418,17 +418,19 @@ __device__ __forceinline__ double loss_decode(const float* in) {
   return (double)q / LOSS_FX;
 }
 
-template <int KP, bool STAMP = false>
+// TB trial models per workgroup (TB = 4, opt-in: the four trials of one spec, launches with tstride 1):
+// the slice row lists, the column metadata and inv_std / pmask loaded once for the TB models and their
+// residual rows gathered together.  The sums per model and their order are those of TB = 1.
+template <int KP, bool STAMP = false, int TB = 1>
 __device__ __forceinline__ void logreg_grad_body(const LogregGradArgs& a, int bx, int by, uint64_t* st = nullptr) {
   HAR_LR_STAMP(0)
-  __shared__ float part[256 * KP];
+  __shared__ float part[256 * KP * TB];
   __shared__ int cs_l[257];                        // col_slice[c0 .. c1] of the block
   __shared__ float tl[256];                        // tile losses (block 0)
-  const int bt = a.model0 + by * a.tstride;
-  const int s = bt / a.T;
+  const int bt0 = a.model0 + TB * by * a.tstride;  // model of trial slot 0 (slot tt: bt0 + tt * tstride)
+  const int s = bt0 / a.T;                         // (TB > 1: the TB models share the spec)
   const int Fp1 = a.F + 1;
   const int SW = a.Fd * KP + KP + 1;
-  const float* slab = a.slab + (int64_t)bt * a.ntiles * SW;
   // col_blk (balanced blocks, ops/logreg.py LogregDesign.col_blocks): block bx = columns [c0, c1), slices
   // [s0, s1), and slice sl covers the CSC rows [srow[sl], srow[sl + 1]) — no slice -> column search;
   // everything a lane needs is loaded in ONE round at entry (its slice's rows, its column's slice range,
@@ -464,16 +466,22 @@ __device__ __forceinline__ void logreg_grad_body(const LogregGradArgs& a, int bx
       if (k < a.K) pmv[k] = pm[(int64_t)k * Fp1 + col];
   }
   const bool loss_block = bx == 0;
-  if (loss_block && (int)threadIdx.x < a.ntiles) tl[threadIdx.x] = slab[(int64_t)threadIdx.x * SW + SW - 1];
-  __syncthreads();
-  if (loss_block && threadIdx.x == 0) {
-    double l = 0.0;
-    for (int t = 0; t < a.ntiles; ++t)  // tile order (ntiles > 256: the rest straight from the slabs)
-      l += (double)(t < 256 ? tl[t] : slab[(int64_t)t * SW + SW - 1]);
-    if (a.loss_fx)
-      loss_encode(l, a.loss_fx + (int64_t)bt * 5);
-    else
-      a.loss[bt] = l;
+#pragma unroll
+  for (int tt = 0; tt < TB; ++tt) {
+    const int bt = bt0 + tt * a.tstride;
+    const float* slab = a.slab + (int64_t)bt * a.ntiles * SW;
+    if (tt) __syncthreads();  // tl consumed
+    if (loss_block && (int)threadIdx.x < a.ntiles) tl[threadIdx.x] = slab[(int64_t)threadIdx.x * SW + SW - 1];
+    __syncthreads();
+    if (loss_block && threadIdx.x == 0) {
+      double l = 0.0;
+      for (int t = 0; t < a.ntiles; ++t)  // tile order (ntiles > 256: the rest straight from the slabs)
+        l += (double)(t < 256 ? tl[t] : slab[(int64_t)t * SW + SW - 1]);
+      if (a.loss_fx)
+        loss_encode(l, a.loss_fx + (int64_t)bt * 5);
+      else
+        a.loss[bt] = l;
+    }
   }
   HAR_LR_STAMP(1)
   if (!fast) {
@@ -482,10 +490,12 @@ __device__ __forceinline__ void logreg_grad_body(const LogregGradArgs& a, int bx
     cs0 = col < c1 ? cs_l[threadIdx.x] : 0;
     cs1 = col < c1 ? cs_l[threadIdx.x + 1] : 0;
   }
-  const float* R = a.R + (int64_t)by * a.N * KP;  // this launch's residual slot of the model
-  float g[KP];
+  const float* R = a.R + (int64_t)TB * by * a.N * KP;  // this launch's residual slots of the TB models
+  float g[TB][KP];
 #pragma unroll
-  for (int k = 0; k < KP; ++k) g[k] = 0.f;
+  for (int tt = 0; tt < TB; ++tt)
+#pragma unroll
+    for (int k = 0; k < KP; ++k) g[tt][k] = 0.f;
   for (int base = s0; base < s1; base += 256) {
     if (base > s0) __syncthreads();  // the previous round's partials are consumed
     const int sl = base + threadIdx.x;
@@ -504,43 +514,54 @@ __device__ __forceinline__ void logreg_grad_body(const LogregGradArgs& a, int bx
         r0 = a.csc_off[c0 + lo] + (sl - cs_l[lo]) * a.SL;
         r1 = min(r0 + a.SL, a.csc_off[c0 + lo + 1]);
       }
-      float gs[KP];
+      float gs[TB][KP];
 #pragma unroll
-      for (int k = 0; k < KP; ++k) gs[k] = 0.f;
-      // groups of RG rows: RG row indices, then their RG residual rows in flight (two dependent round
-      // trips per group, the slice's last partial group included: rows past r1 re-read row r1 - 1 and
-      // add +0, an exact identity since gs is never -0 — the sums are bitwise the row-by-row ones;
-      // a row-at-a-time tail cost two round trips PER ROW, up to 14 for a 7-row tail: grad stamps)
-      constexpr int RG = KP == 8 ? 8 : 4;
+      for (int tt = 0; tt < TB; ++tt)
+#pragma unroll
+        for (int k = 0; k < KP; ++k) gs[tt][k] = 0.f;
+      // groups of RG rows: RG row indices, then their RG residual rows (of each of the TB models) in
+      // flight (two dependent round trips per group, the slice's last partial group included: rows past
+      // r1 re-read row r1 - 1 and add +0, an exact identity since gs is never -0 — the sums are bitwise
+      // the row-by-row ones; a row-at-a-time tail cost two round trips PER ROW: grad stamps)
+      constexpr int RG = TB > 1 ? 4 : (KP == 8 ? 8 : 4);
       for (int i0 = r0; i0 < r1; i0 += RG) {
         int rid[RG];
 #pragma unroll
         for (int j = 0; j < RG; ++j) rid[j] = a.csc_rows[min(i0 + j, r1 - 1)];
-        f32x4_t rr[RG][KP / 4];
+        f32x4_t rr[TB][RG][KP / 4];
 #pragma unroll
-        for (int j = 0; j < RG; ++j)
+        for (int tt = 0; tt < TB; ++tt)
 #pragma unroll
-          for (int q = 0; q < KP / 4; ++q) rr[j][q] = reinterpret_cast<const f32x4_t*>(R + (int64_t)rid[j] * KP)[q];
+          for (int j = 0; j < RG; ++j)
+#pragma unroll
+            for (int q = 0; q < KP / 4; ++q)
+              rr[tt][j][q] = reinterpret_cast<const f32x4_t*>(R + ((int64_t)tt * a.N + rid[j]) * KP)[q];
 #pragma unroll
         for (int j = 0; j < RG; ++j) {
           const bool on = i0 + j < r1;
 #pragma unroll
-          for (int q = 0; q < KP / 4; ++q) {
-            gs[4 * q + 0] += on ? rr[j][q][0] : 0.f;
-            gs[4 * q + 1] += on ? rr[j][q][1] : 0.f;
-            gs[4 * q + 2] += on ? rr[j][q][2] : 0.f;
-            gs[4 * q + 3] += on ? rr[j][q][3] : 0.f;
-          }
+          for (int tt = 0; tt < TB; ++tt)
+#pragma unroll
+            for (int q = 0; q < KP / 4; ++q) {
+              gs[tt][4 * q + 0] += on ? rr[tt][j][q][0] : 0.f;
+              gs[tt][4 * q + 1] += on ? rr[tt][j][q][1] : 0.f;
+              gs[tt][4 * q + 2] += on ? rr[tt][j][q][2] : 0.f;
+              gs[tt][4 * q + 3] += on ? rr[tt][j][q][3] : 0.f;
+            }
         }
       }
 #pragma unroll
-      for (int k = 0; k < KP; ++k) part[threadIdx.x * KP + k] = gs[k];
+      for (int tt = 0; tt < TB; ++tt)
+#pragma unroll
+        for (int k = 0; k < KP; ++k) part[(threadIdx.x * TB + tt) * KP + k] = gs[tt][k];
     }
     __syncthreads();
     const int e0 = max(cs0, base), e1 = min(cs1, base + 256);
     for (int e = e0; e < e1; ++e) {  // this column's slices of the round, in order
 #pragma unroll
-      for (int k = 0; k < KP; ++k) g[k] += part[(e - base) * KP + k];
+      for (int tt = 0; tt < TB; ++tt)
+#pragma unroll
+        for (int k = 0; k < KP; ++k) g[tt][k] += part[((e - base) * TB + tt) * KP + k];
     }
   }
   HAR_LR_STAMP(2)
@@ -548,24 +569,31 @@ __device__ __forceinline__ void logreg_grad_body(const LogregGradArgs& a, int bx
   const int cm = a.col_map[col];
   if (cm >= 0 || cm == -1) {  // dense column j = cm, or the intercept (slab entries after the dense block)
     const int off = cm >= 0 ? cm * KP : a.Fd * KP;
-#pragma unroll 8
-    for (int t = 0; t < a.ntiles; ++t) {
-      const float* p = slab + (int64_t)t * SW + off;
 #pragma unroll
-      for (int k = 0; k < KP; ++k) g[k] += p[k];
+    for (int tt = 0; tt < TB; ++tt) {
+      const float* slab = a.slab + (int64_t)(bt0 + tt * a.tstride) * a.ntiles * SW;
+#pragma unroll 8
+      for (int t = 0; t < a.ntiles; ++t) {
+        const float* p = slab + (int64_t)t * SW + off;
+#pragma unroll
+        for (int k = 0; k < KP; ++k) g[tt][k] += p[k];
+      }
     }
   }
   HAR_LR_STAMP(3)
-  float* G = a.G + (int64_t)bt * D;
 #pragma unroll
-  for (int k = 0; k < KP; ++k)
-    if (k < a.K) G[(int64_t)k * Fp1 + col] = g[k] * sc * pmv[k];
+  for (int tt = 0; tt < TB; ++tt) {
+    float* G = a.G + (int64_t)(bt0 + tt * a.tstride) * D;
+#pragma unroll
+    for (int k = 0; k < KP; ++k)
+      if (k < a.K) G[(int64_t)k * Fp1 + col] = g[tt][k] * sc * pmv[k];
+  }
   HAR_LR_STAMP(4)
 }
 
-template <int KP, bool STAMP = false>
+template <int KP, bool STAMP = false, int TB = 1>
 __global__ __launch_bounds__(256) void logreg_grad_kernel(LogregGradArgs a, uint64_t* st) {
-  logreg_grad_body<KP, STAMP>(a, blockIdx.x, blockIdx.y, st);
+  logreg_grad_body<KP, STAMP, TB>(a, blockIdx.x, blockIdx.y, st);
 }
 
 // after the data-parallel all-reduce of the bucket: the summed fixed-point losses -> fp64
@@ -1465,6 +1493,22 @@ extern "C" int har_logreg_grad(const LogregGradArgs* args, int KP, int n_models,
     return -2;
   if (n_models == 0) return 0;
   if (a.col_blk && (a.nblk < 1 || a.srow == nullptr)) return -2;
+  // opt-in (HAR_LR_GRAD_TB=4): four trial models per workgroup for large launches of consecutive trials
+  // of one spec — measured SLOWER for the batched CrossValidator (grad 54.8 vs 35.6 us per launch, LR-CV
+  // 4.8-5.3 vs 4.1-4.5 ms: a quarter of the workgroups, each with 4x the gathers in flight per lane,
+  // profiles/r5/lr_grad_blocks.md)
+  static const int tb_env = [] {
+    const char* e = std::getenv("HAR_LR_GRAD_TB");
+    return e ? std::atoi(e) : 1;
+  }();
+  const bool tb4 = tb_env == 4 && KP == 8 && a.T == 4 && a.tstride == 1 && a.model0 % 4 == 0 && n_models % 4 == 0 &&
+                   n_models >= 64;
+  if (tb4) {
+    dim3 g4(a.col_blk ? a.nblk : (a.F + 1 + 255) / 256, n_models / 4);
+    logreg_grad_kernel<8, false, 4><<<g4, 256, 0, s>>>(a, nullptr);
+    HAR_CHECK_LAUNCH();
+    return 0;
+  }
   dim3 grid(a.col_blk ? a.nblk : (a.F + 1 + 255) / 256, n_models);
   if (KP == 8)
     if (g_lr_stamps_grd)
