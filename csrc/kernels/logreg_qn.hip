@@ -886,10 +886,10 @@ struct DirElem {
   float s[QN_MAX_M], y[QN_MAX_M];
 };
 
-__device__ __forceinline__ DirElem dir_load(const QnArgs& a, int b, int e) {
+__device__ __forceinline__ DirElem dir_load(const QnArgs& a, int b, int k, int col) {
   const int64_t D = a.D, sstride = (int64_t)a.B * D;
   const int Fp1 = a.F + 1;
-  const int k = e / Fp1, col = e - k * Fp1;
+  const int e = k * Fp1 + col;
   DirElem v;
   v.x = a.x[b * D + e];
   v.g = a.g[b * D + e];
@@ -911,7 +911,8 @@ __device__ __forceinline__ DirElem dir_load(const QnArgs& a, int b, int e) {
 
 // phase 1
 template <int KP, bool FULLM, bool STAMP = false>
-__device__ __forceinline__ void qn_direction_body(const QnArgs& a, int c, int b, uint64_t* st = nullptr) {
+__device__ __forceinline__ void qn_direction_body(const QnArgs& a, int c, int b, uint64_t* st = nullptr,
+                                                  float* wt = nullptr) {
   HAR_LR_STAMP(0)
   __shared__ double sh[4 * NP2];
   __shared__ float cS[QN_MAX_M], cY[QN_MAX_M];
@@ -924,12 +925,24 @@ __device__ __forceinline__ void qn_direction_body(const QnArgs& a, int c, int b,
   // matrices, rho and the coefficient vectors (per-lane arrays indexed by slot would spill to scratch)
   __shared__ double p1v[NP1], SY[QN_MAX_M * QN_MAX_M], YY[QN_MAX_M * QN_MAX_M], rho_s[QN_MAX_M];
   const bool rec = !a.init && !steep;  // block-uniform
-  const int csz = (D + a.nch - 1) / a.nch, e1 = min(D, (c + 1) * csz);
-  const int e0 = c * csz + threadIdx.x;
+  // chunk c = the columns [cc0, cc0 + ccn) x every class k (element e = k (F+1) + col), walked k-major
+  // (i = k ccn + j: consecutive lanes, consecutive columns -> coalesced loads and xtrial stores); with
+  // `wt` (an LDS tile [T][KP][ccs]) the chunk's W_eff rows are assembled on chip and stored as whole
+  // 32-byte rows — written per element they were 4-byte stores 32 bytes apart, the batched CV
+  // direction's bound (profiles/r5/lr_grad_blocks.md)
+  const int ccs = (Fp1 + a.nch - 1) / a.nch, cc0 = c * ccs, ccn = max(0, min(Fp1, cc0 + ccs) - cc0);
+  const int nel = ccn * a.K;
+  const uint32_t cmag = 0xffffffffu / (uint32_t)max(ccn, 1) + 1u;  // i / ccn = umulhi(i, cmag) (i ccn < 2^32)
+  const int e0 = threadIdx.x, e1 = nel;
+  auto kof = [&](int i) { return (int)__umulhi((uint32_t)i, cmag); };
   // each thread's first three elements in flight during the prologue + recursion (a refill three ahead),
   // issued AFTER the recursion's operand loads (Gram, rho, P1 totals): a counted wait for those then
   // does not also wait for the 75 element loads behind them
   auto dclamp = [&](int e) { return max(min(e, e1 - 1), 0); };
+  auto dload = [&](int i) {
+    const int k = ccn ? kof(i) : 0;
+    return dir_load(a, b, k, cc0 + (ccn ? i - k * ccn : 0));
+  };
   const int i = threadIdx.x;
   double syv = 0.0, yyv = 0.0, rhv = 0.0, p1x = 0.0;
   if (rec) {
@@ -942,8 +955,7 @@ __device__ __forceinline__ void qn_direction_body(const QnArgs& a, int c, int b,
     if (i < NP1) p1x = a.P1[(int64_t)b * a.nch * NP1 + i];  // the totals (the last update's last chunk)
   }
   __builtin_amdgcn_sched_barrier(0);
-  DirElem d0 = dir_load(a, b, dclamp(e0)), d1 = dir_load(a, b, dclamp(e0 + QN_BLOCK)),
-          d2 = dir_load(a, b, dclamp(e0 + 2 * QN_BLOCK));
+  DirElem d0 = dload(dclamp(e0)), d1 = dload(dclamp(e0 + QN_BLOCK)), d2 = dload(dclamp(e0 + 2 * QN_BLOCK));
   __builtin_amdgcn_sched_barrier(0);
   if (rec) {
     // every entry of the [QN_MAX_M]^2 images written (zeros past m^2): the recursion below reads whole
@@ -1047,7 +1059,8 @@ __device__ __forceinline__ void qn_direction_body(const QnArgs& a, int c, int b,
   float r[NP2];
 #pragma unroll
   for (int t = 0; t < NP2; ++t) r[t] = 0.f;
-  auto proc = [&](const DirElem& cur, int e) __attribute__((always_inline)) {
+  auto proc = [&](const DirElem& cur, int i) __attribute__((always_inline)) {
+    const int k = kof(i), jc = i - k * ccn, col = cc0 + jc, e = k * Fp1 + col;
     const float xe = cur.x;
     const float l1e = cur.l1;
     const float pg = a.init ? 0.f : pseudo_grad(xe, cur.g, l1e);
@@ -1072,7 +1085,6 @@ __device__ __forceinline__ void qn_direction_body(const QnArgs& a, int c, int b,
     r[3 * QN_MAX_TRIALS + 1] = fmaf(pg, pg, r[3 * QN_MAX_TRIALS + 1]);
     const float xi = xe != 0.f ? sgnf(xe) : sgnf(-pg);
     const float hl2 = cur.hl2;
-    const int k = e / Fp1, col = e - k * Fp1;
     const float wsc = cur.wsc;
 #pragma unroll
     for (int t = 0; t < QN_MAX_TRIALS; ++t) {
@@ -1087,20 +1099,33 @@ __device__ __forceinline__ void qn_direction_body(const QnArgs& a, int c, int b,
         a.xtrial[(int64_t)bt * D + e] = xn;
         r[3 * t] = fmaf(hl2, xn * xn, r[3 * t]);
         r[3 * t + 1] = fmaf(l1e, fabsf(xn), r[3 * t + 1]);
-        a.weff[((int64_t)bt * Fp1 + col) * KP + k] = xn * wsc;
+        if (wt)
+          wt[(t * KP + k) * ccs + jc] = xn * wsc;
+        else
+          a.weff[((int64_t)bt * Fp1 + col) * KP + k] = xn * wsc;
       }
     }
   };
   for (int e = e0; e < e1; e += 3 * QN_BLOCK) {
     proc(d0, e);
-    if (e + 3 * QN_BLOCK < e1) d0 = dir_load(a, b, e + 3 * QN_BLOCK);
+    if (e + 3 * QN_BLOCK < e1) d0 = dload(e + 3 * QN_BLOCK);
     if (e + QN_BLOCK < e1) {
       proc(d1, e + QN_BLOCK);
-      if (e + 4 * QN_BLOCK < e1) d1 = dir_load(a, b, e + 4 * QN_BLOCK);
+      if (e + 4 * QN_BLOCK < e1) d1 = dload(e + 4 * QN_BLOCK);
     }
     if (e + 2 * QN_BLOCK < e1) {
       proc(d2, e + 2 * QN_BLOCK);
-      if (e + 5 * QN_BLOCK < e1) d2 = dir_load(a, b, e + 5 * QN_BLOCK);
+      if (e + 5 * QN_BLOCK < e1) d2 = dload(e + 5 * QN_BLOCK);
+    }
+  }
+  if (wt) {  // the chunk's W_eff rows from the tile, 8 lanes per 32-byte row (classes >= K: zeros)
+    __syncthreads();
+    for (int t = 0; t < T; ++t) {
+      float* wrow = a.weff + ((int64_t)(b * a.T + t) * Fp1 + cc0) * KP;
+      for (int idx = threadIdx.x; idx < ccn * KP; idx += QN_BLOCK) {
+        const int jc = idx / KP, k = idx % KP;
+        wrow[idx] = k < a.K ? wt[(t * KP + k) * ccs + jc] : 0.f;
+      }
     }
   }
   HAR_LR_STAMP(3)
@@ -1116,8 +1141,9 @@ __device__ __forceinline__ void qn_direction_body(const QnArgs& a, int c, int b,
 }
 
 template <int KP, bool FULLM, bool STAMP = false>
-__global__ __launch_bounds__(QN_BLOCK) void qn_direction_kernel(QnArgs a, uint64_t* st) {
-  qn_direction_body<KP, FULLM, STAMP>(a, blockIdx.x, blockIdx.y, st);
+__global__ __launch_bounds__(QN_BLOCK) void qn_direction_kernel(QnArgs a, uint64_t* st, int use_wt) {
+  extern __shared__ float wtile[];
+  qn_direction_body<KP, FULLM, STAMP>(a, blockIdx.x, blockIdx.y, st, use_wt ? wtile : nullptr);
 }
 
 // One parameter element's phase-2 operands that do not depend on the picked trial (x, g, L1 / L2
@@ -1636,17 +1662,28 @@ extern "C" int har_lbfgs_phase(const QnArgs* args, int KP, int phase, hipStream_
   const bool full = a.m == QN_MAX_M;
   const dim3 grid(a.nch, a.B);
   if (phase == 1) {
+    // the W_eff tile [T][KP][columns per chunk] in LDS when it fits 64 KB and the launch is a batch of
+    // >= 256 workgroups (CV direction 42.7 -> 26.0 us; a single fit's 32 workgroups are latency-bound and
+    // the tile's extra pass cost ~1 us there, profiles/r5/lr_grad_blocks.md); HAR_LR_WTILE=0: never
+    static const bool wt_on = [] {
+      const char* e = std::getenv("HAR_LR_WTILE");
+      return !e || std::atoi(e) != 0;
+    }();
+    const int ccs = (a.F + 1 + a.nch - 1) / a.nch;
+    const size_t wb = (size_t)(a.init ? 1 : a.T) * KP * ccs * sizeof(float);
+    const int uw = wt_on && wb <= 64 * 1024 && (int64_t)a.nch * a.B >= 256 ? 1 : 0;
+    const size_t lds = uw ? wb : 0;
     if (KP == 8 && full)
       if (g_lr_stamps)
-        qn_direction_kernel<8, true, true><<<grid, QN_BLOCK, 0, s>>>(a, g_lr_stamps_dir);
+        qn_direction_kernel<8, true, true><<<grid, QN_BLOCK, lds, s>>>(a, g_lr_stamps_dir, uw);
       else
-        qn_direction_kernel<8, true><<<grid, QN_BLOCK, 0, s>>>(a, nullptr);
+        qn_direction_kernel<8, true><<<grid, QN_BLOCK, lds, s>>>(a, nullptr, uw);
     else if (KP == 8)
-      qn_direction_kernel<8, false><<<grid, QN_BLOCK, 0, s>>>(a, nullptr);
+      qn_direction_kernel<8, false><<<grid, QN_BLOCK, lds, s>>>(a, nullptr, uw);
     else if (full)
-      qn_direction_kernel<16, true><<<grid, QN_BLOCK, 0, s>>>(a, nullptr);
+      qn_direction_kernel<16, true><<<grid, QN_BLOCK, lds, s>>>(a, nullptr, uw);
     else
-      qn_direction_kernel<16, false><<<grid, QN_BLOCK, 0, s>>>(a, nullptr);
+      qn_direction_kernel<16, false><<<grid, QN_BLOCK, lds, s>>>(a, nullptr, uw);
   } else {
     if (full)  // 170 VGPRs: the 54-model CV batch at 9 chunks still fits one round (40.6 us vs 42.5 lean)
       if (g_lr_stamps)
