@@ -595,6 +595,14 @@ template <int KP, bool STAMP = false, int TB = 1>
 __global__ __launch_bounds__(256) void logreg_grad_kernel(LogregGradArgs a, uint64_t* st) {
   logreg_grad_body<KP, STAMP, TB>(a, blockIdx.x, blockIdx.y, st);
 }
+// the same body held to 5+ waves per SIMD (94 VGPRs): more resident workgroups for the batched
+// CrossValidator launch — opt-in (HAR_LR_GRAD_WPE=5): LR-CV 4.07-4.24 vs 4.12-4.17 ms, within noise
+// (profiles/r5/lr_grad_blocks.md)
+template <int KP>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void logreg_grad_kernel_w5(LogregGradArgs a,
+                                                                                                  uint64_t* st) {
+  logreg_grad_body<KP, false, 1>(a, blockIdx.x, blockIdx.y, st);
+}
 
 // after the data-parallel all-reduce of the bucket: the summed fixed-point losses -> fp64
 __global__ void logreg_loss_decode_kernel(const float* __restrict__ fx, double* __restrict__ loss, int n) {
@@ -1536,6 +1544,15 @@ extern "C" int har_logreg_grad(const LogregGradArgs* args, int KP, int n_models,
     return 0;
   }
   dim3 grid(a.col_blk ? a.nblk : (a.F + 1 + 255) / 256, n_models);
+  static const int wpe_env = [] {
+    const char* e = std::getenv("HAR_LR_GRAD_WPE");
+    return e ? std::atoi(e) : 0;
+  }();
+  if (KP == 8 && wpe_env == 5 && (int64_t)grid.x * grid.y >= 1024 && !g_lr_stamps_grd) {
+    logreg_grad_kernel_w5<8><<<grid, 256, 0, s>>>(a, nullptr);
+    HAR_CHECK_LAUNCH();
+    return 0;
+  }
   if (KP == 8)
     if (g_lr_stamps_grd)
       logreg_grad_kernel<8, true><<<grid, 256, 0, s>>>(a, g_lr_stamps_grd);
