@@ -30,6 +30,7 @@ import numpy as np
 import torch
 
 from ..data.split import kfold_ids, split_ids
+from ..ops import rng
 from ..data.table import Column, Table
 from ..models.base import Estimator, Model, dp_allreduce, dp_context, dp_rows, features_tensor, labels_tensor, \
     new_uid, num_label_classes, resolve_device
@@ -122,7 +123,16 @@ class CrossValidator(Estimator):
 
     def fit(self, table: Table) -> CrossValidatorModel:
         est, maps, ev, k = self.estimator, self.estimatorParamMaps, self.evaluator, self.numFolds
-        fold = kfold_ids(table.count(), k, self.seed)
+        n_rows = table.count()
+
+        def fold_ids_on(dev):
+            # the Philox fold assignment (data/split.py kfold_ids) on the device for the batched paths: the
+            # host form (numpy Philox + an upload) was ~0.5 ms of an ~4 ms LR CrossValidator fit with the
+            # GPU idle (profiles/r5/lr_grad_blocks.md); bitwise the same ids (tests/test_gpu_models.py)
+            if dev.type == "cuda":
+                return rng.device_buckets(self.seed, rng.STREAM_KFOLD, 0, n_rows, [1.0] * k, dev)
+            return torch.as_tensor(kfold_ids(n_rows, k, self.seed), device=dev)
+
         metrics = np.zeros((len(maps), k), dtype=np.float64)
         from ..models.logreg import FitSpec, LogisticRegression
 
@@ -134,7 +144,7 @@ class CrossValidator(Estimator):
             hm = hybrid_features(table, est.featuresCol, dev)
             y = labels_tensor(table, est.labelCol, dev)
             K = num_label_classes(table, est.labelCol, dev)
-            fold_t = torch.as_tensor(fold, device=dev)
+            fold_t = fold_ids_on(dev)
             in_fold = fold_t[None, :] == torch.arange(k, device=dev)[:, None]  # [k, N]: ONE launch, not k
             train_w = (~in_fold).float()
             specs, index = [], []
@@ -163,7 +173,7 @@ class CrossValidator(Estimator):
             # every (map, fold) model scored on its validation fold in ONE batched pass
             raw = _lr_margins(models, hm)                                          # [n, N, K]
             pred = _batched_predictions(models, raw)
-            mask = in_fold[torch.tensor([f for _, f in index], device=dev)]
+            mask = in_fold[torch.arange(len(index), device=dev) % k]  # fold of model i = i % k (no upload)
             vals = ev.evaluate_batched(y, pred, mask, K, raw)
             for (mi, f), v in zip(index, vals):
                 metrics[mi, f] = v
@@ -171,7 +181,7 @@ class CrossValidator(Estimator):
             # trees: every fold's tree(s) in one lock-step build; NaiveBayes: fold masks as row weights
             dev = resolve_device(est.device)
             X, y, K = est._prep(table)
-            fold_t = torch.as_tensor(fold, device=dev)
+            fold_t = fold_ids_on(dev)
             masks = torch.stack([(fold_t != f).float() for f in range(k)])
             for mi, pm in enumerate(maps):
                 fms = est.copy(pm).fit_folds(X, y, K, masks)
@@ -180,6 +190,7 @@ class CrossValidator(Estimator):
                 vals = ev.evaluate_batched(y, pred, masks == 0, K, torch.stack(raws))
                 metrics[mi, :] = vals
         else:
+            fold = kfold_ids(n_rows, k, self.seed)
             for f in range(k):
                 tr = table.take_rows(np.nonzero(fold != f)[0])
                 va = table.take_rows(np.nonzero(fold == f)[0])
