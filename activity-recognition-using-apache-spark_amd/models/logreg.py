@@ -343,6 +343,20 @@ class LogisticRegression(Estimator, ClassifierParams):
         B, D = len(specs), Kp * (F + 1)
         poll = 10 if self.maxIter > 20 else 0
         rounds = None
+
+        def finish_coefs(xs):
+            # every model's coefficients / intercepts in a few batched ops (per-model views below): a
+            # 45-model CrossValidator otherwise pays ~4 small launches per model on the host
+            xs = xs.view(B, Kp, F + 1) * pmask
+            coef_all = xs[:, :, :F] * inv_std[:, None, :]
+            icpt_all = xs[:, :, F].clone()
+            if binomial:
+                coef_all, icpt_all = coef_all[:, 1:2], icpt_all[:, 1:2]
+            elif self.fitIntercept:
+                icpt_all = icpt_all - icpt_all.mean(dim=1, keepdim=True)
+            return xs, coef_all, icpt_all
+
+        coefs_pre = None
         if wolfe:
             if design.native:  # the evaluation kernels at each round's trial points (+ the DP all-reduce)
                 solver = DeviceLogregSolver(design, B, 1, 10, inv_std, pmask, inv_wsum, l2v, l1v, self.maxIter,
@@ -379,6 +393,10 @@ class LogisticRegression(Estimator, ClassifierParams):
                                                             (inv_std, inv_wsum, pmask, l2v, l1v, x0)))
             xs, fobj, iters = solver.solve(x0, poll=poll)
             n_evals = solver.n_evals
+            # the coefficient post-processing enqueued BEFORE the host transfer below (its sync): these
+            # small kernels then run right behind the solve instead of one by one after it, with the GPU
+            # idle between Python launches (LR fit kernel trace, profiles/r5/lr_grad_blocks.md)
+            coefs_pre = finish_coefs(xs)
             # objective history, objectives and iteration counts to the host in ONE transfer
             packed = torch.cat([solver.hist.reshape(-1), fobj.double(), iters.double()]).cpu()
             nh = solver.hist.numel()
@@ -400,18 +418,10 @@ class LogisticRegression(Estimator, ClassifierParams):
                                         tol=self.tol, trials=T, poll=poll)
             xs, fobj, iters, n_evals = res.x, res.f, res.iterations, res.n_evals
             history = res.history_per_model  # each model's own objective per iteration
-        xs = xs.view(B, Kp, F + 1) * pmask
+        xs, coef_all, icpt_all = coefs_pre if coefs_pre is not None else finish_coefs(xs)
         models = []
         fobj_h = fobj.double().cpu()
         iters_h = iters.cpu()
-        # every model's coefficients / intercepts in a few batched ops (per-model views below): a
-        # 45-model CrossValidator otherwise pays ~4 small launches per model on the host
-        coef_all = xs[:, :, :F] * inv_std[:, None, :]
-        icpt_all = xs[:, :, F].clone()
-        if binomial:
-            coef_all, icpt_all = coef_all[:, 1:2], icpt_all[:, 1:2]
-        elif self.fitIntercept:
-            icpt_all = icpt_all - icpt_all.mean(dim=1, keepdim=True)
         # per-model views in one unbind each and the scalars as Python lists: per-model tensor indexing
         # was ~20 us of host time per model (a 54-model CrossValidator batch)
         coefs, icpts = coef_all.detach().unbind(0), icpt_all.detach().unbind(0)
