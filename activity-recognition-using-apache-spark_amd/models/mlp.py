@@ -144,13 +144,17 @@ class MLPEngine:
     """Device-resident training state + the fused native step."""
 
     def __init__(self, layers: Sequence[int], batch_size: int, device, lr=1e-3, betas=(0.9, 0.999), eps=1e-8,
-                 weight_decay=0.0, seed=0, process_group=None, world_size: int = 1):
+                 weight_decay=0.0, seed=0, process_group=None, world_size: int = 1, force_dp: bool = False):
         self.layout = FlatLayout(layers)
         self.device = torch.device(device)
         self.B = int(batch_size)
         self.lr, self.betas, self.eps, self.wd = lr, betas, eps, weight_decay
         self.pg = process_group
         self.world = world_size
+        # the DP step (collectives on process_group) runs at world > 1, or at world 1 when forced: a
+        # 1-rank RCCL group then carries the same reduce-scatter / all-gather (or all-reduce) calls,
+        # and the step must equal the N = 1 step bit for bit (tests/test_gpu_rccl.py)
+        self.dp = world_size > 1 or bool(force_dp)
         L = self.layout
         dev = self.device
         # Data parallel, sharded optimizer (ZeRO-1 style, the default for world > 1;
@@ -158,10 +162,21 @@ class MLPEngine:
         # chunk (chunk a multiple of 64 elements: 256-byte aligned slices), rank r owns
         # [r chunk, (r + 1) chunk) of P / m / v, the step is reduce-scatter(G) -> Adam on the owned
         # slice -> all-gather(P) -> bf16 / fragment refresh
-        self.sharded = world_size > 1 and os.environ.get("HAR_MLP_SHARDED_OPT", "1") != "0"
+        self.sharded = self.dp and os.environ.get("HAR_MLP_SHARDED_OPT", "1") != "0"
+        if world_size > 1:
+            # every rank must take the same step form (reduce-scatter + all-gather vs all-reduce) or the
+            # collectives mismatch and the job hangs: agree on it once (MIN and MAX of the flag)
+            import torch.distributed as tdist
+
+            from ..parallel import comm
+
+            fl = torch.tensor([int(self.sharded), -int(self.sharded)], dtype=torch.int32)
+            comm.all_reduce(fl, op=tdist.ReduceOp.MIN, group=process_group)
+            if int(fl[0]) != -int(fl[1]):
+                raise RuntimeError("HAR_MLP_SHARDED_OPT differs across ranks: the DP step forms would not match")
         n = L.total
-        self.chunk = -(-n // (64 * world_size)) * 64 if world_size > 1 else n
-        npad = self.chunk * world_size if world_size > 1 else n
+        self.chunk = -(-n // (64 * world_size)) * 64 if self.dp else n
+        npad = self.chunk * world_size if self.dp else n
         self.Pfull = torch.zeros(npad, dtype=torch.float32, device=dev)
         self.Gfull = torch.zeros(npad, dtype=torch.float32, device=dev)
         self.P = self.Pfull[:n]
@@ -227,7 +242,7 @@ class MLPEngine:
                 self._pack_frag()
             # small batches (B <= 512, B % 32 == 0, one GPU): the whole forward + backward of each 32-row
             # tile in one workgroup (mlp_small.hip) + the reduction / Adam kernel — two launches per step
-            self.small_ok = (self.fused_ok and L.hidden[0] in (128, 256) and self.world == 1
+            self.small_ok = (self.fused_ok and L.hidden[0] in (128, 256) and not self.dp
                              and os.environ.get("HAR_MLP_SMALL", "1") != "0")
             self.small_max = _native.kernels().mlp_small_step_max_batch() if self.small_ok else 0
             if self.small_ok:
@@ -302,6 +317,22 @@ class MLPEngine:
         if self.native:
             self.Pb.copy_(self.P.to(torch.bfloat16))
             self._pack_frag()
+
+    def _refresh_native(self):
+        """Pb and every fragment copy (W0 | W1 | W1^T) rebuilt from P by ONE kernel (grad_reduce_adam,
+        GR_REFRESH): the sharded DP step after its all-gather of P.  Bitwise the torch cast + pack
+        it replaces (the same round-to-nearest-even conversion)."""
+        dst, w0, w1, k0, h = self._frag_args()
+        if not dst and getattr(self, "Pf", None) is not None:  # (small path only: Pf without the step)
+            L = self.layout
+            dst, w0, w1, k0, h = self.Pf.data_ptr(), L.by_name["W0"].offset, L.by_name["W1"].offset, L.in_pad, L.hidden[0]
+        b1, b2 = self.betas
+        _native.kernels().grad_reduce_adam(
+            [], [], [], [], [], self.layout.total, self.G.data_ptr(), self.P.data_ptr(), self.m.data_ptr(),
+            self.v.data_ptr(), self.Pb.data_ptr(), float(self.lr), b1, b2, float(self.eps), float(self.wd),
+            self.step_count.data_ptr(), 0, self.GR_REFRESH, _native.stream_ptr(), dst, w0, w1, k0, h, 1 if dst else 0)
+        if dst:
+            self._pf_fresh = True
 
     def _slab(self, name):
         s = self.layout.by_name[name]
@@ -504,7 +535,7 @@ class MLPEngine:
             regions.append((bo, bo + 16, fs + 4 * 16 * H, self.fused_nwg, w))
         return regions
 
-    GR_REDUCE, GR_STORE, GR_ADAM = 1, 2, 4
+    GR_REDUCE, GR_STORE, GR_ADAM, GR_REFRESH = 1, 2, 4, 8
 
     def _grad_kernel(self, mode: int, tick: bool = False):
         """mlp.hip grad_reduce_adam: one deterministic single-level reduction of every gradient
@@ -532,16 +563,19 @@ class MLPEngine:
         step (default) is ONE reduce-scatter of the fp32 gradient + ONE all-gather of the fp32
         parameters (world x chunk elements each, ~0.34 MB for 43-256-256-6: latency-bound on xGMI,
         so one flat message each, no bucketing); HAR_MLP_SHARDED_OPT=0: ONE all-reduce of G."""
-        if self.world <= 1:
-            return {"all_reduce": 0, "bytes": 0}
+        if not self.dp:
+            return {"all_reduce": 0, "bytes": 0, "kernels": 3 if getattr(self, "step_ok", False) else None}
         if self.sharded:
             nb = int(self.Gfull.numel() * 4)
+            # kernels: forward, backward, reduction -> G | Adam on the owned slice | Pb + fragment refresh
             return {"all_reduce": 0, "reduce_scatter": 1, "all_gather": 1, "bytes": 2 * nb,
-                    "reduce_scatter_bytes": nb, "all_gather_bytes": nb, "world": self.world}
-        return {"all_reduce": 1, "bytes": int(self.G.numel() * 4), "world": self.world}
+                    "reduce_scatter_bytes": nb, "all_gather_bytes": nb, "world": self.world,
+                    "kernels": 5 if self.native else 0}
+        return {"all_reduce": 1, "bytes": int(self.G.numel() * 4), "world": self.world,
+                "kernels": 4 if self.native else 0}
 
     def allreduce_grads(self):
-        if self.world > 1:
+        if self.dp:
             from ..parallel import comm
             comm.all_reduce(self.G, group=self.pg)
 
@@ -556,7 +590,7 @@ class MLPEngine:
 
     def comm_phase(self):
         """The gradient collective of the DP step: reduce-scatter (sharded) or all-reduce of G."""
-        if self.world <= 1:
+        if not self.dp:
             return
         if not self.sharded:
             return self.allreduce_grads()
@@ -583,15 +617,14 @@ class MLPEngine:
     def gather_phase(self):
         """Sharded DP step, last part: all-gather of the owned fp32 parameter slices (every rank
         then holds the identical P) and the bf16 / fragment copies rebuilt from it."""
-        if not (self.world > 1 and self.sharded):
+        if not (self.dp and self.sharded):
             return
         from ..parallel import comm
 
         comm.all_gather_into_tensor(self.Pfull, self.Pfull[self.rank * self.chunk:(self.rank + 1) * self.chunk],
                                     group=self.pg)
         if self.native:
-            self.Pb.copy_(self.P)  # round-to-nearest-even, as the Adam kernel's own bf16 copy
-            self._pack_frag()
+            self._refresh_native()  # Pb + fragment copies: one kernel
 
     def _gather_moments(self):
         """Sharded optimizer: every rank's owned slices of m / v into the full vectors (a checkpoint
@@ -624,7 +657,7 @@ class MLPEngine:
         """DP step, part 3 (graph-capturable): Adam from the all-reduced G (part 2 is the RCCL
         collective, ``comm_phase``, issued eagerly between the two graph replays); sharded: Adam on
         this rank's slice, then ``gather_phase``."""
-        if self.world > 1 and self.sharded:
+        if self.dp and self.sharded:
             return self._adam_shard()
         if not self.native:
             return self._adam_torch()
@@ -665,7 +698,7 @@ class MLPEngine:
         update is fused into that kernel, at N > 1 it stores G, one RCCL all-reduce of G follows and
         Adam runs from G — the same kernels and the same summation order at every N.  The
         three-kernel step goes through the native plan (one host call per phase)."""
-        if self.native and self.world == 1 and self._small_ok(Xb, yb):
+        if self.native and not self.dp and self._small_ok(Xb, yb):
             return self._small_step(Xb, yb, global_batch)
         if self.native:
             self._pf_fresh = False  # (every other native path leaves the W1^T copy behind W1)
@@ -674,7 +707,7 @@ class MLPEngine:
             plan, self.step_nwg, self.step_S = self._plan(B)
             self.last_path, self.last_fused, self.last_bwd, self.last_batch = "step", True, True, B
             s = _native.stream_ptr()
-            if self.world > 1:
+            if self.dp:
                 plan.run(Xb.data_ptr(), yb.data_ptr(), B, 1.0 / global_batch, 2, s)
                 if self.sharded:
                     self.sharded_update()
@@ -686,7 +719,7 @@ class MLPEngine:
             return
         if self.native:
             self.forward_backward_native(Xb, yb, 1.0 / global_batch)
-            if self.world > 1:
+            if self.dp:
                 self.reduce_grads_native()
                 if self.sharded:
                     self.sharded_update()

@@ -29,7 +29,7 @@ def _import():
             import sys
             alt = os.environ.get("HAR_NATIVE_SO")
             if alt:
-                # A/B tooling only (tools/gpu_ab.sh): load another build of the extension, e.g. the
+                # A/B tooling only (tools/sessions/gpu_ab.sh): load another build of the extension, e.g. the
                 # previous commit's, so two builds are compared on the same GPU box; no source check
                 from importlib.machinery import ExtensionFileLoader
                 from importlib.util import module_from_spec, spec_from_file_location

@@ -37,7 +37,7 @@ from .dist import DistContext, shard_range
 
 
 def allreduce_sum(ctx: Optional[DistContext]):
-    if ctx is None or not ctx.is_distributed:
+    if ctx is None or not ctx.collective:
         return None
 
     def _ar(t: torch.Tensor):
@@ -65,7 +65,7 @@ def global_thresholds(X_shard: torch.Tensor, max_bins: int, ctx: DistContext, sa
     every rank, and every rank runs the device findSplits on it: the same thresholds as a
     single process, on every rank, without a broadcast."""
     X = X_shard.detach().float()
-    if not ctx.is_distributed:
+    if not ctx.collective:
         return T.thresholds_for(X, max_bins, sample_rows, seed)
     P = ctx.world_size
 
@@ -97,10 +97,13 @@ class NodeOwner:
 
     The send / receive buffers are grow-only workspaces kept for the lifetime of the object
     (one fit): a level reuses them as views instead of allocating and padding fresh tensors.
-    ``stats`` counts the collectives issued and their bytes (bench records)."""
+    ``stats`` counts the collectives issued and their bytes (bench records).  On a forced 1-rank
+    group (``HAR_DIST_FORCE_PG=1``) the collectives are issued too (an identity over one rank), so
+    the owner path runs through a real communicator on one GPU (tests/test_gpu_rccl.py)."""
 
     def __init__(self, ctx: DistContext):
         self.ctx = ctx
+        self.solo = ctx.world_size == 1 and not ctx.forced  # no group: nothing to reduce
         self.allreduce = allreduce_sum(ctx) or (lambda t: None)
         self._ws = {}
         self.stats = {"reduce_scatter": 0, "all_gather": 0, "bytes": 0}
@@ -122,7 +125,7 @@ class NodeOwner:
         A = hist.shape[0]
         S = max(1, -(-A // P))
         a0, a1 = min(A, r * S), min(A, (r + 1) * S)
-        if P == 1:
+        if self.solo:
             return hist, 0, A
         flat = hist.reshape(A, -1)
         w = flat.shape[1]
@@ -144,7 +147,7 @@ class NodeOwner:
         P, r = self.ctx.world_size, self.ctx.rank
         S = max(1, -(-A // P))
         a0, a1 = min(A, r * S), min(A, (r + 1) * S)
-        if P == 1:
+        if self.solo:
             return store[:A], 0, A
         w = store.shape[1]
         dev = self._dev() or store.device
@@ -193,7 +196,7 @@ class NodeOwner:
 
     def all_gather(self, local: torch.Tensor, A: int) -> torch.Tensor:
         P = self.ctx.world_size
-        if P == 1:
+        if self.solo:
             return local
         S = max(1, -(-A // P))
         inner = tuple(local.shape[1:])
@@ -213,7 +216,7 @@ def fit_forest_dp(estimator, X_shard, y_shard, num_classes: int, row_offset: int
                   reduction: str = "owner"):
     """``reduction``: ``owner`` (reduce-scatter + all-gather of winners) or ``allreduce``."""
     thr = global_thresholds(X_shard, estimator.maxBins, ctx, seed=estimator.seed)
-    if reduction == "owner" and ctx.is_distributed:
+    if reduction == "owner" and ctx.collective:
         return estimator.fit_tensors(X_shard, y_shard, num_classes, row_offset=row_offset, thresholds=thr,
                                      owner=NodeOwner(ctx))
     return estimator.fit_tensors(X_shard, y_shard, num_classes, allreduce=allreduce_sum(ctx), row_offset=row_offset,
@@ -237,7 +240,7 @@ def fit_forest_tree_parallel(estimator, X, y, num_classes: int, ctx: DistContext
     if thresholds is None:
         thresholds = T.thresholds_for(X, estimator.maxBins, seed=estimator.seed)
     part = estimator.fit_tensors(X, y, num_classes, thresholds=thresholds, tree_offset=lo, num_trees=hi - lo)
-    if not ctx.is_distributed:
+    if not ctx.collective:
         return part
     a = part.arrs
     S = -(-T_ // P)  # trees per rank, padded

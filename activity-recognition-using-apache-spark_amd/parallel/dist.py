@@ -7,7 +7,11 @@ WORLD_SIZE, MASTER_ADDR/PORT), pins the process to ``cuda:LOCAL_RANK`` and
 creates the process group: backend ``nccl`` — which IS RCCL on ROCm, running
 over xGMI between the GPUs of a node — when GPUs are present, ``gloo``
 otherwise (CPU tests exercise the same code path).  Without the env it is a
-single-process world of size 1 with no process group at all.
+single-process world of size 1 with no process group at all, unless
+``HAR_DIST_FORCE_PG=1``: then a 1-rank group is created anyway (RCCL on a GPU), so
+the collective paths — communicator setup, device-buffer reduce-scatter /
+all-gather, ``barrier(device_ids)``, host-scalar staging — run on one GPU
+(tests/test_gpu_rccl.py; ``DistContext.forced``).
 """
 from __future__ import annotations
 
@@ -28,10 +32,16 @@ class DistContext:
     device: torch.device
     backend: Optional[str]
     group: Optional[object] = None
+    forced: bool = False  # a 1-rank process group created by HAR_DIST_FORCE_PG=1
 
     @property
     def is_distributed(self) -> bool:
         return self.world_size > 1
+
+    @property
+    def collective(self) -> bool:
+        """True when the DP code paths issue real collectives: world > 1, or a forced 1-rank group."""
+        return self.world_size > 1 or self.forced
 
     @property
     def is_main(self) -> bool:
@@ -62,9 +72,12 @@ def init(expected_world: Optional[int] = None, backend: Optional[str] = None, de
     else:
         dev = torch.device("cpu")
     be = None
-    if world > 1:
+    forced = world == 1 and os.environ.get("HAR_DIST_FORCE_PG", "0") == "1"
+    if world > 1 or forced:
         be = backend or ("nccl" if use_cuda else "gloo")
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if forced and "MASTER_PORT" not in os.environ:
+            os.environ["MASTER_PORT"] = str(_free_port())
         kw = dict(backend=be, rank=rank, world_size=world, timeout=datetime.timedelta(seconds=timeout_s))
         if be == "nccl":
             kw["device_id"] = dev
@@ -78,11 +91,19 @@ def init(expected_world: Optional[int] = None, backend: Optional[str] = None, de
             kw["store"] = dist.PrefixStore(f"har/attempt{restart}", store)
         if not dist.is_initialized():
             dist.init_process_group(**kw)
-    return DistContext(rank, local_rank, world, dev, be, None)
+    return DistContext(rank, local_rank, world, dev, be, None, forced)
+
+
+def _free_port() -> int:
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
 
 
 def barrier(ctx: DistContext):
-    if ctx.is_distributed:
+    if ctx.collective:
         if ctx.backend == "nccl":
             dist.barrier(device_ids=[ctx.device.index])
         else:
@@ -95,7 +116,7 @@ def sync(device):
 
 
 def _reduce_scalar(ctx: DistContext, x: float, op) -> float:
-    if not ctx.is_distributed:
+    if not ctx.collective:
         return x
     from . import comm
 
@@ -117,7 +138,7 @@ def mean_over_ranks(ctx: DistContext, x: float) -> float:
 
 
 def shutdown(ctx: DistContext):
-    if ctx.is_distributed and dist.is_initialized():
+    if ctx.collective and dist.is_initialized():
         barrier(ctx)
         dist.destroy_process_group()
 

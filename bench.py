@@ -140,7 +140,8 @@ def bench_mlp(args, ctx):
     dev, rank, world = ctx.device, ctx.rank, ctx.world_size
     B = args.batch
     layers = [N_FEATURES, args.hidden, args.hidden, N_CLASSES]
-    eng = MLPEngine(layers, B, dev, lr=args.lr, seed=1234, process_group=ctx.group, world_size=world)
+    eng = MLPEngine(layers, B, dev, lr=args.lr, seed=1234, process_group=ctx.group, world_size=world,
+                    force_dp=ctx.forced)
     n_local = B * 8  # resident per-rank shard: 8 batches of windows
     X, y = synthetic_windows(n_local, seed=100 + rank, device=dev)
     Xin = pad_input_bf16(X, eng.layout.in_pad) if eng.native else X
@@ -210,8 +211,9 @@ def mlp_phase_times(ctx, eng, Xin, y32, B, nb, global_batch, n=50):
     sharded optimizer, the all-reduce otherwise), Adam (on this rank's slice when sharded), and
     ``all_gather`` (sharded: the all-gather of P + the bf16 / fragment refresh).  Device time from
     HIP events around each phase on the compute stream (host clock on the CPU path); mean per step,
-    max over ranks.  At N = 1 the collectives are absent and the N = 1 step fuses Adam into the
-    reduction kernel, so compute + adam there is the split form of the timed step (one extra launch)."""
+    max over ranks.  At N = 1 the collectives are absent (reported null, not as the HIP-event floor
+    of an empty interval) and the N = 1 step fuses Adam into the reduction kernel, so compute + adam
+    there is the split form of the timed step (one extra launch)."""
     from har.parallel import dist as hdist
 
     cuda = Xin.is_cuda
@@ -242,6 +244,12 @@ def mlp_phase_times(ctx, eng, Xin, y32, B, nb, global_batch, n=50):
             for q, k in enumerate(tot):
                 tot[k] += e[q].elapsed_time(e[q + 1])
     out = {k: hdist.max_over_ranks(ctx, v / n) for k, v in tot.items()}
+    # a collective the step does not issue is null, not the HIP-event floor of an empty interval
+    # (N = 1 without a forced group: neither; the all-reduce form: no all-gather)
+    if not getattr(eng, "dp", False):
+        out["allreduce"] = out["all_gather"] = None
+    elif not getattr(eng, "sharded", False):
+        out["all_gather"] = None
     out.update(steps=n, clock="HIP events" if cuda else "host", world=ctx.world_size)
     return out
 
@@ -662,6 +670,9 @@ def main():
 
         rec["reference_suite"] = run_reference_suite(ctx.device, args.wisdm, repeats=3, warmup=1)
     rec["bench_config"] = args.config
+    rec["dist_backend"] = ctx.backend  # None: one process, no group; "nccl" = RCCL
+    if ctx.forced:
+        rec["dist_forced_group"] = True  # HAR_DIST_FORCE_PG=1: a 1-rank RCCL group carried the DP collectives
     rec["device"] = torch.cuda.get_device_name(ctx.device) if ctx.device.type == "cuda" else "cpu"
     if ctx.rank == 0:
         line = json.dumps(rec)

@@ -657,8 +657,8 @@ PYBIND11_MODULE(_har_native, m) {
   m.def("grad_reduce_adam", [](std::vector<u> src, std::vector<int64_t> start, std::vector<int64_t> len,
                                std::vector<int64_t> lds, std::vector<int> nsl, int64_t n, u G, u param, u mm, u vv,
                                u pb, float lr, float b1, float b2, float eps, float wd, u step, int tick, int mode,
-                               u stream, u frag_dst, int64_t w0_off, int64_t w1_off, int fK0, int fH) {
-    const MlpFragSpec frag{P<uint16_t>(frag_dst), w0_off, w1_off, fK0, fH};
+                               u stream, u frag_dst, int64_t w0_off, int64_t w1_off, int fK0, int fH, int fw1t) {
+    const MlpFragSpec frag{P<uint16_t>(frag_dst), w0_off, w1_off, fK0, fH, fw1t};
     const int k = (int)src.size();
     if ((int)start.size() != k || (int)len.size() != k || (int)lds.size() != k || (int)nsl.size() != k)
       throw std::runtime_error("grad_reduce_adam: region lists differ in length");
@@ -671,7 +671,8 @@ PYBIND11_MODULE(_har_native, m) {
   }, py::arg("src"), py::arg("start"), py::arg("len"), py::arg("lds"), py::arg("nsl"), py::arg("n"), py::arg("G"),
      py::arg("param"), py::arg("m"), py::arg("v"), py::arg("pb"), py::arg("lr"), py::arg("b1"), py::arg("b2"),
      py::arg("eps"), py::arg("wd"), py::arg("step"), py::arg("tick"), py::arg("mode"), py::arg("stream"),
-     py::arg("frag_dst") = 0, py::arg("w0_off") = 0, py::arg("w1_off") = 0, py::arg("fK0") = 0, py::arg("fH") = 0);
+     py::arg("frag_dst") = 0, py::arg("w0_off") = 0, py::arg("w1_off") = 0, py::arg("fK0") = 0, py::arg("fH") = 0,
+     py::arg("fw1t") = 0);
   // small-batch step: the fused tile kernel, then ONE region reduction of its B / 32 slabs + Adam that
   // refreshes Pb and all three fragment copies (mlp_small.hip)
   m.def("mlp_small_step_max_batch", &har_mlp_small_step_max_batch);

@@ -240,6 +240,9 @@ __global__ void cast_pad_kernel(const float* __restrict__ in, int rows, int cin,
 //   GR_STORE   G[i] = g                                         (DP: before the all-reduce)
 //   GR_ADAM    Adam update of param / m / v / bf16 copy with t = *step (ticked earlier in the step
 //              by the fused backward kernel or adam_tick_kernel: no kernel both ticks and reads it)
+//   GR_REFRESH (alone) the bf16 copy and the fragment copies from param, no update: the sharded DP
+//              step after its all-gather of the fp32 parameters (one launch instead of a torch cast +
+//              the pack kernel)
 // A workgroup = GR_W (4 by default; 8 / 16 by HAR_GR_W) waves x 64 float4 columns: wave q sums slabs
 // q, q + GR_W, q + 2 GR_W, ... (eight loads in flight per step), the GR_W partials are added in a
 // fixed tree order -> bitwise reproducible, and N = 1 (GR_REDUCE |
@@ -247,7 +250,7 @@ __global__ void cast_pad_kernel(const float* __restrict__ in, int rows, int cin,
 // same Adam arithmetic.  With fragment copies (MlpFragSpec) the new bf16 values also go to the W0 and
 // W1 fragment copies (8-byte runs); the W1^T copy is written by the step's forward kernel, which
 // holds W1 in registers anyway (a tiled transposing variant of this kernel measured 1.5 us slower).
-constexpr int GR_REDUCE = 1, GR_STORE = 2, GR_ADAM = 4;
+constexpr int GR_REDUCE = 1, GR_STORE = 2, GR_ADAM = 4, GR_REFRESH = 8;
 template <int GR_W>  // waves per workgroup
 __global__ __launch_bounds__(64 * GR_W) void grad_reduce_adam_kernel(GradRegions rg, int64_t n, float* __restrict__ G,
                                                                 float* __restrict__ param, float* __restrict__ m,
@@ -258,6 +261,18 @@ __global__ __launch_bounds__(64 * GR_W) void grad_reduce_adam_kernel(GradRegions
   __shared__ float4 part[GR_W][64];
   const int q = threadIdx.x >> 6, k = threadIdx.x & 63;
   const int64_t i4 = (int64_t)blockIdx.x * 64 + k, e = i4 * 4;
+  if (mode == GR_REFRESH) {
+    if (q == 0 && e < n) {
+      const float4 pp = reinterpret_cast<const float4*>(param)[i4];
+      const ushort4 ob = make_ushort4(f2bf(pp.x), f2bf(pp.y), f2bf(pp.z), f2bf(pp.w));
+      reinterpret_cast<ushort4*>(pb)[i4] = ob;
+      if (frag.dst) {
+        if (frag.w1t) frag_store4<true>(frag, e, ob);
+        else frag_store4<false>(frag, e, ob);
+      }
+    }
+    return;
+  }
   // the Adam operands do not depend on the reduction: wave 0 issues their loads first, so their
   // latency overlaps the slab loads instead of following them
   const bool do_adam = q == 0 && e < n && (mode & GR_ADAM);
@@ -428,6 +443,7 @@ extern "C" int har_grad_reduce_adam(int nreg, const float* const* src, const int
                                     int32_t* step, int tick, int mode, const MlpFragSpec* frag_spec,
                                     hipStream_t s) {
   if (n % 4 || nreg < 0 || nreg > 8 || ((mode & GR_REDUCE) && nreg == 0)) return -2;
+  if ((mode & GR_REFRESH) && mode != GR_REFRESH) return -2;  // the refresh runs alone
   MlpFragSpec frag{};
   if (frag_spec && frag_spec->dst) {
     frag = *frag_spec;

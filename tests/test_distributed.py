@@ -319,3 +319,63 @@ def test_rf_parallel_modes_same_forest_at_n1():
                                     thresholds=thr)
     b = RandomForestClassifier(numTrees=6, maxDepth=4, seed=5).fit_tensors(X, y, 4, thresholds=thr)
     torch.testing.assert_close(a.predict_raw(X), b.predict_raw(X))
+
+
+def _forced_worker(rank, port, out_dir):
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        os.environ.pop(k, None)
+    os.environ.update(HAR_DIST_FORCE_PG="1", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.set_num_threads(1)
+    import torch.distributed as tdist
+
+    from har.models.mlp import MLPEngine
+    from har.parallel import comm
+    from har.parallel import data_parallel as dp
+    from har.parallel import dist as hd
+
+    ctx = hd.init(device="cpu")
+    res = {"forced": ctx.forced, "collective": ctx.collective, "backend": ctx.backend,
+           "initialized": tdist.is_initialized(), "allreduce_fn": dp.allreduce_sum(ctx) is not None,
+           "sum": hd.sum_over_ranks(ctx, 2.5)}
+    X, y = _data()
+    for sharded in ("1", "0"):
+        os.environ["HAR_MLP_SHARDED_OPT"] = sharded
+        a = MLPEngine([12, 32, 4], 128, "cpu", lr=1e-2, seed=1)
+        b = MLPEngine([12, 32, 4], 128, "cpu", lr=1e-2, seed=1, process_group=ctx.group, world_size=1, force_dp=True)
+        n = [0]
+        real = (comm.reduce_scatter_tensor, comm.all_reduce)
+
+        def rs(*x, **k):
+            n[0] += 1
+            return real[0](*x, **k)
+
+        def ar(*x, **k):
+            n[0] += 1
+            return real[1](*x, **k)
+
+        comm.reduce_scatter_tensor, comm.all_reduce = rs, ar
+        try:
+            for s in range(3):
+                a.train_step(X[s * 128:(s + 1) * 128], y[s * 128:(s + 1) * 128], 128)
+                b.train_step(X[s * 128:(s + 1) * 128], y[s * 128:(s + 1) * 128], 128)
+        finally:
+            comm.reduce_scatter_tensor, comm.all_reduce = real
+        res[f"equal_{sharded}"] = bool(torch.equal(a.P, b.P) and torch.equal(a.m, b.m) and torch.equal(a.v, b.v))
+        res[f"coll_{sharded}"] = n[0]
+        res[f"dp_{sharded}"] = (b.dp, b.sharded)
+    torch.save(res, os.path.join(out_dir, "forced.pt"))
+    hd.shutdown(ctx)
+
+
+def test_forced_one_rank_group_runs_the_dp_paths():
+    """HAR_DIST_FORCE_PG=1 at WORLD_SIZE 1: a 1-rank group (gloo here, RCCL on a GPU) is created, the
+    DP paths issue their collectives on it, and the DP MLP step (sharded and all-reduce) equals the
+    single-process step bit for bit."""
+    d = tempfile.mkdtemp()
+    mp.spawn(_forced_worker, args=(_free_port(), d), nprocs=1, join=True)
+    r = torch.load(os.path.join(d, "forced.pt"), weights_only=True)
+    assert r["forced"] and r["collective"] and r["backend"] == "gloo" and r["initialized"]
+    assert r["allreduce_fn"] and r["sum"] == 2.5
+    assert r["equal_1"] and r["equal_0"], r
+    assert r["coll_1"] == 3 and r["coll_0"] == 3, r  # one gradient collective per step
+    assert tuple(r["dp_1"]) == (True, True) and tuple(r["dp_0"]) == (True, False)

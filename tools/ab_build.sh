@@ -1,5 +1,5 @@
 #!/bin/bash
-# Build the native extension of another commit into ab/<name>/_har_native.so (for tools/gpu_ab.sh):
+# Build the native extension of another commit into ab/<name>/_har_native.so (for tools/sessions/gpu_ab.sh):
 #   bash tools/ab_build.sh <commit> <name>
 set -eu
 ROOT="$(cd "$(dirname "$0")/.." && pwd)"

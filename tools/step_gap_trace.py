@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Timeline of the MLP step kernels in a rocprofv3 kernel trace of bench.py (tools/gpu_step_gaps.sh):
+"""Timeline of the MLP step kernels in a rocprofv3 kernel trace of bench.py (tools/sessions/gpu_step_gaps.sh):
 per step the start offset, each kernel's duration and the idle gap before it, so the driver window's
 fixed cost (first-launch latency, slow first steps, gaps) is visible.
 usage: python tools/step_gap_trace.py <r_kernel_trace.csv> [n_steps]"""
