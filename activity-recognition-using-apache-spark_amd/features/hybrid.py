@@ -136,3 +136,21 @@ def hybrid_features(table, col: str, device) -> HybridMatrix:
     if c.cache is not None:
         c.cache[key] = hm
     return hm
+
+
+def tree_hybrid(table, col: str, device) -> Optional[HybridMatrix]:
+    """The HybridMatrix of ``col`` when it has one-hot blocks (the device assembler's layout, or its
+    assembler metadata), else None — a plain numeric column is not copied into a hybrid form."""
+    from ..data.table import DeviceColumn
+
+    c = table[col]
+    if c.kind != "vector":
+        return None
+    if isinstance(c, DeviceColumn):
+        hm = c.hybrid
+        if str(hm.device) == str(torch.device(device)) and hm.cat.shape[1] > 0:
+            return hm
+    if not onehot_blocks((c.meta or {}).get("structure")):
+        return None
+    hm = hybrid_features(table, col, device)
+    return hm if hm.cat.shape[1] > 0 else None

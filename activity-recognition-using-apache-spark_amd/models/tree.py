@@ -114,9 +114,32 @@ class ForestBuilder:
         if owner is not None and allreduce is None:
             self.allreduce = owner.allreduce
 
-    def prepare(self, X: torch.Tensor, thresholds=None):
+    def prepare(self, X: torch.Tensor, thresholds=None, hybrid=None):
         from ..ops.stats import bin_features
 
+        self.sparse = None
+        if (hybrid is not None and X.is_cuda and T.hybrid_tree_ok(hybrid) and hybrid.n_rows == X.shape[0]
+                and self.max_bins <= 32):
+            # one-hot-aware path (ops/tree.py): findSplits sorts the numeric block only (on the device,
+            # no host round trip), the bins come from the hybrid parts, the level histograms of the
+            # one-hot columns run over their entries
+            if thresholds is None:
+                thresholds = (T.thresholds_hybrid_device(hybrid, self.max_bins, seed=self.seed)
+                              or T.find_thresholds_hybrid(hybrid, self.max_bins, seed=self.seed))
+            if isinstance(thresholds, T.DeviceThresholds) and thresholds.thr_mat.shape[1] == self.max_bins:
+                self.thresholds = thresholds
+                self.nbins, self.thr_mat = thresholds.nbins, thresholds.thr_mat
+            else:
+                if isinstance(thresholds, T.DeviceThresholds):
+                    thresholds = thresholds.to_table()
+                self.thresholds = tt = T.ThresholdTable.from_any(thresholds)
+                self.nbins = torch.from_numpy((tt.counts + 1).astype(np.int32)).to(X.device)
+                self.thr_mat = torch.from_numpy(tt.padded(self.max_bins)).to(X.device)
+            self.bins = T.bins_hybrid(hybrid, self.thr_mat, self.nbins)
+            self.sparse = T.sparse_tree_input(hybrid)
+            return
+        if isinstance(thresholds, T.DeviceThresholds):
+            thresholds = thresholds.to_table()
         if thresholds is None:
             # GPU: device findSplits (one sort, one small copy back; the same thresholds)
             thresholds = T.thresholds_for(X, self.max_bins, seed=self.seed)
@@ -133,12 +156,13 @@ class ForestBuilder:
                                                       N, row_offset, self.cdf)).float().to(device)
 
     def fit(self, X: torch.Tensor, y: torch.Tensor, row_offset: int = 0, thresholds=None,
-            row_weight: Optional[torch.Tensor] = None) -> ForestArrays:
+            row_weight: Optional[torch.Tensor] = None, hybrid=None) -> ForestArrays:
         """``row_weight`` [T, N] multiplies the bootstrap weights (0 = row not seen by that
-        tree): the cross-validation folds of several forests grow in one lock-step build."""
+        tree): the cross-validation folds of several forests grow in one lock-step build.
+        ``hybrid`` (features.hybrid.HybridMatrix of the same rows as X): the one-hot-aware path."""
         dev = X.device
         N, F = X.shape
-        self.prepare(X, thresholds)
+        self.prepare(X, thresholds, hybrid)
         Tn, K, D = self.T, self.K, self.D
         m = subset_size(self.subset, F, Tn)
         y32 = y.to(torch.int32).contiguous()
@@ -324,7 +348,10 @@ def _levels_device_frontier(b: "ForestBuilder", y32, W, N: int, F: int, m: int, 
     st = _native.stream_ptr()
     i32 = dict(dtype=torch.int32, device=dev)
     Wf = W.reshape(-1).contiguous()
-    bins_rm = b.bins.t().contiguous()  # [N, F] for the histogram gathers (partition keeps [F, N])
+    sparse = getattr(b, "sparse", None)
+    # [N, F] for the histogram gathers (partition keeps [F, N]); the one-hot-aware kernel gathers only
+    # the numeric columns' bytes and reads the feature-major bins
+    bins_rm = b.bins.t().contiguous() if sparse is None else None
     nch = mod.tree_level_group_chunks(N)
     nch_g = mod.tree_level_group_chunks(n_all)  # rank-independent bound checks (DP: every rank decides alike)
     planned = not FORCE_NODE_BLOCKS
@@ -403,18 +430,19 @@ def _levels_device_frontier(b: "ForestBuilder", y32, W, N: int, F: int, m: int, 
                                           bins_rm=bins_rm,
                                           # fp16 transport only for integer counts (exact below 2048)
                                           max_weight=max_w if exact and getattr(b, "int_weights", False) else -1.0,
-                                          node_cc=node_cc)
+                                          node_cc=node_cc, sparse=sparse)
         elif planned:
             # one device: work items by rows (big nodes chunked), no host sync (ops/tree.py)
             res = T.hist_split_planned(b.bins, b.nbins, y32, rows, row_w, starts, counts, feats, K, b.max_bins,
                                        b.min_inst, b.min_gain, b.impurity, rows_bound=Tn * N, bins_rm=bins_rm,
+                                       prows=T.PLAN_ROWS if sparse is None else T.SPARSE_PLAN_ROWS,
                                        a_dev=a_dev, store=store, hprev=hprev, derive_from=derive_from,
-                                       parent_of=parent_of)
+                                       parent_of=parent_of, sparse=sparse)
         else:
             res = T.hist_split_native(b.bins, b.nbins, y32, rows, row_w, starts, counts, feats, K, b.max_bins,
                                       b.min_inst, b.min_gain, b.impurity,
                                       allreduce=None if b.owner is not None else b.allreduce, owner=b.owner,
-                                      max_rows=int(max_w), check_labels=False, bins_rm=bins_rm)
+                                      max_rows=int(max_w), check_labels=False, bins_rm=bins_rm, sparse=sparse)
         res = T.LevelResult(gain=res.gain.contiguous(), feat=res.feat.contiguous(), bin=res.bin.contiguous(),
                             left=res.left.contiguous(), total=res.total.contiguous())
         dec = torch.empty(5, A, dtype=torch.float32, device=dev)
@@ -509,6 +537,10 @@ class _FitGraph:
         self.thr_mat = torch.empty_like(b.thr_mat)
         self.y32 = torch.empty_like(y32)
         self.rw = None if rw is None else torch.empty_like(rw)
+        sp = getattr(b, "sparse", None)
+        # the one-hot-aware kernels' inputs are baked into the graph too: static copies
+        self.sparse = None if sp is None else T.SparseTreeInput(torch.empty_like(sp.cat), torch.empty_like(sp.onehot),
+                                                                 sp.n_features)
         self.bufs = _alloc_fit_buffers(Tn, N, K, maxn, dev)
         self.graph = None
         self.maxn = maxn
@@ -520,18 +552,37 @@ class _FitGraph:
         self.y32.copy_(y32)
         if rw is not None:
             self.rw.copy_(rw)
+        if self.sparse is not None:
+            self.sparse.cat.copy_(b.sparse.cat)
+            self.sparse.onehot.copy_(b.sparse.onehot)
+
+
+_OUT_ARRAYS = (("feature", torch.int32, False), ("thresh", torch.float32, False), ("left", torch.int32, False),
+               ("right", torch.int32, False), ("stats", torch.float32, True), ("gains", torch.float32, False))
 
 
 def _alloc_fit_buffers(Tn: int, N: int, K: int, maxn: int, dev) -> dict:
-    return dict(W=torch.empty(Tn, N, dtype=torch.float32, device=dev),
+    """Work arrays of one device fit; the six output arrays are views of ONE flat 32-bit buffer
+    (``out``), so a fit's result is one clone, not six."""
+    per = Tn * maxn
+    sizes = [per * K if wide else per for _, _, wide in _OUT_ARRAYS]
+    flat = torch.empty(sum(sizes), dtype=torch.int32, device=dev)
+    bufs = dict(W=torch.empty(Tn, N, dtype=torch.float32, device=dev),
                 node_of=torch.empty(Tn, N, dtype=torch.int32, device=dev),
-                bad=torch.empty(1, dtype=torch.int32, device=dev),
-                feature=torch.empty(Tn, maxn, dtype=torch.int32, device=dev),
-                thresh=torch.empty(Tn, maxn, dtype=torch.float32, device=dev),
-                left=torch.empty(Tn, maxn, dtype=torch.int32, device=dev),
-                right=torch.empty(Tn, maxn, dtype=torch.int32, device=dev),
-                stats=torch.empty(Tn, maxn, K, dtype=torch.float32, device=dev),
-                gains=torch.empty(Tn, maxn, dtype=torch.float32, device=dev))
+                bad=torch.empty(1, dtype=torch.int32, device=dev), out=flat)
+    bufs.update(_out_views(flat, Tn, maxn, K))
+    return bufs
+
+
+def _out_views(flat: torch.Tensor, Tn: int, maxn: int, K: int) -> dict:
+    views, o = {}, 0
+    for (name, dt, wide) in _OUT_ARRAYS:
+        n = Tn * maxn * (K if wide else 1)
+        v = flat[o:o + n]
+        v = v.view(torch.float32) if dt == torch.float32 else v
+        views[name] = v.view(Tn, maxn, K) if wide else v.view(Tn, maxn)
+        o += n
+    return views
 
 
 def _enqueue_fit(b: "ForestBuilder", bufs: dict, y32, rw, row_offset: int, N: int, F: int, m: int, maxn: int,
@@ -540,9 +591,8 @@ def _enqueue_fit(b: "ForestBuilder", bufs: dict, y32, rw, row_offset: int, N: in
     arrays, tree_init (bootstrap weights x row weights, node ids, root class counts, label check), the
     DP all-reduce of the root counts, the level loop.  Returns the node-count tensor."""
     Tn, K = b.T, b.K
+    bufs["out"].zero_()  # (thresh / left / right / stats / gains; one fill)
     bufs["feature"].fill_(-1)
-    for k in ("thresh", "left", "right", "stats", "gains"):
-        bufs[k].zero_()
     bufs["bad"].zero_()
     cdf = [] if b.cdf is None else [int(v) for v in b.cdf]
     _native.kernels().tree_init(b.seed, b.tree_offset, Tn, row_offset, N, cdf, 0 if rw is None else rw.data_ptr(),
@@ -568,7 +618,8 @@ def _finish_fit(b: "ForestBuilder", bufs: dict, nn, clone: bool) -> ForestArrays
     h = torch.cat([nn, bufs["bad"]]).cpu().numpy()  # the fit's one device -> host read
     if h[-1] != 0:
         raise ValueError("labels out of range")
-    o = {k: (v.clone() if clone else v) for k, v in bufs.items()}
+    Tn, maxn = bufs["feature"].shape
+    o = _out_views(bufs["out"].clone(), Tn, maxn, b.K) if clone else bufs
     return ForestArrays(o["feature"], o["thresh"], o["left"], o["right"], o["stats"], h[:-1].astype(np.int64), b.D,
                         o["gains"])
 
@@ -583,14 +634,15 @@ def _fit_device(b: "ForestBuilder", y32, rw, row_offset: int, N: int, F: int, m:
         key = (dev.index, b.T, b.K, b.D, N, F, m, maxn, b.max_bins, b.impurity, b.min_inst, b.min_gain, b.seed,
                b.tree_offset, None if b.cdf is None else tuple(int(v) for v in b.cdf), rw is not None, row_offset,
                SIBLING_SUBTRACTION, SUBTRACT_MIN_PAIRS, SUBTRACT_MAX_BYTES, ASYNC_MAX_NODES, ASYNC_MAX_COUNT_WS,
-               b.bins.shape, tuple(b.thr_mat.shape))
+               b.bins.shape, tuple(b.thr_mat.shape),
+               None if getattr(b, "sparse", None) is None else tuple(b.sparse.cat.shape))
     ent = _fit_graphs.get(key) if key is not None else None
     if ent is None and key is not None and _fit_graph_seen.get(key, 0) >= 1 and len(_fit_graphs) < FIT_GRAPH_MAX:
         # second fit of this signature: capture it (the first, eager fit warmed every kernel up)
         ent = _FitGraph(b, y32, rw, N, F, maxn)
         ent.load(b, y32, rw)
-        own = (b.bins, b.nbins, b.thr_mat)
-        b.bins, b.nbins, b.thr_mat = ent.bins, ent.nbins, ent.thr_mat
+        own = (b.bins, b.nbins, b.thr_mat, getattr(b, "sparse", None))
+        b.bins, b.nbins, b.thr_mat, b.sparse = ent.bins, ent.nbins, ent.thr_mat, ent.sparse
         try:
             torch.cuda.synchronize(dev)
             g = torch.cuda.CUDAGraph()
@@ -598,7 +650,7 @@ def _fit_device(b: "ForestBuilder", y32, rw, row_offset: int, N: int, F: int, m:
                 ent.nn = _enqueue_fit(b, ent.bufs, ent.y32, ent.rw, row_offset, N, F, m, maxn, n_all)
             ent.graph = g
         finally:
-            b.bins, b.nbins, b.thr_mat = own
+            b.bins, b.nbins, b.thr_mat, b.sparse = own
         _fit_graphs[key] = ent
         LAST_FIT_KIND = "capture"
     elif ent is not None:
@@ -717,6 +769,20 @@ class _TreeEstimatorBase(Estimator, ClassifierParams):
         K = num_label_classes(table, self.labelCol, dev)
         return X, y, K
 
+    def _hybrid(self, table: Table, device):
+        """The column's one-hot index + numeric layout when it has one-hot blocks (the reference
+        encoding) and the one-hot-aware tree path takes it, else None (features.hybrid)."""
+        from ..features.hybrid import tree_hybrid
+
+        hm = tree_hybrid(table, self.featuresCol, device)
+        return hm if T.hybrid_tree_ok(hm) else None
+
+    def _thresholds(self, X, hybrid):
+        if hybrid is not None:
+            return (T.thresholds_hybrid_device(hybrid, self.maxBins, seed=self.seed)
+                    or T.find_thresholds_hybrid(hybrid, self.maxBins, seed=self.seed))
+        return T.thresholds_for(X, self.maxBins, seed=self.seed)
+
 
 class DecisionTreeClassifier(_TreeEstimatorBase):
     def __init__(self, featuresCol="features", labelCol="label", maxDepth: int = 5, maxBins: int = 32,
@@ -729,25 +795,27 @@ class DecisionTreeClassifier(_TreeEstimatorBase):
 
     def fit(self, table: Table) -> DecisionTreeClassificationModel:
         X, y, K = self._prep(table)
+        hm = self._hybrid(table, X.device)
         if dp_context() is None:
-            return self.fit_tensors(X, y, K)
-        thr = T.thresholds_for(X, self.maxBins, seed=self.seed)
+            return self.fit_tensors(X, y, K, hybrid=hm)
+        thr = self._thresholds(X, hm)
         lo, hi = dp_rows(X.shape[0])
-        return self.fit_tensors(X[lo:hi], y[lo:hi], K, thresholds=thr, owner=dp_owner(), row_offset=lo)
+        return self.fit_tensors(X[lo:hi], y[lo:hi], K, thresholds=thr, owner=dp_owner(), row_offset=lo,
+                                hybrid=None if hm is None else hm.rows(lo, hi))
 
     def fit_tensors(self, X, y, K, thresholds=None, allreduce=None, owner=None,
-                    row_offset: int = 0) -> DecisionTreeClassificationModel:
+                    row_offset: int = 0, hybrid=None) -> DecisionTreeClassificationModel:
         b = ForestBuilder(K, 1, self.maxDepth, self.maxBins, self.minInstancesPerNode, self.minInfoGain,
                           self.impurity, "all", bootstrap=False, seed=self.seed, allreduce=allreduce, owner=owner)
-        return DecisionTreeClassificationModel(b.fit(X, y, row_offset=row_offset, thresholds=thresholds), X.shape[1],
-                                               K, uid=self.uid, device=X.device)
+        return DecisionTreeClassificationModel(b.fit(X, y, row_offset=row_offset, thresholds=thresholds, hybrid=hybrid),
+                                               X.shape[1], K, uid=self.uid, device=X.device)
 
-    def fit_folds(self, X, y, K, masks: torch.Tensor) -> List["DecisionTreeClassificationModel"]:
+    def fit_folds(self, X, y, K, masks: torch.Tensor, hybrid=None) -> List["DecisionTreeClassificationModel"]:
         """One tree per fold (``masks`` [k, N]: 1 = training row of fold f), all grown together
         (data parallel inside ``data_parallel``: row shards, owner-computes splits)."""
         b = ForestBuilder(K, masks.shape[0], self.maxDepth, self.maxBins, self.minInstancesPerNode, self.minInfoGain,
                           self.impurity, "all", bootstrap=False, seed=self.seed, owner=dp_owner())
-        arrs = _fit_sharded(b, X, y, masks, self.maxBins, self.seed)
+        arrs = _fit_sharded(b, X, y, masks, self.maxBins, self.seed, hybrid)
         return [DecisionTreeClassificationModel(_slice_arrays(arrs, f, f + 1), X.shape[1], K, uid=self.uid,
                                                 device=X.device) for f in range(masks.shape[0])]
 
@@ -797,28 +865,33 @@ class RandomForestClassifier(_TreeEstimatorBase):
 
     def fit(self, table: Table) -> RandomForestClassificationModel:
         X, y, K = self._prep(table)
+        hm = self._hybrid(table, X.device)
         ctx = dp_context()
         if ctx is None:
-            return self.fit_tensors(X, y, K)
-        thr = T.thresholds_for(X, self.maxBins, seed=self.seed)
+            return self.fit_tensors(X, y, K, hybrid=hm)
+        thr = self._thresholds(X, hm)
         if self.resolve_parallelism(X.shape[0], X.shape[1], ctx.world_size) == "tree":
             from ..parallel.data_parallel import fit_forest_tree_parallel
 
-            return fit_forest_tree_parallel(self, X, y, K, ctx, thresholds=thr)
+            return fit_forest_tree_parallel(self, X, y, K, ctx, thresholds=thr, hybrid=hm)
         lo, hi = dp_rows(X.shape[0])
-        return self.fit_tensors(X[lo:hi], y[lo:hi], K, row_offset=lo, thresholds=thr, owner=dp_owner())
+        return self.fit_tensors(X[lo:hi], y[lo:hi], K, row_offset=lo, thresholds=thr, owner=dp_owner(),
+                                hybrid=None if hm is None else hm.rows(lo, hi))
 
     def fit_tensors(self, X, y, K, allreduce=None, row_offset: int = 0, thresholds=None,
                     tree_wave: int = 0, checkpoint_dir: Optional[str] = None, rank: int = 0, owner=None,
-                    tree_offset: int = 0, num_trees: Optional[int] = None):
+                    tree_offset: int = 0, num_trees: Optional[int] = None, hybrid=None):
         """Grow the forest (all trees in lock step, or in waves of ``tree_wave`` trees —
         each wave checkpointed under ``checkpoint_dir`` and skipped on resume).  Trees
-        are keyed by their global id, so a waved forest equals the one-shot forest."""
+        are keyed by their global id, so a waved forest equals the one-shot forest.
+        ``hybrid``: the one-hot-aware path (same forest)."""
         strategy = self.featureSubsetStrategy
         if str(strategy).lower() == "auto":
             strategy = "all" if self.numTrees == 1 else "sqrt"
+        if hybrid is not None and not (X.is_cuda and T.hybrid_tree_ok(hybrid)):
+            hybrid = None
         if thresholds is None:
-            thresholds = T.thresholds_for(X, self.maxBins, seed=self.seed)
+            thresholds = self._thresholds(X, hybrid)
         # tree-parallel mode grows trees [tree_offset, tree_offset + num_trees) of the forest: global tree
         # ids key the bootstrap and feature-subset streams, so the slices concatenate into the forest
         total = self.numTrees if num_trees is None else int(num_trees)
@@ -862,7 +935,7 @@ class RandomForestClassifier(_TreeEstimatorBase):
                               self.impurity, strategy, bootstrap=self.numTrees > 1, seed=self.seed,
                               allreduce=allreduce, tree_offset=tree_offset + done, owner=owner,
                               subsample=self.subsamplingRate)
-            parts.append(b.fit(X, y, row_offset=row_offset, thresholds=thresholds))
+            parts.append(b.fit(X, y, row_offset=row_offset, thresholds=thresholds, hybrid=hybrid))
             done += nt
             if ckpt is not None and done < total:
                 merged = _concat_arrays(parts)
@@ -871,7 +944,7 @@ class RandomForestClassifier(_TreeEstimatorBase):
         arrs = _concat_arrays(parts) if len(parts) > 1 else parts[0]
         return RandomForestClassificationModel(arrs.to(X.device), X.shape[1], K, uid=self.uid, device=X.device)
 
-    def fit_folds(self, X, y, K, masks: torch.Tensor) -> List["RandomForestClassificationModel"]:
+    def fit_folds(self, X, y, K, masks: torch.Tensor, hybrid=None) -> List["RandomForestClassificationModel"]:
         """k forests of numTrees trees (fold f: trees f*T .. f*T+T-1, its own bootstrap / feature
         streams) grown as ONE level-synchronous build of k*T trees over the shared binned matrix."""
         T_, k = self.numTrees, masks.shape[0]
@@ -881,19 +954,24 @@ class RandomForestClassifier(_TreeEstimatorBase):
         b = ForestBuilder(K, k * T_, self.maxDepth, self.maxBins, self.minInstancesPerNode, self.minInfoGain,
                           self.impurity, strategy, bootstrap=T_ > 1, seed=self.seed, owner=dp_owner(),
                           subsample=self.subsamplingRate)
-        arrs = _fit_sharded(b, X, y, masks.repeat_interleave(T_, dim=0), self.maxBins, self.seed)
+        arrs = _fit_sharded(b, X, y, masks.repeat_interleave(T_, dim=0), self.maxBins, self.seed, hybrid)
         return [RandomForestClassificationModel(_slice_arrays(arrs, f * T_, (f + 1) * T_), X.shape[1], K, uid=self.uid,
                                                 device=X.device) for f in range(k)]
 
 
-def _fit_sharded(b: "ForestBuilder", X, y, row_weight, max_bins: int, seed: int) -> ForestArrays:
+def _fit_sharded(b: "ForestBuilder", X, y, row_weight, max_bins: int, seed: int, hybrid=None) -> ForestArrays:
     """``b.fit`` over the whole matrix, or — inside ``data_parallel`` — over this rank's
     row shard (thresholds from the whole matrix, so every rank bins identically)."""
+    if hybrid is not None and not (X.is_cuda and T.hybrid_tree_ok(hybrid)):
+        hybrid = None
     if dp_context() is None:
-        return b.fit(X, y, row_weight=row_weight)
-    thr = T.thresholds_for(X, max_bins, seed=seed)
+        return b.fit(X, y, row_weight=row_weight, hybrid=hybrid)
+    thr = ((T.thresholds_hybrid_device(hybrid, max_bins, seed=seed) or T.find_thresholds_hybrid(hybrid, max_bins,
+                                                                                                seed=seed))
+           if hybrid is not None else T.thresholds_for(X, max_bins, seed=seed))
     lo, hi = dp_rows(X.shape[0])
-    return b.fit(X[lo:hi], y[lo:hi], row_offset=lo, thresholds=thr, row_weight=row_weight[:, lo:hi])
+    return b.fit(X[lo:hi], y[lo:hi], row_offset=lo, thresholds=thr, row_weight=row_weight[:, lo:hi],
+                 hybrid=None if hybrid is None else hybrid.rows(lo, hi))
 
 
 def _slice_arrays(a: ForestArrays, lo: int, hi: int) -> ForestArrays:

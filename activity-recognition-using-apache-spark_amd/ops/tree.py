@@ -200,6 +200,153 @@ def bin_features(X: np.ndarray, thresholds) -> np.ndarray:
     return bins
 
 
+# ---------------------------------------------------------------------------------------------------
+# One-hot-aware findSplits / binning / histograms for hybrid matrices (features.hybrid.HybridMatrix:
+# the reference encoding — three one-hot blocks of 934 + 1401 + 755 binary columns beside 10 numeric
+# ones, Main/main.py:51-66).  Spark grows its trees on these columns as categorical features of arity 2
+# (the OneHotEncoder's attribute metadata: SURVEY.md N8, §3.4), so a one-hot column's only split is
+# 0 | 1 — threshold 0.5 here, the midpoint find_thresholds takes for the two distinct values.  Nothing
+# needs a sort for them: a column has its split iff the sampled rows hold both values (0 < ones < n).
+# The forest is bit-identical to the dense path's (tests/test_gpu_tree_sparse.py).
+SPARSE_TREES = os.environ.get("HAR_TREE_SPARSE", "1") != "0"
+SPARSE_MAX_NCAT = 4  # tree.hip SP_NCAT
+
+
+@dataclass
+class SparseTreeInput:
+    """What the one-hot-aware level kernels read beside the bins: the rows' one-hot entries and the
+    one-hot column flags."""
+    cat: torch.Tensor     # [N, ncat] int32 global column of each row's 1 per block (-1 none)
+    onehot: torch.Tensor  # [F] uint8, 1 = one-hot column
+    n_features: int
+
+
+def sparse_args(sparse: Optional[SparseTreeInput]):
+    if sparse is None:
+        return (0, 0, 0)
+    return (sparse.cat.data_ptr(), int(sparse.cat.shape[1]), sparse.onehot.data_ptr())
+
+
+def hybrid_tree_ok(hm) -> bool:
+    """A hybrid matrix the one-hot-aware tree path takes: on a GPU, 1..SPARSE_MAX_NCAT one-hot blocks."""
+    return (SPARSE_TREES and hm is not None and hm.device.type == "cuda"
+            and 0 < int(hm.cat.shape[1]) <= SPARSE_MAX_NCAT and hm.n_features <= 32767)
+
+
+def find_thresholds_hybrid(hm, max_bins: int, sample_rows: int = 10000, seed: int = 0, row_offset: int = 0,
+                           n_total: int = None) -> "ThresholdTable":
+    """``find_thresholds`` of ``hm.to_dense()`` without densifying: the same Philox row sample, the
+    device findSplits of the numeric block alone, and for every one-hot column the 0 | 1 split when
+    the sampled rows hold both values (ones counted from the rows' one-hot entries)."""
+    N, F = hm.n_rows, hm.n_features
+    dev = hm.device
+    ns = max_bins - 1
+    keep = threshold_sample_mask(N, max_bins, sample_rows, seed, row_offset, n_total, device=dev)
+    dense = hm.dense if keep is None else hm.dense[keep]
+    cat = hm.cat if keep is None else hm.cat[keep]
+    n = int(cat.shape[0])
+    counts = np.zeros(F, dtype=np.int64)
+    mat = np.full((F, max(1, ns)), np.inf, dtype=np.float32)
+    if n == 0 or ns <= 0:
+        return ThresholdTable(mat, counts)
+    cv = cat.reshape(-1)
+    ones = torch.bincount(cv[cv >= 0].long(), minlength=F)[:F]
+    has = ((ones > 0) & (ones < n)).cpu().numpy()
+    counts[has] = 1
+    mat[has, 0] = np.float32(0.5)
+    dcols = hm.dense_cols.cpu().numpy().astype(np.int64)
+    if len(dcols):
+        # the numeric block's findSplits on the rows already sampled (no second draw)
+        td = ThresholdTable.from_any(find_thresholds_device(dense.contiguous(), max_bins, sample_rows=max(sample_rows, n),
+                                                            seed=seed))
+        w = td.mat.shape[1]
+        counts[dcols] = td.counts
+        mat[dcols, :min(w, mat.shape[1])] = td.mat[:, :mat.shape[1]]
+    return ThresholdTable(mat, counts)
+
+
+@dataclass
+class DeviceThresholds:
+    """findSplits' result kept on the device: ``thr_mat`` [F, W] fp32 (+inf padded) and ``nbins`` [F]
+    int32 (thresholds + 1) — what the forest builder uploads from a ThresholdTable, without the host
+    round trip."""
+    thr_mat: torch.Tensor
+    nbins: torch.Tensor
+
+    def to_table(self) -> "ThresholdTable":
+        cnt = (self.nbins.cpu().numpy() - 1).astype(np.int64)
+        return ThresholdTable(self.thr_mat.cpu().numpy(), cnt)
+
+
+def _hybrid_static(hm):
+    """Per-matrix device constants of the one-hot-aware path (memoized on the immutable matrix): the
+    int32 one-hot entries, the one-hot column flags and the column -> numeric index map."""
+    memo = hm.__dict__.setdefault("_tree_static", {})
+    if not memo:
+        F = hm.n_features
+        onehot = torch.zeros(F, dtype=torch.uint8, device=hm.device)
+        for off, w in hm.blocks:
+            onehot[off:off + w] = 1
+        colmap = hm.col_map()[:F].contiguous()
+        memo.update(cat=hm.cat.to(torch.int32).contiguous(), onehot=onehot, colmap=colmap,
+                    dcols=hm.dense_cols.to(device=hm.device, dtype=torch.int32).contiguous(),
+                    dense=hm.dense.float().contiguous())
+    return memo
+
+
+def thresholds_hybrid_device(hm, max_bins: int, sample_rows: int = 10000, seed: int = 0, row_offset: int = 0,
+                             n_total: int = None) -> Optional[DeviceThresholds]:
+    """``find_thresholds_hybrid`` left on the device (no host read unless the rows are sampled, whose
+    compaction needs the sample size): the numeric block's LDS sort + post-sort kernels, then one
+    kernel for the one-hot ones and one for the padded threshold matrix.  None when the shape needs
+    the host version (sample > 16,384 rows, maxBins > 64)."""
+    ns = max_bins - 1
+    if ns <= 0 or ns > 63:
+        return None
+    st = _hybrid_static(hm)
+    N, F = hm.n_rows, hm.n_features
+    keep = threshold_sample_mask(N, max_bins, sample_rows, seed, row_offset, n_total, device=hm.device)
+    dense, cat = (st["dense"], st["cat"]) if keep is None else (st["dense"][keep].contiguous(), st["cat"][keep].contiguous())
+    n = int(cat.shape[0])
+    if n == 0 or n > 16384:
+        return None
+    mod, stp = _native.kernels(), _native.stream_ptr()
+    Fd = int(dense.shape[1])
+    dthr = torch.empty(max(Fd, 1), ns + 1, dtype=torch.float32, device=hm.device)
+    if Fd:
+        srt = torch.empty(Fd, n, dtype=torch.float32, device=hm.device)
+        mod.sort_columns(dense.data_ptr(), n, Fd, Fd, srt.data_ptr(), stp)
+        mod.find_splits_post_sort(srt.data_ptr(), Fd, n, ns, dthr.data_ptr(), stp)
+    ones = torch.empty(F, dtype=torch.int32, device=hm.device)
+    thr_mat = torch.empty(F, max_bins, dtype=torch.float32, device=hm.device)
+    nbins = torch.empty(F, dtype=torch.int32, device=hm.device)
+    mod.tree_thresholds_hybrid(cat.data_ptr(), n, int(cat.shape[1]), F, st["colmap"].data_ptr(), dthr.data_ptr(), ns,
+                               max_bins, ones.data_ptr(), thr_mat.data_ptr(), nbins.data_ptr(), stp)
+    return DeviceThresholds(thr_mat, nbins)
+
+
+def bins_hybrid(hm, thr_mat: torch.Tensor, nbins: torch.Tensor) -> torch.Tensor:
+    """uint8 bins [F, N] of ``hm`` (= bin_features of its dense form) from its parts (tree.hip)."""
+    N, F = hm.n_rows, hm.n_features
+    out = torch.empty(F, N, dtype=torch.uint8, device=hm.device)
+    st = _hybrid_static(hm)
+    dense, cat, dcols = st["dense"], st["cat"], st["dcols"]
+    _native.kernels().tree_bins_hybrid(dense.data_ptr(), N, int(dense.shape[1]), dcols.data_ptr(), cat.data_ptr(),
+                                       int(cat.shape[1]), F, thr_mat.data_ptr(), int(thr_mat.shape[1]),
+                                       nbins.data_ptr(), out.data_ptr(), _native.stream_ptr())
+    return out
+
+
+def sparse_tree_input(hm) -> SparseTreeInput:
+    st = _hybrid_static(hm)
+    return SparseTreeInput(st["cat"], st["onehot"], hm.n_features)
+
+
+# rows per work item of a one-hot-aware level: a node's row pass is a few loads per row, so a node is
+# chunked (and its chunks merged + searched in a second pass) only when far bigger than PLAN_ROWS
+SPARSE_PLAN_ROWS = 16384  # 8 x PLAN_ROWS
+
+
 @dataclass
 class LevelResult:
     gain: torch.Tensor      # [A] best gain (-inf if no valid split)
@@ -301,7 +448,7 @@ def split_owner(hist: torch.Tensor, feats: torch.Tensor, K: int, owner, split_fn
 
 def hist_split_native(bins, nbins_feat, label, rows, row_w, node_start, node_count, feats, K, max_bins,
                       min_instances, min_info_gain, impurity, allreduce=None, owner=None, max_rows=None,
-                      check_labels: bool = True, bins_rm=None) -> LevelResult:
+                      check_labels: bool = True, bins_rm=None, sparse=None) -> LevelResult:
     """Fused LDS histogram + split on one device; in data parallel the kernel runs twice:
     histogram-only into a [A, m, bins, K] buffer, then either one RCCL all-reduce of it and
     split search for every node (``allreduce``), or a reduce-scatter by node owner, split
@@ -335,9 +482,10 @@ def hist_split_native(bins, nbins_feat, label, rows, row_w, node_start, node_cou
     if blocks < 1024 and max_rows > 4096:
         row_chunks = int(min((1024 + blocks - 1) // blocks, (max_rows + 2047) // 2048))
     st = _native.stream_ptr()
+    sp = sparse_args(sparse)
     if owner is not None:
         ghist = (torch.zeros if row_chunks > 1 else torch.empty)(A, m, max_bins, K, dtype=torch.float32, device=dev)
-        mod.tree_hist_split(*args, 1, ghist.data_ptr(), row_chunks, st)
+        mod.tree_hist_split(*args, 1, ghist.data_ptr(), row_chunks, *sp, st)
 
         def split_slice(local, a0, a1):
             n = a1 - a0
@@ -351,18 +499,18 @@ def hist_split_native(bins, nbins_feat, label, rows, row_w, node_start, node_cou
                   node_start.data_ptr() + 4 * a0, node_count.data_ptr() + 4 * a0, n, feats.data_ptr() + 4 * a0 * m,
                   m, fc, label.data_ptr(), K, max_bins, float(min_instances), float(min_info_gain), impurity,
                   g.data_ptr(), f.data_ptr(), b.data_ptr(), lf.data_ptr(), tot.data_ptr()]
-            mod.tree_hist_split(*sl, 2, loc.data_ptr(), 1, st)
+            mod.tree_hist_split(*sl, 2, loc.data_ptr(), 1, *sp, st)
             return _best_chunk(g, f, b, lf, tot, n, chunks, K)
 
         return split_owner(ghist, feats, K, owner, split_slice)
     if allreduce is None and row_chunks == 1:
-        mod.tree_hist_split(*args, 0, 0, 1, st)
+        mod.tree_hist_split(*args, 0, 0, 1, *sp, st)
     else:
         ghist = (torch.zeros if row_chunks > 1 else torch.empty)(A, m, max_bins, K, dtype=torch.float32, device=dev)
-        mod.tree_hist_split(*args, 1, ghist.data_ptr(), row_chunks, st)
+        mod.tree_hist_split(*args, 1, ghist.data_ptr(), row_chunks, *sp, st)
         if allreduce is not None:
             allreduce(ghist)
-        mod.tree_hist_split(*args, 2, ghist.data_ptr(), 1, st)
+        mod.tree_hist_split(*args, 2, ghist.data_ptr(), 1, *sp, st)
     return _best_chunk(gain, feat, bin_, left, total, A, chunks, K)
 
 
@@ -372,7 +520,7 @@ PLAN_ROWS = 2048  # rows per work item of a load-balanced level (larger nodes ar
 def hist_split_planned(bins, nbins_feat, label, rows, row_w, node_start, node_count, feats, K, max_bins,
                        min_instances, min_info_gain, impurity, rows_bound: int, bins_rm=None,
                        prows: int = PLAN_ROWS, a_dev: int = 0, store=None, hprev=None, derive_from=None,
-                       parent_of=None) -> LevelResult:
+                       parent_of=None, sparse=None) -> LevelResult:
     """Load-balanced fused histogram + split for one level on one device (no host sync).
 
     Work is split by ROWS, not by node: a node of <= ``prows`` rows is one work item (fused LDS
@@ -415,13 +563,14 @@ def hist_split_planned(bins, nbins_feat, label, rows, row_w, node_start, node_co
             float(min_info_gain), impurity, gain.data_ptr(), feat.data_ptr(), bin_.data_ptr(), left.data_ptr(),
             total.data_ptr()]
     dptr = derive_from.data_ptr() if derive_from is not None else 0
+    sp = sparse_args(sparse)
     mod.tree_hist_split_planned(*args, 3, ghist.data_ptr(), plan.data_ptr(), prows, items_ub, int(by_node), 0, dptr,
-                                0, st)
+                                0, *sp, st)
     mod.tree_hist_split_planned(*args, 4, ghist.data_ptr(), plan.data_ptr(), prows, max_big, int(by_node), 0, 0, 0,
-                                st)
+                                *sp, st)
     if derive_from is not None:
         mod.tree_hist_split_planned(*args, 5, ghist.data_ptr(), plan.data_ptr(), prows, A, 1, hprev.data_ptr(), dptr,
-                                    parent_of.data_ptr(), st)
+                                    parent_of.data_ptr(), *sp, st)
     return _best_chunk(gain, feat, bin_, left, total, A, chunks, K)
 
 
@@ -470,7 +619,7 @@ def dp_wire_plan(node_cc: torch.Tensor, mb: int, P: int):
 def hist_split_planned_dp(bins, nbins_feat, label, rows, row_w, node_start, node_count, feats, K, max_bins,
                           min_instances, min_info_gain, impurity, rows_bound: int, a_dev: int, allreduce=None,
                           owner=None, bins_rm=None, prows: int = PLAN_ROWS, max_weight: float = -1.0,
-                          node_cc: Optional[torch.Tensor] = None) -> LevelResult:
+                          node_cc: Optional[torch.Tensor] = None, sparse=None) -> LevelResult:
     """The data-parallel level on the planned path.  ``feats.shape[0]`` = A is the level's node count:
     EXACT when ``a_dev`` is 0 (the level loop read its 16-byte count record back), else a bound shared
     by every rank with ``a_dev`` pointing at the device count.
@@ -509,6 +658,7 @@ def hist_split_planned_dp(bins, nbins_feat, label, rows, row_w, node_start, node
     mod, st = _native.kernels(), _native.stream_ptr()
     mod.tree_plan(node_count.data_ptr(), A, prows, plan.data_ptr(), slot, store.data_ptr(), max(1, A), 1, a_dev, st)
     bptr, row_major = (bins_rm.data_ptr(), 1) if bins_rm is not None else (bins.data_ptr(), 0)
+    sp = sparse_args(sparse)
 
     def launch(mode, n, a0, hist_ptr, fptr, outs, bound):
         g, f, b, lf, tot = outs
@@ -516,7 +666,7 @@ def hist_split_planned_dp(bins, nbins_feat, label, rows, row_w, node_start, node
                                     node_start.data_ptr(), node_count.data_ptr(), n, fptr, m, fc, label.data_ptr(),
                                     K, max_bins, float(min_instances), float(min_info_gain), impurity, g.data_ptr(),
                                     f.data_ptr(), b.data_ptr(), lf.data_ptr(), tot.data_ptr(), mode, hist_ptr,
-                                    plan.data_ptr(), a0 if mode == 7 else prows, bound, 1, 0, 0, 0, st)
+                                    plan.data_ptr(), a0 if mode == 7 else prows, bound, 1, 0, 0, 0, *sp, st)
 
     def outs(n):
         return (torch.empty(n * chunks, dtype=torch.float32, device=dev),

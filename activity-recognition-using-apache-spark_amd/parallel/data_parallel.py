@@ -223,7 +223,8 @@ def fit_forest_dp(estimator, X_shard, y_shard, num_classes: int, row_offset: int
                                  thresholds=thr)
 
 
-def fit_forest_tree_parallel(estimator, X, y, num_classes: int, ctx: DistContext, thresholds=None, stats=None):
+def fit_forest_tree_parallel(estimator, X, y, num_classes: int, ctx: DistContext, thresholds=None, stats=None,
+                             hybrid=None):
     """Tree parallelism: every rank holds ALL rows and grows its contiguous
     slice of the forest's trees — keyed by global tree id, so bootstraps and feature subsets
     are those of the single-process forest — with zero communication until ONE all-gather at the
@@ -239,7 +240,8 @@ def fit_forest_tree_parallel(estimator, X, y, num_classes: int, ctx: DistContext
     lo, hi = (T_ * r) // P, (T_ * (r + 1)) // P
     if thresholds is None:
         thresholds = T.thresholds_for(X, estimator.maxBins, seed=estimator.seed)
-    part = estimator.fit_tensors(X, y, num_classes, thresholds=thresholds, tree_offset=lo, num_trees=hi - lo)
+    part = estimator.fit_tensors(X, y, num_classes, thresholds=thresholds, tree_offset=lo, num_trees=hi - lo,
+                                 hybrid=hybrid)
     if not ctx.collective:
         return part
     a = part.arrs

@@ -183,8 +183,11 @@ class CrossValidator(Estimator):
             X, y, K = est._prep(table)
             fold_t = fold_ids_on(dev)
             masks = torch.stack([(fold_t != f).float() for f in range(k)])
+            # trees on the reference encoding: the one-hot-aware path (same forests)
+            hyb = est._hybrid(table, X.device) if hasattr(est, "_hybrid") else None
             for mi, pm in enumerate(maps):
-                fms = est.copy(pm).fit_folds(X, y, K, masks)
+                e = est.copy(pm)
+                fms = e.fit_folds(X, y, K, masks, hybrid=hyb) if hyb is not None else e.fit_folds(X, y, K, masks)
                 raws = [m.predict_raw(X) for m in fms]
                 pred = _batched_predictions(fms, torch.stack(raws))
                 vals = ev.evaluate_batched(y, pred, masks == 0, K, torch.stack(raws))

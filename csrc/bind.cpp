@@ -576,12 +576,13 @@ PYBIND11_MODULE(_har_native, m) {
   m.def("tree_hist_split", [](u bins, int64_t N, int F, int row_major, u nbins, u rows, u row_w, u node_start, u node_count, int A,
                               u feats, int m, int fc, u label, int K, int maxbins, float min_inst, float min_gain,
                               int impurity, u gain, u feat, u bin, u left, u total, int mode, u ghist, int row_chunks,
-                              u stream) {
+                              u cat, int ncat, u onehot, u stream) {
+    const TreeSparse sp{P<const int32_t>(cat), ncat, P<const uint8_t>(onehot), F};
     check(har_tree_hist_split(P<const uint8_t>(bins), N, F, row_major, P<const int32_t>(nbins), P<const int32_t>(rows),
                               P<const float>(row_w), P<const int32_t>(node_start), P<const int32_t>(node_count), A,
                               P<const int32_t>(feats), m, fc, P<const int32_t>(label), K, maxbins, min_inst, min_gain,
                               impurity, P<float>(gain), P<int32_t>(feat), P<int32_t>(bin), P<float>(left),
-                              P<float>(total), mode, P<float>(ghist), row_chunks, S(stream)),
+                              P<float>(total), mode, P<float>(ghist), row_chunks, cat ? &sp : nullptr, S(stream)),
           "tree_hist_split");
   });
 
@@ -595,7 +596,8 @@ PYBIND11_MODULE(_har_native, m) {
                                       u node_count, int A, u feats, int m, int fc, u label, int K, int maxbins,
                                       float min_inst, float min_gain, int impurity, u gain, u feat, u bin, u left,
                                       u total, int mode, u ghist, u plan, int prows, int bound, int by_node,
-                                      u hprev, u derive_from, u parent_of, u stream) {
+                                      u hprev, u derive_from, u parent_of, u cat, int ncat, u onehot, u stream) {
+    const TreeSparse sp{P<const int32_t>(cat), ncat, P<const uint8_t>(onehot), F};
     check(har_tree_hist_split_planned(P<const uint8_t>(bins), N, F, row_major, P<const int32_t>(nbins),
                                       P<const int32_t>(rows), P<const float>(row_w), P<const int32_t>(node_start),
                                       P<const int32_t>(node_count), A, P<const int32_t>(feats), m, fc,
@@ -603,7 +605,7 @@ PYBIND11_MODULE(_har_native, m) {
                                       P<float>(gain), P<int32_t>(feat), P<int32_t>(bin), P<float>(left),
                                       P<float>(total), mode, P<float>(ghist), 1, P<const int32_t>(plan), prows, bound,
                                       by_node, P<const float>(hprev), P<const int32_t>(derive_from),
-                                      P<const int32_t>(parent_of), S(stream)),
+                                      P<const int32_t>(parent_of), cat ? &sp : nullptr, S(stream)),
           "tree_hist_split_planned");
   });
 
@@ -832,6 +834,18 @@ PYBIND11_MODULE(_har_native, m) {
     check(har_column_stats(P<const float>(X), n, ncols, ld, P<const float>(w), P<double>(stats), P<double>(ws),
                            S(stream)),
           "column_stats");
+  });
+  m.def("tree_thresholds_hybrid", [](u cat, int64_t n, int ncat, int F, u colmap, u dthr, int ns, int maxb, u ones,
+                                     u thr_mat, u nbins, u stream) {
+    check(har_tree_thresholds_hybrid(P<const int32_t>(cat), n, ncat, F, P<const int32_t>(colmap), P<const float>(dthr),
+                                     ns, maxb, P<int32_t>(ones), P<float>(thr_mat), P<int32_t>(nbins), S(stream)),
+          "tree_thresholds_hybrid");
+  });
+  m.def("tree_bins_hybrid", [](u dense, int64_t n, int Fd, u dense_cols, u cat, int ncat, int F, u thr, int maxb,
+                               u nbins, u bins, u stream) {
+    check(har_tree_bins_hybrid(P<const float>(dense), n, Fd, P<const int32_t>(dense_cols), P<const int32_t>(cat), ncat,
+                               F, P<const float>(thr), maxb, P<const int32_t>(nbins), P<uint8_t>(bins), S(stream)),
+          "tree_bins_hybrid");
   });
   m.def("bin_features", [](u X, int64_t n, int F, int ld, u thr, int maxb, u nthr, u bins, u stream) {
     check(har_bin_features(P<const float>(X), n, F, ld, P<const float>(thr), maxb, P<const int32_t>(nthr),

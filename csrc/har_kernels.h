@@ -351,12 +351,27 @@ void har_window_set_legacy(int on);
 // out_total [A][K] = node class counts.  mode 0 fused; 1 histogram only -> ghist [A][m][maxbins][K];
 // 2 split search from ghist (after a cross-rank reduction).  row_chunks > 1 (mode 1 only): each node's
 // rows are split over that many workgroups that atomically merge into a ZEROED ghist.
+// One-hot-aware histograms (tree.hip SPARSE): cat [N][ncat] int32 = the global column of each row's 1 in
+// every one-hot block (-1 none), onehot [F] uint8 = 1 for the one-hot columns; F = the feature count.
+typedef struct TreeSparse {
+  const int32_t* cat;
+  int ncat;
+  const uint8_t* onehot;
+  int F;
+} TreeSparse;
+// bins [F][n] of a hybrid matrix (numeric block dense [n][Fd] at columns dense_cols, one-hot entries cat)
+// findSplits of a hybrid matrix (its sampled rows: cat [n][ncat]; colmap [F] = numeric index or < 0 for
+// one-hot; dthr [Fd][ns + 1] = find_splits_post_sort of the numeric block) -> thr_mat [F][maxb], nbins [F]
+int har_tree_thresholds_hybrid(const int32_t* cat, int64_t n, int ncat, int F, const int32_t* colmap, const float* dthr,
+                               int ns, int maxb, int32_t* ones, float* thr_mat, int32_t* nbins, hipStream_t s);
+int har_tree_bins_hybrid(const float* dense, int64_t n, int Fd, const int32_t* dense_cols, const int32_t* cat, int ncat,
+                         int F, const float* thr, int maxb, const int32_t* nbins, uint8_t* bins, hipStream_t s);
 int har_tree_hist_split(const uint8_t* bins, int64_t N, int F, int row_major, const int32_t* nbins_feat, const int32_t* rows,
                         const float* row_w, const int32_t* node_start, const int32_t* node_count, int A,
                         const int32_t* feats, int m, int fc, const int32_t* label, int K, int maxbins,
                         float min_inst, float min_gain, int impurity, float* out_gain, int32_t* out_feat,
                         int32_t* out_bin, float* out_left, float* out_total, int mode, float* ghist,
-                        int row_chunks, hipStream_t s);
+                        int row_chunks, const TreeSparse* sparse, hipStream_t s);
 // Device-count convention of the level kernels below: a non-null a_dev / p_dev / s_dev points at the
 // level's real count on the device and the host's A / P / S is then only an upper bound (grid size
 // and array stride), so a whole fit can be enqueued without reading counts back per level.
@@ -376,7 +391,7 @@ int har_tree_hist_split_planned(const uint8_t* bins, int64_t N, int F, int row_m
                                 float* out_gain, int32_t* out_feat, int32_t* out_bin, float* out_left,
                                 float* out_total, int mode, float* ghist, int row_chunks, const int32_t* plan,
                                 int prows, int bound, int by_node, const float* hprev, const int32_t* derive_from,
-                                const int32_t* parent_of, hipStream_t s);
+                                const int32_t* parent_of, const TreeSparse* sparse, hipStream_t s);
 // Sum over trees of (normalized) leaf statistics; trees as SoA [T][maxn] arrays, feature < 0 = leaf.
 // Level bookkeeping of the forest builder (tree_level.hip): Floyd feature subsets per (tree, node)
 // (bit-identical to har/ops/rng.py), per-(tree,row) candidate keys, and the row -> child partition.

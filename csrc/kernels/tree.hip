@@ -30,15 +30,19 @@ constexpr int KMAX = 32;
 // 6-step 64-lane scan per class and slot.  The per-lane gain arithmetic (fp64, classes summed in
 // order) and the lowest-index tie rule are those of the one-slot-per-wave search, so the winner
 // is bit for bit the same.
+// smap (optional): the slots to search, smap[0 .. f_n) (the numeric slots of a SPARSE chunk); the winner
+// index is still slot * maxbins + bin
 template <int KC>
 __device__ __forceinline__ void split_search_pairs(const float* hist, const int* fid, const int32_t* nbins_feat,
                                                    int f_n, int maxbins, int K, float min_inst, int impurity,
-                                                   int wave, int nwaves, int lane, double& best_g, int& best_i) {
+                                                   int wave, int nwaves, int lane, double& best_g, int& best_i,
+                                                   const short* smap = nullptr) {
   const int half = lane >> 5, bl = lane & 31;
   const wops::LaneSwap sw(lane);
   for (int fp = wave; 2 * fp < f_n; fp += nwaves) {
-    const int fs = 2 * fp + half;
-    const bool fv = fs < f_n;
+    const int fi = 2 * fp + half;
+    const bool fv = fi < f_n;
+    const int fs = smap ? (fv ? (int)smap[fi] : 0) : fi;
     const int nb = fv ? nbins_feat[fid[fs]] : 0;
     // each half's last bin (uniform per half): the totals are two scalar lane reads, not a permute
     const int last0 = max(__builtin_amdgcn_readlane(nb, 0) - 1, 0);
@@ -98,7 +102,17 @@ __device__ __forceinline__ void hist_add(float* p, float w) {
   else atomicAdd(p, w);
 }
 
-template <bool INTW>
+// One-hot-aware histograms (SPARSE; ops/tree.py, the reference encoding's 3,090 binary one-hot
+// columns beside 10 numeric ones, Main/main.py:51-66).  Per row the one-hot blocks hold at most one 1
+// each (sp.cat [N][ncat]: the global column of the row's 1, -1 = none), so a node's histogram of a
+// one-hot column with the split 0 | 1 (the column's one threshold, 0.5) is: bin 1 = the weight of the
+// node's rows whose entry is that column, added over the ncat entries of every row — O(rows x ncat)
+// instead of O(rows x features) — and bin 0 = the node's class totals minus bin 1 (integer weights:
+// exact).  The numeric columns of the chunk are histogrammed from the bins as in the dense path.  The
+// split search, the stores and every mode are the dense kernel's: the forest is the same node for node.
+constexpr int SP_NCAT = 4;  // one-hot blocks per row handled in registers (more: the dense path)
+
+template <bool INTW, bool SPARSE>
 __global__ __launch_bounds__(256) void tree_hist_split_kernel(
     const uint8_t* __restrict__ bins, int64_t fstride, int64_t rstride, const int32_t* __restrict__ nbins_feat,
     const int32_t* __restrict__ rows, const float* __restrict__ row_w, const int32_t* __restrict__ node_start,
@@ -107,7 +121,7 @@ __global__ __launch_bounds__(256) void tree_hist_split_kernel(
     float* __restrict__ out_gain, int32_t* __restrict__ out_feat, int32_t* __restrict__ out_bin,
     float* __restrict__ out_left, float* __restrict__ out_total, int mode, float* __restrict__ ghist,
     const int32_t* __restrict__ plan, int prows, int by_node, const float* __restrict__ hprev,
-    const int32_t* __restrict__ derive_from, const int32_t* __restrict__ parent_of) {
+    const int32_t* __restrict__ derive_from, const int32_t* __restrict__ parent_of, TreeSparse sp) {
   // mode 0: fused histogram + split; 1: histogram only -> ghist [A][m][maxbins][K] (data parallel:
   // summed across ranks by RCCL); 2: split search from a (reduced) ghist.
   // Planned (load-balanced) level, plan = tree_plan_kernel's output (see there):
@@ -131,6 +145,14 @@ __global__ __launch_bounds__(256) void tree_hist_split_kernel(
   const int f_n = min(fc, m - f_lo);
   float* hist = smem;                                          // [fc][maxbins][K]
   int* fid = reinterpret_cast<int*>(smem + (size_t)fc * maxbins * K);  // [fc]
+  // SPARSE: class totals [K] (uint32), global column -> chunk slot [F] (-1: not in the chunk), the
+  // chunk's numeric slots, per-slot kind (0 numeric, 1 one-hot with its 0 | 1 split, 2 one-hot
+  // without a threshold: every row in bin 0)
+  unsigned int* ktot = reinterpret_cast<unsigned int*>(fid + fc);
+  short* slot_of = reinterpret_cast<short*>(ktot + K);
+  short* dlist = slot_of + (SPARSE ? sp.F : 0);
+  uint8_t* sflag = reinterpret_cast<uint8_t*>(dlist + fc);
+  __shared__ int nd_s;
   __shared__ double red_gain[4];
   __shared__ int red_idx[4];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -201,11 +223,96 @@ __global__ __launch_bounds__(256) void tree_hist_split_kernel(
     for (int i = tid; i < f_n * maxbins * K; i += blockDim.x) hist[i] = (mode == 2) ? gh[i] : 0.f;
   }
   for (int i = tid; i < f_n; i += blockDim.x) fid[i] = feats[(size_t)a * m + f_lo + i];
+  if constexpr (SPARSE) {
+    // (every mode: the split search takes the one-hot and the numeric slots apart)
+    if (mode != 2)
+      for (int i = tid; i < sp.F; i += blockDim.x) slot_of[i] = -1;
+    for (int k = tid; k < K; k += blockDim.x) ktot[k] = 0u;
+    if (tid == 0) nd_s = 0;
+    __syncthreads();
+    for (int i = tid; i < f_n; i += blockDim.x) {
+      const int f = feats[(size_t)a * m + f_lo + i];
+      const bool oh = sp.onehot[f] != 0;
+      if (mode != 2) slot_of[f] = (short)i;
+      sflag[i] = oh ? (nbins_feat[f] >= 2 ? 1 : 2) : 0;
+      if (!oh) dlist[atomicAdd(&nd_s, 1)] = (short)i;  // (order free: integer sums, index-ordered ties)
+    }
+  }
   __syncthreads();
 
   // ---- histogram ----
   const int rpi = f_n <= 64 ? (int)blockDim.x / f_n : 0;
-  if (mode != 2 && rpi > 0) {
+  if constexpr (SPARSE) {
+    if (mode != 2) {
+      // one thread per row, U rows in flight (the row id -> label / one-hot entries loads are a
+      // dependent chain); class totals in registers (K <= 8) or LDS atomics
+      unsigned int* hu = reinterpret_cast<unsigned int*>(hist);
+      const int nd = nd_s, nc = sp.ncat;
+      unsigned int acc[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
+      auto row_add = [&](int r, unsigned int wu, int l, const int (&fr)[SP_NCAT]) __attribute__((always_inline)) {
+#pragma unroll
+        for (int c = 0; c < SP_NCAT; ++c) {
+          if (fr[c] >= 0) {
+            const int sl = slot_of[fr[c]];
+            if (sl >= 0 && sflag[sl] == 1) atomicAdd(hu + (sl * maxbins + 1) * K + l, wu);
+          }
+        }
+        for (int d = 0; d < nd; ++d) {
+          const int sl = dlist[d];
+          const int b = bins[(int64_t)fid[sl] * fstride + (int64_t)r * rstride];
+          atomicAdd(hu + (sl * maxbins + b) * K + l, wu);
+        }
+        if (K <= 8) {
+#pragma unroll
+          for (int k = 0; k < 8; ++k) acc[k] += l == k ? wu : 0u;
+        } else {
+          atomicAdd(ktot + l, wu);
+        }
+      };
+      constexpr int U = 4;
+      int ri = tid;
+      for (; ri + (U - 1) * (int)blockDim.x < cnt; ri += U * (int)blockDim.x) {
+        int r[U], l[U], fr[U][SP_NCAT];
+        unsigned int wu[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          r[u] = rows[start + ri + u * (int)blockDim.x];
+          wu[u] = (unsigned int)row_w[start + ri + u * (int)blockDim.x];
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          l[u] = label[r[u]];
+#pragma unroll
+          for (int c = 0; c < SP_NCAT; ++c) fr[u][c] = c < nc ? sp.cat[(int64_t)r[u] * nc + c] : -1;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) row_add(r[u], wu[u], l[u], fr[u]);
+      }
+      for (; ri < cnt; ri += blockDim.x) {
+        const int r = rows[start + ri];
+        const unsigned int wu = (unsigned int)row_w[start + ri];
+        int fr[SP_NCAT];
+#pragma unroll
+        for (int c = 0; c < SP_NCAT; ++c) fr[c] = c < nc ? sp.cat[(int64_t)r * nc + c] : -1;
+        row_add(r, wu, label[r], fr);
+      }
+      if (K <= 8) {
+        const wops::LaneSwap sw(lane);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          // (integer-valued sums below 2^24: exact in fp32)
+          const float v = wops::wave_sum_dpp((float)acc[k], sw);
+          if (k < K && lane == 0 && v != 0.f) atomicAdd(ktot + k, (unsigned int)v);
+        }
+      }
+      __syncthreads();
+      // bin 0 of every one-hot slot = class totals - bin 1
+      for (int i = tid; i < f_n * K; i += blockDim.x) {
+        const int sl = i / K, k = i - sl * K;
+        if (sflag[sl]) hu[sl * maxbins * K + k] = ktot[k] - hu[(sl * maxbins + 1) * K + k];
+      }
+    }
+  } else if (mode != 2 && rpi > 0) {
     // (row, feature slot) pairs with the feature slot fastest: the lanes of one instruction
     // add into f_n different feature histograms (a row-at-a-time mapping sends most lanes of a
     // nearly pure node to the same (bin, class) word — same-address LDS atomics serialize), and
@@ -295,7 +402,49 @@ __global__ __launch_bounds__(256) void tree_hist_split_kernel(
   int best_i = 0x7fffffff;
   const int nwaves = (int)(blockDim.x >> 6);
   const bool pairs = maxbins <= 32;
-  if (pairs)
+  if constexpr (SPARSE) {
+    // one-hot slots: one LANE per slot — their only candidate is bin 0 (the 0 | 1 split); the per-lane
+    // arithmetic is the pair search's at bin 0 (v = bin 0, t = bin 0 + bin 1 in fp32, classes in order),
+    // so the gains, and with the (gain, lowest index) rule the winner, are bit for bit the same
+    const wops::LaneSwap sws(lane);
+    for (int base = wave * 64; base < f_n; base += nwaves * 64) {
+      const int fs = base + lane;
+      double g = -INFINITY;
+      if (fs < f_n && sflag[fs] == 1) {
+        double wl = 0.0, wt = 0.0, ql = 0.0, qr = 0.0, qt = 0.0;
+        for (int k = 0; k < K; ++k) {
+          const float c0 = hist[fs * maxbins * K + k], c1 = hist[(fs * maxbins + 1) * K + k];
+          const float tf = c0 + c1;
+          const double v = (double)c0, t = (double)tf, r = t - v;
+          wl += v;
+          wt += t;
+          if (impurity == 0) {
+            ql += v * v; qr += r * r; qt += t * t;
+          } else {
+            ql += v > 0 ? v * log2(v) : 0.0;
+            qr += r > 0 ? r * log2(r) : 0.0;
+            qt += t > 0 ? t * log2(t) : 0.0;
+          }
+        }
+        const double wr = wt - wl;
+        if (wl >= min_inst && wr >= min_inst && wt > 0) {
+          double ip, il, ir;
+          if (impurity == 0) {
+            ip = 1.0 - qt / (wt * wt); il = 1.0 - ql / (wl * wl); ir = 1.0 - qr / (wr * wr);
+          } else {
+            ip = log2(wt) - qt / wt; il = log2(wl) - ql / wl; ir = log2(wr) - qr / wr;
+          }
+          g = ip - (wl / wt) * il - (wr / wt) * ir;
+        }
+      }
+      int idx = fs * maxbins;
+      wops::wave_argmax(g, idx, sws);
+      if (g > best_g || (g == best_g && idx < best_i)) { best_g = g; best_i = idx; }
+    }
+    // numeric slots: the pair search over their list
+    split_search_pairs<8>(hist, fid, nbins_feat, nd_s, maxbins, K, min_inst, impurity, wave, nwaves, lane, best_g,
+                          best_i, dlist);
+  } else if (pairs)
     split_search_pairs<8>(hist, fid, nbins_feat, f_n, maxbins, K, min_inst, impurity, wave, nwaves, lane, best_g,
                           best_i);
   const wops::LaneSwap swl(lane);
@@ -681,7 +830,96 @@ __global__ __launch_bounds__(256) void tree_plan_zero_kernel(const int32_t* __re
   }
 }
 
+// Bins of a hybrid (one-hot index + numeric) matrix straight from its parts, feature-major [F][n]
+// like bin_features of the dense matrix (zeroed by the launcher): a numeric column's bin = #thresholds
+// strictly below x (NaN -> last), a one-hot column with its threshold (0.5) gets bin 1 in the rows
+// whose entry it is.  One thread per row; no dense [n][F] matrix is read.
+__global__ __launch_bounds__(256) void tree_bins_hybrid_kernel(const float* __restrict__ dense, int64_t n, int Fd,
+                                                               const int32_t* __restrict__ dense_cols,
+                                                               const int32_t* __restrict__ cat, int ncat,
+                                                               const float* __restrict__ thr, int maxb,
+                                                               const int32_t* __restrict__ nbins,
+                                                               uint8_t* __restrict__ bins) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  for (int j = 0; j < Fd; ++j) {
+    const int f = dense_cols[j];
+    const int nt = nbins[f] - 1;
+    const float* t = thr + (size_t)f * maxb;
+    const float x = dense[i * Fd + j];
+    int lo = 0, hi = nt;
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (t[mid] < x) lo = mid + 1; else hi = mid;
+    }
+    bins[(size_t)f * n + i] = (uint8_t)(x == x ? lo : nt);
+  }
+  for (int c = 0; c < ncat; ++c) {
+    const int f = cat[i * ncat + c];
+    if (f >= 0 && nbins[f] >= 2) bins[(size_t)f * n + i] = 1;
+  }
+}
+
+// findSplits of a hybrid matrix on the device (ops/tree.py thresholds_hybrid_device): the ones of every
+// one-hot column over the (sampled) rows, then per column its thresholds row of the padded matrix
+// [F][maxb] (+inf after the count) and its bin count: a one-hot column gets the 0 | 1 split (0.5) when
+// the rows hold both values, a numeric column the sorted-sample thresholds of find_splits_post_sort
+// (dthr [Fd][ns + 1], the count last).  No host round trip.
+__global__ __launch_bounds__(256) void tree_onehot_counts_kernel(const int32_t* __restrict__ cat, int64_t n, int ncat,
+                                                                 int32_t* __restrict__ ones) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n * ncat) return;
+  const int f = cat[i];
+  if (f >= 0) atomicAdd(ones + f, 1);
+}
+
+__global__ __launch_bounds__(256) void tree_thresholds_hybrid_kernel(int F, const int32_t* __restrict__ colmap,
+                                                                     const int32_t* __restrict__ ones, int n,
+                                                                     const float* __restrict__ dthr, int ns, int maxb,
+                                                                     float* __restrict__ thr_mat,
+                                                                     int32_t* __restrict__ nbins) {
+  const int f = blockIdx.x * blockDim.x + threadIdx.x;
+  if (f >= F) return;
+  float* row = thr_mat + (size_t)f * maxb;
+  const int j = colmap[f];  // numeric column index, < 0: one-hot
+  int cnt;
+  if (j >= 0) {
+    const float* d = dthr + (size_t)j * (ns + 1);
+    cnt = (int)d[ns];
+    for (int k = 0; k < maxb; ++k) row[k] = k < cnt ? d[k] : INFINITY;
+  } else {
+    const int o = ones[f];
+    cnt = (o > 0 && o < n) ? 1 : 0;
+    for (int k = 0; k < maxb; ++k) row[k] = (k == 0 && cnt) ? 0.5f : INFINITY;
+  }
+  nbins[f] = cnt + 1;
+}
+
 }  // namespace
+
+extern "C" int har_tree_thresholds_hybrid(const int32_t* cat, int64_t n, int ncat, int F, const int32_t* colmap,
+                                          const float* dthr, int ns, int maxb, int32_t* ones, float* thr_mat,
+                                          int32_t* nbins, hipStream_t s) {
+  if (n <= 0 || ncat < 0 || F <= 0 || ns <= 0 || maxb < ns || n > 0x7fffffff) return -2;
+  if (hipMemsetAsync(ones, 0, (size_t)F * sizeof(int32_t), s) != hipSuccess) return -1;
+  if (ncat > 0)
+    tree_onehot_counts_kernel<<<(unsigned)((n * ncat + 255) / 256), 256, 0, s>>>(cat, n, ncat, ones);
+  tree_thresholds_hybrid_kernel<<<(F + 255) / 256, 256, 0, s>>>(F, colmap, ones, (int)n, dthr, ns, maxb, thr_mat, nbins);
+  HAR_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int har_tree_bins_hybrid(const float* dense, int64_t n, int Fd, const int32_t* dense_cols,
+                                    const int32_t* cat, int ncat, int F, const float* thr, int maxb,
+                                    const int32_t* nbins, uint8_t* bins, hipStream_t s) {
+  if (n < 0 || Fd < 0 || ncat < 0 || F <= 0 || maxb <= 0) return -2;
+  if (n == 0) return 0;
+  if (hipMemsetAsync(bins, 0, (size_t)F * n, s) != hipSuccess) return -1;
+  tree_bins_hybrid_kernel<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(dense, n, Fd, dense_cols, cat, ncat, thr, maxb,
+                                                                     nbins, bins);
+  HAR_CHECK_LAUNCH();
+  return 0;
+}
 
 // bins: feature-major [F][N] (row_major = 0) or row-major [N][F] (row_major = 1: the bytes of one
 // row's sampled features share one or two cache lines — the deep levels gather far less).
@@ -691,11 +929,11 @@ extern "C" int har_tree_hist_split(const uint8_t* bins, int64_t N, int F, int ro
                                    const int32_t* label, int K, int maxbins, float min_inst, float min_gain,
                                    int impurity, float* out_gain, int32_t* out_feat, int32_t* out_bin,
                                    float* out_left, float* out_total, int mode, float* ghist, int row_chunks,
-                                   hipStream_t s) {
+                                   const TreeSparse* sparse, hipStream_t s) {
   return har_tree_hist_split_planned(bins, N, F, row_major, nbins_feat, rows, row_w, node_start, node_count, A, feats,
                                      m, fc, label, K, maxbins, min_inst, min_gain, impurity, out_gain, out_feat,
                                      out_bin, out_left, out_total, mode, ghist, row_chunks, nullptr, 0, 0, 0,
-                                     nullptr, nullptr, nullptr, s);
+                                     nullptr, nullptr, nullptr, sparse, s);
 }
 
 // planned modes (plan != nullptr): grid.y = `bound` (work items for modes 3 / 6, big-node slots for
@@ -709,8 +947,11 @@ extern "C" int har_tree_hist_split_planned(const uint8_t* bins, int64_t N, int F
                                            float* out_total, int mode, float* ghist, int row_chunks,
                                            const int32_t* plan, int prows, int bound, int by_node,
                                            const float* hprev, const int32_t* derive_from,
-                                           const int32_t* parent_of, hipStream_t s) {
+                                           const int32_t* parent_of, const TreeSparse* sparse, hipStream_t s) {
   if (K > KMAX || maxbins > 64 || fc <= 0 || m <= 0) return -2;
+  // one-hot-aware histograms: integer weights, <= SP_NCAT one-hot entries per row, the maps in LDS
+  const bool sp_on = sparse && sparse->cat && sparse->onehot && sparse->ncat > 0;
+  if (sp_on && (sparse->ncat > SP_NCAT || sparse->F != F || maxbins < 2 || maxbins > 32 || F > 32767)) return -8;
   if (mode != 0 && !ghist) return -4;
   const bool planned = mode >= 3 && mode <= 7;
   if (planned && (!plan || (mode != 7 && prows <= 0) || prows < 0)) return -6;
@@ -719,7 +960,8 @@ extern "C" int har_tree_hist_split_planned(const uint8_t* bins, int64_t N, int F
   if (by_node && !planned) return -7;
   if (A == 0) return 0;
   const int chunks = (m + fc - 1) / fc;
-  const size_t lds = (size_t)fc * maxbins * K * sizeof(float) + (size_t)fc * sizeof(int);
+  const size_t lds = (size_t)fc * maxbins * K * sizeof(float) + (size_t)fc * sizeof(int) +
+                     (sp_on ? (size_t)K * 4 + (size_t)F * 2 + (size_t)fc * 3 : 0);
   if (lds > 150 * 1024) return -3;
   if (row_chunks > 1 && mode != 1) return -5;
   if (planned && bound <= 0) return 0;
@@ -730,11 +972,14 @@ extern "C" int har_tree_hist_split_planned(const uint8_t* bins, int64_t N, int F
     const char* e = getenv("HAR_HIST_FLOAT_ATOMICS");
     return e && e[0] == '1';
   }();
-  auto kern = float_atomics ? tree_hist_split_kernel<false> : tree_hist_split_kernel<true>;
+  if (sp_on && float_atomics) return -8;  // (bin 0 = totals - bin 1 is exact for the integer counts only)
+  const TreeSparse spv = sp_on ? *sparse : TreeSparse{};
+  auto kern = sp_on ? tree_hist_split_kernel<true, true>
+              : float_atomics ? tree_hist_split_kernel<false, false> : tree_hist_split_kernel<true, false>;
   kern<<<grid, 256, lds, s>>>(bins, fstride, rstride, nbins_feat, rows, row_w, node_start, node_count, feats, m, fc,
                               label, K, maxbins, min_inst, min_gain, impurity, out_gain, out_feat, out_bin, out_left,
                               out_total, mode, ghist, planned ? plan : nullptr, prows, by_node, hprev, derive_from,
-                              parent_of);
+                              parent_of, spv);
   HAR_CHECK_LAUNCH();
   return 0;
 }
