@@ -377,12 +377,9 @@ class LogisticRegression(Estimator, ClassifierParams):
                                        tol=self.tol)
             xs, fobj, iters, n_evals = res.x, res.f, res.iterations, res.n_evals
             rounds = res.rounds_per_iter
-            history = []
-            for h in res.history_per_model:  # as Spark's objectiveHistory: no repeats after a model stopped
-                h = list(h)
-                while len(h) > 1 and h[-1] == h[-2]:
-                    h.pop()
-                history.append(h)
+            # as Spark's objectiveHistory: the start + one entry per iteration the model took (the batch
+            # rows of a model that stopped earlier are cut by its own count, not by comparing values)
+            history = [list(h)[: int(iters[bi]) + 1] for bi, h in enumerate(res.history_per_model)]
         elif design.native:
             if ent is not None:
                 solver = ent.solver

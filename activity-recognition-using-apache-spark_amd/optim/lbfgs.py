@@ -337,8 +337,8 @@ def _interp_bracket(lo_t, lo_f, lo_d, hi_t, hi_f, hi_d):
 
 def minimize_wolfe(evaluate, x0: torch.Tensor, l2v: torch.Tensor, l1v: Optional[torch.Tensor] = None,
                    max_iter: int = 100, m: int = 10, tol: float = 1e-6, c1: float = 1e-4, c2: float = 0.9,
-                   max_ls: int = 10, max_zoom: int = 10, max_backtrack: int = 20, fval_memory: int = 20
-                   ) -> TrialResult:
+                   max_ls: int = 10, max_zoom: int = 10, max_backtrack: int = 20, fval_memory: int = 20,
+                   trace: Optional[list] = None) -> TrialResult:
     """Minimize ``B`` problems ``data(x_b) + 0.5 sum l2v x^2 + sum l1v |x|`` with Breeze's line
     searches (module comment above): strong Wolfe for the models without an L1 term (L-BFGS),
     projected backtracking with the weak Wolfe condition for the models with one (OWL-QN).
@@ -346,7 +346,9 @@ def minimize_wolfe(evaluate, x0: torch.Tensor, l2v: torch.Tensor, l1v: Optional[
     ``evaluate(x [B, D]) -> (loss [B] float64, grad [B, D])`` is the DATA part (as in
     ``minimize_trials`` with one trial).  float32 vectors, float64 reductions and line-search
     scalars; every operation is a batched tensor op on x's device.  ``n_evals`` counts the
-    batched evaluations (the initial one plus one per line-search round)."""
+    batched evaluations (the initial one plus one per line-search round).  ``trace`` (a list, optional)
+    receives one dict per model and accepted step: the step ``t``, phi(0) ``f0``, phi'(0) ``d0``,
+    phi(t) ``ft`` and phi'(t) ``dt`` of its line search (tests/test_wolfe.py checks the conditions)."""
     B, D = x0.shape
     dev = x0.device
     f64 = torch.float64
@@ -409,9 +411,11 @@ def minimize_wolfe(evaluate, x0: torch.Tensor, l2v: torch.Tensor, l1v: Optional[
         lo_t, lo_f, lo_d = torch.zeros_like(t), F.clone(), dd0.clone()   # phi(0)
         hi_t, hi_f, hi_d = torch.zeros_like(t), F.clone(), dd0.clone()
         x_acc, g_acc, F_acc = x.clone(), g.clone(), F.clone()
+        t_acc, d_acc = torch.zeros_like(t), torch.zeros_like(dd0)
         rounds = 0
         while bool(searching.any()):
             rounds += 1
+            t_cur = t
             xt = x + t.float()[:, None] * d
             xt = torch.where(owl[:, None] & (torch.sign(xt) != xi), torch.zeros_like(xt), xt)
             xt = torch.where(searching[:, None], xt, x)
@@ -473,6 +477,8 @@ def minimize_wolfe(evaluate, x0: torch.Tensor, l2v: torch.Tensor, l1v: Optional[
             t = torch.where(bt, t_bt, torch.where(halve, t / 2, torch.where(grow, t * 1.5,
                                                                           torch.where(zoom, t_zoom, t))))
             # accepted trial points
+            t_acc = torch.where(done_now, t_cur, t_acc)
+            d_acc = torch.where(done_now, dt, d_acc)
             x_acc = torch.where(done_now[:, None], xt, x_acc)
             g_acc = torch.where(done_now[:, None], gt, g_acc)
             F_acc = torch.where(done_now, Ft, F_acc)
@@ -480,6 +486,10 @@ def minimize_wolfe(evaluate, x0: torch.Tensor, l2v: torch.Tensor, l1v: Optional[
             searching = searching & ~done_now & ~fail_now
         rounds_per_iter.append(rounds)
         take = active & success
+        if trace is not None:
+            for b in torch.nonzero(take).flatten().tolist():
+                trace.append({"model": b, "iter": int(iters[b]), "owl": bool(owl[b]), "t": float(t_acc[b]),
+                              "f0": float(F[b]), "d0": float(dd0[b]), "ft": float(F_acc[b]), "dt": float(d_acc[b])})
         s_vec = x_acc - x
         y_vec = g_acc - g
         sy = dot(s_vec, y_vec)

@@ -108,7 +108,7 @@ __global__ __launch_bounds__(512) void mlp_fwd3_kernel(
     const float* __restrict__ bo, const int32_t* __restrict__ labels, int B, int C, float scale,
     bf16_t* __restrict__ dact2_out, float* __restrict__ slab,
     float* __restrict__ block_loss, int32_t* __restrict__ block_correct, uint64_t* __restrict__ stamps,
-    int stagger) {
+    int stagger, int wt) {
   constexpr int K0C = K0 / 32, KC = HH / 32;
   extern __shared__ __attribute__((aligned(16))) bf16_t lds[];
   bf16_t* const h1s = lds;                                                // [2 bufs][32][FHP]
@@ -339,6 +339,7 @@ __global__ __launch_bounds__(512) void mlp_fwd3_kernel(
   // (a wave-uniform row base + a 32-bit lane offset: the stores take the SGPR-base form, no 64-bit
   // address arithmetic per store)
   const int d2off = c16 * HH + ((u0 + 8 * g) ^ hsw);
+  const __amdgpu_buffer_rsrc_t d2rs = wt_rsrc(dact2_out);
   auto stage5 = [&](int buf, int r0) __attribute__((always_inline)) {
     const bf16_t* zb = dzs + buf * FIMG;
     // (the permuted k order of frag_rows on both operands: k runs over the 32 tile rows)
@@ -367,8 +368,12 @@ __global__ __launch_bounds__(512) void mlp_fwd3_kernel(
         const uint32_t he = hv[e];
         o[e] = relu_d_mul(ov[e], he);
       }
-      bf16_t* const rowp = dact2_out + (size_t)(r0 + 16 * h) * HH;
-      *reinterpret_cast<u32x4_t*>(rowp + d2off) = o;
+      if (wt) {  // (uniform: a kernel argument)
+        wt_store16(d2rs, (uint32_t)(((r0 + 16 * h) * HH + d2off) * 2), o);
+      } else {
+        bf16_t* const rowp = dact2_out + (size_t)(r0 + 16 * h) * HH;
+        *reinterpret_cast<u32x4_t*>(rowp + d2off) = o;
+      }
     }
   };
 
@@ -482,8 +487,13 @@ __global__ __launch_bounds__(512) void mlp_fwd3_kernel(
   // ---- this workgroup's slab: dWout rows 0..15 x this wave's units, dbout; loss, #correct ----
   float* out = slab + (size_t)blockIdx.x * FWD_SLAB;
 #pragma unroll
-  for (int t = 0; t < 2; ++t)
-    nt_store16(out + (size_t)c16 * HH + u0 + 16 * t + 4 * g, __builtin_bit_cast(u32x4_t, acc5[t]));
+  for (int t = 0; t < 2; ++t) {
+    if (wt)
+      wt_store16(wt_rsrc(slab), (uint32_t)(((size_t)blockIdx.x * FWD_SLAB + c16 * HH + u0 + 16 * t + 4 * g) * 4),
+                 __builtin_bit_cast(u32x4_t, acc5[t]));
+    else
+      nt_store16(out + (size_t)c16 * HH + u0 + 16 * t + 4 * g, __builtin_bit_cast(u32x4_t, acc5[t]));
+  }
   {  // (VALU lane swaps / DPP, not LDS-routed shuffles)
     const LaneSwap sw(lane);
     dbo += sw.x16f(dbo);
@@ -788,10 +798,20 @@ __global__ __launch_bounds__(512) void mlp_bwd4_kernel(
     HAR_STAMP(8, 34)
     if (n > 0) tile_c(n - 1);
     float* w0o = gw0 + (size_t)slice * slab_stride;
+    if (nt_slab == 2) {  // write-through (see the consumers' slab stores)
+      const __amdgpu_buffer_rsrc_t rs = wt_rsrc(gw0);
 #pragma unroll
-    for (int f = 0; f < NFB; ++f)
+      for (int f = 0; f < NFB; ++f)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) w0o[(size_t)(qu0 + 16 * pw + 4 * g + r) * K0 + 16 * f + c16] = acc0[f][r];
+        for (int r = 0; r < 4; ++r)
+          wt_store4(rs, (uint32_t)(((size_t)slice * slab_stride + (size_t)(qu0 + 16 * pw + 4 * g + r) * K0 + 16 * f + c16) * 4),
+                    acc0[f][r]);
+    } else {
+#pragma unroll
+      for (int f = 0; f < NFB; ++f)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) w0o[(size_t)(qu0 + 16 * pw + 4 * g + r) * K0 + 16 * f + c16] = acc0[f][r];
+    }
     if (c16 == 0) *reinterpret_cast<f32x4_t*>(gb0 + (size_t)slice * slab_stride + qu0 + 16 * pw + 4 * g) = accd0;
     // the forward's dWout / dbout slabs (one per forward workgroup) -> gwo / gbo: 4-column group
     // 4 b + pw per producer wave (b the XCD-remapped index: the 8 groups of a 128-byte line in two
@@ -928,11 +948,17 @@ __global__ __launch_bounds__(512) void mlp_bwd4_kernel(
     __builtin_amdgcn_s_setprio(0);
     // ---- this wave's parts of slab `slice` (flat parameter layout) ----
     float* w1o = gw1 + (size_t)slice * slab_stride;
+    // nt_slab: 1 nontemporal, 2 write-through (sc1: the slabs are not left dirty in L2 for the reduction
+    // launch's boundary), 0 plain
+    const __amdgpu_buffer_rsrc_t w1rs = wt_rsrc(gw1);
 #pragma unroll
     for (int j = 0; j < 4; ++j)
 #pragma unroll
       for (int u = 0; u < 4; ++u)
-        if (nt_slab)
+        if (nt_slab == 2)
+          wt_store16(w1rs, (uint32_t)(((size_t)slice * slab_stride + (size_t)(16 * (4 * pw + j) + c16) * HH + qu0 + 16 * u + 4 * g) * 4),
+                     __builtin_bit_cast(u32x4_t, acc1[j][u]));
+        else if (nt_slab)
           nt_store16(w1o + (size_t)(16 * (4 * pw + j) + c16) * HH + qu0 + 16 * u + 4 * g, __builtin_bit_cast(u32x4_t, acc1[j][u]));
         else
           *reinterpret_cast<f32x4_t*>(w1o + (size_t)(16 * (4 * pw + j) + c16) * HH + qu0 + 16 * u + 4 * g) = acc1[j][u];
@@ -965,15 +991,23 @@ void launch_fwd3(const bf16_t* X, bf16_t* Wf, const float* b0, const float* b1, 
            : fill == 2      ? mlp_fwd3_kernel<K0, false, false, 2>
            : fill >= 3      ? mlp_fwd3_kernel<K0, false, false, 3>
                             : mlp_fwd3_kernel<K0, false>;
+  // dact2 / dWout slab stores write-through (sc1; HAR_MLP_WT=0: plain / nontemporal): the 33.5 MB of
+  // dact2 are then not dirty in the L2s when the backward launches — forward 22.0 -> 19.3 us, step
+  // 0.0571 -> 0.0540 ms (profiles/r6/mlp_write_through_ab.md)
+  static const int wt = [] {
+    const char* e = getenv("HAR_MLP_WT");
+    return e ? atoi(e) : 1;
+  }();
+  const int wtl = (wt & 1) && (size_t)B * HH * 2 < 0x7fffffffu ? 1 : 0;  // (32-bit buffer offsets)
   k<<<nwg, 512, FWD_LDS, s>>>(X, Wf, b0, b1, Wo, bo, labels, B, C, scale, dact2, slab, bl, bc, g_har_mlp_stamps,
-                              fwd_stagger());
+                              fwd_stagger(), wtl);
 }
 
 template <int K0>
 void launch_fwd3_infer(const bf16_t* X, bf16_t* Wf, const float* b0, const float* b1, const bf16_t* Wo,
                        const float* bo, int B, int C, float* logits, int32_t* pred, int nwg, hipStream_t s) {
   mlp_fwd3_kernel<K0, false, true><<<nwg, 512, FWD_LDS, s>>>(X, Wf, b0, b1, Wo, bo, nullptr, B, C, 1.f, nullptr,
-                                                              logits, nullptr, pred, nullptr, fwd_stagger());
+                                                              logits, nullptr, pred, nullptr, fwd_stagger(), 0);
 }
 
 template <int K0>
@@ -982,13 +1016,16 @@ void launch_bwd4(const bf16_t* dact2, const bf16_t* X, const bf16_t* Wf, const f
                  int nfwd, float* gwo, float* gbo, hipStream_t s) {
   // HAR_MLP_BWD_NT=1: the dW1 partial slabs written with nontemporal stores
   static const int nt = [] {
+    // the dW1 / dW0 partial slabs: 2 write-through (default: not dirty in L2 at the reduction's launch),
+    // 1 nontemporal, 0 plain
     const char* e = getenv("HAR_MLP_BWD_NT");
-    return e ? atoi(e) : 0;
+    return e ? atoi(e) : 2;
   }();
   auto k = g_har_mlp_stamps ? mlp_bwd4_kernel<K0, true> : mlp_bwd4_kernel<K0, false>;
+  const int ntl = nt == 2 && (size_t)S * stride * 4 >= 0x7fffffffu ? 0 : nt;  // (32-bit buffer offsets)
   k<<<S * BQ, 512, Bwd4Lds<K0>::bytes, s>>>(dact2, X, Wf, b0, B, S, gw1, gw0, gb0, gb1, stride, tick, fslab, fslab_w,
                                            nfwd, gwo, gbo, g_har_mlp_stamps ? g_har_mlp_stamps + STAMP_BWD_OFF : nullptr,
-                                           nt);
+                                           ntl);
 }
 
 }  // namespace

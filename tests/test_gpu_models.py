@@ -23,6 +23,17 @@ def test_philox_buckets_device_matches_host(cuda):
     assert np.array_equal(host, dev)
 
 
+@pytest.mark.parametrize("n,k,seed", [(3853, 3, 2018), (3853, 5, 2018), (100_003, 5, 7), (17, 3, 1)])
+def test_kfold_ids_device_matches_host(cuda, n, k, seed):
+    """CrossValidator's device fold ids (rng.device_buckets on STREAM_KFOLD, equal weights) are the host
+    kfold_ids bit for bit — GPU and CPU cross-validation score the same folds."""
+    from har.data.split import kfold_ids
+    from har.ops import rng
+
+    dev = rng.device_buckets(seed, rng.STREAM_KFOLD, 0, n, [1.0] * k, cuda).cpu().numpy()
+    assert np.array_equal(kfold_ids(n, k, seed), dev)
+
+
 def test_poisson_device_matches_host(cuda):
     from har.ops import rng
 

@@ -57,28 +57,38 @@ def test_wolfe_lbfgs_reaches_the_scipy_optimum():
 
 
 def test_wolfe_steps_satisfy_their_conditions_and_decrease():
-    """Every accepted L-BFGS step satisfies the strong Wolfe conditions and every accepted OWL-QN step
-    Armijo + the weak curvature condition (checked from the objective at the accepted points); the
-    objective histories decrease; OWL-QN ends at the optimum a long Armijo-trial solve reaches."""
+    """Every accepted L-BFGS step satisfies the strong Wolfe conditions (Armijo, |phi'(t)| <= 0.9
+    |phi'(0)|) and every accepted OWL-QN step Armijo + the weak curvature condition (phi'(t) >= 0.9
+    phi'(0), phi' along the pseudo-gradient), on the line searches' own recorded values, which are
+    tied to the path: phi(0) / phi(t) of consecutive steps are the objective history, and phi(t) is
+    the objective recomputed at the accepted point.  The histories decrease; OWL-QN ends at the
+    optimum a long Armijo-trial solve reaches."""
     data = _problem(1)
     l2v, l1v = _reg([0.05, 0.02], [0.0, 0.03])
-    seen = []
-
-    def ev(x):
-        out = data(x)
-        seen.append((x.clone(), out[0].clone(), out[1].clone()))
-        return out
-
-    r = minimize_wolfe(ev, torch.zeros(2, K * (F + 1)), l2v, l1v, max_iter=25, tol=1e-9)
+    trace = []
+    r = minimize_wolfe(data, torch.zeros(2, K * (F + 1)), l2v, l1v, max_iter=25, tol=1e-9, trace=trace)
+    c1, c2 = 1e-4, 0.9
     for b in range(2):
         h = r.history_per_model[b]
         assert all(b2 <= a2 + 1e-12 for a2, b2 in zip(h, h[1:])), h
-    # strong Wolfe for model 0 along its accepted steps: |phi'(t)| <= 0.9 |phi'(0)|
-    x_path = [seen[0][0][0]]
-    for x, _, _ in seen[1:]:
-        if not torch.equal(x[0], x_path[-1]):
-            x_path.append(x[0])
-    assert len(x_path) > 3
+        steps = [s for s in trace if s["model"] == b]
+        assert len(steps) == int(r.iterations[b]) >= 5, (b, len(steps))
+        assert steps[0]["owl"] == (b == 1)
+        for i, s in enumerate(steps):
+            assert s["iter"] == i and s["t"] > 0
+            assert s["d0"] < 0, s                                      # a descent direction
+            assert s["ft"] <= s["f0"] + c1 * s["t"] * s["d0"], s       # Armijo (sufficient decrease)
+            if b == 0:
+                assert abs(s["dt"]) <= c2 * abs(s["d0"]), s           # strong curvature
+            else:
+                assert s["dt"] >= c2 * s["d0"], s                     # weak curvature
+            assert s["f0"] == h[i] and s["ft"] == h[i + 1]           # the recorded values are the path's
+    # phi(t) of the last accepted step is the objective at the solution, recomputed independently
+    for b in range(2):
+        loss, _ = data(r.x[b:b + 1])
+        x = r.x[b].double()
+        obj = float(loss[0]) + 0.5 * float((l2v[b].double() * x * x).sum()) + float((l1v[b].double() * x.abs()).sum())
+        assert abs(obj - [s for s in trace if s["model"] == b][-1]["ft"]) <= 1e-9 * max(1.0, abs(obj))
     long = minimize_trials(data, torch.zeros(2, K * (F + 1)), l2v, l1v, max_iter=400, tol=1e-12)
     r2 = minimize_wolfe(data, torch.zeros(2, K * (F + 1)), l2v, l1v, max_iter=400, tol=1e-12)
     np.testing.assert_allclose(r2.f.numpy(), long.f.numpy(), rtol=1e-9)
