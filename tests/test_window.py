@@ -85,3 +85,34 @@ def test_window_kernel_mlp_output(cuda, axes, window, stride):
     assert out.shape == (ref.shape[0], pad) and out.dtype == torch.bfloat16
     assert torch.count_nonzero(out[:, F:]) == 0
     torch.testing.assert_close(out[:, :F].float(), ref.to(torch.bfloat16).float(), rtol=0, atol=0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("stride,nwin", [(200, 100_000), (100, 131_071)])
+def test_window_kernel_large_counts_match_torch(cuda, stride, nwin):
+    """The large-count dispatches of the window kernel at >= 100k windows — stride 200 (16-lane groups,
+    padded per-window images) and stride 100 (8-lane groups on a shared span, the 1B-sample pass's shape)
+    — against the PyTorch oracle (torch ops on the device), fp32 features and the MLP-input rows."""
+    from har.features.window import window_features, window_features_mlp
+
+    W = 200
+    spec = StreamSpec(axes=3, window=W, seed=11 + stride)
+    n_seg = ((nwin - 1) * stride + W + W - 1) // W
+    s, _ = generate_stream(n_seg, spec, cuda)
+    s = s[: (nwin - 1) * stride + W]
+    assert window_count(s.shape[0], W, stride) == nwin
+    ref = window_features_torch(s, W, stride, 50.0)
+    out = window_features(s, W, stride, 50.0)
+    assert out.shape == ref.shape == (nwin, n_features(3))
+    nb = 30
+    assert float((out[:, :nb] - ref[:, :nb]).abs().max()) <= 1.0 / W + 1e-6
+    # (the oracle computes in float64 on the device; bins may move a boundary sample by one bin)
+    torch.testing.assert_close(out[:, nb:], ref[:, nb:].to(out.dtype), rtol=2e-4, atol=2e-4, equal_nan=True)
+    F = n_features(3)
+    g = torch.Generator(device=cuda).manual_seed(3)
+    mean = torch.randn(F, device=cuda, generator=g)
+    inv_std = torch.rand(F, device=cuda, generator=g) + 0.5
+    mo = window_features_mlp(s, W, stride, 50.0, mean, inv_std, 64)
+    assert mo.shape == (nwin, 64) and torch.count_nonzero(mo[:, F:]) == 0
+    want = ((torch.nan_to_num(out, nan=-1.0) - mean) * inv_std).to(torch.bfloat16)
+    torch.testing.assert_close(mo[:, :F].float(), want.float(), rtol=0, atol=0)
