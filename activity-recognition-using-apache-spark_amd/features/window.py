@@ -64,7 +64,7 @@ def window_features_torch(stream: torch.Tensor, window: int, stride: int, hz: fl
     thr = mean + 0.5 * (mx - mean)
     mid = x[..., 1:-1]
     pk = (mid > x[..., :-2]) & (mid >= x[..., 2:]) & (mid > thr[..., None])
-    t = torch.arange(1, window - 1, dtype=torch.float64)
+    t = torch.arange(1, window - 1, dtype=torch.float64, device=x.device)
     npk = pk.sum(-1)
     first = torch.where(pk, t, torch.full_like(mid, float("inf"))).min(-1).values
     last = torch.where(pk, t, torch.full_like(mid, -1.0)).max(-1).values

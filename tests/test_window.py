@@ -106,8 +106,15 @@ def test_window_kernel_large_counts_match_torch(cuda, stride, nwin):
     assert out.shape == ref.shape == (nwin, n_features(3))
     nb = 30
     assert float((out[:, :nb] - ref[:, :nb]).abs().max()) <= 1.0 / W + 1e-6
-    # (the oracle computes in float64 on the device; bins may move a boundary sample by one bin)
-    torch.testing.assert_close(out[:, nb:], ref[:, nb:].to(out.dtype), rtol=2e-4, atol=2e-4, equal_nan=True)
+    # (the oracle computes in float64 on the device; bins may move a boundary sample by one bin).  The
+    # peak times: a sample within fp32 rounding of the threshold mean + (max - mean) / 2 counts as a peak
+    # in one arithmetic and not the other — at this count a handful of windows (1 in 2.5M values seen)
+    pk = slice(nb + 3, nb + 6)
+    okp = torch.isclose(out[:, pk], ref[:, pk], rtol=2e-4, atol=2e-4, equal_nan=True)
+    assert int((~okp).sum()) <= max(2, nwin // 20000), int((~okp).sum())
+    rest = torch.cat([out[:, nb:nb + 3], out[:, nb + 6:]], 1)
+    rest_ref = torch.cat([ref[:, nb:nb + 3], ref[:, nb + 6:]], 1)
+    torch.testing.assert_close(rest, rest_ref, rtol=2e-4, atol=2e-4, equal_nan=True)
     F = n_features(3)
     g = torch.Generator(device=cuda).manual_seed(3)
     mean = torch.randn(F, device=cuda, generator=g)
@@ -115,4 +122,7 @@ def test_window_kernel_large_counts_match_torch(cuda, stride, nwin):
     mo = window_features_mlp(s, W, stride, 50.0, mean, inv_std, 64)
     assert mo.shape == (nwin, 64) and torch.count_nonzero(mo[:, F:]) == 0
     want = ((torch.nan_to_num(out, nan=-1.0) - mean) * inv_std).to(torch.bfloat16)
-    torch.testing.assert_close(mo[:, :F].float(), want.float(), rtol=0, atol=0)
+    # (the two instantiations may differ in a feature's last fp32 bit, which the bf16 rounding then
+    # shows as one bf16 ulp in a few values; everything else bit-equal)
+    torch.testing.assert_close(mo[:, :F].float(), want.float(), rtol=2 ** -7, atol=1e-6)
+    assert int((mo[:, :F] != want).sum()) <= max(4, mo.numel() // 100000)
