@@ -618,34 +618,6 @@ __global__ __launch_bounds__(512) void mlp_bwd4_kernel(
                                                               : s16x8_t{0, 0, 0, 0, 0, 0, 0, 0});
   const int tlast = ntiles - 1;
 
-  // ---- epilogue images: after the last tile both roles stage their partials in LDS (the tile buffers
-  // are free), dW1 [256 j][64 u] (consumers) and dW0 [64 u][K0] (producers), and all 512 threads store
-  // whole rows — 16 consecutive lanes per 256-byte row, every store instruction full lines — instead of
-  // each wave storing its accumulators as 16 x 64-byte (dW1) / 4-byte (dW0) pieces per instruction ----
-  constexpr int SGP = BQU + 4, S0P = K0 + 4;  // image pitches (floats): conflict-free 16-byte writes
-  float* const stg1 = reinterpret_cast<float*>(lds);  // [HH][SGP]
-  float* const stg0 = stg1 + HH * SGP;                // [BQU][S0P]
-  static_assert((size_t)(HH * SGP + BQU * S0P) * 4 <= L::bytes, "the epilogue images fit the tile buffers");
-  auto store_images = [&]() __attribute__((always_inline)) {
-    constexpr int C1 = HH * BQU / 4, C0 = BQU * K0 / 4, CR0 = K0 / 4;  // 16-byte chunks
-    const __amdgpu_buffer_rsrc_t r1 = wt_rsrc(gw1), r0 = wt_rsrc(gw0);
-    for (int c = tid; c < C1 + C0; c += 512) {
-      if (c < C1) {
-        const int row = c >> 4, c4 = c & 15;
-        const u32x4_t v = *reinterpret_cast<const u32x4_t*>(stg1 + row * SGP + 4 * c4);
-        const size_t e = (size_t)slice * slab_stride + (size_t)row * HH + qu0 + 4 * c4;
-        if (nt_slab == 2) wt_store16(r1, (uint32_t)(e * 4), v);
-        else *reinterpret_cast<u32x4_t*>(gw1 + e) = v;
-      } else {
-        const int cc = c - C1, row = cc / CR0, c4 = cc - row * CR0;
-        const u32x4_t v = *reinterpret_cast<const u32x4_t*>(stg0 + row * S0P + 4 * c4);
-        const size_t e = (size_t)slice * slab_stride + (size_t)(qu0 + row) * K0 + 4 * c4;
-        if (nt_slab == 2) wt_store16(r0, (uint32_t)(e * 4), v);
-        else *reinterpret_cast<u32x4_t*>(gw0 + e) = v;
-      }
-    }
-  };
-
   if (prod) {
     // ================================ producer ================================
     const int ptid = tid;  // 0..255
@@ -656,7 +628,6 @@ __global__ __launch_bounds__(512) void mlp_bwd4_kernel(
     // (lane offsets 32-bit, tile bases wave-uniform: the loads take the SGPR-base form)
     const uint32_t d2src = (uint32_t)((ptid >> 5) * HH + (ptid & 31) * 8);  // (unsigned: zero-extended offsets)
     const int d2dst = (ptid >> 5) * BDP + (ptid & 31) * 8;
-
     // (macros, not lambdas: a lambda-captured register array is kept in scratch)
     // two register sets of dact2 pieces: the tile staged at iteration i was loaded at iteration i - 2
     // (one iteration ahead left ~700 cycles of the refill still in flight at its use, profiles/r5)
@@ -829,13 +800,21 @@ __global__ __launch_bounds__(512) void mlp_bwd4_kernel(
 #undef HAR_B4_STAGE_XR
     HAR_STAMP(8, 34)
     if (n > 0) tile_c(n - 1);
-    __syncthreads();  // (epilogue A, paired with the consumers') every wave is done with the tile buffers
+    float* w0o = gw0 + (size_t)slice * slab_stride;
+    if (nt_slab == 2) {  // write-through (see the consumers' slab stores)
+      const __amdgpu_buffer_rsrc_t rs = wt_rsrc(gw0);
 #pragma unroll
-    for (int f = 0; f < NFB; ++f)
+      for (int f = 0; f < NFB; ++f)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) stg0[(16 * pw + 4 * g + r) * S0P + 16 * f + c16] = acc0[f][r];
-    __syncthreads();  // (epilogue B) both images complete
-    store_images();
+        for (int r = 0; r < 4; ++r)
+          wt_store4(rs, (uint32_t)(((size_t)slice * slab_stride + (size_t)(qu0 + 16 * pw + 4 * g + r) * K0 + 16 * f + c16) * 4),
+                    acc0[f][r]);
+    } else {
+#pragma unroll
+      for (int f = 0; f < NFB; ++f)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) w0o[(size_t)(qu0 + 16 * pw + 4 * g + r) * K0 + 16 * f + c16] = acc0[f][r];
+    }
     if (c16 == 0) *reinterpret_cast<f32x4_t*>(gb0 + (size_t)slice * slab_stride + qu0 + 16 * pw + 4 * g) = accd0;
     // the forward's dWout / dbout slabs (one per forward workgroup) -> gwo / gbo: 4-column group
     // 4 b + pw per producer wave (b the XCD-remapped index: the 8 groups of a 128-byte line in two
@@ -970,17 +949,24 @@ __global__ __launch_bounds__(512) void mlp_bwd4_kernel(
     if (i < n) citer(i, std::integral_constant<int, 0>{});
     HAR_STAMP(8, 34)
     __builtin_amdgcn_s_setprio(0);
-    // ---- this wave's part of slab `slice` (flat parameter layout), through the epilogue image ----
-    // (nt_slab: 2 write-through — sc1: the slabs are not left dirty in L2 for the reduction launch's
-    // boundary — else plain)
-    __syncthreads();  // (epilogue A)
+    // ---- this wave's parts of slab `slice` (flat parameter layout) ----
+    // (staging both roles' partials through an LDS image and storing whole rows measured 0.5 us slower
+    // per step on one box: 0.0540 / 0.0536 / 0.0535 vs 0.0530 / 0.0532 / 0.0530 ms, gpurun_out/ab_epi)
+    float* w1o = gw1 + (size_t)slice * slab_stride;
+    // nt_slab: 1 nontemporal, 2 write-through (sc1: the slabs are not left dirty in L2 for the reduction
+    // launch's boundary), 0 plain
+    const __amdgpu_buffer_rsrc_t w1rs = wt_rsrc(gw1);
 #pragma unroll
     for (int j = 0; j < 4; ++j)
 #pragma unroll
       for (int u = 0; u < 4; ++u)
-        *reinterpret_cast<f32x4_t*>(stg1 + (16 * (4 * pw + j) + c16) * SGP + 16 * u + 4 * g) = acc1[j][u];
-    __syncthreads();  // (epilogue B)
-    store_images();
+        if (nt_slab == 2)
+          wt_store16(w1rs, (uint32_t)(((size_t)slice * slab_stride + (size_t)(16 * (4 * pw + j) + c16) * HH + qu0 + 16 * u + 4 * g) * 4),
+                     __builtin_bit_cast(u32x4_t, acc1[j][u]));
+        else if (nt_slab)
+          nt_store16(w1o + (size_t)(16 * (4 * pw + j) + c16) * HH + qu0 + 16 * u + 4 * g, __builtin_bit_cast(u32x4_t, acc1[j][u]));
+        else
+          *reinterpret_cast<f32x4_t*>(w1o + (size_t)(16 * (4 * pw + j) + c16) * HH + qu0 + 16 * u + 4 * g) = acc1[j][u];
     if (g == 0) gb1[(size_t)slice * slab_stride + 16 * (4 * q + pw) + c16] = accb[0];
   }
   if constexpr (STAMP) __builtin_amdgcn_s_waitcnt(0x0f70);
@@ -989,17 +975,6 @@ __global__ __launch_bounds__(512) void mlp_bwd4_kernel(
 }
 
 // HAR_MLP_FWD_STAGGER=1: waves 4..7 run their softmax after the MFMA stages (off by default)
-// dact2 / dWout slab stores write-through (sc1; HAR_MLP_WT=0: plain / nontemporal): the 33.5 MB of
-// dact2 are then not dirty in the L2s when the backward launches — forward 22.0 -> 19.3 us, step
-// 0.0571 -> 0.0540 ms (profiles/r6/mlp_write_through_ab.md)
-static bool wt_enabled() {
-  static const bool v = [] {
-    const char* e = getenv("HAR_MLP_WT");
-    return e ? atoi(e) != 0 : true;
-  }();
-  return v;
-}
-
 static int fwd_stagger() {
   static const int v = [] {
     const char* e = getenv("HAR_MLP_FWD_STAGGER");
@@ -1021,7 +996,14 @@ void launch_fwd3(const bf16_t* X, bf16_t* Wf, const float* b0, const float* b1, 
            : fill == 2      ? mlp_fwd3_kernel<K0, false, false, 2>
            : fill >= 3      ? mlp_fwd3_kernel<K0, false, false, 3>
                             : mlp_fwd3_kernel<K0, false>;
-  const int wtl = wt_enabled() && (size_t)B * HH * 2 < 0x7fffffffu ? 1 : 0;  // (32-bit buffer offsets)
+  // dact2 / dWout slab stores write-through (sc1; HAR_MLP_WT=0: plain / nontemporal): the 33.5 MB of
+  // dact2 are then not dirty in the L2s when the backward launches — forward 22.0 -> 19.3 us, step
+  // 0.0571 -> 0.0540 ms (profiles/r6/mlp_write_through_ab.md)
+  static const int wt = [] {
+    const char* e = getenv("HAR_MLP_WT");
+    return e ? atoi(e) : 1;
+  }();
+  const int wtl = (wt & 1) && (size_t)B * HH * 2 < 0x7fffffffu ? 1 : 0;  // (32-bit buffer offsets)
   k<<<nwg, 512, FWD_LDS, s>>>(X, Wf, b0, b1, Wo, bo, labels, B, C, scale, dact2, slab, bl, bc, g_har_mlp_stamps,
                               fwd_stagger(), wtl);
 }
@@ -1037,14 +1019,15 @@ template <int K0>
 void launch_bwd4(const bf16_t* dact2, const bf16_t* X, const bf16_t* Wf, const float* b0, int B, int S, float* gw1,
                  float* gw0, float* gb0, float* gb1, int64_t stride, int32_t* tick, const float* fslab, int fslab_w,
                  int nfwd, float* gwo, float* gbo, hipStream_t s) {
+  // HAR_MLP_BWD_NT=1: the dW1 partial slabs written with nontemporal stores
   static const int nt = [] {
     // the dW1 / dW0 partial slabs: 2 write-through (default: not dirty in L2 at the reduction's launch),
     // 1 nontemporal, 0 plain
     const char* e = getenv("HAR_MLP_BWD_NT");
     return e ? atoi(e) : 2;
   }();
-  const int ntl = nt == 2 && (size_t)S * stride * 4 >= 0x7fffffffu ? 0 : nt;  // (32-bit buffer offsets)
   auto k = g_har_mlp_stamps ? mlp_bwd4_kernel<K0, true> : mlp_bwd4_kernel<K0, false>;
+  const int ntl = nt == 2 && (size_t)S * stride * 4 >= 0x7fffffffu ? 0 : nt;  // (32-bit buffer offsets)
   k<<<S * BQ, 512, Bwd4Lds<K0>::bytes, s>>>(dact2, X, Wf, b0, B, S, gw1, gw0, gb0, gb1, stride, tick, fslab, fslab_w,
                                            nfwd, gwo, gbo, g_har_mlp_stamps ? g_har_mlp_stamps + STAMP_BWD_OFF : nullptr,
                                            ntl);
