@@ -387,28 +387,6 @@ __global__ __launch_bounds__(512) void mlp_fwd3_kernel(
   if (nt > 0) {
     stage1(0);
     load_x(1);
-    // The W1^T fragment copy the backward of this step reads (Wf + H K0 + H H; the Adam kernel writes
-    // only the W0 / W1 copies): fragment f = (unit block ub = f & 15, k chunk jc = f >> 4) holds
-    // W1[32 jc .. + 32][16 ub .. + 16], i.e. rows this workgroup's wave jc has in registers (W1 rows
-    // 32 jc .. + 32 = its units): transposed through the (still unused) partial-logit buffer.
-    for (int f = blockIdx.x; !INFER && f < 8 * (HH / 16); f += gridDim.x) {
-      const int ub = f & 15, jc = f >> 4;
-      if (wave == jc) {
-        bf16_t* tt = reinterpret_cast<bf16_t*>(zs) + wave * 32 * 24;  // this wave's [32 j][16 u] (+ pad)
-        const int kcs = ((ub >> 1) - krot) & (KC - 1);
-#pragma unroll
-        for (int t = 0; t < 2; ++t)
-#pragma unroll
-          for (int kc = 0; kc < KC; ++kc)
-            if (kc == kcs && (g >> 1) == (ub & 1))
-              *reinterpret_cast<bf16x8_t*>(tt + (16 * t + c16) * 24 + 8 * (g & 1)) = w1f[t][kc];
-        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the wave's own LDS stores
-        __builtin_amdgcn_wave_barrier();
-        *reinterpret_cast<bf16x8_t*>(Wf + HH * K0 + HH * HH + (size_t)(ub * KC + jc) * 512 + frag_lane_off(lane)) =
-            frag_tr(tt, 24, 0, lane);
-        __builtin_amdgcn_wave_barrier();
-      }
-    }
     __syncthreads();  // h1 of tile 0
     stage23(0, 0, no_fill);
     stage1(1);
@@ -486,6 +464,29 @@ __global__ __launch_bounds__(512) void mlp_fwd3_kernel(
   }
   HAR_STAMP(FW, 34)
   if constexpr (INFER) return;
+  // The W1^T fragment copy the backward of this step reads (Wf + H K0 + H H; the Adam kernel writes
+  // only the W0 / W1 copies): fragment f = (unit block ub = f & 15, k chunk jc = f >> 4) holds
+  // W1[32 jc .. + 32][16 ub .. + 16], i.e. rows this workgroup's wave jc has in registers (W1 rows
+  // 32 jc .. + 32 = its units): transposed through the h1 buffer, free after the last tile.  (Done here,
+  // not in the prologue, where wave jc had to wait for its W1 loads before the workgroup's first barrier.)
+  for (int f = blockIdx.x; nt > 0 && f < 8 * (HH / 16); f += gridDim.x) {
+    const int ub = f & 15, jc = f >> 4;
+    if (wave == jc) {
+      bf16_t* tt = h1s + wave * 32 * 24;  // this wave's [32 j][16 u] (+ pad)
+      const int kcs = ((ub >> 1) - krot) & (KC - 1);
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int kc = 0; kc < KC; ++kc)
+          if (kc == kcs && (g >> 1) == (ub & 1))
+            *reinterpret_cast<bf16x8_t*>(tt + (16 * t + c16) * 24 + 8 * (g & 1)) = w1f[t][kc];
+      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the wave's own LDS stores
+      __builtin_amdgcn_wave_barrier();
+      *reinterpret_cast<bf16x8_t*>(Wf + HH * K0 + HH * HH + (size_t)(ub * KC + jc) * 512 + frag_lane_off(lane)) =
+          frag_tr(tt, 24, 0, lane);
+      __builtin_amdgcn_wave_barrier();
+    }
+  }
   if (nt > 0) stage5((nt - 1) & 1, tile_of(nt - 1) * FRT);
   // ---- this workgroup's slab: dWout rows 0..15 x this wave's units, dbout; loss, #correct ----
   float* out = slab + (size_t)blockIdx.x * FWD_SLAB;
