@@ -520,6 +520,17 @@ __device__ __forceinline__ float vmax(float a, float b) {
   asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
   return r;
 }
+// three-operand forms: pass 1 folds two run samples into the running min / max per instruction
+__device__ __forceinline__ float vmin3(float a, float b, float c) {
+  float r;
+  asm("v_min3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+__device__ __forceinline__ float vmax3(float a, float b, float c) {
+  float r;
+  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
 
 // One sample's peak flags into the two shift registers: R = 2R + (x > prev), PT = 2PT + (x > prev &&
 // x > thr), as two compares into SGPR masks and two v_addc (R + R + carry); written by hipcc it is a
@@ -538,6 +549,7 @@ __device__ __forceinline__ void flag_step(uint32_t& R, uint32_t& PT, float x, fl
 
 // bin of a sample: (x - lo) * (10 / range) in fp32, the legacy kernel's arithmetic (x >= lo, so the
 // conversion never sees a negative), clamped to bin 9
+__device__ __forceinline__ uint32_t bin_raw(float x, float sc, float lo) { return (uint32_t)((x - lo) * sc); }
 __device__ __forceinline__ uint32_t bin_of(float x, float sc, float lo) {
   const uint32_t b = (uint32_t)((x - lo) * sc);
   return b < (uint32_t)(NB - 1) ? b : (uint32_t)(NB - 1);
@@ -551,69 +563,18 @@ __device__ __forceinline__ uint32_t bin_of(float x, float sc, float lo) {
 __host__ __device__ constexpr int p32_pos(int t, int A) { return t * A + 4 * (t >> 5); }
 __host__ __device__ inline int p32_pitch(int W, int A) { return (p32_pos(W, A) + 4 + 3) & ~3; }
 
-// FIXC: the run length is RCMAX itself (a compile-time constant): no per-k-step `k < C` guards, whose
-// compare + branch cost ~6 instructions per step and sample pass, and only the registers the runs use
-template <int A, int LPW, bool MLP, int RCMAX, bool P32 = false, int WPE = 1, bool FIXC = false>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void window_features_reg_kernel(const float* __restrict__ stream, int W,
-                                                                  int stride, int64_t n_windows, float ms_per_sample,
-                                                                  float* __restrict__ out, int ld_out, MlpOut mo,
-                                                                  int Carg, int wpb, int ipw) {
-  const int C = FIXC ? RCMAX : Carg;
-  static_assert(LPW == 8 || LPW == 16 || LPW == 32 || LPW == 64, "groups of 8, 16, 32 or 64 lanes");
+// The statistics of one staged batch (windows w0 .. w0 + nwin - 1, their samples at `span`, `ip` floats
+// per window image): each lane reads its run into registers, then both passes, the reductions and the
+// row write.
+template <int A, int LPW, bool MLP, int RCMAX, bool P32, bool FIXC>
+__device__ __forceinline__ void reg_window_batch(const float* span, int64_t w0, int nwin, int W, int ip, int C,
+                                                 float ms_per_sample, float* __restrict__ out, int ld_out,
+                                                 const MlpOut& mo) {
   constexpr int T3 = A / 3, GPW = 64 / LPW;
-  extern __shared__ __attribute__((aligned(16))) float lds[];
-  const int nt = (int)blockDim.x, tid = (int)threadIdx.x;
-  const int64_t w0 = (int64_t)blockIdx.x * wpb;
-  const int nwin = (int)min<int64_t>(wpb, n_windows - w0);
-  float* const span = lds + PAD;
-  // image pitch (floats) between consecutive windows: P32 images, padded images (ipw > 0, non-overlapping
-  // windows: a pitch of 16 mod 32 floats puts the two 16-lane windows of a 32-lane LDS bank group on
-  // disjoint banks — the contiguous 600-float pitch of W = 200 x 3 axes had 32% bank-conflict cycles,
-  // profiles/r5/window_pmc.md), or the shared span (stride A floats per window)
-  const int ip = P32 ? p32_pitch(W, A) : ipw > 0 ? ipw : stride * A;
+  const int tid = (int)threadIdx.x;
   auto pos = [&](int t) { return P32 ? p32_pos(t, A) : t * A; };
-
-  if (P32 || ipw > 0) {  // ---- stage the windows, one padded image each (float4 granules) ----
-    const v4f* s4 = reinterpret_cast<const v4f*>(stream + w0 * (int64_t)W * A);
-    const int n4w = W * A / 4, n4 = nwin * n4w;
-    const uint32_t magic = 0xffffffffu / (uint32_t)n4w + 1u;  // f / n4w = umulhi(f, magic) for f * n4w < 2^32
-    for (int f0 = tid; f0 < n4; f0 += 8 * nt) {
-      v4f r[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) r[u] = s4[min(f0 + u * nt, n4 - 1)];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int f = min(f0 + u * nt, n4 - 1), wl = (int)__umulhi((uint32_t)f, magic), e = 4 * (f - wl * n4w);
-        *reinterpret_cast<v4f*>(span + wl * ip + e + (P32 ? 4 * (e / (32 * A)) : 0)) = r[u];
-      }
-    }
-  } else {
-  // ---- stage the span: samples [w0 * stride, (w0 + nwin - 1) * stride + W), A floats each ----
-  {
-    const float* src = stream + w0 * stride * A;
-    const int nspan = ((nwin - 1) * stride + W) * A;
-    int done = 0;
-    if ((reinterpret_cast<uintptr_t>(src) & 15) == 0) {
-      const int n4 = nspan >> 2;
-      const v4f* s4 = reinterpret_cast<const v4f*>(src);
-      v4f* d4 = reinterpret_cast<v4f*>(span);
-      // unconditional (clamped) loads and stores: no exec-masked branches between them, so all eight
-      // loads are in flight before the first store waits (a clamped slot rewrites the last float4)
-      for (int f0 = tid; f0 < n4; f0 += 8 * nt) {
-        v4f r[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) r[u] = s4[min(f0 + u * nt, n4 - 1)];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) d4[min(f0 + u * nt, n4 - 1)] = r[u];
-      }
-      done = n4 * 4;
-    }
-    for (int e = done + tid; e < nspan; e += nt) span[e] = src[e];
-  }
-  }
-  __syncthreads();
-
-  const int lane = tid & 63, wave = tid >> 6, sub = lane % LPW;
+  const int lane = tid & 63;
+  const int wave = tid >> 6, sub = lane % LPW;
   const int g = wave % T3;
   const int wi = GPW * (wave / T3) + lane / LPW;
   const bool valid = wi < nwin;
@@ -656,9 +617,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
 #pragma unroll
         for (int c = 0; c < 3; ++c) {
           const float v = x[c][k];
-          s[c] += v; q[c] = fmaf(v, v, q[c]); lo[c] = vmin(lo[c], v); hi[c] = vmax(hi[c], v);
+          s[c] += v; q[c] = fmaf(v, v, q[c]);
         }
       }
+    // min / max: samples 1, 2 | 3, 4 | ... in one v_min3 / v_max3 each (sample 0 is the seed)
+#pragma unroll
+    for (int k = 1; k < RCMAX; k += 2) {
+      if (k + 1 < RCMAX && k + 1 < C) {
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+          lo[c] = vmin3(lo[c], x[c][k], x[c][k + 1]);
+          hi[c] = vmax3(hi[c], x[c][k], x[c][k + 1]);
+        }
+      } else if (k < C) {
+#pragma unroll
+        for (int c = 0; c < 3; ++c) { lo[c] = vmin(lo[c], x[c][k]); hi[c] = vmax(hi[c], x[c][k]); }
+      }
+    }
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
       const float S = greduce<LPW, float>(s[c], [](float a, float b) { return a + b; }, sw) - D * xl[c];
@@ -679,6 +654,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     thr[c] = mean[c] + 0.5f * (mx[c] - mean[c]);
   }
   float ad[3] = {0.f, 0.f, 0.f}, v2[3] = {0.f, 0.f, 0.f}, res = 0.f, cxy = 0.f, cxz = 0.f, cyz = 0.f;
+  // per-lane bin counts packed SB bits per slot: runs of C <= 31 samples fit 5 bits, so the 11 slots of
+  // an unclamped bin (0..10: (x - lo) * sc reaches 10 only at x == max) fit 55 bits and the clamp to
+  // bin 9 happens once per window (slot 10 folded into bin 9) instead of once per sample
+  constexpr int SB = RCMAX <= 31 ? 5 : 6;
+  const auto slot = [](uint64_t hh, int j) { return (uint32_t)(hh >> (SB * j)) & ((1u << SB) - 1u); };
   uint64_t h[3] = {0, 0, 0};
   uint32_t R[3] = {0, 0, 0}, PT[3] = {0, 0, 0};  // bit j <-> run sample k = C - 1 - j
 #pragma unroll
@@ -692,13 +672,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         d[c] = dc;
         ad[c] += fabsf(dc);
         v2[c] = fmaf(dc, dc, v2[c]);
-        h[c] += 1ull << __umul24(bin_of(xv, sc[c], off[c]), 6u);  // v_mul_u32_u24, not the quarter-rate mul_lo
+        // v_mul_u32_u24, not the quarter-rate mul_lo; 5-bit slots take the unclamped bin (slot 10: x == max)
+        h[c] += 1ull << __umul24(SB == 5 ? bin_raw(xv, sc[c], off[c]) : bin_of(xv, sc[c], off[c]), (uint32_t)SB);
         flag_step(R[c], PT[c], xv, pv, thr[c]);
       }
       res += __builtin_amdgcn_sqrtf(fmaf(x[0][k], x[0][k], fmaf(x[1][k], x[1][k], x[2][k] * x[2][k])));
       cxy = fmaf(d[0], d[1], cxy);
       cxz = fmaf(d[0], d[2], cxz);
       cyz = fmaf(d[1], d[2], cyz);
+      // (fixed-length runs: pin the resultant sum to its k-step — left free, LLVM sinks every square root
+      // past the reductions and keeps all 75 run samples alive there: 65 spilled VGPRs)
+      if constexpr (FIXC) asm volatile("" : "+v"(res));
     }
 
   // peak positions: 0 < t < W - 1 (t = tb + k), i.e. bits j in [C - 1 - kh, C - 1 - kl]
@@ -747,7 +731,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     uint32_t hw[5];
 #pragma unroll
     for (int j = 0; j < 5; ++j)
-      hw[j] = greduce<LPW, uint32_t>((uint32_t)((h[c] >> (12 * j)) & 63) | ((uint32_t)((h[c] >> (12 * j + 6)) & 63) << 16),
+      hw[j] = greduce<LPW, uint32_t>(slot(h[c], 2 * j) | (slot(h[c], 2 * j + 1) + (j == 4 && SB == 5 ? slot(h[c], 10) : 0u)) << 16,
                                      usum, sw);
     // lane `sub` writes bin `sub` (and bin sub + 8 for 8-lane groups)
 #pragma unroll
@@ -789,6 +773,71 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     v = sub == 3 ? ryz : v;  f = sub == 3 ? off_corr + 3 * g + 2 : f;
     emit(sub < 4, f, v);
   }
+}
+
+// FIXC: the run length is RCMAX itself (a compile-time constant): no per-k-step `k < C` guards, whose
+// compare + branch cost ~6 instructions per step and sample pass, and only the registers the runs use.
+// (A persistent variant — the next batch's span copied HBM -> LDS by global_load_lds while the current one
+// is computed from registers — measured slower on the stride-100 shape: 83 us with 4-wave and 103 us with
+// 1-wave blocks vs 63 us one-shot at 131k windows, and 1.3x slower at 1.3M; one-shot blocks it is.)
+template <int A, int LPW, bool MLP, int RCMAX, bool P32 = false, int WPE = 1, bool FIXC = false>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void window_features_reg_kernel(const float* __restrict__ stream, int W,
+                                                                  int stride, int64_t n_windows, float ms_per_sample,
+                                                                  float* __restrict__ out, int ld_out, MlpOut mo,
+                                                                  int Carg, int wpb, int ipw) {
+  const int C = FIXC ? RCMAX : Carg;
+  static_assert(LPW == 8 || LPW == 16 || LPW == 32 || LPW == 64, "groups of 8, 16, 32 or 64 lanes");
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int nt = (int)blockDim.x, tid = (int)threadIdx.x;
+  float* const span = lds + PAD;
+  // image pitch (floats) between consecutive windows: P32 images, padded images (ipw > 0, non-overlapping
+  // windows: a pitch of 16 mod 32 floats puts the two 16-lane windows of a 32-lane LDS bank group on
+  // disjoint banks — the contiguous 600-float pitch of W = 200 x 3 axes had 32% bank-conflict cycles,
+  // profiles/r5/window_pmc.md), or the shared span (stride A floats per window)
+  const int ip = P32 ? p32_pitch(W, A) : ipw > 0 ? ipw : stride * A;
+
+  const int64_t w0 = (int64_t)blockIdx.x * wpb;
+  const int nwin = (int)min<int64_t>(wpb, n_windows - w0);
+  if (P32 || ipw > 0) {  // ---- stage the windows, one padded image each (float4 granules) ----
+    const v4f* s4 = reinterpret_cast<const v4f*>(stream + w0 * (int64_t)W * A);
+    const int n4w = W * A / 4, n4 = nwin * n4w;
+    const uint32_t magic = 0xffffffffu / (uint32_t)n4w + 1u;  // f / n4w = umulhi(f, magic) for f * n4w < 2^32
+    for (int f0 = tid; f0 < n4; f0 += 8 * nt) {
+      v4f r[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) r[u] = s4[min(f0 + u * nt, n4 - 1)];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int f = min(f0 + u * nt, n4 - 1), wl = (int)__umulhi((uint32_t)f, magic), e = 4 * (f - wl * n4w);
+        *reinterpret_cast<v4f*>(span + wl * ip + e + (P32 ? 4 * (e / (32 * A)) : 0)) = r[u];
+      }
+    }
+  } else {
+  // ---- stage the span: samples [w0 * stride, (w0 + nwin - 1) * stride + W), A floats each ----
+  {
+    const float* src = stream + w0 * stride * A;
+    const int nspan = ((nwin - 1) * stride + W) * A;
+    int done = 0;
+    if ((reinterpret_cast<uintptr_t>(src) & 15) == 0) {
+      const int n4 = nspan >> 2;
+      const v4f* s4 = reinterpret_cast<const v4f*>(src);
+      v4f* d4 = reinterpret_cast<v4f*>(span);
+      // unconditional (clamped) loads and stores: no exec-masked branches between them, so all eight
+      // loads are in flight before the first store waits (a clamped slot rewrites the last float4)
+      for (int f0 = tid; f0 < n4; f0 += 8 * nt) {
+        v4f r[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) r[u] = s4[min(f0 + u * nt, n4 - 1)];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) d4[min(f0 + u * nt, n4 - 1)] = r[u];
+      }
+      done = n4 * 4;
+    }
+    for (int e = done + tid; e < nspan; e += nt) span[e] = src[e];
+  }
+  }
+  __syncthreads();
+  reg_window_batch<A, LPW, MLP, RCMAX, P32, FIXC>(span, w0, nwin, W, ip, C, ms_per_sample, out, ld_out, mo);
 }
 
 int cu_count() {
@@ -910,10 +959,11 @@ int launch_axes(const float* stream, int64_t n_samples, int window, int stride, 
         if (p32)
           window_features_reg_kernel<A, 16, MLP, 32, true><<<grid, nt, bytes, s>>>(stream, window, stride, n_windows,
                                                                                    ms, out, ld_out, mo, C, wpb, ipw);
-        else if (lpw == 8 && C > 17 && C <= 25)  // (the stride-100 200-sample shape: 8 x 25, held to 128 VGPRs:
-                                                 // 4 waves per SIMD, not 3; fixed-length runs spilled 65 VGPRs there)
-          window_features_reg_kernel<A, 8, MLP, 25, false, 4><<<grid, nt, bytes, s>>>(stream, window, stride, n_windows,
-                                                                                     ms, out, ld_out, mo, C, wpb, ipw);
+        else if (lpw == 8 && C == 25) {  // (the stride-100 200-sample shape: 8 x 25, held to 128 VGPRs: 4 waves
+                                          // per SIMD, not 3; fixed-length runs)
+          window_features_reg_kernel<A, 8, MLP, 25, false, 4, true><<<grid, nt, bytes, s>>>(
+              stream, window, stride, n_windows, ms, out, ld_out, mo, C, wpb, ipw);
+        }
         else if (lpw == 16 && C == 13)  // (the 200-sample non-overlapping shape: 16 x 13, fixed-length runs)
           window_features_reg_kernel<A, 16, MLP, 13, false, 1, true><<<grid, nt, bytes, s>>>(
               stream, window, stride, n_windows, ms, out, ld_out, mo, C, wpb, ipw);

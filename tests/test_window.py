@@ -126,3 +126,4 @@ def test_window_kernel_large_counts_match_torch(cuda, stride, nwin):
     # shows as one bf16 ulp in a few values; everything else bit-equal)
     torch.testing.assert_close(mo[:, :F].float(), want.float(), rtol=2 ** -7, atol=1e-6)
     assert int((mo[:, :F] != want).sum()) <= max(4, mo.numel() // 100000)
+

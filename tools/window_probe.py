@@ -64,6 +64,10 @@ for name, legacy in modes:
     print(f"{name:7s} 3 axes W=200 MLP rows : {us:8.1f} us  {s3.numel() * 4 / us / 1e6:6.2f} TB/s")
     us = timed(lambda: window_features(s3, 200, 100, 20.0))
     print(f"{name:7s} 3 axes W=200 stride=100: {us:8.1f} us  {s3.numel() * 4 / us / 1e6:6.2f} TB/s ({s3.shape[0] // 100 - 1} windows)")
+    # the 1B-sample stream pass's kernel: 50%-overlapping windows straight into bf16 MLP rows
+    out2 = torch.empty(s3.shape[0] // 100 - 1, 64, dtype=torch.bfloat16, device=dev)
+    us = timed(lambda: window_features_mlp(s3, 200, 100, 20.0, mean, inv, 64, -1.0, out=out2))
+    print(f"{name:7s} 3 axes W=200 stride=100 MLP rows: {us:8.1f} us  ({out2.shape[0] / us * 1e-3:.2f} G windows/s)")
 mod.window_set_legacy(0)
 torch.cuda.synchronize()
 print("ok")
