@@ -911,7 +911,7 @@ int launch_axes(const float* stream, int64_t n_samples, int window, int stride, 
     // per window, the fewer cross-lane reductions per sample (~a third of the VALU at 32 lanes)
     // (8-lane groups only for overlapping windows: their span is shared, so the LDS per window — which
     // bounds the waves per CU — stays small; measured: W = 200 stride 100 69 vs 77 us, stride 200 54
-    // vs 47 us with 8- vs 16-lane groups)
+    // vs 47 us with 8- vs 16-lane groups; round 6 with fixed-length runs, stride 100: 64 vs 77.5 us)
     int lpw = 0, C = 0;
     for (int l = stride < window ? 8 : 16; l <= 64 && !lpw; l *= 2)
       for (int c = 5; c <= RCMAX_LONG; c += 2)
@@ -941,6 +941,8 @@ int launch_axes(const float* stream, int64_t n_samples, int window, int stride, 
       };
       // waves per block: a multiple of T3, at most 4; the most whose span fits 48 KB (>= 3 blocks per CU)
       int m = 0;
+      // (measured on the stride-100 shape: 2- and 1-wave blocks 70 / 68 us vs 64 us with 4 — the staged span is
+      // shared by fewer windows and more blocks start on a stage)
       for (int mm = 4 / T3; mm >= 1; --mm)
         if (span_bytes(mm * gpw) <= 48 * 1024) { m = mm; break; }
       if (!m && span_bytes(gpw) <= 160 * 1024) m = 1;
