@@ -479,7 +479,9 @@ class DeviceLogregSolver:
     def history(self, b: int, hist_host=None):
         """Objective history of model ``b`` (a list like Spark's ``objectiveHistory``: the objective
         after each iteration, trailing repeats of the final value — iterations after convergence —
-        dropped).  ``hist_host``: this solver's ``hist`` already on the host."""
+        dropped).  ``hist_host``: this solver's ``hist`` already on the host.  (Not cut by the
+        iteration count: the solver writes a row every round, a rejected line-search round included —
+        it repeats the objective — while ``iters`` counts accepted steps only, logreg_qn.hip:866/885.)"""
         h = (self.hist if hist_host is None else hist_host)[: self.hist_rows, b].tolist()
         while len(h) > 1 and h[-1] == h[-2]:
             h.pop()

@@ -2,7 +2,7 @@
 # Config-4 1B-sample full pass: bench record + a rocprofv3 kernel trace of the same run (where the pass's
 # time goes outside the MLP steps).  -> gpurun_out/stream_<tag>
 set -u
-ROOT="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
+ROOT="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/../.." && pwd)}"
 OUT="$ROOT/gpurun_out/stream_${1:-x}"
 mkdir -p "$OUT"
 export TMPDIR=/tmp
