@@ -2,7 +2,7 @@
 # PMC passes over the MLP step (one rocprofv3 --pmc run per counter group of tools/pmc_groups_step.txt,
 # never combined with tracing) + a kernel-trace stats pass; summaries -> gpurun_out/pmc5_<tag>.
 set -u
-ROOT="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
+ROOT="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/../.." && pwd)}"
 OUT="$ROOT/gpurun_out/pmc5_${1:-x}"
 mkdir -p "$OUT"
 export TMPDIR=/tmp
