@@ -852,6 +852,9 @@ __global__ __launch_bounds__(512) void mlp_bwd4_kernel(
 #pragma unroll
       for (int u = 0; u < 4; ++u) acc1[j][u] = f32x4_t{0.f, 0.f, 0.f, 0.f};
     // (a) dact1^T = W1^T[u] . dact2^T over row blocks ra0, ra0 + 1; relu'(h1); dact1 -> LDS
+    // (the same 32 x 32 block as 16 v_mfma_f32_32x32x16 per tile — A fragments gathered from w1q, one 1 KB
+    // dact2 read per k step — measured slower on one box: backward 30.3 vs 28.0 us, step 0.0551 vs
+    // 0.0525 ms with one accumulator chain, 31.5 vs 28.5 us with two; profiles/r6/mlp_a32_ab.txt)
     // Software-pipelined: the dact2 fragments of k chunk kc + 3 are read while the MFMAs of chunk kc
     // run (pinned by scheduling groups: 2 LDS reads, then 4 MFMAs, per chunk), and the relu'(h1)
     // words are read first; written plainly, each chunk's reads were issued right before their MFMAs
