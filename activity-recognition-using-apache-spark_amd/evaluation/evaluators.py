@@ -26,10 +26,11 @@ class Evaluator:
     def isLargerBetter(self) -> bool:
         return True
 
-    def evaluate_batched(self, label, pred, mask, num_classes: int, raw=None) -> np.ndarray:
+    def evaluate_batched(self, label, pred, mask, num_classes: int, raw=None, host: bool = True):
         """This evaluator's metric for B models at once (``pred``/``mask`` [B, N]); the
-        CrossValidator scores all (param map, fold) models with one call."""
-        return M.batched_metrics(self._metric(None), label, pred, mask, num_classes, raw)
+        CrossValidator scores all (param map, fold) models with one call.  ``host=False`` may return
+        a device tensor (regression metrics: no host read inside)."""
+        return M.batched_metrics(self._metric(None), label, pred, mask, num_classes, raw, host=host)
 
     def _metric(self, params):
         if params:

@@ -108,13 +108,15 @@ def regression_metrics(label, pred) -> Dict[str, float]:
 
 
 def batched_metrics(metric: str, label: torch.Tensor, pred: torch.Tensor, mask: torch.Tensor, num_classes: int,
-                    raw: torch.Tensor = None) -> np.ndarray:
+                    raw: torch.Tensor = None, host: bool = True):
     """One metric for B models at once: ``pred`` / ``mask`` are ``[B, N]`` (mask = the rows each
     model is scored on, e.g. its CrossValidator validation fold); returns ``[B]`` with the same
     definitions as the single-model functions above.  On the GPU multiclass metrics come from ONE
     batched confusion-matrix launch (metrics.hip) and binary metrics from ONE segmented sort + ONE
     batched roc.hip launch; regression metrics from masked moments; one host read.  On the CPU the
-    same definitions in torch (one-hot einsum, one sort per model for the binary areas)."""
+    same definitions in torch (one-hot einsum, one sort per model for the binary areas).
+    ``host=False``: the regression metrics stay a device tensor (no host read here; the caller reads
+    it after its own sync) — the other metrics are returned as on the host."""
     B, N = pred.shape
     y = label.to(pred.device).long().view(1, N)
     w = mask.to(torch.float64)
@@ -137,15 +139,18 @@ def batched_metrics(metric: str, label: torch.Tensor, pred: torch.Tensor, mask: 
         # only the requested metric's terms (each is a few [B, N] launches; the CrossValidator asks one)
         yd = y.double().expand(B, N)
         n = w.sum(1).clamp_min(1e-300)
+        def out_(t):
+            return t.cpu().numpy() if host else t
+
         if metric == "mae":
-            return ((w * (pred.double() - yd).abs()).sum(1) / n).cpu().numpy()
+            return out_((w * (pred.double() - yd).abs()).sum(1) / n)
 
         def var_y():
             my = (w * yd).sum(1) / n
             return (w * yd * yd).sum(1) / n - my * my
 
         if metric == "var":
-            return var_y().cpu().numpy()
+            return out_(var_y())
         e = pred.double() - yd
         se = (w * e * e).sum(1)
         if metric == "mse":
@@ -155,7 +160,7 @@ def batched_metrics(metric: str, label: torch.Tensor, pred: torch.Tensor, mask: 
         else:  # r2
             ss_tot = var_y() * n
             out = torch.where(ss_tot > 0, 1.0 - se / ss_tot.clamp_min(1e-300), torch.full_like(se, float("nan")))
-        return out.cpu().numpy()
+        return out_(out)
     K = num_classes
     # the batched kernel counts rows (0/1 masks: CrossValidator folds); fractional row weights take
     # the weighted einsum below, as on the CPU

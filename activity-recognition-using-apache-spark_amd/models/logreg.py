@@ -220,11 +220,25 @@ class LogisticRegression(Estimator, ClassifierParams):
         if all(s.row_weight is None for s in specs) and native:
             rw = None                                                               # every row weight 1
         else:
-            rw = torch.stack([torch.ones(N, device=dev) if s.row_weight is None else s.row_weight.to(dev).float()
-                              for s in specs])                                        # [B, N]
+            ones = None  # one fill for every unweighted spec (a CrossValidator batch has one per param map)
+
+            def row_w(s):
+                nonlocal ones
+                if s.row_weight is not None:
+                    return s.row_weight.to(dev).float()
+                if ones is None:
+                    ones = torch.ones(N, device=dev)
+                return ones
+
+            parts = [row_w(s) for s in specs]
+            # the cached design: this fit's row weights stacked straight into its buffer (one launch)
+            if reuse is not None and reuse.design.rw is not None and tuple(reuse.design.rw.shape) == (B, N):
+                rw = torch.stack(parts, out=reuse.design.rw)
+            else:
+                rw = torch.stack(parts)                                               # [B, N]
         if reuse is not None:  # the cached design: this fit's row weights into its buffer
             design = reuse.design
-            if rw is not None:
+            if rw is not None and (design.rw is None or rw.data_ptr() != design.rw.data_ptr()):
                 design.rw.copy_(rw)
         else:
             design = LogregDesign(hm, y, rw, Kp, native=native)
@@ -293,8 +307,14 @@ class LogisticRegression(Estimator, ClassifierParams):
         return design, binomial, Kp, inv_std, inv_wsum, pmask, l2v, l1v, x0 * pmask
 
     def fit_many(self, X, y: torch.Tensor, specs: Sequence[FitSpec], num_classes: Optional[int] = None,
-                 allreduce=None) -> List[LogisticRegressionModel]:
+                 allreduce=None, deferred: bool = False):
         """Train ``len(specs)`` models in one batched device optimization.
+
+        ``deferred`` (device solver, no checkpoint): return ``(models, finalize)`` right after the
+        solve is enqueued — the models' coefficients are device views already, their summaries
+        (objective, iterations, history: host values) are filled by ``finalize()``, the one host
+        sync.  A caller can enqueue work on the coefficients (the CrossValidator's fold scoring)
+        before that sync, and the model objects are built while the GPU is still solving.
 
         ``X`` is a dense ``[N, F]`` tensor or a :class:`HybridMatrix` (one-hot indices + dense
         columns).  Data parallel: every rank passes its own row shard and ``allreduce`` (an
@@ -329,7 +349,8 @@ class LogisticRegression(Estimator, ClassifierParams):
             ckpt = Checkpointer(os.path.join(self.checkpointDir, f"lr-{key}"), rank=ctx.rank if ctx else 0)
             last = ckpt.latest(fingerprint=fp)
             if last is not None:
-                return self._models_from_state(last[0], last[1], len(specs), dev)
+                resumed = self._models_from_state(last[0], last[1], len(specs), dev)
+                return (resumed, lambda: resumed) if deferred else resumed
         wolfe = getattr(self, "lineSearch", "armijo") == "wolfe"
         T = 1 if wolfe else max(1, int(self.lineSearchTrials))
         # repeated single-device fits on one resident design reuse the solver (ops/logreg.py)
@@ -358,7 +379,7 @@ class LogisticRegression(Estimator, ClassifierParams):
                 icpt_all = icpt_all - icpt_all.mean(dim=1, keepdim=True)
             return xs, coef_all, icpt_all
 
-        coefs_pre = None
+        coefs_pre = pending = None
         if wolfe:
             if design.native:  # the evaluation kernels at each round's trial points (+ the DP all-reduce)
                 solver = DeviceLogregSolver(design, B, 1, 10, inv_std, pmask, inv_wsum, l2v, l1v, self.maxIter,
@@ -390,18 +411,24 @@ class LogisticRegression(Estimator, ClassifierParams):
                 if ckey is not None:
                     solver_cache_put(ckey, SolverCacheEntry(hm, y, design, solver,
                                                             (inv_std, inv_wsum, pmask, l2v, l1v, x0)))
-            xs, fobj, iters = solver.solve(x0, poll=poll)
+            xs, fobj_d, iters_d = solver.solve(x0, poll=poll)
             n_evals = solver.n_evals
-            # the coefficient post-processing enqueued BEFORE the host transfer below (its sync): these
+            # the coefficient post-processing enqueued BEFORE the host transfer (its sync): these
             # small kernels then run right behind the solve instead of one by one after it, with the GPU
             # idle between Python launches (LR fit kernel trace, profiles/r5/lr_grad_blocks.md)
             coefs_pre = finish_coefs(xs)
-            # objective history, objectives and iteration counts to the host in ONE transfer
-            packed = torch.cat([solver.hist.reshape(-1), fobj.double(), iters.double()]).cpu()
-            nh = solver.hist.numel()
-            hist_h = packed[:nh].view(solver.hist.shape)
-            fobj, iters = packed[nh:nh + B], packed[nh + B:].to(torch.int64)
-            history = [solver.history(bi, hist_h) for bi in range(B)]
+            # the cat is enqueued now; its host copy (the sync) waits until the models are built
+            packed_d = torch.cat([solver.hist.reshape(-1), fobj_d.double(), iters_d.double()])
+
+            def host_results():
+                # objective history, objectives and iteration counts to the host in ONE transfer
+                packed = packed_d.cpu()
+                nh = solver.hist.numel()
+                hist_h = packed[:nh].view(solver.hist.shape)
+                fo, it = packed[nh:nh + B], packed[nh + B:].to(torch.int64)
+                return fo, it, solver.histories(hist_h)
+
+            pending = host_results
         else:
             def evaluate(xt):
                 loss, G = design.eval_torch(xt.view(-1, Kp, F + 1), T if xt.shape[0] != B else 1, inv_std, pmask,
@@ -418,27 +445,32 @@ class LogisticRegression(Estimator, ClassifierParams):
             xs, fobj, iters, n_evals = res.x, res.f, res.iterations, res.n_evals
             history = res.history_per_model  # each model's own objective per iteration
         xs, coef_all, icpt_all = coefs_pre if coefs_pre is not None else finish_coefs(xs)
-        models = []
-        fobj_h = fobj.double().cpu()
-        iters_h = iters.cpu()
-        # per-model views in one unbind each and the scalars as Python lists: per-model tensor indexing
-        # was ~20 us of host time per model (a 54-model CrossValidator batch)
+        # per-model views in one unbind each: per-model tensor indexing was ~20 us of host time per
+        # model (a 54-model CrossValidator batch).  Built before the host values are read, so on the
+        # device solver this Python runs while the GPU is still solving
         coefs, icpts = coef_all.detach().unbind(0), icpt_all.detach().unbind(0)
-        fobj_l, iters_l = fobj_h.tolist(), iters_h.tolist()
-        for bi in range(B):
-            summary = {"objective": float(fobj_l[bi]), "iterations": int(iters_l[bi]), "n_evals": n_evals,
-                       "objectiveHistory": history[bi], "lineSearch": "wolfe" if wolfe else "armijo"}
-            if rounds is not None:
-                summary["lineSearchRounds"] = rounds  # batched evaluation rounds per iteration
-            models.append(self._apply_thresholds(LogisticRegressionModel(coefs[bi], icpts[bi], binomial, device=dev,
-                                                                         summary=summary)))
-        if ckpt is not None:
-            st = {}
+        models = [self._apply_thresholds(LogisticRegressionModel(coefs[bi], icpts[bi], binomial, device=dev))
+                  for bi in range(B)]
+
+        def finalize():
+            fo, it, hist = pending() if pending is not None else (fobj, iters, history)
+            fobj_l, iters_l = fo.double().cpu().tolist(), it.cpu().tolist()
             for bi, mo in enumerate(models):
-                st[f"coef{bi}"], st[f"icpt{bi}"] = mo.coefficientMatrix, mo.interceptVector
-            ckpt.save(1, st, {"binomial": binomial, "summaries": [dict(mo.summary) for mo in models]},
-                      fingerprint=fp)
-        return models
+                mo.summary = {"objective": float(fobj_l[bi]), "iterations": int(iters_l[bi]), "n_evals": n_evals,
+                              "objectiveHistory": hist[bi], "lineSearch": "wolfe" if wolfe else "armijo"}
+                if rounds is not None:
+                    mo.summary["lineSearchRounds"] = rounds  # batched evaluation rounds per iteration
+            if ckpt is not None:
+                st = {}
+                for bi, mo in enumerate(models):
+                    st[f"coef{bi}"], st[f"icpt{bi}"] = mo.coefficientMatrix, mo.interceptVector
+                ckpt.save(1, st, {"binomial": binomial, "summaries": [dict(mo.summary) for mo in models]},
+                          fingerprint=fp)
+            return models
+
+        if deferred:
+            return models, finalize
+        return finalize()
 
     def _models_from_state(self, st, meta, B: int, dev) -> List[LogisticRegressionModel]:
         out = []

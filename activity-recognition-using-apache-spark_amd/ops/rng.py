@@ -154,16 +154,22 @@ def feature_subsets(seed: int, trees, nodes, n_features: int, m: int) -> np.ndar
     return chosen.astype(np.int32)
 
 
+_THR_CACHE = {}
+
+
 def device_buckets(seed: int, stream: int, row0: int, n: int, weights, device):
     """``assign_buckets`` on the GPU (HIP kernel ``har_philox_buckets``); int32 [n]."""
     import torch
 
     from . import _native
 
-    thr = bucket_thresholds(weights)[:-1].astype(np.uint32)
-    thr_t = torch.from_numpy(thr.view(np.int32)).to(device)
+    key = (tuple(float(w) for w in weights), str(torch.device(device)))
+    thr_t = _THR_CACHE.get(key)
+    if thr_t is None:  # (a pageable 16-byte upload per call waited on the stream: cached per weights)
+        thr = bucket_thresholds(weights)[:-1].astype(np.uint32)
+        thr_t = _THR_CACHE[key] = torch.from_numpy(thr.view(np.int32)).to(device)
     out = torch.empty(n, dtype=torch.int32, device=device)
-    _native.kernels().philox_buckets(seed, stream, row0, n, thr_t.data_ptr(), len(thr), out.data_ptr(),
+    _native.kernels().philox_buckets(seed, stream, row0, n, thr_t.data_ptr(), thr_t.numel(), out.data_ptr(),
                                      _native.stream_ptr())
     return out
 

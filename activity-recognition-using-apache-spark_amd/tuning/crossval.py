@@ -168,13 +168,18 @@ class CrossValidator(Estimator):
             if dp_context() is not None:
                 specs = [FitSpec(None if s.row_weight is None else s.row_weight[lo:hi], s.regParam, s.elasticNetParam)
                          for s in specs]
-            models_all = base.fit_many(hm.rows(lo, hi), y[lo:hi], specs, K, allreduce=dp_allreduce())
+            # deferred: the fold scoring below is enqueued behind the batched solve before the one host
+            # sync (finalize), and the model objects are built while the GPU solves
+            models_all, finalize = base.fit_many(hm.rows(lo, hi), y[lo:hi], specs, K, allreduce=dp_allreduce(),
+                                                 deferred=True)
             models, refits = models_all[:n_cv], models_all[n_cv:]
             # every (map, fold) model scored on its validation fold in ONE batched pass
             raw = _lr_margins(models, hm)                                          # [n, N, K]
             pred = _batched_predictions(models, raw)
             mask = in_fold[torch.arange(len(index), device=dev) % k]  # fold of model i = i % k (no upload)
-            vals = ev.evaluate_batched(y, pred, mask, K, raw)
+            vals = ev.evaluate_batched(y, pred, mask, K, raw, host=False)
+            finalize()
+            vals = vals.cpu().numpy() if torch.is_tensor(vals) else vals
             for (mi, f), v in zip(index, vals):
                 metrics[mi, f] = v
         elif hasattr(est, "fit_folds") and not getattr(est, "weightCol", None):
