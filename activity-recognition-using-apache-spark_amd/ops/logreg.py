@@ -208,8 +208,13 @@ class LogregDesign:
         dev = self.device
         if self.native:
             mod, st = _native.kernels(), _native.stream_ptr()
-            nt = mod.logreg_summary_tiles(N)
-            part = torch.empty(S_, max(1, nt), 2 * self.Fd + K + 1, dtype=torch.float64, device=dev)
+            sb = getattr(self, "_summary_bufs", None)
+            if sb is None:  # (a design reused by the solver cache keeps its summary buffers: no allocations)
+                nt = mod.logreg_summary_tiles(N)
+                sb = self._summary_bufs = (nt, torch.empty(S_, max(1, nt), 2 * self.Fd + K + 1, dtype=torch.float64,
+                                                           device=dev))
+            nt, part = sb
+            # (a fresh output per call: callers keep it, e.g. expanded into the prepare kernel's input)
             out = torch.empty(S_, 1 + 2 * F + K, dtype=torch.float64, device=dev)
             cs = self.col_slice()
             srow = self.col_blocks()[2]
