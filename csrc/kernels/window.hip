@@ -779,7 +779,9 @@ __device__ __forceinline__ void reg_window_batch(const float* span, int64_t w0, 
 // compare + branch cost ~6 instructions per step and sample pass, and only the registers the runs use.
 // (A persistent variant — the next batch's span copied HBM -> LDS by global_load_lds while the current one
 // is computed from registers — measured slower on the stride-100 shape: 83 us with 4-wave and 103 us with
-// 1-wave blocks vs 63 us one-shot at 131k windows, and 1.3x slower at 1.3M; one-shot blocks it is.)
+// 1-wave blocks vs 63 us one-shot at 131k windows, and 1.3x slower at 1.3M; and a register-prefetch
+// persistent variant — the next span's 10 float4 per thread loaded right after the runs are read, stored to
+// LDS after pass 2, 168 VGPRs at 3 waves per SIMD, no spills — 73 vs 62 us: one-shot blocks it is.)
 template <int A, int LPW, bool MLP, int RCMAX, bool P32 = false, int WPE = 1, bool FIXC = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void window_features_reg_kernel(const float* __restrict__ stream, int W,
                                                                   int stride, int64_t n_windows, float ms_per_sample,
