@@ -459,3 +459,18 @@ def test_mlp_crossvalidator_device_fold_rows_match_row_subsets():
                             .transform(t.take_rows(np.nonzero(fold == f)[0]))) for f in range(3)]
         want.append(float(np.mean(vals)))
     np.testing.assert_allclose(cv.avgMetrics, want, rtol=0, atol=1e-6)
+
+
+def test_native_solver_histories_equal_per_model_history():
+    """DeviceLogregSolver.histories (one host conversion for every model) == history(b) per model:
+    trailing repeats of the final value dropped, interior repeats (a rejected line-search round) kept."""
+    from types import SimpleNamespace
+
+    from har.ops.logreg import DeviceLogregSolver
+
+    hist = torch.tensor([[5.0, 4.0, 9.0], [3.0, 4.0, 8.0], [3.0, 2.0, 8.0], [2.0, 2.0, 8.0], [2.0, 2.0, 8.0]],
+                        dtype=torch.float64)
+    ns = SimpleNamespace(hist=hist, hist_rows=4)
+    many = DeviceLogregSolver.histories(ns, hist)
+    assert many == [DeviceLogregSolver.history(ns, b, hist) for b in range(3)]
+    assert many == [[5.0, 3.0, 3.0, 2.0], [4.0, 4.0, 2.0], [9.0, 8.0]]
