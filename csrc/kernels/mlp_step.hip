@@ -431,7 +431,9 @@ __global__ __launch_bounds__(512) void mlp_fwd3_kernel(
       if (k == 4) HAR_STAMP(FW, 12)
       // stage 1 reads the X tile whose loads were issued just before the last barrier: hoisted to the
       // top of the body (as the scheduler likes, to fill the MFMA pipe beside the softmax) it waits out
-      // their whole latency there; here the softmax and stages 2 + 3 cover it
+      // their whole latency there; here the softmax and stages 2 + 3 cover it.  (Moved ahead of stage
+      // 5 so that its X wait no longer also covers stage 5's write-through stores — hipcc's counted
+      // wait cannot count a store — measured 0.5 us slower per forward on one box, gpurun_out/abso_es1.)
       __builtin_amdgcn_sched_barrier(0);
       stage1(k & 1);   // tile k+2 (clamped) into the buffer tile k left
       load_x(k + 3);
