@@ -325,19 +325,21 @@ def test_rccl_forest_node_owner(rccl, cuda, kind):
     assert torch.equal(m.arrs.stats, r.arrs.stats)
 
 
-def test_rccl_bench_graph2_subprocess(cuda, tmp_path):
+@pytest.mark.parametrize("graph", ["2", "-1"])
+def test_rccl_bench_graph2_subprocess(cuda, tmp_path, graph):
     """bench.py in its DP form on the forced RCCL group: segmented graphs around the eager RCCL
-    reduce-scatter / all-gather, one JSON line, the collectives recorded."""
+    reduce-scatter / all-gather (--graph 2), and the driver's default eager step (--graph -1: what the
+    N > 1 scaling runs execute, one rank per GPU), one JSON line, the collectives recorded."""
     env = dict(os.environ, HAR_DIST_FORCE_PG="1", PYTHONUNBUFFERED="1")
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT"):
         env.pop(k, None)
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "5", "--warmup", "2",
-                        "--graph", "2", "--no-wisdm", "--settle-ms", "0"],
+                        "--graph", graph, "--no-wisdm", "--settle-ms", "0"],
                        cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-3000:]
     line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1]
     rec = json.loads(line)
-    assert rec["hip_graph"] == "segmented" and rec["n_gpus"] == 1
+    assert rec["hip_graph"] == ("segmented" if graph == "2" else "off") and rec["n_gpus"] == 1
     cps = rec["collectives_per_step"]
     assert cps["reduce_scatter"] == 1 and cps["all_gather"] == 1 and cps["kernels"] == 5, cps
     ph = rec["phase_ms"]
