@@ -140,6 +140,11 @@ def init_params(layout: FlatLayout, seed: int) -> torch.Tensor:
     return flat
 
 
+# the DP step shards the optimizer (reduce-scatter + all-gather) from this many parameters up, and
+# all-reduces the gradient below it (HAR_MLP_SHARDED_OPT overrides; see MLPEngine.__init__)
+SHARD_MIN_PARAMS = 4 << 20
+
+
 class MLPEngine:
     """Device-resident training state + the fused native step."""
 
@@ -157,12 +162,19 @@ class MLPEngine:
         self.dp = world_size > 1 or bool(force_dp)
         L = self.layout
         dev = self.device
-        # Data parallel, sharded optimizer (ZeRO-1 style, the default for world > 1;
-        # HAR_MLP_SHARDED_OPT=0 keeps the all-reduce step): the flat buffers are padded to world x
+        # Data parallel, sharded optimizer (ZeRO-1 style): the flat buffers are padded to world x
         # chunk (chunk a multiple of 64 elements: 256-byte aligned slices), rank r owns
         # [r chunk, (r + 1) chunk) of P / m / v, the step is reduce-scatter(G) -> Adam on the owned
-        # slice -> all-gather(P) -> bf16 / fragment refresh
-        self.sharded = self.dp and os.environ.get("HAR_MLP_SHARDED_OPT", "1") != "0"
+        # slice -> all-gather(P) -> bf16 / fragment refresh.  Chosen by size (HAR_MLP_SHARDED_OPT=1 / 0
+        # forces it / the all-reduce step): a gradient below SHARD_MIN_PARAMS is a latency-bound message,
+        # where the two collectives cost two latencies and sharding saves nothing worth having — measured
+        # on a 1-rank RCCL group at 43-256-256-6 (86k parameters): all-reduce step 0.068-0.070 ms,
+        # sharded 0.083-0.085 (profiles/r6/dp_step_forced_rccl.txt); above it the messages are
+        # bandwidth-bound (reduce-scatter + all-gather move what one all-reduce does) and Adam's
+        # optimizer-state traffic splits N ways
+        env = os.environ.get("HAR_MLP_SHARDED_OPT")
+        want = (env != "0") if env is not None else L.total >= SHARD_MIN_PARAMS
+        self.sharded = self.dp and want
         if world_size > 1:
             # every rank must take the same step form (reduce-scatter + all-gather vs all-reduce) or the
             # collectives mismatch and the job hangs: agree on it once (MIN and MAX of the flag)
@@ -560,9 +572,10 @@ class MLPEngine:
 
     def collective_stats(self):
         """Collectives of one DP training step and the bytes each rank hands to them: the sharded
-        step (default) is ONE reduce-scatter of the fp32 gradient + ONE all-gather of the fp32
-        parameters (world x chunk elements each, ~0.34 MB for 43-256-256-6: latency-bound on xGMI,
-        so one flat message each, no bucketing); HAR_MLP_SHARDED_OPT=0: ONE all-reduce of G."""
+        step (SHARD_MIN_PARAMS parameters and up, or HAR_MLP_SHARDED_OPT=1) is ONE reduce-scatter of
+        the fp32 gradient + ONE all-gather of the fp32 parameters (world x chunk elements each); the
+        all-reduce step (smaller models, e.g. 43-256-256-6's ~0.34 MB: latency-bound on xGMI, so one
+        flat message, no bucketing) is ONE all-reduce of G."""
         if not self.dp:
             return {"all_reduce": 0, "bytes": 0, "kernels": 3 if getattr(self, "step_ok", False) else None}
         if self.sharded:
@@ -571,8 +584,8 @@ class MLPEngine:
             return {"all_reduce": 0, "reduce_scatter": 1, "all_gather": 1, "bytes": 2 * nb,
                     "reduce_scatter_bytes": nb, "all_gather_bytes": nb, "world": self.world,
                     "kernels": 5 if self.native else 0}
-        return {"all_reduce": 1, "bytes": int(self.G.numel() * 4), "world": self.world,
-                "kernels": 4 if self.native else 0}
+        return {"all_reduce": 1, "reduce_scatter": 0, "all_gather": 0, "bytes": int(self.G.numel() * 4),
+                "world": self.world, "kernels": 4 if self.native else 0}
 
     def allreduce_grads(self):
         if self.dp:

@@ -328,11 +328,15 @@ def test_rccl_forest_node_owner(rccl, cuda, kind):
 @pytest.mark.parametrize("graph", ["2", "-1"])
 def test_rccl_bench_graph2_subprocess(cuda, tmp_path, graph):
     """bench.py in its DP form on the forced RCCL group: segmented graphs around the eager RCCL
-    reduce-scatter / all-gather (--graph 2), and the driver's default eager step (--graph -1: what the
-    N > 1 scaling runs execute, one rank per GPU), one JSON line, the collectives recorded."""
+    reduce-scatter / all-gather of the sharded optimizer (--graph 2, HAR_MLP_SHARDED_OPT=1), and the
+    driver's default eager step (--graph -1: what the N > 1 scaling runs execute, one rank per GPU: at
+    86k parameters one all-reduce, models/mlp.py SHARD_MIN_PARAMS), one JSON line, the collectives
+    recorded."""
     env = dict(os.environ, HAR_DIST_FORCE_PG="1", PYTHONUNBUFFERED="1")
-    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT"):
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT", "HAR_MLP_SHARDED_OPT"):
         env.pop(k, None)
+    if graph == "2":
+        env["HAR_MLP_SHARDED_OPT"] = "1"
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "5", "--warmup", "2",
                         "--graph", graph, "--no-wisdm", "--settle-ms", "0"],
                        cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
@@ -341,7 +345,11 @@ def test_rccl_bench_graph2_subprocess(cuda, tmp_path, graph):
     rec = json.loads(line)
     assert rec["hip_graph"] == ("segmented" if graph == "2" else "off") and rec["n_gpus"] == 1
     cps = rec["collectives_per_step"]
-    assert cps["reduce_scatter"] == 1 and cps["all_gather"] == 1 and cps["kernels"] == 5, cps
     ph = rec["phase_ms"]
-    assert ph["allreduce"] is not None and ph["all_gather"] is not None
+    if graph == "2":
+        assert cps["reduce_scatter"] == 1 and cps["all_gather"] == 1 and cps["kernels"] == 5, cps
+        assert ph["allreduce"] is not None and ph["all_gather"] is not None
+    else:
+        assert cps["all_reduce"] == 1 and cps["reduce_scatter"] == 0 and cps["kernels"] == 4, cps
+        assert ph["allreduce"] is not None and ph["all_gather"] is None
     assert rec["dist_backend"] == "nccl"
