@@ -148,8 +148,8 @@ class CrossValidator(Estimator):
             in_fold = fold_t[None, :] == torch.arange(k, device=dev)[:, None]  # [k, N]: ONE launch, not k
             train_w = (~in_fold).float()
             specs, index = [], []
-            for mi, pm in enumerate(maps):
-                sub = est.copy(pm)
+            subs = [est.copy(pm) for pm in maps]  # (one copy per map: the fold specs and the refits share it)
+            for mi, sub in enumerate(subs):
                 for f in range(k):
                     specs.append(FitSpec(train_w[f], sub.regParam, sub.elasticNetParam))
                     index.append((mi, f))
@@ -159,11 +159,10 @@ class CrossValidator(Estimator):
             n_cv = len(specs)
             batch_refit = not est.weightCol and all(set(pm) <= {"regParam", "elasticNetParam"} for pm in maps)
             if batch_refit:
-                for pm in maps:
-                    sub = est.copy(pm)
+                for sub in subs:
                     specs.append(FitSpec(None, sub.regParam, sub.elasticNetParam))
             # maxIter / tol / family etc. may differ per map only through regParam/elasticNetParam
-            base = est.copy(maps[0]) if maps else est
+            base = subs[0] if maps else est
             lo, hi = dp_rows(hm.n_rows)  # data parallel: every fit on this rank's row shard
             if dp_context() is not None:
                 specs = [FitSpec(None if s.row_weight is None else s.row_weight[lo:hi], s.regParam, s.elasticNetParam)
