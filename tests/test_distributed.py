@@ -363,6 +363,19 @@ def _forced_worker(rank, port, out_dir):
         res[f"equal_{sharded}"] = bool(torch.equal(a.P, b.P) and torch.equal(a.m, b.m) and torch.equal(a.v, b.v))
         res[f"coll_{sharded}"] = n[0]
         res[f"dp_{sharded}"] = (b.dp, b.sharded)
+    # unset: the form follows the parameter count (models/mlp.py SHARD_MIN_PARAMS)
+    import har.models.mlp as mlp_mod
+
+    os.environ.pop("HAR_MLP_SHARDED_OPT", None)
+    small = MLPEngine([12, 32, 4], 128, "cpu", lr=1e-2, seed=1, process_group=ctx.group, world_size=1, force_dp=True)
+    old_min = mlp_mod.SHARD_MIN_PARAMS
+    mlp_mod.SHARD_MIN_PARAMS = 16
+    try:
+        big = MLPEngine([12, 32, 4], 128, "cpu", lr=1e-2, seed=1, process_group=ctx.group, world_size=1,
+                        force_dp=True)
+    finally:
+        mlp_mod.SHARD_MIN_PARAMS = old_min
+    res["auto"] = (small.sharded, big.sharded)
     torch.save(res, os.path.join(out_dir, "forced.pt"))
     hd.shutdown(ctx)
 
@@ -379,3 +392,4 @@ def test_forced_one_rank_group_runs_the_dp_paths():
     assert r["equal_1"] and r["equal_0"], r
     assert r["coll_1"] == 3 and r["coll_0"] == 3, r  # one gradient collective per step
     assert tuple(r["dp_1"]) == (True, True) and tuple(r["dp_0"]) == (True, False)
+    assert tuple(r["auto"]) == (False, True)  # small gradient: one all-reduce; from SHARD_MIN_PARAMS: sharded
