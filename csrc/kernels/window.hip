@@ -267,9 +267,12 @@ __device__ __forceinline__ void window_groups(const float* img0, int64_t w0, int
 #pragma unroll
   for (int c = 0; c < 3; ++c) {
     const int ax = 3 * g + c;
-    const float ad = rsum<LPW>(a.ad[c]) * invW;
+    // a constant axis (max == min) has exactly zero spread: its fp32 mean need not equal the sample, so
+    // the deviation sums need not cancel (a clipped, saturated sensor gave correlations of +-1 for 0)
+    const bool flat = !(mx[c] > mn[c]);
+    const float ad = flat ? 0.f : rsum<LPW>(a.ad[c]) * invW;
     const float var = rsum<LPW>(a.v2[c]) * invW;
-    sd[c] = __builtin_amdgcn_sqrtf(var);
+    sd[c] = flat ? 0.f : __builtin_amdgcn_sqrtf(var);
     const int npk = (int)rsumu<LPW>((uint32_t)a.npk[c]);
     const int first = rmini<LPW>(a.first[c]), last = rmaxi<LPW>(a.last[c]);
     // bins: lane `sub` writes bin `sub` (and lanes 0, 1 of 8-lane groups bins 8, 9); the word is
@@ -685,6 +688,17 @@ __device__ __forceinline__ void reg_window_batch(const float* span, int64_t w0, 
       if constexpr (FIXC) asm volatile("" : "+v"(res));
     }
 
+  // a constant axis (max == min: its bin scale sc is 0) has exactly zero spread, but its fp32 mean need
+  // not equal the sample, so the deviation sums need not cancel (a clipped, saturated sensor gave
+  // correlations of +-1 for 0): its per-lane deviation sums are zeroed before the reductions
+  {
+    const bool f0 = sc[0] == 0.f, f1 = sc[1] == 0.f, f2 = sc[2] == 0.f;
+    ad[0] = f0 ? 0.f : ad[0]; v2[0] = f0 ? 0.f : v2[0];
+    ad[1] = f1 ? 0.f : ad[1]; v2[1] = f1 ? 0.f : v2[1];
+    ad[2] = f2 ? 0.f : ad[2]; v2[2] = f2 ? 0.f : v2[2];
+    cxy = (f0 || f1) ? 0.f : cxy; cxz = (f0 || f2) ? 0.f : cxz; cyz = (f1 || f2) ? 0.f : cyz;
+  }
+
   // peak positions: 0 < t < W - 1 (t = tb + k), i.e. bits j in [C - 1 - kh, C - 1 - kl]
   const int kl = sub == 0 ? 1 : 0, kh = min(C - 1, W - 2 - tb);
   const uint32_t pmask =
@@ -716,7 +730,7 @@ __device__ __forceinline__ void reg_window_batch(const float* span, int64_t w0, 
 #pragma unroll
   for (int c = 0; c < 3; ++c) {
     const int ax = 3 * g + c;
-    dl[c] = xl[c] - mean[c];
+    dl[c] = sc[c] == 0.f ? 0.f : xl[c] - mean[c];  // (a constant axis: no deviation, see above)
     const float adv = (greduce<LPW, float>(ad[c], fsum, sw) - D * fabsf(dl[c])) * invW;
     const float var = fmaxf(greduce<LPW, float>(v2[c], fsum, sw) - D * dl[c] * dl[c], 0.f) * invW;
     sd[c] = __builtin_amdgcn_sqrtf(var);

@@ -127,3 +127,34 @@ def test_window_kernel_large_counts_match_torch(cuda, stride, nwin):
     torch.testing.assert_close(mo[:, :F].float(), want.float(), rtol=2 ** -7, atol=1e-6)
     assert int((mo[:, :F] != want).sum()) <= max(4, mo.numel() // 100000)
 
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("stride", [200, 100])
+def test_window_kernel_saturated_and_constant_runs(cuda, stride):
+    """Clipped sensor data: runs where every sample of a lane's 25 (stride 100) or 13 (stride 200) sits
+    at the window maximum — the unclamped bin-10 slot of the 5-bit packed histogram (window.hip SB = 5)
+    full, then folded into bin 9 — and constant windows (range 0: every sample in bin 0, std 0,
+    correlations 0), against the PyTorch oracle."""
+    from har.features.window import window_features
+
+    W = 200
+    spec = StreamSpec(axes=3, window=W, seed=21)
+    n_seg = 40
+    s, _ = generate_stream(n_seg, spec, cuda)
+    s = s.clone()
+    hi = float(s.max()) * 0.25
+    s = s.clamp(max=hi)                      # long runs at the clip value = the window max
+    s[5 * W:7 * W] = 1.5                     # two constant windows (stride 200), more overlapping ones
+    s[11 * W:11 * W + 60, 1] = 9.0           # a spike at the start of a window: max at t < 60 only
+    nwin = (s.shape[0] - W) // stride + 1
+    s = s[: (nwin - 1) * stride + W]
+    ref = window_features_torch(s, W, stride, 50.0)
+    out = window_features(s, W, stride, 50.0)
+    assert out.shape == ref.shape
+    nb = 30
+    assert float((out[:, :nb] - ref[:, :nb]).abs().max()) <= 1.0 / W + 1e-6
+    # every window's 10 bins of an axis sum to 1 (nothing lost in the packed slots)
+    sums = out[:, :nb].reshape(-1, 3, 10).sum(-1)
+    torch.testing.assert_close(sums, torch.ones_like(sums), rtol=0, atol=1e-5)
+    torch.testing.assert_close(out[:, nb:], ref[:, nb:], rtol=2e-4, atol=2e-4, equal_nan=True)
