@@ -158,3 +158,22 @@ def test_window_kernel_saturated_and_constant_runs(cuda, stride):
     sums = out[:, :nb].reshape(-1, 3, 10).sum(-1)
     torch.testing.assert_close(sums, torch.ones_like(sums), rtol=0, atol=1e-5)
     torch.testing.assert_close(out[:, nb:], ref[:, nb:], rtol=2e-4, atol=2e-4, equal_nan=True)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("axes,window,stride", [(3, 3, 1), (3, 5, 2), (3, 8, 8), (6, 16, 3), (3, 17, 17), (9, 33, 11),
+                                               (3, 64, 64), (3, 129, 64)])
+def test_window_kernel_short_windows_match_torch(cuda, axes, window, stride):
+    """Short windows: runs much longer than the window (up to LPW x 5 run slots for 3 samples), so most
+    lanes hold only copies of sample W - 1 whose contributions the kernel subtracts (D = LPW C - W), and
+    the peak masks cover almost every bit — against the PyTorch oracle."""
+    from har.features.window import window_features
+
+    spec = StreamSpec(axes=axes, window=max(window, 16), seed=window + axes)
+    s, _ = generate_stream(24, spec)
+    ref = window_features_torch(s, window, stride, 50.0)
+    out = window_features(s.to(cuda), window, stride, 50.0).cpu()
+    assert out.shape == ref.shape and out.shape[0] > 0
+    nb = 10 * axes
+    assert (out[:, :nb] - ref[:, :nb]).abs().max() <= 1.0 / window + 1e-6
+    torch.testing.assert_close(out[:, nb:], ref[:, nb:], rtol=2e-4, atol=2e-4, equal_nan=True)
