@@ -85,8 +85,35 @@ def window_features_torch(stream: torch.Tensor, window: int, stride: int, hz: fl
     return out.float()
 
 
+_WIDE_WARNED = set()
+
+
+def _wide_windows(stream: torch.Tensor, window: int, stride: int, hz: float) -> torch.Tensor:
+    """Windows the HIP kernel cannot stage (contract code -5: one block's window images — 4 windows of
+    ``window x axes`` floats per axis triad — exceed the 160 KB LDS, e.g. 9 axes x 2,600 samples): the
+    float64 torch definition on the stream's device, in chunks of ~1 GB of temporaries."""
+    S, A = stream.shape
+    nw = window_count(S, window, stride)
+    key = (A, window)
+    if key not in _WIDE_WARNED:
+        _WIDE_WARNED.add(key)
+        import warnings
+
+        warnings.warn(f"window_features: {A}-axis windows of {window} samples exceed the kernel's LDS images; "
+                      f"computed with the torch definition on {stream.device}")
+    per = max(1, (1 << 30) // (A * window * 8 * 6))
+    outs = [window_features_torch(stream[w0 * stride: (w0 + min(per, nw - w0) - 1) * stride + window],
+                                  window, stride, hz) for w0 in range(0, nw, per)]
+    return torch.cat(outs) if outs else torch.empty(0, n_features(A), device=stream.device)
+
+
+def _is_wide(err: RuntimeError) -> bool:
+    return "contract violation code -5" in str(err)
+
+
 def window_features(stream: torch.Tensor, window: int, stride: int, hz: float) -> torch.Tensor:
-    """[S, A] raw samples -> [n_windows, n_features(A)] features (GPU kernel on device tensors)."""
+    """[S, A] raw samples -> [n_windows, n_features(A)] features (GPU kernel on device tensors; windows too
+    wide for its LDS images: the torch definition on the device, with a warning)."""
     S, A = stream.shape
     if A % 3 or A > 9:
         raise ValueError("axes must be 3, 6 or 9")
@@ -97,8 +124,13 @@ def window_features(stream: torch.Tensor, window: int, stride: int, hz: float) -
     out = torch.empty(nw, F, dtype=torch.float32, device=stream.device)
     if nw:
         s = stream.contiguous().float()
-        _native.kernels().window_features(s.data_ptr(), S, A, window, stride, nw, float(hz), NBINS, out.data_ptr(),
-                                          F, _native.stream_ptr())
+        try:
+            _native.kernels().window_features(s.data_ptr(), S, A, window, stride, nw, float(hz), NBINS,
+                                              out.data_ptr(), F, _native.stream_ptr())
+        except RuntimeError as e:
+            if not _is_wide(e):
+                raise
+            return _wide_windows(s, window, stride, hz)
     return out
 
 
@@ -123,9 +155,16 @@ def window_features_mlp(stream: torch.Tensor, window: int, stride: int, hz: floa
         s = stream.contiguous().float()
         m = mean.float().contiguous()
         r = inv_std.float().contiguous()
-        _native.kernels().window_features_mlp(s.data_ptr(), S, A, window, stride, nw, float(hz), m.data_ptr(),
-                                              r.data_ptr(), float(nan_value), out.data_ptr(), in_pad,
-                                              _native.stream_ptr())
+        try:
+            _native.kernels().window_features_mlp(s.data_ptr(), S, A, window, stride, nw, float(hz), m.data_ptr(),
+                                                  r.data_ptr(), float(nan_value), out.data_ptr(), in_pad,
+                                                  _native.stream_ptr())
+        except RuntimeError as e:
+            if not _is_wide(e):
+                raise
+            X = torch.nan_to_num(_wide_windows(s, window, stride, hz), nan=nan_value)
+            out.zero_()
+            out[:, :F] = ((X - m) * r).to(torch.bfloat16)
     return out
 
 

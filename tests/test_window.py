@@ -177,3 +177,35 @@ def test_window_kernel_short_windows_match_torch(cuda, axes, window, stride):
     nb = 10 * axes
     assert (out[:, :nb] - ref[:, :nb]).abs().max() <= 1.0 / window + 1e-6
     torch.testing.assert_close(out[:, nb:], ref[:, nb:], rtol=2e-4, atol=2e-4, equal_nan=True)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("axes,window,stride", [(3, 1984, 1984), (3, 1985, 1000), (9, 2600, 1300), (6, 4001, 4001)])
+def test_window_kernel_long_windows_match_torch(cuda, axes, window, stride):
+    """Long windows: 64-lane groups of 31-sample runs up to 1,984 samples, then the LDS-streaming kernel;
+    windows whose images exceed the LDS (9 x 2,600, 6 x 4,001: kernel contract code -5) fall back to the
+    torch definition on the device with a warning — all against the PyTorch oracle, fp32 features and
+    the MLP-input rows."""
+    import warnings
+
+    from har.features.window import window_features, window_features_mlp
+
+    spec = StreamSpec(axes=axes, window=window, seed=window % 97)
+    s, _ = generate_stream(6, spec)
+    ref = window_features_torch(s, window, stride, 50.0)
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        out = window_features(s.to(cuda), window, stride, 50.0).cpu()
+    assert out.shape == ref.shape and out.shape[0] > 0
+    nb = 10 * axes
+    assert (out[:, :nb] - ref[:, :nb]).abs().max() <= 1.0 / window + 1e-6
+    torch.testing.assert_close(out[:, nb:], ref[:, nb:], rtol=2e-4, atol=2e-4, equal_nan=True)
+    F = n_features(axes)
+    mean = torch.zeros(F, device=cuda)
+    inv_std = torch.ones(F, device=cuda)
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        mo = window_features_mlp(s.to(cuda), window, stride, 50.0, mean, inv_std, (F + 31) // 32 * 32)
+    assert mo.shape == (ref.shape[0], (F + 31) // 32 * 32) and torch.count_nonzero(mo[:, F:]) == 0
+    want = torch.nan_to_num(out, nan=-1.0).to(torch.bfloat16)
+    torch.testing.assert_close(mo[:, :F].float().cpu(), want.float(), rtol=2 ** -7, atol=1e-3)
