@@ -551,7 +551,9 @@ __device__ __forceinline__ void flag_step(uint32_t& R, uint32_t& PT, float x, fl
 }
 
 // bin of a sample: (x - lo) * (10 / range) in fp32, the legacy kernel's arithmetic (x >= lo, so the
-// conversion never sees a negative), clamped to bin 9
+// conversion never sees a negative), clamped to bin 9.  (The one-fma form x sc + (-lo sc), one VALU less
+// per sample and axis, moved boundary samples of quantized sensor data — WISDM's 2-decimal readings sit
+// exactly on bin edges — off the float64 definition's bins: tests/test_raw.py; rejected)
 __device__ __forceinline__ uint32_t bin_raw(float x, float sc, float lo) { return (uint32_t)((x - lo) * sc); }
 __device__ __forceinline__ uint32_t bin_of(float x, float sc, float lo) {
   const uint32_t b = (uint32_t)((x - lo) * sc);
@@ -591,10 +593,14 @@ __device__ __forceinline__ void reg_window_batch(const float* span, int64_t w0, 
   // Runtime C <= RCMAX: every k-step is guarded by the uniform k < C, which also keeps the
   // scheduler from hoisting all 3*RCMAX loads and their consumers at once (register pressure)
   float x[3][RCMAX];
+  // FIXC: the run read unclamped from one base address (immediate LDS offsets — the clamped form cost a
+  // 24-bit multiply, a min and a 64-bit address multiply-add per sample); run positions past W - 1 read
+  // the span's next samples or its slack (sized by the launcher) and get the copies of sample W - 1 below
+  constexpr bool FLAT = FIXC && !P32;
 #pragma unroll
   for (int k = 0; k < RCMAX; ++k)
     if (k < C) {
-      const float* p = img + pos(min(tb + k, W - 1));
+      const float* p = FLAT ? img + (tb + k) * A : img + pos(min(tb + k, W - 1));
 #pragma unroll
       for (int c = 0; c < 3; ++c) x[c][k] = p[c];
     }
@@ -606,6 +612,16 @@ __device__ __forceinline__ void reg_window_batch(const float* span, int64_t w0, 
     const float* pp = img + (P32 ? pos(max(min(tb, W) - 1, 0)) : (min(tb, W) - 1) * A);
 #pragma unroll
     for (int c = 0; c < 3; ++c) { xl[c] = pl[c]; pv0[c] = pp[c]; }
+  }
+  if constexpr (FLAT) {
+    if (LPW * RCMAX != W) {  // (uniform: runs that overhang the window; none at W = LPW C)
+#pragma unroll
+      for (int k = 0; k < RCMAX; ++k) {
+        const bool over = tb + k > W - 1;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) x[c][k] = over ? xl[c] : x[c][k];
+      }
+    }
   }
 
   // ---- pass 1 ----
@@ -950,10 +966,13 @@ int launch_axes(const float* stream, int64_t n_samples, int window, int stride, 
                         (reinterpret_cast<uintptr_t>(stream) & 15) == 0 && (window * A) % 32 != 16 &&
                         !std::getenv("HAR_WINDOW_NOPAD");
       const int ipw = pimg ? window * A + (((16 - window * A) % 32) + 32) % 32 : 0;
+      // (the fixed-length runs read D = lpw C - window samples past the last window unclamped)
+      const bool fixc = !p32 && ((lpw == 8 && C == 25) || (lpw == 16 && C == 13));
+      const int slack = fixc ? std::max(SLACK, (lpw * C - window) * A + 4) : SLACK;
       auto span_bytes = [&](int wpb) -> int64_t {
-        if (p32) return (PAD + (int64_t)wpb * p32_pitch(window, A) + SLACK) * (int64_t)sizeof(float);
-        if (ipw) return (PAD + (int64_t)wpb * ipw + SLACK) * (int64_t)sizeof(float);
-        return (PAD + ((int64_t)(wpb - 1) * stride + window) * A + SLACK) * (int64_t)sizeof(float);
+        if (p32) return (PAD + (int64_t)wpb * p32_pitch(window, A) + slack) * (int64_t)sizeof(float);
+        if (ipw) return (PAD + (int64_t)wpb * ipw + slack) * (int64_t)sizeof(float);
+        return (PAD + ((int64_t)(wpb - 1) * stride + window) * A + slack) * (int64_t)sizeof(float);
       };
       // waves per block: a multiple of T3, at most 4; the most whose span fits 48 KB (>= 3 blocks per CU)
       int m = 0;

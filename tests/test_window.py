@@ -51,7 +51,11 @@ def test_synth_stream_shard_invariant():
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("axes,window,stride", [(3, 200, 200), (3, 500, 250), (9, 500, 500), (6, 97, 31), (3, 97, 40),
-                                               (9, 37, 37), (3, 700, 350), (6, 1100, 1100)])
+                                               (9, 37, 37), (3, 700, 350), (6, 1100, 1100),
+                                               # fixed-length runs overhanging the window (8 x 25 / 16 x 13
+                                               # groups, D = 1 .. 15 copies of sample W - 1)
+                                               (3, 193, 97), (6, 199, 50), (9, 185, 100), (3, 195, 195),
+                                               (3, 207, 207), (6, 193, 193)])
 def test_window_kernel_matches_torch(cuda, axes, window, stride):
     from har.features.window import window_features
 
