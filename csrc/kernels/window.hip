@@ -805,6 +805,9 @@ __device__ __forceinline__ void reg_window_batch(const float* span, int64_t w0, 
   }
 }
 
+// (Rejected, same-box A/B in profiles/r6/window_rows_flags_rejected.txt: MLP rows assembled in the freed
+// span and stored as 16-byte chunks — stride 100 unchanged, stride 200 +2 us (100 VGPRs: 4 waves per SIMD
+// instead of 5); the peak bits as R & T with no per-sample s_and_b64 — no gain.)
 // FIXC: the run length is RCMAX itself (a compile-time constant): no per-k-step `k < C` guards, whose
 // compare + branch cost ~6 instructions per step and sample pass, and only the registers the runs use.
 // (A persistent variant — the next batch's span copied HBM -> LDS by global_load_lds while the current one
