@@ -805,6 +805,8 @@ __device__ __forceinline__ void reg_window_batch(const float* span, int64_t w0, 
   }
 }
 
+// (Rejected, same-box A/B in profiles/r6/window_global_reads_rejected.txt: the 8 x 25 runs read straight from
+// global memory with no LDS staging — fp32 rows 2% faster, MLP rows, the 1B pass's mode, 2.5% slower.)
 // (Rejected, same-box A/B in profiles/r6/window_rows_flags_rejected.txt: MLP rows assembled in the freed
 // span and stored as 16-byte chunks — stride 100 unchanged, stride 200 +2 us (100 VGPRs: 4 waves per SIMD
 // instead of 5); the peak bits as R & T with no per-sample s_and_b64 — no gain.)
