@@ -698,7 +698,11 @@ class MLPEngine:
                      K0=L.in_pad, H=self.dims[-1], C=L.num_classes, stride=L.total, n=L.total, lr=float(self.lr),
                      beta1=float(self.betas[0]), beta2=float(self.betas[1]), eps=float(self.eps), wd=float(self.wd),
                      regions=[(a, e, p, ns, ld) for a, e, p, ns, ld in self._grad_regions()])
-            plans[B] = (mod.MlpStepPlan(d), self.step_nwg, self.step_S)
+            plan = mod.MlpStepPlan(d)
+            if getattr(self, "pf_sink", None) is None:  # scratch word of the reduction's prefetch workgroups
+                self.pf_sink = torch.zeros(4, dtype=torch.int32, device=self.device)
+            plan.pf_sink = self.pf_sink.data_ptr()
+            plans[B] = (plan, self.step_nwg, self.step_S)
         return plans[B]
 
     def _plan_ok(self, Xb, yb):
@@ -706,11 +710,14 @@ class MLPEngine:
                 and Xb.dtype == torch.bfloat16 and yb.dtype == torch.int32 and Xb.is_contiguous()
                 and os.environ.get("HAR_MLP_PLAN", "1") != "0")
 
-    def train_step(self, Xb: torch.Tensor, yb: torch.Tensor, global_batch: int):
+    def train_step(self, Xb: torch.Tensor, yb: torch.Tensor, global_batch: int, prefetch=None):
         """One step.  Native: fwd kernel + bwd kernel + ONE reduction kernel; at N = 1 the Adam
         update is fused into that kernel, at N > 1 it stores G, one RCCL all-reduce of G follows and
         Adam runs from G — the same kernels and the same summation order at every N.  The
-        three-kernel step goes through the native plan (one host call per phase)."""
+        three-kernel step goes through the native plan (one host call per phase).  ``prefetch``: the
+        next step's input rows (a device tensor, or a (rows, labels) pair), read once per cache line by extra workgroups of this
+        step's reduction launch, so the next forward finds them in the memory-side cache — for epochs
+        over more rows than it holds (reads only: the step's results do not depend on it)."""
         if self.native and not self.dp and self._small_ok(Xb, yb):
             return self._small_step(Xb, yb, global_batch)
         if self.native:
@@ -720,15 +727,19 @@ class MLPEngine:
             plan, self.step_nwg, self.step_S = self._plan(B)
             self.last_path, self.last_fused, self.last_bwd, self.last_batch = "step", True, True, B
             s = _native.stream_ptr()
+            pf = [0, 0, 0, 0]  # (pointer, bytes) of up to two regions
+            regions = prefetch if isinstance(prefetch, (tuple, list)) else (prefetch,)
+            for r, t in enumerate(t for t in regions if t is not None and t.is_cuda and t.numel()):
+                pf[2 * r:2 * r + 2] = t.data_ptr(), t.numel() * t.element_size()
             if self.dp:
-                plan.run(Xb.data_ptr(), yb.data_ptr(), B, 1.0 / global_batch, 2, s)
+                plan.run(Xb.data_ptr(), yb.data_ptr(), B, 1.0 / global_batch, 2, s, *pf)
                 if self.sharded:
                     self.sharded_update()
                 else:
                     self.allreduce_grads()
                     plan.run(0, 0, B, 0.0, 4, s)
             else:
-                plan.run(Xb.data_ptr(), yb.data_ptr(), B, 1.0 / global_batch, 1, s)
+                plan.run(Xb.data_ptr(), yb.data_ptr(), B, 1.0 / global_batch, 1, s, *pf)
             return
         if self.native:
             self.forward_backward_native(Xb, yb, 1.0 / global_batch)

@@ -587,7 +587,10 @@ def _stream_full_pass(args, ctx, spec, stream, labels, eng, mean, inv_std, sampl
             lab = labels[(torch.arange(first_w, first_w + nb * B, device=dev) * fz.stride) // W - offset // W]
             y32 = xin_rows[("y", first_w)] = lab.to(torch.int32)
         for j in range(nb):
-            eng.train_step(X[j * B:(j + 1) * B], y32[j * B:(j + 1) * B], gb)
+            # (the next batch's rows touched by this step's reduction launch: the epoch's 1.3 GB of rows
+            # are not cache-resident, profiles/r6/mlp_cold_x_probe.txt)
+            nxt = (X[(j + 1) * B:(j + 2) * B], y32[(j + 1) * B:(j + 2) * B]) if j + 1 < nb and eng.native else None
+            eng.train_step(X[j * B:(j + 1) * B], y32[j * B:(j + 1) * B], gb, prefetch=nxt)
 
     settle_ms = settle_clocks(ctx, one_pass, args.settle_ms, dev)
     elapsed = timed(ctx, one_pass, args.steps, args.warmup, dev)

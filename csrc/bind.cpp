@@ -263,8 +263,11 @@ struct MlpStepPlan {
   std::vector<const float*> src;
   std::vector<int64_t> start, len, lds;
   std::vector<int> S;
-  // mode: 1 reduce + Adam (N = 1), 2 reduce + store G (DP, before the all-reduce), 4 Adam from G
-  void run(u X, u y, int B, float scale, int mode, u stream) {
+  u pf_sink = 0;  // 4-byte scratch word of the prefetch workgroups (set once by the engine)
+  // mode: 1 reduce + Adam (N = 1), 2 reduce + store G (DP, before the all-reduce), 4 Adam from G;
+  // pf / pf_bytes (and pf1 / pf1_bytes): the next step's input rows (and labels), read by the reduction
+  // launch's prefetch workgroups
+  void run(u X, u y, int B, float scale, int mode, u stream, u pf, int64_t pf_bytes, u pf1, int64_t pf1_bytes) {
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     if (mode & 3) {
       check(har_mlp_step_fwd(P<const uint16_t>(X), K0, P<uint16_t>(Wf), P<const float>(b0), P<const float>(b1), H,
@@ -280,7 +283,8 @@ struct MlpStepPlan {
     const int k = (gm & 1) ? (int)src.size() : 0;
     check(har_grad_reduce_adam(k, src.data(), start.data(), len.data(), lds.data(), S.data(), n, P<float>(G),
                                P<float>(Pw), P<float>(m), P<float>(v), P<uint16_t>(Pb), lr, b1c, b2c, eps, wd,
-                               P<int32_t>(step), 0, gm, &frag, s),
+                               P<int32_t>(step), 0, gm, &frag, s, pf && pf_sink ? P<const void>(pf) : nullptr,
+                               pf_bytes, P<uint32_t>(pf_sink), P<const void>(pf1), pf1_bytes),
           "grad_reduce_adam");
   }
 };
@@ -758,7 +762,9 @@ PYBIND11_MODULE(_har_native, m) {
         }
         return p;
       }))
-      .def("run", &MlpStepPlan::run);
+      .def("run", &MlpStepPlan::run, py::arg("X"), py::arg("y"), py::arg("B"), py::arg("scale"), py::arg("mode"),
+           py::arg("stream"), py::arg("pf") = 0, py::arg("pf_bytes") = 0, py::arg("pf1") = 0, py::arg("pf1_bytes") = 0)
+      .def_readwrite("pf_sink", &MlpStepPlan::pf_sink);
   m.def("mlp_step_grid", &har_mlp_step_grid);
   m.def("mlp_step_slices", &har_mlp_step_slices);
   m.def("mlp_step_fwd_slab_width", &har_mlp_step_fwd_slab_width);

@@ -79,7 +79,9 @@ int har_mlp_small_step_max_batch();
 int har_grad_reduce_adam(int nreg, const float* const* src, const int64_t* start, const int64_t* len,
                          const int64_t* lds, const int* S, int64_t n, float* G, float* param, float* m, float* v,
                          uint16_t* pb, float lr, float b1, float b2, float eps, float wd, int32_t* step, int tick,
-                         int mode, const MlpFragSpec* frag, hipStream_t s);
+                         int mode, const MlpFragSpec* frag, hipStream_t s, const void* pf = nullptr,
+                         int64_t pf_bytes = 0, uint32_t* pf_sink = nullptr, const void* pf1 = nullptr,
+                         int64_t pf1_bytes = 0);
 int har_mlp_pack_frag(const uint16_t* pb, const MlpFragSpec* f, hipStream_t s);
 int har_adam_step(float* param, const float* grad, const float* slabs, int nslabs, float* m, float* v,
                   uint16_t* param_bf16, int64_t n, float lr, float beta1, float beta2, float eps,

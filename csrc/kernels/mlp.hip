@@ -250,6 +250,22 @@ __global__ void cast_pad_kernel(const float* __restrict__ in, int rows, int cin,
 // same Adam arithmetic.  With fragment copies (MlpFragSpec) the new bf16 values also go to the W0 and
 // W1 fragment copies (8-byte runs); the W1^T copy is written by the step's forward kernel, which
 // holds W1 in registers anyway (a tiled transposing variant of this kernel measured 1.5 us slower).
+// Prefetch workgroups (PrefetchSpec: blocks main_blocks .. of the launch): the NEXT step's input rows read
+// once per 64-byte line while the reduction runs, so the next forward stages them from the memory-side
+// cache instead of HBM — an epoch over more rows than that cache holds (the 1.3 GB of rows of the
+// 1B-sample pass) lost ~5 us per step in the forward; with the prefetch ~2 (profiles/r6/mlp_cold_x_probe.txt;
+// a separate prefetch kernel on a side stream beside the backward cost ~6 us per step instead).  Reads
+// only: the loaded words are folded into one value stored to a scratch word under a data-dependent test,
+// so every thread's loads stay.
+struct PrefetchSpec {
+  const uint32_t* p;   // region 0 (the rows) ...
+  int64_t lines;       // ... in 64-byte lines
+  const uint32_t* p1;  // region 1 (the labels), its lines follow region 0's
+  int64_t lines1;
+  uint32_t* sink;
+  int main_blocks;
+};
+
 constexpr int GR_REDUCE = 1, GR_STORE = 2, GR_ADAM = 4, GR_REFRESH = 8;
 template <int GR_W>  // waves per workgroup
 __global__ __launch_bounds__(64 * GR_W) void grad_reduce_adam_kernel(GradRegions rg, int64_t n, float* __restrict__ G,
@@ -257,7 +273,25 @@ __global__ __launch_bounds__(64 * GR_W) void grad_reduce_adam_kernel(GradRegions
                                                                 float* __restrict__ v, bf16_t* __restrict__ pb,
                                                                 float lr, float b1, float b2, float eps, float wd,
                                                                 const int32_t* __restrict__ step, int mode,
-                                                                MlpFragSpec frag, int wide) {
+                                                                MlpFragSpec frag, int wide, PrefetchSpec pf) {
+  if ((int)blockIdx.x >= pf.main_blocks) {  // a prefetch workgroup (uniform per block)
+    const int64_t nt = (int64_t)(gridDim.x - pf.main_blocks) * blockDim.x;
+    const int64_t t0 = (int64_t)(blockIdx.x - pf.main_blocks) * blockDim.x + threadIdx.x;
+    uint32_t acc = 0;
+    const int64_t all = pf.lines + pf.lines1;
+    for (int64_t l = t0; l < all; l += 8 * nt) {
+      uint32_t x[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {  // 8 loads in flight
+        const int64_t q = min(l + j * nt, all - 1);
+        x[j] = q < pf.lines ? pf.p[q * 16] : pf.p1[(q - pf.lines) * 16];
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc += x[j];
+    }
+    if (t0 == 0 || acc == 0x9e3779b9u) *pf.sink = acc;
+    return;
+  }
   __shared__ float4 part[GR_W][64];
   const int q = threadIdx.x >> 6, k = threadIdx.x & 63;
   const int64_t i4 = (int64_t)blockIdx.x * 64 + k, e = i4 * 4;
@@ -441,8 +475,11 @@ extern "C" int har_grad_reduce_adam(int nreg, const float* const* src, const int
                                     const int64_t* lds, const int* S, int64_t n, float* G, float* param, float* m,
                                     float* v, uint16_t* pb, float lr, float b1, float b2, float eps, float wd,
                                     int32_t* step, int tick, int mode, const MlpFragSpec* frag_spec,
-                                    hipStream_t s) {
+                                    hipStream_t s, const void* pf, int64_t pf_bytes, uint32_t* pf_sink,
+                                    const void* pf1, int64_t pf1_bytes) {
   if (n % 4 || nreg < 0 || nreg > 8 || ((mode & GR_REDUCE) && nreg == 0)) return -2;
+  if (pf && (!pf_sink || pf_bytes < 0 || (reinterpret_cast<uintptr_t>(pf) & 3))) return -2;
+  if (pf1 && (!pf || pf1_bytes < 0 || (reinterpret_cast<uintptr_t>(pf1) & 3))) return -2;
   if ((mode & GR_REFRESH) && mode != GR_REFRESH) return -2;  // the refresh runs alone
   MlpFragSpec frag{};
   if (frag_spec && frag_spec->dst) {
@@ -462,6 +499,12 @@ extern "C" int har_grad_reduce_adam(int nreg, const float* const* src, const int
   const int64_t blocks = (n / 4 + 63) / 64;
   if (blocks == 0) return 0;
   if (tick) adam_tick_kernel<<<1, 1, 0, s>>>(step);
+  // prefetch workgroups: one per 2048 lines (8 loads per thread), at most 256
+  PrefetchSpec ps{reinterpret_cast<const uint32_t*>(pf), pf ? pf_bytes / 64 : 0,
+                  reinterpret_cast<const uint32_t*>(pf1), pf && pf1 ? pf1_bytes / 64 : 0, pf_sink, (int)blocks};
+  const int64_t pfl = ps.lines + ps.lines1;
+  const int64_t pfb = pf && pfl > 0 ? std::min<int64_t>(256, (pfl + 2047) / 2048) : 0;
+  const int64_t grid = blocks + pfb;
   // waves per workgroup: 4 (tools/gpu_qnwg_ab.sh a: flagship reduction + Adam 6.6 -> 4.9 us with 64 slabs,
   // the small-batch step 21.7 -> 20.8 us with 8; 8 waves 5.4 / 20.9; 16 was the round-3 choice)
   static const int w = [] {
@@ -473,14 +516,14 @@ extern "C" int har_grad_reduce_adam(int nreg, const float* const* src, const int
     return e && atoi(e) == 16 ? 1 : 0;
   }();
   if (w == 4)
-    grad_reduce_adam_kernel<4><<<(int)blocks, 256, 0, s>>>(rg, n, G, param, m, v, pb, lr, b1, b2, eps, wd, step, mode,
-                                                           frag, wide);
+    grad_reduce_adam_kernel<4><<<(int)grid, 256, 0, s>>>(rg, n, G, param, m, v, pb, lr, b1, b2, eps, wd, step, mode,
+                                                         frag, wide, ps);
   else if (w == 8)
-    grad_reduce_adam_kernel<8><<<(int)blocks, 512, 0, s>>>(rg, n, G, param, m, v, pb, lr, b1, b2, eps, wd, step, mode,
-                                                           frag, wide);
+    grad_reduce_adam_kernel<8><<<(int)grid, 512, 0, s>>>(rg, n, G, param, m, v, pb, lr, b1, b2, eps, wd, step, mode,
+                                                         frag, wide, ps);
   else
-    grad_reduce_adam_kernel<16><<<(int)blocks, 1024, 0, s>>>(rg, n, G, param, m, v, pb, lr, b1, b2, eps, wd, step,
-                                                             mode, frag, wide);
+    grad_reduce_adam_kernel<16><<<(int)grid, 1024, 0, s>>>(rg, n, G, param, m, v, pb, lr, b1, b2, eps, wd, step,
+                                                           mode, frag, wide, ps);
   HAR_CHECK_LAUNCH();
   return 0;
 }

@@ -382,6 +382,31 @@ def test_mlp_step_matches_gemm_path_and_is_deterministic(cuda, monkeypatch, F, B
     assert abs(lc1[0] - lcr[0]) / lcr[0] < 1e-3 and abs(lc1[1] - lcr[1]) <= 2
 
 
+def test_mlp_step_prefetch_leaves_training_bitwise_unchanged(cuda):
+    """train_step(prefetch=the next batch's rows): the reduction launch's extra workgroups only read
+    those rows (bind.cpp MlpStepPlan, mlp.hip PrefetchSpec) — parameters, Adam moments and the bf16
+    copy after six flagship-batch steps are bit-identical to plain steps."""
+    from har.models.mlp import MLPEngine, pad_input_bf16
+
+    B, F, nb = 65536, 43, 3
+    g = torch.Generator(device=cuda).manual_seed(5)
+    X = torch.randn(B * nb, F, device=cuda, generator=g)
+    y = torch.randint(0, 6, (B * nb,), device=cuda, generator=g).to(torch.int32)
+    outs = []
+    for pf in (False, True):
+        e = MLPEngine([F, 256, 256, 6], B, cuda, lr=1e-3, seed=7)
+        Xb = pad_input_bf16(X, e.layout.in_pad)
+        for i in range(2 * nb):
+            j, k = i % nb, (i + 1) % nb
+            e.train_step(Xb[j * B:(j + 1) * B], y[j * B:(j + 1) * B], B,
+                         prefetch=(Xb[k * B:(k + 1) * B], y[k * B:(k + 1) * B]) if pf else None)
+        torch.cuda.synchronize()
+        assert e.last_path == "step"
+        outs.append((e.P.clone(), e.m.clone(), e.v.clone(), e.Pb.clone()))
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+
+
 def test_mlp_step_outputs(cuda):
     """What the step forward hands the backward: dact2 = ((softmax - onehot) * scale) . Wout * relu'(h2)
     in bf16, in the backward's tile order (16-byte chunks of rows with bit 2 set swapped in pairs),
