@@ -701,7 +701,8 @@ class MLPEngine:
             plan = mod.MlpStepPlan(d)
             if getattr(self, "pf_sink", None) is None:  # scratch word of the reduction's prefetch workgroups
                 self.pf_sink = torch.zeros(4, dtype=torch.int32, device=self.device)
-            plan.pf_sink = self.pf_sink.data_ptr()
+            if hasattr(plan, "pf_sink"):  # (absent from a library built before the prefetch: A/B runs)
+                plan.pf_sink = self.pf_sink.data_ptr()
             plans[B] = (plan, self.step_nwg, self.step_S)
         return plans[B]
 
@@ -727,10 +728,11 @@ class MLPEngine:
             plan, self.step_nwg, self.step_S = self._plan(B)
             self.last_path, self.last_fused, self.last_bwd, self.last_batch = "step", True, True, B
             s = _native.stream_ptr()
-            pf = [0, 0, 0, 0]  # (pointer, bytes) of up to two regions
+            pf = []  # (pointer, bytes) of up to two regions; none: the plain launch
             regions = prefetch if isinstance(prefetch, (tuple, list)) else (prefetch,)
-            for r, t in enumerate(t for t in regions if t is not None and t.is_cuda and t.numel()):
-                pf[2 * r:2 * r + 2] = t.data_ptr(), t.numel() * t.element_size()
+            for t in regions:
+                if t is not None and t.is_cuda and t.numel():
+                    pf += [t.data_ptr(), t.numel() * t.element_size()]
             if self.dp:
                 plan.run(Xb.data_ptr(), yb.data_ptr(), B, 1.0 / global_batch, 2, s, *pf)
                 if self.sharded:
