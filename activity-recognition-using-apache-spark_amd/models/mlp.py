@@ -718,7 +718,8 @@ class MLPEngine:
         three-kernel step goes through the native plan (one host call per phase).  ``prefetch``: the
         next step's input rows (a device tensor, or a (rows, labels) pair), read once per cache line by extra workgroups of this
         step's reduction launch, so the next forward finds them in the memory-side cache — for epochs
-        over more rows than it holds (reads only: the step's results do not depend on it)."""
+        over more rows than it holds (reads only: the step's results do not depend on it; the other
+        step paths ignore it)."""
         if self.native and not self.dp and self._small_ok(Xb, yb):
             return self._small_step(Xb, yb, global_batch)
         if self.native:
