@@ -86,6 +86,7 @@ def window_features_torch(stream: torch.Tensor, window: int, stride: int, hz: fl
 
 
 _WIDE_WARNED = set()
+_WIDE_CHUNK_BYTES = 1 << 30  # float64 temporaries per chunk of the wide-window fallback
 
 
 def _wide_windows(stream: torch.Tensor, window: int, stride: int, hz: float) -> torch.Tensor:
@@ -101,7 +102,7 @@ def _wide_windows(stream: torch.Tensor, window: int, stride: int, hz: float) -> 
 
         warnings.warn(f"window_features: {A}-axis windows of {window} samples exceed the kernel's LDS images; "
                       f"computed with the torch definition on {stream.device}")
-    per = max(1, (1 << 30) // (A * window * 8 * 6))
+    per = max(1, _WIDE_CHUNK_BYTES // (A * window * 8 * 6))
     outs = [window_features_torch(stream[w0 * stride: (w0 + min(per, nw - w0) - 1) * stride + window],
                                   window, stride, hz) for w0 in range(0, nw, per)]
     return torch.cat(outs) if outs else torch.empty(0, n_features(A), device=stream.device)

@@ -41,6 +41,28 @@ def test_window_count_and_halo():
     assert fz.window == 500 and fz.stride == 250 and fz.halo() == 250
 
 
+def test_wide_window_fallback_chunks_match_one_shot(monkeypatch):
+    """The fallback for windows too wide for the kernel's LDS images computes the torch definition in
+    chunks of windows (each chunk's sample range sliced from the stream): with tiny chunks (1 and 3
+    windows) the rows equal the one-shot definition, and the warning is raised once per shape."""
+    import warnings
+
+    from har.features import window as wmod
+
+    spec = StreamSpec(axes=6, window=300, seed=4)
+    s, _ = generate_stream(6, spec)
+    ref = window_features_torch(s, 300, 170, 50.0)
+    for chunk_windows in (1, 3):
+        monkeypatch.setattr(wmod, "_WIDE_CHUNK_BYTES", 6 * 300 * 8 * 6 * chunk_windows)
+        monkeypatch.setattr(wmod, "_WIDE_WARNED", set())
+        with warnings.catch_warnings(record=True) as rec:
+            warnings.simplefilter("always")
+            out = wmod._wide_windows(s, 300, 170, 50.0)
+        assert len(rec) == 1 and "exceed the kernel" in str(rec[0].message)
+        assert out.shape == ref.shape
+        torch.testing.assert_close(out, ref, rtol=0, atol=0, equal_nan=True)
+
+
 def test_synth_stream_shard_invariant():
     spec = StreamSpec(seed=3)
     s_all, y_all = generate_stream(12, spec)
