@@ -43,6 +43,8 @@ constexpr int MAXA = 9;
 constexpr int NB = 10;
 constexpr int PAD = 12;    // floats of LDS before the staged span: the t = -1 neighbour read stays inside
 constexpr int SLACK = 16;  // floats after it: the t = W neighbour read of the last window stays inside
+// floats of the register kernel's MLP-mode normalization image (F means + F inverse std devs, 16-byte rounded)
+__host__ __device__ constexpr int reg_nrm_floats(int A) { return (2 * (17 * A + 4 * (A / 3)) + 3) & ~3; }
 
 typedef float v4f __attribute__((ext_vector_type(4)));
 
@@ -574,7 +576,7 @@ __host__ __device__ inline int p32_pitch(int W, int A) { return (p32_pos(W, A) +
 template <int A, int LPW, bool MLP, int RCMAX, bool P32, bool FIXC>
 __device__ __forceinline__ void reg_window_batch(const float* span, int64_t w0, int nwin, int W, int ip, int C,
                                                  float ms_per_sample, float* __restrict__ out, int ld_out,
-                                                 const MlpOut& mo) {
+                                                 const MlpOut& mo, const float* nrm) {
   constexpr int T3 = A / 3, GPW = 64 / LPW;
   const int tid = (int)threadIdx.x;
   auto pos = [&](int t) { return P32 ? p32_pos(t, A) : t * A; };
@@ -727,7 +729,7 @@ __device__ __forceinline__ void reg_window_batch(const float* span, int64_t w0, 
     if (!(on && valid)) return;
     if constexpr (MLP) {
       const float xv = v != v ? mo.nan_value : v;
-      ob[f] = f2bf((xv - mo.mean[f]) * mo.inv_std[f]);
+      ob[f] = f2bf((xv - nrm[f]) * nrm[17 * A + 4 * T3 + f]);  // (the staged means / inverse std devs)
     } else {
       o[f] = v;
     }
@@ -826,7 +828,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
   static_assert(LPW == 8 || LPW == 16 || LPW == 32 || LPW == 64, "groups of 8, 16, 32 or 64 lanes");
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int nt = (int)blockDim.x, tid = (int)threadIdx.x;
-  float* const span = lds + PAD;
+  // MLP rows: the F means and inverse std devs staged in LDS ahead of the span (reg_nrm_floats), so the
+  // row write reads them there instead of ~20 scattered global loads per lane at the kernel's end
+  constexpr int NR = MLP ? reg_nrm_floats(A) : 0;
+  float* const span = lds + NR + PAD;
+  if constexpr (MLP) {
+    constexpr int F = 17 * A + 4 * (A / 3);
+    for (int f = tid; f < 2 * F; f += nt) lds[f] = f < F ? mo.mean[f] : mo.inv_std[f - F];
+  }
   // image pitch (floats) between consecutive windows: P32 images, padded images (ipw > 0, non-overlapping
   // windows: a pitch of 16 mod 32 floats puts the two 16-lane windows of a 32-lane LDS bank group on
   // disjoint banks — the contiguous 600-float pitch of W = 200 x 3 axes had 32% bank-conflict cycles,
@@ -874,7 +883,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
   }
   }
   __syncthreads();
-  reg_window_batch<A, LPW, MLP, RCMAX, P32, FIXC>(span, w0, nwin, W, ip, C, ms_per_sample, out, ld_out, mo);
+  reg_window_batch<A, LPW, MLP, RCMAX, P32, FIXC>(span, w0, nwin, W, ip, C, ms_per_sample, out, ld_out, mo,
+                                                 MLP ? lds : nullptr);
 }
 
 int cu_count() {
@@ -974,10 +984,11 @@ int launch_axes(const float* stream, int64_t n_samples, int window, int stride, 
       // (the fixed-length runs read D = lpw C - window samples past the last window unclamped)
       const bool fixc = !p32 && ((lpw == 8 && C == 25) || (lpw == 16 && C == 13));
       const int slack = fixc ? std::max(SLACK, (lpw * C - window) * A + 4) : SLACK;
+      constexpr int NR = MLP ? reg_nrm_floats(A) : 0;
       auto span_bytes = [&](int wpb) -> int64_t {
-        if (p32) return (PAD + (int64_t)wpb * p32_pitch(window, A) + slack) * (int64_t)sizeof(float);
-        if (ipw) return (PAD + (int64_t)wpb * ipw + slack) * (int64_t)sizeof(float);
-        return (PAD + ((int64_t)(wpb - 1) * stride + window) * A + slack) * (int64_t)sizeof(float);
+        if (p32) return (NR + PAD + (int64_t)wpb * p32_pitch(window, A) + slack) * (int64_t)sizeof(float);
+        if (ipw) return (NR + PAD + (int64_t)wpb * ipw + slack) * (int64_t)sizeof(float);
+        return (NR + PAD + ((int64_t)(wpb - 1) * stride + window) * A + slack) * (int64_t)sizeof(float);
       };
       // waves per block: a multiple of T3, at most 4; the most whose span fits 48 KB (>= 3 blocks per CU)
       int m = 0;
