@@ -844,16 +844,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
 
   const int64_t w0 = (int64_t)blockIdx.x * wpb;
   const int nwin = (int)min<int64_t>(wpb, n_windows - w0);
+  // float4 loads in flight per thread while staging: 12 — a 4-wave block's ~2,470-float4 span (the
+  // 200-sample shapes) is then ONE round of loads instead of two dependent ones
+  constexpr int SU = 12;
   if (P32 || ipw > 0) {  // ---- stage the windows, one padded image each (float4 granules) ----
     const v4f* s4 = reinterpret_cast<const v4f*>(stream + w0 * (int64_t)W * A);
     const int n4w = W * A / 4, n4 = nwin * n4w;
     const uint32_t magic = 0xffffffffu / (uint32_t)n4w + 1u;  // f / n4w = umulhi(f, magic) for f * n4w < 2^32
-    for (int f0 = tid; f0 < n4; f0 += 8 * nt) {
-      v4f r[8];
+    for (int f0 = tid; f0 < n4; f0 += SU * nt) {
+      v4f r[SU];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) r[u] = s4[min(f0 + u * nt, n4 - 1)];
+      for (int u = 0; u < SU; ++u) r[u] = s4[min(f0 + u * nt, n4 - 1)];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
+      for (int u = 0; u < SU; ++u) {
         const int f = min(f0 + u * nt, n4 - 1), wl = (int)__umulhi((uint32_t)f, magic), e = 4 * (f - wl * n4w);
         *reinterpret_cast<v4f*>(span + wl * ip + e + (P32 ? 4 * (e / (32 * A)) : 0)) = r[u];
       }
@@ -868,14 +871,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
       const int n4 = nspan >> 2;
       const v4f* s4 = reinterpret_cast<const v4f*>(src);
       v4f* d4 = reinterpret_cast<v4f*>(span);
-      // unconditional (clamped) loads and stores: no exec-masked branches between them, so all eight
+      // unconditional (clamped) loads and stores: no exec-masked branches between them, so all SU
       // loads are in flight before the first store waits (a clamped slot rewrites the last float4)
-      for (int f0 = tid; f0 < n4; f0 += 8 * nt) {
-        v4f r[8];
+      for (int f0 = tid; f0 < n4; f0 += SU * nt) {
+        v4f r[SU];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) r[u] = s4[min(f0 + u * nt, n4 - 1)];
+        for (int u = 0; u < SU; ++u) r[u] = s4[min(f0 + u * nt, n4 - 1)];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) d4[min(f0 + u * nt, n4 - 1)] = r[u];
+        for (int u = 0; u < SU; ++u) d4[min(f0 + u * nt, n4 - 1)] = r[u];
       }
       done = n4 * 4;
     }
