@@ -259,7 +259,8 @@ __global__ void cast_pad_kernel(const float* __restrict__ in, int rows, int cin,
 // so every thread's loads stay.
 struct PrefetchSpec {
   const uint32_t* p;   // region 0 (the rows) ...
-  int64_t lines;       // ... in 64-byte lines
+  int64_t lines;       // ... in lines of `dw` dwords (64 bytes; HAR_PF_LINE)
+  int dw;
   const uint32_t* p1;  // region 1 (the labels), its lines follow region 0's
   int64_t lines1;
   uint32_t* sink;
@@ -284,7 +285,7 @@ __global__ __launch_bounds__(64 * GR_W) void grad_reduce_adam_kernel(GradRegions
 #pragma unroll
       for (int j = 0; j < 8; ++j) {  // 8 loads in flight
         const int64_t q = min(l + j * nt, all - 1);
-        x[j] = q < pf.lines ? pf.p[q * 16] : pf.p1[(q - pf.lines) * 16];
+        x[j] = q < pf.lines ? pf.p[q * pf.dw] : pf.p1[(q - pf.lines) * pf.dw];
       }
 #pragma unroll
       for (int j = 0; j < 8; ++j) acc += x[j];
@@ -500,8 +501,13 @@ extern "C" int har_grad_reduce_adam(int nreg, const float* const* src, const int
   if (blocks == 0) return 0;
   if (tick) adam_tick_kernel<<<1, 1, 0, s>>>(step);
   // prefetch workgroups: one per 2048 lines (8 loads per thread), at most 256
-  PrefetchSpec ps{reinterpret_cast<const uint32_t*>(pf), pf ? pf_bytes / 64 : 0,
-                  reinterpret_cast<const uint32_t*>(pf1), pf && pf1 ? pf1_bytes / 64 : 0, pf_sink, (int)blocks};
+  static const int pf_line = [] {  // bytes per touched line (tuning: HAR_PF_LINE = 64 / 128 / 256)
+    const char* e = getenv("HAR_PF_LINE");
+    const int v = e ? atoi(e) : 64;
+    return v == 128 || v == 256 ? v : 64;
+  }();
+  PrefetchSpec ps{reinterpret_cast<const uint32_t*>(pf), pf ? pf_bytes / pf_line : 0, pf_line / 4,
+                  reinterpret_cast<const uint32_t*>(pf1), pf && pf1 ? pf1_bytes / pf_line : 0, pf_sink, (int)blocks};
   const int64_t pfl = ps.lines + ps.lines1;
   const int64_t pfb = pf && pfl > 0 ? std::min<int64_t>(256, (pfl + 2047) / 2048) : 0;
   const int64_t grid = blocks + pfb;
