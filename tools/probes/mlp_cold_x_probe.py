@@ -27,10 +27,15 @@ def main():
         y32 = y.to(torch.int32).contiguous()
         del X, y
 
-        for pf in (0, 1, 2):  # none, the next rows, the next rows + labels
+        # none, the next rows, the next rows + labels, their first quarter / eighth (the forward's first
+        # two / one tiles per workgroup: later tiles are staged two tiles ahead by the kernel itself)
+        for pf in [int(a) for a in os.environ.get("PF_MODES", "0,1,2").split(",")]:
             def step(i):
                 j, k = i % nb, (i + 1) % nb
-                nxt = (None, Xin[k * B:(k + 1) * B], (Xin[k * B:(k + 1) * B], y32[k * B:(k + 1) * B]))[pf]
+                part = {3: B // 4, 4: B // 8}.get(pf, B)
+                nxt = (None, Xin[k * B:(k + 1) * B], (Xin[k * B:(k + 1) * B], y32[k * B:(k + 1) * B]),
+                       (Xin[k * B:k * B + part], y32[k * B:k * B + part]),
+                       (Xin[k * B:k * B + part], y32[k * B:k * B + part]))[pf]
                 eng.train_step(Xin[j * B:(j + 1) * B], y32[j * B:(j + 1) * B], B, prefetch=nxt)
 
             for i in range(max(40, nb)):
